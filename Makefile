@@ -1,0 +1,48 @@
+# Build of the MI355X (gfx950) admission engine. `python -c "import __graft_entry__ as g; g.build()"`
+# runs this; hipcc cross-compiles for gfx950 without a GPU.
+#   policy-server_amd/libkwgpu.so    product: HIP kernels + host engine + C ABI (include/kwgpu.h)
+#   policy-server_amd/libkwsynth.so  bench/test workload generator
+#   oracle/build/libkworacle.so      CPU restatement (test infrastructure only)
+HIPCC ?= /opt/rocm/bin/hipcc
+CXX ?= g++
+CC ?= gcc
+ARCH ?= gfx950
+PKG := policy-server_amd
+SRC := $(PKG)/csrc
+OBJ := $(PKG)/build
+HIPDEF := -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include
+CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wextra $(HIPDEF)
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -munsafe-fp-atomics
+
+HOST_SRCS := json automaton expr env flatten service capi
+HOST_OBJS := $(addprefix $(OBJ)/,$(addsuffix .o,$(HOST_SRCS)))
+HEADERS := $(wildcard $(SRC)/*.hpp) include/kwgpu.h
+
+all: $(PKG)/libkwgpu.so $(PKG)/libkwsynth.so oracle/build/libkworacle.so
+
+$(OBJ)/%.o: $(SRC)/%.cpp $(HEADERS)
+	@mkdir -p $(OBJ)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(OBJ)/kernels.o: $(SRC)/kernels.hip $(HEADERS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(PKG)/libkwgpu.so: $(HOST_OBJS) $(OBJ)/kernels.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
+$(PKG)/libkwsynth.so: $(SRC)/synth.cpp include/kwgpu.h
+	$(CXX) -O3 -std=c++17 -fPIC -shared -Wall -o $@ $<
+
+oracle/build/libkworacle.so: oracle/kworacle.c oracle/kworacle.h include/kwgpu.h
+	@mkdir -p oracle/build
+	$(CC) -O2 -std=c11 -fPIC -shared -Wall -Wextra -o $@ $< -lpthread
+
+# kernel resource usage (VGPR/SGPR/LDS/occupancy) report
+resources: $(SRC)/kernels.hip
+	$(HIPCC) $(HIPFLAGS) -Rpass-analysis=kernel-resource-usage -c $< -o /dev/null
+
+clean:
+	rm -rf $(OBJ) $(PKG)/*.so oracle/build
+
+.PHONY: all clean resources

@@ -1,0 +1,176 @@
+"""bench.py — batched admission evaluation on MI355X (BASELINE.json metric).
+
+Workload (the configuration the metric "at 64 policies" is quoted on):
+1M synthetic Pod AdmissionReviews per GPU x 64 compiled policies (22 psp-capabilities,
+21 psp-apparmor, 21 safe-labels; configs/c4_64.yml). A step = one validate pass of the hot path
+(string classification kernel + policy evaluation kernel) over the GPU's whole resident batch,
+producing 64M verdict words. Inputs are resident in HBM before the timed region.
+
+  python bench.py [--gpus N --steps K --warmup W]
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+      --master-port P bench.py --gpus N --steps K --warmup W
+
+Multi-GPU: one process per GPU; rank 0 compiles the policy set and broadcasts the compiled-table
+blob once over RCCL (torch.distributed "nccl" = RCCL on ROCm); every rank evaluates its own request
+shard (weak scaling, no collective on the per-request path). Timing: barrier + synchronize on both
+sides of exactly K steps, max over ranks. Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "policy-server_amd"))
+
+METRIC = "admission requests evaluated/sec (node) at 64 policies; HBM GB/s vs peak"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rows", type=int, default=1_000_000, help="requests per GPU")
+    ap.add_argument("--config", default="c4_64")
+    ap.add_argument("--synth", type=int, default=4)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (rank 0)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import yaml
+
+    import kwgpu as K
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    device = local
+
+    with open(os.path.join(ROOT, "configs", f"{args.config}.yml")) as f:
+        policies = yaml.safe_load(f)
+
+    # compiled tables: built once on rank 0, broadcast over RCCL to the other GPUs
+    if world > 1:
+        if rank == 0:
+            env = K.EvaluationEnvironment(policies, device=device)
+            blob = env.serialize()
+            n = torch.tensor([len(blob)], dtype=torch.int64, device="cuda")
+        else:
+            n = torch.zeros(1, dtype=torch.int64, device="cuda")
+        dist.broadcast(n, 0)
+        buf = torch.empty(int(n.item()), dtype=torch.uint8, device="cuda")
+        if rank == 0:
+            buf.copy_(torch.frombuffer(bytearray(blob), dtype=torch.uint8))
+        dist.broadcast(buf, 0)
+        if rank != 0:
+            env = K.EvaluationEnvironment.from_serialized(bytes(buf.cpu().numpy()), device=device)
+    else:
+        env = K.EvaluationEnvironment(policies, device=device)
+    ids = env.policy_ids()
+    npol = len(ids)
+
+    t0 = time.time()
+    syn = K.SynthBatch(args.synth, args.rows, seed=20250509, row0=rank * args.rows)
+    batch = syn.batch().to_device(device)
+    log(f"rank {rank}: {args.rows} requests generated + resident in {time.time() - t0:.1f}s; {npol} policies")
+
+    for _ in range(args.warmup):
+        batch.validate(env, ids)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        batch.validate(env, ids)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = world * args.rows * args.steps / elapsed
+
+    # per-kernel device time with HIP events on the launch stream
+    tm = batch.timed(env, ids, warmup=2, reps=max(5, args.steps))
+    kernels = {"classify": (tm.classify_ms, tm.classify_bytes), "evaluate": (tm.evaluate_ms, tm.evaluate_bytes)}
+    dom = max(kernels, key=lambda k: kernels[k][0])
+    ms, nbytes = kernels[dom]
+    achieved = nbytes / (ms * 1e-3) / 1e9
+    # sanity: a sample of verdicts is non-trivial
+    v = batch.verdicts()
+    frac_allowed = float(((v & K._native.KW_F_ALLOWED) != 0).mean())
+
+    result = None
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline(policies, ids, args)
+        result = {
+            "metric": METRIC, "value": value, "unit": "requests/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": f"C4: {args.rows} synthetic Pod AdmissionReviews per GPU x {npol} compiled "
+                                   f"policies ({args.config}.yml: 22 psp-capabilities, 21 psp-apparmor, "
+                                   f"21 safe-labels)",
+                       "requests_per_gpu": args.rows, "policies": npol, "parallelism": f"dp{world} (request shards)"},
+            "evaluations_per_s": value * npol,
+            "kernel_ms": {"classify": tm.classify_ms, "evaluate": tm.evaluate_ms, "total": tm.total_ms},
+            "roofline": {"kernel": f"{dom}_kernel", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "algorithmic_bytes_per_launch": nbytes},
+            "cpu_baseline": cpu,
+            "verdicts_final_allowed_fraction": frac_allowed,
+        }
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+    return result
+
+
+def cpu_baseline(policies, ids, args):
+    """The oracle (C restatement of EvaluationEnvironment::validate, oracle/kworacle.c) on the host
+    cores, on a bounded sample of the same workload. The reference's own wasmtime path cannot run
+    here (no Rust toolchain, policy modules are remote OCI artifacts: SURVEY §8(c))."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    import kwgpu as K
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    oe = O.OracleEnv(policies)
+    probe_rows = 2000
+    syn = K.SynthBatch(args.synth, probe_rows, seed=20250509)
+    t = time.perf_counter()
+    oe.eval(syn.soa(), ids, threads=threads)
+    per_row = (time.perf_counter() - t) / probe_rows
+    rows = int(min(2_000_000, max(probe_rows, args.cpu_seconds / max(per_row, 1e-9))))
+    syn = K.SynthBatch(args.synth, rows, seed=20250509)
+    t = time.perf_counter()
+    oe.eval(syn.soa(), ids, threads=threads)
+    dt = time.perf_counter() - t
+    return {"value": rows / dt, "unit": "requests/s", "cores": threads, "kind": "port",
+            "sample": f"{rows} synthetic C4 requests x {len(ids)} policies ({dt:.1f}s, oracle/kworacle.c, "
+                      f"{threads} threads)"}
+
+
+if __name__ == "__main__":
+    main()

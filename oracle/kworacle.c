@@ -1,0 +1,498 @@
+/*
+ * kworacle.c — CPU restatement of the declarative-policy hot path. TEST INFRASTRUCTURE ONLY
+ * (see kworacle.h for what is restated, from which reference file:line, and who may load it).
+ * Parity status: service constraints / bypass / group short-circuit are pinned by the reference's
+ * own tests (tests/golden/); the policy-family arithmetic is parity UNPINNED (upstream Wasm absent)
+ * and follows DESIGN.md §"Policy families".
+ */
+#define _GNU_SOURCE
+#include "kworacle.h"
+
+#include <fnmatch.h>
+#include <pthread.h>
+#include <regex.h>
+#include <stdlib.h>
+#include <string.h>
+
+struct orc_env {
+  const orc_policy *pol;
+  int32_t npol;
+  char *always_ns; /* NULL = None */
+  regex_t **re;    /* per policy: compiled l3 regexes (labels) */
+};
+
+static char *dupz(const char *s) {
+  size_t n = strlen(s);
+  char *d = (char *)malloc(n + 1);
+  memcpy(d, s, n + 1);
+  return d;
+}
+
+orc_env *orc_env_new(const orc_policy *policies, int32_t npol, const char *always_ns, char *err,
+                     int errlen) {
+  orc_env *e = (orc_env *)calloc(1, sizeof(orc_env));
+  e->pol = policies;
+  e->npol = npol;
+  e->always_ns = always_ns ? dupz(always_ns) : NULL;
+  e->re = (regex_t **)calloc((size_t)npol, sizeof(regex_t *));
+  for (int32_t p = 0; p < npol; ++p) {
+    const orc_policy *P = &policies[p];
+    if (P->family != ORC_F_LABELS || P->n[3] == 0) continue;
+    e->re[p] = (regex_t *)calloc((size_t)P->n[3], sizeof(regex_t));
+    for (int32_t i = 0; i < P->n[3]; ++i) {
+      int rc = regcomp(&e->re[p][i], P->l[3][i], REG_EXTENDED | REG_NOSUB);
+      if (rc != 0) {
+        if (err) regerror(rc, &e->re[p][i], err, (size_t)errlen);
+        return NULL;
+      }
+    }
+  }
+  return e;
+}
+
+void orc_env_free(orc_env *e) {
+  if (!e) return;
+  for (int32_t p = 0; p < e->npol; ++p) {
+    if (!e->re[p]) continue;
+    for (int32_t i = 0; i < e->pol[p].n[3]; ++i) regfree(&e->re[p][i]);
+    free(e->re[p]);
+  }
+  free(e->re);
+  free(e->always_ns);
+  free(e);
+}
+
+int orc_regex_ok(const char *pattern) {
+  regex_t re;
+  if (regcomp(&re, pattern, REG_EXTENDED | REG_NOSUB) != 0) return 0;
+  regfree(&re);
+  return 1;
+}
+
+/* ------------------------------------------------------------------ string helpers */
+typedef struct {
+  const char *p;
+  uint32_t n;
+} sv;
+
+static sv col(const kw_strcol *c, uint64_t i) {
+  sv s;
+  s.p = (const char *)c->bytes + c->off[i];
+  s.n = c->off[i + 1] - c->off[i];
+  return s;
+}
+
+/* NUL-terminated scratch copy (strings are short; long ones get a heap buffer) */
+typedef struct {
+  char small[512];
+  char *big;
+} zbuf;
+static const char *z(zbuf *b, sv s) {
+  char *d = b->small;
+  if (s.n + 1 > sizeof(b->small)) {
+    free(b->big);
+    b->big = (char *)malloc(s.n + 1);
+    d = b->big;
+  }
+  memcpy(d, s.p, s.n);
+  d[s.n] = 0;
+  return d;
+}
+
+static int sv_eq(sv s, const char *t) { return strlen(t) == s.n && memcmp(s.p, t, s.n) == 0; }
+
+static int any_glob(const char *const *pats, int32_t n, const char *s) {
+  for (int32_t i = 0; i < n; ++i)
+    if (fnmatch(pats[i], s, 0) == 0) return 1;
+  return 0;
+}
+static int any_eq(const char *const *lst, int32_t n, sv s) {
+  for (int32_t i = 0; i < n; ++i)
+    if (sv_eq(s, lst[i])) return 1;
+  return 0;
+}
+
+/* ------------------------------------------------------------------ image references */
+/* DESIGN.md §trusted-repos "image reference normalisation":
+   name@digest split at the first '@'; the first '/'-component is a registry iff it contains '.'
+   or ':' or equals "localhost", else the registry is docker.io; the tag is what follows the last
+   ':' of the remainder; docker.io single-component paths get "library/"; the effective tag is the
+   explicit tag, else "latest" when there is no digest, else none. */
+int orc_image_parts(const char *s, char *registry, char *tag, char *norm, int cap) {
+  (void)cap;
+  size_t n = strlen(s);
+  const char *at = memchr(s, '@', n);
+  size_t name_n = at ? (size_t)(at - s) : n;
+  const char *slash = memchr(s, '/', name_n);
+  size_t reg_b = 0, reg_n = 0, rest_b = 0;
+  int explicit_reg = 0;
+  if (slash) {
+    size_t c0 = (size_t)(slash - s);
+    int isreg = (memchr(s, '.', c0) != NULL) || (memchr(s, ':', c0) != NULL) ||
+                (c0 == 9 && memcmp(s, "localhost", 9) == 0);
+    if (isreg) {
+      explicit_reg = 1;
+      reg_b = 0;
+      reg_n = c0;
+      rest_b = c0 + 1;
+    }
+  }
+  if (explicit_reg) {
+    memcpy(registry, s + reg_b, reg_n);
+    registry[reg_n] = 0;
+  } else {
+    strcpy(registry, "docker.io");
+  }
+  size_t rest_n = name_n - rest_b;
+  const char *rest = s + rest_b;
+  const char *colon = NULL;
+  for (size_t i = rest_n; i > 0; --i)
+    if (rest[i - 1] == ':') {
+      colon = rest + i - 1;
+      break;
+    }
+  size_t path_n = colon ? (size_t)(colon - rest) : rest_n;
+  int has_tag = colon != NULL;
+  int is_docker = strcmp(registry, "docker.io") == 0;
+  int path_slash = memchr(rest, '/', path_n) != NULL;
+  int eff_tag = 1;
+  if (has_tag) {
+    size_t tn = rest_n - path_n - 1;
+    memcpy(tag, colon + 1, tn);
+    tag[tn] = 0;
+  } else if (!at) {
+    strcpy(tag, "latest");
+  } else {
+    tag[0] = 0;
+    eff_tag = 0;
+  }
+  char *w = norm;
+  size_t rl = strlen(registry);
+  memcpy(w, registry, rl);
+  w += rl;
+  *w++ = '/';
+  if (is_docker && !path_slash) {
+    memcpy(w, "library/", 8);
+    w += 8;
+  }
+  memcpy(w, rest, path_n);
+  w += path_n;
+  if (eff_tag) {
+    *w++ = ':';
+    size_t tl = strlen(tag);
+    memcpy(w, tag, tl);
+    w += tl;
+  }
+  if (at) {
+    size_t dn = n - name_n;
+    memcpy(w, at, dn); /* '@' + digest */
+    w += dn;
+  }
+  *w = 0;
+  return eff_tag;
+}
+
+/* ------------------------------------------------------------------ families */
+/* reason arguments saturate: one index to 16 bits, a pair of indices to 8 bits each */
+static uint32_t pack1(uint32_t a) { return a < 65535u ? a : 65535u; }
+static uint32_t pack2(uint32_t a, uint32_t b) { return ((a < 255u ? a : 255u) << 8) | (b < 255u ? b : 255u); }
+
+typedef struct {
+  uint32_t reason, arg, mutated;
+} fam_out;
+
+static int ctr_considered(const orc_policy *P, uint8_t f) {
+  if ((P->flags & 1) && (f & KW_CTR_INIT)) return 0;
+  if ((P->flags & 2) && (f & KW_CTR_EPHEMERAL)) return 0;
+  return 1;
+}
+
+static fam_out fam_privileged(const orc_policy *P, const kw_soa *S, uint64_t r) {
+  fam_out o = {0, 0, 0};
+  if (!(S->req_flags[r] & KW_REQ_HAS_PODSPEC)) return o;
+  for (uint32_t c = S->ctr_off[r]; c < S->ctr_off[r + 1]; ++c) {
+    uint8_t f = S->ctr_flags[c];
+    if (ctr_considered(P, f) && (f & KW_CTR_PRIVILEGED)) {
+      o.reason = KW_R_PRIVILEGED;
+      o.arg = pack1(c - S->ctr_off[r]);
+      return o;
+    }
+  }
+  return o;
+}
+
+static fam_out fam_namespace(const orc_policy *P, const kw_soa *S, uint64_t r) {
+  fam_out o = {0, 0, 0};
+  sv ns = col(&S->ns, r);
+  int ok = (S->req_flags[r] & KW_REQ_HAS_NAMESPACE) && P->n[0] > 0 && sv_eq(ns, P->l[0][0]);
+  if (!ok) o.reason = KW_R_NAMESPACE;
+  return o;
+}
+
+static fam_out fam_trusted(const orc_policy *P, const kw_soa *S, uint64_t r, zbuf *zb) {
+  fam_out o = {0, 0, 0};
+  if (!(S->req_flags[r] & KW_REQ_HAS_PODSPEC)) return o;
+  char sreg[512], stag[512], snorm[1024];
+  for (uint32_t c = S->ctr_off[r]; c < S->ctr_off[r + 1]; ++c) {
+    uint8_t f = S->ctr_flags[c];
+    if (!(f & KW_CTR_HAS_IMAGE)) continue;
+    sv im = col(&S->ctr_image, c);
+    char *reg = sreg, *tag = stag, *norm = snorm, *heap = NULL;
+    if (im.n + 32 > sizeof(sreg)) { /* long references: scratch on the heap */
+      heap = (char *)malloc(4 * (size_t)im.n + 128);
+      reg = heap;
+      tag = heap + im.n + 32;
+      norm = heap + 2 * (size_t)im.n + 64;
+    }
+    int eff = orc_image_parts(z(zb, im), reg, tag, norm, 0);
+    uint32_t why = 0;
+    if (P->n[0] > 0 && !any_glob(P->l[0], P->n[0], reg))
+      why = KW_R_REG_NOT_ALLOWED;
+    else if (P->n[1] > 0 && any_glob(P->l[1], P->n[1], reg))
+      why = KW_R_REG_REJECTED;
+    else if (eff && P->n[2] > 0 && any_glob(P->l[2], P->n[2], tag))
+      why = KW_R_TAG_REJECTED;
+    else if (P->n[3] > 0 && !any_glob(P->l[3], P->n[3], norm))
+      why = KW_R_IMG_NOT_ALLOWED;
+    else if (P->n[4] > 0 && any_glob(P->l[4], P->n[4], norm))
+      why = KW_R_IMG_REJECTED;
+    free(heap);
+    if (why) {
+      o.reason = why;
+      o.arg = pack1(c - S->ctr_off[r]);
+      return o;
+    }
+  }
+  return o;
+}
+
+static fam_out fam_caps(const orc_policy *P, const kw_soa *S, uint64_t r) {
+  fam_out o = {0, 0, 0};
+  if (!(S->req_flags[r] & KW_REQ_HAS_PODSPEC)) return o;
+  int allow_all = (P->flags & 4) != 0;
+  /* validation: every added capability must be allowed (allowed_capabilities or
+     default_add_capabilities), unless allowed_capabilities contains "*" */
+  for (uint32_t c = S->ctr_off[r]; c < S->ctr_off[r + 1]; ++c) {
+    if (allow_all) break;
+    for (uint32_t k = S->capadd_off[c]; k < S->capadd_off[c + 1]; ++k) {
+      sv cap = col(&S->cap_add, k);
+      if (!any_eq(P->l[0], P->n[0], cap) && !any_eq(P->l[2], P->n[2], cap)) {
+        o.reason = KW_R_CAP_NOT_ALLOWED;
+        o.arg = pack2(c - S->ctr_off[r], k - S->capadd_off[c]);
+        return o;
+      }
+    }
+  }
+  /* mutation: a container that does not drop a required capability (and does not drop ALL), or
+     that neither adds nor drops a default capability, gets a patch */
+  for (uint32_t c = S->ctr_off[r]; c < S->ctr_off[r + 1]; ++c) {
+    int drop_all = 0;
+    for (uint32_t k = S->capdrop_off[c]; k < S->capdrop_off[c + 1]; ++k)
+      if (sv_eq(col(&S->cap_drop, k), "ALL")) drop_all = 1;
+    for (int32_t i = 0; i < P->n[1] && !drop_all; ++i) {
+      int dropped = 0;
+      for (uint32_t k = S->capdrop_off[c]; k < S->capdrop_off[c + 1]; ++k)
+        if (sv_eq(col(&S->cap_drop, k), P->l[1][i])) dropped = 1;
+      if (!dropped) o.mutated = 1;
+    }
+    for (int32_t i = 0; i < P->n[2]; ++i) {
+      int seen = 0;
+      for (uint32_t k = S->capadd_off[c]; k < S->capadd_off[c + 1]; ++k)
+        if (sv_eq(col(&S->cap_add, k), P->l[2][i])) seen = 1;
+      for (uint32_t k = S->capdrop_off[c]; k < S->capdrop_off[c + 1]; ++k)
+        if (sv_eq(col(&S->cap_drop, k), P->l[2][i])) seen = 1;
+      if (!seen) o.mutated = 1;
+    }
+  }
+  return o;
+}
+
+static fam_out fam_apparmor(const orc_policy *P, const kw_soa *S, uint64_t r) {
+  fam_out o = {0, 0, 0};
+  if (!(S->req_flags[r] & KW_REQ_HAS_PODSPEC)) return o;
+  for (uint32_t c = S->ctr_off[r]; c < S->ctr_off[r + 1]; ++c) {
+    if (!(S->ctr_flags[c] & KW_CTR_HAS_APPARMOR)) continue;
+    if (!any_eq(P->l[0], P->n[0], col(&S->ctr_apparmor, c))) {
+      o.reason = KW_R_APPARMOR;
+      o.arg = pack1(c - S->ctr_off[r]);
+      return o;
+    }
+  }
+  return o;
+}
+
+static fam_out fam_labels(const orc_env *e, int32_t p, const kw_soa *S, uint64_t r, zbuf *zb) {
+  const orc_policy *P = &e->pol[p];
+  fam_out o = {0, 0, 0};
+  for (uint32_t l = S->lbl_off[r]; l < S->lbl_off[r + 1]; ++l) {
+    sv key = col(&S->lbl_key, l);
+    if (any_eq(P->l[0], P->n[0], key)) {
+      o.reason = KW_R_LABEL_DENIED;
+      o.arg = pack1(l - S->lbl_off[r]);
+      return o;
+    }
+    for (int32_t i = 0; i < P->n[2]; ++i) {
+      if (!sv_eq(key, P->l[2][i])) continue;
+      if (regexec(&e->re[p][i], z(zb, col(&S->lbl_val, l)), 0, NULL, 0) != 0) {
+        o.reason = KW_R_LABEL_CONSTRAINT;
+        o.arg = pack2(l - S->lbl_off[r], (uint32_t)i);
+        return o;
+      }
+    }
+  }
+  for (int32_t i = 0; i < P->n[1]; ++i) {
+    int present = 0;
+    for (uint32_t l = S->lbl_off[r]; l < S->lbl_off[r + 1]; ++l)
+      if (sv_eq(col(&S->lbl_key, l), P->l[1][i])) present = 1;
+    if (!present) {
+      o.reason = KW_R_LABEL_MANDATORY;
+      o.arg = (uint32_t)i;
+      return o;
+    }
+  }
+  return o;
+}
+
+static fam_out eval_family(const orc_env *e, int32_t p, const kw_soa *S, uint64_t r, zbuf *zb) {
+  const orc_policy *P = &e->pol[p];
+  fam_out none = {0, 0, 0};
+  switch (P->family) {
+  case ORC_F_PRIVILEGED: return fam_privileged(P, S, r);
+  case ORC_F_NAMESPACE: return fam_namespace(P, S, r);
+  case ORC_F_TRUSTED_REPOS: return fam_trusted(P, S, r, zb);
+  case ORC_F_CAPABILITIES: return fam_caps(P, S, r);
+  case ORC_F_APPARMOR: return fam_apparmor(P, S, r);
+  case ORC_F_LABELS: return fam_labels(e, p, S, r, zb);
+  default: return none;
+  }
+}
+
+/* ------------------------------------------------------------------ groups (short-circuit) */
+typedef struct {
+  const orc_env *e;
+  const orc_policy *G;
+  const kw_soa *S;
+  uint64_t r;
+  zbuf *zb;
+  uint32_t done, ok, causes;
+} gctx;
+
+/* member "returns true" iff allowed and not mutated (a patch inside a group is refused,
+   integration_test.rs:247-250); evaluation is lazy, as rhai evaluates || and && */
+static int gcall(gctx *g, int32_t slot) {
+  if (!((g->done >> slot) & 1)) {
+    fam_out fo = eval_family(g->e, g->G->members[slot], g->S, g->r, g->zb);
+    int ok = fo.reason == 0 && !fo.mutated;
+    g->done |= 1u << slot;
+    if (ok) g->ok |= 1u << slot;
+    else g->causes |= 1u << slot;
+  }
+  return (g->ok >> slot) & 1;
+}
+static int geval(gctx *g, int32_t n) {
+  const orc_xnode *x = &g->G->nodes[n];
+  switch (x->op) {
+  case ORC_X_CONST: return x->a != 0;
+  case ORC_X_CALL: return gcall(g, x->a);
+  case ORC_X_NOT: return !geval(g, x->a);
+  case ORC_X_AND: return geval(g, x->a) ? geval(g, x->b) : 0;
+  case ORC_X_OR: return geval(g, x->a) ? 1 : geval(g, x->b);
+  case ORC_X_EQ: { int l = geval(g, x->a); return l == geval(g, x->b); }
+  case ORC_X_NE: { int l = geval(g, x->a); return l != geval(g, x->b); }
+  }
+  return 0;
+}
+
+/* ------------------------------------------------------------------ service::evaluate */
+static uint32_t verdict(const orc_env *e, int32_t p, const kw_soa *S, uint64_t r, int32_t origin,
+                        zbuf *zb) {
+  const orc_policy *P = &e->pol[p];
+  /* namespace bypass first (service.rs:40-71): AdmissionRequest only */
+  if (e->always_ns && !(S->req_flags[r] & KW_REQ_RAW) && (S->req_flags[r] & KW_REQ_HAS_NAMESPACE) &&
+      sv_eq(col(&S->ns, r), e->always_ns))
+    return KW_V_ALLOWED | KW_F_ALLOWED | KW_BYPASS;
+  /* PolicyInitialization -> reject(uid, msg, 500), before any constraint (service.rs:78-91) */
+  if (P->init_error)
+    return ((uint32_t)KW_FST_INIT_ERROR << KW_F_STATUS_SHIFT) | ((uint32_t)KW_R_INIT_ERROR << 8);
+  uint32_t reason = 0, arg = 0, mutated = 0;
+  if (P->family == ORC_F_GROUP) {
+    if (P->expr_error) {
+      reason = KW_R_GROUP_EXPR;
+    } else {
+      gctx g = {e, P, S, r, zb, 0, 0, 0};
+      int res = geval(&g, P->n_nodes - 1);
+      if (!res) {
+        reason = KW_R_GROUP;
+        arg = g.causes;
+      }
+    }
+  } else {
+    fam_out fo = eval_family(e, p, S, r, zb);
+    reason = fo.reason;
+    arg = fo.arg;
+    mutated = fo.mutated;
+  }
+  uint32_t v = (reason << 8) | ((arg & 0xffffu) << 16);
+  int allowed = reason == 0;
+  if (allowed) v |= KW_V_ALLOWED;
+  if (mutated) v |= KW_V_MUTATED;
+  /* validation_response_with_constraints (service.rs:160-208) for the Validate origin only */
+  uint32_t fst = allowed ? KW_FST_NONE : KW_FST_VANILLA;
+  int fallowed = allowed;
+  if (origin == KW_ORIGIN_VALIDATE) {
+    if (P->mode == KW_MODE_MONITOR) {
+      fallowed = 1;
+      fst = KW_FST_NONE;
+    } else if (mutated && !P->allowed_to_mutate) {
+      fallowed = 0;
+      fst = KW_FST_MUTATION_REFUSED;
+    }
+  }
+  if (fallowed) v |= KW_F_ALLOWED;
+  if (mutated && fst == KW_FST_NONE && (origin == KW_ORIGIN_AUDIT || P->mode == KW_MODE_PROTECT)) v |= KW_F_PATCH;
+  v |= fst << KW_F_STATUS_SHIFT;
+  return v;
+}
+
+void orc_eval(const orc_env *e, const kw_soa *S, const int32_t *pols, int32_t npol, int32_t origin,
+              uint64_t row0, uint64_t row1, uint32_t *out) {
+  zbuf zb;
+  zb.big = NULL;
+  for (uint64_t r = row0; r < row1; ++r)
+    for (int32_t j = 0; j < npol; ++j) out[r * (uint64_t)npol + (uint64_t)j] = verdict(e, pols[j], S, r, origin, &zb);
+  free(zb.big);
+}
+
+typedef struct {
+  const orc_env *e;
+  const kw_soa *S;
+  const int32_t *pols;
+  int32_t npol, origin;
+  uint64_t r0, r1;
+  uint32_t *out;
+} mt_arg;
+static void *mt_main(void *a_) {
+  mt_arg *a = (mt_arg *)a_;
+  orc_eval(a->e, a->S, a->pols, a->npol, a->origin, a->r0, a->r1, a->out);
+  return NULL;
+}
+void orc_eval_mt(const orc_env *e, const kw_soa *S, const int32_t *pols, int32_t npol,
+                 int32_t origin, uint64_t nrows, int threads, uint32_t *out) {
+  if (threads < 1) threads = 1;
+  pthread_t *th = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+  mt_arg *args = (mt_arg *)calloc((size_t)threads, sizeof(mt_arg));
+  for (int t = 0; t < threads; ++t) {
+    args[t].e = e;
+    args[t].S = S;
+    args[t].pols = pols;
+    args[t].npol = npol;
+    args[t].origin = origin;
+    args[t].r0 = nrows * (uint64_t)t / (uint64_t)threads;
+    args[t].r1 = nrows * (uint64_t)(t + 1) / (uint64_t)threads;
+    args[t].out = out;
+    pthread_create(&th[t], NULL, mt_main, &args[t]);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+  free(th);
+  free(args);
+}

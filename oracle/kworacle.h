@@ -1,0 +1,97 @@
+/*
+ * kworacle.h — CPU restatement of the declarative-policy hot path. TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library, and
+ * only as the checker / the timed CPU baseline — never as a product path. The product
+ * (libkwgpu.so) has no link to it and fails loudly without its HIP kernels.
+ *
+ * What it restates (reference file:line):
+ *   - EvaluationEnvironment::validate_policy dispatch (src/evaluation/evaluation_environment.rs:546-581)
+ *   - the per-policy arithmetic of the declarative class, which upstream lives in Wasm modules that
+ *     are NOT in /root/reference (policy-evaluator v0.24.0 @ f097b70a, Cargo.lock:4308-4347; OCI
+ *     modules named in policies.yml.example:1-33). Parity for these families is UNPINNED: the
+ *     semantics follow the spec in DESIGN.md §"Policy families", except pod-privileged whose
+ *     message is pinned by tests/integration_test.rs:58-68.
+ *   - service::evaluate namespace bypass + validation_response_with_constraints
+ *     (src/api/service.rs:40-71, 78-91, 108-116, 160-208): pinned by service.rs:285-718.
+ *   - PolicyGroupEvaluator short-circuit semantics [upstream, rhai 1.21.0] as exercised by
+ *     evaluation_environment.rs:979-1042 and integration_test.rs:101-131, 204-251.
+ * It consumes the kw_soa columns declared in include/kwgpu.h (the boundary's data format) and an
+ * oracle-side policy description built by oracle/oracle.py from the parsed policies document.
+ * Strings are matched with libc fnmatch(3) (globs) and POSIX regcomp/regexec (REG_EXTENDED) —
+ * an implementation independent of the product's DFA compiler.
+ */
+#ifndef KWORACLE_H
+#define KWORACLE_H
+#include <stdint.h>
+#include "../include/kwgpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  ORC_F_PRIVILEGED = 1,
+  ORC_F_NAMESPACE = 2,
+  ORC_F_TRUSTED_REPOS = 3,
+  ORC_F_CAPABILITIES = 4,
+  ORC_F_APPARMOR = 5,
+  ORC_F_LABELS = 6,
+  ORC_F_GROUP = 7
+};
+
+/* group expression tree node (built by oracle.py's own parser of the rhai subset) */
+enum { ORC_X_CONST = 0, ORC_X_CALL = 1, ORC_X_NOT = 2, ORC_X_AND = 3, ORC_X_OR = 4, ORC_X_EQ = 5, ORC_X_NE = 6 };
+typedef struct orc_xnode {
+  int32_t op;
+  int32_t a; /* CONST: 0/1; CALL: member slot; NOT/AND/OR/EQ/NE: left child */
+  int32_t b; /* AND/OR/EQ/NE: right child */
+} orc_xnode;
+
+typedef struct orc_policy {
+  int32_t family;
+  int32_t mode;              /* KW_MODE_* */
+  int32_t allowed_to_mutate;
+  int32_t init_error;        /* PolicyInitialization recorded under continue_on_errors */
+  int32_t expr_error;        /* group: expression does not evaluate to a bool */
+  int32_t flags;             /* bit0 skip_init_containers, bit1 skip_ephemeral_containers,
+                                bit2 allowed_capabilities contains "*" */
+  /* string lists (meaning per family):
+     namespace:     l0 = [valid_namespace]
+     trusted-repos: l0 reg allow, l1 reg reject, l2 tag reject, l3 image allow, l4 image reject (globs)
+     capabilities:  l0 allowed, l1 required_drop, l2 default_add
+     apparmor:      l0 allowed_profiles
+     labels:        l0 denied, l1 mandatory, l2 constrained keys, l3 constrained regexes */
+  int32_t n[5];
+  const char *const *l[5];
+  /* group */
+  int32_t n_members;
+  const int32_t *members;   /* policy indices, settings order */
+  int32_t n_nodes;
+  const orc_xnode *nodes;   /* root = nodes[n_nodes-1] */
+} orc_policy;
+
+typedef struct orc_env orc_env;
+/* Compiles the regexes once; returns NULL and writes err on an invalid regex. */
+orc_env *orc_env_new(const orc_policy *policies, int32_t npol, const char *always_accept_ns,
+                     char *err, int errlen);
+void orc_env_free(orc_env *e);
+
+/* Verdict words (include/kwgpu.h layout) for rows [row0,row1) x policies, row-major. */
+void orc_eval(const orc_env *e, const kw_soa *soa, const int32_t *policies, int32_t npol,
+              int32_t origin, uint64_t row0, uint64_t row1, uint32_t *out);
+/* Same, split over `threads` POSIX threads (the CPU baseline). */
+void orc_eval_mt(const orc_env *e, const kw_soa *soa, const int32_t *policies, int32_t npol,
+                 int32_t origin, uint64_t nrows, int threads, uint32_t *out);
+
+/* 1 if POSIX regcomp(REG_EXTENDED) accepts the pattern. */
+int orc_regex_ok(const char *pattern);
+
+/* Image reference normalisation; writes NUL-terminated parts.
+   Returns 1 if an effective tag exists. */
+int orc_image_parts(const char *image, char *registry, char *tag, char *normalized, int cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,766 @@
+"""oracle.py — CPU restatement of the hot path, Python half. TEST INFRASTRUCTURE ONLY.
+
+May be imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, as the
+checker or the timed CPU baseline; never by the product (policy-server_amd/kwgpu never imports it).
+
+Restates, independently of the product's C++ (env.cpp / expr.cpp / service.cpp):
+  * PolicyID::from_str / Display                     src/evaluation/policy_id.rs:20-47
+  * policies document schema + validate_policies      src/config.rs:237-258, 287-453
+  * EvaluationEnvironmentBuilder::build (continue_on_errors, member Protect/no-mutate)
+                                                      src/evaluation/evaluation_environment.rs:198-365
+  * validation_response_with_constraints              src/api/service.rs:160-208
+  * service::evaluate response shapes                 src/api/service.rs:30-152
+  * PolicyGroupEvaluator expression language (rhai subset, short-circuit) [upstream rhai 1.21.0],
+    as pinned by evaluation_environment.rs:979-1112 and integration_test.rs:101-131, 204-251
+  * policy-family settings rules and message templates: DESIGN.md §Policy families — parity
+    UNPINNED for the families (their Wasm source is not in /root/reference), except the
+    pod-privileged message pinned by integration_test.rs:58-68.
+The per-request family arithmetic runs in oracle/kworacle.c (libc fnmatch + POSIX regex).
+"""
+import ctypes as C
+import json
+import os
+import re
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "libkworacle.so")
+
+PROTECT, MONITOR = 0, 1
+VALIDATE, AUDIT = 0, 1
+F_PRIV, F_NS, F_TRUSTED, F_CAPS, F_AA, F_LABELS, F_GROUP = 1, 2, 3, 4, 5, 6, 7
+X_CONST, X_CALL, X_NOT, X_AND, X_OR, X_EQ, X_NE = 0, 1, 2, 3, 4, 5, 6
+
+R_PRIVILEGED, R_NAMESPACE, R_REG_NOT_ALLOWED, R_REG_REJECTED, R_TAG_REJECTED = 1, 2, 3, 4, 5
+R_IMG_NOT_ALLOWED, R_IMG_REJECTED, R_CAP, R_APPARMOR = 6, 7, 8, 9
+R_LABEL_DENIED, R_LABEL_CONSTRAINT, R_LABEL_MANDATORY, R_GROUP, R_GROUP_EXPR, R_INIT = 10, 11, 12, 13, 14, 15
+
+
+# ----------------------------------------------------------------------------- PolicyID
+class InvalidPolicyId(Exception):
+    pass
+
+
+def parse_policy_id(s):
+    """policy_id.rs:29-47 -> ("policy", name) | ("member", group, name)."""
+    if s == "":
+        raise InvalidPolicyId("Not a valid Policy ID: ")
+    parts = s.split("/")
+    if len(parts) == 1:
+        return ("policy", s)
+    if len(parts) == 2:
+        return ("member", parts[0], parts[1])
+    raise InvalidPolicyId(f"Not a valid Policy ID: {s}")
+
+
+def policy_id_display(pid):
+    return pid[1] if pid[0] == "policy" else f"{pid[1]}/{pid[2]}"
+
+
+# ----------------------------------------------------------------------------- constraints
+def constraints(policy_id, mode, allowed_to_mutate, resp):
+    """validation_response_with_constraints (service.rs:160-208) on a response dict."""
+    resp = dict(resp)
+    if mode == PROTECT:
+        if resp.get("patch") is not None and not allowed_to_mutate:
+            resp["allowed"] = False
+            resp["status"] = {"message": f"Request rejected by policy {policy_id}. The policy attempted to mutate "
+                                         f"the request, but it is currently configured to not allow mutations."}
+            resp.pop("patch", None)
+            resp.pop("patchType", None)
+        return resp
+    resp["allowed"] = True
+    for k in ("patch", "patchType", "status"):
+        resp.pop(k, None)
+    return resp
+
+
+# ----------------------------------------------------------------------------- schema
+class ConfigError(Exception):
+    pass
+
+
+def _is_str_list(v):
+    return isinstance(v, list) and all(isinstance(x, str) for x in v)
+
+
+def _family(module):
+    for key, fam in (("pod-privileged", F_PRIV), ("namespace-validate", F_NS), ("trusted-repos", F_TRUSTED),
+                     ("psp-capabilities", F_CAPS), ("psp-apparmor", F_AA), ("safe-labels", F_LABELS)):
+        if key in module:
+            return fam
+    return 0
+
+
+def _ctx_ok(v):
+    if v is None:
+        return True
+    return isinstance(v, list) and all(isinstance(x, dict) and isinstance(x.get("apiVersion"), str)
+                                       and isinstance(x.get("kind"), str) for x in v)
+
+
+def _mode(v):
+    if v is None:
+        return PROTECT
+    if v == "protect":
+        return PROTECT
+    if v == "monitor":
+        return MONITOR
+    raise ValueError(v)
+
+
+def parse_entry(name, v):
+    """Untagged PolicyOrPolicyGroup (config.rs:360-394)."""
+    if isinstance(v, dict):
+        try:
+            if isinstance(v.get("module"), str):
+                mode = _mode(v.get("policyMode"))
+                a2m = v.get("allowedToMutate")
+                if a2m is not None and not isinstance(a2m, bool):
+                    raise ValueError
+                st = v.get("settings")
+                if st is not None and not isinstance(st, dict):
+                    raise ValueError
+                if not _ctx_ok(v.get("contextAwareResources")):
+                    raise ValueError
+                return {"name": name, "group": False, "module": v["module"], "mode": mode, "a2m": bool(a2m),
+                        "settings": st or {}}
+        except ValueError:
+            pass
+        try:
+            mode = _mode(v.get("policyMode"))
+            pols, ex, msg = v.get("policies"), v.get("expression"), v.get("message")
+            if isinstance(pols, dict) and isinstance(ex, str) and isinstance(msg, str):
+                members = []
+                for mn, mv in pols.items():
+                    if not isinstance(mv, dict) or set(mv) - {"module", "settings", "contextAwareResources"}:
+                        raise ValueError
+                    if not isinstance(mv.get("module"), str):
+                        raise ValueError
+                    if mv.get("settings") is not None and not isinstance(mv.get("settings"), dict):
+                        raise ValueError
+                    if not _ctx_ok(mv.get("contextAwareResources")):
+                        raise ValueError
+                    members.append({"name": mn, "module": mv["module"], "settings": mv.get("settings") or {}})
+                return {"name": name, "group": True, "mode": mode, "expression": ex, "message": msg,
+                        "members": members}
+        except ValueError:
+            pass
+    raise ConfigError("data did not match any variant of untagged enum PolicyOrPolicyGroup")
+
+
+def validate_policies(entries):
+    """config.rs:237-258"""
+    for e in entries:
+        if "/" in e["name"]:
+            raise ConfigError(f"policy name '{e['name']}' contains a '/' character")
+        if e["group"]:
+            bad = [m["name"] for m in e["members"] if "/" in m["name"]]
+            if bad:
+                raise ConfigError(f"policy group '{e['name']}' contains policies with invalid names: "
+                                  + "[" + ", ".join(f'"{b}"' for b in bad) + "]")
+
+
+# ----------------------------------------------------------------------------- settings
+def _translate_regex(r):
+    """Rust-style \\d / \\D to POSIX bracket expressions for regcomp (outside brackets)."""
+    out, i, inb = [], 0, False
+    while i < len(r):
+        c = r[i]
+        if inb:
+            out.append(c)
+            if c == "]":
+                inb = False
+            i += 1
+            continue
+        if c == "[":
+            inb = True
+            out.append(c)
+            i += 1
+            if i < len(r) and r[i] == "^":
+                out.append("^")
+                i += 1
+            if i < len(r) and r[i] == "]":
+                out.append("]")
+                i += 1
+            continue
+        if c == "\\" and i + 1 < len(r) and r[i + 1] in "dD":
+            out.append("[0-9]" if r[i + 1] == "d" else "[^0-9]")
+            i += 2
+            continue
+        if c == "\\" and i + 1 < len(r):
+            out.append(r[i:i + 2])
+            i += 2
+            continue
+        out.append(c)
+        i += 1
+    return "".join(out)
+
+
+def compile_settings(fam, s, olib):
+    """Returns (lists[5], flags) or raises ValueError(message) -> 'Policy settings are invalid: ...'."""
+    L = [[], [], [], [], []]
+    flags = 0
+
+    def lst(obj, key, path):
+        if obj is None:
+            return []
+        v = obj.get(key)
+        if v is None:
+            return []
+        if not _is_str_list(v):
+            raise ValueError(f"{path} must be a list of strings")
+        return list(v)
+
+    def obj_of(key, path):
+        v = s.get(key)
+        if v is None:
+            return None
+        if not isinstance(v, dict):
+            raise ValueError(f"{path} must be a mapping")
+        return v
+
+    if fam == F_PRIV:
+        for k, bit in (("skip_init_containers", 1), ("skip_ephemeral_containers", 2)):
+            v = s.get(k)
+            if v is None:
+                continue
+            if not isinstance(v, bool):
+                raise ValueError(f"{k} must be a boolean")
+            if v:
+                flags |= bit
+    elif fam == F_NS:
+        v = s.get("valid_namespace")
+        if not isinstance(v, str) or v == "":
+            raise ValueError("valid_namespace must be a non-empty string")
+        L[0] = [v]
+    elif fam == F_TRUSTED:
+        reg, tags, imgs = obj_of("registries", "registries"), obj_of("tags", "tags"), obj_of("images", "images")
+        L[0], L[1] = lst(reg, "allow", "registries.allow"), lst(reg, "reject", "registries.reject")
+        L[2] = lst(tags, "reject", "tags.reject")
+        L[3], L[4] = lst(imgs, "allow", "images.allow"), lst(imgs, "reject", "images.reject")
+        if L[0] and L[1]:
+            raise ValueError("registries: allow and reject lists are mutually exclusive")
+        if L[3] and L[4]:
+            raise ValueError("images: allow and reject lists are mutually exclusive")
+    elif fam == F_CAPS:
+        L[0] = lst(s, "allowed_capabilities", "allowed_capabilities")
+        L[1] = lst(s, "required_drop_capabilities", "required_drop_capabilities")
+        L[2] = lst(s, "default_add_capabilities", "default_add_capabilities")
+        if "*" in L[0]:
+            flags |= 4
+        overlap = [c for c in L[2] if c in L[1]]
+        if overlap:
+            raise ValueError("these capabilities cannot be both added by default and required to be dropped: "
+                             + ", ".join(overlap))
+    elif fam == F_AA:
+        L[0] = lst(s, "allowed_profiles", "allowed_profiles")
+    elif fam == F_LABELS:
+        L[0] = lst(s, "denied_labels", "denied_labels")
+        L[1] = lst(s, "mandatory_labels", "mandatory_labels")
+        c = obj_of("constrained_labels", "constrained_labels")
+        for k, v in (c or {}).items():
+            if not isinstance(v, str):
+                raise ValueError("constrained_labels values must be strings")
+            if not olib.orc_regex_ok(_translate_regex(v).encode()):
+                raise ValueError(f"constrained label '{k}' has an invalid regular expression")
+            L[2].append(k)
+            L[3].append(v)
+        for k in L[0]:
+            if k in L[1] or k in L[2]:
+                raise ValueError(f"label '{k}' cannot be both denied and mandatory or constrained")
+        if len(L[1]) > 16 or len(L[2]) > 16:
+            raise ValueError("at most 16 mandatory and 16 constrained labels are supported")
+    return L, flags
+
+
+# ----------------------------------------------------------------------------- group expressions
+_TOK = re.compile(r"\s*(?:(?P<id>[A-Za-z_][A-Za-z0-9_]*)|(?P<int>[0-9][0-9_]*)|(?P<op>\|\||&&|==|!=|<=|>=|[<>+\-*/%!()]))")
+
+
+class ExprError(Exception):
+    pass
+
+
+def _lex(s):
+    toks, i = [], 0
+    while i < len(s):
+        if s[i].isspace():
+            i += 1
+            continue
+        m = _TOK.match(s, i)
+        if not m or m.end() == i:
+            raise ExprError(f"Syntax error: unexpected character '{s[i]}'")
+        if m.group("id"):
+            toks.append(("id", m.group("id")))
+        elif m.group("int"):
+            digits = m.group("int").replace("_", "")
+            if len(digits) > 18:
+                raise ExprError("Syntax error: integer literal too large")
+            toks.append(("int", int(digits)))
+        else:
+            toks.append(("op", m.group("op")))
+        i = m.end()
+    toks.append(("end", None))
+    return toks
+
+
+def parse_expression(s, members):
+    """rhai subset -> typed AST with constant folding. Node: ('const', type, value) | ('call', slot) |
+    ('not', a) | ('and'|'or'|'eq'|'ne', a, b). Raises ExprError (validation failure)."""
+    toks = _lex(s)
+    pos = [0]
+
+    def peek():
+        return toks[pos[0]]
+
+    def take():
+        t = toks[pos[0]]
+        pos[0] += 1
+        return t
+
+    def isop(*ops):
+        t = peek()
+        return t[0] == "op" and t[1] in ops
+
+    def typ(n):
+        return n[1] if n[0] == "const" else "bool"
+
+    def fold_bin(op, a, b):
+        ta, tb = typ(a), typ(b)
+        if op in ("&&", "||"):
+            if ta != "bool" or tb != "bool":
+                raise ExprError(f"Function not found: {op} ({ta}, {tb})")
+            if a[0] == "const" and b[0] == "const":
+                return ("const", "bool", (a[2] and b[2]) if op == "&&" else (a[2] or b[2]))
+            return ("and" if op == "&&" else "or", a, b)
+        if op in ("==", "!="):
+            if ta != tb:
+                raise ExprError(f"Function not found: {op} ({ta}, {tb})")
+            if a[0] == "const" and b[0] == "const":
+                return ("const", "bool", (a[2] == b[2]) == (op == "=="))
+            return ("eq" if op == "==" else "ne", a, b)
+        if ta != "i64" or tb != "i64":
+            raise ExprError(f"Function not found: {op} ({ta}, {tb})")
+        x, y = a[2], b[2]
+        if op in ("<", "<=", ">", ">="):
+            return ("const", "bool", {"<": x < y, "<=": x <= y, ">": x > y, ">=": x >= y}[op])
+        if op in ("/", "%") and y == 0:
+            raise ExprError("Division by zero")
+        if op == "/":
+            v = abs(x) // abs(y) * (1 if (x >= 0) == (y >= 0) else -1)
+        elif op == "%":
+            v = abs(x) % abs(y) * (1 if x >= 0 else -1)
+        else:
+            v = {"+": x + y, "-": x - y, "*": x * y}[op]
+        return ("const", "i64", v)
+
+    def binary(sub, ops):
+        a = sub()
+        while isop(*ops):
+            op = take()[1]
+            b = sub()
+            a = fold_bin(op, a, b)
+        return a
+
+    def orx():
+        return binary(andx, ("||",))
+
+    def andx():
+        return binary(cmp, ("&&",))
+
+    def cmp():
+        return binary(add, ("==", "!=", "<", "<=", ">", ">="))
+
+    def add():
+        return binary(mul, ("+", "-"))
+
+    def mul():
+        return binary(unary, ("*", "/", "%"))
+
+    def unary():
+        if isop("!", "-"):
+            op = take()[1]
+            a = unary()
+            if op == "!":
+                if typ(a) != "bool":
+                    raise ExprError("Function not found: ! (i64)")
+                return ("const", "bool", not a[2]) if a[0] == "const" else ("not", a)
+            if typ(a) != "i64":
+                raise ExprError("Function not found: - (bool)")
+            return ("const", "i64", -a[2])
+        return primary()
+
+    def primary():
+        t = take()
+        if t[0] == "int":
+            return ("const", "i64", t[1])
+        if t[0] == "op" and t[1] == "(":
+            e = orx()
+            if not isop(")"):
+                raise ExprError("Syntax error: expecting ')'")
+            take()
+            return e
+        if t[0] == "id":
+            if t[1] in ("true", "false"):
+                return ("const", "bool", t[1] == "true")
+            if not isop("("):
+                raise ExprError(f"Variable not found: {t[1]}")
+            take()
+            if not isop(")"):
+                raise ExprError("Syntax error: member policies take no arguments")
+            take()
+            if t[1] not in members:
+                raise ExprError(f"Function not found: {t[1]} ()")
+            return ("call", members.index(t[1]))
+        raise ExprError("Syntax error: unexpected token")
+
+    root = orx()
+    if peek()[0] != "end":
+        raise ExprError("Syntax error: unexpected trailing input")
+    return root
+
+
+def expr_depth(n, d=1):
+    """Max stack depth of the left-then-right postfix emission (same bound as the product)."""
+    if n[0] in ("const", "call"):
+        return d
+    if n[0] == "not":
+        return expr_depth(n[1], d)
+    return max(expr_depth(n[1], d), expr_depth(n[2], d + 1))
+
+
+def eval_expression(n, member_ok):
+    """Short-circuit evaluation -> (value, called-members list in call order)."""
+    called = []
+
+    def ev(x):
+        k = x[0]
+        if k == "const":
+            return bool(x[2])
+        if k == "call":
+            if x[1] not in called:
+                called.append(x[1])
+            return member_ok[x[1]]
+        if k == "not":
+            return not ev(x[1])
+        if k == "and":
+            return ev(x[1]) and ev(x[2])
+        if k == "or":
+            return ev(x[1]) or ev(x[2])
+        a = ev(x[1])
+        b = ev(x[2])
+        return (a == b) if k == "eq" else (a != b)
+
+    return ev(n), called
+
+
+def _to_nodes(root):
+    nodes = []
+
+    def emit(x):
+        k = x[0]
+        if k == "const":
+            nodes.append((X_CONST, 1 if x[2] else 0, 0))
+        elif k == "call":
+            nodes.append((X_CALL, x[1], 0))
+        elif k == "not":
+            a = emit(x[1])
+            nodes.append((X_NOT, a, 0))
+        else:
+            a = emit(x[1])
+            b = emit(x[2])
+            nodes.append(({"and": X_AND, "or": X_OR, "eq": X_EQ, "ne": X_NE}[k], a, b))
+        return len(nodes) - 1
+
+    emit(root)
+    return nodes
+
+
+# ----------------------------------------------------------------------------- ctypes
+class _Strcol(C.Structure):
+    _fields_ = [("off", C.POINTER(C.c_uint32)), ("bytes", C.POINTER(C.c_uint8)), ("n", C.c_uint64)]
+
+
+class Soa(C.Structure):
+    """kw_soa layout (include/kwgpu.h)."""
+    _fields_ = [
+        ("n_requests", C.c_uint64), ("req_flags", C.POINTER(C.c_uint8)), ("ctr_off", C.POINTER(C.c_uint32)),
+        ("lbl_off", C.POINTER(C.c_uint32)), ("uid", _Strcol), ("ns", _Strcol), ("op", _Strcol), ("kind", _Strcol),
+        ("ctr_flags", C.POINTER(C.c_uint8)), ("capadd_off", C.POINTER(C.c_uint32)),
+        ("capdrop_off", C.POINTER(C.c_uint32)), ("ctr_name", _Strcol), ("ctr_image", _Strcol),
+        ("ctr_apparmor", _Strcol), ("cap_add", _Strcol), ("cap_drop", _Strcol), ("lbl_key", _Strcol),
+        ("lbl_val", _Strcol),
+    ]
+
+
+class _XNode(C.Structure):
+    _fields_ = [("op", C.c_int32), ("a", C.c_int32), ("b", C.c_int32)]
+
+
+class _OPolicy(C.Structure):
+    _fields_ = [("family", C.c_int32), ("mode", C.c_int32), ("allowed_to_mutate", C.c_int32),
+                ("init_error", C.c_int32), ("expr_error", C.c_int32), ("flags", C.c_int32),
+                ("n", C.c_int32 * 5), ("l", C.POINTER(C.c_char_p) * 5), ("n_members", C.c_int32),
+                ("members", C.POINTER(C.c_int32)), ("n_nodes", C.c_int32), ("nodes", C.POINTER(_XNode))]
+
+
+_olib = None
+
+
+def olib():
+    global _olib
+    if _olib is None:
+        L = C.CDLL(LIB)
+        L.orc_env_new.restype = C.c_void_p
+        L.orc_env_new.argtypes = [C.POINTER(_OPolicy), C.c_int32, C.c_char_p, C.c_char_p, C.c_int]
+        L.orc_env_free.argtypes = [C.c_void_p]
+        L.orc_eval.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_int32), C.c_int32, C.c_int32, C.c_uint64,
+                               C.c_uint64, C.POINTER(C.c_uint32)]
+        L.orc_eval_mt.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_int32), C.c_int32, C.c_int32, C.c_uint64,
+                                  C.c_int, C.POINTER(C.c_uint32)]
+        L.orc_image_parts.restype = C.c_int
+        L.orc_image_parts.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_int]
+        L.orc_regex_ok.restype = C.c_int
+        L.orc_regex_ok.argtypes = [C.c_char_p]
+        _olib = L
+    return _olib
+
+
+def image_parts(image):
+    n = len(image.encode()) * 2 + 64
+    reg, tag, norm = C.create_string_buffer(n), C.create_string_buffer(n), C.create_string_buffer(n * 2)
+    eff = olib().orc_image_parts(image.encode(), reg, tag, norm, len(norm))
+    return reg.value.decode(), tag.value.decode() if eff else None, norm.value.decode()
+
+
+# ----------------------------------------------------------------------------- environment
+class OracleEnv:
+    """Restated EvaluationEnvironment. Policy order: top-level entries in document order, then group
+    members (group order, settings order) — the same order the product uses, checked by tests via ids."""
+
+    def __init__(self, policies, continue_on_errors=False, always_accept_namespace=None):
+        L = olib()
+        if isinstance(policies, (str, bytes)):
+            policies = json.loads(policies)
+        entries = [parse_entry(k, v) for k, v in policies.items()]
+        validate_policies(entries)
+        self.always_ns = always_accept_namespace
+        self.pol = []
+        for e in entries:
+            if e["name"] == "":
+                raise InvalidPolicyId("Not a valid Policy ID: ")
+            p = {"id": e["name"], "name": e["name"], "group": e["group"], "member": False, "mode": e["mode"],
+                 "a2m": False, "registered": True, "init_error": None, "family": F_GROUP if e["group"] else 0,
+                 "lists": [[], [], [], [], []], "flags": 0}
+            if e["group"]:
+                p.update(expression=e["expression"], message=e["message"],
+                         member_names=[m["name"] for m in e["members"]], members=[], broken=None)
+            else:
+                p.update(module=e["module"], a2m=e["a2m"], settings=e["settings"])
+            self.pol.append(p)
+        for gi, e in enumerate(entries):
+            if not e["group"]:
+                continue
+            for m in e["members"]:
+                self.pol[gi]["members"].append(len(self.pol))
+                self.pol.append({"id": f"{e['name']}/{m['name']}", "name": m["name"], "group": False,
+                                 "member": True, "parent": gi, "mode": PROTECT, "a2m": False, "registered": True,
+                                 "init_error": None, "module": m["module"], "settings": m["settings"],
+                                 "lists": [[], [], [], [], []], "flags": 0, "family": 0})
+        for p in self.pol:
+            if p["group"]:
+                continue
+            fam = _family(p["module"])
+            err = None
+            if fam == 0:
+                p["registered"] = False
+                err = (f"bootstrap failure: {p['id']}: policy module '{p['module']}' is not in the declarative "
+                       f"policy class served by kwgpu")
+            else:
+                p["family"] = fam
+                try:
+                    p["lists"], p["flags"] = compile_settings(fam, p["settings"], L)
+                except ValueError as ex:
+                    err = f"Policy settings are invalid: {ex}"
+            if err is not None:
+                if not continue_on_errors:
+                    raise ConfigError(err)
+                p["init_error"] = err
+                if p["member"]:
+                    g = self.pol[p["parent"]]
+                    if g["broken"] is None:
+                        g["broken"] = p["id"]
+        for p in self.pol:
+            if not p["group"]:
+                continue
+            p["expr_error"] = None
+            p["ast"] = None
+            try:
+                if len(p["member_names"]) > 16:
+                    raise ExprError("policy groups with more than 16 members are not supported by the engine")
+                ast = parse_expression(p["expression"], p["member_names"])
+                if ast[0] == "const" and ast[1] == "i64":
+                    p["expr_error"] = ("policy group expression did not evaluate to a boolean: Output type "
+                                       "incorrect: i64 (expecting bool)")
+                    p["valid"] = True
+                elif expr_depth(ast) > 16:
+                    raise ExprError("policy group expression nests too deeply for the engine (max stack 16)")
+                else:
+                    p["ast"] = ast
+                    p["valid"] = True
+            except ExprError as ex:
+                p["expr_error"] = str(ex)
+                p["valid"] = False
+        self.ids = {p["id"]: i for i, p in enumerate(self.pol)}
+        self._build_c()
+
+    def _build_c(self):
+        n = len(self.pol)
+        self._arr = (_OPolicy * n)()
+        self._keep = []
+        for i, p in enumerate(self.pol):
+            o = self._arr[i]
+            o.family = p["family"]
+            o.mode = p["mode"]
+            o.allowed_to_mutate = 1 if p["a2m"] else 0
+            o.init_error = 1 if p["init_error"] else 0
+            o.flags = p["flags"]
+            for k in range(5):
+                items = [s.encode() for s in p["lists"][k]]
+                if p["family"] == F_LABELS and k == 3:
+                    items = [_translate_regex(s).encode() for s in p["lists"][k]]
+                arr = (C.c_char_p * max(len(items), 1))(*items)
+                self._keep.append(arr)
+                o.n[k] = len(items)
+                o.l[k] = C.cast(arr, C.POINTER(C.c_char_p))
+            if p["group"]:
+                o.expr_error = 1 if p["expr_error"] else 0
+                mem = (C.c_int32 * max(len(p["members"]), 1))(*p["members"])
+                self._keep.append(mem)
+                o.n_members = len(p["members"])
+                o.members = C.cast(mem, C.POINTER(C.c_int32))
+                if p["ast"] is not None:
+                    nodes = _to_nodes(p["ast"])
+                    xs = (_XNode * len(nodes))(*[_XNode(*t) for t in nodes])
+                    self._keep.append(xs)
+                    o.n_nodes = len(nodes)
+                    o.nodes = C.cast(xs, C.POINTER(_XNode))
+        err = C.create_string_buffer(512)
+        self._h = olib().orc_env_new(self._arr, n, self.always_ns.encode() if self.always_ns else None, err, 512)
+        if not self._h:
+            raise ConfigError("oracle regex compilation failed: " + err.value.decode())
+
+    def __del__(self):
+        try:
+            olib().orc_env_free(self._h)
+        except Exception:
+            pass
+
+    def lookup(self, policy_id):
+        parse_policy_id(policy_id)
+        if policy_id not in self.ids:
+            raise KeyError(f"unknown policy: {policy_id}")
+        return self.ids[policy_id]
+
+    def eval(self, soa, policies, origin=VALIDATE, rows=None, threads=1):
+        """Verdict words for rows x policies (numpy uint32, row-major)."""
+        idx = [self.lookup(p) if isinstance(p, str) else p for p in policies]
+        n = soa.n_requests if rows is None else rows
+        arr = (C.c_int32 * len(idx))(*idx)
+        out = np.zeros(n * len(idx), dtype=np.uint32)
+        ptr = out.ctypes.data_as(C.POINTER(C.c_uint32))
+        if threads > 1:
+            olib().orc_eval_mt(self._h, C.byref(soa), arr, len(idx), origin, n, threads, ptr)
+        else:
+            olib().orc_eval(self._h, C.byref(soa), arr, len(idx), origin, 0, n, ptr)
+        return out
+
+    # ------------------------------------------------------------------ responses
+    def message(self, soa, row, pidx, reason, arg):
+        """Message templates (DESIGN.md §Policy families)."""
+        P = self.pol[pidx]
+
+        def s(col, i):
+            c = getattr(soa, col)
+            return bytes(c.bytes[c.off[i]:c.off[i + 1]]).decode()
+
+        cb, lb = soa.ctr_off[row], soa.lbl_off[row]
+        q = lambda x: f"'{x}'"  # noqa: E731
+        if reason == R_PRIVILEGED:
+            return "Privileged container is not allowed"
+        if reason == R_NAMESPACE:
+            return f"namespace {q(s('ns', row))} is not accepted: only {q(P['lists'][0][0])} is allowed"
+        if reason in (R_REG_NOT_ALLOWED, R_REG_REJECTED, R_TAG_REJECTED, R_IMG_NOT_ALLOWED, R_IMG_REJECTED):
+            image = s("ctr_image", cb + arg)
+            reg, tag, _ = image_parts(image)
+            head = f"container {q(s('ctr_name', cb + arg))} uses image {q(image)}"
+            return {R_REG_NOT_ALLOWED: f"{head}: registry {q(reg)} is not in the allowed registries",
+                    R_REG_REJECTED: f"{head}: registry {q(reg)} is rejected",
+                    R_TAG_REJECTED: f"{head}: tag {q(tag)} is rejected",
+                    R_IMG_NOT_ALLOWED: f"{head}, which is not in the allowed images",
+                    R_IMG_REJECTED: f"{head}, which is rejected"}[reason]
+        if reason == R_CAP:
+            c, k = arg >> 8, arg & 0xFF
+            cap = s("cap_add", soa.capadd_off[cb + c] + k)
+            return f"container {q(s('ctr_name', cb + c))} adds capability {q(cap)}, which is not allowed"
+        if reason == R_APPARMOR:
+            return (f"container {q(s('ctr_name', cb + arg))} uses AppArmor profile "
+                    f"{q(s('ctr_apparmor', cb + arg))}, which is not allowed")
+        if reason == R_LABEL_DENIED:
+            return f"label {q(s('lbl_key', lb + arg))} is denied"
+        if reason == R_LABEL_CONSTRAINT:
+            l, i = arg >> 8, arg & 0xFF
+            return (f"label {q(s('lbl_key', lb + l))} value {q(s('lbl_val', lb + l))} does not match the "
+                    f"constraint {q(P['lists'][3][i])}")
+        if reason == R_LABEL_MANDATORY:
+            return f"mandatory label {q(P['lists'][1][arg])} is missing"
+        if reason == R_GROUP:
+            return P["message"]
+        if reason == R_GROUP_EXPR:
+            return P["expr_error"]
+        if reason == R_INIT:
+            return P["init_error"]
+        return ""
+
+    def response(self, soa, row, pidx, v, member_v=None):
+        """AdmissionResponse dict the service returns for verdict word v (service.rs:30-152)."""
+        P = self.pol[pidx]
+        c = soa.uid
+        uid = bytes(c.bytes[c.off[row]:c.off[row + 1]]).decode()
+        if v & 0x20:
+            if not P["registered"]:
+                raise KeyError(f"unknown policy: {P['id']}")
+            return {"uid": uid, "allowed": True}
+        if P["group"] and P["broken"]:
+            raise KeyError(f"unknown policy: {P['broken']}")
+        fst = (v >> 3) & 3
+        reason, arg = (v >> 8) & 0xFF, v >> 16
+        resp = {"uid": uid, "allowed": bool(v & 4)}
+        if fst == 0:
+            return resp
+        if fst == 3:
+            resp["status"] = {"message": P["init_error"], "code": 500}
+            return resp
+        if fst == 2:
+            resp["status"] = {"message": f"Request rejected by policy {P['id']}. The policy attempted to mutate the "
+                                         f"request, but it is currently configured to not allow mutations."}
+            return resp
+        st = {"message": self.message(soa, row, pidx, reason, arg)}
+        if reason == R_GROUP_EXPR:
+            st["code"] = 500
+        if reason == R_GROUP:
+            causes = []
+            for slot, m in enumerate(P["members"]):
+                if not (arg >> slot) & 1:
+                    continue
+                mv = member_v[slot]
+                if (mv & 2) and (mv & 1):
+                    msg = "mutation is not allowed inside of policy group"
+                else:
+                    msg = self.message(soa, row, m, (mv >> 8) & 0xFF, mv >> 16)
+                causes.append({"field": f"spec.policies.{self.pol[m]['name']}", "message": msg})
+            st["details"] = {"causes": causes}
+        resp["status"] = st
+        return resp

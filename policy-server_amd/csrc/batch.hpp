@@ -1,0 +1,71 @@
+// batch.hpp — host-side columnar request batch (kw_soa owner) and the JSON flattener.
+//
+// The reference deserializes each AdmissionReview body with serde (JsonExtractor,
+// src/api/handlers.rs:29-39; AdmissionReviewRequest, src/api/admission_review.rs:4-14) and hands
+// the whole AdmissionRequest to a Wasm guest per (request, policy). Here a micro-batch of bodies is
+// flattened once into SoA columns (include/kwgpu.h kw_soa) that the device streams from HBM.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <string_view>
+#include <vector>
+
+#include "../../include/kwgpu.h"
+#include "kwdev.hpp"
+
+namespace kw {
+
+struct StrCol {
+  std::vector<uint32_t> off{0};
+  std::vector<uint8_t> bytes;
+  void push(std::string_view s) {
+    if (bytes.size() != off.back()) bytes.resize(off.back());  // drop device padding
+    bytes.insert(bytes.end(), s.begin(), s.end());
+    off.push_back((uint32_t)bytes.size());
+  }
+  size_t n() const { return off.size() - 1; }
+  std::string_view at(size_t i) const {
+    return std::string_view((const char*)bytes.data() + off[i], off[i + 1] - off[i]);
+  }
+  void reserve(size_t ns, size_t nb) {
+    off.reserve(ns + 1);
+    bytes.reserve(nb + 16);
+  }
+  void pad() { bytes.resize(((size_t)off.back() + 31) & ~(size_t)15, 0); }  // >=16 B zero tail
+  kw_strcol view() const {
+    kw_strcol c;
+    c.off = off.data();
+    c.bytes = bytes.data();
+    c.n = n();
+    return c;
+  }
+  void clear() {
+    off.assign(1, 0);
+    bytes.clear();
+  }
+};
+
+struct DeviceBatch;  // engine.cpp
+
+struct Batch {
+  uint64_t n = 0;
+  std::vector<uint8_t> req_flags;
+  std::vector<uint32_t> ctr_off{0}, lbl_off{0};
+  StrCol uid, ns, op, kind;
+  std::vector<uint8_t> ctr_flags;
+  std::vector<uint32_t> capadd_off{0}, capdrop_off{0};
+  StrCol ctr_name, ctr_image, ctr_aa, cap_add, cap_drop, lbl_key, lbl_val;
+  DeviceBatch* dev = nullptr;
+  uint64_t containers() const { return ctr_flags.size(); }
+  uint64_t labels() const { return lbl_key.n(); }
+  void view(kw_soa* s) const;
+  void finalize();  // pads every byte pool (device loads may read 16 B past a string)
+};
+
+// Flattens one document (AdmissionReview or RawReview) and appends it as a row. On a
+// deserialization error returns false with the 422 rejection text.
+bool flatten_document(const char* doc, size_t len, int doc_kind, Batch* b, std::string* err);
+// Copies a caller SoA into the batch.
+bool batch_from_soa(const kw_soa& s, Batch* b, std::string* err);
+
+}  // namespace kw

@@ -1,0 +1,635 @@
+// capi.cpp — extern "C" implementation of include/kwgpu.h: environment and batch lifetime, HBM
+// residency, launch of the hot path (kernels.hip) and the host epilogue (service.cpp).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/kwgpu.h"
+#include "automaton.hpp"
+#include "batch.hpp"
+#include "env.hpp"
+#include "kernels.hpp"
+#include "service.hpp"
+
+using namespace kw;
+
+struct kw_env {
+  Env e;
+};
+
+namespace kw {
+
+// Device copy of a batch: one allocation for the input columns, lazily sized mask / verdict /
+// policy-list buffers, a private stream and timing events.
+struct DeviceBatch {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  uint8_t* cols = nullptr;
+  size_t cols_bytes = 0;
+  // device views of the columns
+  const uint8_t* req_flags = nullptr;
+  const uint32_t *ctr_off = nullptr, *lbl_off = nullptr, *capadd_off = nullptr, *capdrop_off = nullptr;
+  const uint8_t* ctr_flags = nullptr;
+  struct DCol {
+    const uint32_t* off = nullptr;
+    const uint8_t* bytes = nullptr;
+    uint64_t n = 0;
+    uint64_t nbytes = 0;
+  } ns, ctr_image, ctr_aa, cap_add, cap_drop, lbl_key, lbl_val;
+  uint64_t* masks[NMASK] = {};
+  size_t mask_cap[NMASK] = {};
+  uint32_t* verdicts = nullptr;
+  size_t verdict_cap = 0;
+  int32_t* pols = nullptr;
+  size_t pols_cap = 0;
+  size_t last_verdicts = 0;
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  ~DeviceBatch() {
+    if (device >= 0) (void)hipSetDevice(device);
+    (void)hipFree(cols);
+    for (auto* m : masks) (void)hipFree(m);
+    (void)hipFree(verdicts);
+    (void)hipFree(pols);
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+}  // namespace kw
+
+struct kw_batch {
+  Batch b;
+  std::unique_ptr<DeviceBatch> dev;
+};
+
+namespace {
+
+void put_err(char* buf, size_t cap, const std::string& s) {
+  if (!buf || cap == 0) return;
+  size_t n = std::min(cap - 1, s.size());
+  memcpy(buf, s.data(), n);
+  buf[n] = 0;
+}
+
+int put_out(const std::string& s, char* buf, size_t cap, size_t* need) {
+  if (need) *need = s.size() + 1;
+  if (!buf || cap < s.size() + 1) return KW_E_NOSPACE;
+  memcpy(buf, s.data(), s.size());
+  buf[s.size()] = 0;
+  return KW_OK;
+}
+
+#define HIPCHK(x)                       \
+  do {                                  \
+    hipError_t _e = (x);                \
+    if (_e != hipSuccess) return KW_E_DEVICE; \
+  } while (0)
+
+template <typename T>
+int ensure(T** p, size_t* cap, size_t n) {
+  if (*cap >= n && *p) return KW_OK;
+  (void)hipFree(*p);
+  *p = nullptr;
+  size_t want = std::max<size_t>(n, 1);
+  HIPCHK(hipMalloc((void**)p, want * sizeof(T)));
+  *cap = want;
+  return KW_OK;
+}
+
+int upload_env(kw_env* env, int device) {
+  if (device < 0) return KW_OK;
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(hipMalloc(&env->e.d_blob, env->e.blob.size()));
+  HIPCHK(hipMemcpy(env->e.d_blob, env->e.blob.data(), env->e.blob.size(), hipMemcpyHostToDevice));
+  env->e.device = device;
+  return KW_OK;
+}
+
+// Columns a launch needs: which mask arrays the selected policies read.
+struct Needs {
+  bool m[NMASK] = {};
+};
+
+void add_needs(const Env& E, int32_t p, Needs* n) {
+  const PolicyRec& r = E.pol[(size_t)p];
+  if (E.always_ns) n->m[M_NS] = true;
+  switch (r.family) {
+    case FAM_NAMESPACE: n->m[M_NS] = true; break;
+    case FAM_TRUSTED_REPOS: n->m[M_REG] = n->m[M_TAG] = n->m[M_IMG] = true; break;
+    case FAM_CAPABILITIES: n->m[M_CAPADD] = n->m[M_CAPDROP] = true; break;
+    case FAM_APPARMOR: n->m[M_AA] = true; break;
+    case FAM_LABELS: n->m[M_LK] = n->m[M_LV] = true; break;
+    case FAM_GROUP:
+      for (int32_t m : r.members) add_needs(E, m, n);
+      break;
+    default: break;
+  }
+}
+
+struct PassPlan {
+  ClassifyJobs jobs;
+  EvalArgs args;
+  double classify_bytes = 0, evaluate_bytes = 0;
+};
+
+// Build the classification jobs and evaluation arguments of one validate pass.
+int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npairs, uint32_t npol, int origin,
+              const int32_t* d_pols, const int32_t* d_row_policy, PassPlan* plan) {
+  const Env& E = env->e;
+  DeviceBatch& D = *kb->dev;
+  const DevHeader* H = (const DevHeader*)E.blob.data();
+  memset(&plan->jobs, 0, sizeof(plan->jobs));
+  memset(&plan->args, 0, sizeof(plan->args));
+  ClassifyJobs& J = plan->jobs;
+  uint32_t blocks = 0, lds_max = 0;
+  double cbytes = 0;
+  auto dfa_bytes = [&](uint32_t off) -> uint32_t {
+    return off ? ((const DevDfa*)(E.blob.data() + off))->chain_bytes : 0u;
+  };
+  auto add_job = [&](const DeviceBatch::DCol& c, int mode, std::initializer_list<std::pair<MaskArr, Col>> outs) -> int {
+    ClassifyJob job;
+    memset(&job, 0, sizeof(job));
+    job.off = c.off;
+    job.bytes = c.bytes;
+    job.n = (uint32_t)c.n;
+    job.mode = (uint32_t)mode;
+    int k = 0;
+    uint32_t pos = 0;
+    bool any = false;
+    for (auto& o : outs) {
+      uint32_t off = H->dfa_off[o.second];
+      if (off && need.m[o.first]) {
+        if (int rc = ensure(&D.masks[o.first], &D.mask_cap[o.first], c.n)) return rc;
+        job.out[k] = D.masks[o.first];
+        job.dfa[k] = off;
+        job.lds_pos[k] = pos;
+        pos += dfa_bytes(off);
+        any = true;
+        cbytes += 8.0 * (double)c.n;
+      }
+      ++k;
+    }
+    if (!any || c.n == 0) return KW_OK;
+    if (J.n >= kMaxJobs) return KW_E_ARG;
+    job.lds_bytes = pos;
+    uint32_t nb = (uint32_t)std::min<uint64_t>((c.n + kClassifyThreads - 1) / kClassifyThreads, 1024);
+    job.block_begin = blocks;
+    job.nblocks = nb;
+    blocks += nb;
+    lds_max = std::max(lds_max, pos);
+    cbytes += (double)c.nbytes + 4.0 * (double)(c.n + 1);
+    J.j[J.n++] = job;
+    return KW_OK;
+  };
+  int rc;
+  if ((rc = add_job(D.ns, 0, {{M_NS, COL_NS}}))) return rc;
+  if ((rc = add_job(D.ctr_image, 1, {{M_REG, COL_REG}, {M_TAG, COL_TAG}, {M_IMG, COL_IMG}}))) return rc;
+  if ((rc = add_job(D.cap_add, 0, {{M_CAPADD, COL_CAP}}))) return rc;
+  if ((rc = add_job(D.cap_drop, 0, {{M_CAPDROP, COL_CAP}}))) return rc;
+  if ((rc = add_job(D.ctr_aa, 0, {{M_AA, COL_AA}}))) return rc;
+  if ((rc = add_job(D.lbl_key, 0, {{M_LK, COL_LK}}))) return rc;
+  if ((rc = add_job(D.lbl_val, 0, {{M_LV, COL_LV}}))) return rc;
+  J.total_blocks = blocks;
+  J.lds_bytes = lds_max <= 96 * 1024 ? lds_max : 0;  // very large automata are read through L1/L2
+  plan->classify_bytes = cbytes;
+
+  EvalArgs& A = plan->args;
+  A.blob = (const uint8_t*)E.d_blob;
+  A.nrows = kb->b.n;
+  A.npairs = npairs;
+  A.npol = npol;
+  A.origin = origin;
+  A.pols = d_pols;
+  A.row_policy = d_row_policy;
+  A.req_flags = D.req_flags;
+  A.ctr_off = D.ctr_off;
+  A.lbl_off = D.lbl_off;
+  A.ctr_flags = D.ctr_flags;
+  A.capadd_off = D.capadd_off;
+  A.capdrop_off = D.capdrop_off;
+  for (int m = 0; m < (int)NMASK; ++m) {
+    uint32_t col = (m == M_NS ? COL_NS : m == M_REG ? COL_REG : m == M_TAG ? COL_TAG : m == M_IMG ? COL_IMG
+                    : (m == M_CAPADD || m == M_CAPDROP) ? COL_CAP : m == M_AA ? COL_AA : m == M_LK ? COL_LK : COL_LV);
+    A.m[m] = (need.m[m] && H->dfa_off[col]) ? D.masks[m] : nullptr;
+  }
+  A.out = D.verdicts;
+  // algorithmic bytes of the evaluation pass: per-request headers once, the entity columns and
+  // masks the selected policies read, verdict words written
+  const Batch& B = kb->b;
+  double eb = (double)B.n * (1 + 4 + 4) + 4.0 * (double)npairs;
+  double nc = (double)B.containers(), nl = (double)B.labels();
+  bool ctr = need.m[M_REG] || need.m[M_CAPADD] || need.m[M_AA];
+  for (const PolicyRec& r : E.pol)
+    if (r.family == FAM_PRIVILEGED) ctr = ctr || true;
+  if (ctr) eb += nc * 1.0;
+  if (A.m[M_REG]) eb += nc * 24.0;
+  if (need.m[M_CAPADD]) eb += nc * 8.0 + 8.0 * (double)(B.cap_add.n() + B.cap_drop.n());
+  if (A.m[M_AA]) eb += nc * 8.0;
+  if (A.m[M_LK]) eb += nl * 8.0;
+  if (A.m[M_LV]) eb += nl * 8.0;
+  if (A.m[M_NS]) eb += (double)B.n * 8.0;
+  plan->evaluate_bytes = eb;
+  return KW_OK;
+}
+
+int run_pass(const kw_env* env, kw_batch* kb, const PassPlan& plan, bool timed) {
+  DeviceBatch& D = *kb->dev;
+  if (timed) HIPCHK(hipEventRecord(D.ev[0], D.stream));
+  HIPCHK(launch_classify((const uint8_t*)env->e.d_blob, plan.jobs, D.stream));
+  if (timed) HIPCHK(hipEventRecord(D.ev[1], D.stream));
+  HIPCHK(launch_evaluate(plan.args, D.stream));
+  if (timed) HIPCHK(hipEventRecord(D.ev[2], D.stream));
+  return KW_OK;
+}
+
+int validate_common(const kw_env* env, kw_batch* kb, const int32_t* policies, uint32_t npol, const int32_t* row_policy,
+                    int origin, PassPlan* plan) {
+  if (!env || !kb) return KW_E_ARG;
+  const Env& E = env->e;
+  if (E.device < 0 || !E.d_blob) return KW_E_DEVICE;  // no silent host fallback: the hot path is the GPU
+  if (!kb->dev) return KW_E_ARG;                        // batch not resident
+  if (kb->dev->device != E.device) return KW_E_ARG;
+  if (origin != KW_ORIGIN_VALIDATE && origin != KW_ORIGIN_AUDIT) return KW_E_ARG;
+  DeviceBatch& D = *kb->dev;
+  HIPCHK(hipSetDevice(D.device));
+  Needs need;
+  uint64_t npairs;
+  const int32_t* d_pols = nullptr;
+  const int32_t* d_rows = nullptr;
+  const int32_t np = (int32_t)E.pol.size();
+  if (row_policy) {
+    for (uint64_t r = 0; r < kb->b.n; ++r) {
+      if (row_policy[r] < 0 || row_policy[r] >= np) return KW_E_ARG;
+      add_needs(E, row_policy[r], &need);
+    }
+    npairs = kb->b.n;
+    if (int rc = ensure(&D.pols, &D.pols_cap, kb->b.n)) return rc;
+    HIPCHK(hipMemcpyAsync(D.pols, row_policy, kb->b.n * sizeof(int32_t), hipMemcpyHostToDevice, D.stream));
+    d_rows = D.pols;
+    npol = 1;
+  } else {
+    if (npol == 0 || !policies) return KW_E_ARG;
+    for (uint32_t j = 0; j < npol; ++j) {
+      if (policies[j] < 0 || policies[j] >= np) return KW_E_ARG;
+      add_needs(E, policies[j], &need);
+    }
+    npairs = kb->b.n * (uint64_t)npol;
+    if (int rc = ensure(&D.pols, &D.pols_cap, npol)) return rc;
+    HIPCHK(hipMemcpyAsync(D.pols, policies, npol * sizeof(int32_t), hipMemcpyHostToDevice, D.stream));
+    d_pols = D.pols;
+  }
+  if (int rc = ensure(&D.verdicts, &D.verdict_cap, npairs)) return rc;
+  D.last_verdicts = npairs;
+  return plan_pass(env, kb, need, npairs, npol, origin, d_pols, d_rows, plan);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* kw_version(void) { return "kwgpu 0.1 (gfx950)"; }
+
+int kw_env_build(const char* json, size_t len, const kw_env_options* opts, kw_env** out, char* err, size_t errlen) {
+  if (!json || !out) return KW_E_ARG;
+  auto env = std::make_unique<kw_env>();
+  Status st = build_env(json, len, opts ? opts->continue_on_errors != 0 : false,
+                        opts ? opts->always_accept_namespace : nullptr, &env->e);
+  if (!st.ok()) {
+    put_err(err, errlen, st.message);
+    return st.code;
+  }
+  int dev = opts ? opts->device : -1;
+  if (int rc = upload_env(env.get(), dev)) {
+    put_err(err, errlen, "cannot upload compiled tables to the device");
+    return rc;
+  }
+  *out = env.release();
+  return KW_OK;
+}
+
+int kw_env_serialize(const kw_env* env, void* buf, size_t cap, size_t* need) {
+  if (!env) return KW_E_ARG;
+  std::vector<uint8_t> s = env_serialize(env->e);
+  if (need) *need = s.size();
+  if (!buf || cap < s.size()) return KW_E_NOSPACE;
+  memcpy(buf, s.data(), s.size());
+  return KW_OK;
+}
+
+int kw_env_deserialize(const void* blob, size_t len, int device, kw_env** out, char* err, size_t errlen) {
+  if (!blob || !out) return KW_E_ARG;
+  auto env = std::make_unique<kw_env>();
+  Status st = env_from_blob(blob, len, &env->e);
+  if (!st.ok()) {
+    put_err(err, errlen, st.message);
+    return st.code;
+  }
+  if (int rc = upload_env(env.get(), device)) return rc;
+  *out = env.release();
+  return KW_OK;
+}
+
+void kw_env_destroy(kw_env* env) {
+  if (!env) return;
+  if (env->e.d_blob) {
+    (void)hipSetDevice(env->e.device);
+    (void)hipFree(env->e.d_blob);
+  }
+  delete env;
+}
+
+int kw_env_lookup(const kw_env* env, const char* id, size_t len, int32_t* idx) {
+  if (!env || !id || !idx) return KW_E_ARG;
+  return env_lookup(env->e, std::string(id, len), idx).code;
+}
+
+int kw_env_policy_count(const kw_env* env) { return env ? (int)env->e.pol.size() : -1; }
+
+int kw_env_policy_id(const kw_env* env, int32_t idx, char* buf, size_t cap) {
+  if (!env || idx < 0 || (size_t)idx >= env->e.pol.size()) return KW_E_ARG;
+  return put_out(env->e.pol[(size_t)idx].id, buf, cap, nullptr);
+}
+
+int kw_env_is_group(const kw_env* env, int32_t idx) {
+  if (!env || idx < 0 || (size_t)idx >= env->e.pol.size()) return -1;
+  return env->e.pol[(size_t)idx].is_group ? 1 : 0;
+}
+
+int kw_env_get_policy_mode(const kw_env* env, int32_t idx, int* mode) {
+  if (!env || !mode || idx < 0 || (size_t)idx >= env->e.pol.size()) return KW_E_ARG;
+  const PolicyRec& r = env->e.pol[(size_t)idx];
+  if (!r.registered) return KW_E_NOT_FOUND;
+  *mode = r.mode;
+  return KW_OK;
+}
+
+int kw_env_get_policy_allowed_to_mutate(const kw_env* env, int32_t idx, int* allowed) {
+  if (!env || !allowed || idx < 0 || (size_t)idx >= env->e.pol.size()) return KW_E_ARG;
+  const PolicyRec& r = env->e.pol[(size_t)idx];
+  if (!r.registered) return KW_E_NOT_FOUND;
+  *allowed = r.allowed_to_mutate ? 1 : 0;
+  return KW_OK;
+}
+
+int kw_env_should_always_accept_requests_made_inside_of_namespace(const kw_env* env, const char* ns, size_t len) {
+  if (!env || !ns) return 0;
+  return env->e.always_ns && *env->e.always_ns == std::string(ns, len) ? 1 : 0;
+}
+
+int kw_env_policy_initialization_error(const kw_env* env, int32_t idx, char* buf, size_t cap) {
+  if (!env || idx < 0 || (size_t)idx >= env->e.pol.size()) return -1;
+  const PolicyRec& r = env->e.pol[(size_t)idx];
+  if (!r.init_error) return 0;
+  put_err(buf, cap, r.init_message);
+  return 1;
+}
+
+int kw_env_validate_settings(const kw_env* env, int32_t idx, char* buf, size_t cap) {
+  if (!env || idx < 0 || (size_t)idx >= env->e.pol.size()) return KW_E_ARG;
+  Status st = env_validate_settings(env->e, idx);
+  if (!st.ok()) put_err(buf, cap, st.message);
+  return st.code;
+}
+
+int kw_env_group_members(const kw_env* env, int32_t group, int32_t* out, int cap) {
+  if (!env || group < 0 || (size_t)group >= env->e.pol.size()) return -1;
+  const PolicyRec& r = env->e.pol[(size_t)group];
+  int n = (int)r.members.size();
+  for (int i = 0; i < n && i < cap; ++i) out[i] = r.members[(size_t)i];
+  return n;
+}
+
+int kw_pattern_match(int kind, const char* pat, const char* s, size_t len) {
+  if (!pat || (!s && len)) return -1;
+  std::vector<Pattern> ps{{(Pattern::Kind)kind, pat}};
+  Dfa d;
+  std::string err;
+  if (!compile_dfa(ps, &d, &err)) return -1;
+  return (d.run((const uint8_t*)s, len) & 1ull) ? 1 : 0;
+}
+
+int kw_batch_from_json(const char* const* docs, const size_t* lens, size_t n, int doc_kind, kw_batch** out,
+                       int64_t* bad_row, char* err, size_t errlen) {
+  if (!out || (n && (!docs || !lens))) return KW_E_ARG;
+  auto kb = std::make_unique<kw_batch>();
+  std::string e;
+  for (size_t i = 0; i < n; ++i) {
+    if (!flatten_document(docs[i], lens[i], doc_kind, &kb->b, &e)) {
+      if (bad_row) *bad_row = (int64_t)i;
+      put_err(err, errlen, e);
+      return KW_E_PAYLOAD;
+    }
+  }
+  kb->b.finalize();
+  *out = kb.release();
+  return KW_OK;
+}
+
+int kw_batch_from_soa(const kw_soa* soa, kw_batch** out) {
+  if (!soa || !out) return KW_E_ARG;
+  auto kb = std::make_unique<kw_batch>();
+  std::string e;
+  if (!batch_from_soa(*soa, &kb->b, &e)) return KW_E_ARG;
+  kb->b.finalize();
+  *out = kb.release();
+  return KW_OK;
+}
+
+int kw_batch_view(const kw_batch* b, kw_soa* view) {
+  if (!b || !view) return KW_E_ARG;
+  b->b.view(view);
+  return KW_OK;
+}
+
+int kw_batch_to_device(kw_batch* kb, int device) {
+  if (!kb || device < 0) return KW_E_ARG;
+  HIPCHK(hipSetDevice(device));
+  auto D = std::make_unique<DeviceBatch>();
+  D->device = device;
+  HIPCHK(hipStreamCreateWithFlags(&D->stream, hipStreamNonBlocking));
+  for (auto& e : D->ev) HIPCHK(hipEventCreate(&e));
+  Batch& B = kb->b;
+  B.finalize();
+  // one allocation, 256-B aligned sub-arrays
+  struct Piece {
+    const void* src;
+    size_t bytes;
+    size_t at;
+  };
+  std::vector<Piece> pieces;
+  size_t total = 0;
+  auto add = [&](const void* src, size_t bytes) {
+    size_t at = total;
+    pieces.push_back({src, bytes, at});
+    total += (bytes + 255) & ~(size_t)255;
+    return at;
+  };
+  size_t o_rf = add(B.req_flags.data(), B.req_flags.size());
+  size_t o_co = add(B.ctr_off.data(), B.ctr_off.size() * 4);
+  size_t o_lo = add(B.lbl_off.data(), B.lbl_off.size() * 4);
+  size_t o_cf = add(B.ctr_flags.data(), B.ctr_flags.size());
+  size_t o_ca = add(B.capadd_off.data(), B.capadd_off.size() * 4);
+  size_t o_cd = add(B.capdrop_off.data(), B.capdrop_off.size() * 4);
+  struct ColAt {
+    size_t off, bytes;
+  };
+  auto addcol = [&](const StrCol& c) { return ColAt{add(c.off.data(), c.off.size() * 4), add(c.bytes.data(), c.bytes.size())}; };
+  ColAt c_ns = addcol(B.ns), c_img = addcol(B.ctr_image), c_aa = addcol(B.ctr_aa), c_add = addcol(B.cap_add),
+        c_drop = addcol(B.cap_drop), c_lk = addcol(B.lbl_key), c_lv = addcol(B.lbl_val);
+  D->cols_bytes = total;
+  HIPCHK(hipMalloc((void**)&D->cols, std::max<size_t>(total, 256)));
+  for (auto& p : pieces)
+    if (p.bytes) HIPCHK(hipMemcpy(D->cols + p.at, p.src, p.bytes, hipMemcpyHostToDevice));
+  D->req_flags = D->cols + o_rf;
+  D->ctr_off = (const uint32_t*)(D->cols + o_co);
+  D->lbl_off = (const uint32_t*)(D->cols + o_lo);
+  D->ctr_flags = D->cols + o_cf;
+  D->capadd_off = (const uint32_t*)(D->cols + o_ca);
+  D->capdrop_off = (const uint32_t*)(D->cols + o_cd);
+  auto dcol = [&](const StrCol& c, ColAt at) {
+    DeviceBatch::DCol d;
+    d.off = (const uint32_t*)(D->cols + at.off);
+    d.bytes = D->cols + at.bytes;
+    d.n = c.n();
+    d.nbytes = c.off.back();
+    return d;
+  };
+  D->ns = dcol(B.ns, c_ns);
+  D->ctr_image = dcol(B.ctr_image, c_img);
+  D->ctr_aa = dcol(B.ctr_aa, c_aa);
+  D->cap_add = dcol(B.cap_add, c_add);
+  D->cap_drop = dcol(B.cap_drop, c_drop);
+  D->lbl_key = dcol(B.lbl_key, c_lk);
+  D->lbl_val = dcol(B.lbl_val, c_lv);
+  kb->dev = std::move(D);
+  return KW_OK;
+}
+
+void kw_batch_destroy(kw_batch* b) { delete b; }
+
+int kw_validate_batch(const kw_env* env, kw_batch* b, const int32_t* policies, uint32_t npol, int origin, void* stream) {
+  (void)stream;
+  PassPlan plan;
+  if (int rc = validate_common(env, b, policies, npol, nullptr, origin, &plan)) return rc;
+  return run_pass(env, b, plan, false);
+}
+
+int kw_validate_rows(const kw_env* env, kw_batch* b, const int32_t* row_policy, int origin, void* stream) {
+  (void)stream;
+  if (!row_policy) return KW_E_ARG;
+  PassPlan plan;
+  if (int rc = validate_common(env, b, nullptr, 0, row_policy, origin, &plan)) return rc;
+  return run_pass(env, b, plan, false);
+}
+
+int kw_batch_verdicts(kw_batch* b, uint32_t* host_out, size_t count) {
+  if (!b || !b->dev || !host_out) return KW_E_ARG;
+  DeviceBatch& D = *b->dev;
+  if (count > D.last_verdicts) return KW_E_ARG;
+  HIPCHK(hipSetDevice(D.device));
+  HIPCHK(hipMemcpyAsync(host_out, D.verdicts, count * sizeof(uint32_t), hipMemcpyDeviceToHost, D.stream));
+  HIPCHK(hipStreamSynchronize(D.stream));
+  return KW_OK;
+}
+
+int kw_validate_timed(const kw_env* env, kw_batch* b, const int32_t* policies, uint32_t npol, int origin, int warmup,
+                      int reps, kw_timing* out) {
+  if (!out || reps <= 0) return KW_E_ARG;
+  PassPlan plan;
+  if (int rc = validate_common(env, b, policies, npol, nullptr, origin, &plan)) return rc;
+  DeviceBatch& D = *b->dev;
+  for (int i = 0; i < warmup; ++i)
+    if (int rc = run_pass(env, b, plan, false)) return rc;
+  HIPCHK(hipStreamSynchronize(D.stream));
+  double cl = 0, ev = 0;
+  for (int i = 0; i < reps; ++i) {
+    if (int rc = run_pass(env, b, plan, true)) return rc;
+    HIPCHK(hipEventSynchronize(D.ev[2]));
+    float a = 0, c = 0;
+    HIPCHK(hipEventElapsedTime(&a, D.ev[0], D.ev[1]));
+    HIPCHK(hipEventElapsedTime(&c, D.ev[1], D.ev[2]));
+    cl += a;
+    ev += c;
+  }
+  out->classify_ms = cl / reps;
+  out->evaluate_ms = ev / reps;
+  out->total_ms = (cl + ev) / reps;
+  out->classify_bytes = plan.classify_bytes;
+  out->evaluate_bytes = plan.evaluate_bytes;
+  return KW_OK;
+}
+
+int kw_format_response(const kw_env* env, const kw_batch* b, uint64_t row, int32_t policy, uint32_t verdict,
+                       const uint32_t* member_verdicts, char* buf, size_t cap, size_t* need) {
+  if (!env || !b || row >= b->b.n || policy < 0 || (size_t)policy >= env->e.pol.size()) return KW_E_ARG;
+  std::string out;
+  Status st = format_response(env->e, b->b, row, policy, verdict, member_verdicts, &out);
+  if (!st.ok()) {
+    put_out(st.message, buf, cap, need);
+    return st.code;
+  }
+  return put_out(out, buf, cap, need);
+}
+
+int kw_evaluate(const kw_env* env, const char* policy_id, const char* doc, size_t doc_len, int doc_kind, int origin,
+                char* buf, size_t cap, size_t* need) {
+  if (!env || !policy_id || !doc) return KW_E_ARG;
+  const Env& E = env->e;
+  int32_t idx;
+  Status st = env_lookup(E, policy_id, &idx);  // service.rs:37 + PolicyNotFound
+  if (!st.ok()) {
+    put_out(st.message, buf, cap, need);
+    return st.code;
+  }
+  kw_batch* kb = nullptr;
+  char err[512];
+  int rc = kw_batch_from_json(&doc, &doc_len, 1, doc_kind, &kb, nullptr, err, sizeof(err));
+  if (rc) {
+    put_out(err, buf, cap, need);
+    return rc;
+  }
+  std::unique_ptr<kw_batch> hold(kb);
+  if (E.device < 0) {
+    put_out("engine has no device: the hot path runs only on the GPU", buf, cap, need);
+    return KW_E_DEVICE;
+  }
+  if ((rc = kw_batch_to_device(kb, E.device))) return rc;
+  std::vector<int32_t> pols{idx};
+  const PolicyRec& P = E.pol[(size_t)idx];
+  for (int32_t m : P.members) pols.push_back(m);
+  if ((rc = kw_validate_batch(env, kb, pols.data(), (uint32_t)pols.size(), origin, nullptr))) return rc;
+  std::vector<uint32_t> v(pols.size());
+  if ((rc = kw_batch_verdicts(kb, v.data(), v.size()))) return rc;
+  std::string out;
+  st = format_response(E, kb->b, 0, idx, v[0], v.size() > 1 ? v.data() + 1 : nullptr, &out);
+  if (!st.ok()) {
+    put_out(st.message, buf, cap, need);
+    return st.code;
+  }
+  return put_out(out, buf, cap, need);
+}
+
+int kw_service_constraints(uint32_t in, int mode, int allowed_to_mutate, uint32_t* out_flags) {
+  // validation_response_with_constraints (service.rs:160-208); bit0 allowed, bit1 patch, bit2 status
+  uint32_t o = in;
+  int fst;
+  if (mode == KW_MODE_MONITOR) {
+    o = 1u;
+    fst = KW_FST_NONE;
+  } else if ((in & 2u) && !allowed_to_mutate) {
+    o = 4u;
+    fst = KW_FST_MUTATION_REFUSED;
+  } else {
+    fst = (in & 4u) ? KW_FST_VANILLA : KW_FST_NONE;
+  }
+  if (out_flags) *out_flags = o;
+  return fst;
+}
+
+}  // extern "C"

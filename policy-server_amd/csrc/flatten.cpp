@@ -1,0 +1,294 @@
+// flatten.cpp — AdmissionReview / RawReview JSON -> SoA row (batch.hpp).
+//
+// Deserialization contract (what makes the reference answer 422 before evaluating):
+//   AdmissionReviewRequest { kind?, apiVersion?, request: AdmissionRequest } (admission_review.rs:4-14)
+//   AdmissionRequest [upstream policy-evaluator]: uid, kind{group,version,kind}, resource{group,
+//   version,resource}, operation and userInfo are required; namespace/name are optional strings;
+//   object/oldObject/options are arbitrary JSON.
+//   RawReviewRequest { request: Value } (raw_review.rs:5-9).
+// Extraction: namespace, operation, request kind, uid; the PodSpec of the
+// object (Pod: spec; Deployment/ReplicaSet/StatefulSet/DaemonSet/Job/ReplicationController:
+// spec.template.spec; CronJob: spec.jobTemplate.spec.template.spec), its containers,
+// initContainers and ephemeralContainers (name, image, securityContext.privileged,
+// securityContext.capabilities.add/drop, AppArmor profile from the pod-template annotation
+// container.apparmor.security.beta.kubernetes.io/<name>), and object.metadata.labels.
+#include <cstring>
+
+#include "batch.hpp"
+#include "json.hpp"
+
+namespace kw {
+
+void Batch::view(kw_soa* s) const {
+  memset(s, 0, sizeof(*s));
+  s->n_requests = n;
+  s->req_flags = req_flags.data();
+  s->ctr_off = ctr_off.data();
+  s->lbl_off = lbl_off.data();
+  s->uid = uid.view();
+  s->ns = ns.view();
+  s->op = op.view();
+  s->kind = kind.view();
+  s->ctr_flags = ctr_flags.data();
+  s->capadd_off = capadd_off.data();
+  s->capdrop_off = capdrop_off.data();
+  s->ctr_name = ctr_name.view();
+  s->ctr_image = ctr_image.view();
+  s->ctr_apparmor = ctr_aa.view();
+  s->cap_add = cap_add.view();
+  s->cap_drop = cap_drop.view();
+  s->lbl_key = lbl_key.view();
+  s->lbl_val = lbl_val.view();
+}
+
+void Batch::finalize() {
+  for (StrCol* c : {&uid, &ns, &op, &kind, &ctr_name, &ctr_image, &ctr_aa, &cap_add, &cap_drop, &lbl_key, &lbl_val})
+    c->pad();
+}
+
+namespace {
+
+constexpr std::string_view kAppArmorPrefix = "container.apparmor.security.beta.kubernetes.io/";
+
+int64_t path(const JDoc& d, int64_t n, std::initializer_list<const char*> keys) {
+  for (const char* k : keys) {
+    if (n < 0) return -1;
+    n = d.get((uint32_t)n, k);
+  }
+  return n;
+}
+
+bool is_str(const JDoc& d, int64_t n) { return n >= 0 && d.is((uint32_t)n, JType::Str); }
+std::string_view sv(const JDoc& d, int64_t n) { return is_str(d, n) ? d.str((uint32_t)n) : std::string_view(); }
+
+bool req_string(const JDoc& d, uint32_t obj, const char* key, std::string* err) {
+  int64_t n = d.get(obj, key);
+  if (n < 0) {
+    *err = std::string("Failed to deserialize the JSON body into the target type: request: missing field `") + key + "`";
+    return false;
+  }
+  if (!d.is((uint32_t)n, JType::Str)) {
+    *err = std::string("Failed to deserialize the JSON body into the target type: request.") + key +
+           ": invalid type, expected a string";
+    return false;
+  }
+  return true;
+}
+
+bool req_object(const JDoc& d, uint32_t obj, const char* key, std::initializer_list<const char*> fields,
+                std::string* err) {
+  int64_t n = d.get(obj, key);
+  if (n < 0) {
+    *err = std::string("Failed to deserialize the JSON body into the target type: request: missing field `") + key + "`";
+    return false;
+  }
+  if (!d.is((uint32_t)n, JType::Obj)) {
+    *err = std::string("Failed to deserialize the JSON body into the target type: request.") + key +
+           ": invalid type, expected a struct";
+    return false;
+  }
+  for (const char* f : fields)
+    if (!req_string(d, (uint32_t)n, f, err)) return false;
+  return true;
+}
+
+bool opt_string(const JDoc& d, uint32_t obj, const char* key, std::string* err) {
+  int64_t n = d.get(obj, key);
+  if (n < 0 || d.is((uint32_t)n, JType::Null) || d.is((uint32_t)n, JType::Str)) return true;
+  *err = std::string("Failed to deserialize the JSON body into the target type: request.") + key +
+         ": invalid type, expected a string";
+  return false;
+}
+
+void push_caps(const JDoc& d, int64_t arr, StrCol* col, std::vector<uint32_t>* off) {
+  if (arr >= 0 && d.is((uint32_t)arr, JType::Arr)) {
+    for (uint32_t k = 0; k < d.count((uint32_t)arr); ++k) {
+      uint32_t it = d.kids((uint32_t)arr)[k].node;
+      if (d.is(it, JType::Str)) col->push(d.str(it));
+    }
+  }
+  off->push_back((uint32_t)col->n());
+}
+
+void flatten_request(const JDoc& d, int64_t req, bool raw, Batch* b) {
+  uint8_t rf = raw ? KW_REQ_RAW : 0;
+  bool req_obj = req >= 0 && d.is((uint32_t)req, JType::Obj);
+  int64_t uidn = req_obj ? d.get((uint32_t)req, "uid") : -1;
+  b->uid.push(sv(d, uidn));
+  int64_t nsn = req_obj ? d.get((uint32_t)req, "namespace") : -1;
+  if (is_str(d, nsn)) rf |= KW_REQ_HAS_NAMESPACE;
+  b->ns.push(sv(d, nsn));
+  b->op.push(sv(d, req_obj ? d.get((uint32_t)req, "operation") : -1));
+  std::string_view rkind = sv(d, req_obj ? path(d, req, {"kind", "kind"}) : -1);
+  b->kind.push(rkind);
+
+  int64_t obj = req_obj ? d.get((uint32_t)req, "object") : -1;
+  bool has_obj = obj >= 0 && d.is((uint32_t)obj, JType::Obj);
+  int64_t spec = -1, tmpl_meta = -1;
+  if (has_obj) {
+    rf |= KW_REQ_HAS_OBJECT;
+    std::string_view k = is_str(d, d.get((uint32_t)obj, "kind")) ? d.str((uint32_t)d.get((uint32_t)obj, "kind")) : rkind;
+    if (k == "Pod") {
+      spec = d.get((uint32_t)obj, "spec");
+      tmpl_meta = d.get((uint32_t)obj, "metadata");
+    } else if (k == "Deployment" || k == "ReplicaSet" || k == "StatefulSet" || k == "DaemonSet" || k == "Job" ||
+               k == "ReplicationController") {
+      spec = path(d, obj, {"spec", "template", "spec"});
+      tmpl_meta = path(d, obj, {"spec", "template", "metadata"});
+    } else if (k == "CronJob") {
+      spec = path(d, obj, {"spec", "jobTemplate", "spec", "template", "spec"});
+      tmpl_meta = path(d, obj, {"spec", "jobTemplate", "spec", "template", "metadata"});
+    }
+    if (spec >= 0 && !d.is((uint32_t)spec, JType::Obj)) spec = -1;
+  }
+  if (spec >= 0) rf |= KW_REQ_HAS_PODSPEC;
+  b->req_flags.push_back(rf);
+
+  // containers
+  if (spec >= 0) {
+    int64_t annots = path(d, tmpl_meta, {"annotations"});
+    bool have_annots = annots >= 0 && d.is((uint32_t)annots, JType::Obj);
+    const char* lists[3] = {"containers", "initContainers", "ephemeralContainers"};
+    const uint8_t kinds[3] = {0, KW_CTR_INIT, KW_CTR_EPHEMERAL};
+    for (int li = 0; li < 3; ++li) {
+      int64_t arr = d.get((uint32_t)spec, lists[li]);
+      if (arr < 0 || !d.is((uint32_t)arr, JType::Arr)) continue;
+      for (uint32_t k = 0; k < d.count((uint32_t)arr); ++k) {
+        uint32_t c = d.kids((uint32_t)arr)[k].node;
+        if (!d.is(c, JType::Obj)) continue;
+        uint8_t cf = kinds[li];
+        std::string_view name = sv(d, d.get(c, "name"));
+        b->ctr_name.push(name);
+        int64_t img = d.get(c, "image");
+        if (is_str(d, img)) cf |= KW_CTR_HAS_IMAGE;
+        b->ctr_image.push(sv(d, img));
+        int64_t sc = d.get(c, "securityContext");
+        int64_t priv = path(d, sc, {"privileged"});
+        if (priv >= 0 && d.is((uint32_t)priv, JType::Bool) && d.n((uint32_t)priv).b) cf |= KW_CTR_PRIVILEGED;
+        push_caps(d, path(d, sc, {"capabilities", "add"}), &b->cap_add, &b->capadd_off);
+        push_caps(d, path(d, sc, {"capabilities", "drop"}), &b->cap_drop, &b->capdrop_off);
+        std::string_view profile;
+        if (have_annots) {
+          for (uint32_t j = 0; j < d.count((uint32_t)annots); ++j) {
+            const JKid& kid = d.kids((uint32_t)annots)[j];
+            std::string_view key = d.key(kid);
+            if (key.size() == kAppArmorPrefix.size() + name.size() && key.substr(0, kAppArmorPrefix.size()) == kAppArmorPrefix &&
+                key.substr(kAppArmorPrefix.size()) == name && d.is(kid.node, JType::Str)) {
+              profile = d.str(kid.node);
+              cf |= KW_CTR_HAS_APPARMOR;
+            }
+          }
+        }
+        b->ctr_aa.push(profile);
+        b->ctr_flags.push_back(cf);
+      }
+    }
+  }
+  b->ctr_off.push_back((uint32_t)b->ctr_flags.size());
+
+  // labels of the object itself
+  int64_t labels = has_obj ? path(d, obj, {"metadata", "labels"}) : -1;
+  if (labels >= 0 && d.is((uint32_t)labels, JType::Obj)) {
+    for (uint32_t j = 0; j < d.count((uint32_t)labels); ++j) {
+      const JKid& kid = d.kids((uint32_t)labels)[j];
+      if (!d.is(kid.node, JType::Str)) continue;
+      b->lbl_key.push(d.key(kid));
+      b->lbl_val.push(d.str(kid.node));
+    }
+  }
+  b->lbl_off.push_back((uint32_t)b->lbl_key.n());
+  b->n += 1;
+}
+
+}  // namespace
+
+bool flatten_document(const char* doc, size_t len, int doc_kind, Batch* b, std::string* err) {
+  thread_local JDoc d;
+  std::string perr;
+  if (!d.parse(doc, len, &perr)) {
+    *err = "Failed to parse the request body as JSON: " + perr;
+    return false;
+  }
+  if (!d.is(0, JType::Obj)) {
+    *err = "Failed to deserialize the JSON body into the target type: invalid type, expected a struct";
+    return false;
+  }
+  int64_t req = d.get(0, "request");
+  if (req < 0) {
+    *err = "Failed to deserialize the JSON body into the target type: missing field `request`";
+    return false;
+  }
+  if (doc_kind == KW_DOC_RAW_REVIEW) {
+    flatten_request(d, req, true, b);
+    return true;
+  }
+  for (const char* k : {"kind", "apiVersion"})
+    if (!opt_string(d, 0, k, err)) return false;
+  if (!d.is((uint32_t)req, JType::Obj)) {
+    *err = "Failed to deserialize the JSON body into the target type: request: invalid type, expected struct AdmissionRequest";
+    return false;
+  }
+  uint32_t r = (uint32_t)req;
+  if (!req_string(d, r, "uid", err)) return false;
+  if (!req_object(d, r, "kind", {"group", "version", "kind"}, err)) return false;
+  if (!req_object(d, r, "resource", {"group", "version", "resource"}, err)) return false;
+  if (!req_string(d, r, "operation", err)) return false;
+  int64_t ui = d.get(r, "userInfo");
+  if (ui < 0 || !d.is((uint32_t)ui, JType::Obj)) {
+    *err = "Failed to deserialize the JSON body into the target type: request: missing field `userInfo`";
+    return false;
+  }
+  for (const char* k : {"namespace", "name", "subResource", "requestSubResource"})
+    if (!opt_string(d, r, k, err)) return false;
+  flatten_request(d, req, false, b);
+  return true;
+}
+
+bool batch_from_soa(const kw_soa& s, Batch* b, std::string* err) {
+  auto copy = [](const kw_strcol& c, StrCol* o) {
+    o->off.assign(c.off, c.off + c.n + 1);
+    uint32_t base = c.off[0];
+    if (base != 0)
+      for (auto& x : o->off) x -= base;
+    o->bytes.assign(c.bytes + base, c.bytes + c.off[c.n]);
+  };
+  uint64_t n = s.n_requests;
+  if (!s.req_flags || !s.ctr_off || !s.lbl_off) {
+    *err = "incomplete SoA";
+    return false;
+  }
+  b->n = n;
+  b->req_flags.assign(s.req_flags, s.req_flags + n);
+  b->ctr_off.assign(s.ctr_off, s.ctr_off + n + 1);
+  b->lbl_off.assign(s.lbl_off, s.lbl_off + n + 1);
+  uint64_t nc = s.ctr_off[n] - s.ctr_off[0];
+  b->ctr_flags.assign(s.ctr_flags + s.ctr_off[0], s.ctr_flags + s.ctr_off[n]);
+  b->capadd_off.assign(s.capadd_off, s.capadd_off + nc + 1);
+  b->capdrop_off.assign(s.capdrop_off, s.capdrop_off + nc + 1);
+  if (s.ctr_off[0] != 0 || s.lbl_off[0] != 0 || s.capadd_off[0] != 0 || s.capdrop_off[0] != 0) {
+    *err = "SoA offsets must start at 0";
+    return false;
+  }
+  copy(s.uid, &b->uid);
+  copy(s.ns, &b->ns);
+  copy(s.op, &b->op);
+  copy(s.kind, &b->kind);
+  copy(s.ctr_name, &b->ctr_name);
+  copy(s.ctr_image, &b->ctr_image);
+  copy(s.ctr_apparmor, &b->ctr_aa);
+  copy(s.cap_add, &b->cap_add);
+  copy(s.cap_drop, &b->cap_drop);
+  copy(s.lbl_key, &b->lbl_key);
+  copy(s.lbl_val, &b->lbl_val);
+  // consistency: every per-entity column must match its table size
+  if (b->uid.n() != n || b->ns.n() != n || b->op.n() != n || b->kind.n() != n || b->ctr_name.n() != nc ||
+      b->ctr_image.n() != nc || b->ctr_aa.n() != nc || b->cap_add.n() != b->capadd_off.back() ||
+      b->cap_drop.n() != b->capdrop_off.back() || b->lbl_key.n() != b->lbl_off.back() ||
+      b->lbl_val.n() != b->lbl_off.back()) {
+    *err = "SoA column sizes are inconsistent";
+    return false;
+  }
+  return true;
+}
+
+}  // namespace kw

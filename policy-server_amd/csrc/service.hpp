@@ -1,0 +1,27 @@
+// service.hpp — the service::evaluate epilogue on the host: verdict word -> AdmissionResponse JSON.
+//
+// Mirrors src/api/service.rs:30-152 (namespace bypass response, PolicyInitialization -> reject 500,
+// validate vs audit) and validation_response_with_constraints (service.rs:160-208), plus the
+// group response shape of PolicyGroupEvaluator [upstream] (message + details.causes with
+// field "spec.policies.<member>", evaluation_environment.rs:979-995, integration_test.rs:118-131).
+#pragma once
+#include <cstdint>
+#include <string>
+
+#include "batch.hpp"
+#include "env.hpp"
+
+namespace kw {
+
+// Rejection message of a policy for a row (DESIGN.md §Policy families, message templates).
+std::string policy_message(const Env& env, const Batch& b, uint64_t row, int32_t pidx, uint32_t reason, uint32_t arg);
+
+// Full AdmissionResponse JSON for (row, policy, verdict). member_v: member verdict words for a
+// group (settings order). Returns a non-ok Status for EvaluationError outcomes.
+Status format_response(const Env& env, const Batch& b, uint64_t row, int32_t pidx, uint32_t v, const uint32_t* member_v,
+                       std::string* out);
+
+// Host restatement of the image split used only for message text (registry / tag names).
+void image_parts(std::string_view image, std::string* registry, std::string* tag, bool* has_tag);
+
+}  // namespace kw
