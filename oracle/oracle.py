@@ -76,6 +76,21 @@ def constraints(policy_id, mode, allowed_to_mutate, resp):
     return resp
 
 
+def service_evaluate(policy_id, mode, allowed_to_mutate, origin, vanilla, uid, namespace=None, always_accept=None,
+                     raw=False, init_error=None):
+    """service::evaluate (service.rs:30-152) over a given vanilla response (the reference's mocked
+    EvaluationEnvironment, service.rs:224-283)."""
+    if not raw and namespace is not None and always_accept is not None and namespace == always_accept:
+        return {"uid": uid, "allowed": True}
+    if init_error is not None:
+        return {"uid": uid, "allowed": False, "status": {"message": init_error, "code": 500}}
+    resp = dict(vanilla)
+    resp["uid"] = uid
+    if origin == VALIDATE:
+        resp = constraints(policy_id, mode, allowed_to_mutate, resp)
+    return resp
+
+
 # ----------------------------------------------------------------------------- schema
 class ConfigError(Exception):
     pass

@@ -48,6 +48,7 @@ struct DeviceBatch {
   int32_t* pols = nullptr;
   size_t pols_cap = 0;
   size_t last_verdicts = 0;
+  std::vector<int32_t> host_pols;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
   ~DeviceBatch() {
     if (device >= 0) (void)hipSetDevice(device);
@@ -133,26 +134,82 @@ void add_needs(const Env& E, int32_t p, Needs* n) {
 }
 
 struct PassPlan {
+  bool rows_mode = false;
+  bool fused = false;
   ClassifyJobs jobs;
   EvalArgs args;
+  TileArgs tile;
+  uint32_t grid = 0;
   double classify_bytes = 0, evaluate_bytes = 0;
 };
 
-// Build the classification jobs and evaluation arguments of one validate pass.
+Col mask_col(int m) {
+  switch (m) {
+    case M_NS: return COL_NS;
+    case M_REG: return COL_REG;
+    case M_TAG: return COL_TAG;
+    case M_IMG: return COL_IMG;
+    case M_CAPADD:
+    case M_CAPDROP: return COL_CAP;
+    case M_AA: return COL_AA;
+    case M_LK: return COL_LK;
+    default: return COL_LV;
+  }
+}
+
+const DeviceBatch::DCol& mask_strings(const DeviceBatch& D, int m) {
+  switch (m) {
+    case M_NS: return D.ns;
+    case M_REG:
+    case M_TAG:
+    case M_IMG: return D.ctr_image;
+    case M_CAPADD: return D.cap_add;
+    case M_CAPDROP: return D.cap_drop;
+    case M_AA: return D.ctr_aa;
+    case M_LK: return D.lbl_key;
+    default: return D.lbl_val;
+  }
+}
+
+constexpr uint32_t kFusedTableBudget = 48 * 1024;  // DFA chains staged per workgroup
+constexpr uint32_t kTileLdsBudget = 80 * 1024;      // whole tiled-kernel LDS (two workgroups per CU)
+
+// Build the classification jobs (two-kernel mode) and the evaluation arguments of one pass.
 int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npairs, uint32_t npol, int origin,
               const int32_t* d_pols, const int32_t* d_row_policy, PassPlan* plan) {
   const Env& E = env->e;
   DeviceBatch& D = *kb->dev;
+  const Batch& B = kb->b;
   const DevHeader* H = (const DevHeader*)E.blob.data();
   memset(&plan->jobs, 0, sizeof(plan->jobs));
   memset(&plan->args, 0, sizeof(plan->args));
+  memset(&plan->tile, 0, sizeof(plan->tile));
+  plan->rows_mode = d_row_policy != nullptr;
+  auto chain_bytes = [&](uint32_t off) -> uint32_t {
+    return off ? ((const DevDfa*)(E.blob.data() + off))->chain_bytes : 0u;
+  };
+  // masks this pass reads, restricted to columns that have patterns
+  bool use[NMASK] = {};
+  for (int m = 0; m < (int)NMASK; ++m) use[m] = need.m[m] && H->dfa_off[mask_col(m)] != 0;
+  for (int m = 0; m < (int)NMASK; ++m)
+    if (use[m])
+      if (int rc = ensure(&D.masks[m], &D.mask_cap[m], mask_strings(D, m).n)) return rc;
+
+  // fused when every needed chain fits the per-workgroup table budget
+  uint32_t table_bytes = 0;
+  bool col_staged[NCOL] = {};
+  for (int m = 0; m < (int)NMASK; ++m)
+    if (use[m] && !col_staged[mask_col(m)]) {
+      col_staged[mask_col(m)] = true;
+      table_bytes += chain_bytes(H->dfa_off[mask_col(m)]);
+    }
+  plan->fused = !plan->rows_mode && table_bytes <= kFusedTableBudget;
+
+  // ---- classify jobs (two-kernel mode and the micro-batch mode)
   ClassifyJobs& J = plan->jobs;
   uint32_t blocks = 0, lds_max = 0;
   double cbytes = 0;
-  auto dfa_bytes = [&](uint32_t off) -> uint32_t {
-    return off ? ((const DevDfa*)(E.blob.data() + off))->chain_bytes : 0u;
-  };
-  auto add_job = [&](const DeviceBatch::DCol& c, int mode, std::initializer_list<std::pair<MaskArr, Col>> outs) -> int {
+  auto add_job = [&](const DeviceBatch::DCol& c, int mode, std::initializer_list<MaskArr> outs) -> int {
     ClassifyJob job;
     memset(&job, 0, sizeof(job));
     job.off = c.off;
@@ -162,14 +219,13 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
     int k = 0;
     uint32_t pos = 0;
     bool any = false;
-    for (auto& o : outs) {
-      uint32_t off = H->dfa_off[o.second];
-      if (off && need.m[o.first]) {
-        if (int rc = ensure(&D.masks[o.first], &D.mask_cap[o.first], c.n)) return rc;
-        job.out[k] = D.masks[o.first];
+    for (MaskArr o : outs) {
+      if (use[o]) {
+        uint32_t off = H->dfa_off[mask_col(o)];
+        job.out[k] = D.masks[o];
         job.dfa[k] = off;
         job.lds_pos[k] = pos;
-        pos += dfa_bytes(off);
+        pos += chain_bytes(off);
         any = true;
         cbytes += 8.0 * (double)c.n;
       }
@@ -187,21 +243,24 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
     J.j[J.n++] = job;
     return KW_OK;
   };
-  int rc;
-  if ((rc = add_job(D.ns, 0, {{M_NS, COL_NS}}))) return rc;
-  if ((rc = add_job(D.ctr_image, 1, {{M_REG, COL_REG}, {M_TAG, COL_TAG}, {M_IMG, COL_IMG}}))) return rc;
-  if ((rc = add_job(D.cap_add, 0, {{M_CAPADD, COL_CAP}}))) return rc;
-  if ((rc = add_job(D.cap_drop, 0, {{M_CAPDROP, COL_CAP}}))) return rc;
-  if ((rc = add_job(D.ctr_aa, 0, {{M_AA, COL_AA}}))) return rc;
-  if ((rc = add_job(D.lbl_key, 0, {{M_LK, COL_LK}}))) return rc;
-  if ((rc = add_job(D.lbl_val, 0, {{M_LV, COL_LV}}))) return rc;
-  J.total_blocks = blocks;
-  J.lds_bytes = lds_max <= 96 * 1024 ? lds_max : 0;  // very large automata are read through L1/L2
-  plan->classify_bytes = cbytes;
+  if (!plan->fused) {
+    int rc;
+    if ((rc = add_job(D.ns, 0, {M_NS}))) return rc;
+    if ((rc = add_job(D.ctr_image, 1, {M_REG, M_TAG, M_IMG}))) return rc;
+    if ((rc = add_job(D.cap_add, 0, {M_CAPADD}))) return rc;
+    if ((rc = add_job(D.cap_drop, 0, {M_CAPDROP}))) return rc;
+    if ((rc = add_job(D.ctr_aa, 0, {M_AA}))) return rc;
+    if ((rc = add_job(D.lbl_key, 0, {M_LK}))) return rc;
+    if ((rc = add_job(D.lbl_val, 0, {M_LV}))) return rc;
+    J.total_blocks = blocks;
+    J.lds_bytes = lds_max <= 96 * 1024 ? lds_max : 0;  // very large automata are read through L1/L2
+  }
+  plan->classify_bytes = plan->fused ? 0.0 : cbytes;
 
+  // ---- evaluation arguments
   EvalArgs& A = plan->args;
   A.blob = (const uint8_t*)E.d_blob;
-  A.nrows = kb->b.n;
+  A.nrows = B.n;
   A.npairs = npairs;
   A.npol = npol;
   A.origin = origin;
@@ -213,37 +272,146 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
   A.ctr_flags = D.ctr_flags;
   A.capadd_off = D.capadd_off;
   A.capdrop_off = D.capdrop_off;
-  for (int m = 0; m < (int)NMASK; ++m) {
-    uint32_t col = (m == M_NS ? COL_NS : m == M_REG ? COL_REG : m == M_TAG ? COL_TAG : m == M_IMG ? COL_IMG
-                    : (m == M_CAPADD || m == M_CAPDROP) ? COL_CAP : m == M_AA ? COL_AA : m == M_LK ? COL_LK : COL_LV);
-    A.m[m] = (need.m[m] && H->dfa_off[col]) ? D.masks[m] : nullptr;
-  }
+  for (int m = 0; m < (int)NMASK; ++m) A.m[m] = use[m] ? D.masks[m] : nullptr;
   A.out = D.verdicts;
-  // algorithmic bytes of the evaluation pass: per-request headers once, the entity columns and
-  // masks the selected policies read, verdict words written
-  const Batch& B = kb->b;
-  double eb = (double)B.n * (1 + 4 + 4) + 4.0 * (double)npairs;
-  double nc = (double)B.containers(), nl = (double)B.labels();
-  bool ctr = need.m[M_REG] || need.m[M_CAPADD] || need.m[M_AA];
-  for (const PolicyRec& r : E.pol)
-    if (r.family == FAM_PRIVILEGED) ctr = ctr || true;
+
+  // algorithmic bytes: request headers once, the entity columns and strings the selected
+  // policies read, masks (two-kernel mode only) and the verdict words written
+  double nc = (double)B.containers(), nl = (double)B.labels(), n = (double)B.n;
+  double eb = n * (1 + 4 + 4) + 4.0 * (double)npairs;
+  bool ctr = use[M_REG] || use[M_TAG] || use[M_IMG] || use[M_AA] || use[M_CAPADD] || use[M_CAPDROP];
+  for (uint32_t j = 0; j < npol && !ctr; ++j) ctr = true;  // every pod-spec family reads ctr_flags
   if (ctr) eb += nc * 1.0;
-  if (A.m[M_REG]) eb += nc * 24.0;
-  if (need.m[M_CAPADD]) eb += nc * 8.0 + 8.0 * (double)(B.cap_add.n() + B.cap_drop.n());
-  if (A.m[M_AA]) eb += nc * 8.0;
-  if (A.m[M_LK]) eb += nl * 8.0;
-  if (A.m[M_LV]) eb += nl * 8.0;
-  if (A.m[M_NS]) eb += (double)B.n * 8.0;
-  plan->evaluate_bytes = eb;
+  if (use[M_CAPADD] || use[M_CAPDROP]) eb += nc * 8.0;
+  double strings = 0;
+  for (int m = 0; m < (int)NMASK; ++m) {
+    if (!use[m]) continue;
+    if ((m == M_TAG || m == M_IMG) && use[M_REG]) continue;  // one image column feeds three masks
+    if (m == M_IMG && use[M_TAG]) continue;
+    const DeviceBatch::DCol& c = mask_strings(D, m);
+    strings += (double)c.nbytes + 4.0 * (double)c.n;
+  }
+  double masks = 0;
+  for (int m = 0; m < (int)NMASK; ++m)
+    if (use[m]) masks += 8.0 * (double)mask_strings(D, m).n;
+  (void)nl;
+  plan->evaluate_bytes = plan->fused ? eb + strings : eb + masks;
+  if (plan->rows_mode) return KW_OK;
+
+  // ---- tile geometry and LDS layout
+  TileArgs& T = plan->tile;
+  bool groups = false;
+  for (uint32_t j = 0; j < npol; ++j) groups = groups || E.pol[(size_t)D.host_pols[j]].is_group;
+  auto align = [](uint32_t x) { return (x + 15u) & ~15u; };
+  double cpr = B.n ? nc / n : 1, lpr = B.n ? (double)B.labels() / n : 1;
+  double apr = nc ? (double)B.cap_add.n() / nc : 1, dpr = nc ? (double)B.cap_drop.n() / nc : 1;
+  uint32_t rows = std::max<uint32_t>(64, std::min<uint32_t>(1024, ((4096 / std::max<uint32_t>(npol, 1)) + 63) / 64 * 64));
+  const uint32_t ncap = (uint32_t)E.cols[COL_CAP].size(), naa = (uint32_t)E.cols[COL_AA].size(),
+                 nkey = (uint32_t)E.cols[COL_LK].size();
+  for (;;) {
+    uint32_t cmax = (uint32_t)std::min(65536.0, 1.5 * rows * cpr + 32);
+    uint32_t kmax = (uint32_t)std::min(65536.0, 1.5 * rows * cpr * std::max(apr, dpr) + 32);
+    uint32_t lmax = (uint32_t)std::min(65536.0, 1.5 * rows * lpr + 32);
+    uint32_t off = 16;
+    uint32_t stage_at = off;
+    if (plan->fused) off = align(off + table_bytes);
+    T.o_rf = off;
+    off = align(off + rows);
+    T.o_coff = off;
+    off = align(off + (rows + 1) * 4);
+    T.o_loff = off;
+    off = align(off + (rows + 1) * 4);
+    T.o_cflags = off;
+    off = align(off + cmax);
+    T.o_cadd = off;
+    off = align(off + (cmax + 1) * 4);
+    T.o_cdrop = off;
+    off = align(off + (cmax + 1) * 4);
+    for (int m = 0; m < (int)NMASK; ++m) {
+      T.o_m[m] = 0;
+      if (!use[m]) continue;
+      uint32_t cnt = m == M_NS ? rows : (m == M_CAPADD || m == M_CAPDROP) ? kmax : (m == M_LK || m == M_LV) ? lmax : cmax;
+      T.o_m[m] = off;
+      off = align(off + cnt * 8);
+    }
+    T.o_feat = off;
+    off = align(off + rows * 80);
+    T.o_pos = off;
+    off = align(off + rows * (ncap + naa + nkey) * 4);
+    T.ncap_bits = ncap;
+    T.naa_bits = naa;
+    T.nkey_bits = nkey;
+    T.o_gstk = 0;
+    if (groups) {
+      T.o_gstk = off;
+      off = align(off + kMaxGroupStack * kTileThreads * 2);
+    }
+    if (off > kTileLdsBudget && rows > 16) {
+      rows /= 2;
+      continue;
+    }
+    T.rows = rows;
+    T.cmax = cmax;
+    T.kmax = kmax;
+    T.lmax = lmax;
+    T.lds_bytes = off;
+    // DFA chains staged once per workgroup (fused)
+    if (plan->fused) {
+      uint32_t at = stage_at;
+      uint32_t col_at[NCOL] = {};
+      bool staged[NCOL] = {};
+      for (int m = 0; m < (int)NMASK; ++m) {
+        if (!use[m]) continue;
+        Col c = mask_col(m);
+        if (!staged[c]) {
+          staged[c] = true;
+          col_at[c] = at;
+          T.stage_blob[T.nstage] = H->dfa_off[c];
+          T.stage_lds[T.nstage] = at;
+          T.stage_bytes[T.nstage] = chain_bytes(H->dfa_off[c]);
+          at += chain_bytes(H->dfa_off[c]);
+          ++T.nstage;
+        }
+        T.dfa_head[m] = H->dfa_off[c];
+        T.dfa_lds[m] = col_at[c];
+        const DeviceBatch::DCol& sc = mask_strings(D, m);
+        T.s_off[m] = sc.off;
+        T.s_bytes[m] = sc.bytes;
+      }
+    }
+    break;
+  }
+  if (T.lds_bytes > kTileLdsBudget) return KW_E_ARG;  // npol too large for one tile row
+  T.cap_all_mask = 0;
+  for (size_t i = 0; i < E.cols[COL_CAP].size(); ++i)
+    if (E.cols[COL_CAP][i].text == "ALL") T.cap_all_mask = 1ull << i;
+  if (plan->fused && (use[M_REG] || use[M_TAG] || use[M_IMG])) {  // one parse of the image column feeds all three
+    T.s_off[M_IMG] = D.ctr_image.off;
+    T.s_bytes[M_IMG] = D.ctr_image.bytes;
+  }
+  // every column the kernel dereferences must be present (a null column is a device fault)
+  if (!A.req_flags || !A.ctr_off || !A.lbl_off || !A.ctr_flags || !A.capadd_off || !A.capdrop_off || !A.out || !A.pols)
+    return KW_E_ARG;
+  for (int m = 0; m < (int)NMASK; ++m) {
+    if (use[m] && !A.m[m]) return KW_E_ARG;
+    if (plan->fused && use[m]) {
+      int sm = (m == M_REG || m == M_TAG) ? (int)M_IMG : m;
+      if (!T.s_off[sm] || !T.s_bytes[sm]) return KW_E_ARG;
+    }
+  }
+  uint64_t ntiles = (B.n + T.rows - 1) / T.rows;
+  uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(4, (160 * 1024) / std::max<uint32_t>(T.lds_bytes, 1)));
+  plan->grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ntiles, 256ull * per_cu));
   return KW_OK;
 }
 
 int run_pass(const kw_env* env, kw_batch* kb, const PassPlan& plan, bool timed) {
   DeviceBatch& D = *kb->dev;
   if (timed) HIPCHK(hipEventRecord(D.ev[0], D.stream));
-  HIPCHK(launch_classify((const uint8_t*)env->e.d_blob, plan.jobs, D.stream));
+  if (!plan.fused) HIPCHK(launch_classify((const uint8_t*)env->e.d_blob, plan.jobs, D.stream));
   if (timed) HIPCHK(hipEventRecord(D.ev[1], D.stream));
-  HIPCHK(launch_evaluate(plan.args, D.stream));
+  if (plan.rows_mode) HIPCHK(launch_evaluate_rows(plan.args, D.stream));
+  else HIPCHK(launch_evaluate_tiled(plan.args, plan.tile, plan.fused, plan.grid, D.stream));
   if (timed) HIPCHK(hipEventRecord(D.ev[2], D.stream));
   return KW_OK;
 }
@@ -273,6 +441,7 @@ int validate_common(const kw_env* env, kw_batch* kb, const int32_t* policies, ui
     HIPCHK(hipMemcpyAsync(D.pols, row_policy, kb->b.n * sizeof(int32_t), hipMemcpyHostToDevice, D.stream));
     d_rows = D.pols;
     npol = 1;
+    D.host_pols.clear();
   } else {
     if (npol == 0 || !policies) return KW_E_ARG;
     for (uint32_t j = 0; j < npol; ++j) {
@@ -283,6 +452,7 @@ int validate_common(const kw_env* env, kw_batch* kb, const int32_t* policies, ui
     if (int rc = ensure(&D.pols, &D.pols_cap, npol)) return rc;
     HIPCHK(hipMemcpyAsync(D.pols, policies, npol * sizeof(int32_t), hipMemcpyHostToDevice, D.stream));
     d_pols = D.pols;
+    D.host_pols.assign(policies, policies + npol);
   }
   if (int rc = ensure(&D.verdicts, &D.verdict_cap, npairs)) return rc;
   D.last_verdicts = npairs;

@@ -245,19 +245,58 @@ struct FamOut {
   bool mutated;
 };
 
-__device__ inline uint64_t M(const uint64_t* __restrict__ m, uint64_t i) { return m ? m[i] : 0ull; }
 __device__ inline uint32_t pack2(uint32_t a, uint32_t b) { return (min(a, 255u) << 8) | min(b, 255u); }
 __device__ inline uint32_t pack1(uint32_t a) { return min(a, 65535u); }
 
-__device__ FamOut eval_family(const EvalArgs& a, const DevPolicy& P, uint64_t r) {
+// Column accessors. GlobalSrc reads the HBM arrays; TileSrc reads a tile staged in LDS (indices
+// stay absolute, the accessor rebases them).
+struct GlobalSrc {
+  const EvalArgs* a;
+  __device__ uint8_t rf(uint64_t r) const { return a->req_flags[r]; }
+  __device__ uint32_t coff(uint64_t r) const { return a->ctr_off[r]; }
+  __device__ uint32_t loff(uint64_t r) const { return a->lbl_off[r]; }
+  __device__ uint8_t cflags(uint32_t c) const { return a->ctr_flags[c]; }
+  __device__ uint32_t cadd(uint32_t c) const { return a->capadd_off[c]; }
+  __device__ uint32_t cdrop(uint32_t c) const { return a->capdrop_off[c]; }
+  template <int K>
+  __device__ uint64_t m(uint64_t i) const { return a->m[K] ? a->m[K][i] : 0ull; }
+};
+
+struct TileSrc {
+  const uint8_t* rf_;
+  const uint32_t *coff_, *loff_, *cadd_, *cdrop_;
+  const uint8_t* cflags_;
+  const uint64_t* m_[NMASK];
+  uint64_t r0;
+  uint32_t cb, lb, kab, kdb;
+  __device__ uint8_t rf(uint64_t r) const { return rf_[r - r0]; }
+  __device__ uint32_t coff(uint64_t r) const { return coff_[r - r0]; }
+  __device__ uint32_t loff(uint64_t r) const { return loff_[r - r0]; }
+  __device__ uint8_t cflags(uint32_t c) const { return cflags_[c - cb]; }
+  __device__ uint32_t cadd(uint32_t c) const { return cadd_[c - cb]; }
+  __device__ uint32_t cdrop(uint32_t c) const { return cdrop_[c - cb]; }
+  template <int K>
+  __device__ uint64_t m(uint64_t i) const {
+    const uint64_t* p = m_[K];
+    if (!p) return 0ull;
+    if (K == M_NS) return p[i - r0];
+    if (K == M_CAPADD) return p[i - kab];
+    if (K == M_CAPDROP) return p[i - kdb];
+    if (K == M_LK || K == M_LV) return p[i - lb];
+    return p[i - cb];
+  }
+};
+
+template <class S>
+__device__ FamOut eval_family(const S& src, const DevPolicy& P, uint64_t r) {
   FamOut o{0, 0, false};
-  const uint8_t rf = a.req_flags[r];
-  const uint32_t cb = a.ctr_off[r], ce = a.ctr_off[r + 1];
+  const uint8_t rf = src.rf(r);
+  const uint32_t cb = src.coff(r), ce = src.coff(r + 1);
   switch (P.family) {
     case FAM_PRIVILEGED: {
       if (!(rf & KW_REQ_HAS_PODSPEC)) break;
       for (uint32_t c = cb; c < ce; ++c) {
-        uint8_t f = a.ctr_flags[c];
+        uint8_t f = src.cflags(c);
         bool skip = ((P.flags & PF_SKIP_INIT) && (f & KW_CTR_INIT)) || ((P.flags & PF_SKIP_EPHEMERAL) && (f & KW_CTR_EPHEMERAL));
         if (!skip && (f & KW_CTR_PRIVILEGED)) {
           o.reason = KW_R_PRIVILEGED;
@@ -268,15 +307,15 @@ __device__ FamOut eval_family(const EvalArgs& a, const DevPolicy& P, uint64_t r)
       break;
     }
     case FAM_NAMESPACE: {
-      bool ok = (rf & KW_REQ_HAS_NAMESPACE) && P.nl[0] && (M(a.m[M_NS], r) & P.m[0]);
+      bool ok = (rf & KW_REQ_HAS_NAMESPACE) && P.nl[0] && (src.template m<M_NS>(r) & P.m[0]);
       if (!ok) o.reason = KW_R_NAMESPACE;
       break;
     }
     case FAM_TRUSTED_REPOS: {
       if (!(rf & KW_REQ_HAS_PODSPEC)) break;
       for (uint32_t c = cb; c < ce; ++c) {
-        if (!(a.ctr_flags[c] & KW_CTR_HAS_IMAGE)) continue;
-        uint64_t reg = M(a.m[M_REG], c), tag = M(a.m[M_TAG], c), img = M(a.m[M_IMG], c);
+        if (!(src.cflags(c) & KW_CTR_HAS_IMAGE)) continue;
+        uint64_t reg = src.template m<M_REG>(c), tag = src.template m<M_TAG>(c), img = src.template m<M_IMG>(c);
         uint32_t why = 0;
         if (P.nl[0] && !(reg & P.m[0])) why = KW_R_REG_NOT_ALLOWED;
         else if (P.nl[1] && (reg & P.m[1])) why = KW_R_REG_REJECTED;
@@ -293,31 +332,30 @@ __device__ FamOut eval_family(const EvalArgs& a, const DevPolicy& P, uint64_t r)
     }
     case FAM_CAPABILITIES: {
       if (!(rf & KW_REQ_HAS_PODSPEC)) break;
-      if (!(P.flags & PF_ALLOW_ALL)) {
-        for (uint32_t c = cb; c < ce && !o.reason; ++c) {
-          uint32_t kb = a.capadd_off[c], ke = a.capadd_off[c + 1];
-          for (uint32_t k = kb; k < ke; ++k)
-            if (!(M(a.m[M_CAPADD], k) & P.m[0])) {
-              o.reason = KW_R_CAP_NOT_ALLOWED;
-              o.arg = pack2(c - cb, k - kb);
-              break;
-            }
+      for (uint32_t c = cb; c < ce; ++c) {
+        const uint32_t kb = src.cadd(c), ke = src.cadd(c + 1);
+        uint64_t addm = 0, dropm = 0;
+        for (uint32_t k = kb; k < ke; ++k) {
+          uint64_t mk = src.template m<M_CAPADD>(k);
+          addm |= mk;
+          if (!(P.flags & PF_ALLOW_ALL) && !(mk & P.m[0])) {
+            o.reason = KW_R_CAP_NOT_ALLOWED;
+            o.arg = pack2(c - cb, k - kb);
+            break;
+          }
         }
         if (o.reason) break;
-      }
-      for (uint32_t c = cb; c < ce; ++c) {
-        uint64_t addm = 0, dropm = 0;
-        for (uint32_t k = a.capadd_off[c]; k < a.capadd_off[c + 1]; ++k) addm |= M(a.m[M_CAPADD], k);
-        for (uint32_t k = a.capdrop_off[c]; k < a.capdrop_off[c + 1]; ++k) dropm |= M(a.m[M_CAPDROP], k);
+        for (uint32_t k = src.cdrop(c); k < src.cdrop(c + 1); ++k) dropm |= src.template m<M_CAPDROP>(k);
         if (!(dropm & P.m[3]) && (P.m[1] & ~dropm)) o.mutated = true;
         if (P.m[2] & ~(addm | dropm)) o.mutated = true;
       }
+      if (o.reason) o.mutated = false;
       break;
     }
     case FAM_APPARMOR: {
       if (!(rf & KW_REQ_HAS_PODSPEC)) break;
       for (uint32_t c = cb; c < ce; ++c) {
-        if ((a.ctr_flags[c] & KW_CTR_HAS_APPARMOR) && !(M(a.m[M_AA], c) & P.m[0])) {
+        if ((src.cflags(c) & KW_CTR_HAS_APPARMOR) && !(src.template m<M_AA>(c) & P.m[0])) {
           o.reason = KW_R_APPARMOR;
           o.arg = pack1(c - cb);
           break;
@@ -326,21 +364,24 @@ __device__ FamOut eval_family(const EvalArgs& a, const DevPolicy& P, uint64_t r)
       break;
     }
     case FAM_LABELS: {
-      const uint32_t lb = a.lbl_off[r], le = a.lbl_off[r + 1];
+      const uint32_t lb = src.loff(r), le = src.loff(r + 1);
       uint64_t present = 0;
       for (uint32_t l = lb; l < le && !o.reason; ++l) {
-        uint64_t km = M(a.m[M_LK], l);
+        uint64_t km = src.template m<M_LK>(l);
         present |= km;
         if (km & P.m[0]) {
           o.reason = KW_R_LABEL_DENIED;
           o.arg = pack1(l - lb);
           break;
         }
-        for (uint32_t i = 0; i < P.n_constr; ++i) {
-          if (((km >> P.idx[16 + i]) & 1ull) && !((M(a.m[M_LV], l) >> P.idx[32 + i]) & 1ull)) {
-            o.reason = KW_R_LABEL_CONSTRAINT;
-            o.arg = pack2(l - lb, i);
-            break;
+        if (km) {
+          const uint64_t vm = src.template m<M_LV>(l);
+          for (uint32_t i = 0; i < P.n_constr; ++i) {
+            if (((km >> P.idx[16 + i]) & 1ull) && !((vm >> P.idx[32 + i]) & 1ull)) {
+              o.reason = KW_R_LABEL_CONSTRAINT;
+              o.arg = pack2(l - lb, i);
+              break;
+            }
           }
         }
       }
@@ -358,13 +399,14 @@ __device__ FamOut eval_family(const EvalArgs& a, const DevPolicy& P, uint64_t r)
   return o;
 }
 
-__device__ uint32_t verdict(const EvalArgs& a, const DevHeader& H, const DevPolicy* __restrict__ pols, int32_t pidx,
-                            uint64_t r, uint16_t* gstk) {
-  const DevPolicy& P = pols[pidx];
-  const uint8_t rf = a.req_flags[r];
+// EvaluationEnvironment::validate + service::evaluate constraints for one (request, policy).
+template <class S>
+__device__ uint32_t verdict(const S& src, const EvalArgs& a, const DevHeader& H, const DevPolicy* __restrict__ pols,
+                            const DevPolicy& P, uint64_t r, uint16_t* gstk, uint32_t gstride) {
+  const uint8_t rf = src.rf(r);
   // namespace bypass (service.rs:40-71), AdmissionRequest only
   if (H.bypass_bit >= 0 && !(rf & KW_REQ_RAW) && (rf & KW_REQ_HAS_NAMESPACE) &&
-      ((M(a.m[M_NS], r) >> H.bypass_bit) & 1ull))
+      ((src.template m<M_NS>(r) >> H.bypass_bit) & 1ull))
     return KW_V_ALLOWED | KW_F_ALLOWED | KW_BYPASS;
   // PolicyInitialization -> reject 500 before any constraint (service.rs:78-91)
   if (P.flags & PF_INIT_ERROR) return ((uint32_t)KW_FST_INIT_ERROR << KW_F_STATUS_SHIFT) | ((uint32_t)KW_R_INIT_ERROR << 8);
@@ -379,11 +421,11 @@ __device__ uint32_t verdict(const EvalArgs& a, const DevHeader& H, const DevPoli
       for (uint32_t s = 0; s < P.nmembers; ++s) {
         const DevPolicy& Q = pols[mem[s]];
         if (Q.flags & PF_INIT_ERROR) continue;
-        FamOut fo = eval_family(a, Q, r);
+        FamOut fo = eval_family(src, Q, r);
         if (fo.reason == 0 && !fo.mutated) ok |= 1u << s;
       }
       const uint8_t* prog = a.blob + H.prog_off + P.prog_off;
-      uint32_t vals = 0;  // bit stack of values
+      uint32_t vals = 0;  // bit stack of values; gstk holds the "called" masks
       int sp = 0;
       for (uint32_t pc = 0; pc < P.prog_len; ++pc) {
         uint8_t op = prog[pc];
@@ -395,14 +437,14 @@ __device__ uint32_t verdict(const EvalArgs& a, const DevHeader& H, const DevPoli
             e = 1u << s;
           }
           vals = (vals & ~(1u << sp)) | (v << sp);
-          gstk[sp * kEvalThreads] = (uint16_t)e;
+          gstk[sp * gstride] = (uint16_t)e;
           ++sp;
         } else if (op == G_NOT) {
           vals ^= 1u << (sp - 1);
         } else {
           --sp;
           uint32_t bv = (vals >> sp) & 1u, av = (vals >> (sp - 1)) & 1u;
-          uint32_t be = gstk[sp * kEvalThreads], ae = gstk[(sp - 1) * kEvalThreads];
+          uint32_t be = gstk[sp * gstride], ae = gstk[(sp - 1) * gstride];
           uint32_t v, e;
           if (op == G_AND) {
             v = av & bv;
@@ -418,7 +460,7 @@ __device__ uint32_t verdict(const EvalArgs& a, const DevHeader& H, const DevPoli
             e = ae | be;
           }
           vals = (vals & ~(1u << (sp - 1))) | (v << (sp - 1));
-          gstk[(sp - 1) * kEvalThreads] = (uint16_t)e;
+          gstk[(sp - 1) * gstride] = (uint16_t)e;
         }
       }
       if (!(vals & 1u)) {
@@ -427,7 +469,7 @@ __device__ uint32_t verdict(const EvalArgs& a, const DevHeader& H, const DevPoli
       }
     }
   } else {
-    FamOut fo = eval_family(a, P, r);
+    FamOut fo = eval_family(src, P, r);
     reason = fo.reason;
     arg = fo.arg;
     mutated = fo.mutated;
@@ -454,22 +496,528 @@ __device__ uint32_t verdict(const EvalArgs& a, const DevHeader& H, const DevPoli
   return v;
 }
 
-__global__ void __launch_bounds__(kEvalThreads) evaluate_kernel(EvalArgs a) {
+// Micro-batch form (kw_validate_rows): one lane per row, each row with its own policy.
+__global__ void __launch_bounds__(kEvalThreads) evaluate_rows_kernel(EvalArgs a) {
   __shared__ uint16_t gstk[kMaxGroupStack * kEvalThreads];
   const DevHeader H = *(const DevHeader*)a.blob;
   const DevPolicy* __restrict__ pols = (const DevPolicy*)(a.blob + H.policy_off);
+  GlobalSrc src{&a};
   const uint64_t stride = (uint64_t)gridDim.x * kEvalThreads;
-  for (uint64_t pair = (uint64_t)blockIdx.x * kEvalThreads + threadIdx.x; pair < a.npairs; pair += stride) {
-    uint64_t r;
-    int32_t pidx;
-    if (a.row_policy) {
-      r = pair;
-      pidx = a.row_policy[r];
-    } else {
-      r = pair / a.npol;
-      pidx = a.pols[pair - r * a.npol];
+  for (uint64_t r = (uint64_t)blockIdx.x * kEvalThreads + threadIdx.x; r < a.nrows; r += stride) {
+    const DevPolicy& P = pols[a.row_policy[r]];
+    a.out[r] = verdict(src, a, H, pols, P, r, gstk + threadIdx.x, kEvalThreads);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Tiled all-pairs kernel.
+// A workgroup owns a tile of `rows` consecutive requests at a time (persistent grid). It stages
+// the tile's request headers, container / capability / label offsets and the pattern masks of
+// every string the selected policies read into LDS — in FUSED mode computing the masks itself
+// with the LDS-resident DFA chains (no mask round trip through HBM), otherwise loading them from
+// the classify kernel's output. Evaluation is policy-major: a wave takes (policy, 64-row chunk)
+// items, so the policy, its family branch and its parameters are wave-uniform (scalar loads);
+// lanes are rows. Verdicts collect in an LDS tile buffer (stride npol+1 words, conflict-free) and
+// leave in the ABI's row-major layout with coalesced stores. A tile whose entity counts exceed the
+// LDS capacities is evaluated from global memory (FUSED: its masks are first classified into the
+// global mask arrays by the same workgroup).
+// ------------------------------------------------------------------------------------------
+template <int K>
+__device__ inline uint64_t classify_one(const Chain& ch, const uint8_t* __restrict__ bytes, uint32_t b, uint32_t e) {
+  uint64_t m = 0;
+  for (uint32_t o = ch.head; o; o = chain_next(ch, o)) {
+    DfaView v = chain_view(ch, o);
+    m |= v.acc[feed(v, v.start, bytes, b, e)];
+  }
+  return m;
+}
+
+__device__ inline void classify_image_all(const Chain* ch, const uint8_t* __restrict__ bytes, uint32_t b, uint32_t e,
+                                          uint64_t* mr, uint64_t* mt, uint64_t* mi) {
+  const ImageRef r = parse_image(bytes, b, e);
+  uint64_t m[3] = {0, 0, 0};
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+    for (uint32_t o = ch[k].head; o; o = chain_next(ch[k], o)) m[k] |= image_part(k, chain_view(ch[k], o), bytes, r);
+  *mr = m[0];
+  *mt = m[1];
+  *mi = m[2];
+}
+
+// Per-row features of a staged tile (fast path). Literal columns (capability names, AppArmor
+// profiles, label keys) match at most one pattern per string, so OR / AND reductions over a row's
+// entities answer every policy of those families exactly; the first-occurrence tables (LDS, one
+// u32 per pattern bit, written only for bits that occur) give the exact "first violation"
+// argument without rescanning the row.
+struct RowFeat {
+  uint64_t add_or;       // OR of added-capability masks
+  uint64_t dropx_and;    // AND over containers of drop masks (all ones when a container drops ALL)
+  uint64_t adddrop_and;  // AND over containers of (add | drop) masks
+  uint64_t aa_or;        // OR of AppArmor profile masks of annotated containers
+  uint64_t key_or;       // OR of label-key masks
+  uint64_t ns;           // namespace mask
+  uint32_t unk_add;      // first added capability matching no pattern: (container << 16) | index
+  uint32_t aa_unk;       // first annotated container whose profile matches no pattern
+  uint32_t priv[4];      // first privileged container, by (skip_init | skip_ephemeral << 1)
+  uint32_t rf, pad;
+};
+static_assert(sizeof(RowFeat) == 80, "RowFeat layout");
+constexpr uint32_t kNone = 0xffffffffu;
+
+struct FeatCtx {
+  const uint32_t* capf;  // [cap bits] first (c << 16 | k) of each added-capability bit
+  const uint32_t* aaf;   // [aa bits]  first container of each profile bit
+  const uint32_t* keyp;  // [key bits] label index (within the row) of each key bit
+  const uint64_t* lv;    // staged label-value masks of the tile
+  uint32_t lrow;         // index of the row's first label in lv
+};
+
+__device__ inline uint32_t min_pos(uint64_t bits, const uint32_t* table, uint32_t best) {
+  while (bits) {
+    const uint32_t b = __builtin_ctzll(bits);
+    bits &= bits - 1;
+    best = min(best, table[b]);
+  }
+  return best;
+}
+
+// Fast family evaluation from row features. TRUSTED_REPOS (glob columns, several bits per
+// string) is not reducible and is evaluated by the caller from the staged masks.
+__device__ FamOut eval_feat(const RowFeat& f, const FeatCtx& x, const DevPolicy& P) {
+  FamOut o{0, 0, false};
+  switch (P.family) {
+    case FAM_PRIVILEGED: {
+      if (!(f.rf & KW_REQ_HAS_PODSPEC)) break;
+      const uint32_t v = ((P.flags & PF_SKIP_INIT) ? 1u : 0u) | ((P.flags & PF_SKIP_EPHEMERAL) ? 2u : 0u);
+      const uint32_t p = v == 0 ? f.priv[0] : v == 1 ? f.priv[1] : v == 2 ? f.priv[2] : f.priv[3];
+      if (p != kNone) {
+        o.reason = KW_R_PRIVILEGED;
+        o.arg = pack1(p);
+      }
+      break;
     }
-    a.out[pair] = verdict(a, H, pols, pidx, r, gstk + threadIdx.x);
+    case FAM_NAMESPACE:
+      if (!((f.rf & KW_REQ_HAS_NAMESPACE) && P.nl[0] && (f.ns & P.m[0]))) o.reason = KW_R_NAMESPACE;
+      break;
+    case FAM_CAPABILITIES: {
+      if (!(f.rf & KW_REQ_HAS_PODSPEC)) break;
+      if (!(P.flags & PF_ALLOW_ALL)) {
+        const uint32_t p = min_pos(f.add_or & ~P.m[0], x.capf, f.unk_add);
+        if (p != kNone) {
+          o.reason = KW_R_CAP_NOT_ALLOWED;
+          o.arg = pack2(p >> 16, p & 0xffffu);
+          break;
+        }
+      }
+      o.mutated = (P.m[1] & ~f.dropx_and) || (P.m[2] & ~f.adddrop_and);
+      break;
+    }
+    case FAM_APPARMOR: {
+      if (!(f.rf & KW_REQ_HAS_PODSPEC)) break;
+      const uint32_t p = min_pos(f.aa_or & ~P.m[0], x.aaf, f.aa_unk);
+      if (p != kNone) {
+        o.reason = KW_R_APPARMOR;
+        o.arg = pack1(p);
+      }
+      break;
+    }
+    case FAM_LABELS: {
+      uint32_t best = min_pos(f.key_or & P.m[0], x.keyp, kNone);
+      uint32_t reason = best != kNone ? (uint32_t)KW_R_LABEL_DENIED : 0u, arg = best;
+      for (uint32_t i = 0; i < P.n_constr; ++i) {
+        const uint32_t k = P.idx[16 + i];
+        if (!((f.key_or >> k) & 1ull)) continue;
+        const uint32_t p = x.keyp[k];
+        if (p < best && !((x.lv[x.lrow + p] >> P.idx[32 + i]) & 1ull)) {
+          best = p;
+          reason = KW_R_LABEL_CONSTRAINT;
+          arg = pack2(p, i);
+        }
+      }
+      if (best != kNone) {
+        o.reason = reason;
+        o.arg = reason == KW_R_LABEL_DENIED ? pack1(arg) : arg;
+        break;
+      }
+      for (uint32_t i = 0; i < P.n_mand; ++i)
+        if (!((f.key_or >> P.idx[i]) & 1ull)) {
+          o.reason = KW_R_LABEL_MANDATORY;
+          o.arg = i;
+          break;
+        }
+      break;
+    }
+    default: break;
+  }
+  return o;
+}
+
+// Verdict word from a family result (service.rs:40-116, 160-208 epilogue).
+__device__ inline uint32_t finish(const EvalArgs& a, const DevPolicy& P, uint32_t reason, uint32_t arg, bool mutated) {
+  uint32_t v = (reason << 8) | ((arg & 0xffffu) << 16);
+  const bool allowed = reason == 0;
+  if (allowed) v |= KW_V_ALLOWED;
+  if (mutated) v |= KW_V_MUTATED;
+  uint32_t fst = allowed ? KW_FST_NONE : KW_FST_VANILLA;
+  bool fallowed = allowed;
+  if (a.origin == KW_ORIGIN_VALIDATE) {
+    if (P.mode == KW_MODE_MONITOR) {
+      fallowed = true;
+      fst = KW_FST_NONE;
+    } else if (mutated && !P.a2m) {
+      fallowed = false;
+      fst = KW_FST_MUTATION_REFUSED;
+    }
+  }
+  if (fallowed) v |= KW_F_ALLOWED;
+  if (mutated && fst == KW_FST_NONE && (a.origin == KW_ORIGIN_AUDIT || P.mode == KW_MODE_PROTECT)) v |= KW_F_PATCH;
+  v |= fst << KW_F_STATUS_SHIFT;
+  return v;
+}
+
+// Group program over member results (see verdict()).
+__device__ inline bool run_group(const EvalArgs& a, const DevHeader& H, const DevPolicy& P, uint32_t ok, uint16_t* gstk,
+                                 uint32_t gstride, uint32_t* causes) {
+  const uint8_t* prog = a.blob + H.prog_off + P.prog_off;
+  uint32_t vals = 0;
+  int sp = 0;
+  for (uint32_t pc = 0; pc < P.prog_len; ++pc) {
+    uint8_t op = prog[pc];
+    if (op <= G_CALL) {
+      uint32_t v = op == G_CONST1 ? 1u : 0u, e = 0;
+      if (op == G_CALL) {
+        uint32_t s = prog[++pc];
+        v = (ok >> s) & 1u;
+        e = 1u << s;
+      }
+      vals = (vals & ~(1u << sp)) | (v << sp);
+      gstk[sp * gstride] = (uint16_t)e;
+      ++sp;
+    } else if (op == G_NOT) {
+      vals ^= 1u << (sp - 1);
+    } else {
+      --sp;
+      uint32_t bv = (vals >> sp) & 1u, av = (vals >> (sp - 1)) & 1u;
+      uint32_t be = gstk[sp * gstride], ae = gstk[(sp - 1) * gstride];
+      uint32_t v, e;
+      if (op == G_AND) {
+        v = av & bv;
+        e = ae | (av ? be : 0u);
+      } else if (op == G_OR) {
+        v = av | bv;
+        e = ae | (av ? 0u : be);
+      } else if (op == G_EQ) {
+        v = (av == bv);
+        e = ae | be;
+      } else {
+        v = (av != bv);
+        e = ae | be;
+      }
+      vals = (vals & ~(1u << (sp - 1))) | (v << (sp - 1));
+      gstk[(sp - 1) * gstride] = (uint16_t)e;
+    }
+  }
+  *causes = (uint32_t)gstk[0] & ~ok & 0xffffu;
+  return vals & 1u;
+}
+
+template <bool FUSED>
+__global__ void __launch_bounds__(kTileThreads) evaluate_tiled_kernel(EvalArgs a, TileArgs t) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const DevHeader H = *(const DevHeader*)a.blob;
+  const DevPolicy* __restrict__ pols = (const DevPolicy*)(a.blob + H.policy_off);
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t nwaves = kTileThreads / 64;
+
+  Chain ch[NMASK];
+  if (FUSED) {
+    for (uint32_t s = 0; s < t.nstage; ++s) {
+      const uint4* src = (const uint4*)(a.blob + t.stage_blob[s]);
+      uint4* dst = (uint4*)(lds + t.stage_lds[s]);
+      for (uint32_t i = tid; i < t.stage_bytes[s] / 16; i += kTileThreads) dst[i] = src[i];
+    }
+#pragma unroll
+    for (int k = 0; k < (int)NMASK; ++k) {
+      ch[k].head = t.dfa_head[k];
+      ch[k].base = lds + t.dfa_lds[k];
+    }
+    __syncthreads();
+  }
+  uint8_t* l_rf = lds + t.o_rf;
+  uint32_t* l_coff = (uint32_t*)(lds + t.o_coff);
+  uint32_t* l_loff = (uint32_t*)(lds + t.o_loff);
+  uint8_t* l_cflags = lds + t.o_cflags;
+  uint32_t* l_cadd = (uint32_t*)(lds + t.o_cadd);
+  uint32_t* l_cdrop = (uint32_t*)(lds + t.o_cdrop);
+  RowFeat* l_feat = (RowFeat*)(lds + t.o_feat);
+  uint32_t* l_pos = (uint32_t*)(lds + t.o_pos);
+  uint16_t* gstk = t.o_gstk ? (uint16_t*)(lds + t.o_gstk) : nullptr;
+  uint64_t* l_m[NMASK];
+#pragma unroll
+  for (int k = 0; k < (int)NMASK; ++k) l_m[k] = t.o_m[k] ? (uint64_t*)(lds + t.o_m[k]) : nullptr;
+
+  const uint32_t npol = a.npol;
+  const uint32_t posstride = t.ncap_bits + t.naa_bits + t.nkey_bits;
+  const uint64_t ntiles = (a.nrows + t.rows - 1) / t.rows;
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const uint64_t r0 = tile * t.rows;
+    const uint32_t nr = (uint32_t)min((uint64_t)t.rows, a.nrows - r0);
+    const uint32_t cb = a.ctr_off[r0], ce = a.ctr_off[r0 + nr];
+    const uint32_t lb = a.lbl_off[r0], le = a.lbl_off[r0 + nr];
+    const uint32_t kab = a.capadd_off[cb], kae = a.capadd_off[ce];
+    const uint32_t kdb = a.capdrop_off[cb], kde = a.capdrop_off[ce];
+    const bool fits = (ce - cb) <= t.cmax && (kae - kab) <= t.kmax && (kde - kdb) <= t.kmax && (le - lb) <= t.lmax;
+    const uint32_t chunks = (nr + 63) / 64;
+
+    if (fits) {
+      // ---- A: stage the tile (FUSED: classify its strings with the LDS-resident DFAs)
+      for (uint32_t i = tid; i <= nr; i += kTileThreads) {
+        if (i < nr) l_rf[i] = a.req_flags[r0 + i];
+        l_coff[i] = a.ctr_off[r0 + i];
+        l_loff[i] = a.lbl_off[r0 + i];
+      }
+      const uint32_t nc = ce - cb;
+      for (uint32_t i = tid; i <= nc; i += kTileThreads) {
+        if (i < nc) l_cflags[i] = a.ctr_flags[cb + i];
+        l_cadd[i] = a.capadd_off[cb + i];
+        l_cdrop[i] = a.capdrop_off[cb + i];
+      }
+      if (FUSED) {
+        if (l_m[M_NS])
+          for (uint32_t i = tid; i < nr; i += kTileThreads)
+            l_m[M_NS][i] = classify_one<M_NS>(ch[M_NS], t.s_bytes[M_NS], t.s_off[M_NS][r0 + i], t.s_off[M_NS][r0 + i + 1]);
+        if (l_m[M_REG] || l_m[M_TAG] || l_m[M_IMG])
+          for (uint32_t i = tid; i < nc; i += kTileThreads) {
+            uint64_t mr = 0, mt = 0, mi = 0;
+            if (a.ctr_flags[cb + i] & KW_CTR_HAS_IMAGE)
+              classify_image_all(&ch[M_REG], t.s_bytes[M_IMG], t.s_off[M_IMG][cb + i], t.s_off[M_IMG][cb + i + 1], &mr,
+                                 &mt, &mi);
+            if (l_m[M_REG]) l_m[M_REG][i] = mr;
+            if (l_m[M_TAG]) l_m[M_TAG][i] = mt;
+            if (l_m[M_IMG]) l_m[M_IMG][i] = mi;
+          }
+        if (l_m[M_AA])
+          for (uint32_t i = tid; i < nc; i += kTileThreads)
+            l_m[M_AA][i] = (a.ctr_flags[cb + i] & KW_CTR_HAS_APPARMOR)
+                               ? classify_one<M_AA>(ch[M_AA], t.s_bytes[M_AA], t.s_off[M_AA][cb + i], t.s_off[M_AA][cb + i + 1])
+                               : 0ull;
+        if (l_m[M_CAPADD])
+          for (uint32_t i = tid; i < kae - kab; i += kTileThreads)
+            l_m[M_CAPADD][i] = classify_one<M_CAPADD>(ch[M_CAPADD], t.s_bytes[M_CAPADD], t.s_off[M_CAPADD][kab + i],
+                                                      t.s_off[M_CAPADD][kab + i + 1]);
+        if (l_m[M_CAPDROP])
+          for (uint32_t i = tid; i < kde - kdb; i += kTileThreads)
+            l_m[M_CAPDROP][i] = classify_one<M_CAPDROP>(ch[M_CAPDROP], t.s_bytes[M_CAPDROP], t.s_off[M_CAPDROP][kdb + i],
+                                                        t.s_off[M_CAPDROP][kdb + i + 1]);
+        if (l_m[M_LK])
+          for (uint32_t i = tid; i < le - lb; i += kTileThreads)
+            l_m[M_LK][i] = classify_one<M_LK>(ch[M_LK], t.s_bytes[M_LK], t.s_off[M_LK][lb + i], t.s_off[M_LK][lb + i + 1]);
+        if (l_m[M_LV])
+          for (uint32_t i = tid; i < le - lb; i += kTileThreads)
+            l_m[M_LV][i] = classify_one<M_LV>(ch[M_LV], t.s_bytes[M_LV], t.s_off[M_LV][lb + i], t.s_off[M_LV][lb + i + 1]);
+      } else {
+        const uint32_t base[NMASK] = {(uint32_t)r0, cb, cb, cb, kab, kdb, cb, lb, lb};
+        const uint32_t cnt[NMASK] = {nr, nc, nc, nc, kae - kab, kde - kdb, nc, le - lb, le - lb};
+#pragma unroll
+        for (int k = 0; k < (int)NMASK; ++k)
+          if (l_m[k])
+            for (uint32_t i = tid; i < cnt[k]; i += kTileThreads) l_m[k][i] = a.m[k][base[k] + i];
+      }
+      __syncthreads();
+
+      // ---- B: row features, one lane per row, entities in request order
+      for (uint32_t rr = tid; rr < nr; rr += kTileThreads) {
+        RowFeat f;
+        f.add_or = 0;
+        f.dropx_and = ~0ull;
+        f.adddrop_and = ~0ull;
+        f.aa_or = 0;
+        f.key_or = 0;
+        f.ns = l_m[M_NS] ? l_m[M_NS][rr] : 0ull;
+        f.unk_add = kNone;
+        f.aa_unk = kNone;
+        f.priv[0] = f.priv[1] = f.priv[2] = f.priv[3] = kNone;
+        f.rf = l_rf[rr];
+        f.pad = 0;
+        uint32_t* capf = l_pos + rr * posstride;
+        uint32_t* aaf = capf + t.ncap_bits;
+        uint32_t* keyp = aaf + t.naa_bits;
+        const uint32_t c0 = l_coff[rr], c1 = l_coff[rr + 1];
+        for (uint32_t c = c0; c < c1; ++c) {
+          const uint32_t ci = c - c0;
+          const uint8_t fl = l_cflags[c - cb];
+          if (fl & KW_CTR_PRIVILEGED) {
+            if (f.priv[0] == kNone) f.priv[0] = ci;
+            if (f.priv[1] == kNone && !(fl & KW_CTR_INIT)) f.priv[1] = ci;
+            if (f.priv[2] == kNone && !(fl & KW_CTR_EPHEMERAL)) f.priv[2] = ci;
+            if (f.priv[3] == kNone && !(fl & (KW_CTR_INIT | KW_CTR_EPHEMERAL))) f.priv[3] = ci;
+          }
+          if (l_m[M_CAPADD] || l_m[M_CAPDROP]) {
+            uint64_t addm = 0, dropm = 0;
+            const uint32_t k0 = l_cadd[c - cb], k1 = l_cadd[c - cb + 1];
+            if (l_m[M_CAPADD])
+              for (uint32_t k = k0; k < k1; ++k) {
+                const uint64_t m = l_m[M_CAPADD][k - kab];
+                const uint32_t pos = (ci << 16) | (k - k0);
+                if (!m && f.unk_add == kNone) f.unk_add = pos;
+                const uint64_t nb = m & ~f.add_or;
+                if (nb) capf[__builtin_ctzll(nb)] = pos;
+                f.add_or |= m;
+                addm |= m;
+              }
+            else if (k1 > k0 && f.unk_add == kNone)
+              f.unk_add = (ci << 16);  // no capability patterns at all: every added capability is unknown
+            if (l_m[M_CAPDROP])
+              for (uint32_t k = l_cdrop[c - cb]; k < l_cdrop[c - cb + 1]; ++k) dropm |= l_m[M_CAPDROP][k - kdb];
+            f.dropx_and &= (dropm & t.cap_all_mask) ? ~0ull : dropm;
+            f.adddrop_and &= addm | dropm;
+          }
+          if (l_m[M_AA] && (fl & KW_CTR_HAS_APPARMOR)) {
+            const uint64_t m = l_m[M_AA][c - cb];
+            if (!m && f.aa_unk == kNone) f.aa_unk = ci;
+            const uint64_t nb = m & ~f.aa_or;
+            if (nb) aaf[__builtin_ctzll(nb)] = ci;
+            f.aa_or |= m;
+          } else if (!l_m[M_AA] && (fl & KW_CTR_HAS_APPARMOR) && f.aa_unk == kNone) {
+            f.aa_unk = ci;  // no profile patterns: every annotated container is unknown
+          }
+        }
+        if (l_m[M_LK]) {
+          const uint32_t l0 = l_loff[rr], l1 = l_loff[rr + 1];
+          for (uint32_t l = l0; l < l1; ++l) {
+            const uint64_t km = l_m[M_LK][l - lb];
+            if (km) keyp[__builtin_ctzll(km)] = l - l0;
+            f.key_or |= km;
+          }
+        }
+        l_feat[rr] = f;
+      }
+      __syncthreads();
+
+      // ---- C: items = (policy j, 64-row chunk); the policy is wave-uniform, lanes are rows
+      TileSrc src;
+      src.rf_ = l_rf;
+      src.coff_ = l_coff;
+      src.loff_ = l_loff;
+      src.cadd_ = l_cadd;
+      src.cdrop_ = l_cdrop;
+      src.cflags_ = l_cflags;
+#pragma unroll
+      for (int k = 0; k < (int)NMASK; ++k) src.m_[k] = l_m[k];
+      src.r0 = r0;
+      src.cb = cb;
+      src.lb = lb;
+      src.kab = kab;
+      src.kdb = kdb;
+      const uint32_t ngroups = (npol + 3) / 4;
+      for (uint32_t item = wave; item < ngroups * chunks; item += nwaves) {
+        const uint32_t g = __builtin_amdgcn_readfirstlane(item / chunks);
+        const uint32_t rr = (item - g * chunks) * 64 + lane;
+        if (rr >= nr) continue;
+        const RowFeat f = l_feat[rr];
+        FeatCtx x;
+        x.capf = l_pos + rr * posstride;
+        x.aaf = x.capf + t.ncap_bits;
+        x.keyp = x.aaf + t.naa_bits;
+        x.lv = l_m[M_LV];
+        x.lrow = l_loff[rr] - lb;
+        const bool bypass =
+            H.bypass_bit >= 0 && !(f.rf & KW_REQ_RAW) && (f.rf & KW_REQ_HAS_NAMESPACE) && ((f.ns >> H.bypass_bit) & 1ull);
+        uint32_t vv[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (uint32_t jj = 0; jj < 4; ++jj) {
+          const uint32_t j = g * 4 + jj;
+          if (j >= npol) break;
+          const DevPolicy& P = pols[a.pols[j]];
+          uint32_t v;
+          if (bypass) {
+            v = KW_V_ALLOWED | KW_F_ALLOWED | KW_BYPASS;
+          } else if (P.flags & PF_INIT_ERROR) {
+            v = ((uint32_t)KW_FST_INIT_ERROR << KW_F_STATUS_SHIFT) | ((uint32_t)KW_R_INIT_ERROR << 8);
+          } else if (P.family == FAM_GROUP) {
+            uint32_t reason = 0, arg = 0;
+            if (P.flags & PF_EXPR_ERROR) {
+              reason = KW_R_GROUP_EXPR;
+            } else {
+              const int32_t* mem = (const int32_t*)(a.blob + H.member_off) + P.member_off;
+              uint32_t ok = 0;
+              for (uint32_t sl = 0; sl < P.nmembers; ++sl) {
+                const DevPolicy& Q = pols[mem[sl]];
+                if (Q.flags & PF_INIT_ERROR) continue;
+                FamOut fo = Q.family == FAM_TRUSTED_REPOS ? eval_family(src, Q, r0 + rr) : eval_feat(f, x, Q);
+                if (fo.reason == 0 && !fo.mutated) ok |= 1u << sl;
+              }
+              uint32_t causes;
+              if (!run_group(a, H, P, ok, gstk + tid, kTileThreads, &causes)) {
+                reason = KW_R_GROUP;
+                arg = causes;
+              }
+            }
+            v = finish(a, P, reason, arg, false);
+          } else {
+            FamOut fo = P.family == FAM_TRUSTED_REPOS ? eval_family(src, P, r0 + rr) : eval_feat(f, x, P);
+            v = finish(a, P, fo.reason, fo.arg, fo.mutated);
+          }
+          vv[jj] = v;
+        }
+        uint32_t* dst = a.out + (r0 + rr) * npol + g * 4;
+        if ((npol & 3u) == 0) {
+          *(uint4*)dst = make_uint4(vv[0], vv[1], vv[2], vv[3]);
+        } else {
+#pragma unroll
+          for (uint32_t jj = 0; jj < 4; ++jj)
+            if (g * 4 + jj < npol) dst[jj] = vv[jj];
+        }
+      }
+    } else {
+      // ---- oversize tile: global path
+      if (FUSED) {
+        // classify this tile's strings into the global mask arrays (same workgroup reads them back)
+        const uint32_t nc = ce - cb;
+        if (a.m[M_NS])
+          for (uint32_t i = tid; i < nr; i += kTileThreads)
+            ((uint64_t*)a.m[M_NS])[r0 + i] = classify_one<M_NS>(ch[M_NS], t.s_bytes[M_NS], t.s_off[M_NS][r0 + i], t.s_off[M_NS][r0 + i + 1]);
+        if (a.m[M_REG] || a.m[M_TAG] || a.m[M_IMG])
+          for (uint32_t i = tid; i < nc; i += kTileThreads) {
+            uint64_t mr = 0, mt = 0, mi = 0;
+            if (a.ctr_flags[cb + i] & KW_CTR_HAS_IMAGE)
+              classify_image_all(&ch[M_REG], t.s_bytes[M_IMG], t.s_off[M_IMG][cb + i], t.s_off[M_IMG][cb + i + 1], &mr,
+                                 &mt, &mi);
+            if (a.m[M_REG]) ((uint64_t*)a.m[M_REG])[cb + i] = mr;
+            if (a.m[M_TAG]) ((uint64_t*)a.m[M_TAG])[cb + i] = mt;
+            if (a.m[M_IMG]) ((uint64_t*)a.m[M_IMG])[cb + i] = mi;
+          }
+        if (a.m[M_AA])
+          for (uint32_t i = tid; i < nc; i += kTileThreads)
+            ((uint64_t*)a.m[M_AA])[cb + i] = (a.ctr_flags[cb + i] & KW_CTR_HAS_APPARMOR)
+                                                 ? classify_one<M_AA>(ch[M_AA], t.s_bytes[M_AA], t.s_off[M_AA][cb + i], t.s_off[M_AA][cb + i + 1])
+                                                 : 0ull;
+        if (a.m[M_CAPADD])
+          for (uint32_t i = kab + tid; i < kae; i += kTileThreads)
+            ((uint64_t*)a.m[M_CAPADD])[i] = classify_one<M_CAPADD>(ch[M_CAPADD], t.s_bytes[M_CAPADD], t.s_off[M_CAPADD][i], t.s_off[M_CAPADD][i + 1]);
+        if (a.m[M_CAPDROP])
+          for (uint32_t i = kdb + tid; i < kde; i += kTileThreads)
+            ((uint64_t*)a.m[M_CAPDROP])[i] = classify_one<M_CAPDROP>(ch[M_CAPDROP], t.s_bytes[M_CAPDROP], t.s_off[M_CAPDROP][i], t.s_off[M_CAPDROP][i + 1]);
+        if (a.m[M_LK])
+          for (uint32_t i = lb + tid; i < le; i += kTileThreads)
+            ((uint64_t*)a.m[M_LK])[i] = classify_one<M_LK>(ch[M_LK], t.s_bytes[M_LK], t.s_off[M_LK][i], t.s_off[M_LK][i + 1]);
+        if (a.m[M_LV])
+          for (uint32_t i = lb + tid; i < le; i += kTileThreads)
+            ((uint64_t*)a.m[M_LV])[i] = classify_one<M_LV>(ch[M_LV], t.s_bytes[M_LV], t.s_off[M_LV][i], t.s_off[M_LV][i + 1]);
+        __threadfence();
+        __syncthreads();
+      }
+      GlobalSrc src{&a};
+      for (uint32_t item = wave; item < npol * chunks; item += nwaves) {
+        const uint32_t j = __builtin_amdgcn_readfirstlane(item / chunks);
+        const uint32_t rr = (item - j * chunks) * 64 + lane;
+        const DevPolicy& P = pols[a.pols[j]];
+        if (rr < nr) a.out[(r0 + rr) * npol + j] = verdict(src, a, H, pols, P, r0 + rr, gstk ? gstk + tid : nullptr, kTileThreads);
+      }
+    }
+    __syncthreads();  // the next tile restages LDS
   }
 }
 
@@ -483,11 +1031,29 @@ hipError_t launch_classify(const uint8_t* d_blob, const ClassifyJobs& jobs, hipS
   return hipGetLastError();
 }
 
-hipError_t launch_evaluate(const EvalArgs& a, hipStream_t s) {
-  if (a.npairs == 0) return hipSuccess;
-  uint64_t blocks = (a.npairs + kEvalThreads - 1) / kEvalThreads;
-  if (blocks > 256 * 16) blocks = 256 * 16;  // grid-stride beyond 16 blocks per CU
-  hipLaunchKernelGGL(evaluate_kernel, dim3((uint32_t)blocks), dim3(kEvalThreads), 0, s, a);
+hipError_t launch_evaluate_rows(const EvalArgs& a, hipStream_t s) {
+  if (a.nrows == 0) return hipSuccess;
+  uint64_t blocks = (a.nrows + kEvalThreads - 1) / kEvalThreads;
+  if (blocks > 256 * 16) blocks = 256 * 16;
+  hipLaunchKernelGGL(evaluate_rows_kernel, dim3((uint32_t)blocks), dim3(kEvalThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_evaluate_tiled(const EvalArgs& a, const TileArgs& t, bool fused, uint32_t grid, hipStream_t s) {
+  if (a.nrows == 0 || a.npol == 0) return hipSuccess;
+  static bool attr_set = false;  // allow > 64 KB of dynamic LDS per workgroup (gfx950: 160 KB per CU)
+  if (!attr_set) {
+    hipError_t e1 = hipFuncSetAttribute((const void*)evaluate_tiled_kernel<true>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipError_t e2 = hipFuncSetAttribute((const void*)evaluate_tiled_kernel<false>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e1 != hipSuccess || e2 != hipSuccess) return e1 != hipSuccess ? e1 : e2;
+    attr_set = true;
+  }
+  if (fused)
+    hipLaunchKernelGGL(evaluate_tiled_kernel<true>, dim3(grid), dim3(kTileThreads), t.lds_bytes, s, a, t);
+  else
+    hipLaunchKernelGGL(evaluate_tiled_kernel<false>, dim3(grid), dim3(kTileThreads), t.lds_bytes, s, a, t);
   return hipGetLastError();
 }
 

@@ -53,7 +53,29 @@ struct EvalArgs {
   uint32_t* out;
 };
 
+constexpr int kTileThreads = 512;
+
+// Tiled all-pairs evaluation (kernels.hip evaluate_tiled_kernel): LDS layout and capacities.
+struct TileArgs {
+  uint32_t rows;                  // requests per tile
+  uint32_t cmax, kmax, lmax;      // container / capability / label capacity of a staged tile
+  uint32_t o_rf, o_coff, o_loff, o_cflags, o_cadd, o_cdrop, o_gstk;  // LDS byte offsets
+  uint32_t o_m[NMASK];            // LDS byte offset of each staged mask array, 0 = not read
+  uint32_t o_feat, o_pos;         // per-row features (RowFeat) and first-occurrence tables
+  uint32_t ncap_bits, naa_bits, nkey_bits;  // pattern counts of the literal columns
+  uint64_t cap_all_mask;          // COL_CAP bit of the "ALL" capability (0 if none)
+  uint32_t lds_bytes;
+  // FUSED: DFA chains staged once per workgroup, and the string columns they classify
+  uint32_t nstage;
+  uint32_t stage_blob[NCOL], stage_lds[NCOL], stage_bytes[NCOL];
+  uint32_t dfa_head[NMASK];       // blob offset of the chain used for mask k (0 = none)
+  uint32_t dfa_lds[NMASK];        // LDS offset of that chain's head
+  const uint32_t* s_off[NMASK];   // string offsets feeding mask k (M_REG/TAG use M_IMG's column)
+  const uint8_t* s_bytes[NMASK];
+};
+
 hipError_t launch_classify(const uint8_t* d_blob, const ClassifyJobs& jobs, hipStream_t s);
-hipError_t launch_evaluate(const EvalArgs& a, hipStream_t s);
+hipError_t launch_evaluate_rows(const EvalArgs& a, hipStream_t s);
+hipError_t launch_evaluate_tiled(const EvalArgs& a, const TileArgs& t, bool fused, uint32_t grid, hipStream_t s);
 
 }  // namespace kw

@@ -1,0 +1,195 @@
+"""CPU: the oracle is pinned to the reference's own test tables (tests/golden/reference_cases.json,
+transcribed from src/evaluation/policy_id.rs, src/api/service.rs, src/config.rs,
+src/evaluation/evaluation_environment.rs), and the product's host logic (libkwgpu.so: PolicyID,
+schema, constraints, group-expression validation) agrees with the same tables."""
+import json
+
+import pytest
+import yaml
+
+import kwgpu as K
+import oracle as O
+from helpers import golden
+
+G = golden("reference_cases.json")
+MODE = {"protect": O.PROTECT, "monitor": O.MONITOR}
+ORIGIN = {"validate": O.VALIDATE, "audit": O.AUDIT}
+
+
+# ------------------------------------------------------------------------------ PolicyID
+@pytest.mark.parametrize("case", G["policy_id"], ids=lambda c: c["ref"])
+def test_policy_id_oracle(case):
+    if "error" in case:
+        with pytest.raises(O.InvalidPolicyId) as e:
+            O.parse_policy_id(case["input"])
+        assert str(e.value) == case["error"]
+    else:
+        pid = O.parse_policy_id(case["input"])
+        exp = case["expected"]
+        assert pid == (("policy", exp["policy"]) if "policy" in exp else ("member", exp["group"], exp["name"]))
+        assert O.policy_id_display(pid) == case["input"]
+
+
+@pytest.mark.parametrize("case", G["policy_id"], ids=lambda c: c["ref"])
+def test_policy_id_product(case):
+    env = K.EvaluationEnvironment({
+        "policy1": {"module": "pod-privileged"},
+        "group1": {"policies": {"policy1": {"module": "pod-privileged"}}, "expression": "policy1()", "message": "m"},
+    })
+    if "error" in case:
+        with pytest.raises(K.InvalidPolicyId) as e:
+            env.lookup(case["input"])
+        assert str(e.value) == case["error"]
+    else:
+        idx = env.lookup(case["input"])
+        assert env.policy_id(idx) == case["input"]  # Display round trip (policy_id.rs:20-27)
+
+
+# ------------------------------------------------------------------------------ constraints
+def _flags(resp):
+    return resp["allowed"], resp.get("patch") is not None, resp.get("status") is not None
+
+
+@pytest.mark.parametrize("case", G["constraints"], ids=lambda c: c["ref"])
+def test_constraints_oracle(case):
+    got = O.constraints("policy-id", MODE[case["mode"]], case["a2m"], case["in"])
+    assert got == case["out"]
+
+
+@pytest.mark.parametrize("case", G["constraints"], ids=lambda c: c["ref"])
+def test_constraints_product(case):
+    allowed, patch, status = _flags(case["in"])
+    fst, a, p, s = K.service_constraints(allowed, patch, status, MODE[case["mode"]], case["a2m"])
+    assert (a, p, s) == _flags(case["out"])
+    if fst == K._native.KW_FST_MUTATION_REFUSED:
+        assert case["out"]["status"]["message"] == G["integration"]["mutation_refused"]["template"].format(
+            policy_id="policy-id")
+
+
+# ------------------------------------------------------------------------------ service::evaluate (mock env)
+@pytest.mark.parametrize("case", G["evaluate"], ids=lambda c: c["ref"])
+def test_evaluate_oracle(case):
+    req = G["admission_review_request"]["request"]
+    vanilla = {"allowed": True} if case["env"] == "accept" else {"allowed": False,
+                                                                 "status": {"message": "boom", "code": 500}}
+    ns = case.get("namespace", req["namespace"])
+    got = O.service_evaluate("test_policy1", MODE[case["mode"]], False, ORIGIN[case["origin"]], vanilla,
+                             uid=req["uid"], namespace=ns, always_accept=case.get("always_accept"),
+                             raw=case.get("raw", False))
+    assert got["allowed"] is case["allowed"]
+    if "status" in case:
+        assert got.get("status") == case["status"]
+
+
+# ------------------------------------------------------------------------------ groups
+@pytest.mark.parametrize("case", G["groups"], ids=lambda c: c["ref"])
+def test_group_short_circuit_oracle(case):
+    names = list(case["members"])
+    ast = O.parse_expression(case["expression"], names)
+    ok = [case["members"][n] == "happy" for n in names]
+    value, called = O.eval_expression(ast, ok)
+    assert value is case["allowed"]
+    causes = [{"field": f"spec.policies.{names[s]}", "message": "failing as expected"} for s in called if not ok[s]]
+    if case["allowed"]:
+        assert case["causes"] == []
+    else:
+        for c in case["causes"]:
+            assert c in causes
+
+
+@pytest.mark.parametrize("case", G["group_expressions"], ids=lambda c: c["ref"])
+def test_group_expression_validity(case):
+    members = {m: {"module": "pod-privileged"} for m in case["members"]}
+    doc = {"g": {"policies": members, "expression": case["expression"], "message": "something went wrong"}}
+    # oracle
+    oe = O.OracleEnv(doc)
+    assert oe.pol[0]["valid"] is case["valid"]
+    # product: EvaluationEnvironment::validate_settings
+    env = K.EvaluationEnvironment(doc)
+    if case["valid"]:
+        env.validate_settings("g")
+    else:
+        with pytest.raises(K.PolicyInitialization):
+            env.validate_settings("g")
+
+
+@pytest.mark.parametrize("case", G["lookup"], ids=lambda c: c["ref"])
+def test_lookup(case):
+    env = K.EvaluationEnvironment({"happy_policy_1": {"module": "pod-privileged"}})
+    if case["error"]:
+        with pytest.raises(K.PolicyNotFound):
+            env.get_policy_mode(case["policy"])
+        with pytest.raises(K.PolicyNotFound):
+            env.get_policy_allowed_to_mutate(case["policy"])
+    else:
+        assert env.get_policy_mode(case["policy"]) == K.PROTECT
+        assert env.get_policy_allowed_to_mutate(case["policy"]) is False
+
+
+# ------------------------------------------------------------------------------ policies.yml schema
+def test_read_policies_file():
+    c = G["config"]["read_policies_file"]
+    doc = yaml.safe_load(c["yaml"])
+    entries = {k: O.parse_entry(k, v) for k, v in doc.items()}
+    ex, grp = entries["example"], entries["group_policy"]
+    e = c["expected"]
+    assert ex["module"] == e["example"]["module"] and ex["mode"] == O.PROTECT and ex["a2m"] is True
+    assert ex["settings"] == {}
+    assert grp["group"] and grp["mode"] == O.MONITOR and grp["expression"] == "true"
+    assert grp["message"] == "group policy message"
+    assert [m["name"] for m in grp["members"]] == e["group_policy"]["members"]
+    # product: the same document builds (modules outside the declarative class recorded as init errors)
+    env = K.EvaluationEnvironment(doc, continue_on_errors=True)
+    assert env.policy_ids() == ["example", "group_policy", "group_policy/policy1", "group_policy/policy2"]
+    assert env.get_policy_mode("group_policy") == K.MONITOR
+    assert env.get_policy_allowed_to_mutate("group_policy") is False  # groups never mutate
+    with pytest.raises(K.PolicyNotFound):  # unsupported module -> not registered
+        env.get_policy_mode("example")
+
+
+@pytest.mark.parametrize("case", G["config"]["settings_conversion"], ids=lambda c: c["ref"])
+def test_settings_conversion(case):
+    doc = yaml.safe_load(case["yaml"])
+    assert O.parse_entry("example", doc["example"])["settings"] == case["expected"]
+    # product: identical policies for None / null / {} settings -> identical compiled tables
+    env = K.EvaluationEnvironment(doc, continue_on_errors=True)
+    err = env.policy_initialization_error("example")
+    if case["expected"] == {}:
+        assert err == "Policy settings are invalid: valid_namespace must be a non-empty string"
+
+
+@pytest.mark.parametrize("case", G["config"]["policy_validation"], ids=lambda c: c["ref"])
+def test_policy_validation(case):
+    doc = yaml.safe_load(case["yaml"])
+    entries = [O.parse_entry(k, v) for k, v in doc.items()]
+    if case["valid"]:
+        O.validate_policies(entries)
+        K.EvaluationEnvironment(doc, continue_on_errors=True)
+    else:
+        with pytest.raises(O.ConfigError):
+            O.validate_policies(entries)
+        with pytest.raises(K.BootstrapFailure) as e:
+            K.EvaluationEnvironment(doc, continue_on_errors=True)
+        assert "'/'" in str(e.value) or "invalid names" in str(e.value)
+
+
+def test_untagged_enum_errors():
+    for bad in ({"x": {"policyMode": "protect"}}, {"x": {"module": "m", "policyMode": "loud"}},
+                {"x": {"policies": {"a": {"module": "m", "extra": 1}}, "expression": "a()", "message": "m"}},
+                {"x": {"module": "m", "settings": [1, 2]}}):
+        with pytest.raises(O.ConfigError):
+            [O.parse_entry(k, v) for k, v in bad.items()]
+        with pytest.raises(K.BootstrapFailure) as e:
+            K.EvaluationEnvironment(bad, continue_on_errors=True)
+        assert "did not match any variant" in str(e.value)
+
+
+def test_error_display_strings():
+    e = G["errors"]
+    env = K.EvaluationEnvironment({"p": {"module": "pod-privileged"}})
+    with pytest.raises(K.PolicyNotFound) as x:
+        env.lookup("nope")
+    assert str(x.value) == e["PolicyNotFound"].format("nope")
+    assert K.http_status(K.PolicyNotFound.code) == e["http"]["PolicyNotFound"]
+    assert K.http_status(K.PolicyInitialization.code) == e["http"]["other"]
+    assert json.loads(json.dumps(e))  # fixture well-formed

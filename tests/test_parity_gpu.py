@@ -72,7 +72,7 @@ def test_responses_match_oracle(name, scfg, rows):
             got = b.format_response(env, r, j, int(v[r, j]), mv)
             assert got == want, (r, pid, got, want)
             checked += 1
-    assert checked > 1000
+    assert checked >= min(1000, 600 * len(ids) // 2)
 
 
 def test_row_mode_equals_all_pairs():
