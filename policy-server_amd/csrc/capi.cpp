@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -305,13 +306,23 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
   auto align = [](uint32_t x) { return (x + 15u) & ~15u; };
   double cpr = B.n ? nc / n : 1, lpr = B.n ? (double)B.labels() / n : 1;
   double apr = nc ? (double)B.cap_add.n() / nc : 1, dpr = nc ? (double)B.cap_drop.n() / nc : 1;
+  uint32_t chain_len[NMASK];
+  for (int m = 0; m < (int)NMASK; ++m) {
+    chain_len[m] = 1;
+    // image chains are walked by one item; the non-fused path stages the classify kernel's merged masks
+    if (!plan->fused || !use[m] || m == M_REG || m == M_TAG || m == M_IMG) continue;
+    uint32_t n = 0;
+    for (uint32_t o = H->dfa_off[mask_col(m)]; o; o = ((const DevDfa*)(E.blob.data() + o))->next) ++n;
+    chain_len[m] = std::max<uint32_t>(1, n);
+  }
   uint32_t rows = std::max<uint32_t>(64, std::min<uint32_t>(1024, ((4096 / std::max<uint32_t>(npol, 1)) + 63) / 64 * 64));
   const uint32_t ncap = (uint32_t)E.cols[COL_CAP].size(), naa = (uint32_t)E.cols[COL_AA].size(),
                  nkey = (uint32_t)E.cols[COL_LK].size();
+  double scale = 1.5;  // capacity headroom over the batch average; tiles beyond it take the global path
   for (;;) {
-    uint32_t cmax = (uint32_t)std::min(65536.0, 1.5 * rows * cpr + 32);
-    uint32_t kmax = (uint32_t)std::min(65536.0, 1.5 * rows * cpr * std::max(apr, dpr) + 32);
-    uint32_t lmax = (uint32_t)std::min(65536.0, 1.5 * rows * lpr + 32);
+    uint32_t cmax = (uint32_t)std::min(16.0 * rows + 64, scale * rows * cpr + 32);
+    uint32_t kmax = (uint32_t)std::min(16.0 * rows + 64, scale * rows * cpr * std::max(apr, dpr) + 32);
+    uint32_t lmax = (uint32_t)std::min(16.0 * rows + 64, scale * rows * lpr + 32);
     uint32_t off = 16;
     uint32_t stage_at = off;
     if (plan->fused) off = align(off + table_bytes);
@@ -332,10 +343,16 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
       if (!use[m]) continue;
       uint32_t cnt = m == M_NS ? rows : (m == M_CAPADD || m == M_CAPDROP) ? kmax : (m == M_LK || m == M_LV) ? lmax : cmax;
       T.o_m[m] = off;
-      off = align(off + cnt * 8);
+      T.mask_cap[m] = cnt;
+      off = align(off + cnt * 8 * chain_len[m]);  // one partial slot per DFA of the column chain
+    }
+    T.o_pols = 0;
+    if (E.pol.size() * sizeof(DevPolicy) <= 24 * 1024) {
+      T.o_pols = off;
+      off = align(off + (uint32_t)(E.pol.size() * sizeof(DevPolicy)));
     }
     T.o_feat = off;
-    off = align(off + rows * 80);
+    off = align(off + rows * (5 * 8 + 6 * 4));
     T.o_pos = off;
     off = align(off + rows * (ncap + naa + nkey) * 4);
     T.ncap_bits = ncap;
@@ -346,8 +363,12 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
       T.o_gstk = off;
       off = align(off + kMaxGroupStack * kTileThreads * 2);
     }
-    if (off > kTileLdsBudget && rows > 16) {
+    if (off > kTileLdsBudget && rows > 64) {
       rows /= 2;
+      continue;
+    }
+    if (off > kTileLdsBudget && scale > 0.05) {
+      scale /= 2;
       continue;
     }
     T.rows = rows;
@@ -382,6 +403,8 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
     break;
   }
   if (T.lds_bytes > kTileLdsBudget) return KW_E_ARG;  // npol too large for one tile row
+  if (const char* dbg = getenv("KW_TILE_DEBUG")) T.debug = (uint32_t)atoi(dbg);  // phase ablation (diagnostics)
+  for (int m = 0; m < (int)NMASK; ++m) T.chain_len[m] = chain_len[m];
   T.cap_all_mask = 0;
   for (size_t i = 0; i < E.cols[COL_CAP].size(); ++i)
     if (E.cols[COL_CAP][i].text == "ALL") T.cap_all_mask = 1ull << i;

@@ -262,6 +262,13 @@ struct GlobalSrc {
   __device__ uint64_t m(uint64_t i) const { return a->m[K] ? a->m[K][i] : 0ull; }
 };
 
+// A staged mask of a chained column is the OR of its per-DFA partial slots ([chain][cap]).
+__device__ inline uint64_t staged_mask(const uint64_t* m, uint32_t i, uint32_t clen, uint32_t cap) {
+  uint64_t r = m[i];
+  for (uint32_t e = 1; e < clen; ++e) r |= m[e * cap + i];
+  return r;
+}
+
 struct TileSrc {
   const uint8_t* rf_;
   const uint32_t *coff_, *loff_, *cadd_, *cdrop_;
@@ -269,6 +276,8 @@ struct TileSrc {
   const uint64_t* m_[NMASK];
   uint64_t r0;
   uint32_t cb, lb, kab, kdb;
+  uint32_t clen_[NMASK];  // chain length per mask (indexed by template constants only)
+  uint32_t cap_[NMASK];   // staged capacity per mask
   __device__ uint8_t rf(uint64_t r) const { return rf_[r - r0]; }
   __device__ uint32_t coff(uint64_t r) const { return coff_[r - r0]; }
   __device__ uint32_t loff(uint64_t r) const { return loff_[r - r0]; }
@@ -279,11 +288,9 @@ struct TileSrc {
   __device__ uint64_t m(uint64_t i) const {
     const uint64_t* p = m_[K];
     if (!p) return 0ull;
-    if (K == M_NS) return p[i - r0];
-    if (K == M_CAPADD) return p[i - kab];
-    if (K == M_CAPDROP) return p[i - kdb];
-    if (K == M_LK || K == M_LV) return p[i - lb];
-    return p[i - cb];
+    const uint32_t j = K == M_NS ? (uint32_t)(i - r0) : K == M_CAPADD ? (uint32_t)(i - kab) : K == M_CAPDROP ? (uint32_t)(i - kdb)
+                       : (K == M_LK || K == M_LV) ? (uint32_t)(i - lb) : (uint32_t)(i - cb);
+    return staged_mask(p, j, clen_[K], cap_[K]);
   }
 };
 
@@ -532,16 +539,16 @@ __device__ inline uint64_t classify_one(const Chain& ch, const uint8_t* __restri
   return m;
 }
 
-__device__ inline void classify_image_all(const Chain* ch, const uint8_t* __restrict__ bytes, uint32_t b, uint32_t e,
-                                          uint64_t* mr, uint64_t* mt, uint64_t* mi) {
+__device__ inline void classify_image_all(const Chain cr, const Chain ct, const Chain ci, const uint8_t* __restrict__ bytes,
+                                          uint32_t b, uint32_t e, uint64_t* mr, uint64_t* mt, uint64_t* mi) {
   const ImageRef r = parse_image(bytes, b, e);
-  uint64_t m[3] = {0, 0, 0};
-#pragma unroll
-  for (int k = 0; k < 3; ++k)
-    for (uint32_t o = ch[k].head; o; o = chain_next(ch[k], o)) m[k] |= image_part(k, chain_view(ch[k], o), bytes, r);
-  *mr = m[0];
-  *mt = m[1];
-  *mi = m[2];
+  uint64_t m0 = 0, m1 = 0, m2 = 0;
+  for (uint32_t o = cr.head; o; o = chain_next(cr, o)) m0 |= image_part(0, chain_view(cr, o), bytes, r);
+  for (uint32_t o = ct.head; o; o = chain_next(ct, o)) m1 |= image_part(1, chain_view(ct, o), bytes, r);
+  for (uint32_t o = ci.head; o; o = chain_next(ci, o)) m2 |= image_part(2, chain_view(ci, o), bytes, r);
+  *mr = m0;
+  *mt = m1;
+  *mi = m2;
 }
 
 // Per-row features of a staged tile (fast path). Literal columns (capability names, AppArmor
@@ -732,6 +739,13 @@ __global__ void __launch_bounds__(kTileThreads) evaluate_tiled_kernel(EvalArgs a
   const uint32_t nwaves = kTileThreads / 64;
 
   Chain ch[NMASK];
+  if (t.o_pols) {  // the policy table, read with wave-uniform addresses in phase C (LDS broadcast)
+    const uint4* src = (const uint4*)pols;
+    uint4* dst = (uint4*)(lds + t.o_pols);
+    for (uint32_t i = tid; i < H.npolicies * (uint32_t)sizeof(DevPolicy) / 16; i += kTileThreads) dst[i] = src[i];
+    if (!FUSED) __syncthreads();
+  }
+  const DevPolicy* __restrict__ tpols = t.o_pols ? (const DevPolicy*)(lds + t.o_pols) : pols;
   if (FUSED) {
     for (uint32_t s = 0; s < t.nstage; ++s) {
       const uint4* src = (const uint4*)(a.blob + t.stage_blob[s]);
@@ -751,7 +765,16 @@ __global__ void __launch_bounds__(kTileThreads) evaluate_tiled_kernel(EvalArgs a
   uint8_t* l_cflags = lds + t.o_cflags;
   uint32_t* l_cadd = (uint32_t*)(lds + t.o_cadd);
   uint32_t* l_cdrop = (uint32_t*)(lds + t.o_cdrop);
-  RowFeat* l_feat = (RowFeat*)(lds + t.o_feat);
+  // row features, SoA (lane = row reads are bank-conflict free)
+  const uint32_t rows = t.rows;
+  uint64_t* f_add_or = (uint64_t*)(lds + t.o_feat);
+  uint64_t* f_dropx_and = f_add_or + rows;
+  uint64_t* f_adddrop_and = f_dropx_and + rows;
+  uint64_t* f_aa_or = f_adddrop_and + rows;
+  uint64_t* f_key_or = f_aa_or + rows;
+  uint32_t* f_unk_add = (uint32_t*)(f_key_or + rows);
+  uint32_t* f_aa_unk = f_unk_add + rows;
+  uint32_t* f_priv = f_aa_unk + rows;  // [4][rows]
   uint32_t* l_pos = (uint32_t*)(lds + t.o_pos);
   uint16_t* gstk = t.o_gstk ? (uint16_t*)(lds + t.o_gstk) : nullptr;
   uint64_t* l_m[NMASK];
@@ -772,11 +795,29 @@ __global__ void __launch_bounds__(kTileThreads) evaluate_tiled_kernel(EvalArgs a
     const uint32_t chunks = (nr + 63) / 64;
 
     if (fits) {
-      // ---- A: stage the tile (FUSED: classify its strings with the LDS-resident DFAs)
+      // ---- A: stage the tile; classify its strings (FUSED) from one flattened work list over
+      //      every column and every DFA of a column's chain (chained DFAs OR into pre-zeroed masks)
       for (uint32_t i = tid; i <= nr; i += kTileThreads) {
-        if (i < nr) l_rf[i] = a.req_flags[r0 + i];
+        if (i < nr) {
+          l_rf[i] = a.req_flags[r0 + i];
+          f_add_or[i] = 0;
+          f_aa_or[i] = 0;
+          f_key_or[i] = 0;
+          f_dropx_and[i] = ~0ull;
+          f_adddrop_and[i] = ~0ull;
+          f_unk_add[i] = kNone;
+          f_aa_unk[i] = kNone;
+          f_priv[i] = kNone;
+          f_priv[rows + i] = kNone;
+          f_priv[2 * rows + i] = kNone;
+          f_priv[3 * rows + i] = kNone;
+        }
         l_coff[i] = a.ctr_off[r0 + i];
         l_loff[i] = a.lbl_off[r0 + i];
+      }
+      for (uint32_t i = tid; i < nr * (t.ncap_bits + t.naa_bits); i += kTileThreads) {
+        const uint32_t rr = i / (t.ncap_bits + t.naa_bits), b = i - rr * (t.ncap_bits + t.naa_bits);
+        l_pos[rr * posstride + b] = kNone;
       }
       const uint32_t nc = ce - cb;
       for (uint32_t i = tid; i <= nc; i += kTileThreads) {
@@ -784,40 +825,56 @@ __global__ void __launch_bounds__(kTileThreads) evaluate_tiled_kernel(EvalArgs a
         l_cadd[i] = a.capadd_off[cb + i];
         l_cdrop[i] = a.capdrop_off[cb + i];
       }
-      if (FUSED) {
-        if (l_m[M_NS])
-          for (uint32_t i = tid; i < nr; i += kTileThreads)
-            l_m[M_NS][i] = classify_one<M_NS>(ch[M_NS], t.s_bytes[M_NS], t.s_off[M_NS][r0 + i], t.s_off[M_NS][r0 + i + 1]);
-        if (l_m[M_REG] || l_m[M_TAG] || l_m[M_IMG])
-          for (uint32_t i = tid; i < nc; i += kTileThreads) {
+      if (FUSED && !(t.debug & 1u)) {
+        // work list: (job, string, chain element); jobs in order NS, IMG, AA, CAPADD, CAPDROP, LK, LV.
+        // Per-job parameters come from the kernarg arrays (runtime-indexable without scratch).
+        const uint32_t n0 = t.o_m[M_NS] ? nr : 0u;
+        const uint32_t n1 = (t.o_m[M_REG] || t.o_m[M_TAG] || t.o_m[M_IMG]) ? nc : 0u;
+        const uint32_t n2 = t.o_m[M_AA] ? nc : 0u;
+        const uint32_t n3 = t.o_m[M_CAPADD] ? (kae - kab) * t.chain_len[M_CAPADD] : 0u;
+        const uint32_t n4 = t.o_m[M_CAPDROP] ? (kde - kdb) * t.chain_len[M_CAPDROP] : 0u;
+        const uint32_t n5 = t.o_m[M_LK] ? (le - lb) * t.chain_len[M_LK] : 0u;
+        const uint32_t n6 = t.o_m[M_LV] ? (le - lb) * t.chain_len[M_LV] : 0u;
+        const uint32_t s1 = n0, s2 = s1 + n1, s3 = s2 + n2 * t.chain_len[M_AA], s4 = s3 + n3, s5 = s4 + n4,
+                       s6 = s5 + n5, s7 = s6 + n6;
+        for (uint32_t w = tid; w < s7; w += kTileThreads) {
+          if (w >= s1 && w < s2) {  // image reference: one parse feeds the registry, tag and image chains
+            const uint32_t i = w - s1;
             uint64_t mr = 0, mt = 0, mi = 0;
-            if (a.ctr_flags[cb + i] & KW_CTR_HAS_IMAGE)
-              classify_image_all(&ch[M_REG], t.s_bytes[M_IMG], t.s_off[M_IMG][cb + i], t.s_off[M_IMG][cb + i + 1], &mr,
-                                 &mt, &mi);
+            if (a.ctr_flags[cb + i] & KW_CTR_HAS_IMAGE)  // global: l_cflags is being staged in this phase
+              classify_image_all(ch[M_REG], ch[M_TAG], ch[M_IMG], t.s_bytes[M_IMG], t.s_off[M_IMG][cb + i],
+                                 t.s_off[M_IMG][cb + i + 1], &mr, &mt, &mi);
             if (l_m[M_REG]) l_m[M_REG][i] = mr;
             if (l_m[M_TAG]) l_m[M_TAG][i] = mt;
             if (l_m[M_IMG]) l_m[M_IMG][i] = mi;
+            continue;
           }
-        if (l_m[M_AA])
-          for (uint32_t i = tid; i < nc; i += kTileThreads)
-            l_m[M_AA][i] = (a.ctr_flags[cb + i] & KW_CTR_HAS_APPARMOR)
-                               ? classify_one<M_AA>(ch[M_AA], t.s_bytes[M_AA], t.s_off[M_AA][cb + i], t.s_off[M_AA][cb + i + 1])
-                               : 0ull;
-        if (l_m[M_CAPADD])
-          for (uint32_t i = tid; i < kae - kab; i += kTileThreads)
-            l_m[M_CAPADD][i] = classify_one<M_CAPADD>(ch[M_CAPADD], t.s_bytes[M_CAPADD], t.s_off[M_CAPADD][kab + i],
-                                                      t.s_off[M_CAPADD][kab + i + 1]);
-        if (l_m[M_CAPDROP])
-          for (uint32_t i = tid; i < kde - kdb; i += kTileThreads)
-            l_m[M_CAPDROP][i] = classify_one<M_CAPDROP>(ch[M_CAPDROP], t.s_bytes[M_CAPDROP], t.s_off[M_CAPDROP][kdb + i],
-                                                        t.s_off[M_CAPDROP][kdb + i + 1]);
-        if (l_m[M_LK])
-          for (uint32_t i = tid; i < le - lb; i += kTileThreads)
-            l_m[M_LK][i] = classify_one<M_LK>(ch[M_LK], t.s_bytes[M_LK], t.s_off[M_LK][lb + i], t.s_off[M_LK][lb + i + 1]);
-        if (l_m[M_LV])
-          for (uint32_t i = tid; i < le - lb; i += kTileThreads)
-            l_m[M_LV][i] = classify_one<M_LV>(ch[M_LV], t.s_bytes[M_LV], t.s_off[M_LV][lb + i], t.s_off[M_LV][lb + i + 1]);
-      } else {
+          uint32_t m, local, gbase, cap;
+          if (w < s1) { m = M_NS; local = w; gbase = (uint32_t)r0; cap = t.mask_cap[M_NS]; }
+          else if (w < s3) { m = M_AA; local = w - s2; gbase = cb; cap = t.mask_cap[M_AA]; }
+          else if (w < s4) { m = M_CAPADD; local = w - s3; gbase = kab; cap = t.mask_cap[M_CAPADD]; }
+          else if (w < s5) { m = M_CAPDROP; local = w - s4; gbase = kdb; cap = t.mask_cap[M_CAPDROP]; }
+          else if (w < s6) { m = M_LK; local = w - s5; gbase = lb; cap = t.mask_cap[M_LK]; }
+          else { m = M_LV; local = w - s6; gbase = lb; cap = t.mask_cap[M_LV]; }
+          const uint32_t clen = t.chain_len[m];
+          const uint32_t i = clen == 1 ? local : local / clen;
+          const uint32_t e = local - i * clen;
+          uint64_t* lm = (uint64_t*)(lds + t.o_m[m]);
+          uint64_t r = 0;
+          if (m != M_AA || (a.ctr_flags[cb + i] & KW_CTR_HAS_APPARMOR)) {  // global: see above
+            Chain c;
+            c.head = t.dfa_head[m];
+            c.base = lds + t.dfa_lds[m];
+            uint32_t o = c.head;
+            for (uint32_t q = 0; q < e; ++q) o = chain_next(c, o);
+            const DfaView v = chain_view(c, o);
+            const uint32_t* so = t.s_off[m];
+            const uint32_t g = gbase + i;
+            r = v.acc[feed(v, v.start, t.s_bytes[m], so[g], so[g + 1])];
+          }
+          lm[e * cap + i] = r;  // chain element e -> its own partial slot
+        }
+      } else if (!FUSED) {
         const uint32_t base[NMASK] = {(uint32_t)r0, cb, cb, cb, kab, kdb, cb, lb, lb};
         const uint32_t cnt[NMASK] = {nr, nc, nc, nc, kae - kab, kde - kdb, nc, le - lb, le - lb};
 #pragma unroll
@@ -827,76 +884,73 @@ __global__ void __launch_bounds__(kTileThreads) evaluate_tiled_kernel(EvalArgs a
       }
       __syncthreads();
 
-      // ---- B: row features, one lane per row, entities in request order
-      for (uint32_t rr = tid; rr < nr; rr += kTileThreads) {
-        RowFeat f;
-        f.add_or = 0;
-        f.dropx_and = ~0ull;
-        f.adddrop_and = ~0ull;
-        f.aa_or = 0;
-        f.key_or = 0;
-        f.ns = l_m[M_NS] ? l_m[M_NS][rr] : 0ull;
-        f.unk_add = kNone;
-        f.aa_unk = kNone;
-        f.priv[0] = f.priv[1] = f.priv[2] = f.priv[3] = kNone;
-        f.rf = l_rf[rr];
-        f.pad = 0;
-        uint32_t* capf = l_pos + rr * posstride;
-        uint32_t* aaf = capf + t.ncap_bits;
-        uint32_t* keyp = aaf + t.naa_bits;
-        const uint32_t c0 = l_coff[rr], c1 = l_coff[rr + 1];
-        for (uint32_t c = c0; c < c1; ++c) {
-          const uint32_t ci = c - c0;
-          const uint8_t fl = l_cflags[c - cb];
-          if (fl & KW_CTR_PRIVILEGED) {
-            if (f.priv[0] == kNone) f.priv[0] = ci;
-            if (f.priv[1] == kNone && !(fl & KW_CTR_INIT)) f.priv[1] = ci;
-            if (f.priv[2] == kNone && !(fl & KW_CTR_EPHEMERAL)) f.priv[2] = ci;
-            if (f.priv[3] == kNone && !(fl & (KW_CTR_INIT | KW_CTR_EPHEMERAL))) f.priv[3] = ci;
+      // ---- B: row features, entity-parallel (containers then labels), merged with LDS atomics
+      const uint32_t nl = le - lb;
+      for (uint32_t w = tid; w < nc + nl && !(t.debug & 2u); w += kTileThreads) {
+        if (w < nc) {
+          const uint32_t c = cb + w;
+          uint32_t lo = 0, hi = nr;  // row rr with l_coff[rr] <= c < l_coff[rr + 1]
+          while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (l_coff[mid] <= c) lo = mid;
+            else hi = mid;
           }
+          const uint32_t rr = lo, ci = c - l_coff[rr];
+          const uint8_t fl = l_cflags[w];
+          if (fl & KW_CTR_PRIVILEGED) {
+            atomicMin(&f_priv[rr], ci);
+            if (!(fl & KW_CTR_INIT)) atomicMin(&f_priv[rows + rr], ci);
+            if (!(fl & KW_CTR_EPHEMERAL)) atomicMin(&f_priv[2 * rows + rr], ci);
+            if (!(fl & (KW_CTR_INIT | KW_CTR_EPHEMERAL))) atomicMin(&f_priv[3 * rows + rr], ci);
+          }
+          uint32_t* capf = l_pos + rr * posstride;
           if (l_m[M_CAPADD] || l_m[M_CAPDROP]) {
             uint64_t addm = 0, dropm = 0;
-            const uint32_t k0 = l_cadd[c - cb], k1 = l_cadd[c - cb + 1];
-            if (l_m[M_CAPADD])
-              for (uint32_t k = k0; k < k1; ++k) {
-                const uint64_t m = l_m[M_CAPADD][k - kab];
-                const uint32_t pos = (ci << 16) | (k - k0);
-                if (!m && f.unk_add == kNone) f.unk_add = pos;
-                const uint64_t nb = m & ~f.add_or;
-                if (nb) capf[__builtin_ctzll(nb)] = pos;
-                f.add_or |= m;
-                addm |= m;
-              }
-            else if (k1 > k0 && f.unk_add == kNone)
-              f.unk_add = (ci << 16);  // no capability patterns at all: every added capability is unknown
+            const uint32_t k0 = l_cadd[w], k1 = l_cadd[w + 1];
+            for (uint32_t k = k0; k < k1; ++k) {
+              const uint64_t m = l_m[M_CAPADD] ? staged_mask(l_m[M_CAPADD], k - kab, FUSED ? t.chain_len[M_CAPADD] : 1u, t.mask_cap[M_CAPADD]) : 0ull;
+              const uint32_t pos = (ci << 16) | (k - k0);
+              if (!m) atomicMin(&f_unk_add[rr], pos);
+              else atomicMin(&capf[__builtin_ctzll(m)], pos);
+              addm |= m;
+            }
             if (l_m[M_CAPDROP])
-              for (uint32_t k = l_cdrop[c - cb]; k < l_cdrop[c - cb + 1]; ++k) dropm |= l_m[M_CAPDROP][k - kdb];
-            f.dropx_and &= (dropm & t.cap_all_mask) ? ~0ull : dropm;
-            f.adddrop_and &= addm | dropm;
+              for (uint32_t k = l_cdrop[w]; k < l_cdrop[w + 1]; ++k)
+                dropm |= staged_mask(l_m[M_CAPDROP], k - kdb, FUSED ? t.chain_len[M_CAPDROP] : 1u, t.mask_cap[M_CAPDROP]);
+            if (addm) atomicOr((unsigned long long*)&f_add_or[rr], (unsigned long long)addm);
+            const uint64_t dx = (dropm & t.cap_all_mask) ? ~0ull : dropm;
+            if (~dx) atomicAnd((unsigned long long*)&f_dropx_and[rr], (unsigned long long)dx);
+            if (~(addm | dropm)) atomicAnd((unsigned long long*)&f_adddrop_and[rr], (unsigned long long)(addm | dropm));
           }
-          if (l_m[M_AA] && (fl & KW_CTR_HAS_APPARMOR)) {
-            const uint64_t m = l_m[M_AA][c - cb];
-            if (!m && f.aa_unk == kNone) f.aa_unk = ci;
-            const uint64_t nb = m & ~f.aa_or;
-            if (nb) aaf[__builtin_ctzll(nb)] = ci;
-            f.aa_or |= m;
-          } else if (!l_m[M_AA] && (fl & KW_CTR_HAS_APPARMOR) && f.aa_unk == kNone) {
-            f.aa_unk = ci;  // no profile patterns: every annotated container is unknown
+          if (fl & KW_CTR_HAS_APPARMOR) {
+            const uint64_t m = l_m[M_AA] ? staged_mask(l_m[M_AA], w, FUSED ? t.chain_len[M_AA] : 1u, t.mask_cap[M_AA]) : 0ull;
+            if (!m) {
+              atomicMin(&f_aa_unk[rr], ci);
+            } else {
+              atomicMin(&capf[t.ncap_bits + __builtin_ctzll(m)], ci);
+              atomicOr((unsigned long long*)&f_aa_or[rr], (unsigned long long)m);
+            }
+          }
+        } else if (l_m[M_LK]) {
+          const uint32_t l = lb + (w - nc);
+          uint32_t lo = 0, hi = nr;
+          while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (l_loff[mid] <= l) lo = mid;
+            else hi = mid;
+          }
+          const uint64_t km = staged_mask(l_m[M_LK], w - nc, FUSED ? t.chain_len[M_LK] : 1u, t.mask_cap[M_LK]);
+          if (FUSED && t.chain_len[M_LV] > 1 && l_m[M_LV])  // fold the value-mask partials once, for phase C
+            l_m[M_LV][w - nc] = staged_mask(l_m[M_LV], w - nc, FUSED ? t.chain_len[M_LV] : 1u, t.mask_cap[M_LV]);
+          if (km) {
+            l_pos[lo * posstride + t.ncap_bits + t.naa_bits + __builtin_ctzll(km)] = l - l_loff[lo];
+            atomicOr((unsigned long long*)&f_key_or[lo], (unsigned long long)km);
           }
         }
-        if (l_m[M_LK]) {
-          const uint32_t l0 = l_loff[rr], l1 = l_loff[rr + 1];
-          for (uint32_t l = l0; l < l1; ++l) {
-            const uint64_t km = l_m[M_LK][l - lb];
-            if (km) keyp[__builtin_ctzll(km)] = l - l0;
-            f.key_or |= km;
-          }
-        }
-        l_feat[rr] = f;
       }
       __syncthreads();
 
-      // ---- C: items = (policy j, 64-row chunk); the policy is wave-uniform, lanes are rows
+      // ---- C: items = (4 policies, 64-row chunk); policies wave-uniform, lanes are rows
       TileSrc src;
       src.rf_ = l_rf;
       src.coff_ = l_coff;
@@ -911,12 +965,30 @@ __global__ void __launch_bounds__(kTileThreads) evaluate_tiled_kernel(EvalArgs a
       src.lb = lb;
       src.kab = kab;
       src.kdb = kdb;
+#pragma unroll
+      for (int k = 0; k < (int)NMASK; ++k) {
+        src.clen_[k] = FUSED ? t.chain_len[k] : 1u;
+        src.cap_[k] = t.mask_cap[k];
+      }
       const uint32_t ngroups = (npol + 3) / 4;
-      for (uint32_t item = wave; item < ngroups * chunks; item += nwaves) {
+      for (uint32_t item = wave; item < ngroups * chunks && !(t.debug & 4u); item += nwaves) {
         const uint32_t g = __builtin_amdgcn_readfirstlane(item / chunks);
         const uint32_t rr = (item - g * chunks) * 64 + lane;
         if (rr >= nr) continue;
-        const RowFeat f = l_feat[rr];
+        RowFeat f;
+        f.add_or = f_add_or[rr];
+        f.dropx_and = f_dropx_and[rr];
+        f.adddrop_and = f_adddrop_and[rr];
+        f.aa_or = f_aa_or[rr];
+        f.key_or = f_key_or[rr];
+        f.ns = l_m[M_NS] ? staged_mask(l_m[M_NS], rr, FUSED ? t.chain_len[M_NS] : 1u, t.mask_cap[M_NS]) : 0ull;
+        f.unk_add = f_unk_add[rr];
+        f.aa_unk = f_aa_unk[rr];
+        f.priv[0] = f_priv[rr];
+        f.priv[1] = f_priv[rows + rr];
+        f.priv[2] = f_priv[2 * rows + rr];
+        f.priv[3] = f_priv[3 * rows + rr];
+        f.rf = l_rf[rr];
         FeatCtx x;
         x.capf = l_pos + rr * posstride;
         x.aaf = x.capf + t.ncap_bits;
@@ -930,7 +1002,7 @@ __global__ void __launch_bounds__(kTileThreads) evaluate_tiled_kernel(EvalArgs a
         for (uint32_t jj = 0; jj < 4; ++jj) {
           const uint32_t j = g * 4 + jj;
           if (j >= npol) break;
-          const DevPolicy& P = pols[a.pols[j]];
+          const DevPolicy& P = tpols[a.pols[j]];
           uint32_t v;
           if (bypass) {
             v = KW_V_ALLOWED | KW_F_ALLOWED | KW_BYPASS;
@@ -944,7 +1016,7 @@ __global__ void __launch_bounds__(kTileThreads) evaluate_tiled_kernel(EvalArgs a
               const int32_t* mem = (const int32_t*)(a.blob + H.member_off) + P.member_off;
               uint32_t ok = 0;
               for (uint32_t sl = 0; sl < P.nmembers; ++sl) {
-                const DevPolicy& Q = pols[mem[sl]];
+                const DevPolicy& Q = tpols[mem[sl]];
                 if (Q.flags & PF_INIT_ERROR) continue;
                 FamOut fo = Q.family == FAM_TRUSTED_REPOS ? eval_family(src, Q, r0 + rr) : eval_feat(f, x, Q);
                 if (fo.reason == 0 && !fo.mutated) ok |= 1u << sl;
@@ -983,8 +1055,8 @@ __global__ void __launch_bounds__(kTileThreads) evaluate_tiled_kernel(EvalArgs a
           for (uint32_t i = tid; i < nc; i += kTileThreads) {
             uint64_t mr = 0, mt = 0, mi = 0;
             if (a.ctr_flags[cb + i] & KW_CTR_HAS_IMAGE)
-              classify_image_all(&ch[M_REG], t.s_bytes[M_IMG], t.s_off[M_IMG][cb + i], t.s_off[M_IMG][cb + i + 1], &mr,
-                                 &mt, &mi);
+              classify_image_all(ch[M_REG], ch[M_TAG], ch[M_IMG], t.s_bytes[M_IMG], t.s_off[M_IMG][cb + i],
+                                 t.s_off[M_IMG][cb + i + 1], &mr, &mt, &mi);
             if (a.m[M_REG]) ((uint64_t*)a.m[M_REG])[cb + i] = mr;
             if (a.m[M_TAG]) ((uint64_t*)a.m[M_TAG])[cb + i] = mt;
             if (a.m[M_IMG]) ((uint64_t*)a.m[M_IMG])[cb + i] = mi;

@@ -61,9 +61,13 @@ struct TileArgs {
   uint32_t cmax, kmax, lmax;      // container / capability / label capacity of a staged tile
   uint32_t o_rf, o_coff, o_loff, o_cflags, o_cadd, o_cdrop, o_gstk;  // LDS byte offsets
   uint32_t o_m[NMASK];            // LDS byte offset of each staged mask array, 0 = not read
+  uint32_t o_pols;                // LDS copy of the policy table, 0 = read from global
   uint32_t o_feat, o_pos;         // per-row features (RowFeat) and first-occurrence tables
   uint32_t ncap_bits, naa_bits, nkey_bits;  // pattern counts of the literal columns
   uint64_t cap_all_mask;          // COL_CAP bit of the "ALL" capability (0 if none)
+  uint32_t chain_len[NMASK];      // DFAs in the chain of each mask's column (1 when absent)
+  uint32_t mask_cap[NMASK];       // entries of each staged mask array
+  uint32_t debug;                 // diagnostics: bit0 skip DFA, bit1 skip row features, bit2 skip evaluation
   uint32_t lds_bytes;
   // FUSED: DFA chains staged once per workgroup, and the string columns they classify
   uint32_t nstage;
