@@ -11,8 +11,9 @@ PKG := policy-server_amd
 SRC := $(PKG)/csrc
 OBJ := $(PKG)/build
 HIPDEF := -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include
-CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wextra $(HIPDEF)
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -munsafe-fp-atomics
+TILE ?= 1024
+CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wextra $(HIPDEF) -DKW_TILE_THREADS=$(TILE)
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -munsafe-fp-atomics -DKW_TILE_THREADS=$(TILE)
 
 HOST_SRCS := json automaton expr env flatten service capi
 HOST_OBJS := $(addprefix $(OBJ)/,$(addsuffix .o,$(HOST_SRCS)))

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -51,8 +52,16 @@ struct DeviceBatch {
   size_t last_verdicts = 0;
   std::vector<int32_t> host_pols;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  // device copy of the last tiled-pass TileArgs (read by the kernel from memory, not kernargs)
+  TileArgs* d_tile = nullptr;
+  TileArgs h_tile{};
+  bool tile_valid = false;
+  uint32_t* overflow = nullptr;  // tiles beyond the LDS capacities: count + tile indices
+  size_t overflow_cap = 0;
   ~DeviceBatch() {
     if (device >= 0) (void)hipSetDevice(device);
+    (void)hipFree(d_tile);
+    (void)hipFree(overflow);
     (void)hipFree(cols);
     for (auto* m : masks) (void)hipFree(m);
     (void)hipFree(verdicts);
@@ -173,7 +182,7 @@ const DeviceBatch::DCol& mask_strings(const DeviceBatch& D, int m) {
 }
 
 constexpr uint32_t kFusedTableBudget = 48 * 1024;  // DFA chains staged per workgroup
-constexpr uint32_t kTileLdsBudget = 80 * 1024;      // whole tiled-kernel LDS (two workgroups per CU)
+constexpr uint32_t kTileLdsBudget = 160 * 1024 * kTileThreads / 1024;  // tiled-kernel LDS per workgroup
 
 // Build the classification jobs (two-kernel mode) and the evaluation arguments of one pass.
 int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npairs, uint32_t npol, int origin,
@@ -315,7 +324,7 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
     for (uint32_t o = H->dfa_off[mask_col(m)]; o; o = ((const DevDfa*)(E.blob.data() + o))->next) ++n;
     chain_len[m] = std::max<uint32_t>(1, n);
   }
-  uint32_t rows = std::max<uint32_t>(64, std::min<uint32_t>(1024, ((4096 / std::max<uint32_t>(npol, 1)) + 63) / 64 * 64));
+  uint32_t rows = std::max<uint32_t>(64, std::min<uint32_t>(1024, ((8u * kTileThreads / std::max<uint32_t>(npol, 1)) + 63) / 64 * 64));
   const uint32_t ncap = (uint32_t)E.cols[COL_CAP].size(), naa = (uint32_t)E.cols[COL_AA].size(),
                  nkey = (uint32_t)E.cols[COL_LK].size();
   double scale = 1.5;  // capacity headroom over the batch average; tiles beyond it take the global path
@@ -346,11 +355,20 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
       T.mask_cap[m] = cnt;
       off = align(off + cnt * 8 * chain_len[m]);  // one partial slot per DFA of the column chain
     }
-    T.o_pols = 0;
-    if (E.pol.size() * sizeof(DevPolicy) <= 24 * 1024) {
-      T.o_pols = off;
-      off = align(off + (uint32_t)(E.pol.size() * sizeof(DevPolicy)));
-    }
+    for (int m = 0; m < (int)NMASK; ++m) T.o_so[m] = T.o_sb[m] = T.sb_cap[m] = 0;
+    if (plan->fused)
+      for (int m : {M_NS, M_IMG, M_AA, M_CAPADD, M_CAPDROP, M_LK, M_LV}) {
+        const bool need = m == M_IMG ? (use[M_REG] || use[M_TAG] || use[M_IMG]) : use[m];
+        if (!need) continue;
+        const DeviceBatch::DCol& sc = mask_strings(D, m);
+        const uint32_t cnt = m == M_NS ? rows : (m == M_CAPADD || m == M_CAPDROP) ? kmax : (m == M_LK || m == M_LV) ? lmax : cmax;
+        T.o_so[m] = off;
+        off = align(off + (cnt + 1) * 4);
+        const double bpr = B.n ? (double)sc.nbytes / (double)B.n : 0.0;  // string bytes per request
+        T.sb_cap[m] = align((uint32_t)std::min(16384.0, scale * rows * bpr + 64));  // longer tiles take the global path
+        T.o_sb[m] = off;
+        off = align(off + T.sb_cap[m]);
+      }
     T.o_feat = off;
     off = align(off + rows * (5 * 8 + 6 * 4));
     T.o_pos = off;
@@ -376,6 +394,14 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
     T.kmax = kmax;
     T.lmax = lmax;
     T.lds_bytes = off;
+    // column chains and strings (the overflow kernel reads them in both modes)
+    for (int m = 0; m < (int)NMASK; ++m) {
+      if (!use[m]) continue;
+      T.dfa_head[m] = H->dfa_off[mask_col(m)];
+      const DeviceBatch::DCol& sc = mask_strings(D, m);
+      T.s_off[m] = sc.off;
+      T.s_bytes[m] = sc.bytes;
+    }
     // DFA chains staged once per workgroup (fused)
     if (plan->fused) {
       uint32_t at = stage_at;
@@ -393,22 +419,22 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
           at += chain_bytes(H->dfa_off[c]);
           ++T.nstage;
         }
-        T.dfa_head[m] = H->dfa_off[c];
         T.dfa_lds[m] = col_at[c];
-        const DeviceBatch::DCol& sc = mask_strings(D, m);
-        T.s_off[m] = sc.off;
-        T.s_bytes[m] = sc.bytes;
       }
     }
     break;
   }
   if (T.lds_bytes > kTileLdsBudget) return KW_E_ARG;  // npol too large for one tile row
   if (const char* dbg = getenv("KW_TILE_DEBUG")) T.debug = (uint32_t)atoi(dbg);  // phase ablation (diagnostics)
+  if (T.debug & 256u)
+    fprintf(stderr, "[kw tile] fused=%d rows=%u cmax=%u kmax=%u lmax=%u lds=%u sb=%u/%u/%u/%u/%u/%u/%u\n", (int)plan->fused,
+            T.rows, T.cmax, T.kmax, T.lmax, T.lds_bytes, T.sb_cap[M_NS], T.sb_cap[M_IMG], T.sb_cap[M_AA], T.sb_cap[M_CAPADD],
+            T.sb_cap[M_CAPDROP], T.sb_cap[M_LK], T.sb_cap[M_LV]);
   for (int m = 0; m < (int)NMASK; ++m) T.chain_len[m] = chain_len[m];
   T.cap_all_mask = 0;
   for (size_t i = 0; i < E.cols[COL_CAP].size(); ++i)
     if (E.cols[COL_CAP][i].text == "ALL") T.cap_all_mask = 1ull << i;
-  if (plan->fused && (use[M_REG] || use[M_TAG] || use[M_IMG])) {  // one parse of the image column feeds all three
+  if (use[M_REG] || use[M_TAG] || use[M_IMG]) {  // one parse of the image column feeds all three
     T.s_off[M_IMG] = D.ctr_image.off;
     T.s_bytes[M_IMG] = D.ctr_image.bytes;
   }
@@ -417,13 +443,13 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
     return KW_E_ARG;
   for (int m = 0; m < (int)NMASK; ++m) {
     if (use[m] && !A.m[m]) return KW_E_ARG;
-    if (plan->fused && use[m]) {
+    if (use[m]) {
       int sm = (m == M_REG || m == M_TAG) ? (int)M_IMG : m;
       if (!T.s_off[sm] || !T.s_bytes[sm]) return KW_E_ARG;
     }
   }
   uint64_t ntiles = (B.n + T.rows - 1) / T.rows;
-  uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(4, (160 * 1024) / std::max<uint32_t>(T.lds_bytes, 1)));
+  uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(2048 / kTileThreads, (160 * 1024) / std::max<uint32_t>(T.lds_bytes, 1)));
   plan->grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ntiles, 256ull * per_cu));
   return KW_OK;
 }
@@ -433,8 +459,20 @@ int run_pass(const kw_env* env, kw_batch* kb, const PassPlan& plan, bool timed) 
   if (timed) HIPCHK(hipEventRecord(D.ev[0], D.stream));
   if (!plan.fused) HIPCHK(launch_classify((const uint8_t*)env->e.d_blob, plan.jobs, D.stream));
   if (timed) HIPCHK(hipEventRecord(D.ev[1], D.stream));
-  if (plan.rows_mode) HIPCHK(launch_evaluate_rows(plan.args, D.stream));
-  else HIPCHK(launch_evaluate_tiled(plan.args, plan.tile, plan.fused, plan.grid, D.stream));
+  if (plan.rows_mode) {
+    HIPCHK(launch_evaluate_rows(plan.args, D.stream));
+  } else {
+    if (!D.d_tile) HIPCHK(hipMalloc((void**)&D.d_tile, sizeof(TileArgs)));
+    if (!D.tile_valid || std::memcmp(&D.h_tile, &plan.tile, sizeof(TileArgs)) != 0) {
+      D.h_tile = plan.tile;  // pageable source: the runtime stages it before returning
+      HIPCHK(hipMemcpyAsync(D.d_tile, &D.h_tile, sizeof(TileArgs), hipMemcpyHostToDevice, D.stream));
+      D.tile_valid = true;
+    }
+    const uint64_t ntiles = (plan.args.nrows + plan.tile.rows - 1) / plan.tile.rows;
+    if (int rc = ensure(&D.overflow, &D.overflow_cap, ntiles + 1)) return rc;
+    HIPCHK(launch_evaluate_tiled(plan.args, plan.tile, D.d_tile, plan.fused, plan.grid, D.overflow,
+                                 (uint32_t)std::min<uint64_t>(ntiles, 512), D.stream));
+  }
   if (timed) HIPCHK(hipEventRecord(D.ev[2], D.stream));
   return KW_OK;
 }

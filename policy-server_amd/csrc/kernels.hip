@@ -21,6 +21,8 @@
 // the dependent LDS chain of the DFA walk.
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
+
 #include "../../include/kwgpu.h"
 #include "kernels.hpp"
 
@@ -73,22 +75,26 @@ __device__ inline uint32_t feed(const DfaView& d, uint32_t st, const uint8_t* __
   return st;
 }
 
-__constant__ char kDockerIo[9] = {'d', 'o', 'c', 'k', 'e', 'r', '.', 'i', 'o'};
-__constant__ char kLibrary[8] = {'l', 'i', 'b', 'r', 'a', 'r', 'y', '/'};
-__constant__ char kLatest[6] = {'l', 'a', 't', 'e', 's', 't'};
-__constant__ char kLocalhost[9] = {'l', 'o', 'c', 'a', 'l', 'h', 'o', 's', 't'};
+// Literal fragments of image normalisation; constexpr + unrolled loops turn them into immediates.
+constexpr char kDockerIo[] = "docker.io";
+constexpr char kLibrary[] = "library/";
+constexpr char kLatest[] = "latest";
+constexpr char kLocalhost[] = "localhost";
 
-__device__ inline uint32_t feed_const(const DfaView& d, uint32_t st, const char* s, int n) {
-  for (int i = 0; i < n && st != 0; ++i) st = step(d, st, (uint8_t)s[i]);
+template <int N>
+__device__ inline uint32_t feed_const(const DfaView& d, uint32_t st, const char (&s)[N]) {
+#pragma unroll
+  for (int i = 0; i < N - 1; ++i) st = step(d, st, (uint8_t)s[i]);  // state 0 is absorbing
   return st;
 }
 
 __device__ inline uint32_t byte_at(const uint8_t* __restrict__ bytes, uint32_t p) { return bytes[p]; }
 
-__device__ inline bool equals_const(const uint8_t* __restrict__ bytes, uint32_t b, uint32_t e, const char* s,
-                                    int n) {
-  if ((int)(e - b) != n) return false;
-  for (int i = 0; i < n; ++i)
+template <int N>
+__device__ inline bool equals_const(const uint8_t* __restrict__ bytes, uint32_t b, uint32_t e, const char (&s)[N]) {
+  if ((int)(e - b) != N - 1) return false;
+#pragma unroll
+  for (int i = 0; i < N - 1; ++i)
     if (byte_at(bytes, b + (uint32_t)i) != (uint8_t)s[i]) return false;
   return true;
 }
@@ -149,13 +155,13 @@ __device__ ImageRef parse_image(const uint8_t* __restrict__ bytes, uint32_t b, u
   r.at = at;
   r.slash0 = slash0;
   r.name_end = at != NONE ? at : e;
-  r.is_reg = slash0 != NONE && (dotcolon || equals_const(bytes, b, slash0, kLocalhost, 9));
+  r.is_reg = slash0 != NONE && (dotcolon || equals_const(bytes, b, slash0, kLocalhost));
   r.rest_b = r.is_reg ? slash0 + 1 : b;
   r.colon = (last_colon != NONE && last_colon >= r.rest_b) ? last_colon : NONE;
   r.path_end = r.colon != NONE ? r.colon : r.name_end;
   uint32_t first_slash_rest = r.is_reg ? slash1 : slash0;
   r.path_slash = first_slash_rest != NONE && first_slash_rest < r.path_end;
-  r.is_docker = !r.is_reg || equals_const(bytes, b, slash0, kDockerIo, 9);
+  r.is_docker = !r.is_reg || equals_const(bytes, b, slash0, kDockerIo);
   r.eff_tag = r.colon != NONE || at == NONE;
   return r;
 }
@@ -165,19 +171,19 @@ __device__ uint64_t image_part(int k, const DfaView& d, const uint8_t* __restric
   const uint32_t NONE = 0xffffffffu;
   uint32_t st = d.start;
   if (k == 0) {
-    st = r.is_reg ? feed(d, st, bytes, r.b, r.slash0) : feed_const(d, st, kDockerIo, 9);
+    st = r.is_reg ? feed(d, st, bytes, r.b, r.slash0) : feed_const(d, st, kDockerIo);
   } else if (k == 1) {
     if (r.colon != NONE) st = feed(d, st, bytes, r.colon + 1, r.name_end);
-    else if (r.at == NONE) st = feed_const(d, st, kLatest, 6);
+    else if (r.at == NONE) st = feed_const(d, st, kLatest);
     else return 0ull;  // digest only: no tag
   } else {
-    st = r.is_reg ? feed(d, st, bytes, r.b, r.slash0) : feed_const(d, st, kDockerIo, 9);
+    st = r.is_reg ? feed(d, st, bytes, r.b, r.slash0) : feed_const(d, st, kDockerIo);
     if (st) st = step(d, st, '/');
-    if (r.is_docker && !r.path_slash) st = feed_const(d, st, kLibrary, 8);
+    if (r.is_docker && !r.path_slash) st = feed_const(d, st, kLibrary);
     st = feed(d, st, bytes, r.rest_b, r.path_end);
     if (r.eff_tag) {
       if (st) st = step(d, st, ':');
-      st = r.colon != NONE ? feed(d, st, bytes, r.colon + 1, r.name_end) : feed_const(d, st, kLatest, 6);
+      st = r.colon != NONE ? feed(d, st, bytes, r.colon + 1, r.name_end) : feed_const(d, st, kLatest);
     }
     if (r.at != NONE) st = feed(d, st, bytes, r.at, r.e);
   }
@@ -240,6 +246,20 @@ __global__ void __launch_bounds__(kClassifyThreads) classify_kernel(const uint8_
 // ------------------------------------------------------------------------------------------
 // Policy evaluation
 // ------------------------------------------------------------------------------------------
+// Policy fields are read as whole dwords: with wave-uniform policy indices and __restrict__ kernel
+// parameters the loads become scalar (s_load, K$), the bytes are extracted with SALU ops.
+__device__ inline uint32_t pword(const DevPolicy& P, uint32_t w) { return ((const uint32_t*)&P)[w]; }
+// byte o of a dword-aligned table (group programs), as a dword load
+__device__ inline uint32_t tbyte(const uint8_t* base, uint32_t o) {
+  return (((const uint32_t*)base)[o >> 2] >> (8u * (o & 3u))) & 0xffu;
+}
+__device__ inline uint32_t pbyte(const DevPolicy& P, uint32_t off) { return (pword(P, off >> 2) >> (8u * (off & 3u))) & 0xffu; }
+// byte offsets within DevPolicy (kwdev.hpp)
+constexpr uint32_t PB_FAMILY = 0, PB_MODE = 1, PB_A2M = 2, PB_FLAGS = 3, PB_NL = 4, PB_NMAND = 10, PB_NCONSTR = 11, PB_IDX = 80;
+static_assert(offsetof(DevPolicy, nl) == PB_NL && offsetof(DevPolicy, n_mand) == PB_NMAND &&
+                  offsetof(DevPolicy, n_constr) == PB_NCONSTR && offsetof(DevPolicy, idx) == PB_IDX,
+              "DevPolicy byte offsets");
+
 struct FamOut {
   uint32_t reason, arg;
   bool mutated;
@@ -299,12 +319,12 @@ __device__ FamOut eval_family(const S& src, const DevPolicy& P, uint64_t r) {
   FamOut o{0, 0, false};
   const uint8_t rf = src.rf(r);
   const uint32_t cb = src.coff(r), ce = src.coff(r + 1);
-  switch (P.family) {
+  switch (pbyte(P, PB_FAMILY)) {
     case FAM_PRIVILEGED: {
       if (!(rf & KW_REQ_HAS_PODSPEC)) break;
       for (uint32_t c = cb; c < ce; ++c) {
         uint8_t f = src.cflags(c);
-        bool skip = ((P.flags & PF_SKIP_INIT) && (f & KW_CTR_INIT)) || ((P.flags & PF_SKIP_EPHEMERAL) && (f & KW_CTR_EPHEMERAL));
+        bool skip = ((pbyte(P, PB_FLAGS) & PF_SKIP_INIT) && (f & KW_CTR_INIT)) || ((pbyte(P, PB_FLAGS) & PF_SKIP_EPHEMERAL) && (f & KW_CTR_EPHEMERAL));
         if (!skip && (f & KW_CTR_PRIVILEGED)) {
           o.reason = KW_R_PRIVILEGED;
           o.arg = pack1(c - cb);
@@ -314,7 +334,7 @@ __device__ FamOut eval_family(const S& src, const DevPolicy& P, uint64_t r) {
       break;
     }
     case FAM_NAMESPACE: {
-      bool ok = (rf & KW_REQ_HAS_NAMESPACE) && P.nl[0] && (src.template m<M_NS>(r) & P.m[0]);
+      bool ok = (rf & KW_REQ_HAS_NAMESPACE) && pbyte(P, PB_NL + (0)) && (src.template m<M_NS>(r) & P.m[0]);
       if (!ok) o.reason = KW_R_NAMESPACE;
       break;
     }
@@ -324,11 +344,11 @@ __device__ FamOut eval_family(const S& src, const DevPolicy& P, uint64_t r) {
         if (!(src.cflags(c) & KW_CTR_HAS_IMAGE)) continue;
         uint64_t reg = src.template m<M_REG>(c), tag = src.template m<M_TAG>(c), img = src.template m<M_IMG>(c);
         uint32_t why = 0;
-        if (P.nl[0] && !(reg & P.m[0])) why = KW_R_REG_NOT_ALLOWED;
-        else if (P.nl[1] && (reg & P.m[1])) why = KW_R_REG_REJECTED;
-        else if (P.nl[2] && (tag & P.m[2])) why = KW_R_TAG_REJECTED;
-        else if (P.nl[3] && !(img & P.m[3])) why = KW_R_IMG_NOT_ALLOWED;
-        else if (P.nl[4] && (img & P.m[4])) why = KW_R_IMG_REJECTED;
+        if (pbyte(P, PB_NL + (0)) && !(reg & P.m[0])) why = KW_R_REG_NOT_ALLOWED;
+        else if (pbyte(P, PB_NL + (1)) && (reg & P.m[1])) why = KW_R_REG_REJECTED;
+        else if (pbyte(P, PB_NL + (2)) && (tag & P.m[2])) why = KW_R_TAG_REJECTED;
+        else if (pbyte(P, PB_NL + (3)) && !(img & P.m[3])) why = KW_R_IMG_NOT_ALLOWED;
+        else if (pbyte(P, PB_NL + (4)) && (img & P.m[4])) why = KW_R_IMG_REJECTED;
         if (why) {
           o.reason = why;
           o.arg = pack1(c - cb);
@@ -345,7 +365,7 @@ __device__ FamOut eval_family(const S& src, const DevPolicy& P, uint64_t r) {
         for (uint32_t k = kb; k < ke; ++k) {
           uint64_t mk = src.template m<M_CAPADD>(k);
           addm |= mk;
-          if (!(P.flags & PF_ALLOW_ALL) && !(mk & P.m[0])) {
+          if (!(pbyte(P, PB_FLAGS) & PF_ALLOW_ALL) && !(mk & P.m[0])) {
             o.reason = KW_R_CAP_NOT_ALLOWED;
             o.arg = pack2(c - cb, k - kb);
             break;
@@ -383,8 +403,8 @@ __device__ FamOut eval_family(const S& src, const DevPolicy& P, uint64_t r) {
         }
         if (km) {
           const uint64_t vm = src.template m<M_LV>(l);
-          for (uint32_t i = 0; i < P.n_constr; ++i) {
-            if (((km >> P.idx[16 + i]) & 1ull) && !((vm >> P.idx[32 + i]) & 1ull)) {
+          for (uint32_t i = 0; i < pbyte(P, PB_NCONSTR); ++i) {
+            if (((km >> pbyte(P, PB_IDX + (16 + i))) & 1ull) && !((vm >> pbyte(P, PB_IDX + (32 + i))) & 1ull)) {
               o.reason = KW_R_LABEL_CONSTRAINT;
               o.arg = pack2(l - lb, i);
               break;
@@ -393,8 +413,8 @@ __device__ FamOut eval_family(const S& src, const DevPolicy& P, uint64_t r) {
         }
       }
       if (o.reason) break;
-      for (uint32_t i = 0; i < P.n_mand; ++i)
-        if (!((present >> P.idx[i]) & 1ull)) {
+      for (uint32_t i = 0; i < pbyte(P, PB_NMAND); ++i)
+        if (!((present >> pbyte(P, PB_IDX + (i))) & 1ull)) {
           o.reason = KW_R_LABEL_MANDATORY;
           o.arg = i;
           break;
@@ -416,18 +436,18 @@ __device__ uint32_t verdict(const S& src, const EvalArgs& a, const DevHeader& H,
       ((src.template m<M_NS>(r) >> H.bypass_bit) & 1ull))
     return KW_V_ALLOWED | KW_F_ALLOWED | KW_BYPASS;
   // PolicyInitialization -> reject 500 before any constraint (service.rs:78-91)
-  if (P.flags & PF_INIT_ERROR) return ((uint32_t)KW_FST_INIT_ERROR << KW_F_STATUS_SHIFT) | ((uint32_t)KW_R_INIT_ERROR << 8);
+  if (pbyte(P, PB_FLAGS) & PF_INIT_ERROR) return ((uint32_t)KW_FST_INIT_ERROR << KW_F_STATUS_SHIFT) | ((uint32_t)KW_R_INIT_ERROR << 8);
   uint32_t reason = 0, arg = 0;
   bool mutated = false;
-  if (P.family == FAM_GROUP) {
-    if (P.flags & PF_EXPR_ERROR) {
+  if (pbyte(P, PB_FAMILY) == FAM_GROUP) {
+    if (pbyte(P, PB_FLAGS) & PF_EXPR_ERROR) {
       reason = KW_R_GROUP_EXPR;
     } else {
       const int32_t* mem = (const int32_t*)(a.blob + H.member_off) + P.member_off;
       uint32_t ok = 0;
       for (uint32_t s = 0; s < P.nmembers; ++s) {
         const DevPolicy& Q = pols[mem[s]];
-        if (Q.flags & PF_INIT_ERROR) continue;
+        if (pbyte(Q, PB_FLAGS) & PF_INIT_ERROR) continue;
         FamOut fo = eval_family(src, Q, r);
         if (fo.reason == 0 && !fo.mutated) ok |= 1u << s;
       }
@@ -489,16 +509,16 @@ __device__ uint32_t verdict(const S& src, const EvalArgs& a, const DevHeader& H,
   uint32_t fst = allowed ? KW_FST_NONE : KW_FST_VANILLA;
   bool fallowed = allowed;
   if (a.origin == KW_ORIGIN_VALIDATE) {
-    if (P.mode == KW_MODE_MONITOR) {
+    if (pbyte(P, PB_MODE) == KW_MODE_MONITOR) {
       fallowed = true;
       fst = KW_FST_NONE;
-    } else if (mutated && !P.a2m) {
+    } else if (mutated && !pbyte(P, PB_A2M)) {
       fallowed = false;
       fst = KW_FST_MUTATION_REFUSED;
     }
   }
   if (fallowed) v |= KW_F_ALLOWED;
-  if (mutated && fst == KW_FST_NONE && (a.origin == KW_ORIGIN_AUDIT || P.mode == KW_MODE_PROTECT)) v |= KW_F_PATCH;
+  if (mutated && fst == KW_FST_NONE && (a.origin == KW_ORIGIN_AUDIT || pbyte(P, PB_MODE) == KW_MODE_PROTECT)) v |= KW_F_PATCH;
   v |= fst << KW_F_STATUS_SHIFT;
   return v;
 }
@@ -592,10 +612,10 @@ __device__ inline uint32_t min_pos(uint64_t bits, const uint32_t* table, uint32_
 // string) is not reducible and is evaluated by the caller from the staged masks.
 __device__ FamOut eval_feat(const RowFeat& f, const FeatCtx& x, const DevPolicy& P) {
   FamOut o{0, 0, false};
-  switch (P.family) {
+  switch (pbyte(P, PB_FAMILY)) {
     case FAM_PRIVILEGED: {
       if (!(f.rf & KW_REQ_HAS_PODSPEC)) break;
-      const uint32_t v = ((P.flags & PF_SKIP_INIT) ? 1u : 0u) | ((P.flags & PF_SKIP_EPHEMERAL) ? 2u : 0u);
+      const uint32_t v = ((pbyte(P, PB_FLAGS) & PF_SKIP_INIT) ? 1u : 0u) | ((pbyte(P, PB_FLAGS) & PF_SKIP_EPHEMERAL) ? 2u : 0u);
       const uint32_t p = v == 0 ? f.priv[0] : v == 1 ? f.priv[1] : v == 2 ? f.priv[2] : f.priv[3];
       if (p != kNone) {
         o.reason = KW_R_PRIVILEGED;
@@ -604,11 +624,11 @@ __device__ FamOut eval_feat(const RowFeat& f, const FeatCtx& x, const DevPolicy&
       break;
     }
     case FAM_NAMESPACE:
-      if (!((f.rf & KW_REQ_HAS_NAMESPACE) && P.nl[0] && (f.ns & P.m[0]))) o.reason = KW_R_NAMESPACE;
+      if (!((f.rf & KW_REQ_HAS_NAMESPACE) && pbyte(P, PB_NL + (0)) && (f.ns & P.m[0]))) o.reason = KW_R_NAMESPACE;
       break;
     case FAM_CAPABILITIES: {
       if (!(f.rf & KW_REQ_HAS_PODSPEC)) break;
-      if (!(P.flags & PF_ALLOW_ALL)) {
+      if (!(pbyte(P, PB_FLAGS) & PF_ALLOW_ALL)) {
         const uint32_t p = min_pos(f.add_or & ~P.m[0], x.capf, f.unk_add);
         if (p != kNone) {
           o.reason = KW_R_CAP_NOT_ALLOWED;
@@ -631,11 +651,11 @@ __device__ FamOut eval_feat(const RowFeat& f, const FeatCtx& x, const DevPolicy&
     case FAM_LABELS: {
       uint32_t best = min_pos(f.key_or & P.m[0], x.keyp, kNone);
       uint32_t reason = best != kNone ? (uint32_t)KW_R_LABEL_DENIED : 0u, arg = best;
-      for (uint32_t i = 0; i < P.n_constr; ++i) {
-        const uint32_t k = P.idx[16 + i];
+      for (uint32_t i = 0; i < pbyte(P, PB_NCONSTR); ++i) {
+        const uint32_t k = pbyte(P, PB_IDX + (16 + i));
         if (!((f.key_or >> k) & 1ull)) continue;
         const uint32_t p = x.keyp[k];
-        if (p < best && !((x.lv[x.lrow + p] >> P.idx[32 + i]) & 1ull)) {
+        if (p < best && !((x.lv[x.lrow + p] >> pbyte(P, PB_IDX + (32 + i))) & 1ull)) {
           best = p;
           reason = KW_R_LABEL_CONSTRAINT;
           arg = pack2(p, i);
@@ -646,8 +666,8 @@ __device__ FamOut eval_feat(const RowFeat& f, const FeatCtx& x, const DevPolicy&
         o.arg = reason == KW_R_LABEL_DENIED ? pack1(arg) : arg;
         break;
       }
-      for (uint32_t i = 0; i < P.n_mand; ++i)
-        if (!((f.key_or >> P.idx[i]) & 1ull)) {
+      for (uint32_t i = 0; i < pbyte(P, PB_NMAND); ++i)
+        if (!((f.key_or >> pbyte(P, PB_IDX + (i))) & 1ull)) {
           o.reason = KW_R_LABEL_MANDATORY;
           o.arg = i;
           break;
@@ -668,32 +688,32 @@ __device__ inline uint32_t finish(const EvalArgs& a, const DevPolicy& P, uint32_
   uint32_t fst = allowed ? KW_FST_NONE : KW_FST_VANILLA;
   bool fallowed = allowed;
   if (a.origin == KW_ORIGIN_VALIDATE) {
-    if (P.mode == KW_MODE_MONITOR) {
+    if (pbyte(P, PB_MODE) == KW_MODE_MONITOR) {
       fallowed = true;
       fst = KW_FST_NONE;
-    } else if (mutated && !P.a2m) {
+    } else if (mutated && !pbyte(P, PB_A2M)) {
       fallowed = false;
       fst = KW_FST_MUTATION_REFUSED;
     }
   }
   if (fallowed) v |= KW_F_ALLOWED;
-  if (mutated && fst == KW_FST_NONE && (a.origin == KW_ORIGIN_AUDIT || P.mode == KW_MODE_PROTECT)) v |= KW_F_PATCH;
+  if (mutated && fst == KW_FST_NONE && (a.origin == KW_ORIGIN_AUDIT || pbyte(P, PB_MODE) == KW_MODE_PROTECT)) v |= KW_F_PATCH;
   v |= fst << KW_F_STATUS_SHIFT;
   return v;
 }
 
 // Group program over member results (see verdict()).
-__device__ inline bool run_group(const EvalArgs& a, const DevHeader& H, const DevPolicy& P, uint32_t ok, uint16_t* gstk,
+__device__ inline bool run_group(const uint8_t* __restrict__ blob, const DevHeader& H, const DevPolicy& P, uint32_t ok, uint16_t* gstk,
                                  uint32_t gstride, uint32_t* causes) {
-  const uint8_t* prog = a.blob + H.prog_off + P.prog_off;
+  const uint8_t* prog = blob + H.prog_off;  // 16-B aligned section; P.prog_off is a byte offset in it
   uint32_t vals = 0;
   int sp = 0;
   for (uint32_t pc = 0; pc < P.prog_len; ++pc) {
-    uint8_t op = prog[pc];
+    const uint32_t op = tbyte(prog, P.prog_off + pc);
     if (op <= G_CALL) {
       uint32_t v = op == G_CONST1 ? 1u : 0u, e = 0;
       if (op == G_CALL) {
-        uint32_t s = prog[++pc];
+        uint32_t s = tbyte(prog, P.prog_off + (++pc));
         v = (ok >> s) & 1u;
         e = 1u << s;
       }
@@ -728,28 +748,44 @@ __device__ inline bool run_group(const EvalArgs& a, const DevHeader& H, const De
   return vals & 1u;
 }
 
+// Pointers read from TileArgs are generic to the compiler; these casts make their loads global_load
+// (not flat) in the staging loops.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <class T>
+__device__ inline const __attribute__((address_space(1))) T* gp(const T* p) {
+  return (const __attribute__((address_space(1))) T*)p;
+}
+
+// First global entity index and entity count of mask m's string column within a tile.
+__device__ inline uint32_t tile_g0(int m, uint32_t r0, uint32_t cb, uint32_t kab, uint32_t kdb, uint32_t lb) {
+  return m == M_NS ? r0 : m == M_CAPADD ? kab : m == M_CAPDROP ? kdb : (m == M_LK || m == M_LV) ? lb : cb;
+}
+__device__ inline uint32_t tile_n(int m, uint32_t nr, uint32_t nc, uint32_t nka, uint32_t nkd, uint32_t nl) {
+  return m == M_NS ? nr : m == M_CAPADD ? nka : m == M_CAPDROP ? nkd : (m == M_LK || m == M_LV) ? nl : nc;
+}
+
 template <bool FUSED>
-__global__ void __launch_bounds__(kTileThreads) evaluate_tiled_kernel(EvalArgs a, TileArgs t) {
+__global__ void __launch_bounds__(kTileThreads)
+    evaluate_tiled_kernel(EvalArgs a, const TileArgs* __restrict__ tp, const uint8_t* __restrict__ blob,
+                          const int32_t* __restrict__ plist, uint32_t* __restrict__ out, uint32_t* __restrict__ overflow) {
+  // TileArgs lives in device memory: its fields are scalar-loaded where used instead of all being
+  // hoisted from the kernarg segment into SGPRs at entry. blob / plist / out are __restrict__ so
+  // wave-uniform policy reads compile to scalar loads (nothing in this kernel stores to global
+  // memory except `out` and `overflow`).
+  const TileArgs& t = *tp;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const DevHeader H = *(const DevHeader*)a.blob;
-  const DevPolicy* __restrict__ pols = (const DevPolicy*)(a.blob + H.policy_off);
+  const DevHeader H = *(const DevHeader*)blob;
+  const DevPolicy* __restrict__ tpols = (const DevPolicy*)(blob + H.policy_off);
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t nwaves = kTileThreads / 64;
 
   Chain ch[NMASK];
-  if (t.o_pols) {  // the policy table, read with wave-uniform addresses in phase C (LDS broadcast)
-    const uint4* src = (const uint4*)pols;
-    uint4* dst = (uint4*)(lds + t.o_pols);
-    for (uint32_t i = tid; i < H.npolicies * (uint32_t)sizeof(DevPolicy) / 16; i += kTileThreads) dst[i] = src[i];
-    if (!FUSED) __syncthreads();
-  }
-  const DevPolicy* __restrict__ tpols = t.o_pols ? (const DevPolicy*)(lds + t.o_pols) : pols;
   if (FUSED) {
     for (uint32_t s = 0; s < t.nstage; ++s) {
-      const uint4* src = (const uint4*)(a.blob + t.stage_blob[s]);
-      uint4* dst = (uint4*)(lds + t.stage_lds[s]);
+      const auto* src = gp((const u32x4*)(blob + t.stage_blob[s]));
+      u32x4* dst = (u32x4*)(lds + t.stage_lds[s]);
       for (uint32_t i = tid; i < t.stage_bytes[s] / 16; i += kTileThreads) dst[i] = src[i];
     }
 #pragma unroll
@@ -791,12 +827,23 @@ __global__ void __launch_bounds__(kTileThreads) evaluate_tiled_kernel(EvalArgs a
     const uint32_t lb = a.lbl_off[r0], le = a.lbl_off[r0 + nr];
     const uint32_t kab = a.capadd_off[cb], kae = a.capadd_off[ce];
     const uint32_t kdb = a.capdrop_off[cb], kde = a.capdrop_off[ce];
-    const bool fits = (ce - cb) <= t.cmax && (kae - kab) <= t.kmax && (kde - kdb) <= t.kmax && (le - lb) <= t.lmax;
+    bool fits = (ce - cb) <= t.cmax && (kae - kab) <= t.kmax && (kde - kdb) <= t.kmax && (le - lb) <= t.lmax;
+    // staged string ranges: [sa, sz) of each column's pool, 16-B aligned (pools carry a >= 16 B zero tail)
+    if (FUSED) {
+#pragma unroll
+      for (int m = 0; m < (int)NMASK; ++m) {
+        if (!t.o_sb[m]) continue;
+        const uint32_t g0 = tile_g0(m, (uint32_t)r0, cb, kab, kdb, lb);
+        const uint32_t n = tile_n(m, nr, ce - cb, kae - kab, kde - kdb, le - lb);
+        const auto* so = gp(t.s_off[m]);
+        fits = fits && ((so[g0 + n] + 15u) & ~15u) - (so[g0] & ~15u) <= t.sb_cap[m];
+      }
+    }
     const uint32_t chunks = (nr + 63) / 64;
 
     if (fits) {
-      // ---- A: stage the tile; classify its strings (FUSED) from one flattened work list over
-      //      every column and every DFA of a column's chain (chained DFAs OR into pre-zeroed masks)
+      // ---- A: stage the tile (headers, and for FUSED its strings); then classify the staged strings
+      //      from one flattened work list over every column and every DFA of a column's chain
       for (uint32_t i = tid; i <= nr; i += kTileThreads) {
         if (i < nr) {
           l_rf[i] = a.req_flags[r0 + i];
@@ -825,6 +872,23 @@ __global__ void __launch_bounds__(kTileThreads) evaluate_tiled_kernel(EvalArgs a
         l_cadd[i] = a.capadd_off[cb + i];
         l_cdrop[i] = a.capdrop_off[cb + i];
       }
+      if (FUSED) {
+#pragma unroll
+        for (int m = 0; m < (int)NMASK; ++m) {
+          if (!t.o_sb[m]) continue;
+          const uint32_t g0 = tile_g0(m, (uint32_t)r0, cb, kab, kdb, lb);
+          const uint32_t n = tile_n(m, nr, ce - cb, kae - kab, kde - kdb, le - lb);
+          const auto* go = gp(t.s_off[m]);
+          const uint32_t sa = __builtin_amdgcn_readfirstlane(go[g0] & ~15u);
+          const uint32_t nv = __builtin_amdgcn_readfirstlane((((go[g0 + n] + 15u) & ~15u) - sa) / 16u);
+          uint32_t* so = (uint32_t*)(lds + t.o_so[m]);
+          for (uint32_t i = tid; i <= n; i += kTileThreads) so[i] = go[g0 + i] - sa;
+          const auto* src = gp((const u32x4*)(t.s_bytes[m] + sa));
+          u32x4* dst = (u32x4*)(lds + t.o_sb[m]);
+          for (uint32_t i = tid; i < nv; i += kTileThreads) dst[i] = src[i];
+        }
+        __syncthreads();
+      }
       if (FUSED && !(t.debug & 1u)) {
         // work list: (job, string, chain element); jobs in order NS, IMG, AA, CAPADD, CAPDROP, LK, LV.
         // Per-job parameters come from the kernarg arrays (runtime-indexable without scratch).
@@ -841,36 +905,36 @@ __global__ void __launch_bounds__(kTileThreads) evaluate_tiled_kernel(EvalArgs a
           if (w >= s1 && w < s2) {  // image reference: one parse feeds the registry, tag and image chains
             const uint32_t i = w - s1;
             uint64_t mr = 0, mt = 0, mi = 0;
-            if (a.ctr_flags[cb + i] & KW_CTR_HAS_IMAGE)  // global: l_cflags is being staged in this phase
-              classify_image_all(ch[M_REG], ch[M_TAG], ch[M_IMG], t.s_bytes[M_IMG], t.s_off[M_IMG][cb + i],
-                                 t.s_off[M_IMG][cb + i + 1], &mr, &mt, &mi);
+            if (l_cflags[i] & KW_CTR_HAS_IMAGE) {
+              const uint32_t* so = (const uint32_t*)(lds + t.o_so[M_IMG]);
+              classify_image_all(ch[M_REG], ch[M_TAG], ch[M_IMG], lds + t.o_sb[M_IMG], so[i], so[i + 1], &mr, &mt, &mi);
+            }
             if (l_m[M_REG]) l_m[M_REG][i] = mr;
             if (l_m[M_TAG]) l_m[M_TAG][i] = mt;
             if (l_m[M_IMG]) l_m[M_IMG][i] = mi;
             continue;
           }
-          uint32_t m, local, gbase, cap;
-          if (w < s1) { m = M_NS; local = w; gbase = (uint32_t)r0; cap = t.mask_cap[M_NS]; }
-          else if (w < s3) { m = M_AA; local = w - s2; gbase = cb; cap = t.mask_cap[M_AA]; }
-          else if (w < s4) { m = M_CAPADD; local = w - s3; gbase = kab; cap = t.mask_cap[M_CAPADD]; }
-          else if (w < s5) { m = M_CAPDROP; local = w - s4; gbase = kdb; cap = t.mask_cap[M_CAPDROP]; }
-          else if (w < s6) { m = M_LK; local = w - s5; gbase = lb; cap = t.mask_cap[M_LK]; }
-          else { m = M_LV; local = w - s6; gbase = lb; cap = t.mask_cap[M_LV]; }
+          uint32_t m, local, cap;
+          if (w < s1) { m = M_NS; local = w; cap = t.mask_cap[M_NS]; }
+          else if (w < s3) { m = M_AA; local = w - s2; cap = t.mask_cap[M_AA]; }
+          else if (w < s4) { m = M_CAPADD; local = w - s3; cap = t.mask_cap[M_CAPADD]; }
+          else if (w < s5) { m = M_CAPDROP; local = w - s4; cap = t.mask_cap[M_CAPDROP]; }
+          else if (w < s6) { m = M_LK; local = w - s5; cap = t.mask_cap[M_LK]; }
+          else { m = M_LV; local = w - s6; cap = t.mask_cap[M_LV]; }
           const uint32_t clen = t.chain_len[m];
           const uint32_t i = clen == 1 ? local : local / clen;
           const uint32_t e = local - i * clen;
           uint64_t* lm = (uint64_t*)(lds + t.o_m[m]);
           uint64_t r = 0;
-          if (m != M_AA || (a.ctr_flags[cb + i] & KW_CTR_HAS_APPARMOR)) {  // global: see above
+          if (m != M_AA || (l_cflags[i] & KW_CTR_HAS_APPARMOR)) {
             Chain c;
             c.head = t.dfa_head[m];
             c.base = lds + t.dfa_lds[m];
             uint32_t o = c.head;
             for (uint32_t q = 0; q < e; ++q) o = chain_next(c, o);
             const DfaView v = chain_view(c, o);
-            const uint32_t* so = t.s_off[m];
-            const uint32_t g = gbase + i;
-            r = v.acc[feed(v, v.start, t.s_bytes[m], so[g], so[g + 1])];
+            const uint32_t* so = (const uint32_t*)(lds + t.o_so[m]);
+            r = v.acc[feed(v, v.start, lds + t.o_sb[m], so[i], so[i + 1])];
           }
           lm[e * cap + i] = r;  // chain element e -> its own partial slot
         }
@@ -1002,39 +1066,39 @@ __global__ void __launch_bounds__(kTileThreads) evaluate_tiled_kernel(EvalArgs a
         for (uint32_t jj = 0; jj < 4; ++jj) {
           const uint32_t j = g * 4 + jj;
           if (j >= npol) break;
-          const DevPolicy& P = tpols[a.pols[j]];
+          const DevPolicy& P = tpols[plist[j]];
           uint32_t v;
           if (bypass) {
             v = KW_V_ALLOWED | KW_F_ALLOWED | KW_BYPASS;
-          } else if (P.flags & PF_INIT_ERROR) {
+          } else if (pbyte(P, PB_FLAGS) & PF_INIT_ERROR) {
             v = ((uint32_t)KW_FST_INIT_ERROR << KW_F_STATUS_SHIFT) | ((uint32_t)KW_R_INIT_ERROR << 8);
-          } else if (P.family == FAM_GROUP) {
+          } else if (pbyte(P, PB_FAMILY) == FAM_GROUP) {
             uint32_t reason = 0, arg = 0;
-            if (P.flags & PF_EXPR_ERROR) {
+            if (pbyte(P, PB_FLAGS) & PF_EXPR_ERROR) {
               reason = KW_R_GROUP_EXPR;
             } else {
-              const int32_t* mem = (const int32_t*)(a.blob + H.member_off) + P.member_off;
+              const int32_t* mem = (const int32_t*)(blob + H.member_off) + P.member_off;
               uint32_t ok = 0;
               for (uint32_t sl = 0; sl < P.nmembers; ++sl) {
                 const DevPolicy& Q = tpols[mem[sl]];
-                if (Q.flags & PF_INIT_ERROR) continue;
-                FamOut fo = Q.family == FAM_TRUSTED_REPOS ? eval_family(src, Q, r0 + rr) : eval_feat(f, x, Q);
+                if (pbyte(Q, PB_FLAGS) & PF_INIT_ERROR) continue;
+                FamOut fo = pbyte(Q, PB_FAMILY) == FAM_TRUSTED_REPOS ? eval_family(src, Q, r0 + rr) : eval_feat(f, x, Q);
                 if (fo.reason == 0 && !fo.mutated) ok |= 1u << sl;
               }
               uint32_t causes;
-              if (!run_group(a, H, P, ok, gstk + tid, kTileThreads, &causes)) {
+              if (!run_group(blob, H, P, ok, gstk + tid, kTileThreads, &causes)) {
                 reason = KW_R_GROUP;
                 arg = causes;
               }
             }
             v = finish(a, P, reason, arg, false);
           } else {
-            FamOut fo = P.family == FAM_TRUSTED_REPOS ? eval_family(src, P, r0 + rr) : eval_feat(f, x, P);
+            FamOut fo = pbyte(P, PB_FAMILY) == FAM_TRUSTED_REPOS ? eval_family(src, P, r0 + rr) : eval_feat(f, x, P);
             v = finish(a, P, fo.reason, fo.arg, fo.mutated);
           }
           vv[jj] = v;
         }
-        uint32_t* dst = a.out + (r0 + rr) * npol + g * 4;
+        uint32_t* dst = out + (r0 + rr) * npol + g * 4;
         if ((npol & 3u) == 0) {
           *(uint4*)dst = make_uint4(vv[0], vv[1], vv[2], vv[3]);
         } else {
@@ -1043,53 +1107,89 @@ __global__ void __launch_bounds__(kTileThreads) evaluate_tiled_kernel(EvalArgs a
             if (g * 4 + jj < npol) dst[jj] = vv[jj];
         }
       }
-    } else {
-      // ---- oversize tile: global path
-      if (FUSED) {
-        // classify this tile's strings into the global mask arrays (same workgroup reads them back)
-        const uint32_t nc = ce - cb;
-        if (a.m[M_NS])
-          for (uint32_t i = tid; i < nr; i += kTileThreads)
-            ((uint64_t*)a.m[M_NS])[r0 + i] = classify_one<M_NS>(ch[M_NS], t.s_bytes[M_NS], t.s_off[M_NS][r0 + i], t.s_off[M_NS][r0 + i + 1]);
-        if (a.m[M_REG] || a.m[M_TAG] || a.m[M_IMG])
-          for (uint32_t i = tid; i < nc; i += kTileThreads) {
-            uint64_t mr = 0, mt = 0, mi = 0;
-            if (a.ctr_flags[cb + i] & KW_CTR_HAS_IMAGE)
-              classify_image_all(ch[M_REG], ch[M_TAG], ch[M_IMG], t.s_bytes[M_IMG], t.s_off[M_IMG][cb + i],
-                                 t.s_off[M_IMG][cb + i + 1], &mr, &mt, &mi);
-            if (a.m[M_REG]) ((uint64_t*)a.m[M_REG])[cb + i] = mr;
-            if (a.m[M_TAG]) ((uint64_t*)a.m[M_TAG])[cb + i] = mt;
-            if (a.m[M_IMG]) ((uint64_t*)a.m[M_IMG])[cb + i] = mi;
-          }
-        if (a.m[M_AA])
-          for (uint32_t i = tid; i < nc; i += kTileThreads)
-            ((uint64_t*)a.m[M_AA])[cb + i] = (a.ctr_flags[cb + i] & KW_CTR_HAS_APPARMOR)
-                                                 ? classify_one<M_AA>(ch[M_AA], t.s_bytes[M_AA], t.s_off[M_AA][cb + i], t.s_off[M_AA][cb + i + 1])
-                                                 : 0ull;
-        if (a.m[M_CAPADD])
-          for (uint32_t i = kab + tid; i < kae; i += kTileThreads)
-            ((uint64_t*)a.m[M_CAPADD])[i] = classify_one<M_CAPADD>(ch[M_CAPADD], t.s_bytes[M_CAPADD], t.s_off[M_CAPADD][i], t.s_off[M_CAPADD][i + 1]);
-        if (a.m[M_CAPDROP])
-          for (uint32_t i = kdb + tid; i < kde; i += kTileThreads)
-            ((uint64_t*)a.m[M_CAPDROP])[i] = classify_one<M_CAPDROP>(ch[M_CAPDROP], t.s_bytes[M_CAPDROP], t.s_off[M_CAPDROP][i], t.s_off[M_CAPDROP][i + 1]);
-        if (a.m[M_LK])
-          for (uint32_t i = lb + tid; i < le; i += kTileThreads)
-            ((uint64_t*)a.m[M_LK])[i] = classify_one<M_LK>(ch[M_LK], t.s_bytes[M_LK], t.s_off[M_LK][i], t.s_off[M_LK][i + 1]);
-        if (a.m[M_LV])
-          for (uint32_t i = lb + tid; i < le; i += kTileThreads)
-            ((uint64_t*)a.m[M_LV])[i] = classify_one<M_LV>(ch[M_LV], t.s_bytes[M_LV], t.s_off[M_LV][i], t.s_off[M_LV][i + 1]);
-        __threadfence();
-        __syncthreads();
-      }
-      GlobalSrc src{&a};
-      for (uint32_t item = wave; item < npol * chunks; item += nwaves) {
-        const uint32_t j = __builtin_amdgcn_readfirstlane(item / chunks);
-        const uint32_t rr = (item - j * chunks) * 64 + lane;
-        const DevPolicy& P = pols[a.pols[j]];
-        if (rr < nr) a.out[(r0 + rr) * npol + j] = verdict(src, a, H, pols, P, r0 + rr, gstk ? gstk + tid : nullptr, kTileThreads);
-      }
+    } else if (tid == 0) {
+      overflow[1 + atomicAdd(&overflow[0], 1u)] = (uint32_t)tile;  // evaluated by overflow_kernel
     }
     __syncthreads();  // the next tile restages LDS
+  }
+}
+
+// Tiles whose entity counts or string bytes exceed the LDS capacities (queued by the tiled
+// kernel in `overflow`: count, then tile indices). Rare by construction (capacities carry 1.5x
+// headroom over the batch average); the masks of such a tile are classified into the global mask
+// arrays with the DFA chains read from the blob, then every (row, policy) pair is evaluated from
+// global memory.
+constexpr int kOverflowThreads = 256;
+__global__ void __launch_bounds__(kOverflowThreads)
+    overflow_kernel(EvalArgs a, const TileArgs* __restrict__ tp, const uint32_t* __restrict__ overflow) {
+  __shared__ uint16_t gstk[kMaxGroupStack * kOverflowThreads];
+  const TileArgs& t = *tp;
+  const uint32_t count = overflow[0];
+  if (blockIdx.x >= count) return;
+  const DevHeader H = *(const DevHeader*)a.blob;
+  const DevPolicy* __restrict__ pols = (const DevPolicy*)(a.blob + H.policy_off);
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), nwaves = kOverflowThreads / 64;
+  Chain ch[NMASK];
+#pragma unroll
+  for (int k = 0; k < (int)NMASK; ++k) {
+    ch[k].head = t.dfa_head[k];
+    ch[k].base = a.blob + t.dfa_head[k];
+  }
+  const uint32_t npol = a.npol;
+  for (uint32_t q = blockIdx.x; q < count; q += gridDim.x) {
+    const uint64_t r0 = (uint64_t)overflow[1 + q] * t.rows;
+    const uint32_t nr = (uint32_t)min((uint64_t)t.rows, a.nrows - r0);
+    const uint32_t cb = a.ctr_off[r0], ce = a.ctr_off[r0 + nr];
+    const uint32_t lb = a.lbl_off[r0], le = a.lbl_off[r0 + nr];
+    const uint32_t kab = a.capadd_off[cb], kae = a.capadd_off[ce];
+    const uint32_t kdb = a.capdrop_off[cb], kde = a.capdrop_off[ce];
+    const uint32_t nc = ce - cb;
+    if (a.m[M_NS])
+      for (uint32_t i = tid; i < nr; i += kOverflowThreads)
+        ((uint64_t*)a.m[M_NS])[r0 + i] =
+            classify_one<M_NS>(ch[M_NS], t.s_bytes[M_NS], t.s_off[M_NS][r0 + i], t.s_off[M_NS][r0 + i + 1]);
+    if (a.m[M_REG] || a.m[M_TAG] || a.m[M_IMG])
+      for (uint32_t i = tid; i < nc; i += kOverflowThreads) {
+        uint64_t mr = 0, mt = 0, mi = 0;
+        if (a.ctr_flags[cb + i] & KW_CTR_HAS_IMAGE)
+          classify_image_all(ch[M_REG], ch[M_TAG], ch[M_IMG], t.s_bytes[M_IMG], t.s_off[M_IMG][cb + i],
+                             t.s_off[M_IMG][cb + i + 1], &mr, &mt, &mi);
+        if (a.m[M_REG]) ((uint64_t*)a.m[M_REG])[cb + i] = mr;
+        if (a.m[M_TAG]) ((uint64_t*)a.m[M_TAG])[cb + i] = mt;
+        if (a.m[M_IMG]) ((uint64_t*)a.m[M_IMG])[cb + i] = mi;
+      }
+    if (a.m[M_AA])
+      for (uint32_t i = tid; i < nc; i += kOverflowThreads)
+        ((uint64_t*)a.m[M_AA])[cb + i] =
+            (a.ctr_flags[cb + i] & KW_CTR_HAS_APPARMOR)
+                ? classify_one<M_AA>(ch[M_AA], t.s_bytes[M_AA], t.s_off[M_AA][cb + i], t.s_off[M_AA][cb + i + 1])
+                : 0ull;
+    if (a.m[M_CAPADD])
+      for (uint32_t i = kab + tid; i < kae; i += kOverflowThreads)
+        ((uint64_t*)a.m[M_CAPADD])[i] =
+            classify_one<M_CAPADD>(ch[M_CAPADD], t.s_bytes[M_CAPADD], t.s_off[M_CAPADD][i], t.s_off[M_CAPADD][i + 1]);
+    if (a.m[M_CAPDROP])
+      for (uint32_t i = kdb + tid; i < kde; i += kOverflowThreads)
+        ((uint64_t*)a.m[M_CAPDROP])[i] =
+            classify_one<M_CAPDROP>(ch[M_CAPDROP], t.s_bytes[M_CAPDROP], t.s_off[M_CAPDROP][i], t.s_off[M_CAPDROP][i + 1]);
+    if (a.m[M_LK])
+      for (uint32_t i = lb + tid; i < le; i += kOverflowThreads)
+        ((uint64_t*)a.m[M_LK])[i] = classify_one<M_LK>(ch[M_LK], t.s_bytes[M_LK], t.s_off[M_LK][i], t.s_off[M_LK][i + 1]);
+    if (a.m[M_LV])
+      for (uint32_t i = lb + tid; i < le; i += kOverflowThreads)
+        ((uint64_t*)a.m[M_LV])[i] = classify_one<M_LV>(ch[M_LV], t.s_bytes[M_LV], t.s_off[M_LV][i], t.s_off[M_LV][i + 1]);
+    __threadfence();
+    __syncthreads();
+    GlobalSrc src{&a};
+    const uint32_t chunks = (nr + 63) / 64;
+    for (uint32_t item = wave; item < npol * chunks; item += nwaves) {
+      const uint32_t j = __builtin_amdgcn_readfirstlane(item / chunks);
+      const uint32_t rr = (item - j * chunks) * 64 + lane;
+      const DevPolicy& P = pols[a.pols[j]];
+      if (rr < nr) a.out[(r0 + rr) * npol + j] = verdict(src, a, H, pols, P, r0 + rr, gstk + tid, kOverflowThreads);
+    }
+    __syncthreads();
   }
 }
 
@@ -1111,7 +1211,8 @@ hipError_t launch_evaluate_rows(const EvalArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_evaluate_tiled(const EvalArgs& a, const TileArgs& t, bool fused, uint32_t grid, hipStream_t s) {
+hipError_t launch_evaluate_tiled(const EvalArgs& a, const TileArgs& t, const TileArgs* d_t, bool fused, uint32_t grid,
+                                 uint32_t* d_overflow, uint32_t overflow_grid, hipStream_t s) {
   if (a.nrows == 0 || a.npol == 0) return hipSuccess;
   static bool attr_set = false;  // allow > 64 KB of dynamic LDS per workgroup (gfx950: 160 KB per CU)
   if (!attr_set) {
@@ -1122,10 +1223,16 @@ hipError_t launch_evaluate_tiled(const EvalArgs& a, const TileArgs& t, bool fuse
     if (e1 != hipSuccess || e2 != hipSuccess) return e1 != hipSuccess ? e1 : e2;
     attr_set = true;
   }
+  hipError_t e = hipMemsetAsync(d_overflow, 0, sizeof(uint32_t), s);
+  if (e != hipSuccess) return e;
   if (fused)
-    hipLaunchKernelGGL(evaluate_tiled_kernel<true>, dim3(grid), dim3(kTileThreads), t.lds_bytes, s, a, t);
+    hipLaunchKernelGGL(evaluate_tiled_kernel<true>, dim3(grid), dim3(kTileThreads), t.lds_bytes, s, a, d_t, a.blob, a.pols,
+                       a.out, d_overflow);
   else
-    hipLaunchKernelGGL(evaluate_tiled_kernel<false>, dim3(grid), dim3(kTileThreads), t.lds_bytes, s, a, t);
+    hipLaunchKernelGGL(evaluate_tiled_kernel<false>, dim3(grid), dim3(kTileThreads), t.lds_bytes, s, a, d_t, a.blob, a.pols,
+                       a.out, d_overflow);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(overflow_kernel, dim3(overflow_grid), dim3(kOverflowThreads), 0, s, a, d_t, d_overflow);
   return hipGetLastError();
 }
 

@@ -53,7 +53,12 @@ struct EvalArgs {
   uint32_t* out;
 };
 
-constexpr int kTileThreads = 512;
+#ifndef KW_TILE_THREADS
+#define KW_TILE_THREADS 1024
+#endif
+// 1024: one workgroup per CU (16 waves share one LDS copy of the tables, 160 KB);
+// 512: two workgroups per CU (80 KB each) whose barriers interleave
+constexpr int kTileThreads = KW_TILE_THREADS;
 
 // Tiled all-pairs evaluation (kernels.hip evaluate_tiled_kernel): LDS layout and capacities.
 struct TileArgs {
@@ -61,7 +66,6 @@ struct TileArgs {
   uint32_t cmax, kmax, lmax;      // container / capability / label capacity of a staged tile
   uint32_t o_rf, o_coff, o_loff, o_cflags, o_cadd, o_cdrop, o_gstk;  // LDS byte offsets
   uint32_t o_m[NMASK];            // LDS byte offset of each staged mask array, 0 = not read
-  uint32_t o_pols;                // LDS copy of the policy table, 0 = read from global
   uint32_t o_feat, o_pos;         // per-row features (RowFeat) and first-occurrence tables
   uint32_t ncap_bits, naa_bits, nkey_bits;  // pattern counts of the literal columns
   uint64_t cap_all_mask;          // COL_CAP bit of the "ALL" capability (0 if none)
@@ -76,10 +80,17 @@ struct TileArgs {
   uint32_t dfa_lds[NMASK];        // LDS offset of that chain's head
   const uint32_t* s_off[NMASK];   // string offsets feeding mask k (M_REG/TAG use M_IMG's column)
   const uint8_t* s_bytes[NMASK];
+  // FUSED: each tile's strings staged in LDS (M_NS, M_IMG, M_AA, M_CAPADD, M_CAPDROP, M_LK, M_LV):
+  // offsets rebased to the staged bytes, bytes copied from the 16-B aligned start; 0 = not staged
+  uint32_t o_so[NMASK], o_sb[NMASK], sb_cap[NMASK];
 };
 
 hipError_t launch_classify(const uint8_t* d_blob, const ClassifyJobs& jobs, hipStream_t s);
 hipError_t launch_evaluate_rows(const EvalArgs& a, hipStream_t s);
-hipError_t launch_evaluate_tiled(const EvalArgs& a, const TileArgs& t, bool fused, uint32_t grid, hipStream_t s);
+// t: host copy (launch geometry); d_t: the same TileArgs resident in device memory (read by the kernel)
+// d_overflow: device queue of tiles exceeding the LDS capacities (count + tile indices; ntiles + 1
+// words), drained by a second launch of overflow_grid workgroups
+hipError_t launch_evaluate_tiled(const EvalArgs& a, const TileArgs& t, const TileArgs* d_t, bool fused, uint32_t grid,
+                                 uint32_t* d_overflow, uint32_t overflow_grid, hipStream_t s);
 
 }  // namespace kw

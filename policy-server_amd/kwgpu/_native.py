@@ -8,7 +8,8 @@ import ctypes as C
 import os
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libkwgpu.so")
+# KWGPU_LIB selects another in-tree build of the same library (kernel A/B experiments)
+LIB_PATH = os.environ.get("KWGPU_LIB") or os.path.join(PKG_DIR, "libkwgpu.so")
 SYNTH_PATH = os.path.join(PKG_DIR, "libkwsynth.so")
 
 # status codes (kwgpu.h)
