@@ -66,26 +66,19 @@ def main():
 
     # compiled tables: built once on rank 0, broadcast over RCCL to the other GPUs
     if world > 1:
-        if rank == 0:
-            env = K.EvaluationEnvironment(policies, device=device)
-            blob = env.serialize()
-            n = torch.tensor([len(blob)], dtype=torch.int64, device="cuda")
-        else:
-            n = torch.zeros(1, dtype=torch.int64, device="cuda")
-        dist.broadcast(n, 0)
-        buf = torch.empty(int(n.item()), dtype=torch.uint8, device="cuda")
-        if rank == 0:
-            buf.copy_(torch.frombuffer(bytearray(blob), dtype=torch.uint8))
-        dist.broadcast(buf, 0)
-        if rank != 0:
-            env = K.EvaluationEnvironment.from_serialized(bytes(buf.cpu().numpy()), device=device)
+        from kwgpu.dist import broadcast_environment
+
+        env = broadcast_environment(policies, dist, rank, device=device, tensor_device="cuda")
     else:
         env = K.EvaluationEnvironment(policies, device=device)
     ids = env.policy_ids()
     npol = len(ids)
 
     t0 = time.time()
-    syn = K.SynthBatch(args.synth, args.rows, seed=20250509, row0=rank * args.rows)
+    from kwgpu.dist import shard
+
+    row0, nrows = shard(args.rows, rank)
+    syn = K.SynthBatch(args.synth, nrows, seed=20250509, row0=row0)
     batch = syn.batch().to_device(device)
     log(f"rank {rank}: {args.rows} requests generated + resident in {time.time() - t0:.1f}s; {npol} policies")
 

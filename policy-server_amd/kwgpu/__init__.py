@@ -278,6 +278,7 @@ class Batch:
     def view(self):
         s = KwSoa()
         raise_for(self._L.kw_batch_view(self._h, C.byref(s)), "view")
+        s._owner = self  # the view points into this batch's columns
         return s
 
     @property
@@ -377,6 +378,7 @@ class SynthBatch:
     def soa(self):
         s = KwSoa()
         self._S.kws_view(self._h, C.byref(s))
+        s._owner = self  # the view points into this generator's columns
         return s
 
     def json(self, row):
