@@ -56,11 +56,17 @@ struct DeviceBatch {
   TileArgs* d_tile = nullptr;
   TileArgs h_tile{};
   bool tile_valid = false;
-  uint32_t* overflow = nullptr;  // tiles beyond the LDS capacities: count + tile indices
+  // host-built tile descriptors + overflow list, cached for one plan geometry (desc_key)
+  TileDesc* desc = nullptr;
+  size_t desc_cap = 0;
+  uint32_t* overflow = nullptr;  // [count, tile indices...]
   size_t overflow_cap = 0;
+  uint32_t n_overflow = 0;
+  uint64_t desc_key = 0;
   ~DeviceBatch() {
     if (device >= 0) (void)hipSetDevice(device);
     (void)hipFree(d_tile);
+    (void)hipFree(desc);
     (void)hipFree(overflow);
     (void)hipFree(cols);
     for (auto* m : masks) (void)hipFree(m);
@@ -198,6 +204,26 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
   auto chain_bytes = [&](uint32_t off) -> uint32_t {
     return off ? ((const DevDfa*)(E.blob.data() + off))->chain_bytes : 0u;
   };
+  // literal-eligible masks classify with the column's perfect-hash table in the fused kernel
+  auto lit_of = [&](int m) -> uint32_t {
+    if (m != M_NS && m != M_AA && m != M_CAPADD && m != M_CAPDROP && m != M_LK) return 0u;
+    return H->lit_off[mask_col(m)];
+  };
+  // what the fused kernel stages for a column: its literal table, else its DFA chain
+  // label values classified per key (one small DFA per constrained key) inside the label-key item
+  const bool kv = H->kv_off && lit_of(M_LK) && need.m[M_LK] && H->dfa_off[COL_LK];
+  auto stage_rec = [&](int m, uint32_t* blob_off) -> uint32_t {
+    if (m == M_LV && kv) {
+      *blob_off = H->kv_off;
+      return H->kv_bytes;
+    }
+    if (uint32_t lo = lit_of(m)) {
+      *blob_off = lo;
+      return ((const DevLit*)(E.blob.data() + lo))->bytes;
+    }
+    *blob_off = H->dfa_off[mask_col(m)];
+    return chain_bytes(*blob_off);
+  };
   // masks this pass reads, restricted to columns that have patterns
   bool use[NMASK] = {};
   for (int m = 0; m < (int)NMASK; ++m) use[m] = need.m[m] && H->dfa_off[mask_col(m)] != 0;
@@ -211,7 +237,8 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
   for (int m = 0; m < (int)NMASK; ++m)
     if (use[m] && !col_staged[mask_col(m)]) {
       col_staged[mask_col(m)] = true;
-      table_bytes += chain_bytes(H->dfa_off[mask_col(m)]);
+      uint32_t o;
+      table_bytes += stage_rec(m, &o);
     }
   plan->fused = !plan->rows_mode && table_bytes <= kFusedTableBudget;
 
@@ -319,7 +346,7 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
   for (int m = 0; m < (int)NMASK; ++m) {
     chain_len[m] = 1;
     // image chains are walked by one item; the non-fused path stages the classify kernel's merged masks
-    if (!plan->fused || !use[m] || m == M_REG || m == M_TAG || m == M_IMG) continue;
+    if (!plan->fused || !use[m] || m == M_REG || m == M_TAG || m == M_IMG || lit_of(m) || (m == M_LV && kv)) continue;
     uint32_t n = 0;
     for (uint32_t o = H->dfa_off[mask_col(m)]; o; o = ((const DevDfa*)(E.blob.data() + o))->next) ++n;
     chain_len[m] = std::max<uint32_t>(1, n);
@@ -367,7 +394,7 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
         const double bpr = B.n ? (double)sc.nbytes / (double)B.n : 0.0;  // string bytes per request
         T.sb_cap[m] = align((uint32_t)std::min(16384.0, scale * rows * bpr + 64));  // longer tiles take the global path
         T.o_sb[m] = off;
-        off = align(off + T.sb_cap[m]);
+        off = align(off + T.sb_cap[m] + 16);  // slack: dword reads may run <= 7 bytes past a string
       }
     T.o_feat = off;
     off = align(off + rows * (5 * 8 + 6 * 4));
@@ -413,13 +440,22 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
         if (!staged[c]) {
           staged[c] = true;
           col_at[c] = at;
-          T.stage_blob[T.nstage] = H->dfa_off[c];
+          uint32_t bo;
+          const uint32_t nb = stage_rec(m, &bo);
+          T.stage_blob[T.nstage] = bo;
           T.stage_lds[T.nstage] = at;
-          T.stage_bytes[T.nstage] = chain_bytes(H->dfa_off[c]);
-          at += chain_bytes(H->dfa_off[c]);
+          T.stage_bytes[T.nstage] = nb;
+          at += nb;
           ++T.nstage;
         }
-        T.dfa_lds[m] = col_at[c];
+        if (lit_of(m)) {
+          T.lit_lds[m] = col_at[c];
+        } else if (m == M_LV && kv) {
+          T.kv_lds = col_at[c];
+          T.kv_blob = H->kv_off;
+        } else {
+          T.dfa_lds[m] = col_at[c];
+        }
       }
     }
     break;
@@ -454,6 +490,73 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
   return KW_OK;
 }
 
+const StrCol& host_strings(const Batch& B, int m) {
+  switch (m) {
+    case M_NS: return B.ns;
+    case M_REG:
+    case M_TAG:
+    case M_IMG: return B.ctr_image;
+    case M_CAPADD: return B.cap_add;
+    case M_CAPDROP: return B.cap_drop;
+    case M_AA: return B.ctr_aa;
+    case M_LK: return B.lbl_key;
+    default: return B.lbl_val;
+  }
+}
+
+// Tile descriptors (kernels.hpp TileDesc) and the overflow list of one plan geometry, built from the
+// host copy of the batch and uploaded once; reused while the geometry stays the same.
+int upload_tile_descs(const Batch& B, DeviceBatch* D, const TileArgs& T) {
+  uint64_t key = 1469598103934665603ull;
+  auto mix = [&](uint64_t v) { key = (key ^ v) * 1099511628211ull; };
+  mix(T.rows);
+  mix(T.cmax);
+  mix(T.kmax);
+  mix(T.lmax);
+  for (int m = 0; m < (int)NMASK; ++m) {
+    mix(T.o_sb[m] != 0);
+    mix(T.sb_cap[m]);
+  }
+  if (D->desc && key == D->desc_key) return KW_OK;
+  const uint64_t ntiles = (B.n + T.rows - 1) / T.rows;
+  std::vector<TileDesc> desc(ntiles);
+  std::vector<uint32_t> ovf{0};
+  for (uint64_t tile = 0; tile < ntiles; ++tile) {
+    TileDesc& d = desc[tile];
+    memset(&d, 0, sizeof(d));
+    const uint64_t r0 = tile * T.rows, r1 = std::min<uint64_t>(B.n, r0 + T.rows);
+    d.cb = B.ctr_off[r0];
+    d.ce = B.ctr_off[r1];
+    d.lb = B.lbl_off[r0];
+    d.le = B.lbl_off[r1];
+    d.kab = B.capadd_off[d.cb];
+    d.kae = B.capadd_off[d.ce];
+    d.kdb = B.capdrop_off[d.cb];
+    d.kde = B.capdrop_off[d.ce];
+    bool fits = d.ce - d.cb <= T.cmax && d.kae - d.kab <= T.kmax && d.kde - d.kdb <= T.kmax && d.le - d.lb <= T.lmax;
+    for (int m = 0; m < (int)NMASK; ++m) {
+      if (!T.o_sb[m]) continue;
+      const uint64_t g0 = m == M_NS ? r0 : m == M_CAPADD ? d.kab : m == M_CAPDROP ? d.kdb : (m == M_LK || m == M_LV) ? d.lb : d.cb;
+      const uint64_t g1 = m == M_NS ? r1 : m == M_CAPADD ? d.kae : m == M_CAPDROP ? d.kde : (m == M_LK || m == M_LV) ? d.le : d.ce;
+      const StrCol& c = host_strings(B, m);
+      d.sa[m] = c.off[g0] & ~15u;
+      d.nv[m] = (((c.off[g1] + 15u) & ~15u) - d.sa[m]) / 16u;
+      fits = fits && d.nv[m] * 16u <= T.sb_cap[m];
+    }
+    d.fits = fits ? 1u : 0u;
+    if (!fits) ovf.push_back((uint32_t)tile);
+  }
+  ovf[0] = (uint32_t)(ovf.size() - 1);
+  HIPCHK(hipStreamSynchronize(D->stream));  // a running pass may still read the previous descriptors
+  if (int rc = ensure(&D->desc, &D->desc_cap, (size_t)std::max<uint64_t>(ntiles, 1))) return rc;
+  if (int rc = ensure(&D->overflow, &D->overflow_cap, ovf.size())) return rc;
+  if (ntiles) HIPCHK(hipMemcpy(D->desc, desc.data(), ntiles * sizeof(TileDesc), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(D->overflow, ovf.data(), ovf.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  D->n_overflow = ovf[0];
+  D->desc_key = key;
+  return KW_OK;
+}
+
 int run_pass(const kw_env* env, kw_batch* kb, const PassPlan& plan, bool timed) {
   DeviceBatch& D = *kb->dev;
   if (timed) HIPCHK(hipEventRecord(D.ev[0], D.stream));
@@ -468,10 +571,9 @@ int run_pass(const kw_env* env, kw_batch* kb, const PassPlan& plan, bool timed) 
       HIPCHK(hipMemcpyAsync(D.d_tile, &D.h_tile, sizeof(TileArgs), hipMemcpyHostToDevice, D.stream));
       D.tile_valid = true;
     }
-    const uint64_t ntiles = (plan.args.nrows + plan.tile.rows - 1) / plan.tile.rows;
-    if (int rc = ensure(&D.overflow, &D.overflow_cap, ntiles + 1)) return rc;
-    HIPCHK(launch_evaluate_tiled(plan.args, plan.tile, D.d_tile, plan.fused, plan.grid, D.overflow,
-                                 (uint32_t)std::min<uint64_t>(ntiles, 512), D.stream));
+    if (int rc = upload_tile_descs(kb->b, &D, plan.tile)) return rc;
+    HIPCHK(launch_evaluate_tiled(plan.args, plan.tile, D.d_tile, D.desc, plan.fused, plan.grid, D.overflow,
+                                 D.n_overflow, D.stream));
   }
   if (timed) HIPCHK(hipEventRecord(D.ev[2], D.stream));
   return KW_OK;

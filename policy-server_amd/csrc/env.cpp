@@ -352,6 +352,93 @@ void align16(std::vector<uint8_t>* b) {
   while (b->size() % 16) b->push_back(0);
 }
 
+// Appends one DevDfa record (header, accept masks, transitions; 16-B aligned) and returns its
+// blob offset. trans_off / acc_off are blob offsets.
+size_t emit_dfa(const Dfa& dfa, std::vector<uint8_t>* b) {
+  align16(b);
+  const size_t hdr_at = b->size();
+  DevDfa dd;
+  memset(&dd, 0, sizeof(dd));
+  dd.nstates = dfa.nstates;
+  dd.ncls = dfa.ncls;
+  dd.start = dfa.start;
+  memcpy(dd.cls, dfa.cls.data(), 256);
+  put(b, dd);
+  align16(b);
+  const uint32_t acc_off = (uint32_t)b->size();
+  for (uint64_t a : dfa.accept) put(b, a);
+  align16(b);
+  const uint32_t trans_off = (uint32_t)b->size();
+  for (uint16_t t : dfa.trans) put(b, t);
+  align16(b);
+  DevDfa* w = (DevDfa*)(b->data() + hdr_at);
+  w->acc_off = acc_off;
+  w->trans_off = trans_off;
+  w->bytes = (uint32_t)(b->size() - hdr_at);
+  w->chain_bytes = w->bytes;
+  return hdr_at;
+}
+
+// Canonical dwords of a string: little-endian, the last one zero-padded (what the kernels build
+// from the staged bytes with v_alignbyte).
+std::vector<uint32_t> lit_words(const std::string& s) {
+  std::vector<uint32_t> w((s.size() + 3) / 4, 0u);
+  if (!s.empty()) memcpy(w.data(), s.data(), s.size());
+  return w;
+}
+uint32_t lit_hash(const std::vector<uint32_t>& w, uint32_t len, uint32_t seed) {
+  uint32_t h = lit_init(seed, len);
+  for (uint32_t x : w) h = lit_mix(h, x);
+  return lit_final(h);
+}
+
+// Appends a DevLit record (kwdev.hpp) for an all-literal column: the smallest power-of-two table
+// (>= 2x the patterns) and seed for which the hash is collision-free over the patterns.
+bool build_literal_table(const std::vector<Pattern>& pats, std::vector<uint8_t>* b) {
+  const uint32_t npat = (uint32_t)pats.size();
+  std::vector<std::vector<uint32_t>> words;
+  for (const Pattern& p : pats) words.push_back(lit_words(p.text));
+  for (uint32_t nslots = 16; nslots <= 4096; nslots *= 2) {
+    if (nslots < 2 * npat) continue;
+    for (uint32_t seed = 1; seed <= 4096; ++seed) {
+      std::vector<uint16_t> slot(nslots, 0);
+      bool ok = true;
+      for (uint32_t i = 0; i < npat && ok; ++i) {
+        uint32_t h = lit_hash(words[i], (uint32_t)pats[i].text.size(), seed) & (nslots - 1);
+        if (slot[h]) ok = false;
+        else slot[h] = (uint16_t)(i + 1);
+      }
+      if (!ok) continue;
+      const size_t at = b->size();
+      DevLit L;
+      memset(&L, 0, sizeof(L));
+      L.nslots = nslots;
+      L.seed = seed;
+      L.npat = npat;
+      put(b, L);
+      L.slot_off = (uint32_t)(b->size() - at);
+      for (uint16_t x : slot) put(b, x);
+      align16(b);
+      L.ent_off = (uint32_t)(b->size() - at);
+      uint32_t wi = 0;
+      for (uint32_t i = 0; i < npat; ++i) {
+        put(b, wi);
+        put(b, (uint32_t)pats[i].text.size());
+        wi += (uint32_t)words[i].size();
+      }
+      align16(b);
+      L.word_off = (uint32_t)(b->size() - at);
+      for (const auto& w : words)
+        for (uint32_t x : w) put(b, x);
+      align16(b);
+      L.bytes = (uint32_t)(b->size() - at);
+      memcpy(b->data() + at, &L, sizeof(L));
+      return true;
+    }
+  }
+  return false;
+}
+
 }  // namespace
 
 Env::~Env() = default;  // device memory released by capi (needs HIP)
@@ -569,29 +656,7 @@ Status build_env(const char* json, size_t len, bool continue_on_errors, const ch
     if (!compile_column(env->cols[c], kMaxDfaTableBytes, &chain, &err))
       return {KW_E_BOOTSTRAP, "bootstrap failure: cannot compile column automaton: " + err};
     std::vector<size_t> at;
-    for (const Dfa& dfa : chain) {
-      align16(&b);
-      size_t hdr_at = b.size();
-      at.push_back(hdr_at);
-      DevDfa dd;
-      memset(&dd, 0, sizeof(dd));
-      dd.nstates = dfa.nstates;
-      dd.ncls = dfa.ncls;
-      dd.start = dfa.start;
-      memcpy(dd.cls, dfa.cls.data(), 256);
-      put(&b, dd);
-      align16(&b);
-      uint32_t acc_off = (uint32_t)b.size();
-      for (uint64_t a : dfa.accept) put(&b, a);
-      align16(&b);
-      uint32_t trans_off = (uint32_t)b.size();
-      for (uint16_t t : dfa.trans) put(&b, t);
-      align16(&b);
-      DevDfa* w = (DevDfa*)(b.data() + hdr_at);
-      w->acc_off = acc_off;
-      w->trans_off = trans_off;
-      w->bytes = (uint32_t)(b.size() - hdr_at);
-    }
+    for (const Dfa& dfa : chain) at.push_back(emit_dfa(dfa, &b));
     uint32_t tail = 0;
     for (size_t k = chain.size(); k-- > 0;) {
       DevDfa* w = (DevDfa*)(b.data() + at[k]);
@@ -600,6 +665,56 @@ Status build_env(const char* json, size_t len, bool continue_on_errors, const ch
       w->chain_bytes = tail;
     }
     hdr.dfa_off[c] = (uint32_t)at[0];
+  }
+  // literal columns: perfect-hash tables (the fused kernel's fast path; DFAs stay for the others)
+  for (int c = 0; c < (int)NCOL; ++c) {
+    if (env->cols[c].empty()) continue;
+    bool lit = true;
+    for (const Pattern& p : env->cols[c]) lit = lit && p.kind == Pattern::Literal;
+    if (!lit) continue;
+    align16(&b);
+    hdr.lit_off[c] = (uint32_t)b.size();
+    if (!build_literal_table(env->cols[c], &b))
+      return {KW_E_BOOTSTRAP, "bootstrap failure: cannot build the literal table of column " + std::to_string(c)};
+  }
+  // per-key label-value DFAs: a label's value is only ever tested against the regexes constrained
+  // on its own key, so one small DFA per constrained key replaces the chain over all value regexes
+  if (hdr.lit_off[COL_LK] && !env->cols[COL_LV].empty()) {
+    std::vector<std::vector<uint32_t>> vals(kMaxPatternsPerColumn);
+    for (const DevPolicy& P : dp) {
+      if (P.family != FAM_LABELS) continue;
+      for (uint32_t k = 0; k < P.n_constr; ++k) {
+        auto& v = vals[P.idx[16 + k]];
+        if (std::find(v.begin(), v.end(), (uint32_t)P.idx[32 + k]) == v.end()) v.push_back(P.idx[32 + k]);
+      }
+    }
+    std::vector<Dfa> kd(kMaxPatternsPerColumn);
+    bool ok = true;
+    for (size_t k = 0; k < vals.size() && ok; ++k) {
+      if (vals[k].empty()) continue;
+      std::vector<Pattern> pats;
+      for (uint32_t v : vals[k]) pats.push_back(env->cols[COL_LV][v]);
+      std::string err;
+      ok = compile_dfa(pats, &kd[k], &err) && kd[k].trans.size() * 2 <= kMaxDfaTableBytes;
+      for (uint64_t& a : kd[k].accept) {  // local pattern bits -> the column's global bits
+        uint64_t g = 0;
+        for (size_t i = 0; i < vals[k].size(); ++i)
+          if ((a >> i) & 1ull) g |= 1ull << vals[k][i];
+        a = g;
+      }
+    }
+    if (ok) {
+      align16(&b);
+      const size_t region = b.size();
+      uint32_t idx[kMaxPatternsPerColumn] = {};
+      put(&b, idx);
+      for (size_t k = 0; k < vals.size(); ++k)
+        if (!vals[k].empty()) idx[k] = (uint32_t)(emit_dfa(kd[k], &b) - region);
+      memcpy(b.data() + region, idx, sizeof(idx));
+      align16(&b);
+      hdr.kv_off = (uint32_t)region;
+      hdr.kv_bytes = (uint32_t)(b.size() - region);
+    }
   }
   align16(&b);
   hdr.policy_off = (uint32_t)b.size();

@@ -99,6 +99,32 @@ __device__ inline bool equals_const(const uint8_t* __restrict__ bytes, uint32_t 
   return true;
 }
 
+// Literal-column lookup (DevLit, kwdev.hpp): hash the string's canonical dwords, probe one slot,
+// verify against the pattern's words. `rec` and `bytes` may be LDS or global; dwords are read at
+// 4-aligned addresses and realigned with v_alignbyte (reads may touch <= 7 bytes past the string,
+// inside the pool's zero pad or the staged tile's slack).
+__device__ inline uint32_t lit_word(const uint32_t* base, uint32_t i, uint32_t sh, uint32_t len) {
+  uint32_t w = __builtin_amdgcn_alignbyte(base[i + 1], base[i], sh);
+  const uint32_t rem = len - 4u * i;
+  return rem >= 4u ? w : (w & ((1u << (8u * rem)) - 1u));
+}
+__device__ inline uint64_t lit_lookup(const uint8_t* rec, const uint8_t* bytes, uint32_t b, uint32_t e) {
+  const DevLit* L = (const DevLit*)rec;
+  const uint32_t len = e - b, sh = b & 3u, nw = (len + 3u) >> 2;
+  const uint32_t* base = (const uint32_t*)(bytes + (b & ~3u));
+  uint32_t h = lit_init(L->seed, len);
+  for (uint32_t i = 0; i < nw; ++i) h = lit_mix(h, lit_word(base, i, sh, len));
+  h = lit_final(h);
+  const uint32_t s = ((const uint16_t*)(rec + L->slot_off))[h & (L->nslots - 1u)];
+  if (!s) return 0ull;
+  const uint2 ent = ((const uint2*)(rec + L->ent_off))[s - 1u];
+  if (ent.y != len) return 0ull;
+  const uint32_t* pw = (const uint32_t*)(rec + L->word_off) + ent.x;
+  for (uint32_t i = 0; i < nw; ++i)
+    if (lit_word(base, i, sh, len) != pw[i]) return 0ull;
+  return 1ull << (s - 1u);
+}
+
 // A column's DFA chain, staged contiguously (LDS, or the blob itself): element at blob offset
 // `off` lives at base + (off - head).
 struct Chain {
@@ -766,12 +792,13 @@ __device__ inline uint32_t tile_n(int m, uint32_t nr, uint32_t nc, uint32_t nka,
 
 template <bool FUSED>
 __global__ void __launch_bounds__(kTileThreads)
-    evaluate_tiled_kernel(EvalArgs a, const TileArgs* __restrict__ tp, const uint8_t* __restrict__ blob,
-                          const int32_t* __restrict__ plist, uint32_t* __restrict__ out, uint32_t* __restrict__ overflow) {
+    evaluate_tiled_kernel(EvalArgs a, const TileArgs* __restrict__ tp, const TileDesc* __restrict__ desc,
+                          const uint8_t* __restrict__ blob, const int32_t* __restrict__ plist,
+                          uint32_t* __restrict__ out) {
   // TileArgs lives in device memory: its fields are scalar-loaded where used instead of all being
   // hoisted from the kernarg segment into SGPRs at entry. blob / plist / out are __restrict__ so
   // wave-uniform policy reads compile to scalar loads (nothing in this kernel stores to global
-  // memory except `out` and `overflow`).
+  // memory except `out`).
   const TileArgs& t = *tp;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const DevHeader H = *(const DevHeader*)blob;
@@ -823,22 +850,10 @@ __global__ void __launch_bounds__(kTileThreads)
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const uint64_t r0 = tile * t.rows;
     const uint32_t nr = (uint32_t)min((uint64_t)t.rows, a.nrows - r0);
-    const uint32_t cb = a.ctr_off[r0], ce = a.ctr_off[r0 + nr];
-    const uint32_t lb = a.lbl_off[r0], le = a.lbl_off[r0 + nr];
-    const uint32_t kab = a.capadd_off[cb], kae = a.capadd_off[ce];
-    const uint32_t kdb = a.capdrop_off[cb], kde = a.capdrop_off[ce];
-    bool fits = (ce - cb) <= t.cmax && (kae - kab) <= t.kmax && (kde - kdb) <= t.kmax && (le - lb) <= t.lmax;
-    // staged string ranges: [sa, sz) of each column's pool, 16-B aligned (pools carry a >= 16 B zero tail)
-    if (FUSED) {
-#pragma unroll
-      for (int m = 0; m < (int)NMASK; ++m) {
-        if (!t.o_sb[m]) continue;
-        const uint32_t g0 = tile_g0(m, (uint32_t)r0, cb, kab, kdb, lb);
-        const uint32_t n = tile_n(m, nr, ce - cb, kae - kab, kde - kdb, le - lb);
-        const auto* so = gp(t.s_off[m]);
-        fits = fits && ((so[g0 + n] + 15u) & ~15u) - (so[g0] & ~15u) <= t.sb_cap[m];
-      }
-    }
+    const TileDesc& d = desc[tile];
+    const uint32_t cb = d.cb, ce = d.ce, lb = d.lb, le = d.le;
+    const uint32_t kab = d.kab, kae = d.kae, kdb = d.kdb, kde = d.kde;
+    const bool fits = d.fits != 0;  // else queued for overflow_kernel by the host
     const uint32_t chunks = (nr + 63) / 64;
 
     if (fits) {
@@ -879,8 +894,7 @@ __global__ void __launch_bounds__(kTileThreads)
           const uint32_t g0 = tile_g0(m, (uint32_t)r0, cb, kab, kdb, lb);
           const uint32_t n = tile_n(m, nr, ce - cb, kae - kab, kde - kdb, le - lb);
           const auto* go = gp(t.s_off[m]);
-          const uint32_t sa = __builtin_amdgcn_readfirstlane(go[g0] & ~15u);
-          const uint32_t nv = __builtin_amdgcn_readfirstlane((((go[g0 + n] + 15u) & ~15u) - sa) / 16u);
+          const uint32_t sa = d.sa[m], nv = d.nv[m];
           uint32_t* so = (uint32_t*)(lds + t.o_so[m]);
           for (uint32_t i = tid; i <= n; i += kTileThreads) so[i] = go[g0 + i] - sa;
           const auto* src = gp((const u32x4*)(t.s_bytes[m] + sa));
@@ -898,7 +912,7 @@ __global__ void __launch_bounds__(kTileThreads)
         const uint32_t n3 = t.o_m[M_CAPADD] ? (kae - kab) * t.chain_len[M_CAPADD] : 0u;
         const uint32_t n4 = t.o_m[M_CAPDROP] ? (kde - kdb) * t.chain_len[M_CAPDROP] : 0u;
         const uint32_t n5 = t.o_m[M_LK] ? (le - lb) * t.chain_len[M_LK] : 0u;
-        const uint32_t n6 = t.o_m[M_LV] ? (le - lb) * t.chain_len[M_LV] : 0u;
+        const uint32_t n6 = (t.o_m[M_LV] && !t.kv_lds) ? (le - lb) * t.chain_len[M_LV] : 0u;  // kv: in the LK item
         const uint32_t s1 = n0, s2 = s1 + n1, s3 = s2 + n2 * t.chain_len[M_AA], s4 = s3 + n3, s5 = s4 + n4,
                        s6 = s5 + n5, s7 = s6 + n6;
         for (uint32_t w = tid; w < s7; w += kTileThreads) {
@@ -926,7 +940,12 @@ __global__ void __launch_bounds__(kTileThreads)
           const uint32_t e = local - i * clen;
           uint64_t* lm = (uint64_t*)(lds + t.o_m[m]);
           uint64_t r = 0;
-          if (m != M_AA || (l_cflags[i] & KW_CTR_HAS_APPARMOR)) {
+          if (m == M_AA && !(l_cflags[i] & KW_CTR_HAS_APPARMOR)) {
+            r = 0;
+          } else if (t.lit_lds[m]) {
+            const uint32_t* so = (const uint32_t*)(lds + t.o_so[m]);
+            r = lit_lookup(lds + t.lit_lds[m], lds + t.o_sb[m], so[i], so[i + 1]);
+          } else {
             Chain c;
             c.head = t.dfa_head[m];
             c.base = lds + t.dfa_lds[m];
@@ -937,6 +956,18 @@ __global__ void __launch_bounds__(kTileThreads)
             r = v.acc[feed(v, v.start, lds + t.o_sb[m], so[i], so[i + 1])];
           }
           lm[e * cap + i] = r;  // chain element e -> its own partial slot
+          if (m == M_LK && t.kv_lds) {  // the label's value, against the regexes of its own key only
+            uint64_t lv = 0;
+            if (r) {
+              const uint32_t rel = ((const uint32_t*)(lds + t.kv_lds))[__builtin_ctzll(r)];
+              if (rel) {
+                const DfaView v = make_view(lds + t.kv_lds + rel, nullptr, t.kv_blob + rel);
+                const uint32_t* so = (const uint32_t*)(lds + t.o_so[M_LV]);
+                lv = v.acc[feed(v, v.start, lds + t.o_sb[M_LV], so[i], so[i + 1])];
+              }
+            }
+            ((uint64_t*)(lds + t.o_m[M_LV]))[i] = lv;
+          }
         }
       } else if (!FUSED) {
         const uint32_t base[NMASK] = {(uint32_t)r0, cb, cb, cb, kab, kdb, cb, lb, lb};
@@ -1107,15 +1138,13 @@ __global__ void __launch_bounds__(kTileThreads)
             if (g * 4 + jj < npol) dst[jj] = vv[jj];
         }
       }
-    } else if (tid == 0) {
-      overflow[1 + atomicAdd(&overflow[0], 1u)] = (uint32_t)tile;  // evaluated by overflow_kernel
     }
     __syncthreads();  // the next tile restages LDS
   }
 }
 
-// Tiles whose entity counts or string bytes exceed the LDS capacities (queued by the tiled
-// kernel in `overflow`: count, then tile indices). Rare by construction (capacities carry 1.5x
+// Tiles whose entity counts or string bytes exceed the LDS capacities (listed by the host with the
+// tile descriptors in `overflow`: count, then tile indices). Rare by construction (capacities carry 1.5x
 // headroom over the batch average); the masks of such a tile are classified into the global mask
 // arrays with the DFA chains read from the blob, then every (row, policy) pair is evaluated from
 // global memory.
@@ -1211,8 +1240,9 @@ hipError_t launch_evaluate_rows(const EvalArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_evaluate_tiled(const EvalArgs& a, const TileArgs& t, const TileArgs* d_t, bool fused, uint32_t grid,
-                                 uint32_t* d_overflow, uint32_t overflow_grid, hipStream_t s) {
+hipError_t launch_evaluate_tiled(const EvalArgs& a, const TileArgs& t, const TileArgs* d_t, const TileDesc* d_desc,
+                                 bool fused, uint32_t grid, const uint32_t* d_overflow, uint32_t n_overflow,
+                                 hipStream_t s) {
   if (a.nrows == 0 || a.npol == 0) return hipSuccess;
   static bool attr_set = false;  // allow > 64 KB of dynamic LDS per workgroup (gfx950: 160 KB per CU)
   if (!attr_set) {
@@ -1223,16 +1253,16 @@ hipError_t launch_evaluate_tiled(const EvalArgs& a, const TileArgs& t, const Til
     if (e1 != hipSuccess || e2 != hipSuccess) return e1 != hipSuccess ? e1 : e2;
     attr_set = true;
   }
-  hipError_t e = hipMemsetAsync(d_overflow, 0, sizeof(uint32_t), s);
-  if (e != hipSuccess) return e;
   if (fused)
-    hipLaunchKernelGGL(evaluate_tiled_kernel<true>, dim3(grid), dim3(kTileThreads), t.lds_bytes, s, a, d_t, a.blob, a.pols,
-                       a.out, d_overflow);
+    hipLaunchKernelGGL(evaluate_tiled_kernel<true>, dim3(grid), dim3(kTileThreads), t.lds_bytes, s, a, d_t, d_desc,
+                       a.blob, a.pols, a.out);
   else
-    hipLaunchKernelGGL(evaluate_tiled_kernel<false>, dim3(grid), dim3(kTileThreads), t.lds_bytes, s, a, d_t, a.blob, a.pols,
-                       a.out, d_overflow);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(overflow_kernel, dim3(overflow_grid), dim3(kOverflowThreads), 0, s, a, d_t, d_overflow);
+    hipLaunchKernelGGL(evaluate_tiled_kernel<false>, dim3(grid), dim3(kTileThreads), t.lds_bytes, s, a, d_t, d_desc,
+                       a.blob, a.pols, a.out);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || n_overflow == 0) return e;
+  hipLaunchKernelGGL(overflow_kernel, dim3(std::min<uint32_t>(n_overflow, 512)), dim3(kOverflowThreads), 0, s, a, d_t,
+                     d_overflow);
   return hipGetLastError();
 }
 

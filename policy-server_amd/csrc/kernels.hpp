@@ -78,6 +78,8 @@ struct TileArgs {
   uint32_t stage_blob[NCOL], stage_lds[NCOL], stage_bytes[NCOL];
   uint32_t dfa_head[NMASK];       // blob offset of the chain used for mask k (0 = none)
   uint32_t dfa_lds[NMASK];        // LDS offset of that chain's head
+  uint32_t lit_lds[NMASK];        // LDS offset of the column's literal table (replaces the DFA), 0 = none
+  uint32_t kv_lds, kv_blob;       // per-key label-value DFA region: LDS and blob offsets (0 = LV chain)
   const uint32_t* s_off[NMASK];   // string offsets feeding mask k (M_REG/TAG use M_IMG's column)
   const uint8_t* s_bytes[NMASK];
   // FUSED: each tile's strings staged in LDS (M_NS, M_IMG, M_AA, M_CAPADD, M_CAPDROP, M_LK, M_LV):
@@ -88,9 +90,22 @@ struct TileArgs {
 hipError_t launch_classify(const uint8_t* d_blob, const ClassifyJobs& jobs, hipStream_t s);
 hipError_t launch_evaluate_rows(const EvalArgs& a, hipStream_t s);
 // t: host copy (launch geometry); d_t: the same TileArgs resident in device memory (read by the kernel)
-// d_overflow: device queue of tiles exceeding the LDS capacities (count + tile indices; ntiles + 1
-// words), drained by a second launch of overflow_grid workgroups
-hipError_t launch_evaluate_tiled(const EvalArgs& a, const TileArgs& t, const TileArgs* d_t, bool fused, uint32_t grid,
-                                 uint32_t* d_overflow, uint32_t overflow_grid, hipStream_t s);
+// Per-tile geometry, precomputed on the host from the batch's offsets (one s_load burst per tile
+// instead of a chain of dependent global loads): entity ranges, the 16-B aligned byte range of each
+// staged string column, and whether the tile fits the LDS capacities.
+struct alignas(16) TileDesc {
+  uint32_t cb, ce, lb, le, kab, kae, kdb, kde;
+  uint32_t sa[NMASK];  // staged column m: first byte (16-B aligned) of the tile's strings in the pool
+  uint32_t nv[NMASK];  //                  16-B vectors to copy
+  uint32_t fits;
+  uint32_t pad[5];
+};
+static_assert(sizeof(TileDesc) == 128, "TileDesc layout");
+
+// d_overflow: [count, tile indices...] of the tiles that do not fit (host-built with the
+// descriptors); a second launch evaluates them when n_overflow > 0
+hipError_t launch_evaluate_tiled(const EvalArgs& a, const TileArgs& t, const TileArgs* d_t, const TileDesc* d_desc,
+                                 bool fused, uint32_t grid, const uint32_t* d_overflow, uint32_t n_overflow,
+                                 hipStream_t s);
 
 }  // namespace kw

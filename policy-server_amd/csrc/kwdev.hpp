@@ -7,7 +7,7 @@
 namespace kw {
 
 constexpr uint32_t kBlobMagic = 0x4b574731;  // "KWG1"
-constexpr uint32_t kBlobVersion = 1;
+constexpr uint32_t kBlobVersion = 2;
 
 // request columns that carry strings classified by a DFA
 enum Col : uint32_t {
@@ -57,6 +57,34 @@ struct alignas(16) DevDfa {
   uint8_t cls[256];
 };
 
+// Literal column: a perfect hash over the column's literal patterns (every pattern of the column
+// is a Literal). A string matches at most one pattern; lookup = hash of its canonical little-endian
+// dwords -> slot -> one verify against the pattern's words. Record layout (offsets from its start):
+//   DevLit | u16 slot[nslots] (pattern index + 1, 0 = empty) | u32 ent[npat][2] (word index, len)
+//   | u32 words[] (each pattern zero-padded to whole dwords)
+struct alignas(16) DevLit {
+  uint32_t nslots, seed, npat, bytes;      // bytes: whole record, multiple of 16
+  uint32_t slot_off, ent_off, word_off, pad;
+};
+
+#if defined(__HIPCC__)
+#define KW_HD __host__ __device__
+#else
+#define KW_HD
+#endif
+// hash shared by the host table builder (env.cpp) and the kernels
+inline KW_HD uint32_t lit_init(uint32_t seed, uint32_t len) { return seed ^ (len * 0x9E3779B1u); }
+inline KW_HD uint32_t lit_mix(uint32_t h, uint32_t w) {
+  h ^= w;
+  h *= 0x85EBCA6Bu;
+  return h ^ (h >> 13);
+}
+inline KW_HD uint32_t lit_final(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x7FEB352Du;
+  return h ^ (h >> 15);
+}
+
 // One policy (or group member) — 192 bytes. Mask meaning per family (env.cpp):
 //   NAMESPACE:     m[0] valid-namespace bit (COL_NS)
 //   TRUSTED_REPOS: m[0] registry allow, m[1] registry reject (COL_REG), m[2] tag reject (COL_TAG),
@@ -81,6 +109,10 @@ static_assert(sizeof(DevPolicy) == 192, "DevPolicy layout");
 struct alignas(16) DevHeader {
   uint32_t magic, version, npolicies, blob_bytes;
   uint32_t dfa_off[NCOL];  // head of the column's DFA chain, 0 = no patterns for this column
+  uint32_t lit_off[NCOL];  // DevLit record of an all-literal column, 0 = none
+  // per-key label-value DFAs: region = u32 idx[64] (region-relative offset of the DevDfa for
+  // label-key bit k over the value regexes constrained on that key, 0 = none) + the DFAs
+  uint32_t kv_off, kv_bytes;  // 0 = none (the COL_LV chain is used)
   int32_t bypass_bit;      // COL_NS bit of the always-accept namespace, -1 = none
   uint32_t policy_off;     // DevPolicy[npolicies]
   uint32_t prog_off;       // group programs (bytes)
