@@ -189,6 +189,12 @@ int kw_env_validate_settings(const kw_env *env, int32_t idx, char *buf, size_t c
 /* Diagnostic: does `s` match pattern `pat` (kind 0 literal, 1 glob, 2 regex) under the engine's
  * compiled-automaton semantics? 1/0, or -1 on a pattern syntax error. */
 int kw_pattern_match(int kind, const char *pat, const char *s, size_t len);
+/* Diagnostic: classify `s` for request column `col` (kwdev.hpp Col) through the column's DFA chain
+ * (*dfa_mask) and through the fused kernel's fast table (*fast_mask): the literal perfect-hash
+ * table, or for COL_LV the per-key value DFA of label key `key` (then *dfa_mask is restricted to
+ * the value patterns constrained on that key). Returns 1 if a fast table exists, 0 if not. */
+int kw_env_classify_check(const kw_env *env, int col, const char *key, size_t klen, const char *s,
+                          size_t len, uint64_t *dfa_mask, uint64_t *fast_mask);
 
 /* ---------------------------------------------------------------------------------------------
  * Request batches: the micro-batch handed over by the HTTP front (replaces the one

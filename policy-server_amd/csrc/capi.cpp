@@ -747,6 +747,67 @@ int kw_pattern_match(int kind, const char* pat, const char* s, size_t len) {
   return (d.run((const uint8_t*)s, len) & 1ull) ? 1 : 0;
 }
 
+namespace {
+// Host walks of the compiled blob, mirroring the kernels (diagnostics / tests only).
+uint64_t blob_dfa_run(const uint8_t* blob, uint32_t off, const uint8_t* s, size_t n) {
+  const DevDfa* d = (const DevDfa*)(blob + off);
+  const uint16_t* trans = (const uint16_t*)(blob + d->trans_off);
+  const uint64_t* acc = (const uint64_t*)(blob + d->acc_off);
+  uint32_t st = d->start;
+  for (size_t i = 0; i < n && st != 0; ++i) st = trans[(size_t)st * d->ncls + d->cls[s[i]]];
+  return acc[st];
+}
+uint64_t blob_chain_run(const uint8_t* blob, uint32_t head, const uint8_t* s, size_t n) {
+  uint64_t m = 0;
+  for (uint32_t o = head; o; o = ((const DevDfa*)(blob + o))->next) m |= blob_dfa_run(blob, o, s, n);
+  return m;
+}
+uint64_t blob_lit_lookup(const uint8_t* blob, uint32_t off, const uint8_t* s, size_t n) {
+  const DevLit* L = (const DevLit*)(blob + off);
+  const uint8_t* rec = blob + off;
+  std::vector<uint32_t> w((n + 3) / 4, 0u);
+  if (n) memcpy(w.data(), s, n);
+  uint32_t h = lit_init(L->seed, (uint32_t)n);
+  for (uint32_t x : w) h = lit_mix(h, x);
+  h = lit_final(h);
+  const uint32_t slot = ((const uint16_t*)(rec + L->slot_off))[h & (L->nslots - 1)];
+  if (!slot) return 0;
+  const uint32_t* ent = (const uint32_t*)(rec + L->ent_off) + 2 * (slot - 1);
+  if (ent[1] != n) return 0;
+  const uint32_t* pw = (const uint32_t*)(rec + L->word_off) + ent[0];
+  for (size_t i = 0; i < w.size(); ++i)
+    if (w[i] != pw[i]) return 0;
+  return 1ull << (slot - 1);
+}
+}  // namespace
+
+int kw_env_classify_check(const kw_env* env, int col, const char* key, size_t klen, const char* s, size_t len,
+                          uint64_t* dfa_mask, uint64_t* fast_mask) {
+  if (!env || col < 0 || col >= (int)NCOL || (!s && len) || !dfa_mask || !fast_mask) return KW_E_ARG;
+  const uint8_t* blob = env->e.blob.data();
+  const DevHeader* H = (const DevHeader*)blob;
+  const uint8_t* u = (const uint8_t*)s;
+  *dfa_mask = H->dfa_off[col] ? blob_chain_run(blob, H->dfa_off[col], u, len) : 0ull;
+  *fast_mask = 0;
+  if (col == COL_LV) {
+    if (!H->kv_off || !H->lit_off[COL_LK] || (!key && klen)) return 0;
+    const uint64_t km = blob_lit_lookup(blob, H->lit_off[COL_LK], (const uint8_t*)key, klen);
+    const uint32_t* idx = (const uint32_t*)(blob + H->kv_off);
+    uint64_t keybits = 0;  // value patterns constrained on this key: every bit its DFA can accept
+    if (km && idx[__builtin_ctzll(km)]) {
+      const uint32_t o = H->kv_off + idx[__builtin_ctzll(km)];
+      const DevDfa* d = (const DevDfa*)(blob + o);
+      for (uint32_t q = 0; q < d->nstates; ++q) keybits |= ((const uint64_t*)(blob + d->acc_off))[q];
+      *fast_mask = blob_dfa_run(blob, o, u, len);
+    }
+    *dfa_mask &= keybits;
+    return 1;
+  }
+  if (!H->lit_off[col]) return 0;
+  *fast_mask = blob_lit_lookup(blob, H->lit_off[col], u, len);
+  return 1;
+}
+
 int kw_batch_from_json(const char* const* docs, const size_t* lens, size_t n, int doc_kind, kw_batch** out,
                        int64_t* bad_row, char* err, size_t errlen) {
   if (!out || (n && (!docs || !lens))) return KW_E_ARG;

@@ -200,6 +200,17 @@ class EvaluationEnvironment:
         raise_for(rc, "get_policy_allowed_to_mutate")
         return bool(v.value)
 
+    def classify_check(self, col, s, key=b""):
+        """Diagnostic (kw_env_classify_check): (fast table exists, DFA-chain mask, fast-table mask)
+        of string `s` for request column `col`; `key` selects the label key for COL_LV."""
+        s = s.encode() if isinstance(s, str) else s
+        key = key.encode() if isinstance(key, str) else key
+        dm, fm = C.c_uint64(), C.c_uint64()
+        rc = self._L.kw_env_classify_check(self._h, col, key, len(key), s, len(s), C.byref(dm), C.byref(fm))
+        if rc < 0 or rc > 1:
+            raise_for(rc, "classify_check")
+        return bool(rc), dm.value, fm.value
+
     def should_always_accept_requests_made_inside_of_namespace(self, ns):
         b = ns.encode()
         return self._L.kw_env_should_always_accept_requests_made_inside_of_namespace(self._h, b, len(b)) == 1

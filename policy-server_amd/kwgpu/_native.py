@@ -83,7 +83,7 @@ EXPORTS = [
     "kw_env_policy_count", "kw_env_policy_id", "kw_env_is_group", "kw_env_get_policy_mode",
     "kw_env_get_policy_allowed_to_mutate",
     "kw_env_should_always_accept_requests_made_inside_of_namespace",
-    "kw_env_policy_initialization_error", "kw_env_validate_settings", "kw_pattern_match",
+    "kw_env_policy_initialization_error", "kw_env_validate_settings", "kw_pattern_match", "kw_env_classify_check",
     "kw_batch_from_json", "kw_batch_from_soa", "kw_batch_view", "kw_batch_to_device",
     "kw_batch_destroy", "kw_validate_batch", "kw_validate_rows", "kw_batch_verdicts",
     "kw_validate_timed", "kw_format_response", "kw_env_group_members", "kw_evaluate",
@@ -119,6 +119,7 @@ def lib():
         "kw_env_policy_initialization_error": (ip, [vp, i32, cp, sz]),
         "kw_env_validate_settings": (ip, [vp, i32, cp, sz]),
         "kw_pattern_match": (ip, [ip, cp, cp, sz]),
+        "kw_env_classify_check": (ip, [vp, ip, cp, sz, cp, sz, C.POINTER(u64), C.POINTER(u64)]),
         "kw_batch_from_json": (ip, [C.POINTER(cp), C.POINTER(sz), sz, ip, C.POINTER(vp), C.POINTER(C.c_int64), cp, sz]),
         "kw_batch_from_soa": (ip, [C.POINTER(KwSoa), C.POINTER(vp)]),
         "kw_batch_view": (ip, [vp, C.POINTER(KwSoa)]),
