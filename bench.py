@@ -127,8 +127,9 @@ def main():
                        "requests_per_gpu": args.rows, "policies": npol, "parallelism": f"dp{world} (request shards)"},
             "evaluations_per_s": value * npol,
             "kernel_ms": {"classify": tm.classify_ms, "evaluate": tm.evaluate_ms, "total": tm.total_ms},
-            "roofline": {"kernel": f"{dom}_kernel", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+            "roofline": {"kernel": "evaluate_tiled_kernel" if dom == "evaluate" else "classify_kernel",
+                         "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic(args),
                          "algorithmic_bytes_per_launch": nbytes},
             "cpu_baseline": cpu,
             "verdicts_final_allowed_fraction": frac_allowed,
@@ -138,6 +139,22 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     return result
+
+
+def traffic(args):
+    """HBM bytes per launch of the tiled kernel from the committed PMC summary (profiles/traffic.json,
+    written by scripts/pmc_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
+    of this bench, FETCH_SIZE doubled per the gfx950 calibration). None when absent or measured on a
+    different workload."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if t.get("config") != args.config or t.get("rows") != args.rows:
+        return None
+    return t.get("bytes_per_launch")
 
 
 def cpu_baseline(policies, ids, args):
