@@ -11,11 +11,10 @@ PKG := policy-server_amd
 SRC := $(PKG)/csrc
 OBJ := $(PKG)/build
 HIPDEF := -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include
-TILE ?= 1024
-CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wextra $(HIPDEF) -DKW_TILE_THREADS=$(TILE)
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -munsafe-fp-atomics -DKW_TILE_THREADS=$(TILE)
+CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wextra $(HIPDEF)
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -munsafe-fp-atomics
 
-HOST_SRCS := json automaton expr env flatten service capi
+HOST_SRCS := json automaton expr env flatten service slotplan capi
 HOST_OBJS := $(addprefix $(OBJ)/,$(addsuffix .o,$(HOST_SRCS)))
 HEADERS := $(wildcard $(SRC)/*.hpp) include/kwgpu.h
 

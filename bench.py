@@ -127,7 +127,7 @@ def main():
                        "requests_per_gpu": args.rows, "policies": npol, "parallelism": f"dp{world} (request shards)"},
             "evaluations_per_s": value * npol,
             "kernel_ms": {"classify": tm.classify_ms, "evaluate": tm.evaluate_ms, "total": tm.total_ms},
-            "roofline": {"kernel": "evaluate_tiled_kernel" if dom == "evaluate" else "classify_kernel",
+            "roofline": {"kernel": "evaluate_slots_kernel" if dom == "evaluate" else "classify_kernel",
                          "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic(args),
                          "algorithmic_bytes_per_launch": nbytes},

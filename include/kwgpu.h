@@ -215,6 +215,13 @@ int kw_batch_view(const kw_batch *b, kw_soa *view);
 int kw_batch_to_device(kw_batch *b, int device);
 void kw_batch_destroy(kw_batch *b);
 
+/* Diagnostic (test infrastructure, never called by kw_validate_*): evaluate the batch's rows
+ * against the policy list on the HOST through the same slot compiler and entity walks the device
+ * kernel runs (slots.hpp), with the column automata of the blob. Lets the CPU test suite check the
+ * slot compiler against the oracle without a GPU. out: [row][npol] verdict words. */
+int kw_debug_host_walk(const kw_env *env, const kw_batch *b, const int32_t *policies, uint32_t npol,
+                       int origin, uint32_t *out);
+
 /* ---------------------------------------------------------------------------------------------
  * The hot path: EvaluationEnvironment::validate + service::evaluate constraints, batched.
  * Evaluates every row against each of the npol policies (indices from kw_env_lookup) on the GPU;

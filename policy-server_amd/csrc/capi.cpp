@@ -17,6 +17,7 @@
 #include "env.hpp"
 #include "kernels.hpp"
 #include "service.hpp"
+#include "slotplan.hpp"
 
 using namespace kw;
 
@@ -52,10 +53,14 @@ struct DeviceBatch {
   size_t last_verdicts = 0;
   std::vector<int32_t> host_pols;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-  // device copy of the last tiled-pass TileArgs (read by the kernel from memory, not kernargs)
-  TileArgs* d_tile = nullptr;
-  TileArgs h_tile{};
-  bool tile_valid = false;
+  // device copies of the last all-pairs pass's per-chunk TileArgs and slot records (read by the
+  // kernel from memory, not kernargs); host copies detect a changed plan
+  TileArgs* d_tiles = nullptr;
+  size_t d_tiles_cap = 0;
+  std::vector<TileArgs> h_tiles;
+  uint8_t* d_slots = nullptr;
+  size_t d_slots_cap = 0;
+  std::vector<uint8_t> h_slots;
   // host-built tile descriptors + overflow list, cached for one plan geometry (desc_key)
   TileDesc* desc = nullptr;
   size_t desc_cap = 0;
@@ -65,7 +70,8 @@ struct DeviceBatch {
   uint64_t desc_key = 0;
   ~DeviceBatch() {
     if (device >= 0) (void)hipSetDevice(device);
-    (void)hipFree(d_tile);
+    (void)hipFree(d_tiles);
+    (void)hipFree(d_slots);
     (void)hipFree(desc);
     (void)hipFree(overflow);
     (void)hipFree(cols);
@@ -154,7 +160,11 @@ struct PassPlan {
   bool fused = false;
   ClassifyJobs jobs;
   EvalArgs args;
-  TileArgs tile;
+  TileArgs tile;                   // geometry shared by every chunk
+  std::vector<SlotChunk> chunks;   // all-pairs mode: column chunks
+  std::vector<TileArgs> tiles;     // one per chunk
+  std::vector<uint8_t> slot_blob;  // the chunks' slot records, concatenated
+  std::vector<uint32_t> slot_at;   // offset of each chunk's record in slot_blob
   uint32_t grid = 0;
   double classify_bytes = 0, evaluate_bytes = 0;
 };
@@ -188,7 +198,7 @@ const DeviceBatch::DCol& mask_strings(const DeviceBatch& D, int m) {
 }
 
 constexpr uint32_t kFusedTableBudget = 48 * 1024;  // DFA chains staged per workgroup
-constexpr uint32_t kTileLdsBudget = 160 * 1024 * kTileThreads / 1024;  // tiled-kernel LDS per workgroup
+constexpr uint32_t kTileLdsBudget = 160 * 1024;  // slot-kernel LDS per workgroup (gfx950: 160 KB per CU)
 
 // Build the classification jobs (two-kernel mode) and the evaluation arguments of one pass.
 int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npairs, uint32_t npol, int origin,
@@ -200,6 +210,7 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
   memset(&plan->jobs, 0, sizeof(plan->jobs));
   memset(&plan->args, 0, sizeof(plan->args));
   memset(&plan->tile, 0, sizeof(plan->tile));
+  plan->chunks.clear();
   plan->rows_mode = d_row_policy != nullptr;
   auto chain_bytes = [&](uint32_t off) -> uint32_t {
     return off ? ((const DevDfa*)(E.blob.data() + off))->chain_bytes : 0u;
@@ -335,10 +346,14 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
   plan->evaluate_bytes = plan->fused ? eb + strings : eb + masks;
   if (plan->rows_mode) return KW_OK;
 
-  // ---- tile geometry and LDS layout
+  // ---- slot chunks (all-pairs mode): one slot-kernel launch per chunk of <= 64 slots / columns
+  if (!plan->rows_mode) {
+    Status st = build_slot_chunks(E, kb->dev->host_pols.data(), npol, origin, &plan->chunks);
+    if (!st.ok()) return st.code;
+  }
+
+  // ---- tile geometry and LDS layout (slot kernel: kSlotRows requests per tile)
   TileArgs& T = plan->tile;
-  bool groups = false;
-  for (uint32_t j = 0; j < npol; ++j) groups = groups || E.pol[(size_t)D.host_pols[j]].is_group;
   auto align = [](uint32_t x) { return (x + 15u) & ~15u; };
   double cpr = B.n ? nc / n : 1, lpr = B.n ? (double)B.labels() / n : 1;
   double apr = nc ? (double)B.cap_add.n() / nc : 1, dpr = nc ? (double)B.cap_drop.n() / nc : 1;
@@ -347,21 +362,29 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
     chain_len[m] = 1;
     // image chains are walked by one item; the non-fused path stages the classify kernel's merged masks
     if (!plan->fused || !use[m] || m == M_REG || m == M_TAG || m == M_IMG || lit_of(m) || (m == M_LV && kv)) continue;
-    uint32_t n = 0;
-    for (uint32_t o = H->dfa_off[mask_col(m)]; o; o = ((const DevDfa*)(E.blob.data() + o))->next) ++n;
-    chain_len[m] = std::max<uint32_t>(1, n);
+    uint32_t c = 0;
+    for (uint32_t o = H->dfa_off[mask_col(m)]; o; o = ((const DevDfa*)(E.blob.data() + o))->next) ++c;
+    chain_len[m] = std::max<uint32_t>(1, c);
   }
-  uint32_t rows = std::max<uint32_t>(64, std::min<uint32_t>(1024, ((8u * kTileThreads / std::max<uint32_t>(npol, 1)) + 63) / 64 * 64));
-  const uint32_t ncap = (uint32_t)E.cols[COL_CAP].size(), naa = (uint32_t)E.cols[COL_AA].size(),
-                 nkey = (uint32_t)E.cols[COL_LK].size();
-  double scale = 1.5;  // capacity headroom over the batch average; tiles beyond it take the global path
+  uint32_t slot_bytes = 16, nslots = 1;
+  bool groups = false;
+  for (const SlotChunk& c : plan->chunks) {
+    slot_bytes = std::max<uint32_t>(slot_bytes, (uint32_t)c.rec.size());
+    nslots = std::max(nslots, c.nslots);
+    groups = groups || c.groups;
+  }
+  const uint32_t rows = kSlotRows;
+  const uint32_t vw_stride = nslots | 1u;  // odd stride: lanes (requests) spread over the banks
+  double scale = 1.25;  // capacity headroom over the batch average; tiles beyond it take the overflow path
   for (;;) {
     uint32_t cmax = (uint32_t)std::min(16.0 * rows + 64, scale * rows * cpr + 32);
     uint32_t kmax = (uint32_t)std::min(16.0 * rows + 64, scale * rows * cpr * std::max(apr, dpr) + 32);
     uint32_t lmax = (uint32_t)std::min(16.0 * rows + 64, scale * rows * lpr + 32);
     uint32_t off = 16;
-    uint32_t stage_at = off;
+    const uint32_t stage_at = off;
     if (plan->fused) off = align(off + table_bytes);
+    T.o_slot = off;
+    off = align(off + slot_bytes);
     T.o_rf = off;
     off = align(off + rows);
     T.o_coff = off;
@@ -382,38 +405,39 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
       T.mask_cap[m] = cnt;
       off = align(off + cnt * 8 * chain_len[m]);  // one partial slot per DFA of the column chain
     }
-    for (int m = 0; m < (int)NMASK; ++m) T.o_so[m] = T.o_sb[m] = T.sb_cap[m] = 0;
-    if (plan->fused)
-      for (int m : {M_NS, M_IMG, M_AA, M_CAPADD, M_CAPDROP, M_LK, M_LV}) {
-        const bool need = m == M_IMG ? (use[M_REG] || use[M_TAG] || use[M_IMG]) : use[m];
-        if (!need) continue;
-        const DeviceBatch::DCol& sc = mask_strings(D, m);
-        const uint32_t cnt = m == M_NS ? rows : (m == M_CAPADD || m == M_CAPDROP) ? kmax : (m == M_LK || m == M_LV) ? lmax : cmax;
-        T.o_so[m] = off;
-        off = align(off + (cnt + 1) * 4);
-        const double bpr = B.n ? (double)sc.nbytes / (double)B.n : 0.0;  // string bytes per request
-        T.sb_cap[m] = align((uint32_t)std::min(16384.0, scale * rows * bpr + 64));  // longer tiles take the global path
-        T.o_sb[m] = off;
-        off = align(off + T.sb_cap[m] + 16);  // slack: dword reads may run <= 7 bytes past a string
-      }
-    T.o_feat = off;
-    off = align(off + rows * (5 * 8 + 6 * 4));
-    T.o_pos = off;
-    off = align(off + rows * (ncap + naa + nkey) * 4);
-    T.ncap_bits = ncap;
-    T.naa_bits = naa;
-    T.nkey_bits = nkey;
+    T.o_rej = off;
+    off = align(off + rows * 8);
+    T.o_mut = off;
+    off = align(off + rows * 8);
+    T.o_byp = off;
+    off = align(off + rows);
     T.o_gstk = 0;
     if (groups) {
       T.o_gstk = off;
-      off = align(off + kMaxGroupStack * kTileThreads * 2);
+      off = align(off + kMaxGroupStack * kSlotThreads * 2);
     }
-    if (off > kTileLdsBudget && rows > 64) {
-      rows /= 2;
-      continue;
-    }
-    if (off > kTileLdsBudget && scale > 0.05) {
-      scale /= 2;
+    // union: the staged strings (P0-P1) and the violation words (P2-P3)
+    const uint32_t u0 = off;
+    uint32_t su = u0;
+    for (int m = 0; m < (int)NMASK; ++m) T.o_so[m] = T.o_sb[m] = T.sb_cap[m] = 0;
+    if (plan->fused)
+      for (int m : {M_NS, M_IMG, M_AA, M_CAPADD, M_CAPDROP, M_LK, M_LV}) {
+        const bool needm = m == M_IMG ? (use[M_REG] || use[M_TAG] || use[M_IMG]) : use[m];
+        if (!needm) continue;
+        const DeviceBatch::DCol& sc = mask_strings(D, m);
+        const uint32_t cnt = m == M_NS ? rows : (m == M_CAPADD || m == M_CAPDROP) ? kmax : (m == M_LK || m == M_LV) ? lmax : cmax;
+        T.o_so[m] = su;
+        su = align(su + (cnt + 1) * 4);
+        const double bpr = B.n ? (double)sc.nbytes / (double)B.n : 0.0;  // string bytes per request
+        T.sb_cap[m] = align((uint32_t)std::min(16384.0, scale * rows * bpr + 64));  // longer tiles take the overflow path
+        T.o_sb[m] = su;
+        su = align(su + T.sb_cap[m] + 16);  // slack: dword reads may run <= 7 bytes past a string
+      }
+    T.o_vw = u0;
+    T.vw_stride = vw_stride;
+    off = std::max(su, align(u0 + rows * vw_stride * 4));
+    if (off > kTileLdsBudget && scale > 0.1) {
+      scale *= 0.8;
       continue;
     }
     T.rows = rows;
@@ -429,7 +453,7 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
       T.s_off[m] = sc.off;
       T.s_bytes[m] = sc.bytes;
     }
-    // DFA chains staged once per workgroup (fused)
+    // column tables staged once per workgroup (fused)
     if (plan->fused) {
       uint32_t at = stage_at;
       uint32_t col_at[NCOL] = {};
@@ -460,16 +484,13 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
     }
     break;
   }
-  if (T.lds_bytes > kTileLdsBudget) return KW_E_ARG;  // npol too large for one tile row
+  if (T.lds_bytes > kTileLdsBudget) return KW_E_ARG;  // policy set too large for one tile
   if (const char* dbg = getenv("KW_TILE_DEBUG")) T.debug = (uint32_t)atoi(dbg);  // phase ablation (diagnostics)
   if (T.debug & 256u)
-    fprintf(stderr, "[kw tile] fused=%d rows=%u cmax=%u kmax=%u lmax=%u lds=%u sb=%u/%u/%u/%u/%u/%u/%u\n", (int)plan->fused,
-            T.rows, T.cmax, T.kmax, T.lmax, T.lds_bytes, T.sb_cap[M_NS], T.sb_cap[M_IMG], T.sb_cap[M_AA], T.sb_cap[M_CAPADD],
-            T.sb_cap[M_CAPDROP], T.sb_cap[M_LK], T.sb_cap[M_LV]);
+    fprintf(stderr, "[kw tile] fused=%d rows=%u cmax=%u kmax=%u lmax=%u lds=%u slot=%u chunks=%zu sb=%u/%u/%u/%u/%u/%u/%u\n",
+            (int)plan->fused, T.rows, T.cmax, T.kmax, T.lmax, T.lds_bytes, slot_bytes, plan->chunks.size(), T.sb_cap[M_NS],
+            T.sb_cap[M_IMG], T.sb_cap[M_AA], T.sb_cap[M_CAPADD], T.sb_cap[M_CAPDROP], T.sb_cap[M_LK], T.sb_cap[M_LV]);
   for (int m = 0; m < (int)NMASK; ++m) T.chain_len[m] = chain_len[m];
-  T.cap_all_mask = 0;
-  for (size_t i = 0; i < E.cols[COL_CAP].size(); ++i)
-    if (E.cols[COL_CAP][i].text == "ALL") T.cap_all_mask = 1ull << i;
   if (use[M_REG] || use[M_TAG] || use[M_IMG]) {  // one parse of the image column feeds all three
     T.s_off[M_IMG] = D.ctr_image.off;
     T.s_bytes[M_IMG] = D.ctr_image.bytes;
@@ -484,8 +505,23 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
       if (!T.s_off[sm] || !T.s_bytes[sm]) return KW_E_ARG;
     }
   }
+  // per-chunk TileArgs (slot_plan pointers are filled in at upload, run_pass)
+  plan->tiles.clear();
+  plan->slot_at.clear();
+  plan->slot_blob.clear();
+  for (const SlotChunk& c : plan->chunks) {
+    TileArgs t = T;
+    plan->slot_at.push_back((uint32_t)plan->slot_blob.size());
+    plan->slot_blob.insert(plan->slot_blob.end(), c.rec.begin(), c.rec.end());
+    t.slot_bytes = (uint32_t)c.rec.size();
+    t.col0 = c.col0;
+    t.ncols = c.ncols;
+    t.vec4 = (npol % 4u == 0 && c.col0 % 4u == 0 && c.ncols % 4u == 0) ? 1u : 0u;
+    t.o_gstk = c.groups ? T.o_gstk : 0u;
+    plan->tiles.push_back(t);
+  }
   uint64_t ntiles = (B.n + T.rows - 1) / T.rows;
-  uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(2048 / kTileThreads, (160 * 1024) / std::max<uint32_t>(T.lds_bytes, 1)));
+  uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(2048 / kSlotThreads, (160 * 1024) / std::max<uint32_t>(T.lds_bytes, 1)));
   plan->grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ntiles, 256ull * per_cu));
   return KW_OK;
 }
@@ -565,15 +601,23 @@ int run_pass(const kw_env* env, kw_batch* kb, const PassPlan& plan, bool timed) 
   if (plan.rows_mode) {
     HIPCHK(launch_evaluate_rows(plan.args, D.stream));
   } else {
-    if (!D.d_tile) HIPCHK(hipMalloc((void**)&D.d_tile, sizeof(TileArgs)));
-    if (!D.tile_valid || std::memcmp(&D.h_tile, &plan.tile, sizeof(TileArgs)) != 0) {
-      D.h_tile = plan.tile;  // pageable source: the runtime stages it before returning
-      HIPCHK(hipMemcpyAsync(D.d_tile, &D.h_tile, sizeof(TileArgs), hipMemcpyHostToDevice, D.stream));
-      D.tile_valid = true;
+    // per-chunk TileArgs + slot records, uploaded when the plan changes
+    if (int rc = ensure(&D.d_slots, &D.d_slots_cap, plan.slot_blob.size())) return rc;
+    if (int rc = ensure(&D.d_tiles, &D.d_tiles_cap, plan.tiles.size())) return rc;
+    std::vector<TileArgs> tiles = plan.tiles;
+    for (size_t k = 0; k < tiles.size(); ++k) tiles[k].slot_plan = D.d_slots + plan.slot_at[k];
+    if (D.h_slots != plan.slot_blob || D.h_tiles.size() != tiles.size() ||
+        (!tiles.empty() && std::memcmp(D.h_tiles.data(), tiles.data(), tiles.size() * sizeof(TileArgs)) != 0)) {
+      HIPCHK(hipStreamSynchronize(D.stream));  // a running pass may still read the previous plan
+      D.h_slots = plan.slot_blob;
+      D.h_tiles = tiles;
+      HIPCHK(hipMemcpy(D.d_slots, D.h_slots.data(), D.h_slots.size(), hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(D.d_tiles, D.h_tiles.data(), D.h_tiles.size() * sizeof(TileArgs), hipMemcpyHostToDevice));
     }
     if (int rc = upload_tile_descs(kb->b, &D, plan.tile)) return rc;
-    HIPCHK(launch_evaluate_tiled(plan.args, plan.tile, D.d_tile, D.desc, plan.fused, plan.grid, D.overflow,
-                                 D.n_overflow, D.stream));
+    for (size_t k = 0; k < tiles.size(); ++k)
+      HIPCHK(launch_evaluate_slots(plan.args, tiles[k], D.d_tiles + k, D.desc, plan.fused, plan.grid, D.stream));
+    if (!tiles.empty()) HIPCHK(launch_overflow(plan.args, D.d_tiles, D.overflow, D.n_overflow, D.stream));
   }
   if (timed) HIPCHK(hipEventRecord(D.ev[2], D.stream));
   return KW_OK;
@@ -806,6 +850,148 @@ int kw_env_classify_check(const kw_env* env, int col, const char* key, size_t kl
   if (!H->lit_off[col]) return 0;
   *fast_mask = blob_lit_lookup(blob, H->lit_off[col], u, len);
   return 1;
+}
+
+}  // extern "C"
+
+namespace {
+// Host restatement of the kernel's image-reference classification (kernels.hip parse_image /
+// image_part), for the diagnostic walk below.
+uint64_t host_image_part(const uint8_t* blob, uint32_t head, int k, const uint8_t* s, size_t n) {
+  const size_t NONE = (size_t)-1;
+  size_t at = NONE, slash0 = NONE, slash1 = NONE, last_colon = NONE;
+  bool dotcolon = false;
+  for (size_t q = 0; q < n; ++q) {
+    const uint8_t c = s[q];
+    if (c == '@') {
+      at = q;
+      break;
+    }
+    if (c == '/') {
+      if (slash0 == NONE) slash0 = q;
+      else if (slash1 == NONE) slash1 = q;
+    } else if (c == ':') {
+      last_colon = q;
+      if (slash0 == NONE) dotcolon = true;
+    } else if (c == '.') {
+      if (slash0 == NONE) dotcolon = true;
+    }
+  }
+  auto eq = [&](size_t e, const char* lit) { return e == strlen(lit) && memcmp(s, lit, e) == 0; };
+  const size_t name_end = at != NONE ? at : n;
+  const bool is_reg = slash0 != NONE && (dotcolon || eq(slash0, "localhost"));
+  const size_t rest_b = is_reg ? slash0 + 1 : 0;
+  const size_t colon = (last_colon != NONE && last_colon >= rest_b) ? last_colon : NONE;
+  const size_t path_end = colon != NONE ? colon : name_end;
+  const size_t fsr = is_reg ? slash1 : slash0;
+  const bool path_slash = fsr != NONE && fsr < path_end;
+  const bool is_docker = !is_reg || eq(slash0, "docker.io");
+  const bool eff_tag = colon != NONE || at == NONE;
+  std::string t;
+  auto app = [&](size_t b, size_t e) { t.append((const char*)s + b, e - b); };
+  if (k == 0) {
+    if (is_reg) app(0, slash0);
+    else t = "docker.io";
+  } else if (k == 1) {
+    if (colon != NONE) app(colon + 1, name_end);
+    else if (at == NONE) t = "latest";
+    else return 0;
+  } else {
+    if (is_reg) app(0, slash0);
+    else t = "docker.io";
+    t += '/';
+    if (is_docker && !path_slash) t += "library/";
+    app(rest_b, path_end);
+    if (eff_tag) {
+      t += ':';
+      if (colon != NONE) app(colon + 1, name_end);
+      else t += "latest";
+    }
+    if (at != NONE) app(at, n);
+  }
+  return blob_chain_run(blob, head, (const uint8_t*)t.data(), t.size());
+}
+
+struct HostSrc {
+  const Batch* b;
+  const std::vector<uint64_t>* mk[NMASK];
+  uint8_t rf(uint64_t r) const { return b->req_flags[r]; }
+  uint32_t coff(uint64_t r) const { return b->ctr_off[r]; }
+  uint32_t loff(uint64_t r) const { return b->lbl_off[r]; }
+  uint8_t cflags(uint32_t c) const { return b->ctr_flags[c]; }
+  uint32_t cadd(uint32_t c) const { return b->capadd_off[c]; }
+  uint32_t cdrop(uint32_t c) const { return b->capdrop_off[c]; }
+  template <int K>
+  uint64_t m(uint64_t i) const {
+    return mk[K] ? (*mk[K])[i] : 0ull;
+  }
+};
+}  // namespace
+
+extern "C" {
+
+int kw_debug_host_walk(const kw_env* env, const kw_batch* kb, const int32_t* policies, uint32_t npol, int origin,
+                       uint32_t* out) {
+  if (!env || !kb || (!policies && npol) || (!out && npol && kb->b.n)) return KW_E_ARG;
+  const Env& E = env->e;
+  const Batch& B = kb->b;
+  const uint8_t* blob = E.blob.data();
+  const DevHeader* H = (const DevHeader*)blob;
+  std::vector<SlotChunk> chunks;
+  Status st = build_slot_chunks(E, policies, npol, origin, &chunks);
+  if (!st.ok()) return st.code;
+  // classification of every string, with the column automata of the blob
+  std::vector<uint64_t> mv[NMASK];
+  auto chain = [&](Col c, const StrCol& sc, std::vector<uint64_t>* o) {
+    if (!H->dfa_off[c]) return false;
+    o->resize(sc.n());
+    for (size_t i = 0; i < sc.n(); ++i)
+      (*o)[i] = blob_chain_run(blob, H->dfa_off[c], sc.bytes.data() + sc.off[i], sc.off[i + 1] - sc.off[i]);
+    return true;
+  };
+  HostSrc src;
+  src.b = &B;
+  for (auto& p : src.mk) p = nullptr;
+  if (chain(COL_NS, B.ns, &mv[M_NS])) src.mk[M_NS] = &mv[M_NS];
+  if (chain(COL_CAP, B.cap_add, &mv[M_CAPADD])) src.mk[M_CAPADD] = &mv[M_CAPADD];
+  if (chain(COL_CAP, B.cap_drop, &mv[M_CAPDROP])) src.mk[M_CAPDROP] = &mv[M_CAPDROP];
+  if (chain(COL_AA, B.ctr_aa, &mv[M_AA])) src.mk[M_AA] = &mv[M_AA];
+  if (chain(COL_LK, B.lbl_key, &mv[M_LK])) src.mk[M_LK] = &mv[M_LK];
+  if (chain(COL_LV, B.lbl_val, &mv[M_LV])) src.mk[M_LV] = &mv[M_LV];
+  const Col icol[3] = {COL_REG, COL_TAG, COL_IMG};
+  const int imask[3] = {M_REG, M_TAG, M_IMG};
+  for (int k = 0; k < 3; ++k) {
+    if (!H->dfa_off[icol[k]]) continue;
+    std::vector<uint64_t>& o = mv[imask[k]];
+    o.assign(B.ctr_image.n(), 0);
+    for (size_t c = 0; c < B.ctr_image.n(); ++c)
+      if (B.ctr_flags[c] & KW_CTR_HAS_IMAGE)
+        o[c] = host_image_part(blob, H->dfa_off[icol[k]], k, B.ctr_image.bytes.data() + B.ctr_image.off[c],
+                               B.ctr_image.off[c + 1] - B.ctr_image.off[c]);
+    src.mk[imask[k]] = &o;
+  }
+  std::vector<uint32_t> vw(kSlots);
+  uint16_t gstk[kMaxGroupStack];
+  for (const SlotChunk& ch : chunks) {
+    SlotView sv;
+    sv.h = (const SlotHdr*)ch.rec.data();
+    sv.base = ch.rec.data();
+    const ColInfo* cols = sv.cols();
+    for (uint64_t r = 0; r < B.n; ++r) {
+      const uint32_t rf = B.req_flags[r];
+      const bool byp = H->bypass_bit >= 0 && !(rf & KW_REQ_RAW) && (rf & KW_REQ_HAS_NAMESPACE) && src.mk[M_NS] &&
+                       (((*src.mk[M_NS])[r] >> H->bypass_bit) & 1ull);
+      uint64_t mut = 0;
+      uint64_t rej = walk_privileged_caps(src, sv, r, vw.data(), &mut);
+      rej |= walk_apparmor_images(src, sv, r, vw.data());
+      rej |= walk_labels(src, sv, r, vw.data());
+      rej |= walk_namespace(src, sv, r, vw.data());
+      for (uint32_t j = 0; j < ch.ncols; ++j)
+        out[r * npol + ch.col0 + j] =
+            byp ? kBypassWord : column_word(cols[j], rej, mut, sv.h->init, vw.data(), blob, gstk, 1);
+    }
+  }
+  return KW_OK;
 }
 
 int kw_batch_from_json(const char* const* docs, const size_t* lens, size_t n, int doc_kind, kw_batch** out,

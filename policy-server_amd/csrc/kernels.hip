@@ -2,23 +2,20 @@
 // declarative policy class (src/evaluation/evaluation_environment.rs:546-594) fused with the
 // service::evaluate epilogue (src/api/service.rs:40-116, 160-208).
 //
-// Two kernels per validate pass:
-//  classify_kernel  — every request string that some selected policy reads (namespace, image
-//                     reference, capability names, AppArmor profile, label key / value) runs
-//                     through its column's multi-pattern DFA, one lane per string. The column DFA
-//                     (byte-class map, u16 transitions, u64 accept masks) is staged into LDS once
-//                     per workgroup; string bytes stream from HBM with 4-byte aligned loads.
-//                     Image references are parsed in-lane (registry / path / tag / digest, with
-//                     docker.io / library/ / latest normalisation fed as virtual bytes) and drive
-//                     three DFAs. Output: one u64 pattern-match mask per string.
-//  evaluate_kernel  — one lane per (request, policy) pair; lanes of a wave share a request in the
-//                     all-pairs layout, so entity loads broadcast. Each policy is a few bit tests
-//                     over the masks; groups evaluate their members eagerly and run a postfix
-//                     program that tracks rhai's short-circuit "called" set per stack entry.
-//                     The verdict word (include/kwgpu.h) carries the vanilla response and the
-//                     service-level result.
-// Integer / byte work only: no MFMA. Bound: HBM streaming of string bytes + masks + verdicts, and
-// the dependent LDS chain of the DFA walk.
+// Kernels:
+//  evaluate_slots_kernel — the all-pairs hot path (kw_validate_batch). Persistent 256-thread
+//                     workgroups, several per CU, each owning a 64-request tile at a time: stage the
+//                     tile's columns into LDS, classify every string there (literal perfect hash,
+//                     per-key value DFA, image DFA chains), walk each request's entities once with
+//                     the bit-parallel slot tables (slots.hpp: one lane per request, one wave per
+//                     family group), then write the verdict rows with coalesced 16-B stores.
+//  classify_kernel  — two-kernel form for automata too large for LDS: one lane per string, masks
+//                     to HBM; the slot kernel then stages the masks instead of the strings.
+//  overflow_kernel  — tiles whose entity counts exceed the LDS capacities, from global memory.
+//  evaluate_rows_kernel — micro-batch form (kw_validate_rows): one lane per (row, its policy).
+// The verdict word (include/kwgpu.h) carries the vanilla response and the service-level result.
+// Integer / byte work only: no MFMA. Bound: HBM streaming of request bytes in and verdict words
+// out.
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
@@ -275,10 +272,6 @@ __global__ void __launch_bounds__(kClassifyThreads) classify_kernel(const uint8_
 // Policy fields are read as whole dwords: with wave-uniform policy indices and __restrict__ kernel
 // parameters the loads become scalar (s_load, K$), the bytes are extracted with SALU ops.
 __device__ inline uint32_t pword(const DevPolicy& P, uint32_t w) { return ((const uint32_t*)&P)[w]; }
-// byte o of a dword-aligned table (group programs), as a dword load
-__device__ inline uint32_t tbyte(const uint8_t* base, uint32_t o) {
-  return (((const uint32_t*)base)[o >> 2] >> (8u * (o & 3u))) & 0xffu;
-}
 __device__ inline uint32_t pbyte(const DevPolicy& P, uint32_t off) { return (pword(P, off >> 2) >> (8u * (off & 3u))) & 0xffu; }
 // byte offsets within DevPolicy (kwdev.hpp)
 constexpr uint32_t PB_FAMILY = 0, PB_MODE = 1, PB_A2M = 2, PB_FLAGS = 3, PB_NL = 4, PB_NMAND = 10, PB_NCONSTR = 11, PB_IDX = 80;
@@ -290,9 +283,6 @@ struct FamOut {
   uint32_t reason, arg;
   bool mutated;
 };
-
-__device__ inline uint32_t pack2(uint32_t a, uint32_t b) { return (min(a, 255u) << 8) | min(b, 255u); }
-__device__ inline uint32_t pack1(uint32_t a) { return min(a, 65535u); }
 
 // Column accessors. GlobalSrc reads the HBM arrays; TileSrc reads a tile staged in LDS (indices
 // stay absolute, the accessor rebases them).
@@ -477,48 +467,10 @@ __device__ uint32_t verdict(const S& src, const EvalArgs& a, const DevHeader& H,
         FamOut fo = eval_family(src, Q, r);
         if (fo.reason == 0 && !fo.mutated) ok |= 1u << s;
       }
-      const uint8_t* prog = a.blob + H.prog_off + P.prog_off;
-      uint32_t vals = 0;  // bit stack of values; gstk holds the "called" masks
-      int sp = 0;
-      for (uint32_t pc = 0; pc < P.prog_len; ++pc) {
-        uint8_t op = prog[pc];
-        if (op <= G_CALL) {
-          uint32_t v = op == G_CONST1 ? 1u : 0u, e = 0;
-          if (op == G_CALL) {
-            uint32_t s = prog[++pc];
-            v = (ok >> s) & 1u;
-            e = 1u << s;
-          }
-          vals = (vals & ~(1u << sp)) | (v << sp);
-          gstk[sp * gstride] = (uint16_t)e;
-          ++sp;
-        } else if (op == G_NOT) {
-          vals ^= 1u << (sp - 1);
-        } else {
-          --sp;
-          uint32_t bv = (vals >> sp) & 1u, av = (vals >> (sp - 1)) & 1u;
-          uint32_t be = gstk[sp * gstride], ae = gstk[(sp - 1) * gstride];
-          uint32_t v, e;
-          if (op == G_AND) {
-            v = av & bv;
-            e = ae | (av ? be : 0u);
-          } else if (op == G_OR) {
-            v = av | bv;
-            e = ae | (av ? 0u : be);
-          } else if (op == G_EQ) {
-            v = (av == bv);
-            e = ae | be;
-          } else {
-            v = (av != bv);
-            e = ae | be;
-          }
-          vals = (vals & ~(1u << (sp - 1))) | (v << (sp - 1));
-          gstk[(sp - 1) * gstride] = (uint16_t)e;
-        }
-      }
-      if (!(vals & 1u)) {
+      uint32_t causes;
+      if (!run_group_prog(a.blob + H.prog_off + P.prog_off, P.prog_len, ok, gstk, gstride, &causes)) {
         reason = KW_R_GROUP;
-        arg = (uint32_t)gstk[0] & ~ok & 0xffffu;
+        arg = causes;
       }
     }
   } else {
@@ -527,26 +479,7 @@ __device__ uint32_t verdict(const S& src, const EvalArgs& a, const DevHeader& H,
     arg = fo.arg;
     mutated = fo.mutated;
   }
-  uint32_t v = (reason << 8) | ((arg & 0xffffu) << 16);
-  const bool allowed = reason == 0;
-  if (allowed) v |= KW_V_ALLOWED;
-  if (mutated) v |= KW_V_MUTATED;
-  // validation_response_with_constraints (service.rs:160-208) for the Validate origin
-  uint32_t fst = allowed ? KW_FST_NONE : KW_FST_VANILLA;
-  bool fallowed = allowed;
-  if (a.origin == KW_ORIGIN_VALIDATE) {
-    if (pbyte(P, PB_MODE) == KW_MODE_MONITOR) {
-      fallowed = true;
-      fst = KW_FST_NONE;
-    } else if (mutated && !pbyte(P, PB_A2M)) {
-      fallowed = false;
-      fst = KW_FST_MUTATION_REFUSED;
-    }
-  }
-  if (fallowed) v |= KW_F_ALLOWED;
-  if (mutated && fst == KW_FST_NONE && (a.origin == KW_ORIGIN_AUDIT || pbyte(P, PB_MODE) == KW_MODE_PROTECT)) v |= KW_F_PATCH;
-  v |= fst << KW_F_STATUS_SHIFT;
-  return v;
+  return finish_word(pbyte(P, PB_MODE), pbyte(P, PB_A2M), a.origin, reason, arg, mutated);
 }
 
 // Micro-batch form (kw_validate_rows): one lane per row, each row with its own policy.
@@ -563,17 +496,18 @@ __global__ void __launch_bounds__(kEvalThreads) evaluate_rows_kernel(EvalArgs a)
 }
 
 // ------------------------------------------------------------------------------------------
-// Tiled all-pairs kernel.
-// A workgroup owns a tile of `rows` consecutive requests at a time (persistent grid). It stages
-// the tile's request headers, container / capability / label offsets and the pattern masks of
-// every string the selected policies read into LDS — in FUSED mode computing the masks itself
-// with the LDS-resident DFA chains (no mask round trip through HBM), otherwise loading them from
-// the classify kernel's output. Evaluation is policy-major: a wave takes (policy, 64-row chunk)
-// items, so the policy, its family branch and its parameters are wave-uniform (scalar loads);
-// lanes are rows. Verdicts collect in an LDS tile buffer (stride npol+1 words, conflict-free) and
-// leave in the ABI's row-major layout with coalesced stores. A tile whose entity counts exceed the
-// LDS capacities is evaluated from global memory (FUSED: its masks are first classified into the
-// global mask arrays by the same workgroup).
+// All-pairs slot kernel (evaluate_slots_kernel). A workgroup owns a tile of 64 consecutive
+// requests at a time (persistent grid, several workgroups per CU so one tile's staging latency hides
+// under another's walk). Per tile:
+//  P0 stage the tile's request headers, container offsets and string bytes into LDS (coalesced
+//     16-B loads; byte ranges come from the host-built TileDesc, so there is no dependent
+//     global-load chain);
+//  P1 classify every staged string from LDS-resident tables (literal perfect hash, per-key label
+//     value DFA, image DFA chains);
+//  P2 walk each request's entities once with the slot tables (slots.hpp), lane = request, one wave
+//     per family group;
+//  P3 write the verdict rows (ABI layout, row-major) with coalesced 16-B stores.
+// A tile whose entity counts exceed the LDS capacities is left to overflow_kernel.
 // ------------------------------------------------------------------------------------------
 template <int K>
 __device__ inline uint64_t classify_one(const Chain& ch, const uint8_t* __restrict__ bytes, uint32_t b, uint32_t e) {
@@ -597,183 +531,6 @@ __device__ inline void classify_image_all(const Chain cr, const Chain ct, const 
   *mi = m2;
 }
 
-// Per-row features of a staged tile (fast path). Literal columns (capability names, AppArmor
-// profiles, label keys) match at most one pattern per string, so OR / AND reductions over a row's
-// entities answer every policy of those families exactly; the first-occurrence tables (LDS, one
-// u32 per pattern bit, written only for bits that occur) give the exact "first violation"
-// argument without rescanning the row.
-struct RowFeat {
-  uint64_t add_or;       // OR of added-capability masks
-  uint64_t dropx_and;    // AND over containers of drop masks (all ones when a container drops ALL)
-  uint64_t adddrop_and;  // AND over containers of (add | drop) masks
-  uint64_t aa_or;        // OR of AppArmor profile masks of annotated containers
-  uint64_t key_or;       // OR of label-key masks
-  uint64_t ns;           // namespace mask
-  uint32_t unk_add;      // first added capability matching no pattern: (container << 16) | index
-  uint32_t aa_unk;       // first annotated container whose profile matches no pattern
-  uint32_t priv[4];      // first privileged container, by (skip_init | skip_ephemeral << 1)
-  uint32_t rf, pad;
-};
-static_assert(sizeof(RowFeat) == 80, "RowFeat layout");
-constexpr uint32_t kNone = 0xffffffffu;
-
-struct FeatCtx {
-  const uint32_t* capf;  // [cap bits] first (c << 16 | k) of each added-capability bit
-  const uint32_t* aaf;   // [aa bits]  first container of each profile bit
-  const uint32_t* keyp;  // [key bits] label index (within the row) of each key bit
-  const uint64_t* lv;    // staged label-value masks of the tile
-  uint32_t lrow;         // index of the row's first label in lv
-};
-
-__device__ inline uint32_t min_pos(uint64_t bits, const uint32_t* table, uint32_t best) {
-  while (bits) {
-    const uint32_t b = __builtin_ctzll(bits);
-    bits &= bits - 1;
-    best = min(best, table[b]);
-  }
-  return best;
-}
-
-// Fast family evaluation from row features. TRUSTED_REPOS (glob columns, several bits per
-// string) is not reducible and is evaluated by the caller from the staged masks.
-__device__ FamOut eval_feat(const RowFeat& f, const FeatCtx& x, const DevPolicy& P) {
-  FamOut o{0, 0, false};
-  switch (pbyte(P, PB_FAMILY)) {
-    case FAM_PRIVILEGED: {
-      if (!(f.rf & KW_REQ_HAS_PODSPEC)) break;
-      const uint32_t v = ((pbyte(P, PB_FLAGS) & PF_SKIP_INIT) ? 1u : 0u) | ((pbyte(P, PB_FLAGS) & PF_SKIP_EPHEMERAL) ? 2u : 0u);
-      const uint32_t p = v == 0 ? f.priv[0] : v == 1 ? f.priv[1] : v == 2 ? f.priv[2] : f.priv[3];
-      if (p != kNone) {
-        o.reason = KW_R_PRIVILEGED;
-        o.arg = pack1(p);
-      }
-      break;
-    }
-    case FAM_NAMESPACE:
-      if (!((f.rf & KW_REQ_HAS_NAMESPACE) && pbyte(P, PB_NL + (0)) && (f.ns & P.m[0]))) o.reason = KW_R_NAMESPACE;
-      break;
-    case FAM_CAPABILITIES: {
-      if (!(f.rf & KW_REQ_HAS_PODSPEC)) break;
-      if (!(pbyte(P, PB_FLAGS) & PF_ALLOW_ALL)) {
-        const uint32_t p = min_pos(f.add_or & ~P.m[0], x.capf, f.unk_add);
-        if (p != kNone) {
-          o.reason = KW_R_CAP_NOT_ALLOWED;
-          o.arg = pack2(p >> 16, p & 0xffffu);
-          break;
-        }
-      }
-      o.mutated = (P.m[1] & ~f.dropx_and) || (P.m[2] & ~f.adddrop_and);
-      break;
-    }
-    case FAM_APPARMOR: {
-      if (!(f.rf & KW_REQ_HAS_PODSPEC)) break;
-      const uint32_t p = min_pos(f.aa_or & ~P.m[0], x.aaf, f.aa_unk);
-      if (p != kNone) {
-        o.reason = KW_R_APPARMOR;
-        o.arg = pack1(p);
-      }
-      break;
-    }
-    case FAM_LABELS: {
-      uint32_t best = min_pos(f.key_or & P.m[0], x.keyp, kNone);
-      uint32_t reason = best != kNone ? (uint32_t)KW_R_LABEL_DENIED : 0u, arg = best;
-      for (uint32_t i = 0; i < pbyte(P, PB_NCONSTR); ++i) {
-        const uint32_t k = pbyte(P, PB_IDX + (16 + i));
-        if (!((f.key_or >> k) & 1ull)) continue;
-        const uint32_t p = x.keyp[k];
-        if (p < best && !((x.lv[x.lrow + p] >> pbyte(P, PB_IDX + (32 + i))) & 1ull)) {
-          best = p;
-          reason = KW_R_LABEL_CONSTRAINT;
-          arg = pack2(p, i);
-        }
-      }
-      if (best != kNone) {
-        o.reason = reason;
-        o.arg = reason == KW_R_LABEL_DENIED ? pack1(arg) : arg;
-        break;
-      }
-      for (uint32_t i = 0; i < pbyte(P, PB_NMAND); ++i)
-        if (!((f.key_or >> pbyte(P, PB_IDX + (i))) & 1ull)) {
-          o.reason = KW_R_LABEL_MANDATORY;
-          o.arg = i;
-          break;
-        }
-      break;
-    }
-    default: break;
-  }
-  return o;
-}
-
-// Verdict word from a family result (service.rs:40-116, 160-208 epilogue).
-__device__ inline uint32_t finish(const EvalArgs& a, const DevPolicy& P, uint32_t reason, uint32_t arg, bool mutated) {
-  uint32_t v = (reason << 8) | ((arg & 0xffffu) << 16);
-  const bool allowed = reason == 0;
-  if (allowed) v |= KW_V_ALLOWED;
-  if (mutated) v |= KW_V_MUTATED;
-  uint32_t fst = allowed ? KW_FST_NONE : KW_FST_VANILLA;
-  bool fallowed = allowed;
-  if (a.origin == KW_ORIGIN_VALIDATE) {
-    if (pbyte(P, PB_MODE) == KW_MODE_MONITOR) {
-      fallowed = true;
-      fst = KW_FST_NONE;
-    } else if (mutated && !pbyte(P, PB_A2M)) {
-      fallowed = false;
-      fst = KW_FST_MUTATION_REFUSED;
-    }
-  }
-  if (fallowed) v |= KW_F_ALLOWED;
-  if (mutated && fst == KW_FST_NONE && (a.origin == KW_ORIGIN_AUDIT || pbyte(P, PB_MODE) == KW_MODE_PROTECT)) v |= KW_F_PATCH;
-  v |= fst << KW_F_STATUS_SHIFT;
-  return v;
-}
-
-// Group program over member results (see verdict()).
-__device__ inline bool run_group(const uint8_t* __restrict__ blob, const DevHeader& H, const DevPolicy& P, uint32_t ok, uint16_t* gstk,
-                                 uint32_t gstride, uint32_t* causes) {
-  const uint8_t* prog = blob + H.prog_off;  // 16-B aligned section; P.prog_off is a byte offset in it
-  uint32_t vals = 0;
-  int sp = 0;
-  for (uint32_t pc = 0; pc < P.prog_len; ++pc) {
-    const uint32_t op = tbyte(prog, P.prog_off + pc);
-    if (op <= G_CALL) {
-      uint32_t v = op == G_CONST1 ? 1u : 0u, e = 0;
-      if (op == G_CALL) {
-        uint32_t s = tbyte(prog, P.prog_off + (++pc));
-        v = (ok >> s) & 1u;
-        e = 1u << s;
-      }
-      vals = (vals & ~(1u << sp)) | (v << sp);
-      gstk[sp * gstride] = (uint16_t)e;
-      ++sp;
-    } else if (op == G_NOT) {
-      vals ^= 1u << (sp - 1);
-    } else {
-      --sp;
-      uint32_t bv = (vals >> sp) & 1u, av = (vals >> (sp - 1)) & 1u;
-      uint32_t be = gstk[sp * gstride], ae = gstk[(sp - 1) * gstride];
-      uint32_t v, e;
-      if (op == G_AND) {
-        v = av & bv;
-        e = ae | (av ? be : 0u);
-      } else if (op == G_OR) {
-        v = av | bv;
-        e = ae | (av ? 0u : be);
-      } else if (op == G_EQ) {
-        v = (av == bv);
-        e = ae | be;
-      } else {
-        v = (av != bv);
-        e = ae | be;
-      }
-      vals = (vals & ~(1u << (sp - 1))) | (v << (sp - 1));
-      gstk[(sp - 1) * gstride] = (uint16_t)e;
-    }
-  }
-  *causes = (uint32_t)gstk[0] & ~ok & 0xffffu;
-  return vals & 1u;
-}
-
 // Pointers read from TileArgs are generic to the compiler; these casts make their loads global_load
 // (not flat) in the staging loops.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -791,261 +548,179 @@ __device__ inline uint32_t tile_n(int m, uint32_t nr, uint32_t nc, uint32_t nka,
 }
 
 template <bool FUSED>
-__global__ void __launch_bounds__(kTileThreads)
-    evaluate_tiled_kernel(EvalArgs a, const TileArgs* __restrict__ tp, const TileDesc* __restrict__ desc,
-                          const uint8_t* __restrict__ blob, const int32_t* __restrict__ plist,
-                          uint32_t* __restrict__ out) {
+__global__ void __launch_bounds__(kSlotThreads)
+    evaluate_slots_kernel(EvalArgs a, const TileArgs* __restrict__ tp, const TileDesc* __restrict__ desc,
+                          const uint8_t* __restrict__ blob, uint32_t* __restrict__ out) {
   // TileArgs lives in device memory: its fields are scalar-loaded where used instead of all being
-  // hoisted from the kernarg segment into SGPRs at entry. blob / plist / out are __restrict__ so
-  // wave-uniform policy reads compile to scalar loads (nothing in this kernel stores to global
-  // memory except `out`).
+  // hoisted from the kernarg segment into SGPRs at entry.
   const TileArgs& t = *tp;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const DevHeader H = *(const DevHeader*)blob;
-  const DevPolicy* __restrict__ tpols = (const DevPolicy*)(blob + H.policy_off);
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint32_t nwaves = kTileThreads / 64;
 
+  // ---- once per workgroup: this chunk's slot plan and (FUSED) the column tables
+  {
+    const auto* src = gp((const u32x4*)t.slot_plan);
+    u32x4* dst = (u32x4*)(lds + t.o_slot);
+    for (uint32_t i = tid; i < t.slot_bytes / 16; i += kSlotThreads) dst[i] = src[i];
+  }
   Chain ch[NMASK];
   if (FUSED) {
     for (uint32_t s = 0; s < t.nstage; ++s) {
       const auto* src = gp((const u32x4*)(blob + t.stage_blob[s]));
       u32x4* dst = (u32x4*)(lds + t.stage_lds[s]);
-      for (uint32_t i = tid; i < t.stage_bytes[s] / 16; i += kTileThreads) dst[i] = src[i];
+      for (uint32_t i = tid; i < t.stage_bytes[s] / 16; i += kSlotThreads) dst[i] = src[i];
     }
 #pragma unroll
     for (int k = 0; k < (int)NMASK; ++k) {
       ch[k].head = t.dfa_head[k];
       ch[k].base = lds + t.dfa_lds[k];
     }
-    __syncthreads();
   }
+  __syncthreads();
+  SlotView sv;
+  sv.h = (const SlotHdr*)(lds + t.o_slot);
+  sv.base = lds + t.o_slot;
+
   uint8_t* l_rf = lds + t.o_rf;
   uint32_t* l_coff = (uint32_t*)(lds + t.o_coff);
   uint32_t* l_loff = (uint32_t*)(lds + t.o_loff);
   uint8_t* l_cflags = lds + t.o_cflags;
   uint32_t* l_cadd = (uint32_t*)(lds + t.o_cadd);
   uint32_t* l_cdrop = (uint32_t*)(lds + t.o_cdrop);
-  // row features, SoA (lane = row reads are bank-conflict free)
-  const uint32_t rows = t.rows;
-  uint64_t* f_add_or = (uint64_t*)(lds + t.o_feat);
-  uint64_t* f_dropx_and = f_add_or + rows;
-  uint64_t* f_adddrop_and = f_dropx_and + rows;
-  uint64_t* f_aa_or = f_adddrop_and + rows;
-  uint64_t* f_key_or = f_aa_or + rows;
-  uint32_t* f_unk_add = (uint32_t*)(f_key_or + rows);
-  uint32_t* f_aa_unk = f_unk_add + rows;
-  uint32_t* f_priv = f_aa_unk + rows;  // [4][rows]
-  uint32_t* l_pos = (uint32_t*)(lds + t.o_pos);
+  uint64_t* l_rej = (uint64_t*)(lds + t.o_rej);
+  uint64_t* l_mut = (uint64_t*)(lds + t.o_mut);
+  uint8_t* l_byp = lds + t.o_byp;
+  uint32_t* l_vw = (uint32_t*)(lds + t.o_vw);
   uint16_t* gstk = t.o_gstk ? (uint16_t*)(lds + t.o_gstk) : nullptr;
   uint64_t* l_m[NMASK];
 #pragma unroll
   for (int k = 0; k < (int)NMASK; ++k) l_m[k] = t.o_m[k] ? (uint64_t*)(lds + t.o_m[k]) : nullptr;
 
   const uint32_t npol = a.npol;
-  const uint32_t posstride = t.ncap_bits + t.naa_bits + t.nkey_bits;
-  const uint64_t ntiles = (a.nrows + t.rows - 1) / t.rows;
+  const uint64_t ntiles = (a.nrows + kSlotRows - 1) / kSlotRows;
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const uint64_t r0 = tile * t.rows;
-    const uint32_t nr = (uint32_t)min((uint64_t)t.rows, a.nrows - r0);
     const TileDesc& d = desc[tile];
+    if (!d.fits) continue;  // queued for overflow_kernel by the host (uniform: no barrier skipped unevenly)
+    const uint64_t r0 = tile * kSlotRows;
+    const uint32_t nr = (uint32_t)min((uint64_t)kSlotRows, a.nrows - r0);
     const uint32_t cb = d.cb, ce = d.ce, lb = d.lb, le = d.le;
     const uint32_t kab = d.kab, kae = d.kae, kdb = d.kdb, kde = d.kde;
-    const bool fits = d.fits != 0;  // else queued for overflow_kernel by the host
-    const uint32_t chunks = (nr + 63) / 64;
+    const uint32_t nc = ce - cb;
 
-    if (fits) {
-      // ---- A: stage the tile (headers, and for FUSED its strings); then classify the staged strings
-      //      from one flattened work list over every column and every DFA of a column's chain
-      for (uint32_t i = tid; i <= nr; i += kTileThreads) {
-        if (i < nr) {
-          l_rf[i] = a.req_flags[r0 + i];
-          f_add_or[i] = 0;
-          f_aa_or[i] = 0;
-          f_key_or[i] = 0;
-          f_dropx_and[i] = ~0ull;
-          f_adddrop_and[i] = ~0ull;
-          f_unk_add[i] = kNone;
-          f_aa_unk[i] = kNone;
-          f_priv[i] = kNone;
-          f_priv[rows + i] = kNone;
-          f_priv[2 * rows + i] = kNone;
-          f_priv[3 * rows + i] = kNone;
-        }
-        l_coff[i] = a.ctr_off[r0 + i];
-        l_loff[i] = a.lbl_off[r0 + i];
+    // ---- P0: stage request headers, container offsets and (FUSED) the tile's strings
+    for (uint32_t i = tid; i <= nr; i += kSlotThreads) {
+      if (i < nr) {
+        l_rf[i] = a.req_flags[r0 + i];
+        l_rej[i] = 0;
       }
-      for (uint32_t i = tid; i < nr * (t.ncap_bits + t.naa_bits); i += kTileThreads) {
-        const uint32_t rr = i / (t.ncap_bits + t.naa_bits), b = i - rr * (t.ncap_bits + t.naa_bits);
-        l_pos[rr * posstride + b] = kNone;
-      }
-      const uint32_t nc = ce - cb;
-      for (uint32_t i = tid; i <= nc; i += kTileThreads) {
-        if (i < nc) l_cflags[i] = a.ctr_flags[cb + i];
-        l_cadd[i] = a.capadd_off[cb + i];
-        l_cdrop[i] = a.capdrop_off[cb + i];
-      }
-      if (FUSED) {
+      l_coff[i] = a.ctr_off[r0 + i];
+      l_loff[i] = a.lbl_off[r0 + i];
+    }
+    for (uint32_t i = tid; i <= nc; i += kSlotThreads) {
+      if (i < nc) l_cflags[i] = a.ctr_flags[cb + i];
+      l_cadd[i] = a.capadd_off[cb + i];
+      l_cdrop[i] = a.capdrop_off[cb + i];
+    }
+    if (FUSED) {
 #pragma unroll
-        for (int m = 0; m < (int)NMASK; ++m) {
-          if (!t.o_sb[m]) continue;
-          const uint32_t g0 = tile_g0(m, (uint32_t)r0, cb, kab, kdb, lb);
-          const uint32_t n = tile_n(m, nr, ce - cb, kae - kab, kde - kdb, le - lb);
-          const auto* go = gp(t.s_off[m]);
-          const uint32_t sa = d.sa[m], nv = d.nv[m];
-          uint32_t* so = (uint32_t*)(lds + t.o_so[m]);
-          for (uint32_t i = tid; i <= n; i += kTileThreads) so[i] = go[g0 + i] - sa;
-          const auto* src = gp((const u32x4*)(t.s_bytes[m] + sa));
-          u32x4* dst = (u32x4*)(lds + t.o_sb[m]);
-          for (uint32_t i = tid; i < nv; i += kTileThreads) dst[i] = src[i];
-        }
-        __syncthreads();
+      for (int m = 0; m < (int)NMASK; ++m) {
+        if (!t.o_sb[m]) continue;
+        const uint32_t g0 = tile_g0(m, (uint32_t)r0, cb, kab, kdb, lb);
+        const uint32_t n = tile_n(m, nr, nc, kae - kab, kde - kdb, le - lb);
+        const auto* go = gp(t.s_off[m]);
+        const uint32_t sa = d.sa[m], nv = d.nv[m];
+        uint32_t* so = (uint32_t*)(lds + t.o_so[m]);
+        for (uint32_t i = tid; i <= n; i += kSlotThreads) so[i] = go[g0 + i] - sa;
+        const auto* src = gp((const u32x4*)(t.s_bytes[m] + sa));
+        u32x4* dst = (u32x4*)(lds + t.o_sb[m]);
+        for (uint32_t i = tid; i < nv; i += kSlotThreads) dst[i] = src[i];
       }
-      if (FUSED && !(t.debug & 1u)) {
-        // work list: (job, string, chain element); jobs in order NS, IMG, AA, CAPADD, CAPDROP, LK, LV.
-        // Per-job parameters come from the kernarg arrays (runtime-indexable without scratch).
-        const uint32_t n0 = t.o_m[M_NS] ? nr : 0u;
-        const uint32_t n1 = (t.o_m[M_REG] || t.o_m[M_TAG] || t.o_m[M_IMG]) ? nc : 0u;
-        const uint32_t n2 = t.o_m[M_AA] ? nc : 0u;
-        const uint32_t n3 = t.o_m[M_CAPADD] ? (kae - kab) * t.chain_len[M_CAPADD] : 0u;
-        const uint32_t n4 = t.o_m[M_CAPDROP] ? (kde - kdb) * t.chain_len[M_CAPDROP] : 0u;
-        const uint32_t n5 = t.o_m[M_LK] ? (le - lb) * t.chain_len[M_LK] : 0u;
-        const uint32_t n6 = (t.o_m[M_LV] && !t.kv_lds) ? (le - lb) * t.chain_len[M_LV] : 0u;  // kv: in the LK item
-        const uint32_t s1 = n0, s2 = s1 + n1, s3 = s2 + n2 * t.chain_len[M_AA], s4 = s3 + n3, s5 = s4 + n4,
-                       s6 = s5 + n5, s7 = s6 + n6;
-        for (uint32_t w = tid; w < s7; w += kTileThreads) {
-          if (w >= s1 && w < s2) {  // image reference: one parse feeds the registry, tag and image chains
-            const uint32_t i = w - s1;
-            uint64_t mr = 0, mt = 0, mi = 0;
-            if (l_cflags[i] & KW_CTR_HAS_IMAGE) {
-              const uint32_t* so = (const uint32_t*)(lds + t.o_so[M_IMG]);
-              classify_image_all(ch[M_REG], ch[M_TAG], ch[M_IMG], lds + t.o_sb[M_IMG], so[i], so[i + 1], &mr, &mt, &mi);
-            }
-            if (l_m[M_REG]) l_m[M_REG][i] = mr;
-            if (l_m[M_TAG]) l_m[M_TAG][i] = mt;
-            if (l_m[M_IMG]) l_m[M_IMG][i] = mi;
-            continue;
+    }
+    __syncthreads();
+
+    // ---- P1: classify the staged strings, one flattened work list over every column and every DFA
+    //      of a column's chain (FUSED), or load the classify kernel's masks (two-kernel form)
+    if (FUSED && !(t.debug & 1u)) {
+      // jobs in order NS, IMG, AA, CAPADD, CAPDROP, LK, LV
+      const uint32_t n0 = t.o_m[M_NS] ? nr : 0u;
+      const uint32_t n1 = (t.o_m[M_REG] || t.o_m[M_TAG] || t.o_m[M_IMG]) ? nc : 0u;
+      const uint32_t n2 = t.o_m[M_AA] ? nc : 0u;
+      const uint32_t n3 = t.o_m[M_CAPADD] ? (kae - kab) * t.chain_len[M_CAPADD] : 0u;
+      const uint32_t n4 = t.o_m[M_CAPDROP] ? (kde - kdb) * t.chain_len[M_CAPDROP] : 0u;
+      const uint32_t n5 = t.o_m[M_LK] ? (le - lb) * t.chain_len[M_LK] : 0u;
+      const uint32_t n6 = (t.o_m[M_LV] && !t.kv_lds) ? (le - lb) * t.chain_len[M_LV] : 0u;  // kv: in the LK item
+      const uint32_t s1 = n0, s2 = s1 + n1, s3 = s2 + n2 * t.chain_len[M_AA], s4 = s3 + n3, s5 = s4 + n4,
+                     s6 = s5 + n5, s7 = s6 + n6;
+      for (uint32_t w = tid; w < s7; w += kSlotThreads) {
+        if (w >= s1 && w < s2) {  // image reference: one parse feeds the registry, tag and image chains
+          const uint32_t i = w - s1;
+          uint64_t mr = 0, mt = 0, mi = 0;
+          if (l_cflags[i] & KW_CTR_HAS_IMAGE) {
+            const uint32_t* so = (const uint32_t*)(lds + t.o_so[M_IMG]);
+            classify_image_all(ch[M_REG], ch[M_TAG], ch[M_IMG], lds + t.o_sb[M_IMG], so[i], so[i + 1], &mr, &mt, &mi);
           }
-          uint32_t m, local, cap;
-          if (w < s1) { m = M_NS; local = w; cap = t.mask_cap[M_NS]; }
-          else if (w < s3) { m = M_AA; local = w - s2; cap = t.mask_cap[M_AA]; }
-          else if (w < s4) { m = M_CAPADD; local = w - s3; cap = t.mask_cap[M_CAPADD]; }
-          else if (w < s5) { m = M_CAPDROP; local = w - s4; cap = t.mask_cap[M_CAPDROP]; }
-          else if (w < s6) { m = M_LK; local = w - s5; cap = t.mask_cap[M_LK]; }
-          else { m = M_LV; local = w - s6; cap = t.mask_cap[M_LV]; }
-          const uint32_t clen = t.chain_len[m];
-          const uint32_t i = clen == 1 ? local : local / clen;
-          const uint32_t e = local - i * clen;
-          uint64_t* lm = (uint64_t*)(lds + t.o_m[m]);
-          uint64_t r = 0;
-          if (m == M_AA && !(l_cflags[i] & KW_CTR_HAS_APPARMOR)) {
-            r = 0;
-          } else if (t.lit_lds[m]) {
-            const uint32_t* so = (const uint32_t*)(lds + t.o_so[m]);
-            r = lit_lookup(lds + t.lit_lds[m], lds + t.o_sb[m], so[i], so[i + 1]);
-          } else {
-            Chain c;
-            c.head = t.dfa_head[m];
-            c.base = lds + t.dfa_lds[m];
-            uint32_t o = c.head;
-            for (uint32_t q = 0; q < e; ++q) o = chain_next(c, o);
-            const DfaView v = chain_view(c, o);
-            const uint32_t* so = (const uint32_t*)(lds + t.o_so[m]);
-            r = v.acc[feed(v, v.start, lds + t.o_sb[m], so[i], so[i + 1])];
-          }
-          lm[e * cap + i] = r;  // chain element e -> its own partial slot
-          if (m == M_LK && t.kv_lds) {  // the label's value, against the regexes of its own key only
-            uint64_t lv = 0;
-            if (r) {
-              const uint32_t rel = ((const uint32_t*)(lds + t.kv_lds))[__builtin_ctzll(r)];
-              if (rel) {
-                const DfaView v = make_view(lds + t.kv_lds + rel, nullptr, t.kv_blob + rel);
-                const uint32_t* so = (const uint32_t*)(lds + t.o_so[M_LV]);
-                lv = v.acc[feed(v, v.start, lds + t.o_sb[M_LV], so[i], so[i + 1])];
-              }
-            }
-            ((uint64_t*)(lds + t.o_m[M_LV]))[i] = lv;
-          }
+          if (l_m[M_REG]) l_m[M_REG][i] = mr;
+          if (l_m[M_TAG]) l_m[M_TAG][i] = mt;
+          if (l_m[M_IMG]) l_m[M_IMG][i] = mi;
+          continue;
         }
-      } else if (!FUSED) {
-        const uint32_t base[NMASK] = {(uint32_t)r0, cb, cb, cb, kab, kdb, cb, lb, lb};
-        const uint32_t cnt[NMASK] = {nr, nc, nc, nc, kae - kab, kde - kdb, nc, le - lb, le - lb};
+        uint32_t m, local, cap;
+        if (w < s1) { m = M_NS; local = w; cap = t.mask_cap[M_NS]; }
+        else if (w < s3) { m = M_AA; local = w - s2; cap = t.mask_cap[M_AA]; }
+        else if (w < s4) { m = M_CAPADD; local = w - s3; cap = t.mask_cap[M_CAPADD]; }
+        else if (w < s5) { m = M_CAPDROP; local = w - s4; cap = t.mask_cap[M_CAPDROP]; }
+        else if (w < s6) { m = M_LK; local = w - s5; cap = t.mask_cap[M_LK]; }
+        else { m = M_LV; local = w - s6; cap = t.mask_cap[M_LV]; }
+        const uint32_t clen = t.chain_len[m];
+        const uint32_t i = clen == 1 ? local : local / clen;
+        const uint32_t e = local - i * clen;
+        uint64_t* lm = (uint64_t*)(lds + t.o_m[m]);
+        uint64_t r = 0;
+        if (m == M_AA && !(l_cflags[i] & KW_CTR_HAS_APPARMOR)) {
+          r = 0;
+        } else if (t.lit_lds[m]) {
+          const uint32_t* so = (const uint32_t*)(lds + t.o_so[m]);
+          r = lit_lookup(lds + t.lit_lds[m], lds + t.o_sb[m], so[i], so[i + 1]);
+        } else {
+          Chain c;
+          c.head = t.dfa_head[m];
+          c.base = lds + t.dfa_lds[m];
+          uint32_t o = c.head;
+          for (uint32_t q = 0; q < e; ++q) o = chain_next(c, o);
+          const DfaView v = chain_view(c, o);
+          const uint32_t* so = (const uint32_t*)(lds + t.o_so[m]);
+          r = v.acc[feed(v, v.start, lds + t.o_sb[m], so[i], so[i + 1])];
+        }
+        lm[e * cap + i] = r;  // chain element e -> its own partial slot
+        if (m == M_LK && t.kv_lds) {  // the label's value, against the regexes of its own key only
+          uint64_t lv = 0;
+          if (r) {
+            const uint32_t rel = ((const uint32_t*)(lds + t.kv_lds))[__builtin_ctzll(r)];
+            if (rel) {
+              const DfaView v = make_view(lds + t.kv_lds + rel, nullptr, t.kv_blob + rel);
+              const uint32_t* so = (const uint32_t*)(lds + t.o_so[M_LV]);
+              lv = v.acc[feed(v, v.start, lds + t.o_sb[M_LV], so[i], so[i + 1])];
+            }
+          }
+          ((uint64_t*)(lds + t.o_m[M_LV]))[i] = lv;
+        }
+      }
+    } else if (!FUSED) {
+      const uint32_t base[NMASK] = {(uint32_t)r0, cb, cb, cb, kab, kdb, cb, lb, lb};
+      const uint32_t cnt[NMASK] = {nr, nc, nc, nc, kae - kab, kde - kdb, nc, le - lb, le - lb};
 #pragma unroll
-        for (int k = 0; k < (int)NMASK; ++k)
-          if (l_m[k])
-            for (uint32_t i = tid; i < cnt[k]; i += kTileThreads) l_m[k][i] = a.m[k][base[k] + i];
-      }
-      __syncthreads();
+      for (int k = 0; k < (int)NMASK; ++k)
+        if (l_m[k])
+          for (uint32_t i = tid; i < cnt[k]; i += kSlotThreads) l_m[k][i] = a.m[k][base[k] + i];
+    }
+    __syncthreads();
 
-      // ---- B: row features, entity-parallel (containers then labels), merged with LDS atomics
-      const uint32_t nl = le - lb;
-      for (uint32_t w = tid; w < nc + nl && !(t.debug & 2u); w += kTileThreads) {
-        if (w < nc) {
-          const uint32_t c = cb + w;
-          uint32_t lo = 0, hi = nr;  // row rr with l_coff[rr] <= c < l_coff[rr + 1]
-          while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (l_coff[mid] <= c) lo = mid;
-            else hi = mid;
-          }
-          const uint32_t rr = lo, ci = c - l_coff[rr];
-          const uint8_t fl = l_cflags[w];
-          if (fl & KW_CTR_PRIVILEGED) {
-            atomicMin(&f_priv[rr], ci);
-            if (!(fl & KW_CTR_INIT)) atomicMin(&f_priv[rows + rr], ci);
-            if (!(fl & KW_CTR_EPHEMERAL)) atomicMin(&f_priv[2 * rows + rr], ci);
-            if (!(fl & (KW_CTR_INIT | KW_CTR_EPHEMERAL))) atomicMin(&f_priv[3 * rows + rr], ci);
-          }
-          uint32_t* capf = l_pos + rr * posstride;
-          if (l_m[M_CAPADD] || l_m[M_CAPDROP]) {
-            uint64_t addm = 0, dropm = 0;
-            const uint32_t k0 = l_cadd[w], k1 = l_cadd[w + 1];
-            for (uint32_t k = k0; k < k1; ++k) {
-              const uint64_t m = l_m[M_CAPADD] ? staged_mask(l_m[M_CAPADD], k - kab, FUSED ? t.chain_len[M_CAPADD] : 1u, t.mask_cap[M_CAPADD]) : 0ull;
-              const uint32_t pos = (ci << 16) | (k - k0);
-              if (!m) atomicMin(&f_unk_add[rr], pos);
-              else atomicMin(&capf[__builtin_ctzll(m)], pos);
-              addm |= m;
-            }
-            if (l_m[M_CAPDROP])
-              for (uint32_t k = l_cdrop[w]; k < l_cdrop[w + 1]; ++k)
-                dropm |= staged_mask(l_m[M_CAPDROP], k - kdb, FUSED ? t.chain_len[M_CAPDROP] : 1u, t.mask_cap[M_CAPDROP]);
-            if (addm) atomicOr((unsigned long long*)&f_add_or[rr], (unsigned long long)addm);
-            const uint64_t dx = (dropm & t.cap_all_mask) ? ~0ull : dropm;
-            if (~dx) atomicAnd((unsigned long long*)&f_dropx_and[rr], (unsigned long long)dx);
-            if (~(addm | dropm)) atomicAnd((unsigned long long*)&f_adddrop_and[rr], (unsigned long long)(addm | dropm));
-          }
-          if (fl & KW_CTR_HAS_APPARMOR) {
-            const uint64_t m = l_m[M_AA] ? staged_mask(l_m[M_AA], w, FUSED ? t.chain_len[M_AA] : 1u, t.mask_cap[M_AA]) : 0ull;
-            if (!m) {
-              atomicMin(&f_aa_unk[rr], ci);
-            } else {
-              atomicMin(&capf[t.ncap_bits + __builtin_ctzll(m)], ci);
-              atomicOr((unsigned long long*)&f_aa_or[rr], (unsigned long long)m);
-            }
-          }
-        } else if (l_m[M_LK]) {
-          const uint32_t l = lb + (w - nc);
-          uint32_t lo = 0, hi = nr;
-          while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (l_loff[mid] <= l) lo = mid;
-            else hi = mid;
-          }
-          const uint64_t km = staged_mask(l_m[M_LK], w - nc, FUSED ? t.chain_len[M_LK] : 1u, t.mask_cap[M_LK]);
-          if (FUSED && t.chain_len[M_LV] > 1 && l_m[M_LV])  // fold the value-mask partials once, for phase C
-            l_m[M_LV][w - nc] = staged_mask(l_m[M_LV], w - nc, FUSED ? t.chain_len[M_LV] : 1u, t.mask_cap[M_LV]);
-          if (km) {
-            l_pos[lo * posstride + t.ncap_bits + t.naa_bits + __builtin_ctzll(km)] = l - l_loff[lo];
-            atomicOr((unsigned long long*)&f_key_or[lo], (unsigned long long)km);
-          }
-        }
-      }
-      __syncthreads();
-
-      // ---- C: items = (4 policies, 64-row chunk); policies wave-uniform, lanes are rows
+    // ---- P2: walk. One lane per request; each wave owns a family group (disjoint slots), so the
+    //      violation words of a request never collide; rejected masks merge with ds_or_b64.
+    if (lane < nr) {
       TileSrc src;
       src.rf_ = l_rf;
       src.coff_ = l_coff;
@@ -1054,92 +729,73 @@ __global__ void __launch_bounds__(kTileThreads)
       src.cdrop_ = l_cdrop;
       src.cflags_ = l_cflags;
 #pragma unroll
-      for (int k = 0; k < (int)NMASK; ++k) src.m_[k] = l_m[k];
+      for (int k = 0; k < (int)NMASK; ++k) {
+        src.m_[k] = l_m[k];
+        src.clen_[k] = FUSED ? t.chain_len[k] : 1u;
+        src.cap_[k] = t.mask_cap[k];
+      }
       src.r0 = r0;
       src.cb = cb;
       src.lb = lb;
       src.kab = kab;
       src.kdb = kdb;
-#pragma unroll
-      for (int k = 0; k < (int)NMASK; ++k) {
-        src.clen_[k] = FUSED ? t.chain_len[k] : 1u;
-        src.cap_[k] = t.mask_cap[k];
+      const uint64_t r = r0 + lane;
+      uint32_t* vw = l_vw + lane * t.vw_stride;
+      const bool run = !(t.debug & 2u);
+      uint64_t rej = 0;
+      if (wave == 0) {
+        uint64_t mut = 0;
+        if (run) rej = walk_privileged_caps(src, sv, r, vw, &mut);
+        l_mut[lane] = mut;
+      } else if (wave == 1) {
+        if (run) rej = walk_apparmor_images(src, sv, r, vw);
+      } else if (wave == 2) {
+        if (run) rej = walk_labels(src, sv, r, vw);
+      } else {
+        if (run) rej = walk_namespace(src, sv, r, vw);
+        // namespace bypass (service.rs:40-71): AdmissionRequest in the always-accept namespace
+        const uint32_t rf = l_rf[lane];
+        l_byp[lane] = H.bypass_bit >= 0 && !(rf & KW_REQ_RAW) && (rf & KW_REQ_HAS_NAMESPACE) &&
+                      ((src.template m<M_NS>(r) >> H.bypass_bit) & 1ull);
       }
-      const uint32_t ngroups = (npol + 3) / 4;
-      for (uint32_t item = wave; item < ngroups * chunks && !(t.debug & 4u); item += nwaves) {
-        const uint32_t g = __builtin_amdgcn_readfirstlane(item / chunks);
-        const uint32_t rr = (item - g * chunks) * 64 + lane;
-        if (rr >= nr) continue;
-        RowFeat f;
-        f.add_or = f_add_or[rr];
-        f.dropx_and = f_dropx_and[rr];
-        f.adddrop_and = f_adddrop_and[rr];
-        f.aa_or = f_aa_or[rr];
-        f.key_or = f_key_or[rr];
-        f.ns = l_m[M_NS] ? staged_mask(l_m[M_NS], rr, FUSED ? t.chain_len[M_NS] : 1u, t.mask_cap[M_NS]) : 0ull;
-        f.unk_add = f_unk_add[rr];
-        f.aa_unk = f_aa_unk[rr];
-        f.priv[0] = f_priv[rr];
-        f.priv[1] = f_priv[rows + rr];
-        f.priv[2] = f_priv[2 * rows + rr];
-        f.priv[3] = f_priv[3 * rows + rr];
-        f.rf = l_rf[rr];
-        FeatCtx x;
-        x.capf = l_pos + rr * posstride;
-        x.aaf = x.capf + t.ncap_bits;
-        x.keyp = x.aaf + t.naa_bits;
-        x.lv = l_m[M_LV];
-        x.lrow = l_loff[rr] - lb;
-        const bool bypass =
-            H.bypass_bit >= 0 && !(f.rf & KW_REQ_RAW) && (f.rf & KW_REQ_HAS_NAMESPACE) && ((f.ns >> H.bypass_bit) & 1ull);
-        uint32_t vv[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (uint32_t jj = 0; jj < 4; ++jj) {
-          const uint32_t j = g * 4 + jj;
-          if (j >= npol) break;
-          const DevPolicy& P = tpols[plist[j]];
-          uint32_t v;
-          if (bypass) {
-            v = KW_V_ALLOWED | KW_F_ALLOWED | KW_BYPASS;
-          } else if (pbyte(P, PB_FLAGS) & PF_INIT_ERROR) {
-            v = ((uint32_t)KW_FST_INIT_ERROR << KW_F_STATUS_SHIFT) | ((uint32_t)KW_R_INIT_ERROR << 8);
-          } else if (pbyte(P, PB_FAMILY) == FAM_GROUP) {
-            uint32_t reason = 0, arg = 0;
-            if (pbyte(P, PB_FLAGS) & PF_EXPR_ERROR) {
-              reason = KW_R_GROUP_EXPR;
-            } else {
-              const int32_t* mem = (const int32_t*)(blob + H.member_off) + P.member_off;
-              uint32_t ok = 0;
-              for (uint32_t sl = 0; sl < P.nmembers; ++sl) {
-                const DevPolicy& Q = tpols[mem[sl]];
-                if (pbyte(Q, PB_FLAGS) & PF_INIT_ERROR) continue;
-                FamOut fo = pbyte(Q, PB_FAMILY) == FAM_TRUSTED_REPOS ? eval_family(src, Q, r0 + rr) : eval_feat(f, x, Q);
-                if (fo.reason == 0 && !fo.mutated) ok |= 1u << sl;
-              }
-              uint32_t causes;
-              if (!run_group(blob, H, P, ok, gstk + tid, kTileThreads, &causes)) {
-                reason = KW_R_GROUP;
-                arg = causes;
-              }
-            }
-            v = finish(a, P, reason, arg, false);
+      if (rej) atomicOr((unsigned long long*)&l_rej[lane], (unsigned long long)rej);
+    }
+    __syncthreads();
+
+    // ---- P3: verdict rows. vec4: items = (request, 4 columns); 16 lanes cover a 256-B row and a
+    //      wave writes 1 KiB contiguous. Otherwise one column per item.
+    if (!(t.debug & 4u)) {
+      const ColInfo* cols = sv.cols();
+      const uint64_t init = sv.h->init;
+      uint16_t* gs = gstk ? gstk + tid : nullptr;
+      if (t.vec4) {
+        const uint32_t G = t.ncols >> 2;
+        for (uint32_t it = tid; it < nr * G; it += kSlotThreads) {
+          const uint32_t rr = it / G, g = it - rr * G;
+          uint4 w;
+          if (l_byp[rr]) {
+            w = make_uint4(kBypassWord, kBypassWord, kBypassWord, kBypassWord);
           } else {
-            FamOut fo = pbyte(P, PB_FAMILY) == FAM_TRUSTED_REPOS ? eval_family(src, P, r0 + rr) : eval_feat(f, x, P);
-            v = finish(a, P, fo.reason, fo.arg, fo.mutated);
+            const uint64_t rej = l_rej[rr], mut = l_mut[rr];
+            const uint32_t* vw = l_vw + rr * t.vw_stride;
+            w.x = column_word(cols[4 * g + 0], rej, mut, init, vw, blob, gs, kSlotThreads);
+            w.y = column_word(cols[4 * g + 1], rej, mut, init, vw, blob, gs, kSlotThreads);
+            w.z = column_word(cols[4 * g + 2], rej, mut, init, vw, blob, gs, kSlotThreads);
+            w.w = column_word(cols[4 * g + 3], rej, mut, init, vw, blob, gs, kSlotThreads);
           }
-          vv[jj] = v;
+          *(uint4*)(out + (r0 + rr) * npol + t.col0 + 4 * g) = w;
         }
-        uint32_t* dst = out + (r0 + rr) * npol + g * 4;
-        if ((npol & 3u) == 0) {
-          *(uint4*)dst = make_uint4(vv[0], vv[1], vv[2], vv[3]);
-        } else {
-#pragma unroll
-          for (uint32_t jj = 0; jj < 4; ++jj)
-            if (g * 4 + jj < npol) dst[jj] = vv[jj];
+      } else {
+        const uint32_t G = t.ncols;
+        for (uint32_t it = tid; it < nr * G; it += kSlotThreads) {
+          const uint32_t rr = it / G, g = it - rr * G;
+          uint32_t w = kBypassWord;
+          if (!l_byp[rr]) w = column_word(cols[g], l_rej[rr], l_mut[rr], init, l_vw + rr * t.vw_stride, blob, gs, kSlotThreads);
+          out[(r0 + rr) * npol + t.col0 + g] = w;
         }
       }
     }
-    __syncthreads();  // the next tile restages LDS
+    __syncthreads();  // the next tile restages LDS (its strings alias this tile's violation words)
   }
 }
 
@@ -1240,27 +896,30 @@ hipError_t launch_evaluate_rows(const EvalArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_evaluate_tiled(const EvalArgs& a, const TileArgs& t, const TileArgs* d_t, const TileDesc* d_desc,
-                                 bool fused, uint32_t grid, const uint32_t* d_overflow, uint32_t n_overflow,
-                                 hipStream_t s) {
-  if (a.nrows == 0 || a.npol == 0) return hipSuccess;
+hipError_t launch_evaluate_slots(const EvalArgs& a, const TileArgs& t, const TileArgs* d_t, const TileDesc* d_desc,
+                                 bool fused, uint32_t grid, hipStream_t s) {
+  if (a.nrows == 0 || t.ncols == 0) return hipSuccess;
   static bool attr_set = false;  // allow > 64 KB of dynamic LDS per workgroup (gfx950: 160 KB per CU)
   if (!attr_set) {
-    hipError_t e1 = hipFuncSetAttribute((const void*)evaluate_tiled_kernel<true>,
+    hipError_t e1 = hipFuncSetAttribute((const void*)evaluate_slots_kernel<true>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipError_t e2 = hipFuncSetAttribute((const void*)evaluate_tiled_kernel<false>,
+    hipError_t e2 = hipFuncSetAttribute((const void*)evaluate_slots_kernel<false>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e1 != hipSuccess || e2 != hipSuccess) return e1 != hipSuccess ? e1 : e2;
     attr_set = true;
   }
   if (fused)
-    hipLaunchKernelGGL(evaluate_tiled_kernel<true>, dim3(grid), dim3(kTileThreads), t.lds_bytes, s, a, d_t, d_desc,
-                       a.blob, a.pols, a.out);
+    hipLaunchKernelGGL(evaluate_slots_kernel<true>, dim3(grid), dim3(kSlotThreads), t.lds_bytes, s, a, d_t, d_desc,
+                       a.blob, a.out);
   else
-    hipLaunchKernelGGL(evaluate_tiled_kernel<false>, dim3(grid), dim3(kTileThreads), t.lds_bytes, s, a, d_t, d_desc,
-                       a.blob, a.pols, a.out);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess || n_overflow == 0) return e;
+    hipLaunchKernelGGL(evaluate_slots_kernel<false>, dim3(grid), dim3(kSlotThreads), t.lds_bytes, s, a, d_t, d_desc,
+                       a.blob, a.out);
+  return hipGetLastError();
+}
+
+hipError_t launch_overflow(const EvalArgs& a, const TileArgs* d_t, const uint32_t* d_overflow, uint32_t n_overflow,
+                           hipStream_t s) {
+  if (n_overflow == 0 || a.nrows == 0 || a.npol == 0) return hipSuccess;
   hipLaunchKernelGGL(overflow_kernel, dim3(std::min<uint32_t>(n_overflow, 512)), dim3(kOverflowThreads), 0, s, a, d_t,
                      d_overflow);
   return hipGetLastError();

@@ -5,11 +5,9 @@
 #include <cstdint>
 
 #include "kwdev.hpp"
+#include "slots.hpp"
 
 namespace kw {
-
-// Which mask array a classification job writes (one u64 per string).
-enum MaskArr : uint32_t { M_NS = 0, M_REG, M_TAG, M_IMG, M_CAPADD, M_CAPDROP, M_AA, M_LK, M_LV, NMASK };
 
 struct ClassifyJob {
   const uint32_t* off;   // string offsets (n+1)
@@ -53,27 +51,27 @@ struct EvalArgs {
   uint32_t* out;
 };
 
-#ifndef KW_TILE_THREADS
-#define KW_TILE_THREADS 1024
-#endif
-// 1024: one workgroup per CU (16 waves share one LDS copy of the tables, 160 KB);
-// 512: two workgroups per CU (80 KB each) whose barriers interleave
-constexpr int kTileThreads = KW_TILE_THREADS;
+// Slot kernel geometry: one tile = 64 requests (one lane per request in the walk), 256 threads.
+constexpr uint32_t kSlotRows = 64;
+constexpr uint32_t kSlotThreads = 256;
 
-// Tiled all-pairs evaluation (kernels.hip evaluate_tiled_kernel): LDS layout and capacities.
+// All-pairs evaluation (kernels.hip evaluate_slots_kernel): LDS layout, capacities and the
+// column chunk one launch writes. Lives in device memory (one per chunk); read with scalar loads.
 struct TileArgs {
-  uint32_t rows;                  // requests per tile
+  uint32_t rows;                  // requests per tile (kSlotRows)
   uint32_t cmax, kmax, lmax;      // container / capability / label capacity of a staged tile
   uint32_t o_rf, o_coff, o_loff, o_cflags, o_cadd, o_cdrop, o_gstk;  // LDS byte offsets
   uint32_t o_m[NMASK];            // LDS byte offset of each staged mask array, 0 = not read
-  uint32_t o_feat, o_pos;         // per-row features (RowFeat) and first-occurrence tables
-  uint32_t ncap_bits, naa_bits, nkey_bits;  // pattern counts of the literal columns
-  uint64_t cap_all_mask;          // COL_CAP bit of the "ALL" capability (0 if none)
+  uint32_t o_rej, o_mut, o_byp;   // per-request walk results: rejected / mutated slots, bypass flag
+  uint32_t o_vw, vw_stride;       // violation words [rows][vw_stride] (aliases the staged strings)
+  uint32_t o_slot, slot_bytes;    // staged SlotHdr record of this chunk
+  uint32_t col0, ncols, vec4;     // output columns [col0, col0 + ncols); vec4: 16-B verdict stores
+  const uint8_t* slot_plan;       // device copy of this chunk's SlotHdr record
   uint32_t chain_len[NMASK];      // DFAs in the chain of each mask's column (1 when absent)
   uint32_t mask_cap[NMASK];       // entries of each staged mask array
-  uint32_t debug;                 // diagnostics: bit0 skip DFA, bit1 skip row features, bit2 skip evaluation
+  uint32_t debug;                 // diagnostics: bit0 skip classification, bit1 skip walk, bit2 skip output
   uint32_t lds_bytes;
-  // FUSED: DFA chains staged once per workgroup, and the string columns they classify
+  // FUSED: column tables (literal hash, DFA chains) staged once per workgroup
   uint32_t nstage;
   uint32_t stage_blob[NCOL], stage_lds[NCOL], stage_bytes[NCOL];
   uint32_t dfa_head[NMASK];       // blob offset of the chain used for mask k (0 = none)
@@ -89,7 +87,7 @@ struct TileArgs {
 
 hipError_t launch_classify(const uint8_t* d_blob, const ClassifyJobs& jobs, hipStream_t s);
 hipError_t launch_evaluate_rows(const EvalArgs& a, hipStream_t s);
-// t: host copy (launch geometry); d_t: the same TileArgs resident in device memory (read by the kernel)
+
 // Per-tile geometry, precomputed on the host from the batch's offsets (one s_load burst per tile
 // instead of a chain of dependent global loads): entity ranges, the 16-B aligned byte range of each
 // staged string column, and whether the tile fits the LDS capacities.
@@ -102,10 +100,13 @@ struct alignas(16) TileDesc {
 };
 static_assert(sizeof(TileDesc) == 128, "TileDesc layout");
 
-// d_overflow: [count, tile indices...] of the tiles that do not fit (host-built with the
-// descriptors); a second launch evaluates them when n_overflow > 0
-hipError_t launch_evaluate_tiled(const EvalArgs& a, const TileArgs& t, const TileArgs* d_t, const TileDesc* d_desc,
-                                 bool fused, uint32_t grid, const uint32_t* d_overflow, uint32_t n_overflow,
-                                 hipStream_t s);
+// One launch of the slot kernel for one column chunk. t: host copy (launch geometry); d_t: the
+// same TileArgs resident in device memory (read by the kernel).
+hipError_t launch_evaluate_slots(const EvalArgs& a, const TileArgs& t, const TileArgs* d_t, const TileDesc* d_desc,
+                                 bool fused, uint32_t grid, hipStream_t s);
+// Tiles that do not fit the LDS capacities (d_overflow: [count, tile indices...], host-built with
+// the descriptors), evaluated from global memory for every column.
+hipError_t launch_overflow(const EvalArgs& a, const TileArgs* d_t, const uint32_t* d_overflow, uint32_t n_overflow,
+                           hipStream_t s);
 
 }  // namespace kw

@@ -323,6 +323,17 @@ class Batch:
         raise_for(rc, "kw_batch_verdicts failed")
         return out
 
+    def debug_host_walk(self, env, policies, origin=VALIDATE):
+        """Diagnostic (tests only): the device kernel's slot compiler + entity walks run on the host
+        (kw_debug_host_walk). Never part of the validate path."""
+        import numpy as np
+        arr = (C.c_int32 * len(policies))(*[env._idx(p) for p in policies])
+        out = np.zeros(self.n * len(policies), dtype=np.uint32)
+        rc = self._L.kw_debug_host_walk(env._h, self._h, arr, len(policies), origin,
+                                        out.ctypes.data_as(C.POINTER(C.c_uint32)))
+        raise_for(rc, "kw_debug_host_walk failed")
+        return out
+
     def timed(self, env, policies, origin=VALIDATE, warmup=3, reps=10):
         arr = (C.c_int32 * len(policies))(*[env._idx(p) for p in policies])
         t = KwTiming()

@@ -10,7 +10,7 @@ STEPS=${STEPS:-tests,smoke,bench,prof}
 stop_on_fault() { local rc=$1 what=$2; echo "[gpu_run] $what exit $rc"; if [ "$rc" -ge 124 ] || [ "$rc" -eq 134 ] || [ "$rc" -eq 139 ]; then echo "[gpu_run] stopping after $what"; exit "$rc"; fi; }
 rocm-smi --showproductname > gpurun_out/${TAG}_smi.txt 2>&1 || true
 if [[ $STEPS == *tests* ]]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/${TAG}_gpu_tests.log 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/${TAG}_gpu_tests.log 2>&1
   stop_on_fault $? tests
 fi
 if [[ $STEPS == *smoke* ]]; then
@@ -18,7 +18,7 @@ if [[ $STEPS == *smoke* ]]; then
   stop_on_fault $? smoke
 fi
 if [[ $STEPS == *bench* ]]; then
-  timeout -k 10 600 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err
+  KW_TILE_DEBUG=${KW_TILE_DEBUG:-0} timeout -k 10 600 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err
   stop_on_fault $? bench
 fi
 if [[ $STEPS == *prof* ]]; then

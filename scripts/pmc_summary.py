@@ -5,7 +5,7 @@ import sys
 from collections import defaultdict
 
 
-def summarise(d, match="evaluate_tiled"):
+def summarise(d, match="evaluate_slots"):
     vals = defaultdict(list)
     dur = {}
     for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
@@ -27,7 +27,7 @@ def write_traffic(fetch_dir, write_dir, out, config="c4_64", rows=1_000_000, tag
     f, w = summarise(fetch_dir), summarise(write_dir)
     fetch = 2.0 * f["FETCH_SIZE"] * 1024.0
     write = w["WRITE_SIZE"] * 1024.0
-    doc = {"round": tag, "config": config, "rows": rows, "kernel": "evaluate_tiled_kernel",
+    doc = {"round": tag, "config": config, "rows": rows, "kernel": "evaluate_slots_kernel",
            "fetch_bytes": fetch, "write_bytes": write, "bytes_per_launch": fetch + write,
            "source": f"rocprofv3 --pmc FETCH_SIZE ({fetch_dir}) and WRITE_SIZE ({write_dir}), separate passes; "
                      "FETCH_SIZE x2 (gfx950 calibration)"}

@@ -1,0 +1,86 @@
+"""CPU: the slot compiler (slotplan.cpp) and the bit-parallel entity walks (slots.hpp) that the
+device's evaluate_slots_kernel runs agree with the oracle, bit-exact, on every configuration.
+
+kw_debug_host_walk runs the same walk code on the host with the blob's column automata. It is a
+diagnostic of the slot compiler only (the product path is the GPU: kw_validate_* never calls it);
+the GPU parity tests (test_parity_gpu.py) check the kernel itself against the oracle.
+Covers: every family, monitor mode, allowedToMutate, groups with short-circuit causes, init errors,
+the namespace bypass, raw requests, both origins, policy lists with repeats and > 64 slots (several
+column chunks), and the edge documents of the GPU edge test.
+"""
+import numpy as np
+import pytest
+
+import kwgpu as K
+import oracle as O
+from helpers import config, diff_verdicts
+
+NS = "kubewarden"
+CASES = [("parity", 0, 3000), ("c1_namespace", 1, 2000), ("c2_trusted", 2, 3000), ("c3_group", 3, 3000),
+         ("c4_64", 4, 1500), ("c5_mixed", 5, 800)]
+
+
+def _envs(name):
+    doc = config(name)
+    env = K.EvaluationEnvironment(doc, continue_on_errors=True, always_accept_namespace=NS)
+    oe = O.OracleEnv(doc, continue_on_errors=True, always_accept_namespace=NS)
+    return env, oe
+
+
+@pytest.mark.parametrize("origin", [K.VALIDATE, K.AUDIT])
+@pytest.mark.parametrize("name,scfg,rows", CASES)
+def test_host_walk_matches_oracle(name, scfg, rows, origin):
+    env, oe = _envs(name)
+    ids = env.policy_ids()
+    syn = K.SynthBatch(scfg, rows, seed=500 + scfg)
+    b = syn.batch()
+    got = b.debug_host_walk(env, ids, origin)
+    want = oe.eval(syn.soa(), ids, origin)
+    assert np.array_equal(got, want), diff_verdicts(got, want, len(ids), ids)
+
+
+def test_chunked_policy_lists():
+    """Repeated columns, groups split across chunk boundaries, > 64 slots and unaligned chunks."""
+    env, oe = _envs("parity")
+    ids = env.policy_ids()
+    rng = np.random.default_rng(7)
+    cols = [ids[int(i)] for i in rng.integers(0, len(ids), 150)]
+    syn = K.SynthBatch(0, 700, seed=9)
+    b = syn.batch()
+    got = b.debug_host_walk(env, cols)
+    want = oe.eval(syn.soa(), cols)
+    assert np.array_equal(got, want), diff_verdicts(got, want, len(cols), cols)
+    c4, o4 = _envs("c4_64")
+    ids4 = c4.policy_ids()
+    cols = ids4 + ids4[:37]  # 101 columns: one full chunk and one unaligned
+    syn = K.SynthBatch(4, 500, seed=10)
+    got = syn.batch().debug_host_walk(c4, cols)
+    want = o4.eval(syn.soa(), cols)
+    assert np.array_equal(got, want), diff_verdicts(got, want, len(cols), cols)
+
+
+def test_edge_documents():
+    env, oe = _envs("parity")
+    ids = env.policy_ids()
+    ctrs = [{"name": f"c{i}", "image": f"quay.io/x/y{i}:latest",
+             "securityContext": {"privileged": i == 99, "capabilities": {"add": ["CHOWN"] * (i % 3), "drop": ["ALL"]}}}
+            for i in range(100)]
+    docs = [
+        {"request": {"uid": "a", "kind": {"group": "", "version": "v1", "kind": "Pod"},
+                     "resource": {"group": "", "version": "v1", "resource": "pods"}, "operation": "CREATE",
+                     "userInfo": {}, "object": {"kind": "Pod", "metadata": {"labels": {"app": "x" * 500, "debug": "1"}},
+                                                "spec": {"containers": ctrs}}}},
+        {"request": {"uid": "b", "kind": {"group": "", "version": "v1", "kind": "Pod"},
+                     "resource": {"group": "", "version": "v1", "resource": "pods"}, "operation": "DELETE",
+                     "userInfo": {}, "object": None}},
+        {"request": {"uid": "c", "kind": {"group": "", "version": "v1", "kind": "Pod"}, "namespace": NS,
+                     "resource": {"group": "", "version": "v1", "resource": "pods"}, "operation": "CREATE", "userInfo": {}, "object": {"kind": "Pod", "spec": {"containers": []}}}},
+    ]
+    b = K.Batch.from_json(docs)
+    got = b.debug_host_walk(env, ids)
+    want = oe.eval(b.view(), ids)
+    assert np.array_equal(got, want), diff_verdicts(got, want, len(ids), ids)
+    raw = K.Batch.from_json(['{"request": {"user": "tonio", "namespace": "kubewarden"}}', '{"request": null}'], raw=True)
+    got = raw.debug_host_walk(env, ids)
+    want = oe.eval(raw.view(), ids)
+    assert np.array_equal(got, want), diff_verdicts(got, want, len(ids), ids)
