@@ -27,6 +27,12 @@ struct kw_env {
 
 namespace kw {
 
+// Per-tile entity counts and staged byte ranges of a batch, reduced to a high quantile (tile_stats).
+struct TileStats {
+  uint32_t ctr = 0, lbl = 0, kadd = 0, kdrop = 0;
+  uint32_t bytes[NMASK] = {};
+};
+
 // Device copy of a batch: one allocation for the input columns, lazily sized mask / verdict /
 // policy-list buffers, a private stream and timing events.
 struct DeviceBatch {
@@ -68,6 +74,9 @@ struct DeviceBatch {
   size_t overflow_cap = 0;
   uint32_t n_overflow = 0;
   uint64_t desc_key = 0;
+  // slot-kernel tile capacities of this batch (plan_pass)
+  bool stats_valid = false;
+  TileStats stats;
   ~DeviceBatch() {
     if (device >= 0) (void)hipSetDevice(device);
     (void)hipFree(d_tiles);
@@ -199,6 +208,44 @@ const DeviceBatch::DCol& mask_strings(const DeviceBatch& D, int m) {
 
 constexpr uint32_t kFusedTableBudget = 48 * 1024;  // DFA chains staged per workgroup
 constexpr uint32_t kTileLdsBudget = 160 * 1024;  // slot-kernel LDS per workgroup (gfx950: 160 KB per CU)
+
+// Per-tile entity counts and staged byte ranges of a batch (kSlotRows-request tiles), reduced to a
+// high quantile: the LDS capacities of the slot kernel. Tiles above them (the tail) take the
+// overflow path. Computed once per resident batch.
+
+const StrCol& host_strings(const Batch& B, int m);
+
+TileStats tile_stats(const Batch& B, uint32_t rows) {
+  TileStats st;
+  const uint64_t ntiles = (B.n + rows - 1) / rows;
+  if (!ntiles) return st;
+  std::vector<uint32_t> v(ntiles);
+  const uint64_t q = ntiles < 2000 ? ntiles - 1 : (uint64_t)(0.9995 * (double)(ntiles - 1));
+  auto quant = [&](auto f) {
+    for (uint64_t t = 0; t < ntiles; ++t) v[t] = f(t * rows, std::min<uint64_t>(B.n, (t + 1) * rows));
+    std::nth_element(v.begin(), v.begin() + (long)q, v.end());
+    return v[q];
+  };
+  st.ctr = quant([&](uint64_t r0, uint64_t r1) { return B.ctr_off[r1] - B.ctr_off[r0]; });
+  st.lbl = quant([&](uint64_t r0, uint64_t r1) { return B.lbl_off[r1] - B.lbl_off[r0]; });
+  st.kadd = quant([&](uint64_t r0, uint64_t r1) { return B.capadd_off[B.ctr_off[r1]] - B.capadd_off[B.ctr_off[r0]]; });
+  st.kdrop = quant([&](uint64_t r0, uint64_t r1) { return B.capdrop_off[B.ctr_off[r1]] - B.capdrop_off[B.ctr_off[r0]]; });
+  for (int m : {M_NS, M_IMG, M_AA, M_CAPADD, M_CAPDROP, M_LK, M_LV}) {
+    const StrCol& c = host_strings(B, m);
+    st.bytes[m] = quant([&](uint64_t r0, uint64_t r1) {
+      uint64_t g0, g1;
+      switch (m) {
+        case M_NS: g0 = r0; g1 = r1; break;
+        case M_CAPADD: g0 = B.capadd_off[B.ctr_off[r0]]; g1 = B.capadd_off[B.ctr_off[r1]]; break;
+        case M_CAPDROP: g0 = B.capdrop_off[B.ctr_off[r0]]; g1 = B.capdrop_off[B.ctr_off[r1]]; break;
+        case M_LK: case M_LV: g0 = B.lbl_off[r0]; g1 = B.lbl_off[r1]; break;
+        default: g0 = B.ctr_off[r0]; g1 = B.ctr_off[r1]; break;
+      }
+      return ((c.off[g1] + 15u) & ~15u) - (c.off[g0] & ~15u);
+    });
+  }
+  return st;
+}
 
 // Build the classification jobs (two-kernel mode) and the evaluation arguments of one pass.
 int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npairs, uint32_t npol, int origin,
@@ -355,8 +402,11 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
   // ---- tile geometry and LDS layout (slot kernel: kSlotRows requests per tile)
   TileArgs& T = plan->tile;
   auto align = [](uint32_t x) { return (x + 15u) & ~15u; };
-  double cpr = B.n ? nc / n : 1, lpr = B.n ? (double)B.labels() / n : 1;
-  double apr = nc ? (double)B.cap_add.n() / nc : 1, dpr = nc ? (double)B.cap_drop.n() / nc : 1;
+  if (!D.stats_valid) {
+    D.stats = tile_stats(B, kSlotRows);
+    D.stats_valid = true;
+  }
+  const TileStats& ts = D.stats;
   uint32_t chain_len[NMASK];
   for (int m = 0; m < (int)NMASK; ++m) {
     chain_len[m] = 1;
@@ -375,11 +425,11 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
   }
   const uint32_t rows = kSlotRows;
   const uint32_t vw_stride = nslots | 1u;  // odd stride: lanes (requests) spread over the banks
-  double scale = 1.25;  // capacity headroom over the batch average; tiles beyond it take the overflow path
+  double scale = 1.0;  // shrunk only when the quantile capacities exceed the LDS budget
   for (;;) {
-    uint32_t cmax = (uint32_t)std::min(16.0 * rows + 64, scale * rows * cpr + 32);
-    uint32_t kmax = (uint32_t)std::min(16.0 * rows + 64, scale * rows * cpr * std::max(apr, dpr) + 32);
-    uint32_t lmax = (uint32_t)std::min(16.0 * rows + 64, scale * rows * lpr + 32);
+    uint32_t cmax = (uint32_t)std::max(1.0, scale * ts.ctr);
+    uint32_t kmax = (uint32_t)std::max(1.0, scale * std::max(ts.kadd, ts.kdrop));
+    uint32_t lmax = (uint32_t)std::max(1.0, scale * ts.lbl);
     uint32_t off = 16;
     const uint32_t stage_at = off;
     if (plan->fused) off = align(off + table_bytes);
@@ -392,7 +442,7 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
     T.o_loff = off;
     off = align(off + (rows + 1) * 4);
     T.o_cflags = off;
-    off = align(off + cmax);
+    off = align(off + cmax + 8);  // staged from the dword holding the first flag
     T.o_cadd = off;
     off = align(off + (cmax + 1) * 4);
     T.o_cdrop = off;
@@ -411,6 +461,8 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
     off = align(off + rows * 8);
     T.o_byp = off;
     off = align(off + rows);
+    T.o_sa = off;
+    off = align(off + NMASK * 4);
     T.o_gstk = 0;
     if (groups) {
       T.o_gstk = off;
@@ -428,8 +480,8 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
         const uint32_t cnt = m == M_NS ? rows : (m == M_CAPADD || m == M_CAPDROP) ? kmax : (m == M_LK || m == M_LV) ? lmax : cmax;
         T.o_so[m] = su;
         su = align(su + (cnt + 1) * 4);
-        const double bpr = B.n ? (double)sc.nbytes / (double)B.n : 0.0;  // string bytes per request
-        T.sb_cap[m] = align((uint32_t)std::min(16384.0, scale * rows * bpr + 64));  // longer tiles take the overflow path
+        (void)sc;
+        T.sb_cap[m] = align((uint32_t)std::min(16384.0, scale * ts.bytes[m]));  // longer tiles take the overflow path
         T.o_sb[m] = su;
         su = align(su + T.sb_cap[m] + 16);  // slack: dword reads may run <= 7 bytes past a string
       }

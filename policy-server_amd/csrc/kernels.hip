@@ -547,6 +547,22 @@ __device__ inline uint32_t tile_n(int m, uint32_t nr, uint32_t nc, uint32_t nka,
   return m == M_NS ? nr : m == M_CAPADD ? nka : m == M_CAPDROP ? nkd : (m == M_LK || m == M_LV) ? nl : nc;
 }
 
+// LDS-DMA copies (global_load_lds) issued by every wave of the workgroup: the LDS image is
+// wave-linear (wave-uniform base + lane x size), so lane l of the wave whose first element is i - l
+// lands at dst + i. Tails are masked by the loop bound.
+__device__ inline void glds_dwords(const uint32_t* src, uint32_t* dst, uint32_t n, uint32_t tid) {
+  const uint32_t lane = tid & 63u;
+  for (uint32_t i = tid; i < n; i += kSlotThreads)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + i),
+                                     (__attribute__((address_space(3))) void*)(dst + (i - lane)), 4, 0, 0);
+}
+__device__ inline void glds_x4(const u32x4* src, u32x4* dst, uint32_t n, uint32_t tid) {
+  const uint32_t lane = tid & 63u;
+  for (uint32_t i = tid; i < n; i += kSlotThreads)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + i),
+                                     (__attribute__((address_space(3))) void*)(dst + (i - lane)), 16, 0, 0);
+}
+
 template <bool FUSED>
 __global__ void __launch_bounds__(kSlotThreads)
     evaluate_slots_kernel(EvalArgs a, const TileArgs* __restrict__ tp, const TileDesc* __restrict__ desc,
@@ -593,6 +609,7 @@ __global__ void __launch_bounds__(kSlotThreads)
   uint64_t* l_rej = (uint64_t*)(lds + t.o_rej);
   uint64_t* l_mut = (uint64_t*)(lds + t.o_mut);
   uint8_t* l_byp = lds + t.o_byp;
+  uint32_t* l_sa = (uint32_t*)(lds + t.o_sa);
   uint32_t* l_vw = (uint32_t*)(lds + t.o_vw);
   uint16_t* gstk = t.o_gstk ? (uint16_t*)(lds + t.o_gstk) : nullptr;
   uint64_t* l_m[NMASK];
@@ -610,36 +627,29 @@ __global__ void __launch_bounds__(kSlotThreads)
     const uint32_t kab = d.kab, kae = d.kae, kdb = d.kdb, kde = d.kde;
     const uint32_t nc = ce - cb;
 
-    // ---- P0: stage request headers, container offsets and (FUSED) the tile's strings
-    for (uint32_t i = tid; i <= nr; i += kSlotThreads) {
-      if (i < nr) {
-        l_rf[i] = a.req_flags[r0 + i];
-        l_rej[i] = 0;
-      }
-      l_coff[i] = a.ctr_off[r0 + i];
-      l_loff[i] = a.lbl_off[r0 + i];
-    }
-    for (uint32_t i = tid; i <= nc; i += kSlotThreads) {
-      if (i < nc) l_cflags[i] = a.ctr_flags[cb + i];
-      l_cadd[i] = a.capadd_off[cb + i];
-      l_cdrop[i] = a.capdrop_off[cb + i];
-    }
+    // ---- P0: stage request headers, container offsets and (FUSED) the tile's strings. Every copy is
+    //      an LDS-DMA (global_load_lds: no VGPR round trip), so all of a tile's loads are in flight
+    //      together and the barrier waits for one memory latency, not one per array.
+    glds_dwords((const uint32_t*)(a.req_flags + r0), (uint32_t*)l_rf, (nr + 3u) >> 2, tid);
+    glds_dwords(a.ctr_off + r0, l_coff, nr + 1, tid);
+    glds_dwords(a.lbl_off + r0, l_loff, nr + 1, tid);
+    glds_dwords((const uint32_t*)a.ctr_flags + (cb >> 2), (uint32_t*)l_cflags, ((ce + 3u) >> 2) - (cb >> 2), tid);
+    glds_dwords(a.capadd_off + cb, l_cadd, nc + 1, tid);
+    glds_dwords(a.capdrop_off + cb, l_cdrop, nc + 1, tid);
     if (FUSED) {
 #pragma unroll
       for (int m = 0; m < (int)NMASK; ++m) {
         if (!t.o_sb[m]) continue;
         const uint32_t g0 = tile_g0(m, (uint32_t)r0, cb, kab, kdb, lb);
         const uint32_t n = tile_n(m, nr, nc, kae - kab, kde - kdb, le - lb);
-        const auto* go = gp(t.s_off[m]);
-        const uint32_t sa = d.sa[m], nv = d.nv[m];
-        uint32_t* so = (uint32_t*)(lds + t.o_so[m]);
-        for (uint32_t i = tid; i <= n; i += kSlotThreads) so[i] = go[g0 + i] - sa;
-        const auto* src = gp((const u32x4*)(t.s_bytes[m] + sa));
-        u32x4* dst = (u32x4*)(lds + t.o_sb[m]);
-        for (uint32_t i = tid; i < nv; i += kSlotThreads) dst[i] = src[i];
+        glds_dwords(t.s_off[m] + g0, (uint32_t*)(lds + t.o_so[m]), n + 1, tid);  // absolute: rebased by l_sa
+        glds_x4((const u32x4*)(t.s_bytes[m] + d.sa[m]), (u32x4*)(lds + t.o_sb[m]), d.nv[m], tid);
       }
     }
+    for (uint32_t i = tid; i < nr; i += kSlotThreads) l_rej[i] = 0;
+    if (tid < NMASK) l_sa[tid] = d.sa[tid];
     __syncthreads();
+    const uint8_t* cfl = l_cflags + (cb & 3u);  // staged from the dword holding flag cb
 
     // ---- P1: classify the staged strings, one flattened work list over every column and every DFA
     //      of a column's chain (FUSED), or load the classify kernel's masks (two-kernel form)
@@ -658,9 +668,11 @@ __global__ void __launch_bounds__(kSlotThreads)
         if (w >= s1 && w < s2) {  // image reference: one parse feeds the registry, tag and image chains
           const uint32_t i = w - s1;
           uint64_t mr = 0, mt = 0, mi = 0;
-          if (l_cflags[i] & KW_CTR_HAS_IMAGE) {
+          if (cfl[i] & KW_CTR_HAS_IMAGE) {
             const uint32_t* so = (const uint32_t*)(lds + t.o_so[M_IMG]);
-            classify_image_all(ch[M_REG], ch[M_TAG], ch[M_IMG], lds + t.o_sb[M_IMG], so[i], so[i + 1], &mr, &mt, &mi);
+            const uint32_t sa = l_sa[M_IMG];
+            classify_image_all(ch[M_REG], ch[M_TAG], ch[M_IMG], lds + t.o_sb[M_IMG], so[i] - sa, so[i + 1] - sa, &mr, &mt,
+                               &mi);
           }
           if (l_m[M_REG]) l_m[M_REG][i] = mr;
           if (l_m[M_TAG]) l_m[M_TAG][i] = mt;
@@ -679,11 +691,12 @@ __global__ void __launch_bounds__(kSlotThreads)
         const uint32_t e = local - i * clen;
         uint64_t* lm = (uint64_t*)(lds + t.o_m[m]);
         uint64_t r = 0;
-        if (m == M_AA && !(l_cflags[i] & KW_CTR_HAS_APPARMOR)) {
+        const uint32_t* so = (const uint32_t*)(lds + t.o_so[m]);
+        const uint32_t sa = l_sa[m];
+        if (m == M_AA && !(cfl[i] & KW_CTR_HAS_APPARMOR)) {
           r = 0;
         } else if (t.lit_lds[m]) {
-          const uint32_t* so = (const uint32_t*)(lds + t.o_so[m]);
-          r = lit_lookup(lds + t.lit_lds[m], lds + t.o_sb[m], so[i], so[i + 1]);
+          r = lit_lookup(lds + t.lit_lds[m], lds + t.o_sb[m], so[i] - sa, so[i + 1] - sa);
         } else {
           Chain c;
           c.head = t.dfa_head[m];
@@ -691,8 +704,7 @@ __global__ void __launch_bounds__(kSlotThreads)
           uint32_t o = c.head;
           for (uint32_t q = 0; q < e; ++q) o = chain_next(c, o);
           const DfaView v = chain_view(c, o);
-          const uint32_t* so = (const uint32_t*)(lds + t.o_so[m]);
-          r = v.acc[feed(v, v.start, lds + t.o_sb[m], so[i], so[i + 1])];
+          r = v.acc[feed(v, v.start, lds + t.o_sb[m], so[i] - sa, so[i + 1] - sa)];
         }
         lm[e * cap + i] = r;  // chain element e -> its own partial slot
         if (m == M_LK && t.kv_lds) {  // the label's value, against the regexes of its own key only
@@ -701,8 +713,9 @@ __global__ void __launch_bounds__(kSlotThreads)
             const uint32_t rel = ((const uint32_t*)(lds + t.kv_lds))[__builtin_ctzll(r)];
             if (rel) {
               const DfaView v = make_view(lds + t.kv_lds + rel, nullptr, t.kv_blob + rel);
-              const uint32_t* so = (const uint32_t*)(lds + t.o_so[M_LV]);
-              lv = v.acc[feed(v, v.start, lds + t.o_sb[M_LV], so[i], so[i + 1])];
+              const uint32_t* sv_ = (const uint32_t*)(lds + t.o_so[M_LV]);
+              const uint32_t sav = l_sa[M_LV];
+              lv = v.acc[feed(v, v.start, lds + t.o_sb[M_LV], sv_[i] - sav, sv_[i + 1] - sav)];
             }
           }
           ((uint64_t*)(lds + t.o_m[M_LV]))[i] = lv;
@@ -727,7 +740,7 @@ __global__ void __launch_bounds__(kSlotThreads)
       src.loff_ = l_loff;
       src.cadd_ = l_cadd;
       src.cdrop_ = l_cdrop;
-      src.cflags_ = l_cflags;
+      src.cflags_ = cfl;
 #pragma unroll
       for (int k = 0; k < (int)NMASK; ++k) {
         src.m_[k] = l_m[k];

@@ -63,6 +63,7 @@ struct TileArgs {
   uint32_t o_rf, o_coff, o_loff, o_cflags, o_cadd, o_cdrop, o_gstk;  // LDS byte offsets
   uint32_t o_m[NMASK];            // LDS byte offset of each staged mask array, 0 = not read
   uint32_t o_rej, o_mut, o_byp;   // per-request walk results: rejected / mutated slots, bypass flag
+  uint32_t o_sa;                  // u32[NMASK]: the tile's staged byte start per string column (TileDesc.sa)
   uint32_t o_vw, vw_stride;       // violation words [rows][vw_stride] (aliases the staged strings)
   uint32_t o_slot, slot_bytes;    // staged SlotHdr record of this chunk
   uint32_t col0, ncols, vec4;     // output columns [col0, col0 + ncols); vec4: 16-B verdict stores
@@ -81,7 +82,8 @@ struct TileArgs {
   const uint32_t* s_off[NMASK];   // string offsets feeding mask k (M_REG/TAG use M_IMG's column)
   const uint8_t* s_bytes[NMASK];
   // FUSED: each tile's strings staged in LDS (M_NS, M_IMG, M_AA, M_CAPADD, M_CAPDROP, M_LK, M_LV):
-  // offsets rebased to the staged bytes, bytes copied from the 16-B aligned start; 0 = not staged
+  // absolute offsets (rebased by the tile's staged start, o_sa), bytes copied from the 16-B aligned start;
+  // 0 = not staged
   uint32_t o_so[NMASK], o_sb[NMASK], sb_cap[NMASK];
 };
 
