@@ -299,6 +299,8 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
       table_bytes += stage_rec(m, &o);
     }
   plan->fused = !plan->rows_mode && table_bytes <= kFusedTableBudget;
+  for (int m : {M_NS, M_AA, M_CAPADD, M_CAPDROP, M_LK})  // the fused classifier is the literal hash
+    if (use[m] && !lit_of(m)) plan->fused = false;
 
   // ---- classify jobs (two-kernel mode and the micro-batch mode)
   ClassifyJobs& J = plan->jobs;
@@ -407,19 +409,12 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
     D.stats_valid = true;
   }
   const TileStats& ts = D.stats;
-  uint32_t chain_len[NMASK];
-  for (int m = 0; m < (int)NMASK; ++m) {
-    chain_len[m] = 1;
-    // image chains are walked by one item; the non-fused path stages the classify kernel's merged masks
-    if (!plan->fused || !use[m] || m == M_REG || m == M_TAG || m == M_IMG || lit_of(m) || (m == M_LV && kv)) continue;
-    uint32_t c = 0;
-    for (uint32_t o = H->dfa_off[mask_col(m)]; o; o = ((const DevDfa*)(E.blob.data() + o))->next) ++c;
-    chain_len[m] = std::max<uint32_t>(1, c);
-  }
+  uint32_t chain_len[NMASK];  // per-string masks are whole-chain results (image chains walk in one item)
+  for (int m = 0; m < (int)NMASK; ++m) chain_len[m] = 1;
   uint32_t slot_bytes = 16, nslots = 1;
   bool groups = false;
   for (const SlotChunk& c : plan->chunks) {
-    slot_bytes = std::max<uint32_t>(slot_bytes, (uint32_t)c.rec.size());
+    slot_bytes = std::max<uint32_t>(slot_bytes, c.staged);
     nslots = std::max(nslots, c.nslots);
     groups = groups || c.groups;
   }
@@ -449,11 +444,21 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
     off = align(off + (cmax + 1) * 4);
     for (int m = 0; m < (int)NMASK; ++m) {
       T.o_m[m] = 0;
-      if (!use[m]) continue;
-      uint32_t cnt = m == M_NS ? rows : (m == M_CAPADD || m == M_CAPDROP) ? kmax : (m == M_LK || m == M_LV) ? lmax : cmax;
+      if (!use[m] || m == M_LV) continue;  // label values: derived into o_vl in P1, never staged
+      const uint32_t cnt = m == M_NS ? rows : (m == M_CAPADD || m == M_CAPDROP) ? kmax : m == M_LK ? lmax : cmax;
+      const bool lit = m == M_NS || m == M_CAPADD || m == M_CAPDROP || m == M_LK;
       T.o_m[m] = off;
       T.mask_cap[m] = cnt;
-      off = align(off + cnt * 8 * chain_len[m]);  // one partial slot per DFA of the column chain
+      off = align(off + cnt * (lit ? 1u : 8u));
+    }
+    T.o_vadd = T.o_vl = 0;
+    if (use[M_CAPADD]) {
+      T.o_vadd = off;
+      off = align(off + kmax * 8);
+    }
+    if (use[M_LK]) {
+      T.o_vl = off;
+      off = align(off + lmax * 16);
     }
     T.o_rej = off;
     off = align(off + rows * 8);
@@ -558,6 +563,8 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
     }
   }
   // per-chunk TileArgs (slot_plan pointers are filled in at upload, run_pass)
+  const char* p3env = getenv("KW_P3");
+  const uint32_t p3_item = (p3env && std::string(p3env) == "item") ? 1u : 0u;
   plan->tiles.clear();
   plan->slot_at.clear();
   plan->slot_blob.clear();
@@ -565,11 +572,16 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
     TileArgs t = T;
     plan->slot_at.push_back((uint32_t)plan->slot_blob.size());
     plan->slot_blob.insert(plan->slot_blob.end(), c.rec.begin(), c.rec.end());
-    t.slot_bytes = (uint32_t)c.rec.size();
+    t.slot_bytes = c.staged;
     t.col0 = c.col0;
     t.ncols = c.ncols;
     t.vec4 = (npol % 4u == 0 && c.col0 % 4u == 0 && c.ncols % 4u == 0) ? 1u : 0u;
     t.o_gstk = c.groups ? T.o_gstk : 0u;
+    const SlotHdr* sh = (const SlotHdr*)c.rec.data();
+    t.o_cols_rec = sh->o_cols;
+    t.o_cidx_rec = sh->o_cidx;
+    t.slot_init = sh->init;
+    t.p3_item = p3_item;
     plan->tiles.push_back(t);
   }
   uint64_t ntiles = (B.n + T.rows - 1) / T.rows;
@@ -890,11 +902,12 @@ int kw_env_classify_check(const kw_env* env, int col, const char* key, size_t kl
     const uint64_t km = blob_lit_lookup(blob, H->lit_off[COL_LK], (const uint8_t*)key, klen);
     const uint32_t* idx = (const uint32_t*)(blob + H->kv_off);
     uint64_t keybits = 0;  // value patterns constrained on this key: every bit its DFA can accept
-    if (km && idx[__builtin_ctzll(km)]) {
-      const uint32_t o = H->kv_off + idx[__builtin_ctzll(km)];
+    for (uint32_t rel = km ? idx[__builtin_ctzll(km)] : 0u; rel;) {  // the key's chain (region-relative links)
+      const uint32_t o = H->kv_off + rel;
       const DevDfa* d = (const DevDfa*)(blob + o);
       for (uint32_t q = 0; q < d->nstates; ++q) keybits |= ((const uint64_t*)(blob + d->acc_off))[q];
-      *fast_mask = blob_dfa_run(blob, o, u, len);
+      *fast_mask |= blob_dfa_run(blob, o, u, len);
+      rel = d->next;
     }
     *dfa_mask &= keybits;
     return 1;
@@ -966,6 +979,7 @@ uint64_t host_image_part(const uint8_t* blob, uint32_t head, int k, const uint8_
 
 struct HostSrc {
   const Batch* b;
+  const SlotView* sv;
   const std::vector<uint64_t>* mk[NMASK];
   uint8_t rf(uint64_t r) const { return b->req_flags[r]; }
   uint32_t coff(uint64_t r) const { return b->ctr_off[r]; }
@@ -976,6 +990,18 @@ struct HostSrc {
   template <int K>
   uint64_t m(uint64_t i) const {
     return mk[K] ? (*mk[K])[i] : 0ull;
+  }
+  uint64_t vadd(uint32_t k) const { return derive_capadd(*sv, m<M_CAPADD>(k)); }
+  uint64_t vaa(uint32_t c) const { return derive_apparmor(*sv, m<M_AA>(c)); }
+  uint64_t vden(uint32_t l) const {
+    uint64_t d, c;
+    derive_label(*sv, m<M_LK>(l), m<M_LV>(l), &d, &c);
+    return d;
+  }
+  uint64_t vcon(uint32_t l) const {
+    uint64_t d, c;
+    derive_label(*sv, m<M_LK>(l), m<M_LV>(l), &d, &c);
+    return c;
   }
 };
 }  // namespace
@@ -1028,7 +1054,9 @@ int kw_debug_host_walk(const kw_env* env, const kw_batch* kb, const int32_t* pol
     SlotView sv;
     sv.h = (const SlotHdr*)ch.rec.data();
     sv.base = ch.rec.data();
+    src.sv = &sv;
     const ColInfo* cols = sv.cols();
+    const uint8_t* cidx = ch.rec.data() + sv.h->o_cidx;
     for (uint64_t r = 0; r < B.n; ++r) {
       const uint32_t rf = B.req_flags[r];
       const bool byp = H->bypass_bit >= 0 && !(rf & KW_REQ_RAW) && (rf & KW_REQ_HAS_NAMESPACE) && src.mk[M_NS] &&
@@ -1040,7 +1068,7 @@ int kw_debug_host_walk(const kw_env* env, const kw_batch* kb, const int32_t* pol
       rej |= walk_namespace(src, sv, r, vw.data());
       for (uint32_t j = 0; j < ch.ncols; ++j)
         out[r * npol + ch.col0 + j] =
-            byp ? kBypassWord : column_word(cols[j], rej, mut, sv.h->init, vw.data(), blob, gstk, 1);
+            byp ? kBypassWord : column_word(cols[j], rej, mut, sv.h->init, vw.data(), blob, cidx, gstk, 1);
     }
   }
   return KW_OK;

@@ -688,19 +688,24 @@ Status build_env(const char* json, size_t len, bool continue_on_errors, const ch
         if (std::find(v.begin(), v.end(), (uint32_t)P.idx[32 + k]) == v.end()) v.push_back(P.idx[32 + k]);
       }
     }
-    std::vector<Dfa> kd(kMaxPatternsPerColumn);
+    // one DFA per key while the union of its regexes stays small, else a short chain of DFAs
+    // (compile_column's greedy groups) instead of one large product automaton
+    std::vector<std::vector<Dfa>> kd(kMaxPatternsPerColumn);
     bool ok = true;
     for (size_t k = 0; k < vals.size() && ok; ++k) {
       if (vals[k].empty()) continue;
       std::vector<Pattern> pats;
       for (uint32_t v : vals[k]) pats.push_back(env->cols[COL_LV][v]);
       std::string err;
-      ok = compile_dfa(pats, &kd[k], &err) && kd[k].trans.size() * 2 <= kMaxDfaTableBytes;
-      for (uint64_t& a : kd[k].accept) {  // local pattern bits -> the column's global bits
-        uint64_t g = 0;
-        for (size_t i = 0; i < vals[k].size(); ++i)
-          if ((a >> i) & 1ull) g |= 1ull << vals[k][i];
-        a = g;
+      ok = compile_column(pats, kKvDfaBytes, &kd[k], &err);
+      for (Dfa& d : kd[k]) {
+        ok = ok && d.trans.size() * 2 <= kMaxDfaTableBytes;
+        for (uint64_t& a : d.accept) {  // local pattern bits -> the column's global bits
+          uint64_t g = 0;
+          for (size_t i = 0; i < vals[k].size(); ++i)
+            if ((a >> i) & 1ull) g |= 1ull << vals[k][i];
+          a = g;
+        }
       }
     }
     if (ok) {
@@ -708,8 +713,15 @@ Status build_env(const char* json, size_t len, bool continue_on_errors, const ch
       const size_t region = b.size();
       uint32_t idx[kMaxPatternsPerColumn] = {};
       put(&b, idx);
-      for (size_t k = 0; k < vals.size(); ++k)
-        if (!vals[k].empty()) idx[k] = (uint32_t)(emit_dfa(kd[k], &b) - region);
+      for (size_t k = 0; k < vals.size(); ++k) {
+        uint32_t prev = 0;
+        for (const Dfa& d : kd[k]) {
+          const uint32_t at = (uint32_t)(emit_dfa(d, &b) - region);
+          if (prev) ((DevDfa*)(b.data() + region + prev))->next = at;  // region-relative chain link
+          else idx[k] = at;
+          prev = at;
+        }
+      }
       memcpy(b.data() + region, idx, sizeof(idx));
       align16(&b);
       hdr.kv_off = (uint32_t)region;

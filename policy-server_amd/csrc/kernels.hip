@@ -298,22 +298,15 @@ struct GlobalSrc {
   __device__ uint64_t m(uint64_t i) const { return a->m[K] ? a->m[K][i] : 0ull; }
 };
 
-// A staged mask of a chained column is the OR of its per-DFA partial slots ([chain][cap]).
-__device__ inline uint64_t staged_mask(const uint64_t* m, uint32_t i, uint32_t clen, uint32_t cap) {
-  uint64_t r = m[i];
-  for (uint32_t e = 1; e < clen; ++e) r |= m[e * cap + i];
-  return r;
-}
-
 struct TileSrc {
   const uint8_t* rf_;
   const uint32_t *coff_, *loff_, *cadd_, *cdrop_;
   const uint8_t* cflags_;
-  const uint64_t* m_[NMASK];
+  const uint8_t* m_[NMASK];  // TileArgs.o_m arrays (u8 pattern index or u64, by mask)
+  const uint64_t* vadd_;     // violation set per added capability
+  const uint64_t* vl_;       // (vden, vcon) per label
   uint64_t r0;
   uint32_t cb, lb, kab, kdb;
-  uint32_t clen_[NMASK];  // chain length per mask (indexed by template constants only)
-  uint32_t cap_[NMASK];   // staged capacity per mask
   __device__ uint8_t rf(uint64_t r) const { return rf_[r - r0]; }
   __device__ uint32_t coff(uint64_t r) const { return coff_[r - r0]; }
   __device__ uint32_t loff(uint64_t r) const { return loff_[r - r0]; }
@@ -322,12 +315,20 @@ struct TileSrc {
   __device__ uint32_t cdrop(uint32_t c) const { return cdrop_[c - cb]; }
   template <int K>
   __device__ uint64_t m(uint64_t i) const {
-    const uint64_t* p = m_[K];
+    const uint8_t* p = m_[K];
     if (!p) return 0ull;
     const uint32_t j = K == M_NS ? (uint32_t)(i - r0) : K == M_CAPADD ? (uint32_t)(i - kab) : K == M_CAPDROP ? (uint32_t)(i - kdb)
                        : (K == M_LK || K == M_LV) ? (uint32_t)(i - lb) : (uint32_t)(i - cb);
-    return staged_mask(p, j, clen_[K], cap_[K]);
+    if (K == M_NS || K == M_CAPADD || K == M_CAPDROP || K == M_LK) {
+      const uint32_t v = p[j];
+      return v < 64u ? 1ull << v : 0ull;
+    }
+    return ((const uint64_t*)p)[j];
   }
+  __device__ uint64_t vadd(uint32_t k) const { return vadd_[k - kab]; }
+  __device__ uint64_t vaa(uint32_t c) const { return ((const uint64_t*)m_[M_AA])[c - cb]; }
+  __device__ uint64_t vden(uint32_t l) const { return vl_[2 * (l - lb)]; }
+  __device__ uint64_t vcon(uint32_t l) const { return vl_[2 * (l - lb) + 1]; }
 };
 
 template <class S>
@@ -547,6 +548,32 @@ __device__ inline uint32_t tile_n(int m, uint32_t nr, uint32_t nc, uint32_t nka,
   return m == M_NS ? nr : m == M_CAPADD ? nka : m == M_CAPDROP ? nkd : (m == M_LK || m == M_LV) ? nl : nc;
 }
 
+// Literal pattern index of a one-bit mask (0xff: no pattern).
+__device__ inline uint8_t lit_index(uint64_t r) { return r ? (uint8_t)__builtin_ctzll(r) : (uint8_t)0xffu; }
+
+// A label value against the value regexes constrained on its key (label-key mask km): the key's
+// per-key DFA chain, else the whole label-value column chain.
+__device__ inline uint64_t classify_value(const TileArgs& t, const uint8_t* lds, uint64_t km, const uint8_t* bytes,
+                                          uint32_t b, uint32_t e) {
+  uint64_t vm = 0;
+  if (t.kv_lds) {
+    for (uint32_t rel = ((const uint32_t*)(lds + t.kv_lds))[__builtin_ctzll(km)]; rel;
+         rel = ((const DevDfa*)(lds + t.kv_lds + rel))->next) {
+      const DfaView v = make_view(lds + t.kv_lds + rel, nullptr, t.kv_blob + rel);
+      vm |= v.acc[feed(v, v.start, bytes, b, e)];
+    }
+  } else {
+    Chain c;
+    c.head = t.dfa_head[M_LV];
+    c.base = lds + t.dfa_lds[M_LV];
+    for (uint32_t o = c.head; o; o = chain_next(c, o)) {
+      const DfaView v = chain_view(c, o);
+      vm |= v.acc[feed(v, v.start, bytes, b, e)];
+    }
+  }
+  return vm;
+}
+
 // LDS-DMA copies (global_load_lds) issued by every wave of the workgroup: the LDS image is
 // wave-linear (wave-uniform base + lane x size), so lane l of the wave whose first element is i - l
 // lands at dst + i. Tails are masked by the loop bound.
@@ -610,6 +637,8 @@ __global__ void __launch_bounds__(kSlotThreads)
   uint64_t* l_mut = (uint64_t*)(lds + t.o_mut);
   uint8_t* l_byp = lds + t.o_byp;
   uint32_t* l_sa = (uint32_t*)(lds + t.o_sa);
+  uint64_t* l_vadd = (uint64_t*)(lds + t.o_vadd);
+  uint64_t* l_vl = (uint64_t*)(lds + t.o_vl);
   uint32_t* l_vw = (uint32_t*)(lds + t.o_vw);
   uint16_t* gstk = t.o_gstk ? (uint16_t*)(lds + t.o_gstk) : nullptr;
   uint64_t* l_m[NMASK];
@@ -651,20 +680,21 @@ __global__ void __launch_bounds__(kSlotThreads)
     __syncthreads();
     const uint8_t* cfl = l_cflags + (cb & 3u);  // staged from the dword holding flag cb
 
-    // ---- P1: classify the staged strings, one flattened work list over every column and every DFA
-    //      of a column's chain (FUSED), or load the classify kernel's masks (two-kernel form)
+    // ---- P1: classify the staged strings (FUSED) or take the classify kernel's masks (two-kernel
+    //      form), and derive each entity's violation set from the slot tables, entity-parallel
+    //      (slots.hpp derive_*): added capability -> vadd, AppArmor profile -> its AA entry, label ->
+    //      (vden, vcon). Literal columns keep the pattern index only.
     if (FUSED && !(t.debug & 1u)) {
-      // jobs in order NS, IMG, AA, CAPADD, CAPDROP, LK, LV
+      // one flattened work list: NS, IMG, AA, CAPADD, CAPDROP, LK (the LK item also classifies the
+      // label's value)
       const uint32_t n0 = t.o_m[M_NS] ? nr : 0u;
       const uint32_t n1 = (t.o_m[M_REG] || t.o_m[M_TAG] || t.o_m[M_IMG]) ? nc : 0u;
       const uint32_t n2 = t.o_m[M_AA] ? nc : 0u;
-      const uint32_t n3 = t.o_m[M_CAPADD] ? (kae - kab) * t.chain_len[M_CAPADD] : 0u;
-      const uint32_t n4 = t.o_m[M_CAPDROP] ? (kde - kdb) * t.chain_len[M_CAPDROP] : 0u;
-      const uint32_t n5 = t.o_m[M_LK] ? (le - lb) * t.chain_len[M_LK] : 0u;
-      const uint32_t n6 = (t.o_m[M_LV] && !t.kv_lds) ? (le - lb) * t.chain_len[M_LV] : 0u;  // kv: in the LK item
-      const uint32_t s1 = n0, s2 = s1 + n1, s3 = s2 + n2 * t.chain_len[M_AA], s4 = s3 + n3, s5 = s4 + n4,
-                     s6 = s5 + n5, s7 = s6 + n6;
-      for (uint32_t w = tid; w < s7; w += kSlotThreads) {
+      const uint32_t n3 = t.o_m[M_CAPADD] ? kae - kab : 0u;
+      const uint32_t n4 = t.o_m[M_CAPDROP] ? kde - kdb : 0u;
+      const uint32_t n5 = t.o_m[M_LK] ? le - lb : 0u;
+      const uint32_t s1 = n0, s2 = s1 + n1, s3 = s2 + n2, s4 = s3 + n3, s5 = s4 + n4, s6 = s5 + n5;
+      for (uint32_t w = tid; w < s6; w += kSlotThreads) {
         if (w >= s1 && w < s2) {  // image reference: one parse feeds the registry, tag and image chains
           const uint32_t i = w - s1;
           uint64_t mr = 0, mt = 0, mi = 0;
@@ -674,60 +704,68 @@ __global__ void __launch_bounds__(kSlotThreads)
             classify_image_all(ch[M_REG], ch[M_TAG], ch[M_IMG], lds + t.o_sb[M_IMG], so[i] - sa, so[i + 1] - sa, &mr, &mt,
                                &mi);
           }
-          if (l_m[M_REG]) l_m[M_REG][i] = mr;
-          if (l_m[M_TAG]) l_m[M_TAG][i] = mt;
-          if (l_m[M_IMG]) l_m[M_IMG][i] = mi;
+          if (t.o_m[M_REG]) ((uint64_t*)(lds + t.o_m[M_REG]))[i] = mr;
+          if (t.o_m[M_TAG]) ((uint64_t*)(lds + t.o_m[M_TAG]))[i] = mt;
+          if (t.o_m[M_IMG]) ((uint64_t*)(lds + t.o_m[M_IMG]))[i] = mi;
           continue;
         }
-        uint32_t m, local, cap;
-        if (w < s1) { m = M_NS; local = w; cap = t.mask_cap[M_NS]; }
-        else if (w < s3) { m = M_AA; local = w - s2; cap = t.mask_cap[M_AA]; }
-        else if (w < s4) { m = M_CAPADD; local = w - s3; cap = t.mask_cap[M_CAPADD]; }
-        else if (w < s5) { m = M_CAPDROP; local = w - s4; cap = t.mask_cap[M_CAPDROP]; }
-        else if (w < s6) { m = M_LK; local = w - s5; cap = t.mask_cap[M_LK]; }
-        else { m = M_LV; local = w - s6; cap = t.mask_cap[M_LV]; }
-        const uint32_t clen = t.chain_len[m];
-        const uint32_t i = clen == 1 ? local : local / clen;
-        const uint32_t e = local - i * clen;
-        uint64_t* lm = (uint64_t*)(lds + t.o_m[m]);
-        uint64_t r = 0;
+        uint32_t m, i;
+        if (w < s1) { m = M_NS; i = w; }
+        else if (w < s3) { m = M_AA; i = w - s2; }
+        else if (w < s4) { m = M_CAPADD; i = w - s3; }
+        else if (w < s5) { m = M_CAPDROP; i = w - s4; }
+        else { m = M_LK; i = w - s5; }
         const uint32_t* so = (const uint32_t*)(lds + t.o_so[m]);
         const uint32_t sa = l_sa[m];
-        if (m == M_AA && !(cfl[i] & KW_CTR_HAS_APPARMOR)) {
-          r = 0;
-        } else if (t.lit_lds[m]) {
-          r = lit_lookup(lds + t.lit_lds[m], lds + t.o_sb[m], so[i] - sa, so[i + 1] - sa);
-        } else {
-          Chain c;
-          c.head = t.dfa_head[m];
-          c.base = lds + t.dfa_lds[m];
-          uint32_t o = c.head;
-          for (uint32_t q = 0; q < e; ++q) o = chain_next(c, o);
-          const DfaView v = chain_view(c, o);
-          r = v.acc[feed(v, v.start, lds + t.o_sb[m], so[i] - sa, so[i + 1] - sa)];
+        if (m == M_AA) {
+          uint64_t v = 0;
+          if (cfl[i] & KW_CTR_HAS_APPARMOR)
+            v = derive_apparmor(sv, lit_lookup(lds + t.lit_lds[M_AA], lds + t.o_sb[M_AA], so[i] - sa, so[i + 1] - sa));
+          ((uint64_t*)(lds + t.o_m[M_AA]))[i] = v;
+          continue;
         }
-        lm[e * cap + i] = r;  // chain element e -> its own partial slot
-        if (m == M_LK && t.kv_lds) {  // the label's value, against the regexes of its own key only
-          uint64_t lv = 0;
-          if (r) {
-            const uint32_t rel = ((const uint32_t*)(lds + t.kv_lds))[__builtin_ctzll(r)];
-            if (rel) {
-              const DfaView v = make_view(lds + t.kv_lds + rel, nullptr, t.kv_blob + rel);
-              const uint32_t* sv_ = (const uint32_t*)(lds + t.o_so[M_LV]);
-              const uint32_t sav = l_sa[M_LV];
-              lv = v.acc[feed(v, v.start, lds + t.o_sb[M_LV], sv_[i] - sav, sv_[i + 1] - sav)];
-            }
+        const uint64_t r = lit_lookup(lds + t.lit_lds[m], lds + t.o_sb[m], so[i] - sa, so[i + 1] - sa);
+        lds[t.o_m[m] + i] = lit_index(r);
+        if (m == M_CAPADD) {
+          l_vadd[i] = derive_capadd(sv, r);
+        } else if (m == M_LK) {
+          uint64_t vm = 0;
+          if (r && t.o_sb[M_LV]) {
+            const uint32_t* vo = (const uint32_t*)(lds + t.o_so[M_LV]);
+            const uint32_t vsa = l_sa[M_LV];
+            vm = classify_value(t, lds, r, lds + t.o_sb[M_LV], vo[i] - vsa, vo[i + 1] - vsa);
           }
-          ((uint64_t*)(lds + t.o_m[M_LV]))[i] = lv;
+          uint64_t vden, vcon;
+          derive_label(sv, r, vm, &vden, &vcon);
+          l_vl[2 * i] = vden;
+          l_vl[2 * i + 1] = vcon;
         }
       }
     } else if (!FUSED) {
-      const uint32_t base[NMASK] = {(uint32_t)r0, cb, cb, cb, kab, kdb, cb, lb, lb};
-      const uint32_t cnt[NMASK] = {nr, nc, nc, nc, kae - kab, kde - kdb, nc, le - lb, le - lb};
-#pragma unroll
-      for (int k = 0; k < (int)NMASK; ++k)
-        if (l_m[k])
-          for (uint32_t i = tid; i < cnt[k]; i += kSlotThreads) l_m[k][i] = a.m[k][base[k] + i];
+      for (uint32_t i = tid; i < nr && t.o_m[M_NS]; i += kSlotThreads) lds[t.o_m[M_NS] + i] = lit_index(a.m[M_NS][r0 + i]);
+      for (uint32_t i = tid; i < nc; i += kSlotThreads) {
+        if (t.o_m[M_REG]) ((uint64_t*)(lds + t.o_m[M_REG]))[i] = a.m[M_REG][cb + i];
+        if (t.o_m[M_TAG]) ((uint64_t*)(lds + t.o_m[M_TAG]))[i] = a.m[M_TAG][cb + i];
+        if (t.o_m[M_IMG]) ((uint64_t*)(lds + t.o_m[M_IMG]))[i] = a.m[M_IMG][cb + i];
+        if (t.o_m[M_AA])
+          ((uint64_t*)(lds + t.o_m[M_AA]))[i] =
+              (cfl[i] & KW_CTR_HAS_APPARMOR) ? derive_apparmor(sv, a.m[M_AA][cb + i]) : 0ull;
+      }
+      for (uint32_t i = tid; i < kae - kab && t.o_m[M_CAPADD]; i += kSlotThreads) {
+        const uint64_t r = a.m[M_CAPADD][kab + i];
+        lds[t.o_m[M_CAPADD] + i] = lit_index(r);
+        l_vadd[i] = derive_capadd(sv, r);
+      }
+      for (uint32_t i = tid; i < kde - kdb && t.o_m[M_CAPDROP]; i += kSlotThreads)
+        lds[t.o_m[M_CAPDROP] + i] = lit_index(a.m[M_CAPDROP][kdb + i]);
+      for (uint32_t i = tid; i < le - lb && t.o_m[M_LK]; i += kSlotThreads) {
+        const uint64_t r = a.m[M_LK][lb + i];
+        lds[t.o_m[M_LK] + i] = lit_index(r);
+        uint64_t vden, vcon;
+        derive_label(sv, r, a.m[M_LV] ? a.m[M_LV][lb + i] : 0ull, &vden, &vcon);
+        l_vl[2 * i] = vden;
+        l_vl[2 * i + 1] = vcon;
+      }
     }
     __syncthreads();
 
@@ -742,11 +780,9 @@ __global__ void __launch_bounds__(kSlotThreads)
       src.cdrop_ = l_cdrop;
       src.cflags_ = cfl;
 #pragma unroll
-      for (int k = 0; k < (int)NMASK; ++k) {
-        src.m_[k] = l_m[k];
-        src.clen_[k] = FUSED ? t.chain_len[k] : 1u;
-        src.cap_[k] = t.mask_cap[k];
-      }
+      for (int k = 0; k < (int)NMASK; ++k) src.m_[k] = t.o_m[k] ? lds + t.o_m[k] : nullptr;
+      src.vadd_ = l_vadd;
+      src.vl_ = l_vl;
       src.r0 = r0;
       src.cb = cb;
       src.lb = lb;
@@ -775,36 +811,67 @@ __global__ void __launch_bounds__(kSlotThreads)
     }
     __syncthreads();
 
-    // ---- P3: verdict rows. vec4: items = (request, 4 columns); 16 lanes cover a 256-B row and a
-    //      wave writes 1 KiB contiguous. Otherwise one column per item.
+    // ---- P3: verdict rows. Default: one lane per request, each wave a quarter of the columns; the
+    //      column records come from the global copy of the slot plan with wave-uniform indices
+    //      (scalar loads) and each lane writes 16-B pieces of its own row. p3_item: items =
+    //      (request, 4 columns), 16 lanes per 256-B row, column records from LDS.
     if (!(t.debug & 4u)) {
-      const ColInfo* cols = sv.cols();
-      const uint64_t init = sv.h->init;
+      const uint64_t init = t.slot_init;
+      const uint8_t* cidx = t.slot_plan + t.o_cidx_rec;
       uint16_t* gs = gstk ? gstk + tid : nullptr;
-      if (t.vec4) {
-        const uint32_t G = t.ncols >> 2;
-        for (uint32_t it = tid; it < nr * G; it += kSlotThreads) {
-          const uint32_t rr = it / G, g = it - rr * G;
-          uint4 w;
-          if (l_byp[rr]) {
-            w = make_uint4(kBypassWord, kBypassWord, kBypassWord, kBypassWord);
+      if (!t.p3_item) {
+        if (lane < nr) {
+          const ColInfo* gcols = (const ColInfo*)(t.slot_plan + t.o_cols_rec);
+          const uint64_t rej = l_rej[lane], mut = l_mut[lane];
+          const bool byp = l_byp[lane] != 0;
+          const uint32_t* vw = l_vw + lane * t.vw_stride;
+          uint32_t* orow = out + (r0 + lane) * npol + t.col0;
+          const uint32_t q = ((t.ncols + 15u) >> 4) << 2;
+          const uint32_t j0 = min(t.ncols, wave * q), j1 = min(t.ncols, j0 + q);
+          if (t.vec4) {
+            for (uint32_t j = j0; j < j1; j += 4) {
+              uint4 w = make_uint4(kBypassWord, kBypassWord, kBypassWord, kBypassWord);
+              if (!byp) {
+                w.x = column_word(gcols[j + 0], rej, mut, init, vw, blob, cidx, gs, kSlotThreads);
+                w.y = column_word(gcols[j + 1], rej, mut, init, vw, blob, cidx, gs, kSlotThreads);
+                w.z = column_word(gcols[j + 2], rej, mut, init, vw, blob, cidx, gs, kSlotThreads);
+                w.w = column_word(gcols[j + 3], rej, mut, init, vw, blob, cidx, gs, kSlotThreads);
+              }
+              *(uint4*)(orow + j) = w;
+            }
           } else {
-            const uint64_t rej = l_rej[rr], mut = l_mut[rr];
-            const uint32_t* vw = l_vw + rr * t.vw_stride;
-            w.x = column_word(cols[4 * g + 0], rej, mut, init, vw, blob, gs, kSlotThreads);
-            w.y = column_word(cols[4 * g + 1], rej, mut, init, vw, blob, gs, kSlotThreads);
-            w.z = column_word(cols[4 * g + 2], rej, mut, init, vw, blob, gs, kSlotThreads);
-            w.w = column_word(cols[4 * g + 3], rej, mut, init, vw, blob, gs, kSlotThreads);
+            for (uint32_t j = j0; j < j1; ++j)
+              orow[j] = byp ? kBypassWord : column_word(gcols[j], rej, mut, init, vw, blob, cidx, gs, kSlotThreads);
           }
-          *(uint4*)(out + (r0 + rr) * npol + t.col0 + 4 * g) = w;
         }
       } else {
-        const uint32_t G = t.ncols;
-        for (uint32_t it = tid; it < nr * G; it += kSlotThreads) {
-          const uint32_t rr = it / G, g = it - rr * G;
-          uint32_t w = kBypassWord;
-          if (!l_byp[rr]) w = column_word(cols[g], l_rej[rr], l_mut[rr], init, l_vw + rr * t.vw_stride, blob, gs, kSlotThreads);
-          out[(r0 + rr) * npol + t.col0 + g] = w;
+        const ColInfo* cols = sv.cols();
+        if (t.vec4) {
+          const uint32_t G = t.ncols >> 2;
+          for (uint32_t it = tid; it < nr * G; it += kSlotThreads) {
+            const uint32_t rr = it / G, g = it - rr * G;
+            uint4 w;
+            if (l_byp[rr]) {
+              w = make_uint4(kBypassWord, kBypassWord, kBypassWord, kBypassWord);
+            } else {
+              const uint64_t rej = l_rej[rr], mut = l_mut[rr];
+              const uint32_t* vw = l_vw + rr * t.vw_stride;
+              w.x = column_word(cols[4 * g + 0], rej, mut, init, vw, blob, cidx, gs, kSlotThreads);
+              w.y = column_word(cols[4 * g + 1], rej, mut, init, vw, blob, cidx, gs, kSlotThreads);
+              w.z = column_word(cols[4 * g + 2], rej, mut, init, vw, blob, cidx, gs, kSlotThreads);
+              w.w = column_word(cols[4 * g + 3], rej, mut, init, vw, blob, cidx, gs, kSlotThreads);
+            }
+            *(uint4*)(out + (r0 + rr) * npol + t.col0 + 4 * g) = w;
+          }
+        } else {
+          const uint32_t G = t.ncols;
+          for (uint32_t it = tid; it < nr * G; it += kSlotThreads) {
+            const uint32_t rr = it / G, g = it - rr * G;
+            uint32_t w = kBypassWord;
+            if (!l_byp[rr])
+              w = column_word(cols[g], l_rej[rr], l_mut[rr], init, l_vw + rr * t.vw_stride, blob, cidx, gs, kSlotThreads);
+            out[(r0 + rr) * npol + t.col0 + g] = w;
+          }
         }
       }
     }
@@ -813,28 +880,23 @@ __global__ void __launch_bounds__(kSlotThreads)
 }
 
 // Tiles whose entity counts or string bytes exceed the LDS capacities (listed by the host with the
-// tile descriptors in `overflow`: count, then tile indices). Rare by construction (capacities carry 1.5x
-// headroom over the batch average); the masks of such a tile are classified into the global mask
-// arrays with the DFA chains read from the blob, then every (row, policy) pair is evaluated from
-// global memory.
+// tile descriptors in `overflow`: count, then tile indices; the capacities are a high quantile of the
+// batch's tiles, so the list is a short tail). Two launches: overflow_classify_kernel classifies the
+// strings of those tiles into the global mask arrays (DFA chains read from the blob, one workgroup
+// per tile), then overflow_eval_kernel evaluates every (row, column) pair of them from global
+// memory, one lane per pair.
 constexpr int kOverflowThreads = 256;
 __global__ void __launch_bounds__(kOverflowThreads)
-    overflow_kernel(EvalArgs a, const TileArgs* __restrict__ tp, const uint32_t* __restrict__ overflow) {
-  __shared__ uint16_t gstk[kMaxGroupStack * kOverflowThreads];
+    overflow_classify_kernel(EvalArgs a, const TileArgs* __restrict__ tp, const uint32_t* __restrict__ overflow) {
   const TileArgs& t = *tp;
   const uint32_t count = overflow[0];
-  if (blockIdx.x >= count) return;
-  const DevHeader H = *(const DevHeader*)a.blob;
-  const DevPolicy* __restrict__ pols = (const DevPolicy*)(a.blob + H.policy_off);
-  const uint32_t tid = threadIdx.x, lane = tid & 63u;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), nwaves = kOverflowThreads / 64;
+  const uint32_t tid = threadIdx.x;
   Chain ch[NMASK];
 #pragma unroll
   for (int k = 0; k < (int)NMASK; ++k) {
     ch[k].head = t.dfa_head[k];
     ch[k].base = a.blob + t.dfa_head[k];
   }
-  const uint32_t npol = a.npol;
   for (uint32_t q = blockIdx.x; q < count; q += gridDim.x) {
     const uint64_t r0 = (uint64_t)overflow[1 + q] * t.rows;
     const uint32_t nr = (uint32_t)min((uint64_t)t.rows, a.nrows - r0);
@@ -877,17 +939,28 @@ __global__ void __launch_bounds__(kOverflowThreads)
     if (a.m[M_LV])
       for (uint32_t i = lb + tid; i < le; i += kOverflowThreads)
         ((uint64_t*)a.m[M_LV])[i] = classify_one<M_LV>(ch[M_LV], t.s_bytes[M_LV], t.s_off[M_LV][i], t.s_off[M_LV][i + 1]);
-    __threadfence();
-    __syncthreads();
-    GlobalSrc src{&a};
-    const uint32_t chunks = (nr + 63) / 64;
-    for (uint32_t item = wave; item < npol * chunks; item += nwaves) {
-      const uint32_t j = __builtin_amdgcn_readfirstlane(item / chunks);
-      const uint32_t rr = (item - j * chunks) * 64 + lane;
-      const DevPolicy& P = pols[a.pols[j]];
-      if (rr < nr) a.out[(r0 + rr) * npol + j] = verdict(src, a, H, pols, P, r0 + rr, gstk + tid, kOverflowThreads);
-    }
-    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(kOverflowThreads)
+    overflow_eval_kernel(EvalArgs a, const TileArgs* __restrict__ tp, const uint32_t* __restrict__ overflow) {
+  __shared__ uint16_t gstk[kMaxGroupStack * kOverflowThreads];
+  const TileArgs& t = *tp;
+  const uint32_t count = overflow[0];
+  const DevHeader H = *(const DevHeader*)a.blob;
+  const DevPolicy* __restrict__ pols = (const DevPolicy*)(a.blob + H.policy_off);
+  const uint32_t npol = a.npol, rows = t.rows;
+  const uint64_t items = (uint64_t)count * rows * npol;
+  GlobalSrc src{&a};
+  for (uint64_t it = (uint64_t)blockIdx.x * kOverflowThreads + threadIdx.x; it < items;
+       it += (uint64_t)gridDim.x * kOverflowThreads) {
+    const uint32_t j = (uint32_t)(it % npol);
+    const uint64_t qr = it / npol;
+    const uint32_t rr = (uint32_t)(qr % rows), q = (uint32_t)(qr / rows);
+    const uint64_t r = (uint64_t)overflow[1 + q] * rows + rr;
+    if (r >= a.nrows) continue;
+    const DevPolicy& P = pols[a.pols[j]];
+    a.out[r * npol + j] = verdict(src, a, H, pols, P, r, gstk + threadIdx.x, kOverflowThreads);
   }
 }
 
@@ -933,8 +1006,11 @@ hipError_t launch_evaluate_slots(const EvalArgs& a, const TileArgs& t, const Til
 hipError_t launch_overflow(const EvalArgs& a, const TileArgs* d_t, const uint32_t* d_overflow, uint32_t n_overflow,
                            hipStream_t s) {
   if (n_overflow == 0 || a.nrows == 0 || a.npol == 0) return hipSuccess;
-  hipLaunchKernelGGL(overflow_kernel, dim3(std::min<uint32_t>(n_overflow, 512)), dim3(kOverflowThreads), 0, s, a, d_t,
-                     d_overflow);
+  hipLaunchKernelGGL(overflow_classify_kernel, dim3(std::min<uint32_t>(n_overflow, 1024)), dim3(kOverflowThreads), 0, s,
+                     a, d_t, d_overflow);
+  const uint64_t items = (uint64_t)n_overflow * kSlotRows * a.npol;
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((items + kOverflowThreads - 1) / kOverflowThreads, 4096);
+  hipLaunchKernelGGL(overflow_eval_kernel, dim3(blocks), dim3(kOverflowThreads), 0, s, a, d_t, d_overflow);
   return hipGetLastError();
 }
 

@@ -61,13 +61,19 @@ struct TileArgs {
   uint32_t rows;                  // requests per tile (kSlotRows)
   uint32_t cmax, kmax, lmax;      // container / capability / label capacity of a staged tile
   uint32_t o_rf, o_coff, o_loff, o_cflags, o_cadd, o_cdrop, o_gstk;  // LDS byte offsets
-  uint32_t o_m[NMASK];            // LDS byte offset of each staged mask array, 0 = not read
+  uint32_t o_m[NMASK];            // LDS byte offset of each staged per-string array, 0 = not read: u8 pattern
+                                  // index (0xff none) for NS / CAPADD / CAPDROP / LK, u64 masks for
+                                  // REG / TAG / IMG, u64 violation sets for AA; LV is never staged
+  uint32_t o_vadd, o_vl;          // u64 violation set per added capability; u64[2] (vden, vcon) per label
   uint32_t o_rej, o_mut, o_byp;   // per-request walk results: rejected / mutated slots, bypass flag
   uint32_t o_sa;                  // u32[NMASK]: the tile's staged byte start per string column (TileDesc.sa)
   uint32_t o_vw, vw_stride;       // violation words [rows][vw_stride] (aliases the staged strings)
   uint32_t o_slot, slot_bytes;    // staged SlotHdr record of this chunk
   uint32_t col0, ncols, vec4;     // output columns [col0, col0 + ncols); vec4: 16-B verdict stores
   const uint8_t* slot_plan;       // device copy of this chunk's SlotHdr record
+  uint32_t o_cols_rec, o_cidx_rec;  // ColInfo / cidx sections of the record (global reads in P3)
+  uint32_t p3_item, pad_p3;       // P3 form: 0 = one lane per request, 1 = (request, 4 columns) items
+  uint64_t slot_init;             // SlotHdr.init of this chunk
   uint32_t chain_len[NMASK];      // DFAs in the chain of each mask's column (1 when absent)
   uint32_t mask_cap[NMASK];       // entries of each staged mask array
   uint32_t debug;                 // diagnostics: bit0 skip classification, bit1 skip walk, bit2 skip output

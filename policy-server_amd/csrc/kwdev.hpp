@@ -47,6 +47,7 @@ enum GOp : uint8_t { G_CONST0 = 0, G_CONST1 = 1, G_CALL = 2, G_NOT = 3, G_AND = 
 constexpr int kMaxGroupStack = 16;
 constexpr int kMaxGroupMembers = 16;
 constexpr int kMaxListIdx = 16;
+constexpr size_t kKvDfaBytes = 3072;  // table bytes of one per-key label-value DFA before the key chains
 
 struct alignas(16) DevDfa {
   uint32_t nstates, ncls, start, trans_off;  // trans_off: blob offset of u16 [nstates][ncls]
@@ -110,8 +111,9 @@ struct alignas(16) DevHeader {
   uint32_t magic, version, npolicies, blob_bytes;
   uint32_t dfa_off[NCOL];  // head of the column's DFA chain, 0 = no patterns for this column
   uint32_t lit_off[NCOL];  // DevLit record of an all-literal column, 0 = none
-  // per-key label-value DFAs: region = u32 idx[64] (region-relative offset of the DevDfa for
-  // label-key bit k over the value regexes constrained on that key, 0 = none) + the DFAs
+  // per-key label-value DFAs: region = u32 idx[64] (region-relative offset of the first DevDfa for
+  // label-key bit k over the value regexes constrained on that key, 0 = none) + the DFAs; a key's
+  // DFAs form a chain through DevDfa.next (region-relative here, 0 = last)
   uint32_t kv_off, kv_bytes;  // 0 = none (the COL_LV chain is used)
   int32_t bypass_bit;      // COL_NS bit of the always-accept namespace, -1 = none
   uint32_t policy_off;     // DevPolicy[npolicies]

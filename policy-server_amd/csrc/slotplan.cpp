@@ -3,7 +3,6 @@
 
 #include <cstring>
 #include <map>
-#include <tuple>
 
 namespace kw {
 
@@ -12,7 +11,8 @@ namespace {
 struct Builder {
   SlotHdr h;
   uint64_t tab[NST][kSlots];
-  std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint64_t> constr;  // (key bit, value bit, idx) -> slots
+  std::map<std::pair<uint32_t, uint32_t>, uint64_t> constr;  // (key bit, value bit) -> slots
+  uint8_t cidx[kSlots][64];
   uint8_t mand[kSlots][16];
   std::vector<ColInfo> cols;
   uint32_t nslots = 0;
@@ -22,6 +22,7 @@ struct Builder {
     memset(&h, 0, sizeof(h));
     memset(tab, 0, sizeof(tab));
     memset(mand, 0xff, sizeof(mand));
+    memset(cidx, 0xff, sizeof(cidx));
   }
 
   static void each_bit(uint64_t m, uint64_t* t, uint64_t bit) {
@@ -78,7 +79,11 @@ struct Builder {
       case FAM_LABELS:
         h.lbl |= bit;
         each_bit(P.m[0], tab[ST_DENY], bit);
-        for (uint32_t k = 0; k < P.n_constr && k < 16; ++k) constr[{P.idx[16 + k], P.idx[32 + k], k}] |= bit;
+        for (uint32_t k = 0; k < P.n_constr && k < 16; ++k) {
+          const uint32_t kb = P.idx[16 + k] & 63u;
+          constr[{kb, P.idx[32 + k] & 63u}] |= bit;
+          cidx[s][kb] = (uint8_t)k;
+        }
         for (uint32_t k = 0; k < P.n_mand && k < 16; ++k) {
           tab[ST_MAND][P.idx[k] & 63u] |= bit;
           h.mand_union |= 1ull << (P.idx[k] & 63u);
@@ -100,13 +105,12 @@ struct Builder {
     std::vector<ConstrEnt> ce;
     uint32_t k0 = 0;
     for (auto& [key, slots] : constr) {  // sorted by key bit
-      const uint32_t kb = std::get<0>(key) & 63u;
+      const uint32_t kb = key.first;
       while (k0 <= kb) h.ce_off[k0++] = (uint16_t)ce.size();
       ConstrEnt e;
       memset(&e, 0, sizeof(e));
       e.slots = slots;
-      e.vbit = std::get<1>(key) & 63u;
-      e.idx = std::get<2>(key);
+      e.vbit = key.second;
       ce.push_back(e);
     }
     while (k0 <= kSlots) h.ce_off[k0++] = (uint16_t)ce.size();
@@ -122,6 +126,12 @@ struct Builder {
     h.o_cols = off;
     off += (uint32_t)(cols.size() * sizeof(ColInfo));
     off = (off + 15u) & ~15u;
+    h.o_cidx = 0;
+    if (h.lbl) {
+      h.o_cidx = off;
+      off += nslots * 64u;
+      off = (off + 15u) & ~15u;
+    }
     h.ncols = (uint32_t)cols.size();
     h.nslots = nslots;
     h.nce = (uint32_t)ce.size();
@@ -133,6 +143,7 @@ struct Builder {
     if (!ce.empty()) memcpy(rec.data() + h.o_ce, ce.data(), ce.size() * sizeof(ConstrEnt));
     if (h.lbl) memcpy(rec.data() + h.o_mand, mand, sizeof(mand));
     if (!cols.empty()) memcpy(rec.data() + h.o_cols, cols.data(), cols.size() * sizeof(ColInfo));
+    if (h.lbl) memcpy(rec.data() + h.o_cidx, cidx, (size_t)nslots * 64u);
     return rec;
   }
 };
@@ -195,6 +206,8 @@ Status build_slot_chunks(const Env& E, const int32_t* pols, uint32_t npol, int o
     ch.nslots = b.nslots;
     ch.groups = b.groups;
     ch.rec = b.emit();
+    const SlotHdr* sh = (const SlotHdr*)ch.rec.data();
+    ch.staged = sh->o_cidx ? sh->o_cidx : sh->bytes;
     out->push_back(std::move(ch));
   }
   return {};

@@ -55,7 +55,7 @@ struct alignas(16) SlotHdr {
   uint64_t reqd_union, defa_union, mand_union;  // pattern bits some slot lists (COL_CAP, COL_CAP, COL_LK)
   uint64_t cap_all;         // COL_CAP bit of "ALL" (0 = none)
   uint32_t ncols, nslots, nce, bytes;    // bytes: whole record (multiple of 16)
-  uint32_t o_ce, o_mand, o_cols, pad0;   // byte offsets of the sections from the record start
+  uint32_t o_ce, o_mand, o_cols, o_cidx;  // byte offsets of the sections from the record start
   uint16_t tab_off[NST];        // byte offset of table k from the record start (0 = not emitted)
   uint16_t ce_off[kSlots + 1];  // constraint entries of label-key bit k: [ce_off[k], ce_off[k+1])
   uint16_t pad1[1];
@@ -63,10 +63,10 @@ struct alignas(16) SlotHdr {
 static_assert(sizeof(SlotHdr) == 336, "SlotHdr layout");
 
 // safe-labels constrained_labels: the slots that constrain label-key bit k with value pattern
-// `vbit` as their idx-th constraint (settings order).
+// `vbit` (the settings index of each slot's constraint on k is in the cidx section).
 struct alignas(16) ConstrEnt {
   uint64_t slots;
-  uint32_t vbit, idx;
+  uint32_t vbit, pad;
 };
 
 enum ColKind : uint32_t { CK_CONST = 0, CK_PLAIN = 1, CK_GROUP = 2 };
@@ -81,8 +81,11 @@ struct alignas(16) ColInfo {
 };
 static_assert(sizeof(ColInfo) == 32, "ColInfo layout");
 
-// Record: SlotHdr | emitted tables u64[64] | ConstrEnt ce[nce] | u8 mand[nslots][16] | ColInfo[ncols]
+// Record: SlotHdr | emitted tables u64[64] | ConstrEnt ce[nce] | u8 mand[64][16] | ColInfo[ncols]
+//         | u8 cidx[nslots][64]
 // mand[s]: the label-key bits of slot s's mandatory_labels in settings order, 0xff-terminated.
+// cidx[s][k]: settings index of slot s's constraint on label-key bit k (read only to format a
+// constraint violation; the device keeps it out of LDS and reads it from the global copy).
 
 KW_HD inline uint32_t kw_ctz64(uint64_t x) { return (uint32_t)__builtin_ctzll(x); }
 KW_HD inline uint32_t pack2(uint32_t a, uint32_t b) { return ((a < 255u ? a : 255u) << 8) | (b < 255u ? b : 255u); }
@@ -151,6 +154,30 @@ struct SlotView {
   KW_HD const ColInfo* cols() const { return (const ColInfo*)(base + h->o_cols); }
 };
 
+// ---- per-entity violation sets, derived entity-parallel before the walks (the walks then only
+// apply the first-violation order): an added capability violates the strict psp-capabilities slots
+// that allow none of its pattern bits, an AppArmor profile the psp-apparmor slots that do not allow
+// it, a label the safe-labels slots that deny its key (vden) or whose constraint on the key its
+// value fails (vcon).
+KW_HD inline uint64_t derive_capadd(const SlotView& sv, uint64_t m) {
+  return sv.h->caps_strict ? tab_and(sv.tab(ST_NA_CAP), m, sv.h->caps_strict) : 0ull;
+}
+KW_HD inline uint64_t derive_apparmor(const SlotView& sv, uint64_t m) {
+  return sv.h->aa ? tab_and(sv.tab(ST_NA_AA), m, sv.h->aa) : 0ull;
+}
+KW_HD inline void derive_label(const SlotView& sv, uint64_t km, uint64_t vm, uint64_t* vden, uint64_t* vcon) {
+  uint64_t d = 0, c = 0;
+  if (km && sv.h->lbl) {
+    const uint32_t kb = kw_ctz64(km);  // label keys are literal patterns: at most one bit
+    d = sv.tab(ST_DENY)[kb];
+    const ConstrEnt* ce = sv.ce();
+    for (uint32_t e = sv.h->ce_off[kb]; e < sv.h->ce_off[kb + 1]; ++e)
+      if (!((vm >> ce[e].vbit) & 1ull)) c |= ce[e].slots;
+  }
+  *vden = d;
+  *vcon = c;
+}
+
 // ---- walk A: pod-privileged + psp-capabilities (validation, then mutation), containers in order.
 // Returns the rejected slots; *mut_out gets the mutated-and-not-rejected psp-capabilities slots.
 template <class S>
@@ -176,9 +203,8 @@ KW_HD uint64_t walk_privileged_caps(const S& src, const SlotView& sv, uint64_t r
         const uint32_t k0 = src.cadd(c), k1 = src.cadd(c + 1);
         uint64_t addm = 0, dropm = 0;
         for (uint32_t k = k0; k < k1; ++k) {
-          const uint64_t m = src.template m<M_CAPADD>(k);
-          addm |= m;
-          const uint64_t nw = tab_and(sv.tab(ST_NA_CAP), m, h.caps_strict) & ~rej;
+          addm |= src.template m<M_CAPADD>(k);
+          const uint64_t nw = src.vadd(k) & ~rej;
           if (nw) {
             put_viol(vw, nw, vword(KW_R_CAP_NOT_ALLOWED, pack2(ci, k - k0)));
             rej |= nw;
@@ -206,7 +232,7 @@ KW_HD uint64_t walk_apparmor_images(const S& src, const SlotView& sv, uint64_t r
       const uint32_t ci = c - cb;
       const uint32_t fl = src.cflags(c);
       if (h.aa && (fl & KW_CTR_HAS_APPARMOR)) {
-        const uint64_t nw = tab_and(sv.tab(ST_NA_AA), src.template m<M_AA>(c), h.aa) & ~rej;
+        const uint64_t nw = src.vaa(c) & ~rej;
         put_viol(vw, nw, vword(KW_R_APPARMOR, pack1(ci)));
         rej |= nw;
       }
@@ -234,7 +260,8 @@ KW_HD uint64_t walk_apparmor_images(const S& src, const SlotView& sv, uint64_t r
 }
 
 // ---- walk C: safe-labels (denied, then constrained, label by label in object order; then the
-// first missing mandatory key).
+// first missing mandatory key). A constraint violation carries the label-key bit in its low byte
+// until column_word resolves the slot's settings index (cidx).
 template <class S>
 KW_HD uint64_t walk_labels(const S& src, const SlotView& sv, uint64_t r, uint32_t* vw) {
   const SlotHdr& h = *sv.h;
@@ -247,25 +274,15 @@ KW_HD uint64_t walk_labels(const S& src, const SlotView& sv, uint64_t r, uint32_
     if (!km) continue;
     present |= km;
     const uint32_t li = l - lb;
-    const uint32_t kb = kw_ctz64(km);  // label keys are literal patterns: at most one bit
-    uint64_t nw = sv.tab(ST_DENY)[kb] & ~rej;
+    uint64_t nw = src.vden(l) & ~rej;
     if (nw) {
       put_viol(vw, nw, vword(KW_R_LABEL_DENIED, pack1(li)));
       rej |= nw;
     }
-    const uint32_t e0 = h.ce_off[kb], e1 = h.ce_off[kb + 1];
-    if (e0 != e1) {
-      const uint64_t vm = src.template m<M_LV>(l);
-      const ConstrEnt* ce = sv.ce();
-      for (uint32_t e = e0; e < e1; ++e) {
-        const ConstrEnt x = ce[e];
-        if ((vm >> x.vbit) & 1ull) continue;
-        nw = x.slots & ~rej;
-        if (nw) {
-          put_viol(vw, nw, vword(KW_R_LABEL_CONSTRAINT, pack2(li, x.idx)));
-          rej |= nw;
-        }
-      }
+    nw = src.vcon(l) & ~rej;
+    if (nw) {
+      put_viol(vw, nw, vword(KW_R_LABEL_CONSTRAINT, pack2(li, 0)) | kw_ctz64(km));
+      rej |= nw;
     }
   }
   uint64_t nw = tab_or(sv.tab(ST_MAND), h.mand_union & ~present) & ~rej;
@@ -344,11 +361,17 @@ KW_HD inline bool run_group_prog(const uint8_t* prog, uint32_t len, uint32_t ok,
 }
 
 // Verdict word of one output column for one request. rej / mut: the request's rejected and mutated
-// slots; vw: its violation words (valid where rej is set); blob: the compiled tables (programs).
+// slots; vw: its violation words (valid where rej is set); blob: the compiled tables (programs);
+// cidx: the record's cidx section.
 KW_HD inline uint32_t column_word(const ColInfo& ci, uint64_t rej, uint64_t mut, uint64_t init, const uint32_t* vw,
-                                  const uint8_t* blob, uint16_t* gstk, uint32_t gstride) {
+                                  const uint8_t* blob, const uint8_t* cidx, uint16_t* gstk, uint32_t gstride) {
   if (ci.kind == CK_PLAIN) {
-    if ((rej >> ci.slot) & 1ull) return ci.rejb | vw[ci.slot];
+    if ((rej >> ci.slot) & 1ull) {
+      uint32_t w = vw[ci.slot];
+      if (((w >> 8) & 0xffu) == KW_R_LABEL_CONSTRAINT)  // key bit -> the slot's settings index
+        w = (w & ~0xffu) | ((uint32_t)cidx[ci.slot * 64u + (w & 63u)] << 16);
+      return ci.rejb | w;
+    }
     return ((mut >> ci.slot) & 1ull) ? ci.mutw : ci.okw;
   }
   if (ci.kind == CK_GROUP) {
