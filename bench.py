@@ -146,7 +146,7 @@ def traffic(args):
     written by scripts/pmc_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
     of this bench, FETCH_SIZE doubled per the gfx950 calibration). None when absent or measured on a
     different workload."""
-    path = os.path.join(ROOT, "profiles", "traffic.json")
+    path = os.path.join(ROOT, "profiles", "traffic.json")  # written by scripts/pmc.sh (copied from the GPU box)
     try:
         with open(path) as f:
             t = json.load(f)

@@ -76,7 +76,7 @@ struct DeviceBatch {
   uint64_t desc_key = 0;
   // slot-kernel tile capacities of this batch (plan_pass)
   bool stats_valid = false;
-  TileStats stats;
+  TileStats stats, stats_max;
   ~DeviceBatch() {
     if (device >= 0) (void)hipSetDevice(device);
     (void)hipFree(d_tiles);
@@ -215,12 +215,12 @@ constexpr uint32_t kTileLdsBudget = 160 * 1024;  // slot-kernel LDS per workgrou
 
 const StrCol& host_strings(const Batch& B, int m);
 
-TileStats tile_stats(const Batch& B, uint32_t rows) {
+TileStats tile_stats(const Batch& B, uint32_t rows, double quantile) {
   TileStats st;
   const uint64_t ntiles = (B.n + rows - 1) / rows;
   if (!ntiles) return st;
   std::vector<uint32_t> v(ntiles);
-  const uint64_t q = ntiles < 2000 ? ntiles - 1 : (uint64_t)(0.9995 * (double)(ntiles - 1));
+  const uint64_t q = ntiles < 2000 ? ntiles - 1 : (uint64_t)(quantile * (double)(ntiles - 1));
   auto quant = [&](auto f) {
     for (uint64_t t = 0; t < ntiles; ++t) v[t] = f(t * rows, std::min<uint64_t>(B.n, (t + 1) * rows));
     std::nth_element(v.begin(), v.begin() + (long)q, v.end());
@@ -405,10 +405,10 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
   TileArgs& T = plan->tile;
   auto align = [](uint32_t x) { return (x + 15u) & ~15u; };
   if (!D.stats_valid) {
-    D.stats = tile_stats(B, kSlotRows);
+    D.stats = tile_stats(B, kSlotRows, 0.9995);
+    D.stats_max = tile_stats(B, kSlotRows, 1.0);
     D.stats_valid = true;
   }
-  const TileStats& ts = D.stats;
   uint32_t chain_len[NMASK];  // per-string masks are whole-chain results (image chains walk in one item)
   for (int m = 0; m < (int)NMASK; ++m) chain_len[m] = 1;
   uint32_t slot_bytes = 16, nslots = 1;
@@ -420,127 +420,136 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
   }
   const uint32_t rows = kSlotRows;
   const uint32_t vw_stride = nslots | 1u;  // odd stride: lanes (requests) spread over the banks
-  double scale = 1.0;  // shrunk only when the quantile capacities exceed the LDS budget
-  for (;;) {
-    uint32_t cmax = (uint32_t)std::max(1.0, scale * ts.ctr);
-    uint32_t kmax = (uint32_t)std::max(1.0, scale * std::max(ts.kadd, ts.kdrop));
-    uint32_t lmax = (uint32_t)std::max(1.0, scale * ts.lbl);
-    uint32_t off = 16;
-    const uint32_t stage_at = off;
-    if (plan->fused) off = align(off + table_bytes);
-    T.o_slot = off;
-    off = align(off + slot_bytes);
-    T.o_rf = off;
-    off = align(off + rows);
-    T.o_coff = off;
-    off = align(off + (rows + 1) * 4);
-    T.o_loff = off;
-    off = align(off + (rows + 1) * 4);
-    T.o_cflags = off;
-    off = align(off + cmax + 8);  // staged from the dword holding the first flag
-    T.o_cadd = off;
-    off = align(off + (cmax + 1) * 4);
-    T.o_cdrop = off;
-    off = align(off + (cmax + 1) * 4);
-    for (int m = 0; m < (int)NMASK; ++m) {
-      T.o_m[m] = 0;
-      if (!use[m] || m == M_LV) continue;  // label values: derived into o_vl in P1, never staged
-      const uint32_t cnt = m == M_NS ? rows : (m == M_CAPADD || m == M_CAPDROP) ? kmax : m == M_LK ? lmax : cmax;
-      const bool lit = m == M_NS || m == M_CAPADD || m == M_CAPDROP || m == M_LK;
-      T.o_m[m] = off;
-      T.mask_cap[m] = cnt;
-      off = align(off + cnt * (lit ? 1u : 8u));
-    }
-    T.o_vadd = T.o_vl = 0;
-    if (use[M_CAPADD]) {
-      T.o_vadd = off;
-      off = align(off + kmax * 8);
-    }
-    if (use[M_LK]) {
-      T.o_vl = off;
-      off = align(off + lmax * 16);
-    }
-    T.o_rej = off;
-    off = align(off + rows * 8);
-    T.o_mut = off;
-    off = align(off + rows * 8);
-    T.o_byp = off;
-    off = align(off + rows);
-    T.o_sa = off;
-    off = align(off + NMASK * 4);
-    T.o_gstk = 0;
-    if (groups) {
-      T.o_gstk = off;
-      off = align(off + kMaxGroupStack * kSlotThreads * 2);
-    }
-    // union: the staged strings (P0-P1) and the violation words (P2-P3)
-    const uint32_t u0 = off;
-    uint32_t su = u0;
-    for (int m = 0; m < (int)NMASK; ++m) T.o_so[m] = T.o_sb[m] = T.sb_cap[m] = 0;
-    if (plan->fused)
-      for (int m : {M_NS, M_IMG, M_AA, M_CAPADD, M_CAPDROP, M_LK, M_LV}) {
-        const bool needm = m == M_IMG ? (use[M_REG] || use[M_TAG] || use[M_IMG]) : use[m];
-        if (!needm) continue;
-        const DeviceBatch::DCol& sc = mask_strings(D, m);
-        const uint32_t cnt = m == M_NS ? rows : (m == M_CAPADD || m == M_CAPDROP) ? kmax : (m == M_LK || m == M_LV) ? lmax : cmax;
-        T.o_so[m] = su;
-        su = align(su + (cnt + 1) * 4);
-        (void)sc;
-        T.sb_cap[m] = align((uint32_t)std::min(16384.0, scale * ts.bytes[m]));  // longer tiles take the overflow path
-        T.o_sb[m] = su;
-        su = align(su + T.sb_cap[m] + 16);  // slack: dword reads may run <= 7 bytes past a string
+  // LDS layout for capacities `ts` (shrunk by `scale` only when over the budget); returns the bytes
+  auto layout = [&](const TileStats& ts) -> uint32_t {
+    memset(&T, 0, sizeof(T));
+    double scale = 1.0;
+    for (;;) {
+      uint32_t cmax = (uint32_t)std::max(1.0, scale * ts.ctr);
+      uint32_t kmax = (uint32_t)std::max(1.0, scale * std::max(ts.kadd, ts.kdrop));
+      uint32_t lmax = (uint32_t)std::max(1.0, scale * ts.lbl);
+      uint32_t off = 16;
+      const uint32_t stage_at = off;
+      if (plan->fused) off = align(off + table_bytes);
+      T.o_slot = off;
+      off = align(off + slot_bytes);
+      T.o_rf = off;
+      off = align(off + rows);
+      T.o_coff = off;
+      off = align(off + (rows + 1) * 4);
+      T.o_loff = off;
+      off = align(off + (rows + 1) * 4);
+      T.o_cflags = off;
+      off = align(off + cmax + 8);  // staged from the dword holding the first flag
+      T.o_cadd = off;
+      off = align(off + (cmax + 1) * 4);
+      T.o_cdrop = off;
+      off = align(off + (cmax + 1) * 4);
+      for (int m = 0; m < (int)NMASK; ++m) {
+        T.o_m[m] = 0;
+        if (!use[m] || m == M_LV) continue;  // label values: derived into o_vl in P1, never staged
+        const uint32_t cnt = m == M_NS ? rows : (m == M_CAPADD || m == M_CAPDROP) ? kmax : m == M_LK ? lmax : cmax;
+        const bool lit = m == M_NS || m == M_CAPADD || m == M_CAPDROP || m == M_LK;
+        T.o_m[m] = off;
+        T.mask_cap[m] = cnt;
+        off = align(off + cnt * (lit ? 1u : 8u));
       }
-    T.o_vw = u0;
-    T.vw_stride = vw_stride;
-    off = std::max(su, align(u0 + rows * vw_stride * 4));
-    if (off > kTileLdsBudget && scale > 0.1) {
-      scale *= 0.8;
-      continue;
-    }
-    T.rows = rows;
-    T.cmax = cmax;
-    T.kmax = kmax;
-    T.lmax = lmax;
-    T.lds_bytes = off;
-    // column chains and strings (the overflow kernel reads them in both modes)
-    for (int m = 0; m < (int)NMASK; ++m) {
-      if (!use[m]) continue;
-      T.dfa_head[m] = H->dfa_off[mask_col(m)];
-      const DeviceBatch::DCol& sc = mask_strings(D, m);
-      T.s_off[m] = sc.off;
-      T.s_bytes[m] = sc.bytes;
-    }
-    // column tables staged once per workgroup (fused)
-    if (plan->fused) {
-      uint32_t at = stage_at;
-      uint32_t col_at[NCOL] = {};
-      bool staged[NCOL] = {};
+      T.o_vadd = T.o_vl = 0;
+      if (use[M_CAPADD]) {
+        T.o_vadd = off;
+        off = align(off + kmax * 8);
+      }
+      if (use[M_LK]) {
+        T.o_vl = off;
+        off = align(off + lmax * 16);
+      }
+      T.o_rej = off;
+      off = align(off + rows * 8);
+      T.o_mut = off;
+      off = align(off + rows * 8);
+      T.o_byp = off;
+      off = align(off + rows);
+      T.o_sa = off;
+      off = align(off + NMASK * 4);
+      T.o_gstk = 0;
+      if (groups) {
+        T.o_gstk = off;
+        off = align(off + kMaxGroupStack * kSlotThreads * 2);
+      }
+      // union: the staged strings (P0-P1) and the violation words (P2-P3)
+      const uint32_t u0 = off;
+      uint32_t su = u0;
+      for (int m = 0; m < (int)NMASK; ++m) T.o_so[m] = T.o_sb[m] = T.sb_cap[m] = 0;
+      if (plan->fused)
+        for (int m : {M_NS, M_IMG, M_AA, M_CAPADD, M_CAPDROP, M_LK, M_LV}) {
+          const bool needm = m == M_IMG ? (use[M_REG] || use[M_TAG] || use[M_IMG]) : use[m];
+          if (!needm) continue;
+          const DeviceBatch::DCol& sc = mask_strings(D, m);
+          const uint32_t cnt = m == M_NS ? rows : (m == M_CAPADD || m == M_CAPDROP) ? kmax : (m == M_LK || m == M_LV) ? lmax : cmax;
+          T.o_so[m] = su;
+          su = align(su + (cnt + 1) * 4);
+          (void)sc;
+          T.sb_cap[m] = align((uint32_t)std::min(16384.0, scale * ts.bytes[m]));  // longer tiles take the overflow path
+          T.o_sb[m] = su;
+          su = align(su + T.sb_cap[m] + 16);  // slack: dword reads may run <= 7 bytes past a string
+        }
+      T.o_vw = u0;
+      T.vw_stride = vw_stride;
+      off = std::max(su, align(u0 + rows * vw_stride * 4));
+      if (off > kTileLdsBudget && scale > 0.1) {
+        scale *= 0.8;
+        continue;
+      }
+      T.rows = rows;
+      T.cmax = cmax;
+      T.kmax = kmax;
+      T.lmax = lmax;
+      T.lds_bytes = off;
+      // column chains and strings (the overflow kernel reads them in both modes)
       for (int m = 0; m < (int)NMASK; ++m) {
         if (!use[m]) continue;
-        Col c = mask_col(m);
-        if (!staged[c]) {
-          staged[c] = true;
-          col_at[c] = at;
-          uint32_t bo;
-          const uint32_t nb = stage_rec(m, &bo);
-          T.stage_blob[T.nstage] = bo;
-          T.stage_lds[T.nstage] = at;
-          T.stage_bytes[T.nstage] = nb;
-          at += nb;
-          ++T.nstage;
-        }
-        if (lit_of(m)) {
-          T.lit_lds[m] = col_at[c];
-        } else if (m == M_LV && kv) {
-          T.kv_lds = col_at[c];
-          T.kv_blob = H->kv_off;
-        } else {
-          T.dfa_lds[m] = col_at[c];
+        T.dfa_head[m] = H->dfa_off[mask_col(m)];
+        const DeviceBatch::DCol& sc = mask_strings(D, m);
+        T.s_off[m] = sc.off;
+        T.s_bytes[m] = sc.bytes;
+      }
+      // column tables staged once per workgroup (fused)
+      if (plan->fused) {
+        uint32_t at = stage_at;
+        uint32_t col_at[NCOL] = {};
+        bool staged[NCOL] = {};
+        for (int m = 0; m < (int)NMASK; ++m) {
+          if (!use[m]) continue;
+          Col c = mask_col(m);
+          if (!staged[c]) {
+            staged[c] = true;
+            col_at[c] = at;
+            uint32_t bo;
+            const uint32_t nb = stage_rec(m, &bo);
+            T.stage_blob[T.nstage] = bo;
+            T.stage_lds[T.nstage] = at;
+            T.stage_bytes[T.nstage] = nb;
+            at += nb;
+            ++T.nstage;
+          }
+          if (lit_of(m)) {
+            T.lit_lds[m] = col_at[c];
+          } else if (m == M_LV && kv) {
+            T.kv_lds = col_at[c];
+            T.kv_blob = H->kv_off;
+          } else {
+            T.dfa_lds[m] = col_at[c];
+          }
         }
       }
+      break;
     }
-    break;
-  }
+    return T.lds_bytes;
+  };
+  // the batch maximum when it costs no occupancy over the high quantile (no overflow tiles at all)
+  auto per_cu = [](uint32_t b) { return std::min<uint32_t>(2048 / kSlotThreads, (160 * 1024) / std::max<uint32_t>(b, 1)); };
+  const uint32_t lq = layout(D.stats);
+  if (per_cu(layout(D.stats_max)) < per_cu(lq)) layout(D.stats);
   if (T.lds_bytes > kTileLdsBudget) return KW_E_ARG;  // policy set too large for one tile
   if (const char* dbg = getenv("KW_TILE_DEBUG")) T.debug = (uint32_t)atoi(dbg);  // phase ablation (diagnostics)
   if (T.debug & 256u)
@@ -563,8 +572,8 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
     }
   }
   // per-chunk TileArgs (slot_plan pointers are filled in at upload, run_pass)
-  const char* p3env = getenv("KW_P3");
-  const uint32_t p3_item = (p3env && std::string(p3env) == "item") ? 1u : 0u;
+  const char* p3env = getenv("KW_P3");  // A/B of the verdict-store form (default: items)
+  const uint32_t p3_item = (p3env && std::string(p3env) == "lane") ? 0u : 1u;
   plan->tiles.clear();
   plan->slot_at.clear();
   plan->slot_blob.clear();
@@ -585,8 +594,8 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
     plan->tiles.push_back(t);
   }
   uint64_t ntiles = (B.n + T.rows - 1) / T.rows;
-  uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(2048 / kSlotThreads, (160 * 1024) / std::max<uint32_t>(T.lds_bytes, 1)));
-  plan->grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ntiles, 256ull * per_cu));
+  uint32_t wg_per_cu = std::max<uint32_t>(1, std::min<uint32_t>(2048 / kSlotThreads, (160 * 1024) / std::max<uint32_t>(T.lds_bytes, 1)));
+  plan->grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ntiles, 256ull * wg_per_cu));
   return KW_OK;
 }
 

@@ -21,6 +21,6 @@ for p in "${PASSES[@]}"; do
   i=$((i+1))
 done
 cd "$ROOT"
-python3 scripts/pmc_summary.py --traffic "gpurun_out/${TAG}_pmc_0" "gpurun_out/${TAG}_pmc_1" profiles/traffic.json "$TAG" && \
+python3 scripts/pmc_summary.py --traffic "gpurun_out/${TAG}_pmc_0" "gpurun_out/${TAG}_pmc_1" "gpurun_out/${TAG}_traffic.json" "$TAG" && \
 python3 scripts/pmc_summary.py gpurun_out/${TAG}_pmc_0 gpurun_out/${TAG}_pmc_1 gpurun_out/${TAG}_pmc_2 gpurun_out/${TAG}_pmc_3 > "gpurun_out/${TAG}_pmc_summary.txt"
 echo "[pmc] done"
