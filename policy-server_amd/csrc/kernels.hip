@@ -626,6 +626,10 @@ __global__ void __launch_bounds__(kSlotThreads)
   SlotView sv;
   sv.h = (const SlotHdr*)(lds + t.o_slot);
   sv.base = lds + t.o_slot;
+  // the column records as four u32 arrays (kind | slot << 8, okw, mutw, rejb; slotplan.cpp emit):
+  // P3 items read the words of 4 consecutive columns with one conflict-free ds_read_b128 per array
+  const uint32_t* cs = (const uint32_t*)(sv.base + sv.h->o_csoa);
+  const uint32_t cs_n = (t.ncols + 3u) & ~3u;
 
   uint8_t* l_rf = lds + t.o_rf;
   uint32_t* l_coff = (uint32_t*)(lds + t.o_coff);
@@ -845,7 +849,7 @@ __global__ void __launch_bounds__(kSlotThreads)
           }
         }
       } else {
-        const ColInfo* cols = sv.cols();
+        const ColInfo* cols = (const ColInfo*)(t.slot_plan + t.o_cols_rec);  // global: group / constant columns
         if (t.vec4) {
           const uint32_t G = t.ncols >> 2;
           for (uint32_t it = tid; it < nr * G; it += kSlotThreads) {
@@ -856,10 +860,23 @@ __global__ void __launch_bounds__(kSlotThreads)
             } else {
               const uint64_t rej = l_rej[rr], mut = l_mut[rr];
               const uint32_t* vw = l_vw + rr * t.vw_stride;
-              w.x = column_word(cols[4 * g + 0], rej, mut, init, vw, blob, cidx, gs, kSlotThreads);
-              w.y = column_word(cols[4 * g + 1], rej, mut, init, vw, blob, cidx, gs, kSlotThreads);
-              w.z = column_word(cols[4 * g + 2], rej, mut, init, vw, blob, cidx, gs, kSlotThreads);
-              w.w = column_word(cols[4 * g + 3], rej, mut, init, vw, blob, cidx, gs, kSlotThreads);
+              const uint4 ks = *(const uint4*)(cs + 4 * g), ok = *(const uint4*)(cs + cs_n + 4 * g),
+                          mu = *(const uint4*)(cs + 2 * cs_n + 4 * g), rj = *(const uint4*)(cs + 3 * cs_n + 4 * g);
+              auto word = [&](uint32_t k, uint32_t okw, uint32_t mutw, uint32_t rejb, uint32_t j) -> uint32_t {
+                if ((k & 0xffu) != CK_PLAIN) return column_word(cols[j], rej, mut, init, vw, blob, cidx, gs, kSlotThreads);
+                const uint32_t s = k >> 8;
+                if ((rej >> s) & 1ull) {
+                  uint32_t v = vw[s];
+                  if (((v >> 8) & 0xffu) == KW_R_LABEL_CONSTRAINT)
+                    v = (v & ~0xffu) | ((uint32_t)cidx[s * 64u + (v & 63u)] << 16);
+                  return rejb | v;
+                }
+                return ((mut >> s) & 1ull) ? mutw : okw;
+              };
+              w.x = word(ks.x, ok.x, mu.x, rj.x, 4 * g + 0);
+              w.y = word(ks.y, ok.y, mu.y, rj.y, 4 * g + 1);
+              w.z = word(ks.z, ok.z, mu.z, rj.z, 4 * g + 2);
+              w.w = word(ks.w, ok.w, mu.w, rj.w, 4 * g + 3);
             }
             *(uint4*)(out + (r0 + rr) * npol + t.col0 + 4 * g) = w;
           }

@@ -123,6 +123,13 @@ struct Builder {
     off += (uint32_t)(ce.size() * sizeof(ConstrEnt));
     h.o_mand = h.lbl ? off : 0;
     if (h.lbl) off += sizeof(mand);
+    // the device stages everything up to o_cols: the column arrays are the staged form of the
+    // column records (P3 reads 4 columns per array with one 16-B LDS load); ColInfo and cidx stay
+    // in global memory (group / constant columns and constraint settings indices)
+    const uint32_t cs_n = ((uint32_t)cols.size() + 3u) & ~3u;
+    off = (off + 15u) & ~15u;
+    h.o_csoa = (uint16_t)off;
+    off += 16u * cs_n;
     h.o_cols = off;
     off += (uint32_t)(cols.size() * sizeof(ColInfo));
     off = (off + 15u) & ~15u;
@@ -143,6 +150,13 @@ struct Builder {
     if (!ce.empty()) memcpy(rec.data() + h.o_ce, ce.data(), ce.size() * sizeof(ConstrEnt));
     if (h.lbl) memcpy(rec.data() + h.o_mand, mand, sizeof(mand));
     if (!cols.empty()) memcpy(rec.data() + h.o_cols, cols.data(), cols.size() * sizeof(ColInfo));
+    uint32_t* cs = (uint32_t*)(rec.data() + h.o_csoa);
+    for (uint32_t j = 0; j < (uint32_t)cols.size(); ++j) {
+      cs[j] = cols[j].kind | (cols[j].slot << 8);
+      cs[cs_n + j] = cols[j].okw;
+      cs[2 * cs_n + j] = cols[j].mutw;
+      cs[3 * cs_n + j] = cols[j].rejb;
+    }
     if (h.lbl) memcpy(rec.data() + h.o_cidx, cidx, (size_t)nslots * 64u);
     return rec;
   }
@@ -207,7 +221,7 @@ Status build_slot_chunks(const Env& E, const int32_t* pols, uint32_t npol, int o
     ch.groups = b.groups;
     ch.rec = b.emit();
     const SlotHdr* sh = (const SlotHdr*)ch.rec.data();
-    ch.staged = sh->o_cidx ? sh->o_cidx : sh->bytes;
+    ch.staged = sh->o_cols;
     out->push_back(std::move(ch));
   }
   return {};

@@ -18,7 +18,7 @@ struct SlotChunk {
   uint32_t col0 = 0, ncols = 0, nslots = 0;
   bool groups = false;        // the chunk evaluates a group program (needs the LDS group stack)
   std::vector<uint8_t> rec;   // SlotHdr record, 16-B multiple
-  uint32_t staged = 0;        // leading bytes the device stages in LDS (all but the cidx section)
+  uint32_t staged = 0;        // leading bytes the device stages in LDS (all but the ColInfo and cidx sections)
 };
 
 Status build_slot_chunks(const Env& E, const int32_t* pols, uint32_t npol, int origin, std::vector<SlotChunk>* out);

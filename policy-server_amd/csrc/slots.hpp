@@ -58,7 +58,7 @@ struct alignas(16) SlotHdr {
   uint32_t o_ce, o_mand, o_cols, o_cidx;  // byte offsets of the sections from the record start
   uint16_t tab_off[NST];        // byte offset of table k from the record start (0 = not emitted)
   uint16_t ce_off[kSlots + 1];  // constraint entries of label-key bit k: [ce_off[k], ce_off[k+1])
-  uint16_t pad1[1];
+  uint16_t o_csoa;  // column arrays (kind | slot << 8, okw, mutw, rejb), each ncols rounded up to 4 u32
 };
 static_assert(sizeof(SlotHdr) == 336, "SlotHdr layout");
 
