@@ -461,7 +461,7 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
       }
       if (use[M_LK]) {
         T.o_vl = off;
-        off = align(off + lmax * 16);
+        off = align(off + lmax * 8);
       }
       T.o_rej = off;
       off = align(off + rows * 8);
@@ -909,14 +909,16 @@ int kw_env_classify_check(const kw_env* env, int col, const char* key, size_t kl
   if (col == COL_LV) {
     if (!H->kv_off || !H->lit_off[COL_LK] || (!key && klen)) return 0;
     const uint64_t km = blob_lit_lookup(blob, H->lit_off[COL_LK], (const uint8_t*)key, klen);
-    const uint32_t* idx = (const uint32_t*)(blob + H->kv_off);
+    const uint8_t* R = blob + H->kv_off;
     uint64_t keybits = 0;  // value patterns constrained on this key: every bit its DFA can accept
-    for (uint32_t rel = km ? idx[__builtin_ctzll(km)] : 0u; rel;) {  // the key's chain (region-relative links)
-      const uint32_t o = H->kv_off + rel;
-      const DevDfa* d = (const DevDfa*)(blob + o);
-      for (uint32_t q = 0; q < d->nstates; ++q) keybits |= ((const uint64_t*)(blob + d->acc_off))[q];
-      *fast_mask |= blob_dfa_run(blob, o, u, len);
-      rel = d->next;
+    for (uint32_t rel = km ? ((const uint16_t*)R)[__builtin_ctzll(km)] : 0u; rel;) {  // the key's chain
+      const KvDfa& d = *(const KvDfa*)(R + rel);
+      const uint64_t* accv = (const uint64_t*)(R + d.accv_off);
+      for (uint32_t q = 0; q < d.nstates; ++q) keybits |= accv[R[d.acc_off + q]];
+      uint32_t st = d.start;
+      for (size_t i = 0; i < len && st != 0; ++i) st = kv_step(R, d, st, u[i]);
+      *fast_mask |= accv[R[d.acc_off + st]];
+      rel = d.next;
     }
     *dfa_mask &= keybits;
     return 1;
@@ -1002,16 +1004,7 @@ struct HostSrc {
   }
   uint64_t vadd(uint32_t k) const { return derive_capadd(*sv, m<M_CAPADD>(k)); }
   uint64_t vaa(uint32_t c) const { return derive_apparmor(*sv, m<M_AA>(c)); }
-  uint64_t vden(uint32_t l) const {
-    uint64_t d, c;
-    derive_label(*sv, m<M_LK>(l), m<M_LV>(l), &d, &c);
-    return d;
-  }
-  uint64_t vcon(uint32_t l) const {
-    uint64_t d, c;
-    derive_label(*sv, m<M_LK>(l), m<M_LV>(l), &d, &c);
-    return c;
-  }
+  uint64_t vcon(uint32_t l) const { return derive_label(*sv, m<M_LK>(l), m<M_LV>(l)); }
 };
 }  // namespace
 

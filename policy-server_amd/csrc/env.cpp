@@ -14,6 +14,7 @@
 #include "env.hpp"
 
 #include <algorithm>
+#include <map>
 #include <cstring>
 
 #include "../../include/kwgpu.h"
@@ -708,24 +709,69 @@ Status build_env(const char* json, size_t len, bool continue_on_errors, const ch
         }
       }
     }
+    for (size_t k = 0; k < kd.size() && ok; ++k)
+      for (const Dfa& d : kd[k]) ok = ok && d.nstates <= 256 && d.ncls <= 255;  // u8 transitions and classes
     if (ok) {
-      align16(&b);
-      const size_t region = b.size();
-      uint32_t idx[kMaxPatternsPerColumn] = {};
-      put(&b, idx);
-      for (size_t k = 0; k < vals.size(); ++k) {
-        uint32_t prev = 0;
+      std::vector<uint8_t> r;  // the region, region-relative offsets
+      r.resize(2 * kMaxPatternsPerColumn, 0);
+      std::map<std::vector<uint8_t>, uint16_t> cls_pool;
+      auto at16 = [&](size_t n) {  // reserve n bytes at a 16-B boundary
+        while (r.size() % 16) r.push_back(0);
+        const size_t o = r.size();
+        r.resize(o + n, 0);
+        return o;
+      };
+      std::vector<size_t> recs;  // KvDfa record positions, linked per key below
+      for (size_t k = 0; k < kd.size(); ++k) {
+        size_t prev = 0;
         for (const Dfa& d : kd[k]) {
-          const uint32_t at = (uint32_t)(emit_dfa(d, &b) - region);
-          if (prev) ((DevDfa*)(b.data() + region + prev))->next = at;  // region-relative chain link
-          else idx[k] = at;
-          prev = at;
+          KvDfa kv;
+          memset(&kv, 0, sizeof(kv));
+          bool uniform_hi = true;
+          for (int c = 128; c < 256; ++c) uniform_hi = uniform_hi && d.cls[c] == d.cls[128];
+          kv.wide = uniform_hi ? 0 : 1;
+          kv.hi = d.cls[128];
+          std::vector<uint8_t> cm(d.cls.begin(), d.cls.begin() + (kv.wide ? 256 : 128));
+          auto it = cls_pool.find(cm);
+          if (it == cls_pool.end()) {
+            const size_t o = at16(cm.size());
+            memcpy(r.data() + o, cm.data(), cm.size());
+            it = cls_pool.emplace(cm, (uint16_t)o).first;
+          }
+          kv.cls_off = it->second;
+          std::vector<uint64_t> accv;
+          std::vector<uint8_t> acc(d.nstates);
+          for (uint32_t q = 0; q < d.nstates; ++q) {
+            size_t x = std::find(accv.begin(), accv.end(), d.accept[q]) - accv.begin();
+            if (x == accv.size()) accv.push_back(d.accept[q]);
+            acc[q] = (uint8_t)x;  // nstates <= 256: at most 256 distinct masks
+          }
+          kv.ncls = (uint8_t)d.ncls;
+          kv.start = (uint8_t)d.start;
+          kv.nstates = (uint16_t)d.nstates;
+          const size_t rec = at16(sizeof(KvDfa));
+          kv.accv_off = (uint16_t)at16(accv.size() * 8);
+          memcpy(r.data() + kv.accv_off, accv.data(), accv.size() * 8);
+          kv.acc_off = (uint16_t)r.size();
+          r.insert(r.end(), acc.begin(), acc.end());
+          kv.trans_off = (uint16_t)r.size();
+          for (uint16_t tq : d.trans) r.push_back((uint8_t)tq);
+          memcpy(r.data() + rec, &kv, sizeof(kv));
+          if (prev) ((KvDfa*)(r.data() + prev))->next = (uint16_t)rec;
+          else ((uint16_t*)r.data())[k] = (uint16_t)rec;
+          prev = rec;
+          recs.push_back(rec);
         }
       }
-      memcpy(b.data() + region, idx, sizeof(idx));
-      align16(&b);
-      hdr.kv_off = (uint32_t)region;
-      hdr.kv_bytes = (uint32_t)(b.size() - region);
+      while (r.size() % 16) r.push_back(0);
+      r.resize(r.size() + 16, 0);  // slack: dword-granular readers may run past the last table
+      ok = r.size() < 65536;        // u16 offsets
+      if (ok) {
+        align16(&b);
+        hdr.kv_off = (uint32_t)b.size();
+        hdr.kv_bytes = (uint32_t)r.size();
+        b.insert(b.end(), r.begin(), r.end());
+      }
     }
   }
   align16(&b);

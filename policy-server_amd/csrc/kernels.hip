@@ -304,7 +304,7 @@ struct TileSrc {
   const uint8_t* cflags_;
   const uint8_t* m_[NMASK];  // TileArgs.o_m arrays (u8 pattern index or u64, by mask)
   const uint64_t* vadd_;     // violation set per added capability
-  const uint64_t* vl_;       // (vden, vcon) per label
+  const uint64_t* vl_;       // vcon per label
   uint64_t r0;
   uint32_t cb, lb, kab, kdb;
   __device__ uint8_t rf(uint64_t r) const { return rf_[r - r0]; }
@@ -327,8 +327,7 @@ struct TileSrc {
   }
   __device__ uint64_t vadd(uint32_t k) const { return vadd_[k - kab]; }
   __device__ uint64_t vaa(uint32_t c) const { return ((const uint64_t*)m_[M_AA])[c - cb]; }
-  __device__ uint64_t vden(uint32_t l) const { return vl_[2 * (l - lb)]; }
-  __device__ uint64_t vcon(uint32_t l) const { return vl_[2 * (l - lb) + 1]; }
+  __device__ uint64_t vcon(uint32_t l) const { return vl_[l - lb]; }
 };
 
 template <class S>
@@ -557,10 +556,18 @@ __device__ inline uint64_t classify_value(const TileArgs& t, const uint8_t* lds,
                                           uint32_t b, uint32_t e) {
   uint64_t vm = 0;
   if (t.kv_lds) {
-    for (uint32_t rel = ((const uint32_t*)(lds + t.kv_lds))[__builtin_ctzll(km)]; rel;
-         rel = ((const DevDfa*)(lds + t.kv_lds + rel))->next) {
-      const DfaView v = make_view(lds + t.kv_lds + rel, nullptr, t.kv_blob + rel);
-      vm |= v.acc[feed(v, v.start, bytes, b, e)];
+    const uint8_t* R = lds + t.kv_lds;
+    for (uint32_t rel = ((const uint16_t*)R)[__builtin_ctzll(km)]; rel;) {
+      const KvDfa d = *(const KvDfa*)(R + rel);  // one ds_read_b128
+      uint32_t st = d.start, p = b;
+      while (p < e && st != 0) {  // dword reads of the staged string (16-B zero slack)
+        uint32_t w = *(const uint32_t*)(bytes + (p & ~3u)) >> (8u * (p & 3u));
+        const uint32_t lim = min(4u - (p & 3u), e - p);
+        for (uint32_t j = 0; j < lim; ++j, w >>= 8) st = kv_step(R, d, st, w & 0xffu);
+        p += lim;
+      }
+      vm |= ((const uint64_t*)(R + d.accv_off))[R[d.acc_off + st]];
+      rel = d.next;
     }
   } else {
     Chain c;
@@ -687,7 +694,7 @@ __global__ void __launch_bounds__(kSlotThreads)
     // ---- P1: classify the staged strings (FUSED) or take the classify kernel's masks (two-kernel
     //      form), and derive each entity's violation set from the slot tables, entity-parallel
     //      (slots.hpp derive_*): added capability -> vadd, AppArmor profile -> its AA entry, label ->
-    //      (vden, vcon). Literal columns keep the pattern index only.
+    //      vcon. Literal columns keep the pattern index only.
     if (FUSED && !(t.debug & 1u)) {
       // one flattened work list: NS, IMG, AA, CAPADD, CAPDROP, LK (the LK item also classifies the
       // label's value)
@@ -739,10 +746,7 @@ __global__ void __launch_bounds__(kSlotThreads)
             const uint32_t vsa = l_sa[M_LV];
             vm = classify_value(t, lds, r, lds + t.o_sb[M_LV], vo[i] - vsa, vo[i + 1] - vsa);
           }
-          uint64_t vden, vcon;
-          derive_label(sv, r, vm, &vden, &vcon);
-          l_vl[2 * i] = vden;
-          l_vl[2 * i + 1] = vcon;
+          l_vl[i] = derive_label(sv, r, vm);
         }
       }
     } else if (!FUSED) {
@@ -765,10 +769,7 @@ __global__ void __launch_bounds__(kSlotThreads)
       for (uint32_t i = tid; i < le - lb && t.o_m[M_LK]; i += kSlotThreads) {
         const uint64_t r = a.m[M_LK][lb + i];
         lds[t.o_m[M_LK] + i] = lit_index(r);
-        uint64_t vden, vcon;
-        derive_label(sv, r, a.m[M_LV] ? a.m[M_LV][lb + i] : 0ull, &vden, &vcon);
-        l_vl[2 * i] = vden;
-        l_vl[2 * i + 1] = vcon;
+        l_vl[i] = derive_label(sv, r, a.m[M_LV] ? a.m[M_LV][lb + i] : 0ull);
       }
     }
     __syncthreads();

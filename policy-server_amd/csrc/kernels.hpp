@@ -64,7 +64,7 @@ struct TileArgs {
   uint32_t o_m[NMASK];            // LDS byte offset of each staged per-string array, 0 = not read: u8 pattern
                                   // index (0xff none) for NS / CAPADD / CAPDROP / LK, u64 masks for
                                   // REG / TAG / IMG, u64 violation sets for AA; LV is never staged
-  uint32_t o_vadd, o_vl;          // u64 violation set per added capability; u64[2] (vden, vcon) per label
+  uint32_t o_vadd, o_vl;          // u64 violation set per added capability; u64 vcon per label
   uint32_t o_rej, o_mut, o_byp;   // per-request walk results: rejected / mutated slots, bypass flag
   uint32_t o_sa;                  // u32[NMASK]: the tile's staged byte start per string column (TileDesc.sa)
   uint32_t o_vw, vw_stride;       // violation words [rows][vw_stride] (aliases the staged strings)

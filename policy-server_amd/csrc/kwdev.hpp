@@ -47,7 +47,35 @@ enum GOp : uint8_t { G_CONST0 = 0, G_CONST1 = 1, G_CALL = 2, G_NOT = 3, G_AND = 
 constexpr int kMaxGroupStack = 16;
 constexpr int kMaxGroupMembers = 16;
 constexpr int kMaxListIdx = 16;
-constexpr size_t kKvDfaBytes = 3072;  // table bytes of one per-key label-value DFA before the key chains
+constexpr size_t kKvDfaBytes = 3072;  // u16 table bytes of one per-key label-value DFA before the key chains
+
+#if defined(__HIPCC__)
+#define KW_HD __host__ __device__
+#else
+#define KW_HD
+#endif
+
+// Compact DFA of the per-key label-value region (every offset region-relative, region < 64 KB):
+// u8 transitions (nstates <= 256), accept masks deduplicated (a u8 index per state into u64
+// accv[]), byte-class maps shared between DFAs and cut to 128 entries when every non-ASCII byte
+// falls in one class (`hi`). The region is staged whole in LDS by the slot kernel, so its size is
+// occupancy: these cuts take the C4 region from 16.8 KB of DevDfa records to about 7 KB.
+struct alignas(16) KvDfa {
+  uint16_t cls_off;    // u8 class of bytes [0, cls_len)
+  uint16_t trans_off;  // u8 [nstates][ncls]
+  uint16_t acc_off;    // u8 [nstates]: index into accv
+  uint16_t accv_off;   // u64 [nacc] (8-B aligned): accepted pattern bits (the column's global bits)
+  uint16_t next;       // next DFA of the key's chain, 0 = last
+  uint8_t ncls, start, hi, wide;  // hi: class of bytes >= 128 when !wide; wide: 256-entry map
+  uint16_t nstates;
+};
+static_assert(sizeof(KvDfa) == 16, "KvDfa layout");
+
+// One byte through a KvDfa (r: the region, LDS or blob).
+inline KW_HD uint32_t kv_step(const uint8_t* r, const KvDfa& d, uint32_t st, uint32_t c) {
+  const uint32_t k = (c < 128u || d.wide) ? r[d.cls_off + c] : d.hi;
+  return r[d.trans_off + st * d.ncls + k];
+}
 
 struct alignas(16) DevDfa {
   uint32_t nstates, ncls, start, trans_off;  // trans_off: blob offset of u16 [nstates][ncls]
@@ -68,11 +96,6 @@ struct alignas(16) DevLit {
   uint32_t slot_off, ent_off, word_off, pad;
 };
 
-#if defined(__HIPCC__)
-#define KW_HD __host__ __device__
-#else
-#define KW_HD
-#endif
 // hash shared by the host table builder (env.cpp) and the kernels
 inline KW_HD uint32_t lit_init(uint32_t seed, uint32_t len) { return seed ^ (len * 0x9E3779B1u); }
 inline KW_HD uint32_t lit_mix(uint32_t h, uint32_t w) {
@@ -111,9 +134,9 @@ struct alignas(16) DevHeader {
   uint32_t magic, version, npolicies, blob_bytes;
   uint32_t dfa_off[NCOL];  // head of the column's DFA chain, 0 = no patterns for this column
   uint32_t lit_off[NCOL];  // DevLit record of an all-literal column, 0 = none
-  // per-key label-value DFAs: region = u32 idx[64] (region-relative offset of the first DevDfa for
-  // label-key bit k over the value regexes constrained on that key, 0 = none) + the DFAs; a key's
-  // DFAs form a chain through DevDfa.next (region-relative here, 0 = last)
+  // per-key label-value DFAs: region = u16 idx[64] (region-relative offset of the first KvDfa for
+  // label-key bit k over the value regexes constrained on that key, 0 = none) + shared byte-class
+  // maps + the KvDfa records and tables; a key's DFAs form a chain through KvDfa.next
   uint32_t kv_off, kv_bytes;  // 0 = none (the COL_LV chain is used)
   int32_t bypass_bit;      // COL_NS bit of the always-accept namespace, -1 = none
   uint32_t policy_off;     // DevPolicy[npolicies]

@@ -157,25 +157,23 @@ struct SlotView {
 // ---- per-entity violation sets, derived entity-parallel before the walks (the walks then only
 // apply the first-violation order): an added capability violates the strict psp-capabilities slots
 // that allow none of its pattern bits, an AppArmor profile the psp-apparmor slots that do not allow
-// it, a label the safe-labels slots that deny its key (vden) or whose constraint on the key its
-// value fails (vcon).
+// it, a label the safe-labels slots whose constraint on its key its value fails (vcon; the slots
+// that deny the key are one table read in the walk).
 KW_HD inline uint64_t derive_capadd(const SlotView& sv, uint64_t m) {
   return sv.h->caps_strict ? tab_and(sv.tab(ST_NA_CAP), m, sv.h->caps_strict) : 0ull;
 }
 KW_HD inline uint64_t derive_apparmor(const SlotView& sv, uint64_t m) {
   return sv.h->aa ? tab_and(sv.tab(ST_NA_AA), m, sv.h->aa) : 0ull;
 }
-KW_HD inline void derive_label(const SlotView& sv, uint64_t km, uint64_t vm, uint64_t* vden, uint64_t* vcon) {
-  uint64_t d = 0, c = 0;
+KW_HD inline uint64_t derive_label(const SlotView& sv, uint64_t km, uint64_t vm) {
+  uint64_t c = 0;
   if (km && sv.h->lbl) {
     const uint32_t kb = kw_ctz64(km);  // label keys are literal patterns: at most one bit
-    d = sv.tab(ST_DENY)[kb];
     const ConstrEnt* ce = sv.ce();
     for (uint32_t e = sv.h->ce_off[kb]; e < sv.h->ce_off[kb + 1]; ++e)
       if (!((vm >> ce[e].vbit) & 1ull)) c |= ce[e].slots;
   }
-  *vden = d;
-  *vcon = c;
+  return c;
 }
 
 // ---- walk A: pod-privileged + psp-capabilities (validation, then mutation), containers in order.
@@ -274,7 +272,7 @@ KW_HD uint64_t walk_labels(const S& src, const SlotView& sv, uint64_t r, uint32_
     if (!km) continue;
     present |= km;
     const uint32_t li = l - lb;
-    uint64_t nw = src.vden(l) & ~rej;
+    uint64_t nw = sv.tab(ST_DENY)[kw_ctz64(km)] & ~rej;
     if (nw) {
       put_viol(vw, nw, vword(KW_R_LABEL_DENIED, pack1(li)));
       rej |= nw;
