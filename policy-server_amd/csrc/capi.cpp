@@ -887,14 +887,12 @@ uint64_t blob_lit_lookup(const uint8_t* blob, uint32_t off, const uint8_t* s, si
   uint32_t h = lit_init(L->seed, (uint32_t)n);
   for (uint32_t x : w) h = lit_mix(h, x);
   h = lit_final(h);
-  const uint32_t slot = ((const uint16_t*)(rec + L->slot_off))[h & (L->nslots - 1)];
-  if (!slot) return 0;
-  const uint32_t* ent = (const uint32_t*)(rec + L->ent_off) + 2 * (slot - 1);
-  if (ent[1] != n) return 0;
-  const uint32_t* pw = (const uint32_t*)(rec + L->word_off) + ent[0];
+  const uint32_t slot = ((const uint32_t*)(rec + L->slot_off))[h & (L->nslots - 1)];
+  if (!slot || lit_slot_len(slot) != n) return 0;
+  const uint32_t* pw = (const uint32_t*)(rec + L->word_off) + lit_slot_word(slot);
   for (size_t i = 0; i < w.size(); ++i)
     if (w[i] != pw[i]) return 0;
-  return 1ull << (slot - 1);
+  return 1ull << (lit_slot_pat(slot) - 1);
 }
 }  // namespace
 

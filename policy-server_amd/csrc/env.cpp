@@ -398,16 +398,25 @@ uint32_t lit_hash(const std::vector<uint32_t>& w, uint32_t len, uint32_t seed) {
 bool build_literal_table(const std::vector<Pattern>& pats, std::vector<uint8_t>* b) {
   const uint32_t npat = (uint32_t)pats.size();
   std::vector<std::vector<uint32_t>> words;
-  for (const Pattern& p : pats) words.push_back(lit_words(p.text));
+  std::vector<uint32_t> wi;  // word index of each pattern
+  uint32_t nwords = 0;
+  for (const Pattern& p : pats) {
+    if (p.text.size() > 4095) return false;  // packed slot fields (kwdev.hpp DevLit)
+    words.push_back(lit_words(p.text));
+    wi.push_back(nwords);
+    nwords += (uint32_t)words.back().size();
+  }
+  if (nwords >= 8192 || npat > 126) return false;
   for (uint32_t nslots = 16; nslots <= 4096; nslots *= 2) {
     if (nslots < 2 * npat) continue;
     for (uint32_t seed = 1; seed <= 4096; ++seed) {
-      std::vector<uint16_t> slot(nslots, 0);
+      std::vector<uint32_t> slot(nslots, 0);
       bool ok = true;
       for (uint32_t i = 0; i < npat && ok; ++i) {
-        uint32_t h = lit_hash(words[i], (uint32_t)pats[i].text.size(), seed) & (nslots - 1);
+        const uint32_t len = (uint32_t)pats[i].text.size();
+        uint32_t h = lit_hash(words[i], len, seed) & (nslots - 1);
         if (slot[h]) ok = false;
-        else slot[h] = (uint16_t)(i + 1);
+        else slot[h] = (i + 1) | (len << 7) | (wi[i] << 19);
       }
       if (!ok) continue;
       const size_t at = b->size();
@@ -418,19 +427,12 @@ bool build_literal_table(const std::vector<Pattern>& pats, std::vector<uint8_t>*
       L.npat = npat;
       put(b, L);
       L.slot_off = (uint32_t)(b->size() - at);
-      for (uint16_t x : slot) put(b, x);
-      align16(b);
-      L.ent_off = (uint32_t)(b->size() - at);
-      uint32_t wi = 0;
-      for (uint32_t i = 0; i < npat; ++i) {
-        put(b, wi);
-        put(b, (uint32_t)pats[i].text.size());
-        wi += (uint32_t)words[i].size();
-      }
+      for (uint32_t x : slot) put(b, x);
       align16(b);
       L.word_off = (uint32_t)(b->size() - at);
       for (const auto& w : words)
         for (uint32_t x : w) put(b, x);
+      for (int k = 0; k < 8; ++k) put(b, 0u);
       align16(b);
       L.bytes = (uint32_t)(b->size() - at);
       memcpy(b->data() + at, &L, sizeof(L));
@@ -674,9 +676,9 @@ Status build_env(const char* json, size_t len, bool continue_on_errors, const ch
     for (const Pattern& p : env->cols[c]) lit = lit && p.kind == Pattern::Literal;
     if (!lit) continue;
     align16(&b);
-    hdr.lit_off[c] = (uint32_t)b.size();
-    if (!build_literal_table(env->cols[c], &b))
-      return {KW_E_BOOTSTRAP, "bootstrap failure: cannot build the literal table of column " + std::to_string(c)};
+    const size_t at = b.size();
+    if (build_literal_table(env->cols[c], &b)) hdr.lit_off[c] = (uint32_t)at;
+    else b.resize(at);  // no table (oversized literals): the column keeps its DFA chain
   }
   // per-key label-value DFAs: a label's value is only ever tested against the regexes constrained
   // on its own key, so one small DFA per constrained key replaces the chain over all value regexes

@@ -106,20 +106,35 @@ __device__ inline uint32_t lit_word(const uint32_t* base, uint32_t i, uint32_t s
   return rem >= 4u ? w : (w & ((1u << (8u * rem)) - 1u));
 }
 __device__ inline uint64_t lit_lookup(const uint8_t* rec, const uint8_t* bytes, uint32_t b, uint32_t e) {
+  // LDS only: the first 32 bytes of the string and of the candidate pattern are read in one batch
+  // each (up to 36 bytes past the string: staged slack / other LDS; masked off by len)
   const DevLit* L = (const DevLit*)rec;
   const uint32_t len = e - b, sh = b & 3u, nw = (len + 3u) >> 2;
   const uint32_t* base = (const uint32_t*)(bytes + (b & ~3u));
+  uint32_t raw[9], w[8];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) raw[i] = base[i];
   uint32_t h = lit_init(L->seed, len);
-  for (uint32_t i = 0; i < nw; ++i) h = lit_mix(h, lit_word(base, i, sh, len));
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t x = __builtin_amdgcn_alignbyte(raw[i + 1], raw[i], sh);
+    const uint32_t rem = len - 4u * (uint32_t)i;  // >= 4: whole dword
+    w[i] = rem >= 4u ? x : (x & ((1u << (8u * rem)) - 1u));
+    if ((uint32_t)i < nw) h = lit_mix(h, w[i]);
+  }
+  for (uint32_t i = 8; i < nw; ++i) h = lit_mix(h, lit_word(base, i, sh, len));
   h = lit_final(h);
-  const uint32_t s = ((const uint16_t*)(rec + L->slot_off))[h & (L->nslots - 1u)];
-  if (!s) return 0ull;
-  const uint2 ent = ((const uint2*)(rec + L->ent_off))[s - 1u];
-  if (ent.y != len) return 0ull;
-  const uint32_t* pw = (const uint32_t*)(rec + L->word_off) + ent.x;
-  for (uint32_t i = 0; i < nw; ++i)
-    if (lit_word(base, i, sh, len) != pw[i]) return 0ull;
-  return 1ull << (s - 1u);
+  const uint32_t s = ((const uint32_t*)(rec + L->slot_off))[h & (L->nslots - 1u)];
+  if (!s || lit_slot_len(s) != len) return 0ull;
+  const uint32_t* pw = (const uint32_t*)(rec + L->word_off) + lit_slot_word(s);
+  uint32_t pv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) pv[i] = pw[i];  // zero tail of the words section covers short patterns
+  bool eq = true;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) eq = eq && ((uint32_t)i >= nw || w[i] == pv[i]);
+  for (uint32_t i = 8; i < nw && eq; ++i) eq = lit_word(base, i, sh, len) == pw[i];
+  return eq ? 1ull << (lit_slot_pat(s) - 1u) : 0ull;
 }
 
 // A column's DFA chain, staged contiguously (LDS, or the blob itself): element at blob offset
@@ -559,12 +574,23 @@ __device__ inline uint64_t classify_value(const TileArgs& t, const uint8_t* lds,
     const uint8_t* R = lds + t.kv_lds;
     for (uint32_t rel = ((const uint16_t*)R)[__builtin_ctzll(km)]; rel;) {
       const KvDfa d = *(const KvDfa*)(R + rel);  // one ds_read_b128
-      uint32_t st = d.start, p = b;
-      while (p < e && st != 0) {  // dword reads of the staged string (16-B zero slack)
-        uint32_t w = *(const uint32_t*)(bytes + (p & ~3u)) >> (8u * (p & 3u));
-        const uint32_t lim = min(4u - (p & 3u), e - p);
-        for (uint32_t j = 0; j < lim; ++j, w >>= 8) st = kv_step(R, d, st, w & 0xffu);
-        p += lim;
+      uint32_t st = d.start;
+      // 8-byte windows: the window's dwords, then its 8 byte classes, load as two batches; only the
+      // transitions form a dependent chain (bytes past the string read the staged slack, unused)
+      for (uint32_t p = b; p < e && st != 0; p += 8u) {
+        const uint32_t* q = (const uint32_t*)(bytes + (p & ~3u));
+        const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], sh = p & 3u;
+        const uint32_t x0 = __builtin_amdgcn_alignbyte(q1, q0, sh), x1 = __builtin_amdgcn_alignbyte(q2, q1, sh);
+        uint32_t c[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t by = ((j < 4 ? x0 : x1) >> (8 * (j & 3))) & 0xffu;
+          c[j] = (by < 128u || d.wide) ? R[d.cls_off + by] : d.hi;
+        }
+        const uint32_t lim = min(8u, e - p);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if ((uint32_t)j < lim) st = R[d.trans_off + st * d.ncls + c[j]];
       }
       vm |= ((const uint64_t*)(R + d.accv_off))[R[d.acc_off + st]];
       rel = d.next;
@@ -741,7 +767,7 @@ __global__ void __launch_bounds__(kSlotThreads)
           l_vadd[i] = derive_capadd(sv, r);
         } else if (m == M_LK) {
           uint64_t vm = 0;
-          if (r && t.o_sb[M_LV]) {
+          if (r && t.o_sb[M_LV] && !(t.debug & 512u)) {
             const uint32_t* vo = (const uint32_t*)(lds + t.o_so[M_LV]);
             const uint32_t vsa = l_sa[M_LV];
             vm = classify_value(t, lds, r, lds + t.o_sb[M_LV], vo[i] - vsa, vo[i + 1] - vsa);
@@ -795,7 +821,7 @@ __global__ void __launch_bounds__(kSlotThreads)
       src.kdb = kdb;
       const uint64_t r = r0 + lane;
       uint32_t* vw = l_vw + lane * t.vw_stride;
-      const bool run = !(t.debug & 2u);
+      const bool run = !(t.debug & 2u) && !((t.debug >> (3 + wave)) & 1u);  // bits 8/16/32/64: skip wave 0-3
       uint64_t rej = 0;
       if (wave == 0) {
         uint64_t mut = 0;

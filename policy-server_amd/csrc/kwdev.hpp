@@ -89,12 +89,17 @@ struct alignas(16) DevDfa {
 // Literal column: a perfect hash over the column's literal patterns (every pattern of the column
 // is a Literal). A string matches at most one pattern; lookup = hash of its canonical little-endian
 // dwords -> slot -> one verify against the pattern's words. Record layout (offsets from its start):
-//   DevLit | u16 slot[nslots] (pattern index + 1, 0 = empty) | u32 ent[npat][2] (word index, len)
-//   | u32 words[] (each pattern zero-padded to whole dwords)
+//   DevLit | u32 slot[nslots] | u32 words[]
+// slot: 0 = empty, else (pattern index + 1) | len << 7 | word index << 19 (len < 4096, word
+// index < 8192), so a probe reads the slot and then the pattern words, two dependent loads.
+// words: each pattern zero-padded to whole dwords, followed by 32 zero bytes (batched verify reads).
 struct alignas(16) DevLit {
   uint32_t nslots, seed, npat, bytes;      // bytes: whole record, multiple of 16
-  uint32_t slot_off, ent_off, word_off, pad;
+  uint32_t slot_off, word_off, pad0, pad1;
 };
+constexpr uint32_t lit_slot_pat(uint32_t s) { return s & 127u; }  // pattern index + 1
+constexpr uint32_t lit_slot_len(uint32_t s) { return (s >> 7) & 4095u; }
+constexpr uint32_t lit_slot_word(uint32_t s) { return s >> 19; }
 
 // hash shared by the host table builder (env.cpp) and the kernels
 inline KW_HD uint32_t lit_init(uint32_t seed, uint32_t len) { return seed ^ (len * 0x9E3779B1u); }
