@@ -445,9 +445,11 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
       off = align(off + (cmax + 1) * 4);
       T.o_cdrop = off;
       off = align(off + (cmax + 1) * 4);
+      T.use_mask = 0;
       for (int m = 0; m < (int)NMASK; ++m) {
         T.o_m[m] = 0;
-        if (!use[m] || m == M_LV) continue;  // label values: derived into o_vl in P1, never staged
+        if (use[m]) T.use_mask |= 1u << m;
+        if (!use[m] || m == M_LV || m == M_AA) continue;  // AppArmor profiles / label values: into V_c / V_l
         const uint32_t cnt = m == M_NS ? rows : (m == M_CAPADD || m == M_CAPDROP) ? kmax : m == M_LK ? lmax : cmax;
         const bool lit = m == M_NS || m == M_CAPADD || m == M_CAPDROP || m == M_LK;
         T.o_m[m] = off;
@@ -463,6 +465,12 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
         T.o_vl = off;
         off = align(off + lmax * 8);
       }
+      T.o_vc = off;  // V_c per container
+      off = align(off + cmax * 8);
+      T.o_own_c = off;
+      off = align(off + cmax);
+      T.o_own_l = off;
+      off = align(off + lmax);
       T.o_rej = off;
       off = align(off + rows * 8);
       T.o_mut = off;

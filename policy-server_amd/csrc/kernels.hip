@@ -299,8 +299,7 @@ struct FamOut {
   bool mutated;
 };
 
-// Column accessors. GlobalSrc reads the HBM arrays; TileSrc reads a tile staged in LDS (indices
-// stay absolute, the accessor rebases them).
+// Column accessors of the overflow and row kernels: the HBM arrays, absolute indices.
 struct GlobalSrc {
   const EvalArgs* a;
   __device__ uint8_t rf(uint64_t r) const { return a->req_flags[r]; }
@@ -311,38 +310,6 @@ struct GlobalSrc {
   __device__ uint32_t cdrop(uint32_t c) const { return a->capdrop_off[c]; }
   template <int K>
   __device__ uint64_t m(uint64_t i) const { return a->m[K] ? a->m[K][i] : 0ull; }
-};
-
-struct TileSrc {
-  const uint8_t* rf_;
-  const uint32_t *coff_, *loff_, *cadd_, *cdrop_;
-  const uint8_t* cflags_;
-  const uint8_t* m_[NMASK];  // TileArgs.o_m arrays (u8 pattern index or u64, by mask)
-  const uint64_t* vadd_;     // violation set per added capability
-  const uint64_t* vl_;       // vcon per label
-  uint64_t r0;
-  uint32_t cb, lb, kab, kdb;
-  __device__ uint8_t rf(uint64_t r) const { return rf_[r - r0]; }
-  __device__ uint32_t coff(uint64_t r) const { return coff_[r - r0]; }
-  __device__ uint32_t loff(uint64_t r) const { return loff_[r - r0]; }
-  __device__ uint8_t cflags(uint32_t c) const { return cflags_[c - cb]; }
-  __device__ uint32_t cadd(uint32_t c) const { return cadd_[c - cb]; }
-  __device__ uint32_t cdrop(uint32_t c) const { return cdrop_[c - cb]; }
-  template <int K>
-  __device__ uint64_t m(uint64_t i) const {
-    const uint8_t* p = m_[K];
-    if (!p) return 0ull;
-    const uint32_t j = K == M_NS ? (uint32_t)(i - r0) : K == M_CAPADD ? (uint32_t)(i - kab) : K == M_CAPDROP ? (uint32_t)(i - kdb)
-                       : (K == M_LK || K == M_LV) ? (uint32_t)(i - lb) : (uint32_t)(i - cb);
-    if (K == M_NS || K == M_CAPADD || K == M_CAPDROP || K == M_LK) {
-      const uint32_t v = p[j];
-      return v < 64u ? 1ull << v : 0ull;
-    }
-    return ((const uint64_t*)p)[j];
-  }
-  __device__ uint64_t vadd(uint32_t k) const { return vadd_[k - kab]; }
-  __device__ uint64_t vaa(uint32_t c) const { return ((const uint64_t*)m_[M_AA])[c - cb]; }
-  __device__ uint64_t vcon(uint32_t l) const { return vl_[l - lb]; }
 };
 
 template <class S>
@@ -607,6 +574,22 @@ __device__ inline uint64_t classify_value(const TileArgs& t, const uint8_t* lds,
   return vm;
 }
 
+__device__ inline uint64_t idx_mask(uint32_t v) { return v < 64u ? 1ull << v : 0ull; }
+
+// Trusted-repos reasons of staged container i, in precedence order (registry not allowed, registry
+// rejected, tag rejected, image not allowed, image rejected; oracle fam_trusted).
+__device__ inline void trs_whys(const SlotView& sv, const uint8_t* lds, const TileArgs& t, uint32_t i, uint64_t why[5]) {
+  const SlotHdr& h = *sv.h;
+  const uint64_t reg = t.o_m[M_REG] ? ((const uint64_t*)(lds + t.o_m[M_REG]))[i] : 0ull;
+  const uint64_t tag = t.o_m[M_TAG] ? ((const uint64_t*)(lds + t.o_m[M_TAG]))[i] : 0ull;
+  const uint64_t img = t.o_m[M_IMG] ? ((const uint64_t*)(lds + t.o_m[M_IMG]))[i] : 0ull;
+  why[0] = h.has_ra & ~tab_or(sv.tab(ST_RA), reg);
+  why[1] = tab_or(sv.tab(ST_RR), reg);
+  why[2] = tab_or(sv.tab(ST_TR), tag);
+  why[3] = h.has_ia & ~tab_or(sv.tab(ST_IA), img);
+  why[4] = tab_or(sv.tab(ST_IR), img);
+}
+
 // LDS-DMA copies (global_load_lds) issued by every wave of the workgroup: the LDS image is
 // wave-linear (wave-uniform base + lane x size), so lane l of the wave whose first element is i - l
 // lands at dst + i. Tails are masked by the loop bound.
@@ -678,9 +661,9 @@ __global__ void __launch_bounds__(kSlotThreads)
   uint64_t* l_vl = (uint64_t*)(lds + t.o_vl);
   uint32_t* l_vw = (uint32_t*)(lds + t.o_vw);
   uint16_t* gstk = t.o_gstk ? (uint16_t*)(lds + t.o_gstk) : nullptr;
-  uint64_t* l_m[NMASK];
-#pragma unroll
-  for (int k = 0; k < (int)NMASK; ++k) l_m[k] = t.o_m[k] ? (uint64_t*)(lds + t.o_m[k]) : nullptr;
+  uint64_t* l_vc = (uint64_t*)(lds + t.o_vc);  // V_c per staged container
+  uint8_t* own_c = lds + t.o_own_c;            // tile-local request of each staged container / label
+  uint8_t* own_l = lds + t.o_own_l;
 
   const uint32_t npol = a.npol;
   const uint64_t ntiles = (a.nrows + kSlotRows - 1) / kSlotRows;
@@ -712,133 +695,229 @@ __global__ void __launch_bounds__(kSlotThreads)
         glds_x4((const u32x4*)(t.s_bytes[m] + d.sa[m]), (u32x4*)(lds + t.o_sb[m]), d.nv[m], tid);
       }
     }
-    for (uint32_t i = tid; i < nr; i += kSlotThreads) l_rej[i] = 0;
+    for (uint32_t i = tid; i < nr; i += kSlotThreads) l_rej[i] = l_mut[i] = 0;
     if (tid < NMASK) l_sa[tid] = d.sa[tid];
     __syncthreads();
     const uint8_t* cfl = l_cflags + (cb & 3u);  // staged from the dword holding flag cb
 
     // ---- P1: classify the staged strings (FUSED) or take the classify kernel's masks (two-kernel
-    //      form), and derive each entity's violation set from the slot tables, entity-parallel
-    //      (slots.hpp derive_*): added capability -> vadd, AppArmor profile -> its AA entry, label ->
-    //      vcon. Literal columns keep the pattern index only.
-    if (FUSED && !(t.debug & 1u)) {
-      // one flattened work list: NS, IMG, AA, CAPADD, CAPDROP, LK (the LK item also classifies the
-      // label's value)
-      const uint32_t n0 = t.o_m[M_NS] ? nr : 0u;
-      const uint32_t n1 = (t.o_m[M_REG] || t.o_m[M_TAG] || t.o_m[M_IMG]) ? nc : 0u;
-      const uint32_t n2 = t.o_m[M_AA] ? nc : 0u;
-      const uint32_t n3 = t.o_m[M_CAPADD] ? kae - kab : 0u;
-      const uint32_t n4 = t.o_m[M_CAPDROP] ? kde - kdb : 0u;
-      const uint32_t n5 = t.o_m[M_LK] ? le - lb : 0u;
-      const uint32_t s1 = n0, s2 = s1 + n1, s3 = s2 + n2, s4 = s3 + n3, s5 = s4 + n4, s6 = s5 + n5;
-      for (uint32_t w = tid; w < s6; w += kSlotThreads) {
-        if (w >= s1 && w < s2) {  // image reference: one parse feeds the registry, tag and image chains
+    //      form), and derive each entity's violation set from the slot tables, entity-parallel:
+    //      request items (namespace; owner maps of the tile's containers and labels), image items
+    //      (registry / tag / image masks), container items (privileged candidates, added and
+    //      dropped capabilities, AppArmor profile -> V_c) and label items (key, value -> V_l).
+    const SlotHdr& SH = *sv.h;
+    const uint64_t privany = SH.priv[0] | SH.priv[1] | SH.priv[2] | SH.priv[3];
+    const bool ctr_fam = (privany | SH.caps | SH.aa | SH.trs) != 0;
+    const bool classify = !(t.debug & 1u);  // diagnostics: skip classification (entities match nothing)
+    // pattern mask of string i of literal column m: the staged strings (FUSED) or the classify
+    // kernel's masks (entity index relative to the mask's tile base `g0`)
+    auto lit = [&](int m, uint32_t i, uint32_t g0) -> uint64_t {
+      if (!classify) return 0ull;
+      if (!FUSED) return a.m[m][g0 + i];
+      const uint32_t* so = (const uint32_t*)(lds + t.o_so[m]);
+      const uint32_t sa = l_sa[m];
+      return lit_lookup(lds + t.lit_lds[m], lds + t.o_sb[m], so[i] - sa, so[i + 1] - sa);
+    };
+    {
+      const uint32_t n0 = nr;
+      const uint32_t n1 = (t.use_mask & ((1u << M_REG) | (1u << M_TAG) | (1u << M_IMG))) ? nc : 0u;
+      const uint32_t n2 = ctr_fam ? nc : 0u;
+      const uint32_t n3 = t.o_m[M_LK] ? le - lb : 0u;
+      const uint32_t s1 = n0, s2 = s1 + n1, s3 = s2 + n2, s4 = s3 + n3;
+      for (uint32_t w = tid; w < s4; w += kSlotThreads) {
+        if (w < s1) {  // request: namespace and the owner maps
+          const uint32_t i = w;
+          if (t.o_m[M_NS]) lds[t.o_m[M_NS] + i] = lit_index(lit(M_NS, i, (uint32_t)r0));
+          for (uint32_t c = l_coff[i] - cb, c1 = l_coff[i + 1] - cb; c < c1; ++c) own_c[c] = (uint8_t)i;
+          for (uint32_t l = l_loff[i] - lb, l1 = l_loff[i + 1] - lb; l < l1; ++l) own_l[l] = (uint8_t)i;
+        } else if (w < s2) {  // image reference: one parse feeds the registry, tag and image chains
           const uint32_t i = w - s1;
           uint64_t mr = 0, mt = 0, mi = 0;
-          if (cfl[i] & KW_CTR_HAS_IMAGE) {
-            const uint32_t* so = (const uint32_t*)(lds + t.o_so[M_IMG]);
-            const uint32_t sa = l_sa[M_IMG];
-            classify_image_all(ch[M_REG], ch[M_TAG], ch[M_IMG], lds + t.o_sb[M_IMG], so[i] - sa, so[i + 1] - sa, &mr, &mt,
-                               &mi);
+          if (!classify) {
+          } else if (FUSED) {
+            if (cfl[i] & KW_CTR_HAS_IMAGE) {
+              const uint32_t* so = (const uint32_t*)(lds + t.o_so[M_IMG]);
+              const uint32_t sa = l_sa[M_IMG];
+              classify_image_all(ch[M_REG], ch[M_TAG], ch[M_IMG], lds + t.o_sb[M_IMG], so[i] - sa, so[i + 1] - sa, &mr,
+                                 &mt, &mi);
+            }
+          } else {
+            if (a.m[M_REG]) mr = a.m[M_REG][cb + i];
+            if (a.m[M_TAG]) mt = a.m[M_TAG][cb + i];
+            if (a.m[M_IMG]) mi = a.m[M_IMG][cb + i];
           }
           if (t.o_m[M_REG]) ((uint64_t*)(lds + t.o_m[M_REG]))[i] = mr;
           if (t.o_m[M_TAG]) ((uint64_t*)(lds + t.o_m[M_TAG]))[i] = mt;
           if (t.o_m[M_IMG]) ((uint64_t*)(lds + t.o_m[M_IMG]))[i] = mi;
-          continue;
-        }
-        uint32_t m, i;
-        if (w < s1) { m = M_NS; i = w; }
-        else if (w < s3) { m = M_AA; i = w - s2; }
-        else if (w < s4) { m = M_CAPADD; i = w - s3; }
-        else if (w < s5) { m = M_CAPDROP; i = w - s4; }
-        else { m = M_LK; i = w - s5; }
-        const uint32_t* so = (const uint32_t*)(lds + t.o_so[m]);
-        const uint32_t sa = l_sa[m];
-        if (m == M_AA) {
+        } else if (w < s3) {  // container: V_c over the privileged, capability and AppArmor slots
+          const uint32_t i = w - s2;
+          const uint32_t fl = cfl[i];
           uint64_t v = 0;
-          if (cfl[i] & KW_CTR_HAS_APPARMOR)
-            v = derive_apparmor(sv, lit_lookup(lds + t.lit_lds[M_AA], lds + t.o_sb[M_AA], so[i] - sa, so[i + 1] - sa));
-          ((uint64_t*)(lds + t.o_m[M_AA]))[i] = v;
-          continue;
-        }
-        const uint64_t r = lit_lookup(lds + t.lit_lds[m], lds + t.o_sb[m], so[i] - sa, so[i + 1] - sa);
-        lds[t.o_m[m] + i] = lit_index(r);
-        if (m == M_CAPADD) {
-          l_vadd[i] = derive_capadd(sv, r);
-        } else if (m == M_LK) {
-          uint64_t vm = 0;
-          if (r && t.o_sb[M_LV] && !(t.debug & 512u)) {
-            const uint32_t* vo = (const uint32_t*)(lds + t.o_so[M_LV]);
-            const uint32_t vsa = l_sa[M_LV];
-            vm = classify_value(t, lds, r, lds + t.o_sb[M_LV], vo[i] - vsa, vo[i + 1] - vsa);
+          if ((fl & KW_CTR_PRIVILEGED) && privany) {
+            v |= SH.priv[0];
+            if (!(fl & KW_CTR_INIT)) v |= SH.priv[1];
+            if (!(fl & KW_CTR_EPHEMERAL)) v |= SH.priv[2];
+            if (!(fl & (KW_CTR_INIT | KW_CTR_EPHEMERAL))) v |= SH.priv[3];
           }
-          l_vl[i] = derive_label(sv, r, vm);
+          if (SH.aa && (t.use_mask & (1u << M_AA)) && (fl & KW_CTR_HAS_APPARMOR)) {
+            v |= derive_apparmor(sv, lit(M_AA, i, cb));
+          }
+          if (t.o_m[M_CAPADD]) {
+            for (uint32_t k = l_cadd[i] - kab, k1 = l_cadd[i + 1] - kab; k < k1; ++k) {
+              const uint64_t r = lit(M_CAPADD, k, kab);
+              lds[t.o_m[M_CAPADD] + k] = lit_index(r);
+              const uint64_t va = derive_capadd(sv, r);
+              l_vadd[k] = va;
+              v |= va;
+            }
+          }
+          if (t.o_m[M_CAPDROP]) {
+            for (uint32_t k = l_cdrop[i] - kdb, k1 = l_cdrop[i + 1] - kdb; k < k1; ++k)
+              lds[t.o_m[M_CAPDROP] + k] = lit_index(lit(M_CAPDROP, k, kdb));
+          }
+          l_vc[i] = v;
+        } else {  // label: key, value -> V_l = denied | constrained-and-failed slots
+          const uint32_t i = w - s3;
+          const uint64_t r = lit(M_LK, i, lb);
+          uint64_t vm = 0;
+          if (!r) {
+          } else if (FUSED) {
+            if (t.o_sb[M_LV] && !(t.debug & 512u)) {
+              const uint32_t* vo = (const uint32_t*)(lds + t.o_so[M_LV]);
+              const uint32_t vsa = l_sa[M_LV];
+              vm = classify_value(t, lds, r, lds + t.o_sb[M_LV], vo[i] - vsa, vo[i + 1] - vsa);
+            }
+          } else {
+            vm = a.m[M_LV] ? a.m[M_LV][lb + i] : 0ull;
+          }
+          lds[t.o_m[M_LK] + i] = lit_index(r);
+          l_vl[i] = (r && SH.lbl) ? derive_label(sv, r, vm) | sv.tab(ST_DENY)[kw_ctz64(r)] : 0ull;
         }
-      }
-    } else if (!FUSED) {
-      for (uint32_t i = tid; i < nr && t.o_m[M_NS]; i += kSlotThreads) lds[t.o_m[M_NS] + i] = lit_index(a.m[M_NS][r0 + i]);
-      for (uint32_t i = tid; i < nc; i += kSlotThreads) {
-        if (t.o_m[M_REG]) ((uint64_t*)(lds + t.o_m[M_REG]))[i] = a.m[M_REG][cb + i];
-        if (t.o_m[M_TAG]) ((uint64_t*)(lds + t.o_m[M_TAG]))[i] = a.m[M_TAG][cb + i];
-        if (t.o_m[M_IMG]) ((uint64_t*)(lds + t.o_m[M_IMG]))[i] = a.m[M_IMG][cb + i];
-        if (t.o_m[M_AA])
-          ((uint64_t*)(lds + t.o_m[M_AA]))[i] =
-              (cfl[i] & KW_CTR_HAS_APPARMOR) ? derive_apparmor(sv, a.m[M_AA][cb + i]) : 0ull;
-      }
-      for (uint32_t i = tid; i < kae - kab && t.o_m[M_CAPADD]; i += kSlotThreads) {
-        const uint64_t r = a.m[M_CAPADD][kab + i];
-        lds[t.o_m[M_CAPADD] + i] = lit_index(r);
-        l_vadd[i] = derive_capadd(sv, r);
-      }
-      for (uint32_t i = tid; i < kde - kdb && t.o_m[M_CAPDROP]; i += kSlotThreads)
-        lds[t.o_m[M_CAPDROP] + i] = lit_index(a.m[M_CAPDROP][kdb + i]);
-      for (uint32_t i = tid; i < le - lb && t.o_m[M_LK]; i += kSlotThreads) {
-        const uint64_t r = a.m[M_LK][lb + i];
-        lds[t.o_m[M_LK] + i] = lit_index(r);
-        l_vl[i] = derive_label(sv, r, a.m[M_LV] ? a.m[M_LV][lb + i] : 0ull);
       }
     }
     __syncthreads();
 
-    // ---- P2: walk. One lane per request; each wave owns a family group (disjoint slots), so the
-    //      violation words of a request never collide; rejected masks merge with ds_or_b64.
-    if (lane < nr) {
-      TileSrc src;
-      src.rf_ = l_rf;
-      src.coff_ = l_coff;
-      src.loff_ = l_loff;
-      src.cadd_ = l_cadd;
-      src.cdrop_ = l_cdrop;
-      src.cflags_ = cfl;
-#pragma unroll
-      for (int k = 0; k < (int)NMASK; ++k) src.m_[k] = t.o_m[k] ? lds + t.o_m[k] : nullptr;
-      src.vadd_ = l_vadd;
-      src.vl_ = l_vl;
-      src.r0 = r0;
-      src.cb = cb;
-      src.lb = lb;
-      src.kab = kab;
-      src.kdb = kdb;
-      const uint64_t r = r0 + lane;
-      uint32_t* vw = l_vw + lane * t.vw_stride;
-      const bool run = !(t.debug & 2u) && !((t.debug >> (3 + wave)) & 1u);  // bits 8/16/32/64: skip wave 0-3
-      uint64_t rej = 0;
-      if (wave == 0) {
-        uint64_t mut = 0;
-        if (run) rej = walk_privileged_caps(src, sv, r, vw, &mut);
-        l_mut[lane] = mut;
-      } else if (wave == 1) {
-        if (run) rej = walk_apparmor_images(src, sv, r, vw);
-      } else if (wave == 2) {
-        if (run) rej = walk_labels(src, sv, r, vw);
-      } else {
-        if (run) rej = walk_namespace(src, sv, r, vw);
-        // namespace bypass (service.rs:40-71): AdmissionRequest in the always-accept namespace
-        const uint32_t rf = l_rf[lane];
-        l_byp[lane] = H.bypass_bit >= 0 && !(rf & KW_REQ_RAW) && (rf & KW_REQ_HAS_NAMESPACE) &&
-                      ((src.template m<M_NS>(r) >> H.bypass_bit) & 1ull);
+    // ---- P2: first violations, entity-parallel. A slot's first violation is the first entity of
+    //      the request (object order) whose violation set holds it: each entity thread ORs the sets
+    //      of its predecessors in the request (independent LDS loads) and writes the words of the
+    //      slots it violates first; within an entity the family's own order applies (capabilities
+    //      in list order, trusted-repos reasons in precedence). Request items add the namespace and
+    //      mandatory-label slots and the bypass flag. Rejected / mutated slots merge with ds_or_b64.
+    //      (Sequential form of the same walk: slots.hpp walk_*, the host diagnostic.)
+    if (SH.trs && !(t.debug & 2u)) {  // trusted-repos reasons join V_c once the image masks exist
+      for (uint32_t i = tid; i < nc; i += kSlotThreads) {
+        if (!(cfl[i] & KW_CTR_HAS_IMAGE)) continue;
+        uint64_t why[5];
+        trs_whys(sv, lds, t, i, why);
+        l_vc[i] |= (why[0] | why[1] | why[2] | why[3] | why[4]) & SH.trs;
       }
-      if (rej) atomicOr((unsigned long long*)&l_rej[lane], (unsigned long long)rej);
+      __syncthreads();
+    }
+    if (!(t.debug & 2u)) {
+      const uint32_t n0 = nr, n1 = ctr_fam ? nc : 0u, n2 = (SH.lbl && t.o_m[M_LK]) ? le - lb : 0u;
+      for (uint32_t w = tid; w < n0 + n1 + n2; w += kSlotThreads) {
+        if (w < n0) {  // request: namespace, mandatory labels, bypass
+          const uint32_t i = w;
+          const uint32_t rf = l_rf[i];
+          uint32_t* vw = l_vw + i * t.vw_stride;
+          const uint64_t nsm = t.o_m[M_NS] ? idx_mask(lds[t.o_m[M_NS] + i]) : 0ull;
+          uint64_t rej = 0;
+          if (SH.ns) {
+            const uint64_t ok = (rf & KW_REQ_HAS_NAMESPACE) ? tab_or(sv.tab(ST_NSOK), nsm) : 0ull;
+            rej = SH.ns & ~ok;
+            put_viol(vw, rej, vword(KW_R_NAMESPACE, 0));
+          }
+          if (SH.lbl && SH.mand_union && t.o_m[M_LK]) {
+            uint64_t present = 0, lrej = 0;
+            for (uint32_t l = l_loff[i] - lb, l1 = l_loff[i + 1] - lb; l < l1; ++l) {
+              present |= idx_mask(lds[t.o_m[M_LK] + l]);
+              lrej |= l_vl[l];
+            }
+            uint64_t nw = tab_or(sv.tab(ST_MAND), SH.mand_union & ~present) & ~lrej;
+            rej |= nw;
+            const uint8_t* mand = t.slot_plan + SH.o_mand;  // global: read only for a violation
+            while (nw) {  // the first missing mandatory key of each such slot, settings order
+              const uint32_t sl = kw_ctz64(nw);
+              nw &= nw - 1;
+              const uint4 mk = *(const uint4*)(mand + sl * 16u);
+              const uint32_t mw[4] = {mk.x, mk.y, mk.z, mk.w};
+              uint32_t k = 0;
+              for (; k < 16; ++k) {
+                const uint32_t kb = (mw[k >> 2] >> (8 * (k & 3))) & 0xffu;
+                if (kb == 0xffu || !((present >> kb) & 1ull)) break;
+              }
+              vw[sl] = vword(KW_R_LABEL_MANDATORY, k);
+            }
+          }
+          if (rej) atomicOr((unsigned long long*)&l_rej[i], (unsigned long long)rej);
+          // namespace bypass (service.rs:40-71): AdmissionRequest in the always-accept namespace
+          l_byp[i] = H.bypass_bit >= 0 && !(rf & KW_REQ_RAW) && (rf & KW_REQ_HAS_NAMESPACE) && ((nsm >> H.bypass_bit) & 1ull);
+        } else if (w < n0 + n1) {  // container
+          const uint32_t i = w - n0;
+          const uint32_t q = own_c[i];
+          if (!(l_rf[q] & KW_REQ_HAS_PODSPEC)) continue;
+          const uint32_t c0 = l_coff[q] - cb;
+          uint64_t pre = 0;
+          for (uint32_t j = c0; j < i; ++j) pre |= l_vc[j];
+          const uint64_t nv = l_vc[i] & ~pre;
+          const uint32_t ci = i - c0;
+          uint32_t* vw = l_vw + q * t.vw_stride;
+          if (nv) {
+            put_viol(vw, nv & privany, vword(KW_R_PRIVILEGED, pack1(ci)));
+            put_viol(vw, nv & SH.aa, vword(KW_R_APPARMOR, pack1(ci)));
+            uint64_t cn = nv & SH.caps;  // capability slots: the first added capability of the list
+            for (uint32_t k = l_cadd[i] - kab, k0 = k, k1 = l_cadd[i + 1] - kab; k < k1 && cn; ++k) {
+              const uint64_t nw = l_vadd[k] & cn;
+              put_viol(vw, nw, vword(KW_R_CAP_NOT_ALLOWED, pack2(ci, k - k0)));
+              cn &= ~nw;
+            }
+            uint64_t tn = nv & SH.trs;  // trusted-repos slots: reasons in precedence order
+            if (tn) {
+              uint64_t why[5];
+              trs_whys(sv, lds, t, i, why);
+              for (uint32_t k = 0; k < 5; ++k) {
+                const uint64_t nw = why[k] & tn;
+                put_viol(vw, nw, vword(KW_R_REG_NOT_ALLOWED + k, pack1(ci)));
+                tn &= ~nw;
+              }
+            }
+            atomicOr((unsigned long long*)&l_rej[q], (unsigned long long)nv);
+          }
+          if (SH.caps) {  // mutation: required drops missing, default adds neither added nor dropped
+            uint64_t addm = 0, dropm = 0;
+            if (t.o_m[M_CAPADD])
+              for (uint32_t k = l_cadd[i] - kab, k1 = l_cadd[i + 1] - kab; k < k1; ++k)
+                addm |= idx_mask(lds[t.o_m[M_CAPADD] + k]);
+            if (t.o_m[M_CAPDROP])
+              for (uint32_t k = l_cdrop[i] - kdb, k1 = l_cdrop[i + 1] - kdb; k < k1; ++k)
+                dropm |= idx_mask(lds[t.o_m[M_CAPDROP] + k]);
+            uint64_t mut = 0;
+            if (!(dropm & SH.cap_all)) mut |= tab_or(sv.tab(ST_REQD), SH.reqd_union & ~dropm);
+            mut |= tab_or(sv.tab(ST_DEFA), SH.defa_union & ~(addm | dropm));
+            mut &= SH.caps;
+            if (mut) atomicOr((unsigned long long*)&l_mut[q], (unsigned long long)mut);
+          }
+        } else {  // label
+          const uint32_t i = w - n0 - n1;
+          const uint64_t v = l_vl[i];
+          if (!v) continue;
+          const uint32_t q = own_l[i];
+          const uint32_t l0 = l_loff[q] - lb;
+          uint64_t pre = 0;
+          for (uint32_t j = l0; j < i; ++j) pre |= l_vl[j];
+          const uint64_t nv = v & ~pre;
+          if (!nv) continue;
+          const uint32_t kb = lds[t.o_m[M_LK] + i];
+          const uint64_t den = sv.tab(ST_DENY)[kb];
+          const uint32_t li = i - l0;
+          uint32_t* vw = l_vw + q * t.vw_stride;
+          put_viol(vw, nv & den, vword(KW_R_LABEL_DENIED, pack1(li)));
+          put_viol(vw, nv & ~den, vword(KW_R_LABEL_CONSTRAINT, pack2(li, 0)) | kb);
+          atomicOr((unsigned long long*)&l_rej[q], (unsigned long long)nv);
+        }
+      }
+    } else {
+      for (uint32_t i = tid; i < nr; i += kSlotThreads) l_byp[i] = 0;
     }
     __syncthreads();
 

@@ -61,10 +61,12 @@ struct TileArgs {
   uint32_t rows;                  // requests per tile (kSlotRows)
   uint32_t cmax, kmax, lmax;      // container / capability / label capacity of a staged tile
   uint32_t o_rf, o_coff, o_loff, o_cflags, o_cadd, o_cdrop, o_gstk;  // LDS byte offsets
-  uint32_t o_m[NMASK];            // LDS byte offset of each staged per-string array, 0 = not read: u8 pattern
+  uint32_t o_m[NMASK];            // LDS byte offset of each per-string array P1 fills, 0 = none: u8 pattern
                                   // index (0xff none) for NS / CAPADD / CAPDROP / LK, u64 masks for
-                                  // REG / TAG / IMG, u64 violation sets for AA; LV is never staged
-  uint32_t o_vadd, o_vl;          // u64 violation set per added capability; u64 vcon per label
+                                  // REG / TAG / IMG; AA and LV only feed the violation sets
+  uint32_t use_mask;              // bit m: mask m has patterns (its strings are classified)
+  uint32_t o_vadd, o_vl, o_vc;    // u64 violation sets: per added capability, per label (V_l), per container (V_c)
+  uint32_t o_own_c, o_own_l;      // u8 tile-local request of each staged container / label
   uint32_t o_rej, o_mut, o_byp;   // per-request walk results: rejected / mutated slots, bypass flag
   uint32_t o_sa;                  // u32[NMASK]: the tile's staged byte start per string column (TileDesc.sa)
   uint32_t o_vw, vw_stride;       // violation words [rows][vw_stride] (aliases the staged strings)

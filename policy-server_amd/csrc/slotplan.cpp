@@ -121,11 +121,10 @@ struct Builder {
     }
     h.o_ce = off;
     off += (uint32_t)(ce.size() * sizeof(ConstrEnt));
-    h.o_mand = h.lbl ? off : 0;
-    if (h.lbl) off += sizeof(mand);
     // the device stages everything up to o_cols: the column arrays are the staged form of the
-    // column records (P3 reads 4 columns per array with one 16-B LDS load); ColInfo and cidx stay
-    // in global memory (group / constant columns and constraint settings indices)
+    // column records (P3 reads 4 columns per array with one 16-B LDS load); ColInfo, mand and cidx
+    // stay in global memory (group / constant columns, the arguments of mandatory-label and
+    // constraint violations)
     const uint32_t cs_n = ((uint32_t)cols.size() + 3u) & ~3u;
     off = (off + 15u) & ~15u;
     h.o_csoa = (uint16_t)off;
@@ -133,6 +132,8 @@ struct Builder {
     h.o_cols = off;
     off += (uint32_t)(cols.size() * sizeof(ColInfo));
     off = (off + 15u) & ~15u;
+    h.o_mand = h.lbl ? off : 0;
+    if (h.lbl) off += sizeof(mand);
     h.o_cidx = 0;
     if (h.lbl) {
       h.o_cidx = off;

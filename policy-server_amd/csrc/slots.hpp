@@ -81,11 +81,12 @@ struct alignas(16) ColInfo {
 };
 static_assert(sizeof(ColInfo) == 32, "ColInfo layout");
 
-// Record: SlotHdr | emitted tables u64[64] | ConstrEnt ce[nce] | u8 mand[64][16] | ColInfo[ncols]
-//         | u8 cidx[nslots][64]
+// Record: SlotHdr | emitted tables u64[64] | ConstrEnt ce[nce] | u32 column arrays[4][ncols↑4]
+//         | ColInfo[ncols] | u8 mand[64][16] | u8 cidx[nslots][64]
+// The device stages the record up to o_cols in LDS; the rest it reads from the global copy.
 // mand[s]: the label-key bits of slot s's mandatory_labels in settings order, 0xff-terminated.
 // cidx[s][k]: settings index of slot s's constraint on label-key bit k (read only to format a
-// constraint violation; the device keeps it out of LDS and reads it from the global copy).
+// constraint violation).
 
 KW_HD inline uint32_t kw_ctz64(uint64_t x) { return (uint32_t)__builtin_ctzll(x); }
 KW_HD inline uint32_t pack2(uint32_t a, uint32_t b) { return ((a < 255u ? a : 255u) << 8) | (b < 255u ? b : 255u); }
