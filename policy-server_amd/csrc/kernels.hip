@@ -574,6 +574,7 @@ __device__ inline uint64_t classify_value(const TileArgs& t, const uint8_t* lds,
   return vm;
 }
 
+__device__ inline uint32_t rup64(uint32_t n) { return (n + 63u) & ~63u; }
 __device__ inline uint64_t idx_mask(uint32_t v) { return v < 64u ? 1ull << v : 0ull; }
 
 // Trusted-repos reasons of staged container i, in precedence order (registry not allowed, registry
@@ -723,34 +724,30 @@ __global__ void __launch_bounds__(kSlotThreads)
       const uint32_t n1 = (t.use_mask & ((1u << M_REG) | (1u << M_TAG) | (1u << M_IMG))) ? nc : 0u;
       const uint32_t n2 = ctr_fam ? nc : 0u;
       const uint32_t n3 = t.o_m[M_LK] ? le - lb : 0u;
-      const uint32_t s1 = n0, s2 = s1 + n1, s3 = s2 + n2, s4 = s3 + n3;
-      for (uint32_t w = tid; w < s4; w += kSlotThreads) {
-        if (w < s1) {  // request: namespace and the owner maps
+      // item segments in falling cost order, each padded to whole waves: a wave's 64 items are one
+      // kind (no divergence between kinds) and the round-robin of waves over segments balances
+      const uint32_t e0 = rup64(n3), e1 = e0 + rup64(n2), e2 = e1 + rup64(n1), e3 = e2 + rup64(n0);
+      for (uint32_t w = tid; w < e3; w += kSlotThreads) {
+        if (w < e0) {  // label: key, value -> V_l = denied | constrained-and-failed slots
           const uint32_t i = w;
-          if (t.o_m[M_NS]) lds[t.o_m[M_NS] + i] = lit_index(lit(M_NS, i, (uint32_t)r0));
-          for (uint32_t c = l_coff[i] - cb, c1 = l_coff[i + 1] - cb; c < c1; ++c) own_c[c] = (uint8_t)i;
-          for (uint32_t l = l_loff[i] - lb, l1 = l_loff[i + 1] - lb; l < l1; ++l) own_l[l] = (uint8_t)i;
-        } else if (w < s2) {  // image reference: one parse feeds the registry, tag and image chains
-          const uint32_t i = w - s1;
-          uint64_t mr = 0, mt = 0, mi = 0;
-          if (!classify) {
+          if (i >= n3) continue;
+          const uint64_t r = lit(M_LK, i, lb);
+          uint64_t vm = 0;
+          if (!r) {
           } else if (FUSED) {
-            if (cfl[i] & KW_CTR_HAS_IMAGE) {
-              const uint32_t* so = (const uint32_t*)(lds + t.o_so[M_IMG]);
-              const uint32_t sa = l_sa[M_IMG];
-              classify_image_all(ch[M_REG], ch[M_TAG], ch[M_IMG], lds + t.o_sb[M_IMG], so[i] - sa, so[i + 1] - sa, &mr,
-                                 &mt, &mi);
+            if (t.o_sb[M_LV] && !(t.debug & 512u)) {
+              const uint32_t* vo = (const uint32_t*)(lds + t.o_so[M_LV]);
+              const uint32_t vsa = l_sa[M_LV];
+              vm = classify_value(t, lds, r, lds + t.o_sb[M_LV], vo[i] - vsa, vo[i + 1] - vsa);
             }
           } else {
-            if (a.m[M_REG]) mr = a.m[M_REG][cb + i];
-            if (a.m[M_TAG]) mt = a.m[M_TAG][cb + i];
-            if (a.m[M_IMG]) mi = a.m[M_IMG][cb + i];
+            vm = a.m[M_LV] ? a.m[M_LV][lb + i] : 0ull;
           }
-          if (t.o_m[M_REG]) ((uint64_t*)(lds + t.o_m[M_REG]))[i] = mr;
-          if (t.o_m[M_TAG]) ((uint64_t*)(lds + t.o_m[M_TAG]))[i] = mt;
-          if (t.o_m[M_IMG]) ((uint64_t*)(lds + t.o_m[M_IMG]))[i] = mi;
-        } else if (w < s3) {  // container: V_c over the privileged, capability and AppArmor slots
-          const uint32_t i = w - s2;
+          lds[t.o_m[M_LK] + i] = lit_index(r);
+          l_vl[i] = (r && SH.lbl) ? derive_label(sv, r, vm) | sv.tab(ST_DENY)[kw_ctz64(r)] : 0ull;
+        } else if (w < e1) {  // container: V_c over the privileged, capability and AppArmor slots
+          const uint32_t i = w - e0;
+          if (i >= n2) continue;
           const uint32_t fl = cfl[i];
           uint64_t v = 0;
           if ((fl & KW_CTR_PRIVILEGED) && privany) {
@@ -776,22 +773,32 @@ __global__ void __launch_bounds__(kSlotThreads)
               lds[t.o_m[M_CAPDROP] + k] = lit_index(lit(M_CAPDROP, k, kdb));
           }
           l_vc[i] = v;
-        } else {  // label: key, value -> V_l = denied | constrained-and-failed slots
-          const uint32_t i = w - s3;
-          const uint64_t r = lit(M_LK, i, lb);
-          uint64_t vm = 0;
-          if (!r) {
+        } else if (w < e2) {  // image reference: one parse feeds the registry, tag and image chains
+          const uint32_t i = w - e1;
+          if (i >= n1) continue;
+          uint64_t mr = 0, mt = 0, mi = 0;
+          if (!classify) {
           } else if (FUSED) {
-            if (t.o_sb[M_LV] && !(t.debug & 512u)) {
-              const uint32_t* vo = (const uint32_t*)(lds + t.o_so[M_LV]);
-              const uint32_t vsa = l_sa[M_LV];
-              vm = classify_value(t, lds, r, lds + t.o_sb[M_LV], vo[i] - vsa, vo[i + 1] - vsa);
+            if (cfl[i] & KW_CTR_HAS_IMAGE) {
+              const uint32_t* so = (const uint32_t*)(lds + t.o_so[M_IMG]);
+              const uint32_t sa = l_sa[M_IMG];
+              classify_image_all(ch[M_REG], ch[M_TAG], ch[M_IMG], lds + t.o_sb[M_IMG], so[i] - sa, so[i + 1] - sa, &mr,
+                                 &mt, &mi);
             }
           } else {
-            vm = a.m[M_LV] ? a.m[M_LV][lb + i] : 0ull;
+            if (a.m[M_REG]) mr = a.m[M_REG][cb + i];
+            if (a.m[M_TAG]) mt = a.m[M_TAG][cb + i];
+            if (a.m[M_IMG]) mi = a.m[M_IMG][cb + i];
           }
-          lds[t.o_m[M_LK] + i] = lit_index(r);
-          l_vl[i] = (r && SH.lbl) ? derive_label(sv, r, vm) | sv.tab(ST_DENY)[kw_ctz64(r)] : 0ull;
+          if (t.o_m[M_REG]) ((uint64_t*)(lds + t.o_m[M_REG]))[i] = mr;
+          if (t.o_m[M_TAG]) ((uint64_t*)(lds + t.o_m[M_TAG]))[i] = mt;
+          if (t.o_m[M_IMG]) ((uint64_t*)(lds + t.o_m[M_IMG]))[i] = mi;
+        } else {  // request: namespace and the owner maps
+          const uint32_t i = w - e2;
+          if (i >= n0) continue;
+          if (t.o_m[M_NS]) lds[t.o_m[M_NS] + i] = lit_index(lit(M_NS, i, (uint32_t)r0));
+          for (uint32_t c = l_coff[i] - cb, c1 = l_coff[i + 1] - cb; c < c1; ++c) own_c[c] = (uint8_t)i;
+          for (uint32_t l = l_loff[i] - lb, l1 = l_loff[i + 1] - lb; l < l1; ++l) own_l[l] = (uint8_t)i;
         }
       }
     }
@@ -815,45 +822,11 @@ __global__ void __launch_bounds__(kSlotThreads)
     }
     if (!(t.debug & 2u)) {
       const uint32_t n0 = nr, n1 = ctr_fam ? nc : 0u, n2 = (SH.lbl && t.o_m[M_LK]) ? le - lb : 0u;
-      for (uint32_t w = tid; w < n0 + n1 + n2; w += kSlotThreads) {
-        if (w < n0) {  // request: namespace, mandatory labels, bypass
+      const uint32_t f0 = rup64(n1), f1 = f0 + rup64(n2), f2 = f1 + rup64(n0);  // as in P1
+      for (uint32_t w = tid; w < f2; w += kSlotThreads) {
+        if (w < f0) {  // container
           const uint32_t i = w;
-          const uint32_t rf = l_rf[i];
-          uint32_t* vw = l_vw + i * t.vw_stride;
-          const uint64_t nsm = t.o_m[M_NS] ? idx_mask(lds[t.o_m[M_NS] + i]) : 0ull;
-          uint64_t rej = 0;
-          if (SH.ns) {
-            const uint64_t ok = (rf & KW_REQ_HAS_NAMESPACE) ? tab_or(sv.tab(ST_NSOK), nsm) : 0ull;
-            rej = SH.ns & ~ok;
-            put_viol(vw, rej, vword(KW_R_NAMESPACE, 0));
-          }
-          if (SH.lbl && SH.mand_union && t.o_m[M_LK]) {
-            uint64_t present = 0, lrej = 0;
-            for (uint32_t l = l_loff[i] - lb, l1 = l_loff[i + 1] - lb; l < l1; ++l) {
-              present |= idx_mask(lds[t.o_m[M_LK] + l]);
-              lrej |= l_vl[l];
-            }
-            uint64_t nw = tab_or(sv.tab(ST_MAND), SH.mand_union & ~present) & ~lrej;
-            rej |= nw;
-            const uint8_t* mand = t.slot_plan + SH.o_mand;  // global: read only for a violation
-            while (nw) {  // the first missing mandatory key of each such slot, settings order
-              const uint32_t sl = kw_ctz64(nw);
-              nw &= nw - 1;
-              const uint4 mk = *(const uint4*)(mand + sl * 16u);
-              const uint32_t mw[4] = {mk.x, mk.y, mk.z, mk.w};
-              uint32_t k = 0;
-              for (; k < 16; ++k) {
-                const uint32_t kb = (mw[k >> 2] >> (8 * (k & 3))) & 0xffu;
-                if (kb == 0xffu || !((present >> kb) & 1ull)) break;
-              }
-              vw[sl] = vword(KW_R_LABEL_MANDATORY, k);
-            }
-          }
-          if (rej) atomicOr((unsigned long long*)&l_rej[i], (unsigned long long)rej);
-          // namespace bypass (service.rs:40-71): AdmissionRequest in the always-accept namespace
-          l_byp[i] = H.bypass_bit >= 0 && !(rf & KW_REQ_RAW) && (rf & KW_REQ_HAS_NAMESPACE) && ((nsm >> H.bypass_bit) & 1ull);
-        } else if (w < n0 + n1) {  // container
-          const uint32_t i = w - n0;
+          if (i >= n1) continue;
           const uint32_t q = own_c[i];
           if (!(l_rf[q] & KW_REQ_HAS_PODSPEC)) continue;
           const uint32_t c0 = l_coff[q] - cb;
@@ -897,8 +870,9 @@ __global__ void __launch_bounds__(kSlotThreads)
             mut &= SH.caps;
             if (mut) atomicOr((unsigned long long*)&l_mut[q], (unsigned long long)mut);
           }
-        } else {  // label
-          const uint32_t i = w - n0 - n1;
+        } else if (w < f1) {  // label
+          const uint32_t i = w - f0;
+          if (i >= n2) continue;
           const uint64_t v = l_vl[i];
           if (!v) continue;
           const uint32_t q = own_l[i];
@@ -914,6 +888,43 @@ __global__ void __launch_bounds__(kSlotThreads)
           put_viol(vw, nv & den, vword(KW_R_LABEL_DENIED, pack1(li)));
           put_viol(vw, nv & ~den, vword(KW_R_LABEL_CONSTRAINT, pack2(li, 0)) | kb);
           atomicOr((unsigned long long*)&l_rej[q], (unsigned long long)nv);
+        } else {  // request: namespace, mandatory labels, bypass
+          const uint32_t i = w - f1;
+          if (i >= n0) continue;
+          const uint32_t rf = l_rf[i];
+          uint32_t* vw = l_vw + i * t.vw_stride;
+          const uint64_t nsm = t.o_m[M_NS] ? idx_mask(lds[t.o_m[M_NS] + i]) : 0ull;
+          uint64_t rej = 0;
+          if (SH.ns) {
+            const uint64_t ok = (rf & KW_REQ_HAS_NAMESPACE) ? tab_or(sv.tab(ST_NSOK), nsm) : 0ull;
+            rej = SH.ns & ~ok;
+            put_viol(vw, rej, vword(KW_R_NAMESPACE, 0));
+          }
+          if (SH.lbl && SH.mand_union && t.o_m[M_LK]) {
+            uint64_t present = 0, lrej = 0;
+            for (uint32_t l = l_loff[i] - lb, l1 = l_loff[i + 1] - lb; l < l1; ++l) {
+              present |= idx_mask(lds[t.o_m[M_LK] + l]);
+              lrej |= l_vl[l];
+            }
+            uint64_t nw = tab_or(sv.tab(ST_MAND), SH.mand_union & ~present) & ~lrej;
+            rej |= nw;
+            const uint8_t* mand = t.slot_plan + SH.o_mand;  // global: read only for a violation
+            while (nw) {  // the first missing mandatory key of each such slot, settings order
+              const uint32_t sl = kw_ctz64(nw);
+              nw &= nw - 1;
+              const uint4 mk = *(const uint4*)(mand + sl * 16u);
+              const uint32_t mw[4] = {mk.x, mk.y, mk.z, mk.w};
+              uint32_t k = 0;
+              for (; k < 16; ++k) {
+                const uint32_t kb = (mw[k >> 2] >> (8 * (k & 3))) & 0xffu;
+                if (kb == 0xffu || !((present >> kb) & 1ull)) break;
+              }
+              vw[sl] = vword(KW_R_LABEL_MANDATORY, k);
+            }
+          }
+          if (rej) atomicOr((unsigned long long*)&l_rej[i], (unsigned long long)rej);
+          // namespace bypass (service.rs:40-71): AdmissionRequest in the always-accept namespace
+          l_byp[i] = H.bypass_bit >= 0 && !(rf & KW_REQ_RAW) && (rf & KW_REQ_HAS_NAMESPACE) && ((nsm >> H.bypass_bit) & 1ull);
         }
       }
     } else {
