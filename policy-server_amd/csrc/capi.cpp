@@ -73,10 +73,14 @@ struct DeviceBatch {
   uint32_t* overflow = nullptr;  // [count, tile indices...]
   size_t overflow_cap = 0;
   uint32_t n_overflow = 0;
+  uint64_t ndesc = 0;  // tile descriptors (halved runs included)
   uint64_t desc_key = 0;
   // slot-kernel tile capacities of this batch (plan_pass)
   bool stats_valid = false;
-  TileStats stats, stats_max;
+  std::vector<TileStats> tile_need;  // per-tile entity counts and staged string bytes
+  std::vector<TileStats> tile_q;     // their quantiles at kTileQuantiles
+  uint64_t cap_key = 0;              // layout inputs of the last capacity choice, and the choice
+  int cap_choice = -1;
   ~DeviceBatch() {
     if (device >= 0) (void)hipSetDevice(device);
     (void)hipFree(d_tiles);
@@ -208,6 +212,7 @@ const DeviceBatch::DCol& mask_strings(const DeviceBatch& D, int m) {
 
 constexpr uint32_t kFusedTableBudget = 48 * 1024;  // DFA chains staged per workgroup
 constexpr uint32_t kTileLdsBudget = 160 * 1024;  // slot-kernel LDS per workgroup (gfx950: 160 KB per CU)
+constexpr double kTileQuantiles[] = {1.0, 0.99995, 0.9999, 0.9995, 0.999, 0.998};  // capacity candidates
 
 // Per-tile entity counts and staged byte ranges of a batch (kSlotRows-request tiles), reduced to a
 // high quantile: the LDS capacities of the slot kernel. Tiles above them (the tail) take the
@@ -215,24 +220,20 @@ constexpr uint32_t kTileLdsBudget = 160 * 1024;  // slot-kernel LDS per workgrou
 
 const StrCol& host_strings(const Batch& B, int m);
 
-TileStats tile_stats(const Batch& B, uint32_t rows, double quantile) {
-  TileStats st;
+// What each tile of `rows` requests stages: entity counts and the 16-B aligned byte span of each
+// staged string column.
+std::vector<TileStats> tile_needs(const Batch& B, uint32_t rows) {
   const uint64_t ntiles = (B.n + rows - 1) / rows;
-  if (!ntiles) return st;
-  std::vector<uint32_t> v(ntiles);
-  const uint64_t q = ntiles < 2000 ? ntiles - 1 : (uint64_t)(quantile * (double)(ntiles - 1));
-  auto quant = [&](auto f) {
-    for (uint64_t t = 0; t < ntiles; ++t) v[t] = f(t * rows, std::min<uint64_t>(B.n, (t + 1) * rows));
-    std::nth_element(v.begin(), v.begin() + (long)q, v.end());
-    return v[q];
-  };
-  st.ctr = quant([&](uint64_t r0, uint64_t r1) { return B.ctr_off[r1] - B.ctr_off[r0]; });
-  st.lbl = quant([&](uint64_t r0, uint64_t r1) { return B.lbl_off[r1] - B.lbl_off[r0]; });
-  st.kadd = quant([&](uint64_t r0, uint64_t r1) { return B.capadd_off[B.ctr_off[r1]] - B.capadd_off[B.ctr_off[r0]]; });
-  st.kdrop = quant([&](uint64_t r0, uint64_t r1) { return B.capdrop_off[B.ctr_off[r1]] - B.capdrop_off[B.ctr_off[r0]]; });
-  for (int m : {M_NS, M_IMG, M_AA, M_CAPADD, M_CAPDROP, M_LK, M_LV}) {
-    const StrCol& c = host_strings(B, m);
-    st.bytes[m] = quant([&](uint64_t r0, uint64_t r1) {
+  std::vector<TileStats> v(ntiles);
+  for (uint64_t t = 0; t < ntiles; ++t) {
+    const uint64_t r0 = t * rows, r1 = std::min<uint64_t>(B.n, (t + 1) * rows);
+    TileStats& st = v[t];
+    st.ctr = B.ctr_off[r1] - B.ctr_off[r0];
+    st.lbl = B.lbl_off[r1] - B.lbl_off[r0];
+    st.kadd = B.capadd_off[B.ctr_off[r1]] - B.capadd_off[B.ctr_off[r0]];
+    st.kdrop = B.capdrop_off[B.ctr_off[r1]] - B.capdrop_off[B.ctr_off[r0]];
+    for (int m : {M_NS, M_IMG, M_AA, M_CAPADD, M_CAPDROP, M_LK, M_LV}) {
+      const StrCol& c = host_strings(B, m);
       uint64_t g0, g1;
       switch (m) {
         case M_NS: g0 = r0; g1 = r1; break;
@@ -241,9 +242,30 @@ TileStats tile_stats(const Batch& B, uint32_t rows, double quantile) {
         case M_LK: case M_LV: g0 = B.lbl_off[r0]; g1 = B.lbl_off[r1]; break;
         default: g0 = B.ctr_off[r0]; g1 = B.ctr_off[r1]; break;
       }
-      return ((c.off[g1] + 15u) & ~15u) - (c.off[g0] & ~15u);
-    });
+      st.bytes[m] = ((c.off[g1] + 15u) & ~15u) - (c.off[g0] & ~15u);
+    }
   }
+  return v;
+}
+
+// Per-dimension quantile of the tile needs (quantile 1 = the batch maximum).
+TileStats tile_quantile(const std::vector<TileStats>& need, double quantile) {
+  TileStats st;
+  if (need.empty()) return st;
+  const uint64_t n = need.size();
+  const uint64_t q = quantile >= 1.0 ? n - 1 : (uint64_t)(quantile * (double)(n - 1));
+  std::vector<uint32_t> v(n);
+  auto quant = [&](auto f) {
+    for (uint64_t t = 0; t < n; ++t) v[t] = f(need[t]);
+    std::nth_element(v.begin(), v.begin() + (long)q, v.end());
+    return v[q];
+  };
+  st.ctr = quant([](const TileStats& x) { return x.ctr; });
+  st.lbl = quant([](const TileStats& x) { return x.lbl; });
+  st.kadd = quant([](const TileStats& x) { return x.kadd; });
+  st.kdrop = quant([](const TileStats& x) { return x.kdrop; });
+  for (int m : {M_NS, M_IMG, M_AA, M_CAPADD, M_CAPDROP, M_LK, M_LV})
+    st.bytes[m] = quant([m](const TileStats& x) { return x.bytes[m]; });
   return st;
 }
 
@@ -405,8 +427,10 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
   TileArgs& T = plan->tile;
   auto align = [](uint32_t x) { return (x + 15u) & ~15u; };
   if (!D.stats_valid) {
-    D.stats = tile_stats(B, kSlotRows, 0.9995);
-    D.stats_max = tile_stats(B, kSlotRows, 1.0);
+    D.tile_need = tile_needs(B, kSlotRows);
+    D.tile_q.clear();
+    for (double q : kTileQuantiles) D.tile_q.push_back(tile_quantile(D.tile_need, q));
+    D.cap_choice = -1;
     D.stats_valid = true;
   }
   uint32_t chain_len[NMASK];  // per-string masks are whole-chain results (image chains walk in one item)
@@ -556,8 +580,43 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
   };
   // the batch maximum when it costs no occupancy over the high quantile (no overflow tiles at all)
   auto per_cu = [](uint32_t b) { return std::min<uint32_t>(2048 / kSlotThreads, (160 * 1024) / std::max<uint32_t>(b, 1)); };
-  const uint32_t lq = layout(D.stats);
-  if (per_cu(layout(D.stats_max)) < per_cu(lq)) layout(D.stats);
+  // Capacities: the highest occupancy (workgroups per CU, LDS-bound) whose layout splits at most
+  // 2 % of the tiles (a tile beyond the capacities runs as halves, upload_tile_descs), over
+  // per-dimension quantiles of the tile needs; at a given occupancy the largest capacities (fewest
+  // split tiles). Chosen once per batch and layout signature.
+  uint64_t key = ((uint64_t)table_bytes << 40) ^ ((uint64_t)slot_bytes << 20) ^ ((uint64_t)nslots << 8) ^
+                 (groups ? 1u : 0u) ^ (plan->fused ? 2u : 0u);
+  for (int m = 0; m < (int)NMASK; ++m) key = key * 3 + (use[m] ? 1 : 0);
+  if (D.cap_choice < 0 || D.cap_key != key) {
+    const uint64_t ntl = D.tile_need.size();
+    int best = 0;
+    uint32_t best_cu = 0;
+    for (int k = 0; k < (int)D.tile_q.size(); ++k) {
+      const uint32_t cu = per_cu(layout(D.tile_q[k]));
+      if (T.lds_bytes > kTileLdsBudget) continue;
+      uint64_t over = 0;  // tiles beyond these capacities (split by the descriptors' fit test)
+      for (const TileStats& x : D.tile_need) {
+        bool o = x.ctr > T.cmax || x.lbl > T.lmax || x.kadd > T.kmax || x.kdrop > T.kmax;
+        for (int m = 0; m < (int)NMASK && !o; ++m) o = T.sb_cap[m] && x.bytes[m] > T.sb_cap[m];
+        over += o;
+      }
+      if (getenv("KW_TILE_DEBUG") && (atoi(getenv("KW_TILE_DEBUG")) & 256))
+        fprintf(stderr, "[kw tile] candidate q=%g lds=%u wg/cu=%u split=%llu/%llu\n", kTileQuantiles[k], T.lds_bytes, cu,
+                (unsigned long long)over, (unsigned long long)ntl);
+      const double max_split = getenv("KW_TILE_SPLIT") ? atof(getenv("KW_TILE_SPLIT")) : 0.02;  // A/B knob
+      if (k > 0 && (double)over > max_split * (double)ntl) continue;
+      if (cu > best_cu) {
+        best = k;
+        best_cu = cu;
+      }
+    }
+    D.cap_key = key;
+    D.cap_choice = best;
+  }
+  if (const char* fq = getenv("KW_TILE_QUANTILE"))  // tests / diagnostics: force the capacity quantile
+    layout(tile_quantile(D.tile_need, atof(fq)));
+  else
+    layout(D.tile_q[D.cap_choice]);
   if (T.lds_bytes > kTileLdsBudget) return KW_E_ARG;  // policy set too large for one tile
   if (const char* dbg = getenv("KW_TILE_DEBUG")) T.debug = (uint32_t)atoi(dbg);  // phase ablation (diagnostics)
   if (T.debug & 256u)
@@ -636,12 +695,16 @@ int upload_tile_descs(const Batch& B, DeviceBatch* D, const TileArgs& T) {
   }
   if (D->desc && key == D->desc_key) return KW_OK;
   const uint64_t ntiles = (B.n + T.rows - 1) / T.rows;
-  std::vector<TileDesc> desc(ntiles);
+  std::vector<TileDesc> desc;
+  desc.reserve(ntiles + ntiles / 64 + 1);
   std::vector<uint32_t> ovf{0};
-  for (uint64_t tile = 0; tile < ntiles; ++tile) {
-    TileDesc& d = desc[tile];
+  // descriptor of requests [r0, r1); false when it exceeds the capacities
+  auto make = [&](uint64_t r0, uint64_t r1, TileDesc* dp) {
+    TileDesc& d = *dp;
     memset(&d, 0, sizeof(d));
-    const uint64_t r0 = tile * T.rows, r1 = std::min<uint64_t>(B.n, r0 + T.rows);
+    d.r0lo = (uint32_t)r0;
+    d.r0hi = (uint32_t)(r0 >> 32);
+    d.nr = (uint32_t)(r1 - r0);
     d.cb = B.ctr_off[r0];
     d.ce = B.ctr_off[r1];
     d.lb = B.lbl_off[r0];
@@ -661,13 +724,35 @@ int upload_tile_descs(const Batch& B, DeviceBatch* D, const TileArgs& T) {
       fits = fits && d.nv[m] * 16u <= T.sb_cap[m];
     }
     d.fits = fits ? 1u : 0u;
-    if (!fits) ovf.push_back((uint32_t)tile);
+    return fits;
+  };
+  // a run that does not fit is halved until its parts do; a single request that does not fit
+  // goes to the overflow kernels
+  std::vector<std::pair<uint64_t, uint64_t>> todo;
+  for (uint64_t tile = 0; tile < ntiles; ++tile) {
+    todo.assign(1, {tile * T.rows, std::min<uint64_t>(B.n, (tile + 1) * T.rows)});
+    while (!todo.empty()) {
+      const auto [r0, r1] = todo.back();
+      todo.pop_back();
+      TileDesc d;
+      if (make(r0, r1, &d)) {
+        desc.push_back(d);
+      } else if (r1 - r0 > 1) {
+        const uint64_t mid = r0 + (r1 - r0) / 2;
+        todo.push_back({mid, r1});
+        todo.push_back({r0, mid});
+      } else {
+        if (r0 > 0xffffffffull) return KW_E_ARG;  // overflow list holds u32 request indices
+        ovf.push_back((uint32_t)r0);
+      }
+    }
   }
   ovf[0] = (uint32_t)(ovf.size() - 1);
   HIPCHK(hipStreamSynchronize(D->stream));  // a running pass may still read the previous descriptors
-  if (int rc = ensure(&D->desc, &D->desc_cap, (size_t)std::max<uint64_t>(ntiles, 1))) return rc;
+  if (int rc = ensure(&D->desc, &D->desc_cap, std::max<size_t>(desc.size(), 1))) return rc;
   if (int rc = ensure(&D->overflow, &D->overflow_cap, ovf.size())) return rc;
-  if (ntiles) HIPCHK(hipMemcpy(D->desc, desc.data(), ntiles * sizeof(TileDesc), hipMemcpyHostToDevice));
+  if (!desc.empty()) HIPCHK(hipMemcpy(D->desc, desc.data(), desc.size() * sizeof(TileDesc), hipMemcpyHostToDevice));
+  D->ndesc = desc.size();
   HIPCHK(hipMemcpy(D->overflow, ovf.data(), ovf.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   D->n_overflow = ovf[0];
   D->desc_key = key;
@@ -696,9 +781,11 @@ int run_pass(const kw_env* env, kw_batch* kb, const PassPlan& plan, bool timed) 
       HIPCHK(hipMemcpy(D.d_tiles, D.h_tiles.data(), D.h_tiles.size() * sizeof(TileArgs), hipMemcpyHostToDevice));
     }
     if (int rc = upload_tile_descs(kb->b, &D, plan.tile)) return rc;
+    EvalArgs sa = plan.args;
+    sa.ndesc = D.ndesc;
     for (size_t k = 0; k < tiles.size(); ++k)
-      HIPCHK(launch_evaluate_slots(plan.args, tiles[k], D.d_tiles + k, D.desc, plan.fused, plan.grid, D.stream));
-    if (!tiles.empty()) HIPCHK(launch_overflow(plan.args, D.d_tiles, D.overflow, D.n_overflow, D.stream));
+      HIPCHK(launch_evaluate_slots(sa, tiles[k], D.d_tiles + k, D.desc, plan.fused, plan.grid, D.stream));
+    if (!tiles.empty()) HIPCHK(launch_overflow(sa, D.d_tiles, D.overflow, D.n_overflow, D.stream));
   }
   if (timed) HIPCHK(hipEventRecord(D.ev[2], D.stream));
   return KW_OK;

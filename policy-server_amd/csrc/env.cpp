@@ -724,7 +724,22 @@ Status build_env(const char* json, size_t len, bool continue_on_errors, const ch
         return o;
       };
       std::vector<size_t> recs;  // KvDfa record positions, linked per key below
+      std::map<std::vector<uint8_t>, uint16_t> chains;  // keys constrained by the same regexes share one chain
       for (size_t k = 0; k < kd.size(); ++k) {
+        if (kd[k].empty()) continue;
+        std::vector<uint8_t> sig;
+        for (const Dfa& d : kd[k]) {
+          const uint32_t hd[3] = {d.nstates, d.ncls, d.start};
+          sig.insert(sig.end(), (const uint8_t*)hd, (const uint8_t*)(hd + 3));
+          sig.insert(sig.end(), d.cls.begin(), d.cls.end());
+          sig.insert(sig.end(), (const uint8_t*)d.trans.data(), (const uint8_t*)(d.trans.data() + d.trans.size()));
+          sig.insert(sig.end(), (const uint8_t*)d.accept.data(), (const uint8_t*)(d.accept.data() + d.accept.size()));
+        }
+        auto hit = chains.find(sig);
+        if (hit != chains.end()) {
+          ((uint16_t*)r.data())[k] = hit->second;
+          continue;
+        }
         size_t prev = 0;
         for (const Dfa& d : kd[k]) {
           KvDfa kv;
@@ -764,6 +779,7 @@ Status build_env(const char* json, size_t len, bool continue_on_errors, const ch
           prev = rec;
           recs.push_back(rec);
         }
+        chains.emplace(std::move(sig), ((uint16_t*)r.data())[k]);
       }
       while (r.size() % 16) r.push_back(0);
       r.resize(r.size() + 16, 0);  // slack: dword-granular readers may run past the last table

@@ -667,12 +667,11 @@ __global__ void __launch_bounds__(kSlotThreads)
   uint8_t* own_l = lds + t.o_own_l;
 
   const uint32_t npol = a.npol;
-  const uint64_t ntiles = (a.nrows + kSlotRows - 1) / kSlotRows;
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  for (uint64_t tile = blockIdx.x; tile < a.ndesc; tile += gridDim.x) {
     const TileDesc& d = desc[tile];
-    if (!d.fits) continue;  // queued for overflow_kernel by the host (uniform: no barrier skipped unevenly)
-    const uint64_t r0 = tile * kSlotRows;
-    const uint32_t nr = (uint32_t)min((uint64_t)kSlotRows, a.nrows - r0);
+    if (!d.fits) continue;  // queued for the overflow kernels by the host (uniform: no barrier skipped unevenly)
+    const uint64_t r0 = ((uint64_t)d.r0hi << 32) | d.r0lo;
+    const uint32_t nr = d.nr;
     const uint32_t cb = d.cb, ce = d.ce, lb = d.lb, le = d.le;
     const uint32_t kab = d.kab, kae = d.kae, kdb = d.kdb, kde = d.kde;
     const uint32_t nc = ce - cb;
@@ -1013,12 +1012,11 @@ __global__ void __launch_bounds__(kSlotThreads)
   }
 }
 
-// Tiles whose entity counts or string bytes exceed the LDS capacities (listed by the host with the
-// tile descriptors in `overflow`: count, then tile indices; the capacities are a high quantile of the
-// batch's tiles, so the list is a short tail). Two launches: overflow_classify_kernel classifies the
-// strings of those tiles into the global mask arrays (DFA chains read from the blob, one workgroup
-// per tile), then overflow_eval_kernel evaluates every (row, column) pair of them from global
-// memory, one lane per pair.
+// Requests whose entity counts or string bytes exceed the LDS capacities even in a tile of their
+// own (listed by the host with the tile descriptors in `overflow`: count, then request indices).
+// Two launches: overflow_classify_kernel classifies their strings into the global mask arrays (DFA
+// chains read from the blob, one workgroup per request), then overflow_eval_kernel evaluates every
+// (request, column) pair from global memory, one lane per pair.
 constexpr int kOverflowThreads = 256;
 __global__ void __launch_bounds__(kOverflowThreads)
     overflow_classify_kernel(EvalArgs a, const TileArgs* __restrict__ tp, const uint32_t* __restrict__ overflow) {
@@ -1032,8 +1030,8 @@ __global__ void __launch_bounds__(kOverflowThreads)
     ch[k].base = a.blob + t.dfa_head[k];
   }
   for (uint32_t q = blockIdx.x; q < count; q += gridDim.x) {
-    const uint64_t r0 = (uint64_t)overflow[1 + q] * t.rows;
-    const uint32_t nr = (uint32_t)min((uint64_t)t.rows, a.nrows - r0);
+    const uint64_t r0 = overflow[1 + q];
+    const uint32_t nr = 1;
     const uint32_t cb = a.ctr_off[r0], ce = a.ctr_off[r0 + nr];
     const uint32_t lb = a.lbl_off[r0], le = a.lbl_off[r0 + nr];
     const uint32_t kab = a.capadd_off[cb], kae = a.capadd_off[ce];
@@ -1083,16 +1081,14 @@ __global__ void __launch_bounds__(kOverflowThreads)
   const uint32_t count = overflow[0];
   const DevHeader H = *(const DevHeader*)a.blob;
   const DevPolicy* __restrict__ pols = (const DevPolicy*)(a.blob + H.policy_off);
-  const uint32_t npol = a.npol, rows = t.rows;
-  const uint64_t items = (uint64_t)count * rows * npol;
+  const uint32_t npol = a.npol;
+  const uint64_t items = (uint64_t)count * npol;
   GlobalSrc src{&a};
+  (void)t;
   for (uint64_t it = (uint64_t)blockIdx.x * kOverflowThreads + threadIdx.x; it < items;
        it += (uint64_t)gridDim.x * kOverflowThreads) {
     const uint32_t j = (uint32_t)(it % npol);
-    const uint64_t qr = it / npol;
-    const uint32_t rr = (uint32_t)(qr % rows), q = (uint32_t)(qr / rows);
-    const uint64_t r = (uint64_t)overflow[1 + q] * rows + rr;
-    if (r >= a.nrows) continue;
+    const uint64_t r = overflow[1 + it / npol];
     const DevPolicy& P = pols[a.pols[j]];
     a.out[r * npol + j] = verdict(src, a, H, pols, P, r, gstk + threadIdx.x, kOverflowThreads);
   }
@@ -1142,7 +1138,7 @@ hipError_t launch_overflow(const EvalArgs& a, const TileArgs* d_t, const uint32_
   if (n_overflow == 0 || a.nrows == 0 || a.npol == 0) return hipSuccess;
   hipLaunchKernelGGL(overflow_classify_kernel, dim3(std::min<uint32_t>(n_overflow, 1024)), dim3(kOverflowThreads), 0, s,
                      a, d_t, d_overflow);
-  const uint64_t items = (uint64_t)n_overflow * kSlotRows * a.npol;
+  const uint64_t items = (uint64_t)n_overflow * a.npol;
   const uint32_t blocks = (uint32_t)std::min<uint64_t>((items + kOverflowThreads - 1) / kOverflowThreads, 4096);
   hipLaunchKernelGGL(overflow_eval_kernel, dim3(blocks), dim3(kOverflowThreads), 0, s, a, d_t, d_overflow);
   return hipGetLastError();

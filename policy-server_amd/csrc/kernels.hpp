@@ -36,6 +36,7 @@ struct ClassifyJobs {
 struct EvalArgs {
   const uint8_t* blob;
   uint64_t nrows;
+  uint64_t ndesc;             // slot kernel: tile descriptors (TileDesc) to walk
   uint64_t npairs;
   uint32_t npol;              // policies per row (all-pairs mode)
   int32_t origin;
@@ -101,12 +102,15 @@ hipError_t launch_evaluate_rows(const EvalArgs& a, hipStream_t s);
 // Per-tile geometry, precomputed on the host from the batch's offsets (one s_load burst per tile
 // instead of a chain of dependent global loads): entity ranges, the 16-B aligned byte range of each
 // staged string column, and whether the tile fits the LDS capacities.
+// A tile is a run of at most kSlotRows requests; runs that exceed the LDS capacities are halved
+// until they fit, and single requests that still do not fit go to the overflow kernels.
 struct alignas(16) TileDesc {
   uint32_t cb, ce, lb, le, kab, kae, kdb, kde;
   uint32_t sa[NMASK];  // staged column m: first byte (16-B aligned) of the tile's strings in the pool
   uint32_t nv[NMASK];  //                  16-B vectors to copy
   uint32_t fits;
-  uint32_t pad[5];
+  uint32_t r0lo, r0hi, nr;  // first request (64-bit) and request count
+  uint32_t pad[2];
 };
 static_assert(sizeof(TileDesc) == 128, "TileDesc layout");
 
@@ -114,8 +118,8 @@ static_assert(sizeof(TileDesc) == 128, "TileDesc layout");
 // same TileArgs resident in device memory (read by the kernel).
 hipError_t launch_evaluate_slots(const EvalArgs& a, const TileArgs& t, const TileArgs* d_t, const TileDesc* d_desc,
                                  bool fused, uint32_t grid, hipStream_t s);
-// Tiles that do not fit the LDS capacities (d_overflow: [count, tile indices...], host-built with
-// the descriptors), evaluated from global memory for every column.
+// Requests that do not fit the LDS capacities even alone (d_overflow: [count, request indices...],
+// host-built with the descriptors), evaluated from global memory for every column.
 hipError_t launch_overflow(const EvalArgs& a, const TileArgs* d_t, const uint32_t* d_overflow, uint32_t n_overflow,
                            hipStream_t s);
 

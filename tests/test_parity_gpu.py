@@ -11,7 +11,7 @@ import pytest
 
 import kwgpu as K
 import oracle as O
-from helpers import config, diff_verdicts
+from helpers import config, diff_verdicts, wide_docs
 
 pytestmark = pytest.mark.gpu
 NS = "kubewarden"
@@ -153,3 +153,34 @@ def test_edge_batches():
     empty = K.Batch.from_json([]).to_device(0)
     empty.validate(env, ids)
     assert len(empty.verdicts()) == 0
+
+
+@pytest.mark.parametrize("q", ["0.5", "0.05"])
+@pytest.mark.parametrize("name,scfg,rows", [CASES[0], CASES[4]])
+def test_split_tiles_match_oracle(monkeypatch, name, scfg, rows, q):
+    """Capacities forced below most tiles' needs (KW_TILE_QUANTILE): tiles run as halved request
+    runs and single requests beyond the capacities take the overflow kernels; verdicts unchanged."""
+    monkeypatch.setenv("KW_TILE_QUANTILE", q)
+    env, oe = _envs(name)
+    ids = env.policy_ids()
+    syn = K.SynthBatch(scfg, rows, seed=4242 + scfg)
+    b = syn.batch().to_device(0)
+    b.validate(env, ids, K.VALIDATE)
+    gpu = b.verdicts()
+    ora = oe.eval(syn.soa(), ids, K.VALIDATE)
+    assert np.array_equal(gpu, ora), diff_verdicts(gpu, ora, len(ids), ids)
+
+
+def test_wide_requests():
+    """Requests with more than 64 containers / labels (entity indices past one byte of the reason
+    argument) among ordinary ones, C4 policies."""
+    doc = config("c4_64")
+    env = K.EvaluationEnvironment(doc, device=0)
+    oe = O.OracleEnv(doc)
+    ids = env.policy_ids()
+    docs = wide_docs()
+    b = K.Batch.from_json(docs).to_device(0)
+    b.validate(env, ids)
+    gpu = b.verdicts()
+    ora = oe.eval(b.view(), ids)
+    assert np.array_equal(gpu, ora), diff_verdicts(gpu, ora, len(ids), ids)

@@ -1,8 +1,9 @@
 """CPU: the slot compiler (slotplan.cpp) and the bit-parallel entity walks (slots.hpp) that the
 device's evaluate_slots_kernel runs agree with the oracle, bit-exact, on every configuration.
 
-kw_debug_host_walk runs the same walk code on the host with the blob's column automata. It is a
-diagnostic of the slot compiler only (the product path is the GPU: kw_validate_* never calls it);
+kw_debug_host_walk runs the sequential form of the slot walks (slots.hpp walk_*) on the host with
+the blob's column automata; the device computes the same first violations entity-parallel. It is
+a diagnostic of the slot compiler only (the product path is the GPU: kw_validate_* never calls it);
 the GPU parity tests (test_parity_gpu.py) check the kernel itself against the oracle.
 Covers: every family, monitor mode, allowedToMutate, groups with short-circuit causes, init errors,
 the namespace bypass, raw requests, both origins, policy lists with repeats and > 64 slots (several
@@ -13,7 +14,7 @@ import pytest
 
 import kwgpu as K
 import oracle as O
-from helpers import config, diff_verdicts
+from helpers import config, diff_verdicts, wide_docs
 
 NS = "kubewarden"
 CASES = [("parity", 0, 3000), ("c1_namespace", 1, 2000), ("c2_trusted", 2, 3000), ("c3_group", 3, 3000),
@@ -83,4 +84,14 @@ def test_edge_documents():
     raw = K.Batch.from_json(['{"request": {"user": "tonio", "namespace": "kubewarden"}}', '{"request": null}'], raw=True)
     got = raw.debug_host_walk(env, ids)
     want = oe.eval(raw.view(), ids)
+    assert np.array_equal(got, want), diff_verdicts(got, want, len(ids), ids)
+
+
+def test_wide_documents():
+    doc = config("c4_64")
+    env, oe = K.EvaluationEnvironment(doc), O.OracleEnv(doc)
+    ids = env.policy_ids()
+    b = K.Batch.from_json(wide_docs())
+    got = b.debug_host_walk(env, ids)
+    want = oe.eval(b.view(), ids)
     assert np.array_equal(got, want), diff_verdicts(got, want, len(ids), ids)
