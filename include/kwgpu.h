@@ -216,9 +216,10 @@ int kw_batch_to_device(kw_batch *b, int device);
 void kw_batch_destroy(kw_batch *b);
 
 /* Diagnostic (test infrastructure, never called by kw_validate_*): evaluate the batch's rows
- * against the policy list on the HOST through the same slot compiler and entity walks the device
- * kernel runs (slots.hpp), with the column automata of the blob. Lets the CPU test suite check the
- * slot compiler against the oracle without a GPU. out: [row][npol] verdict words. */
+ * against the policy list on the HOST through the same slot compiler the device uses and the
+ * sequential form of its first-violation walks (slots.hpp walk_*), with the column automata of the
+ * blob. Lets the CPU test suite check the slot compiler against the oracle without a GPU.
+ * out: [row][npol] verdict words. No reference counterpart (diagnostic only). */
 int kw_debug_host_walk(const kw_env *env, const kw_batch *b, const int32_t *policies, uint32_t npol,
                        int origin, uint32_t *out);
 
