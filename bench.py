@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--synth", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (rank 0)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-modes", action="store_true", help="skip the end-to-end / flatten timings")
     args = ap.parse_args()
 
     import torch
@@ -117,6 +118,7 @@ def main():
         cpu = None
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(policies, ids, args)
+        modes = None if args.no_host_modes else host_modes(env, ids, syn, device, args)
         result = {
             "metric": METRIC, "value": value, "unit": "requests/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
@@ -132,6 +134,7 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic(args),
                          "algorithmic_bytes_per_launch": nbytes},
             "cpu_baseline": cpu,
+            "timing_modes": modes,
             "verdicts_final_allowed_fraction": frac_allowed,
         }
         print(json.dumps(result), flush=True)
@@ -139,6 +142,53 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     return result
+
+
+def host_modes(env, ids, syn, device, args):
+    """SURVEY §8(d) timing modes 2 and 3 beside the HBM-resident `value` (mode 1): the end-to-end
+    batch rate (host SoA -> H2D -> kernel -> D2H of the verdicts; pageable host buffers, device
+    allocation included) and the host JSON -> SoA flatten rate (kw_batch_from_json, 1 and N
+    threads) on a sample of the same synthetic requests."""
+    import torch
+
+    import kwgpu as K
+    out = {}
+    best = None
+    for _ in range(2):
+        hb = syn.batch()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        hb.to_device(device)
+        hb.validate(env, ids)
+        hb.verdicts()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t
+        best = dt if best is None else min(best, dt)
+        hb.close()
+    out["end_to_end"] = {"value": syn.n / best, "unit": "requests/s", "rows": syn.n,
+                         "what": "host SoA -> H2D -> evaluate -> D2H verdicts, pageable buffers, allocation included"}
+    import ctypes as C
+    n = min(100_000, syn.n)
+    docs = [syn.json(i).encode() for i in range(n)]
+    nbytes = sum(len(d) for d in docs)
+    arr = (C.c_char_p * n)(*docs)  # the C ABI call alone is timed
+    lens = (C.c_size_t * n)(*[len(d) for d in docs])
+    L = K._native.lib()
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    fl = {}
+    for th in sorted({1, threads}):
+        os.environ["KW_FLATTEN_THREADS"] = str(th)
+        h, bad, err = C.c_void_p(), C.c_int64(-1), C.create_string_buffer(512)
+        t = time.perf_counter()
+        rc = L.kw_batch_from_json(arr, lens, n, K._native.KW_DOC_ADMISSION_REVIEW, C.byref(h), C.byref(bad), err,
+                                  len(err))
+        fl[str(th)] = n / (time.perf_counter() - t)
+        if rc == 0:
+            L.kw_batch_destroy(h)
+    os.environ.pop("KW_FLATTEN_THREADS", None)
+    out["flatten"] = {"unit": "requests/s", "by_threads": fl, "rows": n, "mean_doc_bytes": nbytes / n,
+                      "what": "kw_batch_from_json: AdmissionReview JSON -> SoA columns"}
+    return out
 
 
 def traffic(args):

@@ -43,6 +43,12 @@ struct StrCol {
     off.assign(1, 0);
     bytes.clear();
   }
+  void append(const StrCol& o) {  // o unpadded or padded: only its strings are copied
+    if (bytes.size() != off.back()) bytes.resize(off.back());
+    const uint32_t base = off.back();
+    bytes.insert(bytes.end(), o.bytes.begin(), o.bytes.begin() + o.off.back());
+    for (size_t i = 1; i < o.off.size(); ++i) off.push_back(base + o.off[i]);
+  }
 };
 
 struct DeviceBatch;  // engine.cpp
@@ -60,6 +66,7 @@ struct Batch {
   uint64_t labels() const { return lbl_key.n(); }
   void view(kw_soa* s) const;
   void finalize();  // pads every byte pool (device loads may read 16 B past a string)
+  void append(const Batch& o);  // o's rows after this batch's (multi-threaded flatten)
 };
 
 // Flattens one document (AdmissionReview or RawReview) and appends it as a row. On a

@@ -9,6 +9,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/kwgpu.h"
@@ -1173,12 +1174,41 @@ int kw_batch_from_json(const char* const* docs, const size_t* lens, size_t n, in
                        int64_t* bad_row, char* err, size_t errlen) {
   if (!out || (n && (!docs || !lens))) return KW_E_ARG;
   auto kb = std::make_unique<kw_batch>();
-  std::string e;
-  for (size_t i = 0; i < n; ++i) {
-    if (!flatten_document(docs[i], lens[i], doc_kind, &kb->b, &e)) {
-      if (bad_row) *bad_row = (int64_t)i;
-      put_err(err, errlen, e);
+  // contiguous document ranges flattened by up to KW_FLATTEN_THREADS threads (default: the
+  // hardware threads, at most 16), then concatenated in order; the first bad row wins
+  uint32_t nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  if (const char* t = getenv("KW_FLATTEN_THREADS")) nt = (uint32_t)std::max(1, atoi(t));
+  nt = (uint32_t)std::min<uint64_t>(nt, std::max<size_t>(1, n / 2048));
+  std::vector<Batch> part(nt);
+  std::vector<int64_t> bad(nt, -1);
+  std::vector<std::string> perr(nt);
+  auto work = [&](uint32_t t) {
+    const size_t i0 = n * t / nt, i1 = n * (t + 1) / nt;
+    for (size_t i = i0; i < i1; ++i)
+      if (!flatten_document(docs[i], lens[i], doc_kind, &part[t], &perr[t])) {
+        bad[t] = (int64_t)i;
+        return;
+      }
+  };
+  if (nt == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> th;
+    for (uint32_t t = 0; t < nt; ++t) th.emplace_back(work, t);
+    for (auto& x : th) x.join();
+  }
+  for (uint32_t t = 0; t < nt; ++t)
+    if (bad[t] >= 0) {
+      if (bad_row) *bad_row = bad[t];
+      put_err(err, errlen, perr[t]);
       return KW_E_PAYLOAD;
+    }
+  if (nt == 1) {
+    kb->b = std::move(part[0]);
+  } else {
+    for (uint32_t t = 0; t < nt; ++t) {
+      kb->b.append(part[t]);
+      part[t] = Batch();  // release as we go
     }
   }
   kb->b.finalize();

@@ -41,6 +41,24 @@ void Batch::view(kw_soa* s) const {
   s->lbl_val = lbl_val.view();
 }
 
+void Batch::append(const Batch& o) {
+  auto shift = [](std::vector<uint32_t>* dst, const std::vector<uint32_t>& src) {
+    const uint32_t base = dst->back();
+    for (size_t i = 1; i < src.size(); ++i) dst->push_back(base + src[i]);
+  };
+  n += o.n;
+  req_flags.insert(req_flags.end(), o.req_flags.begin(), o.req_flags.end());
+  shift(&ctr_off, o.ctr_off);
+  shift(&lbl_off, o.lbl_off);
+  ctr_flags.insert(ctr_flags.end(), o.ctr_flags.begin(), o.ctr_flags.end());
+  shift(&capadd_off, o.capadd_off);
+  shift(&capdrop_off, o.capdrop_off);
+  StrCol* mine[] = {&uid, &ns, &op, &kind, &ctr_name, &ctr_image, &ctr_aa, &cap_add, &cap_drop, &lbl_key, &lbl_val};
+  const StrCol* theirs[] = {&o.uid, &o.ns, &o.op, &o.kind, &o.ctr_name, &o.ctr_image, &o.ctr_aa,
+                            &o.cap_add, &o.cap_drop, &o.lbl_key, &o.lbl_val};
+  for (size_t k = 0; k < sizeof(mine) / sizeof(mine[0]); ++k) mine[k]->append(*theirs[k]);
+}
+
 void Batch::finalize() {
   for (StrCol* c : {&uid, &ns, &op, &kind, &ctr_name, &ctr_image, &ctr_aa, &cap_add, &cap_drop, &lbl_key, &lbl_val})
     c->pad();
