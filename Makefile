@@ -2,6 +2,7 @@
 # runs this; hipcc cross-compiles for gfx950 without a GPU.
 #   policy-server_amd/libkwgpu.so    product: HIP kernels + host engine + C ABI (include/kwgpu.h)
 #   policy-server_amd/libkwsynth.so  bench/test workload generator
+#   policy-server_amd/kwhost         HTTP front (/validate, /audit, /validate_raw) over libkwgpu.so
 #   oracle/build/libkworacle.so      CPU restatement (test infrastructure only)
 HIPCC ?= /opt/rocm/bin/hipcc
 CXX ?= g++
@@ -18,7 +19,7 @@ HOST_SRCS := json automaton expr env flatten service slotplan capi
 HOST_OBJS := $(addprefix $(OBJ)/,$(addsuffix .o,$(HOST_SRCS)))
 HEADERS := $(wildcard $(SRC)/*.hpp) include/kwgpu.h
 
-all: $(PKG)/libkwgpu.so $(PKG)/libkwsynth.so oracle/build/libkworacle.so
+all: $(PKG)/libkwgpu.so $(PKG)/libkwsynth.so $(PKG)/kwhost oracle/build/libkworacle.so
 
 $(OBJ)/%.o: $(SRC)/%.cpp $(HEADERS)
 	@mkdir -p $(OBJ)
@@ -30,6 +31,9 @@ $(OBJ)/kernels.o: $(SRC)/kernels.hip $(HEADERS)
 
 $(PKG)/libkwgpu.so: $(HOST_OBJS) $(OBJ)/kernels.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
+$(PKG)/kwhost: $(SRC)/kwhost.cpp include/kwgpu.h $(PKG)/libkwgpu.so
+	$(CXX) -O2 -std=c++17 -Wall -Wextra -o $@ $< -L$(PKG) -lkwgpu -Wl,-rpath,'$$ORIGIN' -lpthread
 
 $(PKG)/libkwsynth.so: $(SRC)/synth.cpp include/kwgpu.h
 	$(CXX) -O3 -std=c++17 -fPIC -shared -Wall -o $@ $<
@@ -43,6 +47,6 @@ resources: $(SRC)/kernels.hip
 	$(HIPCC) $(HIPFLAGS) -Rpass-analysis=kernel-resource-usage -c $< -o /dev/null
 
 clean:
-	rm -rf $(OBJ) $(PKG)/*.so oracle/build
+	rm -rf $(OBJ) $(PKG)/*.so $(PKG)/kwhost oracle/build
 
 .PHONY: all clean resources

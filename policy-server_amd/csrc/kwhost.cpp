@@ -1,0 +1,505 @@
+// kwhost — HTTP front of the admission engine: /validate, /audit and /validate_raw/{policy_id}
+// served from micro-batches on the GPU.
+//
+// Reference: the axum router (src/lib.rs:206-225), validate_handler / audit_handler /
+// validate_raw_handler (src/api/handlers.rs:69-174), the JsonExtractor rejection (handlers.rs:29-39,
+// api_error.rs:7-30), handle_evaluation_error (handlers.rs:321-342) and the per-request
+// semaphore + spawn_blocking (acquire_semaphore_and_evaluate, handlers.rs:256-286), which this
+// server replaces with a micro-batcher: connection threads park their request in a queue; one
+// batcher thread takes up to --max-batch requests (waiting at most --max-wait-us after the first),
+// flattens them with kw_batch_from_json, evaluates them with one kw_validate_rows call per
+// (document kind, origin) and hands each connection its formatted AdmissionReview.
+//
+// Status mapping (reference behaviour):
+//   body not JSON                        400  "Failed to parse the request body as JSON: ..."
+//   JSON not an AdmissionReview / Raw    422  "Failed to deserialize the JSON body into the target type: ..."
+//   Content-Type not application/json    415  "Expected request with `Content-Type: application/json`"
+//   /validate rejections are {"message", "status"} JSON (JsonExtractor); /audit and /validate_raw
+//   use axum's plain-text rejection body.
+//   unknown policy                       404  {"message":"unknown policy: <id>","status":404}
+//   any other evaluation error           500  {"message":"Something went wrong","status":500}
+//   GET /readiness                       200  (empty)
+//   unknown route                        404  (empty)
+//
+// Usage: kwhost --policies policies.json [--addr 127.0.0.1] [--port 3000] [--device 0]
+//   [--max-batch 512] [--max-wait-us 200] [--always-accept-admission-reviews-on-namespace NS]
+//   [--continue-on-errors] [--no-device]
+// --policies is the reference's policies.yml as JSON (configs/*.yml through any YAML -> JSON
+// converter). --no-device serves the HTTP layer without device tables: every evaluation then fails
+// with 500 (used by the CPU test suite for routing and error mapping; never a CPU fallback).
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <signal.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <fstream>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/kwgpu.h"
+
+namespace {
+
+struct Opts {
+  std::string policies, addr = "127.0.0.1", always_ns;
+  int port = 3000, device = 0, max_batch = 512, max_wait_us = 200;
+  bool continue_on_errors = false, no_device = false;
+};
+
+enum Route { R_VALIDATE, R_AUDIT, R_RAW };
+
+struct Reply {
+  int status = 500;
+  std::string body, ctype = "application/json";
+};
+
+// One parked request: filled by its connection thread, answered by the batcher.
+struct Job {
+  Route route;
+  std::string policy, body;
+  Reply reply;
+  bool done = false;
+  std::mutex m;
+  std::condition_variable cv;
+  void finish(Reply r) {
+    std::lock_guard<std::mutex> g(m);
+    reply = std::move(r);
+    done = true;
+    cv.notify_one();
+  }
+};
+
+std::string json_escape(const std::string& s) {
+  std::string o;
+  o.reserve(s.size() + 8);
+  for (unsigned char c : s) {
+    switch (c) {
+      case '"': o += "\\\""; break;
+      case '\\': o += "\\\\"; break;
+      case '\n': o += "\\n"; break;
+      case '\r': o += "\\r"; break;
+      case '\t': o += "\\t"; break;
+      default:
+        if (c < 0x20) {
+          char b[8];
+          snprintf(b, sizeof(b), "\\u%04x", c);
+          o += b;
+        } else {
+          o += (char)c;
+        }
+    }
+  }
+  return o;
+}
+
+Reply api_error(int status, const std::string& msg) {  // ApiError::into_response (api_error.rs:22-30)
+  Reply r;
+  r.status = status;
+  r.body = "{\"message\":\"" + json_escape(msg) + "\",\"status\":" + std::to_string(status) + "}";
+  return r;
+}
+
+// Extractor rejection: JsonExtractor (validate) answers ApiError JSON, axum::Json (audit, raw) the
+// rejection's plain body text.
+Reply rejection(Route route, int status, const std::string& msg) {
+  if (route == R_VALIDATE) return api_error(status, msg);
+  Reply r;
+  r.status = status;
+  r.body = msg;
+  r.ctype = "text/plain; charset=utf-8";
+  return r;
+}
+
+Reply evaluation_error(int code, const std::string& msg) {  // handle_evaluation_error (handlers.rs:321-342)
+  if (code == KW_E_NOT_FOUND) return api_error(404, msg);
+  return api_error(500, "Something went wrong");
+}
+
+class Server {
+ public:
+  Server(const Opts& o, kw_env* env) : o_(o), env_(env) {}
+
+  void submit(Job* j) {
+    {
+      std::lock_guard<std::mutex> g(qm_);
+      q_.push_back(j);
+    }
+    qcv_.notify_one();
+  }
+
+  // The batcher: take up to max_batch jobs (waiting max_wait_us after the first), run them.
+  void batcher() {
+    std::vector<Job*> jobs;
+    for (;;) {
+      jobs.clear();
+      {
+        std::unique_lock<std::mutex> lk(qm_);
+        qcv_.wait(lk, [&] { return !q_.empty(); });
+        const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(o_.max_wait_us);
+        qcv_.wait_until(lk, deadline, [&] { return (int)q_.size() >= o_.max_batch; });
+        while (!q_.empty() && (int)jobs.size() < o_.max_batch) {
+          jobs.push_back(q_.front());
+          q_.pop_front();
+        }
+      }
+      // partition first: a job belongs to its connection thread again once it is answered
+      std::vector<Job*> part[3];
+      for (Job* j : jobs) part[j->route].push_back(j);
+      for (Route r : {R_VALIDATE, R_AUDIT, R_RAW})
+        if (!part[r].empty()) run(r, part[r]);
+    }
+  }
+
+ private:
+  // One kw_validate_rows pass over the jobs of one route. A group's members run as extra rows of
+  // the same document (their verdicts give the causes of a rejected group).
+  void run(Route route, std::vector<Job*> jobs) {
+    const int kind = route == R_RAW ? KW_DOC_RAW_REVIEW : KW_DOC_ADMISSION_REVIEW;
+    const int origin = route == R_AUDIT ? KW_ORIGIN_AUDIT : KW_ORIGIN_VALIDATE;
+    // 1. the extractor: bodies that are not a request of this route's type are answered first
+    //    (the handler's extractor runs before the policy lookup)
+    kw_batch* b = nullptr;
+    char err[1024] = {0};
+    for (;;) {
+      if (jobs.empty()) return;
+      std::vector<const char*> docs;
+      std::vector<size_t> lens;
+      for (Job* j : jobs) {
+        docs.push_back(j->body.data());
+        lens.push_back(j->body.size());
+      }
+      int64_t bad = -1;
+      const int rc = kw_batch_from_json(docs.data(), lens.data(), docs.size(), kind, &b, &bad, err, sizeof(err));
+      if (rc == KW_OK) break;
+      if (rc != KW_E_PAYLOAD || bad < 0 || bad >= (int64_t)jobs.size()) {
+        for (Job* j : jobs) j->finish(evaluation_error(rc, err));
+        return;
+      }
+      const std::string msg(err);
+      const int status = msg.rfind("Failed to parse", 0) == 0 ? 400 : 422;  // JsonSyntaxError vs JsonDataError
+      jobs[(size_t)bad]->finish(rejection(route, status, msg));
+      jobs.erase(jobs.begin() + bad);
+    }
+    // 2. policy lookup (service.rs:37 PolicyID parse, PolicyNotFound -> 404)
+    struct Row {
+      Job* job;
+      int32_t policy;
+      uint32_t first, nmem;
+    };
+    std::vector<Row> rows;
+    std::vector<const char*> docs;
+    std::vector<size_t> lens;
+    std::vector<int32_t> row_policy;
+    bool regroup = false;  // some job failed its lookup or is a group: the batch is rebuilt from `docs`
+    for (Job* j : jobs) {
+      int32_t idx = -1;
+      const int rc = kw_env_lookup(env_, j->policy.data(), j->policy.size(), &idx);
+      if (rc != KW_OK) {
+        j->finish(evaluation_error(rc, rc == KW_E_NOT_FOUND ? "unknown policy: " + j->policy : ""));
+        regroup = true;
+        continue;
+      }
+      int32_t mem[64];
+      const int nm = kw_env_is_group(env_, idx) ? kw_env_group_members(env_, idx, mem, 64) : 0;
+      regroup = regroup || nm > 0;
+      rows.push_back({j, idx, (uint32_t)row_policy.size(), (uint32_t)(nm > 0 ? nm : 0)});
+      docs.push_back(j->body.data());
+      lens.push_back(j->body.size());
+      row_policy.push_back(idx);
+      for (int k = 0; k < nm; ++k) {  // a group's members run as extra rows of the same document
+        docs.push_back(j->body.data());
+        lens.push_back(j->body.size());
+        row_policy.push_back(mem[k]);
+      }
+    }
+    int rc = KW_OK;
+    if (regroup) {
+      kw_batch_destroy(b);
+      b = nullptr;
+      if (rows.empty()) return;
+      int64_t bad = -1;
+      rc = kw_batch_from_json(docs.data(), lens.data(), docs.size(), kind, &b, &bad, err, sizeof(err));
+    }
+    // 3. upload, evaluate, read back
+    if (rc == KW_OK && o_.no_device) rc = KW_E_DEVICE;
+    if (rc == KW_OK) rc = kw_batch_to_device(b, o_.device);
+    if (rc == KW_OK) rc = kw_validate_rows(env_, b, row_policy.data(), origin, nullptr);
+    std::vector<uint32_t> v(row_policy.size());
+    if (rc == KW_OK) rc = kw_batch_verdicts(b, v.data(), v.size());
+    if (rc != KW_OK) {
+      for (Row& r : rows) r.job->finish(evaluation_error(rc, err));
+      if (b) kw_batch_destroy(b);
+      return;
+    }
+    // 4. service epilogue + response envelope (AdmissionReviewResponse / RawReviewResponse)
+    std::vector<char> buf(4096);
+    for (Row& r : rows) {
+      size_t need = 0;
+      const uint32_t* mv = r.nmem ? v.data() + r.first + 1 : nullptr;
+      int frc = kw_format_response(env_, b, r.first, r.policy, v[r.first], mv, buf.data(), buf.size(), &need);
+      if (frc == KW_E_NOSPACE) {
+        buf.resize(need + 1);
+        frc = kw_format_response(env_, b, r.first, r.policy, v[r.first], mv, buf.data(), buf.size(), &need);
+      }
+      if (frc != KW_OK) {
+        r.job->finish(evaluation_error(frc, buf.data()));
+        continue;
+      }
+      Reply rep;
+      rep.status = 200;
+      const std::string resp(buf.data(), strnlen(buf.data(), buf.size()));  // need counts the NUL
+      rep.body = route == R_RAW ? "{\"response\":" + resp + "}"
+                                : "{\"kind\":\"AdmissionReview\",\"apiVersion\":\"admission.k8s.io/v1\",\"response\":" + resp + "}";
+      r.job->finish(std::move(rep));
+    }
+    kw_batch_destroy(b);
+  }
+
+  const Opts& o_;
+  kw_env* env_;
+  std::mutex qm_;
+  std::condition_variable qcv_;
+  std::deque<Job*> q_;
+};
+
+// ---- HTTP/1.1 (Content-Length and chunked bodies, keep-alive)
+struct Conn {
+  int fd;
+  std::string in;
+  bool read_more() {
+    char b[65536];
+    const ssize_t n = recv(fd, b, sizeof(b), 0);
+    if (n <= 0) return false;
+    in.append(b, (size_t)n);
+    return true;
+  }
+  bool send_all(const std::string& s) {
+    size_t o = 0;
+    while (o < s.size()) {
+      const ssize_t n = send(fd, s.data() + o, s.size() - o, MSG_NOSIGNAL);
+      if (n <= 0) return false;
+      o += (size_t)n;
+    }
+    return true;
+  }
+};
+
+std::string lower(std::string s) {
+  for (char& c : s) c = (char)tolower((unsigned char)c);
+  return s;
+}
+
+std::string trim(const std::string& s) {
+  size_t a = s.find_first_not_of(" \t"), e = s.find_last_not_of(" \t\r");
+  return a == std::string::npos ? std::string() : s.substr(a, e - a + 1);
+}
+
+bool percent_decode(const std::string& s, std::string* out) {  // axum Path extractor
+  out->clear();
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] == '%') {
+      if (i + 2 >= s.size() || !isxdigit((unsigned char)s[i + 1]) || !isxdigit((unsigned char)s[i + 2])) return false;
+      *out += (char)strtol(s.substr(i + 1, 2).c_str(), nullptr, 16);
+      i += 2;
+    } else {
+      *out += s[i];
+    }
+  }
+  return true;
+}
+
+const char* reason(int s) {
+  switch (s) {
+    case 200: return "OK";
+    case 400: return "Bad Request";
+    case 404: return "Not Found";
+    case 405: return "Method Not Allowed";
+    case 411: return "Length Required";
+    case 413: return "Payload Too Large";
+    case 415: return "Unsupported Media Type";
+    case 422: return "Unprocessable Entity";
+    default: return "Internal Server Error";
+  }
+}
+
+void serve(Server* srv, int fd) {
+  Conn c{fd, {}};
+  for (;;) {
+    size_t he;
+    while ((he = c.in.find("\r\n\r\n")) == std::string::npos) {
+      if (c.in.size() > (1u << 20) || !c.read_more()) {
+        close(fd);
+        return;
+      }
+    }
+    std::istringstream hs(c.in.substr(0, he));
+    std::string line, method, target, version;
+    std::getline(hs, line);
+    std::istringstream rl(line);
+    rl >> method >> target >> version;
+    std::string ctype;
+    long long clen = -1;
+    bool chunked = false, keep = version != "HTTP/1.0";
+    while (std::getline(hs, line)) {
+      const size_t colon = line.find(':');
+      if (colon == std::string::npos) continue;
+      const std::string k = lower(trim(line.substr(0, colon))), v = trim(line.substr(colon + 1));
+      if (k == "content-length") clen = atoll(v.c_str());
+      else if (k == "content-type") ctype = lower(v);
+      else if (k == "transfer-encoding") chunked = lower(v).find("chunked") != std::string::npos;
+      else if (k == "connection") keep = lower(v) != "close" && (keep || lower(v) == "keep-alive");
+    }
+    c.in.erase(0, he + 4);
+    std::string body;
+    if (chunked) {
+      for (;;) {
+        size_t le;
+        while ((le = c.in.find("\r\n")) == std::string::npos)
+          if (!c.read_more()) return (void)close(fd);
+        const size_t n = strtoul(c.in.substr(0, le).c_str(), nullptr, 16);
+        while (c.in.size() < le + 2 + n + 2)
+          if (!c.read_more()) return (void)close(fd);
+        body.append(c.in, le + 2, n);
+        c.in.erase(0, le + 2 + n + 2);
+        if (n == 0) break;
+      }
+    } else if (clen > 0) {
+      if (clen > (1ll << 30)) return (void)close(fd);
+      while ((long long)c.in.size() < clen)
+        if (!c.read_more()) return (void)close(fd);
+      body = c.in.substr(0, (size_t)clen);
+      c.in.erase(0, (size_t)clen);
+    }
+    // routing (src/lib.rs:206-225)
+    Reply rep;
+    const std::string path = target.substr(0, target.find('?'));
+    Route route = R_VALIDATE;
+    std::string rest;
+    bool known = true;
+    if (path.rfind("/validate/", 0) == 0) {
+      route = R_VALIDATE;
+      rest = path.substr(10);
+    } else if (path.rfind("/audit/", 0) == 0) {
+      route = R_AUDIT;
+      rest = path.substr(7);
+    } else if (path.rfind("/validate_raw/", 0) == 0) {
+      route = R_RAW;
+      rest = path.substr(14);
+    } else {
+      known = false;
+    }
+    std::string policy;
+    if (path == "/readiness") {
+      rep.status = method == "GET" ? 200 : 405;
+      rep.ctype.clear();
+    } else if (!known || rest.empty() || rest.find('/') != std::string::npos || !percent_decode(rest, &policy)) {
+      rep.status = 404;
+      rep.ctype.clear();
+    } else if (method != "POST") {
+      rep.status = 405;
+      rep.ctype.clear();
+    } else if (!(ctype.rfind("application/json", 0) == 0 ||
+                 (ctype.rfind("application/", 0) == 0 && ctype.find("+json") != std::string::npos))) {
+      rep = rejection(route, 415, "Expected request with `Content-Type: application/json`");
+    } else {
+      Job j;
+      j.route = route;
+      j.policy = std::move(policy);
+      j.body = std::move(body);
+      srv->submit(&j);
+      std::unique_lock<std::mutex> lk(j.m);
+      j.cv.wait(lk, [&] { return j.done; });
+      rep = std::move(j.reply);
+    }
+    std::string out = "HTTP/1.1 " + std::to_string(rep.status) + " " + reason(rep.status) + "\r\n";
+    if (!rep.ctype.empty()) out += "content-type: " + rep.ctype + "\r\n";
+    out += "content-length: " + std::to_string(rep.body.size()) + "\r\n";
+    if (!keep) out += "connection: close\r\n";
+    out += "\r\n" + rep.body;
+    if (!c.send_all(out) || !keep) {
+      close(fd);
+      return;
+    }
+  }
+}
+
+int usage() {
+  fprintf(stderr,
+          "usage: kwhost --policies FILE.json [--addr A] [--port P] [--device D] [--max-batch N]\n"
+          "              [--max-wait-us T] [--always-accept-admission-reviews-on-namespace NS]\n"
+          "              [--continue-on-errors] [--no-device]\n");
+  return 2;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Opts o;
+  for (int i = 1; i < argc; ++i) {
+    const std::string a = argv[i];
+    auto val = [&]() -> const char* { return i + 1 < argc ? argv[++i] : nullptr; };
+    const char* v = nullptr;
+    if (a == "--policies" && (v = val())) o.policies = v;
+    else if (a == "--addr" && (v = val())) o.addr = v;
+    else if (a == "--port" && (v = val())) o.port = atoi(v);
+    else if (a == "--device" && (v = val())) o.device = atoi(v);
+    else if (a == "--max-batch" && (v = val())) o.max_batch = std::max(1, atoi(v));
+    else if (a == "--max-wait-us" && (v = val())) o.max_wait_us = std::max(0, atoi(v));
+    else if (a == "--always-accept-admission-reviews-on-namespace" && (v = val())) o.always_ns = v;
+    else if (a == "--continue-on-errors") o.continue_on_errors = true;
+    else if (a == "--no-device") o.no_device = true;
+    else return usage();
+  }
+  if (o.policies.empty()) return usage();
+  std::ifstream f(o.policies, std::ios::binary);
+  if (!f) {
+    fprintf(stderr, "kwhost: cannot read %s\n", o.policies.c_str());
+    return 1;
+  }
+  const std::string doc((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  kw_env_options eo;
+  memset(&eo, 0, sizeof(eo));
+  eo.continue_on_errors = o.continue_on_errors ? 1 : 0;
+  eo.always_accept_namespace = o.always_ns.empty() ? nullptr : o.always_ns.c_str();
+  eo.device = o.no_device ? -1 : o.device;
+  kw_env* env = nullptr;
+  char err[2048] = {0};
+  if (int rc = kw_env_build(doc.data(), doc.size(), &eo, &env, err, sizeof(err))) {
+    fprintf(stderr, "kwhost: %s (code %d)\n", err, rc);
+    return 1;
+  }
+  const int ls = socket(AF_INET, SOCK_STREAM, 0);
+  int one = 1;
+  setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  sockaddr_in sa;
+  memset(&sa, 0, sizeof(sa));
+  sa.sin_family = AF_INET;
+  sa.sin_port = htons((uint16_t)o.port);
+  if (inet_pton(AF_INET, o.addr.c_str(), &sa.sin_addr) != 1 || bind(ls, (sockaddr*)&sa, sizeof(sa)) != 0 ||
+      listen(ls, 1024) != 0) {
+    fprintf(stderr, "kwhost: cannot listen on %s:%d: %s\n", o.addr.c_str(), o.port, strerror(errno));
+    return 1;
+  }
+  signal(SIGPIPE, SIG_IGN);
+  Server srv(o, env);
+  std::thread(&Server::batcher, &srv).detach();
+  fprintf(stderr, "kwhost: %d policies, listening on %s:%d\n", kw_env_policy_count(env), o.addr.c_str(), o.port);
+  for (;;) {
+    const int fd = accept(ls, nullptr, nullptr);
+    if (fd < 0) continue;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+    std::thread(serve, &srv, fd).detach();
+  }
+}

@@ -1,0 +1,80 @@
+"""GPU: the kwhost HTTP front end to end. Concurrent /validate, /audit and /validate_raw calls
+(the micro-batcher groups them into kw_validate_rows passes) answer exactly the oracle's
+AdmissionResponse inside the reference envelope (AdmissionReviewResponse, admission_review.rs:28-35;
+RawReviewResponse, raw_review.rs), or the reference's 404 where the service layer raises
+PolicyNotFound (handlers.rs:321-342)."""
+import json
+from concurrent.futures import ThreadPoolExecutor
+from urllib.parse import quote
+
+import numpy as np
+import pytest
+
+import kwgpu as K
+import oracle as O
+from helpers import config, reference_doc
+from kwhost_util import Host
+
+pytestmark = pytest.mark.gpu
+NS = "kubewarden"
+
+
+def _expect(oe, soa, v, ids, r, j, raw):
+    members = oe.pol[j]["members"] if oe.pol[j]["group"] else []
+    mv = [int(v[r, m]) for m in members] if members else None
+    if int(v[r, j]) & K._native.KW_F_PATCH:  # mutation accepted: patch generation is not served yet
+        return 500, {"message": "Something went wrong", "status": 500}
+    try:
+        resp = oe.response(soa, r, j, int(v[r, j]), mv)
+    except KeyError as e:
+        return 404, {"message": str(e).strip("'\""), "status": 404}
+    if raw:
+        return 200, {"response": resp}
+    return 200, {"kind": "AdmissionReview", "apiVersion": "admission.k8s.io/v1", "response": resp}
+
+
+@pytest.mark.parametrize("name,scfg", [("parity", 0), ("c4_64", 4)])
+def test_concurrent_routes_match_oracle(name, scfg):
+    doc = config(name)
+    oe = O.OracleEnv(doc, continue_on_errors=True, always_accept_namespace=NS)
+    ids = [p["id"] for p in oe.pol]
+    n = 240
+    syn = K.SynthBatch(scfg, n, seed=31337 + scfg)
+    docs = [syn.json(r) for r in range(n)]
+    soa = syn.soa()
+    raw_b = K.Batch.from_json(docs, raw=True)
+    raw_soa = raw_b.view()
+    v_val = oe.eval(soa, ids, K.VALIDATE).reshape(n, len(ids))
+    v_aud = oe.eval(soa, ids, K.AUDIT).reshape(n, len(ids))
+    v_raw = oe.eval(raw_soa, ids, K.VALIDATE).reshape(n, len(ids))
+    calls = []
+    for r in range(n):
+        j = (r * 7) % len(ids)
+        calls.append(("validate", r, j, _expect(oe, soa, v_val, ids, r, j, False)))
+        calls.append(("audit", r, j, _expect(oe, soa, v_aud, ids, r, j, False)))
+        calls.append(("validate_raw", r, j, _expect(oe, raw_soa, v_raw, ids, r, j, True)))
+    with Host(name, extra=["--device", "0", "--max-wait-us", "300"]) as h:
+        def one(c):
+            route, r, j, want = c
+            # member ids ("group/member") travel percent-encoded, as axum's Path extractor decodes them
+            st, _, body = h.request("POST", f"/{route}/{quote(ids[j], safe='')}", docs[r])
+            return c, st, json.loads(body) if body else None
+        with ThreadPoolExecutor(max_workers=24) as ex:
+            results = list(ex.map(one, calls))
+    bad = [(c[0], c[1], ids[c[2]], st, got, c[3]) for c, st, got in results if (st, got) != c[3]]
+    assert not bad, bad[:3]
+    assert sum(1 for c in calls if c[3][0] == 200) > len(calls) // 2
+
+
+def test_reference_fixture_privileged_pod():
+    """integration_test.rs:58-68: pod-privileged rejects tests/data/pod_with_privileged_containers.json
+    with "Privileged container is not allowed" and no code; the unprivileged pod is accepted."""
+    with Host("parity", extra=["--device", "0"]) as h:
+        st, _, body = h.request("POST", "/validate/pod-privileged", reference_doc("pod_with_privileged_containers.json"))
+        assert st == 200
+        resp = json.loads(body)["response"]
+        assert resp["allowed"] is False
+        assert resp["status"] == {"message": "Privileged container is not allowed"}
+        st, _, body = h.request("POST", "/validate/pod-privileged",
+                                reference_doc("pod_without_privileged_containers.json"))
+        assert st == 200 and json.loads(body)["response"]["allowed"] is True
