@@ -257,6 +257,14 @@ int kw_validate_timed(const kw_env *env, kw_batch *b, const int32_t *policies, u
 int kw_format_response(const kw_env *env, const kw_batch *b, uint64_t row, int32_t policy,
                        uint32_t verdict, const uint32_t *member_verdicts, char *buf, size_t cap,
                        size_t *need);
+/* The same with the row's original document (doc_kind KW_DOC_*), which an accepted mutation
+ * (KW_F_PATCH) needs: the response then carries patchType "JSONPatch" and the base64 RFC 6902
+ * patch that adds the psp-capabilities policy's missing required drops / default adds to every
+ * container (the mutated_object of the guest, returned as a patch by policy-evaluator [upstream];
+ * DESIGN.md §2). kw_format_response answers KW_E_ARG for such a verdict. */
+int kw_format_response_doc(const kw_env *env, const kw_batch *b, uint64_t row, int32_t policy,
+                           uint32_t verdict, const uint32_t *member_verdicts, const char *doc,
+                           size_t doc_len, int doc_kind, char *buf, size_t cap, size_t *need);
 /* Group member policy indices (settings order) of a group; returns the count. */
 int kw_env_group_members(const kw_env *env, int32_t group, int32_t *out, int cap);
 

@@ -15,8 +15,11 @@ Restates, independently of the product's C++ (env.cpp / expr.cpp / service.cpp):
   * policy-family settings rules and message templates: DESIGN.md §Policy families — parity
     UNPINNED for the families (their Wasm source is not in /root/reference), except the
     pod-privileged message pinned by integration_test.rs:58-68.
+  * the psp-capabilities mutation as an RFC 6902 patch — parity UNPINNED (the
+    guest's mutated_object and policy-evaluator's diff are upstream, absent here).
 The per-request family arithmetic runs in oracle/kworacle.c (libc fnmatch + POSIX regex).
 """
+import base64
 import ctypes as C
 import json
 import os
@@ -35,6 +38,91 @@ X_CONST, X_CALL, X_NOT, X_AND, X_OR, X_EQ, X_NE = 0, 1, 2, 3, 4, 5, 6
 R_PRIVILEGED, R_NAMESPACE, R_REG_NOT_ALLOWED, R_REG_REJECTED, R_TAG_REJECTED = 1, 2, 3, 4, 5
 R_IMG_NOT_ALLOWED, R_IMG_REJECTED, R_CAP, R_APPARMOR = 6, 7, 8, 9
 R_LABEL_DENIED, R_LABEL_CONSTRAINT, R_LABEL_MANDATORY, R_GROUP, R_GROUP_EXPR, R_INIT = 10, 11, 12, 13, 14, 15
+
+
+# ----------------------------------------------------------------------------- mutation patch
+_WORKLOADS = ("Deployment", "ReplicaSet", "StatefulSet", "DaemonSet", "Job", "ReplicationController")
+
+
+def podspec(doc_obj):
+    """(PodSpec dict, JSON Pointer) of request.object, or (None, None): Pod /spec, workload templates
+    /spec/template/spec, CronJob /spec/jobTemplate/spec/template/spec (object kind, else
+    request.kind.kind)."""
+    req = doc_obj.get("request") if isinstance(doc_obj, dict) else None
+    obj = req.get("object") if isinstance(req, dict) else None
+    if not isinstance(obj, dict):
+        return None, None
+    rk = req.get("kind", {}).get("kind") if isinstance(req.get("kind"), dict) else None
+    kind = obj["kind"] if isinstance(obj.get("kind"), str) else (rk if isinstance(rk, str) else "")
+
+    def walk(o, keys):
+        for k in keys:
+            if not isinstance(o, dict):
+                return None
+            o = o.get(k)
+        return o
+    if kind == "Pod":
+        spec, ptr = obj.get("spec"), "/spec"
+    elif kind in _WORKLOADS:
+        spec, ptr = walk(obj, ["spec", "template", "spec"]), "/spec/template/spec"
+    elif kind == "CronJob":
+        spec, ptr = walk(obj, ["spec", "jobTemplate", "spec", "template", "spec"]), "/spec/jobTemplate/spec/template/spec"
+    else:
+        return None, None
+    return (spec, ptr) if isinstance(spec, dict) else (None, None)
+
+
+def capabilities_patch(required_drops, default_adds, doc):
+    """RFC 6902 ops of the psp-capabilities mutation: per container of containers,
+    initContainers, ephemeralContainers (JSON array index), the required drops it does not drop
+    (none when it drops ALL) and the default adds it neither adds nor drops, settings order; added
+    as a new securityContext / capabilities object / list where absent, else appended ("-")."""
+    def uniq(xs):
+        out = []
+        for x in xs:
+            if x not in out:
+                out.append(x)
+        return out
+    reqd, defa = uniq(required_drops), uniq(default_adds)
+    spec, ptr = podspec(json.loads(doc))
+    ops = []
+    if spec is None:
+        return ops
+    for ln in ("containers", "initContainers", "ephemeralContainers"):
+        arr = spec.get(ln)
+        if not isinstance(arr, list):
+            continue
+        for k, c in enumerate(arr):
+            if not isinstance(c, dict):
+                continue
+            sc = c.get("securityContext")
+            caps = sc.get("capabilities") if isinstance(sc, dict) else None
+            add = caps.get("add") if isinstance(caps, dict) else None
+            drop = caps.get("drop") if isinstance(caps, dict) else None
+            has = lambda lst, x: isinstance(lst, list) and any(isinstance(e, str) and e == x for e in lst)
+            mdrop = [] if has(drop, "ALL") else [x for x in reqd if not has(drop, x)]
+            madd = [x for x in defa if not has(add, x) and not has(drop, x)]
+            if not mdrop and not madd:
+                continue
+            base = f"{ptr}/{ln}/{k}/securityContext"
+            capobj = {}
+            if madd:
+                capobj["add"] = madd
+            if mdrop:
+                capobj["drop"] = mdrop
+            if not isinstance(sc, dict):
+                ops.append({"op": "add", "path": base, "value": {"capabilities": capobj}})
+            elif not isinstance(caps, dict):
+                ops.append({"op": "add", "path": base + "/capabilities", "value": capobj})
+            else:
+                for name, lst, cur in (("add", madd, add), ("drop", mdrop, drop)):
+                    if not lst:
+                        continue
+                    if not isinstance(cur, list):
+                        ops.append({"op": "add", "path": f"{base}/capabilities/{name}", "value": lst})
+                    else:
+                        ops.extend({"op": "add", "path": f"{base}/capabilities/{name}/-", "value": x} for x in lst)
+    return ops
 
 
 # ----------------------------------------------------------------------------- PolicyID
@@ -739,8 +827,9 @@ class OracleEnv:
             return P["init_error"]
         return ""
 
-    def response(self, soa, row, pidx, v, member_v=None):
-        """AdmissionResponse dict the service returns for verdict word v (service.rs:30-152)."""
+    def response(self, soa, row, pidx, v, member_v=None, doc=None):
+        """AdmissionResponse dict the service returns for verdict word v (service.rs:30-152).
+        doc: the row's original JSON text, needed for an accepted mutation (the patch)."""
         P = self.pol[pidx]
         c = soa.uid
         uid = bytes(c.bytes[c.off[row]:c.off[row + 1]]).decode()
@@ -750,6 +839,12 @@ class OracleEnv:
             return {"uid": uid, "allowed": True}
         if P["group"] and P["broken"]:
             raise KeyError(f"unknown policy: {P['broken']}")
+        if v & 0x40:  # F_PATCH: accepted mutation, the response carries the JSONPatch
+            if doc is None:
+                raise ValueError("the original document is required to restate a mutation")
+            ops = capabilities_patch(P["lists"][1], P["lists"][2], doc)
+            patch = base64.b64encode(json.dumps(ops, separators=(",", ":"), ensure_ascii=False).encode()).decode()
+            return {"uid": uid, "allowed": True, "patchType": "JSONPatch", "patch": patch}
         fst = (v >> 3) & 3
         reason, arg = (v >> 8) & 0xFF, v >> 16
         resp = {"uid": uid, "allowed": bool(v & 4)}

@@ -69,6 +69,17 @@ struct Batch {
   void append(const Batch& o);  // o's rows after this batch's (multi-threaded flatten)
 };
 
+class JDoc;
+// The PodSpec of a request's object (Pod: /spec; Deployment, ReplicaSet, StatefulSet, DaemonSet, Job,
+// ReplicationController: /spec/template/spec; CronJob: /spec/jobTemplate/spec/template/spec), its
+// template metadata and that JSON Pointer (relative to the object). spec = -1: none.
+struct PodSpecRef {
+  bool has_obj = false;
+  int64_t spec = -1, meta = -1;
+  const char* pointer = "";
+};
+PodSpecRef find_podspec(const JDoc& d, int64_t req);
+
 // Flattens one document (AdmissionReview or RawReview) and appends it as a row. On a
 // deserialization error returns false with the 422 rejection text.
 bool flatten_document(const char* doc, size_t len, int doc_kind, Batch* b, std::string* err);

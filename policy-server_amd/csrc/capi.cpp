@@ -1362,6 +1362,20 @@ int kw_format_response(const kw_env* env, const kw_batch* b, uint64_t row, int32
   return put_out(out, buf, cap, need);
 }
 
+int kw_format_response_doc(const kw_env* env, const kw_batch* b, uint64_t row, int32_t policy, uint32_t verdict,
+                           const uint32_t* member_verdicts, const char* doc, size_t doc_len, int doc_kind, char* buf,
+                           size_t cap, size_t* need) {
+  if (!env || !b || row >= b->b.n || policy < 0 || (size_t)policy >= env->e.pol.size() || (!doc && doc_len))
+    return KW_E_ARG;
+  std::string out;
+  Status st = format_response(env->e, b->b, row, policy, verdict, member_verdicts, &out, doc, doc_len, doc_kind);
+  if (!st.ok()) {
+    put_out(st.message, buf, cap, need);
+    return st.code;
+  }
+  return put_out(out, buf, cap, need);
+}
+
 int kw_evaluate(const kw_env* env, const char* policy_id, const char* doc, size_t doc_len, int doc_kind, int origin,
                 char* buf, size_t cap, size_t* need) {
   if (!env || !policy_id || !doc) return KW_E_ARG;
@@ -1392,7 +1406,7 @@ int kw_evaluate(const kw_env* env, const char* policy_id, const char* doc, size_
   std::vector<uint32_t> v(pols.size());
   if ((rc = kw_batch_verdicts(kb, v.data(), v.size()))) return rc;
   std::string out;
-  st = format_response(E, kb->b, 0, idx, v[0], v.size() > 1 ? v.data() + 1 : nullptr, &out);
+  st = format_response(E, kb->b, 0, idx, v[0], v.size() > 1 ? v.data() + 1 : nullptr, &out, doc, doc_len, doc_kind);
   if (!st.ok()) {
     put_out(st.message, buf, cap, need);
     return st.code;

@@ -128,6 +128,36 @@ void push_caps(const JDoc& d, int64_t arr, StrCol* col, std::vector<uint32_t>* o
   off->push_back((uint32_t)col->n());
 }
 
+}  // namespace
+
+PodSpecRef find_podspec(const JDoc& d, int64_t req) {
+  PodSpecRef r;
+  const bool req_obj = req >= 0 && d.is((uint32_t)req, JType::Obj);
+  const int64_t obj = req_obj ? d.get((uint32_t)req, "object") : -1;
+  if (obj < 0 || !d.is((uint32_t)obj, JType::Obj)) return r;
+  r.has_obj = true;
+  const std::string_view rkind = sv(d, path(d, req, {"kind", "kind"}));
+  const std::string_view k = is_str(d, d.get((uint32_t)obj, "kind")) ? d.str((uint32_t)d.get((uint32_t)obj, "kind")) : rkind;
+  if (k == "Pod") {
+    r.spec = d.get((uint32_t)obj, "spec");
+    r.meta = d.get((uint32_t)obj, "metadata");
+    r.pointer = "/spec";
+  } else if (k == "Deployment" || k == "ReplicaSet" || k == "StatefulSet" || k == "DaemonSet" || k == "Job" ||
+             k == "ReplicationController") {
+    r.spec = path(d, obj, {"spec", "template", "spec"});
+    r.meta = path(d, obj, {"spec", "template", "metadata"});
+    r.pointer = "/spec/template/spec";
+  } else if (k == "CronJob") {
+    r.spec = path(d, obj, {"spec", "jobTemplate", "spec", "template", "spec"});
+    r.meta = path(d, obj, {"spec", "jobTemplate", "spec", "template", "metadata"});
+    r.pointer = "/spec/jobTemplate/spec/template/spec";
+  }
+  if (r.spec >= 0 && !d.is((uint32_t)r.spec, JType::Obj)) r.spec = -1;
+  return r;
+}
+
+namespace {
+
 void flatten_request(const JDoc& d, int64_t req, bool raw, Batch* b) {
   uint8_t rf = raw ? KW_REQ_RAW : 0;
   bool req_obj = req >= 0 && d.is((uint32_t)req, JType::Obj);
@@ -140,25 +170,9 @@ void flatten_request(const JDoc& d, int64_t req, bool raw, Batch* b) {
   std::string_view rkind = sv(d, req_obj ? path(d, req, {"kind", "kind"}) : -1);
   b->kind.push(rkind);
 
-  int64_t obj = req_obj ? d.get((uint32_t)req, "object") : -1;
-  bool has_obj = obj >= 0 && d.is((uint32_t)obj, JType::Obj);
-  int64_t spec = -1, tmpl_meta = -1;
-  if (has_obj) {
-    rf |= KW_REQ_HAS_OBJECT;
-    std::string_view k = is_str(d, d.get((uint32_t)obj, "kind")) ? d.str((uint32_t)d.get((uint32_t)obj, "kind")) : rkind;
-    if (k == "Pod") {
-      spec = d.get((uint32_t)obj, "spec");
-      tmpl_meta = d.get((uint32_t)obj, "metadata");
-    } else if (k == "Deployment" || k == "ReplicaSet" || k == "StatefulSet" || k == "DaemonSet" || k == "Job" ||
-               k == "ReplicationController") {
-      spec = path(d, obj, {"spec", "template", "spec"});
-      tmpl_meta = path(d, obj, {"spec", "template", "metadata"});
-    } else if (k == "CronJob") {
-      spec = path(d, obj, {"spec", "jobTemplate", "spec", "template", "spec"});
-      tmpl_meta = path(d, obj, {"spec", "jobTemplate", "spec", "template", "metadata"});
-    }
-    if (spec >= 0 && !d.is((uint32_t)spec, JType::Obj)) spec = -1;
-  }
+  const PodSpecRef ps = find_podspec(d, req);
+  if (ps.has_obj) rf |= KW_REQ_HAS_OBJECT;
+  const int64_t spec = ps.spec, tmpl_meta = ps.meta;
   if (spec >= 0) rf |= KW_REQ_HAS_PODSPEC;
   b->req_flags.push_back(rf);
 
@@ -205,7 +219,7 @@ void flatten_request(const JDoc& d, int64_t req, bool raw, Batch* b) {
   b->ctr_off.push_back((uint32_t)b->ctr_flags.size());
 
   // labels of the object itself
-  int64_t labels = has_obj ? path(d, obj, {"metadata", "labels"}) : -1;
+  int64_t labels = ps.has_obj ? path(d, d.get((uint32_t)req, "object"), {"metadata", "labels"}) : -1;
   if (labels >= 0 && d.is((uint32_t)labels, JType::Obj)) {
     for (uint32_t j = 0; j < d.count((uint32_t)labels); ++j) {
       const JKid& kid = d.kids((uint32_t)labels)[j];

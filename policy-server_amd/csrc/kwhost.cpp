@@ -248,10 +248,15 @@ class Server {
     for (Row& r : rows) {
       size_t need = 0;
       const uint32_t* mv = r.nmem ? v.data() + r.first + 1 : nullptr;
-      int frc = kw_format_response(env_, b, r.first, r.policy, v[r.first], mv, buf.data(), buf.size(), &need);
+      const std::string& body = r.job->body;  // an accepted mutation's patch is built from the document
+      auto fmt = [&] {
+        return kw_format_response_doc(env_, b, r.first, r.policy, v[r.first], mv, body.data(), body.size(), kind,
+                                      buf.data(), buf.size(), &need);
+      };
+      int frc = fmt();
       if (frc == KW_E_NOSPACE) {
         buf.resize(need + 1);
-        frc = kw_format_response(env_, b, r.first, r.policy, v[r.first], mv, buf.data(), buf.size(), &need);
+        frc = fmt();
       }
       if (frc != KW_OK) {
         r.job->finish(evaluation_error(frc, buf.data()));

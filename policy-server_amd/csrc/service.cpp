@@ -1,6 +1,8 @@
 // service.cpp — see service.hpp.
 #include "service.hpp"
 
+#include <algorithm>
+
 #include "json.hpp"
 
 namespace kw {
@@ -90,8 +92,143 @@ static void put_kv(std::string* o, const char* k, std::string_view v) {
   json_escape(o, v);
 }
 
+namespace {
+
+std::string base64(const std::string& in) {
+  static const char* T = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+  std::string o;
+  o.reserve((in.size() + 2) / 3 * 4);
+  size_t i = 0;
+  for (; i + 2 < in.size(); i += 3) {
+    const uint32_t x = ((uint8_t)in[i] << 16) | ((uint8_t)in[i + 1] << 8) | (uint8_t)in[i + 2];
+    o += T[x >> 18];
+    o += T[(x >> 12) & 63];
+    o += T[(x >> 6) & 63];
+    o += T[x & 63];
+  }
+  if (i + 1 == in.size()) {
+    const uint32_t x = (uint8_t)in[i] << 16;
+    o += T[x >> 18];
+    o += T[(x >> 12) & 63];
+    o += "==";
+  } else if (i + 2 == in.size()) {
+    const uint32_t x = ((uint8_t)in[i] << 16) | ((uint8_t)in[i + 1] << 8);
+    o += T[x >> 18];
+    o += T[(x >> 12) & 63];
+    o += T[(x >> 6) & 63];
+    o += '=';
+  }
+  return o;
+}
+
+void json_list(std::string* o, const std::vector<std::string>& l) {
+  o->append("[");
+  for (size_t i = 0; i < l.size(); ++i) {
+    if (i) o->append(",");
+    json_escape(o, l[i]);  // quoted
+  }
+  o->append("]");
+}
+
+}  // namespace
+
+Status capabilities_patch(const PolicyRec& P, const char* doc, size_t len, int doc_kind, std::string* ops) {
+  thread_local JDoc d;
+  std::string perr;
+  if (!d.parse(doc, len, &perr) || !d.is(0, JType::Obj)) return {KW_E_ARG, "document does not parse"};
+  (void)doc_kind;  // AdmissionReview and RawReview both carry the object under request.object
+  const int64_t req = d.get(0, "request");
+  const PodSpecRef ps = find_podspec(d, req);
+  ops->assign("[");
+  bool first_op = true;
+  auto op = [&](const std::string& path, const std::string& value) {
+    if (!first_op) ops->append(",");
+    first_op = false;
+    ops->append("{\"op\":\"add\",\"path\":");
+    json_escape(ops, path);
+    ops->append(",\"value\":");
+    ops->append(value);
+    ops->append("}");
+  };
+  auto uniq = [](const std::vector<std::string>& l) {
+    std::vector<std::string> o;
+    for (const auto& x : l)
+      if (std::find(o.begin(), o.end(), x) == o.end()) o.push_back(x);
+    return o;
+  };
+  const std::vector<std::string> reqd = uniq(P.lists[1]), defa = uniq(P.lists[2]);
+  if (ps.spec >= 0) {
+    const char* lists[3] = {"containers", "initContainers", "ephemeralContainers"};
+    for (const char* ln : lists) {
+      const int64_t arr = d.get((uint32_t)ps.spec, ln);
+      if (arr < 0 || !d.is((uint32_t)arr, JType::Arr)) continue;
+      for (uint32_t k = 0; k < d.count((uint32_t)arr); ++k) {
+        const uint32_t c = d.kids((uint32_t)arr)[k].node;
+        if (!d.is(c, JType::Obj)) continue;
+        const int64_t sc = d.get(c, "securityContext");
+        const bool sc_obj = sc >= 0 && d.is((uint32_t)sc, JType::Obj);
+        const int64_t caps = sc_obj ? d.get((uint32_t)sc, "capabilities") : -1;
+        const bool caps_obj = caps >= 0 && d.is((uint32_t)caps, JType::Obj);
+        const int64_t add = caps_obj ? d.get((uint32_t)caps, "add") : -1, drop = caps_obj ? d.get((uint32_t)caps, "drop") : -1;
+        const bool add_arr = add >= 0 && d.is((uint32_t)add, JType::Arr), drop_arr = drop >= 0 && d.is((uint32_t)drop, JType::Arr);
+        auto has = [&](int64_t a, bool is_arr, const std::string& x) {
+          if (!is_arr) return false;
+          for (uint32_t i = 0; i < d.count((uint32_t)a); ++i) {
+            const uint32_t it = d.kids((uint32_t)a)[i].node;
+            if (d.is(it, JType::Str) && d.str(it) == x) return true;
+          }
+          return false;
+        };
+        std::vector<std::string> mdrop, madd;
+        if (!has(drop, drop_arr, "ALL"))
+          for (const auto& x : reqd)
+            if (!has(drop, drop_arr, x)) mdrop.push_back(x);
+        for (const auto& x : defa)
+          if (!has(add, add_arr, x) && !has(drop, drop_arr, x)) madd.push_back(x);
+        if (mdrop.empty() && madd.empty()) continue;
+        const std::string base = std::string(ps.pointer) + "/" + ln + "/" + std::to_string(k) + "/securityContext";
+        std::string cap_obj = "{";
+        if (!madd.empty()) {
+          cap_obj += "\"add\":";
+          json_list(&cap_obj, madd);
+        }
+        if (!mdrop.empty()) {
+          if (!madd.empty()) cap_obj += ",";
+          cap_obj += "\"drop\":";
+          json_list(&cap_obj, mdrop);
+        }
+        cap_obj += "}";
+        if (!sc_obj) {
+          op(base, "{\"capabilities\":" + cap_obj + "}");
+        } else if (!caps_obj) {
+          op(base + "/capabilities", cap_obj);
+        } else {
+          for (const auto* pr : {&madd, &mdrop}) {
+            if (pr->empty()) continue;
+            const bool is_add = pr == &madd;
+            const std::string lp = base + "/capabilities/" + (is_add ? "add" : "drop");
+            if (!(is_add ? add_arr : drop_arr)) {
+              std::string v;
+              json_list(&v, *pr);
+              op(lp, v);
+            } else {
+              for (const auto& x : *pr) {
+                std::string v;
+                json_escape(&v, x);
+                op(lp + "/-", v);
+              }
+            }
+          }
+        }
+      }
+    }
+  }
+  ops->append("]");
+  return {};
+}
+
 Status format_response(const Env& env, const Batch& b, uint64_t row, int32_t pidx, uint32_t v, const uint32_t* member_v,
-                       std::string* out) {
+                       std::string* out, const char* doc, size_t doc_len, int doc_kind) {
   const PolicyRec& P = env.pol[(size_t)pidx];
   out->clear();
   std::string_view uid = b.uid.at(row);
@@ -106,8 +243,19 @@ Status format_response(const Env& env, const Batch& b, uint64_t row, int32_t pid
     return {};
   }
   if (P.is_group && !P.broken_member.empty()) return {KW_E_NOT_FOUND, "unknown policy: " + P.broken_member};
-  if ((v & KW_F_PATCH) != 0)
-    return {KW_E_ENGINE, "JSONPatch generation for mutating policies is not implemented yet"};
+  if ((v & KW_F_PATCH) != 0) {  // accepted mutation: the response carries the JSONPatch
+    if (!doc) return {KW_E_ARG, "the original document is required to format a mutation (kw_format_response_doc)"};
+    if (P.family != FAM_CAPABILITIES) return {KW_E_ENGINE, "mutation by a non-mutating policy family"};
+    std::string ops;
+    Status st = capabilities_patch(P, doc, doc_len, doc_kind, &ops);
+    if (!st.ok()) return st;
+    out->append("{");
+    put_kv(out, "uid", uid);
+    out->append(",\"allowed\":true,\"patchType\":\"JSONPatch\",");
+    put_kv(out, "patch", base64(ops));
+    out->append("}");
+    return {};
+  }
   out->append("{");
   put_kv(out, "uid", uid);
   out->append((v & KW_F_ALLOWED) ? ",\"allowed\":true" : ",\"allowed\":false");

@@ -342,14 +342,22 @@ class Batch:
         self._npol = len(policies)
         return t
 
-    def format_response(self, env, row, policy, verdict, member_verdicts=None):
+    def format_response(self, env, row, policy, verdict, member_verdicts=None, doc=None, raw=False):
+        """AdmissionResponse of (row, policy, verdict); `doc` (the row's original JSON) is needed
+        for an accepted mutation, whose response carries the JSONPatch."""
         mv = None
         if member_verdicts is not None:
             mv = (C.c_uint32 * len(member_verdicts))(*[int(x) for x in member_verdicts])
         need = C.c_size_t()
         buf = C.create_string_buffer(1 << 15)
-        rc = self._L.kw_format_response(env._h, self._h, row, env._idx(policy), int(verdict), mv, buf, len(buf),
-                                        C.byref(need))
+        if doc is not None:
+            d = doc.encode() if isinstance(doc, str) else doc
+            rc = self._L.kw_format_response_doc(env._h, self._h, row, env._idx(policy), int(verdict), mv, d, len(d),
+                                                N.KW_DOC_RAW_REVIEW if raw else N.KW_DOC_ADMISSION_REVIEW, buf,
+                                                len(buf), C.byref(need))
+        else:
+            rc = self._L.kw_format_response(env._h, self._h, row, env._idx(policy), int(verdict), mv, buf, len(buf),
+                                            C.byref(need))
         raise_for(rc, buf.value.decode(errors="replace"))
         return json.loads(buf.value.decode())
 

@@ -86,7 +86,7 @@ EXPORTS = [
     "kw_env_policy_initialization_error", "kw_env_validate_settings", "kw_pattern_match", "kw_env_classify_check",
     "kw_batch_from_json", "kw_batch_from_soa", "kw_batch_view", "kw_batch_to_device",
     "kw_batch_destroy", "kw_debug_host_walk", "kw_validate_batch", "kw_validate_rows", "kw_batch_verdicts",
-    "kw_validate_timed", "kw_format_response", "kw_env_group_members", "kw_evaluate",
+    "kw_validate_timed", "kw_format_response", "kw_format_response_doc", "kw_env_group_members", "kw_evaluate",
     "kw_service_constraints", "kw_version",
 ]
 
@@ -131,6 +131,7 @@ def lib():
         "kw_debug_host_walk": (ip, [vp, vp, C.POINTER(i32), u32, ip, C.POINTER(u32)]),
         "kw_validate_timed": (ip, [vp, vp, C.POINTER(i32), u32, ip, ip, ip, C.POINTER(KwTiming)]),
         "kw_format_response": (ip, [vp, vp, u64, i32, u32, C.POINTER(u32), cp, sz, C.POINTER(sz)]),
+        "kw_format_response_doc": (ip, [vp, vp, u64, i32, u32, C.POINTER(u32), cp, sz, ip, cp, sz, C.POINTER(sz)]),
         "kw_env_group_members": (ip, [vp, i32, C.POINTER(i32), ip]),
         "kw_evaluate": (ip, [vp, cp, cp, sz, ip, ip, cp, sz, C.POINTER(sz)]),
         "kw_service_constraints": (ip, [u32, ip, ip, C.POINTER(u32)]),

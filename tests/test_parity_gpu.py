@@ -47,29 +47,32 @@ def test_all_pairs_match_oracle(name, scfg, rows, origin):
     assert np.array_equal(gpu, ora), diff_verdicts(gpu, ora, len(ids), ids)
 
 
+@pytest.mark.parametrize("origin", [K.VALIDATE, K.AUDIT])
 @pytest.mark.parametrize("name,scfg,rows", CASES[:4])
-def test_responses_match_oracle(name, scfg, rows):
-    """kw_format_response (service epilogue) == the oracle's restated AdmissionResponse."""
+def test_responses_match_oracle(name, scfg, rows, origin):
+    """kw_format_response_doc (service epilogue, JSONPatch of accepted mutations included) == the
+    oracle's restated AdmissionResponse."""
     env, oe = _envs(name)
     ids = env.policy_ids()
     syn = K.SynthBatch(scfg, 600, seed=77 + scfg)
     b = syn.batch().to_device(0)
-    b.validate(env, ids, K.VALIDATE)
+    b.validate(env, ids, origin)
     v = b.verdicts().reshape(600, len(ids))
     soa = syn.soa()
+    docs = [syn.json(r) for r in range(600)]
     checked = 0
     for r in range(600):
         for j, pid in enumerate(ids):
             members = env.group_members(j) if env.is_group(j) else []
             mv = [int(v[r, m]) for m in members] if members else None
             try:
-                want = oe.response(soa, r, j, int(v[r, j]), mv)
+                want = oe.response(soa, r, j, int(v[r, j]), mv, doc=docs[r])
             except KeyError as e:
                 with pytest.raises(K.PolicyNotFound):
-                    b.format_response(env, r, j, int(v[r, j]), mv)
+                    b.format_response(env, r, j, int(v[r, j]), mv, doc=docs[r])
                 assert str(e).strip("'").startswith("unknown policy")
                 continue
-            got = b.format_response(env, r, j, int(v[r, j]), mv)
+            got = b.format_response(env, r, j, int(v[r, j]), mv, doc=docs[r])
             assert got == want, (r, pid, got, want)
             checked += 1
     assert checked >= min(1000, 600 * len(ids) // 2)
