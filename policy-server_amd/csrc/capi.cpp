@@ -28,6 +28,16 @@ struct kw_env {
 
 namespace kw {
 
+// Requests per tile of the slot kernel: kSlotRows, or KW_SLOT_ROWS (8..64, A/B knob) when set.
+uint32_t slot_rows() {
+  static const uint32_t r = [] {
+    const char* e = getenv("KW_SLOT_ROWS");
+    const int v = e ? atoi(e) : 0;
+    return (v >= 8 && v <= (int)kSlotRows) ? (uint32_t)v : kSlotRows;
+  }();
+  return r;
+}
+
 // Per-tile entity counts and staged byte ranges of a batch, reduced to a high quantile (tile_stats).
 struct TileStats {
   uint32_t ctr = 0, lbl = 0, kadd = 0, kdrop = 0;
@@ -427,8 +437,9 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
   // ---- tile geometry and LDS layout (slot kernel: kSlotRows requests per tile)
   TileArgs& T = plan->tile;
   auto align = [](uint32_t x) { return (x + 15u) & ~15u; };
+  const uint32_t rows = slot_rows();
   if (!D.stats_valid) {
-    D.tile_need = tile_needs(B, kSlotRows);
+    D.tile_need = tile_needs(B, rows);
     D.tile_q.clear();
     for (double q : kTileQuantiles) D.tile_q.push_back(tile_quantile(D.tile_need, q));
     D.cap_choice = -1;
@@ -443,7 +454,6 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
     nslots = std::max(nslots, c.nslots);
     groups = groups || c.groups;
   }
-  const uint32_t rows = kSlotRows;
   const uint32_t vw_stride = nslots | 1u;  // odd stride: lanes (requests) spread over the banks
   // LDS layout for capacities `ts` (shrunk by `scale` only when over the budget); returns the bytes
   auto layout = [&](const TileStats& ts) -> uint32_t {

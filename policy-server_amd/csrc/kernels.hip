@@ -907,7 +907,7 @@ __global__ void __launch_bounds__(kSlotThreads)
             }
             uint64_t nw = tab_or(sv.tab(ST_MAND), SH.mand_union & ~present) & ~lrej;
             rej |= nw;
-            const uint8_t* mand = t.slot_plan + SH.o_mand;  // global: read only for a violation
+            const uint8_t* mand = sv.base + SH.o_mand;  // staged with the record (LDS)
             while (nw) {  // the first missing mandatory key of each such slot, settings order
               const uint32_t sl = kw_ctz64(nw);
               nw &= nw - 1;
@@ -1123,6 +1123,29 @@ hipError_t launch_evaluate_slots(const EvalArgs& a, const TileArgs& t, const Til
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e1 != hipSuccess || e2 != hipSuccess) return e1 != hipSuccess ? e1 : e2;
     attr_set = true;
+  }
+  // The grid is persistent (tiles strided by gridDim.x), so it must be co-resident: a workgroup
+  // that only starts when another retires doubles the tail. Clamp the planner's grid to the
+  // runtime's occupancy for this LDS size (queried once per device and LDS size).
+  {
+    thread_local int c_dev = -1, c_ncu = 0, c_occ = 0;
+    thread_local uint64_t c_key = ~0ull;
+    int dev = 0;
+    const uint64_t key = ((uint64_t)t.lds_bytes << 1) | (fused ? 1u : 0u);
+    if (hipGetDevice(&dev) == hipSuccess && (dev != c_dev || key != c_key)) {
+      int ncu = 0, occ = 0;
+      const void* fn = fused ? (const void*)evaluate_slots_kernel<true> : (const void*)evaluate_slots_kernel<false>;
+      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kSlotThreads, t.lds_bytes) != hipSuccess)
+        ncu = occ = 0;
+      c_dev = dev;
+      c_key = key;
+      c_ncu = ncu;
+      c_occ = occ;
+    }
+    if (c_occ > 0 && c_ncu > 0) grid = std::max<uint32_t>(1u, std::min<uint32_t>(grid, (uint32_t)(c_occ * c_ncu)));
+    if (t.debug & 256u)
+      fprintf(stderr, "[kw tile] launch grid=%u occupancy=%d wg/cu x %d CUs lds=%u\n", grid, c_occ, c_ncu, t.lds_bytes);
   }
   if (fused)
     hipLaunchKernelGGL(evaluate_slots_kernel<true>, dim3(grid), dim3(kSlotThreads), t.lds_bytes, s, a, d_t, d_desc,

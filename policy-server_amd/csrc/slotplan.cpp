@@ -122,18 +122,19 @@ struct Builder {
     h.o_ce = off;
     off += (uint32_t)(ce.size() * sizeof(ConstrEnt));
     // the device stages everything up to o_cols: the column arrays are the staged form of the
-    // column records (P3 reads 4 columns per array with one 16-B LDS load); ColInfo, mand and cidx
-    // stay in global memory (group / constant columns, the arguments of mandatory-label and
-    // constraint violations)
+    // column records (P3 reads 4 columns per array with one 16-B LDS load) and the mandatory-key
+    // lists (1 KB; P2 reads one per missing-mandatory slot of a request, a dependent chain that
+    // global latency would serialise). ColInfo and cidx stay in global memory (group / constant
+    // columns, the constraint index of a constraint violation)
     const uint32_t cs_n = ((uint32_t)cols.size() + 3u) & ~3u;
     off = (off + 15u) & ~15u;
     h.o_csoa = (uint16_t)off;
     off += 16u * cs_n;
+    h.o_mand = h.lbl ? off : 0;
+    if (h.lbl) off += sizeof(mand);
     h.o_cols = off;
     off += (uint32_t)(cols.size() * sizeof(ColInfo));
     off = (off + 15u) & ~15u;
-    h.o_mand = h.lbl ? off : 0;
-    if (h.lbl) off += sizeof(mand);
     h.o_cidx = 0;
     if (h.lbl) {
       h.o_cidx = off;
