@@ -280,6 +280,31 @@ int kw_evaluate(const kw_env *env, const char *policy_id, const char *doc, size_
 int kw_service_constraints(uint32_t vanilla_flags, int mode, int allowed_to_mutate,
                            uint32_t *out_flags);
 
+/* ---------------------------------------------------------------------------------------------
+ * Metrics (src/metrics.rs:49-140, src/metrics/policy_evaluations_{total,latency}.rs; recorded by
+ * service::evaluate, src/api/service.rs:40-71, :78-84, :118-150). A kw_metrics aggregates the
+ * counter kubewarden_policy_evaluations_total and the u64 histogram
+ * kubewarden_policy_evaluation_latency_milliseconds with the reference's attribute sets:
+ *   AdmissionRequest: policy_name, policy_mode, resource_kind (requestKind.kind),
+ *     resource_request_operation, accepted, mutated, request_origin[, resource_namespace][, error_code]
+ *   Raw: policy_name, policy_mode, accepted, mutated[, error_code]
+ *   initialization error (counter only): policy_name, initialization_error
+ * accepted / mutated / error_code are the vanilla response's (before constraints); a namespace
+ * bypass counts as accepted, not mutated. Thread-safe; kept off the device path.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct kw_metrics kw_metrics;
+kw_metrics *kw_metrics_create(void);
+void kw_metrics_destroy(kw_metrics *m);
+/* Record n evaluated (row, policy) pairs of one validate pass: rows[i] of batch b against
+ * policies[i], with their final verdict words and the latency from arrival to verdict in ms. Only
+ * the policies the requests addressed are recorded (not a group's member rows). */
+int kw_metrics_record(kw_metrics *m, const kw_env *env, const kw_batch *b, const uint64_t *rows,
+                      const int32_t *policies, const uint32_t *verdicts, const uint64_t *latency_ms,
+                      size_t n, int origin);
+/* Prometheus text exposition (format 0.0.4) of everything recorded so far. */
+int kw_metrics_render(const kw_metrics *m, char *buf, size_t cap, size_t *need);
+void kw_metrics_reset(kw_metrics *m);
+
 const char *kw_version(void);
 
 #ifdef __cplusplus

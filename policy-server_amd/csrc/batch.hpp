@@ -58,6 +58,7 @@ struct Batch {
   std::vector<uint8_t> req_flags;
   std::vector<uint32_t> ctr_off{0}, lbl_off{0};
   StrCol uid, ns, op, kind;
+  StrCol rkind;  // request.requestKind.kind, "" when absent (host only: metrics resource_kind)
   std::vector<uint8_t> ctr_flags;
   std::vector<uint32_t> capadd_off{0}, capdrop_off{0};
   StrCol ctr_name, ctr_image, ctr_aa, cap_add, cap_drop, lbl_key, lbl_val;

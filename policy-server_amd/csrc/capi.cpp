@@ -17,6 +17,7 @@
 #include "batch.hpp"
 #include "env.hpp"
 #include "kernels.hpp"
+#include "metrics.hpp"
 #include "service.hpp"
 #include "slotplan.hpp"
 
@@ -1442,3 +1443,31 @@ int kw_service_constraints(uint32_t in, int mode, int allowed_to_mutate, uint32_
 }
 
 }  // extern "C"
+
+// ---- metrics (metrics.hpp)
+struct kw_metrics {
+  kw::Metrics m;
+};
+
+kw_metrics* kw_metrics_create(void) { return new (std::nothrow) kw_metrics(); }
+void kw_metrics_destroy(kw_metrics* m) { delete m; }
+
+int kw_metrics_record(kw_metrics* m, const kw_env* env, const kw_batch* b, const uint64_t* rows,
+                      const int32_t* policies, const uint32_t* verdicts, const uint64_t* latency_ms, size_t n,
+                      int origin) {
+  if (!m || !env || !b || (n && (!rows || !policies || !verdicts || !latency_ms))) return KW_E_ARG;
+  if (origin != KW_ORIGIN_VALIDATE && origin != KW_ORIGIN_AUDIT) return KW_E_ARG;
+  for (size_t i = 0; i < n; ++i)
+    if (rows[i] >= b->b.n || policies[i] < 0 || (size_t)policies[i] >= env->e.pol.size()) return KW_E_ARG;
+  for (size_t i = 0; i < n; ++i) m->m.record(env->e, b->b, rows[i], policies[i], verdicts[i], origin, latency_ms[i]);
+  return KW_OK;
+}
+
+int kw_metrics_render(const kw_metrics* m, char* buf, size_t cap, size_t* need) {
+  if (!m) return KW_E_ARG;
+  return put_out(m->m.render(), buf, cap, need);
+}
+
+void kw_metrics_reset(kw_metrics* m) {
+  if (m) m->m.reset();
+}

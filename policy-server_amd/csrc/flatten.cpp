@@ -53,8 +53,8 @@ void Batch::append(const Batch& o) {
   ctr_flags.insert(ctr_flags.end(), o.ctr_flags.begin(), o.ctr_flags.end());
   shift(&capadd_off, o.capadd_off);
   shift(&capdrop_off, o.capdrop_off);
-  StrCol* mine[] = {&uid, &ns, &op, &kind, &ctr_name, &ctr_image, &ctr_aa, &cap_add, &cap_drop, &lbl_key, &lbl_val};
-  const StrCol* theirs[] = {&o.uid, &o.ns, &o.op, &o.kind, &o.ctr_name, &o.ctr_image, &o.ctr_aa,
+  StrCol* mine[] = {&uid, &ns, &op, &kind, &rkind, &ctr_name, &ctr_image, &ctr_aa, &cap_add, &cap_drop, &lbl_key, &lbl_val};
+  const StrCol* theirs[] = {&o.uid, &o.ns, &o.op, &o.kind, &o.rkind, &o.ctr_name, &o.ctr_image, &o.ctr_aa,
                             &o.cap_add, &o.cap_drop, &o.lbl_key, &o.lbl_val};
   for (size_t k = 0; k < sizeof(mine) / sizeof(mine[0]); ++k) mine[k]->append(*theirs[k]);
 }
@@ -169,6 +169,7 @@ void flatten_request(const JDoc& d, int64_t req, bool raw, Batch* b) {
   b->op.push(sv(d, req_obj ? d.get((uint32_t)req, "operation") : -1));
   std::string_view rkind = sv(d, req_obj ? path(d, req, {"kind", "kind"}) : -1);
   b->kind.push(rkind);
+  b->rkind.push(sv(d, req_obj && !raw ? path(d, req, {"requestKind", "kind"}) : -1));
 
   const PodSpecRef ps = find_podspec(d, req);
   if (ps.has_obj) rf |= KW_REQ_HAS_OBJECT;
@@ -305,6 +306,8 @@ bool batch_from_soa(const kw_soa& s, Batch* b, std::string* err) {
   copy(s.ns, &b->ns);
   copy(s.op, &b->op);
   copy(s.kind, &b->kind);
+  b->rkind.clear();
+  for (uint64_t i = 0; i < n; ++i) b->rkind.push("");  // not part of kw_soa
   copy(s.ctr_name, &b->ctr_name);
   copy(s.ctr_image, &b->ctr_image);
   copy(s.ctr_apparmor, &b->ctr_aa);

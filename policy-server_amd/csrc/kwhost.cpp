@@ -19,6 +19,9 @@
 //   unknown policy                       404  {"message":"unknown policy: <id>","status":404}
 //   any other evaluation error           500  {"message":"Something went wrong","status":500}
 //   GET /readiness                       200  (empty)
+//   GET /metrics                         200  Prometheus text: kubewarden_policy_evaluations_total and
+//                                             kubewarden_policy_evaluation_latency_milliseconds
+//                                             (src/metrics.rs; the reference exports them over OTLP)
 //   unknown route                        404  (empty)
 //
 // Usage: kwhost --policies policies.json [--addr 127.0.0.1] [--port 3000] [--device 0]
@@ -70,6 +73,7 @@ struct Job {
   Route route;
   std::string policy, body;
   Reply reply;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();  // arrival (service.rs:37)
   bool done = false;
   std::mutex m;
   std::condition_variable cv;
@@ -243,6 +247,20 @@ class Server {
       if (b) kw_batch_destroy(b);
       return;
     }
+    // metrics of the addressed policies (service.rs:40-150), latency = arrival -> verdict
+    if (metrics_) {
+      const auto now = std::chrono::steady_clock::now();
+      std::vector<uint64_t> mrow, mlat;
+      std::vector<int32_t> mpol;
+      std::vector<uint32_t> mv;
+      for (Row& r : rows) {
+        mrow.push_back(r.first);
+        mpol.push_back(r.policy);
+        mv.push_back(v[r.first]);
+        mlat.push_back((uint64_t)std::chrono::duration_cast<std::chrono::milliseconds>(now - r.job->t0).count());
+      }
+      kw_metrics_record(metrics_, env_, b, mrow.data(), mpol.data(), mv.data(), mlat.data(), mrow.size(), origin);
+    }
     // 4. service epilogue + response envelope (AdmissionReviewResponse / RawReviewResponse)
     std::vector<char> buf(4096);
     for (Row& r : rows) {
@@ -274,6 +292,9 @@ class Server {
 
   const Opts& o_;
   kw_env* env_;
+ public:
+  kw_metrics* metrics_ = nullptr;  // GET /metrics (owned by main)
+ private:
   std::mutex qm_;
   std::condition_variable qcv_;
   std::deque<Job*> q_;
@@ -409,6 +430,17 @@ void serve(Server* srv, int fd) {
     if (path == "/readiness") {
       rep.status = method == "GET" ? 200 : 405;
       rep.ctype.clear();
+    } else if (path == "/metrics") {  // the reference pushes OTLP; kwhost exposes the same series
+      rep.status = method == "GET" ? 200 : 405;
+      rep.ctype.clear();
+      if (method == "GET" && srv->metrics_) {
+        size_t need = 0;
+        kw_metrics_render(srv->metrics_, nullptr, 0, &need);
+        std::vector<char> mb(need + 1);
+        kw_metrics_render(srv->metrics_, mb.data(), mb.size(), &need);
+        rep.body.assign(mb.data(), strnlen(mb.data(), mb.size()));
+        rep.ctype = "text/plain; version=0.0.4";
+      }
     } else if (!known || rest.empty() || rest.find('/') != std::string::npos || !percent_decode(rest, &policy)) {
       rep.status = 404;
       rep.ctype.clear();
@@ -499,6 +531,7 @@ int main(int argc, char** argv) {
   }
   signal(SIGPIPE, SIG_IGN);
   Server srv(o, env);
+  srv.metrics_ = kw_metrics_create();
   std::thread(&Server::batcher, &srv).detach();
   fprintf(stderr, "kwhost: %d policies, listening on %s:%d\n", kw_env_policy_count(env), o.addr.c_str(), o.port);
   for (;;) {

@@ -373,6 +373,79 @@ class Batch:
             pass
 
 
+class Metrics:
+    """kubewarden_policy_evaluations_total and kubewarden_policy_evaluation_latency_milliseconds
+    (src/metrics.rs:49-140), aggregated per validate pass from the verdict words (kw_metrics_*)."""
+
+    def __init__(self):
+        self._L = N.lib()
+        self._h = self._L.kw_metrics_create()
+        if not self._h:
+            raise EngineError("kw_metrics_create failed")
+
+    def record(self, env, batch, rows, policies, verdicts, latency_ms, origin=VALIDATE):
+        n = len(rows)
+        if not (len(policies) == len(verdicts) == len(latency_ms) == n):
+            raise ValueError("rows, policies, verdicts and latency_ms must have the same length")
+        r = (C.c_uint64 * max(n, 1))(*[int(x) for x in rows])
+        p = (C.c_int32 * max(n, 1))(*[env._idx(x) if isinstance(x, str) else int(x) for x in policies])
+        v = (C.c_uint32 * max(n, 1))(*[int(x) for x in verdicts])
+        lat = (C.c_uint64 * max(n, 1))(*[int(x) for x in latency_ms])
+        raise_for(self._L.kw_metrics_record(self._h, env._h, batch._h, r, p, v, lat, n, origin), "kw_metrics_record")
+
+    def render(self):
+        need = C.c_size_t(0)
+        self._L.kw_metrics_render(self._h, None, 0, C.byref(need))
+        buf = C.create_string_buffer(need.value + 1)
+        raise_for(self._L.kw_metrics_render(self._h, buf, len(buf), C.byref(need)), "kw_metrics_render")
+        return buf.value.decode()
+
+    def samples(self):
+        """{(metric name, frozenset of (label, value)): value} parsed from render()."""
+        out = {}
+        for line in self.render().splitlines():
+            if not line or line.startswith("#"):
+                continue
+            head, val = line.rsplit(" ", 1)
+            name, _, labels = head.partition("{")
+            kv = []
+            for part in _split_labels(labels.rstrip("}")):
+                k, _, v = part.partition("=")
+                kv.append((k, v[1:-1].replace('\\"', '"').replace("\\n", "\n").replace("\\\\", "\\")))
+            out[(name, frozenset(kv))] = int(val)
+        return out
+
+    def reset(self):
+        self._L.kw_metrics_reset(self._h)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._L.kw_metrics_destroy(self._h)
+            self._h = None
+
+
+def _split_labels(s):
+    parts, cur, q, esc = [], "", False, False
+    for ch in s:
+        if esc:
+            cur += ch
+            esc = False
+        elif ch == "\\":
+            cur += ch
+            esc = True
+        elif ch == '"':
+            cur += ch
+            q = not q
+        elif ch == "," and not q:
+            parts.append(cur)
+            cur = ""
+        else:
+            cur += ch
+    if cur:
+        parts.append(cur)
+    return parts
+
+
 def service_constraints(allowed, has_patch, has_status, mode, allowed_to_mutate):
     """validation_response_with_constraints (service.rs:160-208) on flags."""
     out = C.c_uint32()

@@ -87,7 +87,8 @@ EXPORTS = [
     "kw_batch_from_json", "kw_batch_from_soa", "kw_batch_view", "kw_batch_to_device",
     "kw_batch_destroy", "kw_debug_host_walk", "kw_validate_batch", "kw_validate_rows", "kw_batch_verdicts",
     "kw_validate_timed", "kw_format_response", "kw_format_response_doc", "kw_env_group_members", "kw_evaluate",
-    "kw_service_constraints", "kw_version",
+    "kw_service_constraints", "kw_metrics_create", "kw_metrics_destroy", "kw_metrics_record", "kw_metrics_render",
+    "kw_metrics_reset", "kw_version",
 ]
 
 _lib = None
@@ -135,6 +136,11 @@ def lib():
         "kw_env_group_members": (ip, [vp, i32, C.POINTER(i32), ip]),
         "kw_evaluate": (ip, [vp, cp, cp, sz, ip, ip, cp, sz, C.POINTER(sz)]),
         "kw_service_constraints": (ip, [u32, ip, ip, C.POINTER(u32)]),
+        "kw_metrics_create": (vp, []),
+        "kw_metrics_destroy": (None, [vp]),
+        "kw_metrics_record": (ip, [vp, vp, vp, C.POINTER(u64), C.POINTER(i32), C.POINTER(u32), C.POINTER(u64), sz, ip]),
+        "kw_metrics_render": (ip, [vp, cp, sz, C.POINTER(sz)]),
+        "kw_metrics_reset": (None, [vp]),
         "kw_version": (cp, []),
     }
     for name, (res, args) in sig.items():

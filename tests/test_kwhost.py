@@ -24,6 +24,10 @@ def test_readiness_and_unknown_routes(host):
     assert host.request("GET", "/nope")[0] == 404
     assert host.request("POST", "/validate/")[0] == 404
     assert host.request("GET", "/validate/pod-privileged")[0] == 405
+    st, ct, body = host.request("GET", "/metrics")  # no device: nothing evaluated, nothing recorded
+    assert st == 200 and ct.startswith("text/plain")
+    assert body.decode().splitlines() == ["# TYPE kubewarden_policy_evaluations_total counter",
+                                          "# TYPE kubewarden_policy_evaluation_latency_milliseconds histogram"]
 
 
 @pytest.mark.parametrize("route", ["validate", "audit", "validate_raw"])

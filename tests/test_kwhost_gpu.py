@@ -59,6 +59,12 @@ def test_concurrent_routes_match_oracle(name, scfg):
             return c, st, json.loads(body) if body else None
         with ThreadPoolExecutor(max_workers=24) as ex:
             results = list(ex.map(one, calls))
+        st, _, metrics = h.request("GET", "/metrics")
+    assert st == 200
+    # every evaluated call (200) is one kubewarden_policy_evaluations_total data point (service.rs:40-150)
+    total = sum(int(line.rsplit(" ", 1)[1]) for line in metrics.decode().splitlines()
+                if line.startswith("kubewarden_policy_evaluations_total{"))
+    assert total == sum(1 for _, st, _ in results if st == 200)
     bad = [(c[0], c[1], ids[c[2]], st, got, c[3]) for c, st, got in results if (st, got) != c[3]]
     assert not bad, bad[:3]
     assert sum(1 for c in calls if c[3][0] == 200) > len(calls) // 2
