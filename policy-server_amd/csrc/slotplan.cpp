@@ -172,15 +172,28 @@ Status build_slot_chunks(const Env& E, const int32_t* pols, uint32_t npol, int o
   const DevPolicy* dp = (const DevPolicy*)(E.blob.data() + H->policy_off);
   const int32_t* mem = (const int32_t*)(E.blob.data() + H->member_off);
   // slots a column needs: a plain policy 1, a group its members, a constant column none
+  // Plain policies whose compiled settings are identical share one slot: the column words carry
+  // mode and allowedToMutate, the slot only what the family computes. This is the compiled form of
+  // the reference's module-digest sharing (evaluation_environment.rs:400-418), one level further:
+  // equal settings, not only an equal module, evaluate once per request.
+  auto slot_key = [&](const DevPolicy& P) {
+    DevPolicy k = P;
+    k.mode = k.a2m = 0;
+    k.prog_off = k.prog_len = k.member_off = k.nmembers = k.pad0 = 0;
+    memset(k.pad1, 0, sizeof(k.pad1));
+    return std::string((const char*)&k, sizeof(k));
+  };
+  std::map<std::string, uint32_t> shared;  // slot key -> slot of the current chunk
   auto need = [&](int32_t p) -> uint32_t {
     const DevPolicy& P = dp[p];
     if (P.flags & PF_INIT_ERROR) return 0;
     if (P.family == FAM_GROUP) return (P.flags & PF_EXPR_ERROR) ? 0u : P.nmembers;
-    return 1;
+    return shared.count(slot_key(P)) ? 0u : 1u;
   };
   uint32_t j = 0;
   while (j < npol) {
     Builder b;
+    shared.clear();
     SlotChunk ch;
     ch.col0 = j;
     while (j < npol && b.cols.size() < kSlots) {
@@ -209,7 +222,9 @@ Status build_slot_chunks(const Env& E, const int32_t* pols, uint32_t npol, int o
         b.groups = true;
       } else {
         ci.kind = CK_PLAIN;
-        ci.slot = b.add_slot(P);
+        const std::string key = slot_key(P);
+        auto it = shared.find(key);
+        ci.slot = it != shared.end() ? it->second : (shared[key] = b.add_slot(P));
         ci.okw = finish_word(P.mode, P.a2m, origin, 0, 0, false);
         ci.mutw = finish_word(P.mode, P.a2m, origin, 0, 0, true);
         ci.rejb = finish_word(P.mode, P.a2m, origin, 1, 0, false) & ~0xff00u;

@@ -187,3 +187,20 @@ def test_wide_requests():
     gpu = b.verdicts()
     ora = oe.eval(b.view(), ids)
     assert np.array_equal(gpu, ora), diff_verdicts(gpu, ora, len(ids), ids)
+
+
+@pytest.mark.parametrize("origin", [K.VALIDATE, K.AUDIT])
+def test_shared_slots_match_oracle(origin):
+    """Copies of plain policies under other modes / allowedToMutate share one evaluation slot on the
+    device (slotplan.cpp); each column still answers with its own mode."""
+    from test_slots import dup_config
+    doc = dup_config()
+    env = K.EvaluationEnvironment(doc, continue_on_errors=True, always_accept_namespace=NS, device=0)
+    oe = O.OracleEnv(doc, continue_on_errors=True, always_accept_namespace=NS)
+    ids = env.policy_ids()
+    syn = K.SynthBatch(0, 6000, seed=4242)
+    b = syn.batch().to_device(0)
+    b.validate(env, ids, origin)
+    gpu = b.verdicts()
+    ora = oe.eval(syn.soa(), ids, origin)
+    assert np.array_equal(gpu, ora), diff_verdicts(gpu, ora, len(ids), ids)

@@ -95,3 +95,34 @@ def test_wide_documents():
     got = b.debug_host_walk(env, ids)
     want = oe.eval(b.view(), ids)
     assert np.array_equal(got, want), diff_verdicts(got, want, len(ids), ids)
+
+
+def dup_config():
+    """parity.yml plus copies of its plain policies under other names, modes and allowedToMutate:
+    equal compiled settings share one slot (slotplan.cpp build_slot_chunks), the column words keep
+    each copy's own mode / mutation constraint."""
+    import copy
+    doc = config("parity")
+    out = dict(doc)
+    for name, e in doc.items():
+        if "module" not in e:
+            continue
+        for k, (mode, a2m) in enumerate([("monitor", False), ("protect", True), ("monitor", True)]):
+            c = copy.deepcopy(e)
+            c["policyMode"] = mode
+            c["allowedToMutate"] = a2m
+            out[f"{name}-dup{k}"] = c
+    return out
+
+
+@pytest.mark.parametrize("origin", [K.VALIDATE, K.AUDIT])
+def test_shared_slots_keep_column_modes(origin):
+    doc = dup_config()
+    env = K.EvaluationEnvironment(doc, continue_on_errors=True, always_accept_namespace=NS)
+    oe = O.OracleEnv(doc, continue_on_errors=True, always_accept_namespace=NS)
+    ids = env.policy_ids()
+    assert len(ids) > 64  # several chunks, duplicates within and across them
+    syn = K.SynthBatch(0, 1200, seed=77)
+    got = syn.batch().debug_host_walk(env, ids, origin)
+    want = oe.eval(syn.soa(), ids, origin)
+    assert np.array_equal(got, want), diff_verdicts(got, want, len(ids), ids)
