@@ -66,6 +66,7 @@ struct DeviceBatch {
   size_t mask_cap[NMASK] = {};
   uint32_t* verdicts = nullptr;
   size_t verdict_cap = 0;
+  uint32_t* sched = nullptr;  // slot-kernel tile counters (zeroed once; each launch leaves them zero)
   int32_t* pols = nullptr;
   size_t pols_cap = 0;
   size_t last_verdicts = 0;
@@ -102,6 +103,7 @@ struct DeviceBatch {
     (void)hipFree(cols);
     for (auto* m : masks) (void)hipFree(m);
     (void)hipFree(verdicts);
+    (void)hipFree(sched);
     (void)hipFree(pols);
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
@@ -390,6 +392,7 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
 
   // ---- evaluation arguments
   EvalArgs& A = plan->args;
+  A.sched = nullptr;  // run_pass sets the slot kernel's tile counters
   A.blob = (const uint8_t*)E.d_blob;
   A.nrows = B.n;
   A.npairs = npairs;
@@ -515,6 +518,8 @@ int plan_pass(const kw_env* env, kw_batch* kb, const Needs& need, uint64_t npair
       off = align(off + rows);
       T.o_sa = off;
       off = align(off + NMASK * 4);
+      T.o_nx = off;
+      off = align(off + 8);
       T.o_gstk = 0;
       if (groups) {
         T.o_gstk = off;
@@ -795,6 +800,13 @@ int run_pass(const kw_env* env, kw_batch* kb, const PassPlan& plan, bool timed) 
     if (int rc = upload_tile_descs(kb->b, &D, plan.tile)) return rc;
     EvalArgs sa = plan.args;
     sa.ndesc = D.ndesc;
+    // dynamic tile schedule (per-XCD counters); KW_SCHED=static selects the strided schedule (A/B)
+    static const bool dyn = !(getenv("KW_SCHED") && std::string(getenv("KW_SCHED")) == "static");
+    if (dyn && !D.sched) {
+      HIPCHK(hipMalloc((void**)&D.sched, 512 * sizeof(uint32_t)));
+      HIPCHK(hipMemsetAsync(D.sched, 0, 512 * sizeof(uint32_t), D.stream));
+    }
+    sa.sched = dyn ? D.sched : nullptr;
     for (size_t k = 0; k < tiles.size(); ++k)
       HIPCHK(launch_evaluate_slots(sa, tiles[k], D.d_tiles + k, D.desc, plan.fused, plan.grid, D.stream));
     if (!tiles.empty()) HIPCHK(launch_overflow(sa, D.d_tiles, D.overflow, D.n_overflow, D.stream));

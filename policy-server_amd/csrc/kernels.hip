@@ -667,7 +667,36 @@ __global__ void __launch_bounds__(kSlotThreads)
   uint8_t* own_l = lds + t.o_own_l;
 
   const uint32_t npol = a.npol;
-  for (uint64_t tile = blockIdx.x; tile < a.ndesc; tile += gridDim.x) {
+  // Tile schedule. Static: tiles strided by the grid. Dynamic (a.sched): workgroup b runs on XCD
+  // b % 8 and takes the tiles of that XCD's contiguous range one at a time from the XCD's own
+  // counter (a 128-B line each, so no counter is shared between XCDs); the atomic for the next tile
+  // is issued when the current tile starts and its result is read only at the tile's end, so its
+  // latency hides behind the tile. The XCD's last workgroup to finish zeroes the counter again.
+  const bool dyn = a.sched != nullptr;
+  const uint32_t nx = min(8u, gridDim.x);
+  const uint32_t xcd = blockIdx.x % nx;
+  const uint64_t t_lo = dyn ? a.ndesc * xcd / nx : 0ull, t_hi = dyn ? a.ndesc * (xcd + 1) / nx : a.ndesc;
+  uint32_t* cnt = dyn ? a.sched + xcd * 32u : nullptr;
+  uint32_t* l_nx = (uint32_t*)(lds + t.o_nx);
+  uint64_t tile = blockIdx.x;
+  if (dyn) {
+    if (tid == 0) l_nx[0] = atomicAdd(cnt, 1u);
+    __syncthreads();
+    tile = t_lo + l_nx[0];
+  }
+  uint32_t nxt = 0, it = 1;
+  // next tile: the strided one, or the counter value thread 0 fetched (double-buffered in LDS: a
+  // slot is rewritten only two barriers after every thread read it)
+  auto advance = [&]() -> uint64_t {
+    if (!dyn) return tile + gridDim.x;
+    if (tid == 0) l_nx[it & 1u] = nxt;
+    __syncthreads();  // also: the next tile restages LDS (its strings alias this tile's violation words)
+    const uint64_t nt = t_lo + l_nx[it & 1u];
+    ++it;
+    return nt;
+  };
+  for (; tile < t_hi; tile = advance()) {
+    if (dyn && tid == 0) nxt = atomicAdd(cnt, 1u);
     const TileDesc& d = desc[tile];
     if (!d.fits) continue;  // queued for the overflow kernels by the host (uniform: no barrier skipped unevenly)
     const uint64_t r0 = ((uint64_t)d.r0hi << 32) | d.r0lo;
@@ -1008,7 +1037,16 @@ __global__ void __launch_bounds__(kSlotThreads)
         }
       }
     }
-    __syncthreads();  // the next tile restages LDS (its strings alias this tile's violation words)
+    if (!dyn) __syncthreads();  // the next tile restages LDS (its strings alias this tile's violation words)
+  }
+  if (dyn && tid == 0) {  // the XCD's last workgroup (every other one has taken its last tile) resets
+    uint32_t* done = a.sched + 256u + xcd * 32u;
+    const uint32_t nwg = (gridDim.x - xcd + nx - 1u) / nx;  // workgroups b < gridDim.x with b % nx == xcd
+    __threadfence();  // this workgroup's last counter fetch is ordered before its done count
+    if (atomicAdd(done, 1u) == nwg - 1u) {
+      atomicExch(cnt, 0u);
+      atomicExch(done, 0u);
+    }
   }
 }
 

@@ -50,6 +50,7 @@ struct EvalArgs {
   const uint32_t* capdrop_off;
   const uint64_t* m[NMASK];   // nullptr = column carries no patterns (all-zero masks)
   uint32_t* out;
+  uint32_t* sched;  // slot kernel: per-XCD tile counters (256 u32 + 256 u32 done counts), nullptr = static
 };
 
 // Slot kernel geometry: one tile = 64 requests (one lane per request in the walk), 256 threads.
@@ -69,6 +70,7 @@ struct TileArgs {
   uint32_t o_vadd, o_vl, o_vc;    // u64 violation sets: per added capability, per label (V_l), per container (V_c)
   uint32_t o_own_c, o_own_l;      // u8 tile-local request of each staged container / label
   uint32_t o_rej, o_mut, o_byp;   // per-request walk results: rejected / mutated slots, bypass flag
+  uint32_t o_nx;                  // u32[2]: next tile index (dynamic schedule), double-buffered
   uint32_t o_sa;                  // u32[NMASK]: the tile's staged byte start per string column (TileDesc.sa)
   uint32_t o_vw, vw_stride;       // violation words [rows][vw_stride] (aliases the staged strings)
   uint32_t o_slot, slot_bytes;    // staged SlotHdr record of this chunk

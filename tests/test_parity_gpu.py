@@ -204,3 +204,20 @@ def test_shared_slots_match_oracle(origin):
     gpu = b.verdicts()
     ora = oe.eval(syn.soa(), ids, origin)
     assert np.array_equal(gpu, ora), diff_verdicts(gpu, ora, len(ids), ids)
+
+
+def test_repeated_passes_on_one_batch():
+    """The dynamic tile schedule's per-XCD counters are zeroed by each launch's last workgroups:
+    back-to-back passes over one resident batch (other policy lists and origins in between) all
+    cover every tile."""
+    env, oe = _envs("c4_64")
+    ids = env.policy_ids()
+    syn = K.SynthBatch(4, 30000, seed=99)
+    b = syn.batch().to_device(0)
+    soa = syn.soa()
+    for k, (cols, origin) in enumerate([(ids, K.VALIDATE), (ids[:20], K.AUDIT), (ids, K.VALIDATE),
+                                        (ids[::-1], K.AUDIT), (ids, K.VALIDATE)]):
+        b.validate(env, cols, origin)
+        gpu = b.verdicts()
+        ora = oe.eval(soa, cols, origin)
+        assert np.array_equal(gpu, ora), f"pass {k}: " + diff_verdicts(gpu, ora, len(cols), cols)
