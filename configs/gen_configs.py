@@ -8,6 +8,10 @@
   c4_64.yml          C4: 64 policies = 22 psp-capabilities (validate-only settings, a third with
                      required_drop so the mutation-refused path is live) + 21 psp-apparmor + 21 safe-labels
   c5_mixed.yml       C5: the C4 policy set (served on the mixed Pod/Deployment/Namespace stream)
+  c6_256.yml         256 policies past every per-column pattern count of a 64-bit design: 64 trusted-repos
+                     over 240 registries (literals and globs) and 230 image globs, 64 psp-capabilities,
+                     48 psp-apparmor over 101 profiles, 40 safe-labels over 150 label keys, 24
+                     namespace-validate, 15 pod-privileged and a 40-member group (synth config 6)
   parity.yml         every family, monitor mode, allowedToMutate, groups (incl. an i64 expression),
                      an unsupported module and invalid settings (load with continue_on_errors)
 Deterministic (seeded); run `python configs/gen_configs.py` to regenerate.
@@ -59,6 +63,57 @@ def c4_policies(rng):
     return pols
 
 
+REG6 = [f"reg-{i:03d}.example.com" for i in range(240)]
+IMG6 = [f"reg-{i:03d}.example.com/team-{i % 40:02d}/*" for i in range(230)]
+PROF6 = ["runtime/default"] + [f"localhost/prof-{i:02d}" for i in range(100)]
+KEYS6 = [f"team.example/k-{i:03d}" for i in range(150)]
+
+
+def c6_policies(rng):
+    pols = {}
+    for i in range(64):
+        s = {"registries": {"allow": sorted(rng.sample(REG6, rng.randint(8, 24))) + (["*.corp.example", "reg-1?0.example.com"]
+                                                                                   if i % 8 == 0 else [])},
+             "tags": {"reject": ["latest"] if i % 2 else ["latest", "*-rc*"]}}
+        if i % 4 == 0:
+            s["images"] = {"allow": sorted(rng.sample(IMG6, 16))}
+        elif i % 4 == 1:
+            s["images"] = {"reject": sorted(rng.sample(IMG6, 16))}
+        pols[f"trusted-repos-{i:02d}"] = {"module": MOD["trusted"], "settings": s}
+    for i in range(64):
+        s = {"allowed_capabilities": sorted(rng.sample(CAPS, rng.randint(3, 10)))}
+        if i % 3 == 0:
+            s["required_drop_capabilities"] = ["KILL"]
+        pols[f"psp-capabilities-{i:02d}"] = {"module": MOD["caps"], "settings": s}
+    for i in range(48):
+        pols[f"psp-apparmor-{i:02d}"] = {"module": MOD["aa"],
+                                         "settings": {"allowed_profiles": sorted(rng.sample(PROF6, rng.randint(4, 30)))}}
+    for i in range(40):
+        keys = rng.sample(KEYS6 + KEYS, 8)
+        s = {"denied_labels": keys[:rng.randint(1, 3)]}
+        mand = keys[3:3 + rng.randint(0, 2)]
+        if mand:
+            s["mandatory_labels"] = mand
+        s["constrained_labels"] = {k: rng.choice(REGEXES) for k in keys[5:5 + rng.randint(1, 3)]}
+        pols[f"safe-labels-{i:02d}"] = {"module": MOD["labels"], "settings": s}
+    for i in range(24):
+        pols[f"namespace-{i:02d}"] = {"module": MOD["ns"], "settings": {"valid_namespace": f"ns-{i:03d}"}}
+    for i in range(15):
+        pols[f"pod-privileged-{i:02d}"] = {"module": MOD["priv"], "settings": {"skip_init_containers": i % 2 == 1}}
+    members = {}
+    for m in range(40):
+        if m % 2 == 0:
+            members[f"m{m:02d}"] = {"module": MOD["trusted"], "settings": {"registries": {"allow": sorted(rng.sample(REG6, 40))}}}
+        elif m % 4 == 1:
+            members[f"m{m:02d}"] = {"module": MOD["labels"], "settings": {"mandatory_labels": [rng.choice(KEYS)]}}
+        else:
+            members[f"m{m:02d}"] = {"module": MOD["aa"], "settings": {"allowed_profiles": sorted(rng.sample(PROF6, 20))}}
+    clauses = [f"(m{m:02d}() && m{m + 1:02d}())" for m in range(0, 40, 2)]
+    pols["group-40"] = {"policies": members, "expression": " || ".join(clauses),
+                        "message": "none of the 40-member clauses accepted the request"}
+    return pols
+
+
 def main():
     rng = random.Random(4)
     docs = {
@@ -76,6 +131,7 @@ def main():
         "c4_64.yml": c4_policies(rng),
     }
     docs["c5_mixed.yml"] = docs["c4_64.yml"]
+    docs["c6_256.yml"] = c6_policies(random.Random(6))
     prng = random.Random(0)
     parity = {
         "pod-privileged": {"module": MOD["priv"]},

@@ -113,7 +113,10 @@ typedef struct kw_soa {
  *   bit 6      F_PATCH     the final response carries the vanilla patch (Audit, or Protect with
  *                          allowedToMutate)
  *   bits 8-15  REASON      kw_reason (0 = no violation)
- *   bits 16-31 ARG         reason argument (entity index / packed indices / group cause mask)
+ *   bits 16-31 ARG         reason argument: an entity index within the request, a settings index,
+ *                          or a group's cause mask; KW_ARG_WIDE (0xffff) when the full value does
+ *                          not fit (an index >= 65535, the causes of a group with more than 15
+ *                          members): kw_batch_wide_arg returns it after kw_batch_verdicts
  * ------------------------------------------------------------------------------------------- */
 #define KW_V_ALLOWED 0x1u
 #define KW_V_MUTATED 0x2u
@@ -124,6 +127,7 @@ typedef struct kw_soa {
 #define KW_F_PATCH 0x40u
 #define KW_REASON(v) (((v) >> 8) & 0xffu)
 #define KW_ARG(v) ((v) >> 16)
+#define KW_ARG_WIDE 0xffffu
 enum { KW_FST_NONE = 0, KW_FST_VANILLA = 1, KW_FST_MUTATION_REFUSED = 2, KW_FST_INIT_ERROR = 3 };
 
 /* reason codes (message templates: DESIGN.md §Policy families) */
@@ -136,10 +140,11 @@ enum {
   KW_R_TAG_REJECTED = 5,
   KW_R_IMG_NOT_ALLOWED = 6,
   KW_R_IMG_REJECTED = 7,
-  KW_R_CAP_NOT_ALLOWED = 8,   /* arg: container index << 8 | capability index within add list */
+  KW_R_CAP_NOT_ALLOWED = 8,   /* arg: index in the request's capabilities.add lists, flattened in
+                                 container order (the container is the one whose list holds it) */
   KW_R_APPARMOR = 9,          /* arg: container index */
   KW_R_LABEL_DENIED = 10,     /* arg: label index */
-  KW_R_LABEL_CONSTRAINT = 11, /* arg: label index << 8 | constraint index in settings order */
+  KW_R_LABEL_CONSTRAINT = 11, /* arg: label index (the constraint is the policy's on that key) */
   KW_R_LABEL_MANDATORY = 12,  /* arg: index of the missing key in settings order */
   KW_R_GROUP = 13,            /* arg: cause mask over group members (settings order) */
   KW_R_GROUP_EXPR = 14,       /* group expression does not evaluate to a bool: reject 500 */
@@ -189,12 +194,15 @@ int kw_env_validate_settings(const kw_env *env, int32_t idx, char *buf, size_t c
 /* Diagnostic: does `s` match pattern `pat` (kind 0 literal, 1 glob, 2 regex) under the engine's
  * compiled-automaton semantics? 1/0, or -1 on a pattern syntax error. */
 int kw_pattern_match(int kind, const char *pat, const char *s, size_t len);
-/* Diagnostic: classify `s` for request column `col` (kwdev.hpp Col) through the column's DFA chain
- * (*dfa_mask) and through the fused kernel's fast table (*fast_mask): the literal perfect-hash
- * table, or for COL_LV the per-key value DFA of label key `key` (then *dfa_mask is restricted to
- * the value patterns constrained on that key). Returns 1 if a fast table exists, 0 if not. */
-int kw_env_classify_check(const kw_env *env, int col, const char *key, size_t klen, const char *s,
-                          size_t len, uint64_t *dfa_mask, uint64_t *fast_mask);
+/* Diagnostics over the compiled classifiers (tests): the distinct patterns of request column `col`
+ * (kwdev.hpp Col; kind 0 literal, 1 glob, 2 regex), and the ids of the patterns string `s` matches
+ * through the blob's tables (the tables the kernels run). For COL_LV, `key` is the label key and
+ * the result is restricted to the regexes constrained on it. kw_env_classify returns the number of
+ * matched ids (writing at most `cap`), or -1. */
+int kw_env_pattern_count(const kw_env *env, int col);
+int kw_env_pattern(const kw_env *env, int col, int idx, int *kind, char *buf, size_t cap);
+int kw_env_classify(const kw_env *env, int col, const char *key, size_t klen, const char *s, size_t len,
+                    uint32_t *pats, int cap);
 
 /* ---------------------------------------------------------------------------------------------
  * Request batches: the micro-batch handed over by the HTTP front (replaces the one
@@ -226,8 +234,10 @@ int kw_debug_host_walk(const kw_env *env, const kw_batch *b, const int32_t *poli
 /* ---------------------------------------------------------------------------------------------
  * The hot path: EvaluationEnvironment::validate + service::evaluate constraints, batched.
  * Evaluates every row against each of the npol policies (indices from kw_env_lookup) on the GPU;
- * verdict words are laid out row-major [row][npol]. Runs asynchronously on `stream` into the
- * batch's device verdict buffer; kw_batch_verdicts copies them to the host (synchronising).
+ * verdict words are laid out row-major [row][npol]. Runs asynchronously on `stream` (a
+ * hipStream_t of the batch's device; NULL = the batch's own stream) into the batch's device
+ * verdict buffer; kw_batch_verdicts copies them to the host, synchronising with that stream. A pass
+ * on another stream than the batch's previous pass first waits for the previous one.
  * ------------------------------------------------------------------------------------------- */
 int kw_validate_batch(const kw_env *env, kw_batch *b, const int32_t *policies, uint32_t npol,
                       int origin, void *stream);
@@ -236,13 +246,16 @@ int kw_validate_batch(const kw_env *env, kw_batch *b, const int32_t *policies, u
 int kw_validate_rows(const kw_env *env, kw_batch *b, const int32_t *row_policy, int origin,
                      void *stream);
 int kw_batch_verdicts(kw_batch *b, uint32_t *host_out, size_t count);
+/* The full argument of a verdict word whose ARG is KW_ARG_WIDE, for (row, policy) of the last pass
+ * whose verdicts were copied (kw_batch_verdicts). KW_E_NOT_FOUND when the pass recorded none. */
+int kw_batch_wide_arg(const kw_batch *b, uint64_t row, int32_t policy, uint64_t *value);
 
 typedef struct kw_timing {
-  double classify_ms;   /* avg device time of the string-classification kernel (HIP events) */
-  double evaluate_ms;   /* avg device time of the policy-evaluation kernel */
+  double classify_ms;   /* 0: classification is fused into the evaluation kernel */
+  double evaluate_ms;   /* avg device time of one whole validate pass (every launch of it) */
   double total_ms;      /* avg device time of one whole validate pass */
-  double classify_bytes;/* algorithmic bytes per classify launch */
-  double evaluate_bytes;/* algorithmic bytes per evaluate launch */
+  double classify_bytes;/* 0 */
+  double evaluate_bytes;/* algorithmic bytes per pass */
 } kw_timing;
 /* Time `reps` back-to-back validate passes with HIP events on the launch stream. */
 int kw_validate_timed(const kw_env *env, kw_batch *b, const int32_t *policies, uint32_t npol,

@@ -193,12 +193,13 @@ int orc_image_parts(const char *s, char *registry, char *tag, char *norm, int ca
 }
 
 /* ------------------------------------------------------------------ families */
-/* reason arguments saturate: one index to 16 bits, a pair of indices to 8 bits each */
-static uint32_t pack1(uint32_t a) { return a < 65535u ? a : 65535u; }
-static uint32_t pack2(uint32_t a, uint32_t b) { return ((a < 255u ? a : 255u) << 8) | (b < 255u ? b : 255u); }
-
+/* Full arguments: an entity index within the request (containers; capabilities.add entries
+   flattened in container order; labels) or a settings index. The verdict word carries them in 16
+   bits, KW_ARG_WIDE when they do not fit (include/kwgpu.h). */
 typedef struct {
-  uint32_t reason, arg, mutated;
+  uint32_t reason;
+  uint64_t arg;
+  uint32_t mutated;
 } fam_out;
 
 static int ctr_considered(const orc_policy *P, uint8_t f) {
@@ -214,7 +215,7 @@ static fam_out fam_privileged(const orc_policy *P, const kw_soa *S, uint64_t r) 
     uint8_t f = S->ctr_flags[c];
     if (ctr_considered(P, f) && (f & KW_CTR_PRIVILEGED)) {
       o.reason = KW_R_PRIVILEGED;
-      o.arg = pack1(c - S->ctr_off[r]);
+      o.arg = c - S->ctr_off[r];
       return o;
     }
   }
@@ -259,7 +260,7 @@ static fam_out fam_trusted(const orc_policy *P, const kw_soa *S, uint64_t r, zbu
     free(heap);
     if (why) {
       o.reason = why;
-      o.arg = pack1(c - S->ctr_off[r]);
+      o.arg = c - S->ctr_off[r];
       return o;
     }
   }
@@ -278,7 +279,7 @@ static fam_out fam_caps(const orc_policy *P, const kw_soa *S, uint64_t r) {
       sv cap = col(&S->cap_add, k);
       if (!any_eq(P->l[0], P->n[0], cap) && !any_eq(P->l[2], P->n[2], cap)) {
         o.reason = KW_R_CAP_NOT_ALLOWED;
-        o.arg = pack2(c - S->ctr_off[r], k - S->capadd_off[c]);
+        o.arg = k - S->capadd_off[S->ctr_off[r]];
         return o;
       }
     }
@@ -314,7 +315,7 @@ static fam_out fam_apparmor(const orc_policy *P, const kw_soa *S, uint64_t r) {
     if (!(S->ctr_flags[c] & KW_CTR_HAS_APPARMOR)) continue;
     if (!any_eq(P->l[0], P->n[0], col(&S->ctr_apparmor, c))) {
       o.reason = KW_R_APPARMOR;
-      o.arg = pack1(c - S->ctr_off[r]);
+      o.arg = c - S->ctr_off[r];
       return o;
     }
   }
@@ -328,14 +329,14 @@ static fam_out fam_labels(const orc_env *e, int32_t p, const kw_soa *S, uint64_t
     sv key = col(&S->lbl_key, l);
     if (any_eq(P->l[0], P->n[0], key)) {
       o.reason = KW_R_LABEL_DENIED;
-      o.arg = pack1(l - S->lbl_off[r]);
+      o.arg = l - S->lbl_off[r];
       return o;
     }
     for (int32_t i = 0; i < P->n[2]; ++i) {
       if (!sv_eq(key, P->l[2][i])) continue;
       if (regexec(&e->re[p][i], z(zb, col(&S->lbl_val, l)), 0, NULL, 0) != 0) {
         o.reason = KW_R_LABEL_CONSTRAINT;
-        o.arg = pack2(l - S->lbl_off[r], (uint32_t)i);
+        o.arg = l - S->lbl_off[r];
         return o;
       }
     }
@@ -374,20 +375,18 @@ typedef struct {
   const kw_soa *S;
   uint64_t r;
   zbuf *zb;
-  uint32_t done, ok, causes;
+  uint8_t done[ORC_MAX_MEMBERS], ok[ORC_MAX_MEMBERS];
 } gctx;
 
 /* member "returns true" iff allowed and not mutated (a patch inside a group is refused,
    integration_test.rs:247-250); evaluation is lazy, as rhai evaluates || and && */
 static int gcall(gctx *g, int32_t slot) {
-  if (!((g->done >> slot) & 1)) {
+  if (!g->done[slot]) {
     fam_out fo = eval_family(g->e, g->G->members[slot], g->S, g->r, g->zb);
-    int ok = fo.reason == 0 && !fo.mutated;
-    g->done |= 1u << slot;
-    if (ok) g->ok |= 1u << slot;
-    else g->causes |= 1u << slot;
+    g->done[slot] = 1;
+    g->ok[slot] = fo.reason == 0 && !fo.mutated;
   }
-  return (g->ok >> slot) & 1;
+  return g->ok[slot];
 }
 static int geval(gctx *g, int32_t n) {
   const orc_xnode *x = &g->G->nodes[n];
@@ -404,38 +403,61 @@ static int geval(gctx *g, int32_t n) {
 }
 
 /* ------------------------------------------------------------------ service::evaluate */
-static uint32_t verdict(const orc_env *e, int32_t p, const kw_soa *S, uint64_t r, int32_t origin,
-                        zbuf *zb) {
+static void detail(const orc_env *e, int32_t p, const kw_soa *S, uint64_t r, int32_t origin, zbuf *zb, orc_detail *d) {
   const orc_policy *P = &e->pol[p];
+  d->reason = 0;
+  d->arg = 0;
+  d->mutated = 0;
+  d->bypass = 0;
+  d->ncauses = 0;
   /* namespace bypass first (service.rs:40-71): AdmissionRequest only */
   if (e->always_ns && !(S->req_flags[r] & KW_REQ_RAW) && (S->req_flags[r] & KW_REQ_HAS_NAMESPACE) &&
-      sv_eq(col(&S->ns, r), e->always_ns))
-    return KW_V_ALLOWED | KW_F_ALLOWED | KW_BYPASS;
+      sv_eq(col(&S->ns, r), e->always_ns)) {
+    d->bypass = 1;
+    d->word = KW_V_ALLOWED | KW_F_ALLOWED | KW_BYPASS;
+    return;
+  }
   /* PolicyInitialization -> reject(uid, msg, 500), before any constraint (service.rs:78-91) */
-  if (P->init_error)
-    return ((uint32_t)KW_FST_INIT_ERROR << KW_F_STATUS_SHIFT) | ((uint32_t)KW_R_INIT_ERROR << 8);
-  uint32_t reason = 0, arg = 0, mutated = 0;
+  if (P->init_error) {
+    d->reason = KW_R_INIT_ERROR;
+    d->word = ((uint32_t)KW_FST_INIT_ERROR << KW_F_STATUS_SHIFT) | ((uint32_t)KW_R_INIT_ERROR << 8);
+    return;
+  }
+  uint32_t arg16 = 0;
   if (P->family == ORC_F_GROUP) {
     if (P->expr_error) {
-      reason = KW_R_GROUP_EXPR;
+      d->reason = KW_R_GROUP_EXPR;
     } else {
-      gctx g = {e, P, S, r, zb, 0, 0, 0};
-      int res = geval(&g, P->n_nodes - 1);
-      if (!res) {
-        reason = KW_R_GROUP;
-        arg = g.causes;
+      gctx g;
+      g.e = e;
+      g.G = P;
+      g.S = S;
+      g.r = r;
+      g.zb = zb;
+      memset(g.done, 0, sizeof(g.done));
+      memset(g.ok, 0, sizeof(g.ok));
+      if (!geval(&g, P->n_nodes - 1)) {
+        d->reason = KW_R_GROUP;
+        for (int32_t s = 0; s < P->n_members && s < ORC_MAX_MEMBERS; ++s)
+          if (g.done[s] && !g.ok[s]) {
+            d->causes[d->ncauses++] = s;
+            if (s < 64) d->arg |= 1ull << s;
+          }
+        /* more than 15 members: the cause mask lives in the pass's side data */
+        arg16 = P->n_members > 15 ? 0xffffu : (uint32_t)d->arg;
       }
     }
   } else {
     fam_out fo = eval_family(e, p, S, r, zb);
-    reason = fo.reason;
-    arg = fo.arg;
-    mutated = fo.mutated;
+    d->reason = fo.reason;
+    d->arg = fo.arg;
+    d->mutated = fo.mutated;
+    arg16 = fo.arg < 0xffffu ? (uint32_t)fo.arg : 0xffffu;
   }
-  uint32_t v = (reason << 8) | ((arg & 0xffffu) << 16);
-  int allowed = reason == 0;
+  uint32_t v = (d->reason << 8) | (arg16 << 16);
+  int allowed = d->reason == 0;
   if (allowed) v |= KW_V_ALLOWED;
-  if (mutated) v |= KW_V_MUTATED;
+  if (d->mutated) v |= KW_V_MUTATED;
   /* validation_response_with_constraints (service.rs:160-208) for the Validate origin only */
   uint32_t fst = allowed ? KW_FST_NONE : KW_FST_VANILLA;
   int fallowed = allowed;
@@ -443,15 +465,28 @@ static uint32_t verdict(const orc_env *e, int32_t p, const kw_soa *S, uint64_t r
     if (P->mode == KW_MODE_MONITOR) {
       fallowed = 1;
       fst = KW_FST_NONE;
-    } else if (mutated && !P->allowed_to_mutate) {
+    } else if (d->mutated && !P->allowed_to_mutate) {
       fallowed = 0;
       fst = KW_FST_MUTATION_REFUSED;
     }
   }
   if (fallowed) v |= KW_F_ALLOWED;
-  if (mutated && fst == KW_FST_NONE && (origin == KW_ORIGIN_AUDIT || P->mode == KW_MODE_PROTECT)) v |= KW_F_PATCH;
+  if (d->mutated && fst == KW_FST_NONE && (origin == KW_ORIGIN_AUDIT || P->mode == KW_MODE_PROTECT)) v |= KW_F_PATCH;
   v |= fst << KW_F_STATUS_SHIFT;
-  return v;
+  d->word = v;
+}
+
+static uint32_t verdict(const orc_env *e, int32_t p, const kw_soa *S, uint64_t r, int32_t origin, zbuf *zb) {
+  orc_detail d;
+  detail(e, p, S, r, origin, zb, &d);
+  return d.word;
+}
+
+void orc_eval_detail(const orc_env *e, const kw_soa *S, int32_t policy, int32_t origin, uint64_t row, orc_detail *out) {
+  zbuf zb;
+  zb.big = NULL;
+  detail(e, policy, S, row, origin, &zb, out);
+  free(zb.big);
 }
 
 void orc_eval(const orc_env *e, const kw_soa *S, const int32_t *pols, int32_t npol, int32_t origin,

@@ -84,6 +84,22 @@ void orc_eval(const orc_env *e, const kw_soa *soa, const int32_t *policies, int3
 void orc_eval_mt(const orc_env *e, const kw_soa *soa, const int32_t *policies, int32_t npol,
                  int32_t origin, uint64_t nrows, int threads, uint32_t *out);
 
+/* What one (row, policy) evaluation found, before any encoding into a verdict word: the response
+   is derived from this and the document, never from the product's word (oracle.py response_doc).
+   arg: the FULL argument (entity index within the request, settings index); causes: the group
+   members rhai would have called that rejected, ascending member slots. */
+#define ORC_MAX_MEMBERS 256
+typedef struct orc_detail {
+  uint32_t word;      /* the verdict word (kwgpu.h layout, ARG saturated to KW_ARG_WIDE) */
+  uint32_t reason;    /* KW_R_* of the vanilla response, 0 = accepted */
+  uint64_t arg;       /* full argument of `reason` */
+  uint32_t mutated;   /* the vanilla response carries a patch */
+  uint32_t bypass;    /* namespace bypass (service.rs:40-71) */
+  int32_t ncauses;
+  int32_t causes[ORC_MAX_MEMBERS];
+} orc_detail;
+void orc_eval_detail(const orc_env *e, const kw_soa *soa, int32_t policy, int32_t origin, uint64_t row, orc_detail *out);
+
 /* 1 if POSIX regcomp(REG_EXTENDED) accepts the pattern. */
 int orc_regex_ok(const char *pattern);
 

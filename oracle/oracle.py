@@ -373,9 +373,19 @@ def compile_settings(fam, s, olib):
         for k in L[0]:
             if k in L[1] or k in L[2]:
                 raise ValueError(f"label '{k}' cannot be both denied and mandatory or constrained")
-        if len(L[1]) > 16 or len(L[2]) > 16:
-            raise ValueError("at most 16 mandatory and 16 constrained labels are supported")
     return L, flags
+
+
+def engine_limit_error(pid, fam, L):
+    """The product's per-policy limits of its bit-parallel evaluation (not reference
+    behaviour: a bootstrap failure of that policy): 64 distinct mandatory labels, 63 distinct
+    required-drop / default-add capabilities (+ "ALL")."""
+    if fam == F_LABELS and len(set(L[1])) > 64:
+        return f"bootstrap failure: {pid}: more than 64 distinct mandatory_labels (engine limit)"
+    if fam == F_CAPS and len(set(L[1]) | set(L[2]) | {"ALL"}) > 64:
+        return (f"bootstrap failure: {pid}: more than 63 distinct required-drop / default-add capabilities "
+                f"(engine limit)")
+    return None
 
 
 # ----------------------------------------------------------------------------- group expressions
@@ -526,11 +536,14 @@ def parse_expression(s, members):
 
 
 def expr_depth(n, d=1):
-    """Max stack depth of the left-then-right postfix emission (same bound as the product)."""
+    """Max value-stack depth of the short-circuit jump code (same bound as the product: || and &&
+    pop their left side before the right one runs; == and != keep it)."""
     if n[0] in ("const", "call"):
         return d
     if n[0] == "not":
         return expr_depth(n[1], d)
+    if n[0] in ("and", "or"):
+        return max(expr_depth(n[1], d), expr_depth(n[2], d))
     return max(expr_depth(n[1], d), expr_depth(n[2], d + 1))
 
 
@@ -609,6 +622,11 @@ class _OPolicy(C.Structure):
                 ("members", C.POINTER(C.c_int32)), ("n_nodes", C.c_int32), ("nodes", C.POINTER(_XNode))]
 
 
+class _ODetail(C.Structure):
+    _fields_ = [("word", C.c_uint32), ("reason", C.c_uint32), ("arg", C.c_uint64), ("mutated", C.c_uint32),
+                ("bypass", C.c_uint32), ("ncauses", C.c_int32), ("causes", C.c_int32 * 256)]
+
+
 _olib = None
 
 
@@ -625,6 +643,8 @@ def olib():
                                   C.c_int, C.POINTER(C.c_uint32)]
         L.orc_image_parts.restype = C.c_int
         L.orc_image_parts.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_int]
+        L.orc_eval_detail.restype = None
+        L.orc_eval_detail.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_uint64, C.POINTER(_ODetail)]
         L.orc_regex_ok.restype = C.c_int
         L.orc_regex_ok.argtypes = [C.c_char_p]
         _olib = L
@@ -685,6 +705,7 @@ class OracleEnv:
                 p["family"] = fam
                 try:
                     p["lists"], p["flags"] = compile_settings(fam, p["settings"], L)
+                    err = engine_limit_error(p["id"], fam, p["lists"])
                 except ValueError as ex:
                     err = f"Policy settings are invalid: {ex}"
             if err is not None:
@@ -701,15 +722,15 @@ class OracleEnv:
             p["expr_error"] = None
             p["ast"] = None
             try:
-                if len(p["member_names"]) > 16:
-                    raise ExprError("policy groups with more than 16 members are not supported by the engine")
+                if len(p["member_names"]) > 64:
+                    raise ExprError("policy groups with more than 64 members are not supported by the engine")
                 ast = parse_expression(p["expression"], p["member_names"])
                 if ast[0] == "const" and ast[1] == "i64":
                     p["expr_error"] = ("policy group expression did not evaluate to a boolean: Output type "
                                        "incorrect: i64 (expecting bool)")
                     p["valid"] = True
-                elif expr_depth(ast) > 16:
-                    raise ExprError("policy group expression nests too deeply for the engine (max stack 16)")
+                elif expr_depth(ast) > 64:
+                    raise ExprError("policy group expression nests too deeply for the engine (max stack 64)")
                 else:
                     p["ast"] = ast
                     p["valid"] = True
@@ -804,19 +825,22 @@ class OracleEnv:
                     R_TAG_REJECTED: f"{head}: tag {q(tag)} is rejected",
                     R_IMG_NOT_ALLOWED: f"{head}, which is not in the allowed images",
                     R_IMG_REJECTED: f"{head}, which is rejected"}[reason]
-        if reason == R_CAP:
-            c, k = arg >> 8, arg & 0xFF
-            cap = s("cap_add", soa.capadd_off[cb + c] + k)
-            return f"container {q(s('ctr_name', cb + c))} adds capability {q(cap)}, which is not allowed"
+        if reason == R_CAP:  # arg: index in the request's add lists, flattened in container order
+            k = soa.capadd_off[cb] + arg
+            c = cb
+            while soa.capadd_off[c + 1] <= k:
+                c += 1
+            return f"container {q(s('ctr_name', c))} adds capability {q(s('cap_add', k))}, which is not allowed"
         if reason == R_APPARMOR:
             return (f"container {q(s('ctr_name', cb + arg))} uses AppArmor profile "
                     f"{q(s('ctr_apparmor', cb + arg))}, which is not allowed")
         if reason == R_LABEL_DENIED:
             return f"label {q(s('lbl_key', lb + arg))} is denied"
-        if reason == R_LABEL_CONSTRAINT:
-            l, i = arg >> 8, arg & 0xFF
-            return (f"label {q(s('lbl_key', lb + l))} value {q(s('lbl_val', lb + l))} does not match the "
-                    f"constraint {q(P['lists'][3][i])}")
+        if reason == R_LABEL_CONSTRAINT:  # arg: label index; the constraint is the policy's on its key
+            key = s("lbl_key", lb + arg)
+            regex = P["lists"][3][P["lists"][2].index(key)]
+            return (f"label {q(key)} value {q(s('lbl_val', lb + arg))} does not match the "
+                    f"constraint {q(regex)}")
         if reason == R_LABEL_MANDATORY:
             return f"mandatory label {q(P['lists'][1][arg])} is missing"
         if reason == R_GROUP:
@@ -827,9 +851,63 @@ class OracleEnv:
             return P["init_error"]
         return ""
 
-    def response(self, soa, row, pidx, v, member_v=None, doc=None):
+    def detail(self, soa, row, pidx, origin=VALIDATE):
+        """The oracle's own evaluation of (row, policy): dict(word, reason, arg (full), mutated,
+        bypass, causes (member slots))."""
+        d = _ODetail()
+        olib().orc_eval_detail(self._h, C.byref(soa), pidx, origin, row, C.byref(d))
+        return {"word": d.word, "reason": d.reason, "arg": d.arg, "mutated": bool(d.mutated), "bypass": bool(d.bypass),
+                "causes": list(d.causes[:d.ncauses])}
+
+    def response_doc(self, soa, row, pidx, origin=VALIDATE, doc=None):
+        """AdmissionResponse dict of (row, policy) derived from the oracle's own evaluation of the
+        document (service.rs:30-152, 160-208) — independent of any verdict word: full entity
+        indices, the group's own short-circuit causes and each cause member's own evaluation.
+        Raises KeyError for PolicyNotFound outcomes."""
+        P = self.pol[pidx]
+        c = soa.uid
+        uid = bytes(c.bytes[c.off[row]:c.off[row + 1]]).decode()
+        d = self.detail(soa, row, pidx, origin)
+        if d["bypass"]:
+            if not P["registered"]:
+                raise KeyError(f"unknown policy: {P['id']}")
+            return {"uid": uid, "allowed": True}
+        if P["group"] and P["broken"]:
+            raise KeyError(f"unknown policy: {P['broken']}")
+        if P["init_error"]:
+            return {"uid": uid, "allowed": False, "status": {"message": P["init_error"], "code": 500}}
+        reason = d["reason"]
+        vanilla = {"uid": uid, "allowed": reason == 0}
+        if reason:
+            st = {"message": self.message(soa, row, pidx, reason, d["arg"])}
+            if reason == R_GROUP_EXPR:
+                st["code"] = 500
+            if reason == R_GROUP:
+                causes = []
+                for slot in d["causes"]:
+                    m = P["members"][slot]
+                    md = self.detail(soa, row, m, origin)
+                    if md["reason"] == 0 and md["mutated"]:
+                        msg = "mutation is not allowed inside of policy group"
+                    else:
+                        msg = self.message(soa, row, m, md["reason"], md["arg"])
+                    causes.append({"field": f"spec.policies.{self.pol[m]['name']}", "message": msg})
+                st["details"] = {"causes": causes}
+            vanilla["status"] = st
+        elif d["mutated"]:
+            if doc is None:
+                raise ValueError("the original document is required to restate a mutation")
+            ops = capabilities_patch(P["lists"][1], P["lists"][2], doc)
+            vanilla["patchType"] = "JSONPatch"
+            vanilla["patch"] = base64.b64encode(json.dumps(ops, separators=(",", ":"), ensure_ascii=False).encode()).decode()
+        if origin == VALIDATE:
+            return constraints(P["id"], P["mode"], P["a2m"], vanilla)
+        return vanilla
+
+    def response(self, soa, row, pidx, v, member_v=None, doc=None, wide=None):
         """AdmissionResponse dict the service returns for verdict word v (service.rs:30-152).
-        doc: the row's original JSON text, needed for an accepted mutation (the patch)."""
+        doc: the row's original JSON text, needed for an accepted mutation (the patch); wide(pidx):
+        the full argument of a word whose ARG is KW_ARG_WIDE."""
         P = self.pol[pidx]
         c = soa.uid
         uid = bytes(c.bytes[c.off[row]:c.off[row + 1]]).decode()
@@ -847,6 +925,8 @@ class OracleEnv:
             return {"uid": uid, "allowed": True, "patchType": "JSONPatch", "patch": patch}
         fst = (v >> 3) & 3
         reason, arg = (v >> 8) & 0xFF, v >> 16
+        if arg == 0xFFFF and wide is not None:
+            arg = wide(pidx)
         resp = {"uid": uid, "allowed": bool(v & 4)}
         if fst == 0:
             return resp
@@ -869,7 +949,10 @@ class OracleEnv:
                 if (mv & 2) and (mv & 1):
                     msg = "mutation is not allowed inside of policy group"
                 else:
-                    msg = self.message(soa, row, m, (mv >> 8) & 0xFF, mv >> 16)
+                    marg = mv >> 16
+                    if marg == 0xFFFF and wide is not None:
+                        marg = wide(m)
+                    msg = self.message(soa, row, m, (mv >> 8) & 0xFF, marg)
                 causes.append({"field": f"spec.policies.{self.pol[m]['name']}", "message": msg})
             st["details"] = {"causes": causes}
         resp["status"] = st

@@ -551,17 +551,13 @@ bool regex_ok(const std::string& re, std::string* err) {
   return true;
 }
 
-uint64_t Dfa::run(const uint8_t* s, size_t n) const {
+uint32_t Dfa::run(const uint8_t* s, size_t n) const {
   uint32_t st = start;
   for (size_t i = 0; i < n && st != 0; ++i) st = trans[(size_t)st * ncls + cls[s[i]]];
-  return accept[st];
+  return acc[st];
 }
 
-bool compile_dfa(const std::vector<Pattern>& pats, Dfa* out, std::string* err) {
-  if (pats.size() > kMaxPatternsPerColumn) {
-    *err = "more than 64 distinct patterns for one column";
-    return false;
-  }
+bool compile_dfa(const std::vector<Pattern>& pats, Dfa* out, std::string* err, uint32_t max_states) {
   Nfa nfa;
   uint32_t root = nfa.add();
   BSet any;
@@ -660,14 +656,25 @@ bool compile_dfa(const std::vector<Pattern>& pats, Dfa* out, std::string* err) {
   std::unordered_map<std::vector<uint32_t>, uint32_t, SetHash> ids;
   std::vector<std::vector<uint32_t>> dstates;
   std::vector<uint32_t> trans;
-  std::vector<uint64_t> acc;
+  std::vector<uint32_t> acc;  // accept class per DFA state
+  std::map<std::vector<uint32_t>, uint32_t> class_ids;
+  std::vector<std::vector<uint32_t>> classes;
+  class_ids[{}] = 0;
+  classes.push_back({});
   auto accept_of = [&](const std::vector<uint32_t>& set) {
     std::vector<uint32_t> e = set;
     closure(nfa, &e, false, true, &mark, ++stamp);
-    uint64_t m = 0;
+    std::vector<uint32_t> m;
     for (uint32_t x : e)
-      if (nfa.st[x].acc >= 0) m |= 1ull << nfa.st[x].acc;
-    return m;
+      if (nfa.st[x].acc >= 0) m.push_back((uint32_t)nfa.st[x].acc);
+    std::sort(m.begin(), m.end());
+    m.erase(std::unique(m.begin(), m.end()), m.end());
+    auto it = class_ids.find(m);
+    if (it == class_ids.end()) {
+      it = class_ids.emplace(m, (uint32_t)classes.size()).first;
+      classes.push_back(m);
+    }
+    return it->second;
   };
   // dead state 0
   dstates.push_back({});
@@ -699,7 +706,7 @@ bool compile_dfa(const std::vector<Pattern>& pats, Dfa* out, std::string* err) {
         id = it->second;
       } else {
         id = (uint32_t)dstates.size();
-        if (id >= kMaxDfaStates) {
+        if (id >= max_states) {
           *err = "automaton exceeds the state limit";
           return false;
         }
@@ -714,11 +721,11 @@ bool compile_dfa(const std::vector<Pattern>& pats, Dfa* out, std::string* err) {
   }
   uint32_t ns = (uint32_t)dstates.size();
 
-  // Moore minimisation: initial partition by accept mask (dead state keeps its own block when
-  // its mask is 0 and its transitions are all dead — it merges with equivalent states, fine).
+  // Moore minimisation: initial partition by accept class (dead state keeps its own block when
+  // its class is 0 and its transitions are all dead — it merges with equivalent states, fine).
   std::vector<uint32_t> blk(ns);
   {
-    std::map<uint64_t, uint32_t> m;
+    std::map<uint32_t, uint32_t> m;
     for (uint32_t s = 0; s < ns; ++s) {
       auto it = m.find(acc[s]);
       if (it == m.end()) it = m.emplace(acc[s], (uint32_t)m.size()).first;
@@ -754,11 +761,15 @@ bool compile_dfa(const std::vector<Pattern>& pats, Dfa* out, std::string* err) {
   out->ncls = ncl;
   out->start = (uint32_t)newid[blk[1]];
   for (unsigned b = 0; b < 256; ++b) out->cls[b] = (uint8_t)cl[b];
+  if (next > max_states) {
+    *err = "automaton exceeds the state limit";
+    return false;
+  }
   out->trans.assign((size_t)next * ncl, 0);
-  out->accept.assign(next, 0);
+  out->acc.assign(next, 0);
   for (uint32_t s = 0; s < ns; ++s) {
     uint32_t t = (uint32_t)newid[blk[s]];
-    out->accept[t] = acc[s];
+    out->acc[t] = acc[s];
     for (uint32_t c = 0; c < ncl; ++c)
       out->trans[(size_t)t * ncl + c] = (uint16_t)newid[blk[trans[(size_t)s * ncl + c]]];
   }
@@ -766,38 +777,67 @@ bool compile_dfa(const std::vector<Pattern>& pats, Dfa* out, std::string* err) {
     *err = "too many byte classes";
     return false;
   }
+  // class ids in order of first use by a state (the dead state's empty set stays 0), unused sets
+  // of the unminimised automaton dropped
+  std::vector<int64_t> cmap(classes.size(), -1);
+  cmap[0] = 0;
+  out->classes.assign(1, {});
+  for (uint32_t& a : out->acc) {
+    if (cmap[a] < 0) {
+      cmap[a] = (int64_t)out->classes.size();
+      out->classes.push_back(classes[a]);
+    }
+    a = (uint32_t)cmap[a];
+  }
   return true;
 }
 
-static size_t table_bytes(const Dfa& d) { return d.trans.size() * 2 + d.accept.size() * 8 + 256; }
-
-bool compile_column(const std::vector<Pattern>& pats, size_t max_bytes, std::vector<Dfa>* out, std::string* err) {
+bool compile_column(const std::vector<Pattern>& pats, size_t max_bytes, uint32_t max_states, std::vector<Dfa>* out,
+                    std::string* err, std::vector<uint32_t>* firsts) {
   out->clear();
-  if (pats.size() > kMaxPatternsPerColumn) {
-    *err = "more than 64 distinct patterns for one column";
-    return false;
-  }
+  if (firsts) firsts->clear();
   size_t i = 0;
   while (i < pats.size()) {
-    // grow the group [i, j) while its automaton fits
+    // grow the group [i, j) while its automaton fits; doubling steps, then bisection, so a large
+    // column costs O(log n) compilations per DFA rather than one per pattern
     std::vector<Pattern> group{pats[i]};
     Dfa best;
-    if (!compile_dfa(group, &best, err)) return false;
-    size_t j = i + 1;
-    while (j < pats.size()) {
-      std::vector<Pattern> g2 = group;
-      g2.push_back(pats[j]);
-      Dfa d;
+    if (!compile_dfa(group, &best, err, max_states)) return false;
+    size_t good = 1, step = 1;
+    auto try_n = [&](size_t n, Dfa* d) {
+      std::vector<Pattern> g(pats.begin() + (long)i, pats.begin() + (long)(i + n));
       std::string e2;
-      if (!compile_dfa(g2, &d, &e2) || table_bytes(d) > max_bytes) break;
-      group = std::move(g2);
-      best = std::move(d);
-      ++j;
+      return compile_dfa(g, d, &e2, max_states) && d->table_bytes() <= max_bytes;
+    };
+    size_t bad = 0;  // smallest known size that does not fit (0 = none)
+    while (i + good < pats.size()) {
+      const size_t n = std::min(pats.size() - i, good + step);
+      Dfa d;
+      if (try_n(n, &d)) {
+        good = n;
+        best = std::move(d);
+        step *= 2;
+      } else {
+        bad = n;
+        break;
+      }
     }
-    // local pattern k of the group is global pattern i + k
-    for (auto& m : best.accept) m <<= i;
+    while (bad && bad - good > 1) {
+      const size_t n = good + (bad - good) / 2;
+      Dfa d;
+      if (try_n(n, &d)) {
+        good = n;
+        best = std::move(d);
+      } else {
+        bad = n;
+      }
+    }
+    // local pattern k of the group is column pattern i + k
+    if (firsts) firsts->push_back((uint32_t)i);
+    for (auto& c : best.classes)
+      for (auto& p : c) p += (uint32_t)i;
     out->push_back(std::move(best));
-    i = j;
+    i += good;
   }
   return true;
 }

@@ -30,28 +30,33 @@ struct Pattern {
 };
 
 // A compiled column automaton. State 0 is the dead state; `start` is the initial state.
+// Accepting is by *class*: every state carries the id of the set of patterns matched if the input
+// ends there (acc[state]; class 0 = the empty set), and classes[c] lists that set (pattern indices,
+// ascending). There is no bound on the number of patterns: a string's classification is one small
+// integer, and the policy tables are indexed by it (slots.hpp), not by pattern bits.
 struct Dfa {
   uint32_t nstates = 0;
   uint32_t ncls = 0;
   uint32_t start = 0;
-  std::array<uint8_t, 256> cls{};  // byte -> class
-  std::vector<uint16_t> trans;      // [state][class]
-  std::vector<uint64_t> accept;     // [state] bitmask of patterns matched if input ends here
-  uint64_t run(const uint8_t* s, size_t n) const;
+  std::array<uint8_t, 256> cls{};              // byte -> byte class
+  std::vector<uint16_t> trans;                  // [state][byte class]
+  std::vector<uint32_t> acc;                    // [state] accept class
+  std::vector<std::vector<uint32_t>> classes;   // accept class -> pattern indices (classes[0] empty)
+  uint32_t run(const uint8_t* s, size_t n) const;  // accept class of the whole string
+  size_t table_bytes() const { return trans.size() * 2 + (size_t)nstates * 2 + 256; }
 };
 
 constexpr uint32_t kMaxDfaStates = 8192;
-constexpr size_t kMaxPatternsPerColumn = 64;
-// per-DFA table budget of a column chain (LDS-resident in the classify kernel)
-constexpr size_t kMaxDfaTableBytes = 24 * 1024;
 
-// Compiles up to 64 patterns into one minimised DFA. Returns false with a message on a
-// syntax error or when the automaton exceeds kMaxDfaStates.
-bool compile_dfa(const std::vector<Pattern>& pats, Dfa* out, std::string* err);
-// Compiles a column's patterns into a chain of DFAs, each within `max_table_bytes` of tables
-// (greedy packing in pattern order); accept masks keep the global pattern bit of each pattern.
-bool compile_column(const std::vector<Pattern>& pats, size_t max_table_bytes, std::vector<Dfa>* out,
-                    std::string* err);
+// Compiles patterns into one minimised DFA. Returns false with a message on a syntax error or
+// when the automaton exceeds `max_states` (<= kMaxDfaStates).
+bool compile_dfa(const std::vector<Pattern>& pats, Dfa* out, std::string* err, uint32_t max_states = kMaxDfaStates);
+// Compiles a column's patterns into a chain of DFAs (greedy packing in pattern order), each within
+// `max_table_bytes` of tables and `max_states` states; a string's pattern set is the union of its
+// classes in every DFA of the chain. Class sets hold the column's pattern indices.
+// firsts (optional): the index of the first pattern of each DFA (DFA k covers [firsts[k], firsts[k+1])).
+bool compile_column(const std::vector<Pattern>& pats, size_t max_table_bytes, uint32_t max_states, std::vector<Dfa>* out,
+                    std::string* err, std::vector<uint32_t>* firsts = nullptr);
 // Syntax check of one regex (used by settings validation).
 bool regex_ok(const std::string& re, std::string* err);
 

@@ -24,8 +24,15 @@ struct StrCol {
     off.push_back((uint32_t)bytes.size());
   }
   size_t n() const { return off.size() - 1; }
+  // string i, or "" when i is out of range (callers that must tell the difference use get())
   std::string_view at(size_t i) const {
+    if (i + 1 >= off.size()) return std::string_view();
     return std::string_view((const char*)bytes.data() + off[i], off[i + 1] - off[i]);
+  }
+  bool get(size_t i, std::string_view* s) const {
+    if (i + 1 >= off.size()) return false;
+    *s = at(i);
+    return true;
   }
   void reserve(size_t ns, size_t nb) {
     off.reserve(ns + 1);
@@ -51,7 +58,30 @@ struct StrCol {
   }
 };
 
-struct DeviceBatch;  // engine.cpp
+struct DeviceBatch;  // capi.cpp
+
+// Host copy of a pass's side data (kernels.hpp WideRec): the values of verdict words whose ARG is
+// kArgWide. Filled by kw_batch_verdicts.
+struct WideData {
+  struct Rec {
+    uint64_t row;
+    int32_t policy;
+    uint32_t value;
+  };
+  std::vector<Rec> recs;             // entity indices >= 65535 (sorted by row, policy)
+  std::vector<uint64_t> groups;      // dense [row][nwide] cause masks of > 15-member groups
+  uint32_t nwide = 0;
+  std::vector<int32_t> wide_policy;  // wide index -> group policy (all-pairs mode)
+  bool rows_mode = false;
+  bool lookup(uint64_t row, int32_t policy, uint64_t* v) const;
+  void clear() {
+    recs.clear();
+    groups.clear();
+    nwide = 0;
+    wide_policy.clear();
+    rows_mode = false;
+  }
+};
 
 struct Batch {
   uint64_t n = 0;
@@ -63,6 +93,7 @@ struct Batch {
   std::vector<uint32_t> capadd_off{0}, capdrop_off{0};
   StrCol ctr_name, ctr_image, ctr_aa, cap_add, cap_drop, lbl_key, lbl_val;
   DeviceBatch* dev = nullptr;
+  WideData wide;  // side data of the last pass (kw_batch_verdicts)
   uint64_t containers() const { return ctr_flags.size(); }
   uint64_t labels() const { return lbl_key.n(); }
   void view(kw_soa* s) const;

@@ -314,8 +314,14 @@ bool compile_settings(const JDoc& d, int64_t s, PolicyRec* rec, std::string* err
             *err = "constrained label '" + key + "' has an invalid regular expression: " + rerr;
             return false;
           }
-          rec->lists[2].push_back(key);
-          rec->lists[3].push_back(re);
+          // a repeated key keeps its first position and its last regex (a JSON map, as serde reads it)
+          auto dup = std::find(rec->lists[2].begin(), rec->lists[2].end(), key);
+          if (dup != rec->lists[2].end()) {
+            rec->lists[3][(size_t)(dup - rec->lists[2].begin())] = re;
+          } else {
+            rec->lists[2].push_back(key);
+            rec->lists[3].push_back(re);
+          }
         }
       }
       for (auto& k : rec->lists[0]) {
@@ -326,23 +332,24 @@ bool compile_settings(const JDoc& d, int64_t s, PolicyRec* rec, std::string* err
           return false;
         }
       }
-      if (rec->lists[1].size() > (size_t)kMaxListIdx || rec->lists[2].size() > (size_t)kMaxListIdx) {
-        *err = "at most 16 mandatory and 16 constrained labels are supported";
-        return false;
-      }
       return true;
     }
   }
   return true;
 }
 
-int32_t pattern_bit(std::vector<Pattern>* col, Pattern::Kind k, const std::string& s) {
+
+// Pattern id of (kind, text) in a column, added when new.
+uint32_t pattern_id(ColumnInfo* col, Pattern::Kind k, const std::string& s) {
   Pattern p{k, s};
-  for (size_t i = 0; i < col->size(); ++i)
-    if ((*col)[i] == p) return (int32_t)i;
-  col->push_back(p);
-  return (int32_t)col->size() - 1;
+  for (size_t i = 0; i < col->pats.size(); ++i)
+    if (col->pats[i] == p) return (uint32_t)i;
+  col->pats.push_back(p);
+  return (uint32_t)col->pats.size() - 1;
 }
+
+// A glob without metacharacters is a literal under fnmatch(3) flags 0.
+bool glob_is_literal(const std::string& g) { return g.find_first_of("*?[\\") == std::string::npos; }
 
 template <typename T>
 void put(std::vector<uint8_t>* b, const T& v) {
@@ -353,9 +360,152 @@ void align16(std::vector<uint8_t>* b) {
   while (b->size() % 16) b->push_back(0);
 }
 
-// Appends one DevDfa record (header, accept masks, transitions; 16-B aligned) and returns its
-// blob offset. trans_off / acc_off are blob offsets.
-size_t emit_dfa(const Dfa& dfa, std::vector<uint8_t>* b) {
+// Canonical dwords of a string: little-endian, the last one zero-padded (what the kernels build
+// from the staged bytes).
+std::vector<uint32_t> lit_words(const std::string& s) {
+  std::vector<uint32_t> w((s.size() + 3) / 4, 0u);
+  if (!s.empty()) memcpy(w.data(), s.data(), s.size());
+  return w;
+}
+uint32_t lit_hash(const std::vector<uint32_t>& w, uint32_t len, uint32_t seed) {
+  uint32_t h = lit_init(seed, len);
+  for (uint32_t x : w) h = lit_mix(h, x);
+  return lit_final(h);
+}
+
+// Appends a DevLit record (kwdev.hpp) over literal strings `lits` (class of lits[i] = i + 1).
+// Up to 48 strings: one bucket, the smallest power-of-two table (>= 2x) and seed for which the hash
+// alone is collision-free. Larger sets: hash-and-displace with ~2 strings per bucket and a load
+// factor of at most 1/2 (buckets placed largest first, each with the first displacement whose slots
+// are all free).
+bool build_literal_table(const std::vector<std::string>& lits, std::vector<uint8_t>* b, std::string* err) {
+  const uint32_t npat = (uint32_t)lits.size();
+  std::vector<std::vector<uint32_t>> words;
+  std::vector<uint32_t> wi;
+  uint32_t nwords = 0;
+  for (const std::string& s : lits) {
+    if (s.size() > 65535) {
+      *err = "literal pattern longer than 65535 bytes";
+      return false;
+    }
+    words.push_back(lit_words(s));
+    wi.push_back(nwords);
+    nwords += (uint32_t)words.back().size();
+  }
+  if (npat >= 65535) {
+    *err = "more than 65534 literal patterns in one column";
+    return false;
+  }
+  auto emit = [&](uint32_t nslots, uint32_t seed, uint32_t nb_log2, const std::vector<uint32_t>& slot_of,
+                  const std::vector<uint16_t>& disp) {
+    const size_t at = b->size();
+    DevLit L;
+    memset(&L, 0, sizeof(L));
+    L.nslots = nslots;
+    L.seed = seed;
+    L.npat = npat;
+    L.nb_log2 = nb_log2;
+    put(b, L);
+    L.slot_off = (uint32_t)(b->size() - at);
+    std::vector<uint32_t> sx(nslots, 0), sy(nslots, 0);
+    for (uint32_t i = 0; i < npat; ++i) {
+      sx[slot_of[i]] = (i + 1) | ((uint32_t)lits[i].size() << 16);
+      sy[slot_of[i]] = wi[i];
+    }
+    for (uint32_t k = 0; k < nslots; ++k) {
+      put(b, sx[k]);
+      put(b, sy[k]);
+    }
+    align16(b);
+    L.disp_off = 0;
+    if (nb_log2) {
+      L.disp_off = (uint32_t)(b->size() - at);
+      for (uint16_t d : disp) put(b, d);
+      align16(b);
+    }
+    L.word_off = (uint32_t)(b->size() - at);
+    for (const auto& w : words)
+      for (uint32_t x : w) put(b, x);
+    for (int k = 0; k < 8; ++k) put(b, 0u);
+    align16(b);
+    L.bytes = (uint32_t)(b->size() - at);
+    memcpy(b->data() + at, &L, sizeof(L));
+  };
+  if (npat <= 48) {
+    for (uint32_t nslots = 16; nslots <= 8192; nslots *= 2) {
+      if (nslots < 2 * npat) continue;
+      for (uint32_t seed = 1; seed <= 4096; ++seed) {
+        std::vector<uint32_t> slot_of(npat);
+        std::vector<uint8_t> used(nslots, 0);
+        bool ok = true;
+        for (uint32_t i = 0; i < npat && ok; ++i) {
+          const uint32_t h = lit_slot_index(lit_hash(words[i], (uint32_t)lits[i].size(), seed), 0, nslots);
+          if (used[h]) ok = false;
+          used[h] = 1;
+          slot_of[i] = h;
+        }
+        if (!ok) continue;
+        emit(nslots, seed, 0, slot_of, {});
+        return true;
+      }
+    }
+  }
+  uint32_t nslots = 16, nb_log2 = 1;
+  while (nslots < 2 * npat) nslots *= 2;
+  while ((1u << nb_log2) < (npat + 1) / 2) ++nb_log2;
+  const uint32_t nb = 1u << nb_log2;
+  for (uint32_t seed = 1; seed <= 64; ++seed) {
+    std::vector<uint32_t> g(npat);
+    std::vector<std::vector<uint32_t>> bucket(nb);
+    for (uint32_t i = 0; i < npat; ++i) {
+      g[i] = lit_hash(words[i], (uint32_t)lits[i].size(), seed);
+      bucket[g[i] >> (32 - nb_log2)].push_back(i);
+    }
+    std::vector<uint32_t> order(nb);
+    for (uint32_t k = 0; k < nb; ++k) order[k] = k;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return bucket[x].size() > bucket[y].size(); });
+    std::vector<uint8_t> used(nslots, 0);
+    std::vector<uint16_t> disp(nb, 0);
+    std::vector<uint32_t> slot_of(npat);
+    bool ok = true;
+    for (uint32_t bk : order) {
+      if (bucket[bk].empty()) break;
+      bool placed = false;
+      for (uint32_t d = 0; d < 65536 && !placed; ++d) {
+        std::vector<uint32_t> sl;
+        bool fit = true;
+        for (uint32_t i : bucket[bk]) {
+          const uint32_t s = lit_slot_index(g[i], d, nslots);
+          if (used[s] || std::find(sl.begin(), sl.end(), s) != sl.end()) {
+            fit = false;
+            break;
+          }
+          sl.push_back(s);
+        }
+        if (!fit) continue;
+        for (size_t q = 0; q < sl.size(); ++q) {
+          used[sl[q]] = 1;
+          slot_of[bucket[bk][q]] = sl[q];
+        }
+        disp[bk] = (uint16_t)d;
+        placed = true;
+      }
+      if (!placed) {
+        ok = false;
+        break;
+      }
+    }
+    if (!ok) continue;
+    emit(nslots, seed, nb_log2, slot_of, disp);
+    return true;
+  }
+  *err = "cannot build the literal hash table";
+  return false;
+}
+
+// Appends one DevDfa record (header, accept classes, transitions; 16-B aligned) and returns its
+// blob offset. `cls_map`: the DFA's local accept class -> the column's global class.
+size_t emit_dfa(const Dfa& dfa, const std::vector<uint32_t>& cls_map, std::vector<uint8_t>* b) {
   align16(b);
   const size_t hdr_at = b->size();
   DevDfa dd;
@@ -367,7 +517,7 @@ size_t emit_dfa(const Dfa& dfa, std::vector<uint8_t>* b) {
   put(b, dd);
   align16(b);
   const uint32_t acc_off = (uint32_t)b->size();
-  for (uint64_t a : dfa.accept) put(b, a);
+  for (uint32_t a : dfa.acc) put(b, (uint16_t)cls_map[a]);
   align16(b);
   const uint32_t trans_off = (uint32_t)b->size();
   for (uint16_t t : dfa.trans) put(b, t);
@@ -380,66 +530,190 @@ size_t emit_dfa(const Dfa& dfa, std::vector<uint8_t>* b) {
   return hdr_at;
 }
 
-// Canonical dwords of a string: little-endian, the last one zero-padded (what the kernels build
-// from the staged bytes with v_alignbyte).
-std::vector<uint32_t> lit_words(const std::string& s) {
-  std::vector<uint32_t> w((s.size() + 3) / 4, 0u);
-  if (!s.empty()) memcpy(w.data(), s.data(), s.size());
-  return w;
-}
-uint32_t lit_hash(const std::vector<uint32_t>& w, uint32_t len, uint32_t seed) {
-  uint32_t h = lit_init(seed, len);
-  for (uint32_t x : w) h = lit_mix(h, x);
-  return lit_final(h);
-}
+constexpr size_t kDfaTableBudget = 64 * 1024;  // per DFA of a column chain
+constexpr size_t kKvDfaBudget = 16 * 1024;     // per DFA of a label key's value chain
 
-// Appends a DevLit record (kwdev.hpp) for an all-literal column: the smallest power-of-two table
-// (>= 2x the patterns) and seed for which the hash is collision-free over the patterns.
-bool build_literal_table(const std::vector<Pattern>& pats, std::vector<uint8_t>* b) {
-  const uint32_t npat = (uint32_t)pats.size();
-  std::vector<std::vector<uint32_t>> words;
-  std::vector<uint32_t> wi;  // word index of each pattern
-  uint32_t nwords = 0;
-  for (const Pattern& p : pats) {
-    if (p.text.size() > 4095) return false;  // packed slot fields (kwdev.hpp DevLit)
-    words.push_back(lit_words(p.text));
-    wi.push_back(nwords);
-    nwords += (uint32_t)words.back().size();
-  }
-  if (nwords >= 8192 || npat > 126) return false;
-  for (uint32_t nslots = 16; nslots <= 4096; nslots *= 2) {
-    if (nslots < 2 * npat) continue;
-    for (uint32_t seed = 1; seed <= 4096; ++seed) {
-      std::vector<uint32_t> slot(nslots, 0);
-      bool ok = true;
-      for (uint32_t i = 0; i < npat && ok; ++i) {
-        const uint32_t len = (uint32_t)pats[i].text.size();
-        uint32_t h = lit_hash(words[i], len, seed) & (nslots - 1);
-        if (slot[h]) ok = false;
-        else slot[h] = (i + 1) | (len << 7) | (wi[i] << 19);
-      }
-      if (!ok) continue;
-      const size_t at = b->size();
-      DevLit L;
-      memset(&L, 0, sizeof(L));
-      L.nslots = nslots;
-      L.seed = seed;
-      L.npat = npat;
-      put(b, L);
-      L.slot_off = (uint32_t)(b->size() - at);
-      for (uint32_t x : slot) put(b, x);
-      align16(b);
-      L.word_off = (uint32_t)(b->size() - at);
-      for (const auto& w : words)
-        for (uint32_t x : w) put(b, x);
-      for (int k = 0; k < 8; ++k) put(b, 0u);
-      align16(b);
-      L.bytes = (uint32_t)(b->size() - at);
-      memcpy(b->data() + at, &L, sizeof(L));
-      return true;
+// Compiles one column (ColumnInfo.pats) into its blob records: the literal table over the literal
+// patterns (COL_IMG: none, its strings are constructed), then the DFA chain over the rest.
+Status compile_col(Col c, ColumnInfo* ci, DevCol* dc, std::vector<uint8_t>* b) {
+  memset(dc, 0, sizeof(*dc));
+  ci->class_pats.assign(1, {});
+  ci->lit_cls.assign(ci->pats.size(), 0);
+  std::vector<std::string> lits;
+  std::vector<uint32_t> lit_pid, rest_pid;
+  for (uint32_t p = 0; p < (uint32_t)ci->pats.size(); ++p) {
+    if (ci->pats[p].kind == Pattern::Literal && c != COL_IMG) {
+      lits.push_back(ci->pats[p].text);
+      lit_pid.push_back(p);
+    } else {
+      rest_pid.push_back(p);
     }
   }
-  return false;
+  if (!lits.empty()) {
+    align16(b);
+    const size_t at = b->size();
+    std::string err;
+    if (!build_literal_table(lits, b, &err)) return {KW_E_BOOTSTRAP, "bootstrap failure: " + err};
+    dc->lit_off = (uint32_t)at;
+    dc->lit_bytes = (uint32_t)(b->size() - at);
+    dc->nlit = (uint32_t)lits.size();
+    for (size_t i = 0; i < lit_pid.size(); ++i) {
+      ci->lit_cls[lit_pid[i]] = (uint32_t)i + 1;
+      ci->class_pats.push_back({lit_pid[i]});
+    }
+  }
+  if (!rest_pid.empty()) {
+    std::vector<Pattern> pats;
+    for (uint32_t p : rest_pid) pats.push_back(ci->pats[p]);
+    std::vector<Dfa> chain;
+    std::string err;
+    if (!compile_column(pats, kDfaTableBudget, kMaxDfaStates, &chain, &err))
+      return {KW_E_BOOTSTRAP, "bootstrap failure: cannot compile column automaton: " + err};
+    std::vector<size_t> at;
+    for (const Dfa& dfa : chain) {
+      std::vector<uint32_t> cls_map(dfa.classes.size(), 0);
+      for (size_t a = 1; a < dfa.classes.size(); ++a) {
+        cls_map[a] = (uint32_t)ci->class_pats.size();
+        std::vector<uint32_t> pids;
+        for (uint32_t k : dfa.classes[a]) pids.push_back(rest_pid[k]);
+        ci->class_pats.push_back(pids);
+      }
+      at.push_back(emit_dfa(dfa, cls_map, b));
+    }
+    uint32_t tail = 0;
+    for (size_t k = chain.size(); k-- > 0;) {
+      DevDfa* w = (DevDfa*)(b->data() + at[k]);
+      w->next = k + 1 < chain.size() ? (uint32_t)at[k + 1] : 0;
+      tail += w->bytes;
+      w->chain_bytes = tail;
+    }
+    dc->dfa_off = (uint32_t)at[0];
+    dc->ndfa = (uint32_t)chain.size();
+    dc->dfa_bytes = tail;
+  }
+  dc->nclass = (uint32_t)ci->class_pats.size();
+  if (dc->nclass > 65535) return {KW_E_BOOTSTRAP, "bootstrap failure: a request column needs more than 65535 classes"};
+  return {};
+}
+
+// The per-key label-value region (kwdev.hpp DevHeader kv_*): for each label-key class, a chain of
+// small DFAs over the regexes constrained on that key (keys with the same regexes share one chain).
+Status compile_kv(Env* env, DevHeader* hdr, std::vector<uint8_t>* b) {
+  const uint32_t nlk = hdr->col[COL_LK].nclass;
+  const ColumnInfo& lk = env->cols[COL_LK];
+  std::vector<std::vector<uint32_t>> vals(nlk);  // key class -> LV pattern ids
+  for (const PolicyRec& r : env->pol) {
+    if (r.family != FAM_LABELS || r.init_error) continue;
+    for (size_t k = 0; k < r.pid[2].size(); ++k) {
+      auto& v = vals[lk.lit_cls[r.pid[2][k]]];
+      if (std::find(v.begin(), v.end(), r.pid[3][k]) == v.end()) v.push_back(r.pid[3][k]);
+    }
+  }
+  std::vector<uint8_t> R(8u * nlk, 0);  // kidx[nlk] | kbase[nlk]
+  auto at16 = [&](size_t n) {
+    while (R.size() % 16) R.push_back(0);
+    const size_t o = R.size();
+    R.resize(o + n, 0);
+    return o;
+  };
+  std::map<std::vector<uint8_t>, uint32_t> cls_pool;
+  struct Shared {
+    uint32_t head;
+    std::vector<std::pair<std::vector<uint32_t>, std::vector<std::vector<uint32_t>>>> dfas;  // (covered, class sets)
+  };
+  std::map<std::vector<uint32_t>, Shared> chains;  // regex list -> compiled chain
+  env->kv.clear();
+  env->kv_of_key.assign(nlk, {});
+  uint32_t longest = 0;
+  for (uint32_t k = 1; k < nlk; ++k) {
+    if (vals[k].empty()) continue;
+    auto hit = chains.find(vals[k]);
+    if (hit == chains.end()) {
+      std::vector<Pattern> pats;
+      for (uint32_t v : vals[k]) pats.push_back(env->cols[COL_LV].pats[v]);
+      std::vector<Dfa> kd;
+      std::vector<uint32_t> firsts;
+      std::string err;
+      if (!compile_column(pats, kKvDfaBudget, kMaxDfaStates, &kd, &err, &firsts))
+        return {KW_E_BOOTSTRAP, "bootstrap failure: cannot compile label value automaton: " + err};
+      Shared sh;
+      sh.head = 0;
+      size_t prev = 0;
+      uint32_t cbase = 0;
+      for (const Dfa& d : kd) {
+        if (d.ncls > 65535 || d.nstates > 65535) return {KW_E_BOOTSTRAP, "bootstrap failure: label value automaton too large"};
+        KvDfa kv;
+        memset(&kv, 0, sizeof(kv));
+        bool uniform_hi = true;
+        for (int c = 128; c < 256; ++c) uniform_hi = uniform_hi && d.cls[c] == d.cls[128];
+        kv.wide = uniform_hi ? 0 : 1;
+        kv.hi = d.cls[128];
+        std::vector<uint8_t> cm(d.cls.begin(), d.cls.begin() + (kv.wide ? 256 : 128));
+        auto it = cls_pool.find(cm);
+        if (it == cls_pool.end()) {
+          const size_t o = at16(cm.size());
+          memcpy(R.data() + o, cm.data(), cm.size());
+          it = cls_pool.emplace(cm, (uint32_t)o).first;
+        }
+        kv.cls_off = it->second;
+        kv.ncls = (uint16_t)d.ncls;
+        kv.start = d.start;
+        kv.nstates = (uint16_t)d.nstates;
+        kv.t16 = d.nstates > 256 ? 1 : 0;
+        kv.cbase = (uint16_t)cbase;
+        const size_t rec = at16(sizeof(KvDfa));
+        kv.acc_off = (uint32_t)at16(d.nstates * 2u);
+        for (uint32_t q = 0; q < d.nstates; ++q) ((uint16_t*)(R.data() + kv.acc_off))[q] = (uint16_t)d.acc[q];
+        kv.trans_off = (uint32_t)at16(d.trans.size() * (kv.t16 ? 2u : 1u));
+        for (size_t q = 0; q < d.trans.size(); ++q) {
+          if (kv.t16) ((uint16_t*)(R.data() + kv.trans_off))[q] = d.trans[q];
+          else R[kv.trans_off + q] = (uint8_t)d.trans[q];
+        }
+        memcpy(R.data() + rec, &kv, sizeof(kv));
+        if (prev) ((KvDfa*)(R.data() + prev))->next = (uint32_t)rec;
+        else sh.head = (uint32_t)rec;
+        prev = rec;
+        // covered regexes: the DFA's group of the key's list (compile_column packs in order)
+        const size_t q = sh.dfas.size();
+        const uint32_t f0 = firsts[q], f1 = q + 1 < firsts.size() ? firsts[q + 1] : (uint32_t)vals[k].size();
+        std::vector<uint32_t> covered(vals[k].begin() + f0, vals[k].begin() + f1);
+        std::vector<std::vector<uint32_t>> sets;
+        for (const auto& cs : d.classes) {
+          std::vector<uint32_t> m;
+          for (uint32_t i : cs) m.push_back(vals[k][i]);
+          sets.push_back(m);
+        }
+        sh.dfas.push_back({covered, sets});
+        cbase += (uint32_t)d.classes.size();
+        if (cbase > 65535) return {KW_E_BOOTSTRAP, "bootstrap failure: label value automaton too large"};
+      }
+      hit = chains.emplace(vals[k], std::move(sh)).first;
+    }
+    ((uint32_t*)R.data())[k] = hit->second.head;
+    ((uint32_t*)R.data())[nlk + k] = (uint32_t)env->kv.size();
+    longest = std::max(longest, (uint32_t)hit->second.dfas.size());
+    for (const auto& d : hit->second.dfas)
+      for (const auto& set : d.second) {
+        KvClass kc;
+        kc.key = k;
+        kc.covered = d.first;
+        kc.matched = set;
+        env->kv_of_key[k].push_back((uint32_t)env->kv.size());
+        env->kv.push_back(std::move(kc));
+      }
+  }
+  if (env->kv.size() > 65535) return {KW_E_BOOTSTRAP, "bootstrap failure: more than 65535 label value classes"};
+  while (R.size() % 16) R.push_back(0);
+  R.resize(R.size() + 16, 0);  // slack: dword-granular readers may run past the last table
+  if (env->kv.empty()) return {};
+  align16(b);
+  hdr->kv_off = (uint32_t)b->size();
+  hdr->kv_bytes = (uint32_t)R.size();
+  b->insert(b->end(), R.begin(), R.end());
+  hdr->col[COL_LV].nclass = (uint32_t)env->kv.size();
+  hdr->col[COL_LV].ndfa = longest;
+  hdr->col[COL_LV].dfa_bytes = (uint32_t)R.size();
+  return {};
 }
 
 }  // namespace
@@ -459,6 +733,21 @@ static Status bootstrap(const JDoc& d, int64_t settings, PolicyRec* rec) {
   std::string err;
   if (!compile_settings(d, settings, rec, &err))
     return {KW_E_INIT, "Policy settings are invalid: " + err};
+  // engine limits of the bit-parallel evaluation: 64 local bits per policy
+  auto distinct = [](std::vector<std::string> v) {
+    std::sort(v.begin(), v.end());
+    return (size_t)(std::unique(v.begin(), v.end()) - v.begin());
+  };
+  if (rec->family == FAM_LABELS && distinct(rec->lists[1]) > (size_t)kMaxLocalBits)
+    return {KW_E_BOOTSTRAP, "bootstrap failure: " + rec->id + ": more than 64 distinct mandatory_labels (engine limit)"};
+  if (rec->family == FAM_CAPABILITIES) {
+    std::vector<std::string> m = rec->lists[1];
+    m.insert(m.end(), rec->lists[2].begin(), rec->lists[2].end());
+    m.push_back("ALL");
+    if (distinct(m) > (size_t)kMaxLocalBits)
+      return {KW_E_BOOTSTRAP, "bootstrap failure: " + rec->id +
+                                  ": more than 63 distinct required-drop / default-add capabilities (engine limit)"};
+  }
   return {};
 }
 
@@ -564,88 +853,55 @@ Status build_env(const char* json, size_t len, bool continue_on_errors, const ch
     if (!rec.is_group) continue;
     if (rec.member_names.size() > (size_t)kMaxGroupMembers) {
       rec.prog.valid = false;
-      rec.prog.error = "policy groups with more than 16 members are not supported by the engine";
+      rec.prog.error = "policy groups with more than 64 members are not supported by the engine";
       continue;
     }
     rec.prog = compile_group_expression(rec.expression, rec.member_names);
   }
 
-  // ---- column pattern tables and device parameters
-  std::vector<DevPolicy> dp(env->pol.size());
-  std::vector<uint8_t> progs;
-  std::vector<int32_t> mems;
-  int32_t bypass_bit = -1;
-  if (env->always_ns) bypass_bit = pattern_bit(&env->cols[COL_NS], Pattern::Literal, *env->always_ns);
-  for (size_t i = 0; i < env->pol.size(); ++i) {
-    PolicyRec& r = env->pol[i];
-    DevPolicy& P = dp[i];
-    memset(&P, 0, sizeof(P));
-    P.family = r.family;
-    P.mode = r.mode;
-    P.a2m = r.allowed_to_mutate;
-    P.flags = r.flags | (r.registered ? PF_REGISTERED : 0) | (r.init_error ? PF_INIT_ERROR : 0);
-    if (r.init_error) continue;
-    auto bits = [&](Col c, Pattern::Kind k, const std::vector<std::string>& l) {
-      uint64_t m = 0;
-      for (auto& s : l) m |= 1ull << (pattern_bit(&env->cols[c], k, s) & 63);
-      return m;
+  // ---- the request columns' patterns: every list of every initialised policy as pattern ids
+  if (env->always_ns) pattern_id(&env->cols[COL_NS], Pattern::Literal, *env->always_ns);
+  for (PolicyRec& r : env->pol) {
+    if (r.is_group || r.init_error) continue;
+    auto ids = [&](Col c, Pattern::Kind k, const std::vector<std::string>& l) {
+      std::vector<uint32_t> v;
+      for (const auto& s : l) {
+        const Pattern::Kind kk = (k == Pattern::Glob && c != COL_IMG && glob_is_literal(s)) ? Pattern::Literal : k;
+        v.push_back(pattern_id(&env->cols[c], kk, s));
+      }
+      return v;
     };
-    for (int k = 0; k < 5; ++k) P.nl[k] = (uint8_t)std::min<size_t>(255, r.lists[k].size());
     switch (r.family) {
-      case FAM_NAMESPACE: P.m[0] = bits(COL_NS, Pattern::Literal, r.lists[0]); break;
+      case FAM_NAMESPACE: r.pid[0] = ids(COL_NS, Pattern::Literal, r.lists[0]); break;
       case FAM_TRUSTED_REPOS:
-        P.m[0] = bits(COL_REG, Pattern::Glob, r.lists[0]);
-        P.m[1] = bits(COL_REG, Pattern::Glob, r.lists[1]);
-        P.m[2] = bits(COL_TAG, Pattern::Glob, r.lists[2]);
-        P.m[3] = bits(COL_IMG, Pattern::Glob, r.lists[3]);
-        P.m[4] = bits(COL_IMG, Pattern::Glob, r.lists[4]);
+        r.pid[0] = ids(COL_REG, Pattern::Glob, r.lists[0]);
+        r.pid[1] = ids(COL_REG, Pattern::Glob, r.lists[1]);
+        r.pid[2] = ids(COL_TAG, Pattern::Glob, r.lists[2]);
+        r.pid[3] = ids(COL_IMG, Pattern::Glob, r.lists[3]);
+        r.pid[4] = ids(COL_IMG, Pattern::Glob, r.lists[4]);
         break;
       case FAM_CAPABILITIES: {
         std::vector<std::string> allowed;
         for (auto& c : r.lists[0])
           if (c != "*") allowed.push_back(c);
-        P.m[0] = bits(COL_CAP, Pattern::Literal, allowed) | bits(COL_CAP, Pattern::Literal, r.lists[2]);
-        P.m[1] = bits(COL_CAP, Pattern::Literal, r.lists[1]);
-        P.m[2] = bits(COL_CAP, Pattern::Literal, r.lists[2]);
-        P.m[3] = bits(COL_CAP, Pattern::Literal, {"ALL"});
+        r.pid[0] = ids(COL_CAP, Pattern::Literal, allowed);
+        r.pid[1] = ids(COL_CAP, Pattern::Literal, r.lists[1]);
+        r.pid[2] = ids(COL_CAP, Pattern::Literal, r.lists[2]);
+        r.pid[3] = ids(COL_CAP, Pattern::Literal, {"ALL"});
         break;
       }
-      case FAM_APPARMOR: P.m[0] = bits(COL_AA, Pattern::Literal, r.lists[0]); break;
-      case FAM_LABELS: {
-        P.m[0] = bits(COL_LK, Pattern::Literal, r.lists[0]);
-        P.m[1] = bits(COL_LK, Pattern::Literal, r.lists[1]);
-        P.n_mand = (uint8_t)r.lists[1].size();
-        P.n_constr = (uint8_t)r.lists[2].size();
-        for (size_t k = 0; k < r.lists[1].size(); ++k)
-          P.idx[k] = (uint8_t)pattern_bit(&env->cols[COL_LK], Pattern::Literal, r.lists[1][k]);
-        for (size_t k = 0; k < r.lists[2].size(); ++k) {
-          P.idx[16 + k] = (uint8_t)pattern_bit(&env->cols[COL_LK], Pattern::Literal, r.lists[2][k]);
-          P.idx[32 + k] = (uint8_t)pattern_bit(&env->cols[COL_LV], Pattern::Regex, r.lists[3][k]);
-        }
+      case FAM_APPARMOR: r.pid[0] = ids(COL_AA, Pattern::Literal, r.lists[0]); break;
+      case FAM_LABELS:
+        r.pid[0] = ids(COL_LK, Pattern::Literal, r.lists[0]);
+        r.pid[1] = ids(COL_LK, Pattern::Literal, r.lists[1]);
+        r.pid[2] = ids(COL_LK, Pattern::Literal, r.lists[2]);
+        r.pid[3] = ids(COL_LV, Pattern::Regex, r.lists[3]);
         break;
-      }
-      case FAM_GROUP: {
-        if (!r.prog.valid || r.prog.eval_error) {
-          P.flags |= PF_EXPR_ERROR;
-          break;
-        }
-        P.prog_off = (uint32_t)progs.size();
-        P.prog_len = (uint32_t)r.prog.code.size();
-        progs.insert(progs.end(), r.prog.code.begin(), r.prog.code.end());
-        P.member_off = (uint32_t)mems.size();
-        P.nmembers = (uint32_t)r.members.size();
-        mems.insert(mems.end(), r.members.begin(), r.members.end());
-        break;
-      }
       default: break;
     }
   }
-  for (int c = 0; c < (int)NCOL; ++c)
-    if (env->cols[c].size() > kMaxPatternsPerColumn)
-      return {KW_E_BOOTSTRAP, std::string("bootstrap failure: the policy set needs more than 64 distinct patterns "
-                                          "for one request column (column ") + std::to_string(c) + ")"};
 
-  // ---- DFAs and blob
+  // ---- blob: header, the column classifiers, the per-key label-value region
   std::vector<uint8_t>& b = env->blob;
   b.clear();
   DevHeader hdr;
@@ -653,160 +909,27 @@ Status build_env(const char* json, size_t len, bool continue_on_errors, const ch
   put(&b, hdr);
   align16(&b);
   for (int c = 0; c < (int)NCOL; ++c) {
-    if (env->cols[c].empty()) continue;
-    std::vector<Dfa> chain;
-    std::string err;
-    if (!compile_column(env->cols[c], kMaxDfaTableBytes, &chain, &err))
-      return {KW_E_BOOTSTRAP, "bootstrap failure: cannot compile column automaton: " + err};
-    std::vector<size_t> at;
-    for (const Dfa& dfa : chain) at.push_back(emit_dfa(dfa, &b));
-    uint32_t tail = 0;
-    for (size_t k = chain.size(); k-- > 0;) {
-      DevDfa* w = (DevDfa*)(b.data() + at[k]);
-      w->next = k + 1 < chain.size() ? (uint32_t)at[k + 1] : 0;
-      tail += w->bytes;
-      w->chain_bytes = tail;
-    }
-    hdr.dfa_off[c] = (uint32_t)at[0];
+    if (c == COL_LV) continue;
+    Status st = compile_col((Col)c, &env->cols[c], &hdr.col[c], &b);
+    if (!st.ok()) return st;
   }
-  // literal columns: perfect-hash tables (the fused kernel's fast path; DFAs stay for the others)
-  for (int c = 0; c < (int)NCOL; ++c) {
-    if (env->cols[c].empty()) continue;
-    bool lit = true;
-    for (const Pattern& p : env->cols[c]) lit = lit && p.kind == Pattern::Literal;
-    if (!lit) continue;
-    align16(&b);
-    const size_t at = b.size();
-    if (build_literal_table(env->cols[c], &b)) hdr.lit_off[c] = (uint32_t)at;
-    else b.resize(at);  // no table (oversized literals): the column keeps its DFA chain
-  }
-  // per-key label-value DFAs: a label's value is only ever tested against the regexes constrained
-  // on its own key, so one small DFA per constrained key replaces the chain over all value regexes
-  if (hdr.lit_off[COL_LK] && !env->cols[COL_LV].empty()) {
-    std::vector<std::vector<uint32_t>> vals(kMaxPatternsPerColumn);
-    for (const DevPolicy& P : dp) {
-      if (P.family != FAM_LABELS) continue;
-      for (uint32_t k = 0; k < P.n_constr; ++k) {
-        auto& v = vals[P.idx[16 + k]];
-        if (std::find(v.begin(), v.end(), (uint32_t)P.idx[32 + k]) == v.end()) v.push_back(P.idx[32 + k]);
-      }
-    }
-    // one DFA per key while the union of its regexes stays small, else a short chain of DFAs
-    // (compile_column's greedy groups) instead of one large product automaton
-    std::vector<std::vector<Dfa>> kd(kMaxPatternsPerColumn);
-    bool ok = true;
-    for (size_t k = 0; k < vals.size() && ok; ++k) {
-      if (vals[k].empty()) continue;
-      std::vector<Pattern> pats;
-      for (uint32_t v : vals[k]) pats.push_back(env->cols[COL_LV][v]);
-      std::string err;
-      ok = compile_column(pats, kKvDfaBytes, &kd[k], &err);
-      for (Dfa& d : kd[k]) {
-        ok = ok && d.trans.size() * 2 <= kMaxDfaTableBytes;
-        for (uint64_t& a : d.accept) {  // local pattern bits -> the column's global bits
-          uint64_t g = 0;
-          for (size_t i = 0; i < vals[k].size(); ++i)
-            if ((a >> i) & 1ull) g |= 1ull << vals[k][i];
-          a = g;
-        }
-      }
-    }
-    for (size_t k = 0; k < kd.size() && ok; ++k)
-      for (const Dfa& d : kd[k]) ok = ok && d.nstates <= 256 && d.ncls <= 255;  // u8 transitions and classes
-    if (ok) {
-      std::vector<uint8_t> r;  // the region, region-relative offsets
-      r.resize(2 * kMaxPatternsPerColumn, 0);
-      std::map<std::vector<uint8_t>, uint16_t> cls_pool;
-      auto at16 = [&](size_t n) {  // reserve n bytes at a 16-B boundary
-        while (r.size() % 16) r.push_back(0);
-        const size_t o = r.size();
-        r.resize(o + n, 0);
-        return o;
-      };
-      std::vector<size_t> recs;  // KvDfa record positions, linked per key below
-      std::map<std::vector<uint8_t>, uint16_t> chains;  // keys constrained by the same regexes share one chain
-      for (size_t k = 0; k < kd.size(); ++k) {
-        if (kd[k].empty()) continue;
-        std::vector<uint8_t> sig;
-        for (const Dfa& d : kd[k]) {
-          const uint32_t hd[3] = {d.nstates, d.ncls, d.start};
-          sig.insert(sig.end(), (const uint8_t*)hd, (const uint8_t*)(hd + 3));
-          sig.insert(sig.end(), d.cls.begin(), d.cls.end());
-          sig.insert(sig.end(), (const uint8_t*)d.trans.data(), (const uint8_t*)(d.trans.data() + d.trans.size()));
-          sig.insert(sig.end(), (const uint8_t*)d.accept.data(), (const uint8_t*)(d.accept.data() + d.accept.size()));
-        }
-        auto hit = chains.find(sig);
-        if (hit != chains.end()) {
-          ((uint16_t*)r.data())[k] = hit->second;
-          continue;
-        }
-        size_t prev = 0;
-        for (const Dfa& d : kd[k]) {
-          KvDfa kv;
-          memset(&kv, 0, sizeof(kv));
-          bool uniform_hi = true;
-          for (int c = 128; c < 256; ++c) uniform_hi = uniform_hi && d.cls[c] == d.cls[128];
-          kv.wide = uniform_hi ? 0 : 1;
-          kv.hi = d.cls[128];
-          std::vector<uint8_t> cm(d.cls.begin(), d.cls.begin() + (kv.wide ? 256 : 128));
-          auto it = cls_pool.find(cm);
-          if (it == cls_pool.end()) {
-            const size_t o = at16(cm.size());
-            memcpy(r.data() + o, cm.data(), cm.size());
-            it = cls_pool.emplace(cm, (uint16_t)o).first;
-          }
-          kv.cls_off = it->second;
-          std::vector<uint64_t> accv;
-          std::vector<uint8_t> acc(d.nstates);
-          for (uint32_t q = 0; q < d.nstates; ++q) {
-            size_t x = std::find(accv.begin(), accv.end(), d.accept[q]) - accv.begin();
-            if (x == accv.size()) accv.push_back(d.accept[q]);
-            acc[q] = (uint8_t)x;  // nstates <= 256: at most 256 distinct masks
-          }
-          kv.ncls = (uint8_t)d.ncls;
-          kv.start = (uint8_t)d.start;
-          kv.nstates = (uint16_t)d.nstates;
-          const size_t rec = at16(sizeof(KvDfa));
-          kv.accv_off = (uint16_t)at16(accv.size() * 8);
-          memcpy(r.data() + kv.accv_off, accv.data(), accv.size() * 8);
-          kv.acc_off = (uint16_t)r.size();
-          r.insert(r.end(), acc.begin(), acc.end());
-          kv.trans_off = (uint16_t)r.size();
-          for (uint16_t tq : d.trans) r.push_back((uint8_t)tq);
-          memcpy(r.data() + rec, &kv, sizeof(kv));
-          if (prev) ((KvDfa*)(r.data() + prev))->next = (uint16_t)rec;
-          else ((uint16_t*)r.data())[k] = (uint16_t)rec;
-          prev = rec;
-          recs.push_back(rec);
-        }
-        chains.emplace(std::move(sig), ((uint16_t*)r.data())[k]);
-      }
-      while (r.size() % 16) r.push_back(0);
-      r.resize(r.size() + 16, 0);  // slack: dword-granular readers may run past the last table
-      ok = r.size() < 65536;        // u16 offsets
-      if (ok) {
-        align16(&b);
-        hdr.kv_off = (uint32_t)b.size();
-        hdr.kv_bytes = (uint32_t)r.size();
-        b.insert(b.end(), r.begin(), r.end());
-      }
-    }
-  }
-  align16(&b);
-  hdr.policy_off = (uint32_t)b.size();
-  for (auto& P : dp) put(&b, P);
-  align16(&b);
-  hdr.prog_off = (uint32_t)b.size();
-  b.insert(b.end(), progs.begin(), progs.end());
-  align16(&b);
-  hdr.member_off = (uint32_t)b.size();
-  for (int32_t m : mems) put(&b, m);
+  env->cols[COL_LV].class_pats.clear();
+  env->cols[COL_LV].lit_cls.assign(env->cols[COL_LV].pats.size(), 0);
+  if (Status st = compile_kv(env, &hdr, &b); !st.ok()) return st;
+  auto lit_class = [&](Col c, const char* s) -> uint32_t {
+    const ColumnInfo& ci = env->cols[c];
+    for (size_t p = 0; p < ci.pats.size(); ++p)
+      if (ci.pats[p].kind == Pattern::Literal && ci.pats[p].text == s) return ci.lit_cls[p];
+    return 0;
+  };
+  if (env->always_ns) hdr.bypass_cls = lit_class(COL_NS, env->always_ns->c_str());
+  hdr.docker_io_cls = lit_class(COL_REG, "docker.io");
+  hdr.latest_cls = lit_class(COL_TAG, "latest");
   align16(&b);
   hdr.magic = kBlobMagic;
   hdr.version = kBlobVersion;
-  hdr.npolicies = (uint32_t)env->pol.size();
   hdr.blob_bytes = (uint32_t)b.size();
-  hdr.bypass_bit = bypass_bit;
+  for (int c = 0; c < (int)NCOL; ++c) hdr.npatterns += (uint32_t)env->cols[c].pats.size();
   memcpy(b.data(), &hdr, sizeof(hdr));
   return {};
 }
@@ -832,6 +955,61 @@ Status env_validate_settings(const Env& env, int32_t idx) {
   if (!r.registered) return {KW_E_NOT_FOUND, "unknown policy: " + r.id};
   if (r.init_error) return {KW_E_INIT, r.init_message};
   return {};
+}
+
+// ---- host classification with the blob's tables (mirrors kernels.hip)
+namespace {
+uint32_t blob_lit(const uint8_t* blob, uint32_t off, const uint8_t* s, size_t n) {
+  const DevLit* L = (const DevLit*)(blob + off);
+  const uint8_t* rec = blob + off;
+  std::vector<uint32_t> w((n + 3) / 4, 0u);
+  if (n) memcpy(w.data(), s, n);
+  uint32_t h = lit_init(L->seed, (uint32_t)n);
+  for (uint32_t x : w) h = lit_mix(h, x);
+  const uint32_t g = lit_final(h);
+  const uint32_t d = L->nb_log2 ? ((const uint16_t*)(rec + L->disp_off))[g >> (32 - L->nb_log2)] : 0u;
+  const uint32_t* slot = (const uint32_t*)(rec + L->slot_off) + 2u * lit_slot_index(g, d, L->nslots);
+  if (!slot[0] || lit_slot_len(slot[0]) != n) return 0;
+  const uint32_t* pw = (const uint32_t*)(rec + L->word_off) + slot[1];
+  for (size_t i = 0; i < w.size(); ++i)
+    if (w[i] != pw[i]) return 0;
+  return lit_slot_cls(slot[0]);
+}
+uint32_t blob_dfa(const uint8_t* blob, uint32_t off, const uint8_t* s, size_t n) {
+  const DevDfa* d = (const DevDfa*)(blob + off);
+  const uint16_t* trans = (const uint16_t*)(blob + d->trans_off);
+  const uint16_t* acc = (const uint16_t*)(blob + d->acc_off);
+  uint32_t st = d->start;
+  for (size_t i = 0; i < n && st != 0; ++i) st = trans[(size_t)st * d->ncls + d->cls[s[i]]];
+  return acc[st];
+}
+}  // namespace
+
+std::vector<uint32_t> host_classes(const Env& env, Col c, const uint8_t* s, size_t n) {
+  const DevHeader* H = (const DevHeader*)env.blob.data();
+  const DevCol& dc = H->col[c];
+  std::vector<uint32_t> out;
+  if (dc.lit_off) out.push_back(blob_lit(env.blob.data(), dc.lit_off, s, n));
+  for (uint32_t o = dc.dfa_off; o; o = ((const DevDfa*)(env.blob.data() + o))->next)
+    out.push_back(blob_dfa(env.blob.data(), o, s, n));
+  return out;
+}
+
+std::vector<uint32_t> host_value_classes(const Env& env, uint32_t key, const uint8_t* s, size_t n) {
+  const DevHeader* H = (const DevHeader*)env.blob.data();
+  std::vector<uint32_t> out;
+  if (!H->kv_off || key == 0 || key >= H->col[COL_LK].nclass) return out;
+  const uint8_t* R = env.blob.data() + H->kv_off;
+  const uint32_t nlk = H->col[COL_LK].nclass;
+  const uint32_t kbase = ((const uint32_t*)R)[nlk + key];
+  for (uint32_t rel = ((const uint32_t*)R)[key]; rel;) {
+    const KvDfa& d = *(const KvDfa*)(R + rel);
+    uint32_t st = d.start;
+    for (size_t i = 0; i < n && st != 0; ++i) st = kv_step(R, d, st, s[i]);
+    out.push_back(kbase + d.cbase + ((const uint16_t*)(R + d.acc_off))[st]);
+    rel = d.next;
+  }
+  return out;
 }
 
 // Serialised environment (what rank 0 broadcasts): header, the policies document, the

@@ -4,8 +4,10 @@
 // :130-366) turns the policies document into an immutable registry of policies and groups; the
 // accessors (:373-469) answer mode / allowed-to-mutate / namespace-bypass / settings questions.
 // Where the reference registers a PolicyEvaluatorPre per Wasm digest (:391-431), this builder
-// compiles each policy's settings into column DFAs + bitmask parameters (kwdev.hpp) and emits one
-// position-independent blob that every GPU receives.
+// collects every string pattern the policies' settings name per request column and compiles each
+// column into a classifier (literal perfect hash, DFA chain, per-key label-value DFAs; kwdev.hpp),
+// emitted as one position-independent blob that every GPU receives. What each class means for each
+// policy is compiled per policy list (slotplan.cpp).
 #pragma once
 #include <cstdint>
 #include <optional>
@@ -35,6 +37,11 @@ struct PolicyRec {
   uint8_t flags = 0;        // PF_SKIP_INIT | PF_SKIP_EPHEMERAL | PF_ALLOW_ALL
   // settings lists, same meaning as the oracle (DESIGN.md §Policy families)
   std::vector<std::string> lists[5];
+  // the lists as pattern ids of their request column (env.cpp compile): namespace [0] COL_NS;
+  // trusted-repos [0,1] COL_REG, [2] COL_TAG, [3,4] COL_IMG; capabilities [0] allowed (without "*"),
+  // [1] required drops, [2] default adds, [3] {"ALL"} COL_CAP; apparmor [0] COL_AA; labels [0] denied,
+  // [1] mandatory (settings order), [2] constrained keys COL_LK, [3] their regexes COL_LV
+  std::vector<uint32_t> pid[5];
   // group
   std::string expression, message;
   std::vector<std::string> member_names;  // settings order
@@ -43,13 +50,29 @@ struct PolicyRec {
   std::string broken_member;  // member id that failed to initialise (validate -> PolicyNotFound)
 };
 
+// Host description of one column's classifier (the blob holds its tables).
+struct ColumnInfo {
+  std::vector<Pattern> pats;                      // pattern id = index
+  std::vector<std::vector<uint32_t>> class_pats;  // global class -> pattern ids it matches (class 0: none)
+  std::vector<uint32_t> lit_cls;                  // pattern id -> literal class (0 = not in the literal table)
+};
+
+// COL_LV class: label-key class `key`, the value regexes of the key's DFA that produced it
+// (`covered`) and those it matched.
+struct KvClass {
+  uint32_t key = 0;
+  std::vector<uint32_t> covered, matched;
+};
+
 struct Env {
   std::string source;  // the policies document (re-sent with the blob to other ranks)
   std::vector<PolicyRec> pol;
   std::unordered_map<std::string, int32_t> ids;
   std::optional<std::string> always_ns;
   bool continue_on_errors = false;
-  std::vector<Pattern> cols[NCOL];
+  ColumnInfo cols[NCOL];
+  std::vector<KvClass> kv;                    // per COL_LV class
+  std::vector<std::vector<uint32_t>> kv_of_key;  // label-key class -> its COL_LV classes
   std::vector<uint8_t> blob;  // compiled tables (host copy)
   // device copy
   int device = -1;
@@ -73,5 +96,12 @@ Status env_lookup(const Env& env, const std::string& id, int32_t* idx);
 Status env_validate_settings(const Env& env, int32_t idx);
 
 const char* family_name(uint8_t fam);
+
+// Host classification with the blob's tables (diagnostics and the host walk; the kernels run the
+// same tables). Classes of string s in column c: the literal class when the column has a literal
+// table, then one per DFA of the chain (COL_NS / COL_REG / COL_TAG / COL_IMG / COL_CAP / COL_AA / COL_LK).
+std::vector<uint32_t> host_classes(const Env& env, Col c, const uint8_t* s, size_t n);
+// COL_LV classes of value s under label-key class `key` (one per DFA of the key's chain).
+std::vector<uint32_t> host_value_classes(const Env& env, uint32_t key, const uint8_t* s, size_t n);
 
 }  // namespace kw

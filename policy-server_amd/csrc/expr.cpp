@@ -326,6 +326,8 @@ bool check(Node* n, std::string* err) {
   return true;
 }
 
+// Short-circuit jump code (kwdev.hpp GOp): a || b = a, JT end, b; a && b = a, JF end, b; the other
+// operators evaluate both sides. Only == / != deepen the value stack.
 void emit(const Node* n, std::vector<uint8_t>* code, int depth, int* maxdepth) {
   if (depth > *maxdepth) *maxdepth = depth;
   switch (n->k) {
@@ -341,11 +343,18 @@ void emit(const Node* n, std::vector<uint8_t>* code, int depth, int* maxdepth) {
     case Node::Neg: return;  // folded
     case Node::Bin:
       emit(n->a.get(), code, depth, maxdepth);
+      if (n->op == "&&" || n->op == "||") {
+        code->push_back(n->op == "&&" ? G_JF : G_JT);
+        const size_t at = code->size();
+        code->push_back(0);
+        code->push_back(0);
+        emit(n->b.get(), code, depth, maxdepth);
+        (*code)[at] = (uint8_t)(code->size() & 0xff);
+        (*code)[at + 1] = (uint8_t)(code->size() >> 8);
+        return;
+      }
       emit(n->b.get(), code, depth + 1, maxdepth);
-      if (n->op == "&&") code->push_back(G_AND);
-      else if (n->op == "||") code->push_back(G_OR);
-      else if (n->op == "==") code->push_back(G_EQ);
-      else code->push_back(G_NE);
+      code->push_back(n->op == "==" ? G_EQ : G_NE);
       return;
   }
 }
@@ -382,9 +391,9 @@ GroupProgram compile_group_expression(const std::string& expr, const std::vector
   }
   int maxd = 1;
   emit(root.get(), &g.code, 1, &maxd);
-  if (maxd > kMaxGroupStack) {
+  if (maxd > kMaxGroupStack || g.code.size() > 65535) {
     g.valid = false;
-    g.error = "policy group expression nests too deeply for the engine (max stack 16)";
+    g.error = "policy group expression nests too deeply for the engine (max stack 64)";
     g.code.clear();
   }
   return g;

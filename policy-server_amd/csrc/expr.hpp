@@ -7,9 +7,9 @@
 //   invalid: "unknown_policy() || happy_policy_1()" (function not found),
 //            "something that doesn't make sense" (syntax), "happy_policy_1() + 1" (bool + int)
 // and evaluated with rhai's short-circuit || and && (evaluation_environment.rs:979-1042): a member
-// contributes a cause only if it was actually called. The device evaluates members eagerly and
-// tracks, per stack entry, the mask of members rhai would have called (AND: e1 | (v1 ? e2 : 0),
-// OR: e1 | (v1 ? 0 : e2)), which gives the same causes.
+// contributes a cause only if it was actually called. The device evaluates every member eagerly
+// (one slot each), then runs the expression as short-circuit jump code over the member results: a
+// member counts as called exactly when rhai would have called it, which gives the same causes.
 #pragma once
 #include <cstdint>
 #include <string>
@@ -22,7 +22,7 @@ struct GroupProgram {
   std::string error;           // message when !valid
   bool eval_error = false;     // valid, but the result is not a bool (e.g. "1 + 1")
   std::string eval_message;
-  std::vector<uint8_t> code;   // G_* ops; G_CALL is followed by the member slot byte
+  std::vector<uint8_t> code;   // G_* jump code (kwdev.hpp): G_CALL + slot byte, G_JT / G_JF + u16 target
 };
 
 // members: member names in settings order (the slot of a call is its index here).

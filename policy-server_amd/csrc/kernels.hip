@@ -3,22 +3,22 @@
 // service::evaluate epilogue (src/api/service.rs:40-116, 160-208).
 //
 // Kernels:
-//  evaluate_slots_kernel — the all-pairs hot path (kw_validate_batch). Persistent 256-thread
-//                     workgroups, several per CU, each owning a 64-request tile at a time: stage the
-//                     tile's columns into LDS, classify every string there (literal perfect hash,
-//                     per-key value DFA, image DFA chains), walk each request's entities once with
-//                     the bit-parallel slot tables (slots.hpp: one lane per request, one wave per
-//                     family group), then write the verdict rows with coalesced 16-B stores.
-//  classify_kernel  — two-kernel form for automata too large for LDS: one lane per string, masks
-//                     to HBM; the slot kernel then stages the masks instead of the strings.
-//  overflow_kernel  — tiles whose entity counts exceed the LDS capacities, from global memory.
-//  evaluate_rows_kernel — micro-batch form (kw_validate_rows): one lane per (row, its policy).
+//  evaluate_tiles_kernel — the hot path (kw_validate_batch, kw_validate_rows). Persistent 256-thread
+//      workgroups, several per CU, each owning a tile of up to 64 requests at a time: stage the
+//      tile's columns into LDS, classify every string into its column class (literal perfect hash,
+//      DFA chains, per-key label-value DFAs; kwdev.hpp), then for each slot-plan chunk of the policy
+//      list derive every entity's violation set from the chunk's class tables, find each slot's first
+//      violation entity-parallel, and write the verdict words with coalesced 16-B stores.
+//  overflow_classify_kernel / overflow_eval_kernel — requests whose entities exceed the tile
+//      capacities even alone: classes into HBM, then the sequential walks of slots.hpp per request.
 // The verdict word (include/kwgpu.h) carries the vanilla response and the service-level result.
 // Integer / byte work only: no MFMA. Bound: HBM streaming of request bytes in and verdict words
 // out.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstddef>
+#include <mutex>
 
 #include "../../include/kwgpu.h"
 #include "kernels.hpp"
@@ -26,42 +26,96 @@
 namespace kw {
 
 // ------------------------------------------------------------------------------------------
-// DFA views
+// Classification (LDS or global tables; `bytes` may be LDS-staged strings or an HBM pool, both
+// padded so the dword reads below never leave their buffer)
 // ------------------------------------------------------------------------------------------
+__device__ inline uint32_t align_bytes(uint32_t hi, uint32_t lo, uint32_t sh) {
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * sh));
+}
+__device__ inline uint32_t lit_word(const uint32_t* base, uint32_t i, uint32_t sh, uint32_t len) {
+  const uint32_t w = align_bytes(base[i + 1], base[i], sh);
+  const uint32_t rem = len - 4u * i;
+  return rem >= 4u ? w : (w & ((1u << (8u * rem)) - 1u));
+}
+
+// Literal class of bytes [b, e) (DevLit, kwdev.hpp), 0 = no literal pattern. BATCH: the first 32
+// bytes of the string and of the candidate pattern are read in one batch each (up to 36 bytes past
+// the string start: LDS staging slack); otherwise word by word (<= 7 bytes past the end).
+template <bool BATCH>
+__device__ inline uint32_t lit_lookup(const uint8_t* rec, const uint8_t* bytes, uint32_t b, uint32_t e) {
+  const DevLit* L = (const DevLit*)rec;
+  const uint32_t len = e - b, sh = b & 3u, nw = (len + 3u) >> 2;
+  const uint32_t* base = (const uint32_t*)(bytes + (b & ~3u));
+  uint32_t h = lit_init(L->seed, len);
+  uint32_t w[8];
+  if (BATCH) {
+    uint32_t raw[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) raw[i] = base[i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t x = align_bytes(raw[i + 1], raw[i], sh);
+      const uint32_t rem = len - 4u * (uint32_t)i;
+      w[i] = rem >= 4u ? x : (x & ((1u << (8u * rem)) - 1u));
+      if ((uint32_t)i < nw) h = lit_mix(h, w[i]);
+    }
+    for (uint32_t i = 8; i < nw; ++i) h = lit_mix(h, lit_word(base, i, sh, len));
+  } else {
+    for (uint32_t i = 0; i < nw; ++i) h = lit_mix(h, lit_word(base, i, sh, len));
+  }
+  const uint32_t g = lit_final(h);
+  const uint32_t d = L->nb_log2 ? ((const uint16_t*)(rec + L->disp_off))[g >> (32u - L->nb_log2)] : 0u;
+  const uint2 sl = ((const uint2*)(rec + L->slot_off))[lit_slot_index(g, d, L->nslots)];
+  if (!sl.x || lit_slot_len(sl.x) != len) return 0u;
+  const uint32_t* pw = (const uint32_t*)(rec + L->word_off) + sl.y;
+  bool eq = true;
+  if (BATCH) {
+    uint32_t pv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) pv[i] = pw[i];  // zero tail of the words section covers short patterns
+#pragma unroll
+    for (int i = 0; i < 8; ++i) eq = eq && ((uint32_t)i >= nw || w[i] == pv[i]);
+    for (uint32_t i = 8; i < nw && eq; ++i) eq = lit_word(base, i, sh, len) == pw[i];
+  } else {
+    for (uint32_t i = 0; i < nw && eq; ++i) eq = lit_word(base, i, sh, len) == pw[i];
+  }
+  return eq ? lit_slot_cls(sl.x) : 0u;
+}
+
+// A column's DFA chain, staged contiguously (LDS) or read from the blob: element at blob offset
+// `off` lives at base + (off - head).
+struct Chain {
+  const uint8_t* base;
+  uint32_t head;
+};
 struct DfaView {
   const uint8_t* cls;     // 256
   const uint16_t* trans;  // [state][ncls]
-  const uint64_t* acc;    // [state]
+  const uint16_t* acc;    // [state] global class
   uint32_t ncls, start;
-  bool valid;
 };
-
-__device__ inline DfaView make_view(const uint8_t* base, const uint8_t* blob, uint32_t dfa_off) {
-  // base points at the staged copy of the DevDfa record at blob offset dfa_off (LDS or the blob)
-  DfaView v;
+__device__ inline DfaView chain_view(const Chain& c, uint32_t off) {
+  const uint8_t* base = c.base + (off - c.head);
   const DevDfa* h = (const DevDfa*)base;
+  DfaView v;
   v.cls = h->cls;
   v.ncls = h->ncls;
   v.start = h->start;
-  v.trans = (const uint16_t*)(base + (h->trans_off - dfa_off));
-  v.acc = (const uint64_t*)(base + (h->acc_off - dfa_off));
-  v.valid = true;
-  (void)blob;
+  v.trans = (const uint16_t*)(base + (h->trans_off - off));
+  v.acc = (const uint16_t*)(base + (h->acc_off - off));
   return v;
 }
+__device__ inline uint32_t chain_next(const Chain& c, uint32_t off) { return ((const DevDfa*)(c.base + (off - c.head)))->next; }
 
-__device__ inline uint32_t step(const DfaView& d, uint32_t st, uint32_t byte) {
-  return d.trans[st * d.ncls + d.cls[byte]];
-}
+__device__ inline uint32_t step(const DfaView& d, uint32_t st, uint32_t byte) { return d.trans[st * d.ncls + d.cls[byte]]; }
 
-// Walk bytes [b, e) of a global pool with 4-byte aligned loads (pools carry a 16 B zero tail).
-__device__ inline uint32_t feed(const DfaView& d, uint32_t st, const uint8_t* __restrict__ bytes, uint32_t b,
-                                uint32_t e) {
+// Walk bytes [b, e) with 4-byte aligned loads (pools and staged strings carry a zero tail).
+__device__ inline uint32_t feed(const DfaView& d, uint32_t st, const uint8_t* __restrict__ bytes, uint32_t b, uint32_t e) {
   uint32_t p = b;
   while (p < e && st != 0) {
     uint32_t w = *(const uint32_t*)(bytes + (p & ~3u));
-    uint32_t k = p & 3u;
-    uint32_t lim = min(4u - k, e - p);
+    const uint32_t k = p & 3u;
+    const uint32_t lim = min(4u - k, e - p);
     w >>= 8u * k;
     for (uint32_t j = 0; j < lim; ++j) {
       st = step(d, st, w & 0xffu);
@@ -85,71 +139,16 @@ __device__ inline uint32_t feed_const(const DfaView& d, uint32_t st, const char 
   return st;
 }
 
-__device__ inline uint32_t byte_at(const uint8_t* __restrict__ bytes, uint32_t p) { return bytes[p]; }
-
 template <int N>
 __device__ inline bool equals_const(const uint8_t* __restrict__ bytes, uint32_t b, uint32_t e, const char (&s)[N]) {
   if ((int)(e - b) != N - 1) return false;
 #pragma unroll
   for (int i = 0; i < N - 1; ++i)
-    if (byte_at(bytes, b + (uint32_t)i) != (uint8_t)s[i]) return false;
+    if (bytes[b + (uint32_t)i] != (uint8_t)s[i]) return false;
   return true;
 }
 
-// Literal-column lookup (DevLit, kwdev.hpp): hash the string's canonical dwords, probe one slot,
-// verify against the pattern's words. `rec` and `bytes` may be LDS or global; dwords are read at
-// 4-aligned addresses and realigned with v_alignbyte (reads may touch <= 7 bytes past the string,
-// inside the pool's zero pad or the staged tile's slack).
-__device__ inline uint32_t lit_word(const uint32_t* base, uint32_t i, uint32_t sh, uint32_t len) {
-  uint32_t w = __builtin_amdgcn_alignbyte(base[i + 1], base[i], sh);
-  const uint32_t rem = len - 4u * i;
-  return rem >= 4u ? w : (w & ((1u << (8u * rem)) - 1u));
-}
-__device__ inline uint64_t lit_lookup(const uint8_t* rec, const uint8_t* bytes, uint32_t b, uint32_t e) {
-  // LDS only: the first 32 bytes of the string and of the candidate pattern are read in one batch
-  // each (up to 36 bytes past the string: staged slack / other LDS; masked off by len)
-  const DevLit* L = (const DevLit*)rec;
-  const uint32_t len = e - b, sh = b & 3u, nw = (len + 3u) >> 2;
-  const uint32_t* base = (const uint32_t*)(bytes + (b & ~3u));
-  uint32_t raw[9], w[8];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) raw[i] = base[i];
-  uint32_t h = lit_init(L->seed, len);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const uint32_t x = __builtin_amdgcn_alignbyte(raw[i + 1], raw[i], sh);
-    const uint32_t rem = len - 4u * (uint32_t)i;  // >= 4: whole dword
-    w[i] = rem >= 4u ? x : (x & ((1u << (8u * rem)) - 1u));
-    if ((uint32_t)i < nw) h = lit_mix(h, w[i]);
-  }
-  for (uint32_t i = 8; i < nw; ++i) h = lit_mix(h, lit_word(base, i, sh, len));
-  h = lit_final(h);
-  const uint32_t s = ((const uint32_t*)(rec + L->slot_off))[h & (L->nslots - 1u)];
-  if (!s || lit_slot_len(s) != len) return 0ull;
-  const uint32_t* pw = (const uint32_t*)(rec + L->word_off) + lit_slot_word(s);
-  uint32_t pv[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) pv[i] = pw[i];  // zero tail of the words section covers short patterns
-  bool eq = true;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) eq = eq && ((uint32_t)i >= nw || w[i] == pv[i]);
-  for (uint32_t i = 8; i < nw && eq; ++i) eq = lit_word(base, i, sh, len) == pw[i];
-  return eq ? 1ull << (lit_slot_pat(s) - 1u) : 0ull;
-}
-
-// A column's DFA chain, staged contiguously (LDS, or the blob itself): element at blob offset
-// `off` lives at base + (off - head).
-struct Chain {
-  const uint8_t* base;
-  uint32_t head;
-};
-
-__device__ inline DfaView chain_view(const Chain& c, uint32_t off) { return make_view(c.base + (off - c.head), nullptr, off); }
-__device__ inline uint32_t chain_next(const Chain& c, uint32_t off) {
-  return ((const DevDfa*)(c.base + (off - c.head)))->next;
-}
-
-// Parsed image reference (oracle: orc_image_parts).
+// Parsed image reference (DESIGN.md §2 trusted-repos; oracle: orc_image_parts).
 struct ImageRef {
   uint32_t b, e, at, slash0, rest_b, colon, path_end, name_end;
   bool is_reg, path_slash, is_docker, eff_tag;
@@ -163,13 +162,13 @@ __device__ ImageRef parse_image(const uint8_t* __restrict__ bytes, uint32_t b, u
   bool stop = false;
   while (p < e && !stop) {
     uint32_t w = *(const uint32_t*)(bytes + (p & ~3u));
-    uint32_t k = p & 3u;
-    uint32_t lim = min(4u - k, e - p);
+    const uint32_t k = p & 3u;
+    const uint32_t lim = min(4u - k, e - p);
     w >>= 8u * k;
     for (uint32_t j = 0; j < lim; ++j) {
-      uint32_t c = w & 0xffu;
+      const uint32_t c = w & 0xffu;
       w >>= 8;
-      uint32_t q = p + j;
+      const uint32_t q = p + j;
       if (c == '@') {
         at = q;
         stop = true;
@@ -197,15 +196,15 @@ __device__ ImageRef parse_image(const uint8_t* __restrict__ bytes, uint32_t b, u
   r.rest_b = r.is_reg ? slash0 + 1 : b;
   r.colon = (last_colon != NONE && last_colon >= r.rest_b) ? last_colon : NONE;
   r.path_end = r.colon != NONE ? r.colon : r.name_end;
-  uint32_t first_slash_rest = r.is_reg ? slash1 : slash0;
+  const uint32_t first_slash_rest = r.is_reg ? slash1 : slash0;
   r.path_slash = first_slash_rest != NONE && first_slash_rest < r.path_end;
   r.is_docker = !r.is_reg || equals_const(bytes, b, slash0, kDockerIo);
   r.eff_tag = r.colon != NONE || at == NONE;
   return r;
 }
 
-// Registry (k=0), effective tag (k=1) or normalised image (k=2) through one DFA.
-__device__ uint64_t image_part(int k, const DfaView& d, const uint8_t* __restrict__ bytes, const ImageRef& r) {
+// Registry (k=0), effective tag (k=1) or normalised image (k=2) through one DFA: its class.
+__device__ uint32_t image_part(int k, const DfaView& d, const uint8_t* __restrict__ bytes, const ImageRef& r) {
   const uint32_t NONE = 0xffffffffu;
   uint32_t st = d.start;
   if (k == 0) {
@@ -213,7 +212,7 @@ __device__ uint64_t image_part(int k, const DfaView& d, const uint8_t* __restric
   } else if (k == 1) {
     if (r.colon != NONE) st = feed(d, st, bytes, r.colon + 1, r.name_end);
     else if (r.at == NONE) st = feed_const(d, st, kLatest);
-    else return 0ull;  // digest only: no tag
+    else return 0u;  // digest only: no tag
   } else {
     st = r.is_reg ? feed(d, st, bytes, r.b, r.slash0) : feed_const(d, st, kDockerIo);
     if (st) st = step(d, st, '/');
@@ -228,367 +227,111 @@ __device__ uint64_t image_part(int k, const DfaView& d, const uint8_t* __restric
   return d.acc[st];
 }
 
-template <bool USE_LDS>
-__global__ void __launch_bounds__(kClassifyThreads) classify_kernel(const uint8_t* __restrict__ blob, ClassifyJobs jobs) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const uint32_t bid = blockIdx.x;
-  int jx = 0;
-  for (int k = 1; k < jobs.n; ++k)
-    if (bid >= jobs.j[k].block_begin) jx = k;
-  const ClassifyJob& J = jobs.j[jx];
-
-  Chain ch[3];
-  if (USE_LDS) {
-    // stage this job's DFA chains into LDS (16 B per lane per step, coalesced)
-    for (int k = 0; k < 3; ++k) {
-      if (!J.dfa[k]) continue;
-      const DevDfa* h = (const DevDfa*)(blob + J.dfa[k]);
-      uint32_t nbytes = h->chain_bytes;
-      const uint4* src = (const uint4*)(blob + J.dfa[k]);
-      uint4* dst = (uint4*)(lds + J.lds_pos[k]);
-      for (uint32_t i = threadIdx.x; i < nbytes / 16; i += blockDim.x) dst[i] = src[i];
-    }
-    __syncthreads();
-  }
-  for (int k = 0; k < 3; ++k) {
-    ch[k].head = J.dfa[k];
-    ch[k].base = USE_LDS ? lds + J.lds_pos[k] : blob + J.dfa[k];
-  }
-
-  const uint32_t lb = bid - J.block_begin;
-  const uint32_t stride = J.nblocks * kClassifyThreads;
-  const uint32_t* __restrict__ off = J.off;
-  const uint8_t* __restrict__ bytes = J.bytes;
-  for (uint32_t i = lb * kClassifyThreads + threadIdx.x; i < J.n; i += stride) {
-    const uint32_t b = off[i], e = off[i + 1];
-    if (J.mode == 0) {
-      uint64_t m = 0;
-      for (uint32_t o = ch[0].head; o; o = chain_next(ch[0], o)) {
-        DfaView v = chain_view(ch[0], o);
-        m |= v.acc[feed(v, v.start, bytes, b, e)];
-      }
-      J.out[0][i] = m;
-    } else {
-      const ImageRef r = parse_image(bytes, b, e);
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        if (!ch[k].head) continue;
-        uint64_t m = 0;
-        for (uint32_t o = ch[k].head; o; o = chain_next(ch[k], o)) m |= image_part(k, chain_view(ch[k], o), bytes, r);
-        J.out[k][i] = m;
-      }
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// Policy evaluation
-// ------------------------------------------------------------------------------------------
-// Policy fields are read as whole dwords: with wave-uniform policy indices and __restrict__ kernel
-// parameters the loads become scalar (s_load, K$), the bytes are extracted with SALU ops.
-__device__ inline uint32_t pword(const DevPolicy& P, uint32_t w) { return ((const uint32_t*)&P)[w]; }
-__device__ inline uint32_t pbyte(const DevPolicy& P, uint32_t off) { return (pword(P, off >> 2) >> (8u * (off & 3u))) & 0xffu; }
-// byte offsets within DevPolicy (kwdev.hpp)
-constexpr uint32_t PB_FAMILY = 0, PB_MODE = 1, PB_A2M = 2, PB_FLAGS = 3, PB_NL = 4, PB_NMAND = 10, PB_NCONSTR = 11, PB_IDX = 80;
-static_assert(offsetof(DevPolicy, nl) == PB_NL && offsetof(DevPolicy, n_mand) == PB_NMAND &&
-                  offsetof(DevPolicy, n_constr) == PB_NCONSTR && offsetof(DevPolicy, idx) == PB_IDX,
-              "DevPolicy byte offsets");
-
-struct FamOut {
-  uint32_t reason, arg;
-  bool mutated;
+// The classifiers of one launch, resolved to LDS or blob pointers.
+struct Classifiers {
+  const uint8_t* lit[NCOL];  // DevLit records, nullptr = none
+  Chain dfa[NCOL];           // head 0 = none
+  const uint8_t* kv;         // per-key label-value region, nullptr = none
+  uint32_t nlk, docker_io_cls, latest_cls;
 };
 
-// Column accessors of the overflow and row kernels: the HBM arrays, absolute indices.
-struct GlobalSrc {
-  const EvalArgs* a;
-  __device__ uint8_t rf(uint64_t r) const { return a->req_flags[r]; }
-  __device__ uint32_t coff(uint64_t r) const { return a->ctr_off[r]; }
-  __device__ uint32_t loff(uint64_t r) const { return a->lbl_off[r]; }
-  __device__ uint8_t cflags(uint32_t c) const { return a->ctr_flags[c]; }
-  __device__ uint32_t cadd(uint32_t c) const { return a->capadd_off[c]; }
-  __device__ uint32_t cdrop(uint32_t c) const { return a->capdrop_off[c]; }
-  template <int K>
-  __device__ uint64_t m(uint64_t i) const { return a->m[K] ? a->m[K][i] : 0ull; }
-};
-
-template <class S>
-__device__ FamOut eval_family(const S& src, const DevPolicy& P, uint64_t r) {
-  FamOut o{0, 0, false};
-  const uint8_t rf = src.rf(r);
-  const uint32_t cb = src.coff(r), ce = src.coff(r + 1);
-  switch (pbyte(P, PB_FAMILY)) {
-    case FAM_PRIVILEGED: {
-      if (!(rf & KW_REQ_HAS_PODSPEC)) break;
-      for (uint32_t c = cb; c < ce; ++c) {
-        uint8_t f = src.cflags(c);
-        bool skip = ((pbyte(P, PB_FLAGS) & PF_SKIP_INIT) && (f & KW_CTR_INIT)) || ((pbyte(P, PB_FLAGS) & PF_SKIP_EPHEMERAL) && (f & KW_CTR_EPHEMERAL));
-        if (!skip && (f & KW_CTR_PRIVILEGED)) {
-          o.reason = KW_R_PRIVILEGED;
-          o.arg = pack1(c - cb);
-          break;
-        }
-      }
-      break;
-    }
-    case FAM_NAMESPACE: {
-      bool ok = (rf & KW_REQ_HAS_NAMESPACE) && pbyte(P, PB_NL + (0)) && (src.template m<M_NS>(r) & P.m[0]);
-      if (!ok) o.reason = KW_R_NAMESPACE;
-      break;
-    }
-    case FAM_TRUSTED_REPOS: {
-      if (!(rf & KW_REQ_HAS_PODSPEC)) break;
-      for (uint32_t c = cb; c < ce; ++c) {
-        if (!(src.cflags(c) & KW_CTR_HAS_IMAGE)) continue;
-        uint64_t reg = src.template m<M_REG>(c), tag = src.template m<M_TAG>(c), img = src.template m<M_IMG>(c);
-        uint32_t why = 0;
-        if (pbyte(P, PB_NL + (0)) && !(reg & P.m[0])) why = KW_R_REG_NOT_ALLOWED;
-        else if (pbyte(P, PB_NL + (1)) && (reg & P.m[1])) why = KW_R_REG_REJECTED;
-        else if (pbyte(P, PB_NL + (2)) && (tag & P.m[2])) why = KW_R_TAG_REJECTED;
-        else if (pbyte(P, PB_NL + (3)) && !(img & P.m[3])) why = KW_R_IMG_NOT_ALLOWED;
-        else if (pbyte(P, PB_NL + (4)) && (img & P.m[4])) why = KW_R_IMG_REJECTED;
-        if (why) {
-          o.reason = why;
-          o.arg = pack1(c - cb);
-          break;
-        }
-      }
-      break;
-    }
-    case FAM_CAPABILITIES: {
-      if (!(rf & KW_REQ_HAS_PODSPEC)) break;
-      for (uint32_t c = cb; c < ce; ++c) {
-        const uint32_t kb = src.cadd(c), ke = src.cadd(c + 1);
-        uint64_t addm = 0, dropm = 0;
-        for (uint32_t k = kb; k < ke; ++k) {
-          uint64_t mk = src.template m<M_CAPADD>(k);
-          addm |= mk;
-          if (!(pbyte(P, PB_FLAGS) & PF_ALLOW_ALL) && !(mk & P.m[0])) {
-            o.reason = KW_R_CAP_NOT_ALLOWED;
-            o.arg = pack2(c - cb, k - kb);
-            break;
-          }
-        }
-        if (o.reason) break;
-        for (uint32_t k = src.cdrop(c); k < src.cdrop(c + 1); ++k) dropm |= src.template m<M_CAPDROP>(k);
-        if (!(dropm & P.m[3]) && (P.m[1] & ~dropm)) o.mutated = true;
-        if (P.m[2] & ~(addm | dropm)) o.mutated = true;
-      }
-      if (o.reason) o.mutated = false;
-      break;
-    }
-    case FAM_APPARMOR: {
-      if (!(rf & KW_REQ_HAS_PODSPEC)) break;
-      for (uint32_t c = cb; c < ce; ++c) {
-        if ((src.cflags(c) & KW_CTR_HAS_APPARMOR) && !(src.template m<M_AA>(c) & P.m[0])) {
-          o.reason = KW_R_APPARMOR;
-          o.arg = pack1(c - cb);
-          break;
-        }
-      }
-      break;
-    }
-    case FAM_LABELS: {
-      const uint32_t lb = src.loff(r), le = src.loff(r + 1);
-      uint64_t present = 0;
-      for (uint32_t l = lb; l < le && !o.reason; ++l) {
-        uint64_t km = src.template m<M_LK>(l);
-        present |= km;
-        if (km & P.m[0]) {
-          o.reason = KW_R_LABEL_DENIED;
-          o.arg = pack1(l - lb);
-          break;
-        }
-        if (km) {
-          const uint64_t vm = src.template m<M_LV>(l);
-          for (uint32_t i = 0; i < pbyte(P, PB_NCONSTR); ++i) {
-            if (((km >> pbyte(P, PB_IDX + (16 + i))) & 1ull) && !((vm >> pbyte(P, PB_IDX + (32 + i))) & 1ull)) {
-              o.reason = KW_R_LABEL_CONSTRAINT;
-              o.arg = pack2(l - lb, i);
-              break;
-            }
-          }
-        }
-      }
-      if (o.reason) break;
-      for (uint32_t i = 0; i < pbyte(P, PB_NMAND); ++i)
-        if (!((present >> pbyte(P, PB_IDX + (i))) & 1ull)) {
-          o.reason = KW_R_LABEL_MANDATORY;
-          o.arg = i;
-          break;
-        }
-      break;
-    }
-    default: break;
-  }
-  return o;
-}
-
-// EvaluationEnvironment::validate + service::evaluate constraints for one (request, policy).
-template <class S>
-__device__ uint32_t verdict(const S& src, const EvalArgs& a, const DevHeader& H, const DevPolicy* __restrict__ pols,
-                            const DevPolicy& P, uint64_t r, uint16_t* gstk, uint32_t gstride) {
-  const uint8_t rf = src.rf(r);
-  // namespace bypass (service.rs:40-71), AdmissionRequest only
-  if (H.bypass_bit >= 0 && !(rf & KW_REQ_RAW) && (rf & KW_REQ_HAS_NAMESPACE) &&
-      ((src.template m<M_NS>(r) >> H.bypass_bit) & 1ull))
-    return KW_V_ALLOWED | KW_F_ALLOWED | KW_BYPASS;
-  // PolicyInitialization -> reject 500 before any constraint (service.rs:78-91)
-  if (pbyte(P, PB_FLAGS) & PF_INIT_ERROR) return ((uint32_t)KW_FST_INIT_ERROR << KW_F_STATUS_SHIFT) | ((uint32_t)KW_R_INIT_ERROR << 8);
-  uint32_t reason = 0, arg = 0;
-  bool mutated = false;
-  if (pbyte(P, PB_FAMILY) == FAM_GROUP) {
-    if (pbyte(P, PB_FLAGS) & PF_EXPR_ERROR) {
-      reason = KW_R_GROUP_EXPR;
-    } else {
-      const int32_t* mem = (const int32_t*)(a.blob + H.member_off) + P.member_off;
-      uint32_t ok = 0;
-      for (uint32_t s = 0; s < P.nmembers; ++s) {
-        const DevPolicy& Q = pols[mem[s]];
-        if (pbyte(Q, PB_FLAGS) & PF_INIT_ERROR) continue;
-        FamOut fo = eval_family(src, Q, r);
-        if (fo.reason == 0 && !fo.mutated) ok |= 1u << s;
-      }
-      uint32_t causes;
-      if (!run_group_prog(a.blob + H.prog_off + P.prog_off, P.prog_len, ok, gstk, gstride, &causes)) {
-        reason = KW_R_GROUP;
-        arg = causes;
-      }
-    }
-  } else {
-    FamOut fo = eval_family(src, P, r);
-    reason = fo.reason;
-    arg = fo.arg;
-    mutated = fo.mutated;
-  }
-  return finish_word(pbyte(P, PB_MODE), pbyte(P, PB_A2M), a.origin, reason, arg, mutated);
-}
-
-// Micro-batch form (kw_validate_rows): one lane per row, each row with its own policy.
-__global__ void __launch_bounds__(kEvalThreads) evaluate_rows_kernel(EvalArgs a) {
-  __shared__ uint16_t gstk[kMaxGroupStack * kEvalThreads];
-  const DevHeader H = *(const DevHeader*)a.blob;
-  const DevPolicy* __restrict__ pols = (const DevPolicy*)(a.blob + H.policy_off);
-  GlobalSrc src{&a};
-  const uint64_t stride = (uint64_t)gridDim.x * kEvalThreads;
-  for (uint64_t r = (uint64_t)blockIdx.x * kEvalThreads + threadIdx.x; r < a.nrows; r += stride) {
-    const DevPolicy& P = pols[a.row_policy[r]];
-    a.out[r] = verdict(src, a, H, pols, P, r, gstk + threadIdx.x, kEvalThreads);
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// All-pairs slot kernel (evaluate_slots_kernel). A workgroup owns a tile of 64 consecutive
-// requests at a time (persistent grid, several workgroups per CU so one tile's staging latency hides
-// under another's walk). Per tile:
-//  P0 stage the tile's request headers, container offsets and string bytes into LDS (coalesced
-//     16-B loads; byte ranges come from the host-built TileDesc, so there is no dependent
-//     global-load chain);
-//  P1 classify every staged string from LDS-resident tables (literal perfect hash, per-key label
-//     value DFA, image DFA chains);
-//  P2 walk each request's entities once with the slot tables (slots.hpp), lane = request, one wave
-//     per family group;
-//  P3 write the verdict rows (ABI layout, row-major) with coalesced 16-B stores.
-// A tile whose entity counts exceed the LDS capacities is left to overflow_kernel.
-// ------------------------------------------------------------------------------------------
-template <int K>
-__device__ inline uint64_t classify_one(const Chain& ch, const uint8_t* __restrict__ bytes, uint32_t b, uint32_t e) {
-  uint64_t m = 0;
-  for (uint32_t o = ch.head; o; o = chain_next(ch, o)) {
-    DfaView v = chain_view(ch, o);
-    m |= v.acc[feed(v, v.start, bytes, b, e)];
-  }
-  return m;
-}
-
-__device__ inline void classify_image_all(const Chain cr, const Chain ct, const Chain ci, const uint8_t* __restrict__ bytes,
-                                          uint32_t b, uint32_t e, uint64_t* mr, uint64_t* mt, uint64_t* mi) {
+// All classes of one image reference: il.nreg COL_REG entries (literal, DFAs), il.ntag COL_TAG
+// entries, il.nimg COL_IMG entries.
+template <bool BATCH, class Out>
+__device__ inline void classify_image(const Classifiers& C, const ImgLayout& il, const uint8_t* __restrict__ bytes,
+                                      uint32_t b, uint32_t e, Out out) {
+  const uint32_t NONE = 0xffffffffu;
   const ImageRef r = parse_image(bytes, b, e);
-  uint64_t m0 = 0, m1 = 0, m2 = 0;
-  for (uint32_t o = cr.head; o; o = chain_next(cr, o)) m0 |= image_part(0, chain_view(cr, o), bytes, r);
-  for (uint32_t o = ct.head; o; o = chain_next(ct, o)) m1 |= image_part(1, chain_view(ct, o), bytes, r);
-  for (uint32_t o = ci.head; o; o = chain_next(ci, o)) m2 |= image_part(2, chain_view(ci, o), bytes, r);
-  *mr = m0;
-  *mt = m1;
-  *mi = m2;
+  uint32_t j = 0;
+  if (C.lit[COL_REG]) out(j++, r.is_reg ? lit_lookup<BATCH>(C.lit[COL_REG], bytes, r.b, r.slash0) : C.docker_io_cls);
+  for (uint32_t o = C.dfa[COL_REG].head; o; o = chain_next(C.dfa[COL_REG], o)) out(j++, image_part(0, chain_view(C.dfa[COL_REG], o), bytes, r));
+  if (C.lit[COL_TAG])
+    out(j++, r.colon != NONE ? lit_lookup<BATCH>(C.lit[COL_TAG], bytes, r.colon + 1, r.name_end)
+                             : (r.at == NONE ? C.latest_cls : 0u));
+  for (uint32_t o = C.dfa[COL_TAG].head; o; o = chain_next(C.dfa[COL_TAG], o)) out(j++, image_part(1, chain_view(C.dfa[COL_TAG], o), bytes, r));
+  for (uint32_t o = C.dfa[COL_IMG].head; o; o = chain_next(C.dfa[COL_IMG], o)) out(j++, image_part(2, chain_view(C.dfa[COL_IMG], o), bytes, r));
 }
 
-// Pointers read from TileArgs are generic to the compiler; these casts make their loads global_load
-// (not flat) in the staging loops.
+// COL_LV classes of a label value under label-key class k (one per DFA of the key's chain; 0xffff
+// fills the rest of the nlv entries).
+template <class Out>
+__device__ inline void classify_value(const Classifiers& C, uint32_t k, uint32_t nlv, const uint8_t* __restrict__ bytes,
+                                      uint32_t b, uint32_t e, Out out) {
+  uint32_t j = 0;
+  if (C.kv && k) {
+    const uint8_t* R = C.kv;
+    const uint32_t kbase = ((const uint32_t*)R)[C.nlk + k];
+    for (uint32_t rel = ((const uint32_t*)R)[k]; rel;) {
+      const KvDfa d = *(const KvDfa*)(R + rel);
+      uint32_t st = d.start;
+      // 8-byte windows: the window's dwords, then its 8 byte classes, load as two batches; only the
+      // transitions form a dependent chain (bytes past the string read the zero tail, unused)
+      for (uint32_t p = b; p < e && st != 0; p += 8u) {
+        const uint32_t* q = (const uint32_t*)(bytes + (p & ~3u));
+        const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], sh = p & 3u;
+        const uint32_t x0 = align_bytes(q1, q0, sh), x1 = align_bytes(q2, q1, sh);
+        uint32_t c[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const uint32_t by = ((i < 4 ? x0 : x1) >> (8 * (i & 3))) & 0xffu;
+          c[i] = (by < 128u || d.wide) ? R[d.cls_off + by] : d.hi;
+        }
+        const uint32_t lim = min(8u, e - p);
+        if (d.t16) {
+          const uint16_t* tr = (const uint16_t*)(R + d.trans_off);
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            if ((uint32_t)i < lim) st = tr[st * d.ncls + c[i]];
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            if ((uint32_t)i < lim) st = R[d.trans_off + st * d.ncls + c[i]];
+        }
+      }
+      out(j++, kbase + d.cbase + ((const uint16_t*)(R + d.acc_off))[st]);
+      rel = d.next;
+    }
+  }
+  for (; j < nlv; ++j) out(j, 0xffffu);
+}
+
+// ------------------------------------------------------------------------------------------
+// Per-chunk violation sets (slots.hpp tables) from stored classes
+// ------------------------------------------------------------------------------------------
+__device__ inline uint64_t dv_label(const SlotView& sv, uint32_t k, const uint16_t* lv, uint32_t nlv) {
+  if (!sv.h->lbl || !k) return 0ull;
+  uint64_t v = sv.row(T_DENY, k);
+  for (uint32_t j = 0; j < nlv; ++j) {
+    const uint32_t c = lv[j];
+    if (c != 0xffffu) v |= sv.row(T_FAIL, c);
+  }
+  return v;
+}
+
+__device__ inline uint64_t dv_image(const SlotView& sv, const ImgLayout& il, uint32_t fl, const uint16_t* ic) {
+  if (!sv.h->trs || !(fl & KW_CTR_HAS_IMAGE)) return 0ull;
+  uint64_t why[5];
+  trs_whys(sv, il, [&](uint32_t j) { return (uint32_t)ic[j]; }, why);
+  return (why[0] | why[1] | why[2] | why[3] | why[4]) & sv.h->trs;
+}
+
+// ------------------------------------------------------------------------------------------
+// The tile kernel
+// ------------------------------------------------------------------------------------------
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 template <class T>
 __device__ inline const __attribute__((address_space(1))) T* gp(const T* p) {
   return (const __attribute__((address_space(1))) T*)p;
 }
 
-// First global entity index and entity count of mask m's string column within a tile.
-__device__ inline uint32_t tile_g0(int m, uint32_t r0, uint32_t cb, uint32_t kab, uint32_t kdb, uint32_t lb) {
-  return m == M_NS ? r0 : m == M_CAPADD ? kab : m == M_CAPDROP ? kdb : (m == M_LK || m == M_LV) ? lb : cb;
-}
-__device__ inline uint32_t tile_n(int m, uint32_t nr, uint32_t nc, uint32_t nka, uint32_t nkd, uint32_t nl) {
-  return m == M_NS ? nr : m == M_CAPADD ? nka : m == M_CAPDROP ? nkd : (m == M_LK || m == M_LV) ? nl : nc;
-}
-
-// Literal pattern index of a one-bit mask (0xff: no pattern).
-__device__ inline uint8_t lit_index(uint64_t r) { return r ? (uint8_t)__builtin_ctzll(r) : (uint8_t)0xffu; }
-
-// A label value against the value regexes constrained on its key (label-key mask km): the key's
-// per-key DFA chain, else the whole label-value column chain.
-__device__ inline uint64_t classify_value(const TileArgs& t, const uint8_t* lds, uint64_t km, const uint8_t* bytes,
-                                          uint32_t b, uint32_t e) {
-  uint64_t vm = 0;
-  if (t.kv_lds) {
-    const uint8_t* R = lds + t.kv_lds;
-    for (uint32_t rel = ((const uint16_t*)R)[__builtin_ctzll(km)]; rel;) {
-      const KvDfa d = *(const KvDfa*)(R + rel);  // one ds_read_b128
-      uint32_t st = d.start;
-      // 8-byte windows: the window's dwords, then its 8 byte classes, load as two batches; only the
-      // transitions form a dependent chain (bytes past the string read the staged slack, unused)
-      for (uint32_t p = b; p < e && st != 0; p += 8u) {
-        const uint32_t* q = (const uint32_t*)(bytes + (p & ~3u));
-        const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], sh = p & 3u;
-        const uint32_t x0 = __builtin_amdgcn_alignbyte(q1, q0, sh), x1 = __builtin_amdgcn_alignbyte(q2, q1, sh);
-        uint32_t c[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const uint32_t by = ((j < 4 ? x0 : x1) >> (8 * (j & 3))) & 0xffu;
-          c[j] = (by < 128u || d.wide) ? R[d.cls_off + by] : d.hi;
-        }
-        const uint32_t lim = min(8u, e - p);
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if ((uint32_t)j < lim) st = R[d.trans_off + st * d.ncls + c[j]];
-      }
-      vm |= ((const uint64_t*)(R + d.accv_off))[R[d.acc_off + st]];
-      rel = d.next;
-    }
-  } else {
-    Chain c;
-    c.head = t.dfa_head[M_LV];
-    c.base = lds + t.dfa_lds[M_LV];
-    for (uint32_t o = c.head; o; o = chain_next(c, o)) {
-      const DfaView v = chain_view(c, o);
-      vm |= v.acc[feed(v, v.start, bytes, b, e)];
-    }
-  }
-  return vm;
-}
-
 __device__ inline uint32_t rup64(uint32_t n) { return (n + 63u) & ~63u; }
-__device__ inline uint64_t idx_mask(uint32_t v) { return v < 64u ? 1ull << v : 0ull; }
 
-// Trusted-repos reasons of staged container i, in precedence order (registry not allowed, registry
-// rejected, tag rejected, image not allowed, image rejected; oracle fam_trusted).
-__device__ inline void trs_whys(const SlotView& sv, const uint8_t* lds, const TileArgs& t, uint32_t i, uint64_t why[5]) {
-  const SlotHdr& h = *sv.h;
-  const uint64_t reg = t.o_m[M_REG] ? ((const uint64_t*)(lds + t.o_m[M_REG]))[i] : 0ull;
-  const uint64_t tag = t.o_m[M_TAG] ? ((const uint64_t*)(lds + t.o_m[M_TAG]))[i] : 0ull;
-  const uint64_t img = t.o_m[M_IMG] ? ((const uint64_t*)(lds + t.o_m[M_IMG]))[i] : 0ull;
-  why[0] = h.has_ra & ~tab_or(sv.tab(ST_RA), reg);
-  why[1] = tab_or(sv.tab(ST_RR), reg);
-  why[2] = tab_or(sv.tab(ST_TR), tag);
-  why[3] = h.has_ia & ~tab_or(sv.tab(ST_IA), img);
-  why[4] = tab_or(sv.tab(ST_IR), img);
+// First global entity index of string column m within a tile.
+__device__ inline uint32_t str_g0(int m, uint32_t r0, uint32_t cb, uint32_t kab, uint32_t kdb, uint32_t lb) {
+  return m == S_NS ? r0 : m == S_CAPADD ? kab : m == S_CAPDROP ? kdb : (m == S_LK || m == S_LV) ? lb : cb;
+}
+__device__ inline uint32_t str_n(int m, uint32_t nr, uint32_t nc, uint32_t nka, uint32_t nkd, uint32_t nl) {
+  return m == S_NS ? nr : m == S_CAPADD ? nka : m == S_CAPDROP ? nkd : (m == S_LK || m == S_LV) ? nl : nc;
 }
 
 // LDS-DMA copies (global_load_lds) issued by every wave of the workgroup: the LDS image is
@@ -606,47 +349,50 @@ __device__ inline void glds_x4(const u32x4* src, u32x4* dst, uint32_t n, uint32_
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + i),
                                      (__attribute__((address_space(3))) void*)(dst + (i - lane)), 16, 0, 0);
 }
+__device__ inline void copy_x4(const uint8_t* src, uint8_t* dst, uint32_t bytes, uint32_t tid) {
+  const auto* s = gp((const u32x4*)src);
+  u32x4* d = (u32x4*)dst;
+  for (uint32_t i = tid; i < bytes / 16; i += kSlotThreads) d[i] = s[i];
+}
 
-template <bool FUSED>
+template <bool LDST>
 __global__ void __launch_bounds__(kSlotThreads)
-    evaluate_slots_kernel(EvalArgs a, const TileArgs* __restrict__ tp, const TileDesc* __restrict__ desc,
-                          const uint8_t* __restrict__ blob, uint32_t* __restrict__ out) {
+    evaluate_tiles_kernel(EvalArgs a, const TileArgs* __restrict__ tp, const TileDesc* __restrict__ desc) {
   // TileArgs lives in device memory: its fields are scalar-loaded where used instead of all being
   // hoisted from the kernarg segment into SGPRs at entry.
   const TileArgs& t = *tp;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const DevHeader H = *(const DevHeader*)blob;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  uint32_t* __restrict__ out = a.out;
 
-  // ---- once per workgroup: this chunk's slot plan and (FUSED) the column tables
-  {
-    const auto* src = gp((const u32x4*)t.slot_plan);
-    u32x4* dst = (u32x4*)(lds + t.o_slot);
-    for (uint32_t i = tid; i < t.slot_bytes / 16; i += kSlotThreads) dst[i] = src[i];
-  }
-  Chain ch[NMASK];
-  if (FUSED) {
-    for (uint32_t s = 0; s < t.nstage; ++s) {
-      const auto* src = gp((const u32x4*)(blob + t.stage_blob[s]));
-      u32x4* dst = (u32x4*)(lds + t.stage_lds[s]);
-      for (uint32_t i = tid; i < t.stage_bytes[s] / 16; i += kSlotThreads) dst[i] = src[i];
-    }
-#pragma unroll
-    for (int k = 0; k < (int)NMASK; ++k) {
-      ch[k].head = t.dfa_head[k];
-      ch[k].base = lds + t.dfa_lds[k];
-    }
+  // ---- once per workgroup: the column classifiers and the chunks' staged record prefixes
+  if (LDST) {
+    for (uint32_t s = 0; s < t.nstage; ++s) copy_x4(a.blob + t.stage_blob[s], lds + t.stage_lds[s], t.stage_bytes[s], tid);
+    for (uint32_t c = 0; c < t.nchunk; ++c)
+      copy_x4(t.chunk[c].rec, lds + t.chunk[c].o_lds, ((const SlotHdr*)t.chunk[c].rec)->staged, tid);
   }
   __syncthreads();
-  SlotView sv;
-  sv.h = (const SlotHdr*)(lds + t.o_slot);
-  sv.base = lds + t.o_slot;
-  // the column records as four u32 arrays (kind | slot << 8, okw, mutw, rejb; slotplan.cpp emit):
-  // P3 items read the words of 4 consecutive columns with one conflict-free ds_read_b128 per array
-  const uint32_t* cs = (const uint32_t*)(sv.base + sv.h->o_csoa);
-  const uint32_t cs_n = (t.ncols + 3u) & ~3u;
+  const uint8_t* tb = LDST ? (const uint8_t*)lds : a.blob;
+  Classifiers C;
+#pragma unroll
+  for (int c = 0; c < (int)NCOL; ++c) {
+    const uint32_t lo = LDST ? t.lit_lds[c] : t.lit_blob[c];
+    C.lit[c] = t.lit_blob[c] ? tb + lo : nullptr;
+    C.dfa[c].head = t.dfa_blob[c];
+    C.dfa[c].base = tb + (LDST ? t.dfa_lds[c] : t.dfa_blob[c]);
+  }
+  C.kv = t.kv_blob ? tb + (LDST ? t.kv_lds : t.kv_blob) : nullptr;
+  C.nlk = t.nlk;
+  C.docker_io_cls = t.docker_io_cls;
+  C.latest_cls = t.latest_cls;
+  auto chunk_view = [&](uint32_t c) {
+    SlotView sv;
+    sv.base = LDST ? (const uint8_t*)lds + t.chunk[c].o_lds : t.chunk[c].rec;
+    sv.h = (const SlotHdr*)sv.base;
+    return sv;
+  };
 
   uint8_t* l_rf = lds + t.o_rf;
   uint32_t* l_coff = (uint32_t*)(lds + t.o_coff);
@@ -654,17 +400,27 @@ __global__ void __launch_bounds__(kSlotThreads)
   uint8_t* l_cflags = lds + t.o_cflags;
   uint32_t* l_cadd = (uint32_t*)(lds + t.o_cadd);
   uint32_t* l_cdrop = (uint32_t*)(lds + t.o_cdrop);
+  uint16_t* c_ns = (uint16_t*)(lds + t.o_ns);
+  uint16_t* c_aa = (uint16_t*)(lds + t.o_aa);
+  uint16_t* c_img = (uint16_t*)(lds + t.o_img);
+  uint16_t* c_add = (uint16_t*)(lds + t.o_capadd);
+  uint16_t* c_drop = (uint16_t*)(lds + t.o_capdrop);
+  uint16_t* c_lk = (uint16_t*)(lds + t.o_lk);
+  uint16_t* c_lv = (uint16_t*)(lds + t.o_lv);
   uint64_t* l_rej = (uint64_t*)(lds + t.o_rej);
   uint64_t* l_mut = (uint64_t*)(lds + t.o_mut);
   uint8_t* l_byp = lds + t.o_byp;
   uint32_t* l_sa = (uint32_t*)(lds + t.o_sa);
   uint64_t* l_vadd = (uint64_t*)(lds + t.o_vadd);
   uint64_t* l_vl = (uint64_t*)(lds + t.o_vl);
+  uint64_t* l_vc = (uint64_t*)(lds + t.o_vc);
+  uint64_t* l_vtr = (uint64_t*)(lds + t.o_vtr);
   uint32_t* l_vw = (uint32_t*)(lds + t.o_vw);
-  uint16_t* gstk = t.o_gstk ? (uint16_t*)(lds + t.o_gstk) : nullptr;
-  uint64_t* l_vc = (uint64_t*)(lds + t.o_vc);  // V_c per staged container
-  uint8_t* own_c = lds + t.o_own_c;            // tile-local request of each staged container / label
+  uint8_t* own_c = lds + t.o_own_c;  // tile-local request of each staged container / label
   uint8_t* own_l = lds + t.o_own_l;
+  const ImgLayout il = t.il;
+  const uint32_t nim = il.n(), nlv = t.nlv;
+  const uint32_t need = t.need;
 
   const uint32_t npol = a.npol;
   // Tile schedule. Static: tiles strided by the grid. Dynamic (a.sched): workgroup b runs on XCD
@@ -698,15 +454,18 @@ __global__ void __launch_bounds__(kSlotThreads)
   for (; tile < t_hi; tile = advance()) {
     if (dyn && tid == 0) nxt = atomicAdd(cnt, 1u);
     const TileDesc& d = desc[tile];
-    if (!d.fits) continue;  // queued for the overflow kernels by the host (uniform: no barrier skipped unevenly)
+    if (!d.fits) {  // queued for the overflow kernels by the host (uniform: no barrier skipped unevenly)
+      if (!dyn) __syncthreads();
+      continue;
+    }
     const uint64_t r0 = ((uint64_t)d.r0hi << 32) | d.r0lo;
     const uint32_t nr = d.nr;
     const uint32_t cb = d.cb, ce = d.ce, lb = d.lb, le = d.le;
     const uint32_t kab = d.kab, kae = d.kae, kdb = d.kdb, kde = d.kde;
-    const uint32_t nc = ce - cb;
+    const uint32_t nc = ce - cb, nl = le - lb;
 
-    // ---- P0: stage request headers, container offsets and (FUSED) the tile's strings. Every copy is
-    //      an LDS-DMA (global_load_lds: no VGPR round trip), so all of a tile's loads are in flight
+    // ---- P0: stage request headers, container offsets and the tile's strings. Every copy is an
+    //      LDS-DMA (global_load_lds: no VGPR round trip), so all of a tile's loads are in flight
     //      together and the barrier waits for one memory latency, not one per array.
     glds_dwords((const uint32_t*)(a.req_flags + r0), (uint32_t*)l_rf, (nr + 3u) >> 2, tid);
     glds_dwords(a.ctr_off + r0, l_coff, nr + 1, tid);
@@ -714,328 +473,300 @@ __global__ void __launch_bounds__(kSlotThreads)
     glds_dwords((const uint32_t*)a.ctr_flags + (cb >> 2), (uint32_t*)l_cflags, ((ce + 3u) >> 2) - (cb >> 2), tid);
     glds_dwords(a.capadd_off + cb, l_cadd, nc + 1, tid);
     glds_dwords(a.capdrop_off + cb, l_cdrop, nc + 1, tid);
-    if (FUSED) {
 #pragma unroll
-      for (int m = 0; m < (int)NMASK; ++m) {
-        if (!t.o_sb[m]) continue;
-        const uint32_t g0 = tile_g0(m, (uint32_t)r0, cb, kab, kdb, lb);
-        const uint32_t n = tile_n(m, nr, nc, kae - kab, kde - kdb, le - lb);
-        glds_dwords(t.s_off[m] + g0, (uint32_t*)(lds + t.o_so[m]), n + 1, tid);  // absolute: rebased by l_sa
-        glds_x4((const u32x4*)(t.s_bytes[m] + d.sa[m]), (u32x4*)(lds + t.o_sb[m]), d.nv[m], tid);
-      }
+    for (int m = 0; m < (int)NSTR; ++m) {
+      if (!t.o_sb[m]) continue;
+      const uint32_t g0 = str_g0(m, (uint32_t)r0, cb, kab, kdb, lb);
+      const uint32_t n = str_n(m, nr, nc, kae - kab, kde - kdb, nl);
+      glds_dwords(t.s_off[m] + g0, (uint32_t*)(lds + t.o_so[m]), n + 1, tid);  // absolute: rebased by l_sa
+      glds_x4((const u32x4*)(t.s_bytes[m] + d.sa[m]), (u32x4*)(lds + t.o_sb[m]), d.nv[m], tid);
     }
     for (uint32_t i = tid; i < nr; i += kSlotThreads) l_rej[i] = l_mut[i] = 0;
-    if (tid < NMASK) l_sa[tid] = d.sa[tid];
+    if (tid < NSTR) l_sa[tid] = d.sa[tid];
     __syncthreads();
     const uint8_t* cfl = l_cflags + (cb & 3u);  // staged from the dword holding flag cb
-
-    // ---- P1: classify the staged strings (FUSED) or take the classify kernel's masks (two-kernel
-    //      form), and derive each entity's violation set from the slot tables, entity-parallel:
-    //      request items (namespace; owner maps of the tile's containers and labels), image items
-    //      (registry / tag / image masks), container items (privileged candidates, added and
-    //      dropped capabilities, AppArmor profile -> V_c) and label items (key, value -> V_l).
-    const SlotHdr& SH = *sv.h;
-    const uint64_t privany = SH.priv[0] | SH.priv[1] | SH.priv[2] | SH.priv[3];
-    const bool ctr_fam = (privany | SH.caps | SH.aa | SH.trs) != 0;
     const bool classify = !(t.debug & 1u);  // diagnostics: skip classification (entities match nothing)
-    // pattern mask of string i of literal column m: the staged strings (FUSED) or the classify
-    // kernel's masks (entity index relative to the mask's tile base `g0`)
-    auto lit = [&](int m, uint32_t i, uint32_t g0) -> uint64_t {
-      if (!classify) return 0ull;
-      if (!FUSED) return a.m[m][g0 + i];
+    auto str = [&](int m, uint32_t i, uint32_t* b, uint32_t* e) {
       const uint32_t* so = (const uint32_t*)(lds + t.o_so[m]);
       const uint32_t sa = l_sa[m];
-      return lit_lookup(lds + t.lit_lds[m], lds + t.o_sb[m], so[i] - sa, so[i + 1] - sa);
+      *b = so[i] - sa;
+      *e = so[i + 1] - sa;
     };
+    auto lit = [&](Col c, int m, uint32_t i) -> uint32_t {
+      if (!classify || !C.lit[c]) return 0u;
+      uint32_t b, e;
+      str(m, i, &b, &e);
+      return lit_lookup<true>(C.lit[c], lds + t.o_sb[m], b, e);
+    };
+
+    // ---- P1: classify the staged strings entity-parallel, and derive chunk 0's violation sets.
+    //      Items come in segments padded to whole waves, ordered by cost: labels (key literal,
+    //      value DFAs -> V_l), containers (AppArmor, added / dropped capabilities -> V_c, V_add),
+    //      images (registry / tag / image classes -> V_tr), requests (namespace, owner maps, bypass).
     {
+      const SlotView sv0 = chunk_view(0);
+      const SlotHdr& h0 = *sv0.h;
+      const uint32_t n3 = (need & (1u << S_LK)) ? nl : 0u;
+      const uint32_t n2 = nc;
+      const uint32_t n1 = (need & (1u << S_IMG)) ? nc : 0u;
       const uint32_t n0 = nr;
-      const uint32_t n1 = (t.use_mask & ((1u << M_REG) | (1u << M_TAG) | (1u << M_IMG))) ? nc : 0u;
-      const uint32_t n2 = ctr_fam ? nc : 0u;
-      const uint32_t n3 = t.o_m[M_LK] ? le - lb : 0u;
-      // item segments in falling cost order, each padded to whole waves: a wave's 64 items are one
-      // kind (no divergence between kinds) and the round-robin of waves over segments balances
       const uint32_t e0 = rup64(n3), e1 = e0 + rup64(n2), e2 = e1 + rup64(n1), e3 = e2 + rup64(n0);
       for (uint32_t w = tid; w < e3; w += kSlotThreads) {
-        if (w < e0) {  // label: key, value -> V_l = denied | constrained-and-failed slots
+        if (w < e0) {  // label
           const uint32_t i = w;
           if (i >= n3) continue;
-          const uint64_t r = lit(M_LK, i, lb);
-          uint64_t vm = 0;
-          if (!r) {
-          } else if (FUSED) {
-            if (t.o_sb[M_LV] && !(t.debug & 512u)) {
-              const uint32_t* vo = (const uint32_t*)(lds + t.o_so[M_LV]);
-              const uint32_t vsa = l_sa[M_LV];
-              vm = classify_value(t, lds, r, lds + t.o_sb[M_LV], vo[i] - vsa, vo[i + 1] - vsa);
-            }
+          const uint32_t k = lit(COL_LK, S_LK, i);
+          c_lk[i] = (uint16_t)k;
+          uint16_t* lv = c_lv + i * nlv;
+          if (k && classify && t.o_sb[S_LV]) {
+            uint32_t b, e;
+            str(S_LV, i, &b, &e);
+            classify_value(C, k, nlv, lds + t.o_sb[S_LV], b, e, [&](uint32_t j, uint32_t c) { lv[j] = (uint16_t)c; });
           } else {
-            vm = a.m[M_LV] ? a.m[M_LV][lb + i] : 0ull;
+            for (uint32_t j = 0; j < nlv; ++j) lv[j] = 0xffffu;
           }
-          lds[t.o_m[M_LK] + i] = lit_index(r);
-          l_vl[i] = (r && SH.lbl) ? derive_label(sv, r, vm) | sv.tab(ST_DENY)[kw_ctz64(r)] : 0ull;
-        } else if (w < e1) {  // container: V_c over the privileged, capability and AppArmor slots
+          l_vl[i] = dv_label(sv0, k, lv, nlv);
+        } else if (w < e1) {  // container
           const uint32_t i = w - e0;
           if (i >= n2) continue;
           const uint32_t fl = cfl[i];
-          uint64_t v = 0;
-          if ((fl & KW_CTR_PRIVILEGED) && privany) {
-            v |= SH.priv[0];
-            if (!(fl & KW_CTR_INIT)) v |= SH.priv[1];
-            if (!(fl & KW_CTR_EPHEMERAL)) v |= SH.priv[2];
-            if (!(fl & (KW_CTR_INIT | KW_CTR_EPHEMERAL))) v |= SH.priv[3];
+          uint64_t v = priv_viol(h0, fl);
+          if (need & (1u << S_AA)) {
+            const uint32_t ac = (fl & KW_CTR_HAS_APPARMOR) ? lit(COL_AA, S_AA, i) : 0u;
+            c_aa[i] = (uint16_t)ac;
+            if (h0.aa && (fl & KW_CTR_HAS_APPARMOR)) v |= sv0.row(T_NAAA, ac);
           }
-          if (SH.aa && (t.use_mask & (1u << M_AA)) && (fl & KW_CTR_HAS_APPARMOR)) {
-            v |= derive_apparmor(sv, lit(M_AA, i, cb));
-          }
-          if (t.o_m[M_CAPADD]) {
+          if (need & (1u << S_CAPADD)) {
             for (uint32_t k = l_cadd[i] - kab, k1 = l_cadd[i + 1] - kab; k < k1; ++k) {
-              const uint64_t r = lit(M_CAPADD, k, kab);
-              lds[t.o_m[M_CAPADD] + k] = lit_index(r);
-              const uint64_t va = derive_capadd(sv, r);
+              const uint32_t cc = lit(COL_CAP, S_CAPADD, k);
+              c_add[k] = (uint16_t)cc;
+              const uint64_t va = h0.caps_strict ? sv0.row(T_NACAP, cc) : 0ull;
               l_vadd[k] = va;
               v |= va;
             }
-          }
-          if (t.o_m[M_CAPDROP]) {
-            for (uint32_t k = l_cdrop[i] - kdb, k1 = l_cdrop[i + 1] - kdb; k < k1; ++k)
-              lds[t.o_m[M_CAPDROP] + k] = lit_index(lit(M_CAPDROP, k, kdb));
+            for (uint32_t k = l_cdrop[i] - kdb, k1 = l_cdrop[i + 1] - kdb; k < k1; ++k) c_drop[k] = (uint16_t)lit(COL_CAP, S_CAPDROP, k);
           }
           l_vc[i] = v;
-        } else if (w < e2) {  // image reference: one parse feeds the registry, tag and image chains
+        } else if (w < e2) {  // image reference: one parse feeds the registry, tag and image classes
           const uint32_t i = w - e1;
           if (i >= n1) continue;
-          uint64_t mr = 0, mt = 0, mi = 0;
-          if (!classify) {
-          } else if (FUSED) {
-            if (cfl[i] & KW_CTR_HAS_IMAGE) {
-              const uint32_t* so = (const uint32_t*)(lds + t.o_so[M_IMG]);
-              const uint32_t sa = l_sa[M_IMG];
-              classify_image_all(ch[M_REG], ch[M_TAG], ch[M_IMG], lds + t.o_sb[M_IMG], so[i] - sa, so[i + 1] - sa, &mr,
-                                 &mt, &mi);
-            }
+          uint16_t* ic = c_img + i * nim;
+          const uint32_t fl = cfl[i];
+          if (classify && (fl & KW_CTR_HAS_IMAGE)) {
+            uint32_t b, e;
+            str(S_IMG, i, &b, &e);
+            classify_image<true>(C, il, lds + t.o_sb[S_IMG], b, e, [&](uint32_t j, uint32_t c) { ic[j] = (uint16_t)c; });
           } else {
-            if (a.m[M_REG]) mr = a.m[M_REG][cb + i];
-            if (a.m[M_TAG]) mt = a.m[M_TAG][cb + i];
-            if (a.m[M_IMG]) mi = a.m[M_IMG][cb + i];
+            for (uint32_t j = 0; j < nim; ++j) ic[j] = 0;
           }
-          if (t.o_m[M_REG]) ((uint64_t*)(lds + t.o_m[M_REG]))[i] = mr;
-          if (t.o_m[M_TAG]) ((uint64_t*)(lds + t.o_m[M_TAG]))[i] = mt;
-          if (t.o_m[M_IMG]) ((uint64_t*)(lds + t.o_m[M_IMG]))[i] = mi;
-        } else {  // request: namespace and the owner maps
+          l_vtr[i] = dv_image(sv0, il, fl, ic);
+        } else {  // request: namespace class, owner maps, bypass
           const uint32_t i = w - e2;
           if (i >= n0) continue;
-          if (t.o_m[M_NS]) lds[t.o_m[M_NS] + i] = lit_index(lit(M_NS, i, (uint32_t)r0));
+          const uint32_t nsc = (need & (1u << S_NS)) ? lit(COL_NS, S_NS, i) : 0u;
+          c_ns[i] = (uint16_t)nsc;
           for (uint32_t c = l_coff[i] - cb, c1 = l_coff[i + 1] - cb; c < c1; ++c) own_c[c] = (uint8_t)i;
           for (uint32_t l = l_loff[i] - lb, l1 = l_loff[i + 1] - lb; l < l1; ++l) own_l[l] = (uint8_t)i;
+          l_byp[i] = is_bypass(l_rf[i], nsc, t.bypass_cls) ? 1 : 0;
         }
       }
     }
     __syncthreads();
 
-    // ---- P2: first violations, entity-parallel. A slot's first violation is the first entity of
-    //      the request (object order) whose violation set holds it: each entity thread ORs the sets
-    //      of its predecessors in the request (independent LDS loads) and writes the words of the
-    //      slots it violates first; within an entity the family's own order applies (capabilities
-    //      in list order, trusted-repos reasons in precedence). Request items add the namespace and
-    //      mandatory-label slots and the bypass flag. Rejected / mutated slots merge with ds_or_b64.
-    //      (Sequential form of the same walk: slots.hpp walk_*, the host diagnostic.)
-    if (SH.trs && !(t.debug & 2u)) {  // trusted-repos reasons join V_c once the image masks exist
-      for (uint32_t i = tid; i < nc; i += kSlotThreads) {
-        if (!(cfl[i] & KW_CTR_HAS_IMAGE)) continue;
-        uint64_t why[5];
-        trs_whys(sv, lds, t, i, why);
-        l_vc[i] |= (why[0] | why[1] | why[2] | why[3] | why[4]) & SH.trs;
+    for (uint32_t ck = 0; ck < t.nchunk; ++ck) {
+      const SlotView sv = chunk_view(ck);
+      const SlotHdr& SH = *sv.h;
+      if (ck > 0) {
+        // ---- D: this chunk's violation sets from the stored classes
+        const uint32_t n3 = SH.lbl ? nl : 0u, n2 = nc, n1 = SH.trs ? nc : 0u;
+        const uint32_t e0 = rup64(n3), e1 = e0 + rup64(n2), e2 = e1 + rup64(n1), e3 = e2 + rup64(nr);
+        for (uint32_t w = tid; w < e3; w += kSlotThreads) {
+          if (w < e0) {
+            const uint32_t i = w;
+            if (i < n3) l_vl[i] = dv_label(sv, c_lk[i], c_lv + i * nlv, nlv);
+          } else if (w < e1) {
+            const uint32_t i = w - e0;
+            if (i >= n2) continue;
+            const uint32_t fl = cfl[i];
+            uint64_t v = priv_viol(SH, fl);
+            if (SH.aa && (fl & KW_CTR_HAS_APPARMOR)) v |= sv.row(T_NAAA, c_aa[i]);
+            if (SH.caps)
+              for (uint32_t k = l_cadd[i] - kab, k1 = l_cadd[i + 1] - kab; k < k1; ++k) {
+                const uint64_t va = SH.caps_strict ? sv.row(T_NACAP, c_add[k]) : 0ull;
+                l_vadd[k] = va;
+                v |= va;
+              }
+            l_vc[i] = v;  // (l_vtr is read only by chunks with trusted-repos slots, which rewrite it below)
+          } else if (w < e2) {
+            const uint32_t i = w - e1;
+            if (i < n1) l_vtr[i] = dv_image(sv, il, cfl[i], c_img + i * nim);
+          } else {
+            const uint32_t i = w - e2;
+            if (i < nr) l_rej[i] = l_mut[i] = 0;
+          }
+        }
+        __syncthreads();
+      }
+
+      // ---- P2: first violations, entity-parallel. A slot's first violation is the first entity
+      //      of the request (object order) whose violation set holds it: each entity thread ORs the
+      //      sets of its predecessors in the request (independent LDS loads) and writes the words of
+      //      the slots it violates first; within an entity the family's own order applies
+      //      (capabilities in list order, trusted-repos reasons in precedence). Request items add
+      //      the namespace and mandatory-label slots. Rejected / mutated slots merge with ds_or_b64.
+      //      (Sequential form of the same walk: slots.hpp walk_*.)
+      if (!(t.debug & 2u)) {
+        const uint64_t privany = SH.priv[0] | SH.priv[1] | SH.priv[2] | SH.priv[3];
+        const bool ctr_fam = (privany | SH.caps | SH.aa | SH.trs) != 0;
+        const bool trs = SH.trs != 0;
+        const uint32_t n1 = ctr_fam ? nc : 0u, n2 = SH.lbl ? nl : 0u;
+        const uint32_t f0 = rup64(n1), f1 = f0 + rup64(n2), f2 = f1 + rup64(nr);
+        for (uint32_t w = tid; w < f2; w += kSlotThreads) {
+          if (w < f0) {  // container
+            const uint32_t i = w;
+            if (i >= n1) continue;
+            const uint32_t q = own_c[i];
+            if (!(l_rf[q] & KW_REQ_HAS_PODSPEC)) continue;
+            const uint32_t c0 = l_coff[q] - cb;
+            uint64_t pre = 0;
+            for (uint32_t j = c0; j < i; ++j) pre |= trs ? (l_vc[j] | l_vtr[j]) : l_vc[j];
+            const uint64_t nv = (trs ? (l_vc[i] | l_vtr[i]) : l_vc[i]) & ~pre;
+            const uint32_t ci = i - c0;
+            uint32_t* vw = l_vw + q * t.vw_stride;
+            if (nv) {
+              ViolSink vs{vw, nullptr};
+              vs.put(nv & privany, KW_R_PRIVILEGED, ci);
+              vs.put(nv & SH.aa, KW_R_APPARMOR, ci);
+              uint64_t cn = nv & SH.caps;  // capability slots: the first added capability of the list
+              const uint32_t kfirst = l_cadd[c0] - kab;
+              for (uint32_t k = l_cadd[i] - kab, k1 = l_cadd[i + 1] - kab; k < k1 && cn; ++k) {
+                const uint64_t nw = l_vadd[k] & cn;
+                vs.put(nw, KW_R_CAP_NOT_ALLOWED, k - kfirst);
+                cn &= ~nw;
+              }
+              uint64_t tn = nv & SH.trs;  // trusted-repos slots: reasons in precedence order
+              if (tn) {
+                uint64_t why[5];
+                const uint16_t* ic = c_img + i * nim;
+                trs_whys(sv, il, [&](uint32_t j) { return (uint32_t)ic[j]; }, why);
+                for (uint32_t k = 0; k < 5; ++k) {
+                  const uint64_t nw = why[k] & tn;
+                  vs.put(nw, KW_R_REG_NOT_ALLOWED + k, ci);
+                  tn &= ~nw;
+                }
+              }
+              atomicOr((unsigned long long*)&l_rej[q], (unsigned long long)nv);
+            }
+            if (SH.caps) {  // mutation: required drops missing, default adds neither added nor dropped
+              uint64_t addm = 0, dropm = 0;
+              for (uint32_t k = l_cadd[i] - kab, k1 = l_cadd[i + 1] - kab; k < k1; ++k) addm |= bit_of(sv.capmb(c_add[k]));
+              for (uint32_t k = l_cdrop[i] - kdb, k1 = l_cdrop[i + 1] - kdb; k < k1; ++k) dropm |= bit_of(sv.capmb(c_drop[k]));
+              const uint64_t mut = caps_mutation(sv, addm, dropm);
+              if (mut) atomicOr((unsigned long long*)&l_mut[q], (unsigned long long)mut);
+            }
+          } else if (w < f1) {  // label
+            const uint32_t i = w - f0;
+            if (i >= n2) continue;
+            const uint64_t v = l_vl[i];
+            if (!v) continue;
+            const uint32_t q = own_l[i];
+            const uint32_t l0 = l_loff[q] - lb;
+            uint64_t pre = 0;
+            for (uint32_t j = l0; j < i; ++j) pre |= l_vl[j];
+            const uint64_t nv = v & ~pre;
+            if (!nv) continue;
+            const uint64_t den = sv.row(T_DENY, c_lk[i]);
+            const uint32_t li = i - l0;
+            ViolSink vs{l_vw + q * t.vw_stride, nullptr};
+            vs.put(nv & den, KW_R_LABEL_DENIED, li);
+            vs.put(nv & ~den, KW_R_LABEL_CONSTRAINT, li);
+            atomicOr((unsigned long long*)&l_rej[q], (unsigned long long)nv);
+          } else {  // request: namespace, mandatory labels
+            const uint32_t i = w - f1;
+            if (i >= nr) continue;
+            const uint32_t rf = l_rf[i];
+            ViolSink vs{l_vw + i * t.vw_stride, nullptr};
+            uint64_t rej = 0;
+            if (SH.ns) {
+              const uint64_t ok = (rf & KW_REQ_HAS_NAMESPACE) ? sv.row(T_NSOK, c_ns[i]) : 0ull;
+              rej = SH.ns & ~ok;
+              vs.put(rej, KW_R_NAMESPACE, 0);
+            }
+            if (SH.lbl && SH.mand_union) {
+              uint64_t present = 0, lrej = 0;
+              for (uint32_t l = l_loff[i] - lb, l1 = l_loff[i + 1] - lb; l < l1; ++l) {
+                present |= bit_of(sv.lkmb(c_lk[l]));
+                lrej |= l_vl[l];
+              }
+              uint64_t nw = tab_or(sv.mand(), SH.mand_union & ~present) & ~lrej;
+              rej |= nw;
+              while (nw) {  // the first missing mandatory key of each such slot, settings order
+                const uint32_t s = kw_ctz64(nw);
+                nw &= nw - 1;
+                vs.put(1ull << s, KW_R_LABEL_MANDATORY, first_missing(sv, s, present));
+              }
+            }
+            if (rej) atomicOr((unsigned long long*)&l_rej[i], (unsigned long long)rej);
+          }
+        }
       }
       __syncthreads();
-    }
-    if (!(t.debug & 2u)) {
-      const uint32_t n0 = nr, n1 = ctr_fam ? nc : 0u, n2 = (SH.lbl && t.o_m[M_LK]) ? le - lb : 0u;
-      const uint32_t f0 = rup64(n1), f1 = f0 + rup64(n2), f2 = f1 + rup64(n0);  // as in P1
-      for (uint32_t w = tid; w < f2; w += kSlotThreads) {
-        if (w < f0) {  // container
-          const uint32_t i = w;
-          if (i >= n1) continue;
-          const uint32_t q = own_c[i];
-          if (!(l_rf[q] & KW_REQ_HAS_PODSPEC)) continue;
-          const uint32_t c0 = l_coff[q] - cb;
-          uint64_t pre = 0;
-          for (uint32_t j = c0; j < i; ++j) pre |= l_vc[j];
-          const uint64_t nv = l_vc[i] & ~pre;
-          const uint32_t ci = i - c0;
-          uint32_t* vw = l_vw + q * t.vw_stride;
-          if (nv) {
-            put_viol(vw, nv & privany, vword(KW_R_PRIVILEGED, pack1(ci)));
-            put_viol(vw, nv & SH.aa, vword(KW_R_APPARMOR, pack1(ci)));
-            uint64_t cn = nv & SH.caps;  // capability slots: the first added capability of the list
-            for (uint32_t k = l_cadd[i] - kab, k0 = k, k1 = l_cadd[i + 1] - kab; k < k1 && cn; ++k) {
-              const uint64_t nw = l_vadd[k] & cn;
-              put_viol(vw, nw, vword(KW_R_CAP_NOT_ALLOWED, pack2(ci, k - k0)));
-              cn &= ~nw;
-            }
-            uint64_t tn = nv & SH.trs;  // trusted-repos slots: reasons in precedence order
-            if (tn) {
-              uint64_t why[5];
-              trs_whys(sv, lds, t, i, why);
-              for (uint32_t k = 0; k < 5; ++k) {
-                const uint64_t nw = why[k] & tn;
-                put_viol(vw, nw, vword(KW_R_REG_NOT_ALLOWED + k, pack1(ci)));
-                tn &= ~nw;
-              }
-            }
-            atomicOr((unsigned long long*)&l_rej[q], (unsigned long long)nv);
-          }
-          if (SH.caps) {  // mutation: required drops missing, default adds neither added nor dropped
-            uint64_t addm = 0, dropm = 0;
-            if (t.o_m[M_CAPADD])
-              for (uint32_t k = l_cadd[i] - kab, k1 = l_cadd[i + 1] - kab; k < k1; ++k)
-                addm |= idx_mask(lds[t.o_m[M_CAPADD] + k]);
-            if (t.o_m[M_CAPDROP])
-              for (uint32_t k = l_cdrop[i] - kdb, k1 = l_cdrop[i + 1] - kdb; k < k1; ++k)
-                dropm |= idx_mask(lds[t.o_m[M_CAPDROP] + k]);
-            uint64_t mut = 0;
-            if (!(dropm & SH.cap_all)) mut |= tab_or(sv.tab(ST_REQD), SH.reqd_union & ~dropm);
-            mut |= tab_or(sv.tab(ST_DEFA), SH.defa_union & ~(addm | dropm));
-            mut &= SH.caps;
-            if (mut) atomicOr((unsigned long long*)&l_mut[q], (unsigned long long)mut);
-          }
-        } else if (w < f1) {  // label
-          const uint32_t i = w - f0;
-          if (i >= n2) continue;
-          const uint64_t v = l_vl[i];
-          if (!v) continue;
-          const uint32_t q = own_l[i];
-          const uint32_t l0 = l_loff[q] - lb;
-          uint64_t pre = 0;
-          for (uint32_t j = l0; j < i; ++j) pre |= l_vl[j];
-          const uint64_t nv = v & ~pre;
-          if (!nv) continue;
-          const uint32_t kb = lds[t.o_m[M_LK] + i];
-          const uint64_t den = sv.tab(ST_DENY)[kb];
-          const uint32_t li = i - l0;
-          uint32_t* vw = l_vw + q * t.vw_stride;
-          put_viol(vw, nv & den, vword(KW_R_LABEL_DENIED, pack1(li)));
-          put_viol(vw, nv & ~den, vword(KW_R_LABEL_CONSTRAINT, pack2(li, 0)) | kb);
-          atomicOr((unsigned long long*)&l_rej[q], (unsigned long long)nv);
-        } else {  // request: namespace, mandatory labels, bypass
-          const uint32_t i = w - f1;
-          if (i >= n0) continue;
-          const uint32_t rf = l_rf[i];
-          uint32_t* vw = l_vw + i * t.vw_stride;
-          const uint64_t nsm = t.o_m[M_NS] ? idx_mask(lds[t.o_m[M_NS] + i]) : 0ull;
-          uint64_t rej = 0;
-          if (SH.ns) {
-            const uint64_t ok = (rf & KW_REQ_HAS_NAMESPACE) ? tab_or(sv.tab(ST_NSOK), nsm) : 0ull;
-            rej = SH.ns & ~ok;
-            put_viol(vw, rej, vword(KW_R_NAMESPACE, 0));
-          }
-          if (SH.lbl && SH.mand_union && t.o_m[M_LK]) {
-            uint64_t present = 0, lrej = 0;
-            for (uint32_t l = l_loff[i] - lb, l1 = l_loff[i + 1] - lb; l < l1; ++l) {
-              present |= idx_mask(lds[t.o_m[M_LK] + l]);
-              lrej |= l_vl[l];
-            }
-            uint64_t nw = tab_or(sv.tab(ST_MAND), SH.mand_union & ~present) & ~lrej;
-            rej |= nw;
-            const uint8_t* mand = sv.base + SH.o_mand;  // staged with the record (LDS)
-            while (nw) {  // the first missing mandatory key of each such slot, settings order
-              const uint32_t sl = kw_ctz64(nw);
-              nw &= nw - 1;
-              const uint4 mk = *(const uint4*)(mand + sl * 16u);
-              const uint32_t mw[4] = {mk.x, mk.y, mk.z, mk.w};
-              uint32_t k = 0;
-              for (; k < 16; ++k) {
-                const uint32_t kb = (mw[k >> 2] >> (8 * (k & 3))) & 0xffu;
-                if (kb == 0xffu || !((present >> kb) & 1ull)) break;
-              }
-              vw[sl] = vword(KW_R_LABEL_MANDATORY, k);
-            }
-          }
-          if (rej) atomicOr((unsigned long long*)&l_rej[i], (unsigned long long)rej);
-          // namespace bypass (service.rs:40-71): AdmissionRequest in the always-accept namespace
-          l_byp[i] = H.bypass_bit >= 0 && !(rf & KW_REQ_RAW) && (rf & KW_REQ_HAS_NAMESPACE) && ((nsm >> H.bypass_bit) & 1ull);
-        }
-      }
-    } else {
-      for (uint32_t i = tid; i < nr; i += kSlotThreads) l_byp[i] = 0;
-    }
-    __syncthreads();
 
-    // ---- P3: verdict rows. Default: one lane per request, each wave a quarter of the columns; the
-    //      column records come from the global copy of the slot plan with wave-uniform indices
-    //      (scalar loads) and each lane writes 16-B pieces of its own row. p3_item: items =
-    //      (request, 4 columns), 16 lanes per 256-B row, column records from LDS.
-    if (!(t.debug & 4u)) {
-      const uint64_t init = t.slot_init;
-      const uint8_t* cidx = t.slot_plan + t.o_cidx_rec;
-      uint16_t* gs = gstk ? gstk + tid : nullptr;
-      if (!t.p3_item) {
-        if (lane < nr) {
-          const ColInfo* gcols = (const ColInfo*)(t.slot_plan + t.o_cols_rec);
-          const uint64_t rej = l_rej[lane], mut = l_mut[lane];
-          const bool byp = l_byp[lane] != 0;
-          const uint32_t* vw = l_vw + lane * t.vw_stride;
-          uint32_t* orow = out + (r0 + lane) * npol + t.col0;
-          const uint32_t q = ((t.ncols + 15u) >> 4) << 2;
-          const uint32_t j0 = min(t.ncols, wave * q), j1 = min(t.ncols, j0 + q);
-          if (t.vec4) {
-            for (uint32_t j = j0; j < j1; j += 4) {
-              uint4 w = make_uint4(kBypassWord, kBypassWord, kBypassWord, kBypassWord);
-              if (!byp) {
-                w.x = column_word(gcols[j + 0], rej, mut, init, vw, blob, cidx, gs, kSlotThreads);
-                w.y = column_word(gcols[j + 1], rej, mut, init, vw, blob, cidx, gs, kSlotThreads);
-                w.z = column_word(gcols[j + 2], rej, mut, init, vw, blob, cidx, gs, kSlotThreads);
-                w.w = column_word(gcols[j + 3], rej, mut, init, vw, blob, cidx, gs, kSlotThreads);
-              }
-              *(uint4*)(orow + j) = w;
-            }
-          } else {
-            for (uint32_t j = j0; j < j1; ++j)
-              orow[j] = byp ? kBypassWord : column_word(gcols[j], rej, mut, init, vw, blob, cidx, gs, kSlotThreads);
+      // ---- P3: verdict words. All-pairs: items = (request, 4 columns), 16 lanes per 256-B row,
+      //      column records from LDS (group / constant columns from the record's global copy).
+      //      Rows mode: one word per request, its own column.
+      if (!(t.debug & 4u)) {
+        const ChunkArgs& CA = t.chunk[ck];
+        const uint64_t init = CA.init;
+        const ColInfo* cols = (const ColInfo*)(CA.rec + SH.o_cols);
+        const uint32_t ncols = CA.ncols;
+        auto word = [&](uint32_t rr, uint32_t j) -> uint32_t {
+          uint64_t wide = 0;
+          const uint32_t w = column_word(cols[j], l_rej[rr], l_mut[rr], init, l_vw + rr * t.vw_stride, CA.rec, &wide);
+          if (cols[j].wide != ~0u && KW_REASON(w) == KW_R_GROUP) a.wide_groups[(r0 + rr) * a.nwide + cols[j].wide] = wide;
+          return w;
+        };
+        if (t.rows_mode) {
+          for (uint32_t rr = tid; rr < nr; rr += kSlotThreads) {
+            const uint32_t rc = a.rowcol[r0 + rr];
+            if ((rc >> 16) != ck) continue;
+            out[r0 + rr] = l_byp[rr] ? kBypassWord : word(rr, rc & 0xffffu);
           }
-        }
-      } else {
-        const ColInfo* cols = (const ColInfo*)(t.slot_plan + t.o_cols_rec);  // global: group / constant columns
-        if (t.vec4) {
-          const uint32_t G = t.ncols >> 2;
-          for (uint32_t it = tid; it < nr * G; it += kSlotThreads) {
-            const uint32_t rr = it / G, g = it - rr * G;
-            uint4 w;
+        } else if (CA.vec4) {
+          const uint32_t* cs = (const uint32_t*)(sv.base + SH.o_csoa);
+          const uint32_t cs_n = (ncols + 3u) & ~3u;
+          const uint32_t G = ncols >> 2;
+          for (uint32_t q = tid; q < nr * G; q += kSlotThreads) {
+            const uint32_t rr = q / G, g = q - rr * G;
+            uint4 wv;
             if (l_byp[rr]) {
-              w = make_uint4(kBypassWord, kBypassWord, kBypassWord, kBypassWord);
+              wv = make_uint4(kBypassWord, kBypassWord, kBypassWord, kBypassWord);
             } else {
               const uint64_t rej = l_rej[rr], mut = l_mut[rr];
               const uint32_t* vw = l_vw + rr * t.vw_stride;
               const uint4 ks = *(const uint4*)(cs + 4 * g), ok = *(const uint4*)(cs + cs_n + 4 * g),
                           mu = *(const uint4*)(cs + 2 * cs_n + 4 * g), rj = *(const uint4*)(cs + 3 * cs_n + 4 * g);
-              auto word = [&](uint32_t k, uint32_t okw, uint32_t mutw, uint32_t rejb, uint32_t j) -> uint32_t {
-                if ((k & 0xffu) != CK_PLAIN) return column_word(cols[j], rej, mut, init, vw, blob, cidx, gs, kSlotThreads);
+              auto pw = [&](uint32_t k, uint32_t okw, uint32_t mutw, uint32_t rejb, uint32_t j) -> uint32_t {
+                if ((k & 0xffu) != CK_PLAIN) return word(rr, j);
                 const uint32_t s = k >> 8;
-                if ((rej >> s) & 1ull) {
-                  uint32_t v = vw[s];
-                  if (((v >> 8) & 0xffu) == KW_R_LABEL_CONSTRAINT)
-                    v = (v & ~0xffu) | ((uint32_t)cidx[s * 64u + (v & 63u)] << 16);
-                  return rejb | v;
-                }
+                if ((rej >> s) & 1ull) return rejb | vw[s];
                 return ((mut >> s) & 1ull) ? mutw : okw;
               };
-              w.x = word(ks.x, ok.x, mu.x, rj.x, 4 * g + 0);
-              w.y = word(ks.y, ok.y, mu.y, rj.y, 4 * g + 1);
-              w.z = word(ks.z, ok.z, mu.z, rj.z, 4 * g + 2);
-              w.w = word(ks.w, ok.w, mu.w, rj.w, 4 * g + 3);
+              wv.x = pw(ks.x, ok.x, mu.x, rj.x, 4 * g + 0);
+              wv.y = pw(ks.y, ok.y, mu.y, rj.y, 4 * g + 1);
+              wv.z = pw(ks.z, ok.z, mu.z, rj.z, 4 * g + 2);
+              wv.w = pw(ks.w, ok.w, mu.w, rj.w, 4 * g + 3);
             }
-            *(uint4*)(out + (r0 + rr) * npol + t.col0 + 4 * g) = w;
+            *(uint4*)(out + (r0 + rr) * npol + CA.col0 + 4 * g) = wv;
           }
         } else {
-          const uint32_t G = t.ncols;
-          for (uint32_t it = tid; it < nr * G; it += kSlotThreads) {
-            const uint32_t rr = it / G, g = it - rr * G;
-            uint32_t w = kBypassWord;
-            if (!l_byp[rr])
-              w = column_word(cols[g], l_rej[rr], l_mut[rr], init, l_vw + rr * t.vw_stride, blob, cidx, gs, kSlotThreads);
-            out[(r0 + rr) * npol + t.col0 + g] = w;
+          for (uint32_t q = tid; q < nr * ncols; q += kSlotThreads) {
+            const uint32_t rr = q / ncols, g = q - rr * ncols;
+            out[(r0 + rr) * npol + CA.col0 + g] = l_byp[rr] ? kBypassWord : word(rr, g);
           }
         }
       }
+      if (ck + 1 < t.nchunk) __syncthreads();  // the next chunk rewrites the violation sets and words
     }
     if (!dyn) __syncthreads();  // the next tile restages LDS (its strings alias this tile's violation words)
   }
@@ -1048,131 +779,197 @@ __global__ void __launch_bounds__(kSlotThreads)
       atomicExch(done, 0u);
     }
   }
+  (void)lane;
+  (void)wave;
 }
 
-// Requests whose entity counts or string bytes exceed the LDS capacities even in a tile of their
-// own (listed by the host with the tile descriptors in `overflow`: count, then request indices).
-// Two launches: overflow_classify_kernel classifies their strings into the global mask arrays (DFA
-// chains read from the blob, one workgroup per request), then overflow_eval_kernel evaluates every
-// (request, column) pair from global memory, one lane per pair.
+// ------------------------------------------------------------------------------------------
+// Overflow: requests whose entity counts or string bytes exceed the tile capacities even alone
+// (listed by the host with the tile descriptors: [count, request indices...]). Two launches:
+// overflow_classify_kernel classifies their strings into the HBM class arrays (tables read from the
+// blob, one workgroup per request), then overflow_eval_kernel walks each request sequentially
+// (slots.hpp walk_*, one lane per request) over every chunk of the launch.
+// ------------------------------------------------------------------------------------------
 constexpr int kOverflowThreads = 256;
+
+__device__ inline Classifiers blob_classifiers(const EvalArgs& a, const TileArgs& t) {
+  Classifiers C;
+  for (int c = 0; c < (int)NCOL; ++c) {
+    C.lit[c] = t.lit_blob[c] ? a.blob + t.lit_blob[c] : nullptr;
+    C.dfa[c].head = t.dfa_blob[c];
+    C.dfa[c].base = a.blob + t.dfa_blob[c];
+  }
+  C.kv = t.kv_blob ? a.blob + t.kv_blob : nullptr;
+  C.nlk = t.nlk;
+  C.docker_io_cls = t.docker_io_cls;
+  C.latest_cls = t.latest_cls;
+  return C;
+}
+
 __global__ void __launch_bounds__(kOverflowThreads)
     overflow_classify_kernel(EvalArgs a, const TileArgs* __restrict__ tp, const uint32_t* __restrict__ overflow) {
   const TileArgs& t = *tp;
   const uint32_t count = overflow[0];
   const uint32_t tid = threadIdx.x;
-  Chain ch[NMASK];
-#pragma unroll
-  for (int k = 0; k < (int)NMASK; ++k) {
-    ch[k].head = t.dfa_head[k];
-    ch[k].base = a.blob + t.dfa_head[k];
-  }
+  const Classifiers C = blob_classifiers(a, t);
+  const ImgLayout il = t.il;
+  const uint32_t nim = il.n(), nlv = t.nlv;
   for (uint32_t q = blockIdx.x; q < count; q += gridDim.x) {
-    const uint64_t r0 = overflow[1 + q];
-    const uint32_t nr = 1;
-    const uint32_t cb = a.ctr_off[r0], ce = a.ctr_off[r0 + nr];
-    const uint32_t lb = a.lbl_off[r0], le = a.lbl_off[r0 + nr];
+    const uint64_t r = overflow[1 + q];
+    const uint32_t cb = a.ctr_off[r], ce = a.ctr_off[r + 1];
+    const uint32_t lb = a.lbl_off[r], le = a.lbl_off[r + 1];
     const uint32_t kab = a.capadd_off[cb], kae = a.capadd_off[ce];
     const uint32_t kdb = a.capdrop_off[cb], kde = a.capdrop_off[ce];
-    const uint32_t nc = ce - cb;
-    if (a.m[M_NS])
-      for (uint32_t i = tid; i < nr; i += kOverflowThreads)
-        ((uint64_t*)a.m[M_NS])[r0 + i] =
-            classify_one<M_NS>(ch[M_NS], t.s_bytes[M_NS], t.s_off[M_NS][r0 + i], t.s_off[M_NS][r0 + i + 1]);
-    if (a.m[M_REG] || a.m[M_TAG] || a.m[M_IMG])
-      for (uint32_t i = tid; i < nc; i += kOverflowThreads) {
-        uint64_t mr = 0, mt = 0, mi = 0;
-        if (a.ctr_flags[cb + i] & KW_CTR_HAS_IMAGE)
-          classify_image_all(ch[M_REG], ch[M_TAG], ch[M_IMG], t.s_bytes[M_IMG], t.s_off[M_IMG][cb + i],
-                             t.s_off[M_IMG][cb + i + 1], &mr, &mt, &mi);
-        if (a.m[M_REG]) ((uint64_t*)a.m[M_REG])[cb + i] = mr;
-        if (a.m[M_TAG]) ((uint64_t*)a.m[M_TAG])[cb + i] = mt;
-        if (a.m[M_IMG]) ((uint64_t*)a.m[M_IMG])[cb + i] = mi;
+    auto lit = [&](Col c, int m, uint32_t i) -> uint32_t {
+      return C.lit[c] ? lit_lookup<false>(C.lit[c], t.s_bytes[m], t.s_off[m][i], t.s_off[m][i + 1]) : 0u;
+    };
+    if (tid == 0) a.g_ns[r] = (uint16_t)((t.need & (1u << S_NS)) ? lit(COL_NS, S_NS, (uint32_t)r) : 0u);
+    for (uint32_t c = cb + tid; c < ce; c += kOverflowThreads) {
+      const uint32_t fl = a.ctr_flags[c];
+      if (t.need & (1u << S_AA)) a.g_aa[c] = (uint16_t)((fl & KW_CTR_HAS_APPARMOR) ? lit(COL_AA, S_AA, c) : 0u);
+      if (t.need & (1u << S_IMG)) {
+        uint16_t* ic = a.g_img + (uint64_t)c * nim;
+        if (fl & KW_CTR_HAS_IMAGE)
+          classify_image<false>(C, il, t.s_bytes[S_IMG], t.s_off[S_IMG][c], t.s_off[S_IMG][c + 1],
+                                [&](uint32_t j, uint32_t cl) { ic[j] = (uint16_t)cl; });
+        else
+          for (uint32_t j = 0; j < nim; ++j) ic[j] = 0;
       }
-    if (a.m[M_AA])
-      for (uint32_t i = tid; i < nc; i += kOverflowThreads)
-        ((uint64_t*)a.m[M_AA])[cb + i] =
-            (a.ctr_flags[cb + i] & KW_CTR_HAS_APPARMOR)
-                ? classify_one<M_AA>(ch[M_AA], t.s_bytes[M_AA], t.s_off[M_AA][cb + i], t.s_off[M_AA][cb + i + 1])
-                : 0ull;
-    if (a.m[M_CAPADD])
-      for (uint32_t i = kab + tid; i < kae; i += kOverflowThreads)
-        ((uint64_t*)a.m[M_CAPADD])[i] =
-            classify_one<M_CAPADD>(ch[M_CAPADD], t.s_bytes[M_CAPADD], t.s_off[M_CAPADD][i], t.s_off[M_CAPADD][i + 1]);
-    if (a.m[M_CAPDROP])
-      for (uint32_t i = kdb + tid; i < kde; i += kOverflowThreads)
-        ((uint64_t*)a.m[M_CAPDROP])[i] =
-            classify_one<M_CAPDROP>(ch[M_CAPDROP], t.s_bytes[M_CAPDROP], t.s_off[M_CAPDROP][i], t.s_off[M_CAPDROP][i + 1]);
-    if (a.m[M_LK])
-      for (uint32_t i = lb + tid; i < le; i += kOverflowThreads)
-        ((uint64_t*)a.m[M_LK])[i] = classify_one<M_LK>(ch[M_LK], t.s_bytes[M_LK], t.s_off[M_LK][i], t.s_off[M_LK][i + 1]);
-    if (a.m[M_LV])
-      for (uint32_t i = lb + tid; i < le; i += kOverflowThreads)
-        ((uint64_t*)a.m[M_LV])[i] = classify_one<M_LV>(ch[M_LV], t.s_bytes[M_LV], t.s_off[M_LV][i], t.s_off[M_LV][i + 1]);
+    }
+    if (t.need & (1u << S_CAPADD)) {
+      for (uint32_t k = kab + tid; k < kae; k += kOverflowThreads) a.g_capadd[k] = (uint16_t)lit(COL_CAP, S_CAPADD, k);
+      for (uint32_t k = kdb + tid; k < kde; k += kOverflowThreads) a.g_capdrop[k] = (uint16_t)lit(COL_CAP, S_CAPDROP, k);
+    }
+    if (t.need & (1u << S_LK))
+      for (uint32_t l = lb + tid; l < le; l += kOverflowThreads) {
+        const uint32_t k = lit(COL_LK, S_LK, l);
+        a.g_lk[l] = (uint16_t)k;
+        uint16_t* lv = a.g_lv + (uint64_t)l * nlv;
+        classify_value(C, k, nlv, t.s_bytes[S_LV], t.s_off[S_LV][l], t.s_off[S_LV][l + 1],
+                       [&](uint32_t j, uint32_t c) { lv[j] = (uint16_t)c; });
+      }
   }
 }
+
+// Accessor of the sequential walks over the HBM class arrays (absolute entity indices).
+struct GlobalSrc {
+  const EvalArgs* a;
+  ImgLayout il;
+  uint32_t nlv_;
+  __device__ uint32_t rf(uint64_t r) const { return a->req_flags[r]; }
+  __device__ uint32_t coff(uint64_t r) const { return a->ctr_off[r]; }
+  __device__ uint32_t loff(uint64_t r) const { return a->lbl_off[r]; }
+  __device__ uint32_t cflags(uint32_t c) const { return a->ctr_flags[c]; }
+  __device__ uint32_t cadd(uint32_t c) const { return a->capadd_off[c]; }
+  __device__ uint32_t cdrop(uint32_t c) const { return a->capdrop_off[c]; }
+  __device__ uint32_t ns(uint64_t r) const { return a->g_ns[r]; }
+  __device__ uint32_t aa(uint32_t c) const { return a->g_aa[c]; }
+  __device__ uint32_t capadd(uint32_t k) const { return a->g_capadd[k]; }
+  __device__ uint32_t capdrop(uint32_t k) const { return a->g_capdrop[k]; }
+  __device__ uint32_t lk(uint32_t l) const { return a->g_lk ? a->g_lk[l] : 0u; }
+  __device__ uint32_t nlv() const { return nlv_; }
+  __device__ uint32_t lv(uint32_t l, uint32_t j) const { return a->g_lv[(uint64_t)l * nlv_ + j]; }
+  __device__ uint32_t img(uint32_t c, uint32_t j) const { return a->g_img[(uint64_t)c * il.n() + j]; }
+};
 
 __global__ void __launch_bounds__(kOverflowThreads)
     overflow_eval_kernel(EvalArgs a, const TileArgs* __restrict__ tp, const uint32_t* __restrict__ overflow) {
-  __shared__ uint16_t gstk[kMaxGroupStack * kOverflowThreads];
   const TileArgs& t = *tp;
   const uint32_t count = overflow[0];
-  const DevHeader H = *(const DevHeader*)a.blob;
-  const DevPolicy* __restrict__ pols = (const DevPolicy*)(a.blob + H.policy_off);
-  const uint32_t npol = a.npol;
-  const uint64_t items = (uint64_t)count * npol;
-  GlobalSrc src{&a};
-  (void)t;
-  for (uint64_t it = (uint64_t)blockIdx.x * kOverflowThreads + threadIdx.x; it < items;
-       it += (uint64_t)gridDim.x * kOverflowThreads) {
-    const uint32_t j = (uint32_t)(it % npol);
-    const uint64_t r = overflow[1 + it / npol];
-    const DevPolicy& P = pols[a.pols[j]];
-    a.out[r * npol + j] = verdict(src, a, H, pols, P, r, gstk + threadIdx.x, kOverflowThreads);
+  GlobalSrc src{&a, t.il, t.nlv};
+  for (uint32_t q = blockIdx.x * kOverflowThreads + threadIdx.x; q < count; q += gridDim.x * kOverflowThreads) {
+    const uint64_t r = overflow[1 + q];
+    const bool byp = is_bypass(a.req_flags[r], a.g_ns[r], t.bypass_cls);
+    for (uint32_t ck = 0; ck < t.nchunk; ++ck) {
+      const ChunkArgs& CA = t.chunk[ck];
+      SlotView sv;
+      sv.base = CA.rec;
+      sv.h = (const SlotHdr*)CA.rec;
+      uint32_t vw[kSlots], va[kSlots];
+      const ViolSink vs{vw, va};
+      uint64_t mut = 0, rej = 0;
+      if (!byp) {
+        rej = walk_privileged_caps(src, sv, r, vs, &mut);
+        rej |= walk_apparmor_images(src, sv, r, vs);
+        if (a.g_lk) rej |= walk_labels(src, sv, r, vs);
+        rej |= walk_namespace(src, sv, r, vs);
+      }
+      const ColInfo* cols = (const ColInfo*)(CA.rec + sv.h->o_cols);
+      auto emit = [&](uint32_t j, uint32_t* dst) {
+        if (byp) {
+          *dst = kBypassWord;
+          return;
+        }
+        uint64_t wide = 0;
+        const ColInfo& ci = cols[j];
+        const uint32_t w = column_word(ci, rej, mut, CA.init, vw, CA.rec, &wide);
+        *dst = w;
+        if (KW_REASON(w) == 0 || KW_ARG(w) != kArgWide) return;
+        if (KW_REASON(w) == KW_R_GROUP) {
+          a.wide_groups[r * a.nwide + ci.wide] = wide;
+        } else if (ci.kind == CK_PLAIN && ((rej >> ci.slot) & 1ull)) {  // entity index >= 65535
+          const uint32_t at = atomicAdd(a.wide_count, 1u);
+          if (at < a.wide_cap) {
+            WideRec wr;
+            wr.row_lo = (uint32_t)r;
+            wr.row_hi = (uint32_t)(r >> 32);
+            wr.policy = ci.policy;
+            wr.value = va[ci.slot];
+            a.wide_rec[at] = wr;
+          }
+        }
+      };
+      if (t.rows_mode) {
+        const uint32_t rc = a.rowcol[r];
+        if ((rc >> 16) == ck) emit(rc & 0xffffu, a.out + r);
+      } else {
+        for (uint32_t j = 0; j < CA.ncols; ++j) emit(j, a.out + r * a.npol + CA.col0 + j);
+      }
+    }
   }
 }
 
-hipError_t launch_classify(const uint8_t* d_blob, const ClassifyJobs& jobs, hipStream_t s) {
-  if (jobs.n == 0 || jobs.total_blocks == 0) return hipSuccess;
-  if (jobs.lds_bytes > 0)
-    hipLaunchKernelGGL(classify_kernel<true>, dim3(jobs.total_blocks), dim3(kClassifyThreads), jobs.lds_bytes, s, d_blob,
-                       jobs);
-  else
-    hipLaunchKernelGGL(classify_kernel<false>, dim3(jobs.total_blocks), dim3(kClassifyThreads), 0, s, d_blob, jobs);
-  return hipGetLastError();
-}
+// ------------------------------------------------------------------------------------------
+// Launchers
+// ------------------------------------------------------------------------------------------
+namespace {
+// hipFuncSetAttribute is per device: set once per device, thread-safe (std::call_once).
+constexpr int kMaxDevices = 64;
+std::once_flag g_attr_once[kMaxDevices];
+hipError_t g_attr_err[kMaxDevices];
 
-hipError_t launch_evaluate_rows(const EvalArgs& a, hipStream_t s) {
-  if (a.nrows == 0) return hipSuccess;
-  uint64_t blocks = (a.nrows + kEvalThreads - 1) / kEvalThreads;
-  if (blocks > 256 * 16) blocks = 256 * 16;
-  hipLaunchKernelGGL(evaluate_rows_kernel, dim3((uint32_t)blocks), dim3(kEvalThreads), 0, s, a);
-  return hipGetLastError();
+hipError_t ensure_attrs() {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
+  std::call_once(g_attr_once[dev], [dev] {
+    // allow > 64 KB of dynamic LDS per workgroup (gfx950: 160 KB per CU)
+    hipError_t e1 = hipFuncSetAttribute((const void*)evaluate_tiles_kernel<true>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipError_t e2 = hipFuncSetAttribute((const void*)evaluate_tiles_kernel<false>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    g_attr_err[dev] = e1 != hipSuccess ? e1 : e2;
+  });
+  return g_attr_err[dev];
 }
+}  // namespace
 
-hipError_t launch_evaluate_slots(const EvalArgs& a, const TileArgs& t, const TileArgs* d_t, const TileDesc* d_desc,
-                                 bool fused, uint32_t grid, hipStream_t s) {
-  if (a.nrows == 0 || t.ncols == 0) return hipSuccess;
-  static bool attr_set = false;  // allow > 64 KB of dynamic LDS per workgroup (gfx950: 160 KB per CU)
-  if (!attr_set) {
-    hipError_t e1 = hipFuncSetAttribute((const void*)evaluate_slots_kernel<true>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipError_t e2 = hipFuncSetAttribute((const void*)evaluate_slots_kernel<false>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e1 != hipSuccess || e2 != hipSuccess) return e1 != hipSuccess ? e1 : e2;
-    attr_set = true;
-  }
+hipError_t launch_evaluate_tiles(const EvalArgs& a, const TileArgs& t, const TileArgs* d_t, const TileDesc* d_desc,
+                                 uint32_t grid, hipStream_t s) {
+  if (a.nrows == 0 || t.nchunk == 0 || a.ndesc == 0) return hipSuccess;
+  if (hipError_t e = ensure_attrs(); e != hipSuccess) return e;
   // The grid is persistent (tiles strided by gridDim.x), so it must be co-resident: a workgroup
   // that only starts when another retires doubles the tail. Clamp the planner's grid to the
-  // runtime's occupancy for this LDS size (queried once per device and LDS size).
+  // runtime's occupancy for this LDS size (queried once per device and LDS size, per thread).
   {
     thread_local int c_dev = -1, c_ncu = 0, c_occ = 0;
     thread_local uint64_t c_key = ~0ull;
     int dev = 0;
-    const uint64_t key = ((uint64_t)t.lds_bytes << 1) | (fused ? 1u : 0u);
+    const uint64_t key = ((uint64_t)t.lds_bytes << 1) | (t.lds_tables ? 1u : 0u);
     if (hipGetDevice(&dev) == hipSuccess && (dev != c_dev || key != c_key)) {
       int ncu = 0, occ = 0;
-      const void* fn = fused ? (const void*)evaluate_slots_kernel<true> : (const void*)evaluate_slots_kernel<false>;
+      const void* fn = t.lds_tables ? (const void*)evaluate_tiles_kernel<true> : (const void*)evaluate_tiles_kernel<false>;
       if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
           hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kSlotThreads, t.lds_bytes) != hipSuccess)
         ncu = occ = 0;
@@ -1185,22 +982,19 @@ hipError_t launch_evaluate_slots(const EvalArgs& a, const TileArgs& t, const Til
     if (t.debug & 256u)
       fprintf(stderr, "[kw tile] launch grid=%u occupancy=%d wg/cu x %d CUs lds=%u\n", grid, c_occ, c_ncu, t.lds_bytes);
   }
-  if (fused)
-    hipLaunchKernelGGL(evaluate_slots_kernel<true>, dim3(grid), dim3(kSlotThreads), t.lds_bytes, s, a, d_t, d_desc,
-                       a.blob, a.out);
+  if (t.lds_tables)
+    hipLaunchKernelGGL(evaluate_tiles_kernel<true>, dim3(grid), dim3(kSlotThreads), t.lds_bytes, s, a, d_t, d_desc);
   else
-    hipLaunchKernelGGL(evaluate_slots_kernel<false>, dim3(grid), dim3(kSlotThreads), t.lds_bytes, s, a, d_t, d_desc,
-                       a.blob, a.out);
+    hipLaunchKernelGGL(evaluate_tiles_kernel<false>, dim3(grid), dim3(kSlotThreads), t.lds_bytes, s, a, d_t, d_desc);
   return hipGetLastError();
 }
 
 hipError_t launch_overflow(const EvalArgs& a, const TileArgs* d_t, const uint32_t* d_overflow, uint32_t n_overflow,
                            hipStream_t s) {
-  if (n_overflow == 0 || a.nrows == 0 || a.npol == 0) return hipSuccess;
+  if (n_overflow == 0 || a.nrows == 0) return hipSuccess;
   hipLaunchKernelGGL(overflow_classify_kernel, dim3(std::min<uint32_t>(n_overflow, 1024)), dim3(kOverflowThreads), 0, s,
                      a, d_t, d_overflow);
-  const uint64_t items = (uint64_t)n_overflow * a.npol;
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>((items + kOverflowThreads - 1) / kOverflowThreads, 4096);
+  const uint32_t blocks = std::min<uint32_t>((n_overflow + kOverflowThreads - 1) / kOverflowThreads, 1024);
   hipLaunchKernelGGL(overflow_eval_kernel, dim3(blocks), dim3(kOverflowThreads), 0, s, a, d_t, d_overflow);
   return hipGetLastError();
 }

@@ -1,24 +1,31 @@
 // kwdev.hpp — layout of the compiled-table blob shared by the host compiler (env.cpp) and the
 // HIP kernels (kernels.hip). The blob is position independent (offsets from its start), so the
 // same bytes are uploaded to every GPU and broadcast over RCCL.
+//
+// The blob holds only *classifiers*: for every request column, the tables that turn a string into
+// a small integer class (a literal perfect hash, a DFA chain with an accept class per state, and
+// for label values one DFA chain per constrained label key). Which policies a class violates is a
+// property of the policy list a pass answers, so those tables live in the slot-plan records
+// (slots.hpp), compiled per policy list. No table is indexed by pattern bits, so nothing bounds the
+// number of patterns a policy set may name.
 #pragma once
 #include <cstdint>
 
 namespace kw {
 
-constexpr uint32_t kBlobMagic = 0x4b574731;  // "KWG1"
-constexpr uint32_t kBlobVersion = 2;
+constexpr uint32_t kBlobMagic = 0x4b574733;  // "KWG3"
+constexpr uint32_t kBlobVersion = 3;
 
-// request columns that carry strings classified by a DFA
+// request columns that carry strings classified by a DFA or a literal table
 enum Col : uint32_t {
-  COL_NS = 0,   // request namespace
-  COL_REG = 1,  // image registry (normalised)
-  COL_TAG = 2,  // image effective tag
-  COL_IMG = 3,  // normalised image reference
-  COL_CAP = 4,  // capability names (add and drop lists)
-  COL_AA = 5,   // AppArmor profile
-  COL_LK = 6,   // label key
-  COL_LV = 7,   // label value
+  COL_NS = 0,   // request namespace                                   (literal table)
+  COL_REG = 1,  // image registry (normalised)                         (literal table + DFA chain)
+  COL_TAG = 2,  // image effective tag                                 (literal table + DFA chain)
+  COL_IMG = 3,  // normalised image reference                          (DFA chain)
+  COL_CAP = 4,  // capability names (add and drop lists)               (literal table)
+  COL_AA = 5,   // AppArmor profile                                    (literal table)
+  COL_LK = 6,   // label key                                           (literal table)
+  COL_LV = 7,   // label value, against the regexes of its key         (per-key DFA chains)
   NCOL = 8
 };
 
@@ -36,18 +43,21 @@ enum Family : uint8_t {
 enum PolicyFlag : uint8_t {
   PF_SKIP_INIT = 1,
   PF_SKIP_EPHEMERAL = 2,
-  PF_ALLOW_ALL = 4,     // psp-capabilities allowed_capabilities contains "*"
-  PF_INIT_ERROR = 8,    // PolicyInitialization recorded (continue_on_errors)
-  PF_EXPR_ERROR = 16,   // group expression does not evaluate to a bool
-  PF_REGISTERED = 32
+  PF_ALLOW_ALL = 4,  // psp-capabilities allowed_capabilities contains "*"
 };
 
-// group program opcodes (postfix, bool stack with evaluated-member masks)
-enum GOp : uint8_t { G_CONST0 = 0, G_CONST1 = 1, G_CALL = 2, G_NOT = 3, G_AND = 4, G_OR = 5, G_EQ = 6, G_NE = 7 };
-constexpr int kMaxGroupStack = 16;
-constexpr int kMaxGroupMembers = 16;
-constexpr int kMaxListIdx = 16;
-constexpr size_t kKvDfaBytes = 3072;  // u16 table bytes of one per-key label-value DFA before the key chains
+// Group programs: short-circuit jump code over the member results (expr.cpp emits it, slots.hpp
+// run_group_prog runs it). The value stack is a bit stack in one u64; a member call records the
+// member as evaluated, exactly as rhai's lazy || and && call members (evaluation_environment.rs:979-1042).
+//   G_CONST0 / G_CONST1     push false / true
+//   G_CALL s                push ok(s); s is the member slot (one byte)
+//   G_NOT                   negate the top
+//   G_JT t / G_JF t         (||, &&) top true / false: jump to byte t (u16 LE), keeping it; else pop
+//   G_EQ / G_NE             pop b, pop a, push a == b / a != b
+enum GOp : uint8_t { G_CONST0 = 0, G_CONST1 = 1, G_CALL = 2, G_NOT = 3, G_JT = 4, G_JF = 5, G_EQ = 6, G_NE = 7 };
+constexpr int kMaxGroupStack = 64;    // value-stack depth (only == / != nest it)
+constexpr int kMaxGroupMembers = 64;  // members evaluate as slots of one slot-plan chunk
+constexpr int kMaxLocalBits = 64;     // per chunk: distinct mandatory label keys / mutation capabilities
 
 #if defined(__HIPCC__)
 #define KW_HD __host__ __device__
@@ -55,51 +65,54 @@ constexpr size_t kKvDfaBytes = 3072;  // u16 table bytes of one per-key label-va
 #define KW_HD
 #endif
 
-// Compact DFA of the per-key label-value region (every offset region-relative, region < 64 KB):
-// u8 transitions (nstates <= 256), accept masks deduplicated (a u8 index per state into u64
-// accv[]), byte-class maps shared between DFAs and cut to 128 entries when every non-ASCII byte
-// falls in one class (`hi`). The region is staged whole in LDS by the slot kernel, so its size is
-// occupancy: these cuts take the C4 region from 16.8 KB of DevDfa records to about 7 KB.
+// Compact DFA of the per-key label-value region (offsets region-relative). A label value is only
+// ever tested against the regexes constrained on its own key, so each constrained key has a chain
+// of small DFAs over just those regexes. acc[state] is the DFA's local accept class; the value's
+// global COL_LV class is kbase[key] + cbase + acc[state] (kbase: the region's per-key table), so a
+// chain shared by keys with the same regexes still gives each key its own classes.
 struct alignas(16) KvDfa {
-  uint16_t cls_off;    // u8 class of bytes [0, cls_len)
-  uint16_t trans_off;  // u8 [nstates][ncls]
-  uint16_t acc_off;    // u8 [nstates]: index into accv
-  uint16_t accv_off;   // u64 [nacc] (8-B aligned): accepted pattern bits (the column's global bits)
-  uint16_t next;       // next DFA of the key's chain, 0 = last
-  uint8_t ncls, start, hi, wide;  // hi: class of bytes >= 128 when !wide; wide: 256-entry map
-  uint16_t nstates;
+  uint32_t cls_off;    // u8 byte class of bytes [0, 128) (all 256 when wide)
+  uint32_t trans_off;  // [nstates][ncls]: u8 (t16 = 0) or u16 (t16 = 1) next state
+  uint32_t acc_off;    // u16 [nstates]: local accept class
+  uint32_t next;       // next KvDfa of the key's chain, 0 = last
+  uint32_t start;
+  uint16_t cbase, nstates, ncls;
+  uint8_t hi, wide, t16, pad[3];  // hi: class of bytes >= 128 when !wide
 };
-static_assert(sizeof(KvDfa) == 16, "KvDfa layout");
+static_assert(sizeof(KvDfa) == 32, "KvDfa layout");
 
 // One byte through a KvDfa (r: the region, LDS or blob).
 inline KW_HD uint32_t kv_step(const uint8_t* r, const KvDfa& d, uint32_t st, uint32_t c) {
   const uint32_t k = (c < 128u || d.wide) ? r[d.cls_off + c] : d.hi;
-  return r[d.trans_off + st * d.ncls + k];
+  const uint32_t i = st * d.ncls + k;
+  return d.t16 ? ((const uint16_t*)(r + d.trans_off))[i] : r[d.trans_off + i];
 }
 
+// One DFA of a column chain. acc: u16 [nstates] global class of the column (0 = no pattern).
 struct alignas(16) DevDfa {
   uint32_t nstates, ncls, start, trans_off;  // trans_off: blob offset of u16 [nstates][ncls]
-  uint32_t acc_off;                          // blob offset of u64 [nstates]
+  uint32_t acc_off;                          // blob offset of u16 [nstates]
   uint32_t bytes;                            // bytes of this DFA's record + tables (for LDS staging)
   uint32_t next;                             // blob offset of the next DFA of the column chain, 0 = last
   uint32_t chain_bytes;                      // bytes of this DFA and all that follow it in the chain
   uint8_t cls[256];
 };
 
-// Literal column: a perfect hash over the column's literal patterns (every pattern of the column
-// is a Literal). A string matches at most one pattern; lookup = hash of its canonical little-endian
-// dwords -> slot -> one verify against the pattern's words. Record layout (offsets from its start):
-//   DevLit | u32 slot[nslots] | u32 words[]
-// slot: 0 = empty, else (pattern index + 1) | len << 7 | word index << 19 (len < 4096, word
-// index < 8192), so a probe reads the slot and then the pattern words, two dependent loads.
-// words: each pattern zero-padded to whole dwords, followed by 32 zero bytes (batched verify reads).
+// Literal column part: a minimal-probe perfect hash over the column's literal patterns. A string
+// matches at most one of them; lookup = hash g of its canonical little-endian dwords -> (bucket
+// displacement) -> slot -> one verify against the pattern's words. Small sets use one bucket (no
+// displacement table: g alone is collision-free for the seed); large ones hash-and-displace
+// (bucket = top nb_log2 bits of g, slot = (g ^ lit_disp(disp[bucket])) mod nslots). Record layout
+// (offsets from its start): DevLit | u32x2 slot[nslots] | u16 disp[1 << nb_log2] | u32 words[]
+// slot.x: 0 = empty, else literal class (1 + literal index, < 65536) | len << 16 (len < 65536);
+// slot.y: word index of the pattern. words: each pattern zero-padded to whole dwords, followed by
+// 32 zero bytes (batched verify reads).
 struct alignas(16) DevLit {
-  uint32_t nslots, seed, npat, bytes;      // bytes: whole record, multiple of 16
-  uint32_t slot_off, word_off, pad0, pad1;
+  uint32_t nslots, seed, npat, bytes;  // bytes: whole record, multiple of 16
+  uint32_t slot_off, word_off, disp_off, nb_log2;
 };
-constexpr uint32_t lit_slot_pat(uint32_t s) { return s & 127u; }  // pattern index + 1
-constexpr uint32_t lit_slot_len(uint32_t s) { return (s >> 7) & 4095u; }
-constexpr uint32_t lit_slot_word(uint32_t s) { return s >> 19; }
+constexpr uint32_t lit_slot_cls(uint32_t x) { return x & 0xffffu; }
+constexpr uint32_t lit_slot_len(uint32_t x) { return x >> 16; }
 
 // hash shared by the host table builder (env.cpp) and the kernels
 inline KW_HD uint32_t lit_init(uint32_t seed, uint32_t len) { return seed ^ (len * 0x9E3779B1u); }
@@ -113,40 +126,34 @@ inline KW_HD uint32_t lit_final(uint32_t h) {
   h *= 0x7FEB352Du;
   return h ^ (h >> 15);
 }
+inline KW_HD uint32_t lit_disp(uint32_t d) { return d ? lit_final(d * 0x9E3779B1u) : 0u; }
+inline KW_HD uint32_t lit_slot_index(uint32_t g, uint32_t d, uint32_t nslots) { return (g ^ lit_disp(d)) & (nslots - 1u); }
 
-// One policy (or group member) — 192 bytes. Mask meaning per family (env.cpp):
-//   NAMESPACE:     m[0] valid-namespace bit (COL_NS)
-//   TRUSTED_REPOS: m[0] registry allow, m[1] registry reject (COL_REG), m[2] tag reject (COL_TAG),
-//                  m[3] image allow, m[4] image reject (COL_IMG); nl[k] = list length
-//   CAPABILITIES:  m[0] allowed U default_add, m[1] required_drop, m[2] default_add, m[3] "ALL" (COL_CAP)
-//   APPARMOR:      m[0] allowed profiles (COL_AA)
-//   LABELS:        m[0] denied keys, m[1] mandatory keys (COL_LK); idx[0..16) mandatory key bits,
-//                  idx[16..32) constrained key bits, idx[32..48) constrained value-regex bits (COL_LV)
-//   GROUP:         prog_off/prog_len postfix program, member_off/nmembers member policy indices
-struct alignas(16) DevPolicy {
-  uint8_t family, mode, a2m, flags;
-  uint8_t nl[6];
-  uint8_t n_mand, n_constr;
-  uint32_t prog_off, prog_len, member_off, nmembers;
-  uint32_t pad0;
-  uint64_t m[6];
-  uint8_t idx[48];
-  uint8_t pad1[64];
+// Classifier of one column. Global classes: 0 = no pattern, [1, 1 + nlit) the literal patterns,
+// then the DFA chain's accept classes (each DevDfa.acc holds global ids). A string's pattern set is
+// the union of its literal class and its class in every DFA of the chain.
+struct alignas(16) DevCol {
+  uint32_t lit_off;    // DevLit record, 0 = none
+  uint32_t dfa_off;    // head of the DFA chain, 0 = none
+  uint32_t nclass;     // global classes of the column (COL_LV: of the per-key region)
+  uint32_t nlit;       // literal patterns
+  uint32_t ndfa;       // DFAs in the chain (COL_LV: the longest per-key chain)
+  uint32_t dfa_bytes;  // bytes of the whole chain (COL_LV: of the per-key region)
+  uint32_t lit_bytes;
+  uint32_t pad;
 };
-static_assert(sizeof(DevPolicy) == 192, "DevPolicy layout");
 
 struct alignas(16) DevHeader {
-  uint32_t magic, version, npolicies, blob_bytes;
-  uint32_t dfa_off[NCOL];  // head of the column's DFA chain, 0 = no patterns for this column
-  uint32_t lit_off[NCOL];  // DevLit record of an all-literal column, 0 = none
-  // per-key label-value DFAs: region = u16 idx[64] (region-relative offset of the first KvDfa for
-  // label-key bit k over the value regexes constrained on that key, 0 = none) + shared byte-class
-  // maps + the KvDfa records and tables; a key's DFAs form a chain through KvDfa.next
-  uint32_t kv_off, kv_bytes;  // 0 = none (the COL_LV chain is used)
-  int32_t bypass_bit;      // COL_NS bit of the always-accept namespace, -1 = none
-  uint32_t policy_off;     // DevPolicy[npolicies]
-  uint32_t prog_off;       // group programs (bytes)
-  uint32_t member_off;     // group member indices (i32)
+  uint32_t magic, version, blob_bytes, npatterns;
+  DevCol col[NCOL];
+  // per-key label-value region: u32 kidx[nlk] (region-relative offset of the first KvDfa of label
+  // key class k, 0 = the key has no constraints) | u32 kbase[nlk] (COL_LV class base of key k) |
+  // byte-class maps | KvDfa records and tables; nlk = col[COL_LK].nclass
+  uint32_t kv_off, kv_bytes;
+  uint32_t bypass_cls;     // COL_NS class of the always-accept namespace, 0 = none
+  uint32_t docker_io_cls;  // COL_REG literal class of "docker.io" (implicit registry), 0 = none
+  uint32_t latest_cls;     // COL_TAG literal class of "latest" (implicit tag), 0 = none
+  uint32_t pad[3];
 };
 
 }  // namespace kw

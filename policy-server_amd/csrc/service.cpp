@@ -37,52 +37,112 @@ void image_parts(std::string_view s, std::string* registry, std::string* tag, bo
   }
 }
 
-std::string policy_message(const Env& env, const Batch& b, uint64_t row, int32_t pidx, uint32_t reason, uint32_t arg) {
+bool WideData::lookup(uint64_t row, int32_t policy, uint64_t* v) const {
+  if (nwide) {
+    if (rows_mode) {
+      if (row < groups.size()) {
+        // rows mode: the row's own column is the only wide one it can have
+        for (int32_t p : wide_policy)
+          if (p == policy) {
+            *v = groups[row];
+            return true;
+          }
+      }
+    } else {
+      for (uint32_t k = 0; k < nwide && k < wide_policy.size(); ++k)
+        if (wide_policy[k] == policy && row * nwide + k < groups.size()) {
+          *v = groups[row * nwide + k];
+          return true;
+        }
+    }
+  }
+  auto it = std::lower_bound(recs.begin(), recs.end(), std::make_pair(row, policy), [](const Rec& r, const std::pair<uint64_t, int32_t>& k) {
+    return r.row < k.first || (r.row == k.first && r.policy < k.second);
+  });
+  if (it != recs.end() && it->row == row && it->policy == policy) {
+    *v = it->value;
+    return true;
+  }
+  return false;
+}
+
+// The full argument of a verdict word: its ARG, or the pass's side value when ARG is kArgWide.
+static Status full_arg(const Batch& b, uint64_t row, int32_t pidx, uint32_t arg, uint64_t* out) {
+  if (arg != 0xffffu) {
+    *out = arg;
+    return {};
+  }
+  if (!b.wide.lookup(row, pidx, out)) return {KW_E_ENGINE, "verdict argument not found in the pass's side data"};
+  return {};
+}
+
+Status policy_message(const Env& env, const Batch& b, uint64_t row, int32_t pidx, uint32_t reason, uint64_t arg,
+                      std::string* msg) {
   const PolicyRec& P = env.pol[(size_t)pidx];
-  const uint32_t cb = b.ctr_off[row], lb = b.lbl_off[row];
+  const uint32_t cb = b.ctr_off[row], ce = b.ctr_off[row + 1], lb = b.lbl_off[row], le = b.lbl_off[row + 1];
   auto q = [](std::string_view s) { return "'" + std::string(s) + "'"; };
-  auto cname = [&](uint32_t c) { return std::string(b.ctr_name.at(cb + c)); };
-  auto cimage = [&](uint32_t c) { return std::string(b.ctr_image.at(cb + c)); };
+  const Status bad{KW_E_ENGINE, "verdict argument out of range for the request"};
+  std::string_view name, image, s1, s2;
   switch (reason) {
-    case KW_R_PRIVILEGED: return "Privileged container is not allowed";  // integration_test.rs:64
+    case KW_R_PRIVILEGED: *msg = "Privileged container is not allowed"; return {};  // integration_test.rs:64
     case KW_R_NAMESPACE:
-      return "namespace " + q(b.ns.at(row)) + " is not accepted: only " + q(P.lists[0].empty() ? "" : P.lists[0][0]) +
+      *msg = "namespace " + q(b.ns.at(row)) + " is not accepted: only " + q(P.lists[0].empty() ? "" : P.lists[0][0]) +
              " is allowed";
+      return {};
     case KW_R_REG_NOT_ALLOWED:
     case KW_R_REG_REJECTED:
     case KW_R_TAG_REJECTED:
     case KW_R_IMG_NOT_ALLOWED:
-    case KW_R_IMG_REJECTED: {
+    case KW_R_IMG_REJECTED: {  // arg: container index within the request
+      if (arg >= ce - cb || !b.ctr_name.get(cb + arg, &name) || !b.ctr_image.get(cb + arg, &image)) return bad;
       std::string reg, tag;
       bool has_tag;
-      image_parts(b.ctr_image.at(cb + arg), &reg, &tag, &has_tag);
-      std::string head = "container " + q(cname(arg)) + " uses image " + q(cimage(arg));
-      if (reason == KW_R_REG_NOT_ALLOWED) return head + ": registry " + q(reg) + " is not in the allowed registries";
-      if (reason == KW_R_REG_REJECTED) return head + ": registry " + q(reg) + " is rejected";
-      if (reason == KW_R_TAG_REJECTED) return head + ": tag " + q(tag) + " is rejected";
-      if (reason == KW_R_IMG_NOT_ALLOWED) return head + ", which is not in the allowed images";
-      return head + ", which is rejected";
+      image_parts(image, &reg, &tag, &has_tag);
+      const std::string head = "container " + q(name) + " uses image " + q(image);
+      if (reason == KW_R_REG_NOT_ALLOWED) *msg = head + ": registry " + q(reg) + " is not in the allowed registries";
+      else if (reason == KW_R_REG_REJECTED) *msg = head + ": registry " + q(reg) + " is rejected";
+      else if (reason == KW_R_TAG_REJECTED) *msg = head + ": tag " + q(tag) + " is rejected";
+      else if (reason == KW_R_IMG_NOT_ALLOWED) *msg = head + ", which is not in the allowed images";
+      else *msg = head + ", which is rejected";
+      return {};
     }
-    case KW_R_CAP_NOT_ALLOWED: {
-      uint32_t c = arg >> 8, k = arg & 0xff;
-      uint32_t cap = b.capadd_off[cb + c] + k;
-      return "container " + q(cname(c)) + " adds capability " + q(b.cap_add.at(cap)) + ", which is not allowed";
+    case KW_R_CAP_NOT_ALLOWED: {  // arg: index in the request's capabilities.add lists, flattened
+      const uint64_t k0 = b.capadd_off[cb], k = k0 + arg;
+      if (k >= b.capadd_off[ce]) return bad;
+      // the container whose add list holds entry k
+      const uint32_t c = (uint32_t)(std::upper_bound(b.capadd_off.begin() + cb, b.capadd_off.begin() + ce + 1, (uint32_t)k) -
+                                    b.capadd_off.begin()) - 1;
+      if (c < cb || c >= ce || !b.ctr_name.get(c, &name) || !b.cap_add.get(k, &s1)) return bad;
+      *msg = "container " + q(name) + " adds capability " + q(s1) + ", which is not allowed";
+      return {};
     }
     case KW_R_APPARMOR:
-      return "container " + q(cname(arg)) + " uses AppArmor profile " + q(b.ctr_aa.at(cb + arg)) +
-             ", which is not allowed";
-    case KW_R_LABEL_DENIED: return "label " + q(b.lbl_key.at(lb + arg)) + " is denied";
-    case KW_R_LABEL_CONSTRAINT: {
-      uint32_t l = arg >> 8, i = arg & 0xff;
-      return "label " + q(b.lbl_key.at(lb + l)) + " value " + q(b.lbl_val.at(lb + l)) + " does not match the constraint " +
-             q(P.lists[3][i]);
+      if (arg >= ce - cb || !b.ctr_name.get(cb + arg, &name) || !b.ctr_aa.get(cb + arg, &s1)) return bad;
+      *msg = "container " + q(name) + " uses AppArmor profile " + q(s1) + ", which is not allowed";
+      return {};
+    case KW_R_LABEL_DENIED:
+      if (arg >= le - lb || !b.lbl_key.get(lb + arg, &s1)) return bad;
+      *msg = "label " + q(s1) + " is denied";
+      return {};
+    case KW_R_LABEL_CONSTRAINT: {  // arg: label index; the constraint is the policy's on that key
+      if (arg >= le - lb || !b.lbl_key.get(lb + arg, &s1) || !b.lbl_val.get(lb + arg, &s2)) return bad;
+      for (size_t i = 0; i < P.lists[2].size(); ++i)
+        if (P.lists[2][i] == s1) {
+          *msg = "label " + q(s1) + " value " + q(s2) + " does not match the constraint " + q(P.lists[3][i]);
+          return {};
+        }
+      return bad;
     }
-    case KW_R_LABEL_MANDATORY: return "mandatory label " + q(P.lists[1][arg]) + " is missing";
-    case KW_R_GROUP: return P.message;
-    case KW_R_GROUP_EXPR: return P.prog.valid ? P.prog.eval_message : P.prog.error;
-    case KW_R_INIT_ERROR: return P.init_message;
+    case KW_R_LABEL_MANDATORY:
+      if (arg >= P.lists[1].size()) return bad;
+      *msg = "mandatory label " + q(P.lists[1][arg]) + " is missing";
+      return {};
+    case KW_R_GROUP: *msg = P.message; return {};
+    case KW_R_GROUP_EXPR: *msg = P.prog.valid ? P.prog.eval_message : P.prog.error; return {};
+    case KW_R_INIT_ERROR: *msg = P.init_message; return {};
   }
-  return "";
+  msg->clear();
+  return {};
 }
 
 static void put_kv(std::string* o, const char* k, std::string_view v) {
@@ -277,7 +337,14 @@ Status format_response(const Env& env, const Batch& b, uint64_t row, int32_t pid
     return {};
   }
   // vanilla status
-  put_kv(out, "message", policy_message(env, b, row, pidx, reason, arg));
+  uint64_t full = 0;
+  if (reason != KW_R_GROUP_EXPR && reason != KW_R_INIT_ERROR) {
+    Status st = full_arg(b, row, pidx, arg, &full);
+    if (!st.ok()) return st;
+  }
+  std::string msg;
+  if (Status st = policy_message(env, b, row, pidx, reason, full, &msg); !st.ok()) return st;
+  put_kv(out, "message", msg);
   if (reason == KW_R_GROUP_EXPR) {
     out->append(",\"code\":500}}");
     return {};
@@ -286,13 +353,18 @@ Status format_response(const Env& env, const Batch& b, uint64_t row, int32_t pid
     if (!member_v) return {KW_E_ARG, "member verdicts are required to format a policy-group rejection"};
     out->append(",\"details\":{\"causes\":[");
     bool first = true;
-    for (size_t s = 0; s < P.members.size(); ++s) {
-      if (!((arg >> s) & 1u)) continue;
+    for (size_t s = 0; s < P.members.size() && s < 64; ++s) {
+      if (!((full >> s) & 1ull)) continue;
       int32_t m = P.members[s];
       uint32_t mv = member_v[s];
-      std::string msg = (mv & KW_V_MUTATED) && (mv & KW_V_ALLOWED)
-                            ? std::string("mutation is not allowed inside of policy group")  // integration_test.rs:247-250
-                            : policy_message(env, b, row, m, KW_REASON(mv), KW_ARG(mv));
+      std::string msg;
+      if ((mv & KW_V_MUTATED) && (mv & KW_V_ALLOWED)) {
+        msg = "mutation is not allowed inside of policy group";  // integration_test.rs:247-250
+      } else {
+        uint64_t marg = 0;
+        if (Status st = full_arg(b, row, m, KW_ARG(mv), &marg); !st.ok()) return st;
+        if (Status st = policy_message(env, b, row, m, KW_REASON(mv), marg, &msg); !st.ok()) return st;
+      }
       if (!first) out->push_back(',');
       first = false;
       out->append("{");

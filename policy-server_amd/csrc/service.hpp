@@ -13,8 +13,11 @@
 
 namespace kw {
 
-// Rejection message of a policy for a row (DESIGN.md §Policy families, message templates).
-std::string policy_message(const Env& env, const Batch& b, uint64_t row, int32_t pidx, uint32_t reason, uint32_t arg);
+// Rejection message of a policy for a row (DESIGN.md §Policy families, message templates), from
+// the reason and its full argument (an entity index within the request, a settings index or a group
+// cause mask). An argument out of range for the row is an engine error, never another entity's text.
+Status policy_message(const Env& env, const Batch& b, uint64_t row, int32_t pidx, uint32_t reason, uint64_t arg,
+                      std::string* msg);
 
 // Full AdmissionResponse JSON for (row, policy, verdict). member_v: member verdict words for a
 // group (settings order). Returns a non-ok Status for EvaluationError outcomes.

@@ -1,20 +1,20 @@
-// slots.hpp — bit-parallel evaluation of a policy set against one request.
+// slots.hpp — bit-parallel evaluation of a policy list against one request.
 //
-// A validate pass evaluates up to 64 "slots" per request: the selected plain policies, plus the
-// members of the selected groups (evaluated eagerly, then combined by the group program like
-// PolicyGroupEvaluator::validate [upstream], evaluation_environment.rs:587-651). A slot is one bit
-// of a u64. For every pattern bit of a request column the host compiles the set of slots that an
-// entity carrying that pattern violates (the SlotHdr tables below). A request is then evaluated by
-// walking its entities once, in object order (containers, then labels): each entity ORs its table
-// row into a "rejected" mask, and the slots that become rejected record the entity's (reason, arg).
-// The first violation per slot wins, which is the families' own order (DESIGN.md §2,
-// oracle/kworacle.c fam_*). The cost per request is O(entities + violations), not
-// O(policies x entities).
+// A validate pass answers a list of policy ids for every request of a batch
+// (EvaluationEnvironment::validate, evaluation_environment.rs:546-594). The list compiles into
+// chunks of up to 64 *slots* (one per plain policy or group member; equal settings share one) and
+// the output columns that read them. A slot is one bit of a u64.
 //
-// Shared by the device kernel (kernels.hip evaluate_slots_kernel: one lane per request, operands in
-// LDS) and the host diagnostic kw_debug_host_walk (capi.cpp), which the CPU test suite uses to
-// check the slot compiler against the oracle. The walks are templated on an entity accessor `S`
-// (rf / coff / loff / cflags / cadd / cdrop, and m<MASK>(i): the pattern mask of string i).
+// Every string of a request is first classified into a small integer (kwdev.hpp classifiers). A
+// chunk record then holds, per column class, the set of slots an entity of that class violates
+// (tables below), so an entity's violation set is one table load — however many patterns the
+// policies name. A slot's verdict is its *first* violation in object order (containers, then
+// labels; the families' own order, DESIGN.md §2, oracle/kworacle.c fam_*), and the cost per request
+// is O(entities + violations), not O(policies x entities).
+//
+// Shared by the device kernels (kernels.hip: entity-parallel in the tile kernel, the sequential
+// walks below in the overflow kernel) and the host diagnostic kw_debug_host_walk (capi.cpp), which
+// the CPU test suite uses to check the slot compiler against the oracle.
 #pragma once
 #include <cstdint>
 
@@ -23,26 +23,22 @@
 
 namespace kw {
 
-// Which mask array a classification writes (one u64 per string).
-enum MaskArr : uint32_t { M_NS = 0, M_REG, M_TAG, M_IMG, M_CAPADD, M_CAPDROP, M_AA, M_LK, M_LV, NMASK };
-
 constexpr uint32_t kSlots = 64;
+constexpr uint32_t kArgWide = 0xffffu;  // ARG sentinel: the full value is in the pass's side data
 
-// Per-pattern-bit slot tables, each u64[64] indexed by the column's pattern bit.
+// Per-class slot tables, each u64[nclass of its column] indexed by the column class.
 enum SlotTab : uint32_t {
-  ST_NA_CAP = 0,  // COL_CAP: psp-capabilities slots (without "*") that do not allow the capability
-  ST_REQD,        // COL_CAP: slots whose required_drop_capabilities lists the capability
-  ST_DEFA,        // COL_CAP: slots whose default_add_capabilities lists the capability
-  ST_NA_AA,       // COL_AA:  psp-apparmor slots that do not allow the profile
-  ST_DENY,        // COL_LK:  safe-labels slots that deny the key
-  ST_MAND,        // COL_LK:  safe-labels slots that make the key mandatory
-  ST_NSOK,        // COL_NS:  namespace slots that accept the namespace
-  ST_RA,          // COL_REG: trusted-repos slots whose registries.allow matches
-  ST_RR,          // COL_REG: ... registries.reject
-  ST_TR,          // COL_TAG: ... tags.reject
-  ST_IA,          // COL_IMG: ... images.allow
-  ST_IR,          // COL_IMG: ... images.reject
-  NST
+  T_NSOK = 0,  // COL_NS:  namespace slots whose valid_namespace is this class
+  T_RA,        // COL_REG: trusted-repos slots whose registries.allow matches
+  T_RR,        // COL_REG: ... registries.reject
+  T_TR,        // COL_TAG: ... tags.reject
+  T_IA,        // COL_IMG: ... images.allow
+  T_IR,        // COL_IMG: ... images.reject
+  T_NACAP,     // COL_CAP: strict psp-capabilities slots that allow neither the capability nor default-add it
+  T_NAAA,      // COL_AA:  psp-apparmor slots that do not allow the profile
+  T_DENY,      // COL_LK:  safe-labels slots that deny the key
+  T_FAIL,      // COL_LV:  safe-labels slots whose constraint on the label's key the value fails
+  NTAB
 };
 
 struct alignas(16) SlotHdr {
@@ -52,46 +48,41 @@ struct alignas(16) SlotHdr {
   uint64_t has_ra, has_ia;  // trusted-repos slots with a non-empty registries.allow / images.allow
   uint64_t priv[4];         // pod-privileged slots by (skip_init | skip_ephemeral << 1)
   uint64_t init;            // slots whose policy failed to initialise (group members: never ok)
-  uint64_t reqd_union, defa_union, mand_union;  // pattern bits some slot lists (COL_CAP, COL_CAP, COL_LK)
-  uint64_t cap_all;         // COL_CAP bit of "ALL" (0 = none)
-  uint32_t ncols, nslots, nce, bytes;    // bytes: whole record (multiple of 16)
-  uint32_t o_ce, o_mand, o_cols, o_cidx;  // byte offsets of the sections from the record start
-  uint16_t tab_off[NST];        // byte offset of table k from the record start (0 = not emitted)
-  uint16_t ce_off[kSlots + 1];  // constraint entries of label-key bit k: [ce_off[k], ce_off[k+1])
-  uint16_t o_csoa;  // column arrays (kind | slot << 8, okw, mutw, rejb), each ncols rounded up to 4 u32
+  // local bits (per chunk): capabilities some slot requires dropped / adds by default ("ALL" always
+  // has one when the chunk has psp-capabilities slots), and mandatory label keys
+  uint64_t reqd_union, defa_union, all_bit, mand_union;
+  uint64_t pad0;
+  uint32_t ncols, nslots, bytes, staged;  // bytes: whole record; staged: prefix the device keeps in LDS
+  uint32_t tab_off[NTAB];                 // byte offset of each class table (0 = not emitted)
+  uint32_t o_capmb, o_lkmb;               // u8 per COL_CAP / COL_LK class: its local bit, 0xff = none
+  uint32_t o_reqd, o_defa, o_mand;        // u64[64] per local bit: the slots that list it
+  uint32_t o_mlist;                       // u32 per slot: offset of its mandatory list (local bits in
+                                          // settings order, 0xff-terminated), 0 = none
+  uint32_t o_csoa;   // column arrays (kind | slot << 8, okw, mutw, rejb), each ncols rounded up to 4 u32
+  uint32_t o_cols;   // ColInfo[ncols] (global memory on the device)
+  uint32_t o_prog;   // group programs (global memory on the device)
+  uint32_t nwide;    // group columns of this chunk with more than 15 members
+  uint32_t pad1[2];
 };
-static_assert(sizeof(SlotHdr) == 336, "SlotHdr layout");
-
-// safe-labels constrained_labels: the slots that constrain label-key bit k with value pattern
-// `vbit` (the settings index of each slot's constraint on k is in the cidx section).
-struct alignas(16) ConstrEnt {
-  uint64_t slots;
-  uint32_t vbit, pad;
-};
+static_assert(sizeof(SlotHdr) % 16 == 0, "SlotHdr layout");
 
 enum ColKind : uint32_t { CK_CONST = 0, CK_PLAIN = 1, CK_GROUP = 2 };
 
-// One output column (a selected policy). PLAIN: verdict of slot `slot`. GROUP: the postfix program
-// at blob offset prog_off over the member slots [slot, slot + nmem). CONST: the word `okw` whatever
+// One output column (a selected policy). PLAIN: verdict of slot `slot`. GROUP: the jump program at
+// record offset prog_off over the member slots [slot, slot + nmem). CONST: the word `okw` whatever
 // the request (initialisation error, group expression that is not a bool). okw / mutw / rejb: the
 // service-level verdict word of an accepted, an accepted-and-mutated and a rejected vanilla response
-// (reason/arg bits clear in rejb).
+// (reason/arg bits clear in rejb). wide: index of a > 15-member group in the pass's dense cause
+// array (its causes do not fit ARG), else ~0.
 struct alignas(16) ColInfo {
-  uint32_t kind, slot, nmem, prog_off, prog_len, okw, mutw, rejb;
+  uint32_t kind, slot, nmem, prog_off, prog_len, okw, mutw, rejb, wide, policy, pad[2];
 };
-static_assert(sizeof(ColInfo) == 32, "ColInfo layout");
-
-// Record: SlotHdr | emitted tables u64[64] | ConstrEnt ce[nce] | u32 column arrays[4][ncols↑4]
-//         | ColInfo[ncols] | u8 mand[64][16] | u8 cidx[nslots][64]
-// The device stages the record up to o_cols in LDS; the rest it reads from the global copy.
-// mand[s]: the label-key bits of slot s's mandatory_labels in settings order, 0xff-terminated.
-// cidx[s][k]: settings index of slot s's constraint on label-key bit k (read only to format a
-// constraint violation).
+static_assert(sizeof(ColInfo) == 48, "ColInfo layout");
 
 KW_HD inline uint32_t kw_ctz64(uint64_t x) { return (uint32_t)__builtin_ctzll(x); }
-KW_HD inline uint32_t pack2(uint32_t a, uint32_t b) { return ((a < 255u ? a : 255u) << 8) | (b < 255u ? b : 255u); }
-KW_HD inline uint32_t pack1(uint32_t a) { return a < 65535u ? a : 65535u; }
-KW_HD inline uint32_t vword(uint32_t reason, uint32_t arg) { return (reason << 8) | ((arg & 0xffffu) << 16); }
+KW_HD inline uint32_t sat16(uint32_t a) { return a < kArgWide ? a : kArgWide; }
+KW_HD inline uint32_t vword(uint32_t reason, uint32_t arg) { return (reason << 8) | (sat16(arg) << 16); }
+KW_HD inline uint64_t bit_of(uint32_t b) { return b < 64u ? 1ull << b : 0ull; }  // 0xff: none
 
 // Verdict word from a family result: the vanilla response plus validation_response_with_constraints
 // (service.rs:160-208) for the Validate origin, vanilla for Audit (service.rs:108-116).
@@ -119,13 +110,20 @@ KW_HD inline uint32_t finish_word(uint32_t mode, uint32_t a2m, int origin, uint3
 constexpr uint32_t kInitErrorWord = ((uint32_t)KW_FST_INIT_ERROR << KW_F_STATUS_SHIFT) | ((uint32_t)KW_R_INIT_ERROR << 8);
 constexpr uint32_t kBypassWord = KW_V_ALLOWED | KW_F_ALLOWED | KW_BYPASS;
 
-// Record the violation word of every slot in `nw` (the slots this entity rejects first).
-KW_HD inline void put_viol(uint32_t* vw, uint64_t nw, uint32_t word) {
-  while (nw) {
-    vw[kw_ctz64(nw)] = word;
-    nw &= nw - 1;
-  }
-}
+// The record's sections, resolved once (device: LDS or global pointers; host: the record bytes).
+struct SlotView {
+  const SlotHdr* h;
+  const uint8_t* base;
+  KW_HD const uint64_t* tab(uint32_t k) const { return (const uint64_t*)(base + h->tab_off[k]); }
+  KW_HD uint64_t row(uint32_t k, uint32_t cls) const { return tab(k)[cls]; }
+  KW_HD uint32_t capmb(uint32_t cls) const { return base[h->o_capmb + cls]; }
+  KW_HD uint32_t lkmb(uint32_t cls) const { return base[h->o_lkmb + cls]; }
+  KW_HD const uint64_t* reqd() const { return (const uint64_t*)(base + h->o_reqd); }
+  KW_HD const uint64_t* defa() const { return (const uint64_t*)(base + h->o_defa); }
+  KW_HD const uint64_t* mand() const { return (const uint64_t*)(base + h->o_mand); }
+  KW_HD const uint8_t* mlist(uint32_t s) const { return base + ((const uint32_t*)(base + h->o_mlist))[s]; }
+};
+
 // OR of table rows over the set bits of `bits`.
 KW_HD inline uint64_t tab_or(const uint64_t* t, uint64_t bits) {
   uint64_t r = 0;
@@ -135,94 +133,126 @@ KW_HD inline uint64_t tab_or(const uint64_t* t, uint64_t bits) {
   }
   return r;
 }
-// AND of table rows over the set bits of `bits`, starting from `all` (no bits: `all`).
-KW_HD inline uint64_t tab_and(const uint64_t* t, uint64_t bits, uint64_t all) {
-  uint64_t r = all;
-  while (bits) {
-    r &= t[kw_ctz64(bits)];
-    bits &= bits - 1;
-  }
-  return r;
-}
 
-// The record's sections, resolved once (device: LDS pointers; host: the record bytes).
-struct SlotView {
-  const SlotHdr* h;
-  const uint8_t* base;
-  KW_HD const uint64_t* tab(uint32_t k) const { return (const uint64_t*)(base + h->tab_off[k]); }
-  KW_HD const ConstrEnt* ce() const { return (const ConstrEnt*)(base + h->o_ce); }
-  KW_HD const uint8_t* mand() const { return base + h->o_mand; }
-  KW_HD const ColInfo* cols() const { return (const ColInfo*)(base + h->o_cols); }
+// Image classes of one container: the COL_REG entries (literal class, then one per DFA of the
+// chain), the COL_TAG entries, the COL_IMG entries, in that order.
+struct ImgLayout {
+  uint32_t nreg, ntag, nimg;
+  KW_HD uint32_t n() const { return nreg + ntag + nimg; }
 };
 
-// ---- per-entity violation sets, derived entity-parallel before the walks (the walks then only
-// apply the first-violation order): an added capability violates the strict psp-capabilities slots
-// that allow none of its pattern bits, an AppArmor profile the psp-apparmor slots that do not allow
-// it, a label the safe-labels slots whose constraint on its key its value fails (vcon; the slots
-// that deny the key are one table read in the walk).
-KW_HD inline uint64_t derive_capadd(const SlotView& sv, uint64_t m) {
-  return sv.h->caps_strict ? tab_and(sv.tab(ST_NA_CAP), m, sv.h->caps_strict) : 0ull;
-}
-KW_HD inline uint64_t derive_apparmor(const SlotView& sv, uint64_t m) {
-  return sv.h->aa ? tab_and(sv.tab(ST_NA_AA), m, sv.h->aa) : 0ull;
-}
-KW_HD inline uint64_t derive_label(const SlotView& sv, uint64_t km, uint64_t vm) {
-  uint64_t c = 0;
-  if (km && sv.h->lbl) {
-    const uint32_t kb = kw_ctz64(km);  // label keys are literal patterns: at most one bit
-    const ConstrEnt* ce = sv.ce();
-    for (uint32_t e = sv.h->ce_off[kb]; e < sv.h->ce_off[kb + 1]; ++e)
-      if (!((vm >> ce[e].vbit) & 1ull)) c |= ce[e].slots;
+// Trusted-repos reasons of one container (precedence order: registry not allowed, registry
+// rejected, tag rejected, image not allowed, image rejected; oracle fam_trusted). `ic(j)`: the
+// container's j-th image class.
+template <class F>
+KW_HD inline void trs_whys(const SlotView& sv, const ImgLayout& L, F ic, uint64_t why[5]) {
+  uint64_t ra = 0, rr = 0, tr = 0, ia = 0, ir = 0;
+  for (uint32_t j = 0; j < L.nreg; ++j) {
+    const uint32_t c = ic(j);
+    ra |= sv.row(T_RA, c);
+    rr |= sv.row(T_RR, c);
   }
-  return c;
+  for (uint32_t j = L.nreg; j < L.nreg + L.ntag; ++j) tr |= sv.row(T_TR, ic(j));
+  for (uint32_t j = L.nreg + L.ntag; j < L.n(); ++j) {
+    const uint32_t c = ic(j);
+    ia |= sv.row(T_IA, c);
+    ir |= sv.row(T_IR, c);
+  }
+  why[0] = sv.h->has_ra & ~ra;
+  why[1] = rr;
+  why[2] = tr;
+  why[3] = sv.h->has_ia & ~ia;
+  why[4] = ir;
 }
 
-// ---- walk A: pod-privileged + psp-capabilities (validation, then mutation), containers in order.
-// Returns the rejected slots; *mut_out gets the mutated-and-not-rejected psp-capabilities slots.
+// Privileged slots a container flagged `fl` violates.
+KW_HD inline uint64_t priv_viol(const SlotHdr& h, uint32_t fl) {
+  if (!(fl & KW_CTR_PRIVILEGED)) return 0ull;
+  uint64_t v = h.priv[0];
+  if (!(fl & KW_CTR_INIT)) v |= h.priv[1];
+  if (!(fl & KW_CTR_EPHEMERAL)) v |= h.priv[2];
+  if (!(fl & (KW_CTR_INIT | KW_CTR_EPHEMERAL))) v |= h.priv[3];
+  return v;
+}
+
+// Mutated psp-capabilities slots of a container from its added / dropped local bits: a required
+// drop missing (unless ALL is dropped) or a default add neither added nor dropped.
+KW_HD inline uint64_t caps_mutation(const SlotView& sv, uint64_t addm, uint64_t dropm) {
+  const SlotHdr& h = *sv.h;
+  uint64_t mut = 0;
+  if (!(dropm & h.all_bit)) mut |= tab_or(sv.reqd(), h.reqd_union & ~dropm);
+  mut |= tab_or(sv.defa(), h.defa_union & ~(addm | dropm));
+  return mut & h.caps;
+}
+
+// Index (settings order) of slot s's first mandatory key absent from `present` (local bits).
+KW_HD inline uint32_t first_missing(const SlotView& sv, uint32_t s, uint64_t present) {
+  const uint8_t* m = sv.mlist(s);
+  uint32_t i = 0;
+  for (;; ++i) {
+    const uint32_t b = m[i];
+    if (b == 0xffu || !((present >> b) & 1ull)) break;
+  }
+  return i;
+}
+
+// Violation sink of the sequential walks: the word (16-bit ARG, saturated) and the full argument.
+struct ViolSink {
+  uint32_t* vw;
+  uint32_t* va;  // may be null
+  KW_HD void put(uint64_t nw, uint32_t reason, uint32_t arg) const {
+    const uint32_t w = vword(reason, arg);
+    while (nw) {
+      const uint32_t s = kw_ctz64(nw);
+      vw[s] = w;
+      if (va) va[s] = arg;
+      nw &= nw - 1;
+    }
+  }
+};
+
+// ---- sequential walks over one request (host diagnostic and the overflow kernel). The accessor
+// S gives the request's structure (rf / coff / loff / cflags / cadd / cdrop) and the classes of its
+// strings (ns / aa / capadd / capdrop / lk / lv(l, j) / img(c, j)) with img layout `il` and nlv()
+// classes per label value. Each walk returns the rejected slots of its families.
+
+// walk A: pod-privileged + psp-capabilities (validation, then mutation), containers in order.
+// *mut_out gets the mutated-and-not-rejected psp-capabilities slots.
 template <class S>
-KW_HD uint64_t walk_privileged_caps(const S& src, const SlotView& sv, uint64_t r, uint32_t* vw, uint64_t* mut_out) {
+KW_HD uint64_t walk_privileged_caps(const S& src, const SlotView& sv, uint64_t r, const ViolSink& vs, uint64_t* mut_out) {
   const SlotHdr& h = *sv.h;
   uint64_t rej = 0, mut = 0;
   const uint64_t privany = h.priv[0] | h.priv[1] | h.priv[2] | h.priv[3];
   if ((src.rf(r) & KW_REQ_HAS_PODSPEC) && (privany | h.caps)) {
     const uint32_t cb = src.coff(r), ce = src.coff(r + 1);
+    const uint32_t kfirst = src.cadd(cb);
     for (uint32_t c = cb; c < ce; ++c) {
-      const uint32_t ci = c - cb;
       const uint32_t fl = src.cflags(c);
-      if ((fl & KW_CTR_PRIVILEGED) && privany) {
-        uint64_t cand = h.priv[0];
-        if (!(fl & KW_CTR_INIT)) cand |= h.priv[1];
-        if (!(fl & KW_CTR_EPHEMERAL)) cand |= h.priv[2];
-        if (!(fl & (KW_CTR_INIT | KW_CTR_EPHEMERAL))) cand |= h.priv[3];
-        const uint64_t nw = cand & ~rej;
-        put_viol(vw, nw, vword(KW_R_PRIVILEGED, pack1(ci)));
-        rej |= nw;
-      }
+      const uint64_t pv = priv_viol(h, fl) & ~rej;
+      vs.put(pv, KW_R_PRIVILEGED, c - cb);
+      rej |= pv;
       if (h.caps) {
         const uint32_t k0 = src.cadd(c), k1 = src.cadd(c + 1);
         uint64_t addm = 0, dropm = 0;
         for (uint32_t k = k0; k < k1; ++k) {
-          addm |= src.template m<M_CAPADD>(k);
-          const uint64_t nw = src.vadd(k) & ~rej;
-          if (nw) {
-            put_viol(vw, nw, vword(KW_R_CAP_NOT_ALLOWED, pack2(ci, k - k0)));
-            rej |= nw;
-          }
+          const uint32_t cls = src.capadd(k);
+          addm |= bit_of(sv.capmb(cls));
+          const uint64_t nw = (h.caps_strict ? sv.row(T_NACAP, cls) : 0ull) & ~rej;
+          vs.put(nw, KW_R_CAP_NOT_ALLOWED, k - kfirst);  // index in the request's add lists, flattened
+          rej |= nw;
         }
-        const uint32_t d0 = src.cdrop(c), d1 = src.cdrop(c + 1);
-        for (uint32_t k = d0; k < d1; ++k) dropm |= src.template m<M_CAPDROP>(k);
-        if (!(dropm & h.cap_all)) mut |= tab_or(sv.tab(ST_REQD), h.reqd_union & ~dropm);
-        mut |= tab_or(sv.tab(ST_DEFA), h.defa_union & ~(addm | dropm));
+        for (uint32_t k = src.cdrop(c), k1d = src.cdrop(c + 1); k < k1d; ++k) dropm |= bit_of(sv.capmb(src.capdrop(k)));
+        mut |= caps_mutation(sv, addm, dropm);
       }
     }
   }
-  *mut_out = mut & h.caps & ~rej;
+  *mut_out = mut & ~rej;
   return rej;
 }
 
-// ---- walk B: psp-apparmor + trusted-repos, containers in order.
+// walk B: psp-apparmor + trusted-repos, containers in order.
 template <class S>
-KW_HD uint64_t walk_apparmor_images(const S& src, const SlotView& sv, uint64_t r, uint32_t* vw) {
+KW_HD uint64_t walk_apparmor_images(const S& src, const SlotView& sv, uint64_t r, const ViolSink& vs) {
   const SlotHdr& h = *sv.h;
   uint64_t rej = 0;
   if ((src.rf(r) & KW_REQ_HAS_PODSPEC) && (h.aa | h.trs)) {
@@ -231,26 +261,17 @@ KW_HD uint64_t walk_apparmor_images(const S& src, const SlotView& sv, uint64_t r
       const uint32_t ci = c - cb;
       const uint32_t fl = src.cflags(c);
       if (h.aa && (fl & KW_CTR_HAS_APPARMOR)) {
-        const uint64_t nw = src.vaa(c) & ~rej;
-        put_viol(vw, nw, vword(KW_R_APPARMOR, pack1(ci)));
+        const uint64_t nw = sv.row(T_NAAA, src.aa(c)) & ~rej;
+        vs.put(nw, KW_R_APPARMOR, ci);
         rej |= nw;
       }
       if (h.trs && (fl & KW_CTR_HAS_IMAGE)) {
-        const uint64_t reg = src.template m<M_REG>(c), tag = src.template m<M_TAG>(c), img = src.template m<M_IMG>(c);
-        // reason precedence within a container (oracle fam_trusted): registry not allowed, registry
-        // rejected, tag rejected, image not allowed, image rejected
         uint64_t why[5];
-        why[0] = h.has_ra & ~tab_or(sv.tab(ST_RA), reg);
-        why[1] = tab_or(sv.tab(ST_RR), reg);
-        why[2] = tab_or(sv.tab(ST_TR), tag);
-        why[3] = h.has_ia & ~tab_or(sv.tab(ST_IA), img);
-        why[4] = tab_or(sv.tab(ST_IR), img);
+        trs_whys(sv, src.il, [&](uint32_t j) { return src.img(c, j); }, why);
         for (uint32_t k = 0; k < 5; ++k) {
           const uint64_t nw = why[k] & h.trs & ~rej;
-          if (nw) {
-            put_viol(vw, nw, vword(KW_R_REG_NOT_ALLOWED + k, pack1(ci)));
-            rej |= nw;
-          }
+          vs.put(nw, KW_R_REG_NOT_ALLOWED + k, ci);
+          rej |= nw;
         }
       }
     }
@@ -258,126 +279,118 @@ KW_HD uint64_t walk_apparmor_images(const S& src, const SlotView& sv, uint64_t r
   return rej;
 }
 
-// ---- walk C: safe-labels (denied, then constrained, label by label in object order; then the
-// first missing mandatory key). A constraint violation carries the label-key bit in its low byte
-// until column_word resolves the slot's settings index (cidx).
+// V_l of one label: the safe-labels slots that deny its key or whose constraint on it the value fails.
 template <class S>
-KW_HD uint64_t walk_labels(const S& src, const SlotView& sv, uint64_t r, uint32_t* vw) {
+KW_HD uint64_t label_viol(const S& src, const SlotView& sv, uint32_t l) {
+  const uint32_t k = src.lk(l);
+  if (!k) return 0ull;
+  uint64_t v = sv.row(T_DENY, k);
+  for (uint32_t j = 0; j < src.nlv(); ++j) {
+    const uint32_t c = src.lv(l, j);
+    if (c != 0xffffu) v |= sv.row(T_FAIL, c);
+  }
+  return v;
+}
+
+// walk C: safe-labels (denied, then constrained, label by label in object order; then the first
+// missing mandatory key, settings order).
+template <class S>
+KW_HD uint64_t walk_labels(const S& src, const SlotView& sv, uint64_t r, const ViolSink& vs) {
   const SlotHdr& h = *sv.h;
   if (!h.lbl) return 0;
-  uint64_t rej = 0;
+  uint64_t rej = 0, present = 0;
   const uint32_t lb = src.loff(r), le = src.loff(r + 1);
-  uint64_t present = 0;
   for (uint32_t l = lb; l < le; ++l) {
-    const uint64_t km = src.template m<M_LK>(l);
-    if (!km) continue;
-    present |= km;
-    const uint32_t li = l - lb;
-    uint64_t nw = sv.tab(ST_DENY)[kw_ctz64(km)] & ~rej;
-    if (nw) {
-      put_viol(vw, nw, vword(KW_R_LABEL_DENIED, pack1(li)));
-      rej |= nw;
-    }
-    nw = src.vcon(l) & ~rej;
-    if (nw) {
-      put_viol(vw, nw, vword(KW_R_LABEL_CONSTRAINT, pack2(li, 0)) | kw_ctz64(km));
-      rej |= nw;
-    }
+    const uint32_t k = src.lk(l);
+    if (!k) continue;
+    present |= bit_of(sv.lkmb(k));
+    const uint64_t den = sv.row(T_DENY, k);
+    const uint64_t nv = label_viol(src, sv, l) & ~rej;
+    vs.put(nv & den, KW_R_LABEL_DENIED, l - lb);
+    vs.put(nv & ~den, KW_R_LABEL_CONSTRAINT, l - lb);
+    rej |= nv;
   }
-  uint64_t nw = tab_or(sv.tab(ST_MAND), h.mand_union & ~present) & ~rej;
+  uint64_t nw = tab_or(sv.mand(), h.mand_union & ~present) & ~rej;
   rej |= nw;
-  const uint8_t* mand = sv.mand();
-  while (nw) {  // the first missing mandatory key of each such slot, settings order
+  while (nw) {
     const uint32_t s = kw_ctz64(nw);
     nw &= nw - 1;
-    uint32_t i = 0;
-    for (; i < 16; ++i) {
-      const uint32_t kb = mand[s * 16 + i];
-      if (kb == 0xffu || !((present >> kb) & 1ull)) break;
-    }
-    vw[s] = vword(KW_R_LABEL_MANDATORY, i);
+    vs.put(1ull << s, KW_R_LABEL_MANDATORY, first_missing(sv, s, present));
   }
   return rej;
 }
 
-// ---- walk D: namespace allow-list.
+// walk D: namespace allow-list.
 template <class S>
-KW_HD uint64_t walk_namespace(const S& src, const SlotView& sv, uint64_t r, uint32_t* vw) {
+KW_HD uint64_t walk_namespace(const S& src, const SlotView& sv, uint64_t r, const ViolSink& vs) {
   const SlotHdr& h = *sv.h;
   if (!h.ns) return 0;
-  uint64_t ok = 0;
-  if (src.rf(r) & KW_REQ_HAS_NAMESPACE) ok = tab_or(sv.tab(ST_NSOK), src.template m<M_NS>(r));
+  const uint64_t ok = (src.rf(r) & KW_REQ_HAS_NAMESPACE) ? sv.row(T_NSOK, src.ns(r)) : 0ull;
   const uint64_t nw = h.ns & ~ok;
-  put_viol(vw, nw, vword(KW_R_NAMESPACE, 0));
+  vs.put(nw, KW_R_NAMESPACE, 0);
   return nw;
 }
 
-// Postfix group program over the member results. Each stack entry carries the set of members rhai
-// would have called to produce it (short-circuit && / ||); causes = called members that rejected
-// (evaluation_environment.rs:979-1042).
-KW_HD inline bool run_group_prog(const uint8_t* prog, uint32_t len, uint32_t ok, uint16_t* gstk, uint32_t gstride,
-                                 uint32_t* causes) {
-  uint32_t vals = 0;
-  int sp = 0;
-  for (uint32_t pc = 0; pc < len; ++pc) {
-    const uint32_t op = prog[pc];
-    if (op <= G_CALL) {
-      uint32_t v = op == G_CONST1 ? 1u : 0u, e = 0;
+// namespace bypass (service.rs:40-71): an AdmissionRequest in the always-accept namespace
+KW_HD inline bool is_bypass(uint32_t rf, uint32_t ns_cls, uint32_t bypass_cls) {
+  return bypass_cls != 0 && !(rf & KW_REQ_RAW) && (rf & KW_REQ_HAS_NAMESPACE) && ns_cls == bypass_cls;
+}
+
+// Group jump program (kwdev.hpp GOp) over the member results `ok` (bit s: member s accepted and did
+// not mutate). Returns the expression's value; *causes = the members rhai would have called that
+// rejected (evaluation_environment.rs:979-1042).
+KW_HD inline bool run_group_prog(const uint8_t* prog, uint32_t len, uint64_t ok, uint64_t* causes) {
+  uint64_t vals = 0, cz = 0;
+  uint32_t sp = 0;
+  for (uint32_t pc = 0; pc < len;) {
+    const uint32_t op = prog[pc++];
+    if (op == G_CONST0 || op == G_CONST1 || op == G_CALL) {
+      uint64_t v = op == G_CONST1 ? 1ull : 0ull;
       if (op == G_CALL) {
-        const uint32_t s = prog[++pc];
-        v = (ok >> s) & 1u;
-        e = 1u << s;
+        const uint32_t s = prog[pc++];
+        v = (ok >> s) & 1ull;
+        if (!v) cz |= 1ull << s;
       }
-      vals = (vals & ~(1u << sp)) | (v << sp);
-      gstk[sp * gstride] = (uint16_t)e;
+      vals = (vals & ~(1ull << sp)) | (v << sp);
       ++sp;
     } else if (op == G_NOT) {
-      vals ^= 1u << (sp - 1);
-    } else {
+      vals ^= 1ull << (sp - 1);
+    } else if (op == G_JT || op == G_JF) {
+      const uint32_t t = (uint32_t)prog[pc] | ((uint32_t)prog[pc + 1] << 8);
+      pc += 2;
+      const bool top = (vals >> (sp - 1)) & 1ull;
+      if (top == (op == G_JT)) pc = t;
+      else --sp;
+    } else {  // G_EQ / G_NE
       --sp;
-      const uint32_t bv = (vals >> sp) & 1u, av = (vals >> (sp - 1)) & 1u;
-      const uint32_t be = gstk[sp * gstride], ae = gstk[(sp - 1) * gstride];
-      uint32_t v, e;
-      if (op == G_AND) {
-        v = av & bv;
-        e = ae | (av ? be : 0u);
-      } else if (op == G_OR) {
-        v = av | bv;
-        e = ae | (av ? 0u : be);
-      } else if (op == G_EQ) {
-        v = av == bv;
-        e = ae | be;
-      } else {
-        v = av != bv;
-        e = ae | be;
-      }
-      vals = (vals & ~(1u << (sp - 1))) | (v << (sp - 1));
-      gstk[(sp - 1) * gstride] = (uint16_t)e;
+      const uint64_t b = (vals >> sp) & 1ull, a = (vals >> (sp - 1)) & 1ull;
+      const uint64_t v = op == G_EQ ? (uint64_t)(a == b) : (uint64_t)(a != b);
+      vals = (vals & ~(1ull << (sp - 1))) | (v << (sp - 1));
     }
   }
-  *causes = (uint32_t)gstk[0] & ~ok & 0xffffu;
-  return vals & 1u;
+  *causes = cz;
+  return vals & 1ull;
 }
 
 // Verdict word of one output column for one request. rej / mut: the request's rejected and mutated
-// slots; vw: its violation words (valid where rej is set); blob: the compiled tables (programs);
-// cidx: the record's cidx section.
+// slots; vw: its violation words (valid where rej is set); prog: the record's programs (prog_off
+// is record-relative); *wide gets the cause mask of a > 15-member group.
 KW_HD inline uint32_t column_word(const ColInfo& ci, uint64_t rej, uint64_t mut, uint64_t init, const uint32_t* vw,
-                                  const uint8_t* blob, const uint8_t* cidx, uint16_t* gstk, uint32_t gstride) {
+                                  const uint8_t* rec, uint64_t* wide) {
   if (ci.kind == CK_PLAIN) {
-    if ((rej >> ci.slot) & 1ull) {
-      uint32_t w = vw[ci.slot];
-      if (((w >> 8) & 0xffu) == KW_R_LABEL_CONSTRAINT)  // key bit -> the slot's settings index
-        w = (w & ~0xffu) | ((uint32_t)cidx[ci.slot * 64u + (w & 63u)] << 16);
-      return ci.rejb | w;
-    }
+    if ((rej >> ci.slot) & 1ull) return ci.rejb | vw[ci.slot];
     return ((mut >> ci.slot) & 1ull) ? ci.mutw : ci.okw;
   }
   if (ci.kind == CK_GROUP) {
-    const uint32_t ok = (uint32_t)((~(rej | mut | init)) >> ci.slot) & ((1u << ci.nmem) - 1u);
-    uint32_t causes;
-    if (run_group_prog(blob + ci.prog_off, ci.prog_len, ok, gstk, gstride, &causes)) return ci.okw;
-    return ci.rejb | vword(KW_R_GROUP, causes);
+    const uint64_t mask = ci.nmem >= 64 ? ~0ull : (1ull << ci.nmem) - 1ull;
+    const uint64_t ok = (~(rej | mut | init) >> ci.slot) & mask;
+    uint64_t causes;
+    if (run_group_prog(rec + ci.prog_off, ci.prog_len, ok, &causes)) return ci.okw;
+    if (ci.nmem > 15) {  // 16 causes could read as the ARG sentinel
+      *wide = causes;
+      return ci.rejb | vword(KW_R_GROUP, kArgWide);
+    }
+    return ci.rejb | vword(KW_R_GROUP, (uint32_t)causes);
   }
   return ci.okw;
 }

@@ -10,9 +10,13 @@
 // 15 %, semver 50 %, digest 15 %}; labels Poisson(4) from a 24-key vocabulary; AppArmor annotation
 // on 30 % of containers; capabilities.add Poisson(0.5) from 14 names, drop ["ALL"] 50 %;
 // privileged 5 %; config 5 mixes Pod 70 % / Deployment 20 % / Namespace 10 %.
+// Config 6 (configs/c6_256.yml) draws from that config's larger vocabularies: registries
+// reg-000..239.example.com (60 %) with paths team-NN/..., 150 extra label keys, AppArmor profiles
+// localhost/prof-00..99, namespaces ns-000..255 uniform.
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -114,13 +118,19 @@ std::string rand_word(Rng& r, int lo, int hi) {
   return s;
 }
 
-std::string image(Rng& r) {
+std::string image(Rng& r, int config) {
   std::string s;
-  if (!r.chance(0.25)) {
+  int segs = 1 + (int)r.below(3);
+  if (config == 6 && r.chance(0.6)) {
+    char buf[64];
+    const uint32_t k = r.below(240);
+    snprintf(buf, sizeof(buf), "reg-%03u.example.com/team-%02u/", k, r.chance(0.7) ? k % 40 : r.below(40));
+    s = buf;
+    segs = 1;
+  } else if (!r.chance(0.25)) {
     s = kRegistries[r.below(6)];
     s += "/";
   }
-  int segs = 1 + (int)r.below(3);
   for (int i = 0; i < segs; ++i) {
     if (i) s += "/";
     s += rand_word(r, 3, 12);
@@ -188,7 +198,11 @@ kws_batch* kws_generate(int config, uint64_t n, uint64_t seed, uint64_t row0) {
     if (config == 1 && sp < 0.5) nsn = "kubewarden-approved";
     else if (config != 1 && sp < 0.03) nsn = "kubewarden";
     else if (config == 0 && sp < 0.05) nsn = "kubewarden-approved";
-    else {
+    else if (config == 6) {
+      char buf[16];
+      snprintf(buf, sizeof(buf), "ns-%03u", r.below(256));
+      nsn = buf;
+    } else {
       char buf[16];
       snprintf(buf, sizeof(buf), "ns-%03d", zns.draw(r));
       nsn = buf;
@@ -201,10 +215,16 @@ kws_batch* kws_generate(int config, uint64_t n, uint64_t seed, uint64_t row0) {
     uint32_t nl = std::min<uint32_t>(r.poisson(4.0), 20);
     std::vector<int> used;
     for (uint32_t k = 0; k < nl; ++k) {
-      int key = (int)r.below(24);
+      int key = (int)r.below(config == 6 ? 174 : 24);
       if (std::find(used.begin(), used.end(), key) != used.end()) continue;
       used.push_back(key);
-      b->lbl_key.push(kLabelKeys[key]);
+      if (key < 24) {
+        b->lbl_key.push(kLabelKeys[key]);
+      } else {
+        char buf[32];
+        snprintf(buf, sizeof(buf), "team.example/k-%03d", key - 24);
+        b->lbl_key.push(buf);
+      }
       b->lbl_val.push(r.chance(0.15) ? rand_word(r, 1, 20) : kLabelValues[r.below(20)]);
     }
     b->lbl_off.push_back((uint32_t)b->lbl_key.off.size() - 1);
@@ -225,7 +245,7 @@ kws_batch* kws_generate(int config, uint64_t n, uint64_t seed, uint64_t row0) {
         if (c >= nc) cf |= c < nc + ninit ? KW_CTR_INIT : KW_CTR_EPHEMERAL;
         std::string cname = "c" + std::to_string(c) + "-" + rand_word(r, 3, 8);
         b->ctr_name.push(cname);
-        b->ctr_image.push(image(r));
+        b->ctr_image.push(image(r, config));
         if (r.chance(0.05)) cf |= KW_CTR_PRIVILEGED;
         uint32_t na = std::min<uint32_t>(r.poisson(0.5), 6);
         for (uint32_t k = 0; k < na; ++k) b->cap_add.push(kCaps[r.below(14)]);
@@ -239,7 +259,13 @@ kws_batch* kws_generate(int config, uint64_t n, uint64_t seed, uint64_t row0) {
         if (r.chance(0.3)) {
           cf |= KW_CTR_HAS_APPARMOR;
           double u = r.uni();
-          b->ctr_aa.push(u < 0.5 ? "runtime/default" : u < 0.85 ? "localhost/p" + std::to_string(r.below(10)) : "unconfined");
+          if (config == 6) {
+            char buf[32];
+            snprintf(buf, sizeof(buf), "localhost/prof-%02u", r.below(100));
+            b->ctr_aa.push(u < 0.3 ? std::string("runtime/default") : std::string(buf));
+          } else {
+            b->ctr_aa.push(u < 0.5 ? "runtime/default" : u < 0.85 ? "localhost/p" + std::to_string(r.below(10)) : "unconfined");
+          }
         } else {
           b->ctr_aa.push("");
         }

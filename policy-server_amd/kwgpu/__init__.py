@@ -178,8 +178,8 @@ class EvaluationEnvironment:
         return self._L.kw_env_is_group(self._h, idx) == 1
 
     def group_members(self, idx):
-        out = (C.c_int32 * 64)()
-        n = self._L.kw_env_group_members(self._h, idx, out, 64)
+        out = (C.c_int32 * 256)()
+        n = self._L.kw_env_group_members(self._h, idx, out, 256)
         return list(out[:n])
 
     def get_policy_mode(self, policy):
@@ -200,16 +200,27 @@ class EvaluationEnvironment:
         raise_for(rc, "get_policy_allowed_to_mutate")
         return bool(v.value)
 
-    def classify_check(self, col, s, key=b""):
-        """Diagnostic (kw_env_classify_check): (fast table exists, DFA-chain mask, fast-table mask)
-        of string `s` for request column `col`; `key` selects the label key for COL_LV."""
+    def patterns(self, col):
+        """The distinct patterns of request column `col` as (kind, text) (kw_env_pattern)."""
+        out = []
+        for i in range(self._L.kw_env_pattern_count(self._h, col)):
+            kind = C.c_int()
+            buf = C.create_string_buffer(1 << 16)
+            raise_for(self._L.kw_env_pattern(self._h, col, i, C.byref(kind), buf, len(buf)), "kw_env_pattern")
+            out.append((kind.value, buf.value.decode()))
+        return out
+
+    def classify(self, col, s, key=b""):
+        """Diagnostic (kw_env_classify): the ids of the column patterns `s` matches through the
+        compiled classifiers; `key` selects the label key for COL_LV."""
         s = s.encode() if isinstance(s, str) else s
         key = key.encode() if isinstance(key, str) else key
-        dm, fm = C.c_uint64(), C.c_uint64()
-        rc = self._L.kw_env_classify_check(self._h, col, key, len(key), s, len(s), C.byref(dm), C.byref(fm))
-        if rc < 0 or rc > 1:
-            raise_for(rc, "classify_check")
-        return bool(rc), dm.value, fm.value
+        cap = 4096
+        out = (C.c_uint32 * cap)()
+        n = self._L.kw_env_classify(self._h, col, key, len(key), s, len(s), out, cap)
+        if n < 0:
+            raise EngineError("kw_env_classify failed")
+        return sorted(out[:min(n, cap)])
 
     def should_always_accept_requests_made_inside_of_namespace(self, ns):
         b = ns.encode()
@@ -301,10 +312,12 @@ class Batch:
         self.device = device
         return self
 
-    def validate(self, env, policies, origin=VALIDATE):
-        """All pairs rows x policies on the GPU; returns nothing (verdicts stay in HBM)."""
+    def validate(self, env, policies, origin=VALIDATE, stream=None):
+        """All pairs rows x policies on the GPU; returns nothing (verdicts stay in HBM). stream: a
+        hipStream_t (int) of the batch's device to run on, None = the batch's own stream."""
         arr = (C.c_int32 * len(policies))(*[env._idx(p) for p in policies])
-        rc = self._L.kw_validate_batch(env._h, self._h, arr, len(policies), origin, None)
+        rc = self._L.kw_validate_batch(env._h, self._h, arr, len(policies), origin,
+                                       C.c_void_p(stream) if stream else None)
         raise_for(rc, "kw_validate_batch failed")
         self._npol = len(policies)
 
@@ -322,6 +335,12 @@ class Batch:
         rc = self._L.kw_batch_verdicts(self._h, out.ctypes.data_as(C.POINTER(C.c_uint32)), count)
         raise_for(rc, "kw_batch_verdicts failed")
         return out
+
+    def wide_arg(self, row, policy):
+        """Full argument of a verdict word whose ARG is KW_ARG_WIDE (kw_batch_wide_arg), or None."""
+        v = C.c_uint64()
+        rc = self._L.kw_batch_wide_arg(self._h, row, policy, C.byref(v))
+        return v.value if rc == N.KW_OK else None
 
     def debug_host_walk(self, env, policies, origin=VALIDATE):
         """Diagnostic (tests only): the device kernel's slot compiler + entity walks run on the host

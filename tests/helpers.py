@@ -13,6 +13,12 @@ def config(name):
         return yaml.safe_load(f)
 
 
+def many_policies_config():
+    """configs/c6_256.yml: 256 policies whose request columns hold hundreds of patterns each and a
+    40-member group (synth config 6 draws from the same vocabularies)."""
+    return config("c6_256")
+
+
 def reference_doc(name):
     with open(os.path.join(GOLDEN, "reference_data", name)) as f:
         return f.read()
@@ -58,3 +64,28 @@ def wide_docs():
                                  "operation": "CREATE", "userInfo": {},
                                  "object": {"kind": "Pod", "metadata": meta, "spec": {"containers": ctrs}}}})
     return docs
+
+
+def wide_entity_case():
+    """(AdmissionReview, policies): 300 containers and 300 labels; container c299 adds NET_ADMIN
+    (every other container adds only allowed CHOWN), container c270 runs AppArmor profile
+    localhost/evil, label k299 has value 'bad' against the constraint '^ok$' (every other label's
+    value is 'ok'), and label k280 is denied (VERDICT r01 "What's weak" #1 repro, extended)."""
+    ctrs = [{"name": f"c{i}", "image": "ghcr.io/x/y:1.0",
+             "securityContext": {"capabilities": {"add": ["NET_ADMIN"] if i == 299 else ["CHOWN"]}}}
+            for i in range(300)]
+    labels = {f"k{i}": ("bad" if i == 299 else "ok") for i in range(300)}
+    ann = {f"container.apparmor.security.beta.kubernetes.io/c{i}": ("localhost/evil" if i == 270 else "runtime/default")
+           for i in range(300)}
+    doc = {"request": {"uid": "wide", "kind": {"group": "", "version": "v1", "kind": "Pod"},
+                       "resource": {"group": "", "version": "v1", "resource": "pods"}, "operation": "CREATE",
+                       "userInfo": {}, "object": {"kind": "Pod", "metadata": {"labels": labels, "annotations": ann},
+                                                  "spec": {"containers": ctrs}}}}
+    mod = "registry://ghcr.io/kubewarden/policies/"
+    pols = {
+        "caps": {"module": mod + "psp-capabilities:v0.1.7", "settings": {"allowed_capabilities": ["CHOWN"]}},
+        "labels": {"module": mod + "safe-labels:v0.1.14", "settings": {"constrained_labels": {"k299": "^ok$", "k5": "^ok$"}}},
+        "labels-denied": {"module": mod + "safe-labels:v0.1.14", "settings": {"denied_labels": ["k280", "k290"]}},
+        "apparmor": {"module": mod + "psp-apparmor:v0.1.7", "settings": {"allowed_profiles": ["runtime/default"]}},
+    }
+    return json.dumps(doc), pols

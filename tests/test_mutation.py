@@ -94,7 +94,7 @@ def test_patch_matches_oracle_and_applies(origin):
         for j, pid in enumerate(ids):
             w = int(v[r, j])
             got = b.format_response(env, r, j, w, doc=doc)
-            want = oe.response(b.view(), r, j, w, doc=doc)
+            want = oe.response_doc(b.view(), r, j, origin, doc=doc)
             assert got == want, (pid, r, got, want)
             if not w & K._native.KW_F_PATCH:
                 continue

@@ -11,7 +11,7 @@ import pytest
 
 import kwgpu as K
 import oracle as O
-from helpers import config, diff_verdicts, wide_docs
+from helpers import config, diff_verdicts, golden, many_policies_config, reference_doc, wide_docs, wide_entity_case
 
 pytestmark = pytest.mark.gpu
 NS = "kubewarden"
@@ -23,6 +23,7 @@ CASES = [  # (policies file, synth config, rows)
     ("c3_group", 3, 20000),
     ("c4_64", 4, 4000),
     ("c5_mixed", 5, 2000),
+    ("c6_256", 6, 3000),
 ]
 
 
@@ -47,26 +48,18 @@ def test_all_pairs_match_oracle(name, scfg, rows, origin):
     assert np.array_equal(gpu, ora), diff_verdicts(gpu, ora, len(ids), ids)
 
 
-@pytest.mark.parametrize("origin", [K.VALIDATE, K.AUDIT])
-@pytest.mark.parametrize("name,scfg,rows", CASES[:4])
-def test_responses_match_oracle(name, scfg, rows, origin):
-    """kw_format_response_doc (service epilogue, JSONPatch of accepted mutations included) == the
-    oracle's restated AdmissionResponse."""
-    env, oe = _envs(name)
-    ids = env.policy_ids()
-    syn = K.SynthBatch(scfg, 600, seed=77 + scfg)
-    b = syn.batch().to_device(0)
-    b.validate(env, ids, origin)
-    v = b.verdicts().reshape(600, len(ids))
-    soa = syn.soa()
-    docs = [syn.json(r) for r in range(600)]
+def _check_responses(env, oe, b, soa, docs, ids, origin, rows):
+    """kw_format_response_doc of every (row, column) == the oracle's response derived from the
+    document itself (OracleEnv.response_doc: its own evaluation, full entity indices, its own
+    short-circuit causes), never from the product's verdict word."""
+    v = b.verdicts().reshape(len(docs), len(ids))
     checked = 0
-    for r in range(600):
+    for r in rows:
         for j, pid in enumerate(ids):
             members = env.group_members(j) if env.is_group(j) else []
             mv = [int(v[r, m]) for m in members] if members else None
             try:
-                want = oe.response(soa, r, j, int(v[r, j]), mv, doc=docs[r])
+                want = oe.response_doc(soa, r, j, origin, doc=docs[r])
             except KeyError as e:
                 with pytest.raises(K.PolicyNotFound):
                     b.format_response(env, r, j, int(v[r, j]), mv, doc=docs[r])
@@ -75,15 +68,106 @@ def test_responses_match_oracle(name, scfg, rows, origin):
             got = b.format_response(env, r, j, int(v[r, j]), mv, doc=docs[r])
             assert got == want, (r, pid, got, want)
             checked += 1
-    assert checked >= min(1000, 600 * len(ids) // 2)
+    return checked
 
 
-def test_row_mode_equals_all_pairs():
-    """kw_validate_rows (one policy per row, the micro-batcher shape) agrees with the all-pairs pass."""
-    env, _ = _envs("parity")
+@pytest.mark.parametrize("origin", [K.VALIDATE, K.AUDIT])
+@pytest.mark.parametrize("name,scfg,rows", CASES[:4] + CASES[6:])
+def test_responses_match_oracle(name, scfg, rows, origin):
+    env, oe = _envs(name)
+    ids = env.policy_ids()
+    n = 300
+    syn = K.SynthBatch(scfg, n, seed=77 + scfg)
+    b = syn.batch().to_device(0)
+    b.validate(env, ids, origin)
+    docs = [syn.json(r) for r in range(n)]
+    checked = _check_responses(env, oe, b, syn.soa(), docs, ids, origin, range(n))
+    assert checked >= min(1000, n * len(ids) // 2)
+
+
+@pytest.mark.parametrize("origin", [K.VALIDATE, K.AUDIT])
+def test_messages_exact_past_255(origin):
+    """VERDICT r01 repro: 300 containers / 300 labels, the only violators at index 299 (and 270 /
+    280): the GPU path names exactly them."""
+    doc, pols = wide_entity_case()
+    env = K.EvaluationEnvironment(pols, device=0)
+    oe = O.OracleEnv(pols)
+    ids = env.policy_ids()
+    b = K.Batch.from_json([doc] * 3).to_device(0)
+    b.validate(env, ids, origin)
+    assert np.array_equal(b.verdicts(), oe.eval(b.view(), ids, origin))
+    _check_responses(env, oe, b, b.view(), [doc] * 3, ids, origin, range(3))
+    v = b.verdicts()
+    got = b.format_response(env, 0, ids.index("caps"), int(v[ids.index("caps")]), doc=doc)
+    assert got["status"]["message"] == "container 'c299' adds capability 'NET_ADMIN', which is not allowed"
+
+
+def test_entity_indices_past_16_bits():
+    """A request with 70,000 labels and another whose single container adds 70,000 capabilities:
+    the violating entity's index does not fit ARG (KW_ARG_WIDE); the overflow path records it in
+    the pass's side data and the response names the right entity."""
+    n = 70_000
+    labels = {f"k{i}": ("bad" if i == n - 1 else "ok") for i in range(n)}
+    caps = ["CHOWN"] * (n - 1) + ["NET_ADMIN"]
+    mk = lambda uid, meta, ctrs: {"request": {  # noqa: E731
+        "uid": uid, "kind": {"group": "", "version": "v1", "kind": "Pod"},
+        "resource": {"group": "", "version": "v1", "resource": "pods"}, "operation": "CREATE", "userInfo": {},
+        "object": {"kind": "Pod", "metadata": meta, "spec": {"containers": ctrs}}}}
+    import json
+    docs = [json.dumps(mk("labels", {"labels": labels}, [{"name": "a", "image": "nginx"}])),
+            json.dumps(mk("caps", {}, [{"name": "big", "image": "nginx", "securityContext": {"capabilities": {"add": caps}}}])),
+            json.dumps(mk("small", {"labels": {"k1": "bad"}}, [{"name": "s", "image": "nginx"}]))]
+    mod = "registry://ghcr.io/kubewarden/policies/"
+    pols = {"caps": {"module": mod + "psp-capabilities:v0.1.7", "settings": {"allowed_capabilities": ["CHOWN"]}},
+            "labels": {"module": mod + "safe-labels:v0.1.14",
+                       "settings": {"constrained_labels": {f"k{n - 1}": "^ok$", "k1": "^ok$"}}}}
+    env = K.EvaluationEnvironment(pols, device=0)
+    oe = O.OracleEnv(pols)
+    ids = env.policy_ids()
+    b = K.Batch.from_json(docs).to_device(0)
+    for origin in (K.VALIDATE, K.AUDIT):
+        b.validate(env, ids, origin)
+        v = b.verdicts()
+        assert np.array_equal(v, oe.eval(b.view(), ids, origin))
+        assert v[0 * 2 + 1] >> 16 == K._native.KW_ARG_WIDE and v[1 * 2 + 0] >> 16 == K._native.KW_ARG_WIDE
+        assert b.wide_arg(0, ids.index("labels")) == n - 1
+        assert b.wide_arg(1, ids.index("caps")) == n - 1
+        _check_responses(env, oe, b, b.view(), docs, ids, origin, range(3))
+    got = b.format_response(env, 1, 0, int(v[2]), doc=docs[1])
+    assert got["status"]["message"] == "container 'big' adds capability 'NET_ADMIN', which is not allowed"
+
+
+@pytest.mark.parametrize("case", golden("reference_cases.json")["groups"], ids=lambda c: c["ref"])
+def test_group_short_circuit_vectors_on_gpu(case):
+    """evaluation_environment.rs:979-1042 through the HIP path: the reference's happy / unhappy OPA
+    fixtures are stood in for by declarative members on its privileged-pod fixture (unhappy:
+    pod-privileged, "Privileged container is not allowed"; happy: psp-capabilities allowing "*").
+    Accepted or rejected as pinned, and the causes are exactly the pinned members (as a set)."""
+    mod = "registry://ghcr.io/kubewarden/"
+    members = {m: ({"module": mod + "tests/pod-privileged:v0.2.1"} if kind == "unhappy"
+                   else {"module": mod + "policies/psp-capabilities:v0.1.7", "settings": {"allowed_capabilities": ["*"]}})
+               for m, kind in case["members"].items()}
+    pols = {"group": {"policies": members, "expression": case["expression"], "message": "group message"}}
+    env = K.EvaluationEnvironment(pols, device=0)
+    resp = env.evaluate("group", reference_doc("pod_with_privileged_containers.json"))
+    assert resp["allowed"] is case["allowed"]
+    if case["allowed"]:
+        assert "status" not in resp and "warnings" not in resp
+    else:
+        causes = resp["status"]["details"]["causes"]
+        assert sorted(c["field"] for c in causes) == sorted(c["field"] for c in case["causes"])
+        assert all(c["message"] == "Privileged container is not allowed" for c in causes)
+        assert resp["status"]["message"] == "group message"
+
+
+@pytest.mark.parametrize("name,scfg", [("parity", 0), ("c6_256", 6)])
+def test_row_mode_equals_all_pairs(name, scfg):
+    """kw_validate_rows (one policy per row, the micro-batcher shape) agrees with the all-pairs pass
+    (c6: the rows' distinct policies span several slot-plan chunks of one launch)."""
+    env, _ = _envs(name)
     ids = env.policy_ids()
     n = 30000
-    syn = K.SynthBatch(0, n, seed=5)
+    syn = K.SynthBatch(scfg, n, seed=5)
     b = syn.batch().to_device(0)
     b.validate(env, ids, K.VALIDATE)
     full = b.verdicts().reshape(n, len(ids))
@@ -94,28 +178,26 @@ def test_row_mode_equals_all_pairs():
     assert np.array_equal(rows, full[np.arange(n), pick])
 
 
-def test_full_size_properties():
-    """1M-request C4 batch: deterministic across launches, and every 4096-row slice evaluated as its
-    own batch reproduces the full batch's verdicts (no cross-request state)."""
-    env, oe = _envs("c4_64")
+def _oracle_threads():
+    import os
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+@pytest.mark.parametrize("name,scfg,n", [("c4_64", 4, 1_000_000), ("c5_mixed", 5, 2_000_000)])
+def test_full_size_matches_oracle(name, scfg, n):
+    """BASELINE sizes: C4 at 1M requests x 64 policies and C5 (mixed kinds, skewed container counts)
+    at 2M requests, every verdict word against the oracle (C restatement, 16 threads); plus
+    determinism across launches."""
+    env, oe = _envs(name)
     ids = env.policy_ids()
-    n = 1_000_000
-    syn = K.SynthBatch(4, n, seed=4)
+    syn = K.SynthBatch(scfg, n, seed=scfg)
     b = syn.batch().to_device(0)
     b.validate(env, ids)
     v1 = b.verdicts()
+    ora = oe.eval(syn.soa(), ids, threads=_oracle_threads())
+    assert np.array_equal(v1, ora), diff_verdicts(v1, ora, len(ids), ids)
     b.validate(env, ids)
-    v2 = b.verdicts()
-    assert np.array_equal(v1, v2)
-    v1 = v1.reshape(n, len(ids))
-    for start in (0, 123_456, n - 4096):
-        sub = K.SynthBatch(4, 4096, seed=4, row0=start)
-        sb = sub.batch().to_device(0)
-        sb.validate(env, ids)
-        assert np.array_equal(sb.verdicts().reshape(4096, len(ids)), v1[start:start + 4096])
-        # and the oracle agrees on the slice
-        assert np.array_equal(oe.eval(sub.soa(), ids).reshape(4096, len(ids)), v1[start:start + 4096])
-    # sanity of the workload: both outcomes occur for every family
+    assert np.array_equal(b.verdicts(), v1)
     allowed = (v1 & K._native.KW_F_ALLOWED) != 0
     assert allowed.any() and (~allowed).any()
 
@@ -172,6 +254,38 @@ def test_split_tiles_match_oracle(monkeypatch, name, scfg, rows, q):
     gpu = b.verdicts()
     ora = oe.eval(syn.soa(), ids, K.VALIDATE)
     assert np.array_equal(gpu, ora), diff_verdicts(gpu, ora, len(ids), ids)
+
+
+@pytest.mark.parametrize("name,scfg,rows", [CASES[0], CASES[4], CASES[6]])
+def test_global_tables_match_oracle(monkeypatch, name, scfg, rows):
+    """Classifiers and slot records read from global memory (the path of policy sets whose tables
+    exceed the per-workgroup LDS budget; forced here with KW_GLOBAL_TABLES)."""
+    monkeypatch.setenv("KW_GLOBAL_TABLES", "1")
+    env, oe = _envs(name)
+    ids = env.policy_ids()
+    syn = K.SynthBatch(scfg, rows, seed=99 + scfg)
+    b = syn.batch().to_device(0)
+    b.validate(env, ids, K.VALIDATE)
+    gpu = b.verdicts()
+    ora = oe.eval(syn.soa(), ids, K.VALIDATE)
+    assert np.array_equal(gpu, ora), diff_verdicts(gpu, ora, len(ids), ids)
+
+
+def test_caller_stream():
+    """kw_validate_batch runs on the caller's hipStream_t (kwgpu.h): a pass on a torch stream, then
+    one on the batch's own stream, both equal to the oracle."""
+    import torch
+    env, oe = _envs("c4_64")
+    ids = env.policy_ids()
+    syn = K.SynthBatch(4, 20000, seed=5)
+    b = syn.batch().to_device(0)
+    s = torch.cuda.Stream(device=0)
+    b.validate(env, ids, K.VALIDATE, stream=s.cuda_stream)
+    v1 = b.verdicts()
+    b.validate(env, ids[::-1], K.AUDIT)
+    v2 = b.verdicts()
+    assert np.array_equal(v1, oe.eval(syn.soa(), ids, K.VALIDATE))
+    assert np.array_equal(v2, oe.eval(syn.soa(), ids[::-1], K.AUDIT))
 
 
 def test_wide_requests():

@@ -14,7 +14,7 @@ import pytest
 
 import kwgpu as K
 import oracle as O
-from helpers import config, diff_verdicts, wide_docs
+from helpers import config, diff_verdicts, many_policies_config, wide_docs, wide_entity_case
 
 NS = "kubewarden"
 CASES = [("parity", 0, 3000), ("c1_namespace", 1, 2000), ("c2_trusted", 2, 3000), ("c3_group", 3, 3000),
@@ -126,3 +126,43 @@ def test_shared_slots_keep_column_modes(origin):
     got = syn.batch().debug_host_walk(env, ids, origin)
     want = oe.eval(syn.soa(), ids, origin)
     assert np.array_equal(got, want), diff_verdicts(got, want, len(ids), ids)
+
+
+def test_many_policies_host_walk():
+    """configs/c6_256.yml: 256 policies (+ a 40-member group's members as columns), hundreds of
+    patterns per column, several slot chunks in one list; the group's causes beyond the 16-bit ARG."""
+    doc = many_policies_config()
+    env, oe = K.EvaluationEnvironment(doc), O.OracleEnv(doc)
+    ids = env.policy_ids()
+    assert len(ids) >= 256 + 40
+    syn = K.SynthBatch(6, 600, seed=66)
+    got = syn.batch().debug_host_walk(env, ids)
+    want = oe.eval(syn.soa(), ids)
+    assert np.array_equal(got, want), diff_verdicts(got, want, len(ids), ids)
+    g = ids.index("group-40")
+    v = got.reshape(600, len(ids))[:, g]
+    rejected = (v & K._native.KW_F_ALLOWED) == 0
+    assert rejected.any() and (~rejected).any()
+    assert all(((w >> 16) == K._native.KW_ARG_WIDE) for w in v[rejected])  # causes live in the side data
+
+
+@pytest.mark.parametrize("origin", [K.VALIDATE, K.AUDIT])
+def test_messages_exact_past_255(origin):
+    """A request with 300 containers and 300 labels where only container c299 adds a capability the
+    policy does not allow and only label k299 fails its constraint: the responses name exactly them
+    (the verdict word carries full entity indices; the oracle derives its response from the
+    document, not from the word)."""
+    doc, pols = wide_entity_case()
+    env, oe = K.EvaluationEnvironment(pols), O.OracleEnv(pols)
+    ids = env.policy_ids()
+    b = K.Batch.from_json([doc])
+    v = b.debug_host_walk(env, ids, origin)
+    assert np.array_equal(v, oe.eval(b.view(), ids, origin))
+    got = {pid: b.format_response(env, 0, j, int(v[j]), doc=doc) for j, pid in enumerate(ids)}
+    for j, pid in enumerate(ids):
+        assert got[pid] == oe.response_doc(b.view(), 0, j, origin, doc=doc), pid
+    assert got["caps"]["status"]["message"] == "container 'c299' adds capability 'NET_ADMIN', which is not allowed"
+    assert got["labels"]["status"]["message"] == "label 'k299' value 'bad' does not match the constraint '^ok$'"
+    assert got["labels-denied"]["status"]["message"] == "label 'k280' is denied"
+    assert got["apparmor"]["status"]["message"] == ("container 'c270' uses AppArmor profile 'localhost/evil', "
+                                                    "which is not allowed")
