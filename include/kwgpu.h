@@ -231,6 +231,12 @@ void kw_batch_destroy(kw_batch *b);
 int kw_debug_host_walk(const kw_env *env, const kw_batch *b, const int32_t *policies, uint32_t npol,
                        int origin, uint32_t *out);
 
+/* Diagnostic (tests): plan an all-pairs pass over the batch's host columns without launching it.
+ * out[0..8): LDS bytes per workgroup, launches, slot-plan chunks, classifiers staged in LDS (1) or
+ * read from global memory (0), requests per tile, container / capability / label capacities. */
+int kw_debug_plan(const kw_env *env, kw_batch *b, const int32_t *policies, uint32_t npol, int origin, uint32_t *out,
+                  int cap);
+
 /* ---------------------------------------------------------------------------------------------
  * The hot path: EvaluationEnvironment::validate + service::evaluate constraints, batched.
  * Evaluates every row against each of the npol policies (indices from kw_env_lookup) on the GPU;

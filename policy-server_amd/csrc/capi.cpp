@@ -437,7 +437,7 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
       T.o_vw = u0;
       T.vw_stride = vw_stride;
       off = std::max(su, align(u0 + rows * vw_stride * 4));
-      if (off > kTileLdsBudget && scale > 0.1) {
+      if (off > kTileLdsBudget && scale > 1e-5) {  // capacities shrink until the layout fits; bigger tiles split
         scale *= 0.8;
         continue;
       }
@@ -1269,6 +1269,38 @@ int kw_batch_verdicts(kw_batch* b, uint32_t* host_out, size_t count) {
     });
   }
   return KW_OK;
+}
+
+int kw_debug_plan(const kw_env* env, kw_batch* kb, const int32_t* policies, uint32_t npol, int origin, uint32_t* out,
+                  int cap) {
+  if (!env || !kb || !out || cap < 8 || (!policies && npol)) return KW_E_ARG;
+  // plan against a host view of the batch (no device memory, nothing launched)
+  std::unique_ptr<DeviceBatch> saved = std::move(kb->dev);
+  Batch& B = kb->b;
+  B.finalize();
+  auto D = std::make_unique<DeviceBatch>();
+  static uint32_t dummy;
+  D->req_flags = B.req_flags.data();
+  D->ctr_off = B.ctr_off.data();
+  D->lbl_off = B.lbl_off.data();
+  D->ctr_flags = B.ctr_flags.data();
+  D->capadd_off = B.capadd_off.data();
+  D->capdrop_off = B.capdrop_off.data();
+  for (int m = 0; m < (int)NSTR; ++m) {
+    const StrCol& c = host_str(B, m);
+    D->str[m] = {c.off.data(), c.bytes.data(), c.n(), c.off.back()};
+  }
+  D->verdicts = &dummy;
+  kb->dev = std::move(D);
+  PassPlan plan;
+  int rc = plan_pass(env, kb, policies, npol, nullptr, origin, &plan);
+  const TileArgs& T = plan.geom;
+  const uint32_t vals[8] = {T.lds_bytes, (uint32_t)plan.launches.size(), (uint32_t)plan.chunks.size(), T.lds_tables,
+                            T.rows, T.cmax, T.kmax, T.lmax};
+  for (int i = 0; i < 8; ++i) out[i] = rc == KW_OK ? vals[i] : 0u;
+  kb->dev->verdicts = nullptr;  // host memory: not the DeviceBatch's to free
+  kb->dev = std::move(saved);
+  return rc;
 }
 
 int kw_batch_wide_arg(const kw_batch* b, uint64_t row, int32_t policy, uint64_t* value) {

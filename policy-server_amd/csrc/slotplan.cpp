@@ -196,21 +196,25 @@ struct Builder {
       align();
       return at;
     };
+    // per-local-bit slot tables: only the bits the chunk uses (the record is staged per workgroup)
     if (h.caps) {
       align();
       h.o_capmb = bytemap(COL_CAP, cap_local);
+      const size_t nb = std::max<size_t>(cap_local.size(), 1) * 8;
       h.o_reqd = (uint32_t)rec.size();
-      rec.insert(rec.end(), (const uint8_t*)reqd_l, (const uint8_t*)reqd_l + sizeof(reqd_l));
+      rec.insert(rec.end(), (const uint8_t*)reqd_l, (const uint8_t*)reqd_l + nb);
+      align();
       h.o_defa = (uint32_t)rec.size();
-      rec.insert(rec.end(), (const uint8_t*)defa_l, (const uint8_t*)defa_l + sizeof(defa_l));
+      rec.insert(rec.end(), (const uint8_t*)defa_l, (const uint8_t*)defa_l + nb);
     }
     if (h.lbl) {
       align();
       h.o_lkmb = bytemap(COL_LK, mand_local);
       h.o_mand = (uint32_t)rec.size();
-      rec.insert(rec.end(), (const uint8_t*)mand_l, (const uint8_t*)mand_l + sizeof(mand_l));
+      rec.insert(rec.end(), (const uint8_t*)mand_l, (const uint8_t*)mand_l + std::max<size_t>(mand_local.size(), 1) * 8);
+      align();
       h.o_mlist = (uint32_t)rec.size();
-      rec.resize(rec.size() + 4u * kSlots, 0);
+      rec.resize(rec.size() + 4u * std::max<uint32_t>(nslots, 1), 0);
       for (uint32_t s = 0; s < nslots; ++s) {
         const uint32_t at = (uint32_t)rec.size();
         memcpy(rec.data() + h.o_mlist + 4u * s, &at, 4);

@@ -336,6 +336,14 @@ class Batch:
         raise_for(rc, "kw_batch_verdicts failed")
         return out
 
+    def debug_plan(self, env, policies, origin=VALIDATE):
+        """Diagnostic (kw_debug_plan): the tile kernel's plan for an all-pairs pass, on the host."""
+        arr = (C.c_int32 * len(policies))(*[env._idx(p) for p in policies])
+        out = (C.c_uint32 * 8)()
+        raise_for(self._L.kw_debug_plan(env._h, self._h, arr, len(policies), origin, out, 8), "kw_debug_plan failed")
+        keys = ("lds_bytes", "launches", "chunks", "lds_tables", "rows", "cmax", "kmax", "lmax")
+        return dict(zip(keys, out[:8]))
+
     def wide_arg(self, row, policy):
         """Full argument of a verdict word whose ARG is KW_ARG_WIDE (kw_batch_wide_arg), or None."""
         v = C.c_uint64()

@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out
 TAG=${1:-abl}
 for d in ${DEBUGS:-0 1 2 4 6 7}; do
-  KW_TILE_DEBUG=$d timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/${TAG}_d$d.json 2>gpurun_out/${TAG}_d$d.err
+  KW_TILE_DEBUG=$d timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-host-modes > gpurun_out/${TAG}_d$d.json 2>gpurun_out/${TAG}_d$d.err
   rc=$?; echo "debug=$d rc=$rc $(python -c "import json;d=json.load(open('gpurun_out/${TAG}_d$d.json'));print(d['kernel_ms'], d['value']/1e6)" 2>/dev/null)"
   if [ $rc -ne 0 ]; then exit $rc; fi
 done

@@ -166,3 +166,15 @@ def test_messages_exact_past_255(origin):
     assert got["labels-denied"]["status"]["message"] == "label 'k280' is denied"
     assert got["apparmor"]["status"]["message"] == ("container 'c270' uses AppArmor profile 'localhost/evil', "
                                                     "which is not allowed")
+
+
+def test_planner_budget():
+    """The tile kernel's plan on the host (kw_debug_plan): C4 fits four 256-thread workgroups per CU
+    (<= 40 KB of LDS each, the occupancy the bench is measured at), and the 256-policy set runs all
+    its slot-plan chunks in one launch (each request staged and classified once)."""
+    c4 = K.EvaluationEnvironment(config("c4_64"))
+    p = K.SynthBatch(4, 50000, seed=1).batch().debug_plan(c4, c4.policy_ids())
+    assert p["lds_bytes"] <= 160 * 1024 // 4 and p["lds_tables"] == 1 and p["chunks"] == 1, p
+    c6 = K.EvaluationEnvironment(many_policies_config())
+    p = K.SynthBatch(6, 5000, seed=1).batch().debug_plan(c6, c6.policy_ids())
+    assert p["chunks"] >= 5 and p["launches"] == 1, p
