@@ -15,7 +15,7 @@ HIPDEF := -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include
 CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wextra $(HIPDEF)
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -munsafe-fp-atomics
 
-HOST_SRCS := json automaton expr env flatten service slotplan metrics capi
+HOST_SRCS := json yaml automaton expr env flatten service slotplan metrics capi
 HOST_OBJS := $(addprefix $(OBJ)/,$(addsuffix .o,$(HOST_SRCS)))
 HEADERS := $(wildcard $(SRC)/*.hpp) include/kwgpu.h
 

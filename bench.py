@@ -27,6 +27,24 @@ sys.path.insert(0, os.path.join(ROOT, "policy-server_amd"))
 METRIC = "admission requests evaluated/sec (node) at 64 policies; HBM GB/s vs peak"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 
+# BASELINE.json configs: policies file, synthetic workload id, default requests per GPU,
+# and the workload named in the JSON line. The metric is quoted on C4 (the default); the others are
+# measured with --config and committed under profiles/.
+CONFIGS = {
+    "c1_namespace": (1, 10_000, "C1 namespace_simple: {rows} synthetic Pod AdmissionReviews x namespace-validate "
+                                "(valid_namespace kubewarden-approved)"),
+    "c2_trusted": (2, 1_000_000, "C2 trusted-repos: {rows} synthetic Pods x trusted-repos (registries.allow "
+                                 "[ghcr.io, quay.io, registry.k8s.io], tags.reject [latest])"),
+    "c3_group": (3, 1_000_000, "C3 policy group: {rows} synthetic Pods x sigstore_pgp() || (sigstore_gh_action() && "
+                               "reject_latest_tag()) (image-glob stand-ins for the sigstore members) + its 3 members"),
+    "c4_64": (4, 1_000_000, "C4: {rows} synthetic Pod AdmissionReviews per GPU x {npol} compiled policies (c4_64.yml: "
+                            "22 psp-capabilities, 21 psp-apparmor, 21 safe-labels)"),
+    "c5_mixed": (5, 10_000_000, "C5 mixed-resource stream: {rows} synthetic Pods 70% / Deployments 20% / Namespaces "
+                                "10%, containers Zipf(1.3) over 1..64, x the {npol} C4 policies"),
+    "c6_256": (6, 1_000_000, "C6 (VERDICT r01 #3): {rows} synthetic Pods x {npol} columns (c6_256.yml: 256 policies "
+                             "over 240 registries, 230 image globs, 150 label keys, a 40-member group, + members)"),
+}
+
 
 def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
@@ -37,13 +55,15 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rows", type=int, default=1_000_000, help="requests per GPU")
-    ap.add_argument("--config", default="c4_64")
-    ap.add_argument("--synth", type=int, default=4)
+    ap.add_argument("--rows", type=int, default=None, help="requests per GPU (default: the config's)")
+    ap.add_argument("--config", default="c4_64", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (rank 0)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-modes", action="store_true", help="skip the end-to-end / flatten timings")
     args = ap.parse_args()
+    args.synth, default_rows, workload = CONFIGS[args.config]
+    if args.rows is None:
+        args.rows = default_rows
 
     import torch
     import yaml
@@ -123,13 +143,11 @@ def main():
             "metric": METRIC, "value": value, "unit": "requests/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "config": {"workload": f"C4: {args.rows} synthetic Pod AdmissionReviews per GPU x {npol} compiled "
-                                   f"policies ({args.config}.yml: 22 psp-capabilities, 21 psp-apparmor, "
-                                   f"21 safe-labels)",
+            "config": {"workload": workload.format(rows=args.rows, npol=npol), "config": args.config,
                        "requests_per_gpu": args.rows, "policies": npol, "parallelism": f"dp{world} (request shards)"},
             "evaluations_per_s": value * npol,
             "kernel_ms": {"classify": tm.classify_ms, "evaluate": tm.evaluate_ms, "total": tm.total_ms},
-            "roofline": {"kernel": "evaluate_slots_kernel" if dom == "evaluate" else "classify_kernel",
+            "roofline": {"kernel": "evaluate_tiles_kernel",
                          "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic(args),
                          "algorithmic_bytes_per_launch": nbytes},
@@ -174,7 +192,7 @@ def host_modes(env, ids, syn, device, args):
     arr = (C.c_char_p * n)(*docs)  # the C ABI call alone is timed
     lens = (C.c_size_t * n)(*[len(d) for d in docs])
     L = K._native.lib()
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    threads = max(1, min(16, len(cpu_threads())))
     fl = {}
     for th in sorted({1, threads}):
         os.environ["KW_FLATTEN_THREADS"] = str(th)
@@ -207,29 +225,50 @@ def traffic(args):
     return t.get("bytes_per_launch")
 
 
+def cpu_threads():
+    """The host cores this process may use: its affinity set, capped by the box's CPU share
+    (OMP_NUM_THREADS, which gpurun boxes set to 16)."""
+    cpus = sorted(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return cpus[:share] if share > 0 else cpus
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(policies, ids, args):
     """The oracle (C restatement of EvaluationEnvironment::validate, oracle/kworacle.c) on the host
-    cores, on a bounded sample of the same workload. The reference's own wasmtime path cannot run
-    here (no Rust toolchain, policy modules are remote OCI artifacts: SURVEY §8(c))."""
+    cores, one thread pinned per core, on a bounded sample of the same workload. The reference's own
+    wasmtime path cannot run here (no Rust toolchain, policy modules are remote OCI artifacts:
+    SURVEY §8(c))."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
     import kwgpu as K
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    cpus = cpu_threads()
+    threads = len(cpus)
     oe = O.OracleEnv(policies)
     probe_rows = 2000
     syn = K.SynthBatch(args.synth, probe_rows, seed=20250509)
     t = time.perf_counter()
-    oe.eval(syn.soa(), ids, threads=threads)
+    oe.eval(syn.soa(), ids, threads=threads, cpus=cpus)
     per_row = (time.perf_counter() - t) / probe_rows
     rows = int(min(2_000_000, max(probe_rows, args.cpu_seconds / max(per_row, 1e-9))))
     syn = K.SynthBatch(args.synth, rows, seed=20250509)
     t = time.perf_counter()
-    oe.eval(syn.soa(), ids, threads=threads)
+    oe.eval(syn.soa(), ids, threads=threads, cpus=cpus)
     dt = time.perf_counter() - t
-    return {"value": rows / dt, "unit": "requests/s", "cores": threads, "kind": "port",
-            "sample": f"{rows} synthetic C4 requests x {len(ids)} policies ({dt:.1f}s, oracle/kworacle.c, "
-                      f"{threads} threads)"}
+    return {"value": rows / dt, "unit": "requests/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
+            "sample": f"{rows} synthetic {args.config} requests x {len(ids)} policies ({dt:.1f}s, oracle/kworacle.c, "
+                      f"{threads} threads pinned one per core)"}
 
 
 if __name__ == "__main__":

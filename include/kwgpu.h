@@ -169,6 +169,12 @@ typedef struct kw_env_options {
  * its Display string into err. */
 int kw_env_build(const char *policies_json, size_t len, const kw_env_options *opts, kw_env **out,
                  char *err, size_t errlen);
+/* The same from the policies.yml text itself (read_policies_file + convert_yaml_map_to_json,
+ * src/config.rs:419-453): YAML is converted to JSON, then built as above. A YAML error is a
+ * KW_E_BOOTSTRAP. kw_yaml_to_json exposes the conversion (KW_E_PAYLOAD + message on error). */
+int kw_env_build_yaml(const char *policies_yaml, size_t len, const kw_env_options *opts, kw_env **out,
+                      char *err, size_t errlen);
+int kw_yaml_to_json(const char *yaml, size_t len, char *buf, size_t cap, size_t *need);
 /* Compiled-table blob (what rank 0 broadcasts over RCCL to the other GPUs). */
 int kw_env_serialize(const kw_env *env, void *buf, size_t cap, size_t *need);
 int kw_env_deserialize(const void *blob, size_t len, int device, kw_env **out, char *err, size_t errlen);
@@ -219,8 +225,17 @@ int kw_batch_from_json(const char *const *docs, const size_t *lens, size_t n, in
 int kw_batch_from_soa(const kw_soa *soa, kw_batch **out);
 /* Host view of the batch's columns (valid until kw_batch_destroy). */
 int kw_batch_view(const kw_batch *b, kw_soa *view);
-/* Upload the columns to HBM of `device` (synchronous; the bench times kernels with inputs resident). */
+/* Upload the columns to HBM of `device` (synchronous; the bench times kernels with inputs resident).
+ * Device memory and the pinned host staging come from per-device caching pools (returned when the
+ * batch is destroyed), so a front that uploads thousands of micro-batches per second does not
+ * allocate per batch. */
 int kw_batch_to_device(kw_batch *b, int device);
+/* The same, asynchronous on the caller's hipStream_t `stream` (which later passes of this batch use
+ * by default); the upload completes in stream order. */
+int kw_batch_to_device_async(kw_batch *b, int device, void *stream);
+/* A non-blocking hipStream_t on `device` for callers without HIP headers (the HTTP front). */
+int kw_stream_create(int device, void **stream);
+void kw_stream_destroy(void *stream);
 void kw_batch_destroy(kw_batch *b);
 
 /* Diagnostic (test infrastructure, never called by kw_validate_*): evaluate the batch's rows

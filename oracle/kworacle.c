@@ -505,14 +505,25 @@ typedef struct {
   int32_t npol, origin;
   uint64_t r0, r1;
   uint32_t *out;
+  int cpu; /* -1 = not pinned */
 } mt_arg;
 static void *mt_main(void *a_) {
   mt_arg *a = (mt_arg *)a_;
+  if (a->cpu >= 0) {
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    CPU_SET(a->cpu, &set);
+    pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+  }
   orc_eval(a->e, a->S, a->pols, a->npol, a->origin, a->r0, a->r1, a->out);
   return NULL;
 }
 void orc_eval_mt(const orc_env *e, const kw_soa *S, const int32_t *pols, int32_t npol,
                  int32_t origin, uint64_t nrows, int threads, uint32_t *out) {
+  orc_eval_mt_pinned(e, S, pols, npol, origin, nrows, threads, NULL, out);
+}
+void orc_eval_mt_pinned(const orc_env *e, const kw_soa *S, const int32_t *pols, int32_t npol, int32_t origin,
+                        uint64_t nrows, int threads, const int32_t *cpus, uint32_t *out) {
   if (threads < 1) threads = 1;
   pthread_t *th = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
   mt_arg *args = (mt_arg *)calloc((size_t)threads, sizeof(mt_arg));
@@ -525,6 +536,7 @@ void orc_eval_mt(const orc_env *e, const kw_soa *S, const int32_t *pols, int32_t
     args[t].r0 = nrows * (uint64_t)t / (uint64_t)threads;
     args[t].r1 = nrows * (uint64_t)(t + 1) / (uint64_t)threads;
     args[t].out = out;
+    args[t].cpu = cpus ? cpus[t] : -1;
     pthread_create(&th[t], NULL, mt_main, &args[t]);
   }
   for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);

@@ -83,6 +83,9 @@ void orc_eval(const orc_env *e, const kw_soa *soa, const int32_t *policies, int3
 /* Same, split over `threads` POSIX threads (the CPU baseline). */
 void orc_eval_mt(const orc_env *e, const kw_soa *soa, const int32_t *policies, int32_t npol,
                  int32_t origin, uint64_t nrows, int threads, uint32_t *out);
+/* Same, thread t pinned to CPU cpus[t] (cpus may be NULL). */
+void orc_eval_mt_pinned(const orc_env *e, const kw_soa *soa, const int32_t *policies, int32_t npol, int32_t origin,
+                        uint64_t nrows, int threads, const int32_t *cpus, uint32_t *out);
 
 /* What one (row, policy) evaluation found, before any encoding into a verdict word: the response
    is derived from this and the document, never from the product's word (oracle.py response_doc).

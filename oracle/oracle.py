@@ -641,6 +641,8 @@ def olib():
                                C.c_uint64, C.POINTER(C.c_uint32)]
         L.orc_eval_mt.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_int32), C.c_int32, C.c_int32, C.c_uint64,
                                   C.c_int, C.POINTER(C.c_uint32)]
+        L.orc_eval_mt_pinned.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_int32), C.c_int32, C.c_int32,
+                                         C.c_uint64, C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_uint32)]
         L.orc_image_parts.restype = C.c_int
         L.orc_image_parts.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_int]
         L.orc_eval_detail.restype = None
@@ -788,14 +790,18 @@ class OracleEnv:
             raise KeyError(f"unknown policy: {policy_id}")
         return self.ids[policy_id]
 
-    def eval(self, soa, policies, origin=VALIDATE, rows=None, threads=1):
-        """Verdict words for rows x policies (numpy uint32, row-major)."""
+    def eval(self, soa, policies, origin=VALIDATE, rows=None, threads=1, cpus=None):
+        """Verdict words for rows x policies (numpy uint32, row-major); cpus: pin thread t to CPU
+        cpus[t]."""
         idx = [self.lookup(p) if isinstance(p, str) else p for p in policies]
         n = soa.n_requests if rows is None else rows
         arr = (C.c_int32 * len(idx))(*idx)
         out = np.zeros(n * len(idx), dtype=np.uint32)
         ptr = out.ctypes.data_as(C.POINTER(C.c_uint32))
-        if threads > 1:
+        if cpus is not None:
+            pin = (C.c_int32 * len(cpus))(*cpus)
+            olib().orc_eval_mt_pinned(self._h, C.byref(soa), arr, len(idx), origin, n, len(cpus), pin, ptr)
+        elif threads > 1:
             olib().orc_eval_mt(self._h, C.byref(soa), arr, len(idx), origin, n, threads, ptr)
         else:
             olib().orc_eval(self._h, C.byref(soa), arr, len(idx), origin, 0, n, ptr)

@@ -21,6 +21,7 @@
 #include "metrics.hpp"
 #include "service.hpp"
 #include "slotplan.hpp"
+#include "yaml.hpp"
 
 using namespace kw;
 
@@ -29,6 +30,56 @@ struct kw_env {
 };
 
 namespace kw {
+
+// Caching allocators for device memory and pinned host staging: a micro-batch front evaluates
+// thousands of small batches per second, and hipMalloc / hipHostMalloc per batch would dominate.
+// Blocks are kept per (device, power-of-two size class) up to kMaxCached bytes per pool.
+struct BlockPool {
+  bool host;
+  std::mutex m;
+  std::map<std::pair<int, size_t>, std::vector<void*>> free;
+  size_t cached = 0;
+  static constexpr size_t kMaxCached = (size_t)4 << 30;
+  explicit BlockPool(bool h) : host(h) {}
+  static size_t cls(size_t n) {
+    size_t c = 4096;
+    while (c < n) c <<= 1;
+    return c;
+  }
+  hipError_t alloc(int dev, size_t n, void** p) {
+    const size_t c = cls(n);
+    {
+      std::lock_guard<std::mutex> g(m);
+      auto& v = free[{dev, c}];
+      if (!v.empty()) {
+        *p = v.back();
+        v.pop_back();
+        cached -= c;
+        return hipSuccess;
+      }
+    }
+    return host ? hipHostMalloc(p, c, hipHostMallocDefault) : hipMalloc(p, c);
+  }
+  void release(int dev, void* p, size_t n) {
+    if (!p) return;
+    const size_t c = cls(n);
+    std::lock_guard<std::mutex> g(m);
+    if (cached + c > kMaxCached) {
+      (void)(host ? hipHostFree(p) : hipFree(p));
+      return;
+    }
+    free[{dev, c}].push_back(p);
+    cached += c;
+  }
+};
+BlockPool& dev_pool() {
+  static BlockPool* p = new BlockPool(false);  // process lifetime (blocks outlive every batch)
+  return *p;
+}
+BlockPool& host_pool() {
+  static BlockPool* p = new BlockPool(true);
+  return *p;
+}
 
 // Requests per tile of the tile kernel: kSlotRows, or KW_SLOT_ROWS (8..64, A/B knob) when set.
 uint32_t slot_rows() {
@@ -50,7 +101,10 @@ struct TileStats {
 // side-data buffers, a private stream and timing events.
 struct DeviceBatch {
   int device = -1;
-  hipStream_t stream = nullptr;  // private stream (passes without a caller stream)
+  hipStream_t stream = nullptr;  // the batch's stream (passes without a caller stream)
+  bool owns_stream = true;       // false: the caller's stream (kw_batch_to_device_async)
+  void* staging = nullptr;       // pinned host staging of the last upload
+  size_t staging_bytes = 0;
   hipStream_t cur = nullptr;     // stream of the last pass (kw_batch_verdicts synchronises on it)
   uint8_t* cols = nullptr;
   size_t cols_bytes = 0;
@@ -108,15 +162,27 @@ struct DeviceBatch {
   uint64_t cap_key = 0;
   int cap_choice = -1;
   ~DeviceBatch() {
-    if (device >= 0) (void)hipSetDevice(device);
+    if (device < 0) return;  // host-only view (kw_debug_plan)
+    (void)hipSetDevice(device);
     if (stream) (void)hipStreamSynchronize(stream);
     if (cur && cur != stream) (void)hipStreamSynchronize(cur);
-    for (void* p : {(void*)d_tiles, (void*)d_slots, (void*)rowcol, (void*)desc, (void*)overflow, (void*)cols,
-                    (void*)verdicts, (void*)sched, (void*)g_cls, (void*)wide_count, (void*)wide_rec, (void*)wide_groups})
-      (void)hipFree(p);
+    BlockPool& P = dev_pool();
+    P.release(device, d_tiles, d_tiles_cap * sizeof(TileArgs));
+    P.release(device, d_slots, d_slots_cap);
+    P.release(device, rowcol, rowcol_cap * 4);
+    P.release(device, desc, desc_cap * sizeof(TileDesc));
+    P.release(device, overflow, overflow_cap * 4);
+    P.release(device, cols, cols_bytes);
+    P.release(device, verdicts, verdict_cap * 4);
+    P.release(device, g_cls, g_cls_cap * 2);
+    P.release(device, wide_rec, wide_rec_cap * sizeof(WideRec));
+    P.release(device, wide_groups, wide_groups_cap * 8);
+    P.release(device, sched, 512 * sizeof(uint32_t));  // every launch leaves the tile counters zero
+    P.release(device, wide_count, sizeof(uint32_t));
+    host_pool().release(device, staging, staging_bytes);
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
-    if (stream) (void)hipStreamDestroy(stream);
+    if (stream && owns_stream) (void)hipStreamDestroy(stream);
   }
 };
 
@@ -150,13 +216,18 @@ int put_out(const std::string& s, char* buf, size_t cap, size_t* need) {
     if (_e != hipSuccess) return KW_E_DEVICE; \
   } while (0)
 
+// Device buffer of at least n elements from the pool (the current device's), replacing a smaller one.
 template <typename T>
 int ensure(T** p, size_t* cap, size_t n) {
   if (*cap >= n && *p) return KW_OK;
-  (void)hipFree(*p);
+  int dev = 0;
+  HIPCHK(hipGetDevice(&dev));
+  dev_pool().release(dev, *p, *cap * sizeof(T));
   *p = nullptr;
-  size_t want = std::max<size_t>(n, 1);
-  HIPCHK(hipMalloc((void**)p, want * sizeof(T)));
+  const size_t want = BlockPool::cls(std::max<size_t>(n, 1) * sizeof(T)) / sizeof(T);
+  void* q = nullptr;
+  HIPCHK(dev_pool().alloc(dev, want * sizeof(T), &q));
+  *p = (T*)q;
   *cap = want;
   return KW_OK;
 }
@@ -705,7 +776,7 @@ int ensure_overflow_classes(const Batch& B, DeviceBatch* D, const TileArgs& T, E
   return KW_OK;
 }
 
-int run_pass(const kw_env* env, kw_batch* kb, PassPlan& plan, bool timed, hipStream_t s) {
+int run_pass(kw_batch* kb, PassPlan& plan, bool timed, hipStream_t s) {
   DeviceBatch& D = *kb->dev;
   const Batch& B = kb->b;
   if (D.cur && D.cur != s) HIPCHK(hipStreamSynchronize(D.cur));  // order against the previous pass's stream
@@ -739,7 +810,9 @@ int run_pass(const kw_env* env, kw_batch* kb, PassPlan& plan, bool timed, hipStr
   // dynamic tile schedule (per-XCD counters); KW_SCHED=static selects the strided schedule (A/B)
   static const bool dyn = !(getenv("KW_SCHED") && std::string(getenv("KW_SCHED")) == "static");
   if (dyn && !D.sched) {
-    HIPCHK(hipMalloc((void**)&D.sched, 512 * sizeof(uint32_t)));
+    void* p = nullptr;
+    HIPCHK(dev_pool().alloc(D.device, 512 * sizeof(uint32_t), &p));
+    D.sched = (uint32_t*)p;
     HIPCHK(hipMemsetAsync(D.sched, 0, 512 * sizeof(uint32_t), s));
   }
   A.sched = dyn ? D.sched : nullptr;
@@ -748,7 +821,11 @@ int run_pass(const kw_env* env, kw_batch* kb, PassPlan& plan, bool timed, hipStr
     if (int rc = ensure(&D.wide_groups, &D.wide_groups_cap, (size_t)(B.n * plan.nwide))) return rc;
     A.wide_groups = D.wide_groups;
   }
-  if (!D.wide_count) HIPCHK(hipMalloc((void**)&D.wide_count, sizeof(uint32_t)));
+  if (!D.wide_count) {
+    void* p = nullptr;
+    HIPCHK(dev_pool().alloc(D.device, sizeof(uint32_t), &p));
+    D.wide_count = (uint32_t*)p;
+  }
   HIPCHK(hipMemsetAsync(D.wide_count, 0, sizeof(uint32_t), s));
   A.wide_count = D.wide_count;
   if (D.n_overflow) {
@@ -821,6 +898,26 @@ int kw_env_build(const char* json, size_t len, const kw_env_options* opts, kw_en
   }
   *out = env.release();
   return KW_OK;
+}
+
+int kw_env_build_yaml(const char* yaml, size_t len, const kw_env_options* opts, kw_env** out, char* err, size_t errlen) {
+  if (!yaml || !out) return KW_E_ARG;
+  std::string json, e;
+  if (!yaml_to_json(yaml, len, &json, &e)) {  // read_policies_file: serde_yaml error -> boot failure
+    put_err(err, errlen, "bootstrap failure: cannot parse policies: " + e);
+    return KW_E_BOOTSTRAP;
+  }
+  return kw_env_build(json.data(), json.size(), opts, out, err, errlen);
+}
+
+int kw_yaml_to_json(const char* yaml, size_t len, char* buf, size_t cap, size_t* need) {
+  if (!yaml && len) return KW_E_ARG;
+  std::string json, e;
+  if (!yaml_to_json(yaml, len, &json, &e)) {
+    put_out(e, buf, cap, need);
+    return KW_E_PAYLOAD;
+  }
+  return put_out(json, buf, cap, need);
 }
 
 int kw_env_serialize(const kw_env* env, void* buf, size_t cap, size_t* need) {
@@ -1159,16 +1256,26 @@ int kw_batch_view(const kw_batch* b, kw_soa* view) {
   return KW_OK;
 }
 
-int kw_batch_to_device(kw_batch* kb, int device) {
+}  // extern "C"
+
+namespace {
+// Upload the batch's columns to `device`: one pooled allocation with 256-B aligned sub-arrays,
+// assembled in pinned host staging and copied with one async H2D on `stream` (null: a new stream
+// owned by the batch); `sync` waits for the copy.
+int upload_batch(kw_batch* kb, int device, hipStream_t stream, bool sync) {
   if (!kb || device < 0) return KW_E_ARG;
   HIPCHK(hipSetDevice(device));
+  if (kb->dev) kb->dev.reset();  // re-upload: the previous device copy returns to the pools
   auto D = std::make_unique<DeviceBatch>();
   D->device = device;
-  HIPCHK(hipStreamCreateWithFlags(&D->stream, hipStreamNonBlocking));
-  for (auto& e : D->ev) HIPCHK(hipEventCreate(&e));
+  if (stream) {
+    D->stream = stream;
+    D->owns_stream = false;
+  } else {
+    HIPCHK(hipStreamCreateWithFlags(&D->stream, hipStreamNonBlocking));
+  }
   Batch& B = kb->b;
   B.finalize();
-  // one allocation, 256-B aligned sub-arrays
   struct Piece {
     const void* src;
     size_t bytes;
@@ -1194,10 +1301,19 @@ int kw_batch_to_device(kw_batch* kb, int device) {
   auto addcol = [&](const StrCol& c) { return ColAt{add(c.off.data(), c.off.size() * 4), add(c.bytes.data(), c.bytes.size())}; };
   ColAt c_ns = addcol(B.ns), c_img = addcol(B.ctr_image), c_aa = addcol(B.ctr_aa), c_add = addcol(B.cap_add),
         c_drop = addcol(B.cap_drop), c_lk = addcol(B.lbl_key), c_lv = addcol(B.lbl_val);
+  total = std::max<size_t>(total, 256);
+  void* dcols = nullptr;
+  HIPCHK(dev_pool().alloc(device, total, &dcols));
+  D->cols = (uint8_t*)dcols;
   D->cols_bytes = total;
-  HIPCHK(hipMalloc((void**)&D->cols, std::max<size_t>(total, 256)));
+  HIPCHK(host_pool().alloc(device, total, &D->staging));
+  D->staging_bytes = total;
+  uint8_t* st = (uint8_t*)D->staging;
   for (auto& p : pieces)
-    if (p.bytes) HIPCHK(hipMemcpy(D->cols + p.at, p.src, p.bytes, hipMemcpyHostToDevice));
+    if (p.bytes) memcpy(st + p.at, p.src, p.bytes);
+  HIPCHK(hipMemcpyAsync(D->cols, st, total, hipMemcpyHostToDevice, D->stream));
+  if (sync) HIPCHK(hipStreamSynchronize(D->stream));
+  D->cur = D->stream;
   D->req_flags = D->cols + o_rf;
   D->ctr_off = (const uint32_t*)(D->cols + o_co);
   D->lbl_off = (const uint32_t*)(D->cols + o_lo);
@@ -1222,20 +1338,43 @@ int kw_batch_to_device(kw_batch* kb, int device) {
   kb->dev = std::move(D);
   return KW_OK;
 }
+}  // namespace
+
+extern "C" {
+
+int kw_batch_to_device(kw_batch* kb, int device) { return upload_batch(kb, device, nullptr, true); }
+
+int kw_batch_to_device_async(kw_batch* kb, int device, void* stream) {
+  if (!stream) return KW_E_ARG;
+  return upload_batch(kb, device, (hipStream_t)stream, false);
+}
+
+int kw_stream_create(int device, void** stream) {
+  if (!stream || device < 0) return KW_E_ARG;
+  HIPCHK(hipSetDevice(device));
+  hipStream_t s = nullptr;
+  HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  *stream = (void*)s;
+  return KW_OK;
+}
+
+void kw_stream_destroy(void* stream) {
+  if (stream) (void)hipStreamDestroy((hipStream_t)stream);
+}
 
 void kw_batch_destroy(kw_batch* b) { delete b; }
 
 int kw_validate_batch(const kw_env* env, kw_batch* b, const int32_t* policies, uint32_t npol, int origin, void* stream) {
   PassPlan plan;
   if (int rc = validate_common(env, b, policies, npol, nullptr, origin, &plan)) return rc;
-  return run_pass(env, b, plan, false, stream ? (hipStream_t)stream : b->dev->stream);
+  return run_pass(b, plan, false, stream ? (hipStream_t)stream : b->dev->stream);
 }
 
 int kw_validate_rows(const kw_env* env, kw_batch* b, const int32_t* row_policy, int origin, void* stream) {
   if (!row_policy) return KW_E_ARG;
   PassPlan plan;
   if (int rc = validate_common(env, b, nullptr, 0, row_policy, origin, &plan)) return rc;
-  return run_pass(env, b, plan, false, stream ? (hipStream_t)stream : b->dev->stream);
+  return run_pass(b, plan, false, stream ? (hipStream_t)stream : b->dev->stream);
 }
 
 int kw_batch_verdicts(kw_batch* b, uint32_t* host_out, size_t count) {
@@ -1314,12 +1453,14 @@ int kw_validate_timed(const kw_env* env, kw_batch* b, const int32_t* policies, u
   PassPlan plan;
   if (int rc = validate_common(env, b, policies, npol, nullptr, origin, &plan)) return rc;
   DeviceBatch& D = *b->dev;
+  for (auto& e : D.ev)
+    if (!e) HIPCHK(hipEventCreate(&e));
   for (int i = 0; i < warmup; ++i)
-    if (int rc = run_pass(env, b, plan, false, D.stream)) return rc;
+    if (int rc = run_pass(b, plan, false, D.stream)) return rc;
   HIPCHK(hipStreamSynchronize(D.stream));
   double ev = 0;
   for (int i = 0; i < reps; ++i) {
-    if (int rc = run_pass(env, b, plan, true, D.stream)) return rc;
+    if (int rc = run_pass(b, plan, true, D.stream)) return rc;
     HIPCHK(hipEventSynchronize(D.ev[2]));
     float c = 0;
     HIPCHK(hipEventElapsedTime(&c, D.ev[0], D.ev[2]));

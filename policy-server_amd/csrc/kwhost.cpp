@@ -6,13 +6,18 @@
 // api_error.rs:7-30), handle_evaluation_error (handlers.rs:321-342) and the per-request
 // semaphore + spawn_blocking (acquire_semaphore_and_evaluate, handlers.rs:256-286), which this
 // server replaces with a micro-batcher: connection threads park their request in a queue; one
-// batcher thread takes up to --max-batch requests (waiting at most --max-wait-us after the first),
-// flattens them with kw_batch_from_json, evaluates them with one kw_validate_rows call per
-// (document kind, origin) and hands each connection its formatted AdmissionReview.
+// batcher thread takes up to --max-batch requests (waiting at most --max-wait-us after the first)
+// whenever one of --workers pipeline workers is idle, and hands the batch to it. A worker flattens
+// the batch with kw_batch_from_json, uploads it on its own HIP stream (pooled device memory, pinned
+// staging: no allocation per batch), evaluates it with one kw_validate_rows call per (document kind,
+// origin) and hands each connection its formatted AdmissionReview; with two or more workers the
+// flattening and formatting of one batch overlap the GPU work of the next.
 //
 // Status mapping (reference behaviour):
 //   body not JSON                        400  "Failed to parse the request body as JSON: ..."
 //   JSON not an AdmissionReview / Raw    422  "Failed to deserialize the JSON body into the target type: ..."
+//   body over --max-body-bytes (2 MiB)   413  "Failed to buffer the request body: length limit exceeded"
+//                                             (axum's DefaultBodyLimit; the connection is then closed)
 //   Content-Type not application/json    415  "Expected request with `Content-Type: application/json`"
 //   /validate rejections are {"message", "status"} JSON (JsonExtractor); /audit and /validate_raw
 //   use axum's plain-text rejection body.
@@ -24,12 +29,13 @@
 //                                             (src/metrics.rs; the reference exports them over OTLP)
 //   unknown route                        404  (empty)
 //
-// Usage: kwhost --policies policies.json [--addr 127.0.0.1] [--port 3000] [--device 0]
-//   [--max-batch 512] [--max-wait-us 200] [--always-accept-admission-reviews-on-namespace NS]
-//   [--continue-on-errors] [--no-device]
-// --policies is the reference's policies.yml as JSON (configs/*.yml through any YAML -> JSON
-// converter). --no-device serves the HTTP layer without device tables: every evaluation then fails
-// with 500 (used by the CPU test suite for routing and error mapping; never a CPU fallback).
+// Usage: kwhost --policies policies.yml [--addr 127.0.0.1] [--port 3000] [--device 0]
+//   [--max-batch 512] [--max-wait-us 200] [--workers 2] [--max-body-bytes 2097152]
+//   [--always-accept-admission-reviews-on-namespace NS] [--continue-on-errors] [--no-device]
+// --policies is the reference's policies.yml (read with the native YAML reader, config.rs:449-453;
+// a file whose first character is '{' is read as JSON). --no-device serves the HTTP layer without
+// device tables: every evaluation then fails with 500 (used by the CPU test suite for routing and
+// error mapping; never a CPU fallback).
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -43,6 +49,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <deque>
 #include <fstream>
 #include <mutex>
@@ -57,7 +64,8 @@ namespace {
 
 struct Opts {
   std::string policies, addr = "127.0.0.1", always_ns;
-  int port = 3000, device = 0, max_batch = 512, max_wait_us = 200;
+  int port = 3000, device = 0, max_batch = 512, max_wait_us = 200, workers = 2;
+  size_t max_body = 2u << 20;  // axum DefaultBodyLimit (2 MiB)
   bool continue_on_errors = false, no_device = false;
 };
 
@@ -134,6 +142,7 @@ Reply evaluation_error(int code, const std::string& msg) {  // handle_evaluation
 class Server {
  public:
   Server(const Opts& o, kw_env* env) : o_(o), env_(env) {}
+  size_t max_body() const { return o_.max_body; }
 
   void submit(Job* j) {
     {
@@ -143,11 +152,16 @@ class Server {
     qcv_.notify_one();
   }
 
-  // The batcher: take up to max_batch jobs (waiting max_wait_us after the first), run them.
+  // The batcher: once a worker is idle, take up to max_batch jobs (waiting max_wait_us after the
+  // first) and hand them to it.
   void batcher() {
-    std::vector<Job*> jobs;
     for (;;) {
-      jobs.clear();
+      {
+        std::unique_lock<std::mutex> lk(wm_);
+        wcv_.wait(lk, [&] { return idle_ > 0; });
+        --idle_;
+      }
+      std::vector<Job*> jobs;
       {
         std::unique_lock<std::mutex> lk(qm_);
         qcv_.wait(lk, [&] { return !q_.empty(); });
@@ -158,18 +172,49 @@ class Server {
           q_.pop_front();
         }
       }
+      {
+        std::lock_guard<std::mutex> g(wm_);
+        work_.push_back(std::move(jobs));
+      }
+      wcv_.notify_all();
+    }
+  }
+
+  // A pipeline worker: its own stream; one batch at a time.
+  void worker() {
+    void* stream = nullptr;
+    if (!o_.no_device && kw_stream_create(o_.device, &stream) != KW_OK) stream = nullptr;
+    for (;;) {
+      std::vector<Job*> jobs;
+      {
+        std::unique_lock<std::mutex> lk(wm_);
+        wcv_.wait(lk, [&] { return !work_.empty(); });
+        jobs = std::move(work_.front());
+        work_.pop_front();
+      }
       // partition first: a job belongs to its connection thread again once it is answered
       std::vector<Job*> part[3];
       for (Job* j : jobs) part[j->route].push_back(j);
       for (Route r : {R_VALIDATE, R_AUDIT, R_RAW})
-        if (!part[r].empty()) run(r, part[r]);
+        if (!part[r].empty()) run(r, part[r], stream);
+      {
+        std::lock_guard<std::mutex> g(wm_);
+        ++idle_;
+      }
+      wcv_.notify_all();
     }
+  }
+
+  void start() {
+    idle_ = std::max(1, o_.workers);
+    for (int k = 0; k < std::max(1, o_.workers); ++k) std::thread(&Server::worker, this).detach();
+    std::thread(&Server::batcher, this).detach();
   }
 
  private:
   // One kw_validate_rows pass over the jobs of one route. A group's members run as extra rows of
   // the same document (their verdicts give the causes of a rejected group).
-  void run(Route route, std::vector<Job*> jobs) {
+  void run(Route route, std::vector<Job*> jobs, void* stream) {
     const int kind = route == R_RAW ? KW_DOC_RAW_REVIEW : KW_DOC_ADMISSION_REVIEW;
     const int origin = route == R_AUDIT ? KW_ORIGIN_AUDIT : KW_ORIGIN_VALIDATE;
     // 1. the extractor: bodies that are not a request of this route's type are answered first
@@ -215,8 +260,8 @@ class Server {
         regroup = true;
         continue;
       }
-      int32_t mem[64];
-      const int nm = kw_env_is_group(env_, idx) ? kw_env_group_members(env_, idx, mem, 64) : 0;
+      int32_t mem[256];
+      const int nm = kw_env_is_group(env_, idx) ? kw_env_group_members(env_, idx, mem, 256) : 0;
       regroup = regroup || nm > 0;
       rows.push_back({j, idx, (uint32_t)row_policy.size(), (uint32_t)(nm > 0 ? nm : 0)});
       docs.push_back(j->body.data());
@@ -238,8 +283,8 @@ class Server {
     }
     // 3. upload, evaluate, read back
     if (rc == KW_OK && o_.no_device) rc = KW_E_DEVICE;
-    if (rc == KW_OK) rc = kw_batch_to_device(b, o_.device);
-    if (rc == KW_OK) rc = kw_validate_rows(env_, b, row_policy.data(), origin, nullptr);
+    if (rc == KW_OK) rc = stream ? kw_batch_to_device_async(b, o_.device, stream) : kw_batch_to_device(b, o_.device);
+    if (rc == KW_OK) rc = kw_validate_rows(env_, b, row_policy.data(), origin, stream);
     std::vector<uint32_t> v(row_policy.size());
     if (rc == KW_OK) rc = kw_batch_verdicts(b, v.data(), v.size());
     if (rc != KW_OK) {
@@ -298,6 +343,10 @@ class Server {
   std::mutex qm_;
   std::condition_variable qcv_;
   std::deque<Job*> q_;
+  std::mutex wm_;  // workers: idle count and the batches handed over
+  std::condition_variable wcv_;
+  int idle_ = 0;
+  std::deque<std::vector<Job*>> work_;
 };
 
 // ---- HTTP/1.1 (Content-Length and chunked bodies, keep-alive)
@@ -389,24 +438,46 @@ void serve(Server* srv, int fd) {
     }
     c.in.erase(0, he + 4);
     std::string body;
+    bool too_large = false;
+    size_t drained = 0;
+    constexpr size_t kDrainCap = (size_t)64 << 20;  // an oversized body is drained up to 64 MiB, else the connection drops
     if (chunked) {
       for (;;) {
         size_t le;
-        while ((le = c.in.find("\r\n")) == std::string::npos)
-          if (!c.read_more()) return (void)close(fd);
-        const size_t n = strtoul(c.in.substr(0, le).c_str(), nullptr, 16);
+        while ((le = c.in.find("\r\n")) == std::string::npos) {
+          if (c.in.size() > 64 || !c.read_more()) return (void)close(fd);
+        }
+        const std::string hex = c.in.substr(0, c.in.find_first_of(";\r"));
+        if (hex.empty() || hex.size() > 8 || hex.find_first_not_of("0123456789abcdefABCDEF") != std::string::npos)
+          return (void)close(fd);
+        const size_t n = strtoul(hex.c_str(), nullptr, 16);  // < 2^32: no overflow below
+        if (body.size() + n > srv->max_body()) too_large = true;
+        if (too_large && drained + n > kDrainCap) return (void)close(fd);
         while (c.in.size() < le + 2 + n + 2)
           if (!c.read_more()) return (void)close(fd);
-        body.append(c.in, le + 2, n);
+        if (too_large) drained += n;  // past the limit: read and discard, then answer 413
+        else body.append(c.in, le + 2, n);
         c.in.erase(0, le + 2 + n + 2);
         if (n == 0) break;
       }
+      if (too_large) body.clear();
     } else if (clen > 0) {
-      if (clen > (1ll << 30)) return (void)close(fd);
-      while ((long long)c.in.size() < clen)
-        if (!c.read_more()) return (void)close(fd);
-      body = c.in.substr(0, (size_t)clen);
-      c.in.erase(0, (size_t)clen);
+      if ((unsigned long long)clen > srv->max_body()) {
+        too_large = true;
+        if ((unsigned long long)clen > kDrainCap) return (void)close(fd);
+        size_t left = (size_t)clen;  // read and discard the body so the client sees the answer
+        while (left > 0) {
+          if (c.in.empty() && !c.read_more()) return (void)close(fd);
+          const size_t k = std::min(left, c.in.size());
+          c.in.erase(0, k);
+          left -= k;
+        }
+      } else {
+        while ((long long)c.in.size() < clen)
+          if (!c.read_more()) return (void)close(fd);
+        body = c.in.substr(0, (size_t)clen);
+        c.in.erase(0, (size_t)clen);
+      }
     }
     // routing (src/lib.rs:206-225)
     Reply rep;
@@ -450,6 +521,9 @@ void serve(Server* srv, int fd) {
     } else if (!(ctype.rfind("application/json", 0) == 0 ||
                  (ctype.rfind("application/", 0) == 0 && ctype.find("+json") != std::string::npos))) {
       rep = rejection(route, 415, "Expected request with `Content-Type: application/json`");
+    } else if (too_large) {  // DefaultBodyLimit: the body is not read, the connection closes after the answer
+      rep = rejection(route, 413, "Failed to buffer the request body: length limit exceeded");
+      keep = false;
     } else {
       Job j;
       j.route = route;
@@ -465,6 +539,7 @@ void serve(Server* srv, int fd) {
     out += "content-length: " + std::to_string(rep.body.size()) + "\r\n";
     if (!keep) out += "connection: close\r\n";
     out += "\r\n" + rep.body;
+    if (too_large) keep = false;
     if (!c.send_all(out) || !keep) {
       close(fd);
       return;
@@ -474,9 +549,9 @@ void serve(Server* srv, int fd) {
 
 int usage() {
   fprintf(stderr,
-          "usage: kwhost --policies FILE.json [--addr A] [--port P] [--device D] [--max-batch N]\n"
-          "              [--max-wait-us T] [--always-accept-admission-reviews-on-namespace NS]\n"
-          "              [--continue-on-errors] [--no-device]\n");
+          "usage: kwhost --policies policies.yml [--addr A] [--port P] [--device D] [--max-batch N]\n"
+          "              [--max-wait-us T] [--workers W] [--max-body-bytes B]\n"
+          "              [--always-accept-admission-reviews-on-namespace NS] [--continue-on-errors] [--no-device]\n");
   return 2;
 }
 
@@ -494,6 +569,8 @@ int main(int argc, char** argv) {
     else if (a == "--device" && (v = val())) o.device = atoi(v);
     else if (a == "--max-batch" && (v = val())) o.max_batch = std::max(1, atoi(v));
     else if (a == "--max-wait-us" && (v = val())) o.max_wait_us = std::max(0, atoi(v));
+    else if (a == "--workers" && (v = val())) o.workers = std::max(1, atoi(v));
+    else if (a == "--max-body-bytes" && (v = val())) o.max_body = (size_t)std::max(0ll, atoll(v));
     else if (a == "--always-accept-admission-reviews-on-namespace" && (v = val())) o.always_ns = v;
     else if (a == "--continue-on-errors") o.continue_on_errors = true;
     else if (a == "--no-device") o.no_device = true;
@@ -513,7 +590,10 @@ int main(int argc, char** argv) {
   eo.device = o.no_device ? -1 : o.device;
   kw_env* env = nullptr;
   char err[2048] = {0};
-  if (int rc = kw_env_build(doc.data(), doc.size(), &eo, &env, err, sizeof(err))) {
+  const size_t first = doc.find_first_not_of(" \t\r\n");
+  const bool is_json = first != std::string::npos && doc[first] == '{';
+  if (int rc = is_json ? kw_env_build(doc.data(), doc.size(), &eo, &env, err, sizeof(err))
+                       : kw_env_build_yaml(doc.data(), doc.size(), &eo, &env, err, sizeof(err))) {
     fprintf(stderr, "kwhost: %s (code %d)\n", err, rc);
     return 1;
   }
@@ -532,7 +612,7 @@ int main(int argc, char** argv) {
   signal(SIGPIPE, SIG_IGN);
   Server srv(o, env);
   srv.metrics_ = kw_metrics_create();
-  std::thread(&Server::batcher, &srv).detach();
+  srv.start();
   fprintf(stderr, "kwhost: %d policies, listening on %s:%d\n", kw_env_policy_count(env), o.addr.c_str(), o.port);
   for (;;) {
     const int fd = accept(ls, nullptr, nullptr);

@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/kwgpu.h"
@@ -96,6 +97,11 @@ struct StrCol {
   }
   kw_strcol view() const { return kw_strcol{off.data(), bytes.data(), off.size() - 1}; }
   std::string at(size_t i) const { return std::string((const char*)bytes.data() + off[i], off[i + 1] - off[i]); }
+  void append(const StrCol& o) {
+    const uint32_t base = off.back();
+    bytes.insert(bytes.end(), o.bytes.begin(), o.bytes.end());
+    for (size_t i = 1; i < o.off.size(); ++i) off.push_back(base + o.off[i]);
+  }
 };
 
 }  // namespace
@@ -170,11 +176,56 @@ void json_str(std::string* o, const std::string& s) {
 
 }  // namespace
 
+namespace {
+kws_batch* generate_range(int config, uint64_t n, uint64_t seed, uint64_t row0);
+
+void append_batch(kws_batch* d, const kws_batch& o) {
+  auto shift = [](std::vector<uint32_t>* dst, const std::vector<uint32_t>& src) {
+    const uint32_t base = dst->back();
+    for (size_t i = 1; i < src.size(); ++i) dst->push_back(base + src[i]);
+  };
+  d->n += o.n;
+  d->req_flags.insert(d->req_flags.end(), o.req_flags.begin(), o.req_flags.end());
+  d->ctr_flags.insert(d->ctr_flags.end(), o.ctr_flags.begin(), o.ctr_flags.end());
+  d->obj_kind.insert(d->obj_kind.end(), o.obj_kind.begin(), o.obj_kind.end());
+  shift(&d->ctr_off, o.ctr_off);
+  shift(&d->lbl_off, o.lbl_off);
+  shift(&d->capadd_off, o.capadd_off);
+  shift(&d->capdrop_off, o.capdrop_off);
+  StrCol* mine[] = {&d->uid, &d->ns, &d->op, &d->kind, &d->name, &d->ctr_name, &d->ctr_image, &d->ctr_aa,
+                    &d->cap_add, &d->cap_drop, &d->lbl_key, &d->lbl_val};
+  const StrCol* theirs[] = {&o.uid, &o.ns, &o.op, &o.kind, &o.name, &o.ctr_name, &o.ctr_image, &o.ctr_aa,
+                            &o.cap_add, &o.cap_drop, &o.lbl_key, &o.lbl_val};
+  for (size_t k = 0; k < sizeof(mine) / sizeof(mine[0]); ++k) mine[k]->append(*theirs[k]);
+}
+}  // namespace
+
 extern "C" {
 
-// config: 1..5 as in SURVEY §8(d) (1: namespace-heavy, 5: mixed kinds + skewed containers);
-// 0 = parity mix (all kinds, every field exercised). Rows [row0, row0+n) of the seeded stream.
+// config: 1..6 as in SURVEY §8(d) (1: namespace-heavy, 5: mixed kinds + skewed containers, 6: the
+// c6_256 vocabularies); 0 = parity mix (all kinds, every field exercised). Rows [row0, row0+n) of
+// the seeded stream (every row has its own generator, so large batches are made on 16 threads).
 kws_batch* kws_generate(int config, uint64_t n, uint64_t seed, uint64_t row0) {
+  const uint64_t nt = n >= 200000 ? 16 : 1;
+  if (nt == 1) return generate_range(config, n, seed, row0);
+  std::vector<kws_batch*> part(nt);
+  std::vector<std::thread> th;
+  for (uint64_t t = 0; t < nt; ++t)
+    th.emplace_back([&, t] { part[t] = generate_range(config, n * (t + 1) / nt - n * t / nt, seed, row0 + n * t / nt); });
+  for (auto& x : th) x.join();
+  kws_batch* b = part[0];
+  for (uint64_t t = 1; t < nt; ++t) {
+    append_batch(b, *part[t]);
+    delete part[t];
+  }
+  b->config = config;
+  return b;
+}
+
+}  // extern "C"
+
+namespace {
+kws_batch* generate_range(int config, uint64_t n, uint64_t seed, uint64_t row0) {
   auto* b = new kws_batch();
   b->config = config;
   b->n = n;
@@ -277,6 +328,9 @@ kws_batch* kws_generate(int config, uint64_t n, uint64_t seed, uint64_t row0) {
   }
   return b;
 }
+}  // namespace
+
+extern "C" {
 
 void kws_free(kws_batch* b) { delete b; }
 

@@ -100,7 +100,8 @@ def library():
 class EvaluationEnvironment:
     """Immutable compiled policy set (EvaluationEnvironmentBuilder::build)."""
 
-    def __init__(self, policies, continue_on_errors=False, always_accept_namespace=None, device=-1):
+    def __init__(self, policies, continue_on_errors=False, always_accept_namespace=None, device=-1, yaml=False):
+        """policies: a dict, JSON text, or (yaml=True) the policies.yml text itself."""
         L = N.lib()
         if isinstance(policies, (dict, list)):
             doc = json.dumps(policies).encode()
@@ -113,7 +114,8 @@ class EvaluationEnvironment:
                               device)
         h = C.c_void_p()
         err = C.create_string_buffer(4096)
-        rc = L.kw_env_build(doc, len(doc), C.byref(opts), C.byref(h), err, len(err))
+        build = L.kw_env_build_yaml if yaml else L.kw_env_build
+        rc = build(doc, len(doc), C.byref(opts), C.byref(h), err, len(err))
         raise_for(rc, err.value.decode(errors="replace"))
         self._h = h
         self.device = device
@@ -479,6 +481,19 @@ def service_constraints(allowed, has_patch, has_status, mode, allowed_to_mutate)
     flags = (1 if allowed else 0) | (2 if has_patch else 0) | (4 if has_status else 0)
     fst = N.lib().kw_service_constraints(flags, mode, 1 if allowed_to_mutate else 0, C.byref(out))
     return fst, bool(out.value & 1), bool(out.value & 2), bool(out.value & 4)
+
+
+def yaml_to_json(text):
+    """The native host's YAML reader (kw_yaml_to_json): the JSON value of a YAML document."""
+    b = text.encode() if isinstance(text, str) else text
+    need = C.c_size_t()
+    L = N.lib()
+    L.kw_yaml_to_json(b, len(b), None, 0, C.byref(need))
+    buf = C.create_string_buffer(need.value + 1)
+    rc = L.kw_yaml_to_json(b, len(b), buf, len(buf), C.byref(need))
+    if rc != N.KW_OK:
+        raise ValueError(buf.value.decode(errors="replace"))
+    return json.loads(buf.value.decode())
 
 
 def pattern_match(kind, pattern, s):

@@ -80,13 +80,14 @@ class KwTiming(C.Structure):
 
 
 EXPORTS = [
-    "kw_env_build", "kw_env_serialize", "kw_env_deserialize", "kw_env_destroy", "kw_env_lookup",
+    "kw_env_build", "kw_env_build_yaml", "kw_yaml_to_json", "kw_env_serialize", "kw_env_deserialize", "kw_env_destroy", "kw_env_lookup",
     "kw_env_policy_count", "kw_env_policy_id", "kw_env_is_group", "kw_env_get_policy_mode",
     "kw_env_get_policy_allowed_to_mutate",
     "kw_env_should_always_accept_requests_made_inside_of_namespace",
     "kw_env_policy_initialization_error", "kw_env_validate_settings", "kw_pattern_match", "kw_env_pattern_count",
     "kw_env_pattern", "kw_env_classify", "kw_batch_wide_arg", "kw_debug_plan",
-    "kw_batch_from_json", "kw_batch_from_soa", "kw_batch_view", "kw_batch_to_device",
+    "kw_batch_from_json", "kw_batch_from_soa", "kw_batch_view", "kw_batch_to_device", "kw_batch_to_device_async",
+    "kw_stream_create", "kw_stream_destroy",
     "kw_batch_destroy", "kw_debug_host_walk", "kw_validate_batch", "kw_validate_rows", "kw_batch_verdicts",
     "kw_validate_timed", "kw_format_response", "kw_format_response_doc", "kw_env_group_members", "kw_evaluate",
     "kw_service_constraints", "kw_metrics_create", "kw_metrics_destroy", "kw_metrics_record", "kw_metrics_render",
@@ -109,6 +110,8 @@ def lib():
     cp, ip = C.c_char_p, C.c_int
     sig = {
         "kw_env_build": (ip, [cp, sz, C.POINTER(KwEnvOptions), C.POINTER(vp), cp, sz]),
+        "kw_env_build_yaml": (ip, [cp, sz, C.POINTER(KwEnvOptions), C.POINTER(vp), cp, sz]),
+        "kw_yaml_to_json": (ip, [cp, sz, cp, sz, C.POINTER(sz)]),
         "kw_env_serialize": (ip, [vp, vp, sz, C.POINTER(sz)]),
         "kw_env_deserialize": (ip, [vp, sz, ip, C.POINTER(vp), cp, sz]),
         "kw_env_destroy": (None, [vp]),
@@ -131,6 +134,9 @@ def lib():
         "kw_batch_from_soa": (ip, [C.POINTER(KwSoa), C.POINTER(vp)]),
         "kw_batch_view": (ip, [vp, C.POINTER(KwSoa)]),
         "kw_batch_to_device": (ip, [vp, ip]),
+        "kw_batch_to_device_async": (ip, [vp, ip, vp]),
+        "kw_stream_create": (ip, [ip, C.POINTER(vp)]),
+        "kw_stream_destroy": (None, [vp]),
         "kw_batch_destroy": (None, [vp]),
         "kw_validate_batch": (ip, [vp, vp, C.POINTER(i32), u32, ip, vp]),
         "kw_validate_rows": (ip, [vp, vp, C.POINTER(i32), ip, vp]),

@@ -21,14 +21,23 @@ def free_port():
 
 
 class Host:
-    """kwhost on 127.0.0.1 with configs/<name>.yml (as JSON); a context manager."""
+    """kwhost on 127.0.0.1 with configs/<name>.yml read by its native YAML reader (as_json: the
+    same document as JSON; policies_file: any policies file); a context manager."""
 
-    def __init__(self, name, extra=(), continue_on_errors=True, namespace="kubewarden"):
+    def __init__(self, name, extra=(), continue_on_errors=True, namespace="kubewarden", as_json=False,
+                 policies_file=None):
         self.port = free_port()
-        fd, self.path = tempfile.mkstemp(suffix=".json")
-        with os.fdopen(fd, "w") as f:
-            json.dump(config(name), f)
-        args = [KWHOST, "--policies", self.path, "--port", str(self.port)]
+        self.path = None
+        if policies_file:
+            path = policies_file
+        elif as_json:
+            fd, self.path = tempfile.mkstemp(suffix=".json")
+            with os.fdopen(fd, "w") as f:
+                json.dump(config(name), f)
+            path = self.path
+        else:
+            path = os.path.join(ROOT, "configs", f"{name}.yml")
+        args = [KWHOST, "--policies", path, "--port", str(self.port)]
         if continue_on_errors:
             args.append("--continue-on-errors")
         if namespace:
@@ -58,15 +67,20 @@ class Host:
             print(f"kwhost exit status {rc}; stderr:\n{self.stderr()}")
         self.proc.kill()  # the exact child this object started
         self.proc.wait(timeout=10)
-        os.unlink(self.path)
+        if self.path:
+            os.unlink(self.path)
 
     def conn(self):
         return http.client.HTTPConnection("127.0.0.1", self.port, timeout=60)
 
-    def request(self, method, path, body=None, ctype="application/json", conn=None):
+    def request(self, method, path, body=None, ctype="application/json", conn=None, chunked=False):
         c = conn or self.conn()
         headers = {"Content-Type": ctype} if ctype else {}
-        c.request(method, path, body=body, headers=headers)
+        if chunked:
+            headers["Transfer-Encoding"] = "chunked"
+            data = body.encode() if isinstance(body, str) else body
+            body = iter([data[i:i + 65536] for i in range(0, len(data), 65536)])
+        c.request(method, path, body=body, headers=headers, encode_chunked=chunked)
         r = c.getresponse()
         data = r.read()
         if conn is None:

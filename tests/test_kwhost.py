@@ -90,3 +90,35 @@ def test_concurrent_mixed_routes(host):
         res = list(ex.map(one, range(900)))
     assert res.count(404) == 300 and res.count(500) == 600
     assert host.proc.poll() is None
+
+
+@pytest.mark.parametrize("chunked", [False, True])
+@pytest.mark.parametrize("route,json_body", [("validate", True), ("audit", False)])
+def test_body_limit_413(host, chunked, route, json_body):
+    """axum's DefaultBodyLimit (2 MiB): a larger body is refused with 413 before it is read, on both
+    the Content-Length and the chunked path, and the connection closes."""
+    big = '{"request": {"uid": "' + "x" * (2 << 20) + '"}}'
+    st, ct, body = host.request("POST", f"/{route}/pod-privileged", big, chunked=chunked)
+    assert st == 413
+    msg = "Failed to buffer the request body: length limit exceeded"
+    if json_body:
+        assert json.loads(body) == {"message": msg, "status": 413}
+    else:
+        assert body.decode() == msg and ct.startswith("text/plain")
+    assert host.request("GET", "/readiness")[0] == 200  # the server is still serving
+
+
+def test_reference_policies_yml_example():
+    """The reference's own policies.yml.example, verbatim, read by kwhost's native YAML reader
+    (config.rs:449-453) under --continue-on-errors: every policy and the group are registered (here
+    without device tables their evaluations answer 500; test_kwhost_gpu checks the answers)."""
+    from helpers import GOLDEN
+    import os
+    path = os.path.join(GOLDEN, "reference_data", "policies.yml.example")
+    with Host(None, extra=["--no-device"], policies_file=path) as h:
+        for pid in ("psp-apparmor", "psp-capabilities"):
+            st, _, body = h.request("POST", f"/validate/{pid}", POD)
+            assert st == 500, (pid, st, body)
+        for pid in ("pod-image-signatures", "pod-image-signatures%2Freject_latest_tag"):
+            assert h.request("POST", f"/validate/{pid}", POD)[0] == 500, pid
+        assert h.request("POST", "/validate/nope", POD)[0] == 404

@@ -78,3 +78,30 @@ def test_reference_fixture_privileged_pod():
         st, _, body = h.request("POST", "/validate/pod-privileged",
                                 reference_doc("pod_without_privileged_containers.json"))
         assert st == 200 and json.loads(body)["response"]["allowed"] is True
+
+
+def test_reference_policies_yml_example_served():
+    """The reference's policies.yml.example, verbatim, through kwhost's native YAML reader under
+    --continue-on-errors: psp-capabilities (allowedToMutate, required drop KILL) answers the oracle's
+    response (a JSONPatch adding the drop), psp-apparmor accepts, the trusted-repos member answers
+    as a policy, and the group whose verify-image-signatures members are not declarative (their
+    initialisation failed) answers 404 for its first broken member (service.rs:73-94)."""
+    import os
+
+    import yaml
+    from helpers import GOLDEN
+    path = os.path.join(GOLDEN, "reference_data", "policies.yml.example")
+    with open(path) as f:
+        doc = yaml.safe_load(f)
+    oe = O.OracleEnv(doc, continue_on_errors=True)
+    pod = reference_doc("pod_with_privileged_containers.json")
+    b = K.Batch.from_json([pod])
+    with Host(None, extra=["--device", "0"], policies_file=path, namespace=None) as h:
+        for pid in ("psp-apparmor", "psp-capabilities", "pod-image-signatures/reject_latest_tag"):
+            st, _, body = h.request("POST", f"/validate/{quote(pid, safe='')}", pod)
+            assert st == 200, (pid, body)
+            want = oe.response_doc(b.view(), 0, oe.ids[pid], K.VALIDATE, doc=pod)
+            assert json.loads(body)["response"] == want, pid
+        st, _, body = h.request("POST", "/validate/pod-image-signatures", pod)
+        assert st == 404 and json.loads(body)["message"] == "unknown policy: pod-image-signatures/sigstore_pgp"
+    assert "patch" in oe.response_doc(b.view(), 0, oe.ids["psp-capabilities"], K.VALIDATE, doc=pod)
