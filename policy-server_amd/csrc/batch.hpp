@@ -20,7 +20,8 @@ struct StrCol {
   std::vector<uint8_t> bytes;
   void push(std::string_view s) {
     if (bytes.size() != off.back()) bytes.resize(off.back());  // drop device padding
-    bytes.insert(bytes.end(), s.begin(), s.end());
+    const uint8_t* p = (const uint8_t*)s.data();
+    bytes.insert(bytes.end(), p, p + s.size());  // same element type: one memmove
     off.push_back((uint32_t)bytes.size());
   }
   size_t n() const { return off.size() - 1; }

@@ -91,8 +91,7 @@ bool check_settings_node(const JDoc& d, int64_t n) {
 bool check_ctx_resources(const JDoc& d, int64_t n) {
   if (n < 0 || d.is((uint32_t)n, JType::Null)) return true;
   if (!d.is((uint32_t)n, JType::Arr)) return false;
-  for (uint32_t k = 0; k < d.count((uint32_t)n); ++k) {
-    uint32_t it = d.kids((uint32_t)n)[k].node;
+  for (uint32_t it : d.members((uint32_t)n)) {
     if (!d.is(it, JType::Obj)) return false;
     int64_t av = d.get(it, "apiVersion"), kd = d.get(it, "kind");
     if (av < 0 || kd < 0 || !d.is((uint32_t)av, JType::Str) || !d.is((uint32_t)kd, JType::Str)) return false;
@@ -137,17 +136,16 @@ bool parse_entry(const JDoc& d, const std::string& name, uint32_t node, Entry* e
     ok = ok && pols >= 0 && d.is((uint32_t)pols, JType::Obj) && ex >= 0 && d.is((uint32_t)ex, JType::Str) &&
          msg >= 0 && d.is((uint32_t)msg, JType::Str);
     if (ok) {
-      for (uint32_t k = 0; k < d.count((uint32_t)pols) && ok; ++k) {
-        const JKid& kid = d.kids((uint32_t)pols)[k];
-        uint32_t m = kid.node;
+      for (uint32_t m : d.members((uint32_t)pols)) {
+        if (!ok) break;
         if (!d.is(m, JType::Obj)) {
           ok = false;
           break;
         }
         Entry::Member mem;
-        mem.name = std::string(d.key(kid));
-        for (uint32_t j = 0; j < d.count(m); ++j) {
-          std::string_view key = d.key(d.kids(m)[j]);
+        mem.name = std::string(d.key(m));
+        for (uint32_t f : d.members(m)) {
+          std::string_view key = d.key(f);
           if (key != "module" && key != "settings" && key != "contextAwareResources") {
             ok = false;  // deny_unknown_fields (config.rs:342)
             break;
@@ -190,8 +188,7 @@ bool get_list(const JDoc& d, int64_t obj, const char* key, const std::string& pa
     *err = path + " must be a list of strings";
     return false;
   }
-  for (uint32_t k = 0; k < d.count((uint32_t)n); ++k) {
-    uint32_t it = d.kids((uint32_t)n)[k].node;
+  for (uint32_t it : d.members((uint32_t)n)) {
     if (!d.is(it, JType::Str)) {
       *err = path + " must be a list of strings";
       return false;
@@ -302,13 +299,12 @@ bool compile_settings(const JDoc& d, int64_t s, PolicyRec* rec, std::string* err
       int64_t c;
       if (!get_obj(d, s, "constrained_labels", "constrained_labels", &c, err)) return false;
       if (c >= 0) {
-        for (uint32_t k = 0; k < d.count((uint32_t)c); ++k) {
-          const JKid& kid = d.kids((uint32_t)c)[k];
-          if (!d.is(kid.node, JType::Str)) {
+        for (uint32_t kid : d.members((uint32_t)c)) {
+          if (!d.is(kid, JType::Str)) {
             *err = "constrained_labels values must be strings";
             return false;
           }
-          std::string key(d.key(kid)), re(d.str(kid.node));
+          std::string key(d.key(kid)), re(d.str(kid));
           std::string rerr;
           if (!regex_ok(re, &rerr)) {
             *err = "constrained label '" + key + "' has an invalid regular expression: " + rerr;
@@ -761,11 +757,10 @@ Status build_env(const char* json, size_t len, bool continue_on_errors, const ch
   if (always_ns) env->always_ns = std::string(always_ns);
 
   std::vector<Entry> entries;
-  for (uint32_t k = 0; k < d.count(0); ++k) {
-    const JKid& kid = d.kids(0)[k];
+  for (uint32_t kid : d.members(0)) {
     Entry e;
     std::string err;
-    if (!parse_entry(d, std::string(d.key(kid)), kid.node, &e, &err))
+    if (!parse_entry(d, std::string(d.key(kid)), kid, &e, &err))
       return {KW_E_BOOTSTRAP, "bootstrap failure: " + err};
     entries.push_back(std::move(e));
   }

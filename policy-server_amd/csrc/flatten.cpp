@@ -79,54 +79,14 @@ int64_t path(const JDoc& d, int64_t n, std::initializer_list<const char*> keys) 
 bool is_str(const JDoc& d, int64_t n) { return n >= 0 && d.is((uint32_t)n, JType::Str); }
 std::string_view sv(const JDoc& d, int64_t n) { return is_str(d, n) ? d.str((uint32_t)n) : std::string_view(); }
 
-bool req_string(const JDoc& d, uint32_t obj, const char* key, std::string* err) {
-  int64_t n = d.get(obj, key);
-  if (n < 0) {
-    *err = std::string("Failed to deserialize the JSON body into the target type: request: missing field `") + key + "`";
-    return false;
-  }
-  if (!d.is((uint32_t)n, JType::Str)) {
-    *err = std::string("Failed to deserialize the JSON body into the target type: request.") + key +
-           ": invalid type, expected a string";
-    return false;
-  }
-  return true;
-}
-
-bool req_object(const JDoc& d, uint32_t obj, const char* key, std::initializer_list<const char*> fields,
-                std::string* err) {
-  int64_t n = d.get(obj, key);
-  if (n < 0) {
-    *err = std::string("Failed to deserialize the JSON body into the target type: request: missing field `") + key + "`";
-    return false;
-  }
-  if (!d.is((uint32_t)n, JType::Obj)) {
-    *err = std::string("Failed to deserialize the JSON body into the target type: request.") + key +
-           ": invalid type, expected a struct";
-    return false;
-  }
-  for (const char* f : fields)
-    if (!req_string(d, (uint32_t)n, f, err)) return false;
-  return true;
-}
-
-bool opt_string(const JDoc& d, uint32_t obj, const char* key, std::string* err) {
-  int64_t n = d.get(obj, key);
-  if (n < 0 || d.is((uint32_t)n, JType::Null) || d.is((uint32_t)n, JType::Str)) return true;
-  *err = std::string("Failed to deserialize the JSON body into the target type: request.") + key +
-         ": invalid type, expected a string";
-  return false;
-}
-
 void push_caps(const JDoc& d, int64_t arr, StrCol* col, std::vector<uint32_t>* off) {
-  if (arr >= 0 && d.is((uint32_t)arr, JType::Arr)) {
-    for (uint32_t k = 0; k < d.count((uint32_t)arr); ++k) {
-      uint32_t it = d.kids((uint32_t)arr)[k].node;
+  if (arr >= 0 && d.is((uint32_t)arr, JType::Arr))
+    for (uint32_t it : d.members((uint32_t)arr))
       if (d.is(it, JType::Str)) col->push(d.str(it));
-    }
-  }
   off->push_back((uint32_t)col->n());
 }
+
+int64_t obj_get(const JDoc& d, int64_t n, std::string_view k) { return n >= 0 ? d.get((uint32_t)n, k) : -1; }
 
 }  // namespace
 
@@ -158,18 +118,21 @@ PodSpecRef find_podspec(const JDoc& d, int64_t req) {
 
 namespace {
 
-void flatten_request(const JDoc& d, int64_t req, bool raw, Batch* b) {
+// The request's members, picked in one pass (flatten_document's checks and the row's columns).
+enum ReqKey { RK_UID, RK_KIND, RK_RESOURCE, RK_OPERATION, RK_USERINFO, RK_NAMESPACE, RK_NAME, RK_SUBRES, RK_REQSUBRES,
+              RK_REQKIND, RK_OBJECT, RK_N };
+constexpr std::string_view kReqKeys[RK_N] = {"uid",       "kind", "resource",    "operation",          "userInfo", "namespace",
+                                             "name",      "subResource", "requestSubResource", "requestKind", "object"};
+
+void flatten_request(const JDoc& d, int64_t req, const int64_t* rk, bool raw, Batch* b) {
   uint8_t rf = raw ? KW_REQ_RAW : 0;
-  bool req_obj = req >= 0 && d.is((uint32_t)req, JType::Obj);
-  int64_t uidn = req_obj ? d.get((uint32_t)req, "uid") : -1;
-  b->uid.push(sv(d, uidn));
-  int64_t nsn = req_obj ? d.get((uint32_t)req, "namespace") : -1;
+  b->uid.push(sv(d, rk[RK_UID]));
+  const int64_t nsn = rk[RK_NAMESPACE];
   if (is_str(d, nsn)) rf |= KW_REQ_HAS_NAMESPACE;
   b->ns.push(sv(d, nsn));
-  b->op.push(sv(d, req_obj ? d.get((uint32_t)req, "operation") : -1));
-  std::string_view rkind = sv(d, req_obj ? path(d, req, {"kind", "kind"}) : -1);
-  b->kind.push(rkind);
-  b->rkind.push(sv(d, req_obj && !raw ? path(d, req, {"requestKind", "kind"}) : -1));
+  b->op.push(sv(d, rk[RK_OPERATION]));
+  b->kind.push(sv(d, obj_get(d, rk[RK_KIND], "kind")));
+  b->rkind.push(sv(d, raw ? -1 : obj_get(d, rk[RK_REQKIND], "kind")));
 
   const PodSpecRef ps = find_podspec(d, req);
   if (ps.has_obj) rf |= KW_REQ_HAS_OBJECT;
@@ -179,35 +142,39 @@ void flatten_request(const JDoc& d, int64_t req, bool raw, Batch* b) {
 
   // containers
   if (spec >= 0) {
-    int64_t annots = path(d, tmpl_meta, {"annotations"});
-    bool have_annots = annots >= 0 && d.is((uint32_t)annots, JType::Obj);
-    const char* lists[3] = {"containers", "initContainers", "ephemeralContainers"};
+    const int64_t annots = obj_get(d, tmpl_meta, "annotations");
+    const bool have_annots = annots >= 0 && d.is((uint32_t)annots, JType::Obj);
+    static constexpr std::string_view kLists[3] = {"containers", "initContainers", "ephemeralContainers"};
+    static constexpr std::string_view kCtr[3] = {"name", "image", "securityContext"};
+    static constexpr std::string_view kSc[2] = {"privileged", "capabilities"};
+    static constexpr std::string_view kCaps[2] = {"add", "drop"};
     const uint8_t kinds[3] = {0, KW_CTR_INIT, KW_CTR_EPHEMERAL};
+    int64_t arrs[3];
+    d.pick((uint32_t)spec, kLists, 3, arrs);
     for (int li = 0; li < 3; ++li) {
-      int64_t arr = d.get((uint32_t)spec, lists[li]);
+      const int64_t arr = arrs[li];
       if (arr < 0 || !d.is((uint32_t)arr, JType::Arr)) continue;
-      for (uint32_t k = 0; k < d.count((uint32_t)arr); ++k) {
-        uint32_t c = d.kids((uint32_t)arr)[k].node;
+      for (uint32_t c : d.members((uint32_t)arr)) {
         if (!d.is(c, JType::Obj)) continue;
         uint8_t cf = kinds[li];
-        std::string_view name = sv(d, d.get(c, "name"));
+        int64_t f[3], sc[2] = {-1, -1}, caps[2] = {-1, -1};
+        d.pick(c, kCtr, 3, f);
+        const std::string_view name = sv(d, f[0]);
         b->ctr_name.push(name);
-        int64_t img = d.get(c, "image");
-        if (is_str(d, img)) cf |= KW_CTR_HAS_IMAGE;
-        b->ctr_image.push(sv(d, img));
-        int64_t sc = d.get(c, "securityContext");
-        int64_t priv = path(d, sc, {"privileged"});
-        if (priv >= 0 && d.is((uint32_t)priv, JType::Bool) && d.n((uint32_t)priv).b) cf |= KW_CTR_PRIVILEGED;
-        push_caps(d, path(d, sc, {"capabilities", "add"}), &b->cap_add, &b->capadd_off);
-        push_caps(d, path(d, sc, {"capabilities", "drop"}), &b->cap_drop, &b->capdrop_off);
+        if (is_str(d, f[1])) cf |= KW_CTR_HAS_IMAGE;
+        b->ctr_image.push(sv(d, f[1]));
+        if (f[2] >= 0) d.pick((uint32_t)f[2], kSc, 2, sc);
+        if (sc[0] >= 0 && d.is((uint32_t)sc[0], JType::Bool) && d.n((uint32_t)sc[0]).b) cf |= KW_CTR_PRIVILEGED;
+        if (sc[1] >= 0) d.pick((uint32_t)sc[1], kCaps, 2, caps);
+        push_caps(d, caps[0], &b->cap_add, &b->capadd_off);
+        push_caps(d, caps[1], &b->cap_drop, &b->capdrop_off);
         std::string_view profile;
         if (have_annots) {
-          for (uint32_t j = 0; j < d.count((uint32_t)annots); ++j) {
-            const JKid& kid = d.kids((uint32_t)annots)[j];
-            std::string_view key = d.key(kid);
+          for (uint32_t kid : d.members((uint32_t)annots)) {
+            const std::string_view key = d.key(kid);
             if (key.size() == kAppArmorPrefix.size() + name.size() && key.substr(0, kAppArmorPrefix.size()) == kAppArmorPrefix &&
-                key.substr(kAppArmorPrefix.size()) == name && d.is(kid.node, JType::Str)) {
-              profile = d.str(kid.node);
+                key.substr(kAppArmorPrefix.size()) == name && d.is(kid, JType::Str)) {
+              profile = d.str(kid);
               cf |= KW_CTR_HAS_APPARMOR;
             }
           }
@@ -220,17 +187,57 @@ void flatten_request(const JDoc& d, int64_t req, bool raw, Batch* b) {
   b->ctr_off.push_back((uint32_t)b->ctr_flags.size());
 
   // labels of the object itself
-  int64_t labels = ps.has_obj ? path(d, d.get((uint32_t)req, "object"), {"metadata", "labels"}) : -1;
+  const int64_t labels = ps.has_obj ? obj_get(d, obj_get(d, rk[RK_OBJECT], "metadata"), "labels") : -1;
   if (labels >= 0 && d.is((uint32_t)labels, JType::Obj)) {
-    for (uint32_t j = 0; j < d.count((uint32_t)labels); ++j) {
-      const JKid& kid = d.kids((uint32_t)labels)[j];
-      if (!d.is(kid.node, JType::Str)) continue;
+    for (uint32_t kid : d.members((uint32_t)labels)) {
+      if (!d.is(kid, JType::Str)) continue;
       b->lbl_key.push(d.key(kid));
-      b->lbl_val.push(d.str(kid.node));
+      b->lbl_val.push(d.str(kid));
     }
   }
   b->lbl_off.push_back((uint32_t)b->lbl_key.n());
   b->n += 1;
+}
+
+std::string missing(const char* key) {
+  return std::string("Failed to deserialize the JSON body into the target type: request: missing field `") + key + "`";
+}
+std::string bad_type(const char* key, const char* what) {
+  return std::string("Failed to deserialize the JSON body into the target type: request.") + key + ": invalid type, expected " + what;
+}
+
+bool req_string(const JDoc& d, int64_t n, const char* key, std::string* err) {
+  if (n < 0) {
+    *err = missing(key);
+    return false;
+  }
+  if (!d.is((uint32_t)n, JType::Str)) {
+    *err = bad_type(key, "a string");
+    return false;
+  }
+  return true;
+}
+
+bool req_object(const JDoc& d, int64_t n, const char* key, const std::string_view (&fields)[3], std::string* err) {
+  if (n < 0) {
+    *err = missing(key);
+    return false;
+  }
+  if (!d.is((uint32_t)n, JType::Obj)) {
+    *err = bad_type(key, "a struct");
+    return false;
+  }
+  int64_t f[3];
+  d.pick((uint32_t)n, fields, 3, f);
+  for (int k = 0; k < 3; ++k)
+    if (!req_string(d, f[k], fields[k].data(), err)) return false;
+  return true;
+}
+
+bool opt_string(const JDoc& d, int64_t n, const char* key, std::string* err) {
+  if (n < 0 || d.is((uint32_t)n, JType::Null) || d.is((uint32_t)n, JType::Str)) return true;
+  *err = bad_type(key, "a string");
+  return false;
 }
 
 }  // namespace
@@ -246,34 +253,46 @@ bool flatten_document(const char* doc, size_t len, int doc_kind, Batch* b, std::
     *err = "Failed to deserialize the JSON body into the target type: invalid type, expected a struct";
     return false;
   }
-  int64_t req = d.get(0, "request");
+  static constexpr std::string_view kTop[3] = {"request", "kind", "apiVersion"};
+  int64_t top[3];
+  d.pick(0, kTop, 3, top);
+  const int64_t req = top[0];
   if (req < 0) {
     *err = "Failed to deserialize the JSON body into the target type: missing field `request`";
     return false;
   }
+  int64_t rk[RK_N];
+  if (d.is((uint32_t)req, JType::Obj)) {
+    d.pick((uint32_t)req, kReqKeys, RK_N, rk);
+  } else {
+    for (int64_t& x : rk) x = -1;
+  }
   if (doc_kind == KW_DOC_RAW_REVIEW) {
-    flatten_request(d, req, true, b);
+    flatten_request(d, req, rk, true, b);
     return true;
   }
-  for (const char* k : {"kind", "apiVersion"})
-    if (!opt_string(d, 0, k, err)) return false;
+  if (!opt_string(d, top[1], "kind", err) || !opt_string(d, top[2], "apiVersion", err)) {
+    err->replace(err->find("request."), 8, "");  // top-level fields
+    return false;
+  }
   if (!d.is((uint32_t)req, JType::Obj)) {
     *err = "Failed to deserialize the JSON body into the target type: request: invalid type, expected struct AdmissionRequest";
     return false;
   }
-  uint32_t r = (uint32_t)req;
-  if (!req_string(d, r, "uid", err)) return false;
-  if (!req_object(d, r, "kind", {"group", "version", "kind"}, err)) return false;
-  if (!req_object(d, r, "resource", {"group", "version", "resource"}, err)) return false;
-  if (!req_string(d, r, "operation", err)) return false;
-  int64_t ui = d.get(r, "userInfo");
+  static constexpr std::string_view kGvk[3] = {"group", "version", "kind"}, kGvr[3] = {"group", "version", "resource"};
+  if (!req_string(d, rk[RK_UID], "uid", err)) return false;
+  if (!req_object(d, rk[RK_KIND], "kind", kGvk, err)) return false;
+  if (!req_object(d, rk[RK_RESOURCE], "resource", kGvr, err)) return false;
+  if (!req_string(d, rk[RK_OPERATION], "operation", err)) return false;
+  const int64_t ui = rk[RK_USERINFO];
   if (ui < 0 || !d.is((uint32_t)ui, JType::Obj)) {
-    *err = "Failed to deserialize the JSON body into the target type: request: missing field `userInfo`";
+    *err = missing("userInfo");
     return false;
   }
-  for (const char* k : {"namespace", "name", "subResource", "requestSubResource"})
-    if (!opt_string(d, r, k, err)) return false;
-  flatten_request(d, req, false, b);
+  if (!opt_string(d, rk[RK_NAMESPACE], "namespace", err) || !opt_string(d, rk[RK_NAME], "name", err) ||
+      !opt_string(d, rk[RK_SUBRES], "subResource", err) || !opt_string(d, rk[RK_REQSUBRES], "requestSubResource", err))
+    return false;
+  flatten_request(d, req, rk, false, b);
   return true;
 }
 

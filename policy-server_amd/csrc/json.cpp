@@ -1,27 +1,44 @@
 // json.cpp — see json.hpp.
 #include "json.hpp"
 
-#include <cerrno>
+#include <emmintrin.h>
+
+#include <cmath>
 #include <cstddef>
 #include <cstdlib>
 #include <cstring>
 
 namespace kw {
 
-static constexpr uint32_t kMaxDepth = 256;
+// serde_json's recursion limit: 128 levels of remaining depth, the 128th nested array/object fails
+// (Deserializer::remaining_depth).
+static constexpr uint32_t kMaxDepth = 127;
 
 void JDoc::clear() {
   nodes_.clear();
-  kids_.clear();
-  stack_.clear();
-  strs_.clear();
+  arena_.clear();
 }
 
-void JDoc::ws() {
-  while (p_ < e_ && (*p_ == ' ' || *p_ == '\n' || *p_ == '\r' || *p_ == '\t')) ++p_;
+namespace {
+
+inline bool is_ws(char c) { return c == ' ' || c == '\n' || c == '\r' || c == '\t'; }
+
+// First byte in [p, e) that is '"', '\\' or a control character (< 0x20), or e.
+inline const char* scan_string(const char* p, const char* e) {
+  const __m128i q = _mm_set1_epi8('"'), bs = _mm_set1_epi8('\\'), c1f = _mm_set1_epi8(0x1f);
+  while (e - p >= 16) {
+    const __m128i x = _mm_loadu_si128((const __m128i*)p);
+    const __m128i m = _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(x, q), _mm_cmpeq_epi8(x, bs)),
+                                   _mm_cmpeq_epi8(_mm_min_epu8(x, c1f), x));
+    const int mask = _mm_movemask_epi8(m);
+    if (mask) return p + __builtin_ctz((unsigned)mask);
+    p += 16;
+  }
+  while (p < e && *p != '"' && *p != '\\' && (unsigned char)*p >= 0x20) ++p;
+  return p;
 }
 
-static void put_utf8(std::string* s, uint32_t cp) {
+void put_utf8(std::string* s, uint32_t cp) {
   if (cp < 0x80) {
     s->push_back((char)cp);
   } else if (cp < 0x800) {
@@ -39,10 +56,10 @@ static void put_utf8(std::string* s, uint32_t cp) {
   }
 }
 
-static int hex4(const char* p, uint32_t* v) {
+int hex4(const char* p, uint32_t* v) {
   uint32_t x = 0;
   for (int k = 0; k < 4; ++k) {
-    char c = p[k];
+    const char c = p[k];
     x <<= 4;
     if (c >= '0' && c <= '9') x |= (uint32_t)(c - '0');
     else if (c >= 'a' && c <= 'f') x |= (uint32_t)(c - 'a' + 10);
@@ -53,176 +70,240 @@ static int hex4(const char* p, uint32_t* v) {
   return 1;
 }
 
-bool JDoc::string_into(uint32_t* off, uint32_t* len) {
-  // p_ at opening quote
-  ++p_;
-  *off = (uint32_t)strs_.size();
-  const char* run = p_;
-  while (true) {
-    if (p_ >= e_) {
+inline bool digit(char c) { return c >= '0' && c <= '9'; }
+
+}  // namespace
+
+// p_ at the opening quote. A string without escapes stays in the source text; the first escape
+// moves it to the arena (unescaped).
+bool JDoc::string_into(uint32_t* off, uint32_t* len, bool* arena) {
+  const char* s = ++p_;
+  const char* q = scan_string(s, e_);
+  if (q < e_ && *q == '"') {
+    *off = (uint32_t)(s - src_);
+    *len = (uint32_t)(q - s);
+    *arena = false;
+    p_ = q + 1;
+    return true;
+  }
+  *arena = true;
+  *off = (uint32_t)arena_.size();
+  for (;;) {
+    arena_.append(s, (size_t)(q - s));
+    if (q >= e_) {
       *err_ = "EOF while parsing a string";
       return false;
     }
-    char c = *p_;
+    const char c = *q;
     if (c == '"') {
-      strs_.append(run, (size_t)(p_ - run));
-      ++p_;
+      p_ = q + 1;
       break;
     }
-    if ((unsigned char)c < 0x20) {
-      *err_ = "control character while parsing a string";
+    if (c != '\\') {
+      *err_ = "control character (\\u0000-\\u001F) found while parsing a string";
       return false;
     }
-    if (c == '\\') {
-      strs_.append(run, (size_t)(p_ - run));
-      if (p_ + 1 >= e_) {
-        *err_ = "EOF while parsing a string";
-        return false;
-      }
-      char x = p_[1];
-      p_ += 2;
-      switch (x) {
-        case '"': strs_.push_back('"'); break;
-        case '\\': strs_.push_back('\\'); break;
-        case '/': strs_.push_back('/'); break;
-        case 'b': strs_.push_back('\b'); break;
-        case 'f': strs_.push_back('\f'); break;
-        case 'n': strs_.push_back('\n'); break;
-        case 'r': strs_.push_back('\r'); break;
-        case 't': strs_.push_back('\t'); break;
-        case 'u': {
-          uint32_t cp;
-          if (e_ - p_ < 4 || !hex4(p_, &cp)) {
-            *err_ = "invalid \\u escape";
-            return false;
-          }
-          p_ += 4;
-          if (cp >= 0xD800 && cp < 0xDC00) {
-            uint32_t lo;
-            if (e_ - p_ >= 6 && p_[0] == '\\' && p_[1] == 'u' && hex4(p_ + 2, &lo) && lo >= 0xDC00 &&
-                lo < 0xE000) {
-              p_ += 6;
-              cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
-            } else {
-              *err_ = "lone leading surrogate in hex escape";
-              return false;
-            }
-          } else if (cp >= 0xDC00 && cp < 0xE000) {
-            *err_ = "lone trailing surrogate in hex escape";
-            return false;
-          }
-          put_utf8(&strs_, cp);
-          break;
-        }
-        default: *err_ = "invalid escape"; return false;
-      }
-      run = p_;
-      continue;
+    if (q + 1 >= e_) {
+      *err_ = "EOF while parsing a string";
+      return false;
     }
-    ++p_;
+    const char x = q[1];
+    p_ = q + 2;
+    switch (x) {
+      case '"': arena_.push_back('"'); break;
+      case '\\': arena_.push_back('\\'); break;
+      case '/': arena_.push_back('/'); break;
+      case 'b': arena_.push_back('\b'); break;
+      case 'f': arena_.push_back('\f'); break;
+      case 'n': arena_.push_back('\n'); break;
+      case 'r': arena_.push_back('\r'); break;
+      case 't': arena_.push_back('\t'); break;
+      case 'u': {
+        uint32_t cp;
+        if (e_ - p_ < 4 || !hex4(p_, &cp)) {
+          *err_ = "invalid escape";
+          return false;
+        }
+        p_ += 4;
+        if (cp >= 0xD800 && cp < 0xDC00) {
+          uint32_t lo;
+          if (e_ - p_ >= 6 && p_[0] == '\\' && p_[1] == 'u' && hex4(p_ + 2, &lo) && lo >= 0xDC00 && lo < 0xE000) {
+            p_ += 6;
+            cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+          } else {
+            *err_ = "lone leading surrogate in hex escape";
+            return false;
+          }
+        } else if (cp >= 0xDC00 && cp < 0xE000) {
+          *err_ = "lone trailing surrogate in hex escape";
+          return false;
+        }
+        put_utf8(&arena_, cp);
+        break;
+      }
+      default: *err_ = "invalid escape"; return false;
+    }
+    s = p_;
+    q = scan_string(s, e_);
   }
-  *len = (uint32_t)strs_.size() - *off;
+  *len = (uint32_t)arena_.size() - *off;
+  return true;
+}
+
+// RFC 8259 §6 number grammar: -?(0|[1-9][0-9]*)(\.[0-9]+)?([eE][+-]?[0-9]+)?. A float beyond f64
+// is "number out of range" (serde_json); integers beyond i64/u64 become f64 there and are accepted.
+bool JDoc::number() {
+  const char* s = p_;
+  bool is_float = false;
+  if (p_ < e_ && *p_ == '-') ++p_;
+  if (p_ >= e_ || !digit(*p_)) {
+    *err_ = "invalid number";
+    return false;
+  }
+  if (*p_ == '0') {
+    ++p_;
+    if (p_ < e_ && digit(*p_)) {
+      *err_ = "invalid number";
+      return false;
+    }
+  } else {
+    while (p_ < e_ && digit(*p_)) ++p_;
+  }
+  if (p_ < e_ && *p_ == '.') {
+    is_float = true;
+    ++p_;
+    if (p_ >= e_ || !digit(*p_)) {
+      *err_ = "invalid number";
+      return false;
+    }
+    while (p_ < e_ && digit(*p_)) ++p_;
+  }
+  if (p_ < e_ && (*p_ == 'e' || *p_ == 'E')) {
+    is_float = true;
+    ++p_;
+    if (p_ < e_ && (*p_ == '+' || *p_ == '-')) ++p_;
+    if (p_ >= e_ || !digit(*p_)) {
+      *err_ = "invalid number";
+      return false;
+    }
+    while (p_ < e_ && digit(*p_)) ++p_;
+  }
+  JNode& n = nodes_.back();
+  n.t = is_float ? JType::Float : JType::Int;
+  if (is_float) {
+    char buf[64];
+    const size_t k = (size_t)(p_ - s);
+    std::string big;
+    const char* z;
+    if (k < sizeof(buf)) {
+      memcpy(buf, s, k);
+      buf[k] = 0;
+      z = buf;
+    } else {
+      big.assign(s, k);
+      z = big.c_str();
+    }
+    if (std::isinf(strtod(z, nullptr))) {
+      *err_ = "number out of range";
+      return false;
+    }
+  }
   return true;
 }
 
 bool JDoc::value(uint32_t depth) {
-  if (depth > kMaxDepth) {
-    *err_ = "recursion limit exceeded";
-    return false;
-  }
-  ws();
+  while (p_ < e_ && is_ws(*p_)) ++p_;
   if (p_ >= e_) {
     *err_ = "EOF while parsing a value";
     return false;
   }
-  uint32_t me = (uint32_t)nodes_.size();
+  const uint32_t me = (uint32_t)nodes_.size();
   nodes_.emplace_back();
-  char c = *p_;
-  if (c == '{') {
+  nodes_.back().next = me + 1;
+  const char c = *p_;
+  if (c == '{' || c == '[') {
+    if (depth >= kMaxDepth) {
+      *err_ = "recursion limit exceeded";
+      return false;
+    }
+    const bool obj = c == '{';
+    const char close = obj ? '}' : ']';
     ++p_;
-    size_t base = stack_.size();
-    ws();
-    if (p_ < e_ && *p_ == '}') {
+    uint32_t count = 0;
+    while (p_ < e_ && is_ws(*p_)) ++p_;
+    if (p_ < e_ && *p_ == close) {
       ++p_;
     } else {
-      while (true) {
-        ws();
-        if (p_ >= e_ || *p_ != '"') {
-          *err_ = "key must be a string";
+      for (;;) {
+        uint32_t koff = 0, klen = 0;
+        bool kar = false;
+        if (obj) {
+          while (p_ < e_ && is_ws(*p_)) ++p_;
+          if (p_ >= e_ || *p_ != '"') {
+            *err_ = p_ >= e_ ? "EOF while parsing an object" : "key must be a string";
+            return false;
+          }
+          if (!string_into(&koff, &klen, &kar)) return false;
+          while (p_ < e_ && is_ws(*p_)) ++p_;
+          if (p_ >= e_ || *p_ != ':') {
+            *err_ = p_ >= e_ ? "EOF while parsing an object" : "expected `:`";
+            return false;
+          }
+          ++p_;
+        }
+        const uint32_t kid = (uint32_t)nodes_.size();
+        while (p_ < e_ && is_ws(*p_)) ++p_;
+        if (p_ < e_ && *p_ == '"') {  // string member: the common case, no recursion
+          nodes_.emplace_back();
+          JNode& n = nodes_.back();
+          n.t = JType::Str;
+          n.next = kid + 1;
+          uint32_t off, len;
+          bool ar;
+          if (!string_into(&off, &len, &ar)) return false;
+          JNode& m = nodes_[kid];
+          m.a = off;
+          m.c = len;
+          m.arena = ar;
+        } else if (!value(depth + 1)) {
           return false;
         }
-        JKid k;
-        if (!string_into(&k.key_off, &k.key_len)) return false;
-        ws();
-        if (p_ >= e_ || *p_ != ':') {
-          *err_ = "expected `:`";
-          return false;
+        if (obj) {
+          JNode& k = nodes_[kid];
+          k.key_off = koff;
+          k.key_len = klen;
+          k.key_arena = kar;
         }
-        ++p_;
-        k.node = (uint32_t)nodes_.size();
-        stack_.push_back(k);
-        if (!value(depth + 1)) return false;
-        ws();
+        ++count;
+        while (p_ < e_ && is_ws(*p_)) ++p_;
         if (p_ < e_ && *p_ == ',') {
           ++p_;
           continue;
         }
-        if (p_ < e_ && *p_ == '}') {
+        if (p_ < e_ && *p_ == close) {
           ++p_;
           break;
         }
-        *err_ = "expected `,` or `}`";
+        *err_ = p_ >= e_ ? (obj ? "EOF while parsing an object" : "EOF while parsing a list")
+                         : (obj ? "expected `,` or `}`" : "expected `,` or `]`");
         return false;
       }
     }
     JNode& n = nodes_[me];
-    n.t = JType::Obj;
-    n.k_begin = (uint32_t)kids_.size();
-    n.k_count = (uint32_t)(stack_.size() - base);
-    kids_.insert(kids_.end(), stack_.begin() + (ptrdiff_t)base, stack_.end());
-    stack_.resize(base);
-    return true;
-  }
-  if (c == '[') {
-    ++p_;
-    size_t base = stack_.size();
-    ws();
-    if (p_ < e_ && *p_ == ']') {
-      ++p_;
-    } else {
-      while (true) {
-        JKid k;
-        k.node = (uint32_t)nodes_.size();
-        stack_.push_back(k);
-        if (!value(depth + 1)) return false;
-        ws();
-        if (p_ < e_ && *p_ == ',') {
-          ++p_;
-          continue;
-        }
-        if (p_ < e_ && *p_ == ']') {
-          ++p_;
-          break;
-        }
-        *err_ = "expected `,` or `]`";
-        return false;
-      }
-    }
-    JNode& n = nodes_[me];
-    n.t = JType::Arr;
-    n.k_begin = (uint32_t)kids_.size();
-    n.k_count = (uint32_t)(stack_.size() - base);
-    kids_.insert(kids_.end(), stack_.begin() + (ptrdiff_t)base, stack_.end());
-    stack_.resize(base);
+    n.t = obj ? JType::Obj : JType::Arr;
+    n.c = count;
+    n.next = (uint32_t)nodes_.size();
     return true;
   }
   if (c == '"') {
     uint32_t off, len;
-    if (!string_into(&off, &len)) return false;
+    bool ar;
+    if (!string_into(&off, &len, &ar)) return false;
     JNode& n = nodes_[me];
     n.t = JType::Str;
-    n.s_off = off;
-    n.s_len = len;
+    n.a = off;
+    n.c = len;
+    n.arena = ar;
     return true;
   }
   if (c == 't' && e_ - p_ >= 4 && memcmp(p_, "true", 4) == 0) {
@@ -240,52 +321,24 @@ bool JDoc::value(uint32_t depth) {
     p_ += 4;
     return true;
   }
-  if (c == '-' || (c >= '0' && c <= '9')) {
-    const char* s = p_;
-    bool is_float = false;
-    if (*p_ == '-') ++p_;
-    if (p_ >= e_ || !(*p_ >= '0' && *p_ <= '9')) {
-      *err_ = "invalid number";
-      return false;
-    }
-    while (p_ < e_ && ((*p_ >= '0' && *p_ <= '9') || *p_ == '.' || *p_ == 'e' || *p_ == 'E' ||
-                       *p_ == '+' || *p_ == '-')) {
-      if (*p_ == '.' || *p_ == 'e' || *p_ == 'E') is_float = true;
-      ++p_;
-    }
-    std::string tmp(s, (size_t)(p_ - s));
-    JNode& n = nodes_[me];
-    char* endp = nullptr;
-    if (!is_float) {
-      errno = 0;
-      long long v = strtoll(tmp.c_str(), &endp, 10);
-      if (*endp == 0 && errno == 0) {
-        n.t = JType::Int;
-        n.i = v;
-        n.d = (double)v;
-        return true;
-      }
-    }
-    n.t = JType::Float;
-    n.d = strtod(tmp.c_str(), &endp);
-    if (*endp != 0) {
-      *err_ = "invalid number";
-      return false;
-    }
-    return true;
-  }
+  if (c == '-' || digit(c)) return number();
   *err_ = "expected value";
   return false;
 }
 
 bool JDoc::parse(const char* text, size_t len, std::string* err) {
   clear();
+  src_ = text;
   p_ = text;
   e_ = text + len;
   std::string scratch;
   err_ = err ? err : &scratch;
+  if (len >= 0x7fffffffu) {
+    *err_ = "document too large";
+    return false;
+  }
   if (!value(0)) return false;
-  ws();
+  while (p_ < e_ && is_ws(*p_)) ++p_;
   if (p_ != e_) {
     *err_ = "trailing characters";
     return false;
@@ -297,11 +350,27 @@ int64_t JDoc::get(uint32_t obj, std::string_view k) const {
   const JNode& n = nodes_[obj];
   if (n.t != JType::Obj) return -1;
   int64_t found = -1;
-  for (uint32_t j = 0; j < n.k_count; ++j) {
-    const JKid& kid = kids_[n.k_begin + j];
-    if (key(kid) == k) found = kid.node;
-  }
+  uint32_t m = obj + 1;
+  for (uint32_t j = 0; j < n.c; ++j, m = nodes_[m].next)
+    if (nodes_[m].key_len == k.size() && key(m) == k) found = m;
   return found;
+}
+
+void JDoc::pick(uint32_t obj, const std::string_view* keys, int nkeys, int64_t* out) const {
+  for (int q = 0; q < nkeys; ++q) out[q] = -1;
+  const JNode& n = nodes_[obj];
+  if (n.t != JType::Obj) return;
+  uint32_t m = obj + 1;
+  for (uint32_t j = 0; j < n.c; ++j, m = nodes_[m].next) {
+    const uint32_t kl = nodes_[m].key_len;
+    for (int q = 0; q < nkeys; ++q) {
+      if (keys[q].size() != kl) continue;
+      if (key(m) == keys[q]) {
+        out[q] = m;
+        break;
+      }
+    }
+  }
 }
 
 void json_escape(std::string* out, std::string_view s) {

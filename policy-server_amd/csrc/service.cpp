@@ -222,8 +222,9 @@ Status capabilities_patch(const PolicyRec& P, const char* doc, size_t len, int d
     for (const char* ln : lists) {
       const int64_t arr = d.get((uint32_t)ps.spec, ln);
       if (arr < 0 || !d.is((uint32_t)arr, JType::Arr)) continue;
-      for (uint32_t k = 0; k < d.count((uint32_t)arr); ++k) {
-        const uint32_t c = d.kids((uint32_t)arr)[k].node;
+      uint32_t k = 0;  // item index (the JSON Pointer's)
+      for (uint32_t c : d.members((uint32_t)arr)) {
+        const uint32_t ki = k++;
         if (!d.is(c, JType::Obj)) continue;
         const int64_t sc = d.get(c, "securityContext");
         const bool sc_obj = sc >= 0 && d.is((uint32_t)sc, JType::Obj);
@@ -233,8 +234,7 @@ Status capabilities_patch(const PolicyRec& P, const char* doc, size_t len, int d
         const bool add_arr = add >= 0 && d.is((uint32_t)add, JType::Arr), drop_arr = drop >= 0 && d.is((uint32_t)drop, JType::Arr);
         auto has = [&](int64_t a, bool is_arr, const std::string& x) {
           if (!is_arr) return false;
-          for (uint32_t i = 0; i < d.count((uint32_t)a); ++i) {
-            const uint32_t it = d.kids((uint32_t)a)[i].node;
+          for (uint32_t it : d.members((uint32_t)a)) {
             if (d.is(it, JType::Str) && d.str(it) == x) return true;
           }
           return false;
@@ -246,7 +246,7 @@ Status capabilities_patch(const PolicyRec& P, const char* doc, size_t len, int d
         for (const auto& x : defa)
           if (!has(add, add_arr, x) && !has(drop, drop_arr, x)) madd.push_back(x);
         if (mdrop.empty() && madd.empty()) continue;
-        const std::string base = std::string(ps.pointer) + "/" + ln + "/" + std::to_string(k) + "/securityContext";
+        const std::string base = std::string(ps.pointer) + "/" + ln + "/" + std::to_string(ki) + "/securityContext";
         std::string cap_obj = "{";
         if (!madd.empty()) {
           cap_obj += "\"add\":";

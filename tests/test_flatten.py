@@ -65,3 +65,56 @@ def test_bad_row_reported(monkeypatch, threads):
     with pytest.raises(K.PayloadError) as e:
         K.Batch.from_json(d)
     assert e.value.row == 5000
+
+
+def _one(doc):
+    try:
+        b = K.Batch.from_json([doc])
+    except K.PayloadError as e:
+        return str(e)
+    return columns(b)
+
+
+@pytest.mark.parametrize("text,ok", [
+    ("0", True), ("-0", True), ("12", True), ("1.5e3", True), ("-2E-2", True), ("1e400", False), ("01", False),
+    ("1.", False), (".5", False), ("-", False), ("1e", False), ("1e+", False), ("+1", False), ("0x1", False),
+    ("123456789012345678901234567890", True), ("true", True), ("tru", False), ("null", True), ('"a\\u00e9\\ud83d\\ude00"', True),
+    ('"\\ud83d"', False), ('"\\x"', False), ('"a\tb"', False), ("[1,]", False), ("{\"a\":1,}", False), ("[1 2]", False),
+])
+def test_json_grammar(text, ok):
+    """RFC 8259 values inside an otherwise valid AdmissionReview (as serde_json reads them): number
+    grammar (no leading zeros, digits after '.' and 'e', f64 overflow is an error), escapes and
+    surrogate pairs, raw control characters, trailing commas."""
+    doc = docs(4, 1, 3)[0]
+    doc = doc.replace('"dryRun":false', '"dryRun":false,"extra":' + text)
+    got = _one(doc)
+    if ok:
+        assert isinstance(got, dict), got
+    else:
+        assert isinstance(got, str) and got.startswith("Failed to parse the request body as JSON"), got
+
+
+def test_json_recursion_limit():
+    """serde_json's recursion limit: 127 nested arrays/objects parse (the document's own nesting
+    included), one more is 'recursion limit exceeded' (a 400, not a 422)."""
+    doc = docs(4, 1, 3)[0]
+    base = 2  # the document and request objects enclose "extra"
+    ok = '"extra":' + "[" * (127 - base) + "]" * (127 - base)
+    bad = '"extra":' + "[" * (128 - base) + "]" * (128 - base)
+    assert isinstance(_one(doc.replace('"dryRun":false', '"dryRun":false,' + ok)), dict)
+    got = _one(doc.replace('"dryRun":false', '"dryRun":false,' + bad))
+    assert isinstance(got, str) and "recursion limit exceeded" in got
+
+
+def test_escaped_strings_and_duplicate_keys():
+    """Escaped keys and values are unescaped (the arena path) and match their plain spelling; a
+    duplicate key keeps its last value (serde_json Map)."""
+    doc = docs(4, 1, 3)[0]
+    plain = columns(K.Batch.from_json([doc]))
+    esc = doc.replace('"namespace":"', '"n\\u0061mespace":"', 1).replace('"operation":"CREATE"', '"operation":"CR\\u0045\\u0041TE"')
+    got = _one(esc)
+    assert isinstance(got, dict)
+    for k in ("ns.bytes", "ns.off", "op.bytes"):
+        assert np.array_equal(got[k], plain[k]), k
+    dup = doc.replace('"operation":"CREATE"', '"operation":"DELETE","operation":"CREATE"')
+    assert np.array_equal(columns(K.Batch.from_json([dup]))["op.bytes"], plain["op.bytes"])
