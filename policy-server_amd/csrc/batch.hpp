@@ -5,7 +5,9 @@
 // the whole AdmissionRequest to a Wasm guest per (request, policy). Here a micro-batch of bodies is
 // flattened once into SoA columns (include/kwgpu.h kw_soa) that the device streams from HBM.
 #pragma once
+#include <algorithm>
 #include <cstdint>
+#include <cstring>
 #include <string>
 #include <string_view>
 #include <vector>
@@ -18,11 +20,13 @@ namespace kw {
 struct StrCol {
   std::vector<uint32_t> off{0};
   std::vector<uint8_t> bytes;
+  // Appends one string. The pool grows geometrically and may hold zeroed slack past off.back()
+  // (and device padding after finalize()); off.back() is the byte count, pad() trims.
   void push(std::string_view s) {
-    if (bytes.size() != off.back()) bytes.resize(off.back());  // drop device padding
-    const uint8_t* p = (const uint8_t*)s.data();
-    bytes.insert(bytes.end(), p, p + s.size());  // same element type: one memmove
-    off.push_back((uint32_t)bytes.size());
+    const size_t o = off.back(), n = s.size();
+    if (bytes.size() < o + n) bytes.resize(std::max(o + n, bytes.size() * 2 + 256));
+    if (n) memcpy(bytes.data() + o, s.data(), n);
+    off.push_back((uint32_t)(o + n));
   }
   size_t n() const { return off.size() - 1; }
   // string i, or "" when i is out of range (callers that must tell the difference use get())

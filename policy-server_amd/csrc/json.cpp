@@ -21,7 +21,9 @@ void JDoc::clear() {
 
 namespace {
 
-inline bool is_ws(char c) { return c == ' ' || c == '\n' || c == '\r' || c == '\t'; }
+inline bool is_ws(char c) {  // one compare rejects every non-blank byte
+  return (unsigned char)c <= ' ' && (c == ' ' || c == '\n' || c == '\r' || c == '\t');
+}
 
 // First byte in [p, e) that is '"', '\\' or a control character (< 0x20), or e.
 inline const char* scan_string(const char* p, const char* e) {
@@ -76,10 +78,10 @@ inline bool digit(char c) { return c >= '0' && c <= '9'; }
 
 // p_ at the opening quote. A string without escapes stays in the source text; the first escape
 // moves it to the arena (unescaped).
-bool JDoc::string_into(uint32_t* off, uint32_t* len, bool* arena) {
+inline __attribute__((always_inline)) bool JDoc::string_into(uint32_t* off, uint32_t* len, bool* arena) {
   const char* s = ++p_;
   const char* q = scan_string(s, e_);
-  if (q < e_ && *q == '"') {
+  if (__builtin_expect(q < e_ && *q == '"', 1)) {
     *off = (uint32_t)(s - src_);
     *len = (uint32_t)(q - s);
     *arena = false;
@@ -87,6 +89,11 @@ bool JDoc::string_into(uint32_t* off, uint32_t* len, bool* arena) {
     return true;
   }
   *arena = true;
+  return string_escaped(s, q, off, len);
+}
+
+// The slow path: from the first escape (or error) on, the string is unescaped into the arena.
+bool JDoc::string_escaped(const char* s, const char* q, uint32_t* off, uint32_t* len) {
   *off = (uint32_t)arena_.size();
   for (;;) {
     arena_.append(s, (size_t)(q - s));

@@ -79,7 +79,8 @@ class JDoc {
 
  private:
   bool value(uint32_t depth);
-  bool string_into(uint32_t* off, uint32_t* len, bool* arena);
+  inline bool string_into(uint32_t* off, uint32_t* len, bool* arena);
+  bool string_escaped(const char* s, const char* q, uint32_t* off, uint32_t* len);
   bool number();
   const char* src_ = nullptr;
   const char* p_ = nullptr;
