@@ -3,6 +3,7 @@
 #   policy-server_amd/libkwgpu.so    product: HIP kernels + host engine + C ABI (include/kwgpu.h)
 #   policy-server_amd/libkwsynth.so  bench/test workload generator
 #   policy-server_amd/kwhost         HTTP front (/validate, /audit, /validate_raw) over libkwgpu.so
+#   policy-server_amd/kwload         closed-loop HTTP load generator for kwhost (serving measurement)
 #   oracle/build/libkworacle.so      CPU restatement (test infrastructure only)
 HIPCC ?= /opt/rocm/bin/hipcc
 CXX ?= g++
@@ -19,7 +20,7 @@ HOST_SRCS := json yaml automaton expr env flatten service slotplan metrics capi
 HOST_OBJS := $(addprefix $(OBJ)/,$(addsuffix .o,$(HOST_SRCS)))
 HEADERS := $(wildcard $(SRC)/*.hpp) include/kwgpu.h
 
-all: $(PKG)/libkwgpu.so $(PKG)/libkwsynth.so $(PKG)/kwhost oracle/build/libkworacle.so
+all: $(PKG)/libkwgpu.so $(PKG)/libkwsynth.so $(PKG)/kwhost $(PKG)/kwload oracle/build/libkworacle.so
 
 $(OBJ)/%.o: $(SRC)/%.cpp $(HEADERS)
 	@mkdir -p $(OBJ)
@@ -35,6 +36,9 @@ $(PKG)/libkwgpu.so: $(HOST_OBJS) $(OBJ)/kernels.o
 $(PKG)/kwhost: $(SRC)/kwhost.cpp include/kwgpu.h $(PKG)/libkwgpu.so
 	$(CXX) -O2 -std=c++17 -Wall -Wextra -o $@ $< -L$(PKG) -lkwgpu -Wl,-rpath,'$$ORIGIN' -lpthread
 
+$(PKG)/kwload: $(SRC)/kwload.cpp $(PKG)/libkwsynth.so
+	$(CXX) -O2 -std=c++17 -Wall -Wextra -o $@ $< -L$(PKG) -lkwsynth -Wl,-rpath,'$$ORIGIN' -lpthread
+
 $(PKG)/libkwsynth.so: $(SRC)/synth.cpp include/kwgpu.h
 	$(CXX) -O3 -std=c++17 -fPIC -shared -Wall -o $@ $<
 
@@ -47,6 +51,6 @@ resources: $(SRC)/kernels.hip
 	$(HIPCC) $(HIPFLAGS) -Rpass-analysis=kernel-resource-usage -c $< -o /dev/null
 
 clean:
-	rm -rf $(OBJ) $(PKG)/*.so $(PKG)/kwhost oracle/build
+	rm -rf $(OBJ) $(PKG)/*.so $(PKG)/kwhost $(PKG)/kwload oracle/build
 
 .PHONY: all clean resources

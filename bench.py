@@ -57,7 +57,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rows", type=int, default=None, help="requests per GPU (default: the config's)")
     ap.add_argument("--config", default="c4_64", choices=sorted(CONFIGS))
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (rank 0)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (rank 0), about 10-30 s")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-modes", action="store_true", help="skip the end-to-end / flatten timings")
     args = ap.parse_args()
@@ -261,14 +261,21 @@ def cpu_baseline(policies, ids, args):
     t = time.perf_counter()
     oe.eval(syn.soa(), ids, threads=threads, cpus=cpus)
     per_row = (time.perf_counter() - t) / probe_rows
-    rows = int(min(2_000_000, max(probe_rows, args.cpu_seconds / max(per_row, 1e-9))))
+    # a sample of up to 2M requests, evaluated in repeated passes until the CPU budget is spent
+    rows = int(min(2_000_000, max(probe_rows, args.cpu_seconds / 4 / max(per_row, 1e-9))))
     syn = K.SynthBatch(args.synth, rows, seed=20250509)
+    soa = syn.soa()
+    passes = 0
     t = time.perf_counter()
-    oe.eval(syn.soa(), ids, threads=threads, cpus=cpus)
-    dt = time.perf_counter() - t
-    return {"value": rows / dt, "unit": "requests/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
-            "sample": f"{rows} synthetic {args.config} requests x {len(ids)} policies ({dt:.1f}s, oracle/kworacle.c, "
-                      f"{threads} threads pinned one per core)"}
+    while True:
+        oe.eval(soa, ids, threads=threads, cpus=cpus)
+        passes += 1
+        dt = time.perf_counter() - t
+        if dt >= args.cpu_seconds:
+            break
+    return {"value": rows * passes / dt, "unit": "requests/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
+            "sample": f"{rows} synthetic {args.config} requests x {len(ids)} policies, {passes} passes ({dt:.1f}s, "
+                      f"oracle/kworacle.c, {threads} threads pinned one per core)"}
 
 
 if __name__ == "__main__":
