@@ -25,6 +25,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "policy-server_amd"))
 
 METRIC = "admission requests evaluated/sec (node) at 64 policies; HBM GB/s vs peak"
+SEED = 20250509
+GATHER_MAX_BYTES = 8 << 30  # verdict gather to rank 0 after the timed region (multi-GPU)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 
 # BASELINE.json configs: policies file, synthetic workload id, default requests per GPU,
@@ -96,12 +98,14 @@ def main():
     npol = len(ids)
 
     t0 = time.time()
-    from kwgpu.dist import shard
+    from kwgpu.dist import synth_bounds
 
-    row0, nrows = shard(args.rows, rank)
-    syn = K.SynthBatch(args.synth, nrows, seed=20250509, row0=row0)
+    # the job is world x rows requests, split into shards of equal work (1 + containers per request)
+    bounds = synth_bounds(args.synth, world * args.rows, world, SEED)
+    row0, nrows = int(bounds[rank]), int(bounds[rank + 1] - bounds[rank])
+    syn = K.SynthBatch(args.synth, nrows, seed=SEED, row0=row0)
     batch = syn.batch().to_device(device)
-    log(f"rank {rank}: {args.rows} requests generated + resident in {time.time() - t0:.1f}s; {npol} policies")
+    log(f"rank {rank}: {nrows} requests generated + resident in {time.time() - t0:.1f}s; {npol} policies")
 
     for _ in range(args.warmup):
         batch.validate(env, ids)
@@ -132,6 +136,18 @@ def main():
     # sanity: a sample of verdicts is non-trivial
     v = batch.verdicts()
     frac_allowed = float(((v & K._native.KW_F_ALLOWED) != 0).mean())
+    gather = None
+    if dist:  # verdict words back to rank 0's host, in disjoint slices (after the timed region)
+        from kwgpu.dist import gather_verdicts
+        total_bytes = world * args.rows * npol * 4
+        if total_bytes <= GATHER_MAX_BYTES:
+            t = time.perf_counter()
+            allv = gather_verdicts(v, bounds, npol, dist, rank, world, tensor_device="cuda")
+            if rank == 0:
+                gather = {"rows": int(allv.shape[0]), "bytes": int(allv.nbytes), "s": time.perf_counter() - t,
+                          "allowed_fraction": float(((allv & K._native.KW_F_ALLOWED) != 0).mean())}
+        else:
+            gather = {"skipped": f"{total_bytes / 1e9:.1f} GB of verdict words > {GATHER_MAX_BYTES / 1e9:.0f} GB"}
 
     result = None
     if rank == 0:
@@ -154,6 +170,8 @@ def main():
             "cpu_baseline": cpu,
             "timing_modes": modes,
             "verdicts_final_allowed_fraction": frac_allowed,
+            "shards": {"rows": [int(bounds[k + 1] - bounds[k]) for k in range(world)], "balance": "1 + containers"},
+            "gather": gather,
         }
         print(json.dumps(result), flush=True)
     if dist:
@@ -257,13 +275,13 @@ def cpu_baseline(policies, ids, args):
     threads = len(cpus)
     oe = O.OracleEnv(policies)
     probe_rows = 2000
-    syn = K.SynthBatch(args.synth, probe_rows, seed=20250509)
+    syn = K.SynthBatch(args.synth, probe_rows, seed=SEED)
     t = time.perf_counter()
     oe.eval(syn.soa(), ids, threads=threads, cpus=cpus)
     per_row = (time.perf_counter() - t) / probe_rows
     # a sample of up to 2M requests, evaluated in repeated passes until the CPU budget is spent
     rows = int(min(2_000_000, max(probe_rows, args.cpu_seconds / 4 / max(per_row, 1e-9))))
-    syn = K.SynthBatch(args.synth, rows, seed=20250509)
+    syn = K.SynthBatch(args.synth, rows, seed=SEED)
     soa = syn.soa()
     passes = 0
     t = time.perf_counter()

@@ -179,6 +179,34 @@ void json_str(std::string* o, const std::string& s) {
 namespace {
 kws_batch* generate_range(int config, uint64_t n, uint64_t seed, uint64_t row0);
 
+// The shape of a row, drawn from its own generator so that it can be computed without generating
+// the row (kws_shard_bounds balances shards by it): the object kind and the container counts.
+struct Shape {
+  int ok = 0;  // 0 Pod, 1 Deployment, 2 Namespace
+  uint32_t nc = 0, ninit = 0, neph = 0;
+  uint32_t containers() const { return nc + ninit + neph; }
+};
+
+Shape row_shape(int config, uint64_t seed, uint64_t row) {
+  static const Zipf zc5(64, 1.3);
+  Rng r(seed * 0x9e3779b97f4a7c15ull + row * 0x100000001b3ull + 777);
+  Shape sh;
+  if (config == 5 || config == 0) {
+    const double u = r.uni();
+    sh.ok = u < 0.70 ? 0 : u < 0.90 ? 1 : 2;
+  }
+  if (sh.ok == 2) return sh;
+  if (config == 5) {
+    sh.nc = 1 + (uint32_t)zc5.draw(r);
+  } else {
+    sh.nc = 1;
+    while (sh.nc < 16 && r.chance(0.5)) ++sh.nc;
+  }
+  sh.ninit = (config == 0 || config == 5) && r.chance(0.1) ? 1 : 0;
+  sh.neph = config == 0 && r.chance(0.03) ? 1 : 0;
+  return sh;
+}
+
 void append_batch(kws_batch* d, const kws_batch& o) {
   auto shift = [](std::vector<uint32_t>* dst, const std::vector<uint32_t>& src) {
     const uint32_t base = dst->back();
@@ -222,6 +250,50 @@ kws_batch* kws_generate(int config, uint64_t n, uint64_t seed, uint64_t row0) {
   return b;
 }
 
+// Row weights of the synthetic stream: weight(row) = 1 + its containers (the per-request and
+// per-container work of a pass). Splits rows [0, total) into `world` contiguous shards of equal
+// weight: bounds[0] = 0 <= bounds[1] <= ... <= bounds[world] = total (C5's Zipf
+// container counts make equal row counts unequal work). Computed on 16 threads from the row shapes
+// alone, so every rank derives the same bounds without generating the other shards.
+int kws_shard_bounds(int config, uint64_t total, uint64_t seed, int world, uint64_t* bounds) {
+  if (world < 1 || !bounds) return 1;
+  const uint64_t nt = total >= 200000 ? 16 : 1;
+  std::vector<uint64_t> csum(nt + 1, 0);
+  auto w = [&](uint64_t row) { return (uint64_t)1 + row_shape(config, seed, row).containers(); };
+  {
+    std::vector<std::thread> th;
+    for (uint64_t t = 0; t < nt; ++t)
+      th.emplace_back([&, t] {
+        uint64_t acc = 0;
+        for (uint64_t r = total * t / nt; r < total * (t + 1) / nt; ++r) acc += w(r);
+        csum[t + 1] = acc;
+      });
+    for (auto& x : th) x.join();
+  }
+  for (uint64_t t = 0; t < nt; ++t) csum[t + 1] += csum[t];
+  const uint64_t W = csum[nt];
+  bounds[0] = 0;
+  bounds[world] = total;
+  for (int k = 1; k < world; ++k) {
+    const unsigned __int128 tgt128 = (unsigned __int128)W * (uint64_t)k / (uint64_t)world;
+    const uint64_t target = (uint64_t)tgt128;  // shard k starts at the first row whose prefix reaches it
+    uint64_t t = 0;
+    while (t + 1 < nt && csum[t + 1] <= target) ++t;
+    uint64_t acc = csum[t], r = total * t / nt;
+    const uint64_t end = total * (t + 1) / nt;
+    while (r < end && acc + w(r) <= target) acc += w(r++);
+    if (acc < target && r < end) ++r;  // the row straddling the target goes to the earlier shard
+    bounds[k] = std::max(bounds[k - 1], r);
+  }
+  return 0;
+}
+
+// Containers per row for rows [row0, row0 + n) (tests check the bounds against these).
+int kws_row_containers(int config, uint64_t n, uint64_t seed, uint64_t row0, uint32_t* out) {
+  for (uint64_t i = 0; i < n; ++i) out[i] = row_shape(config, seed, row0 + i).containers();
+  return 0;
+}
+
 }  // extern "C"
 
 namespace {
@@ -229,16 +301,12 @@ kws_batch* generate_range(int config, uint64_t n, uint64_t seed, uint64_t row0) 
   auto* b = new kws_batch();
   b->config = config;
   b->n = n;
-  static const Zipf zns(256, 1.1), zc5(64, 1.3);
+  static const Zipf zns(256, 1.1);
   b->req_flags.reserve(n);
   for (uint64_t i = 0; i < n; ++i) {
     Rng r(seed * 0x100000001b3ull + (row0 + i) * 0x9e3779b97f4a7c15ull + 12345);
-    // kind of object
-    int ok = 0;  // Pod
-    if (config == 5 || config == 0) {
-      double u = r.uni();
-      ok = u < 0.70 ? 0 : u < 0.90 ? 1 : 2;
-    }
+    const Shape sh = row_shape(config, seed, row0 + i);
+    const int ok = sh.ok;  // kind of object
     b->obj_kind.push_back((uint8_t)ok);
     uint8_t rf = KW_REQ_HAS_OBJECT;
     b->uid.push(uuid4(r));
@@ -282,14 +350,7 @@ kws_batch* generate_range(int config, uint64_t n, uint64_t seed, uint64_t row0) 
     // containers
     if (ok != 2) {
       rf |= KW_REQ_HAS_PODSPEC;
-      uint32_t nc;
-      if (config == 5) nc = 1 + (uint32_t)zc5.draw(r);
-      else {
-        nc = 1;
-        while (nc < 16 && r.chance(0.5)) ++nc;
-      }
-      uint32_t ninit = (config == 0 || config == 5) && r.chance(0.1) ? 1 : 0;
-      uint32_t neph = config == 0 && r.chance(0.03) ? 1 : 0;
+      const uint32_t nc = sh.nc, ninit = sh.ninit, neph = sh.neph;
       std::vector<std::string> names;
       for (uint32_t c = 0; c < nc + ninit + neph; ++c) {
         uint8_t cf = KW_CTR_HAS_IMAGE;

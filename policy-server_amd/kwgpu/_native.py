@@ -179,5 +179,9 @@ def synth():
     S.kws_view.argtypes = [C.c_void_p, C.POINTER(KwSoa)]
     S.kws_json.restype = C.c_int
     S.kws_json.argtypes = [C.c_void_p, C.c_uint64, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]
+    S.kws_shard_bounds.restype = C.c_int
+    S.kws_shard_bounds.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_int, C.POINTER(C.c_uint64)]
+    S.kws_row_containers.restype = C.c_int
+    S.kws_row_containers.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint32)]
     _synth = S
     return S

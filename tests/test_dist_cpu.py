@@ -3,18 +3,25 @@
 * the compiled-table blob built on rank 0 reaches rank 1 intact (kwgpu.dist.broadcast_environment,
   the same function bench.py runs over RCCL), and the rebuilt environment answers the host-side
   accessors identically (policy ids, modes, allowed_to_mutate, namespace bypass);
-* the weak-scaling shards partition the job: concatenating the ranks' synthetic shards gives
-  exactly the rows of one batch generated at once (no cross-rank state, no data-path collective).
+* the shards are balanced by work (requests + containers, kws_shard_bounds on C5's Zipf container
+  counts) and partition the job: concatenating the ranks' synthetic shards gives exactly the rows of
+  one batch generated at once (no cross-rank state, no data-path collective);
+* each rank EVALUATES its shard with its own environment (rank 1: the deserialized blob) through
+  the slot compiler's host walk (kw_debug_host_walk: the device kernel's tables and walks on the
+  host), the verdict words are gathered into disjoint slices of one array on rank 0
+  (kwgpu.dist.gather_verdicts), and that array equals the oracle's verdicts for the whole job.
 """
 import os
 import socket
 
 import numpy as np
+import pytest
 import torch.multiprocessing as mp
 
 from helpers import ROOT, config
 
 ROWS = 257
+SEED = 11
 
 
 def _free_port():
@@ -35,15 +42,16 @@ def _worker(rank, world, port, out_dir):
     import torch.distributed as dist
 
     import kwgpu as K
-    from kwgpu.dist import broadcast_environment, shard
+    from kwgpu.dist import broadcast_environment, gather_verdicts, synth_bounds
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
         env = broadcast_environment(config("c5_mixed"), dist, rank, device=-1, continue_on_errors=True,
                                     always_accept_namespace="kubewarden")
         ids = env.policy_ids()
-        row0, n = shard(ROWS, rank)
-        syn = K.SynthBatch(5, n, seed=11, row0=row0)  # owns the columns the view points at
+        bounds = synth_bounds(5, world * ROWS, world, SEED)
+        row0, n = int(bounds[rank]), int(bounds[rank + 1] - bounds[rank])
+        syn = K.SynthBatch(5, n, seed=SEED, row0=row0)  # owns the columns the view points at
         soa = syn.soa()
         np.save(os.path.join(out_dir, f"blob{rank}.npy"), np.frombuffer(env.serialize(), dtype=np.uint8))
         facts = [ids, [env.get_policy_mode(i) for i in ids], [env.get_policy_allowed_to_mutate(i) for i in ids],
@@ -52,22 +60,46 @@ def _worker(rank, world, port, out_dir):
             f.write(repr(facts))
         with open(os.path.join(out_dir, f"uids{rank}.txt"), "wb") as f:
             f.write(b"\n".join(_strings(soa.uid, n)))
+        verdicts = syn.batch().debug_host_walk(env, ids)
+        gathered = gather_verdicts(verdicts, bounds, len(ids), dist, rank, world)
+        if rank == 0:
+            np.save(os.path.join(out_dir, "gathered.npy"), gathered)
+            np.save(os.path.join(out_dir, "bounds.npy"), bounds)
+        else:
+            assert gathered is None
         dist.barrier()
     finally:
         dist.destroy_process_group()
 
 
-def test_blob_broadcast_and_shards(tmp_path):
-    world = 2
+@pytest.mark.parametrize("world", [2, 3])
+def test_blob_broadcast_shards_and_gathered_verdicts(tmp_path, world):
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
-    b0, b1 = np.load(tmp_path / "blob0.npy"), np.load(tmp_path / "blob1.npy")
-    assert b0.size > 0 and np.array_equal(b0, b1)
-    assert (tmp_path / "facts0.txt").read_text() == (tmp_path / "facts1.txt").read_text()
+    b0 = np.load(tmp_path / "blob0.npy")
+    for r in range(1, world):
+        assert b0.size > 0 and np.array_equal(b0, np.load(tmp_path / f"blob{r}.npy"))
+        assert (tmp_path / "facts0.txt").read_text() == (tmp_path / f"facts{r}.txt").read_text()
 
     import kwgpu as K
+    import oracle as O
 
-    syn = K.SynthBatch(5, world * ROWS, seed=11)
+    syn = K.SynthBatch(5, world * ROWS, seed=SEED)
     whole = syn.soa()
     want = _strings(whole.uid, world * ROWS)
-    got = (tmp_path / "uids0.txt").read_bytes().split(b"\n") + (tmp_path / "uids1.txt").read_bytes().split(b"\n")
+    got = []
+    for r in range(world):
+        got += (tmp_path / f"uids{r}.txt").read_bytes().split(b"\n")
     assert got == want
+
+    # the shards carry equal work (1 + containers per row), within one row's weight
+    bounds = np.load(tmp_path / "bounds.npy")
+    ctr = np.ctypeslib.as_array(whole.ctr_off, shape=(world * ROWS + 1,)).astype(np.int64)
+    w = 1 + np.diff(ctr)
+    loads = [int(w[bounds[k]:bounds[k + 1]].sum()) for k in range(world)]
+    assert max(loads) - min(loads) <= 2 * int(w.max()), loads
+
+    oe = O.OracleEnv(config("c5_mixed"), continue_on_errors=True, always_accept_namespace="kubewarden")
+    ids = [p["id"] for p in oe.pol]
+    gathered = np.load(tmp_path / "gathered.npy")
+    expect = oe.eval(whole, ids).reshape(world * ROWS, len(ids))
+    assert gathered.shape == expect.shape and np.array_equal(gathered, expect)
