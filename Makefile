@@ -46,6 +46,13 @@ oracle/build/libkworacle.so: oracle/kworacle.c oracle/kworacle.h include/kwgpu.h
 	@mkdir -p oracle/build
 	$(CC) -O2 -std=c11 -fPIC -shared -Wall -Wextra -o $@ $< -lpthread
 
+# A/B variant of the library with extra kernel flags: make variant NAME=x VFLAGS="-DKW_KV_PAIR=1"
+# -> policy-server_amd/variants/x.so (KWGPU_LIB selects it; scripts/ab.sh benches every variant)
+variant: $(HOST_OBJS)
+	@mkdir -p $(PKG)/variants/obj-$(NAME)
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c $(SRC)/kernels.hip -o $(PKG)/variants/obj-$(NAME)/kernels.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(PKG)/variants/$(NAME).so $(HOST_OBJS) $(PKG)/variants/obj-$(NAME)/kernels.o
+
 # kernel resource usage (VGPR/SGPR/LDS/occupancy) report
 resources: $(SRC)/kernels.hip
 	$(HIPCC) $(HIPFLAGS) -Rpass-analysis=kernel-resource-usage -c $< -o /dev/null
@@ -53,4 +60,4 @@ resources: $(SRC)/kernels.hip
 clean:
 	rm -rf $(OBJ) $(PKG)/*.so $(PKG)/kwhost $(PKG)/kwload oracle/build
 
-.PHONY: all clean resources
+.PHONY: all clean resources variant

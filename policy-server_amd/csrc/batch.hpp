@@ -17,6 +17,33 @@
 
 namespace kw {
 
+// Copies n bytes without a library call for the short strings of a request (two overlapping
+// loads / stores of the largest power of two <= n; memcpy above 16 bytes). Never reads or writes
+// outside [src, src + n) / [dst, dst + n).
+inline void copy_small(uint8_t* dst, const uint8_t* src, size_t n) {
+  if (n >= 8) {
+    if (n > 16) {
+      memcpy(dst, src, n);
+      return;
+    }
+    uint64_t a, b;
+    memcpy(&a, src, 8);
+    memcpy(&b, src + n - 8, 8);
+    memcpy(dst, &a, 8);
+    memcpy(dst + n - 8, &b, 8);
+  } else if (n >= 4) {
+    uint32_t a, b;
+    memcpy(&a, src, 4);
+    memcpy(&b, src + n - 4, 4);
+    memcpy(dst, &a, 4);
+    memcpy(dst + n - 4, &b, 4);
+  } else if (n) {
+    dst[0] = src[0];
+    dst[n / 2] = src[n / 2];
+    dst[n - 1] = src[n - 1];
+  }
+}
+
 struct StrCol {
   std::vector<uint32_t> off{0};
   std::vector<uint8_t> bytes;
@@ -25,7 +52,7 @@ struct StrCol {
   void push(std::string_view s) {
     const size_t o = off.back(), n = s.size();
     if (bytes.size() < o + n) bytes.resize(std::max(o + n, bytes.size() * 2 + 256));
-    if (n) memcpy(bytes.data() + o, s.data(), n);
+    copy_small(bytes.data() + o, (const uint8_t*)s.data(), n);
     off.push_back((uint32_t)(o + n));
   }
   size_t n() const { return off.size() - 1; }

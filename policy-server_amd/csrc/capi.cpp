@@ -81,12 +81,12 @@ BlockPool& host_pool() {
   return *p;
 }
 
-// Requests per tile of the tile kernel: kSlotRows, or KW_SLOT_ROWS (8..64, A/B knob) when set.
+// Requests per tile of the tile kernel: kSlotRows, or KW_SLOT_ROWS (8..255, A/B knob) when set.
 uint32_t slot_rows() {
   static const uint32_t r = [] {
     const char* e = getenv("KW_SLOT_ROWS");
     const int v = e ? atoi(e) : 0;
-    return (v >= 8 && v <= (int)kSlotRows) ? (uint32_t)v : kSlotRows;
+    return (v >= 8 && v <= 255) ? (uint32_t)v : kSlotRows;  // tile-local owners are u8
   }();
   return r;
 }
@@ -839,12 +839,36 @@ int run_pass(kw_batch* kb, PassPlan& plan, bool timed, hipStream_t s) {
   D.last_wide_policy = plan.wide_policy;
   D.last_rows_mode = plan.rows_mode;
   D.last_wide_cap = A.wide_cap;
+  // diagnostics: per-phase clocks of the tile kernel (KW_TILE_DEBUG & 512), printed per launch
+  const bool phases = (plan.geom.debug & 512u) != 0;
+  void* d_phase = nullptr;
+  const size_t phase_bytes = (size_t)plan.grid * 8 * sizeof(uint64_t);
+  if (phases) {
+    HIPCHK(hipMalloc(&d_phase, phase_bytes));
+    A.phase = (uint64_t*)d_phase;
+  }
   if (timed) HIPCHK(hipEventRecord(D.ev[0], s));
   for (size_t l = 0; l < plan.tiles.size(); ++l) {
+    if (phases) HIPCHK(hipMemsetAsync(d_phase, 0, phase_bytes, s));
     HIPCHK(launch_evaluate_tiles(A, plan.tiles[l], D.d_tiles + l, D.desc, plan.grid, s));
+    if (phases) {
+      std::vector<uint64_t> ph((size_t)plan.grid * 8);
+      HIPCHK(hipMemcpyAsync(ph.data(), d_phase, phase_bytes, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      double sum[8] = {0};
+      for (uint32_t g = 0; g < plan.grid; ++g)
+        for (int k = 0; k < 8; ++k) sum[k] += (double)ph[(size_t)g * 8 + k];
+      const double tiles = std::max(1.0, sum[5]);
+      fprintf(stderr,
+              "[kw phase] launch %zu grid %u tiles %.0f: cycles/tile P0 %.0f P1 %.0f D %.0f P2 %.0f P3+next %.0f "
+              "(sum %.0f); per workgroup: %.0f cycles, %.2f tiles, table staging %.0f\n",
+              l, plan.grid, tiles, sum[0] / tiles, sum[1] / tiles, sum[2] / tiles, sum[3] / tiles, sum[4] / tiles,
+              (sum[0] + sum[1] + sum[2] + sum[3] + sum[4]) / tiles, sum[6] / plan.grid, tiles / plan.grid, sum[7] / plan.grid);
+    }
     if (D.n_overflow) HIPCHK(launch_overflow(A, D.d_tiles + l, D.overflow, D.n_overflow, s));
   }
   if (timed) HIPCHK(hipEventRecord(D.ev[2], s));
+  if (phases) HIPCHK(hipFree(d_phase));
   return KW_OK;
 }
 

@@ -23,6 +23,18 @@
 #include "../../include/kwgpu.h"
 #include "kernels.hpp"
 
+// Build-time variants (A/B): KW_KV_PAIR runs a key's label-value DFAs two at a time; KW_LDS_BARRIER
+// uses LDS-only barriers between the compute phases; KW_MAND_BATCH batches the mandatory-label loads.
+#ifndef KW_KV_PAIR
+#define KW_KV_PAIR 0
+#endif
+#ifndef KW_LDS_BARRIER
+#define KW_LDS_BARRIER 1
+#endif
+#ifndef KW_MAND_BATCH
+#define KW_MAND_BATCH 1
+#endif
+
 namespace kw {
 
 // ------------------------------------------------------------------------------------------
@@ -253,7 +265,59 @@ __device__ inline void classify_image(const Classifiers& C, const ImgLayout& il,
 }
 
 // COL_LV classes of a label value under label-key class k (one per DFA of the key's chain; 0xffff
-// fills the rest of the nlv entries).
+// fills the rest of the nlv entries). The chain's DFAs run two at a time over the same byte windows,
+// so their transition chains (the only dependent loads) overlap.
+__device__ inline uint32_t kv_trans(const uint8_t* R, const KvDfa& d, uint32_t st, uint32_t c) {
+  // one aligned u16 load serves both table widths (u8 tables: the byte at the even or odd half;
+  // staged regions are padded, so the pair never leaves the region)
+  const uint32_t a = d.trans_off + ((st * d.ncls + c) << d.t16);
+  const uint32_t v = *(const uint16_t*)(R + (a & ~1u));
+  return d.t16 ? v : ((a & 1u) ? (v >> 8) : (v & 0xffu));
+}
+
+#if KW_KV_PAIR
+template <class Out>
+__device__ inline void classify_value(const Classifiers& C, uint32_t k, uint32_t nlv, const uint8_t* __restrict__ bytes,
+                                      uint32_t b, uint32_t e, Out out) {
+  uint32_t j = 0;
+  if (C.kv && k) {
+    const uint8_t* R = C.kv;
+    const uint32_t kbase = ((const uint32_t*)R)[C.nlk + k];
+    for (uint32_t rel = ((const uint32_t*)R)[k]; rel;) {
+      const KvDfa d0 = *(const KvDfa*)(R + rel);
+      const bool two = d0.next != 0;
+      const KvDfa d1 = *(const KvDfa*)(R + (two ? d0.next : rel));  // alone: d0 again, result unused
+      uint32_t s0 = d0.start, s1 = d1.start;
+      // 8-byte windows: the window's dwords, then its byte classes, load as batches; only the
+      // transitions form dependent chains, two of them interleaved (bytes past the string read
+      // the zero tail, unused)
+      for (uint32_t p = b; p < e && (s0 | s1) != 0; p += 8u) {
+        const uint32_t* q = (const uint32_t*)(bytes + (p & ~3u));
+        const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], sh = p & 3u;
+        const uint32_t x0 = align_bytes(q1, q0, sh), x1 = align_bytes(q2, q1, sh);
+        uint32_t c0[8], c1[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const uint32_t by = ((i < 4 ? x0 : x1) >> (8 * (i & 3))) & 0xffu;
+          c0[i] = (by < 128u || d0.wide) ? R[d0.cls_off + by] : d0.hi;
+          c1[i] = (by < 128u || d1.wide) ? R[d1.cls_off + by] : d1.hi;
+        }
+        const uint32_t lim = min(8u, e - p);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if ((uint32_t)i < lim) {
+            s0 = kv_trans(R, d0, s0, c0[i]);
+            s1 = kv_trans(R, d1, s1, c1[i]);
+          }
+      }
+      out(j++, kbase + d0.cbase + ((const uint16_t*)(R + d0.acc_off))[s0]);
+      if (two) out(j++, kbase + d1.cbase + ((const uint16_t*)(R + d1.acc_off))[s1]);
+      rel = two ? d1.next : 0u;
+    }
+  }
+  for (; j < nlv; ++j) out(j, 0xffffu);
+}
+#else
 template <class Out>
 __device__ inline void classify_value(const Classifiers& C, uint32_t k, uint32_t nlv, const uint8_t* __restrict__ bytes,
                                       uint32_t b, uint32_t e, Out out) {
@@ -294,6 +358,7 @@ __device__ inline void classify_value(const Classifiers& C, uint32_t k, uint32_t
   }
   for (; j < nlv; ++j) out(j, 0xffffu);
 }
+#endif
 
 // ------------------------------------------------------------------------------------------
 // Per-chunk violation sets (slots.hpp tables) from stored classes
@@ -355,7 +420,20 @@ __device__ inline void copy_x4(const uint8_t* src, uint8_t* dst, uint32_t bytes,
   for (uint32_t i = tid; i < bytes / 16; i += kSlotThreads) d[i] = s[i];
 }
 
-template <bool LDST>
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS (and scalar) operations,
+// not for its outstanding global stores — the verdict stores of a tile drain under the next tile
+// instead of stalling every wave at the barrier (__syncthreads waits vmcnt(0)). Used where no
+// global load result is consumed across the barrier; the staging barrier (LDS-DMA, counted by
+// vmcnt) stays __syncthreads.
+#if KW_LDS_BARRIER
+__device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+#else
+__device__ inline void lds_barrier() { __syncthreads(); }
+#endif
+
+// TIMING: the diagnostics instantiation (EvalArgs::phase) — phase clocks add registers, so the
+// product kernel is compiled without them.
+template <bool LDST, bool TIMING>
 __global__ void __launch_bounds__(kSlotThreads)
     evaluate_tiles_kernel(EvalArgs a, const TileArgs* __restrict__ tp, const TileDesc* __restrict__ desc) {
   // TileArgs lives in device memory: its fields are scalar-loaded where used instead of all being
@@ -367,6 +445,19 @@ __global__ void __launch_bounds__(kSlotThreads)
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   uint32_t* __restrict__ out = a.out;
 
+  // phase clocks (diagnostics): thread 0 reads the shader clock right after each barrier
+  constexpr bool timing = TIMING;
+  uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t tk = timing ? clock64() : 0;
+  const uint64_t t_begin = tk;
+  auto mark = [&](int k) {
+    if (timing && tid == 0) {
+      const uint64_t now = clock64();
+      ph[k] += now - tk;
+      tk = now;
+    }
+  };
+
   // ---- once per workgroup: the column classifiers and the chunks' staged record prefixes
   if (LDST) {
     for (uint32_t s = 0; s < t.nstage; ++s) copy_x4(a.blob + t.stage_blob[s], lds + t.stage_lds[s], t.stage_bytes[s], tid);
@@ -374,6 +465,7 @@ __global__ void __launch_bounds__(kSlotThreads)
       copy_x4(t.chunk[c].rec, lds + t.chunk[c].o_lds, ((const SlotHdr*)t.chunk[c].rec)->staged, tid);
   }
   __syncthreads();
+  mark(7);
   const uint8_t* tb = LDST ? (const uint8_t*)lds : a.blob;
   Classifiers C;
 #pragma unroll
@@ -440,13 +532,15 @@ __global__ void __launch_bounds__(kSlotThreads)
     __syncthreads();
     tile = t_lo + l_nx[0];
   }
+  mark(4);
   uint32_t nxt = 0, it = 1;
   // next tile: the strided one, or the counter value thread 0 fetched (double-buffered in LDS: a
   // slot is rewritten only two barriers after every thread read it)
   auto advance = [&]() -> uint64_t {
     if (!dyn) return tile + gridDim.x;
     if (tid == 0) l_nx[it & 1u] = nxt;
-    __syncthreads();  // also: the next tile restages LDS (its strings alias this tile's violation words)
+    lds_barrier();  // also: the next tile restages LDS (its strings alias this tile's violation words)
+    mark(4);
     const uint64_t nt = t_lo + l_nx[it & 1u];
     ++it;
     return nt;
@@ -455,7 +549,7 @@ __global__ void __launch_bounds__(kSlotThreads)
     if (dyn && tid == 0) nxt = atomicAdd(cnt, 1u);
     const TileDesc& d = desc[tile];
     if (!d.fits) {  // queued for the overflow kernels by the host (uniform: no barrier skipped unevenly)
-      if (!dyn) __syncthreads();
+      if (!dyn) lds_barrier();
       continue;
     }
     const uint64_t r0 = ((uint64_t)d.r0hi << 32) | d.r0lo;
@@ -484,6 +578,8 @@ __global__ void __launch_bounds__(kSlotThreads)
     for (uint32_t i = tid; i < nr; i += kSlotThreads) l_rej[i] = l_mut[i] = 0;
     if (tid < NSTR) l_sa[tid] = d.sa[tid];
     __syncthreads();
+    mark(0);
+    if (timing && tid == 0) ++ph[5];
     const uint8_t* cfl = l_cflags + (cb & 3u);  // staged from the dword holding flag cb
     const bool classify = !(t.debug & 1u);  // diagnostics: skip classification (entities match nothing)
     auto str = [&](int m, uint32_t i, uint32_t* b, uint32_t* e) {
@@ -518,7 +614,7 @@ __global__ void __launch_bounds__(kSlotThreads)
           const uint32_t k = lit(COL_LK, S_LK, i);
           c_lk[i] = (uint16_t)k;
           uint16_t* lv = c_lv + i * nlv;
-          if (k && classify && t.o_sb[S_LV]) {
+          if (k && classify && t.o_sb[S_LV] && !(t.debug & 2048u)) {
             uint32_t b, e;
             str(S_LV, i, &b, &e);
             classify_value(C, k, nlv, lds + t.o_sb[S_LV], b, e, [&](uint32_t j, uint32_t c) { lv[j] = (uint16_t)c; });
@@ -571,7 +667,8 @@ __global__ void __launch_bounds__(kSlotThreads)
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
+    mark(1);
 
     for (uint32_t ck = 0; ck < t.nchunk; ++ck) {
       const SlotView sv = chunk_view(ck);
@@ -605,7 +702,8 @@ __global__ void __launch_bounds__(kSlotThreads)
             if (i < nr) l_rej[i] = l_mut[i] = 0;
           }
         }
-        __syncthreads();
+        lds_barrier();
+        mark(2);
       }
 
       // ---- P2: first violations, entity-parallel. A slot's first violation is the first entity
@@ -629,7 +727,8 @@ __global__ void __launch_bounds__(kSlotThreads)
             if (!(l_rf[q] & KW_REQ_HAS_PODSPEC)) continue;
             const uint32_t c0 = l_coff[q] - cb;
             uint64_t pre = 0;
-            for (uint32_t j = c0; j < i; ++j) pre |= trs ? (l_vc[j] | l_vtr[j]) : l_vc[j];
+            if (!(t.debug & 4096u))
+              for (uint32_t j = c0; j < i; ++j) pre |= trs ? (l_vc[j] | l_vtr[j]) : l_vc[j];
             const uint64_t nv = (trs ? (l_vc[i] | l_vtr[i]) : l_vc[i]) & ~pre;
             const uint32_t ci = i - c0;
             uint32_t* vw = l_vw + q * t.vw_stride;
@@ -692,12 +791,43 @@ __global__ void __launch_bounds__(kSlotThreads)
               rej = SH.ns & ~ok;
               vs.put(rej, KW_R_NAMESPACE, 0);
             }
-            if (SH.lbl && SH.mand_union) {
+            if (SH.lbl && SH.mand_union && !(t.debug & 1024u)) {
               uint64_t present = 0, lrej = 0;
               for (uint32_t l = l_loff[i] - lb, l1 = l_loff[i + 1] - lb; l < l1; ++l) {
                 present |= bit_of(sv.lkmb(c_lk[l]));
                 lrej |= l_vl[l];
               }
+#if KW_MAND_BATCH
+              // slots missing a mandatory key: rows of the missing local bits, four loads per round
+              uint64_t miss = SH.mand_union & ~present, nw = 0;
+              const uint64_t* mt = sv.mand();
+              while (miss) {
+                uint32_t bb[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                  bb[u] = miss ? kw_ctz64(miss) : 64u;
+                  miss &= miss - 1;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) nw |= bb[u] < 64u ? mt[bb[u]] : 0ull;
+              }
+              nw &= ~lrej;
+              rej |= nw;
+              while (nw) {  // the first missing mandatory key of each such slot (settings order), four per round
+                uint32_t ss[4];
+                uint64_t pk[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                  ss[u] = nw ? kw_ctz64(nw) : 64u;
+                  nw &= nw - 1;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) pk[u] = ss[u] < 64u ? sv.mpack(ss[u]) : 0ull;
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                  if (ss[u] < 64u) vs.put(1ull << ss[u], KW_R_LABEL_MANDATORY, first_missing_packed(sv, ss[u], pk[u], present));
+              }
+#else
               uint64_t nw = tab_or(sv.mand(), SH.mand_union & ~present) & ~lrej;
               rej |= nw;
               while (nw) {  // the first missing mandatory key of each such slot, settings order
@@ -705,12 +835,14 @@ __global__ void __launch_bounds__(kSlotThreads)
                 nw &= nw - 1;
                 vs.put(1ull << s, KW_R_LABEL_MANDATORY, first_missing(sv, s, present));
               }
+#endif
             }
             if (rej) atomicOr((unsigned long long*)&l_rej[i], (unsigned long long)rej);
           }
         }
       }
-      __syncthreads();
+      lds_barrier();
+      mark(3);
 
       // ---- P3: verdict words. All-pairs: items = (request, 4 columns), 16 lanes per 256-B row,
       //      column records from LDS (group / constant columns from the record's global copy).
@@ -766,9 +898,17 @@ __global__ void __launch_bounds__(kSlotThreads)
           }
         }
       }
-      if (ck + 1 < t.nchunk) __syncthreads();  // the next chunk rewrites the violation sets and words
+      if (ck + 1 < t.nchunk) {
+        lds_barrier();  // the next chunk rewrites the violation sets and words
+        mark(4);
+      }
     }
-    if (!dyn) __syncthreads();  // the next tile restages LDS (its strings alias this tile's violation words)
+    if (!dyn) lds_barrier();  // the next tile restages LDS (its strings alias this tile's violation words)
+    mark(4);  // (dynamic schedule: the barrier is advance()'s, at the loop step)
+  }
+  if (timing && tid == 0) {  // one lane's vector stores
+    ph[6] = clock64() - t_begin;
+    for (int k = 0; k < 8; ++k) a.phase[(uint64_t)blockIdx.x * 8u + (uint32_t)k] = ph[k];
   }
   if (dyn && tid == 0) {  // the XCD's last workgroup (every other one has taken its last tile) resets
     uint32_t* done = a.sched + 256u + xcd * 32u;
@@ -945,11 +1085,14 @@ hipError_t ensure_attrs() {
   if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
   std::call_once(g_attr_once[dev], [dev] {
     // allow > 64 KB of dynamic LDS per workgroup (gfx950: 160 KB per CU)
-    hipError_t e1 = hipFuncSetAttribute((const void*)evaluate_tiles_kernel<true>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipError_t e2 = hipFuncSetAttribute((const void*)evaluate_tiles_kernel<false>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    g_attr_err[dev] = e1 != hipSuccess ? e1 : e2;
+    const void* fns[4] = {(const void*)evaluate_tiles_kernel<true, false>, (const void*)evaluate_tiles_kernel<false, false>,
+                          (const void*)evaluate_tiles_kernel<true, true>, (const void*)evaluate_tiles_kernel<false, true>};
+    hipError_t e = hipSuccess;
+    for (const void* f : fns) {
+      const hipError_t ek = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      if (e == hipSuccess) e = ek;
+    }
+    g_attr_err[dev] = e;
   });
   return g_attr_err[dev];
 }
@@ -966,10 +1109,11 @@ hipError_t launch_evaluate_tiles(const EvalArgs& a, const TileArgs& t, const Til
     thread_local int c_dev = -1, c_ncu = 0, c_occ = 0;
     thread_local uint64_t c_key = ~0ull;
     int dev = 0;
-    const uint64_t key = ((uint64_t)t.lds_bytes << 1) | (t.lds_tables ? 1u : 0u);
+    const uint64_t key = ((uint64_t)t.lds_bytes << 2) | (t.lds_tables ? 1u : 0u) | (a.phase ? 2u : 0u);
     if (hipGetDevice(&dev) == hipSuccess && (dev != c_dev || key != c_key)) {
       int ncu = 0, occ = 0;
-      const void* fn = t.lds_tables ? (const void*)evaluate_tiles_kernel<true> : (const void*)evaluate_tiles_kernel<false>;
+      const void* fn = a.phase ? (t.lds_tables ? (const void*)evaluate_tiles_kernel<true, true> : (const void*)evaluate_tiles_kernel<false, true>)
+                               : (t.lds_tables ? (const void*)evaluate_tiles_kernel<true, false> : (const void*)evaluate_tiles_kernel<false, false>);
       if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
           hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kSlotThreads, t.lds_bytes) != hipSuccess)
         ncu = occ = 0;
@@ -983,9 +1127,11 @@ hipError_t launch_evaluate_tiles(const EvalArgs& a, const TileArgs& t, const Til
       fprintf(stderr, "[kw tile] launch grid=%u occupancy=%d wg/cu x %d CUs lds=%u\n", grid, c_occ, c_ncu, t.lds_bytes);
   }
   if (t.lds_tables)
-    hipLaunchKernelGGL(evaluate_tiles_kernel<true>, dim3(grid), dim3(kSlotThreads), t.lds_bytes, s, a, d_t, d_desc);
+    if (a.phase) hipLaunchKernelGGL((evaluate_tiles_kernel<true, true>), dim3(grid), dim3(kSlotThreads), t.lds_bytes, s, a, d_t, d_desc);
+    else hipLaunchKernelGGL((evaluate_tiles_kernel<true, false>), dim3(grid), dim3(kSlotThreads), t.lds_bytes, s, a, d_t, d_desc);
   else
-    hipLaunchKernelGGL(evaluate_tiles_kernel<false>, dim3(grid), dim3(kSlotThreads), t.lds_bytes, s, a, d_t, d_desc);
+    if (a.phase) hipLaunchKernelGGL((evaluate_tiles_kernel<false, true>), dim3(grid), dim3(kSlotThreads), t.lds_bytes, s, a, d_t, d_desc);
+    else hipLaunchKernelGGL((evaluate_tiles_kernel<false, false>), dim3(grid), dim3(kSlotThreads), t.lds_bytes, s, a, d_t, d_desc);
   return hipGetLastError();
 }
 

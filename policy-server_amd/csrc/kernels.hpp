@@ -41,6 +41,10 @@ struct EvalArgs {
   uint64_t* wide_groups;  // dense [row][nwide] cause masks
   uint32_t nwide;
   const uint32_t* rowcol;  // rows mode: per row (chunk << 16) | column, all-pairs: nullptr
+  // diagnostics (KW_TILE_DEBUG & 512): per workgroup, shader-clock cycles summed over its tiles
+  // [staging P0, classify P1, derive D, walk P2, verdicts P3 + next tile, tiles, whole workgroup,
+  // table staging]; nullptr = off
+  uint64_t* phase;
 };
 
 // Slot kernel geometry: one tile = up to 64 requests (one lane per request where a lane walks a
@@ -86,7 +90,8 @@ struct TileArgs {
   uint32_t nchunk;
   ChunkArgs chunk[kMaxChunks];
   uint32_t rows_mode;
-  uint32_t debug;  // diagnostics: bit0 skip classification, bit1 skip walk, bit2 skip output
+  uint32_t debug;  // diagnostics: bit0 skip classification, bit1 skip walk, bit2 skip output; 512 phase
+                  // clocks; 1024 skip mandatory labels, 2048 skip label-value DFAs, 4096 skip predecessor ORs
   uint32_t lds_bytes;
 };
 

@@ -2,6 +2,7 @@
 #include "slotplan.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 
@@ -222,6 +223,14 @@ struct Builder {
         rec.push_back(0xff);
       }
       align();
+      static const bool no_mpack = getenv("KW_NO_MPACK") != nullptr;  // A/B knob (kernels built without KW_MAND_BATCH)
+      if (!no_mpack) {
+        h.o_mpack = (uint32_t)rec.size();  // the first 8 keys of each list, packed (the kernel's fast path)
+        rec.resize(rec.size() + 8u * std::max<uint32_t>(nslots, 1), 0xff);
+        for (uint32_t s = 0; s < nslots; ++s)
+          for (size_t i = 0; i < mlist[s].size() && i < 8; ++i) rec[h.o_mpack + 8u * s + i] = mlist[s][i];
+        align();
+      }
     }
     // column arrays: the staged form of the column records (P3 reads 4 columns per array with one
     // 16-B LDS load)

@@ -62,7 +62,8 @@ struct alignas(16) SlotHdr {
   uint32_t o_cols;   // ColInfo[ncols] (global memory on the device)
   uint32_t o_prog;   // group programs (global memory on the device)
   uint32_t nwide;    // group columns of this chunk with more than 15 members
-  uint32_t pad1[2];
+  uint32_t o_mpack;  // u64 per slot: its first 8 mandatory local bits packed (0xff pad), 0 = none
+  uint32_t pad1;
 };
 static_assert(sizeof(SlotHdr) % 16 == 0, "SlotHdr layout");
 
@@ -122,6 +123,7 @@ struct SlotView {
   KW_HD const uint64_t* defa() const { return (const uint64_t*)(base + h->o_defa); }
   KW_HD const uint64_t* mand() const { return (const uint64_t*)(base + h->o_mand); }
   KW_HD const uint8_t* mlist(uint32_t s) const { return base + ((const uint32_t*)(base + h->o_mlist))[s]; }
+  KW_HD uint64_t mpack(uint32_t s) const { return ((const uint64_t*)(base + h->o_mpack))[s]; }
 };
 
 // OR of table rows over the set bits of `bits`.
@@ -193,6 +195,19 @@ KW_HD inline uint32_t first_missing(const SlotView& sv, uint32_t s, uint64_t pre
     const uint32_t b = m[i];
     if (b == 0xffu || !((present >> b) & 1ull)) break;
   }
+  return i;
+}
+
+// first_missing from the slot's packed list (one u64 load for lists of up to 8 keys; longer lists
+// continue in mlist): the same index.
+KW_HD inline uint32_t first_missing_packed(const SlotView& sv, uint32_t s, uint64_t packed, uint64_t present) {
+  for (uint32_t i = 0; i < 8; ++i) {
+    const uint32_t b = (uint32_t)(packed >> (8u * i)) & 0xffu;
+    if (b == 0xffu || !((present >> b) & 1ull)) return i;
+  }
+  const uint8_t* m = sv.mlist(s);
+  uint32_t i = 8;
+  while (m[i] != 0xffu && ((present >> m[i]) & 1ull)) ++i;
   return i;
 }
 

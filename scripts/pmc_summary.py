@@ -5,7 +5,7 @@ import sys
 from collections import defaultdict
 
 
-def summarise(d, match="evaluate_slots"):
+def summarise(d, match="evaluate_tiles"):
     vals = defaultdict(list)
     dur = {}
     for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
@@ -27,7 +27,7 @@ def write_traffic(fetch_dir, write_dir, out, config="c4_64", rows=1_000_000, tag
     f, w = summarise(fetch_dir), summarise(write_dir)
     fetch = 2.0 * f["FETCH_SIZE"] * 1024.0
     write = w["WRITE_SIZE"] * 1024.0
-    doc = {"round": tag, "config": config, "rows": rows, "kernel": "evaluate_slots_kernel",
+    doc = {"round": tag, "config": config, "rows": rows, "kernel": "evaluate_tiles_kernel",
            "fetch_bytes": fetch, "write_bytes": write, "bytes_per_launch": fetch + write,
            "source": f"rocprofv3 --pmc FETCH_SIZE ({fetch_dir}) and WRITE_SIZE ({write_dir}), separate passes; "
                      "FETCH_SIZE x2 (gfx950 calibration)"}
@@ -38,7 +38,7 @@ def write_traffic(fetch_dir, write_dir, out, config="c4_64", rows=1_000_000, tag
 
 if __name__ == "__main__":
     if sys.argv[1] == "--traffic":
-        print(write_traffic(sys.argv[2], sys.argv[3], sys.argv[4], tag=sys.argv[5] if len(sys.argv) > 5 else "r01"))
+        print(write_traffic(sys.argv[2], sys.argv[3], sys.argv[4], tag=sys.argv[5] if len(sys.argv) > 5 else "r02"))
         sys.exit(0)
     for d in sys.argv[1:]:
         s = summarise(d)
