@@ -418,7 +418,8 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
   if (need & (1u << S_CAPADD)) stage_col(COL_CAP, true, false);
   if (need & (1u << S_LK)) stage_col(COL_LK, true, false);
   uint32_t kv_stage = 0;
-  if (need & (1u << S_LV)) {
+  static const bool kv_global = getenv("KW_KV_GLOBAL") && atoi(getenv("KW_KV_GLOBAL")) != 0;  // A/B knob
+  if ((need & (1u << S_LV)) && !kv_global) {
     kv_stage = (uint32_t)stages.size() + 1;
     stages.push_back({H->kv_off, H->kv_bytes});
   }
@@ -491,7 +492,8 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
       T.o_mut = take(rows * 8);
       T.o_byp = take(rows);
       T.o_sa = take(NSTR * 4);
-      T.o_nx = take(8);
+      T.o_nx = take(12);
+      T.o_pf = take(256);
       // union: the staged strings (P0-P1) and the violation words (P2-P3)
       const uint32_t u0 = off;
       uint32_t su = u0;
@@ -558,6 +560,9 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
   else
     layout(D.tile_q[D.cap_choice]);
   if (T.lds_bytes > kTileLdsBudget) return KW_E_ARG;  // policy list too large for one tile
+  // next-tile L2 prefetch: a gain where several small tiles share a CU (C4: -2.5 %), a loss where two
+  // large ones do (C5: +2.7 %; r02 A/B)
+  T.prefetch = per_cu(T.lds_bytes) >= 3 ? 1u : 0u;
   T.il = il;
   T.nlv = nlv;
   T.need = need;
@@ -599,14 +604,19 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
     }
     if (kv_stage) {
       T.kv_blob = stages[kv_stage - 1].blob;
-      T.kv_lds = lds_at[kv_stage - 1];
+      T.kv_lds = ldst ? lds_at[kv_stage - 1] : 0u;
+    } else if (need & (1u << S_LV)) {  // the value DFAs read from the blob (global memory, L1/L2)
+      T.kv_blob = H->kv_off;
+      T.kv_lds = 0;
     }
   }
   if (const char* dbg = getenv("KW_TILE_DEBUG")) T.debug = (uint32_t)atoi(dbg);  // phase ablation (diagnostics)
   if (T.debug & 256u)
-    fprintf(stderr, "[kw tile] lds_tables=%u rows=%u cmax=%u kmax=%u lmax=%u lds=%u area=%u chunks=%zu launches=%zu nim=%u nlv=%u\n",
-            T.lds_tables, T.rows, T.cmax, T.kmax, T.lmax, T.lds_bytes, area, plan->chunks.size(), plan->launches.size(), nim,
+    fprintf(stderr, "[kw tile] lds_tables=%u rows=%u cmax=%u kmax=%u lmax=%u lds=%u area=%u (classifiers %u) chunks=%zu launches=%zu nim=%u nlv=%u\n",
+            T.lds_tables, T.rows, T.cmax, T.kmax, T.lmax, T.lds_bytes, area, table_bytes, plan->chunks.size(), plan->launches.size(), nim,
             nlv);
+  if (T.debug & 256u)
+    for (size_t k = 0; k < stages.size(); ++k) fprintf(stderr, "[kw tile]   classifier stage %zu: %u bytes\n", k, stages[k].bytes);
 
   // ---- per-launch TileArgs (record pointers filled in at upload, run_pass)
   plan->slot_blob.clear();

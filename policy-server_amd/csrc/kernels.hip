@@ -34,6 +34,15 @@
 #ifndef KW_MAND_BATCH
 #define KW_MAND_BATCH 1
 #endif
+#ifndef KW_PREFETCH  // tile kernel: warm L2 with the next tile's staged ranges during this tile's walk
+#define KW_PREFETCH 1
+#endif
+#ifndef KW_NT_STORE  // tile kernel: verdict words with non-temporal stores
+#define KW_NT_STORE 1
+#endif
+#ifndef KW_MIN_WAVES  // tile kernel: minimum waves per SIMD the register allocation must allow
+#define KW_MIN_WAVES 1
+#endif
 
 namespace kw {
 
@@ -431,10 +440,20 @@ __device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_b
 __device__ inline void lds_barrier() { __syncthreads(); }
 #endif
 
+// L2 prefetch of `bytes` at `src`: one dword per 128-B line, by LDS-DMA into a 256-B scratch line
+// shared by the waves (never read), so no VGPR waits for the data and no barrier but the next staging barrier
+// (vmcnt) covers it; the next tile's staging loads then hit L2.
+__device__ inline void prefetch_l2(const void* src, uint32_t bytes, uint32_t* scratch, uint32_t tid) {
+  const uint8_t* p = (const uint8_t*)src;
+  for (uint32_t off = tid * 128u; off < bytes; off += kSlotThreads * 128u)  // every wave lands on the same line
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(p + off),
+                                     (__attribute__((address_space(3))) void*)scratch, 4, 0, 0);
+}
+
 // TIMING: the diagnostics instantiation (EvalArgs::phase) — phase clocks add registers, so the
 // product kernel is compiled without them.
 template <bool LDST, bool TIMING>
-__global__ void __launch_bounds__(kSlotThreads)
+__global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
     evaluate_tiles_kernel(EvalArgs a, const TileArgs* __restrict__ tp, const TileDesc* __restrict__ desc) {
   // TileArgs lives in device memory: its fields are scalar-loaded where used instead of all being
   // hoisted from the kernarg segment into SGPRs at entry.
@@ -475,7 +494,7 @@ __global__ void __launch_bounds__(kSlotThreads)
     C.dfa[c].head = t.dfa_blob[c];
     C.dfa[c].base = tb + (LDST ? t.dfa_lds[c] : t.dfa_blob[c]);
   }
-  C.kv = t.kv_blob ? tb + (LDST ? t.kv_lds : t.kv_blob) : nullptr;
+  C.kv = t.kv_blob ? ((LDST && t.kv_lds) ? (const uint8_t*)lds + t.kv_lds : a.blob + t.kv_blob) : nullptr;  // kv_lds 0: global
   C.nlk = t.nlk;
   C.docker_io_cls = t.docker_io_cls;
   C.latest_cls = t.latest_cls;
@@ -580,6 +599,7 @@ __global__ void __launch_bounds__(kSlotThreads)
     __syncthreads();
     mark(0);
     if (timing && tid == 0) ++ph[5];
+    if (KW_PREFETCH && dyn && tid == 0) l_nx[2] = nxt;  // read after the next barrier (prefetch)
     const uint8_t* cfl = l_cflags + (cb & 3u);  // staged from the dword holding flag cb
     const bool classify = !(t.debug & 1u);  // diagnostics: skip classification (entities match nothing)
     auto str = [&](int m, uint32_t i, uint32_t* b, uint32_t* e) {
@@ -669,6 +689,29 @@ __global__ void __launch_bounds__(kSlotThreads)
     }
     lds_barrier();
     mark(1);
+    if (KW_PREFETCH && t.prefetch) {  // the next tile's staged ranges into L2 (covered by this tile's walk and stores)
+      const uint64_t nt = dyn ? t_lo + l_nx[2] : tile + gridDim.x;
+      if (nt < t_hi && desc[nt].fits) {
+        const TileDesc& dn = desc[nt];
+        const uint64_t q0 = ((uint64_t)dn.r0hi << 32) | dn.r0lo;
+        const uint32_t qn = dn.nr, qc = dn.ce - dn.cb;
+        uint32_t* scratch = (uint32_t*)(lds + t.o_pf);
+        prefetch_l2(a.req_flags + q0, qn, scratch, tid);
+        prefetch_l2(a.ctr_off + q0, (qn + 1) * 4u, scratch, tid);
+        prefetch_l2(a.lbl_off + q0, (qn + 1) * 4u, scratch, tid);
+        prefetch_l2(a.ctr_flags + dn.cb, qc, scratch, tid);
+        prefetch_l2(a.capadd_off + dn.cb, (qc + 1) * 4u, scratch, tid);
+        prefetch_l2(a.capdrop_off + dn.cb, (qc + 1) * 4u, scratch, tid);
+#pragma unroll
+        for (int m = 0; m < (int)NSTR; ++m) {
+          if (!t.o_sb[m]) continue;
+          const uint32_t g0 = str_g0(m, (uint32_t)q0, dn.cb, dn.kab, dn.kdb, dn.lb);
+          const uint32_t n = str_n(m, qn, qc, dn.kae - dn.kab, dn.kde - dn.kdb, dn.le - dn.lb);
+          prefetch_l2(t.s_off[m] + g0, (n + 1) * 4u, scratch, tid);
+          prefetch_l2(t.s_bytes[m] + dn.sa[m], dn.nv[m] * 16u, scratch, tid);
+        }
+      }
+    }
 
     for (uint32_t ck = 0; ck < t.nchunk; ++ck) {
       const SlotView sv = chunk_view(ck);
@@ -889,7 +932,12 @@ __global__ void __launch_bounds__(kSlotThreads)
               wv.z = pw(ks.z, ok.z, mu.z, rj.z, 4 * g + 2);
               wv.w = pw(ks.w, ok.w, mu.w, rj.w, 4 * g + 3);
             }
+#if KW_NT_STORE
+            const u32x4 nv4 = {wv.x, wv.y, wv.z, wv.w};
+            __builtin_nontemporal_store(nv4, (u32x4*)(out + (r0 + rr) * npol + CA.col0 + 4 * g));  // streamed once
+#else
             *(uint4*)(out + (r0 + rr) * npol + CA.col0 + 4 * g) = wv;
+#endif
           }
         } else {
           for (uint32_t q = tid; q < nr * ncols; q += kSlotThreads) {

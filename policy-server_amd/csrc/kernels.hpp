@@ -50,7 +50,10 @@ struct EvalArgs {
 // Slot kernel geometry: one tile = up to 64 requests (one lane per request where a lane walks a
 // request), 256 threads.
 constexpr uint32_t kSlotRows = 64;
-constexpr uint32_t kSlotThreads = 256;
+#ifndef KW_THREADS  // threads per tile workgroup (build-time A/B)
+#define KW_THREADS 256
+#endif
+constexpr uint32_t kSlotThreads = KW_THREADS;
 constexpr uint32_t kMaxChunks = 8;  // chunks of one launch (<= 512 slots); longer lists take several launches
 
 struct ChunkArgs {
@@ -74,7 +77,9 @@ struct TileArgs {
   uint32_t o_vadd, o_vl, o_vc, o_vtr;  // u64 violation sets: per added capability, per label, per container (2)
   uint32_t o_own_c, o_own_l;           // u8 tile-local request of each staged container / label
   uint32_t o_rej, o_mut, o_byp;        // per-request results: rejected / mutated slots, bypass flag
-  uint32_t o_nx;                       // u32[2]: next tile index (dynamic schedule), double-buffered
+  uint32_t o_nx;                       // u32[3]: next tile index (dynamic schedule), double-buffered; [2]: prefetch
+  uint32_t o_pf;                       // 256 B: LDS-DMA landing of the L2 prefetch (never read)
+  uint32_t prefetch;                   // warm L2 with the next tile (small tiles at >= 3 workgroups per CU)
   uint32_t o_sa;                       // u32[NSTR]: the tile's staged byte start per string column
   uint32_t o_vw, vw_stride;            // violation words [rows][vw_stride] (aliases the staged strings)
   uint32_t o_so[NSTR], o_sb[NSTR], sb_cap[NSTR];  // staged string offsets / bytes (0 = not staged)
