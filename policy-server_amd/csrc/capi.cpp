@@ -366,7 +366,7 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
 
   // ---- what the chunks classify
   uint32_t need = 0;
-  bool any_ctr = false, any_caps = false, any_trs = false, any_lbl = false;
+  bool any_ctr = false, any_caps = false, any_trs = false, any_lbl = false, any_ctr_fam = false;
   uint32_t nslots = 1;
   for (const SlotChunk& c : plan->chunks) {
     const SlotHdr& h = *(const SlotHdr*)c.rec.data();
@@ -380,6 +380,7 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
       any_lbl = true;
     }
     any_ctr = any_ctr || (h.priv[0] | h.priv[1] | h.priv[2] | h.priv[3] | h.caps | h.aa | h.trs) != 0;
+    any_ctr_fam = any_ctr_fam || (h.priv[0] | h.priv[1] | h.priv[2] | h.priv[3] | h.caps | h.aa) != 0;
     nslots = std::max(nslots, c.nslots);
   }
   if (H->bypass_cls) need |= 1u << S_NS;
@@ -563,6 +564,7 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
   // next-tile L2 prefetch: a gain where several small tiles share a CU (C4: -2.5 %), a loss where two
   // large ones do (C5: +2.7 %; r02 A/B)
   T.prefetch = per_cu(T.lds_bytes) >= 3 ? 1u : 0u;
+  T.feat = ((need & (1u << S_IMG)) ? kFeatImg : 0u) | (any_lbl ? kFeatLbl : 0u) | (any_ctr_fam ? kFeatCtr : 0u);
   T.il = il;
   T.nlv = nlv;
   T.need = need;

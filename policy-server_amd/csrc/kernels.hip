@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstddef>
 #include <mutex>
 
@@ -130,19 +131,21 @@ __device__ inline uint32_t chain_next(const Chain& c, uint32_t off) { return ((c
 
 __device__ inline uint32_t step(const DfaView& d, uint32_t st, uint32_t byte) { return d.trans[st * d.ncls + d.cls[byte]]; }
 
-// Walk bytes [b, e) with 4-byte aligned loads (pools and staged strings carry a zero tail).
+// Walk bytes [b, e) in 8-byte windows: the window's dwords, then its 8 byte classes load as batches;
+// only the transitions form a dependent chain (aligned dword reads up to 11 bytes past the window
+// start: pools and staged strings carry a zero tail).
 __device__ inline uint32_t feed(const DfaView& d, uint32_t st, const uint8_t* __restrict__ bytes, uint32_t b, uint32_t e) {
-  uint32_t p = b;
-  while (p < e && st != 0) {
-    uint32_t w = *(const uint32_t*)(bytes + (p & ~3u));
-    const uint32_t k = p & 3u;
-    const uint32_t lim = min(4u - k, e - p);
-    w >>= 8u * k;
-    for (uint32_t j = 0; j < lim; ++j) {
-      st = step(d, st, w & 0xffu);
-      w >>= 8;
-    }
-    p += lim;
+  for (uint32_t p = b; p < e && st != 0; p += 8u) {
+    const uint32_t* q = (const uint32_t*)(bytes + (p & ~3u));
+    const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], sh = p & 3u;
+    const uint32_t x0 = align_bytes(q1, q0, sh), x1 = align_bytes(q2, q1, sh);
+    uint32_t c[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) c[i] = d.cls[((i < 4 ? x0 : x1) >> (8 * (i & 3))) & 0xffu];
+    const uint32_t lim = min(8u, e - p);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if ((uint32_t)i < lim) st = d.trans[st * d.ncls + c[i]];
   }
   return st;
 }
@@ -452,12 +455,15 @@ __device__ inline void prefetch_l2(const void* src, uint32_t bytes, uint32_t* sc
 
 // TIMING: the diagnostics instantiation (EvalArgs::phase) — phase clocks add registers, so the
 // product kernel is compiled without them.
-template <bool LDST, bool TIMING>
+template <bool LDST, bool TIMING, uint32_t F>
 __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
     evaluate_tiles_kernel(EvalArgs a, const TileArgs* __restrict__ tp, const TileDesc* __restrict__ desc) {
   // TileArgs lives in device memory: its fields are scalar-loaded where used instead of all being
   // hoisted from the kernarg segment into SGPRs at entry.
   const TileArgs& t = *tp;
+  // families compiled into this instantiation (TileArgs::feat): images / trusted-repos, labels,
+  // container families (pod-privileged, psp-capabilities, psp-apparmor)
+  constexpr bool IMG = (F & kFeatImg) != 0, LBL = (F & kFeatLbl) != 0, CTR = (F & kFeatCtr) != 0;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
@@ -622,13 +628,13 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
     {
       const SlotView sv0 = chunk_view(0);
       const SlotHdr& h0 = *sv0.h;
-      const uint32_t n3 = (need & (1u << S_LK)) ? nl : 0u;
-      const uint32_t n2 = nc;
-      const uint32_t n1 = (need & (1u << S_IMG)) ? nc : 0u;
+      const uint32_t n3 = (LBL && (need & (1u << S_LK))) ? nl : 0u;
+      const uint32_t n2 = CTR ? nc : 0u;
+      const uint32_t n1 = (IMG && (need & (1u << S_IMG))) ? nc : 0u;
       const uint32_t n0 = nr;
       const uint32_t e0 = rup64(n3), e1 = e0 + rup64(n2), e2 = e1 + rup64(n1), e3 = e2 + rup64(n0);
       for (uint32_t w = tid; w < e3; w += kSlotThreads) {
-        if (w < e0) {  // label
+        if (LBL && w < e0) {  // label
           const uint32_t i = w;
           if (i >= n3) continue;
           const uint32_t k = lit(COL_LK, S_LK, i);
@@ -642,7 +648,7 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
             for (uint32_t j = 0; j < nlv; ++j) lv[j] = 0xffffu;
           }
           l_vl[i] = dv_label(sv0, k, lv, nlv);
-        } else if (w < e1) {  // container
+        } else if (CTR && w < e1) {  // container
           const uint32_t i = w - e0;
           if (i >= n2) continue;
           const uint32_t fl = cfl[i];
@@ -663,7 +669,7 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
             for (uint32_t k = l_cdrop[i] - kdb, k1 = l_cdrop[i + 1] - kdb; k < k1; ++k) c_drop[k] = (uint16_t)lit(COL_CAP, S_CAPDROP, k);
           }
           l_vc[i] = v;
-        } else if (w < e2) {  // image reference: one parse feeds the registry, tag and image classes
+        } else if (IMG && w < e2) {  // image reference: one parse feeds the registry, tag and image classes
           const uint32_t i = w - e1;
           if (i >= n1) continue;
           uint16_t* ic = c_img + i * nim;
@@ -676,13 +682,15 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
             for (uint32_t j = 0; j < nim; ++j) ic[j] = 0;
           }
           l_vtr[i] = dv_image(sv0, il, fl, ic);
-        } else {  // request: namespace class, owner maps, bypass
+        } else if (w >= e2) {  // request: namespace class, owner maps, bypass
           const uint32_t i = w - e2;
           if (i >= n0) continue;
           const uint32_t nsc = (need & (1u << S_NS)) ? lit(COL_NS, S_NS, i) : 0u;
           c_ns[i] = (uint16_t)nsc;
-          for (uint32_t c = l_coff[i] - cb, c1 = l_coff[i + 1] - cb; c < c1; ++c) own_c[c] = (uint8_t)i;
-          for (uint32_t l = l_loff[i] - lb, l1 = l_loff[i + 1] - lb; l < l1; ++l) own_l[l] = (uint8_t)i;
+          if (CTR || IMG)
+            for (uint32_t c = l_coff[i] - cb, c1 = l_coff[i + 1] - cb; c < c1; ++c) own_c[c] = (uint8_t)i;
+          if (LBL)
+            for (uint32_t l = l_loff[i] - lb, l1 = l_loff[i + 1] - lb; l < l1; ++l) own_l[l] = (uint8_t)i;
           l_byp[i] = is_bypass(l_rf[i], nsc, t.bypass_cls) ? 1 : 0;
         }
       }
@@ -718,13 +726,13 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
       const SlotHdr& SH = *sv.h;
       if (ck > 0) {
         // ---- D: this chunk's violation sets from the stored classes
-        const uint32_t n3 = SH.lbl ? nl : 0u, n2 = nc, n1 = SH.trs ? nc : 0u;
+        const uint32_t n3 = (LBL && SH.lbl) ? nl : 0u, n2 = CTR ? nc : 0u, n1 = (IMG && SH.trs) ? nc : 0u;
         const uint32_t e0 = rup64(n3), e1 = e0 + rup64(n2), e2 = e1 + rup64(n1), e3 = e2 + rup64(nr);
         for (uint32_t w = tid; w < e3; w += kSlotThreads) {
-          if (w < e0) {
+          if (LBL && w < e0) {
             const uint32_t i = w;
             if (i < n3) l_vl[i] = dv_label(sv, c_lk[i], c_lv + i * nlv, nlv);
-          } else if (w < e1) {
+          } else if (CTR && w < e1) {
             const uint32_t i = w - e0;
             if (i >= n2) continue;
             const uint32_t fl = cfl[i];
@@ -737,10 +745,10 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
                 v |= va;
               }
             l_vc[i] = v;  // (l_vtr is read only by chunks with trusted-repos slots, which rewrite it below)
-          } else if (w < e2) {
+          } else if (IMG && w < e2) {
             const uint32_t i = w - e1;
             if (i < n1) l_vtr[i] = dv_image(sv, il, cfl[i], c_img + i * nim);
-          } else {
+          } else if (w >= e2) {
             const uint32_t i = w - e2;
             if (i < nr) l_rej[i] = l_mut[i] = 0;
           }
@@ -758,9 +766,11 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
       //      (Sequential form of the same walk: slots.hpp walk_*.)
       if (!(t.debug & 2u)) {
         const uint64_t privany = SH.priv[0] | SH.priv[1] | SH.priv[2] | SH.priv[3];
-        const bool ctr_fam = (privany | SH.caps | SH.aa | SH.trs) != 0;
-        const bool trs = SH.trs != 0;
-        const uint32_t n1 = ctr_fam ? nc : 0u, n2 = SH.lbl ? nl : 0u;
+        const bool trs = IMG && SH.trs != 0;
+        const bool ctr_fam = (CTR && (privany | SH.caps | SH.aa) != 0) || trs;
+        const uint32_t n1 = ctr_fam ? nc : 0u, n2 = (LBL && SH.lbl) ? nl : 0u;
+        // a container's violation set: its own families' (V_c) and its image's (V_tr)
+        auto vset = [&](uint32_t j) -> uint64_t { return (CTR ? l_vc[j] : 0ull) | (trs ? l_vtr[j] : 0ull); };
         const uint32_t f0 = rup64(n1), f1 = f0 + rup64(n2), f2 = f1 + rup64(nr);
         for (uint32_t w = tid; w < f2; w += kSlotThreads) {
           if (w < f0) {  // container
@@ -771,22 +781,24 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
             const uint32_t c0 = l_coff[q] - cb;
             uint64_t pre = 0;
             if (!(t.debug & 4096u))
-              for (uint32_t j = c0; j < i; ++j) pre |= trs ? (l_vc[j] | l_vtr[j]) : l_vc[j];
-            const uint64_t nv = (trs ? (l_vc[i] | l_vtr[i]) : l_vc[i]) & ~pre;
+              for (uint32_t j = c0; j < i; ++j) pre |= vset(j);
+            const uint64_t nv = vset(i) & ~pre;
             const uint32_t ci = i - c0;
             uint32_t* vw = l_vw + q * t.vw_stride;
             if (nv) {
               ViolSink vs{vw, nullptr};
-              vs.put(nv & privany, KW_R_PRIVILEGED, ci);
-              vs.put(nv & SH.aa, KW_R_APPARMOR, ci);
-              uint64_t cn = nv & SH.caps;  // capability slots: the first added capability of the list
+              if (CTR) {
+                vs.put(nv & privany, KW_R_PRIVILEGED, ci);
+                vs.put(nv & SH.aa, KW_R_APPARMOR, ci);
+              }
+              uint64_t cn = CTR ? (nv & SH.caps) : 0ull;  // capability slots: the first added capability of the list
               const uint32_t kfirst = l_cadd[c0] - kab;
               for (uint32_t k = l_cadd[i] - kab, k1 = l_cadd[i + 1] - kab; k < k1 && cn; ++k) {
                 const uint64_t nw = l_vadd[k] & cn;
                 vs.put(nw, KW_R_CAP_NOT_ALLOWED, k - kfirst);
                 cn &= ~nw;
               }
-              uint64_t tn = nv & SH.trs;  // trusted-repos slots: reasons in precedence order
+              uint64_t tn = IMG ? (nv & SH.trs) : 0ull;  // trusted-repos slots: reasons in precedence order
               if (tn) {
                 uint64_t why[5];
                 const uint16_t* ic = c_img + i * nim;
@@ -799,14 +811,14 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
               }
               atomicOr((unsigned long long*)&l_rej[q], (unsigned long long)nv);
             }
-            if (SH.caps) {  // mutation: required drops missing, default adds neither added nor dropped
+            if (CTR && SH.caps) {  // mutation: required drops missing, default adds neither added nor dropped
               uint64_t addm = 0, dropm = 0;
               for (uint32_t k = l_cadd[i] - kab, k1 = l_cadd[i + 1] - kab; k < k1; ++k) addm |= bit_of(sv.capmb(c_add[k]));
               for (uint32_t k = l_cdrop[i] - kdb, k1 = l_cdrop[i + 1] - kdb; k < k1; ++k) dropm |= bit_of(sv.capmb(c_drop[k]));
               const uint64_t mut = caps_mutation(sv, addm, dropm);
               if (mut) atomicOr((unsigned long long*)&l_mut[q], (unsigned long long)mut);
             }
-          } else if (w < f1) {  // label
+          } else if (LBL && w < f1) {  // label
             const uint32_t i = w - f0;
             if (i >= n2) continue;
             const uint64_t v = l_vl[i];
@@ -823,7 +835,7 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
             vs.put(nv & den, KW_R_LABEL_DENIED, li);
             vs.put(nv & ~den, KW_R_LABEL_CONSTRAINT, li);
             atomicOr((unsigned long long*)&l_rej[q], (unsigned long long)nv);
-          } else {  // request: namespace, mandatory labels
+          } else if (w >= f1) {  // request: namespace, mandatory labels
             const uint32_t i = w - f1;
             if (i >= nr) continue;
             const uint32_t rf = l_rf[i];
@@ -834,7 +846,7 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
               rej = SH.ns & ~ok;
               vs.put(rej, KW_R_NAMESPACE, 0);
             }
-            if (SH.lbl && SH.mand_union && !(t.debug & 1024u)) {
+            if (LBL && SH.lbl && SH.mand_union && !(t.debug & 1024u)) {
               uint64_t present = 0, lrej = 0;
               for (uint32_t l = l_loff[i] - lb, l1 = l_loff[i + 1] - lb; l < l1; ++l) {
                 present |= bit_of(sv.lkmb(c_lk[l]));
@@ -1126,6 +1138,22 @@ constexpr int kMaxDevices = 64;
 std::once_flag g_attr_once[kMaxDevices];
 hipError_t g_attr_err[kMaxDevices];
 
+// The instantiation of a launch: LDS or global tables, phase clocks (diagnostics), image support
+// (passes whose policies read no image reference run a kernel without that code: fewer registers,
+// a tighter schedule for the rest).
+template <bool LDST, uint32_t... Fs>
+constexpr std::array<const void*, sizeof...(Fs)> tile_fns() {
+  return {(const void*)evaluate_tiles_kernel<LDST, false, Fs>...};
+}
+const void* tile_fn(bool ldst, bool timing, uint32_t feat) {
+  static const auto g = tile_fns<false, 0, 1, 2, 3, 4, 5, 6, 7>();
+  static const auto l = tile_fns<true, 0, 1, 2, 3, 4, 5, 6, 7>();
+  if (timing)  // diagnostics: one instantiation with every family
+    return ldst ? (const void*)evaluate_tiles_kernel<true, true, kFeatAll> : (const void*)evaluate_tiles_kernel<false, true, kFeatAll>;
+  return ldst ? l[feat & kFeatAll] : g[feat & kFeatAll];
+}
+uint32_t tile_feat(const TileArgs& t) { return t.feat & kFeatAll; }
+
 hipError_t ensure_attrs() {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
@@ -1133,11 +1161,10 @@ hipError_t ensure_attrs() {
   if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
   std::call_once(g_attr_once[dev], [dev] {
     // allow > 64 KB of dynamic LDS per workgroup (gfx950: 160 KB per CU)
-    const void* fns[4] = {(const void*)evaluate_tiles_kernel<true, false>, (const void*)evaluate_tiles_kernel<false, false>,
-                          (const void*)evaluate_tiles_kernel<true, true>, (const void*)evaluate_tiles_kernel<false, true>};
     hipError_t e = hipSuccess;
-    for (const void* f : fns) {
-      const hipError_t ek = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    for (int k = 0; k < 18; ++k) {
+      const hipError_t ek = hipFuncSetAttribute(tile_fn(k & 1, k >= 16, (uint32_t)(k >> 1) & kFeatAll),
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e == hipSuccess) e = ek;
     }
     g_attr_err[dev] = e;
@@ -1157,11 +1184,10 @@ hipError_t launch_evaluate_tiles(const EvalArgs& a, const TileArgs& t, const Til
     thread_local int c_dev = -1, c_ncu = 0, c_occ = 0;
     thread_local uint64_t c_key = ~0ull;
     int dev = 0;
-    const uint64_t key = ((uint64_t)t.lds_bytes << 2) | (t.lds_tables ? 1u : 0u) | (a.phase ? 2u : 0u);
+    const uint64_t key = ((uint64_t)t.lds_bytes << 8) | ((uint64_t)tile_feat(t) << 2) | (a.phase ? 2u : 0u) | (t.lds_tables ? 1u : 0u);
     if (hipGetDevice(&dev) == hipSuccess && (dev != c_dev || key != c_key)) {
       int ncu = 0, occ = 0;
-      const void* fn = a.phase ? (t.lds_tables ? (const void*)evaluate_tiles_kernel<true, true> : (const void*)evaluate_tiles_kernel<false, true>)
-                               : (t.lds_tables ? (const void*)evaluate_tiles_kernel<true, false> : (const void*)evaluate_tiles_kernel<false, false>);
+      const void* fn = tile_fn(t.lds_tables != 0, a.phase != nullptr, tile_feat(t));
       if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
           hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kSlotThreads, t.lds_bytes) != hipSuccess)
         ncu = occ = 0;
@@ -1174,12 +1200,9 @@ hipError_t launch_evaluate_tiles(const EvalArgs& a, const TileArgs& t, const Til
     if (t.debug & 256u)
       fprintf(stderr, "[kw tile] launch grid=%u occupancy=%d wg/cu x %d CUs lds=%u\n", grid, c_occ, c_ncu, t.lds_bytes);
   }
-  if (t.lds_tables)
-    if (a.phase) hipLaunchKernelGGL((evaluate_tiles_kernel<true, true>), dim3(grid), dim3(kSlotThreads), t.lds_bytes, s, a, d_t, d_desc);
-    else hipLaunchKernelGGL((evaluate_tiles_kernel<true, false>), dim3(grid), dim3(kSlotThreads), t.lds_bytes, s, a, d_t, d_desc);
-  else
-    if (a.phase) hipLaunchKernelGGL((evaluate_tiles_kernel<false, true>), dim3(grid), dim3(kSlotThreads), t.lds_bytes, s, a, d_t, d_desc);
-    else hipLaunchKernelGGL((evaluate_tiles_kernel<false, false>), dim3(grid), dim3(kSlotThreads), t.lds_bytes, s, a, d_t, d_desc);
+  using TileFn = void (*)(EvalArgs, const TileArgs*, const TileDesc*);
+  const TileFn fn = (TileFn)tile_fn(t.lds_tables != 0, a.phase != nullptr, tile_feat(t));
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(kSlotThreads), t.lds_bytes, s, a, d_t, d_desc);
   return hipGetLastError();
 }
 

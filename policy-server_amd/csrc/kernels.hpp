@@ -54,6 +54,8 @@ constexpr uint32_t kSlotRows = 64;
 #define KW_THREADS 256
 #endif
 constexpr uint32_t kSlotThreads = KW_THREADS;
+// Families a tile-kernel instantiation carries (TileArgs::feat).
+constexpr uint32_t kFeatImg = 1, kFeatLbl = 2, kFeatCtr = 4, kFeatAll = 7;
 constexpr uint32_t kMaxChunks = 8;  // chunks of one launch (<= 512 slots); longer lists take several launches
 
 struct ChunkArgs {
@@ -80,6 +82,7 @@ struct TileArgs {
   uint32_t o_nx;                       // u32[3]: next tile index (dynamic schedule), double-buffered; [2]: prefetch
   uint32_t o_pf;                       // 256 B: LDS-DMA landing of the L2 prefetch (never read)
   uint32_t prefetch;                   // warm L2 with the next tile (small tiles at >= 3 workgroups per CU)
+  uint32_t feat;                       // kFeat* families of the launch (selects the kernel instantiation)
   uint32_t o_sa;                       // u32[NSTR]: the tile's staged byte start per string column
   uint32_t o_vw, vw_stride;            // violation words [rows][vw_stride] (aliases the staged strings)
   uint32_t o_so[NSTR], o_sb[NSTR], sb_cap[NSTR];  // staged string offsets / bytes (0 = not staged)
