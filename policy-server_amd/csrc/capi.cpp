@@ -564,7 +564,10 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
   // next-tile L2 prefetch: a gain where several small tiles share a CU (C4: -2.5 %), a loss where two
   // large ones do (C5: +2.7 %; r02 A/B)
   T.prefetch = per_cu(T.lds_bytes) >= 3 ? 1u : 0u;
-  T.feat = ((need & (1u << S_IMG)) ? kFeatImg : 0u) | (any_lbl ? kFeatLbl : 0u) | (any_ctr_fam ? kFeatCtr : 0u);
+  bool any_grp = false;
+  for (const SlotChunk& c : plan->chunks) any_grp = any_grp || c.groups;
+  T.feat = ((need & (1u << S_IMG)) ? kFeatImg : 0u) | (any_lbl ? kFeatLbl : 0u) | (any_ctr_fam ? kFeatCtr : 0u) |
+           (any_grp ? kFeatGrp : 0u);
   T.il = il;
   T.nlv = nlv;
   T.need = need;

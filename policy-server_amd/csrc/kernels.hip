@@ -462,8 +462,8 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
   // hoisted from the kernarg segment into SGPRs at entry.
   const TileArgs& t = *tp;
   // families compiled into this instantiation (TileArgs::feat): images / trusted-repos, labels,
-  // container families (pod-privileged, psp-capabilities, psp-apparmor)
-  constexpr bool IMG = (F & kFeatImg) != 0, LBL = (F & kFeatLbl) != 0, CTR = (F & kFeatCtr) != 0;
+  // container families (pod-privileged, psp-capabilities, psp-apparmor), group columns
+  constexpr bool IMG = (F & kFeatImg) != 0, LBL = (F & kFeatLbl) != 0, CTR = (F & kFeatCtr) != 0, GRP = (F & kFeatGrp) != 0;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
@@ -908,6 +908,12 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
         const ColInfo* cols = (const ColInfo*)(CA.rec + SH.o_cols);
         const uint32_t ncols = CA.ncols;
         auto word = [&](uint32_t rr, uint32_t j) -> uint32_t {
+          if (!GRP) {  // no group column in this launch: plain or constant columns only
+            const ColInfo& ci = cols[j];
+            if (ci.kind != CK_PLAIN) return ci.okw;
+            if ((l_rej[rr] >> ci.slot) & 1ull) return ci.rejb | l_vw[rr * t.vw_stride + ci.slot];
+            return ((l_mut[rr] >> ci.slot) & 1ull) ? ci.mutw : ci.okw;
+          }
           uint64_t wide = 0;
           const uint32_t w = column_word(cols[j], l_rej[rr], l_mut[rr], init, l_vw + rr * t.vw_stride, CA.rec, &wide);
           if (cols[j].wide != ~0u && KW_REASON(w) == KW_R_GROUP) a.wide_groups[(r0 + rr) * a.nwide + cols[j].wide] = wide;
@@ -934,7 +940,7 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
               const uint4 ks = *(const uint4*)(cs + 4 * g), ok = *(const uint4*)(cs + cs_n + 4 * g),
                           mu = *(const uint4*)(cs + 2 * cs_n + 4 * g), rj = *(const uint4*)(cs + 3 * cs_n + 4 * g);
               auto pw = [&](uint32_t k, uint32_t okw, uint32_t mutw, uint32_t rejb, uint32_t j) -> uint32_t {
-                if ((k & 0xffu) != CK_PLAIN) return word(rr, j);
+                if ((k & 0xffu) != CK_PLAIN) return GRP ? word(rr, j) : okw;  // (no group: a constant column)
                 const uint32_t s = k >> 8;
                 if ((rej >> s) & 1ull) return rejb | vw[s];
                 return ((mut >> s) & 1ull) ? mutw : okw;
@@ -1146,8 +1152,8 @@ constexpr std::array<const void*, sizeof...(Fs)> tile_fns() {
   return {(const void*)evaluate_tiles_kernel<LDST, false, Fs>...};
 }
 const void* tile_fn(bool ldst, bool timing, uint32_t feat) {
-  static const auto g = tile_fns<false, 0, 1, 2, 3, 4, 5, 6, 7>();
-  static const auto l = tile_fns<true, 0, 1, 2, 3, 4, 5, 6, 7>();
+  static const auto g = tile_fns<false, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15>();
+  static const auto l = tile_fns<true, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15>();
   if (timing)  // diagnostics: one instantiation with every family
     return ldst ? (const void*)evaluate_tiles_kernel<true, true, kFeatAll> : (const void*)evaluate_tiles_kernel<false, true, kFeatAll>;
   return ldst ? l[feat & kFeatAll] : g[feat & kFeatAll];
@@ -1162,8 +1168,8 @@ hipError_t ensure_attrs() {
   std::call_once(g_attr_once[dev], [dev] {
     // allow > 64 KB of dynamic LDS per workgroup (gfx950: 160 KB per CU)
     hipError_t e = hipSuccess;
-    for (int k = 0; k < 18; ++k) {
-      const hipError_t ek = hipFuncSetAttribute(tile_fn(k & 1, k >= 16, (uint32_t)(k >> 1) & kFeatAll),
+    for (int k = 0; k < 34; ++k) {
+      const hipError_t ek = hipFuncSetAttribute(tile_fn(k & 1, k >= 32, (uint32_t)(k >> 1) & kFeatAll),
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e == hipSuccess) e = ek;
     }

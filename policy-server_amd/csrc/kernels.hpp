@@ -55,7 +55,7 @@ constexpr uint32_t kSlotRows = 64;
 #endif
 constexpr uint32_t kSlotThreads = KW_THREADS;
 // Families a tile-kernel instantiation carries (TileArgs::feat).
-constexpr uint32_t kFeatImg = 1, kFeatLbl = 2, kFeatCtr = 4, kFeatAll = 7;
+constexpr uint32_t kFeatImg = 1, kFeatLbl = 2, kFeatCtr = 4, kFeatGrp = 8, kFeatAll = 15;
 constexpr uint32_t kMaxChunks = 8;  // chunks of one launch (<= 512 slots); longer lists take several launches
 
 struct ChunkArgs {
