@@ -214,13 +214,17 @@ def host_modes(env, ids, syn, device, args):
     fl = {}
     for th in sorted({1, threads}):
         os.environ["KW_FLATTEN_THREADS"] = str(th)
-        h, bad, err = C.c_void_p(), C.c_int64(-1), C.create_string_buffer(512)
-        t = time.perf_counter()
-        rc = L.kw_batch_from_json(arr, lens, n, K._native.KW_DOC_ADMISSION_REVIEW, C.byref(h), C.byref(bad), err,
-                                  len(err))
-        fl[str(th)] = n / (time.perf_counter() - t)
-        if rc == 0:
-            L.kw_batch_destroy(h)
+        best = None
+        for _ in range(3):  # best of three calls (the first also warms the flattener's per-thread buffers)
+            h, bad, err = C.c_void_p(), C.c_int64(-1), C.create_string_buffer(512)
+            t = time.perf_counter()
+            rc = L.kw_batch_from_json(arr, lens, n, K._native.KW_DOC_ADMISSION_REVIEW, C.byref(h), C.byref(bad), err,
+                                      len(err))
+            dt = time.perf_counter() - t
+            best = dt if best is None else min(best, dt)
+            if rc == 0:
+                L.kw_batch_destroy(h)
+        fl[str(th)] = n / best
     os.environ.pop("KW_FLATTEN_THREADS", None)
     out["flatten"] = {"unit": "requests/s", "by_threads": fl, "rows": n, "mean_doc_bytes": nbytes / n,
                       "what": "kw_batch_from_json: AdmissionReview JSON -> SoA columns"}

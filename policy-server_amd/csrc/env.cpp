@@ -527,7 +527,7 @@ size_t emit_dfa(const Dfa& dfa, const std::vector<uint32_t>& cls_map, std::vecto
 }
 
 constexpr size_t kDfaTableBudget = 64 * 1024;  // per DFA of a column chain
-constexpr size_t kKvDfaBudget = 3072;   // per DFA of a label key's value chain (its region is staged per workgroup: occupancy)     // per DFA of a label key's value chain     // per DFA of a label key's value chain     // per DFA of a label key's value chain     // per DFA of a label key's value chain     // per DFA of a label key's value chain
+constexpr size_t kKvDfaBudget = 3072;  // per DFA of a label key's value chain (its region is staged per workgroup: occupancy)
 
 // Compiles one column (ColumnInfo.pats) into its blob records: the literal table over the literal
 // patterns (COL_IMG: none, its strings are constructed), then the DFA chain over the rest.
