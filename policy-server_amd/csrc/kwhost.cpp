@@ -30,7 +30,7 @@
 //   unknown route                        404  (empty)
 //
 // Usage: kwhost --policies policies.yml [--addr 127.0.0.1] [--port 3000] [--device 0]
-//   [--max-batch 512] [--max-wait-us 200] [--workers 2] [--max-body-bytes 2097152]
+//   [--max-batch 512] [--max-wait-us 200] [--workers 4] [--max-body-bytes 2097152]
 //   [--always-accept-admission-reviews-on-namespace NS] [--continue-on-errors] [--no-device]
 // --policies is the reference's policies.yml (read with the native YAML reader, config.rs:449-453;
 // a file whose first character is '{' is read as JSON). --no-device serves the HTTP layer without
@@ -53,7 +53,7 @@
 #include <deque>
 #include <fstream>
 #include <mutex>
-#include <sstream>
+#include <string_view>
 #include <string>
 #include <thread>
 #include <vector>
@@ -64,7 +64,7 @@ namespace {
 
 struct Opts {
   std::string policies, addr = "127.0.0.1", always_ns;
-  int port = 3000, device = 0, max_batch = 512, max_wait_us = 200, workers = 2;
+  int port = 3000, device = 0, max_batch = 512, max_wait_us = 200, workers = 4;
   size_t max_body = 2u << 20;  // axum DefaultBodyLimit (2 MiB)
   bool continue_on_errors = false, no_device = false;
 };
@@ -419,18 +419,25 @@ void serve(Server* srv, int fd) {
         return;
       }
     }
-    std::istringstream hs(c.in.substr(0, he));
-    std::string line, method, target, version;
-    std::getline(hs, line);
-    std::istringstream rl(line);
-    rl >> method >> target >> version;
+    // request line and headers, parsed in place (no stream objects per request)
+    const std::string_view head(c.in.data(), he);
+    size_t le = head.find("\r\n");
+    const std::string_view rline = head.substr(0, le);
+    const size_t s1 = rline.find(' '), s2 = s1 == std::string_view::npos ? s1 : rline.find(' ', s1 + 1);
+    const std::string method(rline.substr(0, s1));
+    const std::string target(s1 == std::string_view::npos ? std::string_view() : rline.substr(s1 + 1, s2 - s1 - 1));
+    const std::string version(s2 == std::string_view::npos ? std::string_view() : rline.substr(s2 + 1));
     std::string ctype;
     long long clen = -1;
     bool chunked = false, keep = version != "HTTP/1.0";
-    while (std::getline(hs, line)) {
+    for (size_t at = le == std::string_view::npos ? head.size() : le + 2; at < head.size();) {
+      size_t end = head.find("\r\n", at);
+      if (end == std::string_view::npos) end = head.size();
+      const std::string_view line = head.substr(at, end - at);
+      at = end + 2;
       const size_t colon = line.find(':');
-      if (colon == std::string::npos) continue;
-      const std::string k = lower(trim(line.substr(0, colon))), v = trim(line.substr(colon + 1));
+      if (colon == std::string_view::npos) continue;
+      const std::string k = lower(trim(std::string(line.substr(0, colon)))), v = trim(std::string(line.substr(colon + 1)));
       if (k == "content-length") clen = atoll(v.c_str());
       else if (k == "content-type") ctype = lower(v);
       else if (k == "transfer-encoding") chunked = lower(v).find("chunked") != std::string::npos;

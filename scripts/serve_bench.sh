@@ -13,7 +13,7 @@ SCFG=${4:-4}
 CONNS=${CONNS:-"16 64 256"}
 DURATION=${DURATION:-8}
 WARMUP=${WARMUP:-2}
-WORKERS=${WORKERS:-2}
+WORKERS=${WORKERS:-4}
 MAXB=${MAXB:-512}
 WAIT=${WAIT:-200}
 PORT=$((20000 + RANDOM % 20000))
