@@ -81,6 +81,23 @@ BlockPool& host_pool() {
   return *p;
 }
 
+// Host copy spread over up to 16 threads for large buffers (staging fills and verdict read-back:
+// one thread moves ≈ 10 GB/s, the host's memory system several times that).
+void parallel_copy(void* dst, const void* src, size_t bytes) {
+  constexpr size_t kMin = (size_t)8 << 20;
+  if (bytes < kMin) {
+    memcpy(dst, src, bytes);
+    return;
+  }
+  const size_t nt = std::min<size_t>(16, std::max<size_t>(1, std::min<size_t>(std::thread::hardware_concurrency(), bytes / (kMin / 2))));
+  std::vector<std::thread> th;
+  for (size_t t = 0; t < nt; ++t) {
+    const size_t a = bytes * t / nt, e = bytes * (t + 1) / nt;
+    th.emplace_back([=] { memcpy((uint8_t*)dst + a, (const uint8_t*)src + a, e - a); });
+  }
+  for (auto& x : th) x.join();
+}
+
 // Requests per tile of the tile kernel: kSlotRows, or KW_SLOT_ROWS (8..255, A/B knob) when set.
 uint32_t slot_rows() {
   static const uint32_t r = [] {
@@ -1349,7 +1366,7 @@ int upload_batch(kw_batch* kb, int device, hipStream_t stream, bool sync) {
   D->staging_bytes = total;
   uint8_t* st = (uint8_t*)D->staging;
   for (auto& p : pieces)
-    if (p.bytes) memcpy(st + p.at, p.src, p.bytes);
+    if (p.bytes) parallel_copy(st + p.at, p.src, p.bytes);
   HIPCHK(hipMemcpyAsync(D->cols, st, total, hipMemcpyHostToDevice, D->stream));
   if (sync) HIPCHK(hipStreamSynchronize(D->stream));
   D->cur = D->stream;
@@ -1422,7 +1439,23 @@ int kw_batch_verdicts(kw_batch* b, uint32_t* host_out, size_t count) {
   if (count > D.last_verdicts) return KW_E_ARG;
   HIPCHK(hipSetDevice(D.device));
   hipStream_t s = D.cur ? D.cur : D.stream;
-  if (count) HIPCHK(hipMemcpyAsync(host_out, D.verdicts, count * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  const size_t vbytes = count * sizeof(uint32_t);
+  constexpr size_t kBounce = (size_t)64 << 20;
+  if (vbytes > ((size_t)16 << 20)) {
+    // large read-backs through a pinned bounce block (full-rate DMA), fanned out to the caller's
+    // (pageable) buffer by several threads
+    void* bounce = nullptr;
+    HIPCHK(host_pool().alloc(D.device, kBounce, &bounce));
+    for (size_t at = 0; at < vbytes; at += kBounce) {
+      const size_t n = std::min(kBounce, vbytes - at);
+      HIPCHK(hipMemcpyAsync(bounce, (const uint8_t*)D.verdicts + at, n, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      parallel_copy((uint8_t*)host_out + at, bounce, n);
+    }
+    host_pool().release(D.device, bounce, kBounce);
+  } else if (count) {
+    HIPCHK(hipMemcpyAsync(host_out, D.verdicts, vbytes, hipMemcpyDeviceToHost, s));
+  }
   // side data of the pass: entity indices >= 65535 and > 15-member group causes (kernels.hpp WideRec)
   WideData& W = b->b.wide;
   W.clear();
