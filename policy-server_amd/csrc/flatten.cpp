@@ -302,6 +302,7 @@ bool batch_from_soa(const kw_soa& s, Batch* b, std::string* err) {
     uint32_t base = c.off[0];
     if (base != 0)
       for (auto& x : o->off) x -= base;
+    o->bytes.reserve((size_t)(c.off[c.n] - base) + 32);  // room for the device padding (finalize)
     o->bytes.assign(c.bytes + base, c.bytes + c.off[c.n]);
   };
   uint64_t n = s.n_requests;

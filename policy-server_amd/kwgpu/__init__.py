@@ -329,11 +329,15 @@ class Batch:
         raise_for(rc, "kw_validate_rows failed")
         self._npol = 1
 
-    def verdicts(self, count=None):
+    def verdicts(self, count=None, out=None):
+        """The last pass's verdict words (kw_batch_verdicts); `out`: a reused uint32 array to fill."""
         import numpy as np
         if count is None:
-            count = self.n * self._npol
-        out = np.zeros(count, dtype=np.uint32)
+            count = self.n * self._npol if out is None else out.size
+        if out is None:
+            out = np.zeros(count, dtype=np.uint32)
+        elif out.dtype != np.uint32 or not out.flags.c_contiguous or out.size < count:
+            raise ValueError("out must be a contiguous uint32 array of at least count words")
         rc = self._L.kw_batch_verdicts(self._h, out.ctypes.data_as(C.POINTER(C.c_uint32)), count)
         raise_for(rc, "kw_batch_verdicts failed")
         return out
