@@ -382,9 +382,15 @@ typedef struct {
    integration_test.rs:247-250); evaluation is lazy, as rhai evaluates || and && */
 static int gcall(gctx *g, int32_t slot) {
   if (!g->done[slot]) {
-    fam_out fo = eval_family(g->e, g->G->members[slot], g->S, g->r, g->zb);
     g->done[slot] = 1;
-    g->ok[slot] = fo.reason == 0 && !fo.mutated;
+    if (g->e->pol[g->G->members[slot]].init_error) {
+      /* a member that failed to initialise never accepts (a cause when evaluated); the response
+         layer answers such a group with PolicyNotFound for that member (oracle.py) */
+      g->ok[slot] = 0;
+    } else {
+      fam_out fo = eval_family(g->e, g->G->members[slot], g->S, g->r, g->zb);
+      g->ok[slot] = fo.reason == 0 && !fo.mutated;
+    }
   }
   return g->ok[slot];
 }

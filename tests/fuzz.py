@@ -1,0 +1,133 @@
+"""Random policy sets for differential tests (product vs oracle): every declarative family with
+settings drawn from the synthetic workload's vocabularies (so that entities match and miss),
+random modes and allowedToMutate, groups with random boolean expressions over 2-6 members, and
+now and then a setting the schema rejects (an init-error row under continue_on_errors)."""
+import random
+
+CAPS = ["NET_ADMIN", "SYS_TIME", "SYS_ADMIN", "NET_RAW", "CHOWN", "KILL", "SETUID", "SETGID", "DAC_OVERRIDE",
+        "FOWNER", "MKNOD", "AUDIT_WRITE", "SYS_PTRACE", "NET_BIND_SERVICE", "ALL"]
+PROFILES = ["runtime/default", "unconfined"] + [f"localhost/p{i}" for i in range(10)] + ["localhost/*", "runtime/*"]
+KEYS = ["app", "tier", "env", "team", "owner", "version", "release", "component", "part-of", "managed-by",
+        "app.kubernetes.io/name", "app.kubernetes.io/version", "app.kubernetes.io/managed-by", "cost-center",
+        "region", "zone", "critical", "debug", "experimental", "legacy", "pci"]
+REGEXES = ["^[a-z0-9-]+$", "^v[0-9]+(\\.[0-9]+)*", "^(dev|staging|prod)$", "^team-[a-z]+$", "[0-9]{3,}",
+           "^(true|false)$", "^[a-z]{1,8}$", "^(eu|us)-(west|east)-[0-9]$", "^(frontend|backend|db|cache|web)$",
+           "^[A-Za-z0-9_.-]{1,63}$", "payments|web", "^x$", "a", "^$", "\\d+", "[[:alpha:]]+_"]
+REGISTRIES = ["docker.io", "ghcr.io", "quay.io", "registry.k8s.io", "gcr.io", "my-corp.example:5000", "*.io", "gcr.[i]o",
+              "my-corp.example:*", "q*", "reg-1?0.example.com"]
+TAGS = ["latest", "0.*", "*.1[0-9].*", "1.*", "*-rc*", "[0-3].*.*"]
+IMAGES = ["docker.io/library/*", "ghcr.io/*", "*/a?c*", "quay.io/[!x]*", "*@sha256:*", "docker.io/library/*:latest",
+          "*/*/*", "gcr.io/*:*"]
+NAMESPACES = ["kubewarden", "kubewarden-approved"] + [f"ns-{i:03d}" for i in range(0, 40, 3)]
+MOD = {
+    "caps": "registry://ghcr.io/kubewarden/policies/psp-capabilities:v0.1.7",
+    "aa": "registry://ghcr.io/kubewarden/policies/psp-apparmor:v0.1.7",
+    "labels": "registry://ghcr.io/kubewarden/policies/safe-labels:v0.1.14",
+    "trusted": "registry://ghcr.io/kubewarden/policies/trusted-repos-policy:v0.1.12",
+    "ns": "file:///tmp/namespace-validate-policy.wasm",
+    "priv": "registry://ghcr.io/kubewarden/tests/pod-privileged:v0.2.1",
+}
+
+
+def _sample(rng, pool, lo, hi):
+    return rng.sample(pool, rng.randint(lo, min(hi, len(pool))))
+
+
+def _settings(rng, fam):
+    bad = rng.random() < 0.04  # a setting the schema or the compiler rejects
+    if fam == "caps":
+        s = {"allowed_capabilities": ["*"] if rng.random() < 0.1 else _sample(rng, CAPS[:-1], 1, 8)}
+        if rng.random() < 0.5:
+            s["required_drop_capabilities"] = _sample(rng, CAPS, 1, 3)
+        if rng.random() < 0.3:
+            s["default_add_capabilities"] = _sample(rng, CAPS[:-1], 1, 2)
+        if bad:
+            s["allowed_capabilities"] = "NET_ADMIN"  # not a list
+        return s
+    if fam == "aa":
+        s = {"allowed_profiles": _sample(rng, PROFILES, 0, 5)}
+        if bad:
+            s["unknown_field"] = True
+        return s
+    if fam == "labels":
+        keys = rng.sample(KEYS, 6)
+        s = {}
+        if rng.random() < 0.7:
+            s["denied_labels"] = keys[:rng.randint(1, 2)]
+        if rng.random() < 0.6:
+            s["mandatory_labels"] = keys[2:2 + rng.randint(1, 2)]
+        if rng.random() < 0.8:
+            s["constrained_labels"] = {k: rng.choice(REGEXES) for k in keys[4:4 + rng.randint(1, 2)]}
+        if bad:
+            s["constrained_labels"] = {keys[5]: "(unclosed"}
+        return s
+    if fam == "trusted":
+        s = {}
+        reg = rng.random()
+        if reg < 0.35:
+            s["registries"] = {"allow": _sample(rng, REGISTRIES, 1, 4)}
+        elif reg < 0.6:
+            s["registries"] = {"reject": _sample(rng, REGISTRIES, 1, 3)}
+        if rng.random() < 0.5:
+            s["tags"] = {"reject": _sample(rng, TAGS, 1, 3)}
+        img = rng.random()
+        if img < 0.25:
+            s["images"] = {"allow": _sample(rng, IMAGES, 1, 3)}
+        elif img < 0.45:
+            s["images"] = {"reject": _sample(rng, IMAGES, 1, 3)}
+        if bad:
+            s["registries"] = {"allow": ["a"], "reject": ["b"]}
+        return s
+    if fam == "ns":
+        return {"valid_namespace": "" if bad else rng.choice(NAMESPACES)}
+    if fam == "priv":
+        s = {}
+        if rng.random() < 0.5:
+            s["skip_init_containers"] = rng.random() < 0.5
+        if rng.random() < 0.5:
+            s["skip_ephemeral_containers"] = rng.random() < 0.5
+        return s
+    raise ValueError(fam)
+
+
+def _expr(rng, names, depth):
+    r = rng.random()
+    if depth <= 0 or r < 0.3:
+        if rng.random() < 0.06:
+            return rng.choice(["true", "false"])
+        return f"{rng.choice(names)}()"
+    if r < 0.42:
+        return f"!({_expr(rng, names, depth - 1)})"
+    op = rng.choice(["&&", "||", "&&", "||", "==", "!="])
+    a, b = _expr(rng, names, depth - 1), _expr(rng, names, depth - 1)
+    return f"({a} {op} {b})" if rng.random() < 0.6 else f"{a} {op} {b}"
+
+
+def random_policies(seed, n=None):
+    """A policies document (dict) of `n` (default 20-90) plain policies and 1-3 groups."""
+    rng = random.Random(seed)
+    n = n or rng.randint(20, 90)
+    fams = ["caps", "aa", "labels", "trusted", "ns", "priv"]
+    doc = {}
+    for i in range(n):
+        fam = rng.choice(fams)
+        e = {"module": MOD[fam]}
+        if fam != "priv" or rng.random() < 0.7:
+            e["settings"] = _settings(rng, fam)
+        if rng.random() < 0.25:
+            e["policyMode"] = "monitor"
+        if fam == "caps" and rng.random() < 0.5:
+            e["allowedToMutate"] = rng.random() < 0.5
+        doc[f"p{i:03d}-{fam}"] = e
+    for g in range(rng.randint(1, 3)):
+        m = rng.randint(2, 6)
+        names = [f"m{j}" for j in range(m)]
+        members = {}
+        for nm in names:
+            fam = rng.choice(fams)
+            members[nm] = {"module": MOD[fam], "settings": _settings(rng, fam)}
+        e = {"policies": members, "expression": _expr(rng, names, 3), "message": f"group {g} rejected"}
+        if rng.random() < 0.25:
+            e["policyMode"] = "monitor"
+        doc[f"group-{g}"] = e
+    return doc
