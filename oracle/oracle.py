@@ -72,6 +72,126 @@ def podspec(doc_obj):
     return (spec, ptr) if isinstance(spec, dict) else (None, None)
 
 
+# ----------------------------------------------------------------------------- document -> row
+class _Obj(list):
+    """A JSON object as its member list in document order (duplicate keys kept, as the product's
+    tape keeps them); get() answers the last occurrence, as serde does."""
+
+    def get(self, k, default=None):
+        for key, v in reversed(self):
+            if key == k:
+                return v
+        return default
+
+
+def _loads_pairs(text):
+    return json.loads(text, object_pairs_hook=_Obj)
+
+
+_AA_PREFIX = "container.apparmor.security.beta.kubernetes.io/"
+# include/kwgpu.h KW_CTR_* / KW_REQ_*
+_CTR_PRIVILEGED, _CTR_INIT, _CTR_EPHEMERAL, _CTR_HAS_IMAGE, _CTR_HAS_APPARMOR = 1, 2, 4, 8, 16
+_REQ_RAW, _REQ_HAS_NAMESPACE, _REQ_HAS_PODSPEC, _REQ_HAS_OBJECT = 1, 2, 4, 8
+
+
+def flatten_doc(text, raw=False):
+    """The columns of one AdmissionReview / RawReview body (the extraction rules of
+    SURVEY a15/a16), restated from the JSON value itself, independently of the product's parser:
+    {"flags", "uid", "ns", "op", "kind", "containers": [(flags, name, image, aa, adds, drops)],
+    "labels": [(key, value)]}, or None when the body is not a request of that type (the product
+    answers 400 / 422; the exact rejection texts are pinned elsewhere)."""
+    try:
+        d = _loads_pairs(text)
+    except (ValueError, RecursionError):
+        return None
+    if not isinstance(d, _Obj) or d.get("request", _Obj) is _Obj:
+        return None
+    req = d.get("request")
+    is_str = lambda v: isinstance(v, str)
+    if not raw:
+        for k in ("kind", "apiVersion"):
+            if d.get(k) is not None and not is_str(d.get(k)):
+                return None
+        if not isinstance(req, _Obj):
+            return None
+        for k, fields in (("uid", None), ("kind", ("group", "version", "kind")), ("resource", ("group", "version", "resource")),
+                          ("operation", None)):
+            v = req.get(k, _Obj)
+            if v is _Obj:
+                return None
+            if fields is None and not is_str(v):
+                return None
+            if fields is not None and (not isinstance(v, _Obj) or any(not is_str(v.get(f)) for f in fields)):
+                return None
+        if not isinstance(req.get("userInfo"), _Obj):
+            return None
+        for k in ("namespace", "name", "subResource", "requestSubResource"):
+            if req.get(k) is not None and not is_str(req.get(k)):
+                return None
+    r = req if isinstance(req, _Obj) else _Obj()
+    sv = lambda v: v if is_str(v) else ""
+    flags = _REQ_RAW if raw else 0
+    if is_str(r.get("namespace")):
+        flags |= _REQ_HAS_NAMESPACE
+    rk = r.get("kind")
+    rkind = sv(rk.get("kind")) if isinstance(rk, _Obj) else ""
+    row = {"uid": sv(r.get("uid")), "ns": sv(r.get("namespace")), "op": sv(r.get("operation")), "kind": rkind,
+           "containers": [], "labels": []}
+    obj = r.get("object")
+
+    def walk(o, keys):
+        for k in keys:
+            if not isinstance(o, _Obj):
+                return None
+            o = o.get(k)
+        return o
+    if isinstance(obj, _Obj):
+        flags |= _REQ_HAS_OBJECT
+        kind = obj.get("kind") if is_str(obj.get("kind")) else rkind
+        spec = meta = None
+        if kind == "Pod":
+            spec, meta = obj.get("spec"), obj.get("metadata")
+        elif kind in _WORKLOADS:
+            spec, meta = walk(obj, ["spec", "template", "spec"]), walk(obj, ["spec", "template", "metadata"])
+        elif kind == "CronJob":
+            spec = walk(obj, ["spec", "jobTemplate", "spec", "template", "spec"])
+            meta = walk(obj, ["spec", "jobTemplate", "spec", "template", "metadata"])
+        if isinstance(spec, _Obj):
+            flags |= _REQ_HAS_PODSPEC
+            ann = meta.get("annotations") if isinstance(meta, _Obj) else None
+            for lst, kf in (("containers", 0), ("initContainers", _CTR_INIT), ("ephemeralContainers", _CTR_EPHEMERAL)):
+                items = spec.get(lst)
+                if not isinstance(items, list) or isinstance(items, _Obj):
+                    continue
+                for c in items:
+                    if not isinstance(c, _Obj):
+                        continue
+                    cf = kf
+                    name, image = sv(c.get("name")), c.get("image")
+                    if is_str(image):
+                        cf |= _CTR_HAS_IMAGE
+                    sc = c.get("securityContext")
+                    if isinstance(sc, _Obj) and sc.get("privileged") is True:
+                        cf |= _CTR_PRIVILEGED
+                    caps = sc.get("capabilities") if isinstance(sc, _Obj) else None
+
+                    def cap_list(k):
+                        v = caps.get(k) if isinstance(caps, _Obj) else None
+                        return [x for x in v if is_str(x)] if isinstance(v, list) and not isinstance(v, _Obj) else []
+                    profile = ""
+                    if isinstance(ann, _Obj):
+                        for k, v in ann:
+                            if k == _AA_PREFIX + name and is_str(v):
+                                profile = v
+                                cf |= _CTR_HAS_APPARMOR
+                    row["containers"].append((cf, name, sv(image), profile, cap_list("add"), cap_list("drop")))
+        labels = walk(obj, ["metadata", "labels"])
+        if isinstance(labels, _Obj):
+            row["labels"] = [(k, v) for k, v in labels if is_str(v)]
+    row["flags"] = flags
+    return row
+
+
 def capabilities_patch(required_drops, default_adds, doc):
     """RFC 6902 ops of the psp-capabilities mutation: per container of containers,
     initContainers, ephemeralContainers (JSON array index), the required drops it does not drop
