@@ -34,3 +34,32 @@ def test_random_policy_sets_on_gpu(seed):
     rows = b.verdicts(count=syn.n)
     full = want.reshape(syn.n, len(ids))
     assert np.array_equal(rows, full[np.arange(syn.n), pick])
+
+
+@pytest.mark.parametrize("raw", [False, True])
+def test_odd_documents_on_gpu(raw):
+    """Randomly shaped documents (tests/test_flatten_fuzz.py: mistyped and missing members, escapes,
+    duplicate keys) through the flattener and the HIP path: all-pairs words equal the oracle's on the
+    same rows in both origins, and for AdmissionReviews every response of a row sample (JSONPatches of
+    odd securityContexts included) equals the oracle's, derived from the document itself."""
+    import random
+
+    from helpers import config
+    from test_flatten_fuzz import _doc
+    from test_parity_gpu import _check_responses
+    doc = config("parity")
+    env = K.EvaluationEnvironment(doc, continue_on_errors=True, always_accept_namespace=NS, device=0)
+    oe = O.OracleEnv(doc, continue_on_errors=True, always_accept_namespace=NS)
+    ids = env.policy_ids()
+    rng = random.Random(77 + raw)
+    docs = [d for d in (_doc(rng, raw) for _ in range(800)) if O.flatten_doc(d, raw=raw) is not None]
+    assert len(docs) > 400
+    b = K.Batch.from_json(docs, raw=raw).to_device(0)
+    soa = b.view()
+    for origin in (K.VALIDATE, K.AUDIT):
+        b.validate(env, ids, origin)
+        got = b.verdicts()
+        want = oe.eval(soa, ids, origin)
+        assert np.array_equal(got, want), diff_verdicts(got, want, len(ids), ids)
+        if not raw:
+            assert _check_responses(env, oe, b, soa, docs, ids, origin, range(0, len(docs), 7)) > 0
