@@ -46,12 +46,21 @@ oracle/build/libkworacle.so: oracle/kworacle.c oracle/kworacle.h include/kwgpu.h
 	@mkdir -p oracle/build
 	$(CC) -O2 -std=c11 -fPIC -shared -Wall -Wextra -o $@ $< -lpthread
 
-# A/B variant of the library with extra kernel flags: make variant NAME=x VFLAGS="-DKW_KV_PAIR=1"
-# -> policy-server_amd/variants/x.so (KWGPU_LIB selects it; scripts/ab.sh benches every variant)
+# A/B variant of the library with extra kernel flags: make variant NAME=x VFLAGS="-DKW_PREFETCH=0"
+# -> policy-server_amd/variants/x.so (KWGPU_LIB selects it; scripts/ab.sh benches every variant);
+# KSRC=<file in csrc/> builds another kernels source (e.g. the previous commit's)
 variant: $(HOST_OBJS)
 	@mkdir -p $(PKG)/variants/obj-$(NAME)
-	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c $(SRC)/kernels.hip -o $(PKG)/variants/obj-$(NAME)/kernels.o
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c $(or $(KSRC),$(SRC)/kernels.hip) -o $(PKG)/variants/obj-$(NAME)/kernels.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(PKG)/variants/$(NAME).so $(HOST_OBJS) $(PKG)/variants/obj-$(NAME)/kernels.o
+
+# A/B variant built entirely (host engine + kernels) from another source directory next to csrc/,
+# e.g. a snapshot of an earlier commit: make variant-full NAME=x VSRC=policy-server_amd/csrc_x
+variant-full:
+	@mkdir -p $(PKG)/variants/obj-$(NAME)
+	for f in $(HOST_SRCS); do $(CXX) $(CXXFLAGS) $(VFLAGS) -c $(VSRC)/$$f.cpp -o $(PKG)/variants/obj-$(NAME)/$$f.o || exit 1; done
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c $(VSRC)/kernels.hip -o $(PKG)/variants/obj-$(NAME)/kernels.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(PKG)/variants/$(NAME).so $(addprefix $(PKG)/variants/obj-$(NAME)/,$(addsuffix .o,$(HOST_SRCS))) $(PKG)/variants/obj-$(NAME)/kernels.o
 
 # kernel resource usage (VGPR/SGPR/LDS/occupancy) report
 resources: $(SRC)/kernels.hip

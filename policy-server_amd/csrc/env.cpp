@@ -467,7 +467,7 @@ bool build_literal_table(const std::vector<std::string>& lits, std::vector<uint8
     for (uint32_t bk : order) {
       if (bucket[bk].empty()) break;
       bool placed = false;
-      for (uint32_t d = 0; d < 65536 && !placed; ++d) {
+      for (uint32_t d = 0; d < std::min<uint32_t>(65536u, nslots) && !placed; ++d) {  // lit_disp(d) = d: every mask once
         std::vector<uint32_t> sl;
         bool fit = true;
         for (uint32_t i : bucket[bk]) {

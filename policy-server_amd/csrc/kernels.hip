@@ -629,12 +629,14 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
       const SlotView sv0 = chunk_view(0);
       const SlotHdr& h0 = *sv0.h;
       const uint32_t n3 = (LBL && (need & (1u << S_LK))) ? nl : 0u;
+      const uint32_t nka = kae - kab, nkd = kde - kdb;
+      const uint32_t nk = (CTR && (need & (1u << S_CAPADD))) ? nka + nkd : 0u;
       const uint32_t n2 = CTR ? nc : 0u;
       const uint32_t n1 = (IMG && (need & (1u << S_IMG))) ? nc : 0u;
       const uint32_t n0 = nr;
-      const uint32_t e0 = rup64(n3), e1 = e0 + rup64(n2), e2 = e1 + rup64(n1), e3 = e2 + rup64(n0);
+      const uint32_t ek = rup64(n3), e0 = ek + rup64(nk), e1 = e0 + rup64(n2), e2 = e1 + rup64(n1), e3 = e2 + rup64(n0);
       for (uint32_t w = tid; w < e3; w += kSlotThreads) {
-        if (LBL && w < e0) {  // label
+        if (LBL && w < ek) {  // label
           const uint32_t i = w;
           if (i >= n3) continue;
           const uint32_t k = lit(COL_LK, S_LK, i);
@@ -648,7 +650,17 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
             for (uint32_t j = 0; j < nlv; ++j) lv[j] = 0xffffu;
           }
           l_vl[i] = dv_label(sv0, k, lv, nlv);
-        } else if (CTR && w < e1) {  // container
+        } else if (CTR && w < e0) {  // capability string: added ones first, then dropped ones
+          const uint32_t k = w - ek;
+          if (k >= nk) continue;
+          if (k < nka) {
+            const uint32_t cc = lit(COL_CAP, S_CAPADD, k);
+            c_add[k] = (uint16_t)cc;
+            l_vadd[k] = (h0.caps && h0.caps_strict) ? sv0.row(T_NACAP, cc) : 0ull;
+          } else {
+            c_drop[k - nka] = (uint16_t)lit(COL_CAP, S_CAPDROP, k - nka);
+          }
+        } else if (CTR && w < e1) {  // container (its added capabilities' sets stay in l_vadd: P2 ORs them)
           const uint32_t i = w - e0;
           if (i >= n2) continue;
           const uint32_t fl = cfl[i];
@@ -657,16 +669,6 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
             const uint32_t ac = (fl & KW_CTR_HAS_APPARMOR) ? lit(COL_AA, S_AA, i) : 0u;
             c_aa[i] = (uint16_t)ac;
             if (h0.aa && (fl & KW_CTR_HAS_APPARMOR)) v |= sv0.row(T_NAAA, ac);
-          }
-          if (need & (1u << S_CAPADD)) {
-            for (uint32_t k = l_cadd[i] - kab, k1 = l_cadd[i + 1] - kab; k < k1; ++k) {
-              const uint32_t cc = lit(COL_CAP, S_CAPADD, k);
-              c_add[k] = (uint16_t)cc;
-              const uint64_t va = h0.caps_strict ? sv0.row(T_NACAP, cc) : 0ull;
-              l_vadd[k] = va;
-              v |= va;
-            }
-            for (uint32_t k = l_cdrop[i] - kdb, k1 = l_cdrop[i + 1] - kdb; k < k1; ++k) c_drop[k] = (uint16_t)lit(COL_CAP, S_CAPDROP, k);
           }
           l_vc[i] = v;
         } else if (IMG && w < e2) {  // image reference: one parse feeds the registry, tag and image classes
@@ -726,24 +728,22 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
       const SlotHdr& SH = *sv.h;
       if (ck > 0) {
         // ---- D: this chunk's violation sets from the stored classes
-        const uint32_t n3 = (LBL && SH.lbl) ? nl : 0u, n2 = CTR ? nc : 0u, n1 = (IMG && SH.trs) ? nc : 0u;
-        const uint32_t e0 = rup64(n3), e1 = e0 + rup64(n2), e2 = e1 + rup64(n1), e3 = e2 + rup64(nr);
+        const uint32_t n3 = (LBL && SH.lbl) ? nl : 0u, nk = (CTR && SH.caps) ? kae - kab : 0u, n2 = CTR ? nc : 0u,
+                       n1 = (IMG && SH.trs) ? nc : 0u;
+        const uint32_t ek = rup64(n3), e0 = ek + rup64(nk), e1 = e0 + rup64(n2), e2 = e1 + rup64(n1), e3 = e2 + rup64(nr);
         for (uint32_t w = tid; w < e3; w += kSlotThreads) {
-          if (LBL && w < e0) {
+          if (LBL && w < ek) {
             const uint32_t i = w;
             if (i < n3) l_vl[i] = dv_label(sv, c_lk[i], c_lv + i * nlv, nlv);
+          } else if (CTR && w < e0) {  // added capability (read by P2 only when this chunk has caps slots)
+            const uint32_t k = w - ek;
+            if (k < nk) l_vadd[k] = SH.caps_strict ? sv.row(T_NACAP, c_add[k]) : 0ull;
           } else if (CTR && w < e1) {
             const uint32_t i = w - e0;
             if (i >= n2) continue;
             const uint32_t fl = cfl[i];
             uint64_t v = priv_viol(SH, fl);
             if (SH.aa && (fl & KW_CTR_HAS_APPARMOR)) v |= sv.row(T_NAAA, c_aa[i]);
-            if (SH.caps)
-              for (uint32_t k = l_cadd[i] - kab, k1 = l_cadd[i + 1] - kab; k < k1; ++k) {
-                const uint64_t va = SH.caps_strict ? sv.row(T_NACAP, c_add[k]) : 0ull;
-                l_vadd[k] = va;
-                v |= va;
-              }
             l_vc[i] = v;  // (l_vtr is read only by chunks with trusted-repos slots, which rewrite it below)
           } else if (IMG && w < e2) {
             const uint32_t i = w - e1;
@@ -779,10 +779,19 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
             const uint32_t q = own_c[i];
             if (!(l_rf[q] & KW_REQ_HAS_PODSPEC)) continue;
             const uint32_t c0 = l_coff[q] - cb;
-            uint64_t pre = 0;
-            if (!(t.debug & 4096u))
+            // predecessors' sets: their own families' and images', and their added capabilities'
+            // (a contiguous range of l_vadd); the same for this container
+            const bool capv = CTR && SH.caps != 0;
+            const uint32_t ka0 = l_cadd[c0] - kab, ka = l_cadd[i] - kab, ka1 = l_cadd[i + 1] - kab;
+            uint64_t pre = 0, own = vset(i);
+            if (!(t.debug & 4096u)) {
               for (uint32_t j = c0; j < i; ++j) pre |= vset(j);
-            const uint64_t nv = vset(i) & ~pre;
+              if (capv)
+                for (uint32_t k = ka0; k < ka; ++k) pre |= l_vadd[k];
+            }
+            if (capv)
+              for (uint32_t k = ka; k < ka1; ++k) own |= l_vadd[k];
+            const uint64_t nv = own & ~pre;
             const uint32_t ci = i - c0;
             uint32_t* vw = l_vw + q * t.vw_stride;
             if (nv) {
@@ -813,7 +822,7 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
             }
             if (CTR && SH.caps) {  // mutation: required drops missing, default adds neither added nor dropped
               uint64_t addm = 0, dropm = 0;
-              for (uint32_t k = l_cadd[i] - kab, k1 = l_cadd[i + 1] - kab; k < k1; ++k) addm |= bit_of(sv.capmb(c_add[k]));
+              for (uint32_t k = ka; k < ka1; ++k) addm |= bit_of(sv.capmb(c_add[k]));
               for (uint32_t k = l_cdrop[i] - kdb, k1 = l_cdrop[i + 1] - kdb; k < k1; ++k) dropm |= bit_of(sv.capmb(c_drop[k]));
               const uint64_t mut = caps_mutation(sv, addm, dropm);
               if (mut) atomicOr((unsigned long long*)&l_mut[q], (unsigned long long)mut);
@@ -929,33 +938,53 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
           const uint32_t* cs = (const uint32_t*)(sv.base + SH.o_csoa);
           const uint32_t cs_n = (ncols + 3u) & ~3u;
           const uint32_t G = ncols >> 2;
-          for (uint32_t q = tid; q < nr * G; q += kSlotThreads) {
-            const uint32_t rr = q / G, g = q - rr * G;
+          // the 4-column group g of request rr: one 16-B non-temporal store. Column data (kind,
+          // slot, ok / mutated / rejected words) comes from the chunk's column arrays.
+          struct Cols4 {
+            uint4 ks, ok, mu, rj;
+          };
+          auto load4 = [&](uint32_t g) -> Cols4 {
+            return {*(const uint4*)(cs + 4 * g), *(const uint4*)(cs + cs_n + 4 * g), *(const uint4*)(cs + 2 * cs_n + 4 * g),
+                    *(const uint4*)(cs + 3 * cs_n + 4 * g)};
+          };
+          auto emit = [&](uint32_t rr, uint32_t g, const Cols4& c4, uint32_t* dst) {
             uint4 wv;
             if (l_byp[rr]) {
               wv = make_uint4(kBypassWord, kBypassWord, kBypassWord, kBypassWord);
             } else {
               const uint64_t rej = l_rej[rr], mut = l_mut[rr];
               const uint32_t* vw = l_vw + rr * t.vw_stride;
-              const uint4 ks = *(const uint4*)(cs + 4 * g), ok = *(const uint4*)(cs + cs_n + 4 * g),
-                          mu = *(const uint4*)(cs + 2 * cs_n + 4 * g), rj = *(const uint4*)(cs + 3 * cs_n + 4 * g);
               auto pw = [&](uint32_t k, uint32_t okw, uint32_t mutw, uint32_t rejb, uint32_t j) -> uint32_t {
                 if ((k & 0xffu) != CK_PLAIN) return GRP ? word(rr, j) : okw;  // (no group: a constant column)
                 const uint32_t s = k >> 8;
                 if ((rej >> s) & 1ull) return rejb | vw[s];
                 return ((mut >> s) & 1ull) ? mutw : okw;
               };
-              wv.x = pw(ks.x, ok.x, mu.x, rj.x, 4 * g + 0);
-              wv.y = pw(ks.y, ok.y, mu.y, rj.y, 4 * g + 1);
-              wv.z = pw(ks.z, ok.z, mu.z, rj.z, 4 * g + 2);
-              wv.w = pw(ks.w, ok.w, mu.w, rj.w, 4 * g + 3);
+              wv.x = pw(c4.ks.x, c4.ok.x, c4.mu.x, c4.rj.x, 4 * g + 0);
+              wv.y = pw(c4.ks.y, c4.ok.y, c4.mu.y, c4.rj.y, 4 * g + 1);
+              wv.z = pw(c4.ks.z, c4.ok.z, c4.mu.z, c4.rj.z, 4 * g + 2);
+              wv.w = pw(c4.ks.w, c4.ok.w, c4.mu.w, c4.rj.w, 4 * g + 3);
             }
 #if KW_NT_STORE
             const u32x4 nv4 = {wv.x, wv.y, wv.z, wv.w};
-            __builtin_nontemporal_store(nv4, (u32x4*)(out + (r0 + rr) * npol + CA.col0 + 4 * g));  // streamed once
+            __builtin_nontemporal_store(nv4, (u32x4*)dst);  // streamed once
 #else
-            *(uint4*)(out + (r0 + rr) * npol + CA.col0 + 4 * g) = wv;
+            *(uint4*)dst = wv;
 #endif
+          };
+          if ((G & (G - 1u)) == 0 && G <= kSlotThreads) {
+            // G a power of two dividing the workgroup: each thread keeps one column group for every
+            // request it writes, so the column data is loaded once and no division is needed
+            const uint32_t lg = (uint32_t)__builtin_ctz(G), g = tid & (G - 1u), step = kSlotThreads >> lg;
+            const Cols4 c4 = load4(g);
+            uint32_t* dst = out + (r0 + (tid >> lg)) * npol + CA.col0 + 4 * g;
+            const uint64_t dstep = (uint64_t)step * npol;
+            for (uint32_t rr = tid >> lg; rr < nr; rr += step, dst += dstep) emit(rr, g, c4, dst);
+          } else {
+            for (uint32_t q = tid; q < nr * G; q += kSlotThreads) {
+              const uint32_t rr = q / G, g = q - rr * G;
+              emit(rr, g, load4(g), out + (r0 + rr) * npol + CA.col0 + 4 * g);
+            }
           }
         } else {
           for (uint32_t q = tid; q < nr * ncols; q += kSlotThreads) {

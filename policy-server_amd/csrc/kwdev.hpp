@@ -116,17 +116,20 @@ constexpr uint32_t lit_slot_len(uint32_t x) { return x >> 16; }
 
 // hash shared by the host table builder (env.cpp) and the kernels
 inline KW_HD uint32_t lit_init(uint32_t seed, uint32_t len) { return seed ^ (len * 0x9E3779B1u); }
+// per-word step without a 32-bit multiply (a quarter-rate VALU op on CDNA): rotate, times 5, add
+// (bijective in h for a fixed word, so strings differing in one word never collide before
+// lit_final's avalanche)
 inline KW_HD uint32_t lit_mix(uint32_t h, uint32_t w) {
   h ^= w;
-  h *= 0x85EBCA6Bu;
-  return h ^ (h >> 13);
+  h = (h << 13) | (h >> 19);
+  return h * 5u + 0xE6546B64u;
 }
 inline KW_HD uint32_t lit_final(uint32_t h) {
   h ^= h >> 16;
   h *= 0x7FEB352Du;
   return h ^ (h >> 15);
 }
-inline KW_HD uint32_t lit_disp(uint32_t d) { return d ? lit_final(d * 0x9E3779B1u) : 0u; }
+inline KW_HD uint32_t lit_disp(uint32_t d) { return d; }  // the builder tries every xor mask below nslots
 inline KW_HD uint32_t lit_slot_index(uint32_t g, uint32_t d, uint32_t nslots) { return (g ^ lit_disp(d)) & (nslots - 1u); }
 
 // Classifier of one column. Global classes: 0 = no pattern, [1, 1 + nlit) the literal patterns,

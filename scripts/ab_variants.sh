@@ -7,7 +7,7 @@ TAG=${1:-abv}
 for v in policy-server_amd/variants/*.so; do
   n=$(basename "$v" .so)
   KWGPU_LIB="$PWD/$v" timeout -k 10 300 python -u -m pytest tests/test_parity_gpu.py -x -q -p no:cacheprovider --timeout 120 \
-    --timeout-method thread -k "${PARITY_K:-c4_64 or parity}" > gpurun_out/${TAG}_${n}_tests.log 2>&1
+    --timeout-method thread -k "${PARITY_K:-(c4_64 or parity) and not stream}" > gpurun_out/${TAG}_${n}_tests.log 2>&1
   rc=$?; echo "[abv] $n tests rc=$rc $(tail -1 gpurun_out/${TAG}_${n}_tests.log)"
   if [ $rc -ne 0 ]; then exit $rc; fi
   KW_TILE_DEBUG=256 KWGPU_LIB="$PWD/$v" timeout -k 10 300 python bench.py --config ${CFG:-c4_64} --no-cpu-baseline --no-host-modes > gpurun_out/${TAG}_${n}.json 2> gpurun_out/${TAG}_${n}.err

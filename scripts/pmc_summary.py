@@ -15,6 +15,7 @@ def summarise(d, match="evaluate_tiles"):
         dur[r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
     out = {k: sum(v) / len(v) for k, v in vals.items()}
     out["dispatches"] = len(dur)
+    out["dur_ns"] = sum(dur.values()) / max(1, len(dur))
     return out
 
 
