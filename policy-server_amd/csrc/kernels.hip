@@ -32,6 +32,9 @@
 #ifndef KW_LDS_BARRIER
 #define KW_LDS_BARRIER 1
 #endif
+#ifndef KW_LIT_SHORT  // tile kernel: a 4-word literal probe when no string of the wave is longer than 16 bytes
+#define KW_LIT_SHORT 1
+#endif
 #ifndef KW_MAND_BATCH
 #define KW_MAND_BATCH 1
 #endif
@@ -63,25 +66,25 @@ __device__ inline uint32_t lit_word(const uint32_t* base, uint32_t i, uint32_t s
 // Literal class of bytes [b, e) (DevLit, kwdev.hpp), 0 = no literal pattern. BATCH: the first 32
 // bytes of the string and of the candidate pattern are read in one batch each (up to 36 bytes past
 // the string start: LDS staging slack); otherwise word by word (<= 7 bytes past the end).
-template <bool BATCH>
+template <bool BATCH, int N = 8>
 __device__ inline uint32_t lit_lookup(const uint8_t* rec, const uint8_t* bytes, uint32_t b, uint32_t e) {
   const DevLit* L = (const DevLit*)rec;
   const uint32_t len = e - b, sh = b & 3u, nw = (len + 3u) >> 2;
   const uint32_t* base = (const uint32_t*)(bytes + (b & ~3u));
   uint32_t h = lit_init(L->seed, len);
-  uint32_t w[8];
+  uint32_t w[N];
   if (BATCH) {
-    uint32_t raw[9];
+    uint32_t raw[N + 1];
 #pragma unroll
-    for (int i = 0; i < 9; ++i) raw[i] = base[i];
+    for (int i = 0; i < N + 1; ++i) raw[i] = base[i];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < N; ++i) {
       const uint32_t x = align_bytes(raw[i + 1], raw[i], sh);
       const uint32_t rem = len - 4u * (uint32_t)i;
       w[i] = rem >= 4u ? x : (x & ((1u << (8u * rem)) - 1u));
       if ((uint32_t)i < nw) h = lit_mix(h, w[i]);
     }
-    for (uint32_t i = 8; i < nw; ++i) h = lit_mix(h, lit_word(base, i, sh, len));
+    for (uint32_t i = N; i < nw; ++i) h = lit_mix(h, lit_word(base, i, sh, len));
   } else {
     for (uint32_t i = 0; i < nw; ++i) h = lit_mix(h, lit_word(base, i, sh, len));
   }
@@ -92,12 +95,12 @@ __device__ inline uint32_t lit_lookup(const uint8_t* rec, const uint8_t* bytes, 
   const uint32_t* pw = (const uint32_t*)(rec + L->word_off) + sl.y;
   bool eq = true;
   if (BATCH) {
-    uint32_t pv[8];
+    uint32_t pv[N];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) pv[i] = pw[i];  // zero tail of the words section covers short patterns
+    for (int i = 0; i < N; ++i) pv[i] = pw[i];  // zero tail of the words section covers short patterns
 #pragma unroll
-    for (int i = 0; i < 8; ++i) eq = eq && ((uint32_t)i >= nw || w[i] == pv[i]);
-    for (uint32_t i = 8; i < nw && eq; ++i) eq = lit_word(base, i, sh, len) == pw[i];
+    for (int i = 0; i < N; ++i) eq = eq && ((uint32_t)i >= nw || w[i] == pv[i]);
+    for (uint32_t i = N; i < nw && eq; ++i) eq = lit_word(base, i, sh, len) == pw[i];
   } else {
     for (uint32_t i = 0; i < nw && eq; ++i) eq = lit_word(base, i, sh, len) == pw[i];
   }
@@ -618,6 +621,10 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
       if (!classify || !C.lit[c]) return 0u;
       uint32_t b, e;
       str(m, i, &b, &e);
+#if KW_LIT_SHORT
+      // every string of the wave within 16 bytes (the common case): the 4-word batch
+      if (!__ballot(e - b > 16u)) return lit_lookup<true, 4>(C.lit[c], lds + t.o_sb[m], b, e);
+#endif
       return lit_lookup<true>(C.lit[c], lds + t.o_sb[m], b, e);
     };
 
