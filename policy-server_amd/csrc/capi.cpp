@@ -98,12 +98,13 @@ void parallel_copy(void* dst, const void* src, size_t bytes) {
   for (auto& x : th) x.join();
 }
 
-// Requests per tile of the tile kernel: kSlotRows, or KW_SLOT_ROWS (8..255, A/B knob) when set.
-uint32_t slot_rows() {
+// Requests per tile of the tile kernel forced by KW_SLOT_ROWS (8..255, A/B knob), 0 = chosen per
+// batch (plan_pass: kSlotRows, or taller tiles where they keep enough workgroups per CU).
+uint32_t slot_rows_forced() {
   static const uint32_t r = [] {
     const char* e = getenv("KW_SLOT_ROWS");
     const int v = e ? atoi(e) : 0;
-    return (v >= 8 && v <= 255) ? (uint32_t)v : kSlotRows;  // tile-local owners are u8
+    return (v >= 8 && v <= 255) ? (uint32_t)v : 0u;  // tile-local owners are u8
   }();
   return r;
 }
@@ -172,12 +173,16 @@ struct DeviceBatch {
   uint32_t last_nwide = 0, last_wide_cap = 0;
   bool last_rows_mode = false;
   std::vector<int32_t> last_wide_policy;
-  // tile capacities of this batch (plan_pass)
-  bool stats_valid = false;
-  std::vector<TileStats> tile_need;
-  std::vector<TileStats> tile_q;
-  uint64_t cap_key = 0;
-  int cap_choice = -1;
+  // tile capacities of this batch (plan_pass), per tile height tried
+  struct RowsPlan {
+    uint32_t rows = 0;
+    std::vector<TileStats> need, q;  // per-tile needs and their quantiles
+    uint64_t cap_key = 0;
+    int cap_choice = -1;   // quantile index chosen for cap_key
+    uint32_t cap_cu = 0;   // its workgroups per CU
+    uint32_t cap_lds = 0;  // its LDS bytes
+  };
+  std::vector<RowsPlan> rows_plans;
   ~DeviceBatch() {
     if (device < 0) return;  // host-only view (kw_debug_plan)
     (void)hipSetDevice(device);
@@ -464,14 +469,7 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
   // ---- tile geometry and LDS layout
   TileArgs& T = plan->geom;
   auto align = [](uint32_t x) { return (x + 15u) & ~15u; };
-  const uint32_t rows = slot_rows();
-  if (!D.stats_valid) {
-    D.tile_need = tile_needs(B, rows);
-    D.tile_q.clear();
-    for (double q : kTileQuantiles) D.tile_q.push_back(tile_quantile(D.tile_need, q));
-    D.cap_choice = -1;
-    D.stats_valid = true;
-  }
+  uint32_t rows = kSlotRows;  // the tile height the layout below is computed for
   const uint32_t vw_stride = nslots | 1u;  // odd stride: lanes (requests) spread over the banks
   const uint32_t nim = il.n();
   auto layout = [&](const TileStats& ts) -> uint32_t {
@@ -542,41 +540,85 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
     return T.lds_bytes;
   };
   auto per_cu = [](uint32_t b) { return std::min<uint32_t>(2048 / kSlotThreads, (160 * 1024) / std::max<uint32_t>(b, 1)); };
-  // Capacities: the highest occupancy (workgroups per CU, LDS-bound) whose layout splits at most
-  // 2 % of the tiles (a tile beyond the capacities runs as halves, upload_tile_descs), over
-  // per-dimension quantiles of the tile needs; at a given occupancy the largest capacities (fewest
-  // split tiles). Chosen once per batch and layout signature.
-  uint64_t key = ((uint64_t)area << 40) ^ ((uint64_t)nslots << 20) ^ ((uint64_t)nim << 12) ^ ((uint64_t)nlv << 8) ^ need;
-  if (D.cap_choice < 0 || D.cap_key != key) {
-    const uint64_t ntl = D.tile_need.size();
-    int best = 0;
-    uint32_t best_cu = 0;
-    const double max_split = getenv("KW_TILE_SPLIT") ? atof(getenv("KW_TILE_SPLIT")) : 0.02;  // A/B knob
-    for (int k = 0; k < (int)D.tile_q.size(); ++k) {
-      const uint32_t cu = per_cu(layout(D.tile_q[k]));
-      if (T.lds_bytes > kTileLdsBudget) continue;
-      uint64_t over = 0;  // tiles beyond these capacities (split by the descriptors' fit test)
-      for (const TileStats& x : D.tile_need) {
-        bool o = x.ctr > T.cmax || x.lbl > T.lmax || x.kadd > T.kmax || x.kdrop > T.kmax;
-        for (int m = 0; m < (int)NSTR && !o; ++m) o = T.sb_cap[m] && x.bytes[m] > T.sb_cap[m];
-        over += o;
+  // Capacities at a tile height: the highest occupancy (workgroups per CU, LDS-bound) whose layout
+  // splits at most 2 % of the tiles (a tile beyond the capacities runs as halves, upload_tile_descs),
+  // over per-dimension quantiles of the tile needs; at a given occupancy the largest capacities
+  // (fewest split tiles). Chosen once per batch, tile height and layout signature.
+  const uint64_t key = ((uint64_t)area << 40) ^ ((uint64_t)nslots << 20) ^ ((uint64_t)nim << 12) ^ ((uint64_t)nlv << 8) ^ need;
+  D.rows_plans.reserve(4);  // at most 64, 128, 96 (or the forced height): references stay valid
+  auto plan_rows = [&](uint32_t r) -> DeviceBatch::RowsPlan& {
+    DeviceBatch::RowsPlan* R = nullptr;
+    for (auto& x : D.rows_plans)
+      if (x.rows == r) R = &x;
+    if (!R) {
+      D.rows_plans.emplace_back();
+      R = &D.rows_plans.back();
+      R->rows = r;
+      R->need = tile_needs(B, r);
+      for (double q : kTileQuantiles) R->q.push_back(tile_quantile(R->need, q));
+    }
+    rows = r;
+    if (R->cap_choice < 0 || R->cap_key != key) {
+      const uint64_t ntl = R->need.size();
+      int best = 0;
+      uint32_t best_cu = 0, best_lds = 0;
+      const double max_split = getenv("KW_TILE_SPLIT") ? atof(getenv("KW_TILE_SPLIT")) : 0.02;  // A/B knob
+      for (int k = 0; k < (int)R->q.size(); ++k) {
+        const uint32_t cu = per_cu(layout(R->q[k]));
+        if (T.lds_bytes > kTileLdsBudget) continue;
+        uint64_t over = 0;  // tiles beyond these capacities (split by the descriptors' fit test)
+        for (const TileStats& x : R->need) {
+          bool o = x.ctr > T.cmax || x.lbl > T.lmax || x.kadd > T.kmax || x.kdrop > T.kmax;
+          for (int m = 0; m < (int)NSTR && !o; ++m) o = T.sb_cap[m] && x.bytes[m] > T.sb_cap[m];
+          over += o;
+        }
+        if (getenv("KW_TILE_DEBUG") && (atoi(getenv("KW_TILE_DEBUG")) & 256))
+          fprintf(stderr, "[kw tile] rows=%u candidate q=%g lds=%u wg/cu=%u split=%llu/%llu\n", r, kTileQuantiles[k], T.lds_bytes, cu,
+                  (unsigned long long)over, (unsigned long long)ntl);
+        if (k > 0 && (double)over > max_split * (double)ntl) continue;
+        if (cu > best_cu) {
+          best = k;
+          best_cu = cu;
+          best_lds = T.lds_bytes;
+        }
       }
+      R->cap_key = key;
+      R->cap_choice = best;
+      R->cap_cu = best_cu;
+      R->cap_lds = best_lds;
+    }
+    return *R;
+  };
+  // Tile height: KW_SLOT_ROWS when forced; else kSlotRows, or 128 / 96 rows when the batch has at
+  // least 4 tiles per workgroup slot and the taller layout still keeps 4 workgroups per CU (its LDS
+  // estimated from the 64-row layout first: the per-request part scales with the height). Taller
+  // tiles amortise the per-tile latency (staging, barriers) where the per-request LDS is small:
+  // C2 -12 %, C3 -25 %; the C4-C6 layouts need 64 rows for 4 workgroups per CU (r02 sweeps).
+  const DeviceBatch::RowsPlan* pick = nullptr;
+  if (const uint32_t f = slot_rows_forced()) {
+    pick = &plan_rows(f);
+  } else {
+    const DeviceBatch::RowsPlan& base = plan_rows(kSlotRows);
+    pick = &base;
+    const uint32_t fixed = 16 + align(area), per64 = base.cap_lds > fixed ? base.cap_lds - fixed : 0u;
+    for (uint32_t r : {128u, 96u}) {
+      const uint64_t est = fixed + (uint64_t)per64 * r / kSlotRows;
       if (getenv("KW_TILE_DEBUG") && (atoi(getenv("KW_TILE_DEBUG")) & 256))
-        fprintf(stderr, "[kw tile] candidate q=%g lds=%u wg/cu=%u split=%llu/%llu\n", kTileQuantiles[k], T.lds_bytes, cu,
-                (unsigned long long)over, (unsigned long long)ntl);
-      if (k > 0 && (double)over > max_split * (double)ntl) continue;
-      if (cu > best_cu) {
-        best = k;
-        best_cu = cu;
+        fprintf(stderr, "[kw tile] rows=%u estimated lds=%llu (64-row layout %u, fixed %u) batch rows %llu\n", r,
+                (unsigned long long)est, base.cap_lds, fixed, (unsigned long long)B.n);
+      if (per_cu((uint32_t)std::min<uint64_t>(est, 1u << 30)) < 4 || B.n < (uint64_t)r * 4 * 256 * 4) continue;
+      const DeviceBatch::RowsPlan& R = plan_rows(r);
+      if (R.cap_cu >= 4) {
+        pick = &R;
+        break;
       }
     }
-    D.cap_key = key;
-    D.cap_choice = best;
   }
+  rows = pick->rows;
   if (const char* fq = getenv("KW_TILE_QUANTILE"))  // tests / diagnostics: force the capacity quantile
-    layout(tile_quantile(D.tile_need, atof(fq)));
+    layout(tile_quantile(pick->need, atof(fq)));
   else
-    layout(D.tile_q[D.cap_choice]);
+    layout(pick->q[pick->cap_choice]);
   if (T.lds_bytes > kTileLdsBudget) return KW_E_ARG;  // policy list too large for one tile
   // next-tile L2 prefetch: a gain where several small tiles share a CU (C4: -2.5 %), a loss where two
   // large ones do (C5: +2.7 %; r02 A/B)

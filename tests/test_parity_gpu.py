@@ -183,11 +183,12 @@ def _oracle_threads():
     return max(1, min(16, len(os.sched_getaffinity(0))))
 
 
-@pytest.mark.parametrize("name,scfg,n", [("c4_64", 4, 1_000_000), ("c5_mixed", 5, 2_000_000)])
+@pytest.mark.parametrize("name,scfg,n", [("c4_64", 4, 1_000_000), ("c5_mixed", 5, 2_000_000), ("c2_trusted", 2, 1_000_000),
+                                         ("c3_group", 3, 1_000_000), ("c1_namespace", 1, 1_000_000)])
 def test_full_size_matches_oracle(name, scfg, n):
-    """BASELINE sizes: C4 at 1M requests x 64 policies and C5 (mixed kinds, skewed container counts)
-    at 2M requests, every verdict word against the oracle (C restatement, 16 threads); plus
-    determinism across launches."""
+    """BASELINE sizes: C4 at 1M requests x 64 policies, C5 (mixed kinds, skewed container counts)
+    at 2M requests, and C1-C3 at 1M (128-row tiles: the planner's taller layout), every verdict word
+    against the oracle (C restatement, 16 threads); plus determinism across launches."""
     env, oe = _envs(name)
     ids = env.policy_ids()
     syn = K.SynthBatch(scfg, n, seed=scfg)

@@ -178,3 +178,18 @@ def test_planner_budget():
     c6 = K.EvaluationEnvironment(many_policies_config())
     p = K.SynthBatch(6, 5000, seed=1).batch().debug_plan(c6, c6.policy_ids())
     assert p["chunks"] >= 5 and p["launches"] == 1, p
+
+
+def test_planner_tile_height():
+    """Tile height (kw_debug_plan rows): 64 requests for small batches and for layouts whose
+    per-request LDS needs them for four workgroups per CU (C4); 128 for large batches with small
+    per-request LDS (C2 trusted-repos, C3 group), still at four or more workgroups per CU."""
+    c4 = K.EvaluationEnvironment(config("c4_64"))
+    p = K.SynthBatch(4, 600_000, seed=1).batch().debug_plan(c4, c4.policy_ids())
+    assert p["rows"] == 64, p
+    for name, scfg in (("c2_trusted", 2), ("c3_group", 3)):
+        env = K.EvaluationEnvironment(config(name))
+        small = K.SynthBatch(scfg, 50_000, seed=1).batch().debug_plan(env, env.policy_ids())
+        assert small["rows"] == 64, (name, small)
+        big = K.SynthBatch(scfg, 600_000, seed=1).batch().debug_plan(env, env.policy_ids())
+        assert big["rows"] == 128 and big["lds_bytes"] <= 160 * 1024 // 4, (name, big)
