@@ -41,6 +41,9 @@
 #ifndef KW_PREFETCH  // tile kernel: warm L2 with the next tile's staged ranges during this tile's walk
 #define KW_PREFETCH 1
 #endif
+#ifndef KW_PF_EARLY  // tile kernel: the L2 prefetch of the next tile right after staging (else after classification)
+#define KW_PF_EARLY 0
+#endif
 #ifndef KW_NT_STORE  // tile kernel: verdict words with non-temporal stores
 #define KW_NT_STORE 1
 #endif
@@ -446,12 +449,15 @@ __device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_b
 __device__ inline void lds_barrier() { __syncthreads(); }
 #endif
 
-// L2 prefetch of `bytes` at `src`: one dword per 128-B line, by LDS-DMA into a 256-B scratch line
-// shared by the waves (never read), so no VGPR waits for the data and no barrier but the next staging barrier
-// (vmcnt) covers it; the next tile's staging loads then hit L2.
-__device__ inline void prefetch_l2(const void* src, uint32_t bytes, uint32_t* scratch, uint32_t tid) {
+// L2 prefetch of `bytes` at `src`: one dword per 128-B line, by LDS-DMA from lanes 0-15 of each wave
+// into a 64-B scratch line shared by the waves (never read; a DMA lane lands at base + 4 x lane), so
+// no VGPR waits for the data and no barrier but the next staging barrier (vmcnt) covers it; the next
+// tile's staging loads then hit L2.
+__device__ inline void prefetch_l2(const void* src, uint32_t bytes, uint8_t* scratch, uint32_t tid) {
   const uint8_t* p = (const uint8_t*)src;
-  for (uint32_t off = tid * 128u; off < bytes; off += kSlotThreads * 128u)  // every wave lands on the same line
+  if ((tid & 63u) >= 16u) return;
+  const uint32_t q = (tid >> 6) * 16u + (tid & 15u);  // 16 lanes per wave
+  for (uint32_t off = q * 128u; off < bytes; off += (kSlotThreads / 4u) * 128u)
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(p + off),
                                      (__attribute__((address_space(3))) void*)scratch, 4, 0, 0);
 }
@@ -548,42 +554,54 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
   // counter (a 128-B line each, so no counter is shared between XCDs); the atomic for the next tile
   // is issued when the current tile starts and its result is read only at the tile's end, so its
   // latency hides behind the tile. The XCD's last workgroup to finish zeroes the counter again.
+  // The schedule runs two tiles ahead: while a tile is evaluated, the index of the next one is
+  // already known, so its descriptor is copied into LDS under this tile's staging (the next tile's
+  // P0 and its L2 prefetch read it there, with no dependent global load), and the counter fetch
+  // issued now names the tile after next.
   const bool dyn = a.sched != nullptr;
   const uint32_t nx = min(8u, gridDim.x);
   const uint32_t xcd = blockIdx.x % nx;
   const uint64_t t_lo = dyn ? a.ndesc * xcd / nx : 0ull, t_hi = dyn ? a.ndesc * (xcd + 1) / nx : a.ndesc;
   uint32_t* cnt = dyn ? a.sched + xcd * 32u : nullptr;
-  uint32_t* l_nx = (uint32_t*)(lds + t.o_nx);
-  uint64_t tile = blockIdx.x;
+  uint32_t* l_nx = (uint32_t*)(lds + t.o_nx);  // the tile after next, double-buffered
+  TileDesc* l_desc = (TileDesc*)(lds + t.o_desc);
+  // descriptor `i` into LDS slot `s`: 32 lanes of wave 0, one dword each (LDS-DMA, counted by vmcnt)
+  auto fetch_desc = [&](uint64_t i, uint32_t s) {
+    if (tid < 32u)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)((const uint32_t*)(desc + i) + tid),
+                                       (__attribute__((address_space(3))) void*)(l_desc + s), 4, 0, 0);
+  };
+  auto sfield = [](const uint32_t& f) -> uint32_t { return __builtin_amdgcn_readfirstlane(f); };
+  uint64_t tile = blockIdx.x, next = tile + gridDim.x;
   if (dyn) {
-    if (tid == 0) l_nx[0] = atomicAdd(cnt, 1u);
+    if (tid == 0) {
+      l_nx[0] = atomicAdd(cnt, 1u);
+      l_nx[1] = atomicAdd(cnt, 1u);
+    }
     __syncthreads();
     tile = t_lo + l_nx[0];
+    next = t_lo + l_nx[1];  // (l_nx is rewritten only after the staging barrier of the first tile)
   }
+  if (tile < t_hi) fetch_desc(tile, 0);
+  __syncthreads();
   mark(4);
-  uint32_t nxt = 0, it = 1;
-  // next tile: the strided one, or the counter value thread 0 fetched (double-buffered in LDS: a
-  // slot is rewritten only two barriers after every thread read it)
-  auto advance = [&]() -> uint64_t {
-    if (!dyn) return tile + gridDim.x;
-    if (tid == 0) l_nx[it & 1u] = nxt;
-    lds_barrier();  // also: the next tile restages LDS (its strings alias this tile's violation words)
-    mark(4);
-    const uint64_t nt = t_lo + l_nx[it & 1u];
-    ++it;
-    return nt;
-  };
-  for (; tile < t_hi; tile = advance()) {
-    if (dyn && tid == 0) nxt = atomicAdd(cnt, 1u);
-    const TileDesc& d = desc[tile];
-    if (!d.fits) {  // queued for the overflow kernels by the host (uniform: no barrier skipped unevenly)
-      if (!dyn) lds_barrier();
+  for (uint32_t it = 0; tile < t_hi; ++it) {
+    const uint32_t cur = it & 1u;
+    uint32_t nxt2 = 0;
+    if (dyn && tid == 0) nxt2 = atomicAdd(cnt, 1u);  // the tile after next (read after the staging barrier)
+    if (next < t_hi) fetch_desc(next, cur ^ 1u);      // the next tile's descriptor (slot free since its last read)
+    const TileDesc& d = l_desc[cur];
+    if (!sfield(d.fits)) {  // queued for the overflow kernels by the host (uniform: no barrier skipped unevenly)
+      if (dyn && tid == 0) l_nx[cur] = nxt2;
+      __syncthreads();  // also waits for the next descriptor
+      tile = next;
+      next = dyn ? t_lo + l_nx[cur] : next + gridDim.x;
       continue;
     }
-    const uint64_t r0 = ((uint64_t)d.r0hi << 32) | d.r0lo;
-    const uint32_t nr = d.nr;
-    const uint32_t cb = d.cb, ce = d.ce, lb = d.lb, le = d.le;
-    const uint32_t kab = d.kab, kae = d.kae, kdb = d.kdb, kde = d.kde;
+    const uint64_t r0 = ((uint64_t)sfield(d.r0hi) << 32) | sfield(d.r0lo);
+    const uint32_t nr = sfield(d.nr);
+    const uint32_t cb = sfield(d.cb), ce = sfield(d.ce), lb = sfield(d.lb), le = sfield(d.le);
+    const uint32_t kab = sfield(d.kab), kae = sfield(d.kae), kdb = sfield(d.kdb), kde = sfield(d.kde);
     const uint32_t nc = ce - cb, nl = le - lb;
 
     // ---- P0: stage request headers, container offsets and the tile's strings. Every copy is an
@@ -601,14 +619,44 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
       const uint32_t g0 = str_g0(m, (uint32_t)r0, cb, kab, kdb, lb);
       const uint32_t n = str_n(m, nr, nc, kae - kab, kde - kdb, nl);
       glds_dwords(t.s_off[m] + g0, (uint32_t*)(lds + t.o_so[m]), n + 1, tid);  // absolute: rebased by l_sa
-      glds_x4((const u32x4*)(t.s_bytes[m] + d.sa[m]), (u32x4*)(lds + t.o_sb[m]), d.nv[m], tid);
+      glds_x4((const u32x4*)(t.s_bytes[m] + sfield(d.sa[m])), (u32x4*)(lds + t.o_sb[m]), sfield(d.nv[m]), tid);
     }
     for (uint32_t i = tid; i < nr; i += kSlotThreads) l_rej[i] = l_mut[i] = 0;
     if (tid < NSTR) l_sa[tid] = d.sa[tid];
-    __syncthreads();
+    __syncthreads();  // staged tile, the next descriptor and the counter fetch have landed
     mark(0);
     if (timing && tid == 0) ++ph[5];
-    if (KW_PREFETCH && dyn && tid == 0) l_nx[2] = nxt;  // read after the next barrier (prefetch)
+    if (dyn && tid == 0) l_nx[cur] = nxt2;  // read after this tile's last barrier
+    // the next tile's staged ranges into L2 (covered by this tile's classification, walk and stores),
+    // from its descriptor in LDS
+    auto prefetch_next = [&]() {
+      if (KW_PREFETCH && t.prefetch && next < t_hi) {
+        const TileDesc& dn = l_desc[cur ^ 1u];
+        if (sfield(dn.fits)) {
+          const uint64_t q0 = ((uint64_t)sfield(dn.r0hi) << 32) | sfield(dn.r0lo);
+          const uint32_t qn = sfield(dn.nr), qcb = sfield(dn.cb), qc = sfield(dn.ce) - qcb;
+          const uint32_t qlb = sfield(dn.lb), qkab = sfield(dn.kab), qkdb = sfield(dn.kdb);
+          uint8_t* scratch = lds + t.o_pf;
+          prefetch_l2(a.req_flags + q0, qn, scratch, tid);
+          prefetch_l2(a.ctr_off + q0, (qn + 1) * 4u, scratch, tid);
+          prefetch_l2(a.lbl_off + q0, (qn + 1) * 4u, scratch, tid);
+          prefetch_l2(a.ctr_flags + qcb, qc, scratch, tid);
+          prefetch_l2(a.capadd_off + qcb, (qc + 1) * 4u, scratch, tid);
+          prefetch_l2(a.capdrop_off + qcb, (qc + 1) * 4u, scratch, tid);
+#pragma unroll
+          for (int m = 0; m < (int)NSTR; ++m) {
+            if (!t.o_sb[m]) continue;
+            const uint32_t g0 = str_g0(m, (uint32_t)q0, qcb, qkab, qkdb, qlb);
+            const uint32_t n = str_n(m, qn, qc, sfield(dn.kae) - qkab, sfield(dn.kde) - qkdb, sfield(dn.le) - qlb);
+            prefetch_l2(t.s_off[m] + g0, (n + 1) * 4u, scratch, tid);
+            prefetch_l2(t.s_bytes[m] + sfield(dn.sa[m]), sfield(dn.nv[m]) * 16u, scratch, tid);
+          }
+        }
+      }
+    };
+#if KW_PF_EARLY
+    prefetch_next();
+#endif
     const uint8_t* cfl = l_cflags + (cb & 3u);  // staged from the dword holding flag cb
     const bool classify = !(t.debug & 1u);  // diagnostics: skip classification (entities match nothing)
     auto str = [&](int m, uint32_t i, uint32_t* b, uint32_t* e) {
@@ -706,29 +754,9 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
     }
     lds_barrier();
     mark(1);
-    if (KW_PREFETCH && t.prefetch) {  // the next tile's staged ranges into L2 (covered by this tile's walk and stores)
-      const uint64_t nt = dyn ? t_lo + l_nx[2] : tile + gridDim.x;
-      if (nt < t_hi && desc[nt].fits) {
-        const TileDesc& dn = desc[nt];
-        const uint64_t q0 = ((uint64_t)dn.r0hi << 32) | dn.r0lo;
-        const uint32_t qn = dn.nr, qc = dn.ce - dn.cb;
-        uint32_t* scratch = (uint32_t*)(lds + t.o_pf);
-        prefetch_l2(a.req_flags + q0, qn, scratch, tid);
-        prefetch_l2(a.ctr_off + q0, (qn + 1) * 4u, scratch, tid);
-        prefetch_l2(a.lbl_off + q0, (qn + 1) * 4u, scratch, tid);
-        prefetch_l2(a.ctr_flags + dn.cb, qc, scratch, tid);
-        prefetch_l2(a.capadd_off + dn.cb, (qc + 1) * 4u, scratch, tid);
-        prefetch_l2(a.capdrop_off + dn.cb, (qc + 1) * 4u, scratch, tid);
-#pragma unroll
-        for (int m = 0; m < (int)NSTR; ++m) {
-          if (!t.o_sb[m]) continue;
-          const uint32_t g0 = str_g0(m, (uint32_t)q0, dn.cb, dn.kab, dn.kdb, dn.lb);
-          const uint32_t n = str_n(m, qn, qc, dn.kae - dn.kab, dn.kde - dn.kdb, dn.le - dn.lb);
-          prefetch_l2(t.s_off[m] + g0, (n + 1) * 4u, scratch, tid);
-          prefetch_l2(t.s_bytes[m] + dn.sa[m], dn.nv[m] * 16u, scratch, tid);
-        }
-      }
-    }
+#if !KW_PF_EARLY
+    prefetch_next();
+#endif
 
     for (uint32_t ck = 0; ck < t.nchunk; ++ck) {
       const SlotView sv = chunk_view(ck);
@@ -801,7 +829,7 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
             const uint64_t nv = own & ~pre;
             const uint32_t ci = i - c0;
             uint32_t* vw = l_vw + q * t.vw_stride;
-            if (nv) {
+            if (nv && !(t.debug & 16384u)) {
               ViolSink vs{vw, nullptr};
               if (CTR) {
                 vs.put(nv & privany, KW_R_PRIVILEGED, ci);
@@ -827,7 +855,7 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
               }
               atomicOr((unsigned long long*)&l_rej[q], (unsigned long long)nv);
             }
-            if (CTR && SH.caps) {  // mutation: required drops missing, default adds neither added nor dropped
+            if (CTR && SH.caps && !(t.debug & 8192u)) {  // mutation: required drops missing, default adds neither added nor dropped
               uint64_t addm = 0, dropm = 0;
               for (uint32_t k = ka; k < ka1; ++k) addm |= bit_of(sv.capmb(c_add[k]));
               for (uint32_t k = l_cdrop[i] - kdb, k1 = l_cdrop[i + 1] - kdb; k < k1; ++k) dropm |= bit_of(sv.capmb(c_drop[k]));
@@ -844,7 +872,7 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
             uint64_t pre = 0;
             for (uint32_t j = l0; j < i; ++j) pre |= l_vl[j];
             const uint64_t nv = v & ~pre;
-            if (!nv) continue;
+            if (!nv || (t.debug & 16384u)) continue;
             const uint64_t den = sv.row(T_DENY, c_lk[i]);
             const uint32_t li = i - l0;
             ViolSink vs{l_vw + q * t.vw_stride, nullptr};
@@ -896,7 +924,7 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
                 for (int u = 0; u < 4; ++u) pk[u] = ss[u] < 64u ? sv.mpack(ss[u]) : 0ull;
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
-                  if (ss[u] < 64u) vs.put(1ull << ss[u], KW_R_LABEL_MANDATORY, first_missing_packed(sv, ss[u], pk[u], present));
+                  if (ss[u] < 64u) vs.vw[ss[u]] = vword(KW_R_LABEL_MANDATORY, first_missing_packed(sv, ss[u], pk[u], present));
               }
 #else
               uint64_t nw = tab_or(sv.mand(), SH.mand_union & ~present) & ~lrej;
@@ -1005,8 +1033,10 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
         mark(4);
       }
     }
-    if (!dyn) lds_barrier();  // the next tile restages LDS (its strings alias this tile's violation words)
-    mark(4);  // (dynamic schedule: the barrier is advance()'s, at the loop step)
+    lds_barrier();  // the next tile restages LDS (its strings alias this tile's violation words)
+    mark(4);
+    tile = next;
+    next = dyn ? t_lo + l_nx[cur] : next + gridDim.x;
   }
   if (timing && tid == 0) {  // one lane's vector stores
     ph[6] = clock64() - t_begin;

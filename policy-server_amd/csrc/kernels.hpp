@@ -79,8 +79,9 @@ struct TileArgs {
   uint32_t o_vadd, o_vl, o_vc, o_vtr;  // u64 violation sets: per added capability, per label, per container (2)
   uint32_t o_own_c, o_own_l;           // u8 tile-local request of each staged container / label
   uint32_t o_rej, o_mut, o_byp;        // per-request results: rejected / mutated slots, bypass flag
-  uint32_t o_nx;                       // u32[3]: next tile index (dynamic schedule), double-buffered; [2]: prefetch
-  uint32_t o_pf;                       // 256 B: LDS-DMA landing of the L2 prefetch (never read)
+  uint32_t o_nx;                       // u32[2]: the tile after next (dynamic schedule), double-buffered
+  uint32_t o_desc;                     // TileDesc[2]: this tile's and the next tile's descriptor
+  uint32_t o_pf;                       // 64 B: LDS-DMA landing of the L2 prefetch (never read)
   uint32_t prefetch;                   // warm L2 with the next tile (small tiles at >= 3 workgroups per CU)
   uint32_t feat;                       // kFeat* families of the launch (selects the kernel instantiation)
   uint32_t o_sa;                       // u32[NSTR]: the tile's staged byte start per string column
@@ -99,7 +100,8 @@ struct TileArgs {
   ChunkArgs chunk[kMaxChunks];
   uint32_t rows_mode;
   uint32_t debug;  // diagnostics: bit0 skip classification, bit1 skip walk, bit2 skip output; 512 phase
-                  // clocks; 1024 skip mandatory labels, 2048 skip label-value DFAs, 4096 skip predecessor ORs
+                  // clocks; 1024 skip mandatory labels, 2048 skip label-value DFAs, 4096 skip predecessor ORs,
+                  // 8192 skip capability mutations (P2), 16384 skip container / label violation words (P2)
   uint32_t lds_bytes;
 };
 

@@ -215,13 +215,17 @@ KW_HD inline uint32_t first_missing_packed(const SlotView& sv, uint32_t s, uint6
 struct ViolSink {
   uint32_t* vw;
   uint32_t* va;  // may be null
+  // (the mask is walked as two 32-bit halves: one find-first-set and one clear per slot)
   KW_HD void put(uint64_t nw, uint32_t reason, uint32_t arg) const {
     const uint32_t w = vword(reason, arg);
-    while (nw) {
-      const uint32_t s = kw_ctz64(nw);
-      vw[s] = w;
-      if (va) va[s] = arg;
-      nw &= nw - 1;
+    for (uint32_t h = 0; h < 2; ++h) {
+      uint32_t m = (uint32_t)(nw >> (32u * h));
+      while (m) {
+        const uint32_t s = 32u * h + (uint32_t)__builtin_ctz(m);
+        vw[s] = w;
+        if (va) va[s] = arg;
+        m &= m - 1u;
+      }
     }
   }
 };

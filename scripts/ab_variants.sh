@@ -13,5 +13,9 @@ for v in policy-server_amd/variants/*.so; do
   KW_TILE_DEBUG=256 KWGPU_LIB="$PWD/$v" timeout -k 10 300 python bench.py --config ${CFG:-c4_64} --no-cpu-baseline --no-host-modes > gpurun_out/${TAG}_${n}.json 2> gpurun_out/${TAG}_${n}.err
   rc=$?; echo "[abv] $n bench rc=$rc $(python -c "import json;d=json.load(open('gpurun_out/${TAG}_${n}.json'));print('evaluate_ms=%.4f' % d['kernel_ms']['evaluate'])" 2>/dev/null) grid=$(grep -o 'grid [0-9]*' gpurun_out/${TAG}_${n}.err | head -1)"
   if [ $rc -ne 0 ]; then tail -3 gpurun_out/${TAG}_${n}.err; exit $rc; fi
+  if [ -n "${PHASE:-}" ]; then  # phase clocks of the diagnostics instantiation
+    KW_TILE_DEBUG=512 KWGPU_LIB="$PWD/$v" timeout -k 10 300 python bench.py --config ${CFG:-c4_64} --steps 2 --warmup 1 --no-cpu-baseline --no-host-modes > /dev/null 2> gpurun_out/${TAG}_${n}_phase.err || exit $?
+    grep "kw phase" gpurun_out/${TAG}_${n}_phase.err | tail -1
+  fi
 done
 echo "[abv] done"
