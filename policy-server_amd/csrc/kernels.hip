@@ -24,11 +24,8 @@
 #include "../../include/kwgpu.h"
 #include "kernels.hpp"
 
-// Build-time variants (A/B): KW_KV_PAIR runs a key's label-value DFAs two at a time; KW_LDS_BARRIER
-// uses LDS-only barriers between the compute phases; KW_MAND_BATCH batches the mandatory-label loads.
-#ifndef KW_KV_PAIR
-#define KW_KV_PAIR 0
-#endif
+// Build-time variants (A/B): KW_LDS_BARRIER uses LDS-only barriers between the compute phases;
+// KW_MAND_BATCH batches the mandatory-label loads.
 #ifndef KW_LDS_BARRIER
 #define KW_LDS_BARRIER 1
 #endif
@@ -282,101 +279,69 @@ __device__ inline void classify_image(const Classifiers& C, const ImgLayout& il,
   for (uint32_t o = C.dfa[COL_IMG].head; o; o = chain_next(C.dfa[COL_IMG], o)) out(j++, image_part(2, chain_view(C.dfa[COL_IMG], o), bytes, r));
 }
 
-// COL_LV classes of a label value under label-key class k (one per DFA of the key's chain; 0xffff
-// fills the rest of the nlv entries). The chain's DFAs run two at a time over the same byte windows,
-// so their transition chains (the only dependent loads) overlap.
-__device__ inline uint32_t kv_trans(const uint8_t* R, const KvDfa& d, uint32_t st, uint32_t c) {
-  // one aligned u16 load serves both table widths (u8 tables: the byte at the even or odd half;
-  // staged regions are padded, so the pair never leaves the region)
-  const uint32_t a = d.trans_off + ((st * d.ncls + c) << d.t16);
-  const uint32_t v = *(const uint16_t*)(R + (a & ~1u));
-  return d.t16 ? v : ((a & 1u) ? (v >> 8) : (v & 0xffu));
-}
+// The region pointer carries its address space (3: LDS, 1: global), so the walk compiles to ds_read /
+// global_load rather than flat loads.
+template <int AS>
+using as_ptr = const __attribute__((address_space(AS))) uint8_t*;
 
-#if KW_KV_PAIR
-template <class Out>
-__device__ inline void classify_value(const Classifiers& C, uint32_t k, uint32_t nlv, const uint8_t* __restrict__ bytes,
-                                      uint32_t b, uint32_t e, Out out) {
+template <int AS, class Out>
+__device__ inline uint32_t classify_value_as(as_ptr<AS> R, uint32_t nlk, uint32_t k, const uint8_t* __restrict__ bytes,
+                                             uint32_t b, uint32_t e, Out out) {
+  typedef const __attribute__((address_space(AS))) uint32_t* u32p;
+  typedef const __attribute__((address_space(AS))) uint16_t* u16p;
   uint32_t j = 0;
-  if (C.kv && k) {
-    const uint8_t* R = C.kv;
-    const uint32_t kbase = ((const uint32_t*)R)[C.nlk + k];
-    for (uint32_t rel = ((const uint32_t*)R)[k]; rel;) {
-      const KvDfa d0 = *(const KvDfa*)(R + rel);
-      const bool two = d0.next != 0;
-      const KvDfa d1 = *(const KvDfa*)(R + (two ? d0.next : rel));  // alone: d0 again, result unused
-      uint32_t s0 = d0.start, s1 = d1.start;
-      // 8-byte windows: the window's dwords, then its byte classes, load as batches; only the
-      // transitions form dependent chains, two of them interleaved (bytes past the string read
-      // the zero tail, unused)
-      for (uint32_t p = b; p < e && (s0 | s1) != 0; p += 8u) {
-        const uint32_t* q = (const uint32_t*)(bytes + (p & ~3u));
-        const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], sh = p & 3u;
-        const uint32_t x0 = align_bytes(q1, q0, sh), x1 = align_bytes(q2, q1, sh);
-        uint32_t c0[8], c1[8];
+  const uint32_t kbase = ((u32p)R)[nlk + k];
+  for (uint32_t rel = ((u32p)R)[k]; rel;) {
+    KvDfa d;  // two 16-B loads (a struct copy cannot bind an address-space-qualified reference)
+    {
+      typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+      typedef const __attribute__((address_space(AS))) v4* v4p;
+      const v4 lo = ((v4p)(R + rel))[0], hi = ((v4p)(R + rel))[1];
+      __builtin_memcpy(&d, &lo, 16);
+      __builtin_memcpy((uint8_t*)&d + 16, &hi, 16);
+    }
+    uint32_t st = d.start;
+    // 8-byte windows: the window's dwords, then its 8 byte classes, load as two batches; only the
+    // transitions form a dependent chain (bytes past the string read the zero tail, unused)
+    for (uint32_t p = b; p < e && st != 0; p += 8u) {
+      const uint32_t* q = (const uint32_t*)(bytes + (p & ~3u));
+      const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], sh = p & 3u;
+      const uint32_t x0 = align_bytes(q1, q0, sh), x1 = align_bytes(q2, q1, sh);
+      uint32_t c[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const uint32_t by = ((i < 4 ? x0 : x1) >> (8 * (i & 3))) & 0xffu;
-          c0[i] = (by < 128u || d0.wide) ? R[d0.cls_off + by] : d0.hi;
-          c1[i] = (by < 128u || d1.wide) ? R[d1.cls_off + by] : d1.hi;
-        }
-        const uint32_t lim = min(8u, e - p);
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t by = ((i < 4 ? x0 : x1) >> (8 * (i & 3))) & 0xffu;
+        c[i] = (by < 128u || d.wide) ? R[d.cls_off + by] : d.hi;
+      }
+      const uint32_t lim = min(8u, e - p);
+      if (d.t16) {
+        const u16p tr = (u16p)(R + d.trans_off);
 #pragma unroll
         for (int i = 0; i < 8; ++i)
-          if ((uint32_t)i < lim) {
-            s0 = kv_trans(R, d0, s0, c0[i]);
-            s1 = kv_trans(R, d1, s1, c1[i]);
-          }
+          if ((uint32_t)i < lim) st = tr[st * d.ncls + c[i]];
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if ((uint32_t)i < lim) st = R[d.trans_off + st * d.ncls + c[i]];
       }
-      out(j++, kbase + d0.cbase + ((const uint16_t*)(R + d0.acc_off))[s0]);
-      if (two) out(j++, kbase + d1.cbase + ((const uint16_t*)(R + d1.acc_off))[s1]);
-      rel = two ? d1.next : 0u;
     }
+    out(j++, kbase + d.cbase + ((u16p)(R + d.acc_off))[st]);
+    rel = d.next;
   }
-  for (; j < nlv; ++j) out(j, 0xffffu);
+  return j;
 }
-#else
+
+// COL_LV classes of a label value under label-key class k: one per DFA of the key's chain, 0xffff
+// fills the rest of the nlv entries. kv_lds: the region is staged in LDS (else the blob in HBM).
 template <class Out>
-__device__ inline void classify_value(const Classifiers& C, uint32_t k, uint32_t nlv, const uint8_t* __restrict__ bytes,
+__device__ inline void classify_value(const Classifiers& C, bool kv_lds, uint32_t k, uint32_t nlv, const uint8_t* __restrict__ bytes,
                                       uint32_t b, uint32_t e, Out out) {
   uint32_t j = 0;
-  if (C.kv && k) {
-    const uint8_t* R = C.kv;
-    const uint32_t kbase = ((const uint32_t*)R)[C.nlk + k];
-    for (uint32_t rel = ((const uint32_t*)R)[k]; rel;) {
-      const KvDfa d = *(const KvDfa*)(R + rel);
-      uint32_t st = d.start;
-      // 8-byte windows: the window's dwords, then its 8 byte classes, load as two batches; only the
-      // transitions form a dependent chain (bytes past the string read the zero tail, unused)
-      for (uint32_t p = b; p < e && st != 0; p += 8u) {
-        const uint32_t* q = (const uint32_t*)(bytes + (p & ~3u));
-        const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], sh = p & 3u;
-        const uint32_t x0 = align_bytes(q1, q0, sh), x1 = align_bytes(q2, q1, sh);
-        uint32_t c[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const uint32_t by = ((i < 4 ? x0 : x1) >> (8 * (i & 3))) & 0xffu;
-          c[i] = (by < 128u || d.wide) ? R[d.cls_off + by] : d.hi;
-        }
-        const uint32_t lim = min(8u, e - p);
-        if (d.t16) {
-          const uint16_t* tr = (const uint16_t*)(R + d.trans_off);
-#pragma unroll
-          for (int i = 0; i < 8; ++i)
-            if ((uint32_t)i < lim) st = tr[st * d.ncls + c[i]];
-        } else {
-#pragma unroll
-          for (int i = 0; i < 8; ++i)
-            if ((uint32_t)i < lim) st = R[d.trans_off + st * d.ncls + c[i]];
-        }
-      }
-      out(j++, kbase + d.cbase + ((const uint16_t*)(R + d.acc_off))[st]);
-      rel = d.next;
-    }
-  }
+  if (C.kv && k)
+    j = kv_lds ? classify_value_as<3>((as_ptr<3>)C.kv, C.nlk, k, bytes, b, e, out)
+               : classify_value_as<1>((as_ptr<1>)C.kv, C.nlk, k, bytes, b, e, out);
   for (; j < nlv; ++j) out(j, 0xffffu);
 }
-#endif
 
 // ------------------------------------------------------------------------------------------
 // Per-chunk violation sets (slots.hpp tables) from stored classes
@@ -700,7 +665,7 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
           if (k && classify && t.o_sb[S_LV] && !(t.debug & 2048u)) {
             uint32_t b, e;
             str(S_LV, i, &b, &e);
-            classify_value(C, k, nlv, lds + t.o_sb[S_LV], b, e, [&](uint32_t j, uint32_t c) { lv[j] = (uint16_t)c; });
+            classify_value(C, LDST && t.kv_lds, k, nlv, lds + t.o_sb[S_LV], b, e, [&](uint32_t j, uint32_t c) { lv[j] = (uint16_t)c; });
           } else {
             for (uint32_t j = 0; j < nlv; ++j) lv[j] = 0xffffu;
           }
@@ -1117,7 +1082,7 @@ __global__ void __launch_bounds__(kOverflowThreads)
         const uint32_t k = lit(COL_LK, S_LK, l);
         a.g_lk[l] = (uint16_t)k;
         uint16_t* lv = a.g_lv + (uint64_t)l * nlv;
-        classify_value(C, k, nlv, t.s_bytes[S_LV], t.s_off[S_LV][l], t.s_off[S_LV][l + 1],
+        classify_value(C, false, k, nlv, t.s_bytes[S_LV], t.s_off[S_LV][l], t.s_off[S_LV][l + 1],
                        [&](uint32_t j, uint32_t c) { lv[j] = (uint16_t)c; });
       }
   }

@@ -126,12 +126,19 @@ struct SlotView {
   KW_HD uint64_t mpack(uint32_t s) const { return ((const uint64_t*)(base + h->o_mpack))[s]; }
 };
 
-// OR of table rows over the set bits of `bits`.
+// OR of table rows over the set bits of `bits` (per 32-bit half, two independent row loads a round).
 KW_HD inline uint64_t tab_or(const uint64_t* t, uint64_t bits) {
   uint64_t r = 0;
-  while (bits) {
-    r |= t[kw_ctz64(bits)];
-    bits &= bits - 1;
+  for (uint32_t h = 0; h < 2; ++h) {
+    uint32_t m = (uint32_t)(bits >> (32u * h));
+    const uint64_t* th = t + 32u * h;
+    while (m) {
+      const uint32_t i = (uint32_t)__builtin_ctz(m);
+      m &= m - 1u;
+      const uint32_t j = m ? (uint32_t)__builtin_ctz(m) : i;
+      m &= m - 1u;
+      r |= th[i] | th[j];
+    }
   }
   return r;
 }
