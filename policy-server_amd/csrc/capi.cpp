@@ -510,7 +510,7 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
       T.o_sa = take(NSTR * 4);
       T.o_nx = take(8);
       T.o_desc = take(2 * sizeof(TileDesc));
-      T.o_pf = take(64);
+      T.o_pf = take(4 * kPfLanes);
       // union: the staged strings (P0-P1) and the violation words (P2-P3)
       const uint32_t u0 = off;
       uint32_t su = u0;

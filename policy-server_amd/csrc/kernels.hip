@@ -38,6 +38,9 @@
 #ifndef KW_PREFETCH  // tile kernel: warm L2 with the next tile's staged ranges during this tile's walk
 #define KW_PREFETCH 1
 #endif
+#ifndef KW_DESC_LDS  // tile kernel: staging reads the tile's descriptor from its LDS copy (else scalar loads)
+#define KW_DESC_LDS 1
+#endif
 #ifndef KW_PF_EARLY  // tile kernel: the L2 prefetch of the next tile right after staging (else after classification)
 #define KW_PF_EARLY 0
 #endif
@@ -414,15 +417,15 @@ __device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_b
 __device__ inline void lds_barrier() { __syncthreads(); }
 #endif
 
-// L2 prefetch of `bytes` at `src`: one dword per 128-B line, by LDS-DMA from lanes 0-15 of each wave
-// into a 64-B scratch line shared by the waves (never read; a DMA lane lands at base + 4 x lane), so
+// L2 prefetch of `bytes` at `src`: one dword per 128-B line, by LDS-DMA from lanes 0..kPfLanes-1 of
+// each wave into a 4 x kPfLanes-byte scratch line shared by the waves (never read; a DMA lane lands at base + 4 x lane), so
 // no VGPR waits for the data and no barrier but the next staging barrier (vmcnt) covers it; the next
 // tile's staging loads then hit L2.
 __device__ inline void prefetch_l2(const void* src, uint32_t bytes, uint8_t* scratch, uint32_t tid) {
   const uint8_t* p = (const uint8_t*)src;
-  if ((tid & 63u) >= 16u) return;
-  const uint32_t q = (tid >> 6) * 16u + (tid & 15u);  // 16 lanes per wave
-  for (uint32_t off = q * 128u; off < bytes; off += (kSlotThreads / 4u) * 128u)
+  if ((tid & 63u) >= kPfLanes) return;
+  const uint32_t q = (tid >> 6) * kPfLanes + (tid & (kPfLanes - 1u));  // kPfLanes lanes per wave
+  for (uint32_t off = q * 128u; off < bytes; off += (kSlotThreads / 64u) * kPfLanes * 128u)
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(p + off),
                                      (__attribute__((address_space(3))) void*)scratch, 4, 0, 0);
 }
@@ -555,18 +558,24 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
     uint32_t nxt2 = 0;
     if (dyn && tid == 0) nxt2 = atomicAdd(cnt, 1u);  // the tile after next (read after the staging barrier)
     if (next < t_hi) fetch_desc(next, cur ^ 1u);      // the next tile's descriptor (slot free since its last read)
+#if KW_DESC_LDS
     const TileDesc& d = l_desc[cur];
-    if (!sfield(d.fits)) {  // queued for the overflow kernels by the host (uniform: no barrier skipped unevenly)
+#define KW_DF(x) sfield(x)
+#else
+    const TileDesc& d = desc[tile];  // scalar loads (the LDS copy serves the prefetch)
+#define KW_DF(x) (x)
+#endif
+    if (!KW_DF(d.fits)) {  // queued for the overflow kernels by the host (uniform: no barrier skipped unevenly)
       if (dyn && tid == 0) l_nx[cur] = nxt2;
       __syncthreads();  // also waits for the next descriptor
       tile = next;
       next = dyn ? t_lo + l_nx[cur] : next + gridDim.x;
       continue;
     }
-    const uint64_t r0 = ((uint64_t)sfield(d.r0hi) << 32) | sfield(d.r0lo);
-    const uint32_t nr = sfield(d.nr);
-    const uint32_t cb = sfield(d.cb), ce = sfield(d.ce), lb = sfield(d.lb), le = sfield(d.le);
-    const uint32_t kab = sfield(d.kab), kae = sfield(d.kae), kdb = sfield(d.kdb), kde = sfield(d.kde);
+    const uint64_t r0 = ((uint64_t)KW_DF(d.r0hi) << 32) | KW_DF(d.r0lo);
+    const uint32_t nr = KW_DF(d.nr);
+    const uint32_t cb = KW_DF(d.cb), ce = KW_DF(d.ce), lb = KW_DF(d.lb), le = KW_DF(d.le);
+    const uint32_t kab = KW_DF(d.kab), kae = KW_DF(d.kae), kdb = KW_DF(d.kdb), kde = KW_DF(d.kde);
     const uint32_t nc = ce - cb, nl = le - lb;
 
     // ---- P0: stage request headers, container offsets and the tile's strings. Every copy is an
@@ -584,10 +593,11 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
       const uint32_t g0 = str_g0(m, (uint32_t)r0, cb, kab, kdb, lb);
       const uint32_t n = str_n(m, nr, nc, kae - kab, kde - kdb, nl);
       glds_dwords(t.s_off[m] + g0, (uint32_t*)(lds + t.o_so[m]), n + 1, tid);  // absolute: rebased by l_sa
-      glds_x4((const u32x4*)(t.s_bytes[m] + sfield(d.sa[m])), (u32x4*)(lds + t.o_sb[m]), sfield(d.nv[m]), tid);
+      glds_x4((const u32x4*)(t.s_bytes[m] + KW_DF(d.sa[m])), (u32x4*)(lds + t.o_sb[m]), KW_DF(d.nv[m]), tid);
     }
     for (uint32_t i = tid; i < nr; i += kSlotThreads) l_rej[i] = l_mut[i] = 0;
     if (tid < NSTR) l_sa[tid] = d.sa[tid];
+#undef KW_DF
     __syncthreads();  // staged tile, the next descriptor and the counter fetch have landed
     mark(0);
     if (timing && tid == 0) ++ph[5];

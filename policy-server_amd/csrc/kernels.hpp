@@ -56,6 +56,10 @@ constexpr uint32_t kSlotRows = 64;
 constexpr uint32_t kSlotThreads = KW_THREADS;
 // Families a tile-kernel instantiation carries (TileArgs::feat).
 constexpr uint32_t kFeatImg = 1, kFeatLbl = 2, kFeatCtr = 4, kFeatGrp = 8, kFeatAll = 15;
+#ifndef KW_PF_LANES  // lanes per wave issuing the next tile's L2 prefetch (its LDS landing line: 4 B each)
+#define KW_PF_LANES 64
+#endif
+constexpr uint32_t kPfLanes = KW_PF_LANES;
 constexpr uint32_t kMaxChunks = 8;  // chunks of one launch (<= 512 slots); longer lists take several launches
 
 struct ChunkArgs {
@@ -81,7 +85,7 @@ struct TileArgs {
   uint32_t o_rej, o_mut, o_byp;        // per-request results: rejected / mutated slots, bypass flag
   uint32_t o_nx;                       // u32[2]: the tile after next (dynamic schedule), double-buffered
   uint32_t o_desc;                     // TileDesc[2]: this tile's and the next tile's descriptor
-  uint32_t o_pf;                       // 64 B: LDS-DMA landing of the L2 prefetch (never read)
+  uint32_t o_pf;                       // 4 x kPfLanes B: LDS-DMA landing of the L2 prefetch (never read)
   uint32_t prefetch;                   // warm L2 with the next tile (small tiles at >= 3 workgroups per CU)
   uint32_t feat;                       // kFeat* families of the launch (selects the kernel instantiation)
   uint32_t o_sa;                       // u32[NSTR]: the tile's staged byte start per string column

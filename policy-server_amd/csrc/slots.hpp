@@ -225,6 +225,15 @@ struct ViolSink {
   // (the mask is walked as two 32-bit halves: one find-first-set and one clear per slot)
   KW_HD void put(uint64_t nw, uint32_t reason, uint32_t arg) const {
     const uint32_t w = vword(reason, arg);
+#ifdef KW_PUT64
+    while (nw) {
+      const uint32_t s = kw_ctz64(nw);
+      vw[s] = w;
+      if (va) va[s] = arg;
+      nw &= nw - 1;
+    }
+    return;
+#endif
     for (uint32_t h = 0; h < 2; ++h) {
       uint32_t m = (uint32_t)(nw >> (32u * h));
       while (m) {
