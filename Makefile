@@ -14,7 +14,7 @@ SRC := $(PKG)/csrc
 OBJ := $(PKG)/build
 HIPDEF := -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include
 CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wextra $(HIPDEF)
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -munsafe-fp-atomics
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -munsafe-fp-atomics $(HIPEXTRA)
 
 HOST_SRCS := json yaml automaton expr env flatten service slotplan metrics capi
 HOST_OBJS := $(addprefix $(OBJ)/,$(addsuffix .o,$(HOST_SRCS)))

@@ -510,7 +510,7 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
       T.o_sa = take(NSTR * 4);
       T.o_nx = take(8);
       T.o_desc = take(2 * sizeof(TileDesc));
-      T.o_pf = take(4 * kPfLanes);
+      T.o_pf = KW_PREFETCH ? take(4 * kPfLanes) : 0u;
       // union: the staged strings (P0-P1) and the violation words (P2-P3)
       const uint32_t u0 = off;
       uint32_t su = u0;
@@ -621,9 +621,10 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
   else
     layout(pick->q[pick->cap_choice]);
   if (T.lds_bytes > kTileLdsBudget) return KW_E_ARG;  // policy list too large for one tile
-  // next-tile L2 prefetch: a gain where several small tiles share a CU (C4: -2.5 %), a loss where two
-  // large ones do (C5: +2.7 %; r02 A/B)
-  T.prefetch = per_cu(T.lds_bytes) >= 3 ? 1u : 0u;
+  // next-tile L2 prefetch (compiled in with KW_PREFETCH, kernels.hpp): a gain where several small
+  // tiles share a CU, a loss where two large ones do (C5: +2.7 %; r02 A/B); off by default since the
+  // descriptor moved to LDS (r02 s60)
+  T.prefetch = KW_PREFETCH && per_cu(T.lds_bytes) >= 3 ? 1u : 0u;
   bool any_grp = false;
   for (const SlotChunk& c : plan->chunks) any_grp = any_grp || c.groups;
   T.feat = ((need & (1u << S_IMG)) ? kFeatImg : 0u) | (any_lbl ? kFeatLbl : 0u) | (any_ctr_fam ? kFeatCtr : 0u) |

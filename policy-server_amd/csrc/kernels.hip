@@ -35,9 +35,6 @@
 #ifndef KW_MAND_BATCH
 #define KW_MAND_BATCH 1
 #endif
-#ifndef KW_PREFETCH  // tile kernel: warm L2 with the next tile's staged ranges during this tile's walk
-#define KW_PREFETCH 1
-#endif
 #ifndef KW_DESC_LDS  // tile kernel: staging reads the tile's descriptor from its LDS copy (else scalar loads)
 #define KW_DESC_LDS 1
 #endif

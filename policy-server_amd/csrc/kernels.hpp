@@ -56,6 +56,9 @@ constexpr uint32_t kSlotRows = 64;
 constexpr uint32_t kSlotThreads = KW_THREADS;
 // Families a tile-kernel instantiation carries (TileArgs::feat).
 constexpr uint32_t kFeatImg = 1, kFeatLbl = 2, kFeatCtr = 4, kFeatGrp = 8, kFeatAll = 15;
+#ifndef KW_PREFETCH  // tile kernel: warm L2 with the next tile's staged ranges during this tile's walk.
+#define KW_PREFETCH 0   // Off: since staging reads the descriptor from LDS, the prefetch costs P2 more
+#endif                  // than it saves P0 (r02 s60: C4 0.3294 vs 0.3442 ms, C6 -1.8 %, C2 +0.6 %)
 #ifndef KW_PF_LANES  // lanes per wave issuing the next tile's L2 prefetch (its LDS landing line: 4 B each)
 #define KW_PF_LANES 64
 #endif
