@@ -884,6 +884,8 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
               }
               nw &= ~lrej;
               rej |= nw;
+              vs.put(nw & SH.mand_one, KW_R_LABEL_MANDATORY, 0);  // single-key lists: index 0, no list read
+              nw &= ~SH.mand_one;
               while (nw) {  // the first missing mandatory key of each such slot (settings order), four per round
                 uint32_t ss[4];
                 uint64_t pk[4];

@@ -215,6 +215,8 @@ struct Builder {
       rec.insert(rec.end(), (const uint8_t*)mand_l, (const uint8_t*)mand_l + std::max<size_t>(mand_local.size(), 1) * 8);
       align();
       h.o_mlist = (uint32_t)rec.size();
+      for (uint32_t s = 0; s < nslots; ++s)
+        if (mlist[s].size() == 1) h.mand_one |= 1ull << s;
       rec.resize(rec.size() + 4u * std::max<uint32_t>(nslots, 1), 0);
       for (uint32_t s = 0; s < nslots; ++s) {
         const uint32_t at = (uint32_t)rec.size();

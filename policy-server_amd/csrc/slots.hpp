@@ -51,7 +51,7 @@ struct alignas(16) SlotHdr {
   // local bits (per chunk): capabilities some slot requires dropped / adds by default ("ALL" always
   // has one when the chunk has psp-capabilities slots), and mandatory label keys
   uint64_t reqd_union, defa_union, all_bit, mand_union;
-  uint64_t pad0;
+  uint64_t mand_one;  // slots whose mandatory list is a single key (its absence: index 0)
   uint32_t ncols, nslots, bytes, staged;  // bytes: whole record; staged: prefix the device keeps in LDS
   uint32_t tab_off[NTAB];                 // byte offset of each class table (0 = not emitted)
   uint32_t o_capmb, o_lkmb;               // u8 per COL_CAP / COL_LK class: its local bit, 0xff = none
