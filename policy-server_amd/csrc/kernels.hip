@@ -988,7 +988,35 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
             const Cols4 c4 = load4(g);
             uint32_t* dst = out + (r0 + (tid >> lg)) * npol + CA.col0 + 4 * g;
             const uint64_t dstep = (uint64_t)step * npol;
-            for (uint32_t rr = tid >> lg; rr < nr; rr += step, dst += dstep) emit(rr, g, c4, dst);
+            if (!GRP) {
+              // branch-free words: the thread's four columns are loop-invariant; every row reads its
+              // four violation words whether or not the slot rejected, then selects
+              const uint32_t cs0 = (c4.ks.x >> 8) & 63u, cs1 = (c4.ks.y >> 8) & 63u, cs2 = (c4.ks.z >> 8) & 63u,
+                             cs3 = (c4.ks.w >> 8) & 63u;
+              const bool pl0 = (c4.ks.x & 0xffu) == CK_PLAIN, pl1 = (c4.ks.y & 0xffu) == CK_PLAIN,
+                         pl2 = (c4.ks.z & 0xffu) == CK_PLAIN, pl3 = (c4.ks.w & 0xffu) == CK_PLAIN;
+              for (uint32_t rr = tid >> lg; rr < nr; rr += step, dst += dstep) {
+                const uint64_t rej = l_rej[rr], mut = l_mut[rr];
+                const uint32_t byp = l_byp[rr];
+                const uint32_t* vw = l_vw + rr * t.vw_stride;
+                const uint32_t a0 = vw[cs0], a1 = vw[cs1], a2 = vw[cs2], a3 = vw[cs3];
+                auto one = [&](bool pl, uint32_t cs, uint32_t av, uint32_t okw, uint32_t mutw, uint32_t rejb) -> uint32_t {
+                  const uint32_t rb = (uint32_t)(rej >> cs) & 1u, mb = (uint32_t)(mut >> cs) & 1u;
+                  const uint32_t w = rb ? (rejb | av) : (mb ? mutw : okw);
+                  return pl ? w : okw;  // (not plain: a constant column)
+                };
+                u32x4 wv = {one(pl0, cs0, a0, c4.ok.x, c4.mu.x, c4.rj.x), one(pl1, cs1, a1, c4.ok.y, c4.mu.y, c4.rj.y),
+                            one(pl2, cs2, a2, c4.ok.z, c4.mu.z, c4.rj.z), one(pl3, cs3, a3, c4.ok.w, c4.mu.w, c4.rj.w)};
+                if (byp) wv = u32x4{kBypassWord, kBypassWord, kBypassWord, kBypassWord};
+#if KW_NT_STORE
+                __builtin_nontemporal_store(wv, (u32x4*)dst);  // streamed once
+#else
+                *(u32x4*)dst = wv;
+#endif
+              }
+            } else {
+              for (uint32_t rr = tid >> lg; rr < nr; rr += step, dst += dstep) emit(rr, g, c4, dst);
+            }
           } else {
             for (uint32_t q = tid; q < nr * G; q += kSlotThreads) {
               const uint32_t rr = q / G, g = q - rr * G;
