@@ -308,12 +308,43 @@ __device__ inline uint32_t classify_value_as(as_ptr<AS> R, uint32_t nlk, uint32_
       const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], sh = p & 3u;
       const uint32_t x0 = align_bytes(q1, q0, sh), x1 = align_bytes(q2, q1, sh);
       uint32_t c[8];
+      const uint32_t lim = min(8u, e - p);
+      if constexpr (AS == 3) {
+        // LDS region: branch-free (every class load and step of the window runs; `fin` keeps the
+        // state after the lane's last byte; a step no lane of the wave needs ends the window). The
+        // global-table form below keeps its masked steps: extra lanes' gathers cost L2 bandwidth.
+        const uint32_t bm = d.wide ? 255u : 127u;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const uint32_t by = ((i < 4 ? x0 : x1) >> (8 * (i & 3))) & 0xffu;
+          const uint32_t cl = R[d.cls_off + (by & bm)];
+          c[i] = by <= bm ? cl : (uint32_t)d.hi;
+        }
+        uint32_t fin = st;
+        if (d.t16) {
+          const u16p tr = (u16p)(R + d.trans_off);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            if (i > 0 && !__any((uint32_t)i < lim)) break;
+            st = tr[st * d.ncls + c[i]];
+            fin = (uint32_t)i < lim ? st : fin;
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            if (i > 0 && !__any((uint32_t)i < lim)) break;
+            st = R[d.trans_off + st * d.ncls + c[i]];
+            fin = (uint32_t)i < lim ? st : fin;
+          }
+        }
+        st = fin;
+        continue;
+      }
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const uint32_t by = ((i < 4 ? x0 : x1) >> (8 * (i & 3))) & 0xffu;
         c[i] = (by < 128u || d.wide) ? R[d.cls_off + by] : d.hi;
       }
-      const uint32_t lim = min(8u, e - p);
       if (d.t16) {
         const u16p tr = (u16p)(R + d.trans_off);
 #pragma unroll
