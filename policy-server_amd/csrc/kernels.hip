@@ -38,6 +38,9 @@
 #ifndef KW_DESC_LDS  // tile kernel: staging reads the tile's descriptor from its LDS copy (else scalar loads)
 #define KW_DESC_LDS 1
 #endif
+#ifndef KW_SWAR_PARSE  // image references scanned four bytes a step (per-byte match masks)
+#define KW_SWAR_PARSE 1
+#endif
 #ifndef KW_PF_EARLY  // tile kernel: the L2 prefetch of the next tile right after staging (else after classification)
 #define KW_PF_EARLY 0
 #endif
@@ -185,6 +188,39 @@ __device__ ImageRef parse_image(const uint8_t* __restrict__ bytes, uint32_t b, u
   const uint32_t NONE = 0xffffffffu;
   uint32_t at = NONE, slash0 = NONE, slash1 = NONE, last_colon = NONE;
   bool dotcolon = false;
+#if KW_SWAR_PARSE
+  // four bytes a step: per-byte match masks (bit 7 of each byte) of '@', '/', ':' and '.', exact
+  // (no borrow between bytes), restricted to the string and cut at the first '@'
+  auto eqb = [](uint32_t x, uint32_t c4) -> uint32_t {
+    const uint32_t y = x ^ c4;
+    return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y | 0x7F7F7F7Fu);
+  };
+  for (uint32_t p0 = b & ~3u; p0 < e; p0 += 4u) {
+    const uint32_t w = *(const uint32_t*)(bytes + p0);
+    const uint32_t lo = p0 < b ? b - p0 : 0u, hi = min(4u, e - p0);  // valid bytes [lo, hi)
+    const uint32_t vm = (0x80808080u << (8u * lo)) & (hi >= 4u ? 0xffffffffu : ((1u << (8u * hi)) - 1u));
+    uint32_t m_at = eqb(w, 0x40404040u) & vm, m_sl = eqb(w, 0x2f2f2f2fu) & vm;
+    uint32_t m_co = eqb(w, 0x3a3a3a3au) & vm, m_dt = eqb(w, 0x2e2e2e2eu) & vm;
+    if (m_at) {  // the digest starts here: nothing at or after the '@' counts
+      const uint32_t keep = (1u << __builtin_ctz(m_at)) - 1u;
+      at = p0 + (uint32_t)__builtin_ctz(m_at) / 8u;
+      m_sl &= keep;
+      m_co &= keep;
+      m_dt &= keep;
+    }
+    if (m_co) last_colon = p0 + (31u - (uint32_t)__builtin_clz(m_co)) / 8u;
+    if (slash0 == NONE) {
+      const uint32_t before = m_sl ? (1u << __builtin_ctz(m_sl)) - 1u : 0xffffffffu;  // bytes before the first '/'
+      if ((m_co | m_dt) & before) dotcolon = true;
+      if (m_sl) {
+        slash0 = p0 + (uint32_t)__builtin_ctz(m_sl) / 8u;
+        m_sl &= m_sl - 1u;
+      }
+    }
+    if (slash1 == NONE && m_sl) slash1 = p0 + (uint32_t)__builtin_ctz(m_sl) / 8u;
+    if (m_at) break;
+  }
+#else
   uint32_t p = b;
   bool stop = false;
   while (p < e && !stop) {
@@ -213,6 +249,7 @@ __device__ ImageRef parse_image(const uint8_t* __restrict__ bytes, uint32_t b, u
     }
     p += lim;
   }
+#endif
   ImageRef r;
   r.b = b;
   r.e = e;
