@@ -625,6 +625,9 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
   // tiles share a CU, a loss where two large ones do (C5: +2.7 %; r02 A/B); off by default since the
   // descriptor moved to LDS (r02 s60)
   T.prefetch = KW_PREFETCH && per_cu(T.lds_bytes) >= 3 ? 1u : 0u;
+  // predecessor ranges four loads a round where tiles hold many containers per request (C5 -6 %;
+  // C4, two per request, keeps the plain loops: r02 s80)
+  T.ctr_ranges = T.cmax > 4u * T.rows ? 1u : 0u;
   bool any_grp = false;
   for (const SlotChunk& c : plan->chunks) any_grp = any_grp || c.groups;
   T.feat = ((need & (1u << S_IMG)) ? kFeatImg : 0u) | (any_lbl ? kFeatLbl : 0u) | (any_ctr_fam ? kFeatCtr : 0u) |

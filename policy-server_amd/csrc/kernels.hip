@@ -431,6 +431,21 @@ __device__ inline uint64_t dv_image(const SlotView& sv, const ImgLayout& il, uin
   return (why[0] | why[1] | why[2] | why[3] | why[4]) & sv.h->trs;
 }
 
+// OR of a[lo, hi), four loads a round issued together (guarded: a short range costs one round, not
+// one dependent loop trip per element). Used for a container's predecessors when tiles carry many containers per request
+// (TileArgs::ctr_ranges: C5's skewed counts, -6 %; C4 +0.8 % with this form, so not there).
+__device__ inline uint64_t or_range(const uint64_t* a, uint32_t lo, uint32_t hi) {
+  uint64_t r = 0;
+  for (uint32_t j = lo; j < hi; j += 4u) {
+    uint64_t x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) x[u] = a[j + (uint32_t)u < hi ? j + (uint32_t)u : lo];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) r |= j + (uint32_t)u < hi ? x[u] : 0ull;
+  }
+  return r;
+}
+
 // ------------------------------------------------------------------------------------------
 // The tile kernel
 // ------------------------------------------------------------------------------------------
@@ -859,13 +874,21 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
             const bool capv = CTR && SH.caps != 0;
             const uint32_t ka0 = l_cadd[c0] - kab, ka = l_cadd[i] - kab, ka1 = l_cadd[i + 1] - kab;
             uint64_t pre = 0, own = vset(i);
-            if (!(t.debug & 4096u)) {
-              for (uint32_t j = c0; j < i; ++j) pre |= vset(j);
+            if (t.ctr_ranges) {  // many containers per request: the ranges four loads a round
+              pre = (CTR ? or_range(l_vc, c0, i) : 0ull) | (trs ? or_range(l_vtr, c0, i) : 0ull);
+              if (capv) {
+                pre |= or_range(l_vadd, ka0, ka);
+                own |= or_range(l_vadd, ka, ka1);
+              }
+            } else {
+              if (!(t.debug & 4096u)) {
+                for (uint32_t j = c0; j < i; ++j) pre |= vset(j);
+                if (capv)
+                  for (uint32_t k = ka0; k < ka; ++k) pre |= l_vadd[k];
+              }
               if (capv)
-                for (uint32_t k = ka0; k < ka; ++k) pre |= l_vadd[k];
+                for (uint32_t k = ka; k < ka1; ++k) own |= l_vadd[k];
             }
-            if (capv)
-              for (uint32_t k = ka; k < ka1; ++k) own |= l_vadd[k];
             const uint64_t nv = own & ~pre;
             const uint32_t ci = i - c0;
             uint32_t* vw = l_vw + q * t.vw_stride;
