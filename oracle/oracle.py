@@ -84,6 +84,21 @@ class _Obj(list):
         return default
 
 
+_REQ_FIELDS = ("uid", "kind", "resource", "subResource", "requestKind", "requestResource", "requestSubResource", "name",
+               "namespace", "operation", "userInfo", "object", "oldObject", "dryRun", "options")
+_GVK, _GVR = ("group", "version", "kind"), ("group", "version", "resource")
+
+
+def _dup_field(obj, fields):
+    seen = set()
+    for k, _ in obj:
+        if k in fields:
+            if k in seen:
+                return True
+            seen.add(k)
+    return False
+
+
 def _loads_pairs(text):
     return json.loads(text, object_pairs_hook=_Obj)
 
@@ -108,6 +123,19 @@ def flatten_doc(text, raw=False):
         return None
     req = d.get("request")
     is_str = lambda v: isinstance(v, str)
+    # serde-derived structs refuse a repeated known field (AdmissionReviewRequest / RawReviewRequest,
+    # AdmissionRequest, GroupVersionKind / Resource, UserInfo); serde_json::Value members (object,
+    # oldObject, a raw request) keep the last one
+    if _dup_field(d, ("request",) if raw else ("request", "kind", "apiVersion")):
+        return None
+    if not raw and isinstance(req, _Obj):
+        if _dup_field(req, _REQ_FIELDS):
+            return None
+        for k, fields in (("kind", _GVK), ("requestKind", _GVK), ("resource", _GVR), ("requestResource", _GVR),
+                          ("userInfo", ("username", "uid", "groups", "extra"))):
+            v = req.get(k)
+            if isinstance(v, _Obj) and _dup_field(v, fields):
+                return None
     if not raw:
         for k in ("kind", "apiVersion"):
             if d.get(k) is not None and not is_str(d.get(k)):

@@ -101,12 +101,9 @@ void parallel_copy(void* dst, const void* src, size_t bytes) {
 // Requests per tile of the tile kernel forced by KW_SLOT_ROWS (8..255, A/B knob), 0 = chosen per
 // batch (plan_pass: kSlotRows, or taller tiles where they keep enough workgroups per CU).
 uint32_t slot_rows_forced() {
-  static const uint32_t r = [] {
-    const char* e = getenv("KW_SLOT_ROWS");
-    const int v = e ? atoi(e) : 0;
-    return (v >= 8 && v <= 255) ? (uint32_t)v : 0u;  // tile-local owners are u8
-  }();
-  return r;
+  const char* e = getenv("KW_SLOT_ROWS");  // read per pass (tests switch it between passes)
+  const int v = e ? atoi(e) : 0;
+  return (v >= 8 && v <= 255) ? (uint32_t)v : 0u;  // tile-local owners are u8
 }
 
 // Per-tile entity counts and staged byte ranges of a batch, reduced to a high quantile (tile_quantile).
@@ -886,6 +883,11 @@ int run_pass(kw_batch* kb, PassPlan& plan, bool timed, hipStream_t s) {
   }
   if (int rc = upload_tile_descs(B, &D, plan.geom, s)) return rc;
   A.ndesc = D.ndesc;
+  // tests: KW_POISON_VERDICTS fills the verdict words with a sentinel no verdict word equals
+  // (reason byte 0xA5) before the pass, so a tile the schedule never ran shows up as a mismatch
+  // instead of keeping an earlier pass's words
+  if (const char* pz = getenv("KW_POISON_VERDICTS"); pz && atoi(pz) != 0)
+    HIPCHK(hipMemsetAsync(D.verdicts, 0xA5, D.last_verdicts * sizeof(uint32_t), s));
   // dynamic tile schedule (per-XCD counters); KW_SCHED=static selects the strided schedule (A/B)
   static const bool dyn = !(getenv("KW_SCHED") && std::string(getenv("KW_SCHED")) == "static");
   if (dyn && !D.sched) {

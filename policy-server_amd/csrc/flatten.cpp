@@ -234,6 +234,25 @@ bool req_object(const JDoc& d, int64_t n, const char* key, const std::string_vie
   return true;
 }
 
+// serde's derived structs (AdmissionReviewRequest, AdmissionRequest and its typed members, the
+// raw review's envelope) refuse a repeated known field; `object` / `oldObject` / a raw request are
+// serde_json::Value, where the last duplicate wins (JDoc::pick). `at`: the field path prefix.
+bool no_dup(const JDoc& d, int64_t obj, const std::string_view* keys, int nkeys, const char* at, std::string* err) {
+  if (obj < 0) return true;
+  const int q = d.dup_field((uint32_t)obj, keys, nkeys);
+  if (q < 0) return true;
+  *err = std::string("Failed to deserialize the JSON body into the target type: ") + at + "duplicate field `" +
+         std::string(keys[q]) + "`";
+  return false;
+}
+// AdmissionRequest's fields (k8s admission/v1, policy-evaluator's AdmissionRequest) and those of its
+// typed members
+constexpr std::string_view kReqFields[] = {"uid",         "kind",        "resource", "subResource", "requestKind",
+                                           "requestResource", "requestSubResource", "name", "namespace", "operation",
+                                           "userInfo",    "object",      "oldObject", "dryRun",     "options"};
+constexpr std::string_view kUserInfo[] = {"username", "uid", "groups", "extra"};
+constexpr std::string_view kGvkF[] = {"group", "version", "kind"}, kGvrF[] = {"group", "version", "resource"};
+
 bool opt_string(const JDoc& d, int64_t n, const char* key, std::string* err) {
   if (n < 0 || d.is((uint32_t)n, JType::Null) || d.is((uint32_t)n, JType::Str)) return true;
   *err = bad_type(key, "a string");
@@ -261,6 +280,7 @@ bool flatten_document(const char* doc, size_t len, int doc_kind, Batch* b, std::
     *err = "Failed to deserialize the JSON body into the target type: missing field `request`";
     return false;
   }
+  if (!no_dup(d, 0, kTop, doc_kind == KW_DOC_RAW_REVIEW ? 1 : 3, "", err)) return false;
   int64_t rk[RK_N];
   if (d.is((uint32_t)req, JType::Obj)) {
     d.pick((uint32_t)req, kReqKeys, RK_N, rk);
@@ -270,6 +290,17 @@ bool flatten_document(const char* doc, size_t len, int doc_kind, Batch* b, std::
   if (doc_kind == KW_DOC_RAW_REVIEW) {
     flatten_request(d, req, rk, true, b);
     return true;
+  }
+  if (!no_dup(d, req, kReqFields, 15, "request: ", err)) return false;
+  {
+    static constexpr std::string_view kSub[4] = {"kind", "requestKind", "resource", "requestResource"};
+    int64_t sub[4];
+    d.pick((uint32_t)req, kSub, 4, sub);
+    if (!no_dup(d, sub[0], kGvkF, 3, "request.kind: ", err) || !no_dup(d, sub[1], kGvkF, 3, "request.requestKind: ", err) ||
+        !no_dup(d, sub[2], kGvrF, 3, "request.resource: ", err) ||
+        !no_dup(d, sub[3], kGvrF, 3, "request.requestResource: ", err) ||
+        !no_dup(d, rk[RK_USERINFO], kUserInfo, 4, "request.userInfo: ", err))
+      return false;
   }
   if (!opt_string(d, top[1], "kind", err) || !opt_string(d, top[2], "apiVersion", err)) {
     err->replace(err->find("request."), 8, "");  // top-level fields

@@ -380,6 +380,23 @@ void JDoc::pick(uint32_t obj, const std::string_view* keys, int nkeys, int64_t* 
   }
 }
 
+int JDoc::dup_field(uint32_t obj, const std::string_view* keys, int nkeys) const {
+  const JNode& n = nodes_[obj];
+  if (n.t != JType::Obj) return -1;
+  uint32_t seen = 0;
+  uint32_t m = obj + 1;
+  for (uint32_t j = 0; j < n.c; ++j, m = nodes_[m].next) {
+    const uint32_t kl = nodes_[m].key_len;
+    for (int q = 0; q < nkeys; ++q) {
+      if (keys[q].size() != kl || key(m) != keys[q]) continue;
+      if (seen & (1u << q)) return q;
+      seen |= 1u << q;
+      break;
+    }
+  }
+  return -1;
+}
+
 void json_escape(std::string* out, std::string_view s) {
   static const char* hexd = "0123456789abcdef";
   out->push_back('"');

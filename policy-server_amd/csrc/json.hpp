@@ -70,10 +70,13 @@ class JDoc {
     It end() const { return {nodes, 0, 0}; }
   };
   Members members(uint32_t i) const { return {nodes_.data(), i + 1, count(i)}; }
-  // Object member lookup; serde keeps the last of duplicate keys, so does this.
+  // Object member lookup; serde_json::Value keeps the last of duplicate keys, so does this.
   int64_t get(uint32_t obj, std::string_view key) const;
   // One pass over an object's members: out[k] = node of the last member named keys[k], or -1.
   void pick(uint32_t obj, const std::string_view* keys, int nkeys, int64_t* out) const;
+  // Index of the first of keys[0..nkeys) (nkeys <= 32) that object obj holds more than once, -1 if
+  // none: serde's derived structs refuse a repeated known field ("duplicate field").
+  int dup_field(uint32_t obj, const std::string_view* keys, int nkeys) const;
   bool is(uint32_t i, JType t) const { return nodes_[i].t == t; }
   void clear();
 

@@ -875,11 +875,11 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
             const uint32_t ka0 = l_cadd[c0] - kab, ka = l_cadd[i] - kab, ka1 = l_cadd[i + 1] - kab;
             uint64_t pre = 0, own = vset(i);
             if (t.ctr_ranges) {  // many containers per request: the ranges four loads a round
-              pre = (CTR ? or_range(l_vc, c0, i) : 0ull) | (trs ? or_range(l_vtr, c0, i) : 0ull);
-              if (capv) {
-                pre |= or_range(l_vadd, ka0, ka);
-                own |= or_range(l_vadd, ka, ka1);
+              if (!(t.debug & 4096u)) {  // (ablation bit 4096: no predecessor ORs, in both forms)
+                pre = (CTR ? or_range(l_vc, c0, i) : 0ull) | (trs ? or_range(l_vtr, c0, i) : 0ull);
+                if (capv) pre |= or_range(l_vadd, ka0, ka);
               }
+              if (capv) own |= or_range(l_vadd, ka, ka1);
             } else {
               if (!(t.debug & 4096u)) {
                 for (uint32_t j = c0; j < i; ++j) pre |= vset(j);

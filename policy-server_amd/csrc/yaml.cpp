@@ -13,6 +13,7 @@
 #include "yaml.hpp"
 
 #include <cctype>
+#include <cerrno>
 #include <cmath>
 #include <cstdlib>
 #include <string>
@@ -70,7 +71,7 @@ struct Parser {
     std::string cur;
     for (size_t k = 0; k <= n; ++k) {
       if (k == n || s[k] == '\n') {
-        raw.push_back(cur);
+        if (k < n || !cur.empty()) raw.push_back(cur);  // text ending in a newline: no empty last line
         cur.clear();
       } else {
         cur.push_back(s[k]);
@@ -117,7 +118,19 @@ struct Parser {
     }
     for (size_t j = k; j < s.size(); ++j)
       if (!isdigit((unsigned char)s[j])) return false;
+    errno = 0;
     *v = strtoll(s.c_str(), nullptr, 10);
+    return errno != ERANGE;  // beyond i64: the exact digits instead (plain())
+  }
+  // A decimal integer beyond i64 as its exact JSON number text (no '+', no leading zeros); the
+  // hexadecimal / octal forms must fit i64.
+  static bool big_decimal(const std::string& s, std::string* out) {
+    size_t k = (s[0] == '+' || s[0] == '-') ? 1 : 0;
+    if (k >= s.size() || s.compare(k, 2, "0x") == 0 || s.compare(k, 2, "0o") == 0) return false;
+    for (size_t j = k; j < s.size(); ++j)
+      if (!isdigit((unsigned char)s[j])) return false;
+    while (k + 1 < s.size() && s[k] == '0') ++k;
+    *out = (s[0] == '-' ? "-" : "") + s.substr(k);
     return true;
   }
   static bool is_float(const std::string& s) {
@@ -151,6 +164,8 @@ struct Parser {
     if (s == "false" || s == "False" || s == "FALSE") return "false";
     long long v;
     if (is_int(s, &v)) return std::to_string(v);
+    std::string big;
+    if (big_decimal(s, &big)) return big;
     if (is_float(s)) {
       std::string t = s;
       if (t[0] == '+') t = t.substr(1);
@@ -377,11 +392,13 @@ struct Parser {
       put_str(o, t);
       return true;
     }
-    // plain scalar, possibly continued on more-indented lines (folded with spaces)
+    // plain scalar, possibly continued on more-indented lines (folded with spaces). ": " inside it
+    // would start a mapping where none may begin (`key: a: b`): an error, as in libyaml/serde_yaml.
     std::string t = v;
     while (i < lines.size() && lines[i].indent > indent && key_colon(lines[i].text) == std::string::npos &&
            !is_seq(lines[i].text))
       t += " " + lines[i++].text;
+    if (t.find(": ") != std::string::npos || t.back() == ':') return fail("mapping values are not allowed in this context", no);
     o->append(plain(t));
     return true;
   }
@@ -419,15 +436,30 @@ struct Parser {
       body.pop_back();
       ++trailing;
     }
+    // Line breaks between content lines L1 and L2 with e empty lines between them: literal keeps
+    // e + 1 of them; folded (YAML 1.2 §8.1.3) turns the break after L1 into a space when e = 0 and
+    // drops it otherwise (the e empty lines give e newlines), unless L1 or L2 is more indented
+    // (starts with a space), whose breaks are kept. Leading empty lines are kept as newlines.
     std::string s;
-    for (size_t q = 0; q < body.size(); ++q) {
-      if (q) {
-        const bool more = !body[q].empty() && body[q][0] == ' ';
-        const bool prev_more = !body[q - 1].empty() && body[q - 1][0] == ' ';
-        if (folded && !body[q].empty() && !body[q - 1].empty() && !more && !prev_more) s.push_back(' ');
-        else s.push_back('\n');
+    size_t q = 0, empties = 0;
+    while (q < body.size() && body[q].empty()) {
+      s.push_back('\n');
+      ++q;
+    }
+    const std::string* prev = nullptr;
+    for (; q < body.size(); ++q) {
+      if (body[q].empty()) {
+        ++empties;
+        continue;
       }
+      if (prev) {
+        const bool more = body[q][0] == ' ', prev_more = (*prev)[0] == ' ';
+        if (folded && !more && !prev_more) s.append(empties ? std::string(empties, '\n') : std::string(" "));
+        else s.append(std::string(empties + 1, '\n'));
+      }
+      empties = 0;
       s += body[q];
+      prev = &body[q];
     }
     if (chomp == 'c' && !body.empty()) s.push_back('\n');
     if (chomp == 'k') s.append(std::string(trailing + (body.empty() ? 0 : 1), '\n'));

@@ -1,8 +1,8 @@
 """Multi-GPU plumbing: the compiled-table blob is built once on rank 0 and broadcast
 to every rank (RCCL over xGMI with the "nccl" backend; gloo on CPU in the tests); each rank then
 evaluates its own contiguous request shard, with shard boundaries balanced by work (requests plus
-containers); the verdict words are gathered back into disjoint slices of one host array after the
-passes. There is no collective on the per-request path."""
+containers); after the passes each rank copies its verdict words D2H into its own disjoint slice of
+one shared host array (a file mapping). There is no collective on the per-request path."""
 import ctypes as C
 
 import numpy as np
@@ -67,26 +67,71 @@ def balanced_shard(config, rows_per_rank, world, rank, seed):
     return int(b[rank]), int(b[rank + 1] - b[rank])
 
 
-def gather_verdicts(verdicts, bounds, npol, dist, rank, world, tensor_device="cpu"):
-    """Gathers every rank's verdict words (its shard's rows x npol, row-major) into disjoint slices
-    of one host array on rank 0 (rows [bounds[k], bounds[k + 1]) from rank k); returns it on rank 0
-    and None elsewhere. Shards may differ in size: each sends a zero-padded buffer of the largest
-    shard (one gather; RCCL over xGMI when tensor_device is a GPU)."""
+def _gather_dirs():
+    import tempfile
+
+    return ("/dev/shm", tempfile.gettempdir())
+
+
+def _gather_dir(total_bytes):
+    """Index into _gather_dirs() of the first file system with room for the job's verdict array:
+    /dev/shm (tmpfs, shared pages), else the temp directory (page-cache backed); -1 when neither."""
+    import os
+
+    for k, d in enumerate(_gather_dirs()):
+        try:
+            st = os.statvfs(d)
+        except OSError:
+            continue
+        if st.f_bavail * st.f_frsize >= total_bytes + (256 << 20):
+            return k
+    return -1
+
+
+def gather_verdicts(source, bounds, npol, dist, rank, world, tensor_device="cpu", chunk_words=1 << 24):
+    """The job's verdict words in one host array on rank 0: rows [bounds[k],
+    bounds[k + 1]) come from rank k, which copies its shard (a device Batch after its pass, through
+    kw_batch_verdicts' pinned bounce, or a host uint32 array, `chunk_words` at a time) straight
+    into its own disjoint slice of one shared file mapping, so no rank holds a second copy and no
+    verdict word crosses RCCL or any other collective: two broadcast int64s (the file's token and
+    directory) and one barrier. Returns the (rows, npol) array on rank 0 (pages of the unlinked
+    file) and None elsewhere. Raises RuntimeError when no file system has room for the words."""
+    import os
+
     import torch
 
-    sizes = [int(bounds[k + 1] - bounds[k]) * npol for k in range(world)]
-    mine = np.asarray(verdicts, dtype=np.uint32).reshape(-1)
-    if mine.size != sizes[rank]:
-        raise ValueError(f"rank {rank}: {mine.size} verdict words, shard holds {sizes[rank]}")
-    cap = max(max(sizes), 1)
-    send = torch.zeros(cap, dtype=torch.int32, device=tensor_device)
-    send[: mine.size].copy_(torch.from_numpy(mine.view(np.int32)))
-    recv = [torch.empty(cap, dtype=torch.int32, device=tensor_device) for _ in range(world)] if rank == 0 else None
-    dist.gather(send, recv, dst=0)
+    total_words = int(bounds[world] - bounds[0]) * npol
+    a = int(bounds[rank] - bounds[0]) * npol
+    n = int(bounds[rank + 1] - bounds[rank]) * npol
+    tok = [0, -1]
+    if rank == 0:  # rank 0 names, places and sizes the file (sparse until the ranks write)
+        tok = [(os.getpid() << 24) | int.from_bytes(os.urandom(3), "little"), _gather_dir(total_words * 4)]
+        if tok[1] >= 0:
+            name = os.path.join(_gather_dirs()[tok[1]], f"kwgpu_verdicts_{tok[0]}.u32")
+            with open(name, "wb") as f:
+                f.truncate(max(total_words, 1) * 4)
+    t = torch.tensor(tok, dtype=torch.int64, device=tensor_device)
+    dist.broadcast(t, 0)
+    tok = [int(x) for x in t.cpu().tolist()]
+    if tok[1] < 0:
+        raise RuntimeError(f"no file system has room for {total_words * 4 / 1e9:.1f} GB of verdict words")
+    name = os.path.join(_gather_dirs()[tok[1]], f"kwgpu_verdicts_{tok[0]}.u32")
+    mm = np.memmap(name, dtype=np.uint32, mode="r+", shape=(max(total_words, 1),))
+    mine = mm[a:a + n]
+    if isinstance(source, np.ndarray):
+        src = np.asarray(source, dtype=np.uint32).reshape(-1)
+        if src.size != n:
+            raise ValueError(f"rank {rank}: {src.size} verdict words, shard holds {n}")
+        for c in range(0, n, chunk_words):
+            mine[c:c + chunk_words] = src[c:c + chunk_words]
+    elif n:
+        source.verdicts(count=n, out=mine)  # one D2H (pinned bounce) into the shared pages
+    mm.flush()
+    del mine
+    dist.barrier()  # every slice written
     if rank != 0:
+        del mm
         return None
-    out = np.empty(int(bounds[world] - bounds[0]) * npol, dtype=np.uint32)
-    for k in range(world):
-        a = int(bounds[k] - bounds[0]) * npol
-        out[a: a + sizes[k]] = recv[k][: sizes[k]].cpu().numpy().view(np.uint32)
+    os.unlink(name)  # the mapping outlives the name
+    out = mm[:total_words]
     return out.reshape(-1, npol) if npol else out

@@ -8,8 +8,9 @@
   one batch generated at once (no cross-rank state, no data-path collective);
 * each rank EVALUATES its shard with its own environment (rank 1: the deserialized blob) through
   the slot compiler's host walk (kw_debug_host_walk: the device kernel's tables and walks on the
-  host), the verdict words are gathered into disjoint slices of one array on rank 0
-  (kwgpu.dist.gather_verdicts), and that array equals the oracle's verdicts for the whole job.
+  host), each rank copies its verdict words into its own disjoint slice of one shared host array
+  (kwgpu.dist.gather_verdicts: a /dev/shm file mapping, written in chunks, no collective carrying
+  verdict words), and rank 0's array equals the oracle's verdicts for the whole job.
 """
 import os
 import socket
@@ -61,8 +62,10 @@ def _worker(rank, world, port, out_dir):
         with open(os.path.join(out_dir, f"uids{rank}.txt"), "wb") as f:
             f.write(b"\n".join(_strings(soa.uid, n)))
         verdicts = syn.batch().debug_host_walk(env, ids)
-        gathered = gather_verdicts(verdicts, bounds, len(ids), dist, rank, world)
+        # each rank's words go straight into its slice of one shared file mapping, 1000 words a copy
+        gathered = gather_verdicts(verdicts, bounds, len(ids), dist, rank, world, chunk_words=1000)
         if rank == 0:
+            assert not [f for f in os.listdir("/dev/shm") if f.startswith("kwgpu_verdicts_")]  # name unlinked
             np.save(os.path.join(out_dir, "gathered.npy"), gathered)
             np.save(os.path.join(out_dir, "bounds.npy"), bounds)
         else:

@@ -6,6 +6,7 @@ import numpy as np
 import pytest
 
 import kwgpu as K
+import oracle as O
 
 STR_COLS = ["uid", "ns", "op", "kind", "ctr_name", "ctr_image", "ctr_apparmor", "cap_add", "cap_drop",
             "lbl_key", "lbl_val"]
@@ -107,8 +108,10 @@ def test_json_recursion_limit():
 
 
 def test_escaped_strings_and_duplicate_keys():
-    """Escaped keys and values are unescaped (the arena path) and match their plain spelling; a
-    duplicate key keeps its last value (serde_json Map)."""
+    """Escaped keys and values are unescaped (the arena path) and match their plain spelling. A
+    repeated field of a typed object (AdmissionRequest, its kind / resource / userInfo, the review
+    envelope) is a deserialize error, 422, as serde's derived structs answer ("duplicate field"); a
+    repeated key inside `object` (a serde_json::Value) keeps its last value."""
     doc = docs(4, 1, 3)[0]
     plain = columns(K.Batch.from_json([doc]))
     esc = doc.replace('"namespace":"', '"n\\u0061mespace":"', 1).replace('"operation":"CREATE"', '"operation":"CR\\u0045\\u0041TE"')
@@ -116,5 +119,16 @@ def test_escaped_strings_and_duplicate_keys():
     assert isinstance(got, dict)
     for k in ("ns.bytes", "ns.off", "op.bytes"):
         assert np.array_equal(got[k], plain[k]), k
-    dup = doc.replace('"operation":"CREATE"', '"operation":"DELETE","operation":"CREATE"')
-    assert np.array_equal(columns(K.Batch.from_json([dup]))["op.bytes"], plain["op.bytes"])
+    for dup, field in ((doc.replace('"operation":"CREATE"', '"operation":"DELETE","operation":"CREATE"'), "operation"),
+                       (doc.replace('"request":{', '"request":{"uid":"x",', 1), "uid"),
+                       (doc.replace('"userInfo":{', '"userInfo":{"username":"a",', 1), "username"),
+                       (doc.replace('"kind":{"group"', '"kind":{"kind":"Pod","group"', 1), "kind"),
+                       ('{"request":{},' + doc[1:], "request")):
+        got = _one(dup)
+        assert isinstance(got, str) and f"duplicate field `{field}`" in got, (field, got)
+        assert O.flatten_doc(dup) is None
+    i = doc.index('"labels":{') + len('"labels":{')
+    dup = doc[:i] + '"app":"first",' + doc[i:]  # inside object: serde_json::Value, the last one wins
+    assert O.flatten_doc(dup) is not None
+    got = _one(dup)
+    assert isinstance(got, dict)

@@ -111,8 +111,10 @@ def _doc(rng, raw):
     req = {k: v for k, v in req.items() if v != "__missing__"}
     text = json.dumps({"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview", "request": req},
                       ensure_ascii=rng.random() < 0.5)
-    if rng.random() < 0.1 and '"operation": "' in text:  # a duplicate member: the last one counts
+    if rng.random() < 0.05 and '"operation": "' in text:  # a repeated AdmissionRequest field: 422 in both
         text = text.replace('"operation": "', '"operation": "DELETE", "operation": "', 1)
+    if rng.random() < 0.1 and '"labels": {' in text:  # a repeated key inside object: the last one counts
+        text = text.replace('"labels": {', '"labels": {"app": "dup", ', 1)
     return text
 
 

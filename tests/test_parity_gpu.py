@@ -16,6 +16,14 @@ from helpers import config, diff_verdicts, golden, many_policies_config, referen
 pytestmark = pytest.mark.gpu
 NS = "kubewarden"
 
+
+@pytest.fixture(autouse=True)
+def _poisoned_verdicts(monkeypatch):
+    """Every pass in this module starts from verdict words filled with a sentinel no verdict word
+    equals (KW_POISON_VERDICTS, capi.cpp run_pass): a tile the schedule skipped cannot pass by
+    keeping an earlier pass's words (the failure signature of r02's s45 build)."""
+    monkeypatch.setenv("KW_POISON_VERDICTS", "1")
+
 CASES = [  # (policies file, synth config, rows)
     ("parity", 0, 20000),
     ("c1_namespace", 1, 20000),
@@ -183,12 +191,13 @@ def _oracle_threads():
     return max(1, min(16, len(os.sched_getaffinity(0))))
 
 
-@pytest.mark.parametrize("name,scfg,n", [("c4_64", 4, 1_000_000), ("c5_mixed", 5, 2_000_000), ("c2_trusted", 2, 1_000_000),
+@pytest.mark.parametrize("name,scfg,n", [("c4_64", 4, 1_000_000), ("c5_mixed", 5, 10_000_000), ("c2_trusted", 2, 1_000_000),
                                          ("c3_group", 3, 1_000_000), ("c1_namespace", 1, 1_000_000)])
 def test_full_size_matches_oracle(name, scfg, n):
     """BASELINE sizes: C4 at 1M requests x 64 policies, C5 (mixed kinds, skewed container counts)
-    at 2M requests, and C1-C3 at 1M (128-row tiles: the planner's taller layout), every verdict word
-    against the oracle (C restatement, 16 threads); plus determinism across launches."""
+    at its 10M requests x 64 policies (640M verdict words), and C1-C3 at 1M (128-row tiles: the
+    planner's taller layout), every verdict word against the oracle (C restatement, 16 threads);
+    plus determinism across launches."""
     env, oe = _envs(name)
     ids = env.policy_ids()
     syn = K.SynthBatch(scfg, n, seed=scfg)
@@ -336,3 +345,76 @@ def test_repeated_passes_on_one_batch():
         gpu = b.verdicts()
         ora = oe.eval(soa, cols, origin)
         assert np.array_equal(gpu, ora), f"pass {k}: " + diff_verdicts(gpu, ora, len(cols), cols)
+
+
+@pytest.mark.parametrize("name,scfg,n,world", [("c4_64", 4, 1_000_000, 4), ("c5_mixed", 5, 2_000_000, 8)])
+def test_serialized_blob_on_device_shards_match_oracle(name, scfg, n, world):
+    """The multi-GPU path of SURVEY §8(e) on one device: the environment is compiled on the host
+    (no device), its blob goes through kw_env_serialize -> kw_env_deserialize(device=0) (what every
+    rank >= 1 runs after the RCCL broadcast), the job is cut into `world` shards by weight_bounds
+    (1 + containers per request; equal to the synthetic stream's kws_shard_bounds), each shard is
+    generated alone and validated on the GPU with the deserialized tables, and the concatenated
+    verdict words equal the oracle's for the whole job, bit-exact."""
+    from kwgpu.dist import synth_bounds, weight_bounds
+
+    doc = config(name)
+    host = K.EvaluationEnvironment(doc, continue_on_errors=True, always_accept_namespace=NS)
+    env = K.EvaluationEnvironment.from_serialized(host.serialize(), device=0)
+    ids = env.policy_ids()
+    assert ids == host.policy_ids()
+    seed = 31 + scfg
+    whole = K.SynthBatch(scfg, n, seed=seed)
+    soa = whole.soa()
+    bounds = weight_bounds(np.ctypeslib.as_array(soa.ctr_off, shape=(n + 1,)), world)
+    assert np.array_equal(bounds, synth_bounds(scfg, n, world, seed))
+    parts = []
+    for k in range(world):
+        syn = K.SynthBatch(scfg, int(bounds[k + 1] - bounds[k]), seed=seed, row0=int(bounds[k]))
+        b = syn.batch().to_device(0)
+        b.validate(env, ids)
+        parts.append(b.verdicts())
+        b.close()
+    got = np.concatenate(parts)
+    ora = O.OracleEnv(doc, continue_on_errors=True, always_accept_namespace=NS).eval(soa, ids, threads=_oracle_threads())
+    assert np.array_equal(got, ora), diff_verdicts(got, ora, len(ids), ids)
+
+
+@pytest.mark.parametrize("tile_rows", ["8", "24"])
+def test_dynamic_schedule_covers_every_tile(monkeypatch, tile_rows):
+    """Stress of the two-ahead per-XCD tile schedule (kernels.hip: the descriptor of the next tile
+    copied into the LDS slot the previous tile used, the counter fetch for the tile after next read
+    after the staging barrier, the XCD's last workgroup zeroing its counter): tiles forced down to
+    8 / 24 requests (tens of thousands of tiles, a dozen per workgroup and XCD range), back-to-back
+    passes over batches of very different sizes (1 to 300k rows: ranges of 0..4.7k tiles per XCD,
+    so counters must restart from zero every launch), origins and policy lists alternating, every
+    pass starting from poisoned verdict words, each compared with the oracle."""
+    monkeypatch.setenv("KW_SLOT_ROWS", tile_rows)
+    for name, scfg in (("c2_trusted", 2), ("c4_64", 4)):
+        env, oe = _envs(name)
+        ids = env.policy_ids()
+        for k, n in enumerate([300_000, 1, 77, 5_003, 300_000 if scfg == 2 else 60_000]):
+            syn = K.SynthBatch(scfg, n, seed=900 + k)
+            b = syn.batch().to_device(0)
+            for cols, origin in ((ids, K.VALIDATE), (ids[::-1], K.AUDIT)):
+                b.validate(env, cols, origin)
+                gpu = b.verdicts()
+                ora = oe.eval(syn.soa(), cols, origin, threads=_oracle_threads())
+                assert np.array_equal(gpu, ora), f"{name} rows {n}: " + diff_verdicts(gpu, ora, len(cols), cols)
+            b.close()
+
+
+def test_container_ranges_path_matches_oracle(monkeypatch):
+    """The P2 form that ORs a container's predecessor ranges four loads a round (TileArgs::ctr_ranges,
+    chosen when a tile's container capacity exceeds 4 x its rows): C5's Zipf container counts in
+    8-row tiles are known to select it (asserted through the host plan), verdicts unchanged."""
+    monkeypatch.setenv("KW_SLOT_ROWS", "8")
+    env, oe = _envs("c5_mixed")
+    ids = env.policy_ids()
+    syn = K.SynthBatch(5, 20000, seed=515)
+    b = syn.batch().to_device(0)
+    plan = b.debug_plan(env, ids)
+    assert plan["rows"] == 8 and plan["cmax"] > 4 * plan["rows"], plan
+    b.validate(env, ids)
+    gpu = b.verdicts()
+    ora = oe.eval(syn.soa(), ids)
+    assert np.array_equal(gpu, ora), diff_verdicts(gpu, ora, len(ids), ids)
