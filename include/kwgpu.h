@@ -270,6 +270,14 @@ int kw_batch_verdicts(kw_batch *b, uint32_t *host_out, size_t count);
 /* The full argument of a verdict word whose ARG is KW_ARG_WIDE, for (row, policy) of the last pass
  * whose verdicts were copied (kw_batch_verdicts). KW_E_NOT_FOUND when the pass recorded none. */
 int kw_batch_wide_arg(const kw_batch *b, uint64_t row, int32_t policy, uint64_t *value);
+/* The causes of a policy-group rejection (REASON KW_R_GROUP) of the last copied pass as a member
+ * bitset (bit s: the group's member s, settings order, was called by the expression and rejected;
+ * evaluation_environment.rs:979-1042): from the word's ARG, or the pass's side data for groups with
+ * more than 15 members (any number of members: `words` holds ceil(members / 64) u64, `needed` gets
+ * that count; KW_E_NOSPACE when nwords is smaller). Replaces the causes of
+ * PolicyGroupEvaluator::validate's AdmissionResponse (upstream policy-evaluator). */
+int kw_batch_group_causes(const kw_batch *b, uint64_t row, int32_t policy, uint32_t verdict, uint64_t *words,
+                          size_t nwords, size_t *needed);
 
 typedef struct kw_timing {
   double classify_ms;   /* 0: classification is fused into the evaluation kernel */

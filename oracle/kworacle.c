@@ -433,6 +433,28 @@ static void detail(const orc_env *e, int32_t p, const kw_soa *S, uint64_t r, int
   if (P->family == ORC_F_GROUP) {
     if (P->expr_error) {
       d->reason = KW_R_GROUP_EXPR;
+    } else if (P->table) {
+      gctx g;
+      g.e = e;
+      g.G = P;
+      g.S = S;
+      g.r = r;
+      g.zb = zb;
+      memset(g.done, 0, sizeof(g.done));
+      uint32_t mask = 0;
+      for (int32_t s = 0; s < P->n_members; ++s) mask |= (uint32_t)gcall(&g, s) << s;
+      const uint32_t ent = P->table[mask];
+      if (ent & 2u) {
+        d->reason = KW_R_GROUP_EXPR;
+      } else if (!(ent & 1u)) {
+        d->reason = KW_R_GROUP;
+        for (int32_t s = 0; s < P->n_members; ++s)
+          if ((ent >> (16 + s)) & 1u) {
+            d->causes[d->ncauses++] = s;
+            d->arg |= 1ull << s;
+          }
+        arg16 = P->n_members > 15 ? 0xffffu : (uint32_t)d->arg;
+      }
     } else {
       gctx g;
       g.e = e;

@@ -69,6 +69,11 @@ typedef struct orc_policy {
   const int32_t *members;   /* policy indices, settings order */
   int32_t n_nodes;
   const orc_xnode *nodes;   /* root = nodes[n_nodes-1] */
+  /* group scripts outside the bool-only subset (let / if / strings / integers, <= 16 members):
+     oracle.py's own interpreter tabulated over every vector of member results, entry[mask] =
+     bit 0 value, bit 1 evaluation error, bits 16.. the members called that rejected; every member
+     is evaluated, the entry picks the outcome; NULL = evaluate `nodes` */
+  const uint32_t *table;
 } orc_policy;
 
 typedef struct orc_env orc_env;
@@ -91,7 +96,7 @@ void orc_eval_mt_pinned(const orc_env *e, const kw_soa *soa, const int32_t *poli
    is derived from this and the document, never from the product's word (oracle.py response_doc).
    arg: the FULL argument (entity index within the request, settings index); causes: the group
    members rhai would have called that rejected, ascending member slots. */
-#define ORC_MAX_MEMBERS 256
+#define ORC_MAX_MEMBERS 4096
 typedef struct orc_detail {
   uint32_t word;      /* the verdict word (kwgpu.h layout, ARG saturated to KW_ARG_WIDE) */
   uint32_t reason;    /* KW_R_* of the vanilla response, 0 = accepted */

@@ -537,7 +537,17 @@ def engine_limit_error(pid, fam, L):
 
 
 # ----------------------------------------------------------------------------- group expressions
-_TOK = re.compile(r"\s*(?:(?P<id>[A-Za-z_][A-Za-z0-9_]*)|(?P<int>[0-9][0-9_]*)|(?P<op>\|\||&&|==|!=|<=|>=|[<>+\-*/%!()]))")
+# The rhai script subset of policy-group expressions (PolicyGroupEvaluator, upstream
+# policy-evaluator v0.24.0 / rhai 1.21.0, absent from the reference tree; pinned only by
+# evaluation_environment.rs:979-1112). Restated here independently of the product's expr.cpp:
+# statements (`let x = e;`, `e;`), blocks whose value is a last expression without `;`, if / else if /
+# else expressions, bool / i64 / string literals, variables, member calls, ! - + and
+# || | ^ && & == != < <= > >= + - * / % with rhai's precedence; == != < ... between different types
+# are false (!= true); other type mismatches are "Function not found"; checked i64 arithmetic.
+# Validation runs the script with every member returning true; evaluation needs a bool.
+_TOK = re.compile(r"\s*(?:(?P<id>[A-Za-z_][A-Za-z0-9_]*)|(?P<int>[0-9][0-9_]*)|(?P<str>\")|"
+                  r"(?P<op>\|\||&&|==|!=|<=|>=|[<>+\-*/%!()|&^{};=]))")
+_I64 = (-(1 << 63), (1 << 63) - 1)
 
 
 class ExprError(Exception):
@@ -550,137 +560,335 @@ def _lex(s):
         if s[i].isspace():
             i += 1
             continue
+        if s.startswith("//", i):
+            while i < len(s) and s[i] != "\n":
+                i += 1
+            continue
         m = _TOK.match(s, i)
         if not m or m.end() == i:
             raise ExprError(f"Syntax error: unexpected character '{s[i]}'")
         if m.group("id"):
             toks.append(("id", m.group("id")))
+            i = m.end()
         elif m.group("int"):
             digits = m.group("int").replace("_", "")
-            if len(digits) > 18:
+            if int(digits) > _I64[1]:
                 raise ExprError("Syntax error: integer literal too large")
             toks.append(("int", int(digits)))
+            i = m.end()
+        elif m.group("str"):
+            j, out = m.end(), []
+            esc = {"n": "\n", "t": "\t", "r": "\r", "0": "\0", "\\": "\\", '"': '"', "'": "'"}
+            while True:
+                if j >= len(s):
+                    raise ExprError("Syntax error: unterminated string literal")
+                ch = s[j]
+                j += 1
+                if ch == '"':
+                    break
+                if ch == "\\":
+                    if j >= len(s):
+                        raise ExprError("Syntax error: unterminated string literal")
+                    e = s[j]
+                    j += 1
+                    if e not in esc:
+                        raise ExprError(f"Syntax error: invalid escape sequence \\{e}")
+                    out.append(esc[e])
+                else:
+                    out.append(ch)
+            toks.append(("str", "".join(out)))
+            i = j
         else:
             toks.append(("op", m.group("op")))
-        i = m.end()
+            i = m.end()
     toks.append(("end", None))
     return toks
 
 
-def parse_expression(s, members):
-    """rhai subset -> typed AST with constant folding. Node: ('const', type, value) | ('call', slot) |
-    ('not', a) | ('and'|'or'|'eq'|'ne', a, b). Raises ExprError (validation failure)."""
+_PREC = {"||": 30, "|": 30, "^": 30, "&&": 60, "&": 60, "==": 90, "!=": 90, "<": 110, "<=": 110, ">": 110, ">=": 110,
+         "+": 150, "-": 150, "*": 180, "/": 180, "%": 180}
+
+
+def parse_script(s, members):
+    """Script -> tree. Nodes: ('lit', value) (value: None for (), bool, int, str) | ('var', name) |
+    ('call', slot or -1, name) | ('un', op, a) | ('bin', op, a, b) | ('if', c, then, else or None) |
+    ('block', [statements], tail) | ('let', name, init). Raises ExprError on a syntax error."""
     toks = _lex(s)
     pos = [0]
+    peek = lambda: toks[pos[0]]  # noqa: E731
 
-    def peek():
-        return toks[pos[0]]
+    def isop(o):
+        return peek() == ("op", o)
 
-    def take():
-        t = toks[pos[0]]
-        pos[0] += 1
-        return t
+    def isid(o):
+        return peek() == ("id", o)
 
-    def isop(*ops):
+    def near():
         t = peek()
-        return t[0] == "op" and t[1] in ops
+        return "end of script" if t[0] == "end" else (f'"{t[1]}"' if t[0] == "str" else f"'{t[1]}'" if t[0] != "int" else str(t[1]))
 
-    def typ(n):
-        return n[1] if n[0] == "const" else "bool"
+    def block(top):
+        stmts, tail = [], False
+        while True:
+            if (peek()[0] == "end") if top else isop("}"):
+                break
+            if peek()[0] == "end":
+                raise ExprError("Syntax error: expecting '}' to close the block")
+            block_like = False
+            if isid("let"):
+                pos[0] += 1
+                t = peek()
+                if t[0] != "id" or t[1] in ("let", "if", "else", "true", "false"):
+                    raise ExprError("Syntax error: expecting a variable name after 'let'")
+                pos[0] += 1
+                if not isop("="):
+                    raise ExprError("Syntax error: expecting '=' after the variable name")
+                pos[0] += 1
+                st = ("let", t[1], expr(0))
+            else:
+                block_like = isid("if") or isop("{")
+                st = expr(0)
+            stmts.append(st)
+            if isop(";"):
+                pos[0] += 1
+                tail = False
+                continue
+            if (peek()[0] == "end") if top else isop("}"):
+                tail = st[0] != "let"
+                break
+            if not block_like:
+                raise ExprError(f"Syntax error: expecting ';' to terminate this statement, found {near()}")
+            tail = False
+        return ("block", stmts, tail)
 
-    def fold_bin(op, a, b):
-        ta, tb = typ(a), typ(b)
-        if op in ("&&", "||"):
-            if ta != "bool" or tb != "bool":
-                raise ExprError(f"Function not found: {op} ({ta}, {tb})")
-            if a[0] == "const" and b[0] == "const":
-                return ("const", "bool", (a[2] and b[2]) if op == "&&" else (a[2] or b[2]))
-            return ("and" if op == "&&" else "or", a, b)
-        if op in ("==", "!="):
-            if ta != tb:
-                raise ExprError(f"Function not found: {op} ({ta}, {tb})")
-            if a[0] == "const" and b[0] == "const":
-                return ("const", "bool", (a[2] == b[2]) == (op == "=="))
-            return ("eq" if op == "==" else "ne", a, b)
-        if ta != "i64" or tb != "i64":
-            raise ExprError(f"Function not found: {op} ({ta}, {tb})")
-        x, y = a[2], b[2]
-        if op in ("<", "<=", ">", ">="):
-            return ("const", "bool", {"<": x < y, "<=": x <= y, ">": x > y, ">=": x >= y}[op])
-        if op in ("/", "%") and y == 0:
-            raise ExprError("Division by zero")
-        if op == "/":
-            v = abs(x) // abs(y) * (1 if (x >= 0) == (y >= 0) else -1)
-        elif op == "%":
-            v = abs(x) % abs(y) * (1 if x >= 0 else -1)
-        else:
-            v = {"+": x + y, "-": x - y, "*": x * y}[op]
-        return ("const", "i64", v)
-
-    def binary(sub, ops):
-        a = sub()
-        while isop(*ops):
-            op = take()[1]
-            b = sub()
-            a = fold_bin(op, a, b)
-        return a
-
-    def orx():
-        return binary(andx, ("||",))
-
-    def andx():
-        return binary(cmp, ("&&",))
-
-    def cmp():
-        return binary(add, ("==", "!=", "<", "<=", ">", ">="))
-
-    def add():
-        return binary(mul, ("+", "-"))
-
-    def mul():
-        return binary(unary, ("*", "/", "%"))
+    def expr(min_prec):
+        a = unary()
+        while True:
+            t = peek()
+            p = _PREC.get(t[1]) if t[0] == "op" else None
+            if p is None or p < min_prec:
+                return a
+            pos[0] += 1
+            a = ("bin", t[1], a, expr(p + 1))
 
     def unary():
-        if isop("!", "-"):
-            op = take()[1]
-            a = unary()
-            if op == "!":
-                if typ(a) != "bool":
-                    raise ExprError("Function not found: ! (i64)")
-                return ("const", "bool", not a[2]) if a[0] == "const" else ("not", a)
-            if typ(a) != "i64":
-                raise ExprError("Function not found: - (bool)")
-            return ("const", "i64", -a[2])
+        if peek()[0] == "op" and peek()[1] in ("!", "-", "+"):
+            op = peek()[1]
+            pos[0] += 1
+            return ("un", op, unary())
         return primary()
 
+    def inner_block():
+        if not isop("{"):
+            raise ExprError(f"Syntax error: expecting '{{' after the if condition, found {near()}")
+        pos[0] += 1
+        b = block(False)
+        pos[0] += 1
+        return b
+
     def primary():
-        t = take()
-        if t[0] == "int":
-            return ("const", "i64", t[1])
-        if t[0] == "op" and t[1] == "(":
-            e = orx()
+        t = peek()
+        pos[0] += 1
+        if t[0] in ("int", "str"):
+            return ("lit", t[1])
+        if t == ("op", "("):
+            e = expr(0)
             if not isop(")"):
-                raise ExprError("Syntax error: expecting ')'")
-            take()
+                raise ExprError(f"Syntax error: expecting ')', found {near()}")
+            pos[0] += 1
             return e
+        if t == ("op", "{"):
+            b = block(False)
+            pos[0] += 1
+            return b
         if t[0] == "id":
             if t[1] in ("true", "false"):
-                return ("const", "bool", t[1] == "true")
+                return ("lit", t[1] == "true")
+            if t[1] == "if":
+                c = expr(0)
+                then = inner_block()
+                other = None
+                if isid("else"):
+                    pos[0] += 1
+                    if isid("if"):
+                        other = primary()
+                    else:
+                        if not isop("{"):
+                            raise ExprError(f"Syntax error: expecting '{{' or 'if' after 'else', found {near()}")
+                        other = inner_block()
+                return ("if", c, then, other)
+            if t[1] in ("let", "else"):
+                raise ExprError(f"Syntax error: unexpected '{t[1]}'")
             if not isop("("):
-                raise ExprError(f"Variable not found: {t[1]}")
-            take()
+                return ("var", t[1])
+            pos[0] += 1
             if not isop(")"):
                 raise ExprError("Syntax error: member policies take no arguments")
-            take()
-            if t[1] not in members:
-                raise ExprError(f"Function not found: {t[1]} ()")
-            return ("call", members.index(t[1]))
-        raise ExprError("Syntax error: unexpected token")
+            pos[0] += 1
+            return ("call", members.index(t[1]) if t[1] in members else -1, t[1])
+        if t[0] == "end":
+            raise ExprError("Syntax error: expecting an expression, found end of script")
+        pos[0] -= 1
+        raise ExprError(f"Syntax error: unexpected {near()}")
 
-    root = orx()
-    if peek()[0] != "end":
-        raise ExprError("Syntax error: unexpected trailing input")
-    return root
+    return block(True)
+
+
+def _tn(v):
+    return "()" if v is None else "bool" if isinstance(v, bool) else "i64" if isinstance(v, int) else "string"
+
+
+def run_script(root, member_ok):
+    """-> (error message or None, bool value, called members in call order)."""
+    called, scopes = [], []
+
+    def nf(op, a, b):
+        raise ExprError(f"Function not found: {op} ({_tn(a)}, {_tn(b)})")
+
+    def ev(n):
+        k = n[0]
+        if k == "lit":
+            return n[1]
+        if k == "var":
+            for name, v in reversed(scopes):
+                if name == n[1]:
+                    return v
+            raise ExprError(f"Variable not found: {n[1]}")
+        if k == "call":
+            if n[1] < 0:
+                raise ExprError(f"Function not found: {n[2]} ()")
+            if n[1] not in called:
+                called.append(n[1])
+            return bool(member_ok[n[1]])
+        if k == "un":
+            a = ev(n[2])
+            if n[1] == "!":
+                if not isinstance(a, bool):
+                    raise ExprError(f"Function not found: ! ({_tn(a)})")
+                return not a
+            if isinstance(a, bool) or not isinstance(a, int):
+                raise ExprError(f"Function not found: {n[1]} ({_tn(a)})")
+            if n[1] == "-" and a == _I64[0]:
+                raise ExprError(f"Negation overflow: -{a}")
+            return -a if n[1] == "-" else a
+        if k == "if":
+            c = ev(n[1])
+            if not isinstance(c, bool):
+                raise ExprError(f"Boolean value expected for the if condition, found {_tn(c)}")
+            if c:
+                return ev(n[2])
+            return ev(n[3]) if n[3] is not None else None
+        if k == "block":
+            depth = len(scopes)
+            v = None
+            for st in n[1]:
+                if st[0] == "let":
+                    scopes.append((st[1], ev(st[2])))
+                    v = None
+                else:
+                    v = ev(st)
+            del scopes[depth:]
+            return v if n[2] else None
+        op, a = n[1], ev(n[2])
+        if op in ("||", "&&"):
+            if not isinstance(a, bool):
+                raise ExprError(f"Function not found: {op} ({_tn(a)}, ...)")
+            if a == (op == "||"):
+                return a
+            b = ev(n[3])
+            if not isinstance(b, bool):
+                nf(op, a, b)
+            return b
+        b = ev(n[3])
+        same = type(a) is type(b)
+        if op in ("==", "!="):
+            return (same and a == b) == (op == "==")
+        if op in ("<", "<=", ">", ">="):
+            if not same:
+                return False
+            if isinstance(a, bool) or a is None:
+                nf(op, a, b)
+            return {"<": a < b, "<=": a <= b, ">": a > b, ">=": a >= b}[op]
+        if op in ("|", "&", "^"):
+            if same and isinstance(a, bool):
+                return {"|": a or b, "&": a and b, "^": a != b}[op]
+            if same and isinstance(a, int):
+                return {"|": a | b, "&": a & b, "^": a ^ b}[op]
+            nf(op, a, b)
+        if op == "+" and isinstance(a, str) and isinstance(b, str):
+            return a + b
+        if not (same and isinstance(a, int) and not isinstance(a, bool)):
+            nf(op, a, b)
+        text = f"{a} {op} {b}"
+        if op in ("/", "%"):
+            if b == 0:
+                raise ExprError(f"Division by zero: {text}")
+            if a == _I64[0] and b == -1:
+                raise ExprError(("Division overflow: " if op == "/" else "Modulo overflow: ") + text)
+            q = abs(a) // abs(b) * (1 if (a >= 0) == (b >= 0) else -1)  # truncation, as i64 division
+            return q if op == "/" else a - q * b
+        r = {"+": a + b, "-": a - b, "*": a * b}[op]
+        if not _I64[0] <= r <= _I64[1]:
+            raise ExprError({"+": "Addition", "-": "Subtraction", "*": "Multiplication"}[op] + " overflow: " + text)
+        return r
+
+    try:
+        v = ev(root)
+    except ExprError as e:
+        return str(e), False, called
+    if not isinstance(v, bool):
+        return f"Output type incorrect: {_tn(v)} (expecting bool)", False, called
+    return None, v, called
+
+
+def group_eval_message(m):
+    if m.startswith("Output type incorrect"):
+        return "policy group expression did not evaluate to a boolean: " + m
+    return "policy group expression evaluation failed: " + m
+
+
+def _has_call(n):
+    if n[0] == "call":
+        return True
+    return any(isinstance(x, tuple) and _has_call(x) for x in n[1:]) or \
+        (n[0] == "block" and any(_has_call(x) for x in n[1]))
+
+
+def _bool_subset(n):
+    """The script as the old bool-only tree (('const', 'bool', v) | ('call', s) | ('not', a) |
+    ('and'|'or'|'eq'|'ne', a, b)) when it is one: call-free subtrees folded to their values first;
+    None when it is not."""
+    if n[0] == "block":
+        if len(n[1]) == 1 and n[2]:
+            return _bool_subset(n[1][0])
+        return None
+    if not _has_call(n):
+        err, v, _ = run_script(("block", [n], True), [])
+        return ("const", "bool", v) if err is None else None
+    if n[0] == "call":
+        return ("call", n[1]) if n[1] >= 0 else None
+    if n[0] == "un" and n[1] == "!":
+        a = _bool_subset(n[2])
+        return ("not", a) if a is not None else None
+    if n[0] == "bin" and n[1] in ("&&", "||", "==", "!="):
+        a, b = _bool_subset(n[2]), _bool_subset(n[3])
+        if a is None or b is None:
+            return None
+        return ({"&&": "and", "||": "or", "==": "eq", "!=": "ne"}[n[1]], a, b)
+    return None
+
+
+def parse_expression(s, members):
+    """The group expression as the bool-only tree the C restatement evaluates (see _bool_subset);
+    raises ExprError when the script does not validate or is not bool-only."""
+    root = parse_script(s, members)
+    err, _, _ = run_script(root, [True] * len(members))
+    if err is not None and not err.startswith("Output type incorrect"):
+        raise ExprError(err)
+    t = _bool_subset(root)
+    if t is None:
+        raise ExprError("not a bool-only expression")
+    return t
 
 
 def expr_depth(n, d=1):
@@ -696,7 +904,7 @@ def expr_depth(n, d=1):
 
 
 def eval_expression(n, member_ok):
-    """Short-circuit evaluation -> (value, called-members list in call order)."""
+    """Short-circuit evaluation of a bool-only tree -> (value, called-members list in call order)."""
     called = []
 
     def ev(x):
@@ -767,12 +975,13 @@ class _OPolicy(C.Structure):
     _fields_ = [("family", C.c_int32), ("mode", C.c_int32), ("allowed_to_mutate", C.c_int32),
                 ("init_error", C.c_int32), ("expr_error", C.c_int32), ("flags", C.c_int32),
                 ("n", C.c_int32 * 5), ("l", C.POINTER(C.c_char_p) * 5), ("n_members", C.c_int32),
-                ("members", C.POINTER(C.c_int32)), ("n_nodes", C.c_int32), ("nodes", C.POINTER(_XNode))]
+                ("members", C.POINTER(C.c_int32)), ("n_nodes", C.c_int32), ("nodes", C.POINTER(_XNode)),
+                ("table", C.POINTER(C.c_uint32))]
 
 
 class _ODetail(C.Structure):
     _fields_ = [("word", C.c_uint32), ("reason", C.c_uint32), ("arg", C.c_uint64), ("mutated", C.c_uint32),
-                ("bypass", C.c_uint32), ("ncauses", C.c_int32), ("causes", C.c_int32 * 256)]
+                ("bypass", C.c_uint32), ("ncauses", C.c_int32), ("causes", C.c_int32 * 4096)]
 
 
 _olib = None
@@ -871,19 +1080,43 @@ class OracleEnv:
                 continue
             p["expr_error"] = None
             p["ast"] = None
+            p["script"] = None
+            p["table"] = None
+            names = p["member_names"]
             try:
-                if len(p["member_names"]) > 64:
-                    raise ExprError("policy groups with more than 64 members are not supported by the engine")
-                ast = parse_expression(p["expression"], p["member_names"])
-                if ast[0] == "const" and ast[1] == "i64":
-                    p["expr_error"] = ("policy group expression did not evaluate to a boolean: Output type "
-                                       "incorrect: i64 (expecting bool)")
-                    p["valid"] = True
-                elif expr_depth(ast) > 64:
-                    raise ExprError("policy group expression nests too deeply for the engine (max stack 64)")
-                else:
-                    p["ast"] = ast
-                    p["valid"] = True
+                root = parse_script(p["expression"], names)
+                err, _, _ = run_script(root, [True] * len(names))  # validate_settings: members return true
+                if err is not None and not err.startswith("Output type incorrect"):
+                    raise ExprError(err)
+                p["valid"] = True
+                p["script"] = root
+                if not _has_call(root):  # one outcome
+                    err, v, _ = run_script(root, [])
+                    if err is not None:
+                        p["expr_error"] = group_eval_message(err)
+                    else:
+                        p["ast"] = ("const", "bool", v)
+                    continue
+                t = _bool_subset(root)
+                if t is not None:
+                    if len(names) > 65535 or expr_depth(t) > 65536:
+                        raise ExprError("policy group expression exceeds the engine's limits (65535 members, value "
+                                        "stack 65536)")
+                    p["ast"] = t
+                elif len(names) > 16:
+                    raise ExprError("policy group expression uses let / if / string / integer values with more "
+                                    "than 16 members, which the engine does not evaluate")
+                else:  # every vector of member results: value, error, causes (the C half looks it up)
+                    tab = []
+                    for mask in range(1 << len(names)):
+                        ok = [bool((mask >> i) & 1) for i in range(len(names))]
+                        err, v, called = run_script(root, ok)
+                        e = 2 if err is not None else (1 if v else 0)
+                        for c in called:
+                            if not ok[c]:
+                                e |= 1 << (16 + c)
+                        tab.append(e)
+                    p["table"] = tab
             except ExprError as ex:
                 p["expr_error"] = str(ex)
                 p["valid"] = False
@@ -915,6 +1148,10 @@ class OracleEnv:
                 self._keep.append(mem)
                 o.n_members = len(p["members"])
                 o.members = C.cast(mem, C.POINTER(C.c_int32))
+                if p["table"] is not None:
+                    tab = (C.c_uint32 * len(p["table"]))(*p["table"])
+                    self._keep.append(tab)
+                    o.table = C.cast(tab, C.POINTER(C.c_uint32))
                 if p["ast"] is not None:
                     nodes = _to_nodes(p["ast"])
                     xs = (_XNode * len(nodes))(*[_XNode(*t) for t in nodes])
@@ -1000,7 +1237,15 @@ class OracleEnv:
         if reason == R_GROUP:
             return P["message"]
         if reason == R_GROUP_EXPR:
-            return P["expr_error"]
+            if P["expr_error"]:
+                return P["expr_error"]
+            # a data-dependent evaluation error: the script over this row's member results
+            ok = []
+            for m in P["members"]:
+                md = self.detail(soa, row, m)
+                ok.append(md["reason"] == 0 and not md["mutated"])
+            err, _, _ = run_script(P["script"], ok)
+            return group_eval_message(err)
         if reason == R_INIT:
             return P["init_error"]
         return ""

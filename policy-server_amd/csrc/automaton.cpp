@@ -777,6 +777,32 @@ bool compile_dfa(const std::vector<Pattern>& pats, Dfa* out, std::string* err, u
     *err = "too many byte classes";
     return false;
   }
+  // absorbing states (all transitions to themselves; e.g. a glob's trailing `*` reached, an
+  // unanchored regex matched) move to the end, [abs_lo, nstates): the kernels' walks stop there
+  {
+    const uint32_t n = out->nstates;
+    std::vector<uint32_t> perm(n, 0);
+    uint32_t at = 1;
+    auto absorbing = [&](uint32_t t) {
+      for (uint32_t c = 0; c < ncl; ++c)
+        if (out->trans[(size_t)t * ncl + c] != t) return false;
+      return true;
+    };
+    for (uint32_t t = 1; t < n; ++t)
+      if (!absorbing(t)) perm[t] = at++;
+    out->abs_lo = at;
+    for (uint32_t t = 1; t < n; ++t)
+      if (absorbing(t)) perm[t] = at++;
+    std::vector<uint16_t> tr(out->trans.size());
+    std::vector<uint32_t> ac(n);
+    for (uint32_t t = 0; t < n; ++t) {
+      ac[perm[t]] = out->acc[t];
+      for (uint32_t c = 0; c < ncl; ++c) tr[(size_t)perm[t] * ncl + c] = (uint16_t)perm[out->trans[(size_t)t * ncl + c]];
+    }
+    out->trans.swap(tr);
+    out->acc.swap(ac);
+    out->start = perm[out->start];
+  }
   // class ids in order of first use by a state (the dead state's empty set stays 0), unused sets
   // of the unminimised automaton dropped
   std::vector<int64_t> cmap(classes.size(), -1);

@@ -38,6 +38,9 @@ struct Dfa {
   uint32_t nstates = 0;
   uint32_t ncls = 0;
   uint32_t start = 0;
+  // States [abs_lo, nstates) are absorbing (every byte keeps them), as is the dead state 0: a walk
+  // may stop as soon as it reaches one (kernels.hip), the accept class cannot change any more.
+  uint32_t abs_lo = 0;
   std::array<uint8_t, 256> cls{};              // byte -> byte class
   std::vector<uint16_t> trans;                  // [state][byte class]
   std::vector<uint32_t> acc;                    // [state] accept class

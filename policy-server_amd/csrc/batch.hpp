@@ -105,13 +105,34 @@ struct WideData {
   uint32_t nwide = 0;
   std::vector<int32_t> wide_policy;  // wide index -> group policy (all-pairs mode)
   bool rows_mode = false;
+  // cause bitsets of wide groups (> 64 members or deep stacks, kernels.hpp WideGroupPass):
+  // [row][big_stride] u64, the group `policy` at words [off, off + words) of its row
+  struct BigRef {
+    int32_t policy;
+    uint32_t off, words;
+  };
+  std::vector<uint64_t> big;
+  uint32_t big_stride = 0;
+  std::vector<BigRef> big_ref;
   bool lookup(uint64_t row, int32_t policy, uint64_t* v) const;
+  // the cause words of wide group `policy` at `row`, nullptr when the pass recorded none
+  const uint64_t* lookup_big(uint64_t row, int32_t policy, uint32_t* words) const {
+    for (const BigRef& r : big_ref)
+      if (r.policy == policy && (row + 1) * big_stride <= big.size()) {
+        *words = r.words;
+        return big.data() + row * big_stride + r.off;
+      }
+    return nullptr;
+  }
   void clear() {
     recs.clear();
     groups.clear();
     nwide = 0;
     wide_policy.clear();
     rows_mode = false;
+    big.clear();
+    big_stride = 0;
+    big_ref.clear();
   }
 };
 

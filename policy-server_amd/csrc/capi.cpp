@@ -166,6 +166,18 @@ struct DeviceBatch {
   size_t wide_rec_cap = 0;
   uint64_t* wide_groups = nullptr;
   size_t wide_groups_cap = 0;
+  // wide policy groups (WideGroupPass): the members' pass output, the combine kernel's records,
+  // value-stack scratch and the cause bitsets
+  uint32_t* member_words = nullptr;
+  size_t member_words_cap = 0;
+  uint8_t* wg_data = nullptr;
+  size_t wg_data_cap = 0;
+  uint64_t* wg_stack = nullptr;
+  size_t wg_stack_cap = 0;
+  uint64_t* big_causes = nullptr;
+  size_t big_causes_cap = 0;
+  uint32_t last_big_stride = 0;
+  std::vector<WideData::BigRef> last_big_ref;
   // what the last pass left in the side buffers
   uint32_t last_nwide = 0, last_wide_cap = 0;
   bool last_rows_mode = false;
@@ -196,6 +208,10 @@ struct DeviceBatch {
     P.release(device, g_cls, g_cls_cap * 2);
     P.release(device, wide_rec, wide_rec_cap * sizeof(WideRec));
     P.release(device, wide_groups, wide_groups_cap * 8);
+    P.release(device, member_words, member_words_cap * 4);
+    P.release(device, wg_data, wg_data_cap);
+    P.release(device, wg_stack, wg_stack_cap * 8);
+    P.release(device, big_causes, big_causes_cap * 8);
     P.release(device, sched, 512 * sizeof(uint32_t));  // every launch leaves the tile counters zero
     P.release(device, wide_count, sizeof(uint32_t));
     host_pool().release(device, staging, staging_bytes);
@@ -345,7 +361,55 @@ struct PassPlan {
   std::vector<uint32_t> rowcol;  // rows mode
   uint64_t wide_cap_per_row = 0;
   double evaluate_bytes = 0;
+  // wide policy groups of the pass (> 64 members or deep stacks): their combine records, jump
+  // code, member slot -> member-pass column maps, the member-pass policy list
+  struct Wide {
+    std::vector<WideGroupArgs> groups;
+    std::vector<int32_t> policy;
+    std::vector<uint8_t> progs;
+    std::vector<uint32_t> midx;
+    std::vector<int32_t> members;
+    uint32_t cause_stride = 0, stack_words = 0;
+  } wide;
 };
+
+// The wide groups among the pass's columns (plan->wide): column ids are the output column
+// (all pairs) or the rows-mode column code ((chunk << 16) | column, as rowcol holds).
+void plan_wide_groups(const Env& E, const std::vector<int32_t>& list, const std::vector<uint32_t>* rows_code,
+                      int origin, PassPlan* plan) {
+  PassPlan::Wide& W = plan->wide;
+  W = PassPlan::Wide{};
+  std::map<int32_t, uint32_t> mcol;
+  for (uint32_t j = 0; j < (uint32_t)list.size(); ++j) {
+    const PolicyRec& P = E.pol[(size_t)list[j]];
+    if (!P.is_group || P.init_error || !P.prog.valid || P.prog.eval_error || !P.prog.wide) continue;
+    WideGroupArgs g;
+    memset(&g, 0, sizeof(g));
+    g.prog_off = (uint32_t)W.progs.size();
+    g.prog_len = (uint32_t)P.prog.code.size();
+    W.progs.insert(W.progs.end(), P.prog.code.begin(), P.prog.code.end());
+    g.col = rows_code ? (*rows_code)[j] : j;
+    g.nmem = (uint32_t)P.members.size();
+    g.midx_off = (uint32_t)W.midx.size();
+    for (int32_t m : P.members) {
+      auto it = mcol.find(m);
+      if (it == mcol.end()) {
+        it = mcol.emplace(m, (uint32_t)W.members.size()).first;
+        W.members.push_back(m);
+      }
+      W.midx.push_back(it->second);
+    }
+    g.okw = finish_word(P.mode, 0, origin, 0, 0, false);
+    g.rejb = finish_word(P.mode, 0, origin, KW_R_GROUP, kArgWide, false);
+    g.cause_words = (g.nmem + 63u) / 64u;
+    // all pairs: every wide column has its own words in a row; rows mode: a row has one column
+    g.cause_off = rows_code ? 0u : W.cause_stride;
+    W.cause_stride = rows_code ? std::max(W.cause_stride, g.cause_words) : W.cause_stride + g.cause_words;
+    W.stack_words = std::max(W.stack_words, (P.prog.depth + 63u) / 64u);
+    W.groups.push_back(g);
+    W.policy.push_back(list[j]);
+  }
+}
 
 // Plan one pass: slot-plan chunks of the policy list, the launches they take, the tile geometry
 // and LDS layout, the kernel arguments.
@@ -367,10 +431,12 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
   }
   Status st = build_slot_chunks(E, list.data(), (uint32_t)list.size(), origin, plan->rows_mode, &plan->chunks);
   if (!st.ok()) return st.code;
+  if (!plan->rows_mode) plan_wide_groups(E, list, nullptr, origin, plan);
   if (plan->rows_mode) {
     std::vector<uint32_t> at(list.size());
     for (uint32_t c = 0; c < plan->chunks.size(); ++c)
       for (uint32_t j = 0; j < plan->chunks[c].ncols; ++j) at[plan->chunks[c].col0 + j] = (c << 16) | j;
+    plan_wide_groups(E, list, &at, origin, plan);
     plan->rowcol.resize(B.n);
     for (uint64_t r = 0; r < B.n; ++r) plan->rowcol[r] = at[col_of[row_policy[r]]];
   }
@@ -953,6 +1019,68 @@ int run_pass(kw_batch* kb, PassPlan& plan, bool timed, hipStream_t s) {
   return KW_OK;
 }
 
+// A planned pass with its wide policy groups (PassPlan::wide): their members first run as a
+// separate all-pairs pass into member_words, then the pass itself (wide columns hold a
+// placeholder), then the combine kernel writes those columns and their cause bitsets. The member
+// pass's own side data (entity indices >= 65535 of members) is not kept: the main pass reuses the
+// buffers. `timed`: HIP events bracket the main pass.
+int run_validate(const kw_env* env, kw_batch* kb, PassPlan& plan, int origin, bool timed, hipStream_t s) {
+  DeviceBatch& D = *kb->dev;
+  const PassPlan::Wide& W = plan.wide;
+  D.last_big_stride = 0;
+  D.last_big_ref.clear();
+  if (W.groups.empty()) return run_pass(kb, plan, timed, s);
+  const uint64_t n = kb->b.n;
+  const size_t nm = W.members.size();
+  if (int rc = ensure(&D.member_words, &D.member_words_cap, (size_t)(n * nm))) return rc;
+  {
+    PassPlan mplan;
+    if (int rc = plan_pass(env, kb, W.members.data(), (uint32_t)nm, nullptr, origin, &mplan)) return rc;
+    mplan.args.out = D.member_words;
+    if (int rc = run_pass(kb, mplan, false, s)) return rc;
+  }
+  if (int rc = run_pass(kb, plan, timed, s)) return rc;
+  // combine: records | jump code | member maps in one upload
+  const size_t g_bytes = W.groups.size() * sizeof(WideGroupArgs);
+  const size_t p_at = g_bytes, m_at = (p_at + W.progs.size() + 15u) & ~(size_t)15u;
+  const size_t bytes = m_at + W.midx.size() * 4;
+  HIPCHK(hipStreamSynchronize(s));  // the upload buffer may still be read by the previous pass
+  if (int rc = ensure(&D.wg_data, &D.wg_data_cap, bytes)) return rc;
+  std::vector<uint8_t> h(bytes, 0);
+  memcpy(h.data(), W.groups.data(), g_bytes);
+  memcpy(h.data() + p_at, W.progs.data(), W.progs.size());
+  memcpy(h.data() + m_at, W.midx.data(), W.midx.size() * 4);
+  HIPCHK(hipMemcpyAsync(D.wg_data, h.data(), bytes, hipMemcpyHostToDevice, s));
+  const uint64_t pairs = n * W.groups.size();
+  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((pairs + 255) / 256, 1024));
+  const size_t stack_words = std::max<uint32_t>(W.stack_words, 1);
+  if (int rc = ensure(&D.wg_stack, &D.wg_stack_cap, (size_t)grid * 256 * stack_words)) return rc;
+  if (int rc = ensure(&D.big_causes, &D.big_causes_cap, (size_t)(n * W.cause_stride))) return rc;
+  HIPCHK(hipMemsetAsync(D.big_causes, 0, (size_t)(n * W.cause_stride) * 8, s));
+  WideGroupPass w;
+  memset(&w, 0, sizeof(w));
+  w.groups = (const WideGroupArgs*)D.wg_data;
+  w.ngroups = (uint32_t)W.groups.size();
+  w.progs = D.wg_data + p_at;
+  w.midx = (const uint32_t*)(D.wg_data + m_at);
+  w.member_words = D.member_words;
+  w.nmw = (uint32_t)nm;
+  w.out = D.verdicts;
+  w.npol = plan.args.npol;
+  w.rowcol = plan.rows_mode ? D.rowcol : nullptr;
+  w.causes = D.big_causes;
+  w.cause_stride = W.cause_stride;
+  w.stack = D.wg_stack;
+  w.stack_words = (uint32_t)stack_words;
+  w.nrows = n;
+  HIPCHK(launch_wide_groups(w, grid, s));
+  D.last_big_stride = W.cause_stride;
+  for (size_t k = 0; k < W.groups.size(); ++k)
+    D.last_big_ref.push_back({W.policy[k], W.groups[k].cause_off, W.groups[k].cause_words});
+  HIPCHK(hipStreamSynchronize(s));  // the host copy `h` is freed on return
+  return KW_OK;
+}
+
 int validate_common(const kw_env* env, kw_batch* kb, const int32_t* policies, uint32_t npol, const int32_t* row_policy,
                     int origin, PassPlan* plan) {
   if (!env || !kb) return KW_E_ARG;
@@ -1296,6 +1424,29 @@ int kw_debug_host_walk(const kw_env* env, const kw_batch* kb, const int32_t* pol
       }
     }
   }
+  // wide groups: their members' words by the same host walk, then the jump code per row
+  PassPlan wp;
+  plan_wide_groups(E, std::vector<int32_t>(policies, policies + npol), nullptr, origin, &wp);
+  const PassPlan::Wide& W = wp.wide;
+  if (!W.groups.empty()) {
+    const size_t nm = W.members.size();
+    std::vector<uint32_t> mw(B.n * nm);
+    if (int rc = kw_debug_host_walk(env, kb, W.members.data(), (uint32_t)nm, origin, mw.data())) return rc;
+    std::vector<uint64_t> stack(std::max<uint32_t>(W.stack_words, 1));
+    for (uint64_t r = 0; r < B.n; ++r)
+      for (const WideGroupArgs& g : W.groups) {
+        uint32_t* dst = out + r * npol + g.col;
+        if (*dst == kBypassWord) continue;
+        const bool v = run_wide_prog(
+            W.progs.data() + g.prog_off, g.prog_len, stack.data(),
+            [&](uint32_t m) {
+              const uint32_t x = mw[r * nm + W.midx[g.midx_off + m]];
+              return (x & KW_V_ALLOWED) && !(x & KW_V_MUTATED);
+            },
+            [](uint32_t) {});
+        *dst = v ? g.okw : g.rejb;
+      }
+  }
   return KW_OK;
 }
 
@@ -1472,14 +1623,14 @@ void kw_batch_destroy(kw_batch* b) { delete b; }
 int kw_validate_batch(const kw_env* env, kw_batch* b, const int32_t* policies, uint32_t npol, int origin, void* stream) {
   PassPlan plan;
   if (int rc = validate_common(env, b, policies, npol, nullptr, origin, &plan)) return rc;
-  return run_pass(b, plan, false, stream ? (hipStream_t)stream : b->dev->stream);
+  return run_validate(env, b, plan, origin, false, stream ? (hipStream_t)stream : b->dev->stream);
 }
 
 int kw_validate_rows(const kw_env* env, kw_batch* b, const int32_t* row_policy, int origin, void* stream) {
   if (!row_policy) return KW_E_ARG;
   PassPlan plan;
   if (int rc = validate_common(env, b, nullptr, 0, row_policy, origin, &plan)) return rc;
-  return run_pass(b, plan, false, stream ? (hipStream_t)stream : b->dev->stream);
+  return run_validate(env, b, plan, origin, false, stream ? (hipStream_t)stream : b->dev->stream);
 }
 
 int kw_batch_verdicts(kw_batch* b, uint32_t* host_out, size_t count) {
@@ -1513,6 +1664,12 @@ int kw_batch_verdicts(kw_batch* b, uint32_t* host_out, size_t count) {
   W.nwide = D.last_nwide;
   W.wide_policy = D.last_wide_policy;
   W.rows_mode = D.last_rows_mode;
+  if (D.last_big_stride && D.big_causes) {  // wide-group cause bitsets
+    W.big_stride = D.last_big_stride;
+    W.big_ref = D.last_big_ref;
+    W.big.resize(b->b.n * W.big_stride);
+    if (!W.big.empty()) HIPCHK(hipMemcpyAsync(W.big.data(), D.big_causes, W.big.size() * 8, hipMemcpyDeviceToHost, s));
+  }
   if (W.nwide) {
     W.groups.resize(b->b.n * W.nwide);
     if (!W.groups.empty())
@@ -1563,6 +1720,22 @@ int kw_debug_plan(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
   return rc;
 }
 
+int kw_batch_group_causes(const kw_batch* b, uint64_t row, int32_t policy, uint32_t verdict, uint64_t* words,
+                          size_t nwords, size_t* needed) {
+  if (!b || (!words && nwords)) return KW_E_ARG;
+  if (KW_REASON(verdict) != KW_R_GROUP) return KW_E_ARG;
+  const WideData& W = b->b.wide;
+  uint32_t bw = 0;
+  const uint64_t* big = W.lookup_big(row, policy, &bw);
+  uint64_t one = KW_ARG(verdict);
+  if (!big && KW_ARG(verdict) == kArgWide && !W.lookup(row, policy, &one)) return KW_E_NOT_FOUND;
+  const size_t n = big ? bw : 1u;
+  if (needed) *needed = n;
+  if (nwords < n) return KW_E_NOSPACE;
+  for (size_t k = 0; k < n; ++k) words[k] = big ? big[k] : one;
+  return KW_OK;
+}
+
 int kw_batch_wide_arg(const kw_batch* b, uint64_t row, int32_t policy, uint64_t* value) {
   if (!b || !value) return KW_E_ARG;
   return b->b.wide.lookup(row, policy, value) ? KW_OK : KW_E_NOT_FOUND;
@@ -1577,11 +1750,11 @@ int kw_validate_timed(const kw_env* env, kw_batch* b, const int32_t* policies, u
   for (auto& e : D.ev)
     if (!e) HIPCHK(hipEventCreate(&e));
   for (int i = 0; i < warmup; ++i)
-    if (int rc = run_pass(b, plan, false, D.stream)) return rc;
+    if (int rc = run_validate(env, b, plan, origin, false, D.stream)) return rc;
   HIPCHK(hipStreamSynchronize(D.stream));
   double ev = 0;
   for (int i = 0; i < reps; ++i) {
-    if (int rc = run_pass(b, plan, true, D.stream)) return rc;
+    if (int rc = run_validate(env, b, plan, origin, true, D.stream)) return rc;
     HIPCHK(hipEventSynchronize(D.ev[2]));
     float c = 0;
     HIPCHK(hipEventElapsedTime(&c, D.ev[0], D.ev[2]));

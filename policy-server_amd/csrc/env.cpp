@@ -509,6 +509,7 @@ size_t emit_dfa(const Dfa& dfa, const std::vector<uint32_t>& cls_map, std::vecto
   dd.nstates = dfa.nstates;
   dd.ncls = dfa.ncls;
   dd.start = dfa.start;
+  dd.abs_lo = dfa.abs_lo;
   memcpy(dd.cls, dfa.cls.data(), 256);
   put(b, dd);
   align16(b);
@@ -655,6 +656,7 @@ Status compile_kv(Env* env, DevHeader* hdr, std::vector<uint8_t>* b) {
         kv.ncls = (uint16_t)d.ncls;
         kv.start = d.start;
         kv.nstates = (uint16_t)d.nstates;
+        kv.abs_lo = (uint16_t)d.abs_lo;
         kv.t16 = d.nstates > 256 ? 1 : 0;
         kv.cbase = (uint16_t)cbase;
         const size_t rec = at16(sizeof(KvDfa));
@@ -846,11 +848,6 @@ Status build_env(const char* json, size_t len, bool continue_on_errors, const ch
   // group expressions (validated here; the reference evaluates them per request)
   for (auto& rec : env->pol) {
     if (!rec.is_group) continue;
-    if (rec.member_names.size() > (size_t)kMaxGroupMembers) {
-      rec.prog.valid = false;
-      rec.prog.error = "policy groups with more than 64 members are not supported by the engine";
-      continue;
-    }
     rec.prog = compile_group_expression(rec.expression, rec.member_names);
   }
 

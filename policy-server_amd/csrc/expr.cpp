@@ -1,82 +1,127 @@
-// expr.cpp — see expr.hpp. Recursive-descent parser with rhai precedence
-// (|| < && < comparison < + - < * / % < unary), static typing (member calls are bool, integer
-// literals are i64), constant folding of every call-free subtree, postfix emission.
+// expr.cpp — see expr.hpp. Lexer, recursive-descent parser with rhai precedence, a host
+// interpreter (validation, response messages, truth tables), constant folding of call-free
+// subtrees, and the device forms: short-circuit jump code or a truth table.
 #include "expr.hpp"
 
 #include <cctype>
-#include <memory>
+#include <climits>
+#include <map>
 
 #include "kwdev.hpp"
 
 namespace kw {
-namespace {
 
-enum class Tk { End, Ident, Int, LParen, RParen, Op, Bad };
-struct Token {
-  Tk t;
+// ------------------------------------------------------------------------------------------
+// Values and the tree
+// ------------------------------------------------------------------------------------------
+enum class VT : uint8_t { Unit, Bool, Int, Str };
+struct Val {
+  VT t = VT::Unit;
+  bool b = false;
+  int64_t i = 0;
   std::string s;
-  int64_t v = 0;
-  size_t pos = 0;
 };
+static const char* tname(VT t) { return t == VT::Bool ? "bool" : t == VT::Int ? "i64" : t == VT::Str ? "string" : "()"; }
 
 struct Node {
-  enum K { Const, Call, Not, Neg, Bin } k;
-  bool is_bool = true;  // type
-  bool bval = false;
-  int64_t ival = 0;
-  int slot = -1;
-  std::string op;
-  std::unique_ptr<Node> a, b;
+  enum K { Lit, Var, Call, Unary, Bin, If, Block, Let } k = Lit;
+  Val lit;            // Lit
+  std::string name;   // Var / Let
+  int slot = -1;      // Call
+  std::string op;     // Unary / Bin
+  std::vector<std::unique_ptr<Node>> kids;  // Unary: a; Bin: a b; If: cond then [else]; Block: statements; Let: init
+  bool tail = false;  // Block: its last statement is a value (no `;` after it)
 };
 using P = std::unique_ptr<Node>;
 
-struct Parser {
-  std::vector<Token> toks;
-  size_t i = 0;
-  const std::vector<std::string>& members;
-  std::string err;
-  explicit Parser(const std::vector<std::string>& m) : members(m) {}
+struct ExprAst {
+  P root;  // a Block (the script)
+};
 
-  bool lex(const std::string& s) {
+namespace {
+
+// ------------------------------------------------------------------------------------------
+// Lexer
+// ------------------------------------------------------------------------------------------
+enum class Tk { End, Ident, Int, Str, Punct };
+struct Token {
+  Tk t = Tk::End;
+  std::string s;
+  int64_t v = 0;
+};
+
+struct Lexer {
+  std::vector<Token> toks;
+  std::string err;
+  bool run(const std::string& s) {
     size_t k = 0;
     while (k < s.size()) {
-      char c = s[k];
+      const char c = s[k];
       if (isspace((unsigned char)c)) {
         ++k;
         continue;
       }
+      if (c == '/' && k + 1 < s.size() && s[k + 1] == '/') {  // line comment
+        while (k < s.size() && s[k] != '\n') ++k;
+        continue;
+      }
       Token t;
-      t.pos = k;
       if (isalpha((unsigned char)c) || c == '_') {
-        size_t b = k;
+        const size_t b = k;
         while (k < s.size() && (isalnum((unsigned char)s[k]) || s[k] == '_')) ++k;
         t.t = Tk::Ident;
         t.s = s.substr(b, k - b);
       } else if (isdigit((unsigned char)c)) {
-        size_t b = k;
+        const size_t b = k;
         while (k < s.size() && (isdigit((unsigned char)s[k]) || s[k] == '_')) ++k;
         std::string d;
         for (size_t j = b; j < k; ++j)
           if (s[j] != '_') d.push_back(s[j]);
-        if (d.size() > 18) {
+        if (d.size() > 19 || (d.size() == 19 && d > "9223372036854775807")) {
           err = "Syntax error: integer literal too large";
           return false;
         }
         t.t = Tk::Int;
         t.v = std::stoll(d);
-      } else if (c == '(') {
-        t.t = Tk::LParen;
+      } else if (c == '"') {
         ++k;
-      } else if (c == ')') {
-        t.t = Tk::RParen;
-        ++k;
+        t.t = Tk::Str;
+        bool closed = false;
+        while (k < s.size()) {
+          const char q = s[k++];
+          if (q == '"') {
+            closed = true;
+            break;
+          }
+          if (q != '\\') {
+            t.s.push_back(q);
+            continue;
+          }
+          if (k >= s.size()) break;
+          const char e = s[k++];
+          switch (e) {
+            case 'n': t.s.push_back('\n'); break;
+            case 't': t.s.push_back('\t'); break;
+            case 'r': t.s.push_back('\r'); break;
+            case '0': t.s.push_back('\0'); break;
+            case '\\': t.s.push_back('\\'); break;
+            case '"': t.s.push_back('"'); break;
+            case '\'': t.s.push_back('\''); break;
+            default: err = std::string("Syntax error: invalid escape sequence \\") + e; return false;
+          }
+        }
+        if (!closed) {
+          err = "Syntax error: unterminated string literal";
+          return false;
+        }
       } else {
-        static const char* ops[] = {"||", "&&", "==", "!=", "<=", ">=", "<", ">", "+", "-", "*", "/", "%", "!"};
+        static const char* ops[] = {"||", "&&", "==", "!=", "<=", ">=", "<", ">", "+", "-", "*", "/", "%",
+                                    "!",  "|",  "&",  "^",  "(",  ")",  "{", "}", ";", "="};
         bool ok = false;
         for (const char* o : ops) {
-          size_t n = std::char_traits<char>::length(o);
+          const size_t n = std::char_traits<char>::length(o);
           if (s.compare(k, n, o) == 0) {
-            t.t = Tk::Op;
+            t.t = Tk::Punct;
             t.s = o;
             k += n;
             ok = true;
@@ -84,317 +129,589 @@ struct Parser {
           }
         }
         if (!ok) {
-          err = std::string("Syntax error: unexpected character '") + c + "' (line 1, position " +
-                std::to_string(k + 1) + ")";
+          err = std::string("Syntax error: unexpected character '") + c + "'";
           return false;
         }
       }
       toks.push_back(t);
     }
-    Token e;
-    e.t = Tk::End;
-    e.pos = s.size();
-    toks.push_back(e);
+    toks.push_back(Token{});
     return true;
   }
+};
+
+bool is_kw(const std::string& s) { return s == "let" || s == "if" || s == "else" || s == "true" || s == "false"; }
+
+// ------------------------------------------------------------------------------------------
+// Parser (script mode: statements, blocks, if-else expressions)
+// ------------------------------------------------------------------------------------------
+struct Parser {
+  const std::vector<Token>& toks;
+  const std::vector<std::string>& members;
+  size_t i = 0;
+  std::string err;
+  Parser(const std::vector<Token>& t, const std::vector<std::string>& m) : toks(t), members(m) {}
 
   const Token& peek() const { return toks[i]; }
-  bool isop(const char* o) const { return peek().t == Tk::Op && peek().s == o; }
+  bool punct(const char* o) const { return peek().t == Tk::Punct && peek().s == o; }
+  bool ident(const char* o) const { return peek().t == Tk::Ident && peek().s == o; }
+  P fail(const std::string& m) {
+    if (err.empty()) err = m;
+    return nullptr;
+  }
+  std::string near() const {
+    const Token& t = peek();
+    if (t.t == Tk::End) return "end of script";
+    if (t.t == Tk::Int) return std::to_string(t.v);
+    if (t.t == Tk::Str) return "\"" + t.s + "\"";
+    return "'" + t.s + "'";
+  }
 
-  P bin(const std::string& op, P a, P b) {
-    auto n = std::make_unique<Node>();
-    n->k = Node::Bin;
-    n->op = op;
-    n->a = std::move(a);
-    n->b = std::move(b);
-    return n;
-  }
-  P expr() { return orx(); }
-  P orx() {
-    P l = andx();
-    while (l && isop("||")) {
-      ++i;
-      P r = andx();
-      if (!r) return nullptr;
-      l = bin("||", std::move(l), std::move(r));
+  // statements until `close` ("}" or end of script)
+  P block_body(bool top) {
+    auto b = std::make_unique<Node>();
+    b->k = Node::Block;
+    for (;;) {
+      if (top ? peek().t == Tk::End : punct("}")) break;
+      if (peek().t == Tk::End) return fail("Syntax error: expecting '}' to close the block");
+      P st;
+      bool block_like = false;
+      if (ident("let")) {
+        ++i;
+        if (peek().t != Tk::Ident || is_kw(peek().s)) return fail("Syntax error: expecting a variable name after 'let'");
+        auto l = std::make_unique<Node>();
+        l->k = Node::Let;
+        l->name = peek().s;
+        ++i;
+        if (!punct("=")) return fail("Syntax error: expecting '=' after the variable name");
+        ++i;
+        P init = expr();
+        if (!init) return nullptr;
+        l->kids.push_back(std::move(init));
+        st = std::move(l);
+      } else {
+        block_like = ident("if") || punct("{");
+        st = expr();
+        if (!st) return nullptr;
+      }
+      const bool is_let = st->k == Node::Let;
+      b->kids.push_back(std::move(st));
+      if (punct(";")) {
+        ++i;
+        b->tail = false;
+        continue;
+      }
+      if (top ? peek().t == Tk::End : punct("}")) {
+        b->tail = !is_let;
+        break;
+      }
+      if (!block_like) return fail("Syntax error: expecting ';' to terminate this statement, found " + near());
+      b->tail = false;
     }
-    return l;
+    return b;
   }
-  P andx() {
-    P l = cmp();
-    while (l && isop("&&")) {
-      ++i;
-      P r = cmp();
-      if (!r) return nullptr;
-      l = bin("&&", std::move(l), std::move(r));
-    }
-    return l;
+
+  // precedence climbing: || | ^ (30), && & (60), == != (90), < <= > >= (110), + - (150), * / % (180)
+  static int prec(const Token& t) {
+    if (t.t != Tk::Punct) return -1;
+    const std::string& o = t.s;
+    if (o == "||" || o == "|" || o == "^") return 30;
+    if (o == "&&" || o == "&") return 60;
+    if (o == "==" || o == "!=") return 90;
+    if (o == "<" || o == "<=" || o == ">" || o == ">=") return 110;
+    if (o == "+" || o == "-") return 150;
+    if (o == "*" || o == "/" || o == "%") return 180;
+    return -1;
   }
-  P cmp() {
-    P l = add();
-    while (l && (isop("==") || isop("!=") || isop("<") || isop("<=") || isop(">") || isop(">="))) {
-      std::string op = peek().s;
-      ++i;
-      P r = add();
-      if (!r) return nullptr;
-      l = bin(op, std::move(l), std::move(r));
-    }
-    return l;
-  }
-  P add() {
-    P l = mul();
-    while (l && (isop("+") || isop("-"))) {
-      std::string op = peek().s;
-      ++i;
-      P r = mul();
-      if (!r) return nullptr;
-      l = bin(op, std::move(l), std::move(r));
-    }
-    return l;
-  }
-  P mul() {
+  P expr(int min_prec = 0) {
     P l = unary();
-    while (l && (isop("*") || isop("/") || isop("%"))) {
-      std::string op = peek().s;
+    while (l) {
+      const int p = prec(peek());
+      if (p < 0 || p < min_prec) break;
+      auto n = std::make_unique<Node>();
+      n->k = Node::Bin;
+      n->op = peek().s;
       ++i;
-      P r = unary();
+      P r = expr(p + 1);
       if (!r) return nullptr;
-      l = bin(op, std::move(l), std::move(r));
+      n->kids.push_back(std::move(l));
+      n->kids.push_back(std::move(r));
+      l = std::move(n);
     }
     return l;
   }
   P unary() {
-    if (isop("!") || isop("-")) {
-      bool neg = peek().s == "-";
+    if (punct("!") || punct("-") || punct("+")) {
+      auto n = std::make_unique<Node>();
+      n->k = Node::Unary;
+      n->op = peek().s;
       ++i;
       P a = unary();
       if (!a) return nullptr;
-      auto n = std::make_unique<Node>();
-      n->k = neg ? Node::Neg : Node::Not;
-      n->a = std::move(a);
+      n->kids.push_back(std::move(a));
       return n;
     }
     return primary();
   }
   P primary() {
-    const Token& t = peek();
+    const Token t = peek();
     auto n = std::make_unique<Node>();
     if (t.t == Tk::Int) {
       ++i;
-      n->k = Node::Const;
-      n->is_bool = false;
-      n->ival = t.v;
+      n->lit.t = VT::Int;
+      n->lit.i = t.v;
       return n;
     }
-    if (t.t == Tk::LParen) {
+    if (t.t == Tk::Str) {
+      ++i;
+      n->lit.t = VT::Str;
+      n->lit.s = t.s;
+      return n;
+    }
+    if (punct("(")) {
       ++i;
       P e = expr();
       if (!e) return nullptr;
-      if (peek().t != Tk::RParen) {
-        err = "Syntax error: expecting ')' (line 1, position " + std::to_string(peek().pos + 1) + ")";
-        return nullptr;
-      }
+      if (!punct(")")) return fail("Syntax error: expecting ')', found " + near());
       ++i;
       return e;
     }
-    if (t.t == Tk::Ident) {
-      std::string name = t.s;
+    if (punct("{")) {
       ++i;
-      if (name == "true" || name == "false") {
-        n->k = Node::Const;
-        n->bval = name == "true";
+      P b = block_body(false);
+      if (!b) return nullptr;
+      ++i;  // '}'
+      return b;
+    }
+    if (t.t == Tk::Ident) {
+      ++i;
+      if (t.s == "true" || t.s == "false") {
+        n->lit.t = VT::Bool;
+        n->lit.b = t.s == "true";
         return n;
       }
-      if (peek().t != Tk::LParen) {
-        err = "Variable not found: " + name + " (line 1, position " + std::to_string(t.pos + 1) + ")";
-        return nullptr;
+      if (t.s == "if") {
+        n->k = Node::If;
+        P c = expr();
+        if (!c) return nullptr;
+        n->kids.push_back(std::move(c));
+        if (!punct("{")) return fail("Syntax error: expecting '{' after the if condition, found " + near());
+        ++i;
+        P th = block_body(false);
+        if (!th) return nullptr;
+        ++i;
+        n->kids.push_back(std::move(th));
+        if (ident("else")) {
+          ++i;
+          if (ident("if")) {
+            P e = primary();
+            if (!e) return nullptr;
+            n->kids.push_back(std::move(e));
+          } else {
+            if (!punct("{")) return fail("Syntax error: expecting '{' or 'if' after 'else', found " + near());
+            ++i;
+            P e = block_body(false);
+            if (!e) return nullptr;
+            ++i;
+            n->kids.push_back(std::move(e));
+          }
+        }
+        return n;
+      }
+      if (t.s == "let" || t.s == "else") return fail("Syntax error: unexpected '" + t.s + "'");
+      if (!punct("(")) {
+        n->k = Node::Var;
+        n->name = t.s;
+        return n;
       }
       ++i;
-      if (peek().t != Tk::RParen) {
-        err = "Syntax error: member policies take no arguments (line 1, position " +
-              std::to_string(peek().pos + 1) + ")";
-        return nullptr;
-      }
+      if (!punct(")")) return fail("Syntax error: member policies take no arguments");
       ++i;
       int slot = -1;
       for (size_t m = 0; m < members.size(); ++m)
-        if (members[m] == name) slot = (int)m;
-      if (slot < 0) {
-        err = "Function not found: " + name + " () (line 1, position " + std::to_string(t.pos + 1) + ")";
-        return nullptr;
-      }
+        if (members[m] == t.s) slot = (int)m;
       n->k = Node::Call;
-      n->slot = slot;
+      n->slot = slot;  // -1: "Function not found" when called (rhai resolves at run time)
+      n->name = t.s;
       return n;
     }
-    if (t.t == Tk::End) err = "Syntax error: expecting an expression (line 1, position " + std::to_string(t.pos + 1) + ")";
-    else err = "Syntax error: unexpected '" + t.s + "' (line 1, position " + std::to_string(t.pos + 1) + ")";
-    return nullptr;
+    if (t.t == Tk::End) return fail("Syntax error: expecting an expression, found end of script");
+    return fail("Syntax error: unexpected " + near());
   }
 };
 
-const char* tname(const Node& n) { return n.is_bool ? "bool" : "i64"; }
+// ------------------------------------------------------------------------------------------
+// Interpreter
+// ------------------------------------------------------------------------------------------
+struct Interp {
+  std::function<bool(uint32_t)> ok;
+  std::vector<std::pair<std::string, Val>> vars;
+  std::vector<uint32_t> called;
+  std::vector<uint8_t> seen;
+  std::string err;
+  explicit Interp(std::function<bool(uint32_t)> f) : ok(std::move(f)) {}
 
-// type check + constant fold; returns false with err on a type error
-bool check(Node* n, std::string* err) {
-  switch (n->k) {
-    case Node::Const:
-    case Node::Call: return true;
-    case Node::Not:
-      if (!check(n->a.get(), err)) return false;
-      if (!n->a->is_bool) {
-        *err = "Function not found: ! (i64)";
-        return false;
-      }
-      n->is_bool = true;
-      if (n->a->k == Node::Const) {
-        n->k = Node::Const;
-        n->bval = !n->a->bval;
-        n->a.reset();
-      }
-      return true;
-    case Node::Neg:
-      if (!check(n->a.get(), err)) return false;
-      if (n->a->is_bool) {
-        *err = "Function not found: - (bool)";
-        return false;
-      }
-      n->is_bool = false;
-      n->k = Node::Const;
-      n->ival = -n->a->ival;
-      n->a.reset();
-      return true;
-    case Node::Bin: {
-      if (!check(n->a.get(), err) || !check(n->b.get(), err)) return false;
-      Node& a = *n->a;
-      Node& b = *n->b;
-      const std::string& op = n->op;
-      if (op == "&&" || op == "||") {
-        if (!a.is_bool || !b.is_bool) {
-          *err = "Function not found: " + op + " (" + tname(a) + ", " + tname(b) + ")";
-          return false;
+  bool fail(const std::string& m) {
+    err = m;
+    return false;
+  }
+  bool nf(const std::string& op, const Val& a, const Val& b) {
+    return fail("Function not found: " + op + " (" + tname(a.t) + ", " + tname(b.t) + ")");
+  }
+
+  bool eval(const Node* n, Val* out) {
+    switch (n->k) {
+      case Node::Lit: *out = n->lit; return true;
+      case Node::Var:
+        for (size_t k = vars.size(); k-- > 0;)
+          if (vars[k].first == n->name) {
+            *out = vars[k].second;
+            return true;
+          }
+        return fail("Variable not found: " + n->name);
+      case Node::Call: {
+        if (n->slot < 0) return fail("Function not found: " + n->name + " ()");
+        const uint32_t s = (uint32_t)n->slot;
+        if (s >= seen.size()) seen.resize(s + 1, 0);
+        if (!seen[s]) {
+          seen[s] = 1;
+          called.push_back(s);
         }
-        n->is_bool = true;
-        if (a.k == Node::Const && b.k == Node::Const) {
-          bool v = op == "&&" ? (a.bval && b.bval) : (a.bval || b.bval);
-          n->k = Node::Const;
-          n->bval = v;
-          n->a.reset();
-          n->b.reset();
-        }
+        out->t = VT::Bool;
+        out->b = ok(s);
         return true;
       }
-      if (op == "==" || op == "!=") {
-        if (a.is_bool != b.is_bool) {
-          *err = "Function not found: " + op + " (" + tname(a) + ", " + tname(b) + ")";
-          return false;
+      case Node::Unary: {
+        Val a;
+        if (!eval(n->kids[0].get(), &a)) return false;
+        if (n->op == "!") {
+          if (a.t != VT::Bool) return fail(std::string("Function not found: ! (") + tname(a.t) + ")");
+          out->t = VT::Bool;
+          out->b = !a.b;
+          return true;
         }
-        n->is_bool = true;
-        if (a.k == Node::Const && b.k == Node::Const) {
-          bool eq = a.is_bool ? a.bval == b.bval : a.ival == b.ival;
-          n->k = Node::Const;
-          n->bval = op == "==" ? eq : !eq;
-          n->a.reset();
-          n->b.reset();
-        }
+        if (a.t != VT::Int) return fail("Function not found: " + n->op + " (" + tname(a.t) + ")");
+        if (n->op == "-" && a.i == INT64_MIN) return fail("Negation overflow: -" + std::to_string(a.i));
+        *out = a;
+        if (n->op == "-") out->i = -a.i;
         return true;
       }
-      // int-only operators
-      if (a.is_bool || b.is_bool) {
-        *err = "Function not found: " + op + " (" + tname(a) + ", " + tname(b) + ")";
-        return false;
-      }
-      // both int -> both constant (no member call returns an int)
-      int64_t x = a.ival, y = b.ival;
-      n->k = Node::Const;
-      n->a.reset();
-      n->b.reset();
-      if (op == "<" || op == "<=" || op == ">" || op == ">=") {
-        n->is_bool = true;
-        n->bval = op == "<" ? x < y : op == "<=" ? x <= y : op == ">" ? x > y : x >= y;
+      case Node::Bin: return bin(n, out);
+      case Node::If: {
+        Val c;
+        if (!eval(n->kids[0].get(), &c)) return false;
+        if (c.t != VT::Bool) return fail("Boolean value expected for the if condition, found " + std::string(tname(c.t)));
+        if (c.b) return eval(n->kids[1].get(), out);
+        if (n->kids.size() > 2) return eval(n->kids[2].get(), out);
+        *out = Val{};
         return true;
       }
-      n->is_bool = false;
-      if ((op == "/" || op == "%") && y == 0) {
-        *err = "Division by zero: " + std::to_string(x) + " " + op + " 0";
-        return false;
+      case Node::Block: {
+        const size_t scope = vars.size();
+        Val v;
+        for (size_t k = 0; k < n->kids.size(); ++k) {
+          const Node* st = n->kids[k].get();
+          if (st->k == Node::Let) {
+            Val x;
+            if (!eval(st->kids[0].get(), &x)) return false;
+            vars.push_back({st->name, x});
+            v = Val{};
+          } else if (!eval(st, &v)) {
+            return false;
+          }
+        }
+        vars.resize(scope);
+        *out = n->tail ? v : Val{};
+        return true;
       }
-      n->ival = op == "+" ? x + y : op == "-" ? x - y : op == "*" ? x * y : op == "/" ? x / y : x % y;
+      case Node::Let: *out = Val{}; return true;  // (handled by Block)
+    }
+    return fail("internal: bad node");
+  }
+
+  bool bin(const Node* n, Val* out) {
+    const std::string& op = n->op;
+    Val a, b;
+    if (!eval(n->kids[0].get(), &a)) return false;
+    if (op == "||" || op == "&&") {
+      if (a.t != VT::Bool) return fail("Function not found: " + op + " (" + tname(a.t) + ", ...)");
+      if ((op == "||") == a.b) {  // short circuit
+        out->t = VT::Bool;
+        out->b = a.b;
+        return true;
+      }
+      if (!eval(n->kids[1].get(), &b)) return false;
+      if (b.t != VT::Bool) return nf(op, a, b);
+      *out = b;
       return true;
     }
+    if (!eval(n->kids[1].get(), &b)) return false;
+    out->t = VT::Bool;
+    if (op == "==" || op == "!=") {  // different types: false (!= true), rhai's built-in comparison
+      bool eq = a.t == b.t && (a.t == VT::Unit || (a.t == VT::Bool && a.b == b.b) || (a.t == VT::Int && a.i == b.i) ||
+                               (a.t == VT::Str && a.s == b.s));
+      out->b = op == "==" ? eq : !eq;
+      return true;
+    }
+    if (op == "<" || op == "<=" || op == ">" || op == ">=") {
+      if (a.t != b.t) {
+        out->b = false;
+        return true;
+      }
+      int c;
+      if (a.t == VT::Int) c = a.i < b.i ? -1 : a.i > b.i ? 1 : 0;
+      else if (a.t == VT::Str) c = a.s.compare(b.s) < 0 ? -1 : a.s == b.s ? 0 : 1;
+      else return nf(op, a, b);
+      out->b = op == "<" ? c < 0 : op == "<=" ? c <= 0 : op == ">" ? c > 0 : c >= 0;
+      return true;
+    }
+    if (op == "|" || op == "&" || op == "^") {
+      if (a.t == VT::Bool && b.t == VT::Bool) {
+        out->b = op == "|" ? (a.b || b.b) : op == "&" ? (a.b && b.b) : (a.b != b.b);
+        return true;
+      }
+      if (a.t == VT::Int && b.t == VT::Int) {
+        out->t = VT::Int;
+        out->i = op == "|" ? (a.i | b.i) : op == "&" ? (a.i & b.i) : (a.i ^ b.i);
+        return true;
+      }
+      return nf(op, a, b);
+    }
+    if (op == "+" && a.t == VT::Str && b.t == VT::Str) {
+      out->t = VT::Str;
+      out->s = a.s + b.s;
+      return true;
+    }
+    if (a.t != VT::Int || b.t != VT::Int) return nf(op, a, b);
+    out->t = VT::Int;
+    const std::string expr = std::to_string(a.i) + " " + op + " " + std::to_string(b.i);
+    long long r = 0;
+    if (op == "+") {
+      if (__builtin_add_overflow(a.i, b.i, &r)) return fail("Addition overflow: " + expr);
+    } else if (op == "-") {
+      if (__builtin_sub_overflow(a.i, b.i, &r)) return fail("Subtraction overflow: " + expr);
+    } else if (op == "*") {
+      if (__builtin_mul_overflow(a.i, b.i, &r)) return fail("Multiplication overflow: " + expr);
+    } else {  // / %
+      if (b.i == 0) return fail("Division by zero: " + expr);
+      if (a.i == INT64_MIN && b.i == -1) return fail((op == "/" ? "Division overflow: " : "Modulo overflow: ") + expr);
+      r = op == "/" ? a.i / b.i : a.i % b.i;
+    }
+    out->i = r;
+    return true;
   }
-  return true;
+};
+
+ExprOutcome run_ast(const ExprAst& ast, const std::function<bool(uint32_t)>& ok) {
+  Interp in(ok);
+  Val v;
+  ExprOutcome o;
+  if (!in.eval(ast.root.get(), &v)) {
+    o.error = true;
+    o.message = in.err;
+  } else if (v.t != VT::Bool) {
+    o.error = true;
+    o.message = std::string("Output type incorrect: ") + tname(v.t) + " (expecting bool)";
+  } else {
+    o.value = v.b;
+  }
+  o.called = std::move(in.called);
+  return o;
 }
 
-// Short-circuit jump code (kwdev.hpp GOp): a || b = a, JT end, b; a && b = a, JF end, b; the other
-// operators evaluate both sides. Only == / != deepen the value stack.
-void emit(const Node* n, std::vector<uint8_t>* code, int depth, int* maxdepth) {
+// ------------------------------------------------------------------------------------------
+// Folding and the bool-only subset
+// ------------------------------------------------------------------------------------------
+bool has_call(const Node* n) {
+  if (n->k == Node::Call) return true;
+  for (const P& k : n->kids)
+    if (has_call(k.get())) return true;
+  return false;
+}
+
+bool has_call_or_var(const Node* n) {
+  if (n->k == Node::Call || n->k == Node::Var || n->k == Node::Let) return true;
+  for (const P& k : n->kids)
+    if (has_call_or_var(k.get())) return true;
+  return false;
+}
+
+// Replace every call-free, variable-free subtree whose evaluation succeeds by its value (an erroring
+// one stays: it may never run, e.g. behind a short circuit).
+void fold(P* np) {
+  Node* n = np->get();
+  for (P& k : n->kids) fold(&k);
+  if (n->k == Node::Lit || has_call_or_var(n)) return;
+  const std::function<bool(uint32_t)> none = [](uint32_t) { return false; };
+  Interp in(none);
+  Val v;
+  if (!in.eval(n, &v)) return;
+  auto l = std::make_unique<Node>();
+  l->lit = v;
+  *np = std::move(l);
+}
+
+// bool-only: bool literals, member calls, ! && || == != (== / != over bools), a script that is a
+// single tail expression
+const Node* bool_root(const ExprAst& a) {
+  const Node* r = a.root.get();
+  while (r->k == Node::Block && r->tail && r->kids.size() == 1) r = r->kids[0].get();
+  return r;
+}
+bool is_bool_subset(const Node* n) {
+  switch (n->k) {
+    case Node::Lit: return n->lit.t == VT::Bool;
+    case Node::Call: return n->slot >= 0;
+    case Node::Unary: return n->op == "!" && is_bool_subset(n->kids[0].get());
+    case Node::Bin:
+      if (n->op != "&&" && n->op != "||" && n->op != "==" && n->op != "!=") return false;
+      return is_bool_subset(n->kids[0].get()) && is_bool_subset(n->kids[1].get());
+    case Node::Block: return n->tail && n->kids.size() == 1 && is_bool_subset(n->kids[0].get());
+    default: return false;
+  }
+}
+
+// Short-circuit jump code (kwdev.hpp GOp): a || b = a, JT end, b; a && b = a, JF end, b; == / !=
+// evaluate both sides and deepen the value stack by one.
+void emit(const Node* n, bool wide, std::vector<uint8_t>* code, uint32_t depth, uint32_t* maxdepth) {
   if (depth > *maxdepth) *maxdepth = depth;
   switch (n->k) {
-    case Node::Const: code->push_back(n->bval ? G_CONST1 : G_CONST0); return;
+    case Node::Lit: code->push_back(n->lit.b ? G_CONST1 : G_CONST0); return;
     case Node::Call:
-      code->push_back(G_CALL);
-      code->push_back((uint8_t)n->slot);
+      if (wide) {
+        code->push_back(G_CALL16);
+        code->push_back((uint8_t)(n->slot & 0xff));
+        code->push_back((uint8_t)(n->slot >> 8));
+      } else {
+        code->push_back(G_CALL);
+        code->push_back((uint8_t)n->slot);
+      }
       return;
-    case Node::Not:
-      emit(n->a.get(), code, depth, maxdepth);
+    case Node::Unary:
+      emit(n->kids[0].get(), wide, code, depth, maxdepth);
       code->push_back(G_NOT);
       return;
-    case Node::Neg: return;  // folded
+    case Node::Block: emit(n->kids[0].get(), wide, code, depth, maxdepth); return;
     case Node::Bin:
-      emit(n->a.get(), code, depth, maxdepth);
+      emit(n->kids[0].get(), wide, code, depth, maxdepth);
       if (n->op == "&&" || n->op == "||") {
         code->push_back(n->op == "&&" ? G_JF : G_JT);
         const size_t at = code->size();
         code->push_back(0);
         code->push_back(0);
-        emit(n->b.get(), code, depth, maxdepth);
-        (*code)[at] = (uint8_t)(code->size() & 0xff);
-        (*code)[at + 1] = (uint8_t)(code->size() >> 8);
+        if (wide) {
+          code->push_back(0);
+          code->push_back(0);
+        }
+        emit(n->kids[1].get(), wide, code, depth, maxdepth);
+        const size_t to = code->size();
+        (*code)[at] = (uint8_t)(to & 0xff);
+        (*code)[at + 1] = (uint8_t)((to >> 8) & 0xff);
+        if (wide) {
+          (*code)[at + 2] = (uint8_t)((to >> 16) & 0xff);
+          (*code)[at + 3] = (uint8_t)(to >> 24);
+        }
         return;
       }
-      emit(n->b.get(), code, depth + 1, maxdepth);
+      emit(n->kids[1].get(), wide, code, depth + 1, maxdepth);
       code->push_back(n->op == "==" ? G_EQ : G_NE);
       return;
+    default: return;
   }
 }
 
 }  // namespace
 
+std::string group_eval_message(const std::string& m) {
+  if (m.rfind("Output type incorrect", 0) == 0) return "policy group expression did not evaluate to a boolean: " + m;
+  return "policy group expression evaluation failed: " + m;
+}
+
+ExprOutcome GroupProgram::run(const std::function<bool(uint32_t)>& member_ok) const {
+  if (!ast) {
+    ExprOutcome o;
+    o.error = true;
+    o.message = error;
+    return o;
+  }
+  return run_ast(*ast, member_ok);
+}
+
 GroupProgram compile_group_expression(const std::string& expr, const std::vector<std::string>& members) {
   GroupProgram g;
-  Parser p(members);
-  if (!p.lex(expr)) {
-    g.error = p.err;
+  g.nmem = (uint32_t)members.size();
+  Lexer lx;
+  if (!lx.run(expr)) {
+    g.error = lx.err;
     return g;
   }
-  P root = p.expr();
-  if (root && p.peek().t != Tk::End) {
-    p.err = "Syntax error: unexpected '" + p.peek().s + "' (line 1, position " + std::to_string(p.peek().pos + 1) + ")";
-    root.reset();
-  }
+  Parser p(lx.toks, members);
+  P root = p.block_body(true);
   if (!root) {
     g.error = p.err;
     return g;
   }
-  std::string terr;
-  if (!check(root.get(), &terr)) {
-    g.error = terr;
-    return g;
+  auto ast = std::make_shared<ExprAst>();
+  ast->root = std::move(root);
+  // validation: the script runs with every member returning true (validate_settings)
+  {
+    Interp in([](uint32_t) { return true; });
+    Val v;
+    if (!in.eval(ast->root.get(), &v)) {
+      g.error = in.err;
+      return g;
+    }
   }
   g.valid = true;
-  if (!root->is_bool) {
-    // rhai accepts the expression at validation time but evaluation yields an i64
-    g.eval_error = true;
-    g.eval_message = "policy group expression did not evaluate to a boolean: Output type incorrect: i64 (expecting bool)";
+  fold(&ast->root);
+  g.ast = ast;
+  // a script without member calls has one outcome: a constant column or a constant program
+  if (!has_call(ast->root.get())) {
+    const ExprOutcome o = run_ast(*ast, [](uint32_t) { return true; });
+    if (o.error) {
+      g.eval_error = true;
+      g.eval_message = group_eval_message(o.message);
+      return g;
+    }
+    g.code.push_back(o.value ? G_CONST1 : G_CONST0);
+    g.depth = 1;
     return g;
   }
-  int maxd = 1;
-  emit(root.get(), &g.code, 1, &maxd);
-  if (maxd > kMaxGroupStack || g.code.size() > 65535) {
-    g.valid = false;
-    g.error = "policy group expression nests too deeply for the engine (max stack 64)";
+  const Node* br = bool_root(*ast);
+  if (is_bool_subset(br)) {
+    uint32_t maxd = 1;
+    emit(br, false, &g.code, 1, &maxd);
+    g.depth = maxd;
+    if (members.size() <= (size_t)kMaxGroupMembers && maxd <= (uint32_t)kMaxGroupStack && g.code.size() <= 65535) return g;
+    // the wide path: u16 member operands, u32 jump targets, a value stack in global scratch
     g.code.clear();
+    maxd = 1;
+    emit(br, true, &g.code, 1, &maxd);
+    g.depth = maxd;
+    if (members.size() > 65535 || maxd > kMaxWideStack) {
+      g.valid = false;
+      g.error = "policy group expression exceeds the engine's limits (65535 members, value stack 65536)";
+      g.code.clear();
+      return g;
+    }
+    g.wide = true;
+    return g;
+  }
+  if (members.size() > kMaxTableMembers) {
+    g.valid = false;
+    g.error = "policy group expression uses let / if / string / integer values with more than 16 members, which the "
+              "engine does not evaluate";
+    return g;
+  }
+  // truth table over the member results: value, error, and the members called that rejected
+  const uint32_t n = (uint32_t)members.size();
+  g.table.assign((size_t)1 << n, 0);
+  for (uint32_t mask = 0; mask < (1u << n); ++mask) {
+    const ExprOutcome o = run_ast(*ast, [mask](uint32_t s) { return ((mask >> s) & 1u) != 0; });
+    uint32_t e = o.error ? kGtError : (o.value ? kGtValue : 0u);
+    for (uint32_t s : o.called)
+      if (!((mask >> s) & 1u)) e |= 1u << (16 + s);
+    g.table[mask] = e;
   }
   return g;
 }

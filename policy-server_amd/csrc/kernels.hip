@@ -50,6 +50,12 @@
 #ifndef KW_MIN_WAVES  // tile kernel: minimum waves per SIMD the register allocation must allow
 #define KW_MIN_WAVES 1
 #endif
+#ifndef KW_KV_ABSORB  // label-value walks also stop at absorbing states (same-box A/B r03 v2: C4 -0.5 %, C3 -0.9 %)
+#define KW_KV_ABSORB 1
+#endif
+#ifndef KW_LATE_ATOMIC  // tile kernel: the counter fetch for the tile after next issued after the staging barrier (r03 v2: neutral, off)
+#define KW_LATE_ATOMIC 0
+#endif
 
 namespace kw {
 
@@ -120,7 +126,7 @@ struct DfaView {
   const uint8_t* cls;     // 256
   const uint16_t* trans;  // [state][ncls]
   const uint16_t* acc;    // [state] global class
-  uint32_t ncls, start;
+  uint32_t ncls, start, abs_lo;
 };
 __device__ inline DfaView chain_view(const Chain& c, uint32_t off) {
   const uint8_t* base = c.base + (off - c.head);
@@ -129,6 +135,7 @@ __device__ inline DfaView chain_view(const Chain& c, uint32_t off) {
   v.cls = h->cls;
   v.ncls = h->ncls;
   v.start = h->start;
+  v.abs_lo = h->abs_lo;
   v.trans = (const uint16_t*)(base + (h->trans_off - off));
   v.acc = (const uint16_t*)(base + (h->acc_off - off));
   return v;
@@ -139,9 +146,10 @@ __device__ inline uint32_t step(const DfaView& d, uint32_t st, uint32_t byte) { 
 
 // Walk bytes [b, e) in 8-byte windows: the window's dwords, then its 8 byte classes load as batches;
 // only the transitions form a dependent chain (aligned dword reads up to 11 bytes past the window
-// start: pools and staged strings carry a zero tail).
+// start: pools and staged strings carry a zero tail). A walk ends at the first window that starts
+// in the dead state or an absorbing one (kwdev.hpp dfa_live).
 __device__ inline uint32_t feed(const DfaView& d, uint32_t st, const uint8_t* __restrict__ bytes, uint32_t b, uint32_t e) {
-  for (uint32_t p = b; p < e && st != 0; p += 8u) {
+  for (uint32_t p = b; p < e && dfa_live(st, d.abs_lo); p += 8u) {
     const uint32_t* q = (const uint32_t*)(bytes + (p & ~3u));
     const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], sh = p & 3u;
     const uint32_t x0 = align_bytes(q1, q0, sh), x1 = align_bytes(q2, q1, sh);
@@ -164,6 +172,7 @@ constexpr char kLocalhost[] = "localhost";
 
 template <int N>
 __device__ inline uint32_t feed_const(const DfaView& d, uint32_t st, const char (&s)[N]) {
+  if (!dfa_live(st, d.abs_lo)) return st;  // dead or absorbing: the constant cannot change it
 #pragma unroll
   for (int i = 0; i < N - 1; ++i) st = step(d, st, (uint8_t)s[i]);  // state 0 is absorbing
   return st;
@@ -279,11 +288,11 @@ __device__ uint32_t image_part(int k, const DfaView& d, const uint8_t* __restric
     else return 0u;  // digest only: no tag
   } else {
     st = r.is_reg ? feed(d, st, bytes, r.b, r.slash0) : feed_const(d, st, kDockerIo);
-    if (st) st = step(d, st, '/');
+    if (dfa_live(st, d.abs_lo)) st = step(d, st, '/');
     if (r.is_docker && !r.path_slash) st = feed_const(d, st, kLibrary);
     st = feed(d, st, bytes, r.rest_b, r.path_end);
     if (r.eff_tag) {
-      if (st) st = step(d, st, ':');
+      if (dfa_live(st, d.abs_lo)) st = step(d, st, ':');
       st = r.colon != NONE ? feed(d, st, bytes, r.colon + 1, r.name_end) : feed_const(d, st, kLatest);
     }
     if (r.at != NONE) st = feed(d, st, bytes, r.at, r.e);
@@ -339,8 +348,13 @@ __device__ inline uint32_t classify_value_as(as_ptr<AS> R, uint32_t nlk, uint32_
     }
     uint32_t st = d.start;
     // 8-byte windows: the window's dwords, then its 8 byte classes, load as two batches; only the
-    // transitions form a dependent chain (bytes past the string read the zero tail, unused)
+    // transitions form a dependent chain (bytes past the string read the zero tail, unused); the
+    // walk ends at a window starting in the dead state or an absorbing one
+#if KW_KV_ABSORB
+    for (uint32_t p = b; p < e && dfa_live(st, d.abs_lo); p += 8u) {
+#else
     for (uint32_t p = b; p < e && st != 0; p += 8u) {
+#endif
       const uint32_t* q = (const uint32_t*)(bytes + (p & ~3u));
       const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], sh = p & 3u;
       const uint32_t x0 = align_bytes(q1, q0, sh), x1 = align_bytes(q2, q1, sh);
@@ -636,7 +650,9 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
   for (uint32_t it = 0; tile < t_hi; ++it) {
     const uint32_t cur = it & 1u;
     uint32_t nxt2 = 0;
+#if !KW_LATE_ATOMIC
     if (dyn && tid == 0) nxt2 = atomicAdd(cnt, 1u);  // the tile after next (read after the staging barrier)
+#endif
     if (next < t_hi) fetch_desc(next, cur ^ 1u);      // the next tile's descriptor (slot free since its last read)
 #if KW_DESC_LDS
     const TileDesc& d = l_desc[cur];
@@ -646,6 +662,9 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
 #define KW_DF(x) (x)
 #endif
     if (!KW_DF(d.fits)) {  // queued for the overflow kernels by the host (uniform: no barrier skipped unevenly)
+#if KW_LATE_ATOMIC
+      if (dyn && tid == 0) nxt2 = atomicAdd(cnt, 1u);
+#endif
       if (dyn && tid == 0) l_nx[cur] = nxt2;
       __syncthreads();  // also waits for the next descriptor
       tile = next;
@@ -681,7 +700,13 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
     __syncthreads();  // staged tile, the next descriptor and the counter fetch have landed
     mark(0);
     if (timing && tid == 0) ++ph[5];
+#if KW_LATE_ATOMIC
+    // the counter fetch for the tile after next: issued now, off the staging barrier's vmcnt(0); its
+    // value is stored to l_nx[cur] after P2 (the wave's only outstanding VMEM op there)
+    if (dyn && tid == 0) nxt2 = atomicAdd(cnt, 1u);
+#else
     if (dyn && tid == 0) l_nx[cur] = nxt2;  // read after this tile's last barrier
+#endif
     // the next tile's staged ranges into L2 (covered by this tile's classification, walk and stores),
     // from its descriptor in LDS
     auto prefetch_next = [&]() {
@@ -1007,6 +1032,9 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
       }
       lds_barrier();
       mark(3);
+#if KW_LATE_ATOMIC
+      if (dyn && tid == 0 && ck == 0) l_nx[cur] = nxt2;  // read after this tile's last barrier
+#endif
 
       // ---- P3: verdict words. All-pairs: items = (request, 4 columns), 16 lanes per 256-B row,
       //      column records from LDS (group / constant columns from the record's global copy).
@@ -1292,6 +1320,50 @@ __global__ void __launch_bounds__(kOverflowThreads)
       }
     }
   }
+}
+
+// ------------------------------------------------------------------------------------------
+// Wide policy groups: the members' verdict words of a separate pass -> each group's jump code per
+// row (slots.hpp run_wide_prog), its value stack in this thread's scratch words and its causes in
+// the per-row side data. A row the main pass answered with the bypass word keeps it.
+// ------------------------------------------------------------------------------------------
+constexpr int kWideThreads = 256;
+
+__global__ void __launch_bounds__(kWideThreads) wide_groups_kernel(WideGroupPass w) {
+  const uint64_t nthreads = (uint64_t)gridDim.x * kWideThreads;
+  const uint64_t gtid = (uint64_t)blockIdx.x * kWideThreads + threadIdx.x;
+  uint64_t* stack = w.stack + gtid * w.stack_words;
+  const uint64_t pairs = w.nrows * w.ngroups;
+  for (uint64_t q = gtid; q < pairs; q += nthreads) {
+    const uint64_t r = q / w.ngroups;
+    const WideGroupArgs& g = w.groups[q - r * w.ngroups];
+    uint32_t* dst;
+    if (w.rowcol) {
+      if (w.rowcol[r] != g.col) continue;
+      dst = w.out + r;
+    } else {
+      dst = w.out + r * w.npol + g.col;
+    }
+    if (*dst == kBypassWord) continue;
+    uint64_t* cz = w.causes + r * w.cause_stride + g.cause_off;
+    for (uint32_t k = 0; k < g.cause_words; ++k) cz[k] = 0;
+    const uint32_t* mw = w.member_words + r * w.nmw;
+    const uint32_t* midx = w.midx + g.midx_off;
+    const bool v = run_wide_prog(
+        w.progs + g.prog_off, g.prog_len, stack,
+        [&](uint32_t s) {
+          const uint32_t x = mw[midx[s]];
+          return (x & KW_V_ALLOWED) && !(x & KW_V_MUTATED);
+        },
+        [&](uint32_t s) { cz[s >> 6] |= 1ull << (s & 63u); });
+    *dst = v ? g.okw : g.rejb;
+  }
+}
+
+hipError_t launch_wide_groups(const WideGroupPass& w, uint32_t grid, hipStream_t s) {
+  if (w.nrows == 0 || w.ngroups == 0) return hipSuccess;
+  hipLaunchKernelGGL(wide_groups_kernel, dim3(grid), dim3(kWideThreads), 0, s, w);
+  return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------

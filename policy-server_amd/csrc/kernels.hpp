@@ -135,6 +135,35 @@ hipError_t launch_evaluate_tiles(const EvalArgs& a, const TileArgs& t, const Til
                                  uint32_t grid, hipStream_t s);
 // Requests that do not fit the LDS capacities even alone (d_overflow: [count, request indices...],
 // host-built with the descriptors): classified into HBM, then walked sequentially per request.
+// Wide policy groups (expr.hpp: more than 64 members, or a value stack deeper than 64): the
+// members ran as a separate all-pairs pass into `member_words` [row][nmw]; the combine kernel runs
+// each group's jump code per row over their results. One record per wide group column of the pass.
+struct WideGroupArgs {
+  uint32_t prog_off, prog_len;  // jump code in `progs`
+  uint32_t col;                 // all-pairs: the group's output column; rows mode: its column id
+  uint32_t nmem, midx_off;      // member slot s -> member_words column midx[midx_off + s]
+  uint32_t okw, rejb;           // the group's accepted / rejected verdict words (reason GROUP, ARG wide)
+  uint32_t cause_off, cause_words;  // its cause bitset in the per-row side data
+  uint32_t pad[3];
+};
+struct WideGroupPass {
+  const WideGroupArgs* groups;
+  uint32_t ngroups;
+  const uint8_t* progs;
+  const uint32_t* midx;
+  const uint32_t* member_words;  // [row][nmw]
+  uint32_t nmw;
+  uint32_t* out;                 // the pass's verdict words
+  uint32_t npol;                 // all-pairs stride; rows mode: 1
+  const uint32_t* rowcol;        // rows mode: the row's column id (== WideGroupArgs::col), nullptr = all pairs
+  uint64_t* causes;              // [row][cause_stride] u64
+  uint32_t cause_stride;
+  uint64_t* stack;               // scratch: stack_words u64 per thread of the grid
+  uint32_t stack_words;
+  uint64_t nrows;
+};
+hipError_t launch_wide_groups(const WideGroupPass& w, uint32_t grid, hipStream_t s);
+
 hipError_t launch_overflow(const EvalArgs& a, const TileArgs* d_t, const uint32_t* d_overflow, uint32_t n_overflow,
                            hipStream_t s);
 

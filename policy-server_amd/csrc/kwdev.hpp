@@ -14,7 +14,7 @@
 namespace kw {
 
 constexpr uint32_t kBlobMagic = 0x4b574733;  // "KWG3"
-constexpr uint32_t kBlobVersion = 3;
+constexpr uint32_t kBlobVersion = 4;
 
 // request columns that carry strings classified by a DFA or a literal table
 enum Col : uint32_t {
@@ -54,7 +54,9 @@ enum PolicyFlag : uint8_t {
 //   G_NOT                   negate the top
 //   G_JT t / G_JF t         (||, &&) top true / false: jump to byte t (u16 LE), keeping it; else pop
 //   G_EQ / G_NE             pop b, pop a, push a == b / a != b
-enum GOp : uint8_t { G_CONST0 = 0, G_CONST1 = 1, G_CALL = 2, G_NOT = 3, G_JT = 4, G_JF = 5, G_EQ = 6, G_NE = 7 };
+//   G_CALL16 s              (wide programs) push ok(s), s a u16 member index; in wide programs the
+//                           G_JT / G_JF targets are u32
+enum GOp : uint8_t { G_CONST0 = 0, G_CONST1 = 1, G_CALL = 2, G_NOT = 3, G_JT = 4, G_JF = 5, G_EQ = 6, G_NE = 7, G_CALL16 = 8 };
 constexpr int kMaxGroupStack = 64;    // value-stack depth (only == / != nest it)
 constexpr int kMaxGroupMembers = 64;  // members evaluate as slots of one slot-plan chunk
 constexpr int kMaxLocalBits = 64;     // per chunk: distinct mandatory label keys / mutation capabilities
@@ -77,7 +79,8 @@ struct alignas(16) KvDfa {
   uint32_t next;       // next KvDfa of the key's chain, 0 = last
   uint32_t start;
   uint16_t cbase, nstates, ncls;
-  uint8_t hi, wide, t16, pad[3];  // hi: class of bytes >= 128 when !wide
+  uint16_t abs_lo;                // states [abs_lo, nstates) and 0 are absorbing: a walk stops there
+  uint8_t hi, wide, t16, pad;     // hi: class of bytes >= 128 when !wide
 };
 static_assert(sizeof(KvDfa) == 32, "KvDfa layout");
 
@@ -95,8 +98,12 @@ struct alignas(16) DevDfa {
   uint32_t bytes;                            // bytes of this DFA's record + tables (for LDS staging)
   uint32_t next;                             // blob offset of the next DFA of the column chain, 0 = last
   uint32_t chain_bytes;                      // bytes of this DFA and all that follow it in the chain
+  uint32_t abs_lo;                           // states [abs_lo, nstates) and 0 are absorbing (walks stop)
+  uint32_t pad[3];
   uint8_t cls[256];
 };
+// A walk may stop at state 0 (dead) and at states >= abs_lo (absorbing): `live` is st in [1, abs_lo).
+inline KW_HD bool dfa_live(uint32_t st, uint32_t abs_lo) { return st - 1u < abs_lo - 1u; }
 
 // Literal column part: a minimal-probe perfect hash over the column's literal patterns. A string
 // matches at most one of them; lookup = hash g of its canonical little-endian dwords -> (bucket

@@ -338,12 +338,23 @@ Status format_response(const Env& env, const Batch& b, uint64_t row, int32_t pid
   }
   // vanilla status
   uint64_t full = 0;
-  if (reason != KW_R_GROUP_EXPR && reason != KW_R_INIT_ERROR) {
+  const bool big_group = reason == KW_R_GROUP && P.is_group && P.prog.wide;  // causes: multi-word side data
+  if (reason != KW_R_GROUP_EXPR && reason != KW_R_INIT_ERROR && !big_group) {
     Status st = full_arg(b, row, pidx, arg, &full);
     if (!st.ok()) return st;
   }
   std::string msg;
-  if (Status st = policy_message(env, b, row, pidx, reason, full, &msg); !st.ok()) return st;
+  if (reason == KW_R_GROUP_EXPR && P.is_group && P.prog.valid && !P.prog.eval_error && member_v) {
+    // a data-dependent evaluation error (truth-table groups): the host interpreter over the
+    // members' results names it
+    const ExprOutcome o = P.prog.run([&](uint32_t s) {
+      const uint32_t mv = member_v[s];
+      return (mv & KW_V_ALLOWED) && !(mv & KW_V_MUTATED);
+    });
+    msg = group_eval_message(o.error ? o.message : "no error");
+  } else if (Status st = policy_message(env, b, row, pidx, reason, full, &msg); !st.ok()) {
+    return st;
+  }
   put_kv(out, "message", msg);
   if (reason == KW_R_GROUP_EXPR) {
     out->append(",\"code\":500}}");
@@ -351,10 +362,15 @@ Status format_response(const Env& env, const Batch& b, uint64_t row, int32_t pid
   }
   if (reason == KW_R_GROUP) {
     if (!member_v) return {KW_E_ARG, "member verdicts are required to format a policy-group rejection"};
+    const uint64_t* big = nullptr;
+    uint32_t big_words = 0;
+    if (big_group && !(big = b.wide.lookup_big(row, pidx, &big_words)))
+      return {KW_E_ENGINE, "group causes not found in the pass's side data"};
     out->append(",\"details\":{\"causes\":[");
     bool first = true;
-    for (size_t s = 0; s < P.members.size() && s < 64; ++s) {
-      if (!((full >> s) & 1ull)) continue;
+    for (size_t s = 0; s < P.members.size(); ++s) {
+      const bool cause = big ? (s / 64 < big_words && ((big[s / 64] >> (s % 64)) & 1ull)) : (s < 64 && ((full >> s) & 1ull));
+      if (!cause) continue;
       int32_t m = P.members[s];
       uint32_t mv = member_v[s];
       std::string msg;

@@ -252,7 +252,7 @@ struct Builder {
     h.o_cols = (uint32_t)rec.size();
     h.o_prog = h.o_cols + (uint32_t)(cols.size() * sizeof(ColInfo));
     for (ColInfo& c : cols)
-      if (c.kind == CK_GROUP) c.prog_off += h.o_prog;
+      if (c.kind == CK_GROUP || c.kind == CK_TABLE) c.prog_off += h.o_prog;
     rec.insert(rec.end(), (const uint8_t*)cols.data(), (const uint8_t*)(cols.data() + cols.size()));
     rec.insert(rec.end(), progs.begin(), progs.end());
     align();
@@ -300,7 +300,8 @@ Status build_slot_chunks(const Env& E, const int32_t* pols, uint32_t npol, int o
       // resources the column needs in this chunk: slots and local bits
       uint32_t need = 0, capb = 0, mandb = 0;
       const bool expr_err = P.is_group && (!P.prog.valid || P.prog.eval_error);
-      if (P.init_error) {
+      const bool wide_group = P.is_group && !expr_err && P.prog.wide;  // members run in their own pass
+      if (P.init_error || wide_group) {
       } else if (P.is_group) {
         if (!expr_err) {
           need = (uint32_t)P.members.size();
@@ -335,14 +336,26 @@ Status build_slot_chunks(const Env& E, const int32_t* pols, uint32_t npol, int o
       } else if (expr_err) {
         ci.kind = CK_CONST;
         ci.okw = ci.mutw = ci.rejb = finish_word(P.mode, 0, origin, KW_R_GROUP_EXPR, 0, false);
+      } else if (wide_group) {  // placeholder: the wide-group combine kernel writes the column
+        ci.kind = CK_WIDE;
+        ci.okw = ci.mutw = ci.rejb = 0;
       } else if (P.is_group) {
-        ci.kind = CK_GROUP;
+        const bool table = !P.prog.table.empty();
+        ci.kind = table ? CK_TABLE : CK_GROUP;
         ci.slot = b.nslots;
         ci.nmem = (uint32_t)P.members.size();
         for (int32_t m : P.members) b.add_slot(m);
+        while (table && b.progs.size() % 4) b.progs.push_back(0);  // u32 entries
         ci.prog_off = (uint32_t)b.progs.size();  // rebased to the record at emit
-        ci.prog_len = (uint32_t)P.prog.code.size();
-        b.progs.insert(b.progs.end(), P.prog.code.begin(), P.prog.code.end());
+        if (table) {
+          ci.prog_len = (uint32_t)(P.prog.table.size() * 4);
+          b.progs.insert(b.progs.end(), (const uint8_t*)P.prog.table.data(),
+                         (const uint8_t*)(P.prog.table.data() + P.prog.table.size()));
+        } else {
+          ci.prog_len = (uint32_t)P.prog.code.size();
+          b.progs.insert(b.progs.end(), P.prog.code.begin(), P.prog.code.end());
+        }
+        ci.errw = finish_word(P.mode, 0, origin, KW_R_GROUP_EXPR, 0, false);
         ci.okw = finish_word(P.mode, 0, origin, 0, 0, false);
         ci.mutw = ci.okw;
         ci.rejb = finish_word(P.mode, 0, origin, KW_R_GROUP, 0, false) & ~0xff00u;

@@ -67,16 +67,19 @@ struct alignas(16) SlotHdr {
 };
 static_assert(sizeof(SlotHdr) % 16 == 0, "SlotHdr layout");
 
-enum ColKind : uint32_t { CK_CONST = 0, CK_PLAIN = 1, CK_GROUP = 2 };
+enum ColKind : uint32_t { CK_CONST = 0, CK_PLAIN = 1, CK_GROUP = 2, CK_TABLE = 3, CK_WIDE = 4 };
 
 // One output column (a selected policy). PLAIN: verdict of slot `slot`. GROUP: the jump program at
-// record offset prog_off over the member slots [slot, slot + nmem). CONST: the word `okw` whatever
+// record offset prog_off over the member slots [slot, slot + nmem). TABLE: the truth table (u32
+// entries, expr.hpp kGt*) at record offset prog_off over member slots [slot, slot + nmem), nmem <= 16;
+// errw: the word of an evaluation error. WIDE: a wide group's placeholder (okw = 0), written after
+// the pass by the wide-group combine kernel (kernels.hpp WideGroupPass). CONST: the word `okw` whatever
 // the request (initialisation error, group expression that is not a bool). okw / mutw / rejb: the
 // service-level verdict word of an accepted, an accepted-and-mutated and a rejected vanilla response
 // (reason/arg bits clear in rejb). wide: index of a > 15-member group in the pass's dense cause
 // array (its causes do not fit ARG), else ~0.
 struct alignas(16) ColInfo {
-  uint32_t kind, slot, nmem, prog_off, prog_len, okw, mutw, rejb, wide, policy, pad[2];
+  uint32_t kind, slot, nmem, prog_off, prog_len, okw, mutw, rejb, wide, policy, errw, pad;
 };
 static_assert(sizeof(ColInfo) == 48, "ColInfo layout");
 
@@ -407,6 +410,45 @@ KW_HD inline bool run_group_prog(const uint8_t* prog, uint32_t len, uint64_t ok,
   return vals & 1ull;
 }
 
+// Wide group jump code (G_CALL16 u16 member operands, u32 G_JT / G_JF targets) over any number of
+// members and any stack depth: `stack` holds the value bits (u64 words, the caller's scratch),
+// ok(s) a member's result, cause(s) records a called member that rejected.
+template <class Ok, class Cause>
+KW_HD inline bool run_wide_prog(const uint8_t* prog, uint32_t len, uint64_t* stack, Ok ok, Cause cause) {
+  uint32_t sp = 0;
+  auto put = [&](uint32_t i, uint64_t v) {
+    uint64_t& w = stack[i >> 6];
+    w = (w & ~(1ull << (i & 63u))) | (v << (i & 63u));
+  };
+  auto get = [&](uint32_t i) -> uint64_t { return (stack[i >> 6] >> (i & 63u)) & 1ull; };
+  for (uint32_t pc = 0; pc < len;) {
+    const uint32_t op = prog[pc++];
+    if (op == G_CONST0 || op == G_CONST1) {
+      put(sp++, op == G_CONST1 ? 1ull : 0ull);
+    } else if (op == G_CALL16) {
+      const uint32_t s = (uint32_t)prog[pc] | ((uint32_t)prog[pc + 1] << 8);
+      pc += 2;
+      const uint64_t v = ok(s) ? 1ull : 0ull;
+      if (!v) cause(s);
+      put(sp++, v);
+    } else if (op == G_NOT) {
+      put(sp - 1, get(sp - 1) ^ 1ull);
+    } else if (op == G_JT || op == G_JF) {
+      const uint32_t t = (uint32_t)prog[pc] | ((uint32_t)prog[pc + 1] << 8) | ((uint32_t)prog[pc + 2] << 16) |
+                         ((uint32_t)prog[pc + 3] << 24);
+      pc += 4;
+      const bool top = get(sp - 1) != 0;
+      if (top == (op == G_JT)) pc = t;
+      else --sp;
+    } else {  // G_EQ / G_NE
+      --sp;
+      const uint64_t b = get(sp), a = get(sp - 1);
+      put(sp - 1, op == G_EQ ? (uint64_t)(a == b) : (uint64_t)(a != b));
+    }
+  }
+  return get(0) != 0;
+}
+
 // Verdict word of one output column for one request. rej / mut: the request's rejected and mutated
 // slots; vw: its violation words (valid where rej is set); prog: the record's programs (prog_off
 // is record-relative); *wide gets the cause mask of a > 15-member group.
@@ -426,6 +468,18 @@ KW_HD inline uint32_t column_word(const ColInfo& ci, uint64_t rej, uint64_t mut,
       return ci.rejb | vword(KW_R_GROUP, kArgWide);
     }
     return ci.rejb | vword(KW_R_GROUP, (uint32_t)causes);
+  }
+  if (ci.kind == CK_TABLE) {
+    const uint32_t ok = (uint32_t)((~(rej | mut | init) >> ci.slot) & ((1ull << ci.nmem) - 1ull));
+    const uint32_t e = ((const uint32_t*)(rec + ci.prog_off))[ok];
+    if (e & 2u) return ci.errw;  // kGtError
+    if (e & 1u) return ci.okw;   // kGtValue
+    const uint32_t causes = e >> 16;
+    if (ci.nmem > 15) {
+      *wide = causes;
+      return ci.rejb | vword(KW_R_GROUP, kArgWide);
+    }
+    return ci.rejb | vword(KW_R_GROUP, causes);
   }
   return ci.okw;
 }

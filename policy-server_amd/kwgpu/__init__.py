@@ -356,6 +356,18 @@ class Batch:
         rc = self._L.kw_batch_wide_arg(self._h, row, policy, C.byref(v))
         return v.value if rc == N.KW_OK else None
 
+    def group_causes(self, row, policy, verdict):
+        """Member slots (settings order) of a group rejection's causes (kw_batch_group_causes): from
+        the word's ARG or the pass's side data, any number of members."""
+        need = C.c_size_t()
+        words = (C.c_uint64 * 1)()
+        rc = self._L.kw_batch_group_causes(self._h, row, policy, int(verdict), words, 1, C.byref(need))
+        if rc == N.KW_E_NOSPACE:
+            words = (C.c_uint64 * need.value)()
+            rc = self._L.kw_batch_group_causes(self._h, row, policy, int(verdict), words, need.value, C.byref(need))
+        raise_for(rc, "kw_batch_group_causes")
+        return [64 * k + b for k in range(need.value) for b in range(64) if (words[k] >> b) & 1]
+
     def debug_host_walk(self, env, policies, origin=VALIDATE):
         """Diagnostic (tests only): the device kernel's slot compiler + entity walks run on the host
         (kw_debug_host_walk). Never part of the validate path."""

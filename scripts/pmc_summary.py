@@ -39,7 +39,27 @@ def write_traffic(fetch_dir, write_dir, out, config="c4_64", rows=1_000_000, tag
 
 if __name__ == "__main__":
     if sys.argv[1] == "--traffic":
-        print(write_traffic(sys.argv[2], sys.argv[3], sys.argv[4], tag=sys.argv[5] if len(sys.argv) > 5 else "r02"))
+        # --traffic fetch_dir write_dir out tag [config rows]
+        a = sys.argv
+        print(write_traffic(a[2], a[3], a[4], tag=a[5] if len(a) > 5 else "r02", config=a[6] if len(a) > 6 else "c4_64",
+                            rows=int(a[7]) if len(a) > 7 else 1_000_000))
+        sys.exit(0)
+    if sys.argv[1] == "--derived":
+        # --derived rows dir... : the ratios the DESIGN tables quote, from the merged passes
+        rows = float(sys.argv[2])
+        m = {}
+        for d in sys.argv[3:]:
+            m.update(summarise(d))
+        g = lambda k: m.get(k, float("nan"))
+        print(f"rows={rows:.0f} dur_ns={g('dur_ns'):.4g}")
+        print(f"SQ_WAIT_ANY/SQ_WAVE_CYCLES={g('SQ_WAIT_ANY') / g('SQ_WAVE_CYCLES'):.3f}  "
+              f"SQ_ACTIVE_INST_ANY/SQ_WAVE_CYCLES={g('SQ_ACTIVE_INST_ANY') / g('SQ_WAVE_CYCLES'):.3f}  "
+              f"SQ_WAIT_INST_ANY/SQ_WAVE_CYCLES={g('SQ_WAIT_INST_ANY') / g('SQ_WAVE_CYCLES'):.3f}")
+        print(f"LDS bank conflict / LDS active={g('SQ_LDS_BANK_CONFLICT') / g('SQ_LDS_IDX_ACTIVE'):.3f}")
+        print(f"per request: VALU={g('SQ_INSTS_VALU') / rows:.1f} SALU={g('SQ_INSTS_SALU') / rows:.1f} "
+              f"LDS={g('SQ_INSTS_LDS') / rows:.1f} SMEM={g('SQ_INSTS_SMEM') / rows:.2f} VMEM_RD={g('SQ_INSTS_VMEM_RD') / rows:.2f} "
+              f"VMEM_WR={g('SQ_INSTS_VMEM_WR') / rows:.2f}")
+        print(f"HBM bytes per request: fetch(x2)={2 * g('FETCH_SIZE') * 1024 / rows:.1f} write={g('WRITE_SIZE') * 1024 / rows:.1f}")
         sys.exit(0)
     for d in sys.argv[1:]:
         s = summarise(d)

@@ -103,6 +103,48 @@ def _expr(rng, names, depth):
     return f"({a} {op} {b})" if rng.random() < 0.6 else f"{a} {op} {b}"
 
 
+def _script(rng, names):
+    """A group script beyond the bool-only subset (expr.hpp: let bindings, if / else, integers,
+    strings, statement sequences), now and then with an operation that fails at evaluation for some
+    member results (a bool + an int behind a branch)."""
+    bools, ints = [], []
+
+    def b(d):
+        r = rng.random()
+        if d <= 0 or r < 0.25:
+            pool = [f"{rng.choice(names)}()"] * 3 + bools
+            return rng.choice(pool)
+        if r < 0.35:
+            return f"!{b(d - 1)}"
+        if r < 0.55:
+            return f"({b(d - 1)} {rng.choice(['&&', '||', '==', '!=', '|', '&', '^'])} {b(d - 1)})"
+        if r < 0.7:
+            return f"(if {b(d - 1)} {{ {b(d - 1)} }} else {{ {b(d - 1)} }})"
+        if r < 0.85:
+            return f"({i(d - 1)} {rng.choice(['<', '<=', '>', '>=', '==', '!='])} {i(d - 1)})"
+        if r < 0.93:
+            return f'("{rng.choice(["a", "b"])}" + "x" {rng.choice(["==", "!="])} "{rng.choice(["ax", "bx"])}")'
+        return f"(if {b(d - 1)} {{ true }} else {{ {rng.choice(names)}() + 1 == 2 }})"  # runtime error on one path
+
+    def i(d):
+        r = rng.random()
+        if d <= 0 or r < 0.3:
+            return rng.choice([str(rng.randint(-3, 9))] + ints)
+        if r < 0.6:
+            return f"({i(d - 1)} {rng.choice(['+', '-', '*'])} {i(d - 1)})"
+        return f"(if {b(d - 1)} {{ {i(d - 1)} }} else {{ {i(d - 1)} }})"
+
+    stmts = []
+    for k in range(rng.randint(0, 3)):
+        if rng.random() < 0.6:
+            stmts.append(f"let v{k} = {b(2)};")
+            bools.append(f"v{k}")
+        else:
+            stmts.append(f"let n{k} = {i(2)};")
+            ints.append(f"n{k}")
+    return " ".join(stmts + [b(3)])
+
+
 def random_policies(seed, n=None):
     """A policies document (dict) of `n` (default 20-90) plain policies and 1-3 groups."""
     rng = random.Random(seed)
@@ -126,7 +168,8 @@ def random_policies(seed, n=None):
         for nm in names:
             fam = rng.choice(fams)
             members[nm] = {"module": MOD[fam], "settings": _settings(rng, fam)}
-        e = {"policies": members, "expression": _expr(rng, names, 3), "message": f"group {g} rejected"}
+        expr = _script(rng, names) if rng.random() < 0.35 else _expr(rng, names, 3)
+        e = {"policies": members, "expression": expr, "message": f"group {g} rejected"}
         if rng.random() < 0.25:
             e["policyMode"] = "monitor"
         doc[f"group-{g}"] = e

@@ -418,3 +418,44 @@ def test_container_ranges_path_matches_oracle(monkeypatch):
     gpu = b.verdicts()
     ora = oe.eval(syn.soa(), ids)
     assert np.array_equal(gpu, ora), diff_verdicts(gpu, ora, len(ids), ids)
+
+
+def test_wide_groups_match_oracle():
+    """Groups past the jump-code limits (a 100-member group, a 100-deep == nest) on the GPU: the
+    members' pass, the placeholder columns of the main pass and the combine kernel, against the
+    oracle bit-exact in both origins and in row mode; causes (kw_batch_group_causes, the pass's
+    multi-word side data) equal the oracle's as sets; responses equal the oracle's."""
+    from test_wide_groups import wide_config
+    doc = wide_config()
+    env = K.EvaluationEnvironment(doc, continue_on_errors=True, always_accept_namespace=NS, device=0)
+    oe = O.OracleEnv(doc, continue_on_errors=True, always_accept_namespace=NS)
+    ids = env.policy_ids()
+    n = 3000
+    syn = K.SynthBatch(0, n, seed=41)
+    b = syn.batch().to_device(0)
+    for origin in (K.VALIDATE, K.AUDIT):
+        b.validate(env, ids, origin)
+        gpu = b.verdicts()
+        ora = oe.eval(syn.soa(), ids, origin)
+        assert np.array_equal(gpu, ora), diff_verdicts(gpu, ora, len(ids), ids)
+    v = gpu.reshape(n, len(ids))
+    checked = 0
+    for g in ("big", "deep"):
+        j = ids.index(g)
+        members = env.group_members(j)
+        for r in range(n):
+            if (int(v[r, j]) >> 8) & 0xFF != O.R_GROUP:
+                continue
+            want = oe.detail(syn.soa(), r, j, K.AUDIT)["causes"]
+            assert b.group_causes(r, j, int(v[r, j])) == sorted(want), (g, r)
+            if checked < 40:
+                resp = b.format_response(env, r, j, int(v[r, j]), [int(v[r, m]) for m in members], doc=syn.json(r))
+                assert resp == oe.response_doc(syn.soa(), r, j, K.AUDIT, doc=syn.json(r)), (g, r)
+                checked += 1
+    assert checked >= 40
+    rng = np.random.default_rng(9)
+    pick = rng.integers(0, len(ids), n)
+    b.validate(env, ids, K.VALIDATE)
+    full = b.verdicts().reshape(n, len(ids))
+    b.validate_rows(env, [int(x) for x in pick], K.VALIDATE)
+    assert np.array_equal(b.verdicts(n), full[np.arange(n), pick])
