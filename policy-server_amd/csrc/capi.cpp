@@ -178,11 +178,6 @@ struct DeviceBatch {
   size_t big_causes_cap = 0;
   uint32_t last_big_stride = 0;
   std::vector<WideData::BigRef> last_big_ref;
-  // column tiles of the classification kernel (pre-classified passes), cached per need set
-  ColTile* col_tiles = nullptr;
-  size_t col_tiles_cap = 0;
-  uint64_t col_key = ~0ull;
-  ColArgs col_args{};
   // what the last pass left in the side buffers
   uint32_t last_nwide = 0, last_wide_cap = 0;
   bool last_rows_mode = false;
@@ -217,7 +212,6 @@ struct DeviceBatch {
     P.release(device, wg_data, wg_data_cap);
     P.release(device, wg_stack, wg_stack_cap * 8);
     P.release(device, big_causes, big_causes_cap * 8);
-    P.release(device, col_tiles, col_tiles_cap * sizeof(ColTile));
     P.release(device, sched, 512 * sizeof(uint32_t));  // every launch leaves the tile counters zero
     P.release(device, wide_count, sizeof(uint32_t));
     host_pool().release(device, staging, staging_bytes);
@@ -901,81 +895,6 @@ int upload_tile_descs(const Batch& B, DeviceBatch* D, const TileArgs& T, hipStre
 }
 
 // Per-string class arrays of the overflow path (absolute entity indices), one allocation.
-// Column tiles of the classification kernel for the string columns `T.need` names: per kind, runs
-// of up to kColTile entities whose two byte windows fit the staging capacities (a run that does
-// not is halved; a single entity that does not is classified from the HBM pools). Built from the
-// host copy of the batch, uploaded once per need set.
-constexpr uint32_t kColWindow = 16384;  // bytes of one staged string window
-int plan_columns(const Batch& B, DeviceBatch* D, const TileArgs& T, hipStream_t s) {
-  const uint64_t key = ((uint64_t)T.need << 32) ^ ((uint64_t)T.lds_tables << 31) ^ B.n;
-  if (D->col_tiles && key == D->col_key) return KW_OK;
-  std::vector<ColTile> tiles;
-  auto window = [&](int m, uint64_t e0, uint64_t e1, uint32_t* sa, uint32_t* nv) {
-    const StrCol& c = host_str(B, m);
-    *sa = c.off[e0] & ~15u;
-    *nv = (((c.off[e1] + 15u) & ~15u) - *sa) / 16u;
-  };
-  auto add_kind = [&](uint32_t kind, uint64_t count, int m0, int m1) {
-    std::vector<std::pair<uint64_t, uint64_t>> todo;
-    for (uint64_t e = count; e > 0;) {  // pushed in reverse, popped in order
-      const uint64_t b = (e - 1) / kColTile * kColTile;
-      todo.push_back({b, e});
-      e = b;
-    }
-    while (!todo.empty()) {
-      const auto [e0, e1] = todo.back();
-      todo.pop_back();
-      ColTile ct;
-      memset(&ct, 0, sizeof(ct));
-      ct.kind = kind;
-      ct.e0 = (uint32_t)e0;
-      ct.n = (uint32_t)(e1 - e0);
-      if (m0 >= 0) window(m0, e0, e1, &ct.sa0, &ct.nv0);
-      if (m1 >= 0) window(m1, e0, e1, &ct.sa1, &ct.nv1);
-      if ((ct.nv0 * 16u <= kColWindow && ct.nv1 * 16u <= kColWindow) || e1 - e0 == 1) {
-        ct.global = (ct.nv0 * 16u > kColWindow || ct.nv1 * 16u > kColWindow) ? 1u : 0u;
-        tiles.push_back(ct);
-      } else {
-        const uint64_t mid = e0 + (e1 - e0) / 2;
-        todo.push_back({mid, e1});
-        todo.push_back({e0, mid});
-      }
-    }
-  };
-  const uint32_t need = T.need;
-  if (need & (1u << S_NS)) add_kind(K_NS, B.n, S_NS, -1);
-  if (need & ((1u << S_AA) | (1u << S_IMG)))
-    add_kind(K_CTR, B.containers(), (need & (1u << S_AA)) ? S_AA : -1, (need & (1u << S_IMG)) ? S_IMG : -1);
-  if (need & (1u << S_CAPADD)) {
-    add_kind(K_ADD, B.cap_add.n(), S_CAPADD, -1);
-    add_kind(K_DROP, B.cap_drop.n(), S_CAPDROP, -1);
-  }
-  if (need & (1u << S_LK)) add_kind(K_LBL, B.labels(), S_LK, (need & (1u << S_LV)) ? S_LV : -1);
-  if (int rc = ensure(&D->col_tiles, &D->col_tiles_cap, std::max<size_t>(tiles.size(), 1))) return rc;
-  HIPCHK(hipStreamSynchronize(s));  // a running pass may still read the previous list
-  if (!tiles.empty()) HIPCHK(hipMemcpyAsync(D->col_tiles, tiles.data(), tiles.size() * sizeof(ColTile), hipMemcpyHostToDevice, s));
-  HIPCHK(hipStreamSynchronize(s));
-  ColArgs& c = D->col_args;
-  memset(&c, 0, sizeof(c));
-  c.tiles = D->col_tiles;
-  c.ntiles = tiles.size();
-  uint32_t at = 16;
-  if (T.lds_tables)
-    for (uint32_t k = 0; k < T.nstage; ++k) at = std::max(at, T.stage_lds[k] + T.stage_bytes[k]);
-  auto take = [&](uint32_t bytes) {
-    const uint32_t o = (at + 15u) & ~15u;
-    at = o + bytes;
-    return o;
-  };
-  c.o_off0 = take((kColTile + 1) * 4);
-  c.o_off1 = take((kColTile + 1) * 4);
-  c.o_b0 = take(kColWindow + 48);
-  c.o_b1 = take(kColWindow + 48);
-  c.lds_bytes = (at + 15u) & ~15u;
-  D->col_key = key;
-  return KW_OK;
-}
-
 int ensure_overflow_classes(const Batch& B, DeviceBatch* D, const TileArgs& T, EvalArgs* A) {
   const uint64_t nim = T.il.n(), nlv = std::max<uint32_t>(T.nlv, 1);
   const uint64_t n_ns = B.n + 1, n_ctr = B.containers() + 1, n_add = B.cap_add.n() + 1, n_drop = B.cap_drop.n() + 1,
@@ -1056,13 +975,8 @@ int run_pass(kw_batch* kb, PassPlan& plan, bool timed, hipStream_t s) {
   }
   HIPCHK(hipMemsetAsync(D.wide_count, 0, sizeof(uint32_t), s));
   A.wide_count = D.wide_count;
-  // pre-classified pass (KW_PRECLASSIFY): every string classified by the column kernel into the
-  // batch's class arrays first
-  static const bool preclassify = getenv("KW_PRECLASSIFY") && atoi(getenv("KW_PRECLASSIFY")) != 0;
-  if (preclassify || D.n_overflow) {
-    if (int rc = ensure_overflow_classes(B, &D, plan.geom, &A)) return rc;
-  }
   if (D.n_overflow) {
+    if (int rc = ensure_overflow_classes(B, &D, plan.geom, &A)) return rc;
     const size_t cap = (size_t)D.n_overflow * plan.wide_cap_per_row;
     if (int rc = ensure(&D.wide_rec, &D.wide_rec_cap, cap)) return rc;
     A.wide_rec = D.wide_rec;
@@ -1081,14 +995,6 @@ int run_pass(kw_batch* kb, PassPlan& plan, bool timed, hipStream_t s) {
     A.phase = (uint64_t*)d_phase;
   }
   if (timed) HIPCHK(hipEventRecord(D.ev[0], s));
-  if (preclassify && !plan.tiles.empty()) {
-    if (int rc = plan_columns(B, &D, plan.geom, s)) return rc;
-    int ncu = 256;
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, D.device);
-    const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(8, (160u * 1024u) / std::max<uint32_t>(D.col_args.lds_bytes, 1)));
-    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(D.col_args.ntiles, (uint64_t)ncu * per_cu));
-    HIPCHK(launch_classify_columns(A, D.d_tiles, plan.tiles[0], D.col_args, grid, s));
-  }
   for (size_t l = 0; l < plan.tiles.size(); ++l) {
     if (phases) HIPCHK(hipMemsetAsync(d_phase, 0, phase_bytes, s));
     HIPCHK(launch_evaluate_tiles(A, plan.tiles[l], D.d_tiles + l, D.desc, plan.grid, s));

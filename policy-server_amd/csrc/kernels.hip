@@ -1323,134 +1323,6 @@ __global__ void __launch_bounds__(kOverflowThreads)
 }
 
 // ------------------------------------------------------------------------------------------
-// Column classification: persistent workgroups stage the classifiers once, then per column tile
-// its strings' offsets and bytes (LDS-DMA), and classify one entity per thread into the batch's
-// class arrays (coalesced u16 stores). No per-request state, so a workgroup needs only the
-// classifiers and two string windows of LDS: many more waves per CU than the tile kernel's.
-// ------------------------------------------------------------------------------------------
-template <bool LDST>
-__global__ void __launch_bounds__(kColTile)
-    classify_columns_kernel(EvalArgs a, const TileArgs* __restrict__ tp, ColArgs ca) {
-  const TileArgs& t = *tp;
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const uint32_t tid = threadIdx.x;
-  if (LDST)
-    for (uint32_t s = 0; s < t.nstage; ++s) copy_x4(a.blob + t.stage_blob[s], lds + t.stage_lds[s], t.stage_bytes[s], tid);
-  __syncthreads();
-  const uint8_t* tb = LDST ? (const uint8_t*)lds : a.blob;
-  Classifiers C, G;  // staged (LDS) and blob (HBM) classifiers
-  for (int c = 0; c < (int)NCOL; ++c) {
-    C.lit[c] = t.lit_blob[c] ? tb + (LDST ? t.lit_lds[c] : t.lit_blob[c]) : nullptr;
-    C.dfa[c].head = t.dfa_blob[c];
-    C.dfa[c].base = tb + (LDST ? t.dfa_lds[c] : t.dfa_blob[c]);
-  }
-  C.kv = t.kv_blob ? ((LDST && t.kv_lds) ? (const uint8_t*)lds + t.kv_lds : a.blob + t.kv_blob) : nullptr;
-  C.nlk = t.nlk;
-  C.docker_io_cls = t.docker_io_cls;
-  C.latest_cls = t.latest_cls;
-  G = blob_classifiers(a, t);
-  const bool kv_lds = LDST && t.kv_lds;
-  const ImgLayout il = t.il;
-  const uint32_t nim = il.n(), nlv = t.nlv, need = t.need;
-  uint32_t* l_off0 = (uint32_t*)(lds + ca.o_off0);
-  uint32_t* l_off1 = (uint32_t*)(lds + ca.o_off1);
-  uint8_t* l_b0 = lds + ca.o_b0;
-  uint8_t* l_b1 = lds + ca.o_b1;
-  auto sf = [](const uint32_t& f) -> uint32_t { return __builtin_amdgcn_readfirstlane(f); };
-  for (uint64_t k = blockIdx.x; k < ca.ntiles; k += gridDim.x) {
-    const ColTile& T = ca.tiles[k];
-    const uint32_t kind = sf(T.kind), e0 = sf(T.e0), n = sf(T.n), glob = sf(T.global);
-    const uint32_t sa0 = sf(T.sa0), nv0 = sf(T.nv0), sa1 = sf(T.sa1), nv1 = sf(T.nv1);
-    // the kind's string columns
-    const int m0 = kind == K_NS ? S_NS : kind == K_CTR ? S_AA : kind == K_ADD ? S_CAPADD : kind == K_DROP ? S_CAPDROP : S_LK;
-    const int m1 = kind == K_CTR ? S_IMG : S_LV;
-    const bool has0 = nv0 != 0, has1 = (kind == K_CTR || kind == K_LBL) && nv1 != 0;
-    if (!glob) {
-      if (has0) {
-        glds_dwords(t.s_off[m0] + e0, l_off0, n + 1, tid);
-        glds_x4((const u32x4*)(t.s_bytes[m0] + sa0), (u32x4*)l_b0, nv0, tid);
-      }
-      if (has1) {
-        glds_dwords(t.s_off[m1] + e0, l_off1, n + 1, tid);
-        glds_x4((const u32x4*)(t.s_bytes[m1] + sa1), (u32x4*)l_b1, nv1, tid);
-      }
-    }
-    __syncthreads();  // staged
-    if (tid < n) {
-      const uint32_t e = e0 + tid;
-      // string j of column m: staged window (LDS, batched reads) or the HBM pool (word reads)
-      auto span = [&](int m, bool second, uint32_t* b, uint32_t* en) {
-        if (glob) {
-          *b = t.s_off[m][e];
-          *en = t.s_off[m][e + 1];
-        } else {
-          const uint32_t* o = second ? l_off1 : l_off0;
-          const uint32_t sa = second ? sa1 : sa0;
-          *b = o[tid] - sa;
-          *en = o[tid + 1] - sa;
-        }
-      };
-      auto lit = [&](Col c, int m, bool second) -> uint32_t {
-        uint32_t b, en;
-        span(m, second, &b, &en);
-        if (glob) return C.lit[c] ? lit_lookup<false>(G.lit[c], t.s_bytes[m], b, en) : 0u;
-        if (!C.lit[c]) return 0u;
-        const uint8_t* bytes = second ? l_b1 : l_b0;
-        if (!__ballot(en - b > 16u)) return lit_lookup<true, 4>(C.lit[c], bytes, b, en);
-        return lit_lookup<true>(C.lit[c], bytes, b, en);
-      };
-      if (kind == K_NS) {
-        a.g_ns[e] = (uint16_t)lit(COL_NS, S_NS, false);
-      } else if (kind == K_ADD) {
-        a.g_capadd[e] = (uint16_t)lit(COL_CAP, S_CAPADD, false);
-      } else if (kind == K_DROP) {
-        a.g_capdrop[e] = (uint16_t)lit(COL_CAP, S_CAPDROP, false);
-      } else if (kind == K_LBL) {
-        const uint32_t kc = (need & (1u << S_LK)) ? lit(COL_LK, S_LK, false) : 0u;
-        a.g_lk[e] = (uint16_t)kc;
-        uint16_t* lv = a.g_lv + (uint64_t)e * nlv;
-        uint32_t b, en;
-        span(S_LV, true, &b, &en);
-        if (glob || !has1)
-          classify_value(G, false, kc, nlv, t.s_bytes[S_LV], glob ? b : t.s_off[S_LV][e], glob ? en : t.s_off[S_LV][e + 1],
-                         [&](uint32_t j, uint32_t c) { lv[j] = (uint16_t)c; });
-        else
-          classify_value(C, kv_lds, kc, nlv, l_b1, b, en, [&](uint32_t j, uint32_t c) { lv[j] = (uint16_t)c; });
-      } else {  // K_CTR: AppArmor profile, image reference
-        const uint32_t fl = a.ctr_flags[e];
-        if (need & (1u << S_AA)) a.g_aa[e] = (uint16_t)((fl & KW_CTR_HAS_APPARMOR) ? lit(COL_AA, S_AA, false) : 0u);
-        if (need & (1u << S_IMG)) {
-          uint16_t* ic = a.g_img + (uint64_t)e * nim;
-          if (fl & KW_CTR_HAS_IMAGE) {
-            uint32_t b, en;
-            span(S_IMG, true, &b, &en);
-            if (glob)
-              classify_image<false>(G, il, t.s_bytes[S_IMG], b, en, [&](uint32_t j, uint32_t c) { ic[j] = (uint16_t)c; });
-            else
-              classify_image<true>(C, il, l_b1, b, en, [&](uint32_t j, uint32_t c) { ic[j] = (uint16_t)c; });
-          } else {
-            for (uint32_t j = 0; j < nim; ++j) ic[j] = 0;
-          }
-        }
-      }
-    }
-    __syncthreads();  // the next tile restages the windows
-  }
-}
-
-hipError_t launch_classify_columns(const EvalArgs& a, const TileArgs* d_t, const TileArgs& t, const ColArgs& c,
-                                   uint32_t grid, hipStream_t s) {
-  if (c.ntiles == 0) return hipSuccess;
-  static std::once_flag once[2];
-  const void* fns[2] = {(const void*)classify_columns_kernel<false>, (const void*)classify_columns_kernel<true>};
-  const int l = t.lds_tables ? 1 : 0;
-  std::call_once(once[l], [&] { (void)hipFuncSetAttribute(fns[l], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); });
-  using Fn = void (*)(EvalArgs, const TileArgs*, ColArgs);
-  hipLaunchKernelGGL((Fn)fns[l], dim3(grid), dim3(kColTile), c.lds_bytes, s, a, d_t, c);
-  return hipGetLastError();
-}
-
-// ------------------------------------------------------------------------------------------
 // Wide policy groups: the members' verdict words of a separate pass -> each group's jump code per
 // row (slots.hpp run_wide_prog), its value stack in this thread's scratch words and its causes in
 // the per-row side data. A row the main pass answered with the bypass word keeps it.

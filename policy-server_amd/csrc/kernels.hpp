@@ -135,29 +135,6 @@ hipError_t launch_evaluate_tiles(const EvalArgs& a, const TileArgs& t, const Til
                                  uint32_t grid, hipStream_t s);
 // Requests that do not fit the LDS capacities even alone (d_overflow: [count, request indices...],
 // host-built with the descriptors): classified into HBM, then walked sequentially per request.
-// Column classification (pre-classified passes): every string the pass reads is turned into its
-// class by classify_columns_kernel, one thread per entity, in column tiles of up to kColTile
-// consecutive entities of one kind, their strings staged in LDS; the classes land in the batch's
-// class arrays (EvalArgs g_*), which the tile kernel's PRE instantiation stages instead of bytes.
-constexpr uint32_t kColTile = 256;
-enum ColKind2 : uint32_t { K_NS = 0, K_CTR = 1, K_ADD = 2, K_DROP = 3, K_LBL = 4 };
-struct alignas(16) ColTile {
-  uint32_t kind, e0, n;  // entities [e0, e0 + n) of `kind`
-  uint32_t sa0, nv0;     // first string column (K_LBL keys, K_CTR AppArmor, else the kind's column):
-                         //   16-B aligned first byte, 16-B units to stage (0: nothing)
-  uint32_t sa1, nv1;     // second (K_LBL values, K_CTR images)
-  uint32_t global;       // 1: one entity beyond the staging capacity, classified from the HBM pools
-};
-static_assert(sizeof(ColTile) == 32, "ColTile layout");
-struct ColArgs {
-  const ColTile* tiles;
-  uint64_t ntiles;
-  uint32_t o_off0, o_off1, o_b0, o_b1;  // LDS: staged offsets (kColTile + 1 u32 each) and bytes
-  uint32_t lds_bytes;
-};
-hipError_t launch_classify_columns(const EvalArgs& a, const TileArgs* d_t, const TileArgs& t, const ColArgs& c,
-                                   uint32_t grid, hipStream_t s);
-
 // Wide policy groups (expr.hpp: more than 64 members, or a value stack deeper than 64): the
 // members ran as a separate all-pairs pass into `member_words` [row][nmw]; the combine kernel runs
 // each group's jump code per row over their results. One record per wide group column of the pass.
