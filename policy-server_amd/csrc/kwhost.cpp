@@ -67,7 +67,16 @@ struct Opts {
   int port = 3000, device = 0, max_batch = 512, max_wait_us = 200, workers = 4;
   size_t max_body = 2u << 20;  // axum DefaultBodyLimit (2 MiB)
   bool continue_on_errors = false, no_device = false;
+  int stats_ms = 0;  // --stats-ms N: a JSON line of cumulative stage times on stderr every N ms
 };
+
+// Where a worker's time goes (--stats-ms): cumulative nanoseconds per stage over all batches.
+struct StageStats {
+  std::atomic<uint64_t> batches{0}, rows{0}, wait_ns{0}, flatten_ns{0}, gpu_ns{0}, format_ns{0};
+};
+static uint64_t ns_since(std::chrono::steady_clock::time_point t) {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t).count();
+}
 
 enum Route { R_VALIDATE, R_AUDIT, R_RAW };
 
@@ -192,6 +201,13 @@ class Server {
         jobs = std::move(work_.front());
         work_.pop_front();
       }
+      {
+        uint64_t w = 0;
+        for (Job* j : jobs) w += ns_since(j->t0);
+        stats_.wait_ns += w;  // arrival -> a worker holds the batch (summed over requests)
+        stats_.batches += 1;
+        stats_.rows += jobs.size();
+      }
       // partition first: a job belongs to its connection thread again once it is answered
       std::vector<Job*> part[3];
       for (Job* j : jobs) part[j->route].push_back(j);
@@ -221,6 +237,7 @@ class Server {
     //    (the handler's extractor runs before the policy lookup)
     kw_batch* b = nullptr;
     char err[1024] = {0};
+    const auto t_flat = std::chrono::steady_clock::now();
     for (;;) {
       if (jobs.empty()) return;
       std::vector<const char*> docs;
@@ -282,6 +299,8 @@ class Server {
       rc = kw_batch_from_json(docs.data(), lens.data(), docs.size(), kind, &b, &bad, err, sizeof(err));
     }
     // 3. upload, evaluate, read back
+    stats_.flatten_ns += ns_since(t_flat);
+    const auto t_gpu = std::chrono::steady_clock::now();
     if (rc == KW_OK && o_.no_device) rc = KW_E_DEVICE;
     if (rc == KW_OK) rc = stream ? kw_batch_to_device_async(b, o_.device, stream) : kw_batch_to_device(b, o_.device);
     if (rc == KW_OK) rc = kw_validate_rows(env_, b, row_policy.data(), origin, stream);
@@ -307,6 +326,8 @@ class Server {
       kw_metrics_record(metrics_, env_, b, mrow.data(), mpol.data(), mv.data(), mlat.data(), mrow.size(), origin);
     }
     // 4. service epilogue + response envelope (AdmissionReviewResponse / RawReviewResponse)
+    stats_.gpu_ns += ns_since(t_gpu);
+    const auto t_fmt = std::chrono::steady_clock::now();
     std::vector<char> buf(4096);
     for (Row& r : rows) {
       size_t need = 0;
@@ -333,8 +354,24 @@ class Server {
       r.job->finish(std::move(rep));
     }
     kw_batch_destroy(b);
+    stats_.format_ns += ns_since(t_fmt);
   }
 
+ public:
+  StageStats stats_;
+  void stats_loop() {
+    for (;;) {
+      std::this_thread::sleep_for(std::chrono::milliseconds(o_.stats_ms));
+      const uint64_t rows = stats_.rows, batches = stats_.batches;
+      fprintf(stderr,
+              "{\"kwhost_stats\": {\"batches\": %llu, \"rows\": %llu, \"mean_batch\": %.1f, \"wait_s_per_request\": %.3g, "
+              "\"worker_s\": {\"flatten\": %.4f, \"gpu_upload_validate_readback\": %.4f, \"format\": %.4f}}}\n",
+              (unsigned long long)batches, (unsigned long long)rows, batches ? (double)rows / batches : 0.0,
+              rows ? stats_.wait_ns / 1e9 / rows : 0.0, stats_.flatten_ns / 1e9, stats_.gpu_ns / 1e9, stats_.format_ns / 1e9);
+      fflush(stderr);
+    }
+  }
+ private:
   const Opts& o_;
   kw_env* env_;
  public:
@@ -557,7 +594,7 @@ void serve(Server* srv, int fd) {
 int usage() {
   fprintf(stderr,
           "usage: kwhost --policies policies.yml [--addr A] [--port P] [--device D] [--max-batch N]\n"
-          "              [--max-wait-us T] [--workers W] [--max-body-bytes B]\n"
+          "              [--max-wait-us T] [--workers W] [--max-body-bytes B] [--stats-ms N]\n"
           "              [--always-accept-admission-reviews-on-namespace NS] [--continue-on-errors] [--no-device]\n");
   return 2;
 }
@@ -577,6 +614,7 @@ int main(int argc, char** argv) {
     else if (a == "--max-batch" && (v = val())) o.max_batch = std::max(1, atoi(v));
     else if (a == "--max-wait-us" && (v = val())) o.max_wait_us = std::max(0, atoi(v));
     else if (a == "--workers" && (v = val())) o.workers = std::max(1, atoi(v));
+    else if (a == "--stats-ms" && (v = val())) o.stats_ms = std::max(0, atoi(v));
     else if (a == "--max-body-bytes" && (v = val())) o.max_body = (size_t)std::max(0ll, atoll(v));
     else if (a == "--always-accept-admission-reviews-on-namespace" && (v = val())) o.always_ns = v;
     else if (a == "--continue-on-errors") o.continue_on_errors = true;
@@ -620,6 +658,7 @@ int main(int argc, char** argv) {
   Server srv(o, env);
   srv.metrics_ = kw_metrics_create();
   srv.start();
+  if (o.stats_ms > 0) std::thread(&Server::stats_loop, &srv).detach();
   fprintf(stderr, "kwhost: %d policies, listening on %s:%d\n", kw_env_policy_count(env), o.addr.c_str(), o.port);
   for (;;) {
     const int fd = accept(ls, nullptr, nullptr);

@@ -18,9 +18,9 @@ MAXB=${MAXB:-512}
 WAIT=${WAIT:-200}
 PORT=$((20000 + RANDOM % 20000))
 OUT=gpurun_out/${TAG}_serve.jsonl
-: > "$OUT"
+: > "$OUT"; : > gpurun_out/${TAG}_serve_stats.jsonl
 policy-server_amd/kwhost --policies "$YML" --port $PORT --device 0 --continue-on-errors \
-  --always-accept-admission-reviews-on-namespace kubewarden --workers $WORKERS --max-batch $MAXB --max-wait-us $WAIT \
+  --always-accept-admission-reviews-on-namespace kubewarden --workers $WORKERS --max-batch $MAXB --max-wait-us $WAIT --stats-ms 1000 \
   2> gpurun_out/${TAG}_kwhost.err &
 KW=$!
 trap 'kill $KW 2>/dev/null; wait $KW 2>/dev/null' EXIT
@@ -34,5 +34,7 @@ for c in $CONNS; do
   timeout -k 5 $((DURATION + WARMUP + 60)) policy-server_amd/kwload --port $PORT --policy "$POLICY" --connections $c \
     --duration $DURATION --warmup $WARMUP --config $SCFG >> "$OUT" || { echo "[serve] kwload failed at $c"; exit 1; }
   tail -1 "$OUT"
+  sleep 1.2  # kwhost's cumulative stage times (--stats-ms) after this run
+  echo "{\"connections\": $c, $(grep kwhost_stats gpurun_out/${TAG}_kwhost.err | tail -1 | cut -c2-)" >> gpurun_out/${TAG}_serve_stats.jsonl
 done
 echo "[serve] done"
