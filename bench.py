@@ -193,24 +193,47 @@ def host_modes(env, ids, syn, device, args):
 
     import kwgpu as K
     out = {}
-    best = None
     import numpy as np
-    vout = np.empty(syn.n * len(ids), dtype=np.uint32)  # the host's verdict buffer, reused as a server would
+    npol = len(ids)
+
+    def best_of(fn, reps=3):
+        best = None
+        for _ in range(reps):
+            hb = syn.batch()  # fresh host columns each time (nothing resident)
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            fn(hb)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t
+            best = dt if best is None else min(best, dt)
+            hb.close()
+        return best
+
+    # pipelined bulk path (kw_validate_host): row chunks whose staging fill, H2D, kernel and D2H overlap
+    pin = K.PinnedWords(syn.n * npol, device=device)
+    try:
+        dt = best_of(lambda hb: hb.validate_host(env, ids, out=pin.array, device=device))
+        out["end_to_end"] = {"value": syn.n / dt, "unit": "requests/s", "rows": syn.n, "ms": dt * 1e3,
+                             "what": "kw_validate_host: host SoA -> pinned staging (host workers) -> H2D -> evaluate -> "
+                                     "D2H straight into a pinned verdict buffer the caller keeps, in overlapped "
+                                     "131072-row chunks on three streams; plan and tile descriptors included, best of 3"}
+    finally:
+        pin.close()
+    vout = np.empty(syn.n * npol, dtype=np.uint32)  # a pageable verdict buffer, reused as a server would
     vout.fill(0)
-    for _ in range(3):
-        hb = syn.batch()
-        torch.cuda.synchronize()
-        t = time.perf_counter()
+    dt = best_of(lambda hb: hb.validate_host(env, ids, out=vout, device=device))
+    out["end_to_end_pageable"] = {"value": syn.n / dt, "unit": "requests/s", "rows": syn.n, "ms": dt * 1e3,
+                                  "what": "the same into a pageable verdict buffer (pinned bounce blocks, copy-out "
+                                          "on the host workers overlapped with the next chunk)"}
+
+    def serial(hb):
         hb.to_device(device)
         hb.validate(env, ids)
         hb.verdicts(out=vout)
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t
-        best = dt if best is None else min(best, dt)
-        hb.close()
-    out["end_to_end"] = {"value": syn.n / best, "unit": "requests/s", "rows": syn.n,
-                         "what": "host SoA -> pinned staging (parallel fill) -> H2D -> evaluate -> D2H verdicts into a "
-                                 "reused pageable array (pinned bounce), plan and tile descriptors included, best of 3"}
+    dt = best_of(serial)
+    out["end_to_end_serial"] = {"value": syn.n / dt, "unit": "requests/s", "rows": syn.n, "ms": dt * 1e3,
+                                "what": "unpipelined: kw_batch_to_device (every column) -> kw_validate_batch -> "
+                                        "kw_batch_verdicts into the pageable buffer, best of 3"}
     import ctypes as C
     n = min(100_000, syn.n)
     docs = [syn.json(i).encode() for i in range(n)]

@@ -267,6 +267,20 @@ int kw_validate_batch(const kw_env *env, kw_batch *b, const int32_t *policies, u
 int kw_validate_rows(const kw_env *env, kw_batch *b, const int32_t *row_policy, int origin,
                      void *stream);
 int kw_batch_verdicts(kw_batch *b, uint32_t *host_out, size_t count);
+/* Bulk form for callers that hand over host columns and want host verdicts (SURVEY §8(d) timing
+ * mode 2): uploads the batch to `device`, evaluates every row against the npol policies and writes
+ * the [row][npol] verdict words to host `out` (count = rows x npol). The batch is cut into chunks of
+ * about chunk_rows rows (0: 131072) whose upload, evaluation and read-back overlap on three streams;
+ * only the string columns the pass reads are uploaded (a later pass on the batch that needs others
+ * returns KW_E_ARG until the batch is uploaded again). `out` may be pageable (read back through
+ * pinned bounce blocks) or pinned (kw_host_alloc: direct DMA). Passes that need several launches,
+ * overflow requests or wide side data run unchunked with the same result. Synchronous. Replaces,
+ * for a bulk caller, the per-request loop of acquire_semaphore_and_evaluate (handlers.rs:256-286). */
+int kw_validate_host(const kw_env *env, kw_batch *b, const int32_t *policies, uint32_t npol, int origin,
+                     int device, uint32_t *out, size_t count, uint32_t chunk_rows);
+/* Pinned (page-locked) host memory for verdict buffers a caller keeps (direct DMA), and its release. */
+int kw_host_alloc(int device, size_t bytes, void **out);
+void kw_host_free(void *p);
 /* The full argument of a verdict word whose ARG is KW_ARG_WIDE, for (row, policy) of the last pass
  * whose verdicts were copied (kw_batch_verdicts). KW_E_NOT_FOUND when the pass recorded none. */
 int kw_batch_wide_arg(const kw_batch *b, uint64_t row, int32_t policy, uint64_t *value);

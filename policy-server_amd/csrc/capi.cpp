@@ -3,9 +3,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -98,6 +102,86 @@ void parallel_copy(void* dst, const void* src, size_t bytes) {
   for (auto& x : th) x.join();
 }
 
+// Persistent host workers for the bulk path (kw_validate_host): a parallel-for over many short
+// tasks (copy segments, tile ranges) without starting threads per call. The caller runs tasks too.
+class HostWorkers {
+ public:
+  static HostWorkers& get() {
+    static HostWorkers* w = new HostWorkers();  // process lifetime (workers park on a condition)
+    return *w;
+  }
+  unsigned size() const { return (unsigned)th_.size() + 1; }
+  // fn(i) for every i in [0, n), spread over the workers and the caller; returns when all are done
+  void run(size_t n, const std::function<void(size_t)>& fn) {
+    if (n == 0) return;
+    std::lock_guard<std::mutex> one(run_m_);  // one parallel-for at a time
+    {
+      std::lock_guard<std::mutex> g(m_);
+      fn_ = &fn;
+      next_.store(0);
+      n_.store(n);
+      done_ = 0;
+      ++gen_;
+    }
+    cv_.notify_all();
+    const size_t mine = work();
+    std::unique_lock<std::mutex> g(m_);
+    done_ += mine;
+    done_cv_.wait(g, [&] { return done_ == n_; });
+    fn_ = nullptr;
+  }
+
+ private:
+  HostWorkers() {
+    const char* e = getenv("KW_HOST_THREADS");
+    unsigned n = e ? (unsigned)std::max(1, atoi(e)) : std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    for (unsigned i = 1; i < n; ++i) th_.emplace_back([this] { loop(); });
+    for (auto& t : th_) t.detach();
+  }
+  size_t work() {
+    size_t k = 0;
+    for (size_t i; (i = next_.fetch_add(1)) < n_; ++k) (*fn_)(i);
+    return k;
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return gen_ != seen && fn_ != nullptr; });
+        seen = gen_;
+      }
+      const size_t mine = work();
+      std::lock_guard<std::mutex> g(m_);
+      done_ += mine;
+      if (done_ == n_) done_cv_.notify_all();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_, run_m_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(size_t)>* fn_ = nullptr;
+  std::atomic<size_t> n_{0};
+  size_t done_ = 0;
+  std::atomic<size_t> next_{0};
+  uint64_t gen_ = 0;
+};
+
+// Copies of several (dst, src, bytes) segments cut into ~1 MB tasks on the host workers.
+struct CopySeg {
+  void* dst;
+  const void* src;
+  size_t bytes;
+};
+void parallel_copy_segs(const std::vector<CopySeg>& segs) {
+  constexpr size_t kTask = (size_t)1 << 20;
+  std::vector<CopySeg> tasks;
+  for (const CopySeg& c : segs)
+    for (size_t a = 0; a < c.bytes; a += kTask)
+      tasks.push_back({(uint8_t*)c.dst + a, (const uint8_t*)c.src + a, std::min(kTask, c.bytes - a)});
+  HostWorkers::get().run(tasks.size(), [&](size_t i) { memcpy(tasks[i].dst, tasks[i].src, tasks[i].bytes); });
+}
+
 // Requests per tile of the tile kernel forced by KW_SLOT_ROWS (8..255, A/B knob), 0 = chosen per
 // batch (plan_pass: kSlotRows, or taller tiles where they keep enough workgroups per CU).
 uint32_t slot_rows_forced() {
@@ -136,6 +220,7 @@ struct DeviceBatch {
   uint32_t* verdicts = nullptr;
   size_t verdict_cap = 0;
   size_t last_verdicts = 0;
+  uint32_t loaded = 0;        // string columns (bits of Str) whose bytes are resident (kw_validate_host uploads only its pass's)
   uint32_t* sched = nullptr;  // tile counters (zeroed once; each launch leaves them zero)
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
   // the last pass's plan as the kernels read it (host copies detect a changed plan)
@@ -309,7 +394,11 @@ constexpr double kTileQuantiles[] = {1.0, 0.99995, 0.9999, 0.9995, 0.999, 0.998}
 std::vector<TileStats> tile_needs(const Batch& B, uint32_t rows) {
   const uint64_t ntiles = (B.n + rows - 1) / rows;
   std::vector<TileStats> v(ntiles);
-  for (uint64_t t = 0; t < ntiles; ++t) {
+  // tiles in ranges of 4096 on the host workers (each tile's reads are cache misses: 1M requests
+  // take ~3 ms on one thread per tile height)
+  constexpr uint64_t kRange = 4096;
+  HostWorkers::get().run((size_t)((ntiles + kRange - 1) / kRange), [&](size_t q) {
+  for (uint64_t t = q * kRange, t1 = std::min<uint64_t>(ntiles, (q + 1) * kRange); t < t1; ++t) {
     const uint64_t r0 = t * rows, r1 = std::min<uint64_t>(B.n, (t + 1) * rows);
     TileStats& st = v[t];
     st.ctr = B.ctr_off[r1] - B.ctr_off[r0];
@@ -323,6 +412,7 @@ std::vector<TileStats> tile_needs(const Batch& B, uint32_t rows) {
       st.bytes[m] = ((c.off[g1] + 15u) & ~15u) - (c.off[g0] & ~15u);
     }
   }
+  });
   return v;
 }
 
@@ -344,6 +434,41 @@ TileStats tile_quantile(const std::vector<TileStats>& need, double quantile) {
   st.kdrop = quant([](const TileStats& x) { return x.kdrop; });
   for (int m = 0; m < (int)NSTR; ++m) st.bytes[m] = quant([m](const TileStats& x) { return x.bytes[m]; });
   return st;
+}
+
+// All the capacity-candidate quantiles at once (kTileQuantiles order): per dimension one selection
+// at the lowest quantile and a sort of the tail above it (the candidates are all >= 0.998: a few
+// dozen values of a 1M-request batch's 15k tiles), dimensions on the host workers.
+std::vector<TileStats> tile_quantiles(const std::vector<TileStats>& need, const double* qs, size_t nq) {
+  std::vector<TileStats> out(nq);
+  if (need.empty() || nq == 0) return out;
+  const uint64_t n = need.size();
+  std::vector<uint64_t> qi(nq);
+  uint64_t qmin = n - 1;
+  for (size_t k = 0; k < nq; ++k) {
+    qi[k] = qs[k] >= 1.0 ? n - 1 : (uint64_t)(qs[k] * (double)(n - 1));
+    qmin = std::min(qmin, qi[k]);
+  }
+  constexpr int kDims = 4 + (int)NSTR;
+  auto dim = [](const TileStats& x, int d) -> uint32_t {
+    return d == 0 ? x.ctr : d == 1 ? x.lbl : d == 2 ? x.kadd : d == 3 ? x.kdrop : x.bytes[d - 4];
+  };
+  auto put = [](TileStats& x, int d, uint32_t v) {
+    if (d == 0) x.ctr = v;
+    else if (d == 1) x.lbl = v;
+    else if (d == 2) x.kadd = v;
+    else if (d == 3) x.kdrop = v;
+    else x.bytes[d - 4] = v;
+  };
+  HostWorkers::get().run(kDims, [&](size_t di) {
+    const int d = (int)di;
+    std::vector<uint32_t> v(n);
+    for (uint64_t t = 0; t < n; ++t) v[t] = dim(need[t], d);
+    std::nth_element(v.begin(), v.begin() + (long)qmin, v.end());
+    std::sort(v.begin() + (long)qmin, v.end());
+    for (size_t k = 0; k < qi.size(); ++k) put(out[k], d, v[qi[k]]);
+  });
+  return out;
 }
 
 struct PassPlan {
@@ -619,7 +744,7 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
       R = &D.rows_plans.back();
       R->rows = r;
       R->need = tile_needs(B, r);
-      for (double q : kTileQuantiles) R->q.push_back(tile_quantile(R->need, q));
+      R->q = tile_quantiles(R->need, kTileQuantiles, sizeof(kTileQuantiles) / sizeof(kTileQuantiles[0]));
     }
     rows = r;
     if (R->cap_choice < 0 || R->cap_key != key) {
@@ -859,25 +984,39 @@ int upload_tile_descs(const Batch& B, DeviceBatch* D, const TileArgs& T, hipStre
     return fits;
   };
   // a run that does not fit is halved until its parts do; a single request that does not fit
-  // goes to the overflow kernels
-  std::vector<std::pair<uint64_t, uint64_t>> todo;
-  for (uint64_t tile = 0; tile < ntiles; ++tile) {
-    todo.assign(1, {tile * T.rows, std::min<uint64_t>(B.n, (tile + 1) * T.rows)});
-    while (!todo.empty()) {
-      const auto [r0, r1] = todo.back();
-      todo.pop_back();
-      TileDesc d;
-      if (make(r0, r1, &d)) {
-        desc.push_back(d);
-      } else if (r1 - r0 > 1) {
-        const uint64_t mid = r0 + (r1 - r0) / 2;
-        todo.push_back({mid, r1});
-        todo.push_back({r0, mid});
-      } else {
-        if (r0 > 0xffffffffull) return KW_E_ARG;  // overflow list holds u32 request indices
-        ovf.push_back((uint32_t)r0);
+  // goes to the overflow kernels. Tiles in ranges on the host workers, concatenated in row order.
+  constexpr uint64_t kRange = 4096;
+  const size_t nq = (size_t)((ntiles + kRange - 1) / kRange);
+  std::vector<std::vector<TileDesc>> qdesc(nq);
+  std::vector<std::vector<uint32_t>> qovf(nq);
+  std::atomic<bool> too_far{false};
+  HostWorkers::get().run(nq, [&](size_t q) {
+    std::vector<std::pair<uint64_t, uint64_t>> todo;
+    std::vector<TileDesc>& dv = qdesc[q];
+    dv.reserve((size_t)kRange + kRange / 64);
+    for (uint64_t tile = q * kRange, t1 = std::min<uint64_t>(ntiles, (q + 1) * kRange); tile < t1; ++tile) {
+      todo.assign(1, {tile * T.rows, std::min<uint64_t>(B.n, (tile + 1) * T.rows)});
+      while (!todo.empty()) {
+        const auto [r0, r1] = todo.back();
+        todo.pop_back();
+        TileDesc d;
+        if (make(r0, r1, &d)) {
+          dv.push_back(d);
+        } else if (r1 - r0 > 1) {
+          const uint64_t mid = r0 + (r1 - r0) / 2;
+          todo.push_back({mid, r1});
+          todo.push_back({r0, mid});
+        } else {
+          if (r0 > 0xffffffffull) too_far = true;  // overflow list holds u32 request indices
+          qovf[q].push_back((uint32_t)r0);
+        }
       }
     }
+  });
+  if (too_far) return KW_E_ARG;
+  for (size_t q = 0; q < nq; ++q) {
+    desc.insert(desc.end(), qdesc[q].begin(), qdesc[q].end());
+    ovf.insert(ovf.end(), qovf[q].begin(), qovf[q].end());
   }
   ovf[0] = (uint32_t)(ovf.size() - 1);
   HIPCHK(hipStreamSynchronize(s));  // a running pass may still read the previous descriptors
@@ -918,7 +1057,10 @@ int ensure_overflow_classes(const Batch& B, DeviceBatch* D, const TileArgs& T, E
   return KW_OK;
 }
 
-int run_pass(kw_batch* kb, PassPlan& plan, bool timed, hipStream_t s) {
+// Everything a pass's launches need on the device before the first one: the plan's records and
+// TileArgs, the rows-mode column map, tile descriptors and overflow list, schedule counters and the
+// side-data buffers; *out_args: the launch arguments.
+int prepare_pass(kw_batch* kb, PassPlan& plan, hipStream_t s, EvalArgs* out_args) {
   DeviceBatch& D = *kb->dev;
   const Batch& B = kb->b;
   if (D.cur && D.cur != s) HIPCHK(hipStreamSynchronize(D.cur));  // order against the previous pass's stream
@@ -986,10 +1128,18 @@ int run_pass(kw_batch* kb, PassPlan& plan, bool timed, hipStream_t s) {
   D.last_wide_policy = plan.wide_policy;
   D.last_rows_mode = plan.rows_mode;
   D.last_wide_cap = A.wide_cap;
+  *out_args = A;
+  return KW_OK;
+}
+
+int run_pass(kw_batch* kb, PassPlan& plan, bool timed, hipStream_t s) {
+  DeviceBatch& D = *kb->dev;
+  EvalArgs A;
+  if (int rc = prepare_pass(kb, plan, s, &A)) return rc;
   // diagnostics: per-phase clocks of the tile kernel (KW_TILE_DEBUG & 512), printed per launch
   const bool phases = (plan.geom.debug & 512u) != 0;
   void* d_phase = nullptr;
-  const size_t phase_bytes = (size_t)plan.grid * 8 * sizeof(uint64_t);
+  const size_t phase_bytes = (size_t)plan.grid * kPhaseWords * sizeof(uint64_t);
   if (phases) {
     HIPCHK(hipMalloc(&d_phase, phase_bytes));
     A.phase = (uint64_t*)d_phase;
@@ -999,18 +1149,27 @@ int run_pass(kw_batch* kb, PassPlan& plan, bool timed, hipStream_t s) {
     if (phases) HIPCHK(hipMemsetAsync(d_phase, 0, phase_bytes, s));
     HIPCHK(launch_evaluate_tiles(A, plan.tiles[l], D.d_tiles + l, D.desc, plan.grid, s));
     if (phases) {
-      std::vector<uint64_t> ph((size_t)plan.grid * 8);
+      std::vector<uint64_t> ph((size_t)plan.grid * kPhaseWords);
       HIPCHK(hipMemcpyAsync(ph.data(), d_phase, phase_bytes, hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
-      double sum[8] = {0};
+      double sum[kPhaseWords] = {0};
       for (uint32_t g = 0; g < plan.grid; ++g)
-        for (int k = 0; k < 8; ++k) sum[k] += (double)ph[(size_t)g * 8 + k];
+        for (uint32_t k = 0; k < kPhaseWords; ++k) sum[k] += (double)ph[(size_t)g * kPhaseWords + k];
       const double tiles = std::max(1.0, sum[5]);
       fprintf(stderr,
               "[kw phase] launch %zu grid %u tiles %.0f: cycles/tile P0 %.0f P1 %.0f D %.0f P2 %.0f P3+next %.0f "
               "(sum %.0f); per workgroup: %.0f cycles, %.2f tiles, table staging %.0f\n",
               l, plan.grid, tiles, sum[0] / tiles, sum[1] / tiles, sum[2] / tiles, sum[3] / tiles, sum[4] / tiles,
               (sum[0] + sum[1] + sum[2] + sum[3] + sum[4]) / tiles, sum[6] / plan.grid, tiles / plan.grid, sum[7] / plan.grid);
+      // per wave and tile: P1 / P2 segment cycles, each phase's busy time and its barrier wait
+      const double wt = tiles * (double)(kSlotThreads / 64u);
+      const double* g = sum + 8;
+      fprintf(stderr,
+              "[kw seg] per wave-tile: P0 wait %.0f | P1 busy %.0f wait %.0f (label %.0f capstr %.0f ctr %.0f image %.0f req %.0f) "
+              "| P2 busy %.0f wait %.0f (ctr %.0f label %.0f req %.0f) | P3 busy %.0f wait %.0f\n",
+              g[SG_P0_WAIT] / wt, g[SG_P1_BUSY] / wt, g[SG_P1_WAIT] / wt, g[SG_P1_LABEL] / wt, g[SG_P1_CAPSTR] / wt,
+              g[SG_P1_CTR] / wt, g[SG_P1_IMAGE] / wt, g[SG_P1_REQ] / wt, g[SG_P2_BUSY] / wt, g[SG_P2_WAIT] / wt,
+              g[SG_P2_CTR] / wt, g[SG_P2_LABEL] / wt, g[SG_P2_REQ] / wt, g[SG_P3_BUSY] / wt, g[SG_P3_WAIT] / wt);
     }
     if (D.n_overflow) HIPCHK(launch_overflow(A, D.d_tiles + l, D.overflow, D.n_overflow, s));
   }
@@ -1106,7 +1265,8 @@ int validate_common(const kw_env* env, kw_batch* kb, const int32_t* policies, ui
   if (int rc = ensure(&D.verdicts, &D.verdict_cap, npairs)) return rc;
   D.last_verdicts = npairs;
   kb->b.wide.clear();
-  return plan_pass(env, kb, policies, npol, row_policy, origin, plan);
+  if (int rc = plan_pass(env, kb, policies, npol, row_policy, origin, plan)) return rc;
+  return (plan->geom.need & ~D.loaded) ? KW_E_ARG : KW_OK;  // a column the upload left out (kw_validate_host)
 }
 
 }  // namespace
@@ -1518,7 +1678,20 @@ namespace {
 // Upload the batch's columns to `device`: one pooled allocation with 256-B aligned sub-arrays,
 // assembled in pinned host staging and copied with one async H2D on `stream` (null: a new stream
 // owned by the batch); `sync` waits for the copy.
-int upload_batch(kw_batch* kb, int device, hipStream_t stream, bool sync) {
+// A column of the device batch image: where its bytes come from and sit, and how a row range maps
+// onto it (the bulk path uploads row chunks separately).
+enum PieceKind { PK_ROW_U8, PK_ROW_OFF, PK_CTR_U8, PK_CTR_OFF, PK_STR_OFF, PK_STR_BYTES };
+struct Piece {
+  const void* src;
+  size_t bytes;  // source bytes (reserved 256-B aligned in the image)
+  size_t at;     // offset in the device image and in the pinned staging
+  PieceKind kind;
+  int m;         // string column (PK_STR_*), else -1
+};
+
+// Allocates the batch's device image (one pooled allocation, 256-B aligned sub-arrays) and its
+// pinned staging block, and points the DeviceBatch views at it; nothing is copied.
+int layout_batch(kw_batch* kb, int device, hipStream_t stream, std::vector<Piece>* pieces) {
   if (!kb || device < 0) return KW_E_ARG;
   HIPCHK(hipSetDevice(device));
   if (kb->dev) kb->dev.reset();  // re-upload: the previous device copy returns to the pools
@@ -1532,31 +1705,26 @@ int upload_batch(kw_batch* kb, int device, hipStream_t stream, bool sync) {
   }
   Batch& B = kb->b;
   B.finalize();
-  struct Piece {
-    const void* src;
-    size_t bytes;
-    size_t at;
-  };
-  std::vector<Piece> pieces;
+  pieces->clear();
   size_t total = 0;
-  auto add = [&](const void* src, size_t bytes) {
+  auto add = [&](const void* src, size_t bytes, PieceKind k, int m) {
     size_t at = total;
-    pieces.push_back({src, bytes, at});
+    pieces->push_back({src, bytes, at, k, m});
     total += (bytes + 255) & ~(size_t)255;
     return at;
   };
-  size_t o_rf = add(B.req_flags.data(), B.req_flags.size());
-  size_t o_co = add(B.ctr_off.data(), B.ctr_off.size() * 4);
-  size_t o_lo = add(B.lbl_off.data(), B.lbl_off.size() * 4);
-  size_t o_cf = add(B.ctr_flags.data(), B.ctr_flags.size());
-  size_t o_ca = add(B.capadd_off.data(), B.capadd_off.size() * 4);
-  size_t o_cd = add(B.capdrop_off.data(), B.capdrop_off.size() * 4);
-  struct ColAt {
-    size_t off, bytes;
-  };
-  auto addcol = [&](const StrCol& c) { return ColAt{add(c.off.data(), c.off.size() * 4), add(c.bytes.data(), c.bytes.size())}; };
-  ColAt c_ns = addcol(B.ns), c_img = addcol(B.ctr_image), c_aa = addcol(B.ctr_aa), c_add = addcol(B.cap_add),
-        c_drop = addcol(B.cap_drop), c_lk = addcol(B.lbl_key), c_lv = addcol(B.lbl_val);
+  size_t o_rf = add(B.req_flags.data(), B.req_flags.size(), PK_ROW_U8, -1);
+  size_t o_co = add(B.ctr_off.data(), B.ctr_off.size() * 4, PK_ROW_OFF, -1);
+  size_t o_lo = add(B.lbl_off.data(), B.lbl_off.size() * 4, PK_ROW_OFF, -1);
+  size_t o_cf = add(B.ctr_flags.data(), B.ctr_flags.size(), PK_CTR_U8, -1);
+  size_t o_ca = add(B.capadd_off.data(), B.capadd_off.size() * 4, PK_CTR_OFF, -1);
+  size_t o_cd = add(B.capdrop_off.data(), B.capdrop_off.size() * 4, PK_CTR_OFF, -1);
+  size_t c_off[NSTR], c_bytes[NSTR];
+  for (int m = 0; m < (int)NSTR; ++m) {
+    const StrCol& c = host_str(B, m);
+    c_off[m] = add(c.off.data(), c.off.size() * 4, PK_STR_OFF, m);
+    c_bytes[m] = add(c.bytes.data(), c.bytes.size(), PK_STR_BYTES, m);
+  }
   total = std::max<size_t>(total, 256);
   void* dcols = nullptr;
   HIPCHK(dev_pool().alloc(device, total, &dcols));
@@ -1564,11 +1732,6 @@ int upload_batch(kw_batch* kb, int device, hipStream_t stream, bool sync) {
   D->cols_bytes = total;
   HIPCHK(host_pool().alloc(device, total, &D->staging));
   D->staging_bytes = total;
-  uint8_t* st = (uint8_t*)D->staging;
-  for (auto& p : pieces)
-    if (p.bytes) parallel_copy(st + p.at, p.src, p.bytes);
-  HIPCHK(hipMemcpyAsync(D->cols, st, total, hipMemcpyHostToDevice, D->stream));
-  if (sync) HIPCHK(hipStreamSynchronize(D->stream));
   D->cur = D->stream;
   D->req_flags = D->cols + o_rf;
   D->ctr_off = (const uint32_t*)(D->cols + o_co);
@@ -1576,23 +1739,190 @@ int upload_batch(kw_batch* kb, int device, hipStream_t stream, bool sync) {
   D->ctr_flags = D->cols + o_cf;
   D->capadd_off = (const uint32_t*)(D->cols + o_ca);
   D->capdrop_off = (const uint32_t*)(D->cols + o_cd);
-  auto dcol = [&](const StrCol& c, ColAt at) {
-    DeviceBatch::DCol d;
-    d.off = (const uint32_t*)(D->cols + at.off);
-    d.bytes = D->cols + at.bytes;
+  for (int m = 0; m < (int)NSTR; ++m) {
+    const StrCol& c = host_str(B, m);
+    DeviceBatch::DCol& d = D->str[m];
+    d.off = (const uint32_t*)(D->cols + c_off[m]);
+    d.bytes = D->cols + c_bytes[m];
     d.n = c.n();
     d.nbytes = c.off.back();
-    return d;
-  };
-  D->str[S_NS] = dcol(B.ns, c_ns);
-  D->str[S_IMG] = dcol(B.ctr_image, c_img);
-  D->str[S_AA] = dcol(B.ctr_aa, c_aa);
-  D->str[S_CAPADD] = dcol(B.cap_add, c_add);
-  D->str[S_CAPDROP] = dcol(B.cap_drop, c_drop);
-  D->str[S_LK] = dcol(B.lbl_key, c_lk);
-  D->str[S_LV] = dcol(B.lbl_val, c_lv);
+  }
   kb->dev = std::move(D);
   return KW_OK;
+}
+
+int upload_batch(kw_batch* kb, int device, hipStream_t stream, bool sync) {
+  std::vector<Piece> pieces;
+  if (int rc = layout_batch(kb, device, stream, &pieces)) return rc;
+  DeviceBatch& D = *kb->dev;
+  uint8_t* st = (uint8_t*)D.staging;
+  for (auto& p : pieces)
+    if (p.bytes) parallel_copy(st + p.at, p.src, p.bytes);
+  HIPCHK(hipMemcpyAsync(D.cols, st, D.cols_bytes, hipMemcpyHostToDevice, D.stream));
+  if (sync) HIPCHK(hipStreamSynchronize(D.stream));
+  D.loaded = ~0u;
+  return KW_OK;
+}
+
+// Byte range [lo, hi) of piece p that rows [r0, r1) occupy. A chunk's string bytes run 64 bytes past
+// its last string (the device's batched reads past a string end stay inside uploaded bytes); the
+// first chunk starts at 0 and the last runs to the piece's end (its zero padding).
+void piece_range(const Batch& B, const Piece& p, uint64_t r0, uint64_t r1, bool last, size_t* lo, size_t* hi) {
+  size_t a = 0, e = 0;
+  uint64_t g0 = 0, g1 = 0;
+  switch (p.kind) {
+    case PK_ROW_U8: a = r0; e = r1; break;
+    case PK_ROW_OFF: a = 4 * r0; e = 4 * (r1 + 1); break;
+    case PK_CTR_U8: a = B.ctr_off[r0]; e = B.ctr_off[r1]; break;
+    case PK_CTR_OFF: a = 4ull * B.ctr_off[r0]; e = 4ull * ((uint64_t)B.ctr_off[r1] + 1); break;
+    case PK_STR_OFF: str_range(B, p.m, r0, r1, &g0, &g1); a = 4 * g0; e = 4 * (g1 + 1); break;
+    case PK_STR_BYTES: {
+      str_range(B, p.m, r0, r1, &g0, &g1);
+      const StrCol& c = host_str(B, p.m);
+      a = c.off[g0];
+      e = (size_t)c.off[g1] + 64;
+      break;
+    }
+  }
+  if (r0 == 0) a = 0;
+  if (last) e = p.bytes;
+  *lo = std::min(a, p.bytes);
+  *hi = std::min(std::max(e, a), p.bytes);
+}
+
+// Bulk host -> host validation (kw_validate_host): the batch's columns are uploaded, evaluated and
+// read back in row chunks whose stages overlap: the host workers fill chunk k's pinned staging while
+// the copy engines move chunk k-1 in and chunk k-2's verdicts out and the tile kernel evaluates in
+// between (three streams ordered by events). Only the string columns the pass reads are uploaded.
+// Passes with several launches, overflow requests or wide side data run unchunked (upload, pass,
+// read-back) with the same result.
+int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint32_t npol, int origin, int device,
+                  uint32_t* out, size_t count, uint32_t chunk_rows) {
+  if (!env || !kb || !out || !policies || npol == 0) return KW_E_ARG;
+  if (env->e.device < 0 || !env->e.d_blob) return KW_E_DEVICE;
+  if (device != env->e.device || count != kb->b.n * (uint64_t)npol) return KW_E_ARG;
+  // diagnostics (KW_BULK_DEBUG=1): host wall time of each stage, printed at the end
+  static const bool dbg = getenv("KW_BULK_DEBUG") && atoi(getenv("KW_BULK_DEBUG")) != 0;
+  using clk = std::chrono::steady_clock;
+  const auto t_start = clk::now();
+  double t_layout = 0, t_plan = 0, t_prep = 0, t_fill = 0, t_enq = 0, t_out = 0;
+  auto since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
+  std::vector<Piece> pieces;
+  if (int rc = layout_batch(kb, device, nullptr, &pieces)) return rc;
+  t_layout = since(t_start);
+  DeviceBatch& D = *kb->dev;
+  const Batch& B = kb->b;
+  D.loaded = ~0u;  // (planned as if resident; set to the pass's columns below)
+  PassPlan plan;
+  if (int rc = validate_common(env, kb, policies, npol, nullptr, origin, &plan)) {
+    D.loaded = 0;
+    return rc;
+  }
+  const uint32_t need = plan.geom.need;
+  t_plan = since(t_start) - t_layout;
+  auto wanted = [&](const Piece& p) { return p.m < 0 || ((need >> p.m) & 1u); };
+  uint8_t* st = (uint8_t*)D.staging;
+  hipStream_t sc = D.stream;
+  EvalArgs A;
+  bool chunked = plan.tiles.size() == 1 && plan.wide.groups.empty() && plan.nwide == 0 && !plan.rows_mode &&
+                 !(plan.geom.debug & 512u) && B.n > 0;
+  if (chunked) {
+    if (int rc = prepare_pass(kb, plan, sc, &A)) {
+      D.loaded = 0;
+      return rc;
+    }
+    chunked = D.n_overflow == 0 && D.ndesc > 0;
+  }
+  t_prep = since(t_start) - t_layout - t_plan;
+  if (!chunked) {  // one upload, the full pass, one read-back
+    std::vector<CopySeg> segs;
+    for (const Piece& p : pieces)
+      if (p.bytes) segs.push_back({st + p.at, p.src, p.bytes});
+    parallel_copy_segs(segs);
+    HIPCHK(hipMemcpyAsync(D.cols, st, D.cols_bytes, hipMemcpyHostToDevice, sc));
+    if (int rc = run_validate(env, kb, plan, origin, false, sc)) return rc;
+    return kw_batch_verdicts(kb, out, count);
+  }
+  D.loaded = need;
+  const uint64_t per = chunk_rows ? chunk_rows : 131072;
+  const uint64_t K = std::max<uint64_t>(1, std::min<uint64_t>({(B.n + per - 1) / per, D.ndesc, 256}));
+  std::vector<uint64_t> db(K + 1), rb(K + 1);  // chunk k: descriptors [db[k], db[k+1]), rows [rb[k], rb[k+1])
+  for (uint64_t k = 0; k <= K; ++k) {
+    db[k] = D.ndesc * k / K;
+    rb[k] = k == K ? B.n : (k == 0 ? 0 : ((uint64_t)D.h_desc[db[k]].r0hi << 32 | D.h_desc[db[k]].r0lo));
+  }
+  hipPointerAttribute_t attr;
+  const bool pinned = hipPointerGetAttributes(&attr, out) == hipSuccess && attr.type == hipMemoryTypeHost;
+  (void)hipGetLastError();  // a pageable pointer leaves an error state behind
+  uint64_t max_rows = 0;
+  for (uint64_t k = 0; k < K; ++k) max_rows = std::max(max_rows, rb[k + 1] - rb[k]);
+  const size_t bounce_bytes = (size_t)max_rows * npol * 4;
+  void* bounce[2] = {nullptr, nullptr};
+  hipStream_t s_in = nullptr, s_out = nullptr;
+  std::vector<hipEvent_t> ev(3 * K, nullptr);
+  int rc = KW_OK;  // (a failure below leaves the batch's columns partly uploaded: D.loaded is cleared)
+  auto fail = [&](hipError_t e) {
+    if (e != hipSuccess && rc == KW_OK) rc = KW_E_DEVICE;
+    return e != hipSuccess;
+  };
+  if (!pinned)
+    for (auto& b : bounce)
+      if (fail(host_pool().alloc(device, bounce_bytes, &b))) break;
+  if (rc == KW_OK && !fail(hipStreamCreateWithFlags(&s_in, hipStreamNonBlocking)) &&
+      !fail(hipStreamCreateWithFlags(&s_out, hipStreamNonBlocking)))
+    for (auto& e : ev)
+      if (fail(hipEventCreateWithFlags(&e, hipEventDisableTiming))) break;
+  auto copy_out = [&](uint64_t k) {
+    const auto t0 = clk::now();
+    if (pinned || rc != KW_OK || fail(hipEventSynchronize(ev[3 * k + 2]))) return;
+    parallel_copy_segs({{out + rb[k] * npol, bounce[k & 1], (size_t)(rb[k + 1] - rb[k]) * npol * 4}});
+    t_out += since(t0);
+  };
+  for (uint64_t k = 0; k < K && rc == KW_OK; ++k) {
+    const uint64_t r0 = rb[k], r1 = rb[k + 1];
+    std::vector<CopySeg> segs;
+    for (const Piece& p : pieces) {
+      if (!wanted(p)) continue;
+      size_t lo, hi;
+      piece_range(B, p, r0, r1, k + 1 == K, &lo, &hi);
+      if (hi > lo) segs.push_back({st + p.at + lo, (const uint8_t*)p.src + lo, hi - lo});
+    }
+    const auto t0 = clk::now();
+    parallel_copy_segs(segs);
+    t_fill += since(t0);
+    const auto t1 = clk::now();
+    for (const CopySeg& c : segs)
+      if (fail(hipMemcpyAsync(D.cols + ((uint8_t*)c.dst - st), c.dst, c.bytes, hipMemcpyHostToDevice, s_in))) break;
+    if (rc != KW_OK || fail(hipEventRecord(ev[3 * k], s_in)) || fail(hipStreamWaitEvent(sc, ev[3 * k], 0))) break;
+    EvalArgs Ak = A;
+    Ak.ndesc = db[k + 1] - db[k];
+    if (fail(launch_evaluate_tiles(Ak, plan.tiles[0], D.d_tiles, D.desc + db[k], plan.grid, sc))) break;
+    if (fail(hipEventRecord(ev[3 * k + 1], sc)) || fail(hipStreamWaitEvent(s_out, ev[3 * k + 1], 0))) break;
+    uint32_t* dst = pinned ? out + r0 * npol : (uint32_t*)bounce[k & 1];
+    if (fail(hipMemcpyAsync(dst, D.verdicts + r0 * npol, (size_t)(r1 - r0) * npol * 4, hipMemcpyDeviceToHost, s_out))) break;
+    if (fail(hipEventRecord(ev[3 * k + 2], s_out))) break;
+    t_enq += since(t1);
+    if (k >= 1) copy_out(k - 1);  // (bounce[k & 1] was last read by chunk k - 2's copy-out)
+  }
+  if (rc == KW_OK) copy_out(K - 1);
+  const auto t_w = clk::now();
+  if (s_in) (void)hipStreamSynchronize(s_in);
+  (void)hipStreamSynchronize(sc);
+  if (s_out) (void)hipStreamSynchronize(s_out);
+  if (dbg)
+    fprintf(stderr,
+            "[kw bulk] rows %llu chunks %llu pinned %d: layout %.2f plan %.2f prepare %.2f fill %.2f enqueue %.2f "
+            "copy-out %.2f final wait %.2f total %.2f ms\n",
+            (unsigned long long)B.n, (unsigned long long)K, pinned ? 1 : 0, t_layout, t_plan, t_prep, t_fill, t_enq, t_out,
+            since(t_w), since(t_start));
+  for (auto& e : ev)
+    if (e) (void)hipEventDestroy(e);
+  if (s_in) (void)hipStreamDestroy(s_in);
+  if (s_out) (void)hipStreamDestroy(s_out);
+  for (auto& b : bounce) host_pool().release(device, b, bounce_bytes);
+  D.cur = sc;
+  if (rc != KW_OK) D.loaded = 0;
+  return rc;
 }
 }  // namespace
 
@@ -1603,6 +1933,23 @@ int kw_batch_to_device(kw_batch* kb, int device) { return upload_batch(kb, devic
 int kw_batch_to_device_async(kw_batch* kb, int device, void* stream) {
   if (!stream) return KW_E_ARG;
   return upload_batch(kb, device, (hipStream_t)stream, false);
+}
+
+int kw_validate_host(const kw_env* env, kw_batch* b, const int32_t* policies, uint32_t npol, int origin, int device,
+                     uint32_t* out, size_t count, uint32_t chunk_rows) {
+  return validate_host(env, b, policies, npol, origin, device, out, count, chunk_rows);
+}
+
+int kw_host_alloc(int device, size_t bytes, void** out) {
+  if (!out || device < 0) return KW_E_ARG;
+  HIPCHK(hipSetDevice(device));
+  *out = nullptr;
+  HIPCHK(hipHostMalloc(out, std::max<size_t>(bytes, 1), hipHostMallocDefault));
+  return KW_OK;
+}
+
+void kw_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
 }
 
 int kw_stream_create(int device, void** stream) {

@@ -510,6 +510,13 @@ size_t emit_dfa(const Dfa& dfa, const std::vector<uint32_t>& cls_map, std::vecto
   dd.ncls = dfa.ncls;
   dd.start = dfa.start;
   dd.abs_lo = dfa.abs_lo;
+  auto feed = [&](uint32_t st, const char* s) {
+    for (; *s; ++s) st = dfa.trans[(size_t)st * dfa.ncls + dfa.cls[(uint8_t)*s]];
+    return st;
+  };
+  const uint32_t dk = feed(dfa.start, "docker.io"), dks = feed(dk, "/"), dkl = feed(dks, "library/");
+  dd.pre0 = dk | (dks << 16);
+  dd.pre1 = dkl | (feed(dfa.start, "latest") << 16);
   memcpy(dd.cls, dfa.cls.data(), 256);
   put(b, dd);
   align16(b);

@@ -22,6 +22,7 @@
 #include <mutex>
 
 #include "../../include/kwgpu.h"
+#include "imgscan.hpp"
 #include "kernels.hpp"
 
 // Build-time variants (A/B): KW_LDS_BARRIER uses LDS-only barriers between the compute phases;
@@ -38,9 +39,6 @@
 #ifndef KW_DESC_LDS  // tile kernel: staging reads the tile's descriptor from its LDS copy (else scalar loads)
 #define KW_DESC_LDS 1
 #endif
-#ifndef KW_SWAR_PARSE  // image references scanned four bytes a step (per-byte match masks)
-#define KW_SWAR_PARSE 1
-#endif
 #ifndef KW_PF_EARLY  // tile kernel: the L2 prefetch of the next tile right after staging (else after classification)
 #define KW_PF_EARLY 0
 #endif
@@ -49,6 +47,9 @@
 #endif
 #ifndef KW_MIN_WAVES  // tile kernel: minimum waves per SIMD the register allocation must allow
 #define KW_MIN_WAVES 1
+#endif
+#ifndef KW_P1_HOIST  // label items issue their value offsets and deny row before the walk and OR the constraint rows as
+#define KW_P1_HOIST 1  // classes come out; single-chunk passes store capabilities' mutation bits (not classes) in P1
 #endif
 #ifndef KW_KV_ABSORB  // label-value walks also stop at absorbing states (same-box A/B r03 v2: C4 -0.5 %, C3 -0.9 %)
 #define KW_KV_ABSORB 1
@@ -59,13 +60,12 @@
 
 namespace kw {
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 // ------------------------------------------------------------------------------------------
 // Classification (LDS or global tables; `bytes` may be LDS-staged strings or an HBM pool, both
 // padded so the dword reads below never leave their buffer)
 // ------------------------------------------------------------------------------------------
-__device__ inline uint32_t align_bytes(uint32_t hi, uint32_t lo, uint32_t sh) {
-  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * sh));
-}
 __device__ inline uint32_t lit_word(const uint32_t* base, uint32_t i, uint32_t sh, uint32_t len) {
   const uint32_t w = align_bytes(base[i + 1], base[i], sh);
   const uint32_t rem = len - 4u * i;
@@ -127,6 +127,7 @@ struct DfaView {
   const uint16_t* trans;  // [state][ncls]
   const uint16_t* acc;    // [state] global class
   uint32_t ncls, start, abs_lo;
+  uint32_t pre0, pre1;    // states after the normalisation prefixes (DevDfa)
 };
 __device__ inline DfaView chain_view(const Chain& c, uint32_t off) {
   const uint8_t* base = c.base + (off - c.head);
@@ -136,6 +137,8 @@ __device__ inline DfaView chain_view(const Chain& c, uint32_t off) {
   v.ncls = h->ncls;
   v.start = h->start;
   v.abs_lo = h->abs_lo;
+  v.pre0 = h->pre0;
+  v.pre1 = h->pre1;
   v.trans = (const uint16_t*)(base + (h->trans_off - off));
   v.acc = (const uint16_t*)(base + (h->acc_off - off));
   return v;
@@ -164,12 +167,6 @@ __device__ inline uint32_t feed(const DfaView& d, uint32_t st, const uint8_t* __
   return st;
 }
 
-// Literal fragments of image normalisation; constexpr + unrolled loops turn them into immediates.
-constexpr char kDockerIo[] = "docker.io";
-constexpr char kLibrary[] = "library/";
-constexpr char kLatest[] = "latest";
-constexpr char kLocalhost[] = "localhost";
-
 template <int N>
 __device__ inline uint32_t feed_const(const DfaView& d, uint32_t st, const char (&s)[N]) {
   if (!dfa_live(st, d.abs_lo)) return st;  // dead or absorbing: the constant cannot change it
@@ -178,118 +175,26 @@ __device__ inline uint32_t feed_const(const DfaView& d, uint32_t st, const char 
   return st;
 }
 
-template <int N>
-__device__ inline bool equals_const(const uint8_t* __restrict__ bytes, uint32_t b, uint32_t e, const char (&s)[N]) {
-  if ((int)(e - b) != N - 1) return false;
-#pragma unroll
-  for (int i = 0; i < N - 1; ++i)
-    if (bytes[b + (uint32_t)i] != (uint8_t)s[i]) return false;
-  return true;
-}
-
-// Parsed image reference (DESIGN.md §2 trusted-repos; oracle: orc_image_parts).
-struct ImageRef {
-  uint32_t b, e, at, slash0, rest_b, colon, path_end, name_end;
-  bool is_reg, path_slash, is_docker, eff_tag;
-};
-
-__device__ ImageRef parse_image(const uint8_t* __restrict__ bytes, uint32_t b, uint32_t e) {
-  const uint32_t NONE = 0xffffffffu;
-  uint32_t at = NONE, slash0 = NONE, slash1 = NONE, last_colon = NONE;
-  bool dotcolon = false;
-#if KW_SWAR_PARSE
-  // four bytes a step: per-byte match masks (bit 7 of each byte) of '@', '/', ':' and '.', exact
-  // (no borrow between bytes), restricted to the string and cut at the first '@'
-  auto eqb = [](uint32_t x, uint32_t c4) -> uint32_t {
-    const uint32_t y = x ^ c4;
-    return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y | 0x7F7F7F7Fu);
-  };
-  for (uint32_t p0 = b & ~3u; p0 < e; p0 += 4u) {
-    const uint32_t w = *(const uint32_t*)(bytes + p0);
-    const uint32_t lo = p0 < b ? b - p0 : 0u, hi = min(4u, e - p0);  // valid bytes [lo, hi)
-    const uint32_t vm = (0x80808080u << (8u * lo)) & (hi >= 4u ? 0xffffffffu : ((1u << (8u * hi)) - 1u));
-    uint32_t m_at = eqb(w, 0x40404040u) & vm, m_sl = eqb(w, 0x2f2f2f2fu) & vm;
-    uint32_t m_co = eqb(w, 0x3a3a3a3au) & vm, m_dt = eqb(w, 0x2e2e2e2eu) & vm;
-    if (m_at) {  // the digest starts here: nothing at or after the '@' counts
-      const uint32_t keep = (1u << __builtin_ctz(m_at)) - 1u;
-      at = p0 + (uint32_t)__builtin_ctz(m_at) / 8u;
-      m_sl &= keep;
-      m_co &= keep;
-      m_dt &= keep;
-    }
-    if (m_co) last_colon = p0 + (31u - (uint32_t)__builtin_clz(m_co)) / 8u;
-    if (slash0 == NONE) {
-      const uint32_t before = m_sl ? (1u << __builtin_ctz(m_sl)) - 1u : 0xffffffffu;  // bytes before the first '/'
-      if ((m_co | m_dt) & before) dotcolon = true;
-      if (m_sl) {
-        slash0 = p0 + (uint32_t)__builtin_ctz(m_sl) / 8u;
-        m_sl &= m_sl - 1u;
-      }
-    }
-    if (slash1 == NONE && m_sl) slash1 = p0 + (uint32_t)__builtin_ctz(m_sl) / 8u;
-    if (m_at) break;
-  }
-#else
-  uint32_t p = b;
-  bool stop = false;
-  while (p < e && !stop) {
-    uint32_t w = *(const uint32_t*)(bytes + (p & ~3u));
-    const uint32_t k = p & 3u;
-    const uint32_t lim = min(4u - k, e - p);
-    w >>= 8u * k;
-    for (uint32_t j = 0; j < lim; ++j) {
-      const uint32_t c = w & 0xffu;
-      w >>= 8;
-      const uint32_t q = p + j;
-      if (c == '@') {
-        at = q;
-        stop = true;
-        break;
-      }
-      if (c == '/') {
-        if (slash0 == NONE) slash0 = q;
-        else if (slash1 == NONE) slash1 = q;
-      } else if (c == ':') {
-        last_colon = q;
-        if (slash0 == NONE) dotcolon = true;
-      } else if (c == '.') {
-        if (slash0 == NONE) dotcolon = true;
-      }
-    }
-    p += lim;
-  }
-#endif
-  ImageRef r;
-  r.b = b;
-  r.e = e;
-  r.at = at;
-  r.slash0 = slash0;
-  r.name_end = at != NONE ? at : e;
-  r.is_reg = slash0 != NONE && (dotcolon || equals_const(bytes, b, slash0, kLocalhost));
-  r.rest_b = r.is_reg ? slash0 + 1 : b;
-  r.colon = (last_colon != NONE && last_colon >= r.rest_b) ? last_colon : NONE;
-  r.path_end = r.colon != NONE ? r.colon : r.name_end;
-  const uint32_t first_slash_rest = r.is_reg ? slash1 : slash0;
-  r.path_slash = first_slash_rest != NONE && first_slash_rest < r.path_end;
-  r.is_docker = !r.is_reg || equals_const(bytes, b, slash0, kDockerIo);
-  r.eff_tag = r.colon != NONE || at == NONE;
-  return r;
-}
-
 // Registry (k=0), effective tag (k=1) or normalised image (k=2) through one DFA: its class.
 __device__ uint32_t image_part(int k, const DfaView& d, const uint8_t* __restrict__ bytes, const ImageRef& r) {
   const uint32_t NONE = 0xffffffffu;
   uint32_t st = d.start;
+  // an implicit registry ("docker.io", then "/" and "library/" for a one-segment path) and the
+  // implicit tag start from the precomputed prefix states (DevDfa pre0 / pre1): no walk
   if (k == 0) {
-    st = r.is_reg ? feed(d, st, bytes, r.b, r.slash0) : feed_const(d, st, kDockerIo);
+    st = r.is_reg ? feed(d, st, bytes, r.b, r.slash0) : (d.pre0 & 0xffffu);
   } else if (k == 1) {
     if (r.colon != NONE) st = feed(d, st, bytes, r.colon + 1, r.name_end);
-    else if (r.at == NONE) st = feed_const(d, st, kLatest);
+    else if (r.at == NONE) st = d.pre1 >> 16;
     else return 0u;  // digest only: no tag
   } else {
-    st = r.is_reg ? feed(d, st, bytes, r.b, r.slash0) : feed_const(d, st, kDockerIo);
-    if (dfa_live(st, d.abs_lo)) st = step(d, st, '/');
-    if (r.is_docker && !r.path_slash) st = feed_const(d, st, kLibrary);
+    if (r.is_reg) {
+      st = feed(d, st, bytes, r.b, r.slash0);
+      if (dfa_live(st, d.abs_lo)) st = step(d, st, '/');
+      if (r.is_docker && !r.path_slash) st = feed_const(d, st, kLibrary);
+    } else {
+      st = r.path_slash ? (d.pre0 >> 16) : (d.pre1 & 0xffffu);
+    }
     st = feed(d, st, bytes, r.rest_b, r.path_end);
     if (r.eff_tag) {
       if (dfa_live(st, d.abs_lo)) st = step(d, st, ':');
@@ -310,19 +215,25 @@ struct Classifiers {
 
 // All classes of one image reference: il.nreg COL_REG entries (literal, DFAs), il.ntag COL_TAG
 // entries, il.nimg COL_IMG entries.
+// dbg (diagnostics, TileArgs::debug): 32768 skips the DFA chains, 65536 the literal lookups (class 0).
 template <bool BATCH, class Out>
 __device__ inline void classify_image(const Classifiers& C, const ImgLayout& il, const uint8_t* __restrict__ bytes,
-                                      uint32_t b, uint32_t e, Out out) {
+                                      uint32_t b, uint32_t e, Out out, uint32_t dbg = 0) {
   const uint32_t NONE = 0xffffffffu;
   const ImageRef r = parse_image(bytes, b, e);
+  const bool nodfa = (dbg & 32768u) != 0, nolit = (dbg & 65536u) != 0;
   uint32_t j = 0;
-  if (C.lit[COL_REG]) out(j++, r.is_reg ? lit_lookup<BATCH>(C.lit[COL_REG], bytes, r.b, r.slash0) : C.docker_io_cls);
-  for (uint32_t o = C.dfa[COL_REG].head; o; o = chain_next(C.dfa[COL_REG], o)) out(j++, image_part(0, chain_view(C.dfa[COL_REG], o), bytes, r));
+  if (C.lit[COL_REG])
+    out(j++, nolit ? 0u : r.is_reg ? lit_lookup<BATCH>(C.lit[COL_REG], bytes, r.b, r.slash0) : C.docker_io_cls);
+  for (uint32_t o = C.dfa[COL_REG].head; o; o = chain_next(C.dfa[COL_REG], o))
+    out(j++, nodfa ? 0u : image_part(0, chain_view(C.dfa[COL_REG], o), bytes, r));
   if (C.lit[COL_TAG])
-    out(j++, r.colon != NONE ? lit_lookup<BATCH>(C.lit[COL_TAG], bytes, r.colon + 1, r.name_end)
-                             : (r.at == NONE ? C.latest_cls : 0u));
-  for (uint32_t o = C.dfa[COL_TAG].head; o; o = chain_next(C.dfa[COL_TAG], o)) out(j++, image_part(1, chain_view(C.dfa[COL_TAG], o), bytes, r));
-  for (uint32_t o = C.dfa[COL_IMG].head; o; o = chain_next(C.dfa[COL_IMG], o)) out(j++, image_part(2, chain_view(C.dfa[COL_IMG], o), bytes, r));
+    out(j++, nolit ? 0u : r.colon != NONE ? lit_lookup<BATCH>(C.lit[COL_TAG], bytes, r.colon + 1, r.name_end)
+                                          : (r.at == NONE ? C.latest_cls : 0u));
+  for (uint32_t o = C.dfa[COL_TAG].head; o; o = chain_next(C.dfa[COL_TAG], o))
+    out(j++, nodfa ? 0u : image_part(1, chain_view(C.dfa[COL_TAG], o), bytes, r));
+  for (uint32_t o = C.dfa[COL_IMG].head; o; o = chain_next(C.dfa[COL_IMG], o))
+    out(j++, nodfa ? 0u : image_part(2, chain_view(C.dfa[COL_IMG], o), bytes, r));
 }
 
 // The region pointer carries its address space (3: LDS, 1: global), so the walk compiles to ds_read /
@@ -463,7 +374,6 @@ __device__ inline uint64_t or_range(const uint64_t* a, uint32_t lo, uint32_t hi)
 // ------------------------------------------------------------------------------------------
 // The tile kernel
 // ------------------------------------------------------------------------------------------
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 template <class T>
 __device__ inline const __attribute__((address_space(1))) T* gp(const T* p) {
   return (const __attribute__((address_space(1))) T*)p;
@@ -551,6 +461,22 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
       const uint64_t now = clock64();
       ph[k] += now - tk;
       tk = now;
+    }
+  };
+  // per-wave segment clocks (diagnostics, kPhaseWords layout in kernels.hpp): the item loops of P1
+  // and P2 are wave-uniform per iteration, so each wave charges an iteration to its segment
+  // (lane 0 adds to the workgroup's counters in HBM: returnless atomics, no registers held)
+  auto sg_add = [&](uint32_t k, uint64_t d) {
+    if (timing && lane == 0) atomicAdd((unsigned long long*)&a.phase[(uint64_t)blockIdx.x * kPhaseWords + 8u + k], (unsigned long long)d);
+  };
+  uint64_t sg_t = 0;
+  int sg_k = -1;
+  auto seg = [&](int k) {
+    if (timing) {
+      const uint64_t now = clock64();
+      if (sg_k >= 0) sg_add((uint32_t)sg_k, now - sg_t);
+      sg_t = now;
+      sg_k = __builtin_amdgcn_readfirstlane(k);
     }
   };
 
@@ -697,7 +623,9 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
     for (uint32_t i = tid; i < nr; i += kSlotThreads) l_rej[i] = l_mut[i] = 0;
     if (tid < NSTR) l_sa[tid] = d.sa[tid];
 #undef KW_DF
+    const uint64_t p0_end = timing ? clock64() : 0;
     __syncthreads();  // staged tile, the next descriptor and the counter fetch have landed
+    if (timing) sg_add(SG_P0_WAIT, clock64() - p0_end);
     mark(0);
     if (timing && tid == 0) ++ph[5];
 #if KW_LATE_ATOMIC
@@ -770,10 +698,32 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
       const uint32_t n1 = (IMG && (need & (1u << S_IMG))) ? nc : 0u;
       const uint32_t n0 = nr;
       const uint32_t ek = rup64(n3), e0 = ek + rup64(nk), e1 = e0 + rup64(n2), e2 = e1 + rup64(n1), e3 = e2 + rup64(n0);
+      const uint64_t p1_t0 = timing ? clock64() : 0;
       for (uint32_t w = tid; w < e3; w += kSlotThreads) {
+        seg(w < ek ? SG_P1_LABEL : w < e0 ? SG_P1_CAPSTR : w < e1 ? SG_P1_CTR : w < e2 ? SG_P1_IMAGE : SG_P1_REQ);
         if (LBL && w < ek) {  // label
           const uint32_t i = w;
           if (i >= n3) continue;
+#if KW_P1_HOIST
+          // the value's offsets do not depend on the key: loaded before its lookup; the key's deny
+          // row is issued before the value walk, each constraint row as its class comes out
+          uint32_t vb = 0, ve = 0;
+          if (t.o_sb[S_LV]) str(S_LV, i, &vb, &ve);
+          const uint32_t k = lit(COL_LK, S_LK, i);
+          c_lk[i] = (uint16_t)k;
+          uint16_t* lv = c_lv + i * nlv;
+          const bool lbl0 = h0.lbl != 0;
+          uint64_t vl = (lbl0 && k) ? sv0.row(T_DENY, k) : 0ull;
+          if (k && classify && t.o_sb[S_LV] && !(t.debug & 2048u)) {
+            classify_value(C, LDST && t.kv_lds, k, nlv, lds + t.o_sb[S_LV], vb, ve, [&](uint32_t j, uint32_t c) {
+              lv[j] = (uint16_t)c;
+              if (lbl0 && c != 0xffffu) vl |= sv0.row(T_FAIL, c);
+            });
+          } else {
+            for (uint32_t j = 0; j < nlv; ++j) lv[j] = 0xffffu;
+          }
+          l_vl[i] = vl;
+#else
           const uint32_t k = lit(COL_LK, S_LK, i);
           c_lk[i] = (uint16_t)k;
           uint16_t* lv = c_lv + i * nlv;
@@ -785,15 +735,18 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
             for (uint32_t j = 0; j < nlv; ++j) lv[j] = 0xffffu;
           }
           l_vl[i] = dv_label(sv0, k, lv, nlv);
+#endif
         } else if (CTR && w < e0) {  // capability string: added ones first, then dropped ones
           const uint32_t k = w - ek;
           if (k >= nk) continue;
           if (k < nka) {
             const uint32_t cc = lit(COL_CAP, S_CAPADD, k);
-            c_add[k] = (uint16_t)cc;
+            // single-chunk pass: the capability's mutation bit itself (P2 reads no class table)
+            c_add[k] = (uint16_t)((KW_P1_HOIST && t.nchunk == 1 && h0.caps) ? sv0.capmb(cc) : cc);
             l_vadd[k] = (h0.caps && h0.caps_strict) ? sv0.row(T_NACAP, cc) : 0ull;
           } else {
-            c_drop[k - nka] = (uint16_t)lit(COL_CAP, S_CAPDROP, k - nka);
+            const uint32_t dc = lit(COL_CAP, S_CAPDROP, k - nka);
+            c_drop[k - nka] = (uint16_t)((KW_P1_HOIST && t.nchunk == 1 && h0.caps) ? sv0.capmb(dc) : dc);
           }
         } else if (CTR && w < e1) {  // container (its added capabilities' sets stay in l_vadd: P2 ORs them)
           const uint32_t i = w - e0;
@@ -814,7 +767,8 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
           if (classify && (fl & KW_CTR_HAS_IMAGE)) {
             uint32_t b, e;
             str(S_IMG, i, &b, &e);
-            classify_image<true>(C, il, lds + t.o_sb[S_IMG], b, e, [&](uint32_t j, uint32_t c) { ic[j] = (uint16_t)c; });
+            classify_image<true>(C, il, lds + t.o_sb[S_IMG], b, e, [&](uint32_t j, uint32_t c) { ic[j] = (uint16_t)c; },
+                                 t.debug);
           } else {
             for (uint32_t j = 0; j < nim; ++j) ic[j] = 0;
           }
@@ -831,8 +785,12 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
           l_byp[i] = is_bypass(l_rf[i], nsc, t.bypass_cls) ? 1 : 0;
         }
       }
+      seg(-1);
+      if (timing) sg_add(SG_P1_BUSY, clock64() - p1_t0);
     }
+    const uint64_t p1_end = timing ? clock64() : 0;
     lds_barrier();
+    if (timing) sg_add(SG_P1_WAIT, clock64() - p1_end);
     mark(1);
 #if !KW_PF_EARLY
     prefetch_next();
@@ -887,7 +845,9 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
         // a container's violation set: its own families' (V_c) and its image's (V_tr)
         auto vset = [&](uint32_t j) -> uint64_t { return (CTR ? l_vc[j] : 0ull) | (trs ? l_vtr[j] : 0ull); };
         const uint32_t f0 = rup64(n1), f1 = f0 + rup64(n2), f2 = f1 + rup64(nr);
+        const uint64_t p2_t0 = timing ? clock64() : 0;
         for (uint32_t w = tid; w < f2; w += kSlotThreads) {
+          seg(w < f0 ? SG_P2_CTR : w < f1 ? SG_P2_LABEL : SG_P2_REQ);
           if (w < f0) {  // container
             const uint32_t i = w;
             if (i >= n1) continue;
@@ -945,8 +905,13 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
             }
             if (CTR && SH.caps && !(t.debug & 8192u)) {  // mutation: required drops missing, default adds neither added nor dropped
               uint64_t addm = 0, dropm = 0;
-              for (uint32_t k = ka; k < ka1; ++k) addm |= bit_of(sv.capmb(c_add[k]));
-              for (uint32_t k = l_cdrop[i] - kdb, k1 = l_cdrop[i + 1] - kdb; k < k1; ++k) dropm |= bit_of(sv.capmb(c_drop[k]));
+              if (KW_P1_HOIST && t.nchunk == 1) {  // P1 stored the mutation bits
+                for (uint32_t k = ka; k < ka1; ++k) addm |= bit_of(c_add[k]);
+                for (uint32_t k = l_cdrop[i] - kdb, k1 = l_cdrop[i + 1] - kdb; k < k1; ++k) dropm |= bit_of(c_drop[k]);
+              } else {
+                for (uint32_t k = ka; k < ka1; ++k) addm |= bit_of(sv.capmb(c_add[k]));
+                for (uint32_t k = l_cdrop[i] - kdb, k1 = l_cdrop[i + 1] - kdb; k < k1; ++k) dropm |= bit_of(sv.capmb(c_drop[k]));
+              }
               const uint64_t mut = caps_mutation(sv, addm, dropm);
               if (mut) atomicOr((unsigned long long*)&l_mut[q], (unsigned long long)mut);
             }
@@ -1029,8 +994,12 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
             if (rej) atomicOr((unsigned long long*)&l_rej[i], (unsigned long long)rej);
           }
         }
+        seg(-1);
+        if (timing) sg_add(SG_P2_BUSY, clock64() - p2_t0);
       }
+      const uint64_t p2_end = timing ? clock64() : 0;
       lds_barrier();
+      if (timing) sg_add(SG_P2_WAIT, clock64() - p2_end);
       mark(3);
 #if KW_LATE_ATOMIC
       if (dyn && tid == 0 && ck == 0) l_nx[cur] = nxt2;  // read after this tile's last barrier
@@ -1039,6 +1008,7 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
       // ---- P3: verdict words. All-pairs: items = (request, 4 columns), 16 lanes per 256-B row,
       //      column records from LDS (group / constant columns from the record's global copy).
       //      Rows mode: one word per request, its own column.
+      const uint64_t p3_t0 = timing ? clock64() : 0;
       if (!(t.debug & 4u)) {
         const ChunkArgs& CA = t.chunk[ck];
         const uint64_t init = CA.init;
@@ -1149,19 +1119,22 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
           }
         }
       }
+      if (timing) sg_add(SG_P3_BUSY, clock64() - p3_t0);
       if (ck + 1 < t.nchunk) {
         lds_barrier();  // the next chunk rewrites the violation sets and words
         mark(4);
       }
     }
+    const uint64_t p3_end = timing ? clock64() : 0;
     lds_barrier();  // the next tile restages LDS (its strings alias this tile's violation words)
+    if (timing) sg_add(SG_P3_WAIT, clock64() - p3_end);
     mark(4);
     tile = next;
     next = dyn ? t_lo + l_nx[cur] : next + gridDim.x;
   }
   if (timing && tid == 0) {  // one lane's vector stores
     ph[6] = clock64() - t_begin;
-    for (int k = 0; k < 8; ++k) a.phase[(uint64_t)blockIdx.x * 8u + (uint32_t)k] = ph[k];
+    for (int k = 0; k < 8; ++k) a.phase[(uint64_t)blockIdx.x * kPhaseWords + (uint32_t)k] = ph[k];
   }
   if (dyn && tid == 0) {  // the XCD's last workgroup (every other one has taken its last tile) resets
     uint32_t* done = a.sched + 256u + xcd * 32u;
@@ -1385,8 +1358,12 @@ constexpr std::array<const void*, sizeof...(Fs)> tile_fns() {
 const void* tile_fn(bool ldst, bool timing, uint32_t feat) {
   static const auto g = tile_fns<false, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15>();
   static const auto l = tile_fns<true, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15>();
-  if (timing)  // diagnostics: one instantiation with every family
+  if (timing) {  // diagnostics: the C2 / C3 / C4 family sets with LDS tables (same registers as the product), else every family
+    if (ldst && feat == kFeatImg) return (const void*)evaluate_tiles_kernel<true, true, kFeatImg>;
+    if (ldst && feat == (kFeatImg | kFeatGrp)) return (const void*)evaluate_tiles_kernel<true, true, kFeatImg | kFeatGrp>;
+    if (ldst && feat == (kFeatLbl | kFeatCtr)) return (const void*)evaluate_tiles_kernel<true, true, kFeatLbl | kFeatCtr>;
     return ldst ? (const void*)evaluate_tiles_kernel<true, true, kFeatAll> : (const void*)evaluate_tiles_kernel<false, true, kFeatAll>;
+  }
   return ldst ? l[feat & kFeatAll] : g[feat & kFeatAll];
 }
 uint32_t tile_feat(const TileArgs& t) { return t.feat & kFeatAll; }
@@ -1399,8 +1376,8 @@ hipError_t ensure_attrs() {
   std::call_once(g_attr_once[dev], [dev] {
     // allow > 64 KB of dynamic LDS per workgroup (gfx950: 160 KB per CU)
     hipError_t e = hipSuccess;
-    for (int k = 0; k < 34; ++k) {
-      const hipError_t ek = hipFuncSetAttribute(tile_fn(k & 1, k >= 32, (uint32_t)(k >> 1) & kFeatAll),
+    for (int k = 0; k < 64; ++k) {  // (LDS tables, timing, families)
+      const hipError_t ek = hipFuncSetAttribute(tile_fn(k & 1, (k & 2) != 0, (uint32_t)(k >> 2) & kFeatAll),
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e == hipSuccess) e = ek;
     }

@@ -41,11 +41,19 @@ struct EvalArgs {
   uint64_t* wide_groups;  // dense [row][nwide] cause masks
   uint32_t nwide;
   const uint32_t* rowcol;  // rows mode: per row (chunk << 16) | column, all-pairs: nullptr
-  // diagnostics (KW_TILE_DEBUG & 512): per workgroup, shader-clock cycles summed over its tiles
-  // [staging P0, classify P1, derive D, walk P2, verdicts P3 + next tile, tiles, whole workgroup,
-  // table staging]; nullptr = off
+  // diagnostics (KW_TILE_DEBUG & 512): per workgroup kPhaseWords u64: shader-clock cycles of thread
+  // 0 summed over its tiles [staging P0, classify P1, derive D, walk P2, verdicts P3 + next tile,
+  // tiles, whole workgroup, table staging], then the kSegWords segment clocks (Seg) summed over the
+  // workgroup's waves; nullptr = off
   uint64_t* phase;
 };
+// Per-wave segment clocks of the timing instantiation: P1 / P2 item segments (wave-uniform per
+// loop iteration), each phase's busy time and its barrier wait.
+enum Seg : uint32_t {
+  SG_P1_LABEL = 0, SG_P1_CAPSTR, SG_P1_CTR, SG_P1_IMAGE, SG_P1_REQ, SG_P2_CTR, SG_P2_LABEL, SG_P2_REQ,
+  SG_P1_BUSY, SG_P1_WAIT, SG_P2_BUSY, SG_P2_WAIT, SG_P0_WAIT, SG_P3_BUSY, SG_P3_WAIT, kSegWords = 16
+};
+constexpr uint32_t kPhaseWords = 8 + kSegWords;
 
 // Slot kernel geometry: one tile = up to 64 requests (one lane per request where a lane walks a
 // request), 256 threads.
@@ -109,7 +117,8 @@ struct TileArgs {
   uint32_t rows_mode;
   uint32_t debug;  // diagnostics: bit0 skip classification, bit1 skip walk, bit2 skip output; 512 phase
                   // clocks; 1024 skip mandatory labels, 2048 skip label-value DFAs, 4096 skip predecessor ORs,
-                  // 8192 skip capability mutations (P2), 16384 skip container / label violation words (P2)
+                  // 8192 skip capability mutations (P2), 16384 skip container / label violation words (P2),
+                  // 32768 / 65536 skip the image DFA chains / literal lookups (P1)
   uint32_t lds_bytes;
 };
 

@@ -14,7 +14,7 @@
 namespace kw {
 
 constexpr uint32_t kBlobMagic = 0x4b574733;  // "KWG3"
-constexpr uint32_t kBlobVersion = 4;
+constexpr uint32_t kBlobVersion = 5;
 
 // request columns that carry strings classified by a DFA or a literal table
 enum Col : uint32_t {
@@ -99,7 +99,10 @@ struct alignas(16) DevDfa {
   uint32_t next;                             // blob offset of the next DFA of the column chain, 0 = last
   uint32_t chain_bytes;                      // bytes of this DFA and all that follow it in the chain
   uint32_t abs_lo;                           // states [abs_lo, nstates) and 0 are absorbing (walks stop)
-  uint32_t pad[3];
+  // states after the constant prefixes of image normalisation, from `start` (an implicit registry
+  // costs no walk): pre0 = "docker.io" | "docker.io/" << 16, pre1 = "docker.io/library/" | "latest" << 16
+  uint32_t pre0, pre1;
+  uint32_t pad;
   uint8_t cls[256];
 };
 // A walk may stop at state 0 (dead) and at states >= abs_lo (absorbing): `live` is st in [1, abs_lo).

@@ -262,6 +262,32 @@ class EvaluationEnvironment:
         return json.loads(buf.value.decode())
 
 
+class PinnedWords:
+    """A page-locked uint32 host array (kw_host_alloc) for verdict buffers a caller keeps: the bulk
+    path reads verdicts back into it by direct DMA. `.array` is the numpy view; close() frees it."""
+
+    def __init__(self, count, device=0):
+        import numpy as np
+        self._L = N.lib()
+        p = C.c_void_p()
+        raise_for(self._L.kw_host_alloc(device, max(count, 1) * 4, C.byref(p)), "kw_host_alloc failed")
+        self._p = p.value
+        buf = (C.c_uint32 * max(count, 1)).from_address(self._p)
+        self.array = np.frombuffer(buf, dtype=np.uint32, count=count)
+
+    def close(self):
+        if self._p:
+            self.array = None
+            self._L.kw_host_free(C.c_void_p(self._p))
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Batch:
     """A micro-batch of requests in SoA form (kw_batch)."""
 
@@ -341,6 +367,25 @@ class Batch:
         rc = self._L.kw_batch_verdicts(self._h, out.ctypes.data_as(C.POINTER(C.c_uint32)), count)
         raise_for(rc, "kw_batch_verdicts failed")
         return out
+
+    def validate_host(self, env, policies, out=None, origin=VALIDATE, device=0, chunk_rows=0):
+        """Bulk host -> host pass (kw_validate_host): upload, evaluate and read back in overlapped row
+        chunks; returns the [row][npol] verdict words in `out` (a reused uint32 array, pinned ones from
+        PinnedWords read back by direct DMA)."""
+        import numpy as np
+        npol = len(policies)
+        count = self.n * npol
+        if out is None:
+            out = np.empty(count, dtype=np.uint32)
+        elif out.dtype != np.uint32 or not out.flags.c_contiguous or out.size < count:
+            raise ValueError("out must be a contiguous uint32 array of at least rows x policies words")
+        arr = (C.c_int32 * npol)(*[env._idx(p) for p in policies])
+        rc = self._L.kw_validate_host(env._h, self._h, arr, npol, origin, device,
+                                      out.ctypes.data_as(C.POINTER(C.c_uint32)), count, chunk_rows)
+        raise_for(rc, "kw_validate_host failed")
+        self.device = device
+        self._npol = npol
+        return out[:count]
 
     def debug_plan(self, env, policies, origin=VALIDATE):
         """Diagnostic (kw_debug_plan): the tile kernel's plan for an all-pairs pass, on the host."""

@@ -1,0 +1,114 @@
+"""Bulk host -> host path (kw_validate_host): row chunks whose upload, evaluation and read-back
+overlap on three streams must give exactly the oracle's verdict words, for pageable and pinned
+output buffers, chunk sizes down to a few tiles, and passes that fall back to the unchunked form
+(overflow requests, wide group side data). Columns the bulk upload left out are refused by a later
+pass instead of being read from unset device memory."""
+import numpy as np
+import pytest
+
+import kwgpu as K
+import oracle as O
+from helpers import config, diff_verdicts, many_policies_config
+
+pytestmark = pytest.mark.gpu
+NS = "kubewarden"
+
+
+@pytest.fixture(autouse=True)
+def _poisoned_verdicts(monkeypatch):
+    monkeypatch.setenv("KW_POISON_VERDICTS", "1")
+
+
+def _envs(doc):
+    env = K.EvaluationEnvironment(doc, continue_on_errors=True, always_accept_namespace=NS, device=0)
+    oe = O.OracleEnv(doc, continue_on_errors=True, always_accept_namespace=NS)
+    return env, oe
+
+
+@pytest.mark.parametrize("name,scfg,rows,chunk", [
+    ("c4_64", 4, 30000, 2048),     # 15 chunks of 32 tiles
+    ("c4_64", 4, 30000, 0),        # the default chunk size: one chunk
+    ("c2_trusted", 2, 50000, 777),  # chunk sizes that cut mid-tile-range (rounded to descriptors)
+    ("c3_group", 3, 20000, 4096),
+    ("parity", 0, 20000, 1500),
+])
+def test_bulk_matches_oracle(name, scfg, rows, chunk):
+    env, oe = _envs(config(name))
+    ids = env.policy_ids()
+    syn = K.SynthBatch(scfg, rows, seed=4400 + scfg)
+    ora = oe.eval(syn.soa(), ids, K.VALIDATE)
+    b = syn.batch()
+    got = b.validate_host(env, ids, chunk_rows=chunk)
+    assert np.array_equal(got, ora), diff_verdicts(got, ora, len(ids), ids)
+    # pinned output: direct DMA into the caller's buffer, same words
+    pin = K.PinnedWords(rows * len(ids))
+    try:
+        pin.array.fill(0xA5A5A5A5)
+        b2 = syn.batch()
+        got2 = b2.validate_host(env, ids, out=pin.array, chunk_rows=chunk)
+        assert np.array_equal(got2, ora), diff_verdicts(got2, ora, len(ids), ids)
+    finally:
+        pin.close()
+
+
+def test_bulk_audit_origin_and_reuse():
+    """The same batch object through the bulk path twice (the second upload replaces the first),
+    in the audit origin, then a device pass over the resident columns."""
+    env, oe = _envs(config("c4_64"))
+    ids = env.policy_ids()
+    syn = K.SynthBatch(4, 9000, seed=77)
+    b = syn.batch()
+    for origin in (K.VALIDATE, K.AUDIT):
+        got = b.validate_host(env, ids, origin=origin, chunk_rows=1024)
+        ora = oe.eval(syn.soa(), ids, origin)
+        assert np.array_equal(got, ora), diff_verdicts(got, ora, len(ids), ids)
+    b.validate(env, ids)  # the C4 columns are resident: an ordinary pass may reuse them
+    assert np.array_equal(b.verdicts(), oe.eval(syn.soa(), ids, K.VALIDATE))
+
+
+def test_bulk_upload_refuses_missing_columns():
+    """kw_validate_host uploads only the string columns its pass reads: a later pass on the same
+    device batch that needs image references fails loudly (KW_E_ARG) until the batch is uploaded
+    again."""
+    env4, _ = _envs(config("c4_64"))
+    env2, oe2 = _envs(config("c2_trusted"))
+    syn = K.SynthBatch(4, 3000, seed=5)
+    b = syn.batch()
+    b.validate_host(env4, env4.policy_ids())
+    with pytest.raises(K.EvaluationError):
+        b.validate(env2, env2.policy_ids())
+    b.to_device(0)
+    b.validate(env2, env2.policy_ids())
+    ids = env2.policy_ids()
+    assert np.array_equal(b.verdicts(), oe2.eval(syn.soa(), ids, K.VALIDATE))
+
+
+def test_bulk_unchunked_forms_match_oracle():
+    """Passes the chunked schedule does not take run unchunked through the same call: C6's 40-member
+    group (wide side data) and a batch with requests beyond the tile capacities (overflow kernels)."""
+    env, oe = _envs(many_policies_config())
+    ids = env.policy_ids()
+    syn = K.SynthBatch(6, 3000, seed=6)
+    got = syn.batch().validate_host(env, ids, chunk_rows=512)
+    ora = oe.eval(syn.soa(), ids, K.VALIDATE)
+    assert np.array_equal(got, ora), diff_verdicts(got, ora, len(ids), ids)
+
+    env5, oe5 = _envs(config("c5_mixed"))
+    ids5 = env5.policy_ids()
+    syn5 = K.SynthBatch(5, 4000, seed=55)
+    got5 = syn5.batch().validate_host(env5, ids5, chunk_rows=256)
+    ora5 = oe5.eval(syn5.soa(), ids5, K.VALIDATE)
+    assert np.array_equal(got5, ora5), diff_verdicts(got5, ora5, len(ids5), ids5)
+
+
+@pytest.mark.parametrize("q", ["0.5", "0.05"])
+def test_bulk_split_and_overflow_tiles(monkeypatch, q):
+    """Capacities forced low (KW_TILE_QUANTILE): halved request runs inside chunks (chunk bounds fall
+    between split descriptors) and, at 0.05, single requests on the overflow kernels (unchunked)."""
+    monkeypatch.setenv("KW_TILE_QUANTILE", q)
+    env, oe = _envs(config("c4_64"))
+    ids = env.policy_ids()
+    syn = K.SynthBatch(4, 6000, seed=4804)
+    got = syn.batch().validate_host(env, ids, chunk_rows=640)
+    ora = oe.eval(syn.soa(), ids, K.VALIDATE)
+    assert np.array_equal(got, ora), diff_verdicts(got, ora, len(ids), ids)
