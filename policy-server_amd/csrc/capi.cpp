@@ -104,66 +104,74 @@ void parallel_copy(void* dst, const void* src, size_t bytes) {
 
 // Persistent host workers for the bulk path (kw_validate_host): a parallel-for over many short
 // tasks (copy segments, tile ranges) without starting threads per call. The caller runs tasks too.
+// Each call is a Job on the caller's stack; a worker joins it under the lock (users + 1) and the
+// caller returns only when every task is done and every worker that joined has left, so no worker
+// ever sees another call's counters or a finished call's function.
 class HostWorkers {
  public:
   static HostWorkers& get() {
     static HostWorkers* w = new HostWorkers();  // process lifetime (workers park on a condition)
     return *w;
   }
-  unsigned size() const { return (unsigned)th_.size() + 1; }
   // fn(i) for every i in [0, n), spread over the workers and the caller; returns when all are done
   void run(size_t n, const std::function<void(size_t)>& fn) {
     if (n == 0) return;
     std::lock_guard<std::mutex> one(run_m_);  // one parallel-for at a time
+    Job job;
+    job.fn = &fn;
+    job.n = n;
     {
       std::lock_guard<std::mutex> g(m_);
-      fn_ = &fn;
-      next_.store(0);
-      n_.store(n);
-      done_ = 0;
+      job_ = &job;
       ++gen_;
     }
     cv_.notify_all();
-    const size_t mine = work();
+    const size_t mine = job.work();
     std::unique_lock<std::mutex> g(m_);
-    done_ += mine;
-    done_cv_.wait(g, [&] { return done_ == n_; });
-    fn_ = nullptr;
+    job_ = nullptr;  // no worker joins after this
+    job.done += mine;
+    done_cv_.wait(g, [&] { return job.done == job.n && job.users == 0; });
   }
 
  private:
+  struct Job {
+    const std::function<void(size_t)>* fn = nullptr;
+    size_t n = 0;
+    std::atomic<size_t> next{0};
+    size_t done = 0;     // tasks finished (under m_)
+    unsigned users = 0;  // workers inside work() (under m_)
+    size_t work() {
+      size_t k = 0;
+      for (size_t i; (i = next.fetch_add(1)) < n; ++k) (*fn)(i);
+      return k;
+    }
+  };
   HostWorkers() {
     const char* e = getenv("KW_HOST_THREADS");
     unsigned n = e ? (unsigned)std::max(1, atoi(e)) : std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-    for (unsigned i = 1; i < n; ++i) th_.emplace_back([this] { loop(); });
-    for (auto& t : th_) t.detach();
-  }
-  size_t work() {
-    size_t k = 0;
-    for (size_t i; (i = next_.fetch_add(1)) < n_; ++k) (*fn_)(i);
-    return k;
+    for (unsigned i = 1; i < n; ++i) std::thread([this] { loop(); }).detach();
   }
   void loop() {
     uint64_t seen = 0;
     for (;;) {
+      Job* j = nullptr;
       {
         std::unique_lock<std::mutex> g(m_);
-        cv_.wait(g, [&] { return gen_ != seen && fn_ != nullptr; });
+        cv_.wait(g, [&] { return gen_ != seen && job_ != nullptr; });
         seen = gen_;
+        j = job_;
+        ++j->users;
       }
-      const size_t mine = work();
+      const size_t mine = j->work();
       std::lock_guard<std::mutex> g(m_);
-      done_ += mine;
-      if (done_ == n_) done_cv_.notify_all();
+      j->done += mine;
+      --j->users;
+      if (j->done == j->n && j->users == 0) done_cv_.notify_all();
     }
   }
-  std::vector<std::thread> th_;
   std::mutex m_, run_m_;
   std::condition_variable cv_, done_cv_;
-  const std::function<void(size_t)>* fn_ = nullptr;
-  std::atomic<size_t> n_{0};
-  size_t done_ = 0;
-  std::atomic<size_t> next_{0};
+  Job* job_ = nullptr;
   uint64_t gen_ = 0;
 };
 

@@ -193,3 +193,32 @@ def test_planner_tile_height():
         assert small["rows"] == 64, (name, small)
         big = K.SynthBatch(scfg, 600_000, seed=1).batch().debug_plan(env, env.policy_ids())
         assert big["rows"] == 128 and big["lds_bytes"] <= 160 * 1024 // 4, (name, big)
+
+
+def test_planner_host_workers_back_to_back():
+    """The planner's host parallel-fors (tile needs, capacity quantiles, descriptors) run back to back
+    with different task counts (small and large batches alternating, from two Python threads) and
+    always return the same plan: a parallel-for never runs another call's tasks (r03: a worker late
+    for one call could take an index of the next, past its task count, and hang it)."""
+    import threading
+    c4 = K.EvaluationEnvironment(config("c4_64"))
+    ids = c4.policy_ids()
+    sizes = (300_000, 90, 70_000, 1)
+    mine = [[K.SynthBatch(4, n, seed=3).batch() for n in sizes] for _ in range(2)]  # a batch per thread
+    want = [b.debug_plan(c4, ids) for b in mine[0]]
+    errors = []
+
+    def hammer(k):
+        try:
+            for it in range(60):
+                j = (it + k) % len(sizes)
+                assert mine[k][j].debug_plan(c4, ids) == want[j]
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errors.append(e)
+    th = [threading.Thread(target=hammer, args=(k,)) for k in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th), "planner parallel-for hung"
+    assert not errors, errors
