@@ -880,8 +880,19 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
     fprintf(stderr, "[kw tile] lds_tables=%u rows=%u cmax=%u kmax=%u lmax=%u lds=%u area=%u (classifiers %u) chunks=%zu launches=%zu nim=%u nlv=%u\n",
             T.lds_tables, T.rows, T.cmax, T.kmax, T.lmax, T.lds_bytes, area, table_bytes, plan->chunks.size(), plan->launches.size(), nim,
             nlv);
-  if (T.debug & 256u)
+  if (T.debug & 256u) {
     for (size_t k = 0; k < stages.size(); ++k) fprintf(stderr, "[kw tile]   classifier stage %zu: %u bytes\n", k, stages[k].bytes);
+    // the tile's LDS regions (bytes): per-request state, entity classes and sets, the strings / violation-words union
+    uint32_t so = 0, sb = 0;
+    for (int m = 0; m < (int)NSTR; ++m)
+      if (T.o_sb[m]) so += T.o_sb[m] - T.o_so[m], sb += T.sb_cap[m] + 48;
+    fprintf(stderr,
+            "[kw tile]   layout: headers %u | classes ns %u aa %u img %u caps %u lk %u lv %u | sets vadd %u vl %u vc %u vtr %u | "
+            "owners %u | rej/mut/byp %u | union at %u: string offsets %u + bytes %u, violation words %u | total %u\n",
+            T.o_ns - T.o_rf, T.o_aa - T.o_ns, T.o_img - T.o_aa, T.o_capadd - T.o_img, T.o_lk - T.o_capadd, T.o_lv - T.o_lk,
+            T.o_vadd - T.o_lv, T.o_vl - T.o_vadd, T.o_vc - T.o_vl, T.o_vtr - T.o_vc, T.o_own_c - T.o_vtr, T.o_rej - T.o_own_c,
+            T.o_sa - T.o_rej, T.o_vw, so, sb, T.rows * T.vw_stride * 4, T.lds_bytes);
+  }
 
   // ---- per-launch TileArgs (record pointers filled in at upload, run_pass)
   plan->slot_blob.clear();
