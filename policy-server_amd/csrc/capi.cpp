@@ -742,7 +742,7 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
   // over per-dimension quantiles of the tile needs; at a given occupancy the largest capacities
   // (fewest split tiles). Chosen once per batch, tile height and layout signature.
   const uint64_t key = ((uint64_t)area << 40) ^ ((uint64_t)nslots << 20) ^ ((uint64_t)nim << 12) ^ ((uint64_t)nlv << 8) ^ need;
-  D.rows_plans.reserve(4);  // at most 64, 128, 96 (or the forced height): references stay valid
+  D.rows_plans.reserve(8);  // at most 64 and the five taller candidates (or the forced height): references stay valid
   auto plan_rows = [&](uint32_t r) -> DeviceBatch::RowsPlan& {
     DeviceBatch::RowsPlan* R = nullptr;
     for (auto& x : D.rows_plans)
@@ -786,26 +786,46 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
     }
     return *R;
   };
-  // Tile height: KW_SLOT_ROWS when forced; else kSlotRows, or 128 / 96 rows when the batch has at
-  // least 4 tiles per workgroup slot and the taller layout still keeps 4 workgroups per CU (its LDS
-  // estimated from the 64-row layout first: the per-request part scales with the height). Taller
-  // tiles amortise the per-tile latency (staging, barriers) where the per-request LDS is small:
-  // C2 -12 %, C3 -25 %; the C4-C6 layouts need 64 rows for 4 workgroups per CU (r02 sweeps).
+  // Tile height: KW_SLOT_ROWS when forced; else kSlotRows, or a taller tile (128 down to 96 rows)
+  // when the batch has at least 4 tiles per workgroup slot, the taller layout still keeps 4
+  // workgroups per CU (its LDS estimated from the 64-row layout first: the per-request part scales
+  // with the height), and at most KW_ROUND_SPLIT (2 %) of its tiles hold more items in one P1
+  // segment (labels, capability strings, containers / images) than the workgroup has lanes: such a
+  // tile sends one wave through the segment twice, and its phase waits for that wave (r03: half of
+  // C2 / C3's 128-row tiles had more than 256 images). Taller tiles amortise the per-tile latency
+  // (staging, barriers) where the per-request LDS is small: C2 -12 %, C3 -25 % at 128 rows (r02);
+  // the C4-C6 layouts need 64 rows for 4 workgroups per CU (r02 sweeps).
   const DeviceBatch::RowsPlan* pick = nullptr;
+  const double round_split = getenv("KW_ROUND_SPLIT") ? atof(getenv("KW_ROUND_SPLIT")) : 0.02;  // A/B knob
+  auto two_rounds = [&](const DeviceBatch::RowsPlan& R) {  // share of tiles with a segment beyond one round
+    uint64_t over = 0;
+    for (const TileStats& x : R.need) {
+      uint32_t seg = 0;
+      if (any_lbl) seg = std::max(seg, x.lbl);
+      if (any_caps) seg = std::max(seg, x.kadd + x.kdrop);
+      if (any_ctr || (need & (1u << S_IMG))) seg = std::max(seg, x.ctr);
+      over += seg > kSlotThreads;
+    }
+    return R.need.empty() ? 0.0 : (double)over / (double)R.need.size();
+  };
   if (const uint32_t f = slot_rows_forced()) {
     pick = &plan_rows(f);
   } else {
     const DeviceBatch::RowsPlan& base = plan_rows(kSlotRows);
     pick = &base;
     const uint32_t fixed = 16 + align(area), per64 = base.cap_lds > fixed ? base.cap_lds - fixed : 0u;
-    for (uint32_t r : {128u, 96u}) {
+    for (uint32_t r : {128u, 120u, 112u, 104u, 96u}) {
       const uint64_t est = fixed + (uint64_t)per64 * r / kSlotRows;
       if (getenv("KW_TILE_DEBUG") && (atoi(getenv("KW_TILE_DEBUG")) & 256))
         fprintf(stderr, "[kw tile] rows=%u estimated lds=%llu (64-row layout %u, fixed %u) batch rows %llu\n", r,
                 (unsigned long long)est, base.cap_lds, fixed, (unsigned long long)B.n);
       if (per_cu((uint32_t)std::min<uint64_t>(est, 1u << 30)) < 4 || B.n < (uint64_t)r * 4 * 256 * 4) continue;
       const DeviceBatch::RowsPlan& R = plan_rows(r);
-      if (R.cap_cu >= 4) {
+      const double tr = two_rounds(R);
+      if (getenv("KW_TILE_DEBUG") && (atoi(getenv("KW_TILE_DEBUG")) & 256))
+        fprintf(stderr, "[kw tile] rows=%u workgroups/CU %u, tiles with a segment beyond %u items %.4f\n", r, R.cap_cu,
+                kSlotThreads, tr);
+      if (R.cap_cu >= 4 && tr <= round_split) {
         pick = &R;
         break;
       }
