@@ -49,7 +49,10 @@
 #define KW_MIN_WAVES 1
 #endif
 #ifndef KW_P1_HOIST  // label items issue their value offsets and deny row before the walk and OR the constraint rows as
-#define KW_P1_HOIST 1  // classes come out; single-chunk passes store capabilities' mutation bits (not classes) in P1
+#define KW_P1_HOIST 0  // classes come out; single-chunk passes store capabilities' mutation bits (not classes) in P1
+#endif
+#ifndef KW_LK_PACK  // TileArgs::lk_pack launches: label-key classes carry the key's mandatory local bit
+#define KW_LK_PACK 0   // (r03 A/B: C4 +0.5 %, C5 +1 %, C6 -0.8 %: off)
 #endif
 #ifndef KW_KV_ABSORB  // label-value walks also stop at absorbing states (same-box A/B r03 v2: C4 -0.5 %, C3 -0.9 %)
 #define KW_KV_ABSORB 1
@@ -710,7 +713,7 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
           uint32_t vb = 0, ve = 0;
           if (t.o_sb[S_LV]) str(S_LV, i, &vb, &ve);
           const uint32_t k = lit(COL_LK, S_LK, i);
-          c_lk[i] = (uint16_t)k;
+          c_lk[i] = (uint16_t)(KW_LK_PACK && t.lk_pack ? k | ((h0.lbl && h0.mand_union ? sv0.lkmb(k) : 0xffu) << 8) : k);
           uint16_t* lv = c_lv + i * nlv;
           const bool lbl0 = h0.lbl != 0;
           uint64_t vl = (lbl0 && k) ? sv0.row(T_DENY, k) : 0ull;
@@ -725,7 +728,7 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
           l_vl[i] = vl;
 #else
           const uint32_t k = lit(COL_LK, S_LK, i);
-          c_lk[i] = (uint16_t)k;
+          c_lk[i] = (uint16_t)(KW_LK_PACK && t.lk_pack ? k | ((h0.lbl && h0.mand_union ? sv0.lkmb(k) : 0xffu) << 8) : k);
           uint16_t* lv = c_lv + i * nlv;
           if (k && classify && t.o_sb[S_LV] && !(t.debug & 2048u)) {
             uint32_t b, e;
@@ -926,7 +929,7 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
             for (uint32_t j = l0; j < i; ++j) pre |= l_vl[j];
             const uint64_t nv = v & ~pre;
             if (!nv || (t.debug & 16384u)) continue;
-            const uint64_t den = sv.row(T_DENY, c_lk[i]);
+            const uint64_t den = sv.row(T_DENY, KW_LK_PACK && t.lk_pack ? c_lk[i] & 0xffu : c_lk[i]);
             const uint32_t li = i - l0;
             ViolSink vs{l_vw + q * t.vw_stride, nullptr};
             vs.put(nv & den, KW_R_LABEL_DENIED, li);
@@ -945,9 +948,29 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
             }
             if (LBL && SH.lbl && SH.mand_union && !(t.debug & 1024u)) {
               uint64_t present = 0, lrej = 0;
-              for (uint32_t l = l_loff[i] - lb, l1 = l_loff[i + 1] - lb; l < l1; ++l) {
-                present |= bit_of(sv.lkmb(c_lk[l]));
-                lrej |= l_vl[l];
+              if (KW_LK_PACK && t.lk_pack) {  // the keys' mandatory bits stored by P1, four labels a round
+                const uint32_t l0 = l_loff[i] - lb, l1 = l_loff[i + 1] - lb;
+                for (uint32_t l = l0; l < l1; l += 4u) {
+                  uint32_t kk[4];
+                  uint64_t vv[4];
+#pragma unroll
+                  for (int u = 0; u < 4; ++u) {
+                    const uint32_t x = l + (uint32_t)u < l1 ? l + (uint32_t)u : l0;
+                    kk[u] = c_lk[x];
+                    vv[u] = l_vl[x];
+                  }
+#pragma unroll
+                  for (int u = 0; u < 4; ++u)
+                    if (l + (uint32_t)u < l1) {
+                      present |= bit_of(kk[u] >> 8);
+                      lrej |= vv[u];
+                    }
+                }
+              } else {
+                for (uint32_t l = l_loff[i] - lb, l1 = l_loff[i + 1] - lb; l < l1; ++l) {
+                  present |= bit_of(sv.lkmb(c_lk[l]));
+                  lrej |= l_vl[l];
+                }
               }
 #if KW_MAND_BATCH
               // slots missing a mandatory key: rows of the missing local bits, four loads per round

@@ -237,13 +237,25 @@ struct ViolSink {
     }
     return;
 #endif
+#ifndef KW_PUT2  // two slots a loop trip (the second repeats the first when the half runs out: idempotent)
+#define KW_PUT2 1
+#endif
     for (uint32_t h = 0; h < 2; ++h) {
       uint32_t m = (uint32_t)(nw >> (32u * h));
       while (m) {
         const uint32_t s = 32u * h + (uint32_t)__builtin_ctz(m);
-        vw[s] = w;
-        if (va) va[s] = arg;
         m &= m - 1u;
+        uint32_t s2 = s;
+        if (KW_PUT2 && m) {
+          s2 = 32u * h + (uint32_t)__builtin_ctz(m);
+          m &= m - 1u;
+        }
+        vw[s] = w;
+        vw[s2] = w;
+        if (va) {
+          va[s] = arg;
+          va[s2] = arg;
+        }
       }
     }
   }
