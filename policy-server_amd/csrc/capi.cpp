@@ -992,6 +992,8 @@ int upload_tile_descs(const Batch& B, DeviceBatch* D, const TileArgs& T, hipStre
     mix(T.sb_cap[m]);
   }
   if (D->desc && key == D->desc_key) return KW_OK;
+  static const bool dbg = getenv("KW_BULK_DEBUG") && atoi(getenv("KW_BULK_DEBUG")) != 0;  // diagnostics
+  const auto t0 = std::chrono::steady_clock::now();
   const uint64_t ntiles = (B.n + T.rows - 1) / T.rows;
   std::vector<TileDesc> desc;
   desc.reserve(ntiles + ntiles / 64 + 1);
@@ -1060,6 +1062,7 @@ int upload_tile_descs(const Batch& B, DeviceBatch* D, const TileArgs& T, hipStre
     ovf.insert(ovf.end(), qovf[q].begin(), qovf[q].end());
   }
   ovf[0] = (uint32_t)(ovf.size() - 1);
+  const auto t1 = std::chrono::steady_clock::now();
   HIPCHK(hipStreamSynchronize(s));  // a running pass may still read the previous descriptors
   D->h_desc = std::move(desc);
   D->h_ovf = std::move(ovf);
@@ -1071,6 +1074,10 @@ int upload_tile_descs(const Batch& B, DeviceBatch* D, const TileArgs& T, hipStre
   HIPCHK(hipMemcpyAsync(D->overflow, D->h_ovf.data(), D->h_ovf.size() * sizeof(uint32_t), hipMemcpyHostToDevice, s));
   D->n_overflow = D->h_ovf[0];
   D->desc_key = key;
+  if (dbg)
+    fprintf(stderr, "[kw descs] %zu descriptors: build %.2f ms, sync + upload %.2f ms\n", D->h_desc.size(),
+            std::chrono::duration<double, std::milli>(t1 - t0).count(),
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
   return KW_OK;
 }
 
@@ -1885,7 +1892,8 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
     return kw_batch_verdicts(kb, out, count);
   }
   D.loaded = need;
-  const uint64_t per = chunk_rows ? chunk_rows : 131072;
+  static const uint64_t def_chunk = getenv("KW_BULK_CHUNK") ? std::max(1, atoi(getenv("KW_BULK_CHUNK"))) : 131072;  // A/B knob
+  const uint64_t per = chunk_rows ? chunk_rows : def_chunk;
   const uint64_t K = std::max<uint64_t>(1, std::min<uint64_t>({(B.n + per - 1) / per, D.ndesc, 256}));
   std::vector<uint64_t> db(K + 1), rb(K + 1);  // chunk k: descriptors [db[k], db[k+1]), rows [rb[k], rb[k+1])
   for (uint64_t k = 0; k <= K; ++k) {

@@ -23,7 +23,7 @@ if [[ $STEPS == *bench* ]]; then
 fi
 if [[ $STEPS == *prof* ]]; then
   cd /tmp && export TMPDIR=/tmp
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/${TAG}_prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --no-cpu-baseline > "$GRAFT_REPO_ROOT/gpurun_out/${TAG}_prof.log" 2>&1
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/${TAG}_prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --no-cpu-baseline --no-host-modes > "$GRAFT_REPO_ROOT/gpurun_out/${TAG}_prof.log" 2>&1
   stop_on_fault $? prof
   cd "$GRAFT_REPO_ROOT"
 fi
