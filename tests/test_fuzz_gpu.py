@@ -1,6 +1,8 @@
 """GPU: random policy sets (tests/fuzz.py) through the HIP path — all-pairs verdict words equal the
 oracle's bit-exact in both origins, and row mode (one random policy per row, the serving path)
 equals the all-pairs words it selects."""
+import os
+
 import numpy as np
 import pytest
 
@@ -13,7 +15,8 @@ pytestmark = pytest.mark.gpu
 NS = "kubewarden"
 
 
-@pytest.mark.parametrize("seed", range(100, 108))
+# KW_FUZZ_SEEDS widens the sweep for a deep run (profiles/r03_fuzz_deep.log: 200 seeds)
+@pytest.mark.parametrize("seed", range(100, 100 + int(os.environ.get("KW_FUZZ_SEEDS", "8"))))
 def test_random_policy_sets_on_gpu(seed):
     doc = random_policies(seed)
     env = K.EvaluationEnvironment(doc, continue_on_errors=True, always_accept_namespace=NS, device=0)
@@ -34,6 +37,9 @@ def test_random_policy_sets_on_gpu(seed):
     rows = b.verdicts(count=syn.n)
     full = want.reshape(syn.n, len(ids))
     assert np.array_equal(rows, full[np.arange(syn.n), pick])
+    # the bulk host -> host path on a fresh copy of the rows, in chunks of a few tiles
+    bulk = syn.batch().validate_host(env, ids, origin=K.AUDIT, chunk_rows=448)
+    assert np.array_equal(bulk, want), diff_verdicts(bulk, want, len(ids), ids)
 
 
 @pytest.mark.parametrize("raw", [False, True])
