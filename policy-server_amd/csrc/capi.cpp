@@ -1894,12 +1894,21 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
   D.loaded = need;
   static const uint64_t def_chunk = getenv("KW_BULK_CHUNK") ? std::max(1, atoi(getenv("KW_BULK_CHUNK"))) : 131072;  // A/B knob
   const uint64_t per = chunk_rows ? chunk_rows : def_chunk;
-  const uint64_t K = std::max<uint64_t>(1, std::min<uint64_t>({(B.n + per - 1) / per, D.ndesc, 256}));
-  std::vector<uint64_t> db(K + 1), rb(K + 1);  // chunk k: descriptors [db[k], db[k+1]), rows [rb[k], rb[k+1])
-  for (uint64_t k = 0; k <= K; ++k) {
-    db[k] = D.ndesc * k / K;
-    rb[k] = k == K ? B.n : (k == 0 ? 0 : ((uint64_t)D.h_desc[db[k]].r0hi << 32 | D.h_desc[db[k]].r0lo));
+  // chunk k: descriptors [db[k], db[k+1]), rows [rb[k], rb[k+1]). The read-back stream is the
+  // longest (4 B x npol per request out vs the request's columns in), so the first chunks are small
+  // (1/16 of `per`, doubling) to start it early; then `per` rows a chunk, at most 256 chunks.
+  static const bool ramp = !(getenv("KW_BULK_RAMP") && atoi(getenv("KW_BULK_RAMP")) == 0);  // A/B knob
+  const uint64_t dper = std::max<uint64_t>(1, per / std::max<uint32_t>(1, plan.geom.rows));
+  std::vector<uint64_t> db{0};
+  for (uint64_t step = ramp ? std::max<uint64_t>(1, dper / 16) : dper; db.back() < D.ndesc;) {
+    const uint64_t left = D.ndesc - db.back();
+    db.push_back(db.back() + (db.size() >= 256 ? left : std::min(step, left)));
+    step = std::min(dper, step * 2);
   }
+  const uint64_t K = db.size() - 1;
+  std::vector<uint64_t> rb(K + 1);
+  for (uint64_t k = 0; k <= K; ++k)
+    rb[k] = k == K ? B.n : (k == 0 ? 0 : ((uint64_t)D.h_desc[db[k]].r0hi << 32 | D.h_desc[db[k]].r0lo));
   hipPointerAttribute_t attr;
   const bool pinned = hipPointerGetAttributes(&attr, out) == hipSuccess && attr.type == hipMemoryTypeHost;
   (void)hipGetLastError();  // a pageable pointer leaves an error state behind
