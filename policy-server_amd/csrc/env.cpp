@@ -652,7 +652,9 @@ Status compile_kv(Env* env, DevHeader* hdr, std::vector<uint8_t>* b) {
         for (int c = 128; c < 256; ++c) uniform_hi = uniform_hi && d.cls[c] == d.cls[128];
         kv.wide = uniform_hi ? 0 : 1;
         kv.hi = d.cls[128];
-        std::vector<uint8_t> cm(d.cls.begin(), d.cls.begin() + (kv.wide ? 256 : 128));
+        // narrow maps carry the class of every byte >= 128 as entry 128, so a class load indexes
+        // min(byte, 128) (kernels.hip classify_value_as) instead of selecting `hi` per byte
+        std::vector<uint8_t> cm(d.cls.begin(), d.cls.begin() + (kv.wide ? 256 : 129));
         auto it = cls_pool.find(cm);
         if (it == cls_pool.end()) {
           const size_t o = at16(cm.size());

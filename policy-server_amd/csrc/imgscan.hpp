@@ -6,10 +6,18 @@
 
 #include "kwdev.hpp"  // KW_HD
 
+#ifndef KW_ALIGNBIT  // device align_bytes as v_alignbit_b32
+#define KW_ALIGNBIT 1
+#endif
+
 namespace kw {
 
 KW_HD inline uint32_t align_bytes(uint32_t hi, uint32_t lo, uint32_t sh) {
+#if defined(__HIP_DEVICE_COMPILE__) && KW_ALIGNBIT
+  return __builtin_amdgcn_alignbit(hi, lo, 8u * sh);  // one v_alignbit_b32 (sh < 4), not a 64-bit shift
+#else
   return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * sh));
+#endif
 }
 KW_HD inline uint32_t img_min(uint32_t a, uint32_t b) { return a < b ? a : b; }
 

@@ -60,6 +60,12 @@
 #ifndef KW_LATE_ATOMIC  // tile kernel: the counter fetch for the tile after next issued after the staging barrier (r03 v2: neutral, off)
 #define KW_LATE_ATOMIC 0
 #endif
+#ifndef KW_MAD24  // DFA transitions addressed with a 24-bit multiply-add (trans_at)
+#define KW_MAD24 1
+#endif
+#ifndef KW_CLS129  // label-value class loads index min(byte, 128) of the 129-entry narrow maps
+#define KW_CLS129 1
+#endif
 
 namespace kw {
 
@@ -89,11 +95,13 @@ __device__ inline uint32_t lit_lookup(const uint8_t* rec, const uint8_t* bytes, 
     uint32_t raw[N + 1];
 #pragma unroll
     for (int i = 0; i < N + 1; ++i) raw[i] = base[i];
+    // only the last word (nw - 1) is partial: one tail mask (len % 4 == 0: shift 0, all bytes);
+    // words past it are neither hashed nor compared
+    const uint32_t last = nw - 1u, tm = 0xffffffffu >> ((32u - 8u * (len & 3u)) & 31u);
 #pragma unroll
     for (int i = 0; i < N; ++i) {
       const uint32_t x = align_bytes(raw[i + 1], raw[i], sh);
-      const uint32_t rem = len - 4u * (uint32_t)i;
-      w[i] = rem >= 4u ? x : (x & ((1u << (8u * rem)) - 1u));
+      w[i] = (uint32_t)i < last ? x : (x & tm);
       if ((uint32_t)i < nw) h = lit_mix(h, w[i]);
     }
     for (uint32_t i = N; i < nw; ++i) h = lit_mix(h, lit_word(base, i, sh, len));
@@ -148,24 +156,37 @@ __device__ inline DfaView chain_view(const Chain& c, uint32_t off) {
 }
 __device__ inline uint32_t chain_next(const Chain& c, uint32_t off) { return ((const DevDfa*)(c.base + (off - c.head)))->next; }
 
-__device__ inline uint32_t step(const DfaView& d, uint32_t st, uint32_t byte) { return d.trans[st * d.ncls + d.cls[byte]]; }
+// Byte offset of transition (st, class) in a [state][ncls] table of 2^sh-byte entries, with the class
+// pre-shifted (cq = class << sh): one 24-bit multiply-add on the transition chain (states and class
+// counts are < 65536, DevDfa / KvDfa), instead of a quarter-rate 32-bit multiply plus shifts.
+#if KW_MAD24
+__device__ inline uint32_t trans_at(uint32_t st, uint32_t ncls_sh, uint32_t cq) { return (uint32_t)__umul24(st, ncls_sh) + cq; }
+#else
+__device__ inline uint32_t trans_at(uint32_t st, uint32_t ncls_sh, uint32_t cq) { return st * ncls_sh + cq; }
+#endif
+__device__ inline uint32_t tr16(const uint16_t* trans, uint32_t at) { return *(const uint16_t*)((const uint8_t*)trans + at); }
+
+__device__ inline uint32_t step(const DfaView& d, uint32_t st, uint32_t byte) {
+  return tr16(d.trans, trans_at(st, d.ncls << 1, (uint32_t)d.cls[byte] << 1));
+}
 
 // Walk bytes [b, e) in 8-byte windows: the window's dwords, then its 8 byte classes load as batches;
 // only the transitions form a dependent chain (aligned dword reads up to 11 bytes past the window
 // start: pools and staged strings carry a zero tail). A walk ends at the first window that starts
 // in the dead state or an absorbing one (kwdev.hpp dfa_live).
 __device__ inline uint32_t feed(const DfaView& d, uint32_t st, const uint8_t* __restrict__ bytes, uint32_t b, uint32_t e) {
+  const uint32_t nc2 = d.ncls << 1;
   for (uint32_t p = b; p < e && dfa_live(st, d.abs_lo); p += 8u) {
     const uint32_t* q = (const uint32_t*)(bytes + (p & ~3u));
     const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], sh = p & 3u;
     const uint32_t x0 = align_bytes(q1, q0, sh), x1 = align_bytes(q2, q1, sh);
     uint32_t c[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) c[i] = d.cls[((i < 4 ? x0 : x1) >> (8 * (i & 3))) & 0xffu];
+    for (int i = 0; i < 8; ++i) c[i] = (uint32_t)d.cls[((i < 4 ? x0 : x1) >> (8 * (i & 3))) & 0xffu] << 1;
     const uint32_t lim = min(8u, e - p);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
-      if ((uint32_t)i < lim) st = d.trans[st * d.ncls + c[i]];
+      if ((uint32_t)i < lim) st = tr16(d.trans, trans_at(st, nc2, c[i]));
   }
   return st;
 }
@@ -278,27 +299,38 @@ __device__ inline uint32_t classify_value_as(as_ptr<AS> R, uint32_t nlk, uint32_
         // LDS region: branch-free (every class load and step of the window runs; `fin` keeps the
         // state after the lane's last byte; a step no lane of the wave needs ends the window). The
         // global-table form below keeps its masked steps: extra lanes' gathers cost L2 bandwidth.
+        // Classes come out as LDS byte addresses of their column in the transition table (tb +
+        // class << t16), so a step is one 24-bit multiply-add and the load (trans_at).
+        const uint32_t t16 = d.t16, tb = (uint32_t)(uintptr_t)(R + d.trans_off), ncs = (uint32_t)d.ncls << t16;
+#if KW_CLS129
+        const uint32_t bm = 128u + (uint32_t)d.wide * 127u;  // narrow maps: entry 128 is the class of bytes >= 128 (wide: 0 / 1)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const uint32_t by = ((i < 4 ? x0 : x1) >> (8 * (i & 3))) & 0xffu;
+          c[i] = tb + ((uint32_t)R[d.cls_off + min(by, bm)] << t16);
+        }
+#else
         const uint32_t bm = d.wide ? 255u : 127u;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const uint32_t by = ((i < 4 ? x0 : x1) >> (8 * (i & 3))) & 0xffu;
           const uint32_t cl = R[d.cls_off + (by & bm)];
-          c[i] = by <= bm ? cl : (uint32_t)d.hi;
+          c[i] = tb + ((by <= bm ? cl : (uint32_t)d.hi) << t16);
         }
+#endif
         uint32_t fin = st;
-        if (d.t16) {
-          const u16p tr = (u16p)(R + d.trans_off);
+        if (t16) {
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             if (i > 0 && !__any((uint32_t)i < lim)) break;
-            st = tr[st * d.ncls + c[i]];
+            st = *(u16p)(uintptr_t)trans_at(st, ncs, c[i]);
             fin = (uint32_t)i < lim ? st : fin;
           }
         } else {
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             if (i > 0 && !__any((uint32_t)i < lim)) break;
-            st = R[d.trans_off + st * d.ncls + c[i]];
+            st = *(as_ptr<AS>)(uintptr_t)trans_at(st, ncs, c[i]);
             fin = (uint32_t)i < lim ? st : fin;
           }
         }
@@ -308,17 +340,22 @@ __device__ inline uint32_t classify_value_as(as_ptr<AS> R, uint32_t nlk, uint32_
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const uint32_t by = ((i < 4 ? x0 : x1) >> (8 * (i & 3))) & 0xffu;
+#if KW_CLS129
+        c[i] = R[d.cls_off + min(by, 128u + (uint32_t)d.wide * 127u)];
+#else
         c[i] = (by < 128u || d.wide) ? R[d.cls_off + by] : d.hi;
+#endif
       }
+      const as_ptr<AS> tr = R + d.trans_off;
       if (d.t16) {
-        const u16p tr = (u16p)(R + d.trans_off);
+        const uint32_t nc2 = (uint32_t)d.ncls << 1;
 #pragma unroll
         for (int i = 0; i < 8; ++i)
-          if ((uint32_t)i < lim) st = tr[st * d.ncls + c[i]];
+          if ((uint32_t)i < lim) st = *(u16p)(tr + trans_at(st, nc2, c[i] << 1));
       } else {
 #pragma unroll
         for (int i = 0; i < 8; ++i)
-          if ((uint32_t)i < lim) st = R[d.trans_off + st * d.ncls + c[i]];
+          if ((uint32_t)i < lim) st = tr[trans_at(st, d.ncls, c[i])];
       }
     }
     out(j++, kbase + d.cbase + ((u16p)(R + d.acc_off))[st]);

@@ -14,7 +14,7 @@
 namespace kw {
 
 constexpr uint32_t kBlobMagic = 0x4b574733;  // "KWG3"
-constexpr uint32_t kBlobVersion = 5;
+constexpr uint32_t kBlobVersion = 6;
 
 // request columns that carry strings classified by a DFA or a literal table
 enum Col : uint32_t {
@@ -66,6 +66,9 @@ constexpr int kMaxLocalBits = 64;     // per chunk: distinct mandatory label key
 #else
 #define KW_HD
 #endif
+#ifndef KW_MIX_LSHL  // device literal hash: h * 5 as v_lshl_add_u32 (lit_mix); r03 A/B: C3 -0.5 %,
+#define KW_MIX_LSHL 0   // C4 +0.9 / +1.4 % (the asm's hazard padding and VGPR constraint): off
+#endif
 
 // Compact DFA of the per-key label-value region (offsets region-relative). A label value is only
 // ever tested against the regexes constrained on its own key, so each constrained key has a chain
@@ -73,7 +76,7 @@ constexpr int kMaxLocalBits = 64;     // per chunk: distinct mandatory label key
 // global COL_LV class is kbase[key] + cbase + acc[state] (kbase: the region's per-key table), so a
 // chain shared by keys with the same regexes still gives each key its own classes.
 struct alignas(16) KvDfa {
-  uint32_t cls_off;    // u8 byte class of bytes [0, 128) (all 256 when wide)
+  uint32_t cls_off;    // u8 byte class of bytes [0, 128) and entry 128 = hi (all 256 when wide)
   uint32_t trans_off;  // [nstates][ncls]: u8 (t16 = 0) or u16 (t16 = 1) next state
   uint32_t acc_off;    // u16 [nstates]: local accept class
   uint32_t next;       // next KvDfa of the key's chain, 0 = last
@@ -132,7 +135,15 @@ inline KW_HD uint32_t lit_init(uint32_t seed, uint32_t len) { return seed ^ (len
 inline KW_HD uint32_t lit_mix(uint32_t h, uint32_t w) {
   h ^= w;
   h = (h << 13) | (h >> 19);
+#if defined(__HIP_DEVICE_COMPILE__) && KW_MIX_LSHL
+  // h * 5 as one full-rate shift-add: left to itself the compiler folds the multiply and the add
+  // into v_mad_u64_u32, a quarter-rate op on the literal probe's dependent chain
+  uint32_t r;
+  asm("v_lshl_add_u32 %0, %1, 2, %1" : "=v"(r) : "v"(h));
+  return r + 0xE6546B64u;
+#else
   return h * 5u + 0xE6546B64u;
+#endif
 }
 inline KW_HD uint32_t lit_final(uint32_t h) {
   h ^= h >> 16;
