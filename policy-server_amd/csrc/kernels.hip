@@ -63,6 +63,9 @@
 #ifndef KW_MAD24  // DFA transitions addressed with a 24-bit multiply-add (trans_at)
 #define KW_MAD24 1
 #endif
+#ifndef KW_IMG_LDSADDR  // image DFAs staged in LDS: classes pre-offset to LDS addresses (one multiply-add a step)
+#define KW_IMG_LDSADDR 1
+#endif
 #ifndef KW_CLS129  // label-value class loads index min(byte, 128) of the 129-entry narrow maps
 #define KW_CLS129 1
 #endif
@@ -164,67 +167,86 @@ __device__ inline uint32_t trans_at(uint32_t st, uint32_t ncls_sh, uint32_t cq) 
 #else
 __device__ inline uint32_t trans_at(uint32_t st, uint32_t ncls_sh, uint32_t cq) { return st * ncls_sh + cq; }
 #endif
-__device__ inline uint32_t tr16(const uint16_t* trans, uint32_t at) { return *(const uint16_t*)((const uint8_t*)trans + at); }
+// u16 transition at `at`: a byte offset from the table (global or generic tables), or, for tables
+// staged in LDS (L), the entry's LDS address itself (tr_base folded into the pre-shifted classes)
+template <bool L>
+__device__ inline uint32_t tr16(const uint16_t* trans, uint32_t at) {
+  if constexpr (L) return *(const __attribute__((address_space(3))) uint16_t*)(uintptr_t)at;
+  return *(const uint16_t*)((const uint8_t*)trans + at);
+}
+template <bool L>
+__device__ inline uint32_t tr_base(const uint16_t* trans) {
+  return L ? (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint16_t*)trans : 0u;
+}
 
+template <bool L>
 __device__ inline uint32_t step(const DfaView& d, uint32_t st, uint32_t byte) {
-  return tr16(d.trans, trans_at(st, d.ncls << 1, (uint32_t)d.cls[byte] << 1));
+  return tr16<L>(d.trans, trans_at(st, d.ncls << 1, tr_base<L>(d.trans) + ((uint32_t)d.cls[byte] << 1)));
 }
 
 // Walk bytes [b, e) in 8-byte windows: the window's dwords, then its 8 byte classes load as batches;
 // only the transitions form a dependent chain (aligned dword reads up to 11 bytes past the window
 // start: pools and staged strings carry a zero tail). A walk ends at the first window that starts
 // in the dead state or an absorbing one (kwdev.hpp dfa_live).
+template <bool L>
 __device__ inline uint32_t feed(const DfaView& d, uint32_t st, const uint8_t* __restrict__ bytes, uint32_t b, uint32_t e) {
-  const uint32_t nc2 = d.ncls << 1;
+  const uint32_t nc2 = d.ncls << 1, tb = tr_base<L>(d.trans);
   for (uint32_t p = b; p < e && dfa_live(st, d.abs_lo); p += 8u) {
     const uint32_t* q = (const uint32_t*)(bytes + (p & ~3u));
     const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], sh = p & 3u;
     const uint32_t x0 = align_bytes(q1, q0, sh), x1 = align_bytes(q2, q1, sh);
     uint32_t c[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) c[i] = (uint32_t)d.cls[((i < 4 ? x0 : x1) >> (8 * (i & 3))) & 0xffu] << 1;
+    for (int i = 0; i < 8; ++i) c[i] = tb + ((uint32_t)d.cls[((i < 4 ? x0 : x1) >> (8 * (i & 3))) & 0xffu] << 1);
+    // materialised here, after all eight loads and ahead of the masked steps: otherwise the
+    // compiler sinks the shift and base add into each step (three VALU on the chain, not one)
+    if constexpr (L) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) asm volatile("" : "+v"(c[i]));
+    }
     const uint32_t lim = min(8u, e - p);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
-      if ((uint32_t)i < lim) st = tr16(d.trans, trans_at(st, nc2, c[i]));
+      if ((uint32_t)i < lim) st = tr16<L>(d.trans, trans_at(st, nc2, c[i]));
   }
   return st;
 }
 
-template <int N>
+template <bool L, int N>
 __device__ inline uint32_t feed_const(const DfaView& d, uint32_t st, const char (&s)[N]) {
   if (!dfa_live(st, d.abs_lo)) return st;  // dead or absorbing: the constant cannot change it
 #pragma unroll
-  for (int i = 0; i < N - 1; ++i) st = step(d, st, (uint8_t)s[i]);  // state 0 is absorbing
+  for (int i = 0; i < N - 1; ++i) st = step<L>(d, st, (uint8_t)s[i]);  // state 0 is absorbing
   return st;
 }
 
 // Registry (k=0), effective tag (k=1) or normalised image (k=2) through one DFA: its class.
+template <bool L>
 __device__ uint32_t image_part(int k, const DfaView& d, const uint8_t* __restrict__ bytes, const ImageRef& r) {
   const uint32_t NONE = 0xffffffffu;
   uint32_t st = d.start;
   // an implicit registry ("docker.io", then "/" and "library/" for a one-segment path) and the
   // implicit tag start from the precomputed prefix states (DevDfa pre0 / pre1): no walk
   if (k == 0) {
-    st = r.is_reg ? feed(d, st, bytes, r.b, r.slash0) : (d.pre0 & 0xffffu);
+    st = r.is_reg ? feed<L>(d, st, bytes, r.b, r.slash0) : (d.pre0 & 0xffffu);
   } else if (k == 1) {
-    if (r.colon != NONE) st = feed(d, st, bytes, r.colon + 1, r.name_end);
+    if (r.colon != NONE) st = feed<L>(d, st, bytes, r.colon + 1, r.name_end);
     else if (r.at == NONE) st = d.pre1 >> 16;
     else return 0u;  // digest only: no tag
   } else {
     if (r.is_reg) {
-      st = feed(d, st, bytes, r.b, r.slash0);
-      if (dfa_live(st, d.abs_lo)) st = step(d, st, '/');
-      if (r.is_docker && !r.path_slash) st = feed_const(d, st, kLibrary);
+      st = feed<L>(d, st, bytes, r.b, r.slash0);
+      if (dfa_live(st, d.abs_lo)) st = step<L>(d, st, '/');
+      if (r.is_docker && !r.path_slash) st = feed_const<L>(d, st, kLibrary);
     } else {
       st = r.path_slash ? (d.pre0 >> 16) : (d.pre1 & 0xffffu);
     }
-    st = feed(d, st, bytes, r.rest_b, r.path_end);
+    st = feed<L>(d, st, bytes, r.rest_b, r.path_end);
     if (r.eff_tag) {
-      if (dfa_live(st, d.abs_lo)) st = step(d, st, ':');
-      st = r.colon != NONE ? feed(d, st, bytes, r.colon + 1, r.name_end) : feed_const(d, st, kLatest);
+      if (dfa_live(st, d.abs_lo)) st = step<L>(d, st, ':');
+      st = r.colon != NONE ? feed<L>(d, st, bytes, r.colon + 1, r.name_end) : feed_const<L>(d, st, kLatest);
     }
-    if (r.at != NONE) st = feed(d, st, bytes, r.at, r.e);
+    if (r.at != NONE) st = feed<L>(d, st, bytes, r.at, r.e);
   }
   return d.acc[st];
 }
@@ -240,7 +262,7 @@ struct Classifiers {
 // All classes of one image reference: il.nreg COL_REG entries (literal, DFAs), il.ntag COL_TAG
 // entries, il.nimg COL_IMG entries.
 // dbg (diagnostics, TileArgs::debug): 32768 skips the DFA chains, 65536 the literal lookups (class 0).
-template <bool BATCH, class Out>
+template <bool BATCH, bool L, class Out>
 __device__ inline void classify_image(const Classifiers& C, const ImgLayout& il, const uint8_t* __restrict__ bytes,
                                       uint32_t b, uint32_t e, Out out, uint32_t dbg = 0) {
   const uint32_t NONE = 0xffffffffu;
@@ -250,14 +272,14 @@ __device__ inline void classify_image(const Classifiers& C, const ImgLayout& il,
   if (C.lit[COL_REG])
     out(j++, nolit ? 0u : r.is_reg ? lit_lookup<BATCH>(C.lit[COL_REG], bytes, r.b, r.slash0) : C.docker_io_cls);
   for (uint32_t o = C.dfa[COL_REG].head; o; o = chain_next(C.dfa[COL_REG], o))
-    out(j++, nodfa ? 0u : image_part(0, chain_view(C.dfa[COL_REG], o), bytes, r));
+    out(j++, nodfa ? 0u : image_part<L>(0, chain_view(C.dfa[COL_REG], o), bytes, r));
   if (C.lit[COL_TAG])
     out(j++, nolit ? 0u : r.colon != NONE ? lit_lookup<BATCH>(C.lit[COL_TAG], bytes, r.colon + 1, r.name_end)
                                           : (r.at == NONE ? C.latest_cls : 0u));
   for (uint32_t o = C.dfa[COL_TAG].head; o; o = chain_next(C.dfa[COL_TAG], o))
-    out(j++, nodfa ? 0u : image_part(1, chain_view(C.dfa[COL_TAG], o), bytes, r));
+    out(j++, nodfa ? 0u : image_part<L>(1, chain_view(C.dfa[COL_TAG], o), bytes, r));
   for (uint32_t o = C.dfa[COL_IMG].head; o; o = chain_next(C.dfa[COL_IMG], o))
-    out(j++, nodfa ? 0u : image_part(2, chain_view(C.dfa[COL_IMG], o), bytes, r));
+    out(j++, nodfa ? 0u : image_part<L>(2, chain_view(C.dfa[COL_IMG], o), bytes, r));
 }
 
 // The region pointer carries its address space (3: LDS, 1: global), so the walk compiles to ds_read /
@@ -807,7 +829,7 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
           if (classify && (fl & KW_CTR_HAS_IMAGE)) {
             uint32_t b, e;
             str(S_IMG, i, &b, &e);
-            classify_image<true>(C, il, lds + t.o_sb[S_IMG], b, e, [&](uint32_t j, uint32_t c) { ic[j] = (uint16_t)c; },
+            classify_image<true, LDST && KW_IMG_LDSADDR>(C, il, lds + t.o_sb[S_IMG], b, e, [&](uint32_t j, uint32_t c) { ic[j] = (uint16_t)c; },
                                  t.debug);
           } else {
             for (uint32_t j = 0; j < nim; ++j) ic[j] = 0;
@@ -1256,7 +1278,7 @@ __global__ void __launch_bounds__(kOverflowThreads)
       if (t.need & (1u << S_IMG)) {
         uint16_t* ic = a.g_img + (uint64_t)c * nim;
         if (fl & KW_CTR_HAS_IMAGE)
-          classify_image<false>(C, il, t.s_bytes[S_IMG], t.s_off[S_IMG][c], t.s_off[S_IMG][c + 1],
+          classify_image<false, false>(C, il, t.s_bytes[S_IMG], t.s_off[S_IMG][c], t.s_off[S_IMG][c + 1],
                                 [&](uint32_t j, uint32_t cl) { ic[j] = (uint16_t)cl; });
         else
           for (uint32_t j = 0; j < nim; ++j) ic[j] = 0;
