@@ -66,6 +66,9 @@
 #ifndef KW_IMG_LDSADDR  // image DFAs staged in LDS: classes pre-offset to LDS addresses (one multiply-add a step)
 #define KW_IMG_LDSADDR 1
 #endif
+#ifndef KW_P3_BITS  // P3 verdict words from 32-bit halves and bit-selects (no 64-bit shifts or branches)
+#define KW_P3_BITS 1
+#endif
 #ifndef KW_CLS129  // label-value class loads index min(byte, 128) of the 129-entry narrow maps
 #define KW_CLS129 1
 #endif
@@ -1159,6 +1162,52 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
             const Cols4 c4 = load4(g);
             uint32_t* dst = out + (r0 + (tid >> lg)) * npol + CA.col0 + 4 * g;
             const uint64_t dstep = (uint64_t)step * npol;
+#if KW_P3_BITS
+            // (not in image-only instantiations: two more VGPRs there cross C2's 6-wave boundary, +8 %)
+            if (!GRP && (LBL || CTR)) {
+              // branch-free words from 32-bit halves: per column, the slot's rejected / mutated bits
+              // as 0 / -1 masks (v_bfe_i32 of the half holding the slot), then two bit-selects
+              // (v_bitop3_b32 0xCA: S0 ? S1 : S2). A constant column keeps okw: its rejected field
+              // has width 0 (mask 0) and its mutated word is okw.
+              const uint32_t ks[4] = {c4.ks.x, c4.ks.y, c4.ks.z, c4.ks.w};
+              const uint32_t okc[4] = {c4.ok.x, c4.ok.y, c4.ok.z, c4.ok.w};
+              const uint32_t muc[4] = {c4.mu.x, c4.mu.y, c4.mu.z, c4.mu.w};
+              const uint32_t rjc[4] = {c4.rj.x, c4.rj.y, c4.rj.z, c4.rj.w};
+              uint32_t cs[4], bs[4], wd[4], muw[4];
+              bool hi[4];
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                const bool pl = (ks[k] & 0xffu) == CK_PLAIN;
+                cs[k] = (ks[k] >> 8) & 63u;
+                bs[k] = cs[k] & 31u;
+                hi[k] = cs[k] >= 32u;
+                wd[k] = pl ? 1u : 0u;
+                muw[k] = pl ? muc[k] : okc[k];
+              }
+              for (uint32_t rr = tid >> lg; rr < nr; rr += step, dst += dstep) {
+                const uint2 rj = *(const uint2*)&l_rej[rr], mu = *(const uint2*)&l_mut[rr];
+                const uint32_t byp = l_byp[rr];
+                const uint32_t* vw = l_vw + rr * t.vw_stride;
+                uint32_t av[4], wk[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) av[k] = vw[cs[k]];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                  const uint32_t rb = (uint32_t)__builtin_amdgcn_sbfe((int)(hi[k] ? rj.y : rj.x), bs[k], wd[k]);
+                  const uint32_t mb = (uint32_t)__builtin_amdgcn_sbfe((int)(hi[k] ? mu.y : mu.x), bs[k], 1u);
+                  const uint32_t tw = __builtin_amdgcn_bitop3_b32(mb, muw[k], okc[k], 0xCA);
+                  wk[k] = __builtin_amdgcn_bitop3_b32(rb, rjc[k] | av[k], tw, 0xCA);
+                }
+                u32x4 wv = {wk[0], wk[1], wk[2], wk[3]};
+                if (byp) wv = u32x4{kBypassWord, kBypassWord, kBypassWord, kBypassWord};
+#if KW_NT_STORE
+                __builtin_nontemporal_store(wv, (u32x4*)dst);  // streamed once
+#else
+                *(u32x4*)dst = wv;
+#endif
+              }
+            } else
+#endif
             if (!GRP) {
               // branch-free words: the thread's four columns are loop-invariant; every row reads its
               // four violation words whether or not the slot rejected, then selects
