@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <functional>
 #include <map>
 #include <memory>
@@ -114,8 +115,14 @@ class HostWorkers {
     return *w;
   }
   // fn(i) for every i in [0, n), spread over the workers and the caller; returns when all are done
+  // A single task runs inline on the caller: no lock, no wake-up (kwhost's small micro-batches plan
+  // one tile range per pass, and its pipeline workers must not serialise on run_m_ for that).
   void run(size_t n, const std::function<void(size_t)>& fn) {
     if (n == 0) return;
+    if (n == 1) {
+      fn(0);
+      return;
+    }
     std::lock_guard<std::mutex> one(run_m_);  // one parallel-for at a time
     Job job;
     job.fn = &fn;
@@ -284,7 +291,7 @@ struct DeviceBatch {
     uint32_t cap_cu = 0;   // its workgroups per CU
     uint32_t cap_lds = 0;  // its LDS bytes
   };
-  std::vector<RowsPlan> rows_plans;
+  std::deque<RowsPlan> rows_plans;  // deque: plan_rows hands out references that must survive later insertions
   ~DeviceBatch() {
     if (device < 0) return;  // host-only view (kw_debug_plan)
     (void)hipSetDevice(device);
@@ -468,14 +475,19 @@ std::vector<TileStats> tile_quantiles(const std::vector<TileStats>& need, const 
     else if (d == 3) x.kdrop = v;
     else x.bytes[d - 4] = v;
   };
-  HostWorkers::get().run(kDims, [&](size_t di) {
+  auto one_dim = [&](size_t di) {
     const int d = (int)di;
     std::vector<uint32_t> v(n);
     for (uint64_t t = 0; t < n; ++t) v[t] = dim(need[t], d);
     std::nth_element(v.begin(), v.begin() + (long)qmin, v.end());
     std::sort(v.begin() + (long)qmin, v.end());
     for (size_t k = 0; k < qi.size(); ++k) put(out[k], d, v[qi[k]]);
-  });
+  };
+  if (n < 8192) {  // a small batch (kwhost's micro-batches): inline, no worker wake-up
+    for (int d = 0; d < kDims; ++d) one_dim((size_t)d);
+  } else {
+    HostWorkers::get().run(kDims, one_dim);
+  }
   return out;
 }
 
@@ -742,7 +754,6 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
   // over per-dimension quantiles of the tile needs; at a given occupancy the largest capacities
   // (fewest split tiles). Chosen once per batch, tile height and layout signature.
   const uint64_t key = ((uint64_t)area << 40) ^ ((uint64_t)nslots << 20) ^ ((uint64_t)nim << 12) ^ ((uint64_t)nlv << 8) ^ need;
-  D.rows_plans.reserve(8);  // at most 64 and the five taller candidates (or the forced height): references stay valid
   auto plan_rows = [&](uint32_t r) -> DeviceBatch::RowsPlan& {
     DeviceBatch::RowsPlan* R = nullptr;
     for (auto& x : D.rows_plans)

@@ -264,28 +264,29 @@ class EvaluationEnvironment:
 
 class PinnedWords:
     """A page-locked uint32 host array (kw_host_alloc) for verdict buffers a caller keeps: the bulk
-    path reads verdicts back into it by direct DMA. `.array` is the numpy view; close() frees it."""
+    path reads verdicts back into it by direct DMA. `.array` is the numpy view.
+
+    The allocation lives exactly as long as the ctypes buffer the view wraps (a weakref.finalize on
+    it calls kw_host_free): any view or slice of `.array` keeps it alive, whether or not this
+    wrapper still exists. close() only drops the wrapper's own reference."""
 
     def __init__(self, count, device=0):
         import numpy as np
-        self._L = N.lib()
+        import weakref
+        L = N.lib()
         p = C.c_void_p()
-        raise_for(self._L.kw_host_alloc(device, max(count, 1) * 4, C.byref(p)), "kw_host_alloc failed")
-        self._p = p.value
-        buf = (C.c_uint32 * max(count, 1)).from_address(self._p)
+        raise_for(L.kw_host_alloc(device, max(count, 1) * 4, C.byref(p)), "kw_host_alloc failed")
+        buf = (C.c_uint32 * max(count, 1)).from_address(p.value)
+        self._free = weakref.finalize(buf, L.kw_host_free, C.c_void_p(p.value))
         self.array = np.frombuffer(buf, dtype=np.uint32, count=count)
 
-    def close(self):
-        if self._p:
-            self.array = None
-            self._L.kw_host_free(C.c_void_p(self._p))
-            self._p = None
+    @property
+    def alive(self):
+        """True while the page-locked allocation exists (some view still references it)."""
+        return self._free.alive
 
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
+    def close(self):
+        self.array = None
 
 
 class Batch:

@@ -94,8 +94,12 @@ def gather_verdicts(source, bounds, npol, dist, rank, world, tensor_device="cpu"
     kw_batch_verdicts' pinned bounce, or a host uint32 array, `chunk_words` at a time) straight
     into its own disjoint slice of one shared file mapping, so no rank holds a second copy and no
     verdict word crosses RCCL or any other collective: two broadcast int64s (the file's token and
-    directory) and one barrier. Returns the (rows, npol) array on rank 0 (pages of the unlinked
-    file) and None elsewhere. Raises RuntimeError when no file system has room for the words."""
+    directory), one all-reduce that proves every rank mapped the same file, and one barrier.
+    The file is unlinked as soon as every rank has it mapped, so a rank that fails later leaves
+    nothing behind in tmpfs. When the ranks do not share one host (a rank could not open the file,
+    or opened a different one) the words travel by point-to-point sends to rank 0 instead
+    (`_gather_p2p`). Returns the (rows, npol) array on rank 0 and None elsewhere. Raises
+    RuntimeError when no file system on rank 0's host has room for the words."""
     import os
 
     import torch
@@ -103,25 +107,49 @@ def gather_verdicts(source, bounds, npol, dist, rank, world, tensor_device="cpu"
     total_words = int(bounds[world] - bounds[0]) * npol
     a = int(bounds[rank] - bounds[0]) * npol
     n = int(bounds[rank + 1] - bounds[rank]) * npol
-    tok = [0, -1]
-    if rank == 0:  # rank 0 names, places and sizes the file (sparse until the ranks write)
-        tok = [(os.getpid() << 24) | int.from_bytes(os.urandom(3), "little"), _gather_dir(total_words * 4)]
-        if tok[1] >= 0:
-            name = os.path.join(_gather_dirs()[tok[1]], f"kwgpu_verdicts_{tok[0]}.u32")
-            with open(name, "wb") as f:
-                f.truncate(max(total_words, 1) * 4)
-    t = torch.tensor(tok, dtype=torch.int64, device=tensor_device)
-    dist.broadcast(t, 0)
-    tok = [int(x) for x in t.cpu().tolist()]
-    if tok[1] < 0:
-        raise RuntimeError(f"no file system has room for {total_words * 4 / 1e9:.1f} GB of verdict words")
-    name = os.path.join(_gather_dirs()[tok[1]], f"kwgpu_verdicts_{tok[0]}.u32")
-    mm = np.memmap(name, dtype=np.uint32, mode="r+", shape=(max(total_words, 1),))
-    mine = mm[a:a + n]
+    src = None
     if isinstance(source, np.ndarray):
         src = np.asarray(source, dtype=np.uint32).reshape(-1)
         if src.size != n:
             raise ValueError(f"rank {rank}: {src.size} verdict words, shard holds {n}")
+    tok = [0, -1]
+    name = None
+    try:
+        if rank == 0:  # rank 0 names, places and sizes the file (sparse until the ranks write)
+            tok = [(os.getpid() << 24) | int.from_bytes(os.urandom(3), "little"), _gather_dir(total_words * 4)]
+            if tok[1] >= 0:
+                name = os.path.join(_gather_dirs()[tok[1]], f"kwgpu_verdicts_{tok[0]}.u32")
+                with open(name, "wb") as f:
+                    f.truncate(max(total_words, 1) * 4)
+        t = torch.tensor(tok, dtype=torch.int64, device=tensor_device)
+        dist.broadcast(t, 0)
+        tok = [int(x) for x in t.cpu().tolist()]
+        if tok[1] < 0:
+            raise RuntimeError(f"no file system has room for {total_words * 4 / 1e9:.1f} GB of verdict words")
+        path = os.path.join(_gather_dirs()[tok[1]], f"kwgpu_verdicts_{tok[0]}.u32")
+        # every rank must map rank 0's file: same (st_dev, st_ino) everywhere, or nobody uses it
+        mm, ident = None, [-1, -1]
+        try:
+            mm = np.memmap(path, dtype=np.uint32, mode="r+", shape=(max(total_words, 1),))
+            st = os.stat(path)
+            ident = [int(st.st_dev), int(st.st_ino)]
+        except (OSError, ValueError):
+            mm = None
+        rd = torch.tensor([ident[0], ident[1], -ident[0], -ident[1]], dtype=torch.int64, device=tensor_device)
+        dist.all_reduce(rd, op=dist.ReduceOp.MAX)  # max == -max(-x) == min: all equal iff max(x) == min(x)
+        lo_hi = [int(x) for x in rd.cpu().tolist()]
+        shared = lo_hi[0] >= 0 and lo_hi[0] == -lo_hi[2] and lo_hi[1] == -lo_hi[3]
+        if rank == 0 and name is not None:
+            os.unlink(name)  # every rank holds its mapping (or gave up on it): the name is no longer needed
+            name = None
+    finally:
+        if rank == 0 and name is not None:
+            os.unlink(name)
+    if not shared:
+        del mm
+        return _gather_p2p(source, src, n, bounds, npol, dist, rank, world, tensor_device, chunk_words)
+    mine = mm[a:a + n]
+    if src is not None:
         for c in range(0, n, chunk_words):
             mine[c:c + chunk_words] = src[c:c + chunk_words]
     elif n:
@@ -132,6 +160,34 @@ def gather_verdicts(source, bounds, npol, dist, rank, world, tensor_device="cpu"
     if rank != 0:
         del mm
         return None
-    os.unlink(name)  # the mapping outlives the name
     out = mm[:total_words]
+    return out.reshape(-1, npol) if npol else out
+
+
+def _gather_p2p(source, src, n, bounds, npol, dist, rank, world, tensor_device, chunk_words):
+    """gather_verdicts across hosts: every rank k > 0 sends its shard to rank 0 in `chunk_words`
+    pieces (point-to-point, in rank order); rank 0 assembles the whole array in its own memory."""
+    import torch
+
+    if src is None:
+        src = np.empty(n, dtype=np.uint32)
+        if n:
+            source.verdicts(count=n, out=src)
+    if rank != 0:
+        for c in range(0, n, chunk_words):
+            piece = torch.from_numpy(src[c:c + chunk_words].view(np.int32).copy()).to(tensor_device)
+            dist.send(piece, 0)
+        return None
+    total_words = int(bounds[world] - bounds[0]) * npol
+    out = np.empty(max(total_words, 1), dtype=np.uint32)
+    out[:n] = src
+    for k in range(1, world):
+        a = int(bounds[k] - bounds[0]) * npol
+        nk = int(bounds[k + 1] - bounds[k]) * npol
+        for c in range(0, nk, chunk_words):
+            m = min(chunk_words, nk - c)
+            piece = torch.empty(m, dtype=torch.int32, device=tensor_device)
+            dist.recv(piece, k)
+            out[a + c:a + c + m] = piece.cpu().numpy().view(np.uint32)
+    out = out[:total_words]
     return out.reshape(-1, npol) if npol else out

@@ -51,6 +51,31 @@ def test_bulk_matches_oracle(name, scfg, rows, chunk):
         pin.close()
 
 
+def test_pinned_words_outlive_their_wrapper():
+    """the page-locked memory lives as long as any view of it, not as long as the
+    PinnedWords wrapper. Drop the wrapper, keep only a slice, DMA into the array again."""
+    import gc
+    env, oe = _envs(config("c4_64"))
+    ids = env.policy_ids()
+    syn = K.SynthBatch(4, 3000, seed=91)
+    ora = oe.eval(syn.soa(), ids, K.VALIDATE)
+    pin = K.PinnedWords(3000 * len(ids))
+    arr, fin = pin.array, pin._free
+    del pin
+    gc.collect()
+    assert fin.alive  # `arr` still references the buffer
+    arr.fill(0xA5A5A5A5)
+    got = syn.batch().validate_host(env, ids, out=arr, chunk_rows=1024)
+    tail = got[len(got) // 2:]
+    del arr, got
+    gc.collect()
+    assert fin.alive  # the slice alone keeps it
+    assert np.array_equal(tail, ora[len(ora) // 2:])
+    del tail
+    gc.collect()
+    assert not fin.alive  # freed with the last view
+
+
 def test_bulk_audit_origin_and_reuse():
     """The same batch object through the bulk path twice (the second upload replaces the first),
     in the audit origin, then a device pass over the resident columns."""

@@ -35,7 +35,7 @@ def _strings(col, n):
     return [bytes(col.bytes[col.off[i]:col.off[i + 1]]) for i in range(n)]
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, split=False):
     import sys
 
     for p in (os.path.join(ROOT, "policy-server_amd"), os.path.join(ROOT, "tests")):
@@ -43,7 +43,13 @@ def _worker(rank, world, port, out_dir):
     import torch.distributed as dist
 
     import kwgpu as K
+    import kwgpu.dist as D
     from kwgpu.dist import broadcast_environment, gather_verdicts, synth_bounds
+
+    if split and rank > 0:  # this rank "lives on another host": rank 0's file is not in its directories
+        own = os.path.join(out_dir, f"host{rank}")
+        os.makedirs(own, exist_ok=True)
+        D._gather_dirs = lambda: (own, own)
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
@@ -75,9 +81,13 @@ def _worker(rank, world, port, out_dir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_blob_broadcast_shards_and_gathered_verdicts(tmp_path, world):
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+@pytest.mark.parametrize("world,split", [(2, False), (3, False), (3, True)])
+def test_blob_broadcast_shards_and_gathered_verdicts(tmp_path, world, split):
+    """split: ranks 1.. cannot see rank 0's gather file (as on another host), so gather_verdicts
+    must detect it and fall back to point-to-point sends, with the same result."""
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), split), nprocs=world, join=True)
+    if split:
+        assert not [f for r in range(1, world) for f in os.listdir(tmp_path / f"host{r}")]
     b0 = np.load(tmp_path / "blob0.npy")
     for r in range(1, world):
         assert b0.size > 0 and np.array_equal(b0, np.load(tmp_path / f"blob{r}.npy"))
