@@ -42,9 +42,9 @@ $(PKG)/kwload: $(SRC)/kwload.cpp $(PKG)/libkwsynth.so
 $(PKG)/libkwsynth.so: $(SRC)/synth.cpp include/kwgpu.h
 	$(CXX) -O3 -std=c++17 -fPIC -shared -Wall -o $@ $<
 
-oracle/build/libkworacle.so: oracle/kworacle.c oracle/kworacle.h include/kwgpu.h
+oracle/build/libkworacle.so: oracle/kworacle.c oracle/kwregex.c oracle/kworacle.h include/kwgpu.h
 	@mkdir -p oracle/build
-	$(CC) -O2 -std=c11 -fPIC -shared -Wall -Wextra -o $@ $< -lpthread
+	$(CC) -O2 -std=c11 -fPIC -shared -Wall -Wextra -o $@ oracle/kworacle.c oracle/kwregex.c -lpthread
 
 # A/B variant of the library with extra kernel flags: make variant NAME=x VFLAGS="-DKW_PREFETCH=0"
 # -> policy-server_amd/variants/x.so (KWGPU_LIB selects it; scripts/ab.sh benches every variant);

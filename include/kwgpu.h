@@ -200,6 +200,12 @@ int kw_env_validate_settings(const kw_env *env, int32_t idx, char *buf, size_t c
 /* Diagnostic: does `s` match pattern `pat` (kind 0 literal, 1 glob, 2 regex) under the engine's
  * compiled-automaton semantics? 1/0, or -1 on a pattern syntax error. */
 int kw_pattern_match(int kind, const char *pat, const char *s, size_t len);
+/* The same for n subjects with one compilation: out[i] = 1/0; returns KW_OK, or -1 on a syntax
+ * error. A pattern whose DFA exceeds the state budget runs as its NFA (kwdev.hpp DevNfa);
+ * kind | KW_PATTERN_FORCE_NFA runs the NFA form whatever its DFA size (tests: DFA == NFA). */
+#define KW_PATTERN_FORCE_NFA 0x100
+int kw_pattern_match_many(int kind, const char *pat, const char *const *subjects, const size_t *lens, size_t n,
+                          int32_t *out);
 /* Diagnostics over the compiled classifiers (tests): the distinct patterns of request column `col`
  * (kwdev.hpp Col; kind 0 literal, 1 glob, 2 regex), and the ids of the patterns string `s` matches
  * through the blob's tables (the tables the kernels run). For COL_LV, `key` is the label key and

@@ -10,7 +10,6 @@
 
 #include <fnmatch.h>
 #include <pthread.h>
-#include <regex.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -18,7 +17,7 @@ struct orc_env {
   const orc_policy *pol;
   int32_t npol;
   char *always_ns; /* NULL = None */
-  regex_t **re;    /* per policy: compiled l3 regexes (labels) */
+  orc_re ***re;    /* per policy: compiled l3 regexes (labels) */
 };
 
 static char *dupz(const char *s) {
@@ -34,15 +33,16 @@ orc_env *orc_env_new(const orc_policy *policies, int32_t npol, const char *alway
   e->pol = policies;
   e->npol = npol;
   e->always_ns = always_ns ? dupz(always_ns) : NULL;
-  e->re = (regex_t **)calloc((size_t)npol, sizeof(regex_t *));
+  e->re = (orc_re ***)calloc((size_t)npol, sizeof(orc_re **));
   for (int32_t p = 0; p < npol; ++p) {
     const orc_policy *P = &policies[p];
-    if (P->family != ORC_F_LABELS || P->n[3] == 0) continue;
-    e->re[p] = (regex_t *)calloc((size_t)P->n[3], sizeof(regex_t));
+    if (P->family != ORC_F_LABELS || P->n[3] == 0 || P->init_error) continue;
+    e->re[p] = (orc_re **)calloc((size_t)P->n[3], sizeof(orc_re *));
     for (int32_t i = 0; i < P->n[3]; ++i) {
-      int rc = regcomp(&e->re[p][i], P->l[3][i], REG_EXTENDED | REG_NOSUB);
-      if (rc != 0) {
-        if (err) regerror(rc, &e->re[p][i], err, (size_t)errlen);
+      e->re[p][i] = orc_re_compile(P->l[3][i], err, errlen);
+      if (!e->re[p][i]) {
+        e->npol = p + 1;
+        orc_env_free(e);
         return NULL;
       }
     }
@@ -54,7 +54,7 @@ void orc_env_free(orc_env *e) {
   if (!e) return;
   for (int32_t p = 0; p < e->npol; ++p) {
     if (!e->re[p]) continue;
-    for (int32_t i = 0; i < e->pol[p].n[3]; ++i) regfree(&e->re[p][i]);
+    for (int32_t i = 0; i < e->pol[p].n[3]; ++i) orc_re_free(e->re[p][i]);
     free(e->re[p]);
   }
   free(e->re);
@@ -63,10 +63,17 @@ void orc_env_free(orc_env *e) {
 }
 
 int orc_regex_ok(const char *pattern) {
-  regex_t re;
-  if (regcomp(&re, pattern, REG_EXTENDED | REG_NOSUB) != 0) return 0;
-  regfree(&re);
-  return 1;
+  orc_re *re = orc_re_compile(pattern, NULL, 0);
+  orc_re_free(re);
+  return re != NULL;
+}
+
+int orc_re_match(const char *pattern, const char *s, size_t n) {
+  orc_re *re = orc_re_compile(pattern, NULL, 0);
+  if (!re) return -1;
+  int r = orc_re_search(re, s, n);
+  orc_re_free(re);
+  return r;
 }
 
 /* ------------------------------------------------------------------ string helpers */
@@ -325,6 +332,7 @@ static fam_out fam_apparmor(const orc_policy *P, const kw_soa *S, uint64_t r) {
 static fam_out fam_labels(const orc_env *e, int32_t p, const kw_soa *S, uint64_t r, zbuf *zb) {
   const orc_policy *P = &e->pol[p];
   fam_out o = {0, 0, 0};
+  (void)zb;
   for (uint32_t l = S->lbl_off[r]; l < S->lbl_off[r + 1]; ++l) {
     sv key = col(&S->lbl_key, l);
     if (any_eq(P->l[0], P->n[0], key)) {
@@ -334,7 +342,8 @@ static fam_out fam_labels(const orc_env *e, int32_t p, const kw_soa *S, uint64_t
     }
     for (int32_t i = 0; i < P->n[2]; ++i) {
       if (!sv_eq(key, P->l[2][i])) continue;
-      if (regexec(&e->re[p][i], z(zb, col(&S->lbl_val, l)), 0, NULL, 0) != 0) {
+      sv v = col(&S->lbl_val, l);
+      if (!orc_re_search(e->re[p][i], v.p, v.n)) {
         o.reason = KW_R_LABEL_CONSTRAINT;
         o.arg = l - S->lbl_off[r];
         return o;

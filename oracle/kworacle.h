@@ -18,7 +18,7 @@
  *     evaluation_environment.rs:979-1042 and integration_test.rs:101-131, 204-251.
  * It consumes the kw_soa columns declared in include/kwgpu.h (the boundary's data format) and an
  * oracle-side policy description built by oracle/oracle.py from the parsed policies document.
- * Strings are matched with libc fnmatch(3) (globs) and POSIX regcomp/regexec (REG_EXTENDED) —
+ * Strings are matched with libc fnmatch(3) (globs) and the oracle's own regex matcher (kwregex.c) —
  * an implementation independent of the product's DFA compiler.
  */
 #ifndef KWORACLE_H
@@ -108,8 +108,17 @@ typedef struct orc_detail {
 } orc_detail;
 void orc_eval_detail(const orc_env *e, const kw_soa *soa, int32_t policy, int32_t origin, uint64_t row, orc_detail *out);
 
-/* 1 if POSIX regcomp(REG_EXTENDED) accepts the pattern. */
+/* 1 if the regex compiles in the dialect of DESIGN.md §2 (kwregex.c). */
 int orc_regex_ok(const char *pattern);
+
+/* kwregex.c: the oracle's own matcher for that dialect (Rust `regex` syntax, Regex::is_match
+   search semantics, a Pike VM over code points). NULL with a message on a syntax error. */
+typedef struct orc_re orc_re;
+orc_re *orc_re_compile(const char *pattern, char *err, int errlen);
+int orc_re_search(const orc_re *re, const char *s, size_t n);
+void orc_re_free(orc_re *re);
+/* convenience for tests: 1 match, 0 no match, -1 the pattern does not compile */
+int orc_re_match(const char *pattern, const char *s, size_t n);
 
 /* Image reference normalisation; writes NUL-terminated parts.
    Returns 1 if an effective tag exists. */

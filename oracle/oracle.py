@@ -17,7 +17,8 @@ Restates, independently of the product's C++ (env.cpp / expr.cpp / service.cpp):
     pod-privileged message pinned by integration_test.rs:58-68.
   * the psp-capabilities mutation as an RFC 6902 patch — parity UNPINNED (the
     guest's mutated_object and policy-evaluator's diff are upstream, absent here).
-The per-request family arithmetic runs in oracle/kworacle.c (libc fnmatch + POSIX regex).
+The per-request family arithmetic runs in oracle/kworacle.c (libc fnmatch + the oracle's own regex
+matcher, oracle/kwregex.c).
 """
 import base64
 import ctypes as C
@@ -414,41 +415,6 @@ def validate_policies(entries):
 
 
 # ----------------------------------------------------------------------------- settings
-def _translate_regex(r):
-    """Rust-style \\d / \\D to POSIX bracket expressions for regcomp (outside brackets)."""
-    out, i, inb = [], 0, False
-    while i < len(r):
-        c = r[i]
-        if inb:
-            out.append(c)
-            if c == "]":
-                inb = False
-            i += 1
-            continue
-        if c == "[":
-            inb = True
-            out.append(c)
-            i += 1
-            if i < len(r) and r[i] == "^":
-                out.append("^")
-                i += 1
-            if i < len(r) and r[i] == "]":
-                out.append("]")
-                i += 1
-            continue
-        if c == "\\" and i + 1 < len(r) and r[i + 1] in "dD":
-            out.append("[0-9]" if r[i + 1] == "d" else "[^0-9]")
-            i += 2
-            continue
-        if c == "\\" and i + 1 < len(r):
-            out.append(r[i:i + 2])
-            i += 2
-            continue
-        out.append(c)
-        i += 1
-    return "".join(out)
-
-
 def compile_settings(fam, s, olib):
     """Returns (lists[5], flags) or raises ValueError(message) -> 'Policy settings are invalid: ...'."""
     L = [[], [], [], [], []]
@@ -514,7 +480,7 @@ def compile_settings(fam, s, olib):
         for k, v in (c or {}).items():
             if not isinstance(v, str):
                 raise ValueError("constrained_labels values must be strings")
-            if not olib.orc_regex_ok(_translate_regex(v).encode()):
+            if not olib.orc_regex_ok(v.encode()):
                 raise ValueError(f"constrained label '{k}' has an invalid regular expression")
             L[2].append(k)
             L[3].append(v)
@@ -1006,8 +972,17 @@ def olib():
         L.orc_eval_detail.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_uint64, C.POINTER(_ODetail)]
         L.orc_regex_ok.restype = C.c_int
         L.orc_regex_ok.argtypes = [C.c_char_p]
+        L.orc_re_match.restype = C.c_int
+        L.orc_re_match.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t]
         _olib = L
     return _olib
+
+
+def regex_match(pattern, subject):
+    """The oracle's Regex::is_match (oracle/kwregex.c): 1 / 0, or -1 when the pattern does not
+    compile in the dialect of DESIGN.md §2."""
+    b = subject.encode() if isinstance(subject, str) else bytes(subject)
+    return olib().orc_re_match(pattern.encode(), b, len(b))
 
 
 def image_parts(image):
@@ -1136,8 +1111,6 @@ class OracleEnv:
             o.flags = p["flags"]
             for k in range(5):
                 items = [s.encode() for s in p["lists"][k]]
-                if p["family"] == F_LABELS and k == 3:
-                    items = [_translate_regex(s).encode() for s in p["lists"][k]]
                 arr = (C.c_char_p * max(len(items), 1))(*items)
                 self._keep.append(arr)
                 o.n[k] = len(items)

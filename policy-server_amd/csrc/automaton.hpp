@@ -12,10 +12,13 @@
 //   Literal: whole-string byte equality.
 //   Glob:    whole-string fnmatch(3) with flags 0: '*' any bytes (including '/'), '?' one byte,
 //            '[...]' / '[!...]' / '[^...]' sets with ranges and [:class:], '\' escapes.
-//   Regex:   POSIX ERE subset with search semantics (Rust Regex::is_match): alternation, groups,
-//            * + ? {m} {m,} {m,n}, '.', sets, '^' '$' assertions, \d \D \w \W \s \S escapes.
+//   Regex:   the Rust `regex` crate dialect of DESIGN.md §2 with search semantics
+//            (Regex::is_match), matched over UTF-8 (automaton.cpp RParser).
+// A pattern whose DFA exceeds the state budget becomes an NFA element of its chain (Dfa::nfa, the
+// program of kwdev.hpp DevNfa), so no valid pattern fails a column.
 #pragma once
 #include <array>
+#include <cstddef>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -45,8 +48,11 @@ struct Dfa {
   std::vector<uint16_t> trans;                  // [state][byte class]
   std::vector<uint32_t> acc;                    // [state] accept class
   std::vector<std::vector<uint32_t>> classes;   // accept class -> pattern indices (classes[0] empty)
+  // an NFA element: one pattern, classes {{}, {0}}, no tables; `prog` is its DevNfa record
+  bool nfa = false;
+  std::vector<uint8_t> prog;
   uint32_t run(const uint8_t* s, size_t n) const;  // accept class of the whole string
-  size_t table_bytes() const { return trans.size() * 2 + (size_t)nstates * 2 + 256; }
+  size_t table_bytes() const { return nfa ? 0 : trans.size() * 2 + (size_t)nstates * 2 + 256; }
 };
 
 constexpr uint32_t kMaxDfaStates = 8192;
@@ -62,5 +68,12 @@ bool compile_column(const std::vector<Pattern>& pats, size_t max_table_bytes, ui
                     std::string* err, std::vector<uint32_t>* firsts = nullptr);
 // Syntax check of one regex (used by settings validation).
 bool regex_ok(const std::string& re, std::string* err);
+// Syntax check of any pattern (no automaton is built, so no size limit applies).
+bool pattern_ok(const Pattern& p, std::string* err);
+// One pattern as an NFA element (Dfa::nfa); false only on a syntax error or an NFA beyond
+// kMaxNfaStates (Rust's compiled-size limit has the same role).
+bool compile_nfa(const Pattern& p, Dfa* out, std::string* err);
+// Runs a DevNfa record on the host (the kernels' nfa_run over host scratch).
+bool run_nfa_record(const uint8_t* rec, const uint8_t* s, size_t n);
 
 }  // namespace kw

@@ -1467,10 +1467,26 @@ int kw_env_group_members(const kw_env* env, int32_t group, int32_t* out, int cap
 int kw_pattern_match(int kind, const char* pat, const char* s, size_t len) {
   if (!pat || (!s && len)) return -1;
   std::vector<Pattern> ps{{(Pattern::Kind)kind, pat}};
-  Dfa d;
+  std::vector<Dfa> chain;  // one DFA, or the NFA element a pattern beyond the state budget becomes
   std::string err;
-  if (!compile_dfa(ps, &d, &err)) return -1;
-  return d.run((const uint8_t*)s, len) != 0 ? 1 : 0;
+  if (!compile_column(ps, (size_t)1 << 30, kMaxDfaStates, &chain, &err) || chain.size() != 1) return -1;
+  return chain[0].run((const uint8_t*)s, len) != 0 ? 1 : 0;
+}
+
+int kw_pattern_match_many(int kind, const char* pat, const char* const* subjects, const size_t* lens, size_t n,
+                          int32_t* out) {
+  if (!pat || (n && (!subjects || !lens || !out))) return -1;
+  std::vector<Pattern> ps{{(Pattern::Kind)(kind & 0xff), pat}};
+  std::vector<Dfa> chain;
+  std::string err;
+  if (kind & KW_PATTERN_FORCE_NFA) {
+    chain.resize(1);
+    if (!compile_nfa(ps[0], &chain[0], &err)) return -1;
+  } else if (!compile_column(ps, (size_t)1 << 30, kMaxDfaStates, &chain, &err) || chain.size() != 1) {
+    return -1;
+  }
+  for (size_t i = 0; i < n; ++i) out[i] = chain[0].run((const uint8_t*)subjects[i], lens[i]) != 0 ? 1 : 0;
+  return KW_OK;
 }
 
 int kw_env_pattern_count(const kw_env* env, int col) {

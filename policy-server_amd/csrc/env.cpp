@@ -306,8 +306,8 @@ bool compile_settings(const JDoc& d, int64_t s, PolicyRec* rec, std::string* err
           }
           std::string key(d.key(kid)), re(d.str(kid));
           std::string rerr;
-          if (!regex_ok(re, &rerr)) {
-            *err = "constrained label '" + key + "' has an invalid regular expression: " + rerr;
+          if (!regex_ok(re, &rerr)) {  // (the parser's detail stays out: the oracle words it its own way)
+            *err = "constrained label '" + key + "' has an invalid regular expression";
             return false;
           }
           // a repeated key keeps its first position and its last regex (a JSON map, as serde reads it)

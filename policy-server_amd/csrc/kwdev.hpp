@@ -14,7 +14,7 @@
 namespace kw {
 
 constexpr uint32_t kBlobMagic = 0x4b574733;  // "KWG3"
-constexpr uint32_t kBlobVersion = 6;
+constexpr uint32_t kBlobVersion = 7;
 
 // request columns that carry strings classified by a DFA or a literal table
 enum Col : uint32_t {
@@ -83,7 +83,9 @@ struct alignas(16) KvDfa {
   uint32_t start;
   uint16_t cbase, nstates, ncls;
   uint16_t abs_lo;                // states [abs_lo, nstates) and 0 are absorbing: a walk stops there
-  uint8_t hi, wide, t16, pad;     // hi: class of bytes >= 128 when !wide
+  uint8_t hi, wide, t16;          // hi: class of bytes >= 128 when !wide
+  uint8_t nfa;                    // 1: an NFA element (DevNfa): trans_off is the program's blob offset,
+                                  // acc_off its u16 [2] local classes (no match, match); no table
 };
 static_assert(sizeof(KvDfa) == 32, "KvDfa layout");
 
@@ -105,7 +107,7 @@ struct alignas(16) DevDfa {
   // states after the constant prefixes of image normalisation, from `start` (an implicit registry
   // costs no walk): pre0 = "docker.io" | "docker.io/" << 16, pre1 = "docker.io/library/" | "latest" << 16
   uint32_t pre0, pre1;
-  uint32_t pad;
+  uint32_t kind;  // 0 a DFA; 1 an NFA element (DevNfa at blob offset trans_off; acc: u16 [2] classes no match / match)
   uint8_t cls[256];
 };
 // A walk may stop at state 0 (dead) and at states >= abs_lo (absorbing): `live` is st in [1, abs_lo).
@@ -166,6 +168,96 @@ struct alignas(16) DevCol {
   uint32_t lit_bytes;
   uint32_t pad;
 };
+
+// ---- Patterns whose DFA exceeds the state budget (kMaxDfaStates: e.g. `a[a-z]{14}b` searched
+// anywhere, or the glob `*a?????????????????`) run as their Thompson NFA instead (a Pike VM: one
+// list of live states per position, linear in the string), so no valid pattern ever fails the
+// environment (evaluation_environment.rs:216-225, 256-262, 472-510 build any regex the policy
+// accepts). Such a pattern is an element of its column's DFA chain (DevDfa::kind / KvDfa::nfa = 1)
+// that holds no table: nfa_classify_kernel runs the program for every entity of the batch before
+// the tile kernel, which reads the element's class from that pass's HBM array.
+//
+// Record (16-B aligned, offsets from the record start): DevNfa | u32 first[nnodes + 1] (edges of
+// node k: [first[k], first[k + 1])) | u32x2 edge[nedges] | 32-B byte sets[nsets].
+// edge.x = kind (0 byte set, 1 epsilon, 2 assertion) | arg << 8 (set id, or the assertion's 16-bit
+// mask over (previous, next) byte kinds, bit prev * 4 + next, kinds below); edge.y = target node.
+struct alignas(16) DevNfa {
+  uint32_t nnodes, nedges, nsets, start;
+  uint32_t first_off, edge_off, set_off;
+  uint32_t accept;  // the accepting node
+  uint32_t search;  // 1: a regex (Regex::is_match: the accepting node is sticky, a walk may stop there)
+  uint32_t bytes;   // whole record
+  uint32_t pad[2];
+};
+enum NfaEdge : uint32_t { NE_BYTE = 0, NE_EPS = 1, NE_ASSERT = 2 };
+// byte kinds of the assertion masks: EDGE = before the first / after the last byte
+enum : uint32_t { NK_EDGE = 0, NK_NL = 1, NK_WORD = 2, NK_OTHER = 3 };
+inline KW_HD uint32_t nfa_kind(uint32_t c) {
+  if (c == '\n') return NK_NL;
+  const bool w = (c - '0' < 10u) || (c - 'A' < 26u) || (c - 'a' < 26u) || c == '_';
+  return w ? NK_WORD : NK_OTHER;
+}
+// Scratch a walk of `r` needs, in u32 words: mark[nnodes], two lists[nnodes], stack[nedges + 1].
+inline KW_HD uint64_t nfa_scratch_words(const DevNfa& r) { return 3ull * r.nnodes + r.nedges + 1; }
+
+// The Pike VM: 1 if the string s[0, n) is accepted. `scratch`: nfa_scratch_words(r) u32 words;
+// `gen`: the caller's generation counter (mark[] entries equal to a generation the walk uses must not
+// exist: the caller zeroes mark[] once, then keeps passing the same counter).
+inline KW_HD bool nfa_run(const uint8_t* rec, const uint8_t* s, uint32_t n, uint32_t* scratch, uint32_t* gen) {
+  const DevNfa& R = *(const DevNfa*)rec;
+  const uint32_t* first = (const uint32_t*)(rec + R.first_off);
+  const uint32_t* edge = (const uint32_t*)(rec + R.edge_off);
+  const uint32_t* sets = (const uint32_t*)(rec + R.set_off);
+  uint32_t* mark = scratch;
+  uint32_t* cur = scratch + R.nnodes;
+  uint32_t* nxt = cur + R.nnodes;
+  uint32_t* stack = nxt + R.nnodes;
+  uint32_t ncur = 0, nnxt = 0;
+  bool hit = false;
+  // the closure of `node` at a position between byte kinds (p, q) into list L
+  auto add = [&](uint32_t node, uint32_t p, uint32_t q, uint32_t* L, uint32_t* cnt) {
+    const uint32_t g = *gen;
+    const uint32_t bit = 1u << (p * 4u + q);
+    uint32_t sp = 0;
+    stack[sp++] = node;
+    while (sp) {
+      const uint32_t x = stack[--sp];
+      if (mark[x] == g) continue;
+      mark[x] = g;
+      if (x == R.accept) hit = true;
+      bool stepping = false;
+      for (uint32_t e = first[x], e1 = first[x + 1]; e < e1; ++e) {
+        const uint32_t k = edge[2 * e] & 0xffu, arg = edge[2 * e] >> 8, y = edge[2 * e + 1];
+        if (k == NE_BYTE) stepping = true;
+        else if (k == NE_EPS || (arg & bit)) stack[sp++] = y;
+      }
+      if (stepping) L[(*cnt)++] = x;
+    }
+  };
+  ++*gen;
+  add(R.start, NK_EDGE, n ? nfa_kind(s[0]) : NK_EDGE, cur, &ncur);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (hit && R.search) return true;
+    hit = false;
+    const uint32_t c = s[i], p = nfa_kind(c), q = i + 1 < n ? nfa_kind(s[i + 1]) : NK_EDGE;
+    ++*gen;
+    nnxt = 0;
+    for (uint32_t t = 0; t < ncur; ++t) {
+      const uint32_t x = cur[t];
+      for (uint32_t e = first[x], e1 = first[x + 1]; e < e1; ++e) {
+        if ((edge[2 * e] & 0xffu) != NE_BYTE) continue;
+        const uint32_t set = edge[2 * e] >> 8;
+        if ((sets[set * 8u + (c >> 5)] >> (c & 31u)) & 1u) add(edge[2 * e + 1], p, q, nxt, &nnxt);
+      }
+    }
+    uint32_t* t = cur;
+    cur = nxt;
+    nxt = t;
+    ncur = nnxt;
+    if (!ncur && !hit) return false;  // no live state: nothing can match any more
+  }
+  return hit;
+}
 
 struct alignas(16) DevHeader {
   uint32_t magic, version, blob_bytes, npatterns;

@@ -563,6 +563,18 @@ def pattern_match(kind, pattern, s):
     return N.lib().kw_pattern_match(kind, pattern.encode(), b, len(b))
 
 
+def pattern_match_many(kind, pattern, subjects):
+    """kw_pattern_match_many: one compilation, a list of 1/0 per subject; None on a syntax error."""
+    bs = [x.encode() if isinstance(x, str) else bytes(x) for x in subjects]
+    n = len(bs)
+    arr = (C.c_char_p * max(n, 1))(*bs)
+    lens = (C.c_size_t * max(n, 1))(*[len(x) for x in bs])
+    out = (C.c_int32 * max(n, 1))()
+    if N.lib().kw_pattern_match_many(kind, pattern.encode(), arr, lens, n, out) != 0:
+        return None
+    return [int(out[k]) for k in range(n)]
+
+
 def decode(v):
     """Verdict word -> dict (include/kwgpu.h layout)."""
     v = int(v)

@@ -84,7 +84,7 @@ EXPORTS = [
     "kw_env_policy_count", "kw_env_policy_id", "kw_env_is_group", "kw_env_get_policy_mode",
     "kw_env_get_policy_allowed_to_mutate",
     "kw_env_should_always_accept_requests_made_inside_of_namespace",
-    "kw_env_policy_initialization_error", "kw_env_validate_settings", "kw_pattern_match", "kw_env_pattern_count",
+    "kw_env_policy_initialization_error", "kw_env_validate_settings", "kw_pattern_match", "kw_pattern_match_many", "kw_env_pattern_count",
     "kw_env_pattern", "kw_env_classify", "kw_batch_wide_arg", "kw_batch_group_causes", "kw_debug_plan",
     "kw_batch_from_json", "kw_batch_from_soa", "kw_batch_view", "kw_batch_to_device", "kw_batch_to_device_async",
     "kw_stream_create", "kw_stream_destroy", "kw_validate_host", "kw_host_alloc", "kw_host_free",
@@ -125,6 +125,7 @@ def lib():
         "kw_env_policy_initialization_error": (ip, [vp, i32, cp, sz]),
         "kw_env_validate_settings": (ip, [vp, i32, cp, sz]),
         "kw_pattern_match": (ip, [ip, cp, cp, sz]),
+        "kw_pattern_match_many": (ip, [ip, cp, C.POINTER(cp), C.POINTER(sz), sz, C.POINTER(C.c_int32)]),
         "kw_env_pattern_count": (ip, [vp, ip]),
         "kw_env_pattern": (ip, [vp, ip, ip, C.POINTER(ip), cp, sz]),
         "kw_env_classify": (ip, [vp, ip, cp, sz, cp, sz, C.POINTER(u32), ip]),
