@@ -261,6 +261,12 @@ struct DeviceBatch {
   // overflow path: per-string classes in HBM (one allocation) and the wide-argument side data
   uint16_t* g_cls = nullptr;
   size_t g_cls_cap = 0;
+  // NFA elements: their classes ([label][nlv] | [container][nim]) and the Pike VMs' scratch
+  uint16_t* nfa_cls = nullptr;
+  size_t nfa_cls_cap = 0;
+  uint32_t* nfa_scratch = nullptr;
+  size_t nfa_scratch_cap = 0;
+  uint32_t max_image_len = 0xffffffffu;  // longest image reference of the batch (computed on first use)
   uint32_t* wide_count = nullptr;
   WideRec* wide_rec = nullptr;
   size_t wide_rec_cap = 0;
@@ -306,6 +312,8 @@ struct DeviceBatch {
     P.release(device, cols, cols_bytes);
     P.release(device, verdicts, verdict_cap * 4);
     P.release(device, g_cls, g_cls_cap * 2);
+    P.release(device, nfa_cls, nfa_cls_cap * 2);
+    P.release(device, nfa_scratch, nfa_scratch_cap * 4);
     P.release(device, wide_rec, wide_rec_cap * sizeof(WideRec));
     P.release(device, wide_groups, wide_groups_cap * 8);
     P.release(device, member_words, member_words_cap * 4);
@@ -493,6 +501,9 @@ std::vector<TileStats> tile_quantiles(const std::vector<TileStats>& need, const 
 
 struct PassPlan {
   bool rows_mode = false;
+  const uint8_t* env_blob = nullptr;  // host copy of the environment's blob (DevHeader first)
+  NfaPass nfa{};                      // filled by ensure_nfa when the pass has NFA elements
+  uint32_t nfa_threads = 0;
   std::vector<SlotChunk> chunks;
   std::vector<std::pair<uint32_t, uint32_t>> launches;  // chunk ranges [first, last)
   std::vector<TileArgs> tiles;                          // one per launch (record pointers filled at upload)
@@ -564,6 +575,7 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
   DeviceBatch& D = *kb->dev;
   const Batch& B = kb->b;
   const DevHeader* H = (const DevHeader*)E.blob.data();
+  plan->env_blob = E.blob.data();
   plan->rows_mode = row_policy != nullptr;
   // ---- the columns of the pass and their slot-plan chunks
   std::vector<int32_t> list;
@@ -859,6 +871,11 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
   for (const SlotChunk& c : plan->chunks) any_grp = any_grp || c.groups;
   T.feat = ((need & (1u << S_IMG)) ? kFeatImg : 0u) | (any_lbl ? kFeatLbl : 0u) | (any_ctr_fam ? kFeatCtr : 0u) |
            (any_grp ? kFeatGrp : 0u);
+  // NFA elements among the classifiers the pass reads: the one instantiation that reads their classes
+  const bool nfa_img = (need & (1u << S_IMG)) &&
+                       ((H->col[COL_REG].flags | H->col[COL_TAG].flags | H->col[COL_IMG].flags) & 1u);
+  const bool nfa_lv = (need & (1u << S_LV)) && (H->col[COL_LV].flags & 1u);
+  if (nfa_img || nfa_lv) T.feat = kFeatAll | kFeatNfa;
   T.il = il;
   T.nlv = nlv;
   T.need = need;
@@ -1116,6 +1133,45 @@ int ensure_overflow_classes(const Batch& B, DeviceBatch* D, const TileArgs& T, E
   return KW_OK;
 }
 
+// NFA elements of a pass (kwdev.hpp DevNfa): the class arrays the tile kernel reads and the Pike
+// VMs' scratch (nfa_classify_kernel, launched first by run_pass).
+int ensure_nfa(kw_batch* kb, PassPlan& plan, EvalArgs* A) {
+  DeviceBatch& D = *kb->dev;
+  const Batch& B = kb->b;
+  const TileArgs& T = plan.geom;
+  const DevHeader* H = (const DevHeader*)plan.env_blob;
+  NfaPass& np = plan.nfa;
+  memset(&np, 0, sizeof(np));
+  np.nlv = T.nlv;
+  np.nim = T.il.n();
+  np.nlabels = B.labels();
+  np.nctrs = B.containers();
+  np.do_lv = (T.need & (1u << S_LV)) && (H->col[COL_LV].flags & 1u) && np.nlv ? 1u : 0u;
+  np.do_img = (T.need & (1u << S_IMG)) && ((H->col[COL_REG].flags | H->col[COL_TAG].flags | H->col[COL_IMG].flags) & 1u) && np.nim
+                  ? 1u
+                  : 0u;
+  if (np.do_img && D.max_image_len == 0xffffffffu) {
+    uint32_t m = 0;
+    for (uint64_t c = 0; c < B.containers(); ++c) m = std::max(m, B.ctr_image.off[c + 1] - B.ctr_image.off[c]);
+    D.max_image_len = m;
+  }
+  np.nfa_words = H->nfa_words;
+  np.subj_bytes = np.do_img ? ((D.max_image_len + 64u) & ~3u) : 0u;  // + "docker.io/library/" ":latest"
+  np.words_per_thread = np.nfa_words + np.subj_bytes / 4u;
+  const uint64_t nlv = std::max<uint32_t>(np.nlv, 1), nim = std::max<uint32_t>(np.nim, 1);
+  const uint64_t n_lv = np.do_lv ? np.nlabels * nlv : 0, n_img = np.do_img ? np.nctrs * nim : 0;
+  if (int rc = ensure(&D.nfa_cls, &D.nfa_cls_cap, (size_t)(n_lv + n_img + 1))) return rc;
+  np.lv = D.nfa_cls;
+  np.img = D.nfa_cls + n_lv;
+  const uint64_t items = (np.do_lv ? np.nlabels : 0) + (np.do_img ? np.nctrs : 0);
+  plan.nfa_threads = nfa_threads(items, np.words_per_thread);
+  if (int rc = ensure(&D.nfa_scratch, &D.nfa_scratch_cap, (size_t)(plan.nfa_threads * np.words_per_thread + 1))) return rc;
+  np.scratch = D.nfa_scratch;
+  A->nfa_lv = np.do_lv ? np.lv : nullptr;
+  A->nfa_img = np.do_img ? np.img : nullptr;
+  return KW_OK;
+}
+
 // Everything a pass's launches need on the device before the first one: the plan's records and
 // TileArgs, the rows-mode column map, tile descriptors and overflow list, schedule counters and the
 // side-data buffers; *out_args: the launch arguments.
@@ -1183,6 +1239,9 @@ int prepare_pass(kw_batch* kb, PassPlan& plan, hipStream_t s, EvalArgs* out_args
     A.wide_rec = D.wide_rec;
     A.wide_cap = (uint32_t)std::min<size_t>(cap, 0xffffffffu);
   }
+  if (plan.geom.feat & kFeatNfa) {
+    if (int rc = ensure_nfa(kb, plan, &A)) return rc;
+  }
   D.last_nwide = plan.nwide;
   D.last_wide_policy = plan.wide_policy;
   D.last_rows_mode = plan.rows_mode;
@@ -1204,6 +1263,7 @@ int run_pass(kw_batch* kb, PassPlan& plan, bool timed, hipStream_t s) {
     A.phase = (uint64_t*)d_phase;
   }
   if (timed) HIPCHK(hipEventRecord(D.ev[0], s));
+  if (plan.geom.feat & kFeatNfa) HIPCHK(launch_nfa_classify(A, D.d_tiles, plan.nfa, plan.nfa_threads, s));
   for (size_t l = 0; l < plan.tiles.size(); ++l) {
     if (phases) HIPCHK(hipMemsetAsync(d_phase, 0, phase_bytes, s));
     HIPCHK(launch_evaluate_tiles(A, plan.tiles[l], D.d_tiles + l, D.desc, plan.grid, s));
@@ -1899,8 +1959,9 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
   uint8_t* st = (uint8_t*)D.staging;
   hipStream_t sc = D.stream;
   EvalArgs A;
+  // (NFA elements: their pre-pass reads whole columns, so such passes are not chunked)
   bool chunked = plan.tiles.size() == 1 && plan.wide.groups.empty() && plan.nwide == 0 && !plan.rows_mode &&
-                 !(plan.geom.debug & 512u) && B.n > 0;
+                 !(plan.geom.debug & 512u) && !(plan.geom.feat & kFeatNfa) && B.n > 0;
   if (chunked) {
     if (int rc = prepare_pass(kb, plan, sc, &A)) {
       D.loaded = 0;

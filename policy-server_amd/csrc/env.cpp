@@ -263,10 +263,8 @@ bool compile_settings(const JDoc& d, int64_t s, PolicyRec* rec, std::string* err
       }
       for (int k = 0; k < 5; ++k)
         for (auto& g : rec->lists[k]) {
-          std::vector<Pattern> one{{Pattern::Glob, g}};
-          Dfa tmp;
           std::string e2;
-          if (!compile_dfa(one, &tmp, &e2)) {
+          if (!pattern_ok({Pattern::Glob, g}, &e2)) {  // syntax only: a large automaton runs as an NFA
             *err = "invalid pattern '" + g + "': " + e2;
             return false;
           }
@@ -501,11 +499,35 @@ bool build_literal_table(const std::vector<std::string>& lits, std::vector<uint8
 
 // Appends one DevDfa record (header, accept classes, transitions; 16-B aligned) and returns its
 // blob offset. `cls_map`: the DFA's local accept class -> the column's global class.
-size_t emit_dfa(const Dfa& dfa, const std::vector<uint32_t>& cls_map, std::vector<uint8_t>* b) {
+// Appends an NFA element's program (DevNfa) and returns its blob offset.
+size_t emit_nfa_prog(const Dfa& dfa, std::vector<uint8_t>* b) {
+  align16(b);
+  const size_t at = b->size();
+  b->insert(b->end(), dfa.prog.begin(), dfa.prog.end());
+  align16(b);
+  return at;
+}
+
+size_t emit_dfa(const Dfa& dfa, const std::vector<uint32_t>& cls_map, std::vector<uint8_t>* b, size_t nfa_prog = 0) {
   align16(b);
   const size_t hdr_at = b->size();
   DevDfa dd;
   memset(&dd, 0, sizeof(dd));
+  if (dfa.nfa) {  // an NFA element: no tables; acc = its two global classes (no match, match)
+    dd.kind = 1;
+    dd.trans_off = (uint32_t)nfa_prog;
+    put(b, dd);
+    align16(b);
+    const uint32_t acc_off = (uint32_t)b->size();
+    put(b, (uint16_t)cls_map[0]);
+    put(b, (uint16_t)cls_map[1]);
+    align16(b);
+    DevDfa* w = (DevDfa*)(b->data() + hdr_at);
+    w->acc_off = acc_off;
+    w->bytes = (uint32_t)(b->size() - hdr_at);
+    w->chain_bytes = w->bytes;
+    return hdr_at;
+  }
   dd.nstates = dfa.nstates;
   dd.ncls = dfa.ncls;
   dd.start = dfa.start;
@@ -573,17 +595,28 @@ Status compile_col(Col c, ColumnInfo* ci, DevCol* dc, std::vector<uint8_t>* b) {
     std::string err;
     if (!compile_column(pats, kDfaTableBudget, kMaxDfaStates, &chain, &err))
       return {KW_E_BOOTSTRAP, "bootstrap failure: cannot compile column automaton: " + err};
+    // NFA elements' programs first (read from HBM by nfa_classify_kernel, never staged), so the
+    // chain itself stays contiguous (the tile kernel stages it whole)
+    std::vector<size_t> prog_at(chain.size(), 0);
+    for (size_t k = 0; k < chain.size(); ++k)
+      if (chain[k].nfa) {
+        prog_at[k] = emit_nfa_prog(chain[k], b);
+        ci->nfa_words = std::max<uint64_t>(ci->nfa_words, nfa_scratch_words(*(const DevNfa*)chain[k].prog.data()));
+      }
     std::vector<size_t> at;
-    for (const Dfa& dfa : chain) {
+    for (size_t k = 0; k < chain.size(); ++k) {
+      const Dfa& dfa = chain[k];
       std::vector<uint32_t> cls_map(dfa.classes.size(), 0);
       for (size_t a = 1; a < dfa.classes.size(); ++a) {
         cls_map[a] = (uint32_t)ci->class_pats.size();
         std::vector<uint32_t> pids;
-        for (uint32_t k : dfa.classes[a]) pids.push_back(rest_pid[k]);
+        for (uint32_t q : dfa.classes[a]) pids.push_back(rest_pid[q]);
         ci->class_pats.push_back(pids);
       }
-      at.push_back(emit_dfa(dfa, cls_map, b));
+      at.push_back(emit_dfa(dfa, cls_map, b, prog_at[k]));
     }
+    for (const Dfa& dfa : chain)
+      if (dfa.nfa) dc->flags |= 1u;  // the column has NFA elements
     uint32_t tail = 0;
     for (size_t k = chain.size(); k-- > 0;) {
       DevDfa* w = (DevDfa*)(b->data() + at[k]);
@@ -648,6 +681,34 @@ Status compile_kv(Env* env, DevHeader* hdr, std::vector<uint8_t>* b) {
         if (d.ncls > 65535 || d.nstates > 65535) return {KW_E_BOOTSTRAP, "bootstrap failure: label value automaton too large"};
         KvDfa kv;
         memset(&kv, 0, sizeof(kv));
+        if (d.nfa) {  // an NFA element: its program in the blob (before the region), classes {0, 1}
+          kv.nfa = 1;
+          kv.trans_off = (uint32_t)emit_nfa_prog(d, b);
+          env->cols[COL_LV].nfa_words =
+              std::max<uint64_t>(env->cols[COL_LV].nfa_words, nfa_scratch_words(*(const DevNfa*)d.prog.data()));
+          kv.cbase = (uint16_t)cbase;
+          const size_t rec = at16(sizeof(KvDfa));
+          kv.acc_off = (uint32_t)at16(4);
+          ((uint16_t*)(R.data() + kv.acc_off))[0] = 0;
+          ((uint16_t*)(R.data() + kv.acc_off))[1] = 1;
+          memcpy(R.data() + rec, &kv, sizeof(kv));
+          if (prev) ((KvDfa*)(R.data() + prev))->next = (uint32_t)rec;
+          else sh.head = (uint32_t)rec;
+          prev = rec;
+          const size_t q = sh.dfas.size();
+          const uint32_t f0 = firsts[q], f1 = q + 1 < firsts.size() ? firsts[q + 1] : (uint32_t)vals[k].size();
+          std::vector<uint32_t> covered(vals[k].begin() + f0, vals[k].begin() + f1);
+          std::vector<std::vector<uint32_t>> sets;
+          for (const auto& cs : d.classes) {
+            std::vector<uint32_t> m;
+            for (uint32_t i : cs) m.push_back(vals[k][i]);
+            sets.push_back(m);
+          }
+          sh.dfas.push_back({covered, sets});
+          cbase += 2;
+          hdr->col[COL_LV].flags |= 1u;
+          continue;
+        }
         bool uniform_hi = true;
         for (int c = 128; c < 256; ++c) uniform_hi = uniform_hi && d.cls[c] == d.cls[128];
         kv.wide = uniform_hi ? 0 : 1;
@@ -926,6 +987,10 @@ Status build_env(const char* json, size_t len, bool continue_on_errors, const ch
   if (env->always_ns) hdr.bypass_cls = lit_class(COL_NS, env->always_ns->c_str());
   hdr.docker_io_cls = lit_class(COL_REG, "docker.io");
   hdr.latest_cls = lit_class(COL_TAG, "latest");
+  uint64_t nfa_words = 0;
+  for (int c = 0; c < (int)NCOL; ++c) nfa_words = std::max(nfa_words, env->cols[c].nfa_words);
+  if (nfa_words > 0xffffffffull) return {KW_E_BOOTSTRAP, "bootstrap failure: pattern automaton too large"};
+  hdr.nfa_words = (uint32_t)nfa_words;
   align16(&b);
   hdr.magic = kBlobMagic;
   hdr.version = kBlobVersion;
@@ -978,6 +1043,7 @@ uint32_t blob_lit(const uint8_t* blob, uint32_t off, const uint8_t* s, size_t n)
 }
 uint32_t blob_dfa(const uint8_t* blob, uint32_t off, const uint8_t* s, size_t n) {
   const DevDfa* d = (const DevDfa*)(blob + off);
+  if (d->kind == 1) return ((const uint16_t*)(blob + d->acc_off))[run_nfa_record(blob + d->trans_off, s, n) ? 1 : 0];
   const uint16_t* trans = (const uint16_t*)(blob + d->trans_off);
   const uint16_t* acc = (const uint16_t*)(blob + d->acc_off);
   uint32_t st = d->start;
@@ -1006,6 +1072,11 @@ std::vector<uint32_t> host_value_classes(const Env& env, uint32_t key, const uin
   for (uint32_t rel = ((const uint32_t*)R)[key]; rel;) {
     const KvDfa& d = *(const KvDfa*)(R + rel);
     uint32_t st = d.start;
+    if (d.nfa) {
+      out.push_back(kbase + d.cbase + (run_nfa_record(env.blob.data() + d.trans_off, s, n) ? 1u : 0u));
+      rel = d.next;
+      continue;
+    }
     for (size_t i = 0; i < n && st != 0; ++i) st = kv_step(R, d, st, s[i]);
     out.push_back(kbase + d.cbase + ((const uint16_t*)(R + d.acc_off))[st]);
     rel = d.next;

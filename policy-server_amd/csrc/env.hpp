@@ -55,6 +55,7 @@ struct ColumnInfo {
   std::vector<Pattern> pats;                      // pattern id = index
   std::vector<std::vector<uint32_t>> class_pats;  // global class -> pattern ids it matches (class 0: none)
   std::vector<uint32_t> lit_cls;                  // pattern id -> literal class (0 = not in the literal table)
+  uint64_t nfa_words = 0;                         // largest NFA element's scratch (nfa_scratch_words), 0 = none
 };
 
 // COL_LV class: label-key class `key`, the value regexes of the key's DFA that produced it

@@ -161,6 +161,7 @@ __device__ inline DfaView chain_view(const Chain& c, uint32_t off) {
   return v;
 }
 __device__ inline uint32_t chain_next(const Chain& c, uint32_t off) { return ((const DevDfa*)(c.base + (off - c.head)))->next; }
+__device__ inline uint32_t chain_kind(const Chain& c, uint32_t off) { return ((const DevDfa*)(c.base + (off - c.head)))->kind; }
 
 // Byte offset of transition (st, class) in a [state][ncls] table of 2^sh-byte entries, with the class
 // pre-shifted (cq = class << sh): one 24-bit multiply-add on the transition chain (states and class
@@ -265,24 +266,37 @@ struct Classifiers {
 // All classes of one image reference: il.nreg COL_REG entries (literal, DFAs), il.ntag COL_TAG
 // entries, il.nimg COL_IMG entries.
 // dbg (diagnostics, TileArgs::debug): 32768 skips the DFA chains, 65536 the literal lookups (class 0).
-template <bool BATCH, bool L, class Out>
+// NFA (instantiations with NFA elements): an element of kind 1 takes its class from nfa_row[j] (the
+// pass's nfa_classify_kernel output for this container) instead of a walk.
+template <bool BATCH, bool L, bool NFA = false, class Out>
 __device__ inline void classify_image(const Classifiers& C, const ImgLayout& il, const uint8_t* __restrict__ bytes,
-                                      uint32_t b, uint32_t e, Out out, uint32_t dbg = 0) {
+                                      uint32_t b, uint32_t e, Out out, uint32_t dbg = 0,
+                                      const uint16_t* __restrict__ nfa_row = nullptr) {
   const uint32_t NONE = 0xffffffffu;
   const ImageRef r = parse_image(bytes, b, e);
   const bool nodfa = (dbg & 32768u) != 0, nolit = (dbg & 65536u) != 0;
   uint32_t j = 0;
+  auto part = [&](int k, Col c, uint32_t o) -> uint32_t {
+    if (NFA && chain_kind(C.dfa[c], o)) return nfa_row[j];
+    return image_part<L>(k, chain_view(C.dfa[c], o), bytes, r);
+  };
   if (C.lit[COL_REG])
     out(j++, nolit ? 0u : r.is_reg ? lit_lookup<BATCH>(C.lit[COL_REG], bytes, r.b, r.slash0) : C.docker_io_cls);
-  for (uint32_t o = C.dfa[COL_REG].head; o; o = chain_next(C.dfa[COL_REG], o))
-    out(j++, nodfa ? 0u : image_part<L>(0, chain_view(C.dfa[COL_REG], o), bytes, r));
+  for (uint32_t o = C.dfa[COL_REG].head; o; o = chain_next(C.dfa[COL_REG], o)) {
+    out(j, nodfa ? 0u : part(0, COL_REG, o));
+    ++j;
+  }
   if (C.lit[COL_TAG])
     out(j++, nolit ? 0u : r.colon != NONE ? lit_lookup<BATCH>(C.lit[COL_TAG], bytes, r.colon + 1, r.name_end)
                                           : (r.at == NONE ? C.latest_cls : 0u));
-  for (uint32_t o = C.dfa[COL_TAG].head; o; o = chain_next(C.dfa[COL_TAG], o))
-    out(j++, nodfa ? 0u : image_part<L>(1, chain_view(C.dfa[COL_TAG], o), bytes, r));
-  for (uint32_t o = C.dfa[COL_IMG].head; o; o = chain_next(C.dfa[COL_IMG], o))
-    out(j++, nodfa ? 0u : image_part<L>(2, chain_view(C.dfa[COL_IMG], o), bytes, r));
+  for (uint32_t o = C.dfa[COL_TAG].head; o; o = chain_next(C.dfa[COL_TAG], o)) {
+    out(j, nodfa ? 0u : part(1, COL_TAG, o));
+    ++j;
+  }
+  for (uint32_t o = C.dfa[COL_IMG].head; o; o = chain_next(C.dfa[COL_IMG], o)) {
+    out(j, nodfa ? 0u : part(2, COL_IMG, o));
+    ++j;
+  }
 }
 
 // The region pointer carries its address space (3: LDS, 1: global), so the walk compiles to ds_read /
@@ -290,9 +304,9 @@ __device__ inline void classify_image(const Classifiers& C, const ImgLayout& il,
 template <int AS>
 using as_ptr = const __attribute__((address_space(AS))) uint8_t*;
 
-template <int AS, class Out>
+template <int AS, bool NFA, class Out>
 __device__ inline uint32_t classify_value_as(as_ptr<AS> R, uint32_t nlk, uint32_t k, const uint8_t* __restrict__ bytes,
-                                             uint32_t b, uint32_t e, Out out) {
+                                             uint32_t b, uint32_t e, Out out, const uint16_t* __restrict__ nfa_row) {
   typedef const __attribute__((address_space(AS))) uint32_t* u32p;
   typedef const __attribute__((address_space(AS))) uint16_t* u16p;
   uint32_t j = 0;
@@ -305,6 +319,12 @@ __device__ inline uint32_t classify_value_as(as_ptr<AS> R, uint32_t nlk, uint32_
       const v4 lo = ((v4p)(R + rel))[0], hi = ((v4p)(R + rel))[1];
       __builtin_memcpy(&d, &lo, 16);
       __builtin_memcpy((uint8_t*)&d + 16, &hi, 16);
+    }
+    if (NFA && d.nfa) {  // an NFA element: its class from the pass's nfa_classify_kernel
+      out(j, (uint32_t)nfa_row[j]);
+      ++j;
+      rel = d.next;
+      continue;
     }
     uint32_t st = d.start;
     // 8-byte windows: the window's dwords, then its 8 byte classes, load as two batches; only the
@@ -391,13 +411,13 @@ __device__ inline uint32_t classify_value_as(as_ptr<AS> R, uint32_t nlk, uint32_
 
 // COL_LV classes of a label value under label-key class k: one per DFA of the key's chain, 0xffff
 // fills the rest of the nlv entries. kv_lds: the region is staged in LDS (else the blob in HBM).
-template <class Out>
+template <bool NFA = false, class Out>
 __device__ inline void classify_value(const Classifiers& C, bool kv_lds, uint32_t k, uint32_t nlv, const uint8_t* __restrict__ bytes,
-                                      uint32_t b, uint32_t e, Out out) {
+                                      uint32_t b, uint32_t e, Out out, const uint16_t* __restrict__ nfa_row = nullptr) {
   uint32_t j = 0;
   if (C.kv && k)
-    j = kv_lds ? classify_value_as<3>((as_ptr<3>)C.kv, C.nlk, k, bytes, b, e, out)
-               : classify_value_as<1>((as_ptr<1>)C.kv, C.nlk, k, bytes, b, e, out);
+    j = kv_lds ? classify_value_as<3, NFA>((as_ptr<3>)C.kv, C.nlk, k, bytes, b, e, out, nfa_row)
+               : classify_value_as<1, NFA>((as_ptr<1>)C.kv, C.nlk, k, bytes, b, e, out, nfa_row);
   for (; j < nlv; ++j) out(j, 0xffffu);
 }
 
@@ -510,6 +530,7 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
   // families compiled into this instantiation (TileArgs::feat): images / trusted-repos, labels,
   // container families (pod-privileged, psp-capabilities, psp-apparmor), group columns
   constexpr bool IMG = (F & kFeatImg) != 0, LBL = (F & kFeatLbl) != 0, CTR = (F & kFeatCtr) != 0, GRP = (F & kFeatGrp) != 0;
+  constexpr bool NFA = (F & kFeatNfa) != 0;  // classifiers with NFA elements (their classes precomputed in HBM)
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
@@ -795,7 +816,8 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
           if (k && classify && t.o_sb[S_LV] && !(t.debug & 2048u)) {
             uint32_t b, e;
             str(S_LV, i, &b, &e);
-            classify_value(C, LDST && t.kv_lds, k, nlv, lds + t.o_sb[S_LV], b, e, [&](uint32_t j, uint32_t c) { lv[j] = (uint16_t)c; });
+            classify_value<NFA>(C, LDST && t.kv_lds, k, nlv, lds + t.o_sb[S_LV], b, e, [&](uint32_t j, uint32_t c) { lv[j] = (uint16_t)c; },
+                                NFA ? a.nfa_lv + (uint64_t)(lb + i) * nlv : nullptr);
           } else {
             for (uint32_t j = 0; j < nlv; ++j) lv[j] = 0xffffu;
           }
@@ -832,8 +854,8 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
           if (classify && (fl & KW_CTR_HAS_IMAGE)) {
             uint32_t b, e;
             str(S_IMG, i, &b, &e);
-            classify_image<true, LDST && KW_IMG_LDSADDR>(C, il, lds + t.o_sb[S_IMG], b, e, [&](uint32_t j, uint32_t c) { ic[j] = (uint16_t)c; },
-                                 t.debug);
+            classify_image<true, LDST && KW_IMG_LDSADDR, NFA>(C, il, lds + t.o_sb[S_IMG], b, e, [&](uint32_t j, uint32_t c) { ic[j] = (uint16_t)c; },
+                                 t.debug, NFA ? a.nfa_img + (uint64_t)(cb + i) * nim : nullptr);
           } else {
             for (uint32_t j = 0; j < nim; ++j) ic[j] = 0;
           }
@@ -1327,8 +1349,9 @@ __global__ void __launch_bounds__(kOverflowThreads)
       if (t.need & (1u << S_IMG)) {
         uint16_t* ic = a.g_img + (uint64_t)c * nim;
         if (fl & KW_CTR_HAS_IMAGE)
-          classify_image<false, false>(C, il, t.s_bytes[S_IMG], t.s_off[S_IMG][c], t.s_off[S_IMG][c + 1],
-                                [&](uint32_t j, uint32_t cl) { ic[j] = (uint16_t)cl; });
+          classify_image<false, false, true>(C, il, t.s_bytes[S_IMG], t.s_off[S_IMG][c], t.s_off[S_IMG][c + 1],
+                                [&](uint32_t j, uint32_t cl) { ic[j] = (uint16_t)cl; }, 0u,
+                                a.nfa_img ? a.nfa_img + (uint64_t)c * nim : nullptr);
         else
           for (uint32_t j = 0; j < nim; ++j) ic[j] = 0;
       }
@@ -1342,8 +1365,8 @@ __global__ void __launch_bounds__(kOverflowThreads)
         const uint32_t k = lit(COL_LK, S_LK, l);
         a.g_lk[l] = (uint16_t)k;
         uint16_t* lv = a.g_lv + (uint64_t)l * nlv;
-        classify_value(C, false, k, nlv, t.s_bytes[S_LV], t.s_off[S_LV][l], t.s_off[S_LV][l + 1],
-                       [&](uint32_t j, uint32_t c) { lv[j] = (uint16_t)c; });
+        classify_value<true>(C, false, k, nlv, t.s_bytes[S_LV], t.s_off[S_LV][l], t.s_off[S_LV][l + 1],
+                             [&](uint32_t j, uint32_t c) { lv[j] = (uint16_t)c; }, a.nfa_lv ? a.nfa_lv + (uint64_t)l * nlv : nullptr);
       }
   }
 }
@@ -1427,6 +1450,113 @@ __global__ void __launch_bounds__(kOverflowThreads)
 }
 
 // ------------------------------------------------------------------------------------------
+// NFA elements (kwdev.hpp DevNfa): patterns whose DFA exceeds the state budget. Before the tile
+// kernel, one thread per entity runs every NFA element of its classifier chains (a Pike VM over the
+// string, lists in the thread's scratch) and stores the element's class where the tile kernel's
+// classification reads it: label values under their key's chain ([label][nlv]), image references
+// under the registry / tag / normalised-image chains ([container][il.n()]). Rare (a pattern has to
+// blow a DFA past kMaxDfaStates), so it is simple rather than fast.
+// ------------------------------------------------------------------------------------------
+constexpr int kNfaThreads = 256;
+
+__global__ void __launch_bounds__(kNfaThreads) nfa_classify_kernel(EvalArgs a, const TileArgs* __restrict__ tp, NfaPass np) {
+  const TileArgs& t = *tp;
+  const uint64_t nthreads = (uint64_t)gridDim.x * kNfaThreads;
+  const uint64_t gtid = (uint64_t)blockIdx.x * kNfaThreads + threadIdx.x;
+  uint32_t* scratch = np.scratch + gtid * np.words_per_thread;
+  uint8_t* subj = (uint8_t*)(scratch + np.nfa_words);
+  for (uint32_t k = 0; k < np.nfa_words; ++k) scratch[k] = 0u;  // marks: generation 0 is never used
+  uint32_t gen = 0;
+  const uint8_t* blob = a.blob;
+  const uint32_t NONE = 0xffffffffu;
+  const uint64_t items = (np.do_lv ? np.nlabels : 0ull) + (np.do_img ? np.nctrs : 0ull);
+  for (uint64_t q = gtid; q < items; q += nthreads) {
+    if (np.do_lv && q < np.nlabels) {
+      const uint64_t l = q;
+      if (!t.kv_blob || !t.lit_blob[COL_LK]) continue;
+      const uint32_t kb = t.s_off[S_LK][l], ke = t.s_off[S_LK][l + 1];
+      const uint32_t k = lit_lookup<false>(blob + t.lit_blob[COL_LK], t.s_bytes[S_LK], kb, ke);
+      if (!k) continue;
+      const uint8_t* R = blob + t.kv_blob;
+      const uint32_t kbase = ((const uint32_t*)R)[t.nlk + k];
+      const uint32_t vb = t.s_off[S_LV][l], ve = t.s_off[S_LV][l + 1];
+      uint32_t j = 0;
+      for (uint32_t rel = ((const uint32_t*)R)[k]; rel; ++j) {
+        const KvDfa& d = *(const KvDfa*)(R + rel);
+        if (d.nfa) {
+          const bool m = nfa_run(blob + d.trans_off, t.s_bytes[S_LV] + vb, ve - vb, scratch, &gen);
+          np.lv[l * np.nlv + j] = (uint16_t)(kbase + d.cbase + (m ? 1u : 0u));
+        }
+        rel = d.next;
+      }
+      continue;
+    }
+    const uint64_t c = np.do_lv ? q - np.nlabels : q;
+    if (!(a.ctr_flags[c] & KW_CTR_HAS_IMAGE)) continue;
+    const uint8_t* bytes = t.s_bytes[S_IMG];
+    const ImageRef r = parse_image(bytes, t.s_off[S_IMG][c], t.s_off[S_IMG][c + 1]);
+    uint16_t* row = np.img + c * np.nim;
+    auto put = [&](const uint8_t* src, uint32_t n, uint32_t at) {
+      for (uint32_t x = 0; x < n; ++x) subj[at + x] = src[x];
+      return at + n;
+    };
+    auto put_c = [&](const char* src, uint32_t at) {
+      for (; *src; ++src) subj[at++] = (uint8_t)*src;
+      return at;
+    };
+    auto run_chain = [&](Col col, uint32_t j, int part) {
+      const uint32_t head = t.dfa_blob[col];
+      for (uint32_t o = head; o; o = ((const DevDfa*)(blob + o))->next, ++j) {
+        const DevDfa& d = *(const DevDfa*)(blob + o);
+        if (d.kind != 1) continue;
+        const uint16_t* acc = (const uint16_t*)(blob + d.acc_off);
+        uint32_t n = 0;
+        if (part == 0) {  // registry (implicit: docker.io)
+          n = r.is_reg ? put(bytes + r.b, r.slash0 - r.b, 0) : put_c("docker.io", 0);
+        } else if (part == 1) {  // effective tag (implicit: latest); a digest-only reference has none
+          if (r.colon != NONE) n = put(bytes + r.colon + 1, r.name_end - r.colon - 1, 0);
+          else if (r.at == NONE) n = put_c("latest", 0);
+          else {
+            row[j] = 0;
+            continue;
+          }
+        } else {  // normalised reference: registry/[library/]path[:tag][@digest]
+          n = r.is_reg ? put(bytes + r.b, r.slash0 - r.b, 0) : put_c("docker.io", 0);
+          subj[n++] = '/';
+          if (r.is_docker && !r.path_slash) n = put_c("library/", n);
+          n = put(bytes + r.rest_b, r.path_end - r.rest_b, n);
+          if (r.eff_tag) {
+            subj[n++] = ':';
+            n = r.colon != NONE ? put(bytes + r.colon + 1, r.name_end - r.colon - 1, n) : put_c("latest", n);
+          }
+          if (r.at != NONE) n = put(bytes + r.at, r.e - r.at, n);
+        }
+        row[j] = acc[nfa_run(blob + d.trans_off, subj, n, scratch, &gen) ? 1 : 0];
+      }
+      return j;
+    };
+    uint32_t j = t.lit_blob[COL_REG] ? 1u : 0u;
+    j = run_chain(COL_REG, j, 0);
+    j += t.lit_blob[COL_TAG] ? 1u : 0u;
+    j = run_chain(COL_TAG, j, 1);
+    run_chain(COL_IMG, j, 2);
+  }
+}
+
+uint32_t nfa_threads(uint64_t items, uint64_t words_per_thread) {
+  constexpr uint64_t kBudget = 256ull << 20;  // scratch bytes
+  uint64_t n = std::min<uint64_t>(std::max<uint64_t>(items, 1), 256ull * 1024);
+  n = std::min<uint64_t>(n, std::max<uint64_t>(kNfaThreads, kBudget / (4 * std::max<uint64_t>(words_per_thread, 1))));
+  return (uint32_t)((n + kNfaThreads - 1) / kNfaThreads * kNfaThreads);
+}
+
+hipError_t launch_nfa_classify(const EvalArgs& a, const TileArgs* d_t, const NfaPass& np, uint32_t threads, hipStream_t s) {
+  if (!np.do_lv && !np.do_img) return hipSuccess;
+  hipLaunchKernelGGL(nfa_classify_kernel, dim3(threads / kNfaThreads), dim3(kNfaThreads), 0, s, a, d_t, np);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
 // Wide policy groups: the members' verdict words of a separate pass -> each group's jump code per
 // row (slots.hpp run_wide_prog), its value stack in this thread's scratch words and its causes in
 // the per-row side data. A row the main pass answered with the bypass word keeps it.
@@ -1489,6 +1619,9 @@ constexpr std::array<const void*, sizeof...(Fs)> tile_fns() {
 const void* tile_fn(bool ldst, bool timing, uint32_t feat) {
   static const auto g = tile_fns<false, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15>();
   static const auto l = tile_fns<true, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15>();
+  if (feat & kFeatNfa)  // the one instantiation with NFA elements: every family (timing runs it too)
+    return ldst ? (const void*)evaluate_tiles_kernel<true, false, kFeatAll | kFeatNfa>
+                : (const void*)evaluate_tiles_kernel<false, false, kFeatAll | kFeatNfa>;
   if (timing) {  // diagnostics: the C2 / C3 / C4 family sets with LDS tables (same registers as the product), else every family
     if (ldst && feat == kFeatImg) return (const void*)evaluate_tiles_kernel<true, true, kFeatImg>;
     if (ldst && feat == (kFeatImg | kFeatGrp)) return (const void*)evaluate_tiles_kernel<true, true, kFeatImg | kFeatGrp>;
@@ -1497,7 +1630,7 @@ const void* tile_fn(bool ldst, bool timing, uint32_t feat) {
   }
   return ldst ? l[feat & kFeatAll] : g[feat & kFeatAll];
 }
-uint32_t tile_feat(const TileArgs& t) { return t.feat & kFeatAll; }
+uint32_t tile_feat(const TileArgs& t) { return t.feat & (kFeatAll | kFeatNfa); }
 
 hipError_t ensure_attrs() {
   int dev = 0;
@@ -1507,9 +1640,10 @@ hipError_t ensure_attrs() {
   std::call_once(g_attr_once[dev], [dev] {
     // allow > 64 KB of dynamic LDS per workgroup (gfx950: 160 KB per CU)
     hipError_t e = hipSuccess;
-    for (int k = 0; k < 64; ++k) {  // (LDS tables, timing, families)
-      const hipError_t ek = hipFuncSetAttribute(tile_fn(k & 1, (k & 2) != 0, (uint32_t)(k >> 2) & kFeatAll),
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    for (int k = 0; k < 68; ++k) {  // (LDS tables, timing, families; then the two NFA instantiations)
+      const uint32_t feat = k < 64 ? (uint32_t)(k >> 2) & kFeatAll : (kFeatAll | kFeatNfa);
+      const hipError_t ek =
+          hipFuncSetAttribute(tile_fn(k & 1, (k & 2) != 0, feat), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e == hipSuccess) e = ek;
     }
     g_attr_err[dev] = e;

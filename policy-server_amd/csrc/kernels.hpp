@@ -35,6 +35,9 @@ struct EvalArgs {
   uint32_t* sched;  // per-XCD tile counters (256 u32 + 256 u32 done counts), nullptr = static schedule
   // overflow path: per-string classes in HBM (absolute entity indices), the wide-argument list
   uint16_t *g_ns, *g_aa, *g_img, *g_capadd, *g_capdrop, *g_lk, *g_lv;
+  // NFA elements (kwdev.hpp DevNfa): their classes, computed by nfa_classify_kernel before the tile
+  // kernel, [label][nlv] and [container][il.n()] at the element's chain position (nullptr = none)
+  const uint16_t *nfa_lv, *nfa_img;
   uint32_t* wide_count;
   WideRec* wide_rec;
   uint32_t wide_cap;
@@ -64,6 +67,9 @@ constexpr uint32_t kSlotRows = 64;
 constexpr uint32_t kSlotThreads = KW_THREADS;
 // Families a tile-kernel instantiation carries (TileArgs::feat).
 constexpr uint32_t kFeatImg = 1, kFeatLbl = 2, kFeatCtr = 4, kFeatGrp = 8, kFeatAll = 15;
+// A pass whose classifiers hold NFA elements runs the one instantiation that reads their classes
+// (kFeatAll | kFeatNfa): no other instantiation carries that code.
+constexpr uint32_t kFeatNfa = 16;
 #ifndef KW_PREFETCH  // tile kernel: warm L2 with the next tile's staged ranges during this tile's walk.
 #define KW_PREFETCH 0   // Off: since staging reads the descriptor from LDS, the prefetch costs P2 more
 #endif                  // than it saves P0 (r02 s60: C4 0.3294 vs 0.3442 ms, C6 -1.8 %, C2 +0.6 %)
@@ -177,5 +183,23 @@ hipError_t launch_wide_groups(const WideGroupPass& w, uint32_t grid, hipStream_t
 
 hipError_t launch_overflow(const EvalArgs& a, const TileArgs* d_t, const uint32_t* d_overflow, uint32_t n_overflow,
                            hipStream_t s);
+
+// The NFA elements of a pass (kwdev.hpp DevNfa): every label value under its key's chain and every
+// image reference under the registry / tag / image chains, one thread per entity, a Pike VM per
+// element with its lists in `scratch` (words_per_thread u32 per thread of the grid: the largest
+// program's nfa_scratch_words, then room for a normalised image reference of subj_bytes).
+struct NfaPass {
+  uint16_t* lv;   // [nlabels][nlv]
+  uint16_t* img;  // [nctrs][nim]
+  uint32_t* scratch;
+  uint64_t words_per_thread;
+  uint32_t nfa_words, subj_bytes;
+  uint32_t nlv, nim;
+  uint64_t nlabels, nctrs;
+  uint32_t do_lv, do_img;
+};
+hipError_t launch_nfa_classify(const EvalArgs& a, const TileArgs* d_t, const NfaPass& np, uint32_t threads, hipStream_t s);
+// threads of the NFA pass's grid for `items` entities within a scratch budget
+uint32_t nfa_threads(uint64_t items, uint64_t words_per_thread);
 
 }  // namespace kw

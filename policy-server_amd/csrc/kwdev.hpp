@@ -166,7 +166,7 @@ struct alignas(16) DevCol {
   uint32_t ndfa;       // DFAs in the chain (COL_LV: the longest per-key chain)
   uint32_t dfa_bytes;  // bytes of the whole chain (COL_LV: of the per-key region)
   uint32_t lit_bytes;
-  uint32_t pad;
+  uint32_t flags;      // bit 0: the chain has NFA elements (DevDfa::kind / KvDfa::nfa)
 };
 
 // ---- Patterns whose DFA exceeds the state budget (kMaxDfaStates: e.g. `a[a-z]{14}b` searched
@@ -269,7 +269,8 @@ struct alignas(16) DevHeader {
   uint32_t bypass_cls;     // COL_NS class of the always-accept namespace, 0 = none
   uint32_t docker_io_cls;  // COL_REG literal class of "docker.io" (implicit registry), 0 = none
   uint32_t latest_cls;     // COL_TAG literal class of "latest" (implicit tag), 0 = none
-  uint32_t pad[3];
+  uint32_t nfa_words;      // the largest NFA element's scratch in u32 words (nfa_scratch_words), 0 = none
+  uint32_t pad[2];
 };
 
 }  // namespace kw

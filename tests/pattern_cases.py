@@ -1,0 +1,84 @@
+"""Policies and AdmissionReviews for the pattern-dialect and automaton-size cases (VERDICT r03
+"What's weak" 2, "What's missing" 1-2): Rust-`regex` label constraints ((?:), (?i), \\b, \\A / \\z,
+classes with set operations, verbose mode) and patterns whose DFA exceeds the state budget (the
+label regex `a[a-z]{14}b`, the image glob `*a?????????????????`, a registry and a tag glob of the
+same shape), which must evaluate as NFA elements instead of failing the environment, plus refused
+constructs (\\p{L}, look-around) that are init errors on both sides."""
+import json
+
+MOD = "registry://ghcr.io/kubewarden/policies/"
+
+LABEL_REGEXES = {
+    "app": "a[a-z]{14}b",                        # beyond the DFA state budget (NFA element)
+    "tier": "(?i)^(?:front|back)end$",
+    "env": "\\A(?:dev|prod)\\z",
+    "team": "\\bteam\\b",
+    "owner": "[[:lower:]&&[^aeiou]]{3}",
+    "version": "(?x) ^ v \\d+ (?: \\. \\d+ )* $  # semver-ish",
+    "region": "^(?:eu|us)-(?:west|east)-\\d$",
+    "zone": "^.{1,3}$",                          # code points, not bytes
+    "release": "[a-z].{12}[0-9a-z]",            # NFA element as well
+    "component": "\\<web\\>|\\b{start}db",
+    "debug": "^(?m)$",
+}
+
+
+def policies():
+    return {
+        "labels-dialect": {"module": MOD + "safe-labels:v0.1.14",
+                           "settings": {"constrained_labels": LABEL_REGEXES}},
+        # the VERDICT's exact repro: one blow-up constraint alone
+        "labels-blowup": {"module": MOD + "safe-labels:v0.1.14",
+                          "settings": {"constrained_labels": {"app": "a[a-z]{14}b"}}},
+        "labels-refused": {"module": MOD + "safe-labels:v0.1.14",
+                           "settings": {"constrained_labels": {"app": "\\p{L}+"}}},
+        "labels-lookaround": {"module": MOD + "safe-labels:v0.1.14",
+                              "settings": {"constrained_labels": {"tier": "(?<=a)b"}}},
+        "images-blowup": {"module": MOD + "trusted-repos-policy:v0.1.12",
+                          "settings": {"images": {"reject": ["*a?????????????????"]}}},
+        "registries-blowup": {"module": MOD + "trusted-repos-policy:v0.1.12",
+                              "settings": {"registries": {"allow": ["*e??????????????", "docker.io", "ghcr.io"]},
+                                           "tags": {"reject": ["*1??????????????", "latest"]}}},
+        "images-mixed": {"module": MOD + "trusted-repos-policy:v0.1.12",
+                         "settings": {"images": {"allow": ["docker.io/library/*", "*/*b???????????????",
+                                                           "ghcr.io/*"]}}},
+    }
+
+
+VALUES = {
+    "app": ["aabcdefghijklmnb", "xaqwertyuiopasdfbx", "ab", "a" * 16 + "b", "Aabcdefghijklmnb", "aabcdefghijklmnB"],
+    "tier": ["frontend", "BACKEND", "Frontend ", "middle"],
+    "env": ["dev", "prod", "dev\n", "xdev"],
+    "team": ["team", "team-a", "my team", "teams", "ateam"],
+    "owner": ["xyz", "abc", "bcd", "bcé"],
+    "version": ["v1", "v1.2.3", "v", "1.2"],
+    "region": ["eu-west-1", "us-east-2", "eu-north-1", "EU-west-1"],
+    "zone": ["é", "ab", "abcd", "中中中", "𝄞𝄞"],
+    "release": ["abcdefghijklm0", "a0000000000000z", "short", "0bcdefghijklmnop"],
+    "component": ["web", "a web", "webx", "db", "xdb"],
+    "debug": ["", "x"],
+}
+
+IMAGES = ["nginx", "ghcr.io/kubewarden/policy-server:v1.2.3", "quay.io/aaaaaaaaaaaaaaaaaaaaaaaaa:latest",
+          "docker.io/library/busybox@sha256:" + "a" * 64, "registry.example.com:5000/team/app:1abcdefghijklmno",
+          "my-registry.example.org/x/y", "localhost/abcdefghijklmnopqrstuvwxyz", "ghcr.io/a/b:1",
+          "reg-001.example.com/team-01/app:v2.0.1", "docker.io/bbbbbbbbbbbbbbbbbbbbbbbb"]
+
+
+def reviews(n=120):
+    """AdmissionReview documents cycling through the values and images above."""
+    docs = []
+    keys = sorted(VALUES)
+    for r in range(n):
+        labels = {}
+        for k, key in enumerate(keys):
+            if (r + k) % 3 != 2:
+                vals = VALUES[key]
+                labels[key] = vals[(r * 7 + k) % len(vals)]
+        ctrs = [{"name": f"c{i}", "image": IMAGES[(r + 3 * i) % len(IMAGES)]} for i in range(1 + r % 3)]
+        docs.append({"request": {"uid": f"u{r}", "kind": {"group": "", "version": "v1", "kind": "Pod"},
+                                 "resource": {"group": "", "version": "v1", "resource": "pods"},
+                                 "operation": "CREATE", "userInfo": {}, "namespace": "default",
+                                 "object": {"kind": "Pod", "metadata": {"labels": labels},
+                                            "spec": {"containers": ctrs}}}})
+    return [json.dumps(d) for d in docs]
