@@ -12,7 +12,8 @@ producing 64M verdict words. Inputs are resident in HBM before the timed region.
 
 Multi-GPU: one process per GPU; rank 0 compiles the policy set and broadcasts the compiled-table
 blob once over RCCL (torch.distributed "nccl" = RCCL on ROCm); every rank evaluates its own request
-shard (weak scaling, no collective on the per-request path). Timing: barrier + synchronize on both
+shard (weak scaling: --rows per GPU, the default; strong scaling: --total-rows T, one job of T
+requests sharded across the GPUs; no collective on the per-request path). Timing: barrier + synchronize on both
 sides of exactly K steps, max over ranks. Rank 0 prints one JSON line.
 """
 import argparse
@@ -56,14 +57,16 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rows", type=int, default=None, help="requests per GPU (default: the config's)")
+    ap.add_argument("--rows", type=int, default=None, help="requests per GPU, weak scaling (default: the config's)")
+    ap.add_argument("--total-rows", type=int, default=None,
+                    help="a fixed job of this many requests sharded across the GPUs (strong scaling)")
     ap.add_argument("--config", default="c4_64", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (rank 0), about 10-30 s")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-modes", action="store_true", help="skip the end-to-end / flatten timings")
     args = ap.parse_args()
     args.synth, default_rows, workload = CONFIGS[args.config]
-    if args.rows is None:
+    if args.rows is None and args.total_rows is None:
         args.rows = default_rows
 
     import numpy as np
@@ -98,10 +101,14 @@ def main():
     npol = len(ids)
 
     t0 = time.time()
-    from kwgpu.dist import synth_bounds
+    from kwgpu.dist import job_bounds
 
-    # the job is world x rows requests, split into shards of equal work (1 + containers per request)
-    bounds = synth_bounds(args.synth, world * args.rows, world, SEED)
+    # the job: world x rows requests (weak scaling) or total_rows requests (strong scaling), split into
+    # shards of equal work (1 + containers per request)
+    if args.total_rows is not None:
+        bounds, job_rows, scaling = job_bounds(args.synth, world, SEED, total_rows=args.total_rows)
+    else:
+        bounds, job_rows, scaling = job_bounds(args.synth, world, SEED, rows_per_rank=args.rows)
     row0, nrows = int(bounds[rank]), int(bounds[rank + 1] - bounds[rank])
     syn = K.SynthBatch(args.synth, nrows, seed=SEED, row0=row0)
     batch = syn.batch().to_device(device)
@@ -125,7 +132,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed * 1e3 / args.steps
-    value = world * args.rows * args.steps / elapsed
+    value = job_rows * args.steps / elapsed
 
     # per-kernel device time with HIP events on the launch stream
     tm = batch.timed(env, ids, warmup=2, reps=max(5, args.steps))
@@ -161,10 +168,13 @@ def main():
         modes = None if args.no_host_modes else host_modes(env, ids, syn, device, args)
         result = {
             "metric": METRIC, "value": value, "unit": "requests/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": scaling,
             "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "config": {"workload": workload.format(rows=args.rows, npol=npol), "config": args.config,
-                       "requests_per_gpu": args.rows, "policies": npol, "parallelism": f"dp{world} (request shards)"},
+            "config": {"workload": (workload.format(rows=args.rows, npol=npol) if scaling == "weak" else
+                                    workload.format(rows=job_rows, npol=npol).replace(" per GPU", "")
+                                    + f", one job sharded across {world} GPU(s)"),
+                       "config": args.config, "requests_per_gpu": job_rows / world, "total_requests": job_rows,
+                       "policies": npol, "parallelism": f"dp{world} (request shards)"},
             "evaluations_per_s": value * npol,
             "kernel_ms": {"classify": tm.classify_ms, "evaluate": tm.evaluate_ms, "total": tm.total_ms},
             "roofline": {"kernel": "evaluate_tiles_kernel",
@@ -273,7 +283,7 @@ def traffic(args):
             t = json.load(f)
     except (OSError, ValueError):
         return None
-    if t.get("config") != args.config or t.get("rows") != args.rows:
+    if t.get("config") != args.config or t.get("rows") != (args.rows if args.rows is not None else args.total_rows):
         return None
     return t.get("bytes_per_launch")
 

@@ -60,6 +60,20 @@ def synth_bounds(config, total_rows, world, seed):
     return np.array(out[:], dtype=np.int64)
 
 
+def job_bounds(config, world, seed, rows_per_rank=None, total_rows=None):
+    """Shard bounds of a bench job (synth_bounds over the job's rows): weak scaling (the default) is
+    `rows_per_rank` requests per rank, world * rows_per_rank in all; strong scaling is a fixed job of
+    `total_rows` requests whatever the world size (BASELINE C4 "1M requests sharded across 8", C5 10M
+    over 1/2/4/8). Returns (bounds, total_rows, scaling)."""
+    if (rows_per_rank is None) == (total_rows is None):
+        raise ValueError("exactly one of rows_per_rank / total_rows")
+    if total_rows is not None:
+        if total_rows < 0:
+            raise ValueError("total_rows must be >= 0")
+        return synth_bounds(config, total_rows, world, seed), int(total_rows), "strong"
+    return synth_bounds(config, world * rows_per_rank, world, seed), int(world * rows_per_rank), "weak"
+
+
 def balanced_shard(config, rows_per_rank, world, rank, seed):
     """Weak scaling with balanced work: the job is world * rows_per_rank synthetic requests, split by
     synth_bounds; returns (row0, n) of this rank's shard."""

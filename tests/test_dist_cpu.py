@@ -116,3 +116,27 @@ def test_blob_broadcast_shards_and_gathered_verdicts(tmp_path, world, split):
     gathered = np.load(tmp_path / "gathered.npy")
     expect = oe.eval(whole, ids).reshape(world * ROWS, len(ids))
     assert gathered.shape == expect.shape and np.array_equal(gathered, expect)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+def test_job_bounds_weak_and_strong(world):
+    """bench.py's shard arithmetic (kwgpu.dist.job_bounds): weak scaling is world x rows requests,
+    strong scaling (--total-rows) a fixed job; either way the bounds partition the job's rows in
+    order, and every shard's work (1 + containers per row, C5's Zipf counts) is within one row's
+    weight of total / world."""
+    import kwgpu as K
+    from kwgpu.dist import job_bounds
+    total = 997
+    for kw in ({"total_rows": total}, {"rows_per_rank": total // world}):
+        bounds, rows, scaling = job_bounds(5, world, SEED, **kw)
+        assert scaling == ("strong" if "total_rows" in kw else "weak")
+        assert rows == (total if "total_rows" in kw else world * (total // world))
+        assert len(bounds) == world + 1 and bounds[0] == 0 and bounds[-1] == rows
+        assert all(bounds[k] <= bounds[k + 1] for k in range(world))
+        syn = K.SynthBatch(5, rows, seed=SEED)
+        ctr = np.ctypeslib.as_array(syn.soa().ctr_off, shape=(rows + 1,)).astype(np.int64)
+        w = 1 + np.diff(ctr)
+        loads = [int(w[bounds[k]:bounds[k + 1]].sum()) for k in range(world)]
+        assert max(loads) - min(loads) <= 2 * int(w.max()), loads
+    with pytest.raises(ValueError):
+        job_bounds(5, world, SEED)
