@@ -490,18 +490,6 @@ def compile_settings(fam, s, olib):
     return L, flags
 
 
-def engine_limit_error(pid, fam, L):
-    """The product's per-policy limits of its bit-parallel evaluation (not reference
-    behaviour: a bootstrap failure of that policy): 64 distinct mandatory labels, 63 distinct
-    required-drop / default-add capabilities (+ "ALL")."""
-    if fam == F_LABELS and len(set(L[1])) > 64:
-        return f"bootstrap failure: {pid}: more than 64 distinct mandatory_labels (engine limit)"
-    if fam == F_CAPS and len(set(L[1]) | set(L[2]) | {"ALL"}) > 64:
-        return (f"bootstrap failure: {pid}: more than 63 distinct required-drop / default-add capabilities "
-                f"(engine limit)")
-    return None
-
-
 # ----------------------------------------------------------------------------- group expressions
 # The rhai script subset of policy-group expressions (DESIGN.md §2; PolicyGroupEvaluator, upstream
 # policy-evaluator v0.24.0 / rhai 1.21.0, absent from the reference tree; pinned only by
@@ -1039,7 +1027,6 @@ class OracleEnv:
                 p["family"] = fam
                 try:
                     p["lists"], p["flags"] = compile_settings(fam, p["settings"], L)
-                    err = engine_limit_error(p["id"], fam, p["lists"])
                 except ValueError as ex:
                     err = f"Policy settings are invalid: {ex}"
             if err is not None:
@@ -1054,6 +1041,7 @@ class OracleEnv:
             if not p["group"]:
                 continue
             p["expr_error"] = None
+            p["pyscript"] = False
             p["ast"] = None
             p["script"] = None
             p["table"] = None
@@ -1078,9 +1066,8 @@ class OracleEnv:
                         raise ExprError("policy group expression exceeds the engine's limits (65535 members, value "
                                         "stack 65536)")
                     p["ast"] = t
-                elif len(names) > 16:
-                    raise ExprError("policy group expression uses let / if / string / integer values with more "
-                                    "than 16 members, which the engine does not evaluate")
+                elif len(names) > 16:  # too many members for a truth table: run_script per row (_pyscript)
+                    p["pyscript"] = True
                 else:  # every vector of member results: value, error, causes (the C half looks it up)
                     tab = []
                     for mask in range(1 << len(names)):
@@ -1116,7 +1103,8 @@ class OracleEnv:
                 o.n[k] = len(items)
                 o.l[k] = C.cast(arr, C.POINTER(C.c_char_p))
             if p["group"]:
-                o.expr_error = 1 if p["expr_error"] else 0
+                # (a _pyscript group: the C half answers GROUP_EXPR, Python replaces its words)
+                o.expr_error = 1 if (p["expr_error"] or p["pyscript"]) else 0
                 mem = (C.c_int32 * max(len(p["members"]), 1))(*p["members"])
                 self._keep.append(mem)
                 o.n_members = len(p["members"])
@@ -1148,10 +1136,57 @@ class OracleEnv:
             raise KeyError(f"unknown policy: {policy_id}")
         return self.ids[policy_id]
 
+    # ---- groups beyond the bool subset with more than 16 members: the C half has no truth table for
+    # them, so their words come from run_script (this file's own interpreter) over the members' own
+    # evaluations, composed like kworacle.c detail() composes a group's word
+    @staticmethod
+    def _group_word(P, reason, mask, origin):
+        n = len(P["members"])
+        arg16 = 0 if reason != R_GROUP else (0xFFFF if n > 15 else mask)
+        v = (reason << 8) | (arg16 << 16)
+        allowed = reason == 0
+        fst, fallowed = (0 if allowed else 1), allowed
+        if origin == VALIDATE and P["mode"] == MONITOR:
+            fst, fallowed = 0, True
+        if allowed:
+            v |= 1  # V_ALLOWED
+        if fallowed:
+            v |= 4  # F_ALLOWED
+        return v | (fst << 3)
+
+    def _pyscript(self, P, member_ok):
+        """-> (reason, cause mask, cause slots) of a _pyscript group over its members' results."""
+        err, value, called = run_script(P["script"], member_ok)
+        if err is not None:
+            return R_GROUP_EXPR, 0, []
+        if value:
+            return 0, 0, []
+        causes = [c for c in called if not member_ok[c]]
+        return R_GROUP, sum(1 << c for c in causes), causes
+
+    def _member_ok(self, P, words):
+        return [bool(w & 1) and not (w & 2) for w in words]
+
     def eval(self, soa, policies, origin=VALIDATE, rows=None, threads=1, cpus=None):
         """Verdict words for rows x policies (numpy uint32, row-major); cpus: pin thread t to CPU
         cpus[t]."""
         idx = [self.lookup(p) if isinstance(p, str) else p for p in policies]
+        out = self._eval_c(soa, idx, origin, rows, threads, cpus)
+        py = [j for j, i in enumerate(idx) if self.pol[i]["group"] and self.pol[i].get("pyscript")]
+        if py:
+            n = soa.n_requests if rows is None else rows
+            w = out.reshape(n, len(idx))
+            for j in py:
+                P = self.pol[idx[j]]
+                mw = self._eval_c(soa, P["members"], origin, rows, threads, cpus).reshape(n, len(P["members"]))
+                for r in range(n):
+                    if w[r, j] & 0x20:  # the namespace bypass word stays
+                        continue
+                    reason, mask, _ = self._pyscript(P, self._member_ok(P, mw[r]))
+                    w[r, j] = self._group_word(P, reason, mask, origin)
+        return out
+
+    def _eval_c(self, soa, idx, origin, rows, threads, cpus):
         n = soa.n_requests if rows is None else rows
         arr = (C.c_int32 * len(idx))(*idx)
         out = np.zeros(n * len(idx), dtype=np.uint32)
@@ -1228,8 +1263,17 @@ class OracleEnv:
         bypass, causes (member slots))."""
         d = _ODetail()
         olib().orc_eval_detail(self._h, C.byref(soa), pidx, origin, row, C.byref(d))
-        return {"word": d.word, "reason": d.reason, "arg": d.arg, "mutated": bool(d.mutated), "bypass": bool(d.bypass),
-                "causes": list(d.causes[:d.ncauses])}
+        out = {"word": d.word, "reason": d.reason, "arg": d.arg, "mutated": bool(d.mutated), "bypass": bool(d.bypass),
+               "causes": list(d.causes[:d.ncauses])}
+        P = self.pol[pidx]
+        if P["group"] and P.get("pyscript") and not out["bypass"]:
+            ok = []
+            for m in P["members"]:
+                md = self.detail(soa, row, m, origin)
+                ok.append(md["reason"] == 0 and not md["mutated"])
+            reason, mask, causes = self._pyscript(P, ok)
+            out.update(word=self._group_word(P, reason, mask, origin), reason=reason, arg=mask, causes=causes)
+        return out
 
     def response_doc(self, soa, row, pidx, origin=VALIDATE, doc=None):
         """AdmissionResponse dict of (row, policy) derived from the oracle's own evaluation of the

@@ -538,16 +538,24 @@ void plan_wide_groups(const Env& E, const std::vector<int32_t>& list, const std:
   std::map<int32_t, uint32_t> mcol;
   for (uint32_t j = 0; j < (uint32_t)list.size(); ++j) {
     const PolicyRec& P = E.pol[(size_t)list[j]];
-    if (!P.is_group || P.init_error || !P.prog.valid || P.prog.eval_error || !P.prog.wide) continue;
+    const bool split = !P.parts.empty() && !P.init_error;
+    if (!split && (!P.is_group || P.init_error || !P.prog.valid || P.prog.eval_error || !P.prog.wide)) continue;
     WideGroupArgs g;
     memset(&g, 0, sizeof(g));
+    while (W.progs.size() % 4) W.progs.push_back(0);
     g.prog_off = (uint32_t)W.progs.size();
-    g.prog_len = (uint32_t)P.prog.code.size();
-    W.progs.insert(W.progs.end(), P.prog.code.begin(), P.prog.code.end());
+    if (split) {  // the parts' index offsets (u32 each)
+      g.prog_len = (uint32_t)(P.part_off.size() * 4);
+      W.progs.insert(W.progs.end(), (const uint8_t*)P.part_off.data(), (const uint8_t*)(P.part_off.data() + P.part_off.size()));
+    } else {
+      g.prog_len = (uint32_t)P.prog.code.size();
+      W.progs.insert(W.progs.end(), P.prog.code.begin(), P.prog.code.end());
+    }
     g.col = rows_code ? (*rows_code)[j] : j;
-    g.nmem = (uint32_t)P.members.size();
+    const std::vector<int32_t>& mem = split ? P.parts : P.members;
+    g.nmem = (uint32_t)mem.size();
     g.midx_off = (uint32_t)W.midx.size();
-    for (int32_t m : P.members) {
+    for (int32_t m : mem) {
       auto it = mcol.find(m);
       if (it == mcol.end()) {
         it = mcol.emplace(m, (uint32_t)W.members.size()).first;
@@ -555,13 +563,25 @@ void plan_wide_groups(const Env& E, const std::vector<int32_t>& list, const std:
       }
       W.midx.push_back(it->second);
     }
-    g.okw = finish_word(P.mode, 0, origin, 0, 0, false);
-    g.rejb = finish_word(P.mode, 0, origin, KW_R_GROUP, kArgWide, false);
-    g.cause_words = (g.nmem + 63u) / 64u;
+    if (split) {  // a plain policy's words (slotplan.cpp CK_PLAIN), the reason and argument from its parts
+      g.kind = P.family == FAM_CAPABILITIES ? 3u : 2u;
+      g.okw = finish_word(P.mode, P.allowed_to_mutate, origin, 0, 0, false);
+      g.mutw = finish_word(P.mode, P.allowed_to_mutate, origin, 0, 0, true);
+      g.rejb = finish_word(P.mode, P.allowed_to_mutate, origin, 1, 0, false) & ~0xff00u;
+      g.cause_words = 0;
+    } else {
+      g.okw = finish_word(P.mode, 0, origin, 0, 0, false);
+      g.rejb = finish_word(P.mode, 0, origin, KW_R_GROUP, kArgWide, false);
+      g.errw = finish_word(P.mode, 0, origin, KW_R_GROUP_EXPR, 0, false);
+      g.kind = P.prog.script ? 1u : 0u;
+      g.cause_words = (g.nmem + 63u) / 64u;
+    }
     // all pairs: every wide column has its own words in a row; rows mode: a row has one column
     g.cause_off = rows_code ? 0u : W.cause_stride;
     W.cause_stride = rows_code ? std::max(W.cause_stride, g.cause_words) : W.cause_stride + g.cause_words;
-    W.stack_words = std::max(W.stack_words, (P.prog.depth + 63u) / 64u);
+    if (!split)
+      W.stack_words = std::max<uint32_t>(W.stack_words, P.prog.script ? (uint32_t)run_script_words(P.prog.code.data())
+                                                                       : (P.prog.depth + 63u) / 64u);
     W.groups.push_back(g);
     W.policy.push_back(list[j]);
   }
@@ -1369,7 +1389,7 @@ int validate_common(const kw_env* env, kw_batch* kb, const int32_t* policies, ui
   if (origin != KW_ORIGIN_VALIDATE && origin != KW_ORIGIN_AUDIT) return KW_E_ARG;
   DeviceBatch& D = *kb->dev;
   HIPCHK(hipSetDevice(D.device));
-  const int32_t np = (int32_t)E.pol.size();
+  const int32_t np = (int32_t)E.nvisible;  // (the hidden parts of split policies are not addressable)
   uint64_t npairs;
   if (row_policy) {
     for (uint64_t r = 0; r < kb->b.n; ++r)
@@ -1468,20 +1488,20 @@ int kw_env_lookup(const kw_env* env, const char* id, size_t len, int32_t* idx) {
   return env_lookup(env->e, std::string(id, len), idx).code;
 }
 
-int kw_env_policy_count(const kw_env* env) { return env ? (int)env->e.pol.size() : -1; }
+int kw_env_policy_count(const kw_env* env) { return env ? (int)env->e.nvisible : -1; }
 
 int kw_env_policy_id(const kw_env* env, int32_t idx, char* buf, size_t cap) {
-  if (!env || idx < 0 || (size_t)idx >= env->e.pol.size()) return KW_E_ARG;
+  if (!env || idx < 0 || (size_t)idx >= env->e.nvisible) return KW_E_ARG;
   return put_out(env->e.pol[(size_t)idx].id, buf, cap, nullptr);
 }
 
 int kw_env_is_group(const kw_env* env, int32_t idx) {
-  if (!env || idx < 0 || (size_t)idx >= env->e.pol.size()) return -1;
+  if (!env || idx < 0 || (size_t)idx >= env->e.nvisible) return -1;
   return env->e.pol[(size_t)idx].is_group ? 1 : 0;
 }
 
 int kw_env_get_policy_mode(const kw_env* env, int32_t idx, int* mode) {
-  if (!env || !mode || idx < 0 || (size_t)idx >= env->e.pol.size()) return KW_E_ARG;
+  if (!env || !mode || idx < 0 || (size_t)idx >= env->e.nvisible) return KW_E_ARG;
   const PolicyRec& r = env->e.pol[(size_t)idx];
   if (!r.registered) return KW_E_NOT_FOUND;
   *mode = r.mode;
@@ -1489,7 +1509,7 @@ int kw_env_get_policy_mode(const kw_env* env, int32_t idx, int* mode) {
 }
 
 int kw_env_get_policy_allowed_to_mutate(const kw_env* env, int32_t idx, int* allowed) {
-  if (!env || !allowed || idx < 0 || (size_t)idx >= env->e.pol.size()) return KW_E_ARG;
+  if (!env || !allowed || idx < 0 || (size_t)idx >= env->e.nvisible) return KW_E_ARG;
   const PolicyRec& r = env->e.pol[(size_t)idx];
   if (!r.registered) return KW_E_NOT_FOUND;
   *allowed = r.allowed_to_mutate ? 1 : 0;
@@ -1502,7 +1522,7 @@ int kw_env_should_always_accept_requests_made_inside_of_namespace(const kw_env* 
 }
 
 int kw_env_policy_initialization_error(const kw_env* env, int32_t idx, char* buf, size_t cap) {
-  if (!env || idx < 0 || (size_t)idx >= env->e.pol.size()) return -1;
+  if (!env || idx < 0 || (size_t)idx >= env->e.nvisible) return -1;
   const PolicyRec& r = env->e.pol[(size_t)idx];
   if (!r.init_error) return 0;
   put_err(buf, cap, r.init_message);
@@ -1510,14 +1530,14 @@ int kw_env_policy_initialization_error(const kw_env* env, int32_t idx, char* buf
 }
 
 int kw_env_validate_settings(const kw_env* env, int32_t idx, char* buf, size_t cap) {
-  if (!env || idx < 0 || (size_t)idx >= env->e.pol.size()) return KW_E_ARG;
+  if (!env || idx < 0 || (size_t)idx >= env->e.nvisible) return KW_E_ARG;
   Status st = env_validate_settings(env->e, idx);
   if (!st.ok()) put_err(buf, cap, st.message);
   return st.code;
 }
 
 int kw_env_group_members(const kw_env* env, int32_t group, int32_t* out, int cap) {
-  if (!env || group < 0 || (size_t)group >= env->e.pol.size()) return -1;
+  if (!env || group < 0 || (size_t)group >= env->e.nvisible) return -1;
   const PolicyRec& r = env->e.pol[(size_t)group];
   int n = (int)r.members.size();
   for (int i = 0; i < n && i < cap; ++i) out[i] = r.members[(size_t)i];
@@ -1732,13 +1752,21 @@ int kw_debug_host_walk(const kw_env* env, const kw_batch* kb, const int32_t* pol
       for (const WideGroupArgs& g : W.groups) {
         uint32_t* dst = out + r * npol + g.col;
         if (*dst == kBypassWord) continue;
-        const bool v = run_wide_prog(
-            W.progs.data() + g.prog_off, g.prog_len, stack.data(),
-            [&](uint32_t m) {
-              const uint32_t x = mw[r * nm + W.midx[g.midx_off + m]];
-              return (x & KW_V_ALLOWED) && !(x & KW_V_MUTATED);
-            },
-            [](uint32_t) {});
+        auto ok = [&](uint32_t m) {
+          const uint32_t x = mw[r * nm + W.midx[g.midx_off + m]];
+          return (x & KW_V_ALLOWED) && !(x & KW_V_MUTATED);
+        };
+        if (g.kind == 1) {
+          const int v = run_script_prog(W.progs.data() + g.prog_off, stack.data(), ok, [](uint32_t) {});
+          *dst = v == 1 ? g.okw : v == 0 ? g.rejb : g.errw;
+          continue;
+        }
+        if (g.kind >= 2) {
+          *dst = combine_parts(g, (const uint32_t*)(W.progs.data() + g.prog_off),
+                               [&](uint32_t m) { return mw[r * nm + W.midx[g.midx_off + m]]; });
+          continue;
+        }
+        const bool v = run_wide_prog(W.progs.data() + g.prog_off, g.prog_len, stack.data(), ok, [](uint32_t) {});
         *dst = v ? g.okw : g.rejb;
       }
   }
@@ -2263,7 +2291,7 @@ int kw_validate_timed(const kw_env* env, kw_batch* b, const int32_t* policies, u
 
 int kw_format_response(const kw_env* env, const kw_batch* b, uint64_t row, int32_t policy, uint32_t verdict,
                        const uint32_t* member_verdicts, char* buf, size_t cap, size_t* need) {
-  if (!env || !b || row >= b->b.n || policy < 0 || (size_t)policy >= env->e.pol.size()) return KW_E_ARG;
+  if (!env || !b || row >= b->b.n || policy < 0 || (size_t)policy >= env->e.nvisible) return KW_E_ARG;
   std::string out;
   Status st = format_response(env->e, b->b, row, policy, verdict, member_verdicts, &out);
   if (!st.ok()) {
@@ -2276,7 +2304,7 @@ int kw_format_response(const kw_env* env, const kw_batch* b, uint64_t row, int32
 int kw_format_response_doc(const kw_env* env, const kw_batch* b, uint64_t row, int32_t policy, uint32_t verdict,
                            const uint32_t* member_verdicts, const char* doc, size_t doc_len, int doc_kind, char* buf,
                            size_t cap, size_t* need) {
-  if (!env || !b || row >= b->b.n || policy < 0 || (size_t)policy >= env->e.pol.size() || (!doc && doc_len))
+  if (!env || !b || row >= b->b.n || policy < 0 || (size_t)policy >= env->e.nvisible || (!doc && doc_len))
     return KW_E_ARG;
   std::string out;
   Status st = format_response(env->e, b->b, row, policy, verdict, member_verdicts, &out, doc, doc_len, doc_kind);
@@ -2358,7 +2386,7 @@ int kw_metrics_record(kw_metrics* m, const kw_env* env, const kw_batch* b, const
   if (!m || !env || !b || (n && (!rows || !policies || !verdicts || !latency_ms))) return KW_E_ARG;
   if (origin != KW_ORIGIN_VALIDATE && origin != KW_ORIGIN_AUDIT) return KW_E_ARG;
   for (size_t i = 0; i < n; ++i)
-    if (rows[i] >= b->b.n || policies[i] < 0 || (size_t)policies[i] >= env->e.pol.size()) return KW_E_ARG;
+    if (rows[i] >= b->b.n || policies[i] < 0 || (size_t)policies[i] >= env->e.nvisible) return KW_E_ARG;
   for (size_t i = 0; i < n; ++i) m->m.record(env->e, b->b, rows[i], policies[i], verdicts[i], origin, latency_ms[i]);
   return KW_OK;
 }

@@ -801,22 +801,105 @@ static Status bootstrap(const JDoc& d, int64_t settings, PolicyRec* rec) {
   std::string err;
   if (!compile_settings(d, settings, rec, &err))
     return {KW_E_INIT, "Policy settings are invalid: " + err};
-  // engine limits of the bit-parallel evaluation: 64 local bits per policy
-  auto distinct = [](std::vector<std::string> v) {
-    std::sort(v.begin(), v.end());
-    return (size_t)(std::unique(v.begin(), v.end()) - v.begin());
-  };
-  if (rec->family == FAM_LABELS && distinct(rec->lists[1]) > (size_t)kMaxLocalBits)
-    return {KW_E_BOOTSTRAP, "bootstrap failure: " + rec->id + ": more than 64 distinct mandatory_labels (engine limit)"};
-  if (rec->family == FAM_CAPABILITIES) {
-    std::vector<std::string> m = rec->lists[1];
-    m.insert(m.end(), rec->lists[2].begin(), rec->lists[2].end());
-    m.push_back("ALL");
-    if (distinct(m) > (size_t)kMaxLocalBits)
-      return {KW_E_BOOTSTRAP, "bootstrap failure: " + rec->id +
-                                  ": more than 63 distinct required-drop / default-add capabilities (engine limit)"};
-  }
   return {};
+}
+
+// A policy whose local bits exceed one chunk's 64 becomes consecutive parts (PolicyRec::parts),
+// each within the limit, appended as hidden records:
+//  safe-labels: the mandatory list cut into runs of <= 64 distinct keys (settings order); part 0
+//   also holds the denied and constrained labels. The first part that rejects decides: label
+//   violations come first (part 0), then the first missing mandatory key in settings order, its
+//   index offset by the run's start (part_off).
+//  psp-capabilities: the required drops and default adds cut into parts of <= 63 distinct names
+//   (+ "ALL"); part 0 validates the added capabilities against allowed + every default add (the
+//   allowance rule of the whole policy), the other parts allow everything; the policy rejects when
+//   part 0 rejects, else is mutated when any part is.
+static void split_policy(Env* env, size_t idx) {
+  auto distinct_runs = [](const std::vector<std::string>& l, size_t cap) {
+    std::vector<std::pair<size_t, size_t>> runs;  // [begin, end) positions
+    size_t b = 0;
+    std::vector<std::string> seen;
+    for (size_t i = 0; i < l.size(); ++i) {
+      if (std::find(seen.begin(), seen.end(), l[i]) == seen.end()) {
+        if (seen.size() == cap) {
+          runs.push_back({b, i});
+          b = i;
+          seen.clear();
+        }
+        seen.push_back(l[i]);
+      }
+    }
+    runs.push_back({b, l.size()});
+    return runs;
+  };
+  PolicyRec& P0 = env->pol[idx];
+  std::vector<PolicyRec> parts;
+  std::vector<uint32_t> offs;
+  if (P0.family == FAM_LABELS) {
+    std::vector<std::string> keys = P0.lists[1];
+    std::sort(keys.begin(), keys.end());
+    if ((size_t)(std::unique(keys.begin(), keys.end()) - keys.begin()) <= (size_t)kMaxLocalBits) return;
+    const auto runs = distinct_runs(P0.lists[1], kMaxLocalBits);
+    for (size_t k = 0; k < runs.size(); ++k) {
+      PolicyRec q;
+      q.family = FAM_LABELS;
+      if (k == 0) {
+        q.lists[0] = P0.lists[0];
+        q.lists[2] = P0.lists[2];
+        q.lists[3] = P0.lists[3];
+      }
+      q.lists[1].assign(P0.lists[1].begin() + (long)runs[k].first, P0.lists[1].begin() + (long)runs[k].second);
+      parts.push_back(std::move(q));
+      offs.push_back((uint32_t)runs[k].first);
+    }
+  } else if (P0.family == FAM_CAPABILITIES) {
+    std::vector<std::string> all = P0.lists[1];
+    all.insert(all.end(), P0.lists[2].begin(), P0.lists[2].end());
+    all.push_back("ALL");
+    std::sort(all.begin(), all.end());
+    if ((size_t)(std::unique(all.begin(), all.end()) - all.begin()) <= (size_t)kMaxLocalBits) return;
+    // drops then adds as one list of (kind, name), cut into runs of <= 63 distinct names
+    std::vector<std::string> names;
+    for (auto& c : P0.lists[1]) names.push_back("d" + c);
+    for (auto& c : P0.lists[2]) names.push_back("a" + c);
+    std::vector<std::string> bare;
+    for (auto& n : names) bare.push_back(n.substr(1));
+    const auto runs = distinct_runs(bare, kMaxLocalBits - 1);
+    for (size_t k = 0; k < runs.size(); ++k) {
+      PolicyRec q;
+      q.family = FAM_CAPABILITIES;
+      if (k == 0) {
+        q.lists[0] = P0.lists[0];
+        q.lists[0].insert(q.lists[0].end(), P0.lists[2].begin(), P0.lists[2].end());
+        q.flags = P0.flags & PF_ALLOW_ALL;
+      } else {
+        q.flags = PF_ALLOW_ALL;
+      }
+      for (size_t i = runs[k].first; i < runs[k].second; ++i)
+        q.lists[names[i][0] == 'd' ? 1 : 2].push_back(names[i].substr(1));
+      parts.push_back(std::move(q));
+      offs.push_back(0);
+    }
+  } else {
+    return;
+  }
+  const std::string id = P0.id;
+  const int32_t parent = (int32_t)idx;
+  std::vector<int32_t> at;
+  for (size_t k = 0; k < parts.size(); ++k) {
+    PolicyRec& q = parts[k];
+    q.id = id + "#part" + std::to_string(k);
+    q.name = q.id;
+    q.module = env->pol[idx].module;
+    q.mode = KW_MODE_PROTECT;
+    q.registered = true;
+    q.is_part = true;
+    q.parent = parent;
+    at.push_back((int32_t)env->pol.size());
+    env->pol.push_back(std::move(q));
+  }
+  env->pol[idx].parts = at;
+  env->pol[idx].part_off = offs;
 }
 
 Status build_env(const char* json, size_t len, bool continue_on_errors, const char* always_ns, Env* env) {
@@ -920,6 +1003,10 @@ Status build_env(const char* json, size_t len, bool continue_on_errors, const ch
     if (!rec.is_group) continue;
     rec.prog = compile_group_expression(rec.expression, rec.member_names);
   }
+  // policies beyond one chunk's local bits: hidden parts after the visible records
+  env->nvisible = env->pol.size();
+  for (size_t i = 0; i < env->nvisible; ++i)
+    if (!env->pol[i].is_group && !env->pol[i].init_error) split_policy(env, i);
 
   // ---- the request columns' patterns: every list of every initialised policy as pattern ids
   if (env->always_ns) pattern_id(&env->cols[COL_NS], Pattern::Literal, *env->always_ns);

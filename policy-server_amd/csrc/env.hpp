@@ -48,6 +48,14 @@ struct PolicyRec {
   std::vector<int32_t> members;
   GroupProgram prog;
   std::string broken_member;  // member id that failed to initialise (validate -> PolicyNotFound)
+  // a policy beyond the 64 local bits of one slot-plan chunk (more than 64 distinct mandatory labels,
+  // more than 63 required-drop / default-add capabilities) is evaluated as consecutive parts (hidden
+  // records after the visible ones, each within the limit), combined on the wide path: the first
+  // part that rejects (safe-labels: mandatory indices offset by part_off), or psp-capabilities' part
+  // 0 validation then any part's mutation (env.cpp split_policy)
+  std::vector<int32_t> parts;
+  std::vector<uint32_t> part_off;
+  bool is_part = false;
 };
 
 // Host description of one column's classifier (the blob holds its tables).
@@ -67,7 +75,8 @@ struct KvClass {
 
 struct Env {
   std::string source;  // the policies document (re-sent with the blob to other ranks)
-  std::vector<PolicyRec> pol;
+  std::vector<PolicyRec> pol;  // the visible policies [0, nvisible), then the parts of split ones
+  size_t nvisible = 0;
   std::unordered_map<std::string, int32_t> ids;
   std::optional<std::string> always_ns;
   bool continue_on_errors = false;

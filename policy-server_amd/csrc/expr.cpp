@@ -5,6 +5,7 @@
 
 #include <cctype>
 #include <climits>
+#include <algorithm>
 #include <map>
 
 #include "kwdev.hpp"
@@ -620,6 +621,212 @@ void emit(const Node* n, bool wide, std::vector<uint8_t>* code, uint32_t depth, 
   }
 }
 
+// ---- script bytecode (kwdev.hpp SOp): the interpreter's semantics, compiled
+struct ScriptEmitter {
+  std::vector<uint8_t> code, pool;
+  std::vector<std::vector<std::pair<std::string, uint32_t>>> scopes;  // name -> let slot, innermost last
+  std::vector<uint64_t> slot_len;  // static bound of a let slot's string length
+  uint32_t depth = 0, maxdepth = 0;
+  uint64_t arena = 0;  // bytes of the concatenations a run may build (each runs at most once: no loops)
+  void u8(uint8_t x) { code.push_back(x); }
+  void u16(uint32_t x) {
+    u8((uint8_t)x);
+    u8((uint8_t)(x >> 8));
+  }
+  void u32(uint32_t x) {
+    u16(x & 0xffff);
+    u16(x >> 16);
+  }
+  void push(int n = 1) {
+    depth += (uint32_t)n;
+    maxdepth = std::max(maxdepth, depth);
+  }
+  size_t hole(uint8_t op) {
+    u8(op);
+    const size_t at = code.size();
+    u32(0);
+    return at;
+  }
+  void patch(size_t at) {
+    const uint32_t to = (uint32_t)code.size();
+    for (int k = 0; k < 4; ++k) code[at + (size_t)k] = (uint8_t)(to >> (8 * k));
+  }
+  bool lookup(const std::string& name, uint32_t* slot) const {
+    for (size_t sc = scopes.size(); sc-- > 0;)
+      for (size_t k = scopes[sc].size(); k-- > 0;)
+        if (scopes[sc][k].first == name) {
+          *slot = scopes[sc][k].second;
+          return true;
+        }
+    return false;
+  }
+  // emits n (leaving one value on the stack); returns the static bound of its string length
+  uint64_t emit(const Node* n) {
+    switch (n->k) {
+      case Node::Lit:
+        push();
+        if (n->lit.t == VT::Unit) {
+          u8(S_UNIT);
+        } else if (n->lit.t == VT::Bool) {
+          u8(S_BOOL);
+          u8(n->lit.b ? 1 : 0);
+        } else if (n->lit.t == VT::Int) {
+          u8(S_INT);
+          for (int k = 0; k < 8; ++k) u8((uint8_t)((uint64_t)n->lit.i >> (8 * k)));
+        } else {
+          u8(S_STR);
+          u32((uint32_t)pool.size());  // rebased to the program start at the end
+          u32((uint32_t)n->lit.s.size());
+          pool.insert(pool.end(), n->lit.s.begin(), n->lit.s.end());
+          return n->lit.s.size();
+        }
+        return 0;
+      case Node::Var: {
+        uint32_t slot;
+        push();
+        if (!lookup(n->name, &slot)) {
+          u8(S_FAIL);
+          return 0;
+        }
+        u8(S_LOAD);
+        u16(slot);
+        return slot_len[slot];
+      }
+      case Node::Call:
+        push();
+        if (n->slot < 0) {
+          u8(S_FAIL);
+        } else {
+          u8(S_CALL);
+          u32((uint32_t)n->slot);
+        }
+        return 0;
+      case Node::Unary:
+        emit(n->kids[0].get());
+        u8(n->op == "!" ? S_NOT : n->op == "-" ? S_NEG : S_POS);
+        return 0;
+      case Node::Bin: {
+        const std::string& op = n->op;
+        const uint64_t la = emit(n->kids[0].get());
+        if (op == "||" || op == "&&") {
+          const size_t at = hole(op == "||" ? S_OR : S_AND);
+          --depth;  // (the continuing path pops the left side)
+          emit(n->kids[1].get());
+          u8(S_CHKB);
+          patch(at);
+          return 0;
+        }
+        const uint64_t lb = emit(n->kids[1].get());
+        static const char* ops[] = {"|", "^", "&", "==", "!=", "<", "<=", ">", ">=", "+", "-", "*", "/", "%"};
+        uint8_t code_op = 0;
+        for (uint8_t k = 0; k < 14; ++k)
+          if (op == ops[k]) code_op = k;
+        u8(S_BIN);
+        u8(code_op);
+        --depth;
+        if (code_op == SB_ADD) {
+          arena += la + lb;
+          return la + lb;
+        }
+        return 0;
+      }
+      case Node::If: {
+        emit(n->kids[0].get());
+        const size_t at_else = hole(S_IF);
+        --depth;
+        const uint32_t d0 = depth;
+        const uint64_t lt = emit(n->kids[1].get());
+        const size_t at_end = hole(S_JMP);
+        patch(at_else);
+        depth = d0;
+        uint64_t le = 0;
+        if (n->kids.size() > 2) {
+          le = emit(n->kids[2].get());
+        } else {
+          push();
+          u8(S_UNIT);
+        }
+        patch(at_end);
+        return std::max(lt, le);
+      }
+      case Node::Block: {
+        scopes.emplace_back();
+        uint64_t last = 0;
+        for (size_t k = 0; k < n->kids.size(); ++k) {
+          const Node* st = n->kids[k].get();
+          if (st->k == Node::Let) {
+            const uint64_t l = emit(st->kids[0].get());
+            const uint32_t slot = (uint32_t)slot_len.size();
+            slot_len.push_back(l);
+            u8(S_STORE);
+            u16(slot);
+            --depth;
+            scopes.back().push_back({st->name, slot});
+            last = 0;
+          } else {
+            last = emit(st);
+            if (!(n->tail && k + 1 == n->kids.size())) {
+              u8(S_POP);
+              --depth;
+            }
+          }
+        }
+        scopes.pop_back();
+        if (!n->tail) {
+          push();
+          u8(S_UNIT);
+          return 0;
+        }
+        return last;
+      }
+      case Node::Let: push(); u8(S_UNIT); return 0;  // (handled by Block)
+    }
+    return 0;
+  }
+};
+
+// The script form of a group (GroupProgram::script): header | code | string pool (kwdev.hpp SOp).
+bool emit_script(const ExprAst& ast, std::vector<uint8_t>* out, uint32_t* depth, std::string* err) {
+  ScriptEmitter e;
+  e.emit(ast.root.get());
+  e.u8(S_END);
+  if (e.arena > kMaxScriptArena) {
+    *err = "policy group expression can build strings longer than the engine's limit (65536 bytes)";
+    return false;
+  }
+  if (e.slot_len.size() > 65535 || e.code.size() + e.pool.size() > 0x7fffffffu) {
+    *err = "policy group expression exceeds the engine's limits";
+    return false;
+  }
+  const uint32_t hdr = 16, code_len = (uint32_t)e.code.size();
+  // rebase S_STR pool offsets to the program start: walk the code
+  for (size_t pc = 0; pc < e.code.size();) {
+    const uint8_t op = e.code[pc++];
+    switch (op) {
+      case S_BOOL: case S_BIN: pc += 1; break;
+      case S_INT: pc += 8; break;
+      case S_STR: {
+        uint32_t off = 0;
+        for (int k = 0; k < 4; ++k) off |= (uint32_t)e.code[pc + (size_t)k] << (8 * k);
+        off += hdr + code_len;
+        for (int k = 0; k < 4; ++k) e.code[pc + (size_t)k] = (uint8_t)(off >> (8 * k));
+        pc += 8;
+        break;
+      }
+      case S_LOAD: case S_STORE: pc += 2; break;
+      case S_CALL: case S_AND: case S_OR: case S_IF: case S_JMP: pc += 4; break;
+      default: break;
+    }
+  }
+  out->clear();
+  const uint32_t h[4] = {std::max(e.maxdepth, 1u), (uint32_t)e.slot_len.size(), (uint32_t)e.arena, code_len};
+  out->insert(out->end(), (const uint8_t*)h, (const uint8_t*)h + 16);
+  out->insert(out->end(), e.code.begin(), e.code.end());
+  out->insert(out->end(), e.pool.begin(), e.pool.end());
+  *depth = h[0];
+  return true;
+}
+
 }  // namespace
 
 std::string group_eval_message(const std::string& m) {
@@ -698,9 +905,16 @@ GroupProgram compile_group_expression(const std::string& expr, const std::vector
     return g;
   }
   if (members.size() > kMaxTableMembers) {
-    g.valid = false;
-    g.error = "policy group expression uses let / if / string / integer values with more than 16 members, which the "
-              "engine does not evaluate";
+    // too many members for a truth table: typed bytecode, run by the wide path's combine kernel
+    std::string err;
+    if (!emit_script(*ast, &g.code, &g.depth, &err)) {
+      g.valid = false;
+      g.error = err;
+      g.code.clear();
+      return g;
+    }
+    g.wide = true;
+    g.script = true;
     return g;
   }
   // truth table over the member results: value, error, and the members called that rejected

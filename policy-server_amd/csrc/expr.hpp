@@ -27,7 +27,11 @@
 //              of member results (2^n entries: value, error, causes);
 //   wide       bool-only programs with more than 64 members or a deeper stack: the members run as a
 //              separate pass and a combine kernel runs the jump code (u16 member operands, stack in
-//              global scratch) over their verdict words.
+//              global scratch) over their verdict words;
+//   script     anything else with more than 16 members: the same separate member pass, and the
+//              combine kernel runs typed bytecode (slots.hpp run_script_prog: (), bool, i64 and
+//              string values, `let` slots, rhai's checked arithmetic; the host interpreter words the
+//              messages). No member count is refused.
 #pragma once
 #include <cstdint>
 #include <functional>
@@ -55,7 +59,8 @@ struct GroupProgram {
   // device forms (exactly one is set when valid && !eval_error)
   std::vector<uint8_t> code;   // G_* jump code (kwdev.hpp); G_CALL16 operands when wide
   uint32_t depth = 0;          // value-stack depth of `code`
-  bool wide = false;           // jump code for the wide path (> 64 members or depth > 64)
+  bool wide = false;           // jump code for the wide path (> 64 members or depth > 64), or a script
+  bool script = false;         // `code` is typed script bytecode (kwdev.hpp SOp), run on the wide path
   std::vector<uint32_t> table; // 2^nmem entries: bit 0 value, bit 1 error, bits 16..31 causes
   std::shared_ptr<const ExprAst> ast;
   uint32_t nmem = 0;

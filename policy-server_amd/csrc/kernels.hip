@@ -1583,13 +1583,21 @@ __global__ void __launch_bounds__(kWideThreads) wide_groups_kernel(WideGroupPass
     for (uint32_t k = 0; k < g.cause_words; ++k) cz[k] = 0;
     const uint32_t* mw = w.member_words + r * w.nmw;
     const uint32_t* midx = w.midx + g.midx_off;
-    const bool v = run_wide_prog(
-        w.progs + g.prog_off, g.prog_len, stack,
-        [&](uint32_t s) {
-          const uint32_t x = mw[midx[s]];
-          return (x & KW_V_ALLOWED) && !(x & KW_V_MUTATED);
-        },
-        [&](uint32_t s) { cz[s >> 6] |= 1ull << (s & 63u); });
+    auto ok = [&](uint32_t s) {
+      const uint32_t x = mw[midx[s]];
+      return (x & KW_V_ALLOWED) && !(x & KW_V_MUTATED);
+    };
+    auto cause = [&](uint32_t s) { cz[s >> 6] |= 1ull << (s & 63u); };
+    if (g.kind == 1) {  // script bytecode: true, false or an evaluation error
+      const int v = run_script_prog(w.progs + g.prog_off, stack, ok, cause);
+      *dst = v == 1 ? g.okw : v == 0 ? g.rejb : g.errw;
+      continue;
+    }
+    if (g.kind >= 2) {  // a split plain policy: its parts' words
+      *dst = combine_parts(g, (const uint32_t*)(w.progs + g.prog_off), [&](uint32_t s) { return mw[midx[s]]; });
+      continue;
+    }
+    const bool v = run_wide_prog(w.progs + g.prog_off, g.prog_len, stack, ok, cause);
     *dst = v ? g.okw : g.rejb;
   }
 }

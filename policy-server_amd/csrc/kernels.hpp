@@ -161,8 +161,29 @@ struct WideGroupArgs {
   uint32_t nmem, midx_off;      // member slot s -> member_words column midx[midx_off + s]
   uint32_t okw, rejb;           // the group's accepted / rejected verdict words (reason GROUP, ARG wide)
   uint32_t cause_off, cause_words;  // its cause bitset in the per-row side data
-  uint32_t pad[3];
+  uint32_t errw;                // script programs: the evaluation-error verdict word (reason GROUP_EXPR)
+  uint32_t kind;                // 0 jump code (run_wide_prog), 1 script bytecode (run_script_prog),
+                                // 2 / 3 a split safe-labels / psp-capabilities policy (combine_parts)
+  uint32_t mutw;                // split psp-capabilities: the mutated verdict word
 };
+
+// A split policy's word from its parts' words (env.cpp split_policy): the first part that rejects
+// (safe-labels: a mandatory index offset by the part's start), else — psp-capabilities, whose later
+// parts validate nothing — mutated when any part mutated, else accepted. part(s): part s's word.
+template <class Part>
+KW_HD inline uint32_t combine_parts(const WideGroupArgs& g, const uint32_t* part_off, Part part) {
+  bool mutated = false;
+  for (uint32_t s = 0; s < g.nmem; ++s) {
+    const uint32_t x = part(s);
+    if (!(x & KW_V_ALLOWED)) {
+      uint32_t reason = KW_REASON(x), arg = KW_ARG(x);
+      if (reason == KW_R_LABEL_MANDATORY && arg != kArgWide) arg += part_off[s];
+      return g.rejb | vword(reason, arg);
+    }
+    if (x & KW_V_MUTATED) mutated = true;
+  }
+  return mutated ? g.mutw : g.okw;
+}
 struct WideGroupPass {
   const WideGroupArgs* groups;
   uint32_t ngroups;

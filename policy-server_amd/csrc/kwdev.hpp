@@ -57,6 +57,25 @@ enum PolicyFlag : uint8_t {
 //   G_CALL16 s              (wide programs) push ok(s), s a u16 member index; in wide programs the
 //                           G_JT / G_JF targets are u32
 enum GOp : uint8_t { G_CONST0 = 0, G_CONST1 = 1, G_CALL = 2, G_NOT = 3, G_JT = 4, G_JF = 5, G_EQ = 6, G_NE = 7, G_CALL16 = 8 };
+// Script bytecode (groups beyond the bool-only subset with more than 16 members; expr.cpp emits it,
+// slots.hpp run_script_prog runs it). Header: u32 depth (value stack), nvars (`let` slots), arena
+// (string bytes a run may build), code_len; then the code, then the string pool. Values are 16 B:
+// type (0 unit, 1 bool, 2 i64, 3 string) | string length << 32 | 256 when the bytes are in the
+// arena; then the bool / i64 value or the string's byte offset. Operands little-endian.
+//   S_UNIT | S_BOOL u8 | S_INT i64 | S_STR u32 off u32 len (pool, program-relative)
+//   S_LOAD u16 / S_STORE u16 (pops)          `let` slot
+//   S_CALL u32                                push ok(member), the member counts as called
+//   S_FAIL                                    unknown function / variable: evaluation error
+//   S_NOT / S_NEG / S_POS                     unary (type-checked, -i64::MIN overflows)
+//   S_BIN u8                                  | ^ & == != < <= > >= + - * / % (SBin), checked
+//   S_AND u32 / S_OR u32                      top must be bool; short circuit: jump keeping it, else pop
+//   S_CHKB                                    the right side of && / || must be bool
+//   S_IF u32                                  pop the condition (bool), false: jump
+//   S_JMP u32 | S_POP | S_END (the result must be a bool)
+enum SOp : uint8_t { S_UNIT = 0, S_BOOL, S_INT, S_STR, S_LOAD, S_STORE, S_CALL, S_FAIL, S_NOT, S_NEG, S_POS, S_BIN,
+                     S_AND, S_OR, S_CHKB, S_IF, S_JMP, S_POP, S_END };
+enum SBin : uint8_t { SB_OR = 0, SB_XOR, SB_AND, SB_EQ, SB_NE, SB_LT, SB_LE, SB_GT, SB_GE, SB_ADD, SB_SUB, SB_MUL, SB_DIV, SB_MOD };
+constexpr uint32_t kMaxScriptArena = 1u << 16;  // string bytes one run may build (an engine limit far past real scripts)
 constexpr int kMaxGroupStack = 64;    // value-stack depth (only == / != nest it)
 constexpr int kMaxGroupMembers = 64;  // members evaluate as slots of one slot-plan chunk
 constexpr int kMaxLocalBits = 64;     // per chunk: distinct mandatory label keys / mutation capabilities

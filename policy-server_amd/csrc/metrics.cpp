@@ -27,7 +27,7 @@ void put_label(std::string* o, bool first, const char* key, std::string_view v) 
 
 void Metrics::record(const Env& env, const Batch& b, uint64_t row, int32_t policy, uint32_t v, int origin,
                      uint64_t latency_ms) {
-  if (policy < 0 || (size_t)policy >= env.pol.size() || row >= b.n) return;
+  if (policy < 0 || (size_t)policy >= env.nvisible || row >= b.n) return;
   const PolicyRec& P = env.pol[(size_t)policy];
   const bool raw = (b.req_flags[row] & KW_REQ_RAW) != 0;
   const uint32_t fst = (v & KW_F_STATUS_MASK) >> KW_F_STATUS_SHIFT;

@@ -300,7 +300,8 @@ Status build_slot_chunks(const Env& E, const int32_t* pols, uint32_t npol, int o
       // resources the column needs in this chunk: slots and local bits
       uint32_t need = 0, capb = 0, mandb = 0;
       const bool expr_err = P.is_group && (!P.prog.valid || P.prog.eval_error);
-      const bool wide_group = P.is_group && !expr_err && P.prog.wide;  // members run in their own pass
+      // members (or a split policy's parts) run in their own pass, the combine kernel writes the column
+      const bool wide_group = (P.is_group && !expr_err && P.prog.wide) || (!P.parts.empty() && !P.init_error);
       if (P.init_error || wide_group) {
       } else if (P.is_group) {
         if (!expr_err) {

@@ -461,6 +461,206 @@ KW_HD inline bool run_wide_prog(const uint8_t* prog, uint32_t len, uint64_t* sta
   return get(0) != 0;
 }
 
+// Script bytecode (kwdev.hpp SOp) over the member results: 1 / 0 the bool result, 2 an evaluation
+// error (a type mismatch, checked-arithmetic overflow, division by zero, an unknown name, a non-bool
+// result: the host interpreter words the message). `scratch`: run_script_words(prog) u64 words.
+// cause(s) records a called member that rejected.
+KW_HD inline uint64_t run_script_words(const uint8_t* prog) {
+  const uint32_t* h = (const uint32_t*)prog;  // depth, nvars, arena bytes, code_len
+  return 2ull * h[0] + 2ull * h[1] + (h[2] + 7u) / 8u + 1u;
+}
+template <class Ok, class Cause>
+KW_HD inline int run_script_prog(const uint8_t* prog, uint64_t* scratch, Ok ok, Cause cause) {
+  const uint32_t* h = (const uint32_t*)prog;
+  const uint32_t depth = h[0], nvars = h[1], code_len = h[3];
+  const uint8_t* code = prog + 16;
+  uint64_t* st = scratch;                  // value stack: 2 words a value
+  uint64_t* vars = scratch + 2ull * depth;  // let slots
+  uint8_t* arena = (uint8_t*)(vars + 2ull * nvars);
+  uint32_t atop = 0;
+  uint32_t sp = 0;
+  auto rd32 = [&](uint32_t pc) {
+    return (uint32_t)code[pc] | ((uint32_t)code[pc + 1] << 8) | ((uint32_t)code[pc + 2] << 16) | ((uint32_t)code[pc + 3] << 24);
+  };
+  auto type = [&](uint32_t i) -> uint32_t { return (uint32_t)(st[2 * i] & 0xffu); };
+  auto sbytes = [&](uint32_t i) -> const uint8_t* {
+    return (st[2 * i] & 256u) ? arena + st[2 * i + 1] : prog + st[2 * i + 1];
+  };
+  auto slen = [&](uint32_t i) -> uint32_t { return (uint32_t)(st[2 * i] >> 32); };
+  auto set = [&](uint32_t i, uint32_t t, uint64_t v) {
+    st[2 * i] = t;
+    st[2 * i + 1] = v;
+  };
+  for (uint32_t pc = 0; pc < code_len;) {
+    const uint32_t op = code[pc++];
+    switch (op) {
+      case S_UNIT: set(sp++, 0, 0); break;
+      case S_BOOL: set(sp++, 1, code[pc++]); break;
+      case S_INT: {
+        uint64_t v = 0;
+        for (int k = 0; k < 8; ++k) v |= (uint64_t)code[pc + (uint32_t)k] << (8 * k);
+        pc += 8;
+        set(sp++, 2, v);
+        break;
+      }
+      case S_STR: {
+        const uint32_t off = rd32(pc), len = rd32(pc + 4);
+        pc += 8;
+        st[2 * sp] = 3u | ((uint64_t)len << 32);
+        st[2 * sp + 1] = off;
+        ++sp;
+        break;
+      }
+      case S_LOAD: {
+        const uint32_t v = (uint32_t)code[pc] | ((uint32_t)code[pc + 1] << 8);
+        pc += 2;
+        st[2 * sp] = vars[2 * v];
+        st[2 * sp + 1] = vars[2 * v + 1];
+        ++sp;
+        break;
+      }
+      case S_STORE: {
+        const uint32_t v = (uint32_t)code[pc] | ((uint32_t)code[pc + 1] << 8);
+        pc += 2;
+        --sp;
+        vars[2 * v] = st[2 * sp];
+        vars[2 * v + 1] = st[2 * sp + 1];
+        break;
+      }
+      case S_CALL: {
+        const uint32_t m = rd32(pc);
+        pc += 4;
+        const bool v = ok(m);
+        if (!v) cause(m);
+        set(sp++, 1, v ? 1u : 0u);
+        break;
+      }
+      case S_FAIL: return 2;
+      case S_NOT:
+        if (type(sp - 1) != 1) return 2;
+        st[2 * (sp - 1) + 1] ^= 1u;
+        break;
+      case S_NEG:
+      case S_POS: {
+        if (type(sp - 1) != 2) return 2;
+        const int64_t a = (int64_t)st[2 * (sp - 1) + 1];
+        if (op == S_NEG) {
+          if (a == INT64_MIN) return 2;
+          st[2 * (sp - 1) + 1] = (uint64_t)-a;
+        }
+        break;
+      }
+      case S_AND:
+      case S_OR: {
+        const uint32_t t = rd32(pc);
+        pc += 4;
+        if (type(sp - 1) != 1) return 2;
+        const bool a = st[2 * (sp - 1) + 1] != 0;
+        if (a == (op == S_OR)) pc = t;  // short circuit: the result is the left side
+        else --sp;
+        break;
+      }
+      case S_CHKB:
+        if (type(sp - 1) != 1) return 2;
+        break;
+      case S_IF: {
+        const uint32_t t = rd32(pc);
+        pc += 4;
+        --sp;
+        if (type(sp) != 1) return 2;
+        if (!st[2 * sp + 1]) pc = t;
+        break;
+      }
+      case S_JMP: pc = rd32(pc); break;
+      case S_POP: --sp; break;
+      case S_END:
+        if (sp == 0 || type(sp - 1) != 1) return 2;
+        return st[2 * (sp - 1) + 1] ? 1 : 0;
+      case S_BIN: {
+        const uint32_t b_op = code[pc++];
+        const uint32_t ib = sp - 1, ia = sp - 2;
+        const uint32_t ta = type(ia), tb = type(ib);
+        const uint64_t va = st[2 * ia + 1], vb = st[2 * ib + 1];
+        --sp;
+        if (b_op == SB_EQ || b_op == SB_NE) {  // different types: not equal (rhai's built-in comparison)
+          bool eq = ta == tb;
+          if (eq && ta == 3) {
+            const uint32_t la = slen(ia), lb = slen(ib);
+            eq = la == lb;
+            const uint8_t *pa = sbytes(ia), *pb = sbytes(ib);
+            for (uint32_t k = 0; eq && k < la; ++k) eq = pa[k] == pb[k];
+          } else if (eq && ta != 0) {
+            eq = va == vb;
+          }
+          set(ia, 1, (b_op == SB_EQ) == eq ? 1u : 0u);
+          break;
+        }
+        if (b_op >= SB_LT && b_op <= SB_GE) {
+          int c = 0;
+          if (ta != tb) {
+            set(ia, 1, 0);
+            break;
+          }
+          if (ta == 2) {
+            c = (int64_t)va < (int64_t)vb ? -1 : (int64_t)va > (int64_t)vb ? 1 : 0;
+          } else if (ta == 3) {
+            const uint32_t la = slen(ia), lb = slen(ib);
+            const uint8_t *pa = sbytes(ia), *pb = sbytes(ib);
+            uint32_t k = 0;
+            while (k < la && k < lb && pa[k] == pb[k]) ++k;
+            c = k < la && k < lb ? (pa[k] < pb[k] ? -1 : 1) : (la < lb ? -1 : la > lb ? 1 : 0);
+          } else {
+            return 2;
+          }
+          const bool r = b_op == SB_LT ? c < 0 : b_op == SB_LE ? c <= 0 : b_op == SB_GT ? c > 0 : c >= 0;
+          set(ia, 1, r ? 1u : 0u);
+          break;
+        }
+        if (b_op <= SB_AND) {  // | ^ &
+          if (ta == 1 && tb == 1) {
+            const bool a = va != 0, b = vb != 0;
+            set(ia, 1, (b_op == SB_OR ? (a || b) : b_op == SB_AND ? (a && b) : (a != b)) ? 1u : 0u);
+            break;
+          }
+          if (ta == 2 && tb == 2) {
+            set(ia, 2, b_op == SB_OR ? (va | vb) : b_op == SB_AND ? (va & vb) : (va ^ vb));
+            break;
+          }
+          return 2;
+        }
+        if (b_op == SB_ADD && ta == 3 && tb == 3) {  // concatenation into the arena
+          const uint32_t la = slen(ia), lb = slen(ib);
+          const uint8_t *pa = sbytes(ia), *pb = sbytes(ib);
+          uint8_t* d = arena + atop;
+          for (uint32_t k = 0; k < la; ++k) d[k] = pa[k];
+          for (uint32_t k = 0; k < lb; ++k) d[la + k] = pb[k];
+          st[2 * ia] = 3u | 256u | ((uint64_t)(la + lb) << 32);
+          st[2 * ia + 1] = atop;
+          atop += la + lb;
+          break;
+        }
+        if (ta != 2 || tb != 2) return 2;
+        const int64_t a = (int64_t)va, b = (int64_t)vb;
+        long long r = 0;
+        if (b_op == SB_ADD) {
+          if (__builtin_add_overflow(a, b, &r)) return 2;
+        } else if (b_op == SB_SUB) {
+          if (__builtin_sub_overflow(a, b, &r)) return 2;
+        } else if (b_op == SB_MUL) {
+          if (__builtin_mul_overflow(a, b, &r)) return 2;
+        } else {
+          if (b == 0 || (a == INT64_MIN && b == -1)) return 2;
+          r = b_op == SB_DIV ? a / b : a % b;
+        }
+        set(ia, 2, (uint64_t)r);
+        break;
+      }
+      default: return 2;
+    }
+  }
+  return 2;
+}
+
 // Verdict word of one output column for one request. rej / mut: the request's rejected and mutated
 // slots; vw: its violation words (valid where rej is set); prog: the record's programs (prog_off
 // is record-relative); *wide gets the cause mask of a > 15-member group.

@@ -1,0 +1,111 @@
+"""Policies beyond one slot-plan chunk's 64 local bits (VERDICT r03 "What's missing" 4): more than
+64 distinct mandatory labels, more than 63 required-drop / default-add capabilities. The product
+evaluates them as hidden parts combined on the wide path (env.cpp split_policy, kernels.hpp
+combine_parts); the oracle has no such limit. CPU: the host walk against the oracle."""
+import numpy as np
+import pytest
+
+import kwgpu as K
+import oracle as O
+from helpers import diff_verdicts
+
+MOD = "registry://ghcr.io/kubewarden/policies/"
+NS = "kubewarden"
+KEYS = ["app", "tier", "env", "team", "owner", "version", "release", "component", "part-of", "managed-by",
+        "app.kubernetes.io/name", "app.kubernetes.io/instance", "app.kubernetes.io/version", "cost-center",
+        "region", "zone", "critical", "debug", "experimental", "legacy", "pci"]
+CAPS = ["NET_ADMIN", "SYS_TIME", "SYS_ADMIN", "NET_RAW", "CHOWN", "KILL", "SETUID", "SETGID", "DAC_OVERRIDE",
+        "FOWNER", "MKNOD", "AUDIT_WRITE", "SYS_PTRACE", "NET_BIND_SERVICE"]
+
+
+def split_policies():
+    mand100 = [f"team.example/k-{i:03d}" for i in range(90)] + KEYS[:10]  # 100 distinct, the real keys last
+    mand_mixed = KEYS[:3] + [f"x{i}" for i in range(70)] + KEYS[3:8] + KEYS[:2]  # duplicates, runs of 64
+    drops70 = CAPS[4:8] + [f"CAP_X{i}" for i in range(66)]
+    return {
+        "labels-100-mandatory": {"module": MOD + "safe-labels:v0.1.14",
+                                 "settings": {"mandatory_labels": mand100, "denied_labels": ["pci"],
+                                              "constrained_labels": {"env": "^(dev|prod)$"}}},
+        "labels-mixed": {"module": MOD + "safe-labels:v0.1.14", "policyMode": "monitor",
+                         "settings": {"mandatory_labels": mand_mixed}},
+        "labels-tail": {"module": MOD + "safe-labels:v0.1.14",  # only the last run's keys can be present
+                        "settings": {"mandatory_labels": [f"y{i}" for i in range(64)] + ["app", "tier"]}},
+        "caps-70": {"module": MOD + "psp-capabilities:v0.1.7", "allowedToMutate": True,
+                    "settings": {"allowed_capabilities": CAPS[:6], "required_drop_capabilities": drops70,
+                                 "default_add_capabilities": ["NET_RAW", "CAP_Y1"]}},
+        "caps-70-protect": {"module": MOD + "psp-capabilities:v0.1.7",
+                            "settings": {"allowed_capabilities": ["*"],
+                                         "required_drop_capabilities": [f"CAP_Z{i}" for i in range(40)],
+                                         "default_add_capabilities": [f"CAP_W{i}" for i in range(30)] + ["KILL"]}},
+        "small": {"module": MOD + "safe-labels:v0.1.14", "settings": {"mandatory_labels": ["app"]}},
+    }
+
+
+def _envs(device=-1):
+    doc = split_policies()
+    env = K.EvaluationEnvironment(doc, continue_on_errors=False, always_accept_namespace=NS, device=device)
+    oe = O.OracleEnv(doc, continue_on_errors=False, always_accept_namespace=NS)
+    assert env.policy_ids() == [p["id"] for p in oe.pol]  # the parts stay hidden
+    return env, oe
+
+
+def tail_docs(n=200):
+    """Pods whose labels cover a whole run of labels-tail's list, so its verdict depends on the last
+    part (the mandatory index must be offset by the part's start)."""
+    import json
+    docs = []
+    for r in range(n):
+        labels = {f"y{i}": "v" for i in range(64) if (r % 5) or i != r % 64}
+        if r % 3:
+            labels["app"] = "web"
+        if r % 4:
+            labels["tier"] = "x"
+        labels.update({k: "dev" for k in (["env"] if r % 2 else [])})
+        docs.append(json.dumps({"request": {"uid": f"t{r}", "kind": {"group": "", "version": "v1", "kind": "Pod"},
+                                            "resource": {"group": "", "version": "v1", "resource": "pods"},
+                                            "operation": "CREATE", "userInfo": {}, "namespace": "default",
+                                            "object": {"kind": "Pod", "metadata": {"labels": labels},
+                                                       "spec": {"containers": [{"name": "c", "image": "nginx"}]}}}}))
+    return docs
+
+
+@pytest.mark.parametrize("origin", [K.VALIDATE, K.AUDIT])
+def test_split_policies_host_walk_matches_oracle(origin):
+    env, oe = _envs()
+    ids = env.policy_ids()
+    for pid in ids:
+        env.validate_settings(pid)  # no engine-limit bootstrap failure any more
+    syn = K.SynthBatch(4, 3000, seed=5)
+    got = syn.batch().debug_host_walk(env, ids, origin)
+    want = oe.eval(syn.soa(), ids, origin)
+    assert np.array_equal(got, want), diff_verdicts(got, want, len(ids), ids)
+    b = K.Batch.from_json(tail_docs())
+    got = b.debug_host_walk(env, ids, origin)
+    want = oe.eval(b.view(), ids, origin)
+    assert np.array_equal(got, want), diff_verdicts(got, want, len(ids), ids)
+    args = {int(w) >> 16 for w in want.reshape(-1, len(ids))[:, ids.index("labels-tail")] if (int(w) >> 8) & 0xFF == O.R_LABEL_MANDATORY}
+    assert max(args) >= 64  # the last part decided some rows
+
+
+@pytest.mark.gpu
+def test_split_policies_on_gpu():
+    from test_parity_gpu import _check_responses
+    env, oe = _envs(device=0)
+    ids = env.policy_ids()
+    syn = K.SynthBatch(4, 5000, seed=6)
+    b = syn.batch().to_device(0)
+    for origin in (K.VALIDATE, K.AUDIT):
+        b.validate(env, ids, origin)
+        got, want = b.verdicts(), oe.eval(syn.soa(), ids, origin)
+        assert np.array_equal(got, want), diff_verdicts(got, want, len(ids), ids)
+    docs = tail_docs() + [syn.json(i) for i in range(100)]
+    hb = K.Batch.from_json(docs).to_device(0)
+    for origin in (K.VALIDATE, K.AUDIT):
+        hb.validate(env, ids, origin)
+        got, want = hb.verdicts(), oe.eval(hb.view(), ids, origin)
+        assert np.array_equal(got, want), diff_verdicts(got, want, len(ids), ids)
+        assert _check_responses(env, oe, hb, hb.view(), docs, ids, origin, range(0, len(docs), 9)) > 0
+    rng = np.random.default_rng(3)
+    pick = rng.integers(0, len(ids), len(docs))
+    hb.validate_rows(env, [ids[int(j)] for j in pick], K.AUDIT)
+    assert np.array_equal(hb.verdicts(count=len(docs)), want.reshape(len(docs), len(ids))[np.arange(len(docs)), pick])
