@@ -1161,7 +1161,7 @@ class OracleEnv:
             return R_GROUP_EXPR, 0, []
         if value:
             return 0, 0, []
-        causes = [c for c in called if not member_ok[c]]
+        causes = sorted(c for c in called if not member_ok[c])  # slot order, as kworacle.c lists causes
         return R_GROUP, sum(1 << c for c in causes), causes
 
     def _member_ok(self, P, words):

@@ -440,15 +440,20 @@ class Batch:
         if member_verdicts is not None:
             mv = (C.c_uint32 * len(member_verdicts))(*[int(x) for x in member_verdicts])
         need = C.c_size_t()
+        d = None if doc is None else (doc.encode() if isinstance(doc, str) else doc)
+
+        def call(buf):
+            if d is not None:
+                return self._L.kw_format_response_doc(env._h, self._h, row, env._idx(policy), int(verdict), mv, d, len(d),
+                                                      N.KW_DOC_RAW_REVIEW if raw else N.KW_DOC_ADMISSION_REVIEW, buf,
+                                                      len(buf), C.byref(need))
+            return self._L.kw_format_response(env._h, self._h, row, env._idx(policy), int(verdict), mv, buf, len(buf),
+                                              C.byref(need))
         buf = C.create_string_buffer(1 << 15)
-        if doc is not None:
-            d = doc.encode() if isinstance(doc, str) else doc
-            rc = self._L.kw_format_response_doc(env._h, self._h, row, env._idx(policy), int(verdict), mv, d, len(d),
-                                                N.KW_DOC_RAW_REVIEW if raw else N.KW_DOC_ADMISSION_REVIEW, buf,
-                                                len(buf), C.byref(need))
-        else:
-            rc = self._L.kw_format_response(env._h, self._h, row, env._idx(policy), int(verdict), mv, buf, len(buf),
-                                            C.byref(need))
+        rc = call(buf)
+        if rc == N.KW_E_NOSPACE:  # a long response (a big JSONPatch): the size it needs
+            buf = C.create_string_buffer(need.value + 1)
+            rc = call(buf)
         raise_for(rc, buf.value.decode(errors="replace"))
         return json.loads(buf.value.decode())
 
