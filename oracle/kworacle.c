@@ -8,7 +8,6 @@
 #define _GNU_SOURCE
 #include "kworacle.h"
 
-#include <fnmatch.h>
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
@@ -110,7 +109,7 @@ static int sv_eq(sv s, const char *t) { return strlen(t) == s.n && memcmp(s.p, t
 
 static int any_glob(const char *const *pats, int32_t n, const char *s) {
   for (int32_t i = 0; i < n; ++i)
-    if (fnmatch(pats[i], s, 0) == 0) return 1;
+    if (orc_glob_match(pats[i], s, strlen(s)) == 1) return 1;
   return 0;
 }
 static int any_eq(const char *const *lst, int32_t n, sv s) {

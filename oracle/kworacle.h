@@ -120,6 +120,11 @@ void orc_re_free(orc_re *re);
 /* convenience for tests: 1 match, 0 no match, -1 the pattern does not compile */
 int orc_re_match(const char *pattern, const char *s, size_t n);
 
+/* kwregex.c: globs (fnmatch(3) flags 0 over code points), independent of the locale.
+   orc_glob_ok: 1 if the glob is supported; orc_glob_match: 1 match, 0 no match, -1 unsupported. */
+int orc_glob_ok(const char *pattern);
+int orc_glob_match(const char *pattern, const char *s, size_t n);
+
 /* Image reference normalisation; writes NUL-terminated parts.
    Returns 1 if an effective tag exists. */
 int orc_image_parts(const char *image, char *registry, char *tag, char *normalized, int cap);

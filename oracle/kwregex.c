@@ -910,10 +910,9 @@ static int add_thread(const orc_re *R, tlist *L, uint32_t *mark, uint32_t gen_, 
   return matched;
 }
 
-int orc_re_search(const orc_re *R, const char *s, size_t n) {
-  /* the subject's code points (a byte that is not valid UTF-8 becomes a value no set contains) */
-  int64_t small[256];
-  int64_t *cp = n <= 256 ? small : (int64_t *)malloc(n * sizeof(int64_t));
+/* the code points of s[0, n) into cp (a byte that is not valid UTF-8 becomes 0x110000 + the byte, a
+   value no set contains); returns their number */
+static size_t code_points(const char *s, size_t n, int64_t *cp) {
   size_t m = 0;
   const unsigned char *u = (const unsigned char *)s;
   for (size_t i = 0; i < n;) {
@@ -936,6 +935,13 @@ int orc_re_search(const orc_re *R, const char *s, size_t n) {
       i += 1;
     }
   }
+  return m;
+}
+
+int orc_re_search(const orc_re *R, const char *s, size_t n) {
+  int64_t small[256];
+  int64_t *cp = n <= 256 ? small : (int64_t *)malloc(n * sizeof(int64_t));
+  const size_t m = code_points(s, n, cp);
   const int nc = R->ncode;
   int *buf = (int *)malloc((size_t)nc * 2 * sizeof(int));
   uint32_t *mark = (uint32_t *)calloc((size_t)nc, sizeof(uint32_t));
@@ -966,5 +972,182 @@ int orc_re_search(const orc_re *R, const char *s, size_t n) {
   free(mark);
   free(buf);
   if (cp != small) free(cp);
+  return found;
+}
+
+/* ------------------------------------------------------------------ globs
+ * fnmatch(3) with flags 0 in a UTF-8 locale, restated over code points (the dialect DESIGN.md §2
+ * fixes for the trusted-repos lists; the product compiles the same globs into its byte automata,
+ * automaton.cpp parse_glob): `*` any string ('/' included, no leading-dot rule), `?` one character,
+ * `[...]` one character of a set — `!` or `^` first negates, `]` first is literal, `a-z` ranges in
+ * code point order, `[:name:]` the ASCII classes, `\` escapes — `\x` the character x. glibc rules
+ * for the odd cases: an unterminated `[` is an ordinary character and a trailing `\` never matches.
+ * Unlike libc fnmatch this does not depend on the process locale. */
+typedef struct {
+  int star;
+  cset set;
+} gtok;
+
+/* the pattern's tokens; 0 = unsupported (not UTF-8, an unknown class, a collating element) */
+static int glob_compile(const char *p, gtok **out, int *ntok, int *never) {
+  size_t n = strlen(p);
+  rparse P;
+  memset(&P, 0, sizeof(P));
+  P.p = p;
+  P.n = n;
+  for (P.at = 0; P.at < n;)
+    if (next_char(&P) < 0) return 0;
+  gtok *t = (gtok *)calloc(n + 1, sizeof(gtok));
+  int k = 0;
+  *never = 0;
+  P.at = 0;
+  while (P.at < n) {
+    const int c = peek(&P);
+    if (c == '*') {
+      t[k++].star = 1;
+      P.at++;
+    } else if (c == '?') {
+      cset none = {0};
+      t[k++].set = cs_complement(&none);
+      P.at++;
+    } else if (c == '\\') {
+      P.at++;
+      if (at_end(&P)) {
+        *never = 1;
+        break;
+      }
+      int64_t x = next_char(&P);
+      cs_push(&t[k++].set, (uint32_t)x, (uint32_t)x);
+    } else if (c == '[') {
+      size_t j = P.at + 1, save = P.at;
+      int neg = 0, closed = 0, first = 1, bad_syntax = 0;
+      cset s = {0};
+      if (j < n && (p[j] == '!' || p[j] == '^')) neg = 1, j++;
+      P.at = j;
+      while (!at_end(&P)) {
+        const int x = peek(&P);
+        if (x == ']' && !first) {
+          closed = 1;
+          P.at++;
+          break;
+        }
+        first = 0;
+        if (x == '[' && P.at + 1 < n && p[P.at + 1] == ':') {
+          /* a class name: letters a-y closed by ":]" (glibc), else '[' is a member */
+          const char *e = p + P.at + 2;
+          while (*e >= 'a' && *e < 'z') ++e;
+          if (!(e[0] == ':' && e[1] == ']')) {
+            cs_push(&s, '[', '[');
+            P.at++;
+            continue;
+          }
+          cset cl;
+          const char *name = p + P.at + 2;
+          const size_t len = (size_t)(e - name);
+          /* the POSIX classes; [:ascii:] and [:word:] are regex-only names */
+          if ((len == 5 && !memcmp(name, "ascii", 5)) || (len == 4 && !memcmp(name, "word", 4)) ||
+              !named_class(name, len, &cl)) {
+            bad_syntax = 1;
+            break;
+          }
+          cs_add_all(&s, &cl);
+          cs_free(&cl);
+          P.at = (size_t)(e - p) + 2;
+          continue;
+        }
+        if (x == '[' && P.at + 1 < n && (p[P.at + 1] == '.' || p[P.at + 1] == '=')) {
+          bad_syntax = 1;
+          break;
+        }
+        if (x == '\\') {
+          if (P.at + 1 >= n) break; /* unterminated */
+          P.at++;
+        }
+        const uint32_t lo = (uint32_t)next_char(&P);
+        if (P.at < n && p[P.at] == '-' && (P.at + 1 == n || p[P.at + 1] != ']')) {
+          P.at++;
+          if (P.at < n && p[P.at] == '\\') P.at++;
+          if (P.at == n) { /* the range has no upper end: glibc fails the match there */
+            cs_free(&s);
+            *never = 1;
+            break;
+          }
+          const uint32_t hi = (uint32_t)next_char(&P);
+          if (lo <= hi) cs_push(&s, lo, hi);
+        } else {
+          cs_push(&s, lo, lo);
+        }
+      }
+      if (*never) break;
+      if (bad_syntax) {
+        cs_free(&s);
+        for (int q = 0; q < k; ++q) cs_free(&t[q].set);
+        free(t);
+        return 0;
+      }
+      if (!closed) {
+        cs_free(&s);
+        cs_push(&t[k++].set, '[', '[');
+        P.at = save + 1;
+        continue;
+      }
+      cs_canon(&s);
+      if (neg) {
+        cset c2 = cs_complement(&s);
+        cs_free(&s);
+        s = c2;
+      }
+      t[k++].set = s;
+    } else {
+      int64_t x = next_char(&P);
+      cs_push(&t[k++].set, (uint32_t)x, (uint32_t)x);
+    }
+  }
+  *out = t;
+  *ntok = k;
+  return 1;
+}
+
+int orc_glob_ok(const char *pattern) {
+  gtok *t = NULL;
+  int n = 0, never = 0;
+  if (!glob_compile(pattern, &t, &n, &never)) return 0;
+  for (int k = 0; k < n; ++k) cs_free(&t[k].set);
+  free(t);
+  return 1;
+}
+
+int orc_glob_match(const char *pattern, const char *s, size_t n) {
+  gtok *t = NULL;
+  int nt = 0, never = 0;
+  if (!glob_compile(pattern, &t, &nt, &never)) return -1;
+  int found = 0;
+  if (!never) {
+    int64_t small[256];
+    int64_t *cp = n <= 256 ? small : (int64_t *)malloc(n * sizeof(int64_t));
+    const size_t m = code_points(s, n, cp);
+    /* one `*` restart point suffices: the tokens between stars match one character each */
+    int i = 0, star = -1;
+    size_t j = 0, star_j = 0;
+    for (;;) {
+      if (j < m && i < nt && !t[i].star && cs_has(&t[i].set, (uint32_t)cp[j])) {
+        i++, j++;
+      } else if (i < nt && t[i].star) {
+        star = i++;
+        star_j = j;
+      } else if (j == m && i == nt) {
+        found = 1;
+        break;
+      } else if (star >= 0 && star_j < m) {
+        i = star + 1;
+        j = ++star_j;
+      } else {
+        break;
+      }
+    }
+    if (cp != small) free(cp);
+  }
+  for (int k = 0; k < nt; ++k) cs_free(&t[k].set);
+  free(t);
   return found;
 }

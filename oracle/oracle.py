@@ -17,7 +17,7 @@ Restates, independently of the product's C++ (env.cpp / expr.cpp / service.cpp):
     pod-privileged message pinned by integration_test.rs:58-68.
   * the psp-capabilities mutation as an RFC 6902 patch — parity UNPINNED (the
     guest's mutated_object and policy-evaluator's diff are upstream, absent here).
-The per-request family arithmetic runs in oracle/kworacle.c (libc fnmatch + the oracle's own regex
+The per-request family arithmetic runs in oracle/kworacle.c (the oracle's own glob and regex
 matcher, oracle/kwregex.c).
 """
 import base64
@@ -461,6 +461,9 @@ def compile_settings(fam, s, olib):
             raise ValueError("registries: allow and reject lists are mutually exclusive")
         if L[3] and L[4]:
             raise ValueError("images: allow and reject lists are mutually exclusive")
+        for g in L[0] + L[1] + L[2] + L[3] + L[4]:
+            if not olib.orc_glob_ok(g.encode()):
+                raise ValueError(f"invalid pattern '{g}'")
     elif fam == F_CAPS:
         L[0] = lst(s, "allowed_capabilities", "allowed_capabilities")
         L[1] = lst(s, "required_drop_capabilities", "required_drop_capabilities")
@@ -962,6 +965,10 @@ def olib():
         L.orc_regex_ok.argtypes = [C.c_char_p]
         L.orc_re_match.restype = C.c_int
         L.orc_re_match.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t]
+        L.orc_glob_ok.restype = C.c_int
+        L.orc_glob_ok.argtypes = [C.c_char_p]
+        L.orc_glob_match.restype = C.c_int
+        L.orc_glob_match.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t]
         _olib = L
     return _olib
 
@@ -971,6 +978,13 @@ def regex_match(pattern, subject):
     compile in the dialect of DESIGN.md §2."""
     b = subject.encode() if isinstance(subject, str) else bytes(subject)
     return olib().orc_re_match(pattern.encode(), b, len(b))
+
+
+def glob_match(pattern, subject):
+    """The oracle's glob match (oracle/kwregex.c, fnmatch(3) flags 0 over code points): 1 / 0, or -1
+    when the glob is outside the dialect of DESIGN.md §2."""
+    b = subject.encode() if isinstance(subject, str) else bytes(subject)
+    return olib().orc_glob_match(pattern.encode(), b, len(b))
 
 
 def image_parts(image):

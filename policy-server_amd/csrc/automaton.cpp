@@ -87,18 +87,49 @@ bool class_set(const std::string& name, BSet* s) {
 }
 
 // ---------------------------------------------------------------- glob (fnmatch, flags 0)
+// fnmatch(3) without flags, over characters (a UTF-8 locale's multibyte matching): `*` any string
+// ('/' included), `?` one character, `[...]` / `[!...]` / `[^...]` one character of a set with
+// ranges (code point order), `[:class:]` (ASCII classes) and `\` escapes, `\x` the character x; an
+// unterminated `[` is an ordinary character and a trailing `\` never matches (glibc).
 enum class GTok : uint8_t { Set, Star };
 struct GItem {
   GTok t;
-  BSet s;
+  std::vector<std::pair<uint32_t, uint32_t>> cs;  // code point ranges (sorted, disjoint)
 };
+
+// next UTF-8 character of s at *i (advances), -1 when the bytes there are not valid UTF-8
+int64_t utf8_next(const std::string& s, size_t* i) {
+  const unsigned char c = (unsigned char)s[*i];
+  const int n = c < 0x80 ? 1 : (c & 0xE0) == 0xC0 ? 2 : (c & 0xF0) == 0xE0 ? 3 : (c & 0xF8) == 0xF0 ? 4 : 0;
+  if (n == 0 || *i + (size_t)n > s.size()) return -1;
+  uint32_t v = n == 1 ? c : c & (0x7Fu >> n);
+  for (int k = 1; k < n; ++k) {
+    const unsigned char d = (unsigned char)s[*i + (size_t)k];
+    if ((d & 0xC0) != 0x80) return -1;
+    v = (v << 6) | (d & 0x3F);
+  }
+  static const uint32_t min_of[5] = {0, 0, 0x80, 0x800, 0x10000};
+  if (v < min_of[n] || v > 0x10FFFF || (v >= 0xD800 && v <= 0xDFFF)) return -1;
+  *i += (size_t)n;
+  return v;
+}
 
 // Returns false on unsupported syntax; *never = true if glibc would never match (trailing '\').
 bool parse_glob(const std::string& p, std::vector<GItem>* out, bool* never, std::string* err) {
   *never = false;
   size_t i = 0, n = p.size();
+  for (size_t k = 0; k < n;)
+    if (utf8_next(p, &k) < 0) {
+      *err = "glob '" + p + "' is not valid UTF-8";
+      return false;
+    }
+  auto one = [](uint32_t c) {
+    GItem g{GTok::Set, {}};
+    g.cs.push_back({c, c});
+    return g;
+  };
   while (i < n) {
-    unsigned char c = (unsigned char)p[i];
+    const unsigned char c = (unsigned char)p[i];
     if (c == '*') {
       out->push_back({GTok::Star, {}});
       ++i;
@@ -106,7 +137,7 @@ bool parse_glob(const std::string& p, std::vector<GItem>* out, bool* never, std:
     }
     if (c == '?') {
       GItem g{GTok::Set, {}};
-      g.s.fill();
+      g.cs = {{0, 0xD7FF}, {0xE000, 0x10FFFF}};
       out->push_back(g);
       ++i;
       continue;
@@ -116,10 +147,8 @@ bool parse_glob(const std::string& p, std::vector<GItem>* out, bool* never, std:
         *never = true;  // glibc: "Trailing \ loses."
         return true;
       }
-      GItem g{GTok::Set, {}};
-      g.s.set((unsigned char)p[i + 1]);
-      out->push_back(g);
-      i += 2;
+      ++i;
+      out->push_back(one((uint32_t)utf8_next(p, &i)));
       continue;
     }
     if (c == '[') {
@@ -129,10 +158,10 @@ bool parse_glob(const std::string& p, std::vector<GItem>* out, bool* never, std:
         neg = true;
         ++j;
       }
-      BSet s;
+      std::vector<std::pair<uint32_t, uint32_t>> s;
       bool first = true, closed = false;
       while (j < n) {
-        unsigned char x = (unsigned char)p[j];
+        const unsigned char x = (unsigned char)p[j];
         if (x == ']' && !first) {
           closed = true;
           ++j;
@@ -140,16 +169,22 @@ bool parse_glob(const std::string& p, std::vector<GItem>* out, bool* never, std:
         }
         first = false;
         if (x == '[' && j + 1 < n && p[j + 1] == ':') {
-          size_t e = p.find(":]", j + 2);
-          if (e == std::string::npos) {
-            s.set('[');
+          // glibc: a class name is lowercase letters a-y up to ":]"; anything else makes this '['
+          // an ordinary member of the set
+          size_t e = j + 2;
+          while (e < n && p[e] >= 'a' && p[e] < 'z') ++e;
+          if (!(e + 1 < n && p[e] == ':' && p[e + 1] == ']')) {
+            s.push_back({'[', '['});
             ++j;
             continue;
           }
-          if (!class_set(p.substr(j + 2, e - j - 2), &s)) {
+          BSet cls;
+          if (!class_set(p.substr(j + 2, e - j - 2), &cls)) {
             *err = "unsupported character class in glob '" + p + "'";
             return false;
           }
+          for (unsigned b = 0; b < 128; ++b)
+            if (cls.has(b)) s.push_back({b, b});
           j = e + 2;
           continue;
         }
@@ -157,41 +192,58 @@ bool parse_glob(const std::string& p, std::vector<GItem>* out, bool* never, std:
           *err = "collating elements are not supported in glob '" + p + "'";
           return false;
         }
-        unsigned lo = x;
         if (x == '\\') {
           if (j + 1 >= n) break;  // unterminated
-          lo = (unsigned char)p[j + 1];
           ++j;
         }
-        ++j;
-        if (j + 1 < n && p[j] == '-' && p[j + 1] != ']') {
-          unsigned hi = (unsigned char)p[j + 1];
-          j += 2;
-          if (hi == '\\' && j < n) {
-            hi = (unsigned char)p[j];
-            ++j;
+        const uint32_t lo = (uint32_t)utf8_next(p, &j);
+        if (j < n && p[j] == '-' && (j + 1 >= n || p[j + 1] != ']')) {
+          ++j;
+          if (j < n && p[j] == '\\') ++j;
+          if (j >= n) {  // glibc: a range without its upper end fails the match
+            *never = true;
+            return true;
           }
-          if (lo <= hi) s.range(lo, hi);
+          const uint32_t hi = (uint32_t)utf8_next(p, &j);
+          if (lo <= hi) s.push_back({lo, hi});
         } else {
-          s.set(lo);
+          s.push_back({lo, lo});
         }
       }
       if (!closed) {  // glibc: unterminated '[' is an ordinary character
-        GItem g{GTok::Set, {}};
-        g.s.set('[');
-        out->push_back(g);
+        out->push_back(one('['));
         ++i;
         continue;
       }
-      if (neg) s.invert();
-      out->push_back({GTok::Set, s});
+      std::sort(s.begin(), s.end());
+      std::vector<std::pair<uint32_t, uint32_t>> m;
+      for (const auto& r : s) {
+        if (!m.empty() && r.first <= m.back().second + 1) m.back().second = std::max(m.back().second, r.second);
+        else m.push_back(r);
+      }
+      if (neg) {  // the complement within the Unicode scalar values
+        std::vector<std::pair<uint32_t, uint32_t>> c2;
+        uint32_t at = 0;
+        for (const auto& r : m) {
+          if (r.first > at) c2.push_back({at, r.first - 1});
+          at = r.second + 1;
+        }
+        if (at <= 0x10FFFF) c2.push_back({at, 0x10FFFF});
+        m.clear();
+        for (const auto& r : c2) {
+          if (r.second < 0xD800 || r.first > 0xDFFF) {
+            m.push_back(r);
+          } else {
+            if (r.first < 0xD800) m.push_back({r.first, 0xD7FF});
+            if (r.second > 0xDFFF) m.push_back({0xE000, r.second});
+          }
+        }
+      }
+      out->push_back({GTok::Set, m});
       i = j;
       continue;
     }
-    GItem g{GTok::Set, {}};
-    g.s.set(c);
-    out->push_back(g);
-    ++i;
+    out->push_back(one((uint32_t)utf8_next(p, &i)));
   }
   return true;
 }
@@ -1112,15 +1164,18 @@ bool build_nfa(const std::vector<Pattern>& pats, Nfa* out, std::string* err) {
       uint32_t cur = nfa.add();
       nfa.eps(root, cur);
       for (const GItem& g : items) {
-        if (g.t == GTok::Star) {
+        if (g.t == GTok::Star) {  // any bytes: a valid UTF-8 string's characters, whatever they are
           uint32_t nx = nfa.add();
           nfa.eps(cur, nx);
           nfa.edge(nx, any, nx);
           cur = nx;
-        } else {
-          uint32_t nx = nfa.add();
-          nfa.edge(cur, g.s, nx);
-          cur = nx;
+        } else {  // one character of the set (its UTF-8 byte sequences)
+          CSet cs;
+          for (const auto& r : g.cs) cs.push_back({r.first, r.second});
+          Thompson th{nfa, {}};
+          const Frag f = th.set_frag(cs);
+          nfa.eps(cur, f.s);
+          cur = f.e;
         }
       }
       nfa.st[cur].acc = (int)k;

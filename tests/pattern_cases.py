@@ -39,6 +39,11 @@ def policies():
         "registries-blowup": {"module": MOD + "trusted-repos-policy:v0.1.12",
                               "settings": {"registries": {"allow": ["*e??????????????", "docker.io", "ghcr.io"]},
                                            "tags": {"reject": ["*1??????????????", "latest"]}}},
+        # globs over characters (fnmatch in a UTF-8 locale): `?` and bracket sets take one code point
+        "images-utf8": {"module": MOD + "trusted-repos-policy:v0.1.12",
+                        "settings": {"images": {"reject": ["*/caf?/*", "*/[!a-z]pp*", "*:v?"]},
+                                     "tags": {"reject": ["[é-ü]*"]},
+                                     "registries": {"reject": ["reg.?", "*.[à-ÿ]x"]}}},
         "images-mixed": {"module": MOD + "trusted-repos-policy:v0.1.12",
                          "settings": {"images": {"allow": ["docker.io/library/*", "*/*b???????????????",
                                                            "ghcr.io/*"]}}},
@@ -62,7 +67,9 @@ VALUES = {
 IMAGES = ["nginx", "ghcr.io/kubewarden/policy-server:v1.2.3", "quay.io/aaaaaaaaaaaaaaaaaaaaaaaaa:latest",
           "docker.io/library/busybox@sha256:" + "a" * 64, "registry.example.com:5000/team/app:1abcdefghijklmno",
           "my-registry.example.org/x/y", "localhost/abcdefghijklmnopqrstuvwxyz", "ghcr.io/a/b:1",
-          "reg-001.example.com/team-01/app:v2.0.1", "docker.io/bbbbbbbbbbbbbbbbbbbbbbbb"]
+          "reg-001.example.com/team-01/app:v2.0.1", "docker.io/bbbbbbbbbbbbbbbbbbbbbbbb",
+          "ghcr.io/café/app:v1", "ghcr.io/x/épp:1", "ghcr.io/x/app:vé", "ghcr.io/x/app:ü1", "reg.ü/x/y",
+          "ghcr.io/cafée/x", "a.éx/y/z", "ghcr.io/x/app:v𝄞"]
 
 
 def reviews(n=120):
