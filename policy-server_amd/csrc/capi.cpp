@@ -258,6 +258,8 @@ struct DeviceBatch {
   uint32_t n_overflow = 0;
   uint64_t ndesc = 0;
   uint64_t desc_key = 0;
+  bool desc_valid = false;   // D.desc holds the whole batch's descriptors for desc_key
+  uint32_t needs_stride = 1;  // tile needs sampled every needs_stride-th tile (set by kw_validate_host)
   // overflow path: per-string classes in HBM (one allocation) and the wide-argument side data
   uint16_t* g_cls = nullptr;
   size_t g_cls_cap = 0;
@@ -291,6 +293,7 @@ struct DeviceBatch {
   // tile capacities of this batch (plan_pass), per tile height tried
   struct RowsPlan {
     uint32_t rows = 0;
+    uint32_t stride = 1;             // needs of every stride-th tile (kw_validate_host samples)
     std::vector<TileStats> need, q;  // per-tile needs and their quantiles
     uint64_t cap_key = 0;
     int cap_choice = -1;   // quantile index chosen for cap_key
@@ -414,16 +417,18 @@ constexpr double kTileQuantiles[] = {1.0, 0.99995, 0.9999, 0.9995, 0.999, 0.998}
 
 // What each tile of `rows` requests stages: entity counts and the 16-B aligned byte span of each
 // string column.
-std::vector<TileStats> tile_needs(const Batch& B, uint32_t rows) {
-  const uint64_t ntiles = (B.n + rows - 1) / rows;
+std::vector<TileStats> tile_needs(const Batch& B, uint32_t rows, uint32_t stride = 1) {
+  const uint64_t ntiles_all = (B.n + rows - 1) / rows;
+  const uint64_t ntiles = (ntiles_all + stride - 1) / stride;  // sampled tiles: every stride-th
   std::vector<TileStats> v(ntiles);
   // tiles in ranges of 4096 on the host workers (each tile's reads are cache misses: 1M requests
   // take ~3 ms on one thread per tile height)
   constexpr uint64_t kRange = 4096;
   HostWorkers::get().run((size_t)((ntiles + kRange - 1) / kRange), [&](size_t q) {
-  for (uint64_t t = q * kRange, t1 = std::min<uint64_t>(ntiles, (q + 1) * kRange); t < t1; ++t) {
+  for (uint64_t j = q * kRange, t1 = std::min<uint64_t>(ntiles, (q + 1) * kRange); j < t1; ++j) {
+    const uint64_t t = j * stride;
     const uint64_t r0 = t * rows, r1 = std::min<uint64_t>(B.n, (t + 1) * rows);
-    TileStats& st = v[t];
+    TileStats& st = v[j];
     st.ctr = B.ctr_off[r1] - B.ctr_off[r0];
     st.lbl = B.lbl_off[r1] - B.lbl_off[r0];
     st.kadd = B.capadd_off[B.ctr_off[r1]] - B.capadd_off[B.ctr_off[r0]];
@@ -597,6 +602,9 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
   const DevHeader* H = (const DevHeader*)E.blob.data();
   plan->env_blob = E.blob.data();
   plan->rows_mode = row_policy != nullptr;
+  static const bool pdbg = getenv("KW_BULK_DEBUG") && atoi(getenv("KW_BULK_DEBUG")) != 0;  // diagnostics
+  const auto pt0 = std::chrono::steady_clock::now();
+  auto pms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - pt0).count(); };
   // ---- the columns of the pass and their slot-plan chunks
   std::vector<int32_t> list;
   std::map<int32_t, uint32_t> col_of;  // rows mode: policy -> column
@@ -626,6 +634,7 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
   }
   plan->nwide = plan->rows_mode ? (plan->wide_policy.empty() ? 0u : 1u) : (uint32_t)plan->wide_policy.size();
 
+  const double t_slots = pdbg ? pms() : 0.0;
   // ---- what the chunks classify
   uint32_t need = 0;
   bool any_ctr = false, any_caps = false, any_trs = false, any_lbl = false, any_ctr_fam = false;
@@ -794,8 +803,13 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
       D.rows_plans.emplace_back();
       R = &D.rows_plans.back();
       R->rows = r;
-      R->need = tile_needs(B, r);
+      R->stride = 0;
+    }
+    if (R->stride == 0 || R->stride > D.needs_stride) {  // (a sampled plan is refined when a pass wants every tile)
+      R->stride = std::max<uint32_t>(1, D.needs_stride);
+      R->need = tile_needs(B, r, R->stride);
       R->q = tile_quantiles(R->need, kTileQuantiles, sizeof(kTileQuantiles) / sizeof(kTileQuantiles[0]));
+      R->cap_choice = -1;
     }
     rows = r;
     if (R->cap_choice < 0 || R->cap_key != key) {
@@ -875,6 +889,7 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
     }
   }
   rows = pick->rows;
+  if (pdbg) fprintf(stderr, "[kw plan] slot chunks %.2f ms, tile needs + capacities %.2f ms\n", t_slots, pms() - t_slots);
   if (const char* fq = getenv("KW_TILE_QUANTILE"))  // tests / diagnostics: force the capacity quantile
     layout(tile_quantile(pick->need, atof(fq)));
   else
@@ -1028,24 +1043,11 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
 
 // Tile descriptors (kernels.hpp TileDesc) and the overflow list of one plan geometry, built from the
 // host copy of the batch and uploaded once; reused while the geometry stays the same.
-int upload_tile_descs(const Batch& B, DeviceBatch* D, const TileArgs& T, hipStream_t s) {
-  uint64_t key = 1469598103934665603ull;
-  auto mix = [&](uint64_t v) { key = (key ^ v) * 1099511628211ull; };
-  mix(T.rows);
-  mix(T.cmax);
-  mix(T.kmax);
-  mix(T.lmax);
-  for (int m = 0; m < (int)NSTR; ++m) {
-    mix(T.o_sb[m] != 0);
-    mix(T.sb_cap[m]);
-  }
-  if (D->desc && key == D->desc_key) return KW_OK;
-  static const bool dbg = getenv("KW_BULK_DEBUG") && atoi(getenv("KW_BULK_DEBUG")) != 0;  // diagnostics
-  const auto t0 = std::chrono::steady_clock::now();
-  const uint64_t ntiles = (B.n + T.rows - 1) / T.rows;
-  std::vector<TileDesc> desc;
-  desc.reserve(ntiles + ntiles / 64 + 1);
-  std::vector<uint32_t> ovf{0};
+// The descriptors of tiles [t0, t1) of geometry T, in row order, and the requests that exceed the
+// capacities alone (overflow); a run that does not fit is halved until its parts do. Tiles in ranges
+// of `range` on the host workers. KW_E_ARG when an overflow request index exceeds u32.
+int build_descs(const Batch& B, const TileArgs& T, uint64_t t0, uint64_t t1, uint64_t range, std::vector<TileDesc>* desc,
+                std::vector<uint32_t>* ovf) {
   // descriptor of requests [r0, r1); false when it exceeds the capacities
   auto make = [&](uint64_t r0, uint64_t r1, TileDesc* dp) {
     TileDesc& d = *dp;
@@ -1074,18 +1076,15 @@ int upload_tile_descs(const Batch& B, DeviceBatch* D, const TileArgs& T, hipStre
     d.fits = fits ? 1u : 0u;
     return fits;
   };
-  // a run that does not fit is halved until its parts do; a single request that does not fit
-  // goes to the overflow kernels. Tiles in ranges on the host workers, concatenated in row order.
-  constexpr uint64_t kRange = 4096;
-  const size_t nq = (size_t)((ntiles + kRange - 1) / kRange);
+  const size_t nq = (size_t)((t1 - t0 + range - 1) / range);
   std::vector<std::vector<TileDesc>> qdesc(nq);
   std::vector<std::vector<uint32_t>> qovf(nq);
   std::atomic<bool> too_far{false};
   HostWorkers::get().run(nq, [&](size_t q) {
     std::vector<std::pair<uint64_t, uint64_t>> todo;
     std::vector<TileDesc>& dv = qdesc[q];
-    dv.reserve((size_t)kRange + kRange / 64);
-    for (uint64_t tile = q * kRange, t1 = std::min<uint64_t>(ntiles, (q + 1) * kRange); tile < t1; ++tile) {
+    dv.reserve((size_t)range + range / 64);
+    for (uint64_t tile = t0 + q * range, te = std::min<uint64_t>(t1, t0 + (q + 1) * range); tile < te; ++tile) {
       todo.assign(1, {tile * T.rows, std::min<uint64_t>(B.n, (tile + 1) * T.rows)});
       while (!todo.empty()) {
         const auto [r0, r1] = todo.back();
@@ -1106,9 +1105,31 @@ int upload_tile_descs(const Batch& B, DeviceBatch* D, const TileArgs& T, hipStre
   });
   if (too_far) return KW_E_ARG;
   for (size_t q = 0; q < nq; ++q) {
-    desc.insert(desc.end(), qdesc[q].begin(), qdesc[q].end());
-    ovf.insert(ovf.end(), qovf[q].begin(), qovf[q].end());
+    desc->insert(desc->end(), qdesc[q].begin(), qdesc[q].end());
+    ovf->insert(ovf->end(), qovf[q].begin(), qovf[q].end());
   }
+  return KW_OK;
+}
+
+int upload_tile_descs(const Batch& B, DeviceBatch* D, const TileArgs& T, hipStream_t s) {
+  uint64_t key = 1469598103934665603ull;
+  auto mix = [&](uint64_t v) { key = (key ^ v) * 1099511628211ull; };
+  mix(T.rows);
+  mix(T.cmax);
+  mix(T.kmax);
+  mix(T.lmax);
+  for (int m = 0; m < (int)NSTR; ++m) {
+    mix(T.o_sb[m] != 0);
+    mix(T.sb_cap[m]);
+  }
+  if (D->desc && D->desc_valid && key == D->desc_key) return KW_OK;
+  static const bool dbg = getenv("KW_BULK_DEBUG") && atoi(getenv("KW_BULK_DEBUG")) != 0;  // diagnostics
+  const auto t0 = std::chrono::steady_clock::now();
+  const uint64_t ntiles = (B.n + T.rows - 1) / T.rows;
+  std::vector<TileDesc> desc;
+  desc.reserve(ntiles + ntiles / 64 + 1);
+  std::vector<uint32_t> ovf{0};
+  if (int rc = build_descs(B, T, 0, ntiles, 4096, &desc, &ovf)) return rc;
   ovf[0] = (uint32_t)(ovf.size() - 1);
   const auto t1 = std::chrono::steady_clock::now();
   HIPCHK(hipStreamSynchronize(s));  // a running pass may still read the previous descriptors
@@ -1122,6 +1143,7 @@ int upload_tile_descs(const Batch& B, DeviceBatch* D, const TileArgs& T, hipStre
   HIPCHK(hipMemcpyAsync(D->overflow, D->h_ovf.data(), D->h_ovf.size() * sizeof(uint32_t), hipMemcpyHostToDevice, s));
   D->n_overflow = D->h_ovf[0];
   D->desc_key = key;
+  D->desc_valid = true;
   if (dbg)
     fprintf(stderr, "[kw descs] %zu descriptors: build %.2f ms, sync + upload %.2f ms\n", D->h_desc.size(),
             std::chrono::duration<double, std::milli>(t1 - t0).count(),
@@ -1195,7 +1217,7 @@ int ensure_nfa(kw_batch* kb, PassPlan& plan, EvalArgs* A) {
 // Everything a pass's launches need on the device before the first one: the plan's records and
 // TileArgs, the rows-mode column map, tile descriptors and overflow list, schedule counters and the
 // side-data buffers; *out_args: the launch arguments.
-int prepare_pass(kw_batch* kb, PassPlan& plan, hipStream_t s, EvalArgs* out_args) {
+int prepare_pass(kw_batch* kb, PassPlan& plan, hipStream_t s, EvalArgs* out_args, bool descs = true) {
   DeviceBatch& D = *kb->dev;
   const Batch& B = kb->b;
   if (D.cur && D.cur != s) HIPCHK(hipStreamSynchronize(D.cur));  // order against the previous pass's stream
@@ -1224,7 +1246,14 @@ int prepare_pass(kw_batch* kb, PassPlan& plan, hipStream_t s, EvalArgs* out_args
     }
     A.rowcol = D.rowcol;
   }
-  if (int rc = upload_tile_descs(B, &D, plan.geom, s)) return rc;
+  if (descs) {
+    if (int rc = upload_tile_descs(B, &D, plan.geom, s)) return rc;
+  } else {  // the caller builds and uploads descriptors per row chunk (kw_validate_host)
+    HIPCHK(hipStreamSynchronize(s));  // a running pass may still read the previous descriptors
+    D.desc_valid = false;
+    D.ndesc = 0;
+    D.n_overflow = 0;
+  }
   A.ndesc = D.ndesc;
   // tests: KW_POISON_VERDICTS fills the verdict words with a sentinel no verdict word equals
   // (reason byte 0xA5) before the pass, so a tile the schedule never ran shows up as a mismatch
@@ -1954,10 +1983,14 @@ void piece_range(const Batch& B, const Piece& p, uint64_t r0, uint64_t r1, bool 
 }
 
 // Bulk host -> host validation (kw_validate_host): the batch's columns are uploaded, evaluated and
-// read back in row chunks whose stages overlap: the host workers fill chunk k's pinned staging while
-// the copy engines move chunk k-1 in and chunk k-2's verdicts out and the tile kernel evaluates in
-// between (three streams ordered by events). Only the string columns the pass reads are uploaded.
-// Passes with several launches, overflow requests or wide side data run unchunked (upload, pass,
+// read back in row chunks whose stages overlap: the host workers build chunk k's tile descriptors
+// and fill its pinned staging while the copy engines move chunk k-1 in and chunk k-2's verdicts out
+// and the tile kernel evaluates in between (three streams ordered by events). Only the string
+// columns the pass reads are uploaded. The plan's tile capacities come from a sample of the tile
+// needs (every stride-th tile), and each chunk's descriptors are built just before its fill, so the
+// first read-back starts after one small chunk rather than after a whole-batch head; a request
+// that exceeds the capacities alone runs through the overflow kernels right after its chunk's tile
+// launch. Passes with several launches, wide side data or NFA elements run unchunked (upload, pass,
 // read-back) with the same result.
 int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint32_t npol, int origin, int device,
                   uint32_t* out, size_t count, uint32_t chunk_rows) {
@@ -1968,7 +2001,7 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
   static const bool dbg = getenv("KW_BULK_DEBUG") && atoi(getenv("KW_BULK_DEBUG")) != 0;
   using clk = std::chrono::steady_clock;
   const auto t_start = clk::now();
-  double t_layout = 0, t_plan = 0, t_prep = 0, t_fill = 0, t_enq = 0, t_out = 0;
+  double t_layout = 0, t_plan = 0, t_prep = 0, t_desc = 0, t_fill = 0, t_enq = 0, t_out = 0, t_first = -1;
   auto since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
   std::vector<Piece> pieces;
   if (int rc = layout_batch(kb, device, nullptr, &pieces)) return rc;
@@ -1976,10 +2009,15 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
   DeviceBatch& D = *kb->dev;
   const Batch& B = kb->b;
   D.loaded = ~0u;  // (planned as if resident; set to the pass's columns below)
+  // tile capacities from about 2048 sampled tiles (KW_BULK_SAMPLE=0: every tile, A/B knob)
+  static const bool sample = !(getenv("KW_BULK_SAMPLE") && atoi(getenv("KW_BULK_SAMPLE")) == 0);
+  D.needs_stride = sample ? (uint32_t)std::max<uint64_t>(1, B.n / ((uint64_t)kSlotRows * 2048)) : 1u;
   PassPlan plan;
-  if (int rc = validate_common(env, kb, policies, npol, nullptr, origin, &plan)) {
+  const int prc = validate_common(env, kb, policies, npol, nullptr, origin, &plan);
+  D.needs_stride = 1;
+  if (prc) {
     D.loaded = 0;
-    return rc;
+    return prc;
   }
   const uint32_t need = plan.geom.need;
   t_plan = since(t_start) - t_layout;
@@ -1988,16 +2026,8 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
   hipStream_t sc = D.stream;
   EvalArgs A;
   // (NFA elements: their pre-pass reads whole columns, so such passes are not chunked)
-  bool chunked = plan.tiles.size() == 1 && plan.wide.groups.empty() && plan.nwide == 0 && !plan.rows_mode &&
-                 !(plan.geom.debug & 512u) && !(plan.geom.feat & kFeatNfa) && B.n > 0;
-  if (chunked) {
-    if (int rc = prepare_pass(kb, plan, sc, &A)) {
-      D.loaded = 0;
-      return rc;
-    }
-    chunked = D.n_overflow == 0 && D.ndesc > 0;
-  }
-  t_prep = since(t_start) - t_layout - t_plan;
+  const bool chunked = plan.tiles.size() == 1 && plan.wide.groups.empty() && plan.nwide == 0 && !plan.rows_mode &&
+                       !(plan.geom.debug & 512u) && !(plan.geom.feat & kFeatNfa) && B.n > 0;
   if (!chunked) {  // one upload, the full pass, one read-back
     std::vector<CopySeg> segs;
     for (const Piece& p : pieces)
@@ -2007,31 +2037,40 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
     if (int rc = run_validate(env, kb, plan, origin, false, sc)) return rc;
     return kw_batch_verdicts(kb, out, count);
   }
+  if (int rc = prepare_pass(kb, plan, sc, &A, /*descs=*/false)) {
+    D.loaded = 0;
+    return rc;
+  }
+  t_prep = since(t_start) - t_layout - t_plan;
   D.loaded = need;
+  const TileArgs& G = plan.geom;
+  const uint64_t ntiles = (B.n + G.rows - 1) / G.rows;
   static const uint64_t def_chunk = getenv("KW_BULK_CHUNK") ? std::max(1, atoi(getenv("KW_BULK_CHUNK"))) : 131072;  // A/B knob
   const uint64_t per = chunk_rows ? chunk_rows : def_chunk;
-  // chunk k: descriptors [db[k], db[k+1]), rows [rb[k], rb[k+1]). The read-back stream is the
-  // longest (4 B x npol per request out vs the request's columns in), so the first chunks are small
-  // (1/16 of `per`, doubling) to start it early; then `per` rows a chunk, at most 256 chunks.
+  // chunk k: tiles [tb[k], tb[k+1]). The read-back stream is the longest (4 B x npol per request
+  // out vs the request's columns in), so the first chunks are small (1/16 of `per`, doubling) to
+  // start it early; then `per` rows a chunk, at most 256 chunks.
   static const bool ramp = !(getenv("KW_BULK_RAMP") && atoi(getenv("KW_BULK_RAMP")) == 0);  // A/B knob
-  const uint64_t dper = std::max<uint64_t>(1, per / std::max<uint32_t>(1, plan.geom.rows));
-  std::vector<uint64_t> db{0};
-  for (uint64_t step = ramp ? std::max<uint64_t>(1, dper / 16) : dper; db.back() < D.ndesc;) {
-    const uint64_t left = D.ndesc - db.back();
-    db.push_back(db.back() + (db.size() >= 256 ? left : std::min(step, left)));
-    step = std::min(dper, step * 2);
+  const uint64_t tper = std::max<uint64_t>(1, per / G.rows);
+  std::vector<uint64_t> tb{0};
+  for (uint64_t step = ramp ? std::max<uint64_t>(1, tper / 16) : tper; tb.back() < ntiles;) {
+    const uint64_t left = ntiles - tb.back();
+    tb.push_back(tb.back() + (tb.size() >= 256 ? left : std::min(step, left)));
+    step = std::min(tper, step * 2);
   }
-  const uint64_t K = db.size() - 1;
-  std::vector<uint64_t> rb(K + 1);
-  for (uint64_t k = 0; k <= K; ++k)
-    rb[k] = k == K ? B.n : (k == 0 ? 0 : ((uint64_t)D.h_desc[db[k]].r0hi << 32 | D.h_desc[db[k]].r0lo));
+  const uint64_t K = tb.size() - 1;
+  auto row_of = [&](uint64_t t) { return std::min<uint64_t>(B.n, t * G.rows); };
   hipPointerAttribute_t attr;
   const bool pinned = hipPointerGetAttributes(&attr, out) == hipSuccess && attr.type == hipMemoryTypeHost;
   (void)hipGetLastError();  // a pageable pointer leaves an error state behind
-  uint64_t max_rows = 0;
-  for (uint64_t k = 0; k < K; ++k) max_rows = std::max(max_rows, rb[k + 1] - rb[k]);
+  const uint64_t max_rows = std::min<uint64_t>(B.n, tper * G.rows);
   const size_t bounce_bytes = (size_t)max_rows * npol * 4;
   void* bounce[2] = {nullptr, nullptr};
+  // descriptors: two halves of `dcap` on the device and in pinned host memory (chunk k uses half
+  // k & 1; half reuse waits for chunk k-2's kernel on the device and its upload on the host)
+  uint64_t dcap = tper + tper / 4 + 64;
+  void* hdesc = nullptr;
+  size_t hdesc_bytes = 0;
   hipStream_t s_in = nullptr, s_out = nullptr;
   std::vector<hipEvent_t> ev(3 * K, nullptr);
   int rc = KW_OK;  // (a failure below leaves the batch's columns partly uploaded: D.loaded is cleared)
@@ -2039,9 +2078,21 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
     if (e != hipSuccess && rc == KW_OK) rc = KW_E_DEVICE;
     return e != hipSuccess;
   };
+  auto code = [&](int c) {
+    if (c != KW_OK && rc == KW_OK) rc = c;
+    return c != KW_OK;
+  };
   if (!pinned)
     for (auto& b : bounce)
       if (fail(host_pool().alloc(device, bounce_bytes, &b))) break;
+  auto alloc_descs = [&]() {
+    if (hdesc) host_pool().release(device, hdesc, hdesc_bytes);
+    hdesc = nullptr;
+    hdesc_bytes = (size_t)(2 * dcap) * sizeof(TileDesc);
+    if (fail(host_pool().alloc(device, hdesc_bytes, &hdesc))) return false;
+    return !code(ensure(&D.desc, &D.desc_cap, (size_t)(2 * dcap)));
+  };
+  if (rc == KW_OK) (void)alloc_descs();
   if (rc == KW_OK && !fail(hipStreamCreateWithFlags(&s_in, hipStreamNonBlocking)) &&
       !fail(hipStreamCreateWithFlags(&s_out, hipStreamNonBlocking)))
     for (auto& e : ev)
@@ -2049,11 +2100,31 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
   auto copy_out = [&](uint64_t k) {
     const auto t0 = clk::now();
     if (pinned || rc != KW_OK || fail(hipEventSynchronize(ev[3 * k + 2]))) return;
-    parallel_copy_segs({{out + rb[k] * npol, bounce[k & 1], (size_t)(rb[k + 1] - rb[k]) * npol * 4}});
+    const uint64_t r0 = row_of(tb[k]), r1 = row_of(tb[k + 1]);
+    parallel_copy_segs({{out + r0 * npol, bounce[k & 1], (size_t)(r1 - r0) * npol * 4}});
     t_out += since(t0);
   };
+  // overflow requests (alone beyond the tile capacities): their list, classes and side data
+  uint64_t n_ovf = 0;
+  std::vector<TileDesc> cd;
+  std::vector<uint32_t> co;
   for (uint64_t k = 0; k < K && rc == KW_OK; ++k) {
-    const uint64_t r0 = rb[k], r1 = rb[k + 1];
+    const uint64_t r0 = row_of(tb[k]), r1 = row_of(tb[k + 1]);
+    const auto td = clk::now();
+    cd.clear();
+    co.assign(1, 0u);
+    if (code(build_descs(B, G, tb[k], tb[k + 1], 128, &cd, &co))) break;
+    co[0] = (uint32_t)(co.size() - 1);
+    if (cd.size() > dcap) {  // more split tiles than the halves hold: wait for every launch, regrow
+      if (fail(hipStreamSynchronize(s_in)) || fail(hipStreamSynchronize(sc))) break;
+      dcap = cd.size() + cd.size() / 4 + 64;
+      if (!alloc_descs()) break;
+    } else if (k >= 2 && fail(hipEventSynchronize(ev[3 * (k - 2)]))) {  // host half free: its upload is done
+      break;
+    }
+    TileDesc* hd = (TileDesc*)hdesc + (k & 1) * dcap;
+    if (!cd.empty()) memcpy(hd, cd.data(), cd.size() * sizeof(TileDesc));
+    t_desc += since(td);
     std::vector<CopySeg> segs;
     for (const Piece& p : pieces) {
       if (!wanted(p)) continue;
@@ -2065,17 +2136,41 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
     parallel_copy_segs(segs);
     t_fill += since(t0);
     const auto t1 = clk::now();
+    TileDesc* dd = D.desc + (k & 1) * dcap;
+    if (k >= 2 && fail(hipStreamWaitEvent(s_in, ev[3 * (k - 2) + 1], 0))) break;  // device half free
+    if (!cd.empty() && fail(hipMemcpyAsync(dd, hd, cd.size() * sizeof(TileDesc), hipMemcpyHostToDevice, s_in))) break;
     for (const CopySeg& c : segs)
       if (fail(hipMemcpyAsync(D.cols + ((uint8_t*)c.dst - st), c.dst, c.bytes, hipMemcpyHostToDevice, s_in))) break;
     if (rc != KW_OK || fail(hipEventRecord(ev[3 * k], s_in)) || fail(hipStreamWaitEvent(sc, ev[3 * k], 0))) break;
     EvalArgs Ak = A;
-    Ak.ndesc = db[k + 1] - db[k];
-    if (fail(launch_evaluate_tiles(Ak, plan.tiles[0], D.d_tiles, D.desc + db[k], plan.grid, sc))) break;
+    Ak.ndesc = cd.size();
+    if (!cd.empty() && fail(launch_evaluate_tiles(Ak, plan.tiles[0], D.d_tiles, dd, plan.grid, sc))) break;
+    if (co[0]) {  // rare: synchronous set-up, then the overflow kernels on the chunk's requests
+      if (fail(hipStreamSynchronize(sc))) break;
+      n_ovf += co[0];
+      if (code(ensure(&D.overflow, &D.overflow_cap, co.size())) || code(ensure_overflow_classes(B, &D, G, &A))) break;
+      const size_t cap = (size_t)n_ovf * plan.wide_cap_per_row;
+      if (cap > D.wide_rec_cap || !D.wide_rec) {  // grow, keeping the records earlier chunks wrote
+        WideRec* old = D.wide_rec;
+        const size_t old_cap = D.wide_rec_cap;
+        D.wide_rec = nullptr;
+        D.wide_rec_cap = 0;
+        if (code(ensure(&D.wide_rec, &D.wide_rec_cap, std::max(cap, 2 * old_cap)))) break;
+        if (old && fail(hipMemcpy(D.wide_rec, old, old_cap * sizeof(WideRec), hipMemcpyDeviceToDevice))) break;
+        if (old) dev_pool().release(device, old, old_cap * sizeof(WideRec));
+      }
+      A.wide_rec = D.wide_rec;
+      A.wide_cap = (uint32_t)std::min<size_t>(D.wide_rec_cap, 0xffffffffu);
+      Ak = A;
+      if (fail(hipMemcpy(D.overflow, co.data(), co.size() * sizeof(uint32_t), hipMemcpyHostToDevice))) break;
+      if (fail(launch_overflow(Ak, D.d_tiles, D.overflow, co[0], sc))) break;
+    }
     if (fail(hipEventRecord(ev[3 * k + 1], sc)) || fail(hipStreamWaitEvent(s_out, ev[3 * k + 1], 0))) break;
     uint32_t* dst = pinned ? out + r0 * npol : (uint32_t*)bounce[k & 1];
     if (fail(hipMemcpyAsync(dst, D.verdicts + r0 * npol, (size_t)(r1 - r0) * npol * 4, hipMemcpyDeviceToHost, s_out))) break;
     if (fail(hipEventRecord(ev[3 * k + 2], s_out))) break;
     t_enq += since(t1);
+    if (k == 0) t_first = since(t_start);
     if (k >= 1) copy_out(k - 1);  // (bounce[k & 1] was last read by chunk k - 2's copy-out)
   }
   if (rc == KW_OK) copy_out(K - 1);
@@ -2085,15 +2180,17 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
   if (s_out) (void)hipStreamSynchronize(s_out);
   if (dbg)
     fprintf(stderr,
-            "[kw bulk] rows %llu chunks %llu pinned %d: layout %.2f plan %.2f prepare %.2f fill %.2f enqueue %.2f "
-            "copy-out %.2f final wait %.2f total %.2f ms\n",
-            (unsigned long long)B.n, (unsigned long long)K, pinned ? 1 : 0, t_layout, t_plan, t_prep, t_fill, t_enq, t_out,
-            since(t_w), since(t_start));
+            "[kw bulk] rows %llu chunks %llu pinned %d overflow %llu: layout %.2f plan %.2f prepare %.2f descs %.2f fill %.2f "
+            "enqueue %.2f copy-out %.2f first chunk queued at %.2f, final wait %.2f, total %.2f ms\n",
+            (unsigned long long)B.n, (unsigned long long)K, pinned ? 1 : 0, (unsigned long long)n_ovf, t_layout, t_plan, t_prep,
+            t_desc, t_fill, t_enq, t_out, t_first, since(t_w), since(t_start));
   for (auto& e : ev)
     if (e) (void)hipEventDestroy(e);
   if (s_in) (void)hipStreamDestroy(s_in);
   if (s_out) (void)hipStreamDestroy(s_out);
   for (auto& b : bounce) host_pool().release(device, b, bounce_bytes);
+  if (hdesc) host_pool().release(device, hdesc, hdesc_bytes);
+  D.last_wide_cap = A.wide_cap;
   D.cur = sc;
   if (rc != KW_OK) D.loaded = 0;
   return rc;

@@ -33,6 +33,9 @@
 #ifndef KW_LIT_SHORT  // tile kernel: a 4-word literal probe when no string of the wave is longer than 16 bytes
 #define KW_LIT_SHORT 1
 #endif
+#ifndef KW_IMG_LIT_SHORT  // image registry / tag probes: 2- or 4-word batches when the wave's parts are that short
+#define KW_IMG_LIT_SHORT 1
+#endif
 #ifndef KW_MAND_BATCH
 #define KW_MAND_BATCH 1
 #endif
@@ -131,6 +134,17 @@ __device__ inline uint32_t lit_lookup(const uint8_t* rec, const uint8_t* bytes, 
     for (uint32_t i = 0; i < nw && eq; ++i) eq = lit_word(base, i, sh, len) == pw[i];
   }
   return eq ? lit_slot_cls(sl.x) : 0u;
+}
+
+// lit_lookup with the smallest word batch that covers every string of the wave (the words past the
+// batch are read one by one, so any choice is exact); registry and tag parts are mostly <= 8 bytes.
+template <bool BATCH>
+__device__ inline uint32_t lit_lookup_short(const uint8_t* rec, const uint8_t* bytes, uint32_t b, uint32_t e) {
+  if (BATCH && KW_IMG_LIT_SHORT) {
+    if (!__ballot(e - b > 8u)) return lit_lookup<true, 2>(rec, bytes, b, e);
+    if (!__ballot(e - b > 16u)) return lit_lookup<true, 4>(rec, bytes, b, e);
+  }
+  return lit_lookup<BATCH>(rec, bytes, b, e);
 }
 
 // A column's DFA chain, staged contiguously (LDS) or read from the blob: element at blob offset
@@ -281,13 +295,13 @@ __device__ inline void classify_image(const Classifiers& C, const ImgLayout& il,
     return image_part<L>(k, chain_view(C.dfa[c], o), bytes, r);
   };
   if (C.lit[COL_REG])
-    out(j++, nolit ? 0u : r.is_reg ? lit_lookup<BATCH>(C.lit[COL_REG], bytes, r.b, r.slash0) : C.docker_io_cls);
+    out(j++, nolit ? 0u : r.is_reg ? lit_lookup_short<BATCH>(C.lit[COL_REG], bytes, r.b, r.slash0) : C.docker_io_cls);
   for (uint32_t o = C.dfa[COL_REG].head; o; o = chain_next(C.dfa[COL_REG], o)) {
     out(j, nodfa ? 0u : part(0, COL_REG, o));
     ++j;
   }
   if (C.lit[COL_TAG])
-    out(j++, nolit ? 0u : r.colon != NONE ? lit_lookup<BATCH>(C.lit[COL_TAG], bytes, r.colon + 1, r.name_end)
+    out(j++, nolit ? 0u : r.colon != NONE ? lit_lookup_short<BATCH>(C.lit[COL_TAG], bytes, r.colon + 1, r.name_end)
                                           : (r.at == NONE ? C.latest_cls : 0u));
   for (uint32_t o = C.dfa[COL_TAG].head; o; o = chain_next(C.dfa[COL_TAG], o)) {
     out(j, nodfa ? 0u : part(1, COL_TAG, o));

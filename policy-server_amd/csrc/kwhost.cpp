@@ -72,7 +72,7 @@ struct Opts {
 
 // Where a worker's time goes (--stats-ms): cumulative nanoseconds per stage over all batches.
 struct StageStats {
-  std::atomic<uint64_t> batches{0}, rows{0}, wait_ns{0}, flatten_ns{0}, gpu_ns{0}, format_ns{0};
+  std::atomic<uint64_t> batches{0}, rows{0}, wait_ns{0}, flatten_ns{0}, gpu_ns{0}, format_ns{0}, handoff_ns{0};
 };
 static uint64_t ns_since(std::chrono::steady_clock::time_point t) {
   return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t).count();
@@ -329,6 +329,7 @@ class Server {
     stats_.gpu_ns += ns_since(t_gpu);
     const auto t_fmt = std::chrono::steady_clock::now();
     std::vector<char> buf(4096);
+    uint64_t handoff = 0;
     for (Row& r : rows) {
       size_t need = 0;
       const uint32_t* mv = r.nmem ? v.data() + r.first + 1 : nullptr;
@@ -351,10 +352,13 @@ class Server {
       const std::string resp(buf.data(), strnlen(buf.data(), buf.size()));  // need counts the NUL
       rep.body = route == R_RAW ? "{\"response\":" + resp + "}"
                                 : "{\"kind\":\"AdmissionReview\",\"apiVersion\":\"admission.k8s.io/v1\",\"response\":" + resp + "}";
-      r.job->finish(std::move(rep));
+      const auto t_h = std::chrono::steady_clock::now();
+      r.job->finish(std::move(rep));  // wakes the connection thread (a futex wake per request)
+      handoff += ns_since(t_h);
     }
     kw_batch_destroy(b);
-    stats_.format_ns += ns_since(t_fmt);
+    stats_.format_ns += ns_since(t_fmt) - handoff;
+    stats_.handoff_ns += handoff;
   }
 
  public:
@@ -365,9 +369,10 @@ class Server {
       const uint64_t rows = stats_.rows, batches = stats_.batches;
       fprintf(stderr,
               "{\"kwhost_stats\": {\"batches\": %llu, \"rows\": %llu, \"mean_batch\": %.1f, \"wait_s_per_request\": %.3g, "
-              "\"worker_s\": {\"flatten\": %.4f, \"gpu_upload_validate_readback\": %.4f, \"format\": %.4f}}}\n",
+              "\"worker_s\": {\"flatten\": %.4f, \"gpu_upload_validate_readback\": %.4f, \"format\": %.4f, \"handoff\": %.4f}}}\n",
               (unsigned long long)batches, (unsigned long long)rows, batches ? (double)rows / batches : 0.0,
-              rows ? stats_.wait_ns / 1e9 / rows : 0.0, stats_.flatten_ns / 1e9, stats_.gpu_ns / 1e9, stats_.format_ns / 1e9);
+              rows ? stats_.wait_ns / 1e9 / rows : 0.0, stats_.flatten_ns / 1e9, stats_.gpu_ns / 1e9, stats_.format_ns / 1e9,
+              stats_.handoff_ns / 1e9);
       fflush(stderr);
     }
   }
