@@ -165,7 +165,7 @@ def main():
         cpu = None
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(policies, ids, args)
-        modes = None if args.no_host_modes else host_modes(env, ids, syn, device, args)
+        modes = None if args.no_host_modes else host_modes(env, ids, syn, device, args, nbytes)
         result = {
             "metric": METRIC, "value": value, "unit": "requests/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": scaling,
@@ -194,7 +194,29 @@ def main():
     return result
 
 
-def host_modes(env, ids, syn, device, args):
+def pcie_rates(nbytes, reps=5):
+    """Pinned host <-> HBM copy rates (GB/s, best of `reps`) of one `nbytes` buffer each way: the
+    PCIe ceiling of the bulk path, which moves the pass's input columns in and its verdict words out."""
+    import torch
+
+    dev = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    host = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    out = {}
+    for name, fn in (("h2d", lambda: dev.copy_(host, non_blocking=True)), ("d2h", lambda: host.copy_(dev, non_blocking=True))):
+        best = None
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t
+            best = dt if best is None else min(best, dt)
+        out[name] = nbytes / best / 1e9
+    del dev, host
+    return out
+
+
+def host_modes(env, ids, syn, device, args, alg_bytes=None):
     """SURVEY §8(d) timing modes 2 and 3 beside the HBM-resident `value` (mode 1): the end-to-end
     batch rate (host SoA -> H2D -> kernel -> D2H of the verdicts; pageable host buffers, device
     allocation included) and the host JSON -> SoA flatten rate (kw_batch_from_json, 1 and N
@@ -219,6 +241,16 @@ def host_modes(env, ids, syn, device, args):
             hb.close()
         return best
 
+    # the PCIe ceiling of the bulk path: its input columns in and its verdict words out, each at the
+    # measured pinned copy rate of that direction (the two directions overlap)
+    out_bytes = syn.n * npol * 4
+    rates = pcie_rates(out_bytes)
+    in_bytes = max(0.0, (alg_bytes or 0.0) - out_bytes)
+    bound_s = max(in_bytes / (rates["h2d"] * 1e9), out_bytes / (rates["d2h"] * 1e9))
+    out["pcie"] = {"h2d_GB_per_s": rates["h2d"], "d2h_GB_per_s": rates["d2h"], "bytes_in": in_bytes, "bytes_out": out_bytes,
+                   "bulk_bound_requests_per_s": syn.n / bound_s if bound_s > 0 else None,
+                   "what": "pinned copies of one verdict-array-sized buffer each way (best of 5); bound = rows / "
+                           "max(input columns / H2D rate, verdict words / D2H rate)"}
     # pipelined bulk path (kw_validate_host): row chunks whose staging fill, H2D, kernel and D2H overlap
     pin = K.PinnedWords(syn.n * npol, device=device)
     try:

@@ -9,7 +9,7 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 rc=$?; tail -2 gpurun_out/${TAG}_gpu_tests.log; if [ $rc -ne 0 ]; then exit $rc; fi
 for rep in 1 2; do
   for c in ${CFGS:-c2_trusted c3_group c4_64}; do
-    for n in cur bulk_old; do
+    for n in ${VARIANTS:-cur bulk_old kvascii}; do
       KWGPU_LIB="$PWD/policy-server_amd/variants/$n.so" timeout -k 10 300 python bench.py --config $c --no-cpu-baseline --no-host-modes > gpurun_out/${TAG}_${c}_${n}_$rep.json 2> gpurun_out/${TAG}_${c}_${n}_$rep.err
       rc=$?; echo "[ab] rep $rep $c $n rc=$rc $(python -c "import json;d=json.loads(open('gpurun_out/${TAG}_${c}_${n}_$rep.json').read().strip().splitlines()[-1]);print('evaluate_ms=%.4f' % d['kernel_ms']['evaluate'])" 2>/dev/null)" | tee -a gpurun_out/${TAG}_summary.txt
       if [ $rc -ne 0 ]; then exit $rc; fi
