@@ -421,9 +421,9 @@ std::vector<TileStats> tile_needs(const Batch& B, uint32_t rows, uint32_t stride
   const uint64_t ntiles_all = (B.n + rows - 1) / rows;
   const uint64_t ntiles = (ntiles_all + stride - 1) / stride;  // sampled tiles: every stride-th
   std::vector<TileStats> v(ntiles);
-  // tiles in ranges of 4096 on the host workers (each tile's reads are cache misses: 1M requests
+  // tiles in ranges of 256 on the host workers (each tile's reads are cache misses: 1M requests
   // take ~3 ms on one thread per tile height)
-  constexpr uint64_t kRange = 4096;
+  constexpr uint64_t kRange = 256;
   HostWorkers::get().run((size_t)((ntiles + kRange - 1) / kRange), [&](size_t q) {
   for (uint64_t j = q * kRange, t1 = std::min<uint64_t>(ntiles, (q + 1) * kRange); j < t1; ++j) {
     const uint64_t t = j * stride;
@@ -2061,8 +2061,13 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
   const uint64_t K = tb.size() - 1;
   auto row_of = [&](uint64_t t) { return std::min<uint64_t>(B.n, t * G.rows); };
   hipPointerAttribute_t attr;
-  const bool pinned = hipPointerGetAttributes(&attr, out) == hipSuccess && attr.type == hipMemoryTypeHost;
+  static const bool direct = !(getenv("KW_BULK_DIRECT") && atoi(getenv("KW_BULK_DIRECT")) == 0);  // A/B knob
+  const bool pinned = direct && hipPointerGetAttributes(&attr, out) == hipSuccess && attr.type == hipMemoryTypeHost;
   (void)hipGetLastError();  // a pageable pointer leaves an error state behind
+  // pinned output: at most `depth` chunks in flight past the read-back. Unbounded, the host queues
+  // every chunk's copies and launch at once and the copies run slower (C4 1M: 16.0-16.7 ms vs
+  // 9.7-10.9 at depth 2, profiles/r04_bulk_modes.txt). KW_BULK_DEPTH: A/B knob, 0 = unbounded.
+  static const uint64_t depth = getenv("KW_BULK_DEPTH") ? (uint64_t)std::max(0, atoi(getenv("KW_BULK_DEPTH"))) : 2;
   const uint64_t max_rows = std::min<uint64_t>(B.n, tper * G.rows);
   const size_t bounce_bytes = (size_t)max_rows * npol * 4;
   void* bounce[2] = {nullptr, nullptr};
@@ -2110,6 +2115,24 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
   std::vector<uint32_t> co;
   for (uint64_t k = 0; k < K && rc == KW_OK; ++k) {
     const uint64_t r0 = row_of(tb[k]), r1 = row_of(tb[k + 1]);
+    if (pinned && depth && k >= depth && fail(hipEventSynchronize(ev[3 * (k - depth) + 2]))) break;
+    // the chunk's columns first: their H2D starts at once, and the descriptor build below then
+    // reads offsets the fill has just brought into the host caches
+    std::vector<CopySeg> segs;
+    for (const Piece& p : pieces) {
+      if (!wanted(p)) continue;
+      size_t lo, hi;
+      piece_range(B, p, r0, r1, k + 1 == K, &lo, &hi);
+      if (hi > lo) segs.push_back({st + p.at + lo, (const uint8_t*)p.src + lo, hi - lo});
+    }
+    const auto t0 = clk::now();
+    parallel_copy_segs(segs);
+    t_fill += since(t0);
+    const auto t1 = clk::now();
+    for (const CopySeg& c : segs)
+      if (fail(hipMemcpyAsync(D.cols + ((uint8_t*)c.dst - st), c.dst, c.bytes, hipMemcpyHostToDevice, s_in))) break;
+    if (rc != KW_OK) break;
+    t_enq += since(t1);
     const auto td = clk::now();
     cd.clear();
     co.assign(1, 0u);
@@ -2125,23 +2148,11 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
     TileDesc* hd = (TileDesc*)hdesc + (k & 1) * dcap;
     if (!cd.empty()) memcpy(hd, cd.data(), cd.size() * sizeof(TileDesc));
     t_desc += since(td);
-    std::vector<CopySeg> segs;
-    for (const Piece& p : pieces) {
-      if (!wanted(p)) continue;
-      size_t lo, hi;
-      piece_range(B, p, r0, r1, k + 1 == K, &lo, &hi);
-      if (hi > lo) segs.push_back({st + p.at + lo, (const uint8_t*)p.src + lo, hi - lo});
-    }
-    const auto t0 = clk::now();
-    parallel_copy_segs(segs);
-    t_fill += since(t0);
-    const auto t1 = clk::now();
+    const auto t2 = clk::now();
     TileDesc* dd = D.desc + (k & 1) * dcap;
     if (k >= 2 && fail(hipStreamWaitEvent(s_in, ev[3 * (k - 2) + 1], 0))) break;  // device half free
     if (!cd.empty() && fail(hipMemcpyAsync(dd, hd, cd.size() * sizeof(TileDesc), hipMemcpyHostToDevice, s_in))) break;
-    for (const CopySeg& c : segs)
-      if (fail(hipMemcpyAsync(D.cols + ((uint8_t*)c.dst - st), c.dst, c.bytes, hipMemcpyHostToDevice, s_in))) break;
-    if (rc != KW_OK || fail(hipEventRecord(ev[3 * k], s_in)) || fail(hipStreamWaitEvent(sc, ev[3 * k], 0))) break;
+    if (fail(hipEventRecord(ev[3 * k], s_in)) || fail(hipStreamWaitEvent(sc, ev[3 * k], 0))) break;
     EvalArgs Ak = A;
     Ak.ndesc = cd.size();
     if (!cd.empty() && fail(launch_evaluate_tiles(Ak, plan.tiles[0], D.d_tiles, dd, plan.grid, sc))) break;
@@ -2169,7 +2180,7 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
     uint32_t* dst = pinned ? out + r0 * npol : (uint32_t*)bounce[k & 1];
     if (fail(hipMemcpyAsync(dst, D.verdicts + r0 * npol, (size_t)(r1 - r0) * npol * 4, hipMemcpyDeviceToHost, s_out))) break;
     if (fail(hipEventRecord(ev[3 * k + 2], s_out))) break;
-    t_enq += since(t1);
+    t_enq += since(t2);
     if (k == 0) t_first = since(t_start);
     if (k >= 1) copy_out(k - 1);  // (bounce[k & 1] was last read by chunk k - 2's copy-out)
   }
