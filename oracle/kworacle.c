@@ -17,6 +17,7 @@ struct orc_env {
   int32_t npol;
   char *always_ns; /* NULL = None */
   orc_re ***re;    /* per policy: compiled l3 regexes (labels) */
+  orc_glob ***gl;  /* per policy: its five glob lists compiled, concatenated (trusted-repos) */
 };
 
 static char *dupz(const char *s) {
@@ -33,8 +34,16 @@ orc_env *orc_env_new(const orc_policy *policies, int32_t npol, const char *alway
   e->npol = npol;
   e->always_ns = always_ns ? dupz(always_ns) : NULL;
   e->re = (orc_re ***)calloc((size_t)npol, sizeof(orc_re **));
+  e->gl = (orc_glob ***)calloc((size_t)npol, sizeof(orc_glob **));
   for (int32_t p = 0; p < npol; ++p) {
     const orc_policy *P = &policies[p];
+    if (P->family == ORC_F_TRUSTED_REPOS && !P->init_error) {
+      const int32_t tot = P->n[0] + P->n[1] + P->n[2] + P->n[3] + P->n[4];
+      e->gl[p] = (orc_glob **)calloc((size_t)tot + 1, sizeof(orc_glob *));
+      int32_t at = 0;
+      for (int k = 0; k < 5; ++k)
+        for (int32_t i = 0; i < P->n[k]; ++i) e->gl[p][at++] = orc_glob_compile(P->l[k][i]);  /* NULL never matches */
+    }
     if (P->family != ORC_F_LABELS || P->n[3] == 0 || P->init_error) continue;
     e->re[p] = (orc_re **)calloc((size_t)P->n[3], sizeof(orc_re *));
     for (int32_t i = 0; i < P->n[3]; ++i) {
@@ -52,11 +61,18 @@ orc_env *orc_env_new(const orc_policy *policies, int32_t npol, const char *alway
 void orc_env_free(orc_env *e) {
   if (!e) return;
   for (int32_t p = 0; p < e->npol; ++p) {
+    if (e->gl[p]) {
+      const orc_policy *P = &e->pol[p];
+      const int32_t tot = P->n[0] + P->n[1] + P->n[2] + P->n[3] + P->n[4];
+      for (int32_t i = 0; i < tot; ++i) orc_glob_free(e->gl[p][i]);
+      free(e->gl[p]);
+    }
     if (!e->re[p]) continue;
     for (int32_t i = 0; i < e->pol[p].n[3]; ++i) orc_re_free(e->re[p][i]);
     free(e->re[p]);
   }
   free(e->re);
+  free(e->gl);
   free(e->always_ns);
   free(e);
 }
@@ -107,9 +123,10 @@ static const char *z(zbuf *b, sv s) {
 
 static int sv_eq(sv s, const char *t) { return strlen(t) == s.n && memcmp(s.p, t, s.n) == 0; }
 
-static int any_glob(const char *const *pats, int32_t n, const char *s) {
+static int any_glob(orc_glob *const *g, int32_t n, const char *s) {
+  const size_t len = strlen(s);
   for (int32_t i = 0; i < n; ++i)
-    if (orc_glob_match(pats[i], s, strlen(s)) == 1) return 1;
+    if (g[i] && orc_glob_run(g[i], s, len) == 1) return 1;
   return 0;
 }
 static int any_eq(const char *const *lst, int32_t n, sv s) {
@@ -236,8 +253,11 @@ static fam_out fam_namespace(const orc_policy *P, const kw_soa *S, uint64_t r) {
   return o;
 }
 
-static fam_out fam_trusted(const orc_policy *P, const kw_soa *S, uint64_t r, zbuf *zb) {
+static fam_out fam_trusted(const orc_policy *P, orc_glob *const *G, const kw_soa *S, uint64_t r, zbuf *zb) {
   fam_out o = {0, 0, 0};
+  if (!G) return o; /* (an init-error policy is answered before its family runs) */
+  orc_glob *const *g[5];  /* the compiled lists l[0..4] */
+  for (int k = 0, at = 0; k < 5; at += P->n[k], ++k) g[k] = G + at;
   if (!(S->req_flags[r] & KW_REQ_HAS_PODSPEC)) return o;
   char sreg[512], stag[512], snorm[1024];
   for (uint32_t c = S->ctr_off[r]; c < S->ctr_off[r + 1]; ++c) {
@@ -253,15 +273,15 @@ static fam_out fam_trusted(const orc_policy *P, const kw_soa *S, uint64_t r, zbu
     }
     int eff = orc_image_parts(z(zb, im), reg, tag, norm, 0);
     uint32_t why = 0;
-    if (P->n[0] > 0 && !any_glob(P->l[0], P->n[0], reg))
+    if (P->n[0] > 0 && !any_glob(g[0], P->n[0], reg))
       why = KW_R_REG_NOT_ALLOWED;
-    else if (P->n[1] > 0 && any_glob(P->l[1], P->n[1], reg))
+    else if (P->n[1] > 0 && any_glob(g[1], P->n[1], reg))
       why = KW_R_REG_REJECTED;
-    else if (eff && P->n[2] > 0 && any_glob(P->l[2], P->n[2], tag))
+    else if (eff && P->n[2] > 0 && any_glob(g[2], P->n[2], tag))
       why = KW_R_TAG_REJECTED;
-    else if (P->n[3] > 0 && !any_glob(P->l[3], P->n[3], norm))
+    else if (P->n[3] > 0 && !any_glob(g[3], P->n[3], norm))
       why = KW_R_IMG_NOT_ALLOWED;
-    else if (P->n[4] > 0 && any_glob(P->l[4], P->n[4], norm))
+    else if (P->n[4] > 0 && any_glob(g[4], P->n[4], norm))
       why = KW_R_IMG_REJECTED;
     free(heap);
     if (why) {
@@ -368,7 +388,7 @@ static fam_out eval_family(const orc_env *e, int32_t p, const kw_soa *S, uint64_
   switch (P->family) {
   case ORC_F_PRIVILEGED: return fam_privileged(P, S, r);
   case ORC_F_NAMESPACE: return fam_namespace(P, S, r);
-  case ORC_F_TRUSTED_REPOS: return fam_trusted(P, S, r, zb);
+  case ORC_F_TRUSTED_REPOS: return fam_trusted(P, e->gl[p], S, r, zb);
   case ORC_F_CAPABILITIES: return fam_caps(P, S, r);
   case ORC_F_APPARMOR: return fam_apparmor(P, S, r);
   case ORC_F_LABELS: return fam_labels(e, p, S, r, zb);

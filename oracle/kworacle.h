@@ -124,6 +124,11 @@ int orc_re_match(const char *pattern, const char *s, size_t n);
    orc_glob_ok: 1 if the glob is supported; orc_glob_match: 1 match, 0 no match, -1 unsupported. */
 int orc_glob_ok(const char *pattern);
 int orc_glob_match(const char *pattern, const char *s, size_t n);
+/* compiled once (per environment): NULL when unsupported; run: 1 match, 0 no match */
+typedef struct orc_glob orc_glob;
+orc_glob *orc_glob_compile(const char *pattern);
+int orc_glob_run(const orc_glob *g, const char *s, size_t n);
+void orc_glob_free(orc_glob *g);
 
 /* Image reference normalisation; writes NUL-terminated parts.
    Returns 1 if an effective tag exists. */

@@ -1108,46 +1108,67 @@ static int glob_compile(const char *p, gtok **out, int *ntok, int *never) {
   return 1;
 }
 
+struct orc_glob {
+  gtok *t;
+  int n, never;
+};
+
+orc_glob *orc_glob_compile(const char *pattern) {
+  orc_glob *g = (orc_glob *)calloc(1, sizeof(orc_glob));
+  if (!glob_compile(pattern, &g->t, &g->n, &g->never)) {
+    free(g);
+    return NULL;
+  }
+  return g;
+}
+
+void orc_glob_free(orc_glob *g) {
+  if (!g) return;
+  for (int k = 0; k < g->n; ++k) cs_free(&g->t[k].set);
+  free(g->t);
+  free(g);
+}
+
+int orc_glob_run(const orc_glob *g, const char *s, size_t n) {
+  if (g->never) return 0;
+  const gtok *t = g->t;
+  const int nt = g->n;
+  int64_t small[256];
+  int64_t *cp = n <= 256 ? small : (int64_t *)malloc(n * sizeof(int64_t));
+  const size_t m = code_points(s, n, cp);
+  /* one `*` restart point suffices: the tokens between stars match one character each */
+  int i = 0, star = -1, found = 0;
+  size_t j = 0, star_j = 0;
+  for (;;) {
+    if (j < m && i < nt && !t[i].star && cs_has(&t[i].set, (uint32_t)cp[j])) {
+      i++, j++;
+    } else if (i < nt && t[i].star) {
+      star = i++;
+      star_j = j;
+    } else if (j == m && i == nt) {
+      found = 1;
+      break;
+    } else if (star >= 0 && star_j < m) {
+      i = star + 1;
+      j = ++star_j;
+    } else {
+      break;
+    }
+  }
+  if (cp != small) free(cp);
+  return found;
+}
+
 int orc_glob_ok(const char *pattern) {
-  gtok *t = NULL;
-  int n = 0, never = 0;
-  if (!glob_compile(pattern, &t, &n, &never)) return 0;
-  for (int k = 0; k < n; ++k) cs_free(&t[k].set);
-  free(t);
-  return 1;
+  orc_glob *g = orc_glob_compile(pattern);
+  orc_glob_free(g);
+  return g != NULL;
 }
 
 int orc_glob_match(const char *pattern, const char *s, size_t n) {
-  gtok *t = NULL;
-  int nt = 0, never = 0;
-  if (!glob_compile(pattern, &t, &nt, &never)) return -1;
-  int found = 0;
-  if (!never) {
-    int64_t small[256];
-    int64_t *cp = n <= 256 ? small : (int64_t *)malloc(n * sizeof(int64_t));
-    const size_t m = code_points(s, n, cp);
-    /* one `*` restart point suffices: the tokens between stars match one character each */
-    int i = 0, star = -1;
-    size_t j = 0, star_j = 0;
-    for (;;) {
-      if (j < m && i < nt && !t[i].star && cs_has(&t[i].set, (uint32_t)cp[j])) {
-        i++, j++;
-      } else if (i < nt && t[i].star) {
-        star = i++;
-        star_j = j;
-      } else if (j == m && i == nt) {
-        found = 1;
-        break;
-      } else if (star >= 0 && star_j < m) {
-        i = star + 1;
-        j = ++star_j;
-      } else {
-        break;
-      }
-    }
-    if (cp != small) free(cp);
-  }
-  for (int k = 0; k < nt; ++k) cs_free(&t[k].set);
-  free(t);
-  return found;
+  orc_glob *g = orc_glob_compile(pattern);
+  if (!g) return -1;
+  const int r = orc_glob_run(g, s, n);
+  orc_glob_free(g);
+  return r;
 }

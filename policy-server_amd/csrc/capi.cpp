@@ -205,6 +205,15 @@ uint32_t slot_rows_forced() {
   return (v >= 8 && v <= 255) ? (uint32_t)v : 0u;  // tile-local owners are u8
 }
 
+// The next-tile L2 prefetch at run time (KW_L2_PREFETCH=1, A/B knob; the kernel carries its code when
+// built with KW_PREFETCH). Off: running it costs C4 3.5 % and C6 3.8 % (r04 same-box A/B), while the
+// kernel built with the code present and the plan leaving it off was 2 % faster on C2 / C3 / C4
+// than the kernel built without it (profiles/r04_prefetch_ab.txt).
+bool l2_prefetch() {
+  static const bool on = KW_PREFETCH && getenv("KW_L2_PREFETCH") && atoi(getenv("KW_L2_PREFETCH")) != 0;
+  return on;
+}
+
 // Per-tile entity counts and staged byte ranges of a batch, reduced to a high quantile (tile_quantile).
 struct TileStats {
   uint32_t ctr = 0, lbl = 0, kadd = 0, kdrop = 0;
@@ -759,7 +768,7 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
       T.o_sa = take(NSTR * 4);
       T.o_nx = take(8);
       T.o_desc = take(2 * sizeof(TileDesc));
-      T.o_pf = KW_PREFETCH ? take(4 * kPfLanes) : 0u;
+      T.o_pf = l2_prefetch() ? take(4 * kPfLanes) : 0u;
       // union: the staged strings (P0-P1) and the violation words (P2-P3)
       const uint32_t u0 = off;
       uint32_t su = u0;
@@ -898,7 +907,7 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
   // next-tile L2 prefetch (compiled in with KW_PREFETCH, kernels.hpp): a gain where several small
   // tiles share a CU, a loss where two large ones do (C5: +2.7 %; r02 A/B); off by default since the
   // descriptor moved to LDS (r02 s60)
-  T.prefetch = KW_PREFETCH && per_cu(T.lds_bytes) >= 3 ? 1u : 0u;
+  T.prefetch = l2_prefetch() && per_cu(T.lds_bytes) >= 3 ? 1u : 0u;
   // predecessor ranges four loads a round where tiles hold many containers per request (C5 -6 %;
   // C4, two per request, keeps the plain loops: r02 s80)
   T.ctr_ranges = T.cmax > 4u * T.rows ? 1u : 0u;

@@ -70,9 +70,9 @@ constexpr uint32_t kFeatImg = 1, kFeatLbl = 2, kFeatCtr = 4, kFeatGrp = 8, kFeat
 // A pass whose classifiers hold NFA elements runs the one instantiation that reads their classes
 // (kFeatAll | kFeatNfa): no other instantiation carries that code.
 constexpr uint32_t kFeatNfa = 16;
-#ifndef KW_PREFETCH  // tile kernel: warm L2 with the next tile's staged ranges during this tile's walk.
-#define KW_PREFETCH 0   // Off: since staging reads the descriptor from LDS, the prefetch costs P2 more
-#endif                  // than it saves P0 (r02 s60: C4 0.3294 vs 0.3442 ms, C6 -1.8 %, C2 +0.6 %)
+#ifndef KW_PREFETCH  // tile kernel: the code of the next-tile L2 prefetch (run only when the plan asks:
+#define KW_PREFETCH 1   // capi.cpp l2_prefetch, off by default; r02 s60: running it cost C4 0.3442 vs 0.3294 ms)
+#endif
 #ifndef KW_PF_LANES  // lanes per wave issuing the next tile's L2 prefetch (its LDS landing line: 4 B each)
 #define KW_PF_LANES 64
 #endif
