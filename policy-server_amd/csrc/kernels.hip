@@ -738,7 +738,9 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
     // the next tile's staged ranges into L2 (covered by this tile's classification, walk and stores),
     // from its descriptor in LDS
     auto prefetch_next = [&]() {
-      if (KW_PREFETCH && t.prefetch && next < t_hi) {
+      // (instantiated for LDS-staged tables only: in the global-table instantiations the code made
+      // C6 2 % slower, while its presence in the others cut their SGPR spills, r04)
+      if (KW_PREFETCH && LDST && t.prefetch && next < t_hi) {
         const TileDesc& dn = l_desc[cur ^ 1u];
         if (sfield(dn.fits)) {
           const uint64_t q0 = ((uint64_t)sfield(dn.r0hi) << 32) | sfield(dn.r0lo);
