@@ -72,6 +72,9 @@
 #ifndef KW_P3_BITS  // P3 verdict words from 32-bit halves and bit-selects (no 64-bit shifts or branches)
 #define KW_P3_BITS 1
 #endif
+#ifndef KW_VBASE  // tile kernel: LDS region offsets in VGPRs in the label / container instantiation
+#define KW_VBASE 1
+#endif
 #ifndef KW_CLS129  // label-value class loads index min(byte, 128) of the 129-entry narrow maps
 #define KW_CLS129 1
 #endif
@@ -592,12 +595,19 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
   Classifiers C;
 #pragma unroll
   for (int c = 0; c < (int)NCOL; ++c) {
-    const uint32_t lo = LDST ? t.lit_lds[c] : t.lit_blob[c];
+    uint32_t lo = LDST ? t.lit_lds[c] : t.lit_blob[c];
+#if KW_VBASE >= 2
+    if constexpr (!IMG && !GRP && LDST) asm("" : "+v"(lo));  // (KW_VBASE below)
+#endif
     C.lit[c] = t.lit_blob[c] ? tb + lo : nullptr;
     C.dfa[c].head = t.dfa_blob[c];
     C.dfa[c].base = tb + (LDST ? t.dfa_lds[c] : t.dfa_blob[c]);
   }
-  C.kv = t.kv_blob ? ((LDST && t.kv_lds) ? (const uint8_t*)lds + t.kv_lds : a.blob + t.kv_blob) : nullptr;  // kv_lds 0: global
+  uint32_t kvo = t.kv_lds;
+#if KW_VBASE >= 2
+  if constexpr (!IMG && !GRP && LDST) asm("" : "+v"(kvo));
+#endif
+  C.kv = t.kv_blob ? ((LDST && t.kv_lds) ? (const uint8_t*)lds + kvo : a.blob + t.kv_blob) : nullptr;  // kv_lds 0: global
   C.nlk = t.nlk;
   C.docker_io_cls = t.docker_io_cls;
   C.latest_cls = t.latest_cls;
@@ -608,30 +618,40 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
     return sv;
   };
 
-  uint8_t* l_rf = lds + t.o_rf;
-  uint32_t* l_coff = (uint32_t*)(lds + t.o_coff);
-  uint32_t* l_loff = (uint32_t*)(lds + t.o_loff);
-  uint8_t* l_cflags = lds + t.o_cflags;
-  uint32_t* l_cadd = (uint32_t*)(lds + t.o_cadd);
-  uint32_t* l_cdrop = (uint32_t*)(lds + t.o_cdrop);
-  uint16_t* c_ns = (uint16_t*)(lds + t.o_ns);
-  uint16_t* c_aa = (uint16_t*)(lds + t.o_aa);
-  uint16_t* c_img = (uint16_t*)(lds + t.o_img);
-  uint16_t* c_add = (uint16_t*)(lds + t.o_capadd);
-  uint16_t* c_drop = (uint16_t*)(lds + t.o_capdrop);
-  uint16_t* c_lk = (uint16_t*)(lds + t.o_lk);
-  uint16_t* c_lv = (uint16_t*)(lds + t.o_lv);
-  uint64_t* l_rej = (uint64_t*)(lds + t.o_rej);
-  uint64_t* l_mut = (uint64_t*)(lds + t.o_mut);
-  uint8_t* l_byp = lds + t.o_byp;
-  uint32_t* l_sa = (uint32_t*)(lds + t.o_sa);
-  uint64_t* l_vadd = (uint64_t*)(lds + t.o_vadd);
-  uint64_t* l_vl = (uint64_t*)(lds + t.o_vl);
-  uint64_t* l_vc = (uint64_t*)(lds + t.o_vc);
-  uint64_t* l_vtr = (uint64_t*)(lds + t.o_vtr);
-  uint32_t* l_vw = (uint32_t*)(lds + t.o_vw);
-  uint8_t* own_c = lds + t.o_own_c;  // tile-local request of each staged container / label
-  uint8_t* own_l = lds + t.o_own_l;
+  // The tile's LDS regions. Where the instantiation's occupancy is bound by LDS with VGPRs to spare
+  // (KW_VBASE: the label / container families, C4 / C5 at <= 4 workgroups per CU), their offsets
+  // are held in VGPRs: otherwise they are 24 more uniform values competing for the 102 SGPRs, and
+  // the compiler spills SGPRs to VGPR lanes, each reload a v_readlane_b32 in the hot loops.
+  auto region = [&](uint32_t off) -> uint8_t* {
+#if KW_VBASE
+    if constexpr (!IMG && !GRP && LDST) asm("" : "+v"(off));
+#endif
+    return lds + off;
+  };
+  uint8_t* l_rf = region(t.o_rf);
+  uint32_t* l_coff = (uint32_t*)region(t.o_coff);
+  uint32_t* l_loff = (uint32_t*)region(t.o_loff);
+  uint8_t* l_cflags = region(t.o_cflags);
+  uint32_t* l_cadd = (uint32_t*)region(t.o_cadd);
+  uint32_t* l_cdrop = (uint32_t*)region(t.o_cdrop);
+  uint16_t* c_ns = (uint16_t*)region(t.o_ns);
+  uint16_t* c_aa = (uint16_t*)region(t.o_aa);
+  uint16_t* c_img = (uint16_t*)region(t.o_img);
+  uint16_t* c_add = (uint16_t*)region(t.o_capadd);
+  uint16_t* c_drop = (uint16_t*)region(t.o_capdrop);
+  uint16_t* c_lk = (uint16_t*)region(t.o_lk);
+  uint16_t* c_lv = (uint16_t*)region(t.o_lv);
+  uint64_t* l_rej = (uint64_t*)region(t.o_rej);
+  uint64_t* l_mut = (uint64_t*)region(t.o_mut);
+  uint8_t* l_byp = region(t.o_byp);
+  uint32_t* l_sa = (uint32_t*)region(t.o_sa);
+  uint64_t* l_vadd = (uint64_t*)region(t.o_vadd);
+  uint64_t* l_vl = (uint64_t*)region(t.o_vl);
+  uint64_t* l_vc = (uint64_t*)region(t.o_vc);
+  uint64_t* l_vtr = (uint64_t*)region(t.o_vtr);
+  uint32_t* l_vw = (uint32_t*)region(t.o_vw);
+  uint8_t* own_c = region(t.o_own_c);  // tile-local request of each staged container / label
+  uint8_t* own_l = region(t.o_own_l);
   const ImgLayout il = t.il;
   const uint32_t nim = il.n(), nlv = t.nlv;
   const uint32_t need = t.need;
