@@ -598,6 +598,10 @@ __global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
     uint32_t lo = LDST ? t.lit_lds[c] : t.lit_blob[c];
 #if KW_VBASE >= 2
     if constexpr (!IMG && !GRP && LDST) asm("" : "+v"(lo));  // (KW_VBASE below)
+#else
+    // the label-key and capability literal tables, probed in C4's hottest P1 loops
+    if constexpr (KW_VBASE && !IMG && !GRP && LDST)
+      if (c == COL_LK || c == COL_CAP) asm("" : "+v"(lo));
 #endif
     C.lit[c] = t.lit_blob[c] ? tb + lo : nullptr;
     C.dfa[c].head = t.dfa_blob[c];
