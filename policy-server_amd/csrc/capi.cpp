@@ -1991,6 +1991,41 @@ void piece_range(const Batch& B, const Piece& p, uint64_t r0, uint64_t r1, bool 
   *hi = std::min(std::max(e, a), p.bytes);
 }
 
+// The pass's side data into the batch's host copy (kw_batch_wide_arg, the formatter): entity
+// indices >= 65535 and > 15-member group causes (kernels.hpp WideRec), after the pass on stream s.
+int load_side_data(kw_batch* b, hipStream_t s) {
+  DeviceBatch& D = *b->dev;
+  WideData& W = b->b.wide;
+  W.clear();
+  uint32_t nrec = 0;
+  if (D.wide_count) HIPCHK(hipMemcpyAsync(&nrec, D.wide_count, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  W.nwide = D.last_nwide;
+  W.wide_policy = D.last_wide_policy;
+  W.rows_mode = D.last_rows_mode;
+  if (D.last_big_stride && D.big_causes) {  // wide-group cause bitsets
+    W.big_stride = D.last_big_stride;
+    W.big_ref = D.last_big_ref;
+    W.big.resize(b->b.n * W.big_stride);
+    if (!W.big.empty()) HIPCHK(hipMemcpyAsync(W.big.data(), D.big_causes, W.big.size() * 8, hipMemcpyDeviceToHost, s));
+  }
+  if (W.nwide) {
+    W.groups.resize(b->b.n * W.nwide);
+    if (!W.groups.empty())
+      HIPCHK(hipMemcpyAsync(W.groups.data(), D.wide_groups, W.groups.size() * 8, hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  nrec = std::min(nrec, D.last_wide_cap);
+  if (nrec) {
+    std::vector<WideRec> rec(nrec);
+    HIPCHK(hipMemcpy(rec.data(), D.wide_rec, nrec * sizeof(WideRec), hipMemcpyDeviceToHost));
+    for (const WideRec& r : rec) W.recs.push_back({(uint64_t)r.row_lo | ((uint64_t)r.row_hi << 32), (int32_t)r.policy, r.value});
+    std::sort(W.recs.begin(), W.recs.end(), [](const WideData::Rec& x, const WideData::Rec& y) {
+      return x.row < y.row || (x.row == y.row && x.policy < y.policy);
+    });
+  }
+  return KW_OK;
+}
+
 // Bulk host -> host validation (kw_validate_host): the batch's columns are uploaded, evaluated and
 // read back in row chunks whose stages overlap: the host workers build chunk k's tile descriptors
 // and fill its pinned staging while the copy engines move chunk k-1 in and chunk k-2's verdicts out
@@ -2046,6 +2081,8 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
     if (int rc = run_validate(env, kb, plan, origin, false, sc)) return rc;
     return kw_batch_verdicts(kb, out, count);
   }
+  D.last_big_stride = 0;  // (no wide groups in a chunked pass: stale cause bitsets must not be read)
+  D.last_big_ref.clear();
   if (int rc = prepare_pass(kb, plan, sc, &A, /*descs=*/false)) {
     D.loaded = 0;
     return rc;
@@ -2212,8 +2249,11 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
   if (hdesc) host_pool().release(device, hdesc, hdesc_bytes);
   D.last_wide_cap = A.wide_cap;
   D.cur = sc;
-  if (rc != KW_OK) D.loaded = 0;
-  return rc;
+  if (rc != KW_OK) {
+    D.loaded = 0;
+    return rc;
+  }
+  return load_side_data(kb, sc);  // overflow requests' wide arguments (kw_batch_wide_arg)
 }
 }  // namespace
 
@@ -2294,36 +2334,7 @@ int kw_batch_verdicts(kw_batch* b, uint32_t* host_out, size_t count) {
   } else if (count) {
     HIPCHK(hipMemcpyAsync(host_out, D.verdicts, vbytes, hipMemcpyDeviceToHost, s));
   }
-  // side data of the pass: entity indices >= 65535 and > 15-member group causes (kernels.hpp WideRec)
-  WideData& W = b->b.wide;
-  W.clear();
-  uint32_t nrec = 0;
-  if (D.wide_count) HIPCHK(hipMemcpyAsync(&nrec, D.wide_count, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-  W.nwide = D.last_nwide;
-  W.wide_policy = D.last_wide_policy;
-  W.rows_mode = D.last_rows_mode;
-  if (D.last_big_stride && D.big_causes) {  // wide-group cause bitsets
-    W.big_stride = D.last_big_stride;
-    W.big_ref = D.last_big_ref;
-    W.big.resize(b->b.n * W.big_stride);
-    if (!W.big.empty()) HIPCHK(hipMemcpyAsync(W.big.data(), D.big_causes, W.big.size() * 8, hipMemcpyDeviceToHost, s));
-  }
-  if (W.nwide) {
-    W.groups.resize(b->b.n * W.nwide);
-    if (!W.groups.empty())
-      HIPCHK(hipMemcpyAsync(W.groups.data(), D.wide_groups, W.groups.size() * 8, hipMemcpyDeviceToHost, s));
-  }
-  HIPCHK(hipStreamSynchronize(s));
-  nrec = std::min(nrec, D.last_wide_cap);
-  if (nrec) {
-    std::vector<WideRec> rec(nrec);
-    HIPCHK(hipMemcpy(rec.data(), D.wide_rec, nrec * sizeof(WideRec), hipMemcpyDeviceToHost));
-    for (const WideRec& r : rec) W.recs.push_back({(uint64_t)r.row_lo | ((uint64_t)r.row_hi << 32), (int32_t)r.policy, r.value});
-    std::sort(W.recs.begin(), W.recs.end(), [](const WideData::Rec& x, const WideData::Rec& y) {
-      return x.row < y.row || (x.row == y.row && x.policy < y.policy);
-    });
-  }
-  return KW_OK;
+  return load_side_data(b, s);
 }
 
 int kw_debug_plan(const kw_env* env, kw_batch* kb, const int32_t* policies, uint32_t npol, int origin, uint32_t* out,

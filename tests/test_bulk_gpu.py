@@ -109,8 +109,8 @@ def test_bulk_upload_refuses_missing_columns():
 
 
 def test_bulk_unchunked_forms_match_oracle():
-    """Passes the chunked schedule does not take run unchunked through the same call: C6's 40-member
-    group (wide side data) and a batch with requests beyond the tile capacities (overflow kernels)."""
+    """C6's 40-member group (wide side data) runs unchunked through the same call; C5's requests
+    beyond the tile capacities run on the overflow kernels inside their chunks."""
     env, oe = _envs(many_policies_config())
     ids = env.policy_ids()
     syn = K.SynthBatch(6, 3000, seed=6)
@@ -128,8 +128,8 @@ def test_bulk_unchunked_forms_match_oracle():
 
 @pytest.mark.parametrize("q", ["0.5", "0.05"])
 def test_bulk_split_and_overflow_tiles(monkeypatch, q):
-    """Capacities forced low (KW_TILE_QUANTILE): halved request runs inside chunks (chunk bounds fall
-    between split descriptors) and, at 0.05, single requests on the overflow kernels (unchunked)."""
+    """Capacities forced low (KW_TILE_QUANTILE): halved request runs inside chunks and, at 0.05,
+    single requests on the overflow kernels right after their chunk's launch."""
     monkeypatch.setenv("KW_TILE_QUANTILE", q)
     env, oe = _envs(config("c4_64"))
     ids = env.policy_ids()
@@ -137,3 +137,41 @@ def test_bulk_split_and_overflow_tiles(monkeypatch, q):
     got = syn.batch().validate_host(env, ids, chunk_rows=640)
     ora = oe.eval(syn.soa(), ids, K.VALIDATE)
     assert np.array_equal(got, ora), diff_verdicts(got, ora, len(ids), ids)
+
+
+def test_bulk_overflow_wide_arguments_across_chunks():
+    """Two requests beyond every tile capacity (70,000 labels; one container adding 70,000
+    capabilities) in different chunks of a chunked bulk pass: the overflow kernels run per chunk,
+    the second chunk's side data grows the record buffer without losing the first's, and the
+    verdicts, KW_ARG_WIDE arguments and kw_batch_wide_arg values match the oracle."""
+    import json
+    n = 70_000
+    mk = lambda uid, meta, ctrs: json.dumps({"request": {  # noqa: E731
+        "uid": uid, "kind": {"group": "", "version": "v1", "kind": "Pod"},
+        "resource": {"group": "", "version": "v1", "resource": "pods"}, "operation": "CREATE", "userInfo": {},
+        "object": {"kind": "Pod", "metadata": meta, "spec": {"containers": ctrs}}}})
+    big_l = mk("labels", {"labels": {f"k{i}": ("bad" if i == n - 1 else "ok") for i in range(n)}},
+               [{"name": "a", "image": "nginx"}])
+    big_c = mk("caps", {}, [{"name": "big", "image": "nginx",
+                             "securityContext": {"capabilities": {"add": ["CHOWN"] * (n - 1) + ["NET_ADMIN"]}}}])
+    small = [mk(f"s{i}", {"labels": {"k1": "bad" if i % 3 == 0 else "ok"}},
+                [{"name": "s", "image": "nginx", "securityContext": {"capabilities": {"add": ["NET_ADMIN"] if i % 5 == 0 else []}}}])
+             for i in range(1500)]
+    docs = small[:600] + [big_l] + small[600:1200] + [big_c] + small[1200:]
+    rl, rc = 600, 1201
+    mod = "registry://ghcr.io/kubewarden/policies/"
+    pols = {"caps": {"module": mod + "psp-capabilities:v0.1.7", "settings": {"allowed_capabilities": ["CHOWN"]}},
+            "labels": {"module": mod + "safe-labels:v0.1.14",
+                       "settings": {"constrained_labels": {f"k{n - 1}": "^ok$", "k1": "^ok$"}}}}
+    env = K.EvaluationEnvironment(pols, device=0)
+    oe = O.OracleEnv(pols)
+    ids = env.policy_ids()
+    b = K.Batch.from_json(docs)
+    got = b.validate_host(env, ids, chunk_rows=256)
+    ora = oe.eval(b.view(), ids, K.VALIDATE).reshape(len(docs), len(ids))
+    assert np.array_equal(got.reshape(len(docs), len(ids)), ora)
+    li, ci = ids.index("labels"), ids.index("caps")
+    assert int(got.reshape(len(docs), len(ids))[rl, li]) >> 16 == K._native.KW_ARG_WIDE
+    assert int(got.reshape(len(docs), len(ids))[rc, ci]) >> 16 == K._native.KW_ARG_WIDE
+    assert b.wide_arg(rl, li) == n - 1
+    assert b.wide_arg(rc, ci) == n - 1
