@@ -279,6 +279,7 @@ struct DeviceBatch {
   size_t nfa_scratch_cap = 0;
   uint32_t max_image_len = 0xffffffffu;  // longest image reference of the batch (computed on first use)
   uint32_t* wide_count = nullptr;
+  bool wide_valid = false;  // the last pass zeroed wide_count and ran the overflow kernels
   WideRec* wide_rec = nullptr;
   size_t wide_rec_cap = 0;
   uint64_t* wide_groups = nullptr;
@@ -1288,7 +1289,10 @@ int prepare_pass(kw_batch* kb, PassPlan& plan, hipStream_t s, EvalArgs* out_args
     HIPCHK(dev_pool().alloc(D.device, sizeof(uint32_t), &p));
     D.wide_count = (uint32_t*)p;
   }
-  HIPCHK(hipMemsetAsync(D.wide_count, 0, sizeof(uint32_t), s));
+  // only the overflow kernels append wide records: a pass without overflow requests leaves the
+  // counter alone (no fill launched between back-to-back passes) and has no records to read back
+  D.wide_valid = D.n_overflow != 0;
+  if (D.wide_valid) HIPCHK(hipMemsetAsync(D.wide_count, 0, sizeof(uint32_t), s));
   A.wide_count = D.wide_count;
   if (D.n_overflow) {
     if (int rc = ensure_overflow_classes(B, &D, plan.geom, &A)) return rc;
@@ -1998,7 +2002,7 @@ int load_side_data(kw_batch* b, hipStream_t s) {
   WideData& W = b->b.wide;
   W.clear();
   uint32_t nrec = 0;
-  if (D.wide_count) HIPCHK(hipMemcpyAsync(&nrec, D.wide_count, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  if (D.wide_count && D.wide_valid) HIPCHK(hipMemcpyAsync(&nrec, D.wide_count, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   W.nwide = D.last_nwide;
   W.wide_policy = D.last_wide_policy;
   W.rows_mode = D.last_rows_mode;
@@ -2204,6 +2208,8 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
     if (!cd.empty() && fail(launch_evaluate_tiles(Ak, plan.tiles[0], D.d_tiles, dd, plan.grid, sc))) break;
     if (co[0]) {  // rare: synchronous set-up, then the overflow kernels on the chunk's requests
       if (fail(hipStreamSynchronize(sc))) break;
+      if (n_ovf == 0 && fail(hipMemsetAsync(D.wide_count, 0, sizeof(uint32_t), sc))) break;  // (first overflow chunk)
+      D.wide_valid = true;
       n_ovf += co[0];
       if (code(ensure(&D.overflow, &D.overflow_cap, co.size())) || code(ensure_overflow_classes(B, &D, G, &A))) break;
       const size_t cap = (size_t)n_ovf * plan.wide_cap_per_row;
