@@ -72,6 +72,9 @@
 #ifndef KW_P3_BITS  // P3 verdict words from 32-bit halves and bit-selects (no 64-bit shifts or branches)
 #define KW_P3_BITS 1
 #endif
+#ifndef KW_IMG_MIN_WAVES  // image-only instantiation: minimum waves per SIMD (6: at most 80 VGPRs)
+#define KW_IMG_MIN_WAVES KW_MIN_WAVES
+#endif
 #ifndef KW_VBASE  // tile kernel: LDS region offsets in VGPRs in the label / container instantiation
 #define KW_VBASE 1
 #endif
@@ -538,8 +541,15 @@ __device__ inline void prefetch_l2(const void* src, uint32_t bytes, uint8_t* scr
 
 // TIMING: the diagnostics instantiation (EvalArgs::phase) — phase clocks add registers, so the
 // product kernel is compiled without them.
+// Minimum waves per SIMD the register allocation must allow: the image-only instantiation (C2) is
+// register-bound at 5 workgroups per CU (86 VGPRs) while its LDS allows 6 (KW_IMG_MIN_WAVES).
+template <bool LDST, uint32_t F>
+constexpr int tile_min_waves() {
+  return (LDST && F == kFeatImg) ? KW_IMG_MIN_WAVES : KW_MIN_WAVES;
+}
+
 template <bool LDST, bool TIMING, uint32_t F>
-__global__ void __launch_bounds__(kSlotThreads, KW_MIN_WAVES)
+__global__ void __launch_bounds__(kSlotThreads, (tile_min_waves<LDST, F>()))
     evaluate_tiles_kernel(EvalArgs a, const TileArgs* __restrict__ tp, const TileDesc* __restrict__ desc) {
   // TileArgs lives in device memory: its fields are scalar-loaded where used instead of all being
   // hoisted from the kernarg segment into SGPRs at entry.
