@@ -284,6 +284,13 @@ int kw_batch_verdicts(kw_batch *b, uint32_t *host_out, size_t count);
  * for a bulk caller, the per-request loop of acquire_semaphore_and_evaluate (handlers.rs:256-286). */
 int kw_validate_host(const kw_env *env, kw_batch *b, const int32_t *policies, uint32_t npol, int origin,
                      int device, uint32_t *out, size_t count, uint32_t chunk_rows);
+/* Page-lock the batch's large host column arrays in place (hipHostRegister; undone by
+ * kw_batch_destroy) so kw_validate_host sends them to the device by DMA from where they lie instead
+ * of through the pinned staging its host workers fill. For a caller that runs several bulk passes
+ * over one batch, or that builds batches once and keeps them; registering costs about as much as one
+ * staging fill. Arrays under 64 KiB, and any the runtime declines, stay staged. No reference
+ * counterpart (a host-memory option of the bulk entry point). */
+int kw_batch_pin_host(kw_batch *b, int device);
 /* Pinned (page-locked) host memory for verdict buffers a caller keeps (direct DMA), and its release. */
 int kw_host_alloc(int device, size_t bytes, void **out);
 void kw_host_free(void *p);

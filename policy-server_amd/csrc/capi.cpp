@@ -86,6 +86,62 @@ BlockPool& host_pool() {
   return *p;
 }
 
+// Non-blocking streams and timing-free events handed back for reuse, per device: creating a
+// stream costs host time on the order of a tenth of a millisecond, and a bulk pass used three.
+// A stream returns here drained (its owner synchronized it). KW_STREAM_POOL=0: A/B knob.
+struct StreamPool {
+  std::mutex m;
+  std::map<int, std::vector<hipStream_t>> streams;
+  std::map<int, std::vector<hipEvent_t>> events;
+  const bool on = !(getenv("KW_STREAM_POOL") && atoi(getenv("KW_STREAM_POOL")) == 0);
+  hipError_t get(int dev, hipStream_t* s) {
+    if (on) {
+      std::lock_guard<std::mutex> g(m);
+      auto& v = streams[dev];
+      if (!v.empty()) {
+        *s = v.back();
+        v.pop_back();
+        return hipSuccess;
+      }
+    }
+    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+  }
+  void put(int dev, hipStream_t s) {
+    if (!s) return;
+    if (!on) {
+      (void)hipStreamDestroy(s);
+      return;
+    }
+    std::lock_guard<std::mutex> g(m);
+    streams[dev].push_back(s);
+  }
+  hipError_t get(int dev, hipEvent_t* e) {
+    if (on) {
+      std::lock_guard<std::mutex> g(m);
+      auto& v = events[dev];
+      if (!v.empty()) {
+        *e = v.back();
+        v.pop_back();
+        return hipSuccess;
+      }
+    }
+    return hipEventCreateWithFlags(e, hipEventDisableTiming);
+  }
+  void put(int dev, hipEvent_t e) {
+    if (!e) return;
+    if (!on) {
+      (void)hipEventDestroy(e);
+      return;
+    }
+    std::lock_guard<std::mutex> g(m);
+    events[dev].push_back(e);
+  }
+};
+StreamPool& stream_pool() {
+  static StreamPool* p = new StreamPool;  // process lifetime, like the block pools
+  return *p;
+}
+
 // Host copy spread over up to 16 threads for large buffers (staging fills and verdict read-back:
 // one thread moves ≈ 10 GB/s, the host's memory system several times that).
 void parallel_copy(void* dst, const void* src, size_t bytes) {
@@ -338,7 +394,7 @@ struct DeviceBatch {
     host_pool().release(device, staging, staging_bytes);
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
-    if (stream && owns_stream) (void)hipStreamDestroy(stream);
+    if (stream && owns_stream) stream_pool().put(device, stream);
   }
 };
 
@@ -347,6 +403,10 @@ struct DeviceBatch {
 struct kw_batch {
   Batch b;
   std::unique_ptr<DeviceBatch> dev;
+  std::vector<void*> host_pinned;  // kw_batch_pin_host: column arrays page-locked in place
+  ~kw_batch() {
+    for (void* p : host_pinned) (void)hipHostUnregister(p);
+  }
 };
 
 namespace {
@@ -1906,7 +1966,7 @@ int layout_batch(kw_batch* kb, int device, hipStream_t stream, std::vector<Piece
     D->stream = stream;
     D->owns_stream = false;
   } else {
-    HIPCHK(hipStreamCreateWithFlags(&D->stream, hipStreamNonBlocking));
+    HIPCHK(stream_pool().get(device, &D->stream));
   }
   Batch& B = kb->b;
   B.finalize();
@@ -2070,6 +2130,16 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
   const uint32_t need = plan.geom.need;
   t_plan = since(t_start) - t_layout;
   auto wanted = [&](const Piece& p) { return p.m < 0 || ((need >> p.m) & 1u); };
+  // columns page-locked in place (kw_batch_pin_host) go to the device by DMA from where they lie;
+  // the others through the pinned staging, filled by the host workers
+  std::vector<char> dma(pieces.size(), 0);
+  if (!kb->host_pinned.empty())
+    for (size_t i = 0; i < pieces.size(); ++i) {
+      hipPointerAttribute_t pa;
+      dma[i] = pieces[i].bytes && hipPointerGetAttributes(&pa, pieces[i].src) == hipSuccess &&
+               pa.type == hipMemoryTypeHost;
+      (void)hipGetLastError();
+    }
   uint8_t* st = (uint8_t*)D.staging;
   hipStream_t sc = D.stream;
   EvalArgs A;
@@ -2078,10 +2148,14 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
                        !(plan.geom.debug & 512u) && !(plan.geom.feat & kFeatNfa) && B.n > 0;
   if (!chunked) {  // one upload, the full pass, one read-back
     std::vector<CopySeg> segs;
-    for (const Piece& p : pieces)
-      if (p.bytes) segs.push_back({st + p.at, p.src, p.bytes});
+    for (size_t i = 0; i < pieces.size(); ++i)
+      if (pieces[i].bytes && !dma[i]) segs.push_back({st + pieces[i].at, pieces[i].src, pieces[i].bytes});
     parallel_copy_segs(segs);
-    HIPCHK(hipMemcpyAsync(D.cols, st, D.cols_bytes, hipMemcpyHostToDevice, sc));
+    for (const CopySeg& c : segs)
+      HIPCHK(hipMemcpyAsync(D.cols + ((uint8_t*)c.dst - st), c.dst, c.bytes, hipMemcpyHostToDevice, sc));
+    for (size_t i = 0; i < pieces.size(); ++i)
+      if (pieces[i].bytes && dma[i])
+        HIPCHK(hipMemcpyAsync(D.cols + pieces[i].at, pieces[i].src, pieces[i].bytes, hipMemcpyHostToDevice, sc));
     if (int rc = run_validate(env, kb, plan, origin, false, sc)) return rc;
     return kw_batch_verdicts(kb, out, count);
   }
@@ -2148,10 +2222,10 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
     return !code(ensure(&D.desc, &D.desc_cap, (size_t)(2 * dcap)));
   };
   if (rc == KW_OK) (void)alloc_descs();
-  if (rc == KW_OK && !fail(hipStreamCreateWithFlags(&s_in, hipStreamNonBlocking)) &&
-      !fail(hipStreamCreateWithFlags(&s_out, hipStreamNonBlocking)))
+  StreamPool& SP = stream_pool();
+  if (rc == KW_OK && !fail(SP.get(device, &s_in)) && !fail(SP.get(device, &s_out)))
     for (auto& e : ev)
-      if (fail(hipEventCreateWithFlags(&e, hipEventDisableTiming))) break;
+      if (fail(SP.get(device, &e))) break;
   auto copy_out = [&](uint64_t k) {
     const auto t0 = clk::now();
     if (pinned || rc != KW_OK || fail(hipEventSynchronize(ev[3 * k + 2]))) return;
@@ -2168,19 +2242,28 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
     if (pinned && depth && k >= depth && fail(hipEventSynchronize(ev[3 * (k - depth) + 2]))) break;
     // the chunk's columns first: their H2D starts at once, and the descriptor build below then
     // reads offsets the fill has just brought into the host caches
-    std::vector<CopySeg> segs;
-    for (const Piece& p : pieces) {
+    std::vector<CopySeg> segs, dsegs;  // (staged, direct)
+    for (size_t i = 0; i < pieces.size(); ++i) {
+      const Piece& p = pieces[i];
       if (!wanted(p)) continue;
       size_t lo, hi;
       piece_range(B, p, r0, r1, k + 1 == K, &lo, &hi);
-      if (hi > lo) segs.push_back({st + p.at + lo, (const uint8_t*)p.src + lo, hi - lo});
+      if (hi <= lo) continue;
+      if (dma[i])
+        dsegs.push_back({D.cols + p.at + lo, (const uint8_t*)p.src + lo, hi - lo});
+      else
+        segs.push_back({st + p.at + lo, (const uint8_t*)p.src + lo, hi - lo});
     }
     const auto t0 = clk::now();
     parallel_copy_segs(segs);
     t_fill += since(t0);
     const auto t1 = clk::now();
+    for (const CopySeg& c : dsegs)
+      if (fail(hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyHostToDevice, s_in))) break;
     for (const CopySeg& c : segs)
-      if (fail(hipMemcpyAsync(D.cols + ((uint8_t*)c.dst - st), c.dst, c.bytes, hipMemcpyHostToDevice, s_in))) break;
+      if (rc != KW_OK ||
+          fail(hipMemcpyAsync(D.cols + ((uint8_t*)c.dst - st), c.dst, c.bytes, hipMemcpyHostToDevice, s_in)))
+        break;
     if (rc != KW_OK) break;
     t_enq += since(t1);
     const auto td = clk::now();
@@ -2241,16 +2324,11 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
   if (s_in) (void)hipStreamSynchronize(s_in);
   (void)hipStreamSynchronize(sc);
   if (s_out) (void)hipStreamSynchronize(s_out);
-  if (dbg)
-    fprintf(stderr,
-            "[kw bulk] rows %llu chunks %llu pinned %d overflow %llu: layout %.2f plan %.2f prepare %.2f descs %.2f fill %.2f "
-            "enqueue %.2f copy-out %.2f first chunk queued at %.2f, final wait %.2f, total %.2f ms\n",
-            (unsigned long long)B.n, (unsigned long long)K, pinned ? 1 : 0, (unsigned long long)n_ovf, t_layout, t_plan, t_prep,
-            t_desc, t_fill, t_enq, t_out, t_first, since(t_w), since(t_start));
-  for (auto& e : ev)
-    if (e) (void)hipEventDestroy(e);
-  if (s_in) (void)hipStreamDestroy(s_in);
-  if (s_out) (void)hipStreamDestroy(s_out);
+  const double t_wait = since(t_w);
+  const auto t_td = clk::now();
+  for (auto& e : ev) SP.put(device, e);
+  SP.put(device, s_in);
+  SP.put(device, s_out);
   for (auto& b : bounce) host_pool().release(device, b, bounce_bytes);
   if (hdesc) host_pool().release(device, hdesc, hdesc_bytes);
   D.last_wide_cap = A.wide_cap;
@@ -2259,7 +2337,16 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
     D.loaded = 0;
     return rc;
   }
-  return load_side_data(kb, sc);  // overflow requests' wide arguments (kw_batch_wide_arg)
+  rc = load_side_data(kb, sc);  // overflow requests' wide arguments (kw_batch_wide_arg)
+  if (dbg)
+    fprintf(stderr,
+            "[kw bulk] rows %llu chunks %llu pinned %d direct-columns %d overflow %llu: layout %.2f plan %.2f prepare %.2f "
+            "descs %.2f fill %.2f enqueue %.2f copy-out %.2f first chunk queued at %.2f, final wait %.2f, teardown %.2f, "
+            "total %.2f ms\n",
+            (unsigned long long)B.n, (unsigned long long)K, pinned ? 1 : 0, (int)std::count(dma.begin(), dma.end(), 1),
+            (unsigned long long)n_ovf, t_layout, t_plan, t_prep, t_desc, t_fill, t_enq, t_out, t_first, t_wait, since(t_td),
+            since(t_start));
+  return rc;
 }
 }  // namespace
 
@@ -2303,6 +2390,33 @@ void kw_stream_destroy(void* stream) {
 }
 
 void kw_batch_destroy(kw_batch* b) { delete b; }
+
+int kw_batch_pin_host(kw_batch* kb, int device) {
+  if (!kb || device < 0) return KW_E_ARG;
+  if (!kb->host_pinned.empty()) return KW_OK;
+  HIPCHK(hipSetDevice(device));
+  Batch& B = kb->b;
+  B.finalize();  // (pads the byte pools now: later passes do not resize what is registered)
+  std::vector<std::pair<void*, size_t>> cols = {
+      {B.req_flags.data(), B.req_flags.size()},   {B.ctr_off.data(), B.ctr_off.size() * 4},
+      {B.lbl_off.data(), B.lbl_off.size() * 4},   {B.ctr_flags.data(), B.ctr_flags.size()},
+      {B.capadd_off.data(), B.capadd_off.size() * 4}, {B.capdrop_off.data(), B.capdrop_off.size() * 4}};
+  for (int m = 0; m < (int)NSTR; ++m) {
+    const StrCol& c = host_str(B, m);
+    cols.push_back({(void*)c.off.data(), c.off.size() * 4});
+    cols.push_back({(void*)c.bytes.data(), c.bytes.size()});
+  }
+  // small arrays may share a page with another allocation: they stay pageable (staged), as does
+  // any array the runtime declines to register
+  for (const auto& [p, n] : cols) {
+    if (n < ((size_t)1 << 16)) continue;
+    if (hipHostRegister(p, n, hipHostRegisterDefault) == hipSuccess)
+      kb->host_pinned.push_back(p);
+    else
+      (void)hipGetLastError();
+  }
+  return KW_OK;
+}
 
 int kw_validate_batch(const kw_env* env, kw_batch* b, const int32_t* policies, uint32_t npol, int origin, void* stream) {
   PassPlan plan;

@@ -369,6 +369,12 @@ class Batch:
         raise_for(rc, "kw_batch_verdicts failed")
         return out
 
+    def pin_host(self, device=0):
+        """Page-lock the batch's large host columns in place (kw_batch_pin_host): later bulk passes
+        (validate_host) DMA them without the staging copy."""
+        raise_for(self._L.kw_batch_pin_host(self._h, device), "kw_batch_pin_host failed")
+        return self
+
     def validate_host(self, env, policies, out=None, origin=VALIDATE, device=0, chunk_rows=0):
         """Bulk host -> host pass (kw_validate_host): upload, evaluate and read back in overlapped row
         chunks; returns the [row][npol] verdict words in `out` (a reused uint32 array, pinned ones from

@@ -87,7 +87,7 @@ EXPORTS = [
     "kw_env_policy_initialization_error", "kw_env_validate_settings", "kw_pattern_match", "kw_pattern_match_many", "kw_env_pattern_count",
     "kw_env_pattern", "kw_env_classify", "kw_batch_wide_arg", "kw_batch_group_causes", "kw_debug_plan",
     "kw_batch_from_json", "kw_batch_from_soa", "kw_batch_view", "kw_batch_to_device", "kw_batch_to_device_async",
-    "kw_stream_create", "kw_stream_destroy", "kw_validate_host", "kw_host_alloc", "kw_host_free",
+    "kw_stream_create", "kw_stream_destroy", "kw_validate_host", "kw_batch_pin_host", "kw_host_alloc", "kw_host_free",
     "kw_batch_destroy", "kw_debug_host_walk", "kw_validate_batch", "kw_validate_rows", "kw_batch_verdicts",
     "kw_validate_timed", "kw_format_response", "kw_format_response_doc", "kw_env_group_members", "kw_evaluate",
     "kw_service_constraints", "kw_metrics_create", "kw_metrics_destroy", "kw_metrics_record", "kw_metrics_render",
@@ -144,6 +144,7 @@ def lib():
         "kw_validate_rows": (ip, [vp, vp, C.POINTER(i32), ip, vp]),
         "kw_batch_verdicts": (ip, [vp, C.POINTER(u32), sz]),
         "kw_validate_host": (ip, [vp, vp, C.POINTER(i32), u32, ip, ip, C.POINTER(u32), sz, u32]),
+        "kw_batch_pin_host": (ip, [vp, ip]),
         "kw_host_alloc": (ip, [ip, sz, C.POINTER(vp)]),
         "kw_host_free": (None, [vp]),
         "kw_debug_host_walk": (ip, [vp, vp, C.POINTER(i32), u32, ip, C.POINTER(u32)]),

@@ -175,3 +175,33 @@ def test_bulk_overflow_wide_arguments_across_chunks():
     assert int(got.reshape(len(docs), len(ids))[rc, ci]) >> 16 == K._native.KW_ARG_WIDE
     assert b.wide_arg(rl, li) == n - 1
     assert b.wide_arg(rc, ci) == n - 1
+
+
+@pytest.mark.parametrize("name,scfg,rows,chunk", [
+    ("c4_64", 4, 200000, 8192),   # chunked: the big columns DMA'd in place, the small ones staged
+    ("c4_64", 4, 200000, 0),
+    ("c2_trusted", 2, 120000, 3000),
+    ("many", 6, 20000, 512),      # C6's wide group: the unchunked form with in-place columns
+])
+def test_bulk_pinned_columns_match_oracle(name, scfg, rows, chunk):
+    """kw_batch_pin_host: the batch's large columns page-locked in place and sent by DMA from where
+    they lie; the same verdict words as the staged path, pass after pass, into pageable and pinned
+    output, and the batch is destroyed with its registration."""
+    env, oe = _envs(many_policies_config() if name == "many" else config(name))
+    ids = env.policy_ids()
+    syn = K.SynthBatch(scfg, rows, seed=5100 + scfg)
+    ora = oe.eval(syn.soa(), ids, K.VALIDATE)
+    b = syn.batch().pin_host(0)
+    b.pin_host(0)  # idempotent
+    got = b.validate_host(env, ids, chunk_rows=chunk)
+    assert np.array_equal(got, ora), diff_verdicts(got, ora, len(ids), ids)
+    pin = K.PinnedWords(rows * len(ids))
+    try:
+        for origin in (K.AUDIT, K.VALIDATE):
+            pin.array.fill(0xA5A5A5A5)
+            got2 = b.validate_host(env, ids, out=pin.array, origin=origin, chunk_rows=chunk)
+            ora2 = ora if origin == K.VALIDATE else oe.eval(syn.soa(), ids, origin)
+            assert np.array_equal(got2, ora2), diff_verdicts(got2, ora2, len(ids), ids)
+    finally:
+        pin.close()
+    b.close()
