@@ -284,7 +284,7 @@ def host_modes(env, ids, syn, device, args, alg_bytes=None):
         out["end_to_end"] = {"value": syn.n / dt, "unit": "requests/s", "rows": syn.n, "ms": dt * 1e3,
                              "what": "kw_validate_host: host SoA -> pinned staging (host workers) -> H2D -> evaluate -> "
                                      "D2H straight into a pinned verdict buffer the caller keeps, in overlapped "
-                                     "131072-row chunks on three streams; plan and tile descriptors included, best of 3"}
+                                     "262144-row chunks on three streams; plan and tile descriptors included, best of 3"}
         # the same with the batch's columns page-locked in place beforehand (kw_batch_pin_host, untimed;
         # its own cost reported beside): no staging fill on the host workers
         reg = []

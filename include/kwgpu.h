@@ -276,7 +276,7 @@ int kw_batch_verdicts(kw_batch *b, uint32_t *host_out, size_t count);
 /* Bulk form for callers that hand over host columns and want host verdicts (SURVEY §8(d) timing
  * mode 2): uploads the batch to `device`, evaluates every row against the npol policies and writes
  * the [row][npol] verdict words to host `out` (count = rows x npol). The batch is cut into chunks of
- * about chunk_rows rows (0: 131072) whose upload, evaluation and read-back overlap on three streams;
+ * about chunk_rows rows (0: 262144) whose upload, evaluation and read-back overlap on three streams;
  * only the string columns the pass reads are uploaded (a later pass on the batch that needs others
  * returns KW_E_ARG until the batch is uploaded again). `out` may be pageable (read back through
  * pinned bounce blocks) or pinned (kw_host_alloc: direct DMA). Passes that need several launches,

@@ -2169,7 +2169,7 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
   D.loaded = need;
   const TileArgs& G = plan.geom;
   const uint64_t ntiles = (B.n + G.rows - 1) / G.rows;
-  static const uint64_t def_chunk = getenv("KW_BULK_CHUNK") ? std::max(1, atoi(getenv("KW_BULK_CHUNK"))) : 131072;  // A/B knob
+  static const uint64_t def_chunk = getenv("KW_BULK_CHUNK") ? std::max(1, atoi(getenv("KW_BULK_CHUNK"))) : 262144;  // A/B knob (profiles/r04_bulk_sweep.txt)
   const uint64_t per = chunk_rows ? chunk_rows : def_chunk;
   // chunk k: tiles [tb[k], tb[k+1]). The read-back stream is the longest (4 B x npol per request
   // out vs the request's columns in), so the first chunks are small (1/16 of `per`, doubling) to
