@@ -50,6 +50,21 @@ def test_hot_path_requires_a_device():
         b.validate(env, ["pod-privileged"])  # not resident, no device
 
 
+def test_pin_host_arguments():
+    """kw_batch_pin_host refuses a null batch and a negative device (KW_E_ARG) before touching
+    the runtime; on a host without a GPU a real device index fails as a device error."""
+    L = K._native.lib()
+    assert L.kw_batch_pin_host(None, 0) == K._native.KW_E_ARG
+    b = K.Batch.from_json([reference_doc("pod_with_privileged_containers.json")])
+    with pytest.raises(K.EvaluationError) as e:
+        b.pin_host(-1)
+    assert e.value.code == K._native.KW_E_ARG
+    import torch
+    if not torch.cuda.is_available():
+        with pytest.raises(K.DeviceError):
+            b.pin_host(0)
+
+
 def test_lookup_and_accessors():
     env = K.EvaluationEnvironment(config("parity"), continue_on_errors=True, always_accept_namespace="kubewarden")
     assert env.get_policy_mode("trusted-images") == K.MONITOR
