@@ -205,3 +205,36 @@ def test_bulk_pinned_columns_match_oracle(name, scfg, rows, chunk):
     finally:
         pin.close()
     b.close()
+
+
+def test_bulk_concurrent_callers_share_the_pools():
+    """Four host threads run bulk passes at once on their own batches (the ctypes call releases the
+    GIL): the pooled streams, events, staging and device blocks are handed out under their locks, and
+    every thread's verdict words match the oracle, pass after pass."""
+    import threading
+    env, oe = _envs(config("c4_64"))
+    ids = env.policy_ids()
+    syns = [K.SynthBatch(4, 20000 + 1000 * i, seed=6100 + i) for i in range(4)]
+    oras = [oe.eval(s.soa(), ids, K.VALIDATE) for s in syns]
+    errors = []
+
+    def run(i):
+        try:
+            for rep in range(3):
+                b = syns[i].batch()
+                if (i + rep) % 2:
+                    b.pin_host(0)
+                got = b.validate_host(env, ids, chunk_rows=4096)
+                if not np.array_equal(got, oras[i]):
+                    errors.append((i, rep, diff_verdicts(got, oras[i], len(ids), ids)))
+                b.close()
+        except Exception as e:  # noqa: BLE001 (reported below with its thread)
+            errors.append((i, "raised", repr(e)))
+
+    ts = [threading.Thread(target=run, args=(i,)) for i in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=100)
+    assert not any(t.is_alive() for t in ts)
+    assert not errors, errors[:2]
