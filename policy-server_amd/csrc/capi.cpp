@@ -2190,8 +2190,12 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
   (void)hipGetLastError();  // a pageable pointer leaves an error state behind
   // pinned output: at most `depth` chunks in flight past the read-back. Unbounded, the host queues
   // every chunk's copies and launch at once and the copies run slower (C4 1M: 16.0-16.7 ms vs
-  // 9.7-10.9 at depth 2, profiles/r04_bulk_modes.txt). KW_BULK_DEPTH: A/B knob, 0 = unbounded.
-  static const uint64_t depth = getenv("KW_BULK_DEPTH") ? (uint64_t)std::max(0, atoi(getenv("KW_BULK_DEPTH"))) : 2;
+  // 9.7-10.9 at depth 2, profiles/r04_bulk_modes.txt). Staged columns take 3 (the host fills pace
+  // the uploads), columns DMA'd in place 2 (at 3 their uploads crowd the read-backs: 11.0 vs
+  // 7.1 ms, profiles/r04_bulk_sweep.txt). KW_BULK_DEPTH: A/B knob, 0 = unbounded.
+  static const int depth_knob = getenv("KW_BULK_DEPTH") ? std::max(0, atoi(getenv("KW_BULK_DEPTH"))) : -1;
+  const bool any_dma = std::count(dma.begin(), dma.end(), 1) > 0;
+  const uint64_t depth = depth_knob >= 0 ? (uint64_t)depth_knob : (any_dma ? 2 : 3);
   const uint64_t max_rows = std::min<uint64_t>(B.n, tper * G.rows);
   const size_t bounce_bytes = (size_t)max_rows * npol * 4;
   void* bounce[2] = {nullptr, nullptr};
