@@ -28,6 +28,11 @@ import re
 
 import numpy as np
 
+try:
+    from . import rhaisub  # noqa: F401  (package import)
+except ImportError:
+    import rhaisub
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "build", "libkworacle.so")
 
@@ -345,16 +350,28 @@ def _family(module):
     return 0
 
 
+_ABSENT = object()
+
+
 def _ctx_ok(v):
-    if v is None:
+    """`#[serde(default)] context_aware_resources: BTreeSet<_>` (config.rs:349-350, 376-378): an
+    absent key is the empty set; an explicit null is not a sequence and fails the variant."""
+    if v is _ABSENT:
         return True
     return isinstance(v, list) and all(isinstance(x, dict) and isinstance(x.get("apiVersion"), str)
                                        and isinstance(x.get("kind"), str) for x in v)
 
 
 def _mode(v):
-    if v is None:
+    """`#[serde(default)] policy_mode: PolicyMode` (config.rs:287-294, 369-371): absent -> Protect;
+    present -> serde's buffered enum form: the variant name as a string, or a one-key map whose
+    value is unit ({"protect": null}). An explicit null matches neither."""
+    if v is _ABSENT:
         return PROTECT
+    if isinstance(v, dict) and len(v) == 1:
+        (k, val), = v.items()
+        if val is None:
+            v = k
     if v == "protect":
         return PROTECT
     if v == "monitor":
@@ -367,21 +384,21 @@ def parse_entry(name, v):
     if isinstance(v, dict):
         try:
             if isinstance(v.get("module"), str):
-                mode = _mode(v.get("policyMode"))
+                mode = _mode(v.get("policyMode", _ABSENT))
                 a2m = v.get("allowedToMutate")
                 if a2m is not None and not isinstance(a2m, bool):
                     raise ValueError
                 st = v.get("settings")
                 if st is not None and not isinstance(st, dict):
                     raise ValueError
-                if not _ctx_ok(v.get("contextAwareResources")):
+                if not _ctx_ok(v.get("contextAwareResources", _ABSENT)):
                     raise ValueError
                 return {"name": name, "group": False, "module": v["module"], "mode": mode, "a2m": bool(a2m),
                         "settings": st or {}}
         except ValueError:
             pass
         try:
-            mode = _mode(v.get("policyMode"))
+            mode = _mode(v.get("policyMode", _ABSENT))
             pols, ex, msg = v.get("policies"), v.get("expression"), v.get("message")
             if isinstance(pols, dict) and isinstance(ex, str) and isinstance(msg, str):
                 members = []
@@ -392,7 +409,7 @@ def parse_entry(name, v):
                         raise ValueError
                     if mv.get("settings") is not None and not isinstance(mv.get("settings"), dict):
                         raise ValueError
-                    if not _ctx_ok(mv.get("contextAwareResources")):
+                    if not _ctx_ok(mv.get("contextAwareResources", _ABSENT)):
                         raise ValueError
                     members.append({"name": mn, "module": mv["module"], "settings": mv.get("settings") or {}})
                 return {"name": name, "group": True, "mode": mode, "expression": ex, "message": msg,
@@ -494,308 +511,22 @@ def compile_settings(fam, s, olib):
 
 
 # ----------------------------------------------------------------------------- group expressions
-# The rhai script subset of policy-group expressions (PolicyGroupEvaluator, upstream
-# policy-evaluator v0.24.0 / rhai 1.21.0, absent from the reference tree; pinned only by
-# evaluation_environment.rs:979-1112). Restated here independently of the product's expr.cpp:
-# statements (`let x = e;`, `e;`), blocks whose value is a last expression without `;`, if / else if /
-# else expressions, bool / i64 / string literals, variables, member calls, ! - + and
-# || | ^ && & == != < <= > >= + - * / % with rhai's precedence; == != < ... between different types
-# are false (!= true); other type mismatches are "Function not found"; checked i64 arithmetic.
-# Validation runs the script with every member returning true; evaluation needs a bool.
-_TOK = re.compile(r"\s*(?:(?P<id>[A-Za-z_][A-Za-z0-9_]*)|(?P<int>[0-9][0-9_]*)|(?P<str>\")|"
-                  r"(?P<op>\|\||&&|==|!=|<=|>=|[<>+\-*/%!()|&^{};=]))")
-_I64 = (-(1 << 63), (1 << 63) - 1)
-
-
-class ExprError(Exception):
-    pass
-
-
-def _lex(s):
-    toks, i = [], 0
-    while i < len(s):
-        if s[i].isspace():
-            i += 1
-            continue
-        if s.startswith("//", i):
-            while i < len(s) and s[i] != "\n":
-                i += 1
-            continue
-        m = _TOK.match(s, i)
-        if not m or m.end() == i:
-            raise ExprError(f"Syntax error: unexpected character '{s[i]}'")
-        if m.group("id"):
-            toks.append(("id", m.group("id")))
-            i = m.end()
-        elif m.group("int"):
-            digits = m.group("int").replace("_", "")
-            if int(digits) > _I64[1]:
-                raise ExprError("Syntax error: integer literal too large")
-            toks.append(("int", int(digits)))
-            i = m.end()
-        elif m.group("str"):
-            j, out = m.end(), []
-            esc = {"n": "\n", "t": "\t", "r": "\r", "0": "\0", "\\": "\\", '"': '"', "'": "'"}
-            while True:
-                if j >= len(s):
-                    raise ExprError("Syntax error: unterminated string literal")
-                ch = s[j]
-                j += 1
-                if ch == '"':
-                    break
-                if ch == "\\":
-                    if j >= len(s):
-                        raise ExprError("Syntax error: unterminated string literal")
-                    e = s[j]
-                    j += 1
-                    if e not in esc:
-                        raise ExprError(f"Syntax error: invalid escape sequence \\{e}")
-                    out.append(esc[e])
-                else:
-                    out.append(ch)
-            toks.append(("str", "".join(out)))
-            i = j
-        else:
-            toks.append(("op", m.group("op")))
-            i = m.end()
-    toks.append(("end", None))
-    return toks
-
-
-_PREC = {"||": 30, "|": 30, "^": 30, "&&": 60, "&": 60, "==": 90, "!=": 90, "<": 110, "<=": 110, ">": 110, ">=": 110,
-         "+": 150, "-": 150, "*": 180, "/": 180, "%": 180}
+# The rhai subset of policy-group expressions lives in oracle/rhaisub.py (its own tokenizer, parser
+# and evaluator, independent of the product's expr.cpp). Validation runs the script with every
+# member returning true; evaluation needs a bool.
+ExprError = rhaisub.ExprError
+_I64 = (rhaisub.I64_MIN, rhaisub.I64_MAX)
 
 
 def parse_script(s, members):
-    """Script -> tree. Nodes: ('lit', value) (value: None for (), bool, int, str) | ('var', name) |
-    ('call', slot or -1, name) | ('un', op, a) | ('bin', op, a, b) | ('if', c, then, else or None) |
-    ('block', [statements], tail) | ('let', name, init). Raises ExprError on a syntax error."""
-    toks = _lex(s)
-    pos = [0]
-    peek = lambda: toks[pos[0]]  # noqa: E731
-
-    def isop(o):
-        return peek() == ("op", o)
-
-    def isid(o):
-        return peek() == ("id", o)
-
-    def near():
-        t = peek()
-        return "end of script" if t[0] == "end" else (f'"{t[1]}"' if t[0] == "str" else f"'{t[1]}'" if t[0] != "int" else str(t[1]))
-
-    def block(top):
-        stmts, tail = [], False
-        while True:
-            if (peek()[0] == "end") if top else isop("}"):
-                break
-            if peek()[0] == "end":
-                raise ExprError("Syntax error: expecting '}' to close the block")
-            block_like = False
-            if isid("let"):
-                pos[0] += 1
-                t = peek()
-                if t[0] != "id" or t[1] in ("let", "if", "else", "true", "false"):
-                    raise ExprError("Syntax error: expecting a variable name after 'let'")
-                pos[0] += 1
-                if not isop("="):
-                    raise ExprError("Syntax error: expecting '=' after the variable name")
-                pos[0] += 1
-                st = ("let", t[1], expr(0))
-            else:
-                block_like = isid("if") or isop("{")
-                st = expr(0)
-            stmts.append(st)
-            if isop(";"):
-                pos[0] += 1
-                tail = False
-                continue
-            if (peek()[0] == "end") if top else isop("}"):
-                tail = st[0] != "let"
-                break
-            if not block_like:
-                raise ExprError(f"Syntax error: expecting ';' to terminate this statement, found {near()}")
-            tail = False
-        return ("block", stmts, tail)
-
-    def expr(min_prec):
-        a = unary()
-        while True:
-            t = peek()
-            p = _PREC.get(t[1]) if t[0] == "op" else None
-            if p is None or p < min_prec:
-                return a
-            pos[0] += 1
-            a = ("bin", t[1], a, expr(p + 1))
-
-    def unary():
-        if peek()[0] == "op" and peek()[1] in ("!", "-", "+"):
-            op = peek()[1]
-            pos[0] += 1
-            return ("un", op, unary())
-        return primary()
-
-    def inner_block():
-        if not isop("{"):
-            raise ExprError(f"Syntax error: expecting '{{' after the if condition, found {near()}")
-        pos[0] += 1
-        b = block(False)
-        pos[0] += 1
-        return b
-
-    def primary():
-        t = peek()
-        pos[0] += 1
-        if t[0] in ("int", "str"):
-            return ("lit", t[1])
-        if t == ("op", "("):
-            e = expr(0)
-            if not isop(")"):
-                raise ExprError(f"Syntax error: expecting ')', found {near()}")
-            pos[0] += 1
-            return e
-        if t == ("op", "{"):
-            b = block(False)
-            pos[0] += 1
-            return b
-        if t[0] == "id":
-            if t[1] in ("true", "false"):
-                return ("lit", t[1] == "true")
-            if t[1] == "if":
-                c = expr(0)
-                then = inner_block()
-                other = None
-                if isid("else"):
-                    pos[0] += 1
-                    if isid("if"):
-                        other = primary()
-                    else:
-                        if not isop("{"):
-                            raise ExprError(f"Syntax error: expecting '{{' or 'if' after 'else', found {near()}")
-                        other = inner_block()
-                return ("if", c, then, other)
-            if t[1] in ("let", "else"):
-                raise ExprError(f"Syntax error: unexpected '{t[1]}'")
-            if not isop("("):
-                return ("var", t[1])
-            pos[0] += 1
-            if not isop(")"):
-                raise ExprError("Syntax error: member policies take no arguments")
-            pos[0] += 1
-            return ("call", members.index(t[1]) if t[1] in members else -1, t[1])
-        if t[0] == "end":
-            raise ExprError("Syntax error: expecting an expression, found end of script")
-        pos[0] -= 1
-        raise ExprError(f"Syntax error: unexpected {near()}")
-
-    return block(True)
+    """Script -> rhaisub.Program (raises ExprError on a syntax error or a refused construct)."""
+    return rhaisub.parse(s, list(members))
 
 
-def _tn(v):
-    return "()" if v is None else "bool" if isinstance(v, bool) else "i64" if isinstance(v, int) else "string"
-
-
-def run_script(root, member_ok):
+def run_script(prog, members, member_ok):
     """-> (error message or None, bool value, called members in call order)."""
-    called, scopes = [], []
-
-    def nf(op, a, b):
-        raise ExprError(f"Function not found: {op} ({_tn(a)}, {_tn(b)})")
-
-    def ev(n):
-        k = n[0]
-        if k == "lit":
-            return n[1]
-        if k == "var":
-            for name, v in reversed(scopes):
-                if name == n[1]:
-                    return v
-            raise ExprError(f"Variable not found: {n[1]}")
-        if k == "call":
-            if n[1] < 0:
-                raise ExprError(f"Function not found: {n[2]} ()")
-            if n[1] not in called:
-                called.append(n[1])
-            return bool(member_ok[n[1]])
-        if k == "un":
-            a = ev(n[2])
-            if n[1] == "!":
-                if not isinstance(a, bool):
-                    raise ExprError(f"Function not found: ! ({_tn(a)})")
-                return not a
-            if isinstance(a, bool) or not isinstance(a, int):
-                raise ExprError(f"Function not found: {n[1]} ({_tn(a)})")
-            if n[1] == "-" and a == _I64[0]:
-                raise ExprError(f"Negation overflow: -{a}")
-            return -a if n[1] == "-" else a
-        if k == "if":
-            c = ev(n[1])
-            if not isinstance(c, bool):
-                raise ExprError(f"Boolean value expected for the if condition, found {_tn(c)}")
-            if c:
-                return ev(n[2])
-            return ev(n[3]) if n[3] is not None else None
-        if k == "block":
-            depth = len(scopes)
-            v = None
-            for st in n[1]:
-                if st[0] == "let":
-                    scopes.append((st[1], ev(st[2])))
-                    v = None
-                else:
-                    v = ev(st)
-            del scopes[depth:]
-            return v if n[2] else None
-        op, a = n[1], ev(n[2])
-        if op in ("||", "&&"):
-            if not isinstance(a, bool):
-                raise ExprError(f"Function not found: {op} ({_tn(a)}, ...)")
-            if a == (op == "||"):
-                return a
-            b = ev(n[3])
-            if not isinstance(b, bool):
-                nf(op, a, b)
-            return b
-        b = ev(n[3])
-        same = type(a) is type(b)
-        if op in ("==", "!="):
-            return (same and a == b) == (op == "==")
-        if op in ("<", "<=", ">", ">="):
-            if not same:
-                return False
-            if isinstance(a, bool) or a is None:
-                nf(op, a, b)
-            return {"<": a < b, "<=": a <= b, ">": a > b, ">=": a >= b}[op]
-        if op in ("|", "&", "^"):
-            if same and isinstance(a, bool):
-                return {"|": a or b, "&": a and b, "^": a != b}[op]
-            if same and isinstance(a, int):
-                return {"|": a | b, "&": a & b, "^": a ^ b}[op]
-            nf(op, a, b)
-        if op == "+" and isinstance(a, str) and isinstance(b, str):
-            return a + b
-        if not (same and isinstance(a, int) and not isinstance(a, bool)):
-            nf(op, a, b)
-        text = f"{a} {op} {b}"
-        if op in ("/", "%"):
-            if b == 0:
-                raise ExprError(f"Division by zero: {text}")
-            if a == _I64[0] and b == -1:
-                raise ExprError(("Division overflow: " if op == "/" else "Modulo overflow: ") + text)
-            q = abs(a) // abs(b) * (1 if (a >= 0) == (b >= 0) else -1)  # truncation, as i64 division
-            return q if op == "/" else a - q * b
-        r = {"+": a + b, "-": a - b, "*": a * b}[op]
-        if not _I64[0] <= r <= _I64[1]:
-            raise ExprError({"+": "Addition", "-": "Subtraction", "*": "Multiplication"}[op] + " overflow: " + text)
-        return r
-
-    try:
-        v = ev(root)
-    except ExprError as e:
-        return str(e), False, called
-    if not isinstance(v, bool):
-        return f"Output type incorrect: {_tn(v)} (expecting bool)", False, called
-    return None, v, called
+    err, v, called, _ = rhaisub.run(prog, list(members), member_ok)
+    return err, v, called
 
 
 def group_eval_message(m):
@@ -804,45 +535,15 @@ def group_eval_message(m):
     return "policy group expression evaluation failed: " + m
 
 
-def _has_call(n):
-    if n[0] == "call":
-        return True
-    return any(isinstance(x, tuple) and _has_call(x) for x in n[1:]) or \
-        (n[0] == "block" and any(_has_call(x) for x in n[1]))
-
-
-def _bool_subset(n):
-    """The script as the old bool-only tree (('const', 'bool', v) | ('call', s) | ('not', a) |
-    ('and'|'or'|'eq'|'ne', a, b)) when it is one: call-free subtrees folded to their values first;
-    None when it is not."""
-    if n[0] == "block":
-        if len(n[1]) == 1 and n[2]:
-            return _bool_subset(n[1][0])
-        return None
-    if not _has_call(n):
-        err, v, _ = run_script(("block", [n], True), [])
-        return ("const", "bool", v) if err is None else None
-    if n[0] == "call":
-        return ("call", n[1]) if n[1] >= 0 else None
-    if n[0] == "un" and n[1] == "!":
-        a = _bool_subset(n[2])
-        return ("not", a) if a is not None else None
-    if n[0] == "bin" and n[1] in ("&&", "||", "==", "!="):
-        a, b = _bool_subset(n[2]), _bool_subset(n[3])
-        if a is None or b is None:
-            return None
-        return ({"&&": "and", "||": "or", "==": "eq", "!=": "ne"}[n[1]], a, b)
-    return None
-
-
 def parse_expression(s, members):
-    """The group expression as the bool-only tree the C restatement evaluates (see _bool_subset);
+    """The group expression as the bool-only tree the C restatement evaluates (rhaisub.bool_tree);
     raises ExprError when the script does not validate or is not bool-only."""
-    root = parse_script(s, members)
-    err, _, _ = run_script(root, [True] * len(members))
+    members = list(members)
+    prog = rhaisub.parse(s, members)
+    err, _, _, _ = rhaisub.run(prog, members, [True] * len(members))
     if err is not None and not err.startswith("Output type incorrect"):
         raise ExprError(err)
-    t = _bool_subset(root)
+    t = rhaisub.bool_tree(prog, members)
     if t is None:
         raise ExprError("not a bool-only expression")
     return t
@@ -1062,31 +763,32 @@ class OracleEnv:
             names = p["member_names"]
             try:
                 root = parse_script(p["expression"], names)
-                err, _, _ = run_script(root, [True] * len(names))  # validate_settings: members return true
+                # validate_settings: members return true
+                err, _, _, steps = rhaisub.run(root, names, [True] * len(names))
                 if err is not None and not err.startswith("Output type incorrect"):
                     raise ExprError(err)
                 p["valid"] = True
                 p["script"] = root
-                if not _has_call(root):  # one outcome
-                    err, v, _ = run_script(root, [])
+                if not rhaisub.calls_members(root, names):  # one outcome
+                    err, v, _ = run_script(root, names, [True] * len(names))
                     if err is not None:
                         p["expr_error"] = group_eval_message(err)
                     else:
                         p["ast"] = ("const", "bool", v)
                     continue
-                t = _bool_subset(root)
+                t = rhaisub.bool_tree(root, names)
                 if t is not None:
                     if len(names) > 65535 or expr_depth(t) > 65536:
                         raise ExprError("policy group expression exceeds the engine's limits (65535 members, value "
                                         "stack 65536)")
                     p["ast"] = t
-                elif len(names) > 16:  # too many members for a truth table: run_script per row (_pyscript)
-                    p["pyscript"] = True
+                elif len(names) > 12 or (max(steps, 1) << len(names)) > (1 << 18):
+                    p["pyscript"] = True  # run_script per row (_pyscript) instead of a table
                 else:  # every vector of member results: value, error, causes (the C half looks it up)
                     tab = []
                     for mask in range(1 << len(names)):
                         ok = [bool((mask >> i) & 1) for i in range(len(names))]
-                        err, v, called = run_script(root, ok)
+                        err, v, called = run_script(root, names, ok)
                         e = 2 if err is not None else (1 if v else 0)
                         for c in called:
                             if not ok[c]:
@@ -1170,7 +872,7 @@ class OracleEnv:
 
     def _pyscript(self, P, member_ok):
         """-> (reason, cause mask, cause slots) of a _pyscript group over its members' results."""
-        err, value, called = run_script(P["script"], member_ok)
+        err, value, called = run_script(P["script"], P["member_names"], member_ok)
         if err is not None:
             return R_GROUP_EXPR, 0, []
         if value:
@@ -1266,7 +968,7 @@ class OracleEnv:
             for m in P["members"]:
                 md = self.detail(soa, row, m)
                 ok.append(md["reason"] == 0 and not md["mutated"])
-            err, _, _ = run_script(P["script"], ok)
+            err, _, _ = run_script(P["script"], P["member_names"], ok)
             return group_eval_message(err)
         if reason == R_INIT:
             return P["init_error"]

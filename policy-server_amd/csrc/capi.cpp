@@ -405,6 +405,7 @@ struct kw_batch {
   std::unique_ptr<DeviceBatch> dev;
   std::vector<void*> host_pinned;  // kw_batch_pin_host: column arrays page-locked in place
   ~kw_batch() {
+    dev.reset();  // synchronizes the batch's streams: no copy can still read a registered column
     for (void* p : host_pinned) (void)hipHostUnregister(p);
   }
 };
@@ -1452,8 +1453,11 @@ int run_validate(const kw_env* env, kw_batch* kb, PassPlan& plan, int origin, bo
   memcpy(h.data() + m_at, W.midx.data(), W.midx.size() * 4);
   HIPCHK(hipMemcpyAsync(D.wg_data, h.data(), bytes, hipMemcpyHostToDevice, s));
   const uint64_t pairs = n * W.groups.size();
-  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((pairs + 255) / 256, 1024));
   const size_t stack_words = std::max<uint32_t>(W.stack_words, 1);
+  // (a script that builds strings or arrays carries a 16 KB arena per thread: the grid keeps the
+  // scratch under 1 GiB; every thread loops over its pairs)
+  const uint64_t max_grid = std::max<uint64_t>(1, (1ull << 30) / (256ull * 8ull * stack_words));
+  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({(pairs + 255) / 256, 1024, max_grid}));
   if (int rc = ensure(&D.wg_stack, &D.wg_stack_cap, (size_t)grid * 256 * stack_words)) return rc;
   if (int rc = ensure(&D.big_causes, &D.big_causes_cap, (size_t)(n * W.cause_stride))) return rc;
   HIPCHK(hipMemsetAsync(D.big_causes, 0, (size_t)(n * W.cause_stride) * 8, s));
@@ -1858,9 +1862,14 @@ int kw_debug_host_walk(const kw_env* env, const kw_batch* kb, const int32_t* pol
           const uint32_t x = mw[r * nm + W.midx[g.midx_off + m]];
           return (x & KW_V_ALLOWED) && !(x & KW_V_MUTATED);
         };
+        uint64_t cz = 0;  // (the causes of a group of at most 15 members go into ARG)
+        auto cause = [&](uint32_t m) {
+          if (m < 64) cz |= 1ull << m;
+        };
+        auto rej = [&]() { return g.nmem <= 15 ? (g.rejb & 0xffffu) | ((uint32_t)cz << 16) : g.rejb; };
         if (g.kind == 1) {
-          const int v = run_script_prog(W.progs.data() + g.prog_off, stack.data(), ok, [](uint32_t) {});
-          *dst = v == 1 ? g.okw : v == 0 ? g.rejb : g.errw;
+          const int v = run_script_prog(W.progs.data() + g.prog_off, stack.data(), ok, cause);
+          *dst = v == 1 ? g.okw : v == 0 ? rej() : g.errw;
           continue;
         }
         if (g.kind >= 2) {
@@ -1868,8 +1877,8 @@ int kw_debug_host_walk(const kw_env* env, const kw_batch* kb, const int32_t* pol
                                [&](uint32_t m) { return mw[r * nm + W.midx[g.midx_off + m]]; });
           continue;
         }
-        const bool v = run_wide_prog(W.progs.data() + g.prog_off, g.prog_len, stack.data(), ok, [](uint32_t) {});
-        *dst = v ? g.okw : g.rejb;
+        const bool v = run_wide_prog(W.progs.data() + g.prog_off, g.prog_len, stack.data(), ok, cause);
+        *dst = v ? g.okw : rej();
       }
   }
   return KW_OK;
@@ -2196,7 +2205,9 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
   static const int depth_knob = getenv("KW_BULK_DEPTH") ? std::max(0, atoi(getenv("KW_BULK_DEPTH"))) : -1;
   const bool any_dma = std::count(dma.begin(), dma.end(), 1) > 0;
   const uint64_t depth = depth_knob >= 0 ? (uint64_t)depth_knob : (any_dma ? 2 : 3);
-  const uint64_t max_rows = std::min<uint64_t>(B.n, tper * G.rows);
+  // (the largest chunk, not `per`: past 256 chunks the last one takes every remaining tile)
+  uint64_t max_rows = 0;
+  for (uint64_t k = 0; k < K; ++k) max_rows = std::max(max_rows, row_of(tb[k + 1]) - row_of(tb[k]));
   const size_t bounce_bytes = (size_t)max_rows * npol * 4;
   void* bounce[2] = {nullptr, nullptr};
   // descriptors: two halves of `dcap` on the device and in pinned host memory (chunk k uses half

@@ -65,9 +65,33 @@ struct Entry {
   std::vector<Member> members;
 };
 
+// `#[serde(default)] policy_mode: PolicyMode` inside an untagged enum (config.rs:369-371,
+// :384-385): an absent key is the default (Protect); a present key goes through serde's buffered
+// enum deserializer, which takes a variant name as a string, or a single-key map whose value is
+// unit ({protect: null}). An explicit null is neither, so it fails the variant.
 bool parse_mode(const JDoc& d, int64_t n, uint8_t* mode, std::string* err) {
-  if (n < 0 || d.is((uint32_t)n, JType::Null)) {
+  if (n < 0) {
     *mode = KW_MODE_PROTECT;
+    return true;
+  }
+  if (d.is((uint32_t)n, JType::Obj)) {
+    auto ms = d.members((uint32_t)n);
+    uint32_t cnt = 0, only = 0;
+    for (uint32_t m : ms) {
+      only = m;
+      ++cnt;
+    }
+    if (cnt != 1 || !d.is(only, JType::Null)) {
+      *err = "invalid value: map, expected map with a single key";
+      return false;
+    }
+    std::string_view k = d.key(only);
+    if (k == "protect") *mode = KW_MODE_PROTECT;
+    else if (k == "monitor") *mode = KW_MODE_MONITOR;
+    else {
+      *err = "unknown variant `" + std::string(k) + "`, expected `monitor` or `protect`";
+      return false;
+    }
     return true;
   }
   if (!d.is((uint32_t)n, JType::Str)) {
@@ -88,8 +112,10 @@ bool check_settings_node(const JDoc& d, int64_t n) {
   return n < 0 || d.is((uint32_t)n, JType::Null) || d.is((uint32_t)n, JType::Obj);
 }
 
+// `#[serde(default)] context_aware_resources: BTreeSet<..>` (config.rs:349-350, :376-378): absent
+// is the empty set; an explicit null is not a sequence and fails the variant.
 bool check_ctx_resources(const JDoc& d, int64_t n) {
-  if (n < 0 || d.is((uint32_t)n, JType::Null)) return true;
+  if (n < 0) return true;
   if (!d.is((uint32_t)n, JType::Arr)) return false;
   for (uint32_t it : d.members((uint32_t)n)) {
     if (!d.is(it, JType::Obj)) return false;

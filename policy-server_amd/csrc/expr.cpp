@@ -1,12 +1,15 @@
-// expr.cpp — see expr.hpp. Lexer, recursive-descent parser with rhai precedence, a host
+// expr.cpp — see expr.hpp. Lexer, recursive-descent parser with rhai's precedence, a host
 // interpreter (validation, response messages, truth tables), constant folding of call-free
-// subtrees, and the device forms: short-circuit jump code or a truth table.
+// subtrees, and the device forms: short-circuit jump code, a truth table, or script bytecode
+// (kwdev.hpp SOp) for the typed stack machine of slots.hpp.
 #include "expr.hpp"
 
 #include <cctype>
 #include <climits>
 #include <algorithm>
+#include <cstdlib>
 #include <map>
+#include <set>
 
 #include "kwdev.hpp"
 
@@ -15,28 +18,78 @@ namespace kw {
 // ------------------------------------------------------------------------------------------
 // Values and the tree
 // ------------------------------------------------------------------------------------------
-enum class VT : uint8_t { Unit, Bool, Int, Str };
+enum class VT : uint8_t { Unit, Bool, Int, Str, Arr };
 struct Val {
   VT t = VT::Unit;
   bool b = false;
   int64_t i = 0;
   std::string s;
+  std::vector<Val> a;  // arrays (values are copied: rhai's value semantics)
 };
-static const char* tname(VT t) { return t == VT::Bool ? "bool" : t == VT::Int ? "i64" : t == VT::Str ? "string" : "()"; }
+static const char* tname(VT t) {
+  switch (t) {
+    case VT::Bool: return "bool";
+    case VT::Int: return "i64";
+    case VT::Str: return "string";
+    case VT::Arr: return "array";
+    default: return "()";
+  }
+}
+static Val vbool(bool b) {
+  Val v;
+  v.t = VT::Bool;
+  v.b = b;
+  return v;
+}
+static Val vint(int64_t i) {
+  Val v;
+  v.t = VT::Int;
+  v.i = i;
+  return v;
+}
+static Val vstr(std::string s) {
+  Val v;
+  v.t = VT::Str;
+  v.s = std::move(s);
+  return v;
+}
 
-struct Node {
-  enum K { Lit, Var, Call, Unary, Bin, If, Block, Let } k = Lit;
-  Val lit;            // Lit
-  std::string name;   // Var / Let
-  int slot = -1;      // Call
-  std::string op;     // Unary / Bin
-  std::vector<std::unique_ptr<Node>> kids;  // Unary: a; Bin: a b; If: cond then [else]; Block: statements; Let: init
-  bool tail = false;  // Block: its last statement is a value (no `;` after it)
-};
+const char* const kUnsupported = "unsupported by this engine: ";
+
+struct Node;
 using P = std::unique_ptr<Node>;
+struct SwitchCase {
+  std::vector<Val> vals;  // exact values (alternatives)
+  bool range = false, incl = false, wildcard = false;
+  int64_t lo = 0, hi = 0;
+  P guard, body;
+};
+struct Node {
+  enum K {
+    Lit, Var, Call, Unary, Bin, Coalesce, In, Range, If, Block, Let, Assign, IndexAssign, Index, Array, Switch,
+    While, DoWhile, Loop, For, Break, Continue, Return
+  } k = Lit;
+  Val lit;             // Lit
+  std::string name;    // Var / Let / Assign / IndexAssign (the variable) / Call (the function) / For (loop variable)
+  std::string name2;   // For: the index variable of `for (x, i) in ..` ("" none); Range: ".." "..=" or "range"
+  std::string op;      // Unary / Bin; Assign / IndexAssign: "" for `=`, else the operator of `op=`
+  bool flag = false;   // Block: tail value; Let: const; In: `!in`; Range: inclusive; DoWhile: until; Call: method style
+  int slot = -1;       // Call: member slot (a member called with no arguments)
+  int fn = -1;         // Call: script function (ExprAst::fns index)
+  int builtin = -1;    // Call: SFn id
+  std::vector<P> kids;
+  std::vector<SwitchCase> cases;  // Switch (kids[0] is the scrutinee)
+};
+
+struct FnDef {
+  std::string name;
+  std::vector<std::string> params;
+  P body;  // a Block
+};
 
 struct ExprAst {
   P root;  // a Block (the script)
+  std::vector<FnDef> fns;
 };
 
 namespace {
@@ -51,11 +104,34 @@ struct Token {
   int64_t v = 0;
 };
 
+void put_utf8(uint32_t c, std::string* o) {
+  if (c < 0x80) {
+    o->push_back((char)c);
+  } else if (c < 0x800) {
+    o->push_back((char)(0xC0 | (c >> 6)));
+    o->push_back((char)(0x80 | (c & 0x3F)));
+  } else if (c < 0x10000) {
+    o->push_back((char)(0xE0 | (c >> 12)));
+    o->push_back((char)(0x80 | ((c >> 6) & 0x3F)));
+    o->push_back((char)(0x80 | (c & 0x3F)));
+  } else {
+    o->push_back((char)(0xF0 | (c >> 18)));
+    o->push_back((char)(0x80 | ((c >> 12) & 0x3F)));
+    o->push_back((char)(0x80 | ((c >> 6) & 0x3F)));
+    o->push_back((char)(0x80 | (c & 0x3F)));
+  }
+}
+
 struct Lexer {
   std::vector<Token> toks;
   std::string err;
+  bool unsupported(const std::string& what) {
+    err = kUnsupported + what;
+    return false;
+  }
   bool run(const std::string& s) {
     size_t k = 0;
+    auto is_id = [&](size_t j) { return j < s.size() && (isalnum((unsigned char)s[j]) || s[j] == '_'); };
     while (k < s.size()) {
       const char c = s[k];
       if (isspace((unsigned char)c)) {
@@ -66,24 +142,68 @@ struct Lexer {
         while (k < s.size() && s[k] != '\n') ++k;
         continue;
       }
+      if (c == '/' && k + 1 < s.size() && s[k + 1] == '*') {  // block comment (rhai nests them)
+        int lvl = 0;
+        do {
+          if (s.compare(k, 2, "/*") == 0) {
+            ++lvl;
+            k += 2;
+          } else if (s.compare(k, 2, "*/") == 0) {
+            --lvl;
+            k += 2;
+          } else {
+            ++k;
+          }
+        } while (lvl > 0 && k < s.size());
+        if (lvl > 0) {
+          err = "Syntax error: unterminated block comment";
+          return false;
+        }
+        continue;
+      }
       Token t;
       if (isalpha((unsigned char)c) || c == '_') {
         const size_t b = k;
-        while (k < s.size() && (isalnum((unsigned char)s[k]) || s[k] == '_')) ++k;
+        while (is_id(k)) ++k;
         t.t = Tk::Ident;
         t.s = s.substr(b, k - b);
       } else if (isdigit((unsigned char)c)) {
         const size_t b = k;
-        while (k < s.size() && (isdigit((unsigned char)s[k]) || s[k] == '_')) ++k;
+        int base = 10;
+        if (c == '0' && k + 1 < s.size() && (s[k + 1] == 'x' || s[k + 1] == 'o' || s[k + 1] == 'b')) {
+          base = s[k + 1] == 'x' ? 16 : s[k + 1] == 'o' ? 8 : 2;
+          k += 2;
+        }
         std::string d;
-        for (size_t j = b; j < k; ++j)
-          if (s[j] != '_') d.push_back(s[j]);
-        if (d.size() > 19 || (d.size() == 19 && d > "9223372036854775807")) {
+        while (k < s.size() && (isalnum((unsigned char)s[k]) || s[k] == '_')) {
+          if (s[k] != '_') d.push_back(s[k]);
+          ++k;
+        }
+        if (base == 10 && k + 1 < s.size() && s[k] == '.' && isdigit((unsigned char)s[k + 1]))
+          return unsupported("floating-point numbers");
+        if (base == 10 && (d.find('e') != std::string::npos || d.find('E') != std::string::npos))
+          return unsupported("floating-point numbers");
+        if (d.empty()) {
+          err = "Syntax error: invalid number: " + s.substr(b, k - b);
+          return false;
+        }
+        unsigned __int128 v = 0;
+        for (char ch : d) {
+          int dv = isdigit((unsigned char)ch) ? ch - '0' : isxdigit((unsigned char)ch) ? (tolower(ch) - 'a' + 10) : 99;
+          if (dv >= base) {
+            err = "Syntax error: invalid number: " + s.substr(b, k - b);
+            return false;
+          }
+          v = std::min<unsigned __int128>(v * (unsigned)base + (unsigned)dv, (unsigned __int128)UINT64_MAX + 1);
+        }
+        // decimal literals are i64 (a leading '-' is the negation operator); rhai reads a
+        // hexadecimal / octal / binary literal as the bits of an i64
+        if ((base == 10 && v > (unsigned __int128)INT64_MAX) || v > (unsigned __int128)UINT64_MAX) {
           err = "Syntax error: integer literal too large";
           return false;
         }
         t.t = Tk::Int;
-        t.v = std::stoll(d);
+        t.v = (int64_t)(uint64_t)v;
       } else if (c == '"') {
         ++k;
         t.t = Tk::Str;
@@ -108,6 +228,29 @@ struct Lexer {
             case '\\': t.s.push_back('\\'); break;
             case '"': t.s.push_back('"'); break;
             case '\'': t.s.push_back('\''); break;
+            case '\n':  // line continuation: the newline and the next line's leading spaces go
+              while (k < s.size() && (s[k] == ' ' || s[k] == '\t')) ++k;
+              break;
+            case 'x':
+            case 'u':
+            case 'U': {
+              const int n = e == 'x' ? 2 : e == 'u' ? 4 : 8;
+              uint32_t cp = 0;
+              for (int j = 0; j < n; ++j) {
+                if (k >= s.size() || !isxdigit((unsigned char)s[k])) {
+                  err = std::string("Syntax error: invalid escape sequence \\") + e;
+                  return false;
+                }
+                const char h = s[k++];
+                cp = cp * 16u + (uint32_t)(isdigit((unsigned char)h) ? h - '0' : tolower(h) - 'a' + 10);
+              }
+              if (cp > 0x10FFFF || (cp >= 0xD800 && cp <= 0xDFFF)) {
+                err = std::string("Syntax error: invalid escape sequence \\") + e;
+                return false;
+              }
+              put_utf8(cp, &t.s);
+              break;
+            }
             default: err = std::string("Syntax error: invalid escape sequence \\") + e; return false;
           }
         }
@@ -115,9 +258,26 @@ struct Lexer {
           err = "Syntax error: unterminated string literal";
           return false;
         }
+      } else if (c == '\'') {
+        return unsupported("character literals");
+      } else if (c == '`') {
+        return unsupported("back-tick strings and string interpolation");
       } else {
-        static const char* ops[] = {"||", "&&", "==", "!=", "<=", ">=", "<", ">", "+", "-", "*", "/", "%",
-                                    "!",  "|",  "&",  "^",  "(",  ")",  "{", "}", ";", "="};
+        if (c == '!' && s.compare(k, 3, "!in") == 0 && !is_id(k + 3)) {
+          t.t = Tk::Punct;
+          t.s = "!in";
+          k += 3;
+          toks.push_back(t);
+          continue;
+        }
+        static const char* bad[][2] = {{"#{", "object maps"}, {"**", "the ** operator"}, {"<<", "bit shifts"},
+                                       {">>", "bit shifts"},  {"::", "modules and namespaces"},
+                                       {"?.", "the ?. operator"}, {"?[", "the ?[ operator"}};
+        for (auto& b : bad)
+          if (s.compare(k, std::char_traits<char>::length(b[0]), b[0]) == 0) return unsupported(b[1]);
+        static const char* ops[] = {"..=", "=>", "??", "..", "||", "&&", "==", "!=", "<=", ">=", "+=", "-=", "*=", "/=",
+                                    "%=",  "|=", "&=", "^=", "<",  ">",  "+",  "-",  "*",  "/",  "%",  "!",  "|",  "&",
+                                    "^",   "(",  ")",  "{",  "}",  "[",  "]",  ";",  "=",  ",",  "."};
         bool ok = false;
         for (const char* o : ops) {
           const size_t n = std::char_traits<char>::length(o);
@@ -129,8 +289,10 @@ struct Lexer {
             break;
           }
         }
-        if (!ok) {
-          err = std::string("Syntax error: unexpected character '") + c + "'";
+        if (!ok) {  // (the whole UTF-8 sequence of a non-ASCII character)
+          const unsigned char u = (unsigned char)c;
+          const size_t n = u < 0xC0 ? 1 : u < 0xE0 ? 2 : u < 0xF0 ? 3 : 4;
+          err = "Syntax error: unexpected character '" + s.substr(k, n) + "'";
           return false;
         }
       }
@@ -141,25 +303,46 @@ struct Lexer {
   }
 };
 
-bool is_kw(const std::string& s) { return s == "let" || s == "if" || s == "else" || s == "true" || s == "false"; }
+bool is_kw(const std::string& s) {
+  static const std::set<std::string> kw = {"let",   "const", "if",     "else",  "true", "false", "switch", "while",
+                                           "loop",  "do",    "until",  "for",   "in",   "break", "continue",
+                                           "return", "fn"};
+  return kw.count(s) > 0;
+}
+// rhai keywords and functions this engine does not implement: refused by name
+const char* unsupported_word(const std::string& s) {
+  static const std::map<std::string, const char*> m = {
+      {"import", "modules (import)"}, {"export", "modules (export)"}, {"as", "modules (as)"},
+      {"private", "private functions"}, {"try", "try / catch"}, {"catch", "try / catch"}, {"throw", "throw"},
+      {"this", "this"}, {"global", "the global namespace"}, {"Fn", "function pointers"}, {"call", "function pointers"},
+      {"curry", "function pointers"}, {"eval", "eval"}, {"print", "print"}, {"debug", "debug"},
+      {"is_def_var", "is_def_var"}, {"is_def_fn", "is_def_fn"}, {"is_shared", "shared values"},
+      {"static", "static"}, {"exit", "exit"}};
+  auto it = m.find(s);
+  return it == m.end() ? nullptr : it->second;
+}
 
 // ------------------------------------------------------------------------------------------
-// Parser (script mode: statements, blocks, if-else expressions)
+// Parser
 // ------------------------------------------------------------------------------------------
 struct Parser {
   const std::vector<Token>& toks;
-  const std::vector<std::string>& members;
   size_t i = 0;
   std::string err;
-  Parser(const std::vector<Token>& t, const std::vector<std::string>& m) : toks(t), members(m) {}
+  ExprAst* ast = nullptr;
+  int loops = 0;      // enclosing loops (break / continue)
+  bool in_fn = false;
+  std::vector<std::vector<std::pair<std::string, bool>>> scopes;  // (name, const) per block
+  explicit Parser(const std::vector<Token>& t) : toks(t) {}
 
-  const Token& peek() const { return toks[i]; }
-  bool punct(const char* o) const { return peek().t == Tk::Punct && peek().s == o; }
+  const Token& peek(size_t d = 0) const { return toks[std::min(i + d, toks.size() - 1)]; }
+  bool punct(const char* o, size_t d = 0) const { return peek(d).t == Tk::Punct && peek(d).s == o; }
   bool ident(const char* o) const { return peek().t == Tk::Ident && peek().s == o; }
   P fail(const std::string& m) {
     if (err.empty()) err = m;
     return nullptr;
   }
+  P unsupported(const std::string& what) { return fail(kUnsupported + what); }
   std::string near() const {
     const Token& t = peek();
     if (t.t == Tk::End) return "end of script";
@@ -167,59 +350,194 @@ struct Parser {
     if (t.t == Tk::Str) return "\"" + t.s + "\"";
     return "'" + t.s + "'";
   }
+  bool expect(const char* o, const char* what) {
+    if (punct(o)) {
+      ++i;
+      return true;
+    }
+    fail(std::string("Syntax error: expecting '") + o + "' " + what + ", found " + near());
+    return false;
+  }
+  void declare(const std::string& n, bool is_const) { scopes.back().push_back({n, is_const}); }
+  bool is_const_var(const std::string& n) const {
+    for (size_t s = scopes.size(); s-- > 0;)
+      for (size_t k = scopes[s].size(); k-- > 0;)
+        if (scopes[s][k].first == n) return scopes[s][k].second;
+    return false;
+  }
+  static bool block_like(const Node* n) {
+    return n->k == Node::If || n->k == Node::Switch || n->k == Node::While || n->k == Node::Loop || n->k == Node::For ||
+           n->k == Node::Block;
+  }
 
-  // statements until `close` ("}" or end of script)
+  // statements until "}" (or the end of the script at the top level)
   P block_body(bool top) {
     auto b = std::make_unique<Node>();
     b->k = Node::Block;
+    scopes.emplace_back();
     for (;;) {
       if (top ? peek().t == Tk::End : punct("}")) break;
       if (peek().t == Tk::End) return fail("Syntax error: expecting '}' to close the block");
-      P st;
-      bool block_like = false;
-      if (ident("let")) {
+      if (punct(";")) {  // an empty statement
         ++i;
-        if (peek().t != Tk::Ident || is_kw(peek().s)) return fail("Syntax error: expecting a variable name after 'let'");
-        auto l = std::make_unique<Node>();
-        l->k = Node::Let;
-        l->name = peek().s;
+        continue;
+      }
+      if (ident("fn")) {
+        if (!top || in_fn) return fail("Syntax error: functions can only be defined at global level");
+        if (!fn_def()) return nullptr;
+        continue;
+      }
+      P st = statement();
+      if (!st) return nullptr;
+      const bool is_decl = st->k == Node::Let || st->k == Node::Assign || st->k == Node::IndexAssign;
+      const bool blk = block_like(st.get());
+      b->kids.push_back(std::move(st));
+      if (punct(";")) {
         ++i;
-        if (!punct("=")) return fail("Syntax error: expecting '=' after the variable name");
+        b->flag = false;
+        continue;
+      }
+      if (top ? peek().t == Tk::End : punct("}")) {
+        b->flag = !is_decl;
+        break;
+      }
+      if (!blk) return fail("Syntax error: expecting ';' to terminate this statement, found " + near());
+      b->flag = false;
+    }
+    scopes.pop_back();
+    return b;
+  }
+
+  bool fn_def() {
+    ++i;  // fn
+    if (peek().t != Tk::Ident || is_kw(peek().s)) {
+      fail("Syntax error: expecting a function name after 'fn'");
+      return false;
+    }
+    FnDef f;
+    f.name = peek().s;
+    ++i;
+    if (!expect("(", "after the function name")) return false;
+    while (!punct(")")) {
+      if (peek().t != Tk::Ident || is_kw(peek().s)) {
+        fail("Syntax error: expecting a parameter name, found " + near());
+        return false;
+      }
+      if (std::find(f.params.begin(), f.params.end(), peek().s) != f.params.end()) {
+        fail("Syntax error: duplicated parameter '" + peek().s + "' in function '" + f.name + "'");
+        return false;
+      }
+      f.params.push_back(peek().s);
+      ++i;
+      if (punct(",")) ++i;
+      else if (!punct(")")) {
+        fail("Syntax error: expecting ',' or ')' in the parameter list, found " + near());
+        return false;
+      }
+    }
+    ++i;
+    for (const FnDef& g : ast->fns)
+      if (g.name == f.name && g.params.size() == f.params.size()) {
+        fail("Syntax error: function '" + f.name + "' with " + std::to_string(f.params.size()) +
+             " parameters is defined more than once");
+        return false;
+      }
+    if (!expect("{", "to start the function body")) return false;
+    const int saved_loops = loops;
+    auto saved_scopes = std::move(scopes);
+    scopes.clear();
+    scopes.emplace_back();
+    for (const std::string& p : f.params) declare(p, false);
+    loops = 0;
+    in_fn = true;
+    f.body = block_body(false);
+    in_fn = false;
+    loops = saved_loops;
+    scopes = std::move(saved_scopes);
+    if (!f.body) return false;
+    ++i;  // '}'
+    ast->fns.push_back(std::move(f));
+    return true;
+  }
+
+  P statement() {
+    if (ident("let") || ident("const")) {
+      const bool c = ident("const");
+      ++i;
+      if (peek().t != Tk::Ident || is_kw(peek().s)) return fail("Syntax error: expecting a variable name after 'let'");
+      auto l = std::make_unique<Node>();
+      l->k = Node::Let;
+      l->flag = c;
+      l->name = peek().s;
+      ++i;
+      if (punct("=")) {
         ++i;
         P init = expr();
         if (!init) return nullptr;
         l->kids.push_back(std::move(init));
-        st = std::move(l);
-      } else {
-        block_like = ident("if") || punct("{");
-        st = expr();
-        if (!st) return nullptr;
+      } else if (c) {
+        return fail("Syntax error: expecting '=' after the constant name");
       }
-      const bool is_let = st->k == Node::Let;
-      b->kids.push_back(std::move(st));
-      if (punct(";")) {
-        ++i;
-        b->tail = false;
-        continue;
-      }
-      if (top ? peek().t == Tk::End : punct("}")) {
-        b->tail = !is_let;
-        break;
-      }
-      if (!block_like) return fail("Syntax error: expecting ';' to terminate this statement, found " + near());
-      b->tail = false;
+      declare(l->name, c);
+      return l;
     }
-    return b;
+    if (ident("break") || ident("continue") || ident("return")) {
+      auto n = std::make_unique<Node>();
+      n->k = ident("break") ? Node::Break : ident("continue") ? Node::Continue : Node::Return;
+      ++i;
+      if (n->k != Node::Return && loops == 0)
+        return fail(std::string("Syntax error: ") + (n->k == Node::Break ? "break" : "continue") +
+                    " should only be used inside a loop");
+      if (n->k != Node::Continue && !punct(";") && !punct("}") && peek().t != Tk::End && !punct(",")) {
+        P v = expr();
+        if (!v) return nullptr;
+        n->kids.push_back(std::move(v));
+      }
+      return n;
+    }
+    P e = expr();
+    if (!e) return nullptr;
+    static const char* aops[] = {"=", "+=", "-=", "*=", "/=", "%=", "|=", "&=", "^="};
+    for (const char* ao : aops) {
+      if (!punct(ao)) continue;
+      ++i;
+      P rhs = expr();
+      if (!rhs) return nullptr;
+      auto a = std::make_unique<Node>();
+      a->op = std::string(ao) == "=" ? "" : std::string(ao).substr(0, 1);
+      if (e->k == Node::Var) {
+        a->k = Node::Assign;
+        a->name = e->name;
+        a->kids.push_back(std::move(rhs));
+      } else if (e->k == Node::Index && e->kids[0]->k == Node::Var) {
+        a->k = Node::IndexAssign;
+        a->name = e->kids[0]->name;
+        a->kids.push_back(std::move(e->kids[1]));
+        a->kids.push_back(std::move(rhs));
+      } else if (e->k == Node::Index) {
+        return unsupported("assigning to a nested index or to an element of a temporary value");
+      } else {
+        return fail("Syntax error: cannot assign to this expression");
+      }
+      if (is_const_var(a->name)) return fail("Syntax error: cannot assign to the constant '" + a->name + "'");
+      return a;
+    }
+    return e;
   }
 
-  // precedence climbing: || | ^ (30), && & (60), == != (90), < <= > >= (110), + - (150), * / % (180)
+  // precedence climbing (rhai 1.x): || | ^ (30), && & (60), == != (90), in !in (110),
+  // < <= > >= (130), ?? (135), .. ..= (140), + - (150), * / % (180)
   static int prec(const Token& t) {
+    if (t.t == Tk::Ident) return t.s == "in" ? 110 : -1;
     if (t.t != Tk::Punct) return -1;
     const std::string& o = t.s;
     if (o == "||" || o == "|" || o == "^") return 30;
     if (o == "&&" || o == "&") return 60;
     if (o == "==" || o == "!=") return 90;
-    if (o == "<" || o == "<=" || o == ">" || o == ">=") return 110;
+    if (o == "!in") return 110;
+    if (o == "<" || o == "<=" || o == ">" || o == ">=") return 130;
+    if (o == "??") return 135;
+    if (o == ".." || o == "..=") return 140;
     if (o == "+" || o == "-") return 150;
     if (o == "*" || o == "/" || o == "%") return 180;
     return -1;
@@ -229,12 +547,24 @@ struct Parser {
     while (l) {
       const int p = prec(peek());
       if (p < 0 || p < min_prec) break;
-      auto n = std::make_unique<Node>();
-      n->k = Node::Bin;
-      n->op = peek().s;
+      const std::string o = peek().s;
       ++i;
       P r = expr(p + 1);
       if (!r) return nullptr;
+      auto n = std::make_unique<Node>();
+      if (o == "in" || o == "!in") {
+        n->k = Node::In;
+        n->flag = o == "!in";
+      } else if (o == "??") {
+        n->k = Node::Coalesce;
+      } else if (o == ".." || o == "..=") {
+        n->k = Node::Range;
+        n->flag = o == "..=";
+        n->name2 = o;
+      } else {
+        n->k = Node::Bin;
+        n->op = o;
+      }
       n->kids.push_back(std::move(l));
       n->kids.push_back(std::move(r));
       l = std::move(n);
@@ -252,30 +582,212 @@ struct Parser {
       n->kids.push_back(std::move(a));
       return n;
     }
-    return primary();
+    return postfix();
+  }
+  bool args(std::vector<P>* out) {  // after '('
+    while (!punct(")")) {
+      P a = expr();
+      if (!a) return false;
+      out->push_back(std::move(a));
+      if (punct(",")) ++i;
+      else if (!punct(")")) {
+        fail("Syntax error: expecting ',' or ')' in the argument list, found " + near());
+        return false;
+      }
+    }
+    ++i;
+    return true;
+  }
+  P postfix() {
+    P e = primary();
+    while (e) {
+      if (punct(".")) {
+        ++i;
+        if (peek().t != Tk::Ident) return fail("Syntax error: expecting a method name after '.', found " + near());
+        const std::string m = peek().s;
+        ++i;
+        if (!punct("(")) return unsupported("property access (." + m + ")");
+        ++i;
+        auto c = std::make_unique<Node>();
+        c->k = Node::Call;
+        c->name = m;
+        c->flag = true;
+        c->kids.push_back(std::move(e));
+        if (!args(&c->kids)) return nullptr;
+        if (m == "push" && c->kids[0]->k == Node::Index)
+          return unsupported("mutating an element in place (x[i].push(..))");
+        if (m == "push" && c->kids[0]->k == Node::Var && is_const_var(c->kids[0]->name))
+          return fail("Syntax error: cannot assign to the constant '" + c->kids[0]->name + "'");
+        e = std::move(c);
+      } else if (punct("[")) {
+        ++i;
+        P ix = expr();
+        if (!ix) return nullptr;
+        if (!expect("]", "to close the index")) return nullptr;
+        auto n = std::make_unique<Node>();
+        n->k = Node::Index;
+        n->kids.push_back(std::move(e));
+        n->kids.push_back(std::move(ix));
+        e = std::move(n);
+      } else {
+        break;
+      }
+    }
+    return e;
+  }
+  P loop_body() {
+    if (!punct("{")) return fail("Syntax error: expecting '{' to start the loop body, found " + near());
+    ++i;
+    ++loops;
+    P b = block_body(false);
+    --loops;
+    if (!b) return nullptr;
+    ++i;
+    return b;
+  }
+  P inner_block(const char* what) {
+    if (!punct("{")) return fail(std::string("Syntax error: expecting '{' ") + what + ", found " + near());
+    ++i;
+    P b = block_body(false);
+    if (!b) return nullptr;
+    ++i;
+    return b;
+  }
+  bool case_literal(Val* v) {
+    bool neg = false;
+    if (punct("-")) {
+      neg = true;
+      ++i;
+    }
+    const Token t = peek();
+    if (t.t == Tk::Int) {
+      ++i;
+      *v = vint(neg ? -t.v : t.v);
+      return true;
+    }
+    if (neg) return false;
+    if (t.t == Tk::Str) {
+      ++i;
+      *v = vstr(t.s);
+      return true;
+    }
+    if (t.t == Tk::Ident && (t.s == "true" || t.s == "false")) {
+      ++i;
+      *v = vbool(t.s == "true");
+      return true;
+    }
+    if (punct("(") && punct(")", 1)) {
+      i += 2;
+      *v = Val{};
+      return true;
+    }
+    return false;
+  }
+  P switch_expr() {
+    auto n = std::make_unique<Node>();
+    n->k = Node::Switch;
+    P scr = expr();
+    if (!scr) return nullptr;
+    n->kids.push_back(std::move(scr));
+    if (!expect("{", "after the switch value")) return nullptr;
+    bool seen_default = false;
+    std::vector<std::pair<Val, bool>> unguarded;
+    while (!punct("}")) {
+      if (seen_default) return fail("Syntax error: the wildcard case '_' must be the last case");
+      SwitchCase c;
+      if (ident("_")) {
+        ++i;
+        c.wildcard = true;
+        seen_default = true;
+      } else {
+        for (;;) {
+          Val v;
+          if (!case_literal(&v)) return fail("Syntax error: a switch case must be a constant value, found " + near());
+          if (punct("..") || punct("..=")) {
+            c.incl = punct("..=");
+            ++i;
+            Val h;
+            if (v.t != VT::Int || !case_literal(&h) || h.t != VT::Int)
+              return fail("Syntax error: a switch range case needs integer bounds");
+            c.range = true;
+            c.lo = v.i;
+            c.hi = h.i;
+            break;
+          }
+          c.vals.push_back(v);
+          if (!punct("|")) break;
+          ++i;
+        }
+      }
+      if (ident("if")) {
+        if (c.wildcard) return fail("Syntax error: the wildcard case '_' cannot have a condition");
+        ++i;
+        c.guard = expr();
+        if (!c.guard) return nullptr;
+      }
+      if (!expect("=>", "after the switch case")) return nullptr;
+      if (!c.range && !c.wildcard && !c.guard) {
+        for (const Val& v : c.vals) {
+          for (auto& u : unguarded)
+            if (u.first.t == v.t && u.first.b == v.b && u.first.i == v.i && u.first.s == v.s)
+              return fail("Syntax error: duplicated switch case");
+          unguarded.push_back({v, true});
+        }
+      }
+      bool blk = false;
+      if (punct("{")) {
+        c.body = inner_block("");
+        blk = true;
+      } else {
+        c.body = statement();
+        if (c.body && (c.body->k == Node::Let || c.body->k == Node::Assign || c.body->k == Node::IndexAssign))
+          return fail("Syntax error: a switch case body must be an expression or a block");
+      }
+      if (!c.body) return nullptr;
+      n->cases.push_back(std::move(c));
+      if (punct(",")) ++i;
+      else if (!punct("}") && !blk) return fail("Syntax error: expecting ',' between switch cases, found " + near());
+    }
+    ++i;
+    return n;
   }
   P primary() {
     const Token t = peek();
     auto n = std::make_unique<Node>();
     if (t.t == Tk::Int) {
       ++i;
-      n->lit.t = VT::Int;
-      n->lit.i = t.v;
+      n->lit = vint(t.v);
       return n;
     }
     if (t.t == Tk::Str) {
       ++i;
-      n->lit.t = VT::Str;
-      n->lit.s = t.s;
+      n->lit = vstr(t.s);
       return n;
     }
     if (punct("(")) {
       ++i;
+      if (punct(")")) {  // ()
+        ++i;
+        return n;
+      }
       P e = expr();
       if (!e) return nullptr;
       if (!punct(")")) return fail("Syntax error: expecting ')', found " + near());
       ++i;
       return e;
+    }
+    if (punct("[")) {
+      ++i;
+      n->k = Node::Array;
+      while (!punct("]")) {
+        P e = expr();
+        if (!e) return nullptr;
+        n->kids.push_back(std::move(e));
+        if (punct(",")) ++i;
+        else if (!punct("]")) return fail("Syntax error: expecting ',' or ']' in the array literal, found " + near());
+      }
+      ++i;
+      return n;
     }
     if (punct("{")) {
       ++i;
@@ -284,11 +796,12 @@ struct Parser {
       ++i;  // '}'
       return b;
     }
+    if (punct("|") || punct("||")) return unsupported("closures");
     if (t.t == Tk::Ident) {
+      if (const char* u = unsupported_word(t.s)) return unsupported(u);
       ++i;
       if (t.s == "true" || t.s == "false") {
-        n->lit.t = VT::Bool;
-        n->lit.b = t.s == "true";
+        n->lit = vbool(t.s == "true");
         return n;
       }
       if (t.s == "if") {
@@ -296,11 +809,8 @@ struct Parser {
         P c = expr();
         if (!c) return nullptr;
         n->kids.push_back(std::move(c));
-        if (!punct("{")) return fail("Syntax error: expecting '{' after the if condition, found " + near());
-        ++i;
-        P th = block_body(false);
+        P th = inner_block("after the if condition");
         if (!th) return nullptr;
-        ++i;
         n->kids.push_back(std::move(th));
         if (ident("else")) {
           ++i;
@@ -309,31 +819,90 @@ struct Parser {
             if (!e) return nullptr;
             n->kids.push_back(std::move(e));
           } else {
-            if (!punct("{")) return fail("Syntax error: expecting '{' or 'if' after 'else', found " + near());
-            ++i;
-            P e = block_body(false);
+            P e = inner_block("or 'if' after 'else'");
             if (!e) return nullptr;
-            ++i;
             n->kids.push_back(std::move(e));
           }
         }
         return n;
       }
-      if (t.s == "let" || t.s == "else") return fail("Syntax error: unexpected '" + t.s + "'");
+      if (t.s == "switch") return switch_expr();
+      if (t.s == "while") {
+        n->k = Node::While;
+        P c = expr();
+        if (!c) return nullptr;
+        P b = loop_body();
+        if (!b) return nullptr;
+        n->kids.push_back(std::move(c));
+        n->kids.push_back(std::move(b));
+        return n;
+      }
+      if (t.s == "loop") {
+        n->k = Node::Loop;
+        P b = loop_body();
+        if (!b) return nullptr;
+        n->kids.push_back(std::move(b));
+        return n;
+      }
+      if (t.s == "do") {
+        n->k = Node::DoWhile;
+        P b = loop_body();
+        if (!b) return nullptr;
+        if (!ident("while") && !ident("until")) return fail("Syntax error: expecting 'while' or 'until' after the do block");
+        n->flag = ident("until");
+        ++i;
+        P c = expr();
+        if (!c) return nullptr;
+        n->kids.push_back(std::move(b));
+        n->kids.push_back(std::move(c));
+        return n;
+      }
+      if (t.s == "for") {
+        n->k = Node::For;
+        const bool paren = punct("(");
+        if (paren) ++i;
+        if (peek().t != Tk::Ident || is_kw(peek().s)) return fail("Syntax error: expecting a loop variable after 'for'");
+        n->name = peek().s;
+        ++i;
+        if (paren) {
+          if (!expect(",", "after the loop variable")) return nullptr;
+          if (peek().t != Tk::Ident || is_kw(peek().s)) return fail("Syntax error: expecting the counter variable");
+          n->name2 = peek().s;
+          ++i;
+          if (!expect(")", "after the counter variable")) return nullptr;
+        }
+        if (!ident("in")) return fail("Syntax error: expecting 'in' after the loop variable, found " + near());
+        ++i;
+        P it = expr();
+        if (!it) return nullptr;
+        if (it->k == Node::Call && !it->flag && it->name == "range") {  // range(a, b): a..b
+          if (it->kids.size() != 2) return unsupported("range() with a step");
+          it->k = Node::Range;
+          it->flag = false;
+          it->name2 = "range";
+        }
+        n->kids.push_back(std::move(it));
+        scopes.emplace_back();
+        declare(n->name, false);
+        if (!n->name2.empty()) declare(n->name2, false);
+        P b = loop_body();
+        scopes.pop_back();
+        if (!b) return nullptr;
+        n->kids.push_back(std::move(b));
+        return n;
+      }
+      if (t.s == "let" || t.s == "const" || t.s == "else" || t.s == "fn" || t.s == "in" || t.s == "until" ||
+          t.s == "break" || t.s == "continue" || t.s == "return")
+        return fail("Syntax error: unexpected '" + t.s + "'");
       if (!punct("(")) {
         n->k = Node::Var;
         n->name = t.s;
         return n;
       }
       ++i;
-      if (!punct(")")) return fail("Syntax error: member policies take no arguments");
-      ++i;
-      int slot = -1;
-      for (size_t m = 0; m < members.size(); ++m)
-        if (members[m] == t.s) slot = (int)m;
       n->k = Node::Call;
-      n->slot = slot;  // -1: "Function not found" when called (rhai resolves at run time)
       n->name = t.s;
+      if (!args(&n->kids)) return nullptr;
       return n;
     }
     if (t.t == Tk::End) return fail("Syntax error: expecting an expression, found end of script");
@@ -341,173 +910,640 @@ struct Parser {
   }
 };
 
+// ranges are values only as the right side of `in` / `!in` and as a `for` iterable
+bool check_ranges(const Node* n, bool allowed, std::string* err) {
+  if (n->k == Node::Range && !allowed) {
+    *err = std::string(kUnsupported) + "range values outside `for` and `in`";
+    return false;
+  }
+  for (size_t k = 0; k < n->kids.size(); ++k) {
+    const bool ok = (n->k == Node::In && k == 1) || (n->k == Node::For && k == 0);
+    if (!check_ranges(n->kids[k].get(), ok, err)) return false;
+  }
+  for (const SwitchCase& c : n->cases) {
+    if (c.guard && !check_ranges(c.guard.get(), false, err)) return false;
+    if (!check_ranges(c.body.get(), false, err)) return false;
+  }
+  return true;
+}
+
+int builtin_id(const std::string& name, size_t nargs) {
+  static const std::map<std::string, std::pair<int, size_t>> b = {
+      {"len", {F_LEN, 1}},          {"is_empty", {F_IS_EMPTY, 1}},       {"contains", {F_CONTAINS, 2}},
+      {"to_string", {F_TO_STRING, 1}}, {"type_of", {F_TYPE_OF, 1}},     {"starts_with", {F_STARTS_WITH, 2}},
+      {"ends_with", {F_ENDS_WITH, 2}}, {"push", {F_PUSH, 2}}};
+  auto it = b.find(name);
+  return it != b.end() && it->second.second == nargs ? it->second.first : -1;
+}
+
+// call resolution, as rhai's: a script function of that name and arity, else a member policy
+// (a native function of no arguments), else a built-in; anything else is "Function not found"
+// when called (after its arguments ran)
+void resolve(Node* n, const ExprAst& ast, const std::vector<std::string>& members) {
+  if (n->k == Node::Call) {
+    n->fn = -1;
+    n->slot = -1;
+    n->builtin = -1;
+    for (size_t f = 0; f < ast.fns.size(); ++f)
+      if (!n->flag && ast.fns[f].name == n->name && ast.fns[f].params.size() == n->kids.size()) n->fn = (int)f;
+    if (n->fn < 0 && !n->flag && n->kids.empty())
+      for (size_t m = 0; m < members.size(); ++m)
+        if (members[m] == n->name) n->slot = (int)m;
+    if (n->fn < 0 && n->slot < 0) n->builtin = builtin_id(n->name, n->kids.size());
+  }
+  for (P& k : n->kids) resolve(k.get(), ast, members);
+  for (SwitchCase& c : n->cases) {
+    if (c.guard) resolve(c.guard.get(), ast, members);
+    resolve(c.body.get(), ast, members);
+  }
+}
+
+// range(a, b) outside a `for` would be a range value: not supported (check_ranges)
+bool stray_range_call(const Node* n) {
+  if (n->k == Node::Call && n->name == "range" && n->fn < 0 && n->slot < 0 && n->builtin < 0) return true;
+  for (const P& k : n->kids)
+    if (stray_range_call(k.get())) return true;
+  for (const SwitchCase& c : n->cases)
+    if ((c.guard && stray_range_call(c.guard.get())) || stray_range_call(c.body.get())) return true;
+  return false;
+}
+
 // ------------------------------------------------------------------------------------------
 // Interpreter
 // ------------------------------------------------------------------------------------------
+enum Flow { OK, ERR, BRK, CNT, RET };
+
+std::string limit_ops() {
+  return "engine limit: more than " + std::to_string(kMaxScriptOps) + " loop iterations and script-function calls";
+}
+std::string limit_alloc() {
+  return "engine limit: more than " + std::to_string(kMaxScriptAlloc) + " bytes of strings and arrays built";
+}
+std::string limit_depth() {
+  return "engine limit: arrays nested more than " + std::to_string(kMaxCompareDepth) + " deep in a comparison";
+}
+
 struct Interp {
+  const ExprAst* ast = nullptr;
   std::function<bool(uint32_t)> ok;
   std::vector<std::pair<std::string, Val>> vars;
+  size_t base = 0;  // the current function frame's first variable
   std::vector<uint32_t> called;
   std::vector<uint8_t> seen;
   std::string err;
+  uint32_t ops = 0, alloc = 0, depth = 0;
+  uint64_t steps = 0;  // nodes evaluated (the cost of one run, for the truth-table decision)
+  Val fv;              // the value a `break` / `return` carries to its loop / call              // the value a `break` / `return` carries to its loop / call  // nodes evaluated (the cost of one run, for the truth-table decision)
   explicit Interp(std::function<bool(uint32_t)> f) : ok(std::move(f)) {}
 
-  bool fail(const std::string& m) {
+  Flow fail(const std::string& m) {
     err = m;
-    return false;
+    return ERR;
   }
-  bool nf(const std::string& op, const Val& a, const Val& b) {
-    return fail("Function not found: " + op + " (" + tname(a.t) + ", " + tname(b.t) + ")");
+  Flow nf(const std::string& fn, const std::vector<const Val*>& a) {
+    std::string s = "Function not found: " + fn + " (";
+    for (size_t k = 0; k < a.size(); ++k) s += (k ? ", " : "") + std::string(tname(a[k]->t));
+    return fail(s + ")");
+  }
+  bool charge(uint64_t n) {
+    if (n > (uint64_t)(kMaxScriptAlloc - alloc)) return false;
+    alloc += (uint32_t)n;
+    return true;
+  }
+  Val* lookup(const std::string& name) {
+    for (size_t k = vars.size(); k-- > base;)
+      if (vars[k].first == name) return &vars[k].second;
+    return nullptr;
+  }
+  // deep equality: 1 / 0, -1 past kMaxCompareDepth (slots.hpp veq walks in the same order)
+  int eq(const Val& a, const Val& b, uint32_t d) const {
+    if (a.t != b.t) return 0;
+    switch (a.t) {
+      case VT::Unit: return 1;
+      case VT::Bool: return a.b == b.b;
+      case VT::Int: return a.i == b.i;
+      case VT::Str: return a.s == b.s;
+      case VT::Arr: {
+        if (a.a.size() != b.a.size()) return 0;
+        if (a.a.empty()) return 1;
+        if (d == kMaxCompareDepth) return -1;
+        for (size_t k = 0; k < a.a.size(); ++k) {
+          const int e = eq(a.a[k], b.a[k], d + 1);
+          if (e != 1) return e;
+        }
+        return 1;
+      }
+    }
+    return 0;
+  }
+  // to_string of a non-array value
+  static bool text(const Val& v, std::string* out) {
+    switch (v.t) {
+      case VT::Unit: out->clear(); return true;
+      case VT::Bool: *out = v.b ? "true" : "false"; return true;
+      case VT::Int: *out = std::to_string(v.i); return true;
+      case VT::Str: *out = v.s; return true;
+      default: return false;
+    }
+  }
+  static size_t chars(const std::string& s) {
+    size_t n = 0;
+    for (unsigned char c : s) n += (c & 0xC0u) != 0x80u;
+    return n;
+  }
+  static bool index_of(int64_t i, size_t n, size_t* at) {
+    if (i < 0) i += (int64_t)n;
+    if (i < 0 || i >= (int64_t)n) return false;
+    *at = (size_t)i;
+    return true;
+  }
+  Flow bounds(int64_t i, size_t n) {
+    const std::string s = "Array index " + std::to_string(i) + " out of bounds: ";
+    if (n == 0) return fail(s + "array is empty");
+    if (n == 1) return fail(s + "only 1 element in array");
+    return fail(s + "only " + std::to_string(n) + " elements in array");
+  }
+  Flow not_indexable(const Val& v) {
+    if (v.t == VT::Str) return fail(std::string(kUnsupported) + "indexing a string (characters)");
+    return fail(std::string("Indexer unavailable: ") + tname(v.t));
   }
 
-  bool eval(const Node* n, Val* out) {
-    switch (n->k) {
-      case Node::Lit: *out = n->lit; return true;
-      case Node::Var:
-        for (size_t k = vars.size(); k-- > 0;)
-          if (vars[k].first == n->name) {
-            *out = vars[k].second;
-            return true;
-          }
-        return fail("Variable not found: " + n->name);
-      case Node::Call: {
-        if (n->slot < 0) return fail("Function not found: " + n->name + " ()");
-        const uint32_t s = (uint32_t)n->slot;
-        if (s >= seen.size()) seen.resize(s + 1, 0);
-        if (!seen[s]) {
-          seen[s] = 1;
-          called.push_back(s);
-        }
-        out->t = VT::Bool;
-        out->b = ok(s);
-        return true;
+  Flow builtin(int fid, const std::string& name, std::vector<Val>& a, Val* out) {
+    std::vector<const Val*> ap;
+    for (const Val& v : a) ap.push_back(&v);
+    switch (fid) {
+      case F_LEN:
+      case F_IS_EMPTY: {
+        size_t n;
+        if (a[0].t == VT::Arr) n = a[0].a.size();
+        else if (a[0].t == VT::Str) n = chars(a[0].s);
+        else return nf(name, ap);
+        *out = fid == F_LEN ? vint((int64_t)n) : vbool(n == 0);
+        return OK;
       }
+      case F_TYPE_OF: *out = vstr(tname(a[0].t)); return OK;
+      case F_TO_STRING: {
+        if (a[0].t == VT::Str) {
+          *out = a[0];
+          return OK;
+        }
+        std::string s;
+        if (!text(a[0], &s)) return fail(std::string(kUnsupported) + "converting an array to a string");
+        if (!charge(s.size())) return fail(limit_alloc());
+        *out = vstr(s);
+        return OK;
+      }
+      case F_PUSH: {
+        if (a[0].t != VT::Arr) return nf(name, ap);
+        if (!charge(16ull * (a[0].a.size() + 1))) return fail(limit_alloc());
+        *out = a[0];
+        out->a.push_back(a[1]);
+        return OK;
+      }
+      case F_CONTAINS: {
+        const Val &c = a[0], &x = a[1];
+        if (c.t == VT::Arr) {
+          for (const Val& e : c.a) {
+            const int r = eq(e, x, 0);
+            if (r < 0) return fail(limit_depth());
+            if (r) {
+              *out = vbool(true);
+              return OK;
+            }
+          }
+          *out = vbool(false);
+          return OK;
+        }
+        if (c.t == VT::Str && x.t == VT::Str) {
+          *out = vbool(c.s.find(x.s) != std::string::npos);
+          return OK;
+        }
+        return nf(name, ap);
+      }
+      case F_STARTS_WITH:
+      case F_ENDS_WITH: {
+        if (a[0].t != VT::Str || a[1].t != VT::Str) return nf(name, ap);
+        const std::string &h = a[0].s, &n = a[1].s;
+        const bool r = n.size() <= h.size() && (fid == F_STARTS_WITH ? h.compare(0, n.size(), n) == 0
+                                                                      : h.compare(h.size() - n.size(), n.size(), n) == 0);
+        *out = vbool(r);
+        return OK;
+      }
+    }
+    return fail("internal: bad built-in");
+  }
+
+  Flow call(const Node* n, Val* out) {
+    std::vector<Val> a(n->kids.size());
+    for (size_t k = 0; k < n->kids.size(); ++k)
+      if (Flow f = eval(n->kids[k].get(), &a[k])) return f;
+    if (n->fn >= 0) {
+      const FnDef& F = ast->fns[(size_t)n->fn];
+      if (depth >= kMaxCallDepth) return fail("Stack overflow");
+      if (++ops > kMaxScriptOps) return fail(limit_ops());
+      const size_t saved = base;
+      base = vars.size();
+      for (size_t k = 0; k < a.size(); ++k) vars.push_back({F.params[k], std::move(a[k])});
+      ++depth;
+      Flow f = eval(F.body.get(), out);
+      --depth;
+      vars.resize(base);
+      base = saved;
+      if (f == RET) {
+        *out = std::move(fv);
+        f = OK;
+      }
+      return f;
+    }
+    if (n->slot >= 0) {
+      const uint32_t s = (uint32_t)n->slot;
+      if (s >= seen.size()) seen.resize(s + 1, 0);
+      if (!seen[s]) {
+        seen[s] = 1;
+        called.push_back(s);
+      }
+      *out = vbool(ok(s));
+      return OK;
+    }
+    if (n->builtin >= 0) {
+      if (Flow f = builtin(n->builtin, n->name, a, out)) return f;
+      if (n->builtin == F_PUSH && n->flag) {  // method style on a variable: push into it
+        if (n->kids[0]->k == Node::Var) {
+          Val* v = lookup(n->kids[0]->name);
+          if (!v) return fail("Variable not found: " + n->kids[0]->name);
+          *v = std::move(*out);
+        }
+        *out = Val{};
+      }
+      return OK;
+    }
+    std::vector<const Val*> ap;
+    for (const Val& v : a) ap.push_back(&v);
+    return nf(n->name, ap);
+  }
+
+  // a op b for the binary operators and compound assignments (`+=` pushes onto arrays)
+  Flow binop(const std::string& op, bool assign, Val& a, Val& b, Val* out) {
+    const std::string shown = op;
+    if (op == "==" || op == "!=") {
+      const int e = eq(a, b, 0);
+      if (e < 0) return fail(limit_depth());
+      *out = vbool((op == "==") == (e == 1));
+      return OK;
+    }
+    if (op == "<" || op == "<=" || op == ">" || op == ">=") {
+      if (a.t != b.t) {
+        *out = vbool(false);
+        return OK;
+      }
+      int c;
+      if (a.t == VT::Int) c = a.i < b.i ? -1 : a.i > b.i ? 1 : 0;
+      else if (a.t == VT::Str) c = a.s.compare(b.s) < 0 ? -1 : a.s == b.s ? 0 : 1;
+      else return nf(shown, {&a, &b});
+      *out = vbool(op == "<" ? c < 0 : op == "<=" ? c <= 0 : op == ">" ? c > 0 : c >= 0);
+      return OK;
+    }
+    if (op == "|" || op == "&" || op == "^") {
+      if (a.t == VT::Bool && b.t == VT::Bool) {
+        *out = vbool(op == "|" ? (a.b || b.b) : op == "&" ? (a.b && b.b) : (a.b != b.b));
+        return OK;
+      }
+      if (a.t == VT::Int && b.t == VT::Int) {
+        *out = vint(op == "|" ? (a.i | b.i) : op == "&" ? (a.i & b.i) : (a.i ^ b.i));
+        return OK;
+      }
+      return nf(shown, {&a, &b});
+    }
+    if (op == "+" && a.t == VT::Arr && (b.t == VT::Arr || assign)) {
+      const size_t nb = b.t == VT::Arr ? b.a.size() : 1;
+      if (!charge(16ull * (a.a.size() + nb))) return fail(limit_alloc());
+      *out = a;
+      if (b.t == VT::Arr) out->a.insert(out->a.end(), b.a.begin(), b.a.end());
+      else out->a.push_back(b);
+      return OK;
+    }
+    if (op == "+" && (a.t == VT::Str || b.t == VT::Str) && a.t != VT::Arr && b.t != VT::Arr) {
+      std::string sa, sb;
+      text(a, &sa);
+      text(b, &sb);
+      if (!charge(sa.size() + sb.size())) return fail(limit_alloc());
+      *out = vstr(sa + sb);
+      return OK;
+    }
+    if (op == "+" && (a.t == VT::Str || b.t == VT::Str))
+      return fail(std::string(kUnsupported) + "converting an array to a string");
+    if (a.t != VT::Int || b.t != VT::Int) return nf(shown, {&a, &b});
+    const std::string ex = std::to_string(a.i) + " " + op + " " + std::to_string(b.i);
+    long long r = 0;
+    if (op == "+") {
+      if (__builtin_add_overflow(a.i, b.i, &r)) return fail("Addition overflow: " + ex);
+    } else if (op == "-") {
+      if (__builtin_sub_overflow(a.i, b.i, &r)) return fail("Subtraction overflow: " + ex);
+    } else if (op == "*") {
+      if (__builtin_mul_overflow(a.i, b.i, &r)) return fail("Multiplication overflow: " + ex);
+    } else {  // / %
+      if (b.i == 0) return fail("Division by zero: " + ex);
+      if (a.i == INT64_MIN && b.i == -1) return fail((op == "/" ? "Division overflow: " : "Modulo overflow: ") + ex);
+      r = op == "/" ? a.i / b.i : a.i % b.i;
+    }
+    *out = vint(r);
+    return OK;
+  }
+
+  Flow cond(const Node* n, const char* what, bool* c) {
+    Val v;
+    if (Flow f = eval(n, &v)) return f;
+    if (v.t != VT::Bool) return fail(std::string("Boolean value expected for the ") + what + " condition, found " + tname(v.t));
+    *c = v.b;
+    return OK;
+  }
+  bool tick() { return ++ops <= kMaxScriptOps; }
+
+  // a loop body's outcome: OK go on, BRK leave with *out, anything else propagates
+  Flow body(const Node* b, Val* out, bool* leave) {
+    Val v;
+    *leave = false;
+    Flow f = eval(b, &v);
+    if (f == CNT) return OK;
+    if (f == BRK) {
+      *leave = true;
+      *out = std::move(fv);
+      return OK;
+    }
+    return f;
+  }
+
+  Flow range_bounds(const Node* r, int64_t* lo, int64_t* hi) {
+    Val a, b;
+    if (Flow f = eval(r->kids[0].get(), &a)) return f;
+    if (Flow f = eval(r->kids[1].get(), &b)) return f;
+    if (a.t != VT::Int || b.t != VT::Int) return nf(r->name2, {&a, &b});
+    *lo = a.i;
+    *hi = b.i;
+    return OK;
+  }
+
+  Flow eval(const Node* n, Val* out) {
+    ++steps;
+    switch (n->k) {
+      case Node::Lit: *out = n->lit; return OK;
+      case Node::Var: {
+        Val* v = lookup(n->name);
+        if (!v) return fail("Variable not found: " + n->name);
+        *out = *v;
+        return OK;
+      }
+      case Node::Call: return call(n, out);
       case Node::Unary: {
         Val a;
-        if (!eval(n->kids[0].get(), &a)) return false;
+        if (Flow f = eval(n->kids[0].get(), &a)) return f;
         if (n->op == "!") {
-          if (a.t != VT::Bool) return fail(std::string("Function not found: ! (") + tname(a.t) + ")");
-          out->t = VT::Bool;
-          out->b = !a.b;
-          return true;
+          if (a.t != VT::Bool) return nf("!", {&a});
+          *out = vbool(!a.b);
+          return OK;
         }
-        if (a.t != VT::Int) return fail("Function not found: " + n->op + " (" + tname(a.t) + ")");
+        if (a.t != VT::Int) return nf(n->op, {&a});
         if (n->op == "-" && a.i == INT64_MIN) return fail("Negation overflow: -" + std::to_string(a.i));
-        *out = a;
-        if (n->op == "-") out->i = -a.i;
-        return true;
+        *out = vint(n->op == "-" ? -a.i : a.i);
+        return OK;
       }
-      case Node::Bin: return bin(n, out);
+      case Node::Bin: {
+        const std::string& op = n->op;
+        Val a, b;
+        if (Flow f = eval(n->kids[0].get(), &a)) return f;
+        if (op == "||" || op == "&&") {
+          if (a.t != VT::Bool) return fail("Function not found: " + op + " (" + tname(a.t) + ", ...)");
+          if ((op == "||") == a.b) {  // short circuit
+            *out = a;
+            return OK;
+          }
+          if (Flow f = eval(n->kids[1].get(), &b)) return f;
+          if (b.t != VT::Bool) return nf(op, {&a, &b});
+          *out = b;
+          return OK;
+        }
+        if (Flow f = eval(n->kids[1].get(), &b)) return f;
+        return binop(op, false, a, b, out);
+      }
+      case Node::Coalesce: {
+        if (Flow f = eval(n->kids[0].get(), out)) return f;
+        if (out->t != VT::Unit) return OK;
+        return eval(n->kids[1].get(), out);
+      }
+      case Node::In: {
+        Val x;
+        if (Flow f = eval(n->kids[0].get(), &x)) return f;
+        const Node* h = n->kids[1].get();
+        bool r;
+        if (h->k == Node::Range) {
+          int64_t lo, hi;
+          if (Flow f = range_bounds(h, &lo, &hi)) return f;
+          if (x.t != VT::Int) {
+            const std::string sig = std::string("Function not found: contains (") + (h->flag ? "range=" : "range") + ", " +
+                                    tname(x.t) + ")";
+            return fail(sig);
+          }
+          r = x.i >= lo && (h->flag ? x.i <= hi : x.i < hi);
+        } else {
+          std::vector<Val> a(2);
+          if (Flow f = eval(h, &a[0])) return f;
+          a[1] = std::move(x);
+          Val v;
+          if (Flow f = builtin(F_CONTAINS, "contains", a, &v)) return f;
+          r = v.b;
+        }
+        *out = vbool(n->flag ? !r : r);
+        return OK;
+      }
+      case Node::Range: return fail("internal: range value");
       case Node::If: {
-        Val c;
-        if (!eval(n->kids[0].get(), &c)) return false;
-        if (c.t != VT::Bool) return fail("Boolean value expected for the if condition, found " + std::string(tname(c.t)));
-        if (c.b) return eval(n->kids[1].get(), out);
+        bool c;
+        if (Flow f = cond(n->kids[0].get(), "if", &c)) return f;
+        if (c) return eval(n->kids[1].get(), out);
         if (n->kids.size() > 2) return eval(n->kids[2].get(), out);
         *out = Val{};
-        return true;
+        return OK;
       }
       case Node::Block: {
         const size_t scope = vars.size();
         Val v;
         for (size_t k = 0; k < n->kids.size(); ++k) {
-          const Node* st = n->kids[k].get();
-          if (st->k == Node::Let) {
-            Val x;
-            if (!eval(st->kids[0].get(), &x)) return false;
-            vars.push_back({st->name, x});
-            v = Val{};
-          } else if (!eval(st, &v)) {
-            return false;
+          if (Flow f = eval(n->kids[k].get(), &v)) {
+            vars.resize(scope);
+            return f;
           }
         }
         vars.resize(scope);
-        *out = n->tail ? v : Val{};
-        return true;
+        *out = n->flag ? std::move(v) : Val{};
+        return OK;
       }
-      case Node::Let: *out = Val{}; return true;  // (handled by Block)
+      case Node::Let: {
+        Val x;
+        if (!n->kids.empty())
+          if (Flow f = eval(n->kids[0].get(), &x)) return f;
+        vars.push_back({n->name, std::move(x)});
+        *out = Val{};
+        return OK;
+      }
+      case Node::Assign: {
+        Val r;
+        if (Flow f = eval(n->kids[0].get(), &r)) return f;  // (rhai evaluates the right side first)
+        Val* v = lookup(n->name);
+        if (!v) return fail("Variable not found: " + n->name);
+        if (n->op.empty()) {
+          *v = std::move(r);
+        } else {
+          Val nv;
+          if (Flow f = binop(n->op, true, *v, r, &nv)) return f;
+          *v = std::move(nv);
+        }
+        *out = Val{};
+        return OK;
+      }
+      case Node::IndexAssign: {
+        Val r, ix;
+        if (Flow f = eval(n->kids[1].get(), &r)) return f;
+        if (Flow f = eval(n->kids[0].get(), &ix)) return f;
+        Val* v = lookup(n->name);
+        if (!v) return fail("Variable not found: " + n->name);
+        if (v->t != VT::Arr) return not_indexable(*v);
+        if (ix.t != VT::Int) return fail(std::string("Array index must be an i64, found ") + tname(ix.t));
+        size_t at;
+        if (!index_of(ix.i, v->a.size(), &at)) return bounds(ix.i, v->a.size());
+        Val nv;
+        if (n->op.empty()) {
+          nv = std::move(r);
+        } else if (Flow f = binop(n->op, true, v->a[at], r, &nv)) {
+          return f;
+        }
+        if (!charge(16ull * v->a.size())) return fail(limit_alloc());
+        v->a[at] = std::move(nv);
+        *out = Val{};
+        return OK;
+      }
+      case Node::Index: {
+        Val a, ix;
+        if (Flow f = eval(n->kids[0].get(), &a)) return f;
+        if (Flow f = eval(n->kids[1].get(), &ix)) return f;
+        if (a.t != VT::Arr) return not_indexable(a);
+        if (ix.t != VT::Int) return fail(std::string("Array index must be an i64, found ") + tname(ix.t));
+        size_t at;
+        if (!index_of(ix.i, a.a.size(), &at)) return bounds(ix.i, a.a.size());
+        *out = std::move(a.a[at]);
+        return OK;
+      }
+      case Node::Array: {
+        Val v;
+        v.t = VT::Arr;
+        v.a.resize(n->kids.size());
+        for (size_t k = 0; k < n->kids.size(); ++k)
+          if (Flow f = eval(n->kids[k].get(), &v.a[k])) return f;
+        if (!charge(16ull * n->kids.size())) return fail(limit_alloc());
+        *out = std::move(v);
+        return OK;
+      }
+      case Node::Switch: {
+        Val x;
+        if (Flow f = eval(n->kids[0].get(), &x)) return f;
+        // exact cases first (in order), then range cases, then the wildcard
+        for (int pass = 0; pass < 3; ++pass)
+          for (const SwitchCase& c : n->cases) {
+            if ((pass == 0) != (!c.range && !c.wildcard) || (pass == 1) != c.range || (pass == 2) != c.wildcard) continue;
+            bool m = c.wildcard;
+            if (c.range) m = x.t == VT::Int && x.i >= c.lo && (c.incl ? x.i <= c.hi : x.i < c.hi);
+            for (const Val& v : c.vals) m = m || eq(x, v, 0) == 1;
+            if (!m) continue;
+            if (c.guard) {
+              bool g;
+              if (Flow f = cond(c.guard.get(), "switch case", &g)) return f;
+              if (!g) continue;
+            }
+            return eval(c.body.get(), out);
+          }
+        *out = Val{};
+        return OK;
+      }
+      case Node::While:
+      case Node::Loop:
+      case Node::DoWhile: {
+        const bool is_do = n->k == Node::DoWhile;
+        const Node* b = n->kids[is_do ? 0 : n->k == Node::Loop ? 0 : 1].get();
+        for (bool first = true;; first = false) {
+          if (n->k == Node::While) {
+            bool c;
+            if (Flow f = cond(n->kids[0].get(), "while", &c)) return f;
+            if (!c) break;
+          } else if (is_do && !first) {
+            bool c;
+            if (Flow f = cond(n->kids[1].get(), n->flag ? "do-until" : "do-while", &c)) return f;
+            if (c == n->flag) break;
+          }
+          if (!tick()) return fail(limit_ops());
+          bool leave;
+          if (Flow f = body(b, out, &leave)) return f;
+          if (leave) return OK;
+        }
+        *out = Val{};
+        return OK;
+      }
+      case Node::For: {
+        const Node* it = n->kids[0].get();
+        const Node* b = n->kids[1].get();
+        const size_t scope = vars.size();
+        auto run = [&](Val x, int64_t idx, bool* leave) -> Flow {
+          vars.resize(scope);
+          vars.push_back({n->name, std::move(x)});
+          if (!n->name2.empty()) vars.push_back({n->name2, vint(idx)});
+          if (!tick()) return fail(limit_ops());
+          Flow f = body(b, out, leave);
+          vars.resize(scope);
+          return f;
+        };
+        bool leave = false;
+        if (it->k == Node::Range) {
+          int64_t lo, hi;
+          if (Flow f = range_bounds(it, &lo, &hi)) return f;
+          int64_t k = 0;
+          for (int64_t x = lo; it->flag ? x <= hi : x < hi; ++x, ++k) {
+            if (Flow f = run(vint(x), k, &leave)) return f;
+            if (leave) return OK;
+            if (x == INT64_MAX) break;
+          }
+        } else {
+          Val a;
+          if (Flow f = eval(it, &a)) return f;
+          if (a.t == VT::Str) return fail(std::string(kUnsupported) + "iterating over a string (characters)");
+          if (a.t != VT::Arr) return fail(std::string("For loop expects an iterable type, found ") + tname(a.t));
+          for (size_t k = 0; k < a.a.size(); ++k) {
+            if (Flow f = run(a.a[k], (int64_t)k, &leave)) return f;
+            if (leave) return OK;
+          }
+        }
+        *out = Val{};
+        return OK;
+      }
+      case Node::Break:
+      case Node::Return: {
+        Val v;
+        if (!n->kids.empty())
+          if (Flow f = eval(n->kids[0].get(), &v)) return f;
+        fv = std::move(v);
+        return n->k == Node::Break ? BRK : RET;
+      }
+      case Node::Continue: return CNT;
     }
     return fail("internal: bad node");
   }
-
-  bool bin(const Node* n, Val* out) {
-    const std::string& op = n->op;
-    Val a, b;
-    if (!eval(n->kids[0].get(), &a)) return false;
-    if (op == "||" || op == "&&") {
-      if (a.t != VT::Bool) return fail("Function not found: " + op + " (" + tname(a.t) + ", ...)");
-      if ((op == "||") == a.b) {  // short circuit
-        out->t = VT::Bool;
-        out->b = a.b;
-        return true;
-      }
-      if (!eval(n->kids[1].get(), &b)) return false;
-      if (b.t != VT::Bool) return nf(op, a, b);
-      *out = b;
-      return true;
-    }
-    if (!eval(n->kids[1].get(), &b)) return false;
-    out->t = VT::Bool;
-    if (op == "==" || op == "!=") {  // different types: false (!= true), rhai's built-in comparison
-      bool eq = a.t == b.t && (a.t == VT::Unit || (a.t == VT::Bool && a.b == b.b) || (a.t == VT::Int && a.i == b.i) ||
-                               (a.t == VT::Str && a.s == b.s));
-      out->b = op == "==" ? eq : !eq;
-      return true;
-    }
-    if (op == "<" || op == "<=" || op == ">" || op == ">=") {
-      if (a.t != b.t) {
-        out->b = false;
-        return true;
-      }
-      int c;
-      if (a.t == VT::Int) c = a.i < b.i ? -1 : a.i > b.i ? 1 : 0;
-      else if (a.t == VT::Str) c = a.s.compare(b.s) < 0 ? -1 : a.s == b.s ? 0 : 1;
-      else return nf(op, a, b);
-      out->b = op == "<" ? c < 0 : op == "<=" ? c <= 0 : op == ">" ? c > 0 : c >= 0;
-      return true;
-    }
-    if (op == "|" || op == "&" || op == "^") {
-      if (a.t == VT::Bool && b.t == VT::Bool) {
-        out->b = op == "|" ? (a.b || b.b) : op == "&" ? (a.b && b.b) : (a.b != b.b);
-        return true;
-      }
-      if (a.t == VT::Int && b.t == VT::Int) {
-        out->t = VT::Int;
-        out->i = op == "|" ? (a.i | b.i) : op == "&" ? (a.i & b.i) : (a.i ^ b.i);
-        return true;
-      }
-      return nf(op, a, b);
-    }
-    if (op == "+" && a.t == VT::Str && b.t == VT::Str) {
-      out->t = VT::Str;
-      out->s = a.s + b.s;
-      return true;
-    }
-    if (a.t != VT::Int || b.t != VT::Int) return nf(op, a, b);
-    out->t = VT::Int;
-    const std::string expr = std::to_string(a.i) + " " + op + " " + std::to_string(b.i);
-    long long r = 0;
-    if (op == "+") {
-      if (__builtin_add_overflow(a.i, b.i, &r)) return fail("Addition overflow: " + expr);
-    } else if (op == "-") {
-      if (__builtin_sub_overflow(a.i, b.i, &r)) return fail("Subtraction overflow: " + expr);
-    } else if (op == "*") {
-      if (__builtin_mul_overflow(a.i, b.i, &r)) return fail("Multiplication overflow: " + expr);
-    } else {  // / %
-      if (b.i == 0) return fail("Division by zero: " + expr);
-      if (a.i == INT64_MIN && b.i == -1) return fail((op == "/" ? "Division overflow: " : "Modulo overflow: ") + expr);
-      r = op == "/" ? a.i / b.i : a.i % b.i;
-    }
-    out->i = r;
-    return true;
-  }
 };
 
-ExprOutcome run_ast(const ExprAst& ast, const std::function<bool(uint32_t)>& ok) {
+ExprOutcome run_ast(const ExprAst& ast, const std::function<bool(uint32_t)>& ok, uint64_t* steps = nullptr) {
   Interp in(ok);
+  in.ast = &ast;
   Val v;
   ExprOutcome o;
-  if (!in.eval(ast.root.get(), &v)) {
+  Flow f = in.eval(ast.root.get(), &v);
+  if (f == RET) v = std::move(in.fv);
+  if (f == ERR) {
     o.error = true;
     o.message = in.err;
   } else if (v.t != VT::Bool) {
@@ -517,36 +1553,62 @@ ExprOutcome run_ast(const ExprAst& ast, const std::function<bool(uint32_t)>& ok)
     o.value = v.b;
   }
   o.called = std::move(in.called);
+  if (steps) *steps = in.steps;
   return o;
 }
 
 // ------------------------------------------------------------------------------------------
 // Folding and the bool-only subset
 // ------------------------------------------------------------------------------------------
-bool has_call(const Node* n) {
-  if (n->k == Node::Call) return true;
+bool has_member_call(const Node* n) {
+  if (n->k == Node::Call && n->slot >= 0) return true;
   for (const P& k : n->kids)
-    if (has_call(k.get())) return true;
+    if (has_member_call(k.get())) return true;
+  for (const SwitchCase& c : n->cases)
+    if ((c.guard && has_member_call(c.guard.get())) || has_member_call(c.body.get())) return true;
+  return false;
+}
+bool program_calls_members(const ExprAst& a) {
+  if (has_member_call(a.root.get())) return true;
+  for (const FnDef& f : a.fns)
+    if (has_member_call(f.body.get())) return true;
   return false;
 }
 
-bool has_call_or_var(const Node* n) {
-  if (n->k == Node::Call || n->k == Node::Var || n->k == Node::Let) return true;
-  for (const P& k : n->kids)
-    if (has_call_or_var(k.get())) return true;
-  return false;
+// a subtree that folds: literals and operators over them only (no variables, calls, loops,
+// arrays or strings: a folded string would change what a run charges against its budget)
+bool foldable(const Node* n) {
+  switch (n->k) {
+    case Node::Lit: return n->lit.t != VT::Str;
+    case Node::Unary:
+    case Node::Bin:
+    case Node::Coalesce:
+    case Node::If:
+      for (const P& k : n->kids)
+        if (!foldable(k.get())) return false;
+      return true;
+    case Node::Block:
+      for (const P& k : n->kids)
+        if (!foldable(k.get())) return false;
+      return true;
+    default: return false;
+  }
 }
 
-// Replace every call-free, variable-free subtree whose evaluation succeeds by its value (an erroring
-// one stays: it may never run, e.g. behind a short circuit).
-void fold(P* np) {
+// Replace every foldable subtree whose evaluation succeeds by its value (an erroring one stays:
+// it may never run, e.g. behind a short circuit).
+void fold(P* np, const ExprAst& ast) {
   Node* n = np->get();
-  for (P& k : n->kids) fold(&k);
-  if (n->k == Node::Lit || has_call_or_var(n)) return;
-  const std::function<bool(uint32_t)> none = [](uint32_t) { return false; };
-  Interp in(none);
+  for (P& k : n->kids) fold(&k, ast);
+  for (SwitchCase& c : n->cases) {
+    if (c.guard) fold(&c.guard, ast);
+    fold(&c.body, ast);
+  }
+  if (n->k == Node::Lit || !foldable(n)) return;
+  Interp in([](uint32_t) { return false; });
+  in.ast = &ast;
   Val v;
-  if (!in.eval(n, &v)) return;
+  if (in.eval(n, &v) != OK || (v.t != VT::Bool && v.t != VT::Int && v.t != VT::Unit)) return;
   auto l = std::make_unique<Node>();
   l->lit = v;
   *np = std::move(l);
@@ -556,7 +1618,7 @@ void fold(P* np) {
 // single tail expression
 const Node* bool_root(const ExprAst& a) {
   const Node* r = a.root.get();
-  while (r->k == Node::Block && r->tail && r->kids.size() == 1) r = r->kids[0].get();
+  while (r->k == Node::Block && r->flag && r->kids.size() == 1) r = r->kids[0].get();
   return r;
 }
 bool is_bool_subset(const Node* n) {
@@ -567,7 +1629,7 @@ bool is_bool_subset(const Node* n) {
     case Node::Bin:
       if (n->op != "&&" && n->op != "||" && n->op != "==" && n->op != "!=") return false;
       return is_bool_subset(n->kids[0].get()) && is_bool_subset(n->kids[1].get());
-    case Node::Block: return n->tail && n->kids.size() == 1 && is_bool_subset(n->kids[0].get());
+    case Node::Block: return n->flag && n->kids.size() == 1 && is_bool_subset(n->kids[0].get());
     default: return false;
   }
 }
@@ -623,11 +1685,24 @@ void emit(const Node* n, bool wide, std::vector<uint8_t>* code, uint32_t depth, 
 
 // ---- script bytecode (kwdev.hpp SOp): the interpreter's semantics, compiled
 struct ScriptEmitter {
+  const ExprAst& ast;
   std::vector<uint8_t> code, pool;
-  std::vector<std::vector<std::pair<std::string, uint32_t>>> scopes;  // name -> let slot, innermost last
-  std::vector<uint64_t> slot_len;  // static bound of a let slot's string length
-  uint32_t depth = 0, maxdepth = 0;
-  uint64_t arena = 0;  // bytes of the concatenations a run may build (each runs at most once: no loops)
+  bool allocates = false, uses_type_of = false;
+  struct Loop {
+    uint32_t depth;                  // value-stack depth before the loop expression
+    std::vector<size_t> breaks, conts;  // jump operands to patch
+  };
+  struct Fn {  // the function being emitted
+    std::vector<std::vector<std::pair<std::string, uint32_t>>> scopes;
+    uint32_t nslots = 0, depth = 0, maxdepth = 0;
+    std::vector<Loop> loops;
+    std::vector<size_t> slot_patches;  // S_CALLF caller-slot operands of this function's calls
+  };
+  Fn* cur = nullptr;
+  std::vector<size_t> fn_at;                          // code offset of each script function
+  std::vector<std::pair<size_t, int>> call_patches;  // (operand, fn)
+  explicit ScriptEmitter(const ExprAst& a) : ast(a) {}
+
   void u8(uint8_t x) { code.push_back(x); }
   void u16(uint32_t x) {
     u8((uint8_t)x);
@@ -637,190 +1712,574 @@ struct ScriptEmitter {
     u16(x & 0xffff);
     u16(x >> 16);
   }
-  void push(int n = 1) {
-    depth += (uint32_t)n;
-    maxdepth = std::max(maxdepth, depth);
+  void u64(uint64_t x) {
+    u32((uint32_t)x);
+    u32((uint32_t)(x >> 32));
   }
+  void push(int n = 1) {
+    cur->depth = (uint32_t)((int)cur->depth + n);
+    cur->maxdepth = std::max(cur->maxdepth, cur->depth);
+  }
+  void pop(int n = 1) { cur->depth = (uint32_t)((int)cur->depth - n); }
   size_t hole(uint8_t op) {
     u8(op);
     const size_t at = code.size();
     u32(0);
     return at;
   }
-  void patch(size_t at) {
-    const uint32_t to = (uint32_t)code.size();
+  void patch_to(size_t at, uint32_t to) {
     for (int k = 0; k < 4; ++k) code[at + (size_t)k] = (uint8_t)(to >> (8 * k));
   }
+  void patch(size_t at) { patch_to(at, (uint32_t)code.size()); }
+  uint32_t new_slot() { return cur->nslots++; }
+  uint32_t declare(const std::string& name) {
+    const uint32_t s = new_slot();
+    cur->scopes.back().push_back({name, s});
+    return s;
+  }
   bool lookup(const std::string& name, uint32_t* slot) const {
-    for (size_t sc = scopes.size(); sc-- > 0;)
-      for (size_t k = scopes[sc].size(); k-- > 0;)
-        if (scopes[sc][k].first == name) {
-          *slot = scopes[sc][k].second;
+    for (size_t sc = cur->scopes.size(); sc-- > 0;)
+      for (size_t k = cur->scopes[sc].size(); k-- > 0;)
+        if (cur->scopes[sc][k].first == name) {
+          *slot = cur->scopes[sc][k].second;
           return true;
         }
     return false;
   }
-  // emits n (leaving one value on the stack); returns the static bound of its string length
-  uint64_t emit(const Node* n) {
+  void load(uint32_t s) {
+    u8(S_LOAD);
+    u16(s);
+    push();
+  }
+  void store(uint32_t s) {
+    u8(S_STORE);
+    u16(s);
+    pop();
+  }
+  void lit(const Val& v) {
+    push();
+    if (v.t == VT::Unit) {
+      u8(S_UNIT);
+    } else if (v.t == VT::Bool) {
+      u8(S_BOOL);
+      u8(v.b ? 1 : 0);
+    } else if (v.t == VT::Int) {
+      u8(S_INT);
+      u64((uint64_t)v.i);
+    } else {
+      u8(S_STR);
+      u32((uint32_t)pool.size());  // rebased to the program start at the end
+      u32((uint32_t)v.s.size());
+      pool.insert(pool.end(), v.s.begin(), v.s.end());
+    }
+  }
+  void bin(uint8_t b) {
+    u8(S_BIN);
+    u8(b);
+    pop();
+    if (b == SB_ADD || b == SB_ADDA) allocates = true;
+  }
+  static uint8_t bin_code(const std::string& op, bool assign) {
+    static const char* ops[] = {"|", "^", "&", "==", "!=", "<", "<=", ">", ">=", "+", "-", "*", "/", "%"};
+    if (assign && op == "+") return SB_ADDA;
+    for (uint8_t k = 0; k < 14; ++k)
+      if (op == ops[k]) return k;
+    return 0;
+  }
+  void fail_op() {  // a value the run never gets past
+    u8(S_FAIL);
+    push();
+  }
+  // drop the values above depth d (keeping the top when `keep`)
+  void unwind(uint32_t d, bool keep) {
+    const uint32_t n = cur->depth - d - (keep ? 1u : 0u);
+    if (n == 0) return;
+    u8(keep ? S_DROPKEEP : S_DROP);
+    u16(n);
+  }
+
+  // emits n, leaving one value on the stack
+  void emit(const Node* n) {
     switch (n->k) {
-      case Node::Lit:
-        push();
-        if (n->lit.t == VT::Unit) {
-          u8(S_UNIT);
-        } else if (n->lit.t == VT::Bool) {
-          u8(S_BOOL);
-          u8(n->lit.b ? 1 : 0);
-        } else if (n->lit.t == VT::Int) {
-          u8(S_INT);
-          for (int k = 0; k < 8; ++k) u8((uint8_t)((uint64_t)n->lit.i >> (8 * k)));
-        } else {
-          u8(S_STR);
-          u32((uint32_t)pool.size());  // rebased to the program start at the end
-          u32((uint32_t)n->lit.s.size());
-          pool.insert(pool.end(), n->lit.s.begin(), n->lit.s.end());
-          return n->lit.s.size();
-        }
-        return 0;
+      case Node::Lit: lit(n->lit); return;
       case Node::Var: {
-        uint32_t slot;
-        push();
-        if (!lookup(n->name, &slot)) {
-          u8(S_FAIL);
-          return 0;
-        }
-        u8(S_LOAD);
-        u16(slot);
-        return slot_len[slot];
+        uint32_t s;
+        if (lookup(n->name, &s)) load(s);
+        else fail_op();
+        return;
       }
-      case Node::Call:
-        push();
-        if (n->slot < 0) {
-          u8(S_FAIL);
-        } else {
+      case Node::Call: {
+        for (const P& k : n->kids) emit(k.get());
+        const int na = (int)n->kids.size();
+        if (n->fn >= 0) {
+          u8(S_CALLF);
+          call_patches.push_back({code.size(), n->fn});
+          u32(0);
+          u8((uint8_t)na);
+          cur->slot_patches.push_back(code.size());
+          u16(0);
+          pop(na);
+          push();
+          return;
+        }
+        if (n->slot >= 0) {
           u8(S_CALL);
           u32((uint32_t)n->slot);
+          push();
+          return;
         }
-        return 0;
+        if (n->builtin >= 0) {
+          u8(S_FN);
+          u8((uint8_t)n->builtin);
+          pop(na);
+          push();
+          if (n->builtin == F_TO_STRING || n->builtin == F_PUSH) allocates = true;
+          if (n->builtin == F_TYPE_OF) uses_type_of = true;
+          if (n->builtin == F_PUSH && n->flag) {  // method style: into the variable, the value is ()
+            uint32_t s;
+            if (n->kids[0]->k == Node::Var) {
+              if (lookup(n->kids[0]->name, &s)) store(s);
+              else {
+                u8(S_FAIL);
+                pop();
+              }
+            } else {
+              u8(S_POP);
+              pop();
+            }
+            lit(Val{});
+          }
+          return;
+        }
+        u8(S_FAIL);
+        pop(na);
+        push();
+        return;
+      }
       case Node::Unary:
         emit(n->kids[0].get());
         u8(n->op == "!" ? S_NOT : n->op == "-" ? S_NEG : S_POS);
-        return 0;
+        return;
       case Node::Bin: {
         const std::string& op = n->op;
-        const uint64_t la = emit(n->kids[0].get());
+        emit(n->kids[0].get());
         if (op == "||" || op == "&&") {
           const size_t at = hole(op == "||" ? S_OR : S_AND);
-          --depth;  // (the continuing path pops the left side)
+          pop();  // (the continuing path pops the left side)
           emit(n->kids[1].get());
           u8(S_CHKB);
           patch(at);
-          return 0;
+          return;
         }
-        const uint64_t lb = emit(n->kids[1].get());
-        static const char* ops[] = {"|", "^", "&", "==", "!=", "<", "<=", ">", ">=", "+", "-", "*", "/", "%"};
-        uint8_t code_op = 0;
-        for (uint8_t k = 0; k < 14; ++k)
-          if (op == ops[k]) code_op = k;
-        u8(S_BIN);
-        u8(code_op);
-        --depth;
-        if (code_op == SB_ADD) {
-          arena += la + lb;
-          return la + lb;
-        }
-        return 0;
+        emit(n->kids[1].get());
+        bin(bin_code(op, false));
+        return;
       }
+      case Node::Coalesce: {
+        emit(n->kids[0].get());
+        const size_t at = hole(S_COAL);
+        pop();
+        emit(n->kids[1].get());
+        patch(at);
+        return;
+      }
+      case Node::In: {
+        emit(n->kids[0].get());
+        const Node* h = n->kids[1].get();
+        if (h->k == Node::Range) {
+          emit(h->kids[0].get());
+          emit(h->kids[1].get());
+          u8(S_INRANGE);
+          u8(h->flag ? 1 : 0);
+          pop(2);
+        } else {
+          emit(h);
+          u8(S_FN);
+          u8(F_IN);
+          pop();
+        }
+        if (n->flag) u8(S_NOT);
+        return;
+      }
+      case Node::Range: fail_op(); return;
       case Node::If: {
         emit(n->kids[0].get());
         const size_t at_else = hole(S_IF);
-        --depth;
-        const uint32_t d0 = depth;
-        const uint64_t lt = emit(n->kids[1].get());
+        pop();
+        const uint32_t d0 = cur->depth;
+        emit(n->kids[1].get());
         const size_t at_end = hole(S_JMP);
         patch(at_else);
-        depth = d0;
-        uint64_t le = 0;
-        if (n->kids.size() > 2) {
-          le = emit(n->kids[2].get());
-        } else {
-          push();
-          u8(S_UNIT);
-        }
+        cur->depth = d0;
+        if (n->kids.size() > 2) emit(n->kids[2].get());
+        else lit(Val{});
         patch(at_end);
-        return std::max(lt, le);
+        return;
       }
       case Node::Block: {
-        scopes.emplace_back();
-        uint64_t last = 0;
+        cur->scopes.emplace_back();
         for (size_t k = 0; k < n->kids.size(); ++k) {
           const Node* st = n->kids[k].get();
-          if (st->k == Node::Let) {
-            const uint64_t l = emit(st->kids[0].get());
-            const uint32_t slot = (uint32_t)slot_len.size();
-            slot_len.push_back(l);
-            u8(S_STORE);
-            u16(slot);
-            --depth;
-            scopes.back().push_back({st->name, slot});
-            last = 0;
-          } else {
-            last = emit(st);
-            if (!(n->tail && k + 1 == n->kids.size())) {
-              u8(S_POP);
-              --depth;
-            }
+          emit(st);
+          if (!(n->flag && k + 1 == n->kids.size())) {
+            u8(S_POP);
+            pop();
           }
         }
-        scopes.pop_back();
-        if (!n->tail) {
-          push();
-          u8(S_UNIT);
-          return 0;
-        }
-        return last;
+        cur->scopes.pop_back();
+        if (!n->flag) lit(Val{});
+        return;
       }
-      case Node::Let: push(); u8(S_UNIT); return 0;  // (handled by Block)
+      case Node::Let: {
+        if (n->kids.empty()) lit(Val{});
+        else emit(n->kids[0].get());
+        const uint32_t s = declare(n->name);  // (after the initializer: `let x = x + 1` reads the old x)
+        store(s);
+        lit(Val{});
+        return;
+      }
+      case Node::Assign: {
+        uint32_t s;
+        const bool found = lookup(n->name, &s);
+        emit(n->kids[0].get());
+        if (!found) {
+          u8(S_FAIL);
+          return;  // (the right side's value stands for the statement)
+        }
+        if (n->op.empty()) {
+          store(s);
+        } else {
+          const uint32_t t = new_slot();
+          store(t);
+          load(s);
+          load(t);
+          bin(bin_code(n->op, true));
+          store(s);
+        }
+        lit(Val{});
+        return;
+      }
+      case Node::IndexAssign: {
+        uint32_t s;
+        const bool found = lookup(n->name, &s);
+        const uint32_t tv = new_slot(), ti = new_slot();
+        emit(n->kids[1].get());  // value first (rhai evaluates the right side first)
+        store(tv);
+        emit(n->kids[0].get());
+        store(ti);
+        if (!found) {
+          fail_op();
+          return;
+        }
+        load(ti);
+        if (n->op.empty()) {
+          load(tv);
+        } else {
+          load(s);
+          load(ti);
+          u8(S_INDEX);
+          pop();
+          load(tv);
+          bin(bin_code(n->op, true));
+        }
+        u8(S_SETIDX);
+        u16(s);
+        pop(2);
+        allocates = true;
+        lit(Val{});
+        return;
+      }
+      case Node::Index:
+        emit(n->kids[0].get());
+        emit(n->kids[1].get());
+        u8(S_INDEX);
+        pop();
+        return;
+      case Node::Array:
+        for (const P& k : n->kids) emit(k.get());
+        u8(S_ARR);
+        u16((uint32_t)n->kids.size());
+        pop((int)n->kids.size());
+        push();
+        allocates = true;
+        return;
+      case Node::Switch: {
+        emit(n->kids[0].get());
+        const uint32_t s = new_slot();
+        store(s);
+        std::vector<size_t> ends;
+        const uint32_t d0 = cur->depth;
+        for (int pass = 0; pass < 3; ++pass)
+          for (const SwitchCase& c : n->cases) {
+            if ((pass == 0) != (!c.range && !c.wildcard) || (pass == 1) != c.range || (pass == 2) != c.wildcard) continue;
+            std::vector<size_t> nexts;
+            if (!c.wildcard) {
+              if (c.range) {
+                load(s);
+                u8(S_RCASE);
+                u64((uint64_t)c.lo);
+                u64((uint64_t)c.hi);
+                u8(c.incl ? 1 : 0);
+              } else {
+                std::vector<size_t> ors;
+                for (size_t v = 0; v < c.vals.size(); ++v) {
+                  load(s);
+                  lit(c.vals[v]);
+                  bin(SB_EQ);
+                  if (v + 1 < c.vals.size()) {
+                    ors.push_back(hole(S_OR));
+                    pop();
+                  }
+                }
+                for (size_t at : ors) patch(at);
+              }
+              nexts.push_back(hole(S_IF));
+              pop();
+            }
+            if (c.guard) {
+              emit(c.guard.get());
+              nexts.push_back(hole(S_IF));
+              pop();
+            }
+            emit(c.body.get());
+            ends.push_back(hole(S_JMP));
+            cur->depth = d0;
+            for (size_t at : nexts) patch(at);
+          }
+        lit(Val{});
+        for (size_t at : ends) patch(at);
+        return;
+      }
+      case Node::While:
+      case Node::Loop:
+      case Node::DoWhile: {
+        const uint32_t d0 = cur->depth;
+        cur->loops.push_back({d0, {}, {}});
+        size_t exit_at = 0;
+        bool has_exit = false;
+        uint32_t top = (uint32_t)code.size(), cont;
+        if (n->k == Node::DoWhile) {
+          u8(S_TICK);
+          emit(n->kids[0].get());
+          u8(S_POP);
+          pop();
+          cont = (uint32_t)code.size();
+          emit(n->kids[1].get());
+          if (n->flag) u8(S_NOT);
+          exit_at = hole(S_IF);  // while: false leaves; until: true leaves
+          pop();
+          has_exit = true;
+          const size_t j = hole(S_JMP);
+          patch_to(j, top);
+        } else {
+          cont = top;
+          if (n->k == Node::While) {
+            emit(n->kids[0].get());
+            exit_at = hole(S_IF);
+            pop();
+            has_exit = true;
+          }
+          u8(S_TICK);
+          emit(n->kids[n->k == Node::Loop ? 0 : 1].get());
+          u8(S_POP);
+          pop();
+          const size_t j = hole(S_JMP);
+          patch_to(j, top);
+        }
+        if (has_exit) patch(exit_at);
+        lit(Val{});  // the normal exit's value
+        Loop L = std::move(cur->loops.back());
+        cur->loops.pop_back();
+        for (size_t at : L.breaks) patch(at);
+        for (size_t at : L.conts) patch_to(at, cont);
+        cur->depth = d0 + 1;
+        return;
+      }
+      case Node::For: {
+        const uint32_t d0 = cur->depth;
+        const Node* it = n->kids[0].get();
+        const uint32_t sa = new_slot(), si = new_slot();
+        const bool range = it->k == Node::Range;
+        if (range) {
+          emit(it->kids[0].get());
+          emit(it->kids[1].get());
+          u8(S_RANGECHK);
+          store(si);  // hi (the end slot is `si` here; `sa` holds the cursor)
+          store(sa);
+        } else {
+          emit(it);
+          store(sa);
+          lit(vint(0));
+          store(si);
+        }
+        uint32_t sc = 0;
+        if (range && !n->name2.empty()) {
+          sc = new_slot();
+          lit(vint(0));
+          store(sc);
+        }
+        cur->loops.push_back({d0, {}, {}});
+        const uint32_t top = (uint32_t)code.size();
+        size_t exit_at;
+        if (range) {
+          u8(S_FORR);
+          u16(sa);
+          u16(si);
+          u8(it->flag ? 1 : 0);
+          exit_at = code.size();
+          u32(0);
+          push();
+        } else {
+          u8(S_FORA);
+          u16(sa);
+          u16(si);
+          u8(n->name2.empty() ? 0 : 1);
+          exit_at = code.size();
+          u32(0);
+          push(n->name2.empty() ? 1 : 2);
+        }
+        cur->scopes.emplace_back();
+        const uint32_t sx = declare(n->name);
+        if (!n->name2.empty()) {
+          const uint32_t sk = declare(n->name2);
+          if (range) {  // the counter of a range loop lives in slot sc (zeroed before `top`)
+            store(sx);
+            load(sc);
+            store(sk);
+            load(sc);
+            lit(vint(1));
+            bin(SB_ADD);
+            store(sc);
+          } else {
+            store(sk);
+            store(sx);
+          }
+        } else {
+          store(sx);
+        }
+        u8(S_TICK);
+        emit(n->kids[1].get());
+        u8(S_POP);
+        pop();
+        cur->scopes.pop_back();
+        const size_t j = hole(S_JMP);
+        patch_to(j, top);
+        patch(exit_at);
+        lit(Val{});
+        Loop L = std::move(cur->loops.back());
+        cur->loops.pop_back();
+        for (size_t at : L.breaks) patch(at);
+        for (size_t at : L.conts) patch_to(at, top);
+        cur->depth = d0 + 1;
+        return;
+      }
+      case Node::Break:
+      case Node::Continue: {
+        Loop& L = cur->loops.back();
+        if (n->k == Node::Break) {
+          if (n->kids.empty()) lit(Val{});
+          else emit(n->kids[0].get());
+          unwind(L.depth, true);
+          L.breaks.push_back(hole(S_JMP));
+        } else {
+          unwind(L.depth, false);
+          L.conts.push_back(hole(S_JMP));
+          push();
+        }
+        cur->depth = L.depth + 1;  // (unreachable after the jump; keeps the bookkeeping whole)
+        return;
+      }
+      case Node::Return: {
+        if (n->kids.empty()) lit(Val{});
+        else emit(n->kids[0].get());
+        u8(cur == &main_fn ? S_END : S_RET);
+        return;
+      }
     }
-    return 0;
   }
+
+  Fn main_fn;
+  std::vector<Fn> fns;
 };
 
 // The script form of a group (GroupProgram::script): header | code | string pool (kwdev.hpp SOp).
 bool emit_script(const ExprAst& ast, std::vector<uint8_t>* out, uint32_t* depth, std::string* err) {
-  ScriptEmitter e;
+  ScriptEmitter e(ast);
+  e.cur = &e.main_fn;
+  e.main_fn.scopes.emplace_back();
   e.emit(ast.root.get());
   e.u8(S_END);
-  if (e.arena > kMaxScriptArena) {
-    *err = "policy group expression can build strings longer than the engine's limit (65536 bytes)";
-    return false;
+  e.fns.resize(ast.fns.size());
+  e.fn_at.assign(ast.fns.size(), 0);
+  for (size_t f = 0; f < ast.fns.size(); ++f) {
+    e.cur = &e.fns[f];
+    e.cur->scopes.emplace_back();
+    for (const std::string& p : ast.fns[f].params) e.declare(p);
+    e.fn_at[f] = e.code.size();
+    e.emit(ast.fns[f].body.get());
+    e.u8(S_RET);
   }
-  if (e.slot_len.size() > 65535 || e.code.size() + e.pool.size() > 0x7fffffffu) {
+  for (auto& c : e.call_patches) e.patch_to(c.first, (uint32_t)e.fn_at[(size_t)c.second]);
+  auto patch_slots = [&](ScriptEmitter::Fn& f) {
+    for (size_t at : f.slot_patches) {
+      e.code[at] = (uint8_t)f.nslots;
+      e.code[at + 1] = (uint8_t)(f.nslots >> 8);
+    }
+  };
+  patch_slots(e.main_fn);
+  uint32_t fn_depth = 0, fn_slots = 0;
+  for (ScriptEmitter::Fn& f : e.fns) {
+    patch_slots(f);
+    fn_depth = std::max(fn_depth, f.maxdepth);
+    fn_slots = std::max(fn_slots, f.nslots);
+  }
+  const bool has_fns = !ast.fns.empty();
+  const uint64_t total_depth = (uint64_t)e.main_fn.maxdepth + (has_fns ? (uint64_t)kMaxCallDepth * fn_depth : 0) + 1;
+  const uint64_t total_slots = (uint64_t)e.main_fn.nslots + (has_fns ? (uint64_t)kMaxCallDepth * fn_slots : 0);
+  if (e.main_fn.nslots > 65535 || fn_slots > 65535 || total_depth > (1u << 24) || total_slots > (1u << 24) ||
+      e.code.size() + e.pool.size() > 0x7fffffffu) {
     *err = "policy group expression exceeds the engine's limits";
     return false;
   }
-  const uint32_t hdr = 16, code_len = (uint32_t)e.code.size();
+  uint32_t tnames = 0;
+  if (e.uses_type_of) {
+    tnames = (uint32_t)e.pool.size();
+    const char* names = "()booli64stringarray";
+    e.pool.insert(e.pool.end(), names, names + 20);
+  }
+  const uint32_t code_len = (uint32_t)e.code.size();
   // rebase S_STR pool offsets to the program start: walk the code
   for (size_t pc = 0; pc < e.code.size();) {
     const uint8_t op = e.code[pc++];
     switch (op) {
-      case S_BOOL: case S_BIN: pc += 1; break;
+      case S_BOOL: case S_BIN: case S_FN: case S_INRANGE: pc += 1; break;
       case S_INT: pc += 8; break;
       case S_STR: {
         uint32_t off = 0;
         for (int k = 0; k < 4; ++k) off |= (uint32_t)e.code[pc + (size_t)k] << (8 * k);
-        off += hdr + code_len;
+        off += kScriptHeader + code_len;
         for (int k = 0; k < 4; ++k) e.code[pc + (size_t)k] = (uint8_t)(off >> (8 * k));
         pc += 8;
         break;
       }
-      case S_LOAD: case S_STORE: pc += 2; break;
-      case S_CALL: case S_AND: case S_OR: case S_IF: case S_JMP: pc += 4; break;
+      case S_LOAD: case S_STORE: case S_ARR: case S_SETIDX: case S_DROP: case S_DROPKEEP: pc += 2; break;
+      case S_CALL: case S_AND: case S_OR: case S_IF: case S_JMP: case S_COAL: pc += 4; break;
+      case S_RCASE: pc += 17; break;
+      case S_FORR: case S_FORA: pc += 9; break;
+      case S_CALLF: pc += 7; break;
       default: break;
     }
   }
   out->clear();
-  const uint32_t h[4] = {std::max(e.maxdepth, 1u), (uint32_t)e.slot_len.size(), (uint32_t)e.arena, code_len};
-  out->insert(out->end(), (const uint8_t*)h, (const uint8_t*)h + 16);
+  const uint32_t h[8] = {(uint32_t)total_depth,
+                         (uint32_t)std::max<uint64_t>(total_slots, 1),
+                         e.allocates ? kMaxScriptAlloc : 0u,
+                         code_len,
+                         has_fns ? kMaxCallDepth : 0u,
+                         tnames + kScriptHeader + code_len,
+                         0,
+                         0};
+  out->insert(out->end(), (const uint8_t*)h, (const uint8_t*)h + kScriptHeader);
   out->insert(out->end(), e.code.begin(), e.code.end());
   out->insert(out->end(), e.pool.begin(), e.pool.end());
   *depth = h[0];
@@ -852,28 +2311,49 @@ GroupProgram compile_group_expression(const std::string& expr, const std::vector
     g.error = lx.err;
     return g;
   }
-  Parser p(lx.toks, members);
+  auto ast = std::make_shared<ExprAst>();
+  Parser p(lx.toks);
+  p.ast = ast.get();
   P root = p.block_body(true);
   if (!root) {
     g.error = p.err;
     return g;
   }
-  auto ast = std::make_shared<ExprAst>();
   ast->root = std::move(root);
-  // validation: the script runs with every member returning true (validate_settings)
   {
-    Interp in([](uint32_t) { return true; });
-    Val v;
-    if (!in.eval(ast->root.get(), &v)) {
-      g.error = in.err;
+    std::string rerr;
+    bool ok = check_ranges(ast->root.get(), false, &rerr);
+    for (const FnDef& f : ast->fns) ok = ok && check_ranges(f.body.get(), false, &rerr);
+    if (!ok) {
+      g.error = rerr;
+      return g;
+    }
+  }
+  resolve(ast->root.get(), *ast, members);
+  for (FnDef& f : ast->fns) resolve(f.body.get(), *ast, members);
+  {
+    bool stray = stray_range_call(ast->root.get());
+    for (const FnDef& f : ast->fns) stray = stray || stray_range_call(f.body.get());
+    if (stray) {
+      g.error = std::string(kUnsupported) + "range values outside `for` and `in`";
+      return g;
+    }
+  }
+  // validation: the script runs with every member returning true (validate_settings)
+  uint64_t steps = 0;
+  {
+    const ExprOutcome o = run_ast(*ast, [](uint32_t) { return true; }, &steps);
+    if (o.error && o.message.rfind("Output type incorrect", 0) != 0) {
+      g.error = o.message;
       return g;
     }
   }
   g.valid = true;
-  fold(&ast->root);
+  fold(&ast->root, *ast);
+  for (FnDef& f : ast->fns) fold(&f.body, *ast);
   g.ast = ast;
   // a script without member calls has one outcome: a constant column or a constant program
-  if (!has_call(ast->root.get())) {
+  if (!program_calls_members(*ast)) {
     const ExprOutcome o = run_ast(*ast, [](uint32_t) { return true; });
     if (o.error) {
       g.eval_error = true;
@@ -884,8 +2364,11 @@ GroupProgram compile_group_expression(const std::string& expr, const std::vector
     g.depth = 1;
     return g;
   }
+  // KW_GROUP_FORM=script: every group with member calls takes the bytecode form (a test knob: the
+  // CPU suite runs the stack machine through the host walk, the GPU suite through the combine kernel)
+  const bool force_script = getenv("KW_GROUP_FORM") && std::string(getenv("KW_GROUP_FORM")) == "script";
   const Node* br = bool_root(*ast);
-  if (is_bool_subset(br)) {
+  if (!force_script && ast->fns.empty() && is_bool_subset(br)) {
     uint32_t maxd = 1;
     emit(br, false, &g.code, 1, &maxd);
     g.depth = maxd;
@@ -904,8 +2387,11 @@ GroupProgram compile_group_expression(const std::string& expr, const std::vector
     g.wide = true;
     return g;
   }
-  if (members.size() > kMaxTableMembers) {
-    // too many members for a truth table: typed bytecode, run by the wide path's combine kernel
+  // a truth table when it is small and cheap to fill (2^n runs of the interpreter); otherwise
+  // typed bytecode, run per request by the wide path's combine kernel
+  const bool table = !force_script && members.size() <= kMaxTableMembers &&
+                     (std::max<uint64_t>(steps, 1) << members.size()) <= (1ull << 24);
+  if (!table) {
     std::string err;
     if (!emit_script(*ast, &g.code, &g.depth, &err)) {
       g.valid = false;

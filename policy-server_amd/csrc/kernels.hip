@@ -1638,9 +1638,11 @@ __global__ void __launch_bounds__(kWideThreads) wide_groups_kernel(WideGroupPass
       return (x & KW_V_ALLOWED) && !(x & KW_V_MUTATED);
     };
     auto cause = [&](uint32_t s) { cz[s >> 6] |= 1ull << (s & 63u); };
+    // a group of at most 15 members carries its causes in ARG, as column_word's forms do
+    auto rej = [&]() { return g.nmem <= 15 ? (g.rejb & 0xffffu) | ((uint32_t)cz[0] << 16) : g.rejb; };
     if (g.kind == 1) {  // script bytecode: true, false or an evaluation error
       const int v = run_script_prog(w.progs + g.prog_off, stack, ok, cause);
-      *dst = v == 1 ? g.okw : v == 0 ? g.rejb : g.errw;
+      *dst = v == 1 ? g.okw : v == 0 ? rej() : g.errw;
       continue;
     }
     if (g.kind >= 2) {  // a split plain policy: its parts' words
@@ -1648,7 +1650,7 @@ __global__ void __launch_bounds__(kWideThreads) wide_groups_kernel(WideGroupPass
       continue;
     }
     const bool v = run_wide_prog(w.progs + g.prog_off, g.prog_len, stack, ok, cause);
-    *dst = v ? g.okw : g.rejb;
+    *dst = v ? g.okw : rej();
   }
 }
 

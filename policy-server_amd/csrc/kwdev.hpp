@@ -57,25 +57,61 @@ enum PolicyFlag : uint8_t {
 //   G_CALL16 s              (wide programs) push ok(s), s a u16 member index; in wide programs the
 //                           G_JT / G_JF targets are u32
 enum GOp : uint8_t { G_CONST0 = 0, G_CONST1 = 1, G_CALL = 2, G_NOT = 3, G_JT = 4, G_JF = 5, G_EQ = 6, G_NE = 7, G_CALL16 = 8 };
-// Script bytecode (groups beyond the bool-only subset with more than 16 members; expr.cpp emits it,
-// slots.hpp run_script_prog runs it). Header: u32 depth (value stack), nvars (`let` slots), arena
-// (string bytes a run may build), code_len; then the code, then the string pool. Values are 16 B:
-// type (0 unit, 1 bool, 2 i64, 3 string) | string length << 32 | 256 when the bytes are in the
-// arena; then the bool / i64 value or the string's byte offset. Operands little-endian.
+// Script bytecode (groups beyond the bool-only subset that no truth table covers; expr.cpp emits
+// it, slots.hpp run_script_prog runs it). Header (32 B): u32 depth (value stack bound), nvars
+// (variable slots of every frame a run can hold), arena (bytes of strings and arrays a run may
+// build), code_len, nframes (script-function frames: 0 or kMaxCallDepth), 3 reserved; then the
+// code, then the string pool. Values are 16 B: word 0 = type (0 unit, 1 bool, 2 i64, 3 string,
+// 4 array) | 256 when the bytes are in the arena | length << 32 (string bytes, array elements);
+// word 1 = the bool / i64 value, or the byte offset of the string (program-relative, or
+// arena-relative with 256) or of the array's 16-B cells (arena-relative). Values are immutable:
+// every operation that changes an array or builds a string writes a new arena block, charged
+// against kMaxScriptAlloc exactly as the host interpreter charges it. Operands little-endian.
 //   S_UNIT | S_BOOL u8 | S_INT i64 | S_STR u32 off u32 len (pool, program-relative)
-//   S_LOAD u16 / S_STORE u16 (pops)          `let` slot
+//   S_LOAD u16 / S_STORE u16 (pops)          variable slot of the current frame
 //   S_CALL u32                                push ok(member), the member counts as called
-//   S_FAIL                                    unknown function / variable: evaluation error
+//   S_FAIL                                    an evaluation error found at compile time (unknown
+//                                             function or variable, ...): the host words it
 //   S_NOT / S_NEG / S_POS                     unary (type-checked, -i64::MIN overflows)
-//   S_BIN u8                                  | ^ & == != < <= > >= + - * / % (SBin), checked
+//   S_BIN u8                                  SBin (checked; string + any concatenates)
 //   S_AND u32 / S_OR u32                      top must be bool; short circuit: jump keeping it, else pop
 //   S_CHKB                                    the right side of && / || must be bool
 //   S_IF u32                                  pop the condition (bool), false: jump
 //   S_JMP u32 | S_POP | S_END (the result must be a bool)
+//   S_ARR u16 n                               pop n values, push an array of them
+//   S_INDEX                                   pop index, pop array: push the element (rhai's
+//                                             negative indices count from the end)
+//   S_SETIDX u16 slot                         pop value, pop index: slot's array with that element set
+//   S_FN u8 fid                               built-in function (SFn) over its arguments
+//   S_COAL u32                                ??: top not (): jump keeping it, else pop
+//   S_INRANGE u8 incl                         pop hi, lo, x: x in lo..hi (all i64, else an error)
+//   S_RCASE i64 lo i64 hi u8 incl             pop x: push x is an i64 in the range (switch cases)
+//   S_TICK                                    one loop iteration: counts against kMaxScriptOps
+//   S_FORR u16 i u16 e u8 incl u32 exit       range loop: slots i / e hold the cursor and the end;
+//                                             done: jump to exit, else push the cursor, advance it
+//   S_FORA u16 a u16 i u8 with_index u32 exit array loop over slot a's array, cursor slot i;
+//                                             push the element (and its index)
+//   S_RANGECHK                                the two range bounds on the top must be i64
+//   S_CALLF u32 at u8 nargs u16 caller_slots  call a script function (counts against
+//                                             kMaxScriptOps; more than kMaxCallDepth frames: error)
+//   S_RET                                     return the top value to the caller
+//   S_DROP u16 n / S_DROPKEEP u16 n           drop n values / n values under the top (break, continue)
 enum SOp : uint8_t { S_UNIT = 0, S_BOOL, S_INT, S_STR, S_LOAD, S_STORE, S_CALL, S_FAIL, S_NOT, S_NEG, S_POS, S_BIN,
-                     S_AND, S_OR, S_CHKB, S_IF, S_JMP, S_POP, S_END };
-enum SBin : uint8_t { SB_OR = 0, SB_XOR, SB_AND, SB_EQ, SB_NE, SB_LT, SB_LE, SB_GT, SB_GE, SB_ADD, SB_SUB, SB_MUL, SB_DIV, SB_MOD };
-constexpr uint32_t kMaxScriptArena = 1u << 16;  // string bytes one run may build (an engine limit far past real scripts)
+                     S_AND, S_OR, S_CHKB, S_IF, S_JMP, S_POP, S_END, S_ARR, S_INDEX, S_SETIDX, S_FN, S_COAL,
+                     S_INRANGE, S_RCASE, S_TICK, S_FORR, S_FORA, S_RANGECHK, S_CALLF, S_RET, S_DROP, S_DROPKEEP };
+// | ^ & == != < <= > >= + - * / %, then the compound assignments that differ from their operator:
+// `+=` (an array pushes / appends; otherwise `+`) and the `x op= y` forms whose errors name `op=`
+enum SBin : uint8_t { SB_OR = 0, SB_XOR, SB_AND, SB_EQ, SB_NE, SB_LT, SB_LE, SB_GT, SB_GE, SB_ADD, SB_SUB, SB_MUL, SB_DIV,
+                      SB_MOD, SB_ADDA };
+// Built-in functions (method or function-call style; `x in y` is contains(y, x))
+enum SFn : uint8_t { F_LEN = 0, F_IS_EMPTY, F_CONTAINS, F_TO_STRING, F_TYPE_OF, F_STARTS_WITH, F_ENDS_WITH, F_PUSH, F_IN };
+// Engine limits of one run of a group expression (host interpreter, device bytecode and the oracle
+// apply them identically; each is named in the run's error message)
+constexpr uint32_t kMaxScriptAlloc = 16384;   // bytes of strings and array cells a run may build
+constexpr uint32_t kMaxScriptOps = 100000;    // loop iterations + script-function calls
+constexpr uint32_t kMaxCallDepth = 64;        // nested script-function calls ("Stack overflow")
+constexpr uint32_t kMaxCompareDepth = 16;     // array nesting inside one comparison
+constexpr uint32_t kScriptHeader = 32;
 constexpr int kMaxGroupStack = 64;    // value-stack depth (only == / != nest it)
 constexpr int kMaxGroupMembers = 64;  // members evaluate as slots of one slot-plan chunk
 constexpr int kMaxLocalBits = 64;     // per chunk: distinct mandatory label keys / mutation capabilities

@@ -338,7 +338,8 @@ Status format_response(const Env& env, const Batch& b, uint64_t row, int32_t pid
   }
   // vanilla status
   uint64_t full = 0;
-  const bool big_group = reason == KW_R_GROUP && P.is_group && P.prog.wide;  // causes: multi-word side data
+  // causes: multi-word side data (a wide group of more than 15 members; smaller ones carry them in ARG)
+  const bool big_group = reason == KW_R_GROUP && P.is_group && P.prog.wide && arg == KW_ARG_WIDE;
   if (reason != KW_R_GROUP_EXPR && reason != KW_R_INIT_ERROR && !big_group) {
     Status st = full_arg(b, row, pidx, arg, &full);
     if (!st.ok()) return st;

@@ -462,57 +462,154 @@ KW_HD inline bool run_wide_prog(const uint8_t* prog, uint32_t len, uint64_t* sta
 }
 
 // Script bytecode (kwdev.hpp SOp) over the member results: 1 / 0 the bool result, 2 an evaluation
-// error (a type mismatch, checked-arithmetic overflow, division by zero, an unknown name, a non-bool
-// result: the host interpreter words the message). `scratch`: run_script_words(prog) u64 words.
-// cause(s) records a called member that rejected.
+// error (a type mismatch, checked-arithmetic overflow, division by zero, an index out of bounds, an
+// unknown name, an engine limit, a non-bool result: the host interpreter words the message).
+// `scratch`: run_script_words(prog) u64 words. cause(s) records a called member that rejected.
 KW_HD inline uint64_t run_script_words(const uint8_t* prog) {
-  const uint32_t* h = (const uint32_t*)prog;  // depth, nvars, arena bytes, code_len
-  return 2ull * h[0] + 2ull * h[1] + (h[2] + 7u) / 8u + 1u;
+  const uint32_t* h = (const uint32_t*)prog;  // depth, nvars, arena bytes, code_len, nframes
+  return 2ull * h[0] + 2ull * h[1] + 2ull * h[4] + (h[2] + 15u) / 16u * 2u + 1u;
 }
+
+namespace sv {
+constexpr uint32_t UNIT = 0, BOOL = 1, INT = 2, STR = 3, ARR = 4, ARENA = 256;
+}
+
 template <class Ok, class Cause>
 KW_HD inline int run_script_prog(const uint8_t* prog, uint64_t* scratch, Ok ok, Cause cause) {
   const uint32_t* h = (const uint32_t*)prog;
-  const uint32_t depth = h[0], nvars = h[1], code_len = h[3];
-  const uint8_t* code = prog + 16;
-  uint64_t* st = scratch;                  // value stack: 2 words a value
-  uint64_t* vars = scratch + 2ull * depth;  // let slots
-  uint8_t* arena = (uint8_t*)(vars + 2ull * nvars);
-  uint32_t atop = 0;
-  uint32_t sp = 0;
-  auto rd32 = [&](uint32_t pc) {
-    return (uint32_t)code[pc] | ((uint32_t)code[pc + 1] << 8) | ((uint32_t)code[pc + 2] << 16) | ((uint32_t)code[pc + 3] << 24);
-  };
+  const uint32_t depth = h[0], nvars = h[1], arena_cap = (h[2] + 15u) & ~15u, code_len = h[3], nframes = h[4];
+  const uint32_t tnames = h[5];  // program-relative offset of "()booli64stringarray" (type_of)
+  const uint8_t* code = prog + kScriptHeader;
+  uint64_t* st = scratch;                     // value stack: 2 words a value
+  uint64_t* vars = st + 2ull * depth;         // variable slots of every frame
+  uint64_t* frames = vars + 2ull * nvars;     // call frames: (return pc | caller fp << 32, sp)
+  uint8_t* arena = (uint8_t*)(frames + 2ull * nframes);
+  uint32_t sbot = 0, atop = arena_cap;  // strings grow up from 0, array cells down from the cap
+  uint32_t alloc = 0, ops = 0, sp = 0, fp = 0, nf = 0;
+  auto rd16 = [&](uint32_t pc) { return (uint32_t)code[pc] | ((uint32_t)code[pc + 1] << 8); };
+  auto rd32 = [&](uint32_t pc) { return rd16(pc) | (rd16(pc + 2) << 16); };
+  auto rd64 = [&](uint32_t pc) { return (uint64_t)rd32(pc) | ((uint64_t)rd32(pc + 4) << 32); };
   auto type = [&](uint32_t i) -> uint32_t { return (uint32_t)(st[2 * i] & 0xffu); };
-  auto sbytes = [&](uint32_t i) -> const uint8_t* {
-    return (st[2 * i] & 256u) ? arena + st[2 * i + 1] : prog + st[2 * i + 1];
-  };
-  auto slen = [&](uint32_t i) -> uint32_t { return (uint32_t)(st[2 * i] >> 32); };
+  auto bytes_of = [&](uint64_t w0, uint64_t w1) -> const uint8_t* { return (w0 & sv::ARENA) ? arena + w1 : prog + w1; };
+  auto len_of = [&](uint64_t w0) -> uint32_t { return (uint32_t)(w0 >> 32); };
+  auto cells_of = [&](uint64_t w1) -> uint64_t* { return (uint64_t*)(arena + w1); };
   auto set = [&](uint32_t i, uint32_t t, uint64_t v) {
     st[2 * i] = t;
     st[2 * i + 1] = v;
   };
+  // charge `n` bytes of a run's kMaxScriptAlloc budget (the host interpreter charges the same)
+  auto charge = [&](uint32_t n) {
+    if (n > kMaxScriptAlloc - alloc) return false;
+    alloc += n;
+    return true;
+  };
+  auto new_str = [&](uint32_t n) -> uint8_t* {  // (charged by the caller)
+    if (sbot + n > atop) return nullptr;
+    uint8_t* p = arena + sbot;
+    sbot += n;
+    return p;
+  };
+  auto new_cells = [&](uint32_t n) -> uint64_t* {
+    if (atop < sbot + 16u * n) return nullptr;
+    atop -= 16u * n;
+    return (uint64_t*)(arena + atop);
+  };
+  // deep equality: 1 / 0, or -1 when arrays nest deeper than kMaxCompareDepth
+  auto veq = [&](uint64_t x0, uint64_t x1, uint64_t y0, uint64_t y1) -> int {
+    const uint64_t* fa[kMaxCompareDepth];
+    const uint64_t* fb[kMaxCompareDepth];
+    uint32_t fn[kMaxCompareDepth];
+    uint32_t d = 0;
+    for (;;) {
+      const uint32_t tx = (uint32_t)(x0 & 0xffu), ty = (uint32_t)(y0 & 0xffu);
+      bool eq = tx == ty, descend = false;
+      if (eq && (tx == sv::BOOL || tx == sv::INT)) {
+        eq = x1 == y1;
+      } else if (eq && tx == sv::STR) {
+        const uint32_t n = len_of(x0);
+        eq = n == len_of(y0);
+        const uint8_t *pa = bytes_of(x0, x1), *pb = bytes_of(y0, y1);
+        for (uint32_t k = 0; eq && k < n; ++k) eq = pa[k] == pb[k];
+      } else if (eq && tx == sv::ARR) {
+        const uint32_t n = len_of(x0);
+        eq = n == len_of(y0);
+        if (eq && n) {
+          if (d == kMaxCompareDepth) return -1;
+          fa[d] = cells_of(x1);
+          fb[d] = cells_of(y1);
+          fn[d] = n;
+          ++d;
+          descend = true;
+        }
+      }
+      if (!eq) return 0;
+      (void)descend;
+      while (d > 0 && fn[d - 1] == 0) --d;
+      if (d == 0) return 1;
+      x0 = fa[d - 1][0];
+      x1 = fa[d - 1][1];
+      y0 = fb[d - 1][0];
+      y1 = fb[d - 1][1];
+      fa[d - 1] += 2;
+      fb[d - 1] += 2;
+      --fn[d - 1];
+    }
+  };
+  // decimal text of an i64 into `buf` (20 bytes), returns its length
+  auto itoa = [](int64_t v, uint8_t* buf) -> uint32_t {
+    uint8_t t[20];
+    uint32_t n = 0;
+    uint64_t u = v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;
+    do {
+      t[n++] = (uint8_t)('0' + u % 10u);
+      u /= 10u;
+    } while (u);
+    uint32_t k = 0;
+    if (v < 0) buf[k++] = '-';
+    while (n) buf[k++] = t[--n];
+    return k;
+  };
+  // to_string of a scalar as (length, bytes in `tmp` or the value's own bytes); false for an array
+  auto text_of = [&](uint64_t w0, uint64_t w1, uint8_t* tmp, const uint8_t** p, uint32_t* n) -> bool {
+    const uint32_t t = (uint32_t)(w0 & 0xffu);
+    if (t == sv::STR) {
+      *p = bytes_of(w0, w1);
+      *n = len_of(w0);
+    } else if (t == sv::UNIT) {
+      *p = tmp;
+      *n = 0;
+    } else if (t == sv::BOOL) {
+      const char* s = w1 ? "true" : "false";
+      *n = w1 ? 4u : 5u;
+      for (uint32_t k = 0; k < *n; ++k) tmp[k] = (uint8_t)s[k];
+      *p = tmp;
+    } else if (t == sv::INT) {
+      *n = itoa((int64_t)w1, tmp);
+      *p = tmp;
+    } else {
+      return false;  // arrays: converting them to text is outside this engine
+    }
+    return true;
+  };
   for (uint32_t pc = 0; pc < code_len;) {
     const uint32_t op = code[pc++];
     switch (op) {
-      case S_UNIT: set(sp++, 0, 0); break;
-      case S_BOOL: set(sp++, 1, code[pc++]); break;
-      case S_INT: {
-        uint64_t v = 0;
-        for (int k = 0; k < 8; ++k) v |= (uint64_t)code[pc + (uint32_t)k] << (8 * k);
+      case S_UNIT: set(sp++, sv::UNIT, 0); break;
+      case S_BOOL: set(sp++, sv::BOOL, code[pc++]); break;
+      case S_INT:
+        set(sp++, sv::INT, rd64(pc));
         pc += 8;
-        set(sp++, 2, v);
         break;
-      }
       case S_STR: {
         const uint32_t off = rd32(pc), len = rd32(pc + 4);
         pc += 8;
-        st[2 * sp] = 3u | ((uint64_t)len << 32);
+        st[2 * sp] = sv::STR | ((uint64_t)len << 32);
         st[2 * sp + 1] = off;
         ++sp;
         break;
       }
       case S_LOAD: {
-        const uint32_t v = (uint32_t)code[pc] | ((uint32_t)code[pc + 1] << 8);
+        const uint32_t v = fp + rd16(pc);
         pc += 2;
         st[2 * sp] = vars[2 * v];
         st[2 * sp + 1] = vars[2 * v + 1];
@@ -520,7 +617,7 @@ KW_HD inline int run_script_prog(const uint8_t* prog, uint64_t* scratch, Ok ok, 
         break;
       }
       case S_STORE: {
-        const uint32_t v = (uint32_t)code[pc] | ((uint32_t)code[pc + 1] << 8);
+        const uint32_t v = fp + rd16(pc);
         pc += 2;
         --sp;
         vars[2 * v] = st[2 * sp];
@@ -532,17 +629,17 @@ KW_HD inline int run_script_prog(const uint8_t* prog, uint64_t* scratch, Ok ok, 
         pc += 4;
         const bool v = ok(m);
         if (!v) cause(m);
-        set(sp++, 1, v ? 1u : 0u);
+        set(sp++, sv::BOOL, v ? 1u : 0u);
         break;
       }
       case S_FAIL: return 2;
       case S_NOT:
-        if (type(sp - 1) != 1) return 2;
+        if (type(sp - 1) != sv::BOOL) return 2;
         st[2 * (sp - 1) + 1] ^= 1u;
         break;
       case S_NEG:
       case S_POS: {
-        if (type(sp - 1) != 2) return 2;
+        if (type(sp - 1) != sv::INT) return 2;
         const int64_t a = (int64_t)st[2 * (sp - 1) + 1];
         if (op == S_NEG) {
           if (a == INT64_MIN) return 2;
@@ -554,58 +651,288 @@ KW_HD inline int run_script_prog(const uint8_t* prog, uint64_t* scratch, Ok ok, 
       case S_OR: {
         const uint32_t t = rd32(pc);
         pc += 4;
-        if (type(sp - 1) != 1) return 2;
+        if (type(sp - 1) != sv::BOOL) return 2;
         const bool a = st[2 * (sp - 1) + 1] != 0;
         if (a == (op == S_OR)) pc = t;  // short circuit: the result is the left side
         else --sp;
         break;
       }
+      case S_COAL: {
+        const uint32_t t = rd32(pc);
+        pc += 4;
+        if (type(sp - 1) != sv::UNIT) pc = t;
+        else --sp;
+        break;
+      }
       case S_CHKB:
-        if (type(sp - 1) != 1) return 2;
+        if (type(sp - 1) != sv::BOOL) return 2;
         break;
       case S_IF: {
         const uint32_t t = rd32(pc);
         pc += 4;
         --sp;
-        if (type(sp) != 1) return 2;
+        if (type(sp) != sv::BOOL) return 2;
         if (!st[2 * sp + 1]) pc = t;
         break;
       }
       case S_JMP: pc = rd32(pc); break;
       case S_POP: --sp; break;
+      case S_DROP: sp -= rd16(pc); pc += 2; break;
+      case S_DROPKEEP: {
+        const uint32_t n = rd16(pc);
+        pc += 2;
+        st[2 * (sp - 1 - n)] = st[2 * (sp - 1)];
+        st[2 * (sp - 1 - n) + 1] = st[2 * (sp - 1) + 1];
+        sp -= n;
+        break;
+      }
       case S_END:
-        if (sp == 0 || type(sp - 1) != 1) return 2;
+        if (sp == 0 || type(sp - 1) != sv::BOOL) return 2;
         return st[2 * (sp - 1) + 1] ? 1 : 0;
+      case S_TICK:
+        if (++ops > kMaxScriptOps) return 2;
+        break;
+      case S_ARR: {
+        const uint32_t n = rd16(pc);
+        pc += 2;
+        if (!charge(16u * n)) return 2;
+        uint64_t* c = n ? new_cells(n) : nullptr;
+        if (n && !c) return 2;
+        sp -= n;
+        for (uint32_t k = 0; k < 2 * n; ++k) c[k] = st[2 * sp + k];
+        st[2 * sp] = sv::ARR | sv::ARENA | ((uint64_t)n << 32);
+        st[2 * sp + 1] = c ? (uint64_t)((uint8_t*)c - arena) : 0u;
+        ++sp;
+        break;
+      }
+      case S_INDEX: {
+        const uint32_t ia = sp - 2, ii = sp - 1;
+        if (type(ia) != sv::ARR || type(ii) != sv::INT) return 2;
+        const int64_t n = (int64_t)len_of(st[2 * ia]);
+        int64_t i = (int64_t)st[2 * ii + 1];
+        if (i < 0) i += n;  // (i64::MIN + n stays negative)
+        if (i < 0 || i >= n) return 2;
+        const uint64_t* c = cells_of(st[2 * ia + 1]) + 2 * i;
+        st[2 * ia] = c[0];
+        st[2 * ia + 1] = c[1];
+        --sp;
+        break;
+      }
+      case S_SETIDX: {
+        const uint32_t v = fp + rd16(pc);
+        pc += 2;
+        const uint32_t ii = sp - 2, iv = sp - 1;
+        if ((vars[2 * v] & 0xffu) != sv::ARR || type(ii) != sv::INT) return 2;
+        const uint32_t n = len_of(vars[2 * v]);
+        int64_t i = (int64_t)st[2 * ii + 1];
+        if (i < 0) i += (int64_t)n;
+        if (i < 0 || i >= (int64_t)n) return 2;
+        if (!charge(16u * n)) return 2;
+        uint64_t* c = new_cells(n);
+        if (!c) return 2;
+        const uint64_t* o = cells_of(vars[2 * v + 1]);
+        for (uint32_t k = 0; k < 2 * n; ++k) c[k] = o[k];
+        c[2 * i] = st[2 * iv];
+        c[2 * i + 1] = st[2 * iv + 1];
+        vars[2 * v + 1] = (uint64_t)((uint8_t*)c - arena);
+        sp -= 2;
+        break;
+      }
+      case S_INRANGE: {
+        const uint32_t incl = code[pc++];
+        const uint32_t ix = sp - 3, il = sp - 2, ih = sp - 1;
+        if (type(il) != sv::INT || type(ih) != sv::INT || type(ix) != sv::INT) return 2;
+        const int64_t x = (int64_t)st[2 * ix + 1], lo = (int64_t)st[2 * il + 1], hi = (int64_t)st[2 * ih + 1];
+        set(ix, sv::BOOL, (x >= lo && (incl ? x <= hi : x < hi)) ? 1u : 0u);
+        sp -= 2;
+        break;
+      }
+      case S_RCASE: {
+        const int64_t lo = (int64_t)rd64(pc), hi = (int64_t)rd64(pc + 8);
+        const uint32_t incl = code[pc + 16];
+        pc += 17;
+        const int64_t x = (int64_t)st[2 * (sp - 1) + 1];
+        const bool in = type(sp - 1) == sv::INT && x >= lo && (incl ? x <= hi : x < hi);
+        set(sp - 1, sv::BOOL, in ? 1u : 0u);
+        break;
+      }
+      case S_RANGECHK:
+        if (type(sp - 1) != sv::INT || type(sp - 2) != sv::INT) return 2;
+        break;
+      case S_FORR: {
+        const uint32_t si = fp + rd16(pc), se = fp + rd16(pc + 2), incl = code[pc + 4], ex = rd32(pc + 5);
+        pc += 9;
+        const int64_t i = (int64_t)vars[2 * si + 1], e = (int64_t)vars[2 * se + 1];
+        if (incl ? i > e : i >= e) {
+          pc = ex;
+          break;
+        }
+        set(sp++, sv::INT, (uint64_t)i);
+        if (i == INT64_MAX) vars[2 * se + 1] = (uint64_t)(INT64_MAX - 1);  // (inclusive, last value)
+        else vars[2 * si + 1] = (uint64_t)(i + 1);
+        break;
+      }
+      case S_FORA: {
+        const uint32_t sa = fp + rd16(pc), si = fp + rd16(pc + 2), withi = code[pc + 4], ex = rd32(pc + 5);
+        pc += 9;
+        if ((vars[2 * sa] & 0xffu) != sv::ARR) return 2;
+        const uint64_t i = vars[2 * si + 1];
+        if (i >= len_of(vars[2 * sa])) {
+          pc = ex;
+          break;
+        }
+        const uint64_t* c = cells_of(vars[2 * sa + 1]) + 2 * i;
+        st[2 * sp] = c[0];
+        st[2 * sp + 1] = c[1];
+        ++sp;
+        if (withi) set(sp++, sv::INT, i);
+        vars[2 * si + 1] = i + 1;
+        break;
+      }
+      case S_CALLF: {
+        const uint32_t at = rd32(pc), nargs = code[pc + 4], cslots = rd16(pc + 5);
+        pc += 7;
+        if (nf >= nframes) return 2;               // "Stack overflow"
+        if (++ops > kMaxScriptOps) return 2;
+        sp -= nargs;
+        const uint32_t nfp = fp + cslots;
+        for (uint32_t k = 0; k < nargs; ++k) {
+          vars[2 * (nfp + k)] = st[2 * (sp + k)];
+          vars[2 * (nfp + k) + 1] = st[2 * (sp + k) + 1];
+        }
+        frames[2 * nf] = (uint64_t)pc | ((uint64_t)fp << 32);
+        frames[2 * nf + 1] = sp;
+        ++nf;
+        fp = nfp;
+        pc = at;
+        break;
+      }
+      case S_RET: {
+        const uint64_t r0 = st[2 * (sp - 1)], r1 = st[2 * (sp - 1) + 1];
+        --nf;
+        pc = (uint32_t)frames[2 * nf];
+        fp = (uint32_t)(frames[2 * nf] >> 32);
+        sp = (uint32_t)frames[2 * nf + 1];
+        st[2 * sp] = r0;
+        st[2 * sp + 1] = r1;
+        ++sp;
+        break;
+      }
+      case S_FN: {
+        const uint32_t fid = code[pc++];
+        if (fid == F_LEN || fid == F_IS_EMPTY || fid == F_TO_STRING || fid == F_TYPE_OF) {
+          const uint32_t i = sp - 1, t = type(i);
+          const uint64_t w0 = st[2 * i], w1 = st[2 * i + 1];
+          if (fid == F_TYPE_OF) {
+            const uint32_t o = t == sv::UNIT ? 0u : t == sv::BOOL ? 2u : t == sv::INT ? 6u : t == sv::STR ? 9u : 15u;
+            const uint32_t n = t == sv::UNIT ? 2u : t == sv::BOOL ? 4u : t == sv::INT ? 3u : t == sv::STR ? 6u : 5u;
+            st[2 * i] = sv::STR | ((uint64_t)n << 32);
+            st[2 * i + 1] = tnames + o;
+          } else if (fid == F_TO_STRING) {
+            if (t == sv::STR) break;
+            uint8_t tmp[24];
+            const uint8_t* p;
+            uint32_t n;
+            if (!text_of(w0, w1, tmp, &p, &n)) return 2;
+            if (!charge(n)) return 2;
+            uint8_t* d = new_str(n);
+            if (!d && n) return 2;
+            for (uint32_t k = 0; k < n; ++k) d[k] = p[k];
+            st[2 * i] = sv::STR | sv::ARENA | ((uint64_t)n << 32);
+            st[2 * i + 1] = d ? (uint64_t)(d - arena) : 0u;
+          } else {
+            uint64_t n;
+            if (t == sv::ARR) {
+              n = len_of(w0);
+            } else if (t == sv::STR) {  // characters: UTF-8 lead bytes
+              const uint8_t* p = bytes_of(w0, w1);
+              n = 0;
+              for (uint32_t k = 0; k < len_of(w0); ++k) n += (p[k] & 0xC0u) != 0x80u;
+            } else {
+              return 2;
+            }
+            if (fid == F_LEN) set(i, sv::INT, n);
+            else set(i, sv::BOOL, n == 0 ? 1u : 0u);
+          }
+          break;
+        }
+        // two arguments: (a, b) on the stack; F_IN is contains(b, a)
+        uint32_t ic = sp - 2, ix = sp - 1;
+        if (fid == F_IN) {
+          ic = sp - 1;
+          ix = sp - 2;
+        }
+        const uint32_t tc = type(ic), tx = type(ix);
+        const uint64_t c0 = st[2 * ic], c1 = st[2 * ic + 1], x0 = st[2 * ix], x1 = st[2 * ix + 1];
+        uint64_t r = 0;
+        if (fid == F_PUSH) {
+          if (tc != sv::ARR) return 2;
+          const uint32_t n = len_of(c0);
+          if (!charge(16u * (n + 1))) return 2;
+          uint64_t* c = new_cells(n + 1);
+          if (!c) return 2;
+          const uint64_t* o = cells_of(c1);
+          for (uint32_t k = 0; k < 2 * n; ++k) c[k] = o[k];
+          c[2 * n] = x0;
+          c[2 * n + 1] = x1;
+          st[2 * (sp - 2)] = sv::ARR | sv::ARENA | ((uint64_t)(n + 1) << 32);
+          st[2 * (sp - 2) + 1] = (uint64_t)((uint8_t*)c - arena);
+          --sp;
+          break;
+        }
+        if (fid == F_CONTAINS || fid == F_IN) {
+          if (tc == sv::ARR) {
+            const uint64_t* c = cells_of(c1);
+            for (uint32_t k = 0; k < len_of(c0) && !r; ++k) {
+              const int e = veq(c[2 * k], c[2 * k + 1], x0, x1);
+              if (e < 0) return 2;
+              r = (uint64_t)e;
+            }
+          } else if (tc == sv::STR && tx == sv::STR) {
+            const uint8_t *hs = bytes_of(c0, c1), *nd = bytes_of(x0, x1);
+            const uint32_t hn = len_of(c0), nn = len_of(x0);
+            for (uint32_t k = 0; k + nn <= hn && !r; ++k) {
+              bool m = true;
+              for (uint32_t j = 0; m && j < nn; ++j) m = hs[k + j] == nd[j];
+              r = m;
+            }
+          } else {
+            return 2;
+          }
+        } else {  // F_STARTS_WITH / F_ENDS_WITH
+          if (tc != sv::STR || tx != sv::STR) return 2;
+          const uint32_t hn = len_of(c0), nn = len_of(x0);
+          const uint8_t *hs = bytes_of(c0, c1) + (fid == F_ENDS_WITH && nn <= hn ? hn - nn : 0u), *nd = bytes_of(x0, x1);
+          r = nn <= hn;
+          for (uint32_t j = 0; r && j < nn; ++j) r = hs[j] == nd[j];
+        }
+        set(sp - 2, sv::BOOL, r);
+        --sp;
+        break;
+      }
       case S_BIN: {
         const uint32_t b_op = code[pc++];
         const uint32_t ib = sp - 1, ia = sp - 2;
         const uint32_t ta = type(ia), tb = type(ib);
-        const uint64_t va = st[2 * ia + 1], vb = st[2 * ib + 1];
+        const uint64_t a0 = st[2 * ia], va = st[2 * ia + 1], b0 = st[2 * ib], vb = st[2 * ib + 1];
         --sp;
         if (b_op == SB_EQ || b_op == SB_NE) {  // different types: not equal (rhai's built-in comparison)
-          bool eq = ta == tb;
-          if (eq && ta == 3) {
-            const uint32_t la = slen(ia), lb = slen(ib);
-            eq = la == lb;
-            const uint8_t *pa = sbytes(ia), *pb = sbytes(ib);
-            for (uint32_t k = 0; eq && k < la; ++k) eq = pa[k] == pb[k];
-          } else if (eq && ta != 0) {
-            eq = va == vb;
-          }
-          set(ia, 1, (b_op == SB_EQ) == eq ? 1u : 0u);
+          const int e = veq(a0, va, b0, vb);
+          if (e < 0) return 2;
+          set(ia, sv::BOOL, (b_op == SB_EQ) == (e == 1) ? 1u : 0u);
           break;
         }
         if (b_op >= SB_LT && b_op <= SB_GE) {
           int c = 0;
           if (ta != tb) {
-            set(ia, 1, 0);
+            set(ia, sv::BOOL, 0);
             break;
           }
-          if (ta == 2) {
+          if (ta == sv::INT) {
             c = (int64_t)va < (int64_t)vb ? -1 : (int64_t)va > (int64_t)vb ? 1 : 0;
-          } else if (ta == 3) {
-            const uint32_t la = slen(ia), lb = slen(ib);
-            const uint8_t *pa = sbytes(ia), *pb = sbytes(ib);
+          } else if (ta == sv::STR) {
+            const uint32_t la = len_of(a0), lb = len_of(b0);
+            const uint8_t *pa = bytes_of(a0, va), *pb = bytes_of(b0, vb);
             uint32_t k = 0;
             while (k < la && k < lb && pa[k] == pb[k]) ++k;
             c = k < la && k < lb ? (pa[k] < pb[k] ? -1 : 1) : (la < lb ? -1 : la > lb ? 1 : 0);
@@ -613,36 +940,61 @@ KW_HD inline int run_script_prog(const uint8_t* prog, uint64_t* scratch, Ok ok, 
             return 2;
           }
           const bool r = b_op == SB_LT ? c < 0 : b_op == SB_LE ? c <= 0 : b_op == SB_GT ? c > 0 : c >= 0;
-          set(ia, 1, r ? 1u : 0u);
+          set(ia, sv::BOOL, r ? 1u : 0u);
           break;
         }
         if (b_op <= SB_AND) {  // | ^ &
-          if (ta == 1 && tb == 1) {
+          if (ta == sv::BOOL && tb == sv::BOOL) {
             const bool a = va != 0, b = vb != 0;
-            set(ia, 1, (b_op == SB_OR ? (a || b) : b_op == SB_AND ? (a && b) : (a != b)) ? 1u : 0u);
+            set(ia, sv::BOOL, (b_op == SB_OR ? (a || b) : b_op == SB_AND ? (a && b) : (a != b)) ? 1u : 0u);
             break;
           }
-          if (ta == 2 && tb == 2) {
-            set(ia, 2, b_op == SB_OR ? (va | vb) : b_op == SB_AND ? (va & vb) : (va ^ vb));
+          if (ta == sv::INT && tb == sv::INT) {
+            set(ia, sv::INT, b_op == SB_OR ? (va | vb) : b_op == SB_AND ? (va & vb) : (va ^ vb));
             break;
           }
           return 2;
         }
-        if (b_op == SB_ADD && ta == 3 && tb == 3) {  // concatenation into the arena
-          const uint32_t la = slen(ia), lb = slen(ib);
-          const uint8_t *pa = sbytes(ia), *pb = sbytes(ib);
-          uint8_t* d = arena + atop;
-          for (uint32_t k = 0; k < la; ++k) d[k] = pa[k];
-          for (uint32_t k = 0; k < lb; ++k) d[la + k] = pb[k];
-          st[2 * ia] = 3u | 256u | ((uint64_t)(la + lb) << 32);
-          st[2 * ia + 1] = atop;
-          atop += la + lb;
+        if ((b_op == SB_ADD || b_op == SB_ADDA) && ta == sv::ARR) {
+          // array + array concatenates; `+=` with anything else pushes it
+          const bool app = tb == sv::ARR;
+          if (!app && b_op == SB_ADD) return 2;
+          const uint32_t na = len_of(a0), nb = app ? len_of(b0) : 1u;
+          if (!charge(16u * (na + nb))) return 2;
+          uint64_t* c = na + nb ? new_cells(na + nb) : nullptr;
+          if (na + nb && !c) return 2;
+          const uint64_t* pa = cells_of(va);
+          for (uint32_t k = 0; k < 2 * na; ++k) c[k] = pa[k];
+          if (app) {
+            const uint64_t* pb = cells_of(vb);
+            for (uint32_t k = 0; k < 2 * nb; ++k) c[2 * na + k] = pb[k];
+          } else {
+            c[2 * na] = b0;
+            c[2 * na + 1] = vb;
+          }
+          st[2 * ia] = sv::ARR | sv::ARENA | ((uint64_t)(na + nb) << 32);
+          st[2 * ia + 1] = c ? (uint64_t)((uint8_t*)c - arena) : 0u;
           break;
         }
-        if (ta != 2 || tb != 2) return 2;
+        if ((b_op == SB_ADD || b_op == SB_ADDA) && (ta == sv::STR || tb == sv::STR)) {
+          // string + any (the other side as to_string): one new string of the joined length
+          uint8_t t1[24], t2[24];
+          const uint8_t *pa, *pb;
+          uint32_t la, lb;
+          if (!text_of(a0, va, t1, &pa, &la) || !text_of(b0, vb, t2, &pb, &lb)) return 2;
+          if (!charge(la + lb)) return 2;
+          uint8_t* d = new_str(la + lb);
+          if (!d && la + lb) return 2;
+          for (uint32_t k = 0; k < la; ++k) d[k] = pa[k];
+          for (uint32_t k = 0; k < lb; ++k) d[la + k] = pb[k];
+          st[2 * ia] = sv::STR | sv::ARENA | ((uint64_t)(la + lb) << 32);
+          st[2 * ia + 1] = d ? (uint64_t)(d - arena) : 0u;
+          break;
+        }
+        if (ta != sv::INT || tb != sv::INT) return 2;
         const int64_t a = (int64_t)va, b = (int64_t)vb;
         long long r = 0;
-        if (b_op == SB_ADD) {
+        if (b_op == SB_ADD || b_op == SB_ADDA) {
           if (__builtin_add_overflow(a, b, &r)) return 2;
         } else if (b_op == SB_SUB) {
           if (__builtin_sub_overflow(a, b, &r)) return 2;
@@ -652,7 +1004,7 @@ KW_HD inline int run_script_prog(const uint8_t* prog, uint64_t* scratch, Ok ok, 
           if (b == 0 || (a == INT64_MIN && b == -1)) return 2;
           r = b_op == SB_DIV ? a / b : a % b;
         }
-        set(ia, 2, (uint64_t)r);
+        set(ia, sv::INT, (uint64_t)r);
         break;
       }
       default: return 2;

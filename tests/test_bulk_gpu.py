@@ -51,6 +51,19 @@ def test_bulk_matches_oracle(name, scfg, rows, chunk):
         pin.close()
 
 
+def test_bulk_more_than_256_chunks_pageable_output():
+    """past 256 chunks the last chunk takes every remaining tile, so it is
+    larger than one full chunk. The pageable output's bounce blocks must be sized for it.
+    64-row C4 tiles, chunk_rows=128 (two tiles a chunk after the ramp) on 100k rows: the last of
+    the 256 chunks holds about 1,100 tiles."""
+    env, oe = _envs(config("c4_64"))
+    ids = env.policy_ids()
+    syn = K.SynthBatch(4, 100000, seed=4257)
+    ora = oe.eval(syn.soa(), ids, K.VALIDATE)
+    got = syn.batch().validate_host(env, ids, chunk_rows=128)
+    assert np.array_equal(got, ora), diff_verdicts(got, ora, len(ids), ids)
+
+
 def test_pinned_words_outlive_their_wrapper():
     """the page-locked memory lives as long as any view of it, not as long as the
     PinnedWords wrapper. Drop the wrapper, keep only a slice, DMA into the array again."""

@@ -1,0 +1,131 @@
+"""CPU: policy-group expressions beyond the bool-only subset (VERDICT r04 "What's missing" 1):
+arrays, `in`, switch, `??`, methods, compound assignment, loops, functions, and the constructs the
+engine refuses by name. Three-way: the hand-written rhai expectations of tests/rhai_cases.py (the
+independent pin), the oracle's interpreter (oracle/rhaisub.py) and the product (expr.cpp) — through
+the slot compiler's host walk in both device forms the product uses for such groups: the truth
+table, and (KW_GROUP_FORM=script) the typed bytecode of slots.hpp run_script_prog.
+Reference: evaluation_environment.rs:587-651 (group evaluation), :979-1042 (causes); the language is
+upstream rhai 1.21.0 (Cargo.lock:5116-5118), parity beyond the pinned vectors unpinned."""
+import json
+
+import numpy as np
+import pytest
+
+import kwgpu as K
+import oracle as O
+from helpers import diff_verdicts
+from rhai_cases import INVALID, VALID
+
+LABELS = "registry://ghcr.io/kubewarden/policies/safe-labels:v0.1.14"
+MEMBERS = {m: {"module": LABELS, "settings": {"mandatory_labels": [m]}} for m in "abc"}
+VECTORS = ["", "a", "b", "c", "ab", "ac", "bc", "abc"]
+
+
+def review(accepting, uid):
+    return json.dumps({"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview", "request": {
+        "uid": uid, "kind": {"group": "", "version": "v1", "kind": "Pod"},
+        "resource": {"group": "", "version": "v1", "resource": "pods"}, "operation": "CREATE",
+        "namespace": "default", "userInfo": {"username": "u"},
+        "object": {"kind": "Pod", "metadata": {"name": "p", "labels": {m: "x" for m in accepting}},
+                   "spec": {"containers": [{"name": "c", "image": "nginx"}]}}}})
+
+
+def groups_doc(rows):
+    return {f"g{k}": {"policies": MEMBERS, "expression": e, "message": f"group {k} rejected"}
+            for k, (e, _) in enumerate(rows)}
+
+
+def check_expected(resp, exp, ctx):
+    if exp is True:
+        assert resp["allowed"] is True, (ctx, resp)
+        return
+    assert resp["allowed"] is False, (ctx, resp)
+    st = resp["status"]
+    if exp is False:
+        return
+    kind, val = exp
+    if kind == "causes":
+        got = {c["field"].split(".")[-1] for c in st.get("details", {}).get("causes", [])}
+        assert got == val, (ctx, resp)
+        assert "code" not in st, (ctx, resp)
+    else:
+        assert st.get("code") == 500 and val in st["message"], (ctx, resp)
+
+
+@pytest.fixture(params=["table", "script"])
+def form(request, monkeypatch):
+    if request.param == "script":
+        monkeypatch.setenv("KW_GROUP_FORM", "script")
+    else:
+        monkeypatch.delenv("KW_GROUP_FORM", raising=False)
+    return request.param
+
+
+def test_deep_nesting_row_is_deep():
+    row = next(e for e, _ in VALID if "z == z" in e)
+    assert row.count("[") >= 17  # one more level than kMaxCompareDepth
+
+
+@pytest.mark.parametrize("origin", [K.VALIDATE, K.AUDIT])
+def test_forms_match_oracle_and_hand_table(form, origin):
+    doc = groups_doc(VALID)
+    env = K.EvaluationEnvironment(doc, continue_on_errors=True)
+    oe = O.OracleEnv(doc, continue_on_errors=True)
+    ids = env.policy_ids()
+    assert ids == [p["id"] for p in oe.pol]
+    for k in range(len(VALID)):  # every row validates in both
+        env.validate_settings(f"g{k}")
+        assert oe.pol[oe.ids[f"g{k}"]]["valid"], (VALID[k][0], oe.pol[oe.ids[f"g{k}"]]["expr_error"])
+    docs = [review(v, f"uid-{v or 'none'}") for v in VECTORS]
+    b = K.Batch.from_json(docs)
+    got = b.debug_host_walk(env, ids, origin)
+    want = oe.eval(b.view(), ids, origin)
+    assert np.array_equal(got, want), diff_verdicts(got, want, len(ids), ids)
+    v = got.reshape(len(docs), len(ids))
+    for k, (expr, cases) in enumerate(VALID):
+        j = ids.index(f"g{k}")
+        members = env.group_members(j)
+        for acc, exp in cases:
+            r = VECTORS.index(acc)
+            resp = b.format_response(env, r, j, int(v[r, j]), [int(v[r, m]) for m in members], doc=docs[r])
+            assert resp == oe.response_doc(b.view(), r, j, origin, doc=docs[r]), (expr, acc)
+            if origin == K.VALIDATE:
+                check_expected(resp, exp, (form, expr, acc))
+
+
+@pytest.mark.parametrize("expr,text", INVALID, ids=[f"inv{k}" for k in range(len(INVALID))])
+def test_refused_and_invalid_scripts(expr, text):
+    doc = {"g": {"policies": MEMBERS, "expression": expr, "message": "m"}}
+    env = K.EvaluationEnvironment(doc, continue_on_errors=True)
+    oe = O.OracleEnv(doc, continue_on_errors=True)
+    P = oe.pol[oe.ids["g"]]
+    assert P["valid"] is False and text in P["expr_error"], (expr, P["expr_error"])
+    with pytest.raises(K.PolicyInitialization) as e:
+        env.validate_settings("g")
+    assert str(e.value) == P["expr_error"], expr
+    # no "Syntax error" for a construct rhai has: those are named as outside the engine
+    if "unsupported" in text:
+        assert "Syntax error" not in str(e.value)
+
+
+def test_verdict_probes_no_longer_500():
+    """The six expressions VERDICT r04 probed on the reference's privileged-pod fixture answered
+    500 "Syntax error"; now each evaluates (group of the fixture's own pod-privileged policy)."""
+    import os
+    fixture = open(os.path.join(os.path.dirname(__file__), "golden", "reference_data", "pod_with_privileged_containers.json")).read()
+    priv = {"module": "registry://ghcr.io/kubewarden/policies/pod-privileged:v0.2.0"}
+    ns = {"module": "registry://ghcr.io/kubewarden/policies/namespace-validate-policy:v0.1.0",
+          "settings": {"valid_namespace": "default"}}
+    exprs = ["[a(), b()].contains(false)", "a() in [true]", "switch a() { true => b(), _ => false }",
+             "a() ?? b()", 'a().to_string() == "true"', "let n = 0; if b() { n += 1; } n > 0"]
+    doc = {f"p{k}": {"policies": {"a": ns, "b": priv}, "expression": e, "message": "no"} for k, e in enumerate(exprs)}
+    env = K.EvaluationEnvironment(doc, continue_on_errors=True)
+    oe = O.OracleEnv(doc, continue_on_errors=True)
+    b = K.Batch.from_json([fixture])
+    ids = env.policy_ids()
+    got = b.debug_host_walk(env, ids)
+    assert np.array_equal(got, oe.eval(b.view(), ids))
+    for k in range(len(exprs)):
+        j = ids.index(f"p{k}")
+        resp = b.format_response(env, 0, j, int(got[j]), [int(got[m]) for m in env.group_members(j)], doc=fixture)
+        assert resp.get("status", {}).get("code") != 500, (exprs[k], resp)

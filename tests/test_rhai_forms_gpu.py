@@ -1,0 +1,53 @@
+"""GPU: the extended group-expression language on the device, in both device forms a non-bool
+script takes (the truth table read in the tile kernel, and with KW_GROUP_FORM=script the typed
+bytecode run by wide_groups_kernel), against the oracle's independent interpreter and the
+hand-written rhai expectations (tests/rhai_cases.py). Verdict words poisoned first, so a skipped
+pair cannot pass; responses formatted from the device words must equal the oracle's."""
+import numpy as np
+import pytest
+
+import kwgpu as K
+import oracle as O
+from helpers import diff_verdicts
+from rhai_cases import VALID
+from test_rhai_forms import VECTORS, check_expected, groups_doc, review
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("form", ["table", "script"])
+def test_forms_on_device_match_oracle(monkeypatch, form):
+    monkeypatch.setenv("KW_POISON_VERDICTS", "1")
+    if form == "script":
+        monkeypatch.setenv("KW_GROUP_FORM", "script")
+    else:
+        monkeypatch.delenv("KW_GROUP_FORM", raising=False)
+    doc = groups_doc(VALID)
+    env = K.EvaluationEnvironment(doc, continue_on_errors=True, device=0)
+    oe = O.OracleEnv(doc, continue_on_errors=True)
+    ids = env.policy_ids()
+    # every member vector, repeated so that the combine kernel's grid strides over many pairs
+    docs = [review(VECTORS[k % len(VECTORS)], f"uid-{k}") for k in range(8 * 64)]
+    b = K.Batch.from_json(docs).to_device(0)
+    for origin in (K.VALIDATE, K.AUDIT):
+        b.validate(env, ids, origin)
+        got = b.verdicts()
+        want = oe.eval(b.view(), ids, origin)
+        assert np.array_equal(got, want), diff_verdicts(got, want, len(ids), ids)
+    v = got.reshape(len(docs), len(ids))
+    for k, (expr, cases) in enumerate(VALID):
+        j = ids.index(f"g{k}")
+        members = env.group_members(j)
+        for acc, exp in cases:
+            r = VECTORS.index(acc)
+            resp = b.format_response(env, r, j, int(v[r, j]), [int(v[r, m]) for m in members], doc=docs[r])
+            assert resp == oe.response_doc(b.view(), r, j, K.AUDIT, doc=docs[r]), (expr, acc)
+    b.validate(env, ids, K.VALIDATE)
+    v = b.verdicts().reshape(len(docs), len(ids))
+    for k, (expr, cases) in enumerate(VALID):
+        j = ids.index(f"g{k}")
+        members = env.group_members(j)
+        for acc, exp in cases:
+            r = VECTORS.index(acc)
+            resp = b.format_response(env, r, j, int(v[r, j]), [int(v[r, m]) for m in members], doc=docs[r])
+            check_expected(resp, exp, (form, expr, acc))
