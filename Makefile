@@ -50,7 +50,7 @@ $(PKG)/kwload: $(SRC)/kwload.cpp $(PKG)/libkwsynth.so
 $(PKG)/libkwsynth.so: $(SRC)/synth.cpp include/kwgpu.h
 	$(CXX) -O3 -std=c++17 -fPIC -shared -Wall -o $@ $<
 
-oracle/build/libkworacle.so: oracle/kworacle.c oracle/kwregex.c oracle/kworacle.h include/kwgpu.h
+oracle/build/libkworacle.so: oracle/kworacle.c oracle/kwregex.c oracle/kworacle.h oracle/unicode_data.h include/kwgpu.h
 	@mkdir -p oracle/build
 	$(CC) -O2 -std=c11 -fPIC -shared -Wall -Wextra -o $@ oracle/kworacle.c oracle/kwregex.c -lpthread
 

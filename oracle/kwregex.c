@@ -4,8 +4,9 @@
  *
  * Restates `Regex::new(p)?.is_match(s)` of the Rust `regex` crate for the label constraints of the
  * safe-labels family (constrained_labels; upstream policy absent),
- * in the dialect DESIGN.md §2 fixes: Rust syntax, matching over Unicode scalar values, ASCII
- * `\d \w \s`, `\b` and case folding, `\p{..}` / back-references / look-around / the R flag refused.
+ * in the dialect DESIGN.md §2 fixes: Rust syntax, matching over Unicode scalar values, Rust's
+ * Unicode `\d \w \s`, word boundaries and simple case folding (ASCII ones under `(?-u)`; tables:
+ * oracle/unicode_data.h), `\p{..}` / back-references / look-around / the R flag refused.
  *
  * Independent of the product's automaton compiler (policy-server_amd/csrc/automaton.cpp, a byte-level
  * DFA built by subset construction): this file parses the pattern itself into a tree over code
@@ -19,6 +20,7 @@
 #include <string.h>
 
 #include "kworacle.h"
+#include "unicode_data.h"
 
 /* ------------------------------------------------------------------ code point sets */
 typedef struct {
@@ -120,7 +122,7 @@ static cset cs_minus(const cset *a, const cset *b) {
   return o;
 }
 /* ASCII simple case folding: add the other case of every ASCII letter in the set */
-static void cs_casefold(cset *s) {
+static void cs_casefold_ascii(cset *s) {
   int n = s->n;
   for (int k = 0; k < n; ++k) {
     for (uint32_t c = s->r[k].lo; c <= s->r[k].hi && c <= 'z'; ++c) {
@@ -131,6 +133,46 @@ static void cs_casefold(cset *s) {
   cs_canon(s);
 }
 static int cs_beyond_ascii(const cset *s) { return s->n > 0 && s->r[s->n - 1].hi > 0x7F; }
+
+static int cmp_u32(const void *a, const void *b) {
+  uint32_t x = *(const uint32_t *)a, y = *(const uint32_t *)b;
+  return x < y ? -1 : x > y;
+}
+/* Unicode simple case folding: the set of folds its members have, then every code point whose
+   fold is one of them (orc_uni_fold: (code point, fold) pairs of the non-trivial orbits) */
+static void cs_casefold_unicode(cset *s) {
+  uint32_t *keys = (uint32_t *)malloc(ORC_UNI_FOLD_N * sizeof(uint32_t));
+  size_t nk = 0;
+  for (size_t k = 0; k < ORC_UNI_FOLD_N; ++k)
+    if (cs_has(s, orc_uni_fold[2 * k])) keys[nk++] = orc_uni_fold[2 * k + 1];
+  qsort(keys, nk, sizeof(uint32_t), cmp_u32);
+  for (size_t k = 0; k < ORC_UNI_FOLD_N; ++k) {
+    uint32_t f = orc_uni_fold[2 * k + 1];
+    if (nk && bsearch(&f, keys, nk, sizeof(uint32_t), cmp_u32)) cs_push(s, orc_uni_fold[2 * k], orc_uni_fold[2 * k]);
+  }
+  free(keys);
+  cs_canon(s);
+}
+static void cs_casefold_mode(cset *s, int unicode) {
+  if (unicode) cs_casefold_unicode(s);
+  else cs_casefold_ascii(s);
+}
+#define cs_casefold(s) cs_casefold_mode((s), P->fl.u)
+/* the Unicode classes of \d \w \s (Rust regex: Nd; Alphabetic + M + Nd + Pc + Join_Control;
+   White_Space) */
+static void uni_class(char which, cset *out) {
+  memset(out, 0, sizeof(*out));
+  if (which == 's') {
+    static const uint32_t ws[] = {9, 13, 0x20, 0x20, 0x85, 0x85, 0xA0, 0xA0, 0x1680, 0x1680, 0x2000, 0x200A,
+                                  0x2028, 0x2029, 0x202F, 0x202F, 0x205F, 0x205F, 0x3000, 0x3000};
+    for (size_t k = 0; k < sizeof(ws) / sizeof(ws[0]); k += 2) cs_push(out, ws[k], ws[k + 1]);
+  } else {
+    const uint32_t *t = which == 'd' ? orc_uni_digit : orc_uni_word;
+    size_t n = which == 'd' ? ORC_UNI_DIGIT_N : ORC_UNI_WORD_N;
+    for (size_t k = 0; k < n; ++k) cs_push(out, t[2 * k], t[2 * k + 1]);
+  }
+  cs_canon(out);
+}
 
 /* the ASCII classes ([:name:], \d \w \s) */
 static int named_class(const char *name, size_t len, cset *out) {
@@ -158,6 +200,7 @@ static int named_class(const char *name, size_t len, cset *out) {
 enum { N_EMPTY, N_SET, N_CAT, N_ALT, N_REP, N_ASSERT };
 enum { A_TEXT_START, A_TEXT_END, A_LINE_START, A_LINE_END, A_WORD, A_NOT_WORD, A_WORD_START, A_WORD_END,
        A_WORD_START_HALF, A_WORD_END_HALF };
+#define A_UNI 0x100 /* a word boundary over Unicode word characters */
 typedef struct {
   int kind;
   cset set;
@@ -311,7 +354,8 @@ static int parse_escape(rparse *P, int in_class, cset *out, int64_t *single, int
   default: break;
   }
   if (cls) {
-    named_class(cls, strlen(cls), out);
+    if (P->fl.u) uni_class(cls[0], out);
+    else named_class(cls, strlen(cls), out);
     if (negate) {
       cset n = cs_complement(out);
       cs_free(out);
@@ -369,6 +413,8 @@ static int parse_escape(rparse *P, int in_class, cset *out, int64_t *single, int
         }
       }
       if (k >= 0) {
+        /* word boundaries in Unicode mode read Unicode word characters */
+        if (P->fl.u && k != A_TEXT_START && k != A_TEXT_END) k |= A_UNI;
         *akind = k;
         return 2;
       }
@@ -859,12 +905,22 @@ void orc_re_free(orc_re *R) {
 }
 
 /* ------------------------------------------------------------------ matching */
-static int is_word_cp(int64_t c) {
-  return c >= 0 && ((c >= '0' && c <= '9') || (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z') || c == '_');
+static int is_word_cp(int64_t c, int unicode) {
+  if (c >= 0 && c < 0x80)
+    return (c >= '0' && c <= '9') || (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z') || c == '_';
+  if (!unicode || c < 0 || c > 0x10FFFF) return 0;
+  size_t lo = 0, hi = ORC_UNI_WORD_N;
+  while (lo < hi) {
+    size_t m = (lo + hi) / 2;
+    if (orc_uni_word[2 * m + 1] < (uint32_t)c) lo = m + 1;
+    else hi = m;
+  }
+  return lo < ORC_UNI_WORD_N && orc_uni_word[2 * lo] <= (uint32_t)c;
 }
 static int assert_holds(int kind, int64_t prev, int64_t next) { /* -1: start / end of the text */
-  int wp = is_word_cp(prev), wn = is_word_cp(next);
-  switch (kind) {
+  int uni = (kind & A_UNI) != 0;
+  int wp = is_word_cp(prev, uni), wn = is_word_cp(next, uni);
+  switch (kind & ~A_UNI) {
   case A_TEXT_START: return prev < 0;
   case A_TEXT_END: return next < 0;
   case A_LINE_START: return prev < 0 || prev == '\n';

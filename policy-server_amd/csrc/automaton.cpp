@@ -9,6 +9,7 @@
 #include <cstring>
 
 #include "kwdev.hpp"
+#include "unicode_data.hpp"
 
 #include <algorithm>
 #include <map>
@@ -38,7 +39,9 @@ struct BSet {
 struct NState {
   std::vector<std::pair<uint32_t, uint32_t>> tr;    // (set id, target)
   std::vector<uint32_t> eps;
-  std::vector<std::pair<uint16_t, uint32_t>> asrt;  // (allowed (prev, next) byte kinds, target)
+  // (allowed (prev, next) kinds: a 16-bit mask, | kAssertUni when the kinds are those of the code
+  // points around the position (Unicode word boundaries), target)
+  std::vector<std::pair<uint32_t, uint32_t>> asrt;
   int acc = -1;
 };
 
@@ -334,6 +337,38 @@ void cs_fold_ascii(CSet* s) {  // close under ASCII case folding
   *s = cs_union(*s, add);
 }
 bool cs_nonascii(const CSet& s) { return !s.empty() && s.back().hi >= 0x80; }
+// close under Unicode simple case folding (every member of a code point's fold orbit)
+void cs_fold_unicode(CSet* s) {
+  CSet add;
+  for (const CRange& r : *s) {
+    const UniFold* b = std::lower_bound(kUniFold, kUniFold + kUniFoldN, r.lo,
+                                        [](const UniFold& f, uint32_t v) { return f.cp < v; });
+    for (const UniFold* f = b; f < kUniFold + kUniFoldN && f->cp <= r.hi; ++f)
+      for (uint32_t c = f->next; c != f->cp;) {
+        add.push_back({c, c});
+        const UniFold* g = std::lower_bound(kUniFold, kUniFold + kUniFoldN, c,
+                                            [](const UniFold& x, uint32_t v) { return x.cp < v; });
+        c = g->next;
+      }
+  }
+  *s = cs_union(*s, add);
+}
+// (?i): Unicode simple case folding in Unicode mode, ASCII folding with `u` off (regex-syntax)
+void cs_fold(CSet* s, bool unicode) {
+  if (unicode) cs_fold_unicode(s);
+  else cs_fold_ascii(s);
+}
+CSet cs_table(const UniRange* t, uint32_t n) {
+  CSet o;
+  for (uint32_t k = 0; k < n; ++k) o.push_back({t[k].lo, t[k].hi});
+  return o;
+}
+// White_Space (PropList.txt), Rust's Unicode \s
+CSet cs_uni_space() {
+  return {{9, 13}, {0x20, 0x20}, {0x85, 0x85}, {0xA0, 0xA0}, {0x1680, 0x1680}, {0x2000, 0x200A},
+          {0x2028, 0x2029}, {0x202F, 0x202F}, {0x205F, 0x205F}, {0x3000, 0x3000}};
+}
+constexpr uint32_t kAssertUni = 1u << 16;  // an assertion over the kinds of code points
 
 // ASCII classes: [:name:] and the \d \w \s escapes
 bool ascii_class(const std::string& name, CSet* s) {
@@ -362,7 +397,7 @@ bool ascii_class(const std::string& name, CSet* s) {
 struct RNode {
   enum K : uint8_t { Empty, Set, Cat, Alt, Star, Plus, Opt, Rep, Assert } k = Empty;
   CSet cs;
-  uint16_t mask = 0;  // Assert: allowed (prev kind, next kind) pairs
+  uint32_t mask = 0;  // Assert: allowed (prev kind, next kind) pairs | kAssertUni
   int a = -1, b = -1;
   int lo = 0, hi = 0;  // Rep; hi < 0 = unbounded
 };
@@ -512,17 +547,22 @@ struct RParser {
   int set_node(CSet cs) {
     RNode n;
     n.k = RNode::Set;
-    if (f.i) cs_fold_ascii(&cs);
+    if (f.i) cs_fold(&cs, f.u);
     cs = cs_inter(cs, cs_valid());
     if (!f.u && cs_nonascii(cs)) return fail("pattern can match invalid UTF-8 (Unicode mode is off)");
     n.cs = std::move(cs);
     return mk(n);
   }
-  int assert_node(uint16_t mask) {
+  int assert_node(uint32_t mask) {
     RNode n;
     n.k = RNode::Assert;
     n.mask = mask;
     return mk(n);
+  }
+  // a word-boundary assertion just set in *mask: over the kinds of code points in Unicode mode
+  uint32_t* cur_mask = nullptr;
+  void uni_word(int64_t c) {
+    if (f.u && c != 'A' && c != 'z' && cur_mask) *cur_mask |= kAssertUni;
   }
   // hex digits of \x / \u / \U: exactly `fixed` digits, or {1-8 digits}
   bool hex_escape(int fixed, uint32_t* v) {
@@ -555,19 +595,24 @@ struct RParser {
   }
   // An escape after '\' (i at the escaped character). Literal / class escapes set *cs and return 1;
   // assertions set *mask and return 2 (not in classes); errors return 0.
-  int escape(bool in_class, CSet* cs, uint16_t* mask) {
+  int escape(bool in_class, CSet* cs, uint32_t* mask) {
     if (eof()) {
       err = "incomplete escape sequence";
       return 0;
     }
     const size_t at = i;
+    cur_mask = mask;
     const int64_t c = getc_();
     if (c < 0) {
       err = "invalid UTF-8 in pattern";
       return 0;
     }
+    // \d \w \s: Unicode (Nd; Alphabetic + M + Nd + Pc + Join_Control; White_Space), ASCII with `u` off
     auto cls = [&](const char* name, bool neg) {
-      ascii_class(name, cs);
+      if (!f.u) ascii_class(name, cs);
+      else if (name[0] == 'd') *cs = cs_table(kUniDigit, kUniDigitN);
+      else if (name[0] == 'w') *cs = cs_table(kUniWord, kUniWordN);
+      else *cs = cs_uni_space();
       if (neg) *cs = cs_neg(*cs);
       return 1;
     };
@@ -607,11 +652,11 @@ struct RParser {
     }
     if (!in_class) {
       switch (c) {
-        case 'A': *mask = kind_mask([](uint32_t p_, uint32_t) { return p_ == BK_EDGE; }); return 2;
-        case 'z': *mask = kind_mask([](uint32_t, uint32_t n) { return n == BK_EDGE; }); return 2;
-        case 'B': *mask = kind_mask([](uint32_t p_, uint32_t n) { return kw_word(p_) == kw_word(n); }); return 2;
-        case '<': *mask = kind_mask([](uint32_t p_, uint32_t n) { return !kw_word(p_) && kw_word(n); }); return 2;
-        case '>': *mask = kind_mask([](uint32_t p_, uint32_t n) { return kw_word(p_) && !kw_word(n); }); return 2;
+        case 'A': *mask = kind_mask([](uint32_t p_, uint32_t) { return p_ == BK_EDGE; }); return uni_word(c), 2;
+        case 'z': *mask = kind_mask([](uint32_t, uint32_t n) { return n == BK_EDGE; }); return uni_word(c), 2;
+        case 'B': *mask = kind_mask([](uint32_t p_, uint32_t n) { return kw_word(p_) == kw_word(n); }); return uni_word(c), 2;
+        case '<': *mask = kind_mask([](uint32_t p_, uint32_t n) { return !kw_word(p_) && kw_word(n); }); return uni_word(c), 2;
+        case '>': *mask = kind_mask([](uint32_t p_, uint32_t n) { return kw_word(p_) && !kw_word(n); }); return uni_word(c), 2;
         case 'b': {
           if (!eof() && p[i] == '{') {
             const size_t e = p.find('}', i);
@@ -625,10 +670,10 @@ struct RParser {
               return 0;
             }
             i = e + 1;
-            return 2;
+            return uni_word(c), 2;
           }
           *mask = kind_mask([](uint32_t p_, uint32_t n) { return kw_word(p_) != kw_word(n); });
-          return 2;
+          return uni_word(c), 2;
         }
         default: break;
       }
@@ -768,7 +813,7 @@ struct RParser {
     if (c == '\\') {
       ++i;
       CSet cs;
-      uint16_t mask = 0;
+      uint32_t mask = 0;
       const int k = escape(false, &cs, &mask);
       if (k == 0) return -1;
       if (k == 2) return assert_node(mask);
@@ -778,7 +823,7 @@ struct RParser {
     if (ch < 0) return fail("invalid UTF-8 in pattern");
     // a literal character; with `u` off a non-ASCII one is still its UTF-8 bytes (allowed)
     CSet cs{{(uint32_t)ch, (uint32_t)ch}};
-    if (f.i) cs_fold_ascii(&cs);
+    if (f.i) cs_fold(&cs, f.u);
     RNode n;
     n.k = RNode::Set;
     n.cs = cs;
@@ -867,7 +912,7 @@ struct RParser {
           }
           if (ascii_class(name, s)) {
             i = e + 2;
-            if (f.i) cs_fold_ascii(s);
+            if (f.i) cs_fold(s, f.u);
             if (neg) *s = cs_neg(*s);
             return true;
           }
@@ -878,7 +923,7 @@ struct RParser {
     }
     if (c == '\\') {
       ++i;
-      uint16_t mask = 0;
+      uint32_t mask = 0;
       const size_t at = i;
       const int k = escape(true, s, &mask);
       if (k == 0) return false;
@@ -886,7 +931,7 @@ struct RParser {
         const char e = p[at];
         if (e != 'd' && e != 'D' && e != 'w' && e != 'W' && e != 's' && e != 'S') *cp = (*s)[0].lo;
       }
-      if (f.i) cs_fold_ascii(s);
+      if (f.i) cs_fold(s, f.u);
       return true;
     }
     (void)first;
@@ -897,7 +942,7 @@ struct RParser {
     }
     *s = {{(uint32_t)ch, (uint32_t)ch}};
     *cp = ch;
-    if (f.i) cs_fold_ascii(s);
+    if (f.i) cs_fold(s, f.u);
     return true;
   }
   bool class_item(CSet* out, bool first) {
@@ -929,7 +974,7 @@ struct RParser {
         return false;
       }
       s = {{(uint32_t)lo, (uint32_t)hi}};
-      if (f.i) cs_fold_ascii(&s);
+      if (f.i) cs_fold(&s, f.u);
     }
     *out = s;
     return true;
@@ -1285,8 +1330,17 @@ bool compile_nfa(const Pattern& p, Dfa* out, std::string* err) {
   R.edge_off = a16(R.first_off + first.size() * 4);
   R.set_off = a16(R.edge_off + edges.size() * 4);
   R.bytes = a16(R.set_off + (size_t)R.nsets * 32);
+  bool uni = false;
+  for (const NState& S : nfa.st)
+    for (const auto& a : S.asrt) uni = uni || (a.first & kAssertUni);
+  if (uni) {  // the Unicode \w ranges the assertions' code-point kinds are read from
+    R.uni_off = R.bytes;
+    R.uni_n = kUniWordN;
+    R.bytes = a16(R.uni_off + (size_t)kUniWordN * 8);
+  }
   std::vector<uint8_t>& b = out->prog;
   b.assign(R.bytes, 0);
+  if (uni) memcpy(b.data() + R.uni_off, kUniWord, (size_t)kUniWordN * 8);
   memcpy(b.data(), &R, sizeof(R));
   memcpy(b.data() + R.first_off, first.data(), first.size() * 4);
   memcpy(b.data() + R.edge_off, edges.data(), edges.size() * 4);
@@ -1322,6 +1376,14 @@ uint32_t Dfa::run(const uint8_t* s, size_t n) const {
 bool compile_dfa(const std::vector<Pattern>& pats, Dfa* out, std::string* err, uint32_t max_states) {
   Nfa nfa;
   if (!build_nfa(pats, &nfa, err)) return false;
+  // a Unicode word boundary reads the code points around a position, not the bytes: such a
+  // pattern runs as an NFA element (compile_column), whose Pike VM decodes them
+  for (const NState& st : nfa.st)
+    for (const auto& a : st.asrt)
+      if (a.first & kAssertUni) {
+        *err = kStateLimitError;
+        return false;
+      }
   const uint32_t root = 0;
   bool need_nl, need_word;
   assertion_kinds(nfa, &need_nl, &need_word);

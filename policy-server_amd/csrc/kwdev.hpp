@@ -235,15 +235,19 @@ struct alignas(16) DevCol {
 // Record (16-B aligned, offsets from the record start): DevNfa | u32 first[nnodes + 1] (edges of
 // node k: [first[k], first[k + 1])) | u32x2 edge[nedges] | 32-B byte sets[nsets].
 // edge.x = kind (0 byte set, 1 epsilon, 2 assertion) | arg << 8 (set id, or the assertion's 16-bit
-// mask over (previous, next) byte kinds, bit prev * 4 + next, kinds below); edge.y = target node.
+// mask over (previous, next) kinds, bit prev * 4 + next, kinds below, | kNfaUni when the kinds are
+// those of the code points before and after the position: Unicode word boundaries); edge.y =
+// target node. A record with such assertions carries the Unicode \w ranges (u32 lo, hi pairs) at
+// uni_off.
 struct alignas(16) DevNfa {
   uint32_t nnodes, nedges, nsets, start;
   uint32_t first_off, edge_off, set_off;
   uint32_t accept;  // the accepting node
   uint32_t search;  // 1: a regex (Regex::is_match: the accepting node is sticky, a walk may stop there)
   uint32_t bytes;   // whole record
-  uint32_t pad[2];
+  uint32_t uni_off, uni_n;  // Unicode \w ranges (0, 0: the record has no code-point assertions)
 };
+constexpr uint32_t kNfaUni = 1u << 16;
 enum NfaEdge : uint32_t { NE_BYTE = 0, NE_EPS = 1, NE_ASSERT = 2 };
 // byte kinds of the assertion masks: EDGE = before the first / after the last byte
 enum : uint32_t { NK_EDGE = 0, NK_NL = 1, NK_WORD = 2, NK_OTHER = 3 };
@@ -251,6 +255,33 @@ inline KW_HD uint32_t nfa_kind(uint32_t c) {
   if (c == '\n') return NK_NL;
   const bool w = (c - '0' < 10u) || (c - 'A' < 26u) || (c - 'a' < 26u) || c == '_';
   return w ? NK_WORD : NK_OTHER;
+}
+// the kind of code point c for a Unicode assertion: NL, WORD (the Unicode \w ranges), OTHER
+inline KW_HD uint32_t nfa_uni_kind(uint32_t c, const uint32_t* word, uint32_t n) {
+  if (c < 0x80) return nfa_kind(c);
+  uint32_t lo = 0, hi = n;  // first range whose hi >= c
+  while (lo < hi) {
+    const uint32_t m = (lo + hi) >> 1;
+    if (word[2 * m + 1] < c) lo = m + 1;
+    else hi = m;
+  }
+  return lo < n && word[2 * lo] <= c ? NK_WORD : NK_OTHER;
+}
+// the code point that starts at byte i / ends at byte i (lenient: a malformed sequence reads as a
+// non-word code point; positions inside a character never carry an assertion)
+inline KW_HD uint32_t nfa_cp_at(const uint8_t* s, uint32_t i, uint32_t n) {
+  const uint32_t c = s[i];
+  const uint32_t len = c < 0x80 ? 1u : c >= 0xF0 ? 4u : c >= 0xE0 ? 3u : c >= 0xC0 ? 2u : 0u;
+  if (len == 0 || i + len > n) return 0xFFFFFFFFu;
+  if (len == 1) return c;
+  uint32_t v = c & (0x7Fu >> len);
+  for (uint32_t k = 1; k < len; ++k) v = (v << 6) | (s[i + k] & 0x3Fu);
+  return v;
+}
+inline KW_HD uint32_t nfa_cp_before(const uint8_t* s, uint32_t i, uint32_t n) {
+  uint32_t j = i - 1;
+  for (uint32_t k = 0; k < 3 && j > 0 && (s[j] & 0xC0u) == 0x80u; ++k) --j;
+  return nfa_cp_at(s, j, n);
 }
 // Scratch a walk of `r` needs, in u32 words: mark[nnodes], two lists[nnodes], stack[nedges + 1].
 inline KW_HD uint64_t nfa_scratch_words(const DevNfa& r) { return 3ull * r.nnodes + r.nedges + 1; }
@@ -269,8 +300,17 @@ inline KW_HD bool nfa_run(const uint8_t* rec, const uint8_t* s, uint32_t n, uint
   uint32_t* stack = nxt + R.nnodes;
   uint32_t ncur = 0, nnxt = 0;
   bool hit = false;
-  // the closure of `node` at a position between byte kinds (p, q) into list L
-  auto add = [&](uint32_t node, uint32_t p, uint32_t q, uint32_t* L, uint32_t* cnt) {
+  const uint32_t* uword = (const uint32_t*)(rec + R.uni_off);
+  // kinds of the code points around position i (a record with Unicode word boundaries only)
+  auto uni_bit = [&](uint32_t i) -> uint32_t {
+    if (!R.uni_n) return 0u;
+    const uint32_t p = i == 0 ? NK_EDGE : nfa_uni_kind(nfa_cp_before(s, i, n), uword, R.uni_n);
+    const uint32_t q = i >= n ? NK_EDGE : nfa_uni_kind(nfa_cp_at(s, i, n), uword, R.uni_n);
+    return 1u << (p * 4u + q);
+  };
+  // the closure of `node` at a position between byte kinds (p, q) into list L; ubit: the
+  // position's code-point kinds as a mask bit (assertions flagged kNfaUni test that one)
+  auto add = [&](uint32_t node, uint32_t p, uint32_t q, uint32_t ubit, uint32_t* L, uint32_t* cnt) {
     const uint32_t g = *gen;
     const uint32_t bit = 1u << (p * 4u + q);
     uint32_t sp = 0;
@@ -284,25 +324,26 @@ inline KW_HD bool nfa_run(const uint8_t* rec, const uint8_t* s, uint32_t n, uint
       for (uint32_t e = first[x], e1 = first[x + 1]; e < e1; ++e) {
         const uint32_t k = edge[2 * e] & 0xffu, arg = edge[2 * e] >> 8, y = edge[2 * e + 1];
         if (k == NE_BYTE) stepping = true;
-        else if (k == NE_EPS || (arg & bit)) stack[sp++] = y;
+        else if (k == NE_EPS || (arg & ((arg & kNfaUni) ? ubit : bit))) stack[sp++] = y;
       }
       if (stepping) L[(*cnt)++] = x;
     }
   };
   ++*gen;
-  add(R.start, NK_EDGE, n ? nfa_kind(s[0]) : NK_EDGE, cur, &ncur);
+  add(R.start, NK_EDGE, n ? nfa_kind(s[0]) : NK_EDGE, uni_bit(0), cur, &ncur);
   for (uint32_t i = 0; i < n; ++i) {
     if (hit && R.search) return true;
     hit = false;
     const uint32_t c = s[i], p = nfa_kind(c), q = i + 1 < n ? nfa_kind(s[i + 1]) : NK_EDGE;
     ++*gen;
     nnxt = 0;
+    const uint32_t ub = uni_bit(i + 1);
     for (uint32_t t = 0; t < ncur; ++t) {
       const uint32_t x = cur[t];
       for (uint32_t e = first[x], e1 = first[x + 1]; e < e1; ++e) {
         if ((edge[2 * e] & 0xffu) != NE_BYTE) continue;
         const uint32_t set = edge[2 * e] >> 8;
-        if ((sets[set * 8u + (c >> 5)] >> (c & 31u)) & 1u) add(edge[2 * e + 1], p, q, nxt, &nnxt);
+        if ((sets[set * 8u + (c >> 5)] >> (c & 31u)) & 1u) add(edge[2 * e + 1], p, q, ub, nxt, &nnxt);
       }
     }
     uint32_t* t = cur;

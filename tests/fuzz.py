@@ -112,44 +112,87 @@ def _expr(rng, names, depth):
 
 
 def _script(rng, names):
-    """A group script beyond the bool-only subset (expr.hpp: let bindings, if / else, integers,
-    strings, statement sequences), now and then with an operation that fails at evaluation for some
-    member results (a bool + an int behind a branch)."""
+    """A group script beyond the bool-only subset (expr.hpp / DESIGN.md §2: let bindings, if / else,
+    integers, strings, statement sequences, arrays with contains / in / len / indexing, ranges in
+    `in`, switch, `??`, to_string, compound assignment, for and while loops, script functions), now
+    and then with an operation that fails at evaluation for some member results (a bool + an int
+    behind a branch, an index out of bounds)."""
     bools, ints = [], []
+    fns = []
 
     def b(d):
         r = rng.random()
-        if d <= 0 or r < 0.25:
+        if d <= 0 or r < 0.2:
             pool = [f"{rng.choice(names)}()"] * 3 + bools
             return rng.choice(pool)
-        if r < 0.35:
+        if r < 0.27:
             return f"!{b(d - 1)}"
-        if r < 0.55:
+        if r < 0.4:
             return f"({b(d - 1)} {rng.choice(['&&', '||', '==', '!=', '|', '&', '^'])} {b(d - 1)})"
-        if r < 0.7:
+        if r < 0.47:
             return f"(if {b(d - 1)} {{ {b(d - 1)} }} else {{ {b(d - 1)} }})"
-        if r < 0.85:
+        if r < 0.55:
             return f"({i(d - 1)} {rng.choice(['<', '<=', '>', '>=', '==', '!='])} {i(d - 1)})"
-        if r < 0.93:
+        if r < 0.58:
             return f'("{rng.choice(["a", "b"])}" + "x" {rng.choice(["==", "!="])} "{rng.choice(["ax", "bx"])}")'
-        return f"(if {b(d - 1)} {{ true }} else {{ {rng.choice(names)}() + 1 == 2 }})"  # runtime error on one path
+        if r < 0.61:
+            return f"(if {b(d - 1)} {{ true }} else {{ {rng.choice(names)}() + 1 == 2 }})"  # runtime error on one path
+        if r < 0.65:
+            return f"[{b(d - 1)}, {b(d - 1)}].contains({b(d - 1)})"
+        if r < 0.69:
+            return f"({b(d - 1)} {rng.choice(['in', '!in'])} [{b(d - 1)}, {rng.choice(['true', 'false'])}])"
+        if r < 0.72:
+            return f"({i(d - 1)} in {i(d - 1)}{rng.choice(['..', '..='])}{i(d - 1)})"
+        if r < 0.77:
+            return (f"(switch {i(d - 1)} {{ 0 => {b(d - 1)}, 1 | 2 => {b(d - 1)}, 3..6 => {b(d - 1)}, "
+                    f"_ => {b(d - 1)} }})")
+        if r < 0.8:
+            return f'({b(d - 1)}.to_string() == "{rng.choice(["true", "false"])}")'
+        if r < 0.84:
+            return f"((if {b(d - 1)} {{ () }} else {{ {b(d - 1)} }}) ?? {b(d - 1)})"
+        if r < 0.88:
+            k = rng.choice([-3, -2, -1, 0, 1, 2] if rng.random() < 0.9 else [3, -4])  # now and then out of bounds
+            return f"([{i(d - 1)}, {i(d - 1)}, {i(d - 1)}][{k}] > {i(d - 1)})"
+        if r < 0.93 and fns:
+            f = rng.choice(fns)
+            return f"{f}({b(d - 1)}, {i(d - 1)})"
+        return f"{rng.choice(names)}()"
 
     def i(d):
         r = rng.random()
         if d <= 0 or r < 0.3:
             return rng.choice([str(rng.randint(-3, 9))] + ints)
-        if r < 0.6:
+        if r < 0.55:
             return f"({i(d - 1)} {rng.choice(['+', '-', '*'])} {i(d - 1)})"
-        return f"(if {b(d - 1)} {{ {i(d - 1)} }} else {{ {i(d - 1)} }})"
+        if r < 0.7:
+            return f"(if {b(d - 1)} {{ {i(d - 1)} }} else {{ {i(d - 1)} }})"
+        if r < 0.8:
+            return f"[{b(d - 1)}, {i(d - 1)}, \"s\"].len()"
+        if r < 0.9:
+            return f"(switch {b(d - 1)} {{ true => {i(d - 1)}, false => {i(d - 1)} }})"
+        return f'"{"xy" * rng.randint(0, 3)}".len()'
 
     stmts = []
-    for k in range(rng.randint(0, 3)):
-        if rng.random() < 0.6:
+    for k in range(rng.randint(0, 2)):
+        if rng.random() < 0.5:
+            fns.append(f"f{k}")
+            stmts.append(f"fn f{k}(x, y) {{ if x {{ y > {rng.randint(-1, 3)} }} else {{ y < {rng.randint(0, 5)} }} }}")
+    for k in range(rng.randint(0, 4)):
+        r = rng.random()
+        if r < 0.4:
             stmts.append(f"let v{k} = {b(2)};")
             bools.append(f"v{k}")
-        else:
+        elif r < 0.6:
             stmts.append(f"let n{k} = {i(2)};")
             ints.append(f"n{k}")
+        elif r < 0.75:
+            stmts.append(f"let n{k} = 0; for x in [{b(1)}, {b(1)}, {b(1)}] {{ if x {{ n{k} += 1; }} }}")
+            ints.append(f"n{k}")
+        elif r < 0.85:
+            stmts.append(f"let n{k} = 0; while n{k} < {rng.randint(0, 4)} {{ n{k} += 1; }}")
+            ints.append(f"n{k}")
+        elif ints:
+            stmts.append(f"{rng.choice(ints)} {rng.choice(['+=', '-=', '*='])} {i(1)};")
     return " ".join(stmts + [b(3)])
 
 

@@ -1,81 +1,74 @@
 """Random label-constraint regexes in the dialect of DESIGN.md §2, each rendered twice from one
 tree: as Rust `regex` source (what a policies.yml holds, fed to the product and to the oracle's
-kwregex.c) and as an equivalent Python `re` pattern whose every construct is explicit (case folding
-as classes, classes as code point ranges, ^ $ \\b and friends as ASCII look-arounds), so that
-Python's own engine is a third, independent statement of the semantics:
+kwregex.c) and as a Python `re` pattern matched WITHOUT re.ASCII, so that Python's own Unicode
+engine — its \\w \\d \\s, word boundaries and case folding, built from its own Unicode tables — is a
+third, independent statement of the semantics (Unicode is the Rust default).
+
+The two engines agree only on a common subset of Unicode (DESIGN.md §2 lists where they differ:
+marks, Other_Alphabetic symbols, Pc / Join_Control, No digits, \\x1c-\\x1f, dotted / dotless i).
+Subjects are therefore drawn from ALPHA, characters on which Rust's and Python's definitions
+agree (tests/test_regex_dialect.py pins each one's properties by hand), and a class is the set of
+ALPHA characters Python puts in it:
 
   Rust construct                 Python rendering
-  x under (?i)                   [xX]                       (ASCII folding only)
+  x under (?i)                   the ALPHA characters Python's (?i)x matches
   .  /  (?s).                    [^\\n]  /  [\\s\\S]
-  [...] with &&, --, ~~, nesting  [\\uXXXX-\\uYYYY...] (the set computed here), (?!) when empty
-  \\d \\w \\s \\D \\W \\S           the ASCII sets / their complements over code points
+  [...] with &&, --, ~~, nesting  the ALPHA characters of the set (each item's members asked of
+                                 Python's engine), (?!) when empty
+  \\d \\w \\s \\D \\W \\S           \\d \\w \\s \\D \\W \\S (Unicode)
+  [:name:]                       its ASCII members (Rust's ASCII classes stay ASCII)
   ^ $ \\A \\z  (?m)^ (?m)$        \\A \\Z \\A \\Z (?<![^\\n]) (?![^\\n])
-  \\b \\< \\> \\b{start-half} \\b{end-half}   with re.ASCII: \\b \\b(?=\\w) \\b(?<=\\w) (?<!\\w) (?!\\w)
+  \\b \\< \\> \\b{start-half} \\b{end-half}   \\b \\b(?=\\w) \\b(?<=\\w) (?<!\\w) (?!\\w) (Unicode \\w)
   \\B                            (?<=\\w)(?=\\w)|(?<!\\w)(?!\\w)  (Python's \\B never matches an empty string)
   (?flags) mid-group             applied by the generator to the rest of the group (no Python flag)
   (?x) white space, # comments   dropped
 """
 import random
+import re
 
 META = set("\\.+*?()|[]{}^$#")
 CLASS_META = set("\\[]^-&~")
+# characters whose \\w / \\d / \\s membership and simple case folding are the same in Rust's regex
+# (UTS #18 Annex C) and Python's re: ASCII, Latin / Greek / CJK letters, Nd digits of two scripts,
+# an Nl numeral, Lt titlecase, Zs spaces, and the multi-member fold orbits k / K / KELVIN SIGN,
+# s / S / LONG S, ß / ẞ, σ / ς / Σ, µ / μ / Μ, θ / ϑ / Θ / ϴ, å / Å / ANGSTROM SIGN
 ALPHA = ["a", "b", "c", "k", "z", "A", "B", "K", "Z", "0", "1", "9", "_", "-", ".", " ", "\n", "#", "&", "~",
-         "é", "É", "ÿ", "Ω", "中", "\U0001D11E"]
-WORD = [(48, 57), (65, 90), (95, 95), (97, 122)]
+         "s", "S", "é", "É", "ÿ", "Ω", "ω", "中", "\U0001D11E", "ǅ", "ǈ", "ǉ", "Ǉ", "ª", "ⅻ", "٣", "۵",
+         "\u00a0", "\u2003", "ß", "ẞ", "σ", "ς", "Σ", "\u212a", "ſ", "µ", "μ", "Μ", "θ", "ϑ", "Θ", "ϴ",
+         "Å", "å", "\u212b"]
+UNIVERSE = frozenset(ALPHA)
 NAMED = {"alnum": [(48, 57), (65, 90), (97, 122)], "alpha": [(65, 90), (97, 122)], "digit": [(48, 57)],
-         "lower": [(97, 122)], "upper": [(65, 90)], "space": [(9, 13), (32, 32)], "word": WORD,
-         "xdigit": [(48, 57), (65, 70), (97, 102)], "punct": [(33, 47), (58, 64), (91, 96), (123, 126)],
-         "blank": [(9, 9), (32, 32)], "ascii": [(0, 127)]}
-VALID = [(0, 0xD7FF), (0xE000, 0x10FFFF)]
+         "lower": [(97, 122)], "upper": [(65, 90)], "space": [(9, 13), (32, 32)], "word": [(48, 57), (65, 90),
+         (95, 95), (97, 122)], "xdigit": [(48, 57), (65, 70), (97, 102)],
+         "punct": [(33, 47), (58, 64), (91, 96), (123, 126)], "blank": [(9, 9), (32, 32)], "ascii": [(0, 127)]}
 
 
-def norm(rs):
-    out = []
-    for lo, hi in sorted(rs):
-        if out and lo <= out[-1][1] + 1:
-            out[-1] = (out[-1][0], max(out[-1][1], hi))
-        else:
-            out.append((lo, hi))
-    return out
+def py_members(py_item):
+    """The ALPHA characters Python's engine puts in a one-character pattern."""
+    rx = re.compile(py_item)
+    return frozenset(c for c in ALPHA if rx.fullmatch(c))
 
 
-def inter(a, b):
-    return norm([(max(x, u), min(y, v)) for x, y in a for u, v in b if max(x, u) <= min(y, v)])
+def named(nm):
+    return frozenset(c for c in ALPHA if any(lo <= ord(c) <= hi for lo, hi in NAMED[nm]))
 
 
 def neg(a):
-    out, at = [], 0
-    for lo, hi in norm(a):
-        if lo > at:
-            out.append((at, lo - 1))
-        at = hi + 1
-    if at <= 0x10FFFF:
-        out.append((at, 0x10FFFF))
-    return inter(out, VALID)
-
-
-def union(a, b):
-    return norm(list(a) + list(b))
+    return UNIVERSE - a
 
 
 def fold(a):
-    add = []
-    for lo, hi in a:
-        for c in range(max(lo, 65), min(hi, 90) + 1):
-            add.append((c + 32, c + 32))
-        for c in range(max(lo, 97), min(hi, 122) + 1):
-            add.append((c - 32, c - 32))
-    return union(a, add)
+    """(?i): every ALPHA character that Python's case-insensitive match of a member accepts"""
+    out = set(a)
+    for c in a:
+        out |= py_members("(?i)" + re.escape(c))
+    return frozenset(out)
 
 
-def py_class(rs):
-    rs = norm(rs)
-    if not rs:
+def py_class(chars):
+    if not chars:
         return "(?!)"
-
-    def e(c):
-        return f"\\U{c:08x}"
-    return "[" + "".join(e(lo) if lo == hi else f"{e(lo)}-{e(hi)}" for lo, hi in rs) + "]"
+    return "[" + "".join(f"\\U{ord(c):08x}" for c in sorted(chars)) + "]"
 
 
 class Flags:
@@ -100,6 +93,8 @@ class Gen:
     def lit_rust(self, ch, f):
         r = self.r.random()
         cp = ord(ch)
+        if f.x and ch.isspace() and cp >= 0x80:  # verbose mode skips Unicode white space too
+            return f"\\x{{{cp:x}}}"
         if ch in META or (f.x and ch in " \t\n"):
             return "\\" + ch if ch not in "\n\t" else ("\\n" if ch == "\n" else "\\t")
         if ch == "\n":
@@ -113,6 +108,8 @@ class Gen:
         return ch
 
     def cls_char_rust(self, ch, f):
+        if f.x and ch.isspace() and ord(ch) >= 0x80:
+            return f"\\x{{{ord(ch):x}}}"
         if ch in CLASS_META or (f.x and ch in " \t\n#"):
             return "\\" + ch if ch not in "\n\t" else ("\\n" if ch == "\n" else "\\t")
         if ch == "\n":
@@ -124,26 +121,25 @@ class Gen:
         r = self.r.random()
         if r < 0.35:
             ch = self.r.choice(ALPHA)
-            s = [(ord(ch), ord(ch))]
+            s = frozenset([ch])
             return self.cls_char_rust(ch, f), fold(s) if f.i else s
         if r < 0.55:
             a, b = sorted(self.r.sample(ALPHA, 2), key=ord)
-            s = [(ord(a), ord(b))]
+            s = frozenset(c for c in ALPHA if ord(a) <= ord(c) <= ord(b))
             return f"{self.cls_char_rust(a, f)}-{self.cls_char_rust(b, f)}", fold(s) if f.i else s
         if r < 0.7:
             e = self.r.choice("dDwWsS")
-            base = {"d": [(48, 57)], "w": WORD, "s": [(9, 13), (32, 32)]}[e.lower()]
-            return "\\" + e, neg(base) if e.isupper() else base
+            return "\\" + e, py_members("\\" + e)
         if r < 0.82:
             nm = self.r.choice(sorted(NAMED))
-            s = fold(NAMED[nm]) if f.i else NAMED[nm]
+            s = fold(named(nm)) if f.i else named(nm)
             if self.r.random() < 0.25:
                 return f"[:^{nm}:]", neg(s)
             return f"[:{nm}:]", s
         if depth < 2:
             return self.cls(f, depth + 1)
         ch = self.r.choice(ALPHA)
-        return self.cls_char_rust(ch, f), [(ord(ch), ord(ch))]
+        return self.cls_char_rust(ch, f), frozenset([ch])
 
     def cls(self, f, depth=0):
         """(rust text '[...]', set)"""
@@ -151,13 +147,13 @@ class Gen:
         parts = []
 
         def union_part():
-            txt, s = "", []
+            txt, s = "", frozenset()
             for _ in range(self.r.randint(1, 3)):
                 t, x = self.cls_item(f, depth)
                 if txt and txt[-1] == "-" and t.startswith("-"):
                     t = "\\" + t
                 txt += t + self.ws(f).replace("#", "").replace(" note\n", "")
-                s = union(s, x)
+                s = s | x
             return txt, s
         txt, s = union_part()
         if txt.startswith("]") or txt.startswith("^"):
@@ -170,11 +166,11 @@ class Gen:
                 t2 = "\\" + t2
             parts.append(op + t2)
             if op == "&&":
-                s = inter(s, s2)
+                s = s & s2
             elif op == "--":
-                s = inter(s, neg(s2))
+                s = s - s2
             else:
-                s = union(inter(s, neg(s2)), inter(s2, neg(s)))
+                s = s ^ s2
         body = "".join(parts)
         if negate:
             return "[^" + body + "]", neg(s)
@@ -184,17 +180,15 @@ class Gen:
         r = self.r.random()
         if r < 0.38:
             ch = self.r.choice(ALPHA)
-            s = [(ord(ch), ord(ch))]
-            return self.lit_rust(ch, f), py_class(fold(s) if f.i else s)
+            return self.lit_rust(ch, f), py_class(fold(frozenset([ch])) if f.i else frozenset([ch]))
         if r < 0.46:
             return ".", "[\\s\\S]" if f.s else "[^\\n]"
         if r < 0.6:
             t, s = self.cls(f)
-            return t, py_class(inter(s, VALID))
+            return t, py_class(s)
         if r < 0.68:
             e = self.r.choice("dDwWsS")
-            base = {"d": [(48, 57)], "w": WORD, "s": [(9, 13), (32, 32)]}[e.lower()]
-            return "\\" + e, py_class(neg(base) if e.isupper() else base)
+            return "\\" + e, "\\" + e
         if r < 0.8:
             k = self.r.choice(["^", "$", "\\A", "\\z", "\\b", "\\B", "\\<", "\\>", "\\b{start}", "\\b{end}",
                                "\\b{start-half}", "\\b{end-half}"])
@@ -282,5 +276,5 @@ class Gen:
 
     def subject(self, rust):
         n = self.r.randint(0, 10)
-        pool = ALPHA + [c for c in rust if c.isalnum()][:12]
+        pool = ALPHA + [c for c in rust if c in UNIVERSE][:12]
         return "".join(self.r.choice(pool) for _ in range(n))

@@ -11,7 +11,7 @@ import oracle as O
 from helpers import diff_verdicts
 from pattern_cases import policies, reviews
 
-VALID = ["labels-dialect", "labels-blowup", "images-blowup", "registries-blowup", "images-mixed", "images-utf8"]
+VALID = ["labels-dialect", "labels-unicode", "labels-blowup", "images-blowup", "registries-blowup", "images-mixed", "images-utf8"]
 
 
 def test_blowup_patterns_never_fail_the_environment():

@@ -129,3 +129,42 @@ def test_verdict_probes_no_longer_500():
         j = ids.index(f"p{k}")
         resp = b.format_response(env, 0, j, int(got[j]), [int(got[m]) for m in env.group_members(j)], doc=fixture)
         assert resp.get("status", {}).get("code") != 500, (exprs[k], resp)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_scripts_match_oracle(form, seed):
+    """tests/fuzz.py's script generator (every form above, plus runtime errors on some paths) over
+    the a / b / c members: 60 random groups per seed, every member vector, both device forms."""
+    import random
+
+    from fuzz import _script
+    rng = random.Random(7000 + seed)
+    rows = [(_script(rng, ["a", "b", "c"]), []) for _ in range(60)]
+    doc = groups_doc(rows)
+    env = K.EvaluationEnvironment(doc, continue_on_errors=True)
+    oe = O.OracleEnv(doc, continue_on_errors=True)
+    ids = env.policy_ids()
+    for k in range(len(rows)):  # validity and load-time messages agree
+        P = oe.pol[oe.ids[f"g{k}"]]
+        if P["valid"]:
+            env.validate_settings(f"g{k}")
+        else:
+            with pytest.raises(K.PolicyInitialization) as e:
+                env.validate_settings(f"g{k}")
+            assert str(e.value) == P["expr_error"], rows[k][0]
+    docs = [review(v, f"uid-{v or 'none'}") for v in VECTORS]
+    b = K.Batch.from_json(docs)
+    for origin in (K.VALIDATE, K.AUDIT):
+        got = b.debug_host_walk(env, ids, origin)
+        want = oe.eval(b.view(), ids, origin)
+        assert np.array_equal(got, want), diff_verdicts(got, want, len(ids), ids)
+    v = got.reshape(len(docs), len(ids))
+    reasons = set()
+    for k in range(len(rows)):
+        j = ids.index(f"g{k}")
+        members = env.group_members(j)
+        for r in range(len(docs)):
+            resp = b.format_response(env, r, j, int(v[r, j]), [int(v[r, m]) for m in members], doc=docs[r])
+            assert resp == oe.response_doc(b.view(), r, j, K.AUDIT, doc=docs[r]), (rows[k][0], VECTORS[r])
+            reasons.add((int(v[r, j]) >> 8) & 0xFF)
+    assert {0, O.R_GROUP} <= reasons
