@@ -601,6 +601,9 @@ struct PassPlan {
     std::vector<uint8_t> progs;
     std::vector<uint32_t> midx;
     std::vector<int32_t> members;
+    // split group members (env.cpp split_policy): records of kind 2 / 3 after the groups' own in
+    // the upload; a member slot's midx entry is kSplitMember | record index
+    std::vector<WideGroupArgs> aux;
     uint32_t cause_stride = 0, stack_words = 0;
   } wide;
 };
@@ -611,7 +614,41 @@ void plan_wide_groups(const Env& E, const std::vector<int32_t>& list, const std:
                       int origin, PassPlan* plan) {
   PassPlan::Wide& W = plan->wide;
   W = PassPlan::Wide{};
-  std::map<int32_t, uint32_t> mcol;
+  std::map<int32_t, uint32_t> mcol, aux_of;
+  auto member_col = [&](int32_t m) {
+    auto it = mcol.find(m);
+    if (it == mcol.end()) {
+      it = mcol.emplace(m, (uint32_t)W.members.size()).first;
+      W.members.push_back(m);
+    }
+    return it->second;
+  };
+  // a group member that is split: its word is combined from its parts' words where the group
+  // reads it (before, the member pass left a placeholder and the group rejected)
+  auto split_member = [&](int32_t m) -> uint32_t {
+    auto it = aux_of.find(m);
+    if (it != aux_of.end()) return it->second;
+    const PolicyRec& M = E.pol[(size_t)m];
+    WideGroupArgs a;
+    memset(&a, 0, sizeof(a));
+    while (W.progs.size() % 4) W.progs.push_back(0);
+    a.prog_off = (uint32_t)W.progs.size();
+    a.prog_len = (uint32_t)(M.part_off.size() * 4);
+    W.progs.insert(W.progs.end(), (const uint8_t*)M.part_off.data(), (const uint8_t*)(M.part_off.data() + M.part_off.size()));
+    a.kind = M.family == FAM_CAPABILITIES ? 3u : 2u;
+    a.nmem = (uint32_t)M.parts.size();
+    a.okw = finish_word(M.mode, M.allowed_to_mutate, origin, 0, 0, false);
+    a.mutw = finish_word(M.mode, M.allowed_to_mutate, origin, 0, 0, true);
+    a.rejb = finish_word(M.mode, M.allowed_to_mutate, origin, 1, 0, false) & ~0xff00u;
+    std::vector<uint32_t> cols;
+    for (int32_t q : M.parts) cols.push_back(member_col(q));
+    a.midx_off = (uint32_t)W.midx.size();
+    W.midx.insert(W.midx.end(), cols.begin(), cols.end());
+    const uint32_t k = (uint32_t)W.aux.size();
+    W.aux.push_back(a);
+    aux_of.emplace(m, k);
+    return k;
+  };
   for (uint32_t j = 0; j < (uint32_t)list.size(); ++j) {
     const PolicyRec& P = E.pol[(size_t)list[j]];
     const bool split = !P.parts.empty() && !P.init_error;
@@ -630,15 +667,13 @@ void plan_wide_groups(const Env& E, const std::vector<int32_t>& list, const std:
     g.col = rows_code ? (*rows_code)[j] : j;
     const std::vector<int32_t>& mem = split ? P.parts : P.members;
     g.nmem = (uint32_t)mem.size();
-    g.midx_off = (uint32_t)W.midx.size();
+    std::vector<uint32_t> cols;
     for (int32_t m : mem) {
-      auto it = mcol.find(m);
-      if (it == mcol.end()) {
-        it = mcol.emplace(m, (uint32_t)W.members.size()).first;
-        W.members.push_back(m);
-      }
-      W.midx.push_back(it->second);
+      const PolicyRec& M = E.pol[(size_t)m];
+      cols.push_back(!split && !M.parts.empty() && !M.init_error ? kSplitMember | split_member(m) : member_col(m));
     }
+    g.midx_off = (uint32_t)W.midx.size();
+    W.midx.insert(W.midx.end(), cols.begin(), cols.end());
     if (split) {  // a plain policy's words (slotplan.cpp CK_PLAIN), the reason and argument from its parts
       g.kind = P.family == FAM_CAPABILITIES ? 3u : 2u;
       g.okw = finish_word(P.mode, P.allowed_to_mutate, origin, 0, 0, false);
@@ -1441,14 +1476,15 @@ int run_validate(const kw_env* env, kw_batch* kb, PassPlan& plan, int origin, bo
     if (int rc = run_pass(kb, mplan, false, s)) return rc;
   }
   if (int rc = run_pass(kb, plan, timed, s)) return rc;
-  // combine: records | jump code | member maps in one upload
-  const size_t g_bytes = W.groups.size() * sizeof(WideGroupArgs);
+  // combine: records (the groups', then the split members') | jump code | member maps in one upload
+  const size_t g_bytes = (W.groups.size() + W.aux.size()) * sizeof(WideGroupArgs);
   const size_t p_at = g_bytes, m_at = (p_at + W.progs.size() + 15u) & ~(size_t)15u;
   const size_t bytes = m_at + W.midx.size() * 4;
   HIPCHK(hipStreamSynchronize(s));  // the upload buffer may still be read by the previous pass
   if (int rc = ensure(&D.wg_data, &D.wg_data_cap, bytes)) return rc;
   std::vector<uint8_t> h(bytes, 0);
-  memcpy(h.data(), W.groups.data(), g_bytes);
+  memcpy(h.data(), W.groups.data(), W.groups.size() * sizeof(WideGroupArgs));
+  if (!W.aux.empty()) memcpy(h.data() + W.groups.size() * sizeof(WideGroupArgs), W.aux.data(), W.aux.size() * sizeof(WideGroupArgs));
   memcpy(h.data() + p_at, W.progs.data(), W.progs.size());
   memcpy(h.data() + m_at, W.midx.data(), W.midx.size() * 4);
   HIPCHK(hipMemcpyAsync(D.wg_data, h.data(), bytes, hipMemcpyHostToDevice, s));
@@ -1859,7 +1895,15 @@ int kw_debug_host_walk(const kw_env* env, const kw_batch* kb, const int32_t* pol
         uint32_t* dst = out + r * npol + g.col;
         if (*dst == kBypassWord) continue;
         auto ok = [&](uint32_t m) {
-          const uint32_t x = mw[r * nm + W.midx[g.midx_off + m]];
+          const uint32_t c = W.midx[g.midx_off + m];
+          uint32_t x;
+          if (c & kSplitMember) {
+            const WideGroupArgs& a = W.aux[c & ~kSplitMember];
+            x = combine_parts(a, (const uint32_t*)(W.progs.data() + a.prog_off),
+                              [&](uint32_t t) { return mw[r * nm + W.midx[a.midx_off + t]]; });
+          } else {
+            x = mw[r * nm + c];
+          }
           return (x & KW_V_ALLOWED) && !(x & KW_V_MUTATED);
         };
         uint64_t cz = 0;  // (the causes of a group of at most 15 members go into ARG)

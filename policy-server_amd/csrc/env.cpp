@@ -1033,6 +1033,15 @@ Status build_env(const char* json, size_t len, bool continue_on_errors, const ch
   env->nvisible = env->pol.size();
   for (size_t i = 0; i < env->nvisible; ++i)
     if (!env->pol[i].is_group && !env->pol[i].init_error) split_policy(env, i);
+  // a group with a split member reads that member's word combined from its parts: only the wide
+  // path's combine kernel does, so the group takes a wide form (wide jump code or script bytecode)
+  for (size_t i = 0; i < env->nvisible; ++i) {
+    PolicyRec& g = env->pol[i];
+    if (!g.is_group || !g.prog.valid || g.prog.eval_error || g.prog.wide) continue;
+    bool split_member = false;
+    for (int32_t m : g.members) split_member = split_member || (!env->pol[(size_t)m].parts.empty() && !env->pol[(size_t)m].init_error);
+    if (split_member) g.prog = compile_group_expression(g.expression, g.member_names, /*force_wide=*/true);
+  }
 
   // ---- the request columns' patterns: every list of every initialised policy as pattern ids
   if (env->always_ns) pattern_id(&env->cols[COL_NS], Pattern::Literal, *env->always_ns);

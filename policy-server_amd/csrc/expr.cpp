@@ -2303,7 +2303,8 @@ ExprOutcome GroupProgram::run(const std::function<bool(uint32_t)>& member_ok) co
   return run_ast(*ast, member_ok);
 }
 
-GroupProgram compile_group_expression(const std::string& expr, const std::vector<std::string>& members) {
+GroupProgram compile_group_expression(const std::string& expr, const std::vector<std::string>& members,
+                                      bool force_wide) {
   GroupProgram g;
   g.nmem = (uint32_t)members.size();
   Lexer lx;
@@ -2353,7 +2354,7 @@ GroupProgram compile_group_expression(const std::string& expr, const std::vector
   for (FnDef& f : ast->fns) fold(&f.body, *ast);
   g.ast = ast;
   // a script without member calls has one outcome: a constant column or a constant program
-  if (!program_calls_members(*ast)) {
+  if (!program_calls_members(*ast) && !force_wide) {
     const ExprOutcome o = run_ast(*ast, [](uint32_t) { return true; });
     if (o.error) {
       g.eval_error = true;
@@ -2372,7 +2373,9 @@ GroupProgram compile_group_expression(const std::string& expr, const std::vector
     uint32_t maxd = 1;
     emit(br, false, &g.code, 1, &maxd);
     g.depth = maxd;
-    if (members.size() <= (size_t)kMaxGroupMembers && maxd <= (uint32_t)kMaxGroupStack && g.code.size() <= 65535) return g;
+    if (!force_wide && members.size() <= (size_t)kMaxGroupMembers && maxd <= (uint32_t)kMaxGroupStack &&
+        g.code.size() <= 65535)
+      return g;
     // the wide path: u16 member operands, u32 jump targets, a value stack in global scratch
     g.code.clear();
     maxd = 1;
@@ -2389,7 +2392,7 @@ GroupProgram compile_group_expression(const std::string& expr, const std::vector
   }
   // a truth table when it is small and cheap to fill (2^n runs of the interpreter); otherwise
   // typed bytecode, run per request by the wide path's combine kernel
-  const bool table = !force_script && members.size() <= kMaxTableMembers &&
+  const bool table = !force_script && !force_wide && members.size() <= kMaxTableMembers &&
                      (std::max<uint64_t>(steps, 1) << members.size()) <= (1ull << 24);
   if (!table) {
     std::string err;

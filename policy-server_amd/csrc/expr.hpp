@@ -77,6 +77,9 @@ constexpr uint32_t kMaxWideStack = 1u << 16;  // value-stack bound of the wide p
 std::string group_eval_message(const std::string& outcome_message);
 
 // members: member names in settings order (the slot of a call is its index here).
-GroupProgram compile_group_expression(const std::string& expr, const std::vector<std::string>& members);
+// force_wide: a form the wide path runs (wide jump code or script bytecode), for groups whose
+// members' words are combined in the wide path (a split member).
+GroupProgram compile_group_expression(const std::string& expr, const std::vector<std::string>& members,
+                                      bool force_wide = false);
 
 }  // namespace kw

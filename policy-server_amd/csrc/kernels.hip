@@ -1634,7 +1634,15 @@ __global__ void __launch_bounds__(kWideThreads) wide_groups_kernel(WideGroupPass
     const uint32_t* mw = w.member_words + r * w.nmw;
     const uint32_t* midx = w.midx + g.midx_off;
     auto ok = [&](uint32_t s) {
-      const uint32_t x = mw[midx[s]];
+      const uint32_t c = midx[s];
+      uint32_t x;
+      if (c & kSplitMember) {  // a split member: its word from its parts' words
+        const WideGroupArgs& a = w.groups[w.ngroups + (c & ~kSplitMember)];
+        const uint32_t* am = w.midx + a.midx_off;
+        x = combine_parts(a, (const uint32_t*)(w.progs + a.prog_off), [&](uint32_t t) { return mw[am[t]]; });
+      } else {
+        x = mw[c];
+      }
       return (x & KW_V_ALLOWED) && !(x & KW_V_MUTATED);
     };
     auto cause = [&](uint32_t s) { cz[s >> 6] |= 1ull << (s & 63u); };

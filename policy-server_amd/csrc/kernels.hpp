@@ -167,6 +167,8 @@ struct WideGroupArgs {
   uint32_t mutw;                // split psp-capabilities: the mutated verdict word
 };
 
+constexpr uint32_t kSplitMember = 0x80000000u;  // a group's midx entry naming a split member's record
+
 // A split policy's word from its parts' words (env.cpp split_policy): the first part that rejects
 // (safe-labels: a mandatory index offset by the part's start), else — psp-capabilities, whose later
 // parts validate nothing — mutated when any part mutated, else accepted. part(s): part s's word.

@@ -38,6 +38,27 @@ def split_policies():
                                          "required_drop_capabilities": [f"CAP_Z{i}" for i in range(40)],
                                          "default_add_capabilities": [f"CAP_W{i}" for i in range(30)] + ["KILL"]}},
         "small": {"module": MOD + "safe-labels:v0.1.14", "settings": {"mandatory_labels": ["app"]}},
+        # split policies as group members, in a small group (now a wide form), a script
+        # group and a wide group (70 members); their words are combined from the parts where the
+        # group reads them
+        "group-small": {"policies": {
+            "tail": {"module": MOD + "safe-labels:v0.1.14",
+                     "settings": {"mandatory_labels": [f"y{i}" for i in range(64)] + ["app", "tier"]}},
+            "small": {"module": MOD + "safe-labels:v0.1.14", "settings": {"mandatory_labels": ["app"]}}},
+            "expression": "tail() || small()", "message": "small group rejected"},
+        "group-script": {"policies": {
+            "tail": {"module": MOD + "safe-labels:v0.1.14",
+                     "settings": {"mandatory_labels": [f"y{i}" for i in range(64)] + ["app", "tier"]}},
+            "caps": {"module": MOD + "psp-capabilities:v0.1.7",
+                     "settings": {"allowed_capabilities": CAPS[:6], "required_drop_capabilities": drops70}}},
+            "expression": "let n = 0; if tail() { n += 1; } if caps() { n += 1; } n >= 1",
+            "message": "script group rejected"},
+        "group-wide": {"policies": dict(
+            {f"m{i}": {"module": MOD + "safe-labels:v0.1.14", "settings": {"mandatory_labels": [KEYS[i % 21]]}}
+             for i in range(69)},
+            big={"module": MOD + "safe-labels:v0.1.14", "settings": {"mandatory_labels": mand100}}),
+            "expression": "big() || (" + " && ".join(f"m{i}()" for i in range(69)) + ")",
+            "message": "wide group rejected"},
     }
 
 
