@@ -12,10 +12,14 @@ producing 64M verdict words. Inputs are resident in HBM before the timed region.
 
 Multi-GPU: one process per GPU; rank 0 compiles the policy set and broadcasts the compiled-table
 blob once over RCCL (torch.distributed "nccl" = RCCL on ROCm); every rank evaluates its own request
-shard (weak scaling: --rows per GPU, the default; strong scaling: --total-rows T, one job of T
-requests sharded across the GPUs; no collective on the per-request path). Timing: barrier + synchronize on both
-sides of exactly K steps, max over ranks. Rank 0 prints one JSON line.
+shard; no collective on the per-request path. With several GPUs and no size flag, `value` is BASELINE's
+own multi-GPU workload, strong scaling: the config's request count as ONE job sharded across the GPUs
+(C4: 1M requests over N GPUs; --config c5_mixed: 10M), and the same run then measures weak scaling
+(that many requests per GPU) as the `weak_scaling` field. --rows R (per GPU, weak) or --total-rows T
+(one job, strong) choose one measurement explicitly. Timing: barrier + synchronize on both sides of
+exactly K steps, max over ranks. Rank 0 prints one JSON line.
 """
+import hashlib
 import argparse
 import json
 import os
@@ -64,10 +68,22 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (rank 0), about 10-30 s")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-modes", action="store_true", help="skip the end-to-end / flatten timings")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: gloo, the host walk (kw_debug_host_walk) as the step over a 1/1000 sample of "
+                         "the config's rows; exercises the argument path and the JSON fields only (tests)")
     args = ap.parse_args()
+    dry = args.dry_run
     args.synth, default_rows, workload = CONFIGS[args.config]
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    also_weak = False
+    if dry:
+        default_rows = max(100, default_rows // 1000)
     if args.rows is None and args.total_rows is None:
-        args.rows = default_rows
+        if world_env > 1:  # BASELINE's multi-GPU configs are fixed jobs: strong first, weak beside it
+            args.total_rows = default_rows
+            also_weak = True
+        else:
+            args.rows = default_rows
 
     import numpy as np
     import torch
@@ -83,9 +99,11 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    device = local
+        if not dry:
+            torch.cuda.set_device(local)
+        dist.init_process_group("gloo" if dry else "nccl")
+    device = -1 if dry else local
+    sync = (lambda: None) if dry else torch.cuda.synchronize
 
     with open(os.path.join(ROOT, "configs", f"{args.config}.yml")) as f:
         policies = yaml.safe_load(f)
@@ -94,54 +112,72 @@ def main():
     if world > 1:
         from kwgpu.dist import broadcast_environment
 
-        env = broadcast_environment(policies, dist, rank, device=device, tensor_device="cuda")
+        env = broadcast_environment(policies, dist, rank, device=device, tensor_device="cpu" if dry else "cuda")
     else:
         env = K.EvaluationEnvironment(policies, device=device)
     ids = env.policy_ids()
     npol = len(ids)
 
-    t0 = time.time()
     from kwgpu.dist import job_bounds
 
-    # the job: world x rows requests (weak scaling) or total_rows requests (strong scaling), split into
-    # shards of equal work (1 + containers per request)
-    if args.total_rows is not None:
-        bounds, job_rows, scaling = job_bounds(args.synth, world, SEED, total_rows=args.total_rows)
-    else:
-        bounds, job_rows, scaling = job_bounds(args.synth, world, SEED, rows_per_rank=args.rows)
-    row0, nrows = int(bounds[rank]), int(bounds[rank + 1] - bounds[rank])
-    syn = K.SynthBatch(args.synth, nrows, seed=SEED, row0=row0)
-    batch = syn.batch().to_device(device)
-    log(f"rank {rank}: {nrows} requests generated + resident in {time.time() - t0:.1f}s; {npol} policies")
+    def measure(total_rows=None, rows_per_rank=None):
+        """One job (world x rows_per_rank requests, weak; or total_rows, strong) split into shards of
+        equal work (1 + containers per request): generate this rank's shard resident in HBM, W warmup
+        steps, then exactly K timed steps between barriers; the time is the max over ranks."""
+        t0 = time.time()
+        bounds, job_rows, scaling = job_bounds(args.synth, world, SEED, total_rows=total_rows, rows_per_rank=rows_per_rank)
+        row0, nrows = int(bounds[rank]), int(bounds[rank + 1] - bounds[rank])
+        syn = K.SynthBatch(args.synth, nrows, seed=SEED, row0=row0)
+        batch = syn.batch() if dry else syn.batch().to_device(device)
+        step = (lambda: batch.debug_host_walk(env, ids)) if dry else (lambda: batch.validate(env, ids))
+        log(f"rank {rank}: {nrows} requests generated + resident in {time.time() - t0:.1f}s; {npol} policies ({scaling})")
+        for _ in range(args.warmup):
+            step()
+        sync()
+        if dist:
+            dist.barrier()
+        sync()
+        t_start = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        sync()
+        if dist:
+            dist.barrier()
+        elapsed = time.perf_counter() - t_start
+        if dist:
+            t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if dry else "cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        return syn, batch, bounds, job_rows, scaling, nrows, elapsed
 
-    for _ in range(args.warmup):
-        batch.validate(env, ids)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        batch.validate(env, ids)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    weak = None
+    if also_weak:  # the weak-scaling field first (its batch is released before the primary job's)
+        wsyn, wbatch, _, wjob, _, wrows, welapsed = measure(rows_per_rank=default_rows)
+        weak = {"value": wjob * args.steps / welapsed, "unit": "requests/s", "ms_per_step": welapsed * 1e3 / args.steps,
+                "requests_per_gpu": wrows, "total_requests": wjob, "scaling": "weak",
+                "workload": workload.format(rows=default_rows, npol=npol)}
+        wbatch.close()
+        del wsyn, wbatch
+    syn, batch, bounds, job_rows, scaling, nrows, elapsed = measure(total_rows=args.total_rows, rows_per_rank=args.rows)
     ms_per_step = elapsed * 1e3 / args.steps
     value = job_rows * args.steps / elapsed
 
     # per-kernel device time with HIP events on the launch stream
-    tm = batch.timed(env, ids, warmup=2, reps=max(5, args.steps))
+    if dry:
+        from types import SimpleNamespace
+        tm = SimpleNamespace(classify_ms=0.0, evaluate_ms=ms_per_step, total_ms=ms_per_step, classify_bytes=0.0,
+                             evaluate_bytes=0.0)
+        args.no_cpu_baseline = args.no_host_modes = True
+    else:
+        tm = batch.timed(env, ids, warmup=2, reps=max(5, args.steps))
     kernels = {"classify": (tm.classify_ms, tm.classify_bytes), "evaluate": (tm.evaluate_ms, tm.evaluate_bytes)}
     dom = max(kernels, key=lambda k: kernels[k][0])
     ms, nbytes = kernels[dom]
-    achieved = nbytes / (ms * 1e-3) / 1e9
+    achieved = nbytes / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
     gather = None
-    if dist:
+    if dry:
+        frac_allowed = None
+    elif dist:
         # verdict words back to the host after the timed region: each rank copies its shard D2H into
         # its own disjoint slice of one shared host array (kwgpu.dist.gather_verdicts), rank 0 holds it
         from kwgpu.dist import gather_verdicts
@@ -162,6 +198,7 @@ def main():
 
     result = None
     if rank == 0:
+        traffic_bytes, traffic_src = (None, "dry run") if dry else traffic(args, nrows)
         cpu = None
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(policies, ids, args)
@@ -169,18 +206,21 @@ def main():
         result = {
             "metric": METRIC, "value": value, "unit": "requests/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": scaling,
-            "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic" + (" (dry run: host walk, no GPU)" if dry else ""),
             "config": {"workload": (workload.format(rows=args.rows, npol=npol) if scaling == "weak" else
                                     workload.format(rows=job_rows, npol=npol).replace(" per GPU", "")
-                                    + f", one job sharded across {world} GPU(s)"),
+                                    + f", one job sharded across {world} GPU(s)"
+                                    + (f" (strong scaling; weak_scaling: {default_rows} per GPU)" if weak else "")),
                        "config": args.config, "requests_per_gpu": job_rows / world, "total_requests": job_rows,
                        "policies": npol, "parallelism": f"dp{world} (request shards)"},
             "evaluations_per_s": value * npol,
             "kernel_ms": {"classify": tm.classify_ms, "evaluate": tm.evaluate_ms, "total": tm.total_ms},
             "roofline": {"kernel": "evaluate_tiles_kernel",
                          "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic(args),
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_bytes,
+                         "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": nbytes, "algorithmic_bytes_per_request": nbytes / nrows},
+            "weak_scaling": weak,
             "cpu_baseline": cpu,
             "timing_modes": modes,
             "verdicts_final_allowed_fraction": frac_allowed,
@@ -344,20 +384,34 @@ def host_modes(env, ids, syn, device, args, alg_bytes=None):
     return out
 
 
-def traffic(args):
-    """HBM bytes per launch of the tiled kernel from the committed PMC summary (profiles/traffic.json,
-    written by scripts/pmc_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
-    of this bench, FETCH_SIZE doubled per the gfx950 calibration). None when absent or measured on a
-    different workload."""
+def library_sha256():
+    """sha256 of the libkwgpu.so this process evaluates with (KWGPU_LIB or the in-tree build)."""
+    import kwgpu._native as N
+    h = hashlib.sha256()
+    with open(N.LIB_PATH, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
+def traffic(args, rows):
+    """(HBM bytes per launch of the tiled kernel, provenance) from the committed PMC summary
+    (profiles/traffic.json, written by scripts/pmc_summary.py from separate rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE passes of this bench, FETCH_SIZE doubled per the gfx950 calibration). The bytes are
+    None when the file is absent, was measured on another workload or shard size, or on another build
+    of the library (its sha256 differs from the running one's): a kernel change must not keep printing
+    an old measurement."""
     path = os.path.join(ROOT, "profiles", "traffic.json")  # written by scripts/pmc.sh (copied from the GPU box)
     try:
         with open(path) as f:
             t = json.load(f)
     except (OSError, ValueError):
-        return None
-    if t.get("config") != args.config or t.get("rows") != (args.rows if args.rows is not None else args.total_rows):
-        return None
-    return t.get("bytes_per_launch")
+        return None, "no profiles/traffic.json"
+    if t.get("config") != args.config or t.get("rows") != rows:
+        return None, f"profiles/traffic.json is for {t.get('config')} x {t.get('rows')} rows, not this workload"
+    if t.get("lib_sha256") != library_sha256():
+        return None, "profiles/traffic.json was measured on another build of libkwgpu.so (sha256 differs)"
+    return t.get("bytes_per_launch"), f"{t.get('source')}; round {t.get('round')}; lib sha256 {t.get('lib_sha256')[:16]}"
 
 
 def cpu_threads():

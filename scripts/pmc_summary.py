@@ -28,7 +28,13 @@ def write_traffic(fetch_dir, write_dir, out, config="c4_64", rows=1_000_000, tag
     f, w = summarise(fetch_dir), summarise(write_dir)
     fetch = 2.0 * f["FETCH_SIZE"] * 1024.0
     write = w["WRITE_SIZE"] * 1024.0
-    doc = {"round": tag, "config": config, "rows": rows, "kernel": "evaluate_tiles_kernel",
+    import hashlib
+    import os
+    lib = os.environ.get("KWGPU_LIB") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                     "policy-server_amd", "libkwgpu.so")
+    with open(lib, "rb") as fh:
+        sha = hashlib.sha256(fh.read()).hexdigest()
+    doc = {"round": tag, "config": config, "rows": rows, "kernel": "evaluate_tiles_kernel", "lib_sha256": sha,
            "fetch_bytes": fetch, "write_bytes": write, "bytes_per_launch": fetch + write,
            "source": f"rocprofv3 --pmc FETCH_SIZE ({fetch_dir}) and WRITE_SIZE ({write_dir}), separate passes; "
                      "FETCH_SIZE x2 (gfx950 calibration)"}

@@ -140,3 +140,30 @@ def test_job_bounds_weak_and_strong(world):
         assert max(loads) - min(loads) <= 2 * int(w.max()), loads
     with pytest.raises(ValueError):
         job_bounds(5, world, SEED)
+
+
+def test_bench_multi_gpu_default_is_baselines_strong_job():
+    """with WORLD_SIZE > 1 and no size flag, bench.py's `value` is BASELINE's own
+    multi-GPU workload — the config's request count as one job sharded across the ranks (strong
+    scaling: C4's 1M over N, C5's 10M) — and weak scaling (that many per rank) is measured beside it
+    as `weak_scaling`. A 2-process gloo dry run (--dry-run: the host walk, 1/1000 of the rows)
+    exercises that argument path and prints both fields."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", "29561", os.path.join(root, "bench.py"),
+                          "--gpus", "2", "--steps", "2", "--warmup", "1", "--dry-run"],
+                         capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong"
+    assert d["config"]["total_requests"] == 1000  # C4's 1M / 1000 in a dry run, one job over both ranks
+    assert sum(d["shards"]["rows"]) == 1000 and "one job sharded across 2 GPU(s)" in d["config"]["workload"]
+    w = d["weak_scaling"]
+    assert w["scaling"] == "weak" and w["total_requests"] == 2000 and w["value"] > 0
+    assert d["value"] > 0 and "weak_scaling" in d["config"]["workload"]
