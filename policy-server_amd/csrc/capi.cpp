@@ -1094,8 +1094,6 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
   for (const auto& [c0, c1] : plan->launches) {
     TileArgs t = T;
     t.nchunk = c1 - c0;
-    // one chunk (no derive step reads the classes back) and key classes that fit a byte
-    t.lk_pack = (t.nchunk == 1 && H->col[COL_LK].nclass <= 256u) ? 1u : 0u;
     uint32_t at = 16 + table_bytes;
     for (uint32_t k = 0; k < t.nchunk; ++k) {
       const SlotChunk& c = plan->chunks[c0 + k];

@@ -25,62 +25,9 @@
 #include "imgscan.hpp"
 #include "kernels.hpp"
 
-// Build-time variants (A/B): KW_LDS_BARRIER uses LDS-only barriers between the compute phases;
-// KW_MAND_BATCH batches the mandatory-label loads.
-#ifndef KW_LDS_BARRIER
-#define KW_LDS_BARRIER 1
-#endif
-#ifndef KW_LIT_SHORT  // tile kernel: a 4-word literal probe when no string of the wave is longer than 16 bytes
-#define KW_LIT_SHORT 1
-#endif
-#ifndef KW_IMG_LIT_SHORT  // image registry / tag probes: 2- or 4-word batches when the wave's parts are that short
-#define KW_IMG_LIT_SHORT 1
-#endif
-#ifndef KW_MAND_BATCH
-#define KW_MAND_BATCH 1
-#endif
-#ifndef KW_DESC_LDS  // tile kernel: staging reads the tile's descriptor from its LDS copy (else scalar loads)
-#define KW_DESC_LDS 1
-#endif
-#ifndef KW_PF_EARLY  // tile kernel: the L2 prefetch of the next tile right after staging (else after classification)
-#define KW_PF_EARLY 0
-#endif
-#ifndef KW_NT_STORE  // tile kernel: verdict words with non-temporal stores
-#define KW_NT_STORE 1
-#endif
-#ifndef KW_MIN_WAVES  // tile kernel: minimum waves per SIMD the register allocation must allow
-#define KW_MIN_WAVES 1
-#endif
-#ifndef KW_P1_HOIST  // label items issue their value offsets and deny row before the walk and OR the constraint rows as
-#define KW_P1_HOIST 0  // classes come out; single-chunk passes store capabilities' mutation bits (not classes) in P1
-#endif
-#ifndef KW_LK_PACK  // TileArgs::lk_pack launches: label-key classes carry the key's mandatory local bit
-#define KW_LK_PACK 0   // (r03 A/B: C4 +0.5 %, C5 +1 %, C6 -0.8 %: off)
-#endif
-#ifndef KW_KV_ABSORB  // label-value walks also stop at absorbing states (same-box A/B r03 v2: C4 -0.5 %, C3 -0.9 %)
-#define KW_KV_ABSORB 1
-#endif
-#ifndef KW_LATE_ATOMIC  // tile kernel: the counter fetch for the tile after next issued after the staging barrier (r03 v2: neutral, off)
-#define KW_LATE_ATOMIC 0
-#endif
-#ifndef KW_MAD24  // DFA transitions addressed with a 24-bit multiply-add (trans_at)
-#define KW_MAD24 1
-#endif
-#ifndef KW_IMG_LDSADDR  // image DFAs staged in LDS: classes pre-offset to LDS addresses (one multiply-add a step)
-#define KW_IMG_LDSADDR 1
-#endif
-#ifndef KW_P3_BITS  // P3 verdict words from 32-bit halves and bit-selects (no 64-bit shifts or branches)
-#define KW_P3_BITS 1
-#endif
-#ifndef KW_IMG_MIN_WAVES  // image-only instantiation: minimum waves per SIMD (6: at most 80 VGPRs)
-#define KW_IMG_MIN_WAVES KW_MIN_WAVES
-#endif
-#ifndef KW_VBASE  // tile kernel: LDS region offsets in VGPRs in the label / container instantiation
-#define KW_VBASE 1
-#endif
-#ifndef KW_CLS129  // label-value class loads index min(byte, 128) of the 129-entry narrow maps
-#define KW_CLS129 1
-#endif
+// The measured-and-dropped variants of r01-r04 (A/B knobs) are gone from the source; git history
+// and DESIGN.md §10 keep what each measured. KW_PREFETCH (kernels.hpp) stays: the next-tile L2
+// prefetch is a documented diagnostic (KW_L2_PREFETCH=1 runs it).
 
 namespace kw {
 
@@ -146,7 +93,7 @@ __device__ inline uint32_t lit_lookup(const uint8_t* rec, const uint8_t* bytes, 
 // batch are read one by one, so any choice is exact); registry and tag parts are mostly <= 8 bytes.
 template <bool BATCH>
 __device__ inline uint32_t lit_lookup_short(const uint8_t* rec, const uint8_t* bytes, uint32_t b, uint32_t e) {
-  if (BATCH && KW_IMG_LIT_SHORT) {
+  if (BATCH) {
     if (!__ballot(e - b > 8u)) return lit_lookup<true, 2>(rec, bytes, b, e);
     if (!__ballot(e - b > 16u)) return lit_lookup<true, 4>(rec, bytes, b, e);
   }
@@ -186,11 +133,7 @@ __device__ inline uint32_t chain_kind(const Chain& c, uint32_t off) { return ((c
 // Byte offset of transition (st, class) in a [state][ncls] table of 2^sh-byte entries, with the class
 // pre-shifted (cq = class << sh): one 24-bit multiply-add on the transition chain (states and class
 // counts are < 65536, DevDfa / KvDfa), instead of a quarter-rate 32-bit multiply plus shifts.
-#if KW_MAD24
 __device__ inline uint32_t trans_at(uint32_t st, uint32_t ncls_sh, uint32_t cq) { return (uint32_t)__umul24(st, ncls_sh) + cq; }
-#else
-__device__ inline uint32_t trans_at(uint32_t st, uint32_t ncls_sh, uint32_t cq) { return st * ncls_sh + cq; }
-#endif
 // u16 transition at `at`: a byte offset from the table (global or generic tables), or, for tables
 // staged in LDS (L), the entry's LDS address itself (tr_base folded into the pre-shifted classes)
 template <bool L>
@@ -350,11 +293,7 @@ __device__ inline uint32_t classify_value_as(as_ptr<AS> R, uint32_t nlk, uint32_
     // 8-byte windows: the window's dwords, then its 8 byte classes, load as two batches; only the
     // transitions form a dependent chain (bytes past the string read the zero tail, unused); the
     // walk ends at a window starting in the dead state or an absorbing one
-#if KW_KV_ABSORB
     for (uint32_t p = b; p < e && dfa_live(st, d.abs_lo); p += 8u) {
-#else
-    for (uint32_t p = b; p < e && st != 0; p += 8u) {
-#endif
       const uint32_t* q = (const uint32_t*)(bytes + (p & ~3u));
       const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], sh = p & 3u;
       const uint32_t x0 = align_bytes(q1, q0, sh), x1 = align_bytes(q2, q1, sh);
@@ -367,22 +306,12 @@ __device__ inline uint32_t classify_value_as(as_ptr<AS> R, uint32_t nlk, uint32_
         // Classes come out as LDS byte addresses of their column in the transition table (tb +
         // class << t16), so a step is one 24-bit multiply-add and the load (trans_at).
         const uint32_t t16 = d.t16, tb = (uint32_t)(uintptr_t)(R + d.trans_off), ncs = (uint32_t)d.ncls << t16;
-#if KW_CLS129
         const uint32_t bm = 128u + (uint32_t)d.wide * 127u;  // narrow maps: entry 128 is the class of bytes >= 128 (wide: 0 / 1)
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const uint32_t by = ((i < 4 ? x0 : x1) >> (8 * (i & 3))) & 0xffu;
           c[i] = tb + ((uint32_t)R[d.cls_off + min(by, bm)] << t16);
         }
-#else
-        const uint32_t bm = d.wide ? 255u : 127u;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const uint32_t by = ((i < 4 ? x0 : x1) >> (8 * (i & 3))) & 0xffu;
-          const uint32_t cl = R[d.cls_off + (by & bm)];
-          c[i] = tb + ((by <= bm ? cl : (uint32_t)d.hi) << t16);
-        }
-#endif
         uint32_t fin = st;
         if (t16) {
 #pragma unroll
@@ -405,11 +334,7 @@ __device__ inline uint32_t classify_value_as(as_ptr<AS> R, uint32_t nlk, uint32_
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const uint32_t by = ((i < 4 ? x0 : x1) >> (8 * (i & 3))) & 0xffu;
-#if KW_CLS129
         c[i] = R[d.cls_off + min(by, 128u + (uint32_t)d.wide * 127u)];
-#else
-        c[i] = (by < 128u || d.wide) ? R[d.cls_off + by] : d.hi;
-#endif
       }
       const as_ptr<AS> tr = R + d.trans_off;
       if (d.t16) {
@@ -520,11 +445,7 @@ __device__ inline void copy_x4(const uint8_t* src, uint8_t* dst, uint32_t bytes,
 // instead of stalling every wave at the barrier (__syncthreads waits vmcnt(0)). Used where no
 // global load result is consumed across the barrier; the staging barrier (LDS-DMA, counted by
 // vmcnt) stays __syncthreads.
-#if KW_LDS_BARRIER
 __device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-#else
-__device__ inline void lds_barrier() { __syncthreads(); }
-#endif
 
 // L2 prefetch of `bytes` at `src`: one dword per 128-B line, by LDS-DMA from lanes 0..kPfLanes-1 of
 // each wave into a 4 x kPfLanes-byte scratch line shared by the waves (never read; a DMA lane lands at base + 4 x lane), so
@@ -541,15 +462,8 @@ __device__ inline void prefetch_l2(const void* src, uint32_t bytes, uint8_t* scr
 
 // TIMING: the diagnostics instantiation (EvalArgs::phase) — phase clocks add registers, so the
 // product kernel is compiled without them.
-// Minimum waves per SIMD the register allocation must allow: the image-only instantiation (C2) is
-// register-bound at 5 workgroups per CU (86 VGPRs) while its LDS allows 6 (KW_IMG_MIN_WAVES).
-template <bool LDST, uint32_t F>
-constexpr int tile_min_waves() {
-  return (LDST && F == kFeatImg) ? KW_IMG_MIN_WAVES : KW_MIN_WAVES;
-}
-
 template <bool LDST, bool TIMING, uint32_t F>
-__global__ void __launch_bounds__(kSlotThreads, (tile_min_waves<LDST, F>()))
+__global__ void __launch_bounds__(kSlotThreads, 1)
     evaluate_tiles_kernel(EvalArgs a, const TileArgs* __restrict__ tp, const TileDesc* __restrict__ desc) {
   // TileArgs lives in device memory: its fields are scalar-loaded where used instead of all being
   // hoisted from the kernarg segment into SGPRs at entry.
@@ -606,21 +520,14 @@ __global__ void __launch_bounds__(kSlotThreads, (tile_min_waves<LDST, F>()))
 #pragma unroll
   for (int c = 0; c < (int)NCOL; ++c) {
     uint32_t lo = LDST ? t.lit_lds[c] : t.lit_blob[c];
-#if KW_VBASE >= 2
-    if constexpr (!IMG && !GRP && LDST) asm("" : "+v"(lo));  // (KW_VBASE below)
-#else
     // the label-key and capability literal tables, probed in C4's hottest P1 loops
-    if constexpr (KW_VBASE && !IMG && !GRP && LDST)
+    if constexpr (!IMG && !GRP && LDST)
       if (c == COL_LK || c == COL_CAP) asm("" : "+v"(lo));
-#endif
     C.lit[c] = t.lit_blob[c] ? tb + lo : nullptr;
     C.dfa[c].head = t.dfa_blob[c];
     C.dfa[c].base = tb + (LDST ? t.dfa_lds[c] : t.dfa_blob[c]);
   }
   uint32_t kvo = t.kv_lds;
-#if KW_VBASE >= 2
-  if constexpr (!IMG && !GRP && LDST) asm("" : "+v"(kvo));
-#endif
   C.kv = t.kv_blob ? ((LDST && t.kv_lds) ? (const uint8_t*)lds + kvo : a.blob + t.kv_blob) : nullptr;  // kv_lds 0: global
   C.nlk = t.nlk;
   C.docker_io_cls = t.docker_io_cls;
@@ -633,13 +540,11 @@ __global__ void __launch_bounds__(kSlotThreads, (tile_min_waves<LDST, F>()))
   };
 
   // The tile's LDS regions. Where the instantiation's occupancy is bound by LDS with VGPRs to spare
-  // (KW_VBASE: the label / container families, C4 / C5 at <= 4 workgroups per CU), their offsets
+  // (the label / container families, C4 / C5 at <= 4 workgroups per CU), their offsets
   // are held in VGPRs: otherwise they are 24 more uniform values competing for the 102 SGPRs, and
   // the compiler spills SGPRs to VGPR lanes, each reload a v_readlane_b32 in the hot loops.
   auto region = [&](uint32_t off) -> uint8_t* {
-#if KW_VBASE
     if constexpr (!IMG && !GRP && LDST) asm("" : "+v"(off));
-#endif
     return lds + off;
   };
   uint8_t* l_rf = region(t.o_rf);
@@ -710,21 +615,11 @@ __global__ void __launch_bounds__(kSlotThreads, (tile_min_waves<LDST, F>()))
   for (uint32_t it = 0; tile < t_hi; ++it) {
     const uint32_t cur = it & 1u;
     uint32_t nxt2 = 0;
-#if !KW_LATE_ATOMIC
     if (dyn && tid == 0) nxt2 = atomicAdd(cnt, 1u);  // the tile after next (read after the staging barrier)
-#endif
     if (next < t_hi) fetch_desc(next, cur ^ 1u);      // the next tile's descriptor (slot free since its last read)
-#if KW_DESC_LDS
     const TileDesc& d = l_desc[cur];
 #define KW_DF(x) sfield(x)
-#else
-    const TileDesc& d = desc[tile];  // scalar loads (the LDS copy serves the prefetch)
-#define KW_DF(x) (x)
-#endif
     if (!KW_DF(d.fits)) {  // queued for the overflow kernels by the host (uniform: no barrier skipped unevenly)
-#if KW_LATE_ATOMIC
-      if (dyn && tid == 0) nxt2 = atomicAdd(cnt, 1u);
-#endif
       if (dyn && tid == 0) l_nx[cur] = nxt2;
       __syncthreads();  // also waits for the next descriptor
       tile = next;
@@ -762,13 +657,7 @@ __global__ void __launch_bounds__(kSlotThreads, (tile_min_waves<LDST, F>()))
     if (timing) sg_add(SG_P0_WAIT, clock64() - p0_end);
     mark(0);
     if (timing && tid == 0) ++ph[5];
-#if KW_LATE_ATOMIC
-    // the counter fetch for the tile after next: issued now, off the staging barrier's vmcnt(0); its
-    // value is stored to l_nx[cur] after P2 (the wave's only outstanding VMEM op there)
-    if (dyn && tid == 0) nxt2 = atomicAdd(cnt, 1u);
-#else
     if (dyn && tid == 0) l_nx[cur] = nxt2;  // read after this tile's last barrier
-#endif
     // the next tile's staged ranges into L2 (covered by this tile's classification, walk and stores),
     // from its descriptor in LDS
     auto prefetch_next = [&]() {
@@ -798,9 +687,6 @@ __global__ void __launch_bounds__(kSlotThreads, (tile_min_waves<LDST, F>()))
         }
       }
     };
-#if KW_PF_EARLY
-    prefetch_next();
-#endif
     const uint8_t* cfl = l_cflags + (cb & 3u);  // staged from the dword holding flag cb
     const bool classify = !(t.debug & 1u);  // diagnostics: skip classification (entities match nothing)
     auto str = [&](int m, uint32_t i, uint32_t* b, uint32_t* e) {
@@ -813,10 +699,8 @@ __global__ void __launch_bounds__(kSlotThreads, (tile_min_waves<LDST, F>()))
       if (!classify || !C.lit[c]) return 0u;
       uint32_t b, e;
       str(m, i, &b, &e);
-#if KW_LIT_SHORT
       // every string of the wave within 16 bytes (the common case): the 4-word batch
       if (!__ballot(e - b > 16u)) return lit_lookup<true, 4>(C.lit[c], lds + t.o_sb[m], b, e);
-#endif
       return lit_lookup<true>(C.lit[c], lds + t.o_sb[m], b, e);
     };
 
@@ -840,28 +724,8 @@ __global__ void __launch_bounds__(kSlotThreads, (tile_min_waves<LDST, F>()))
         if (LBL && w < ek) {  // label
           const uint32_t i = w;
           if (i >= n3) continue;
-#if KW_P1_HOIST
-          // the value's offsets do not depend on the key: loaded before its lookup; the key's deny
-          // row is issued before the value walk, each constraint row as its class comes out
-          uint32_t vb = 0, ve = 0;
-          if (t.o_sb[S_LV]) str(S_LV, i, &vb, &ve);
           const uint32_t k = lit(COL_LK, S_LK, i);
-          c_lk[i] = (uint16_t)(KW_LK_PACK && t.lk_pack ? k | ((h0.lbl && h0.mand_union ? sv0.lkmb(k) : 0xffu) << 8) : k);
-          uint16_t* lv = c_lv + i * nlv;
-          const bool lbl0 = h0.lbl != 0;
-          uint64_t vl = (lbl0 && k) ? sv0.row(T_DENY, k) : 0ull;
-          if (k && classify && t.o_sb[S_LV] && !(t.debug & 2048u)) {
-            classify_value(C, LDST && t.kv_lds, k, nlv, lds + t.o_sb[S_LV], vb, ve, [&](uint32_t j, uint32_t c) {
-              lv[j] = (uint16_t)c;
-              if (lbl0 && c != 0xffffu) vl |= sv0.row(T_FAIL, c);
-            });
-          } else {
-            for (uint32_t j = 0; j < nlv; ++j) lv[j] = 0xffffu;
-          }
-          l_vl[i] = vl;
-#else
-          const uint32_t k = lit(COL_LK, S_LK, i);
-          c_lk[i] = (uint16_t)(KW_LK_PACK && t.lk_pack ? k | ((h0.lbl && h0.mand_union ? sv0.lkmb(k) : 0xffu) << 8) : k);
+          c_lk[i] = (uint16_t)k;
           uint16_t* lv = c_lv + i * nlv;
           if (k && classify && t.o_sb[S_LV] && !(t.debug & 2048u)) {
             uint32_t b, e;
@@ -872,18 +736,17 @@ __global__ void __launch_bounds__(kSlotThreads, (tile_min_waves<LDST, F>()))
             for (uint32_t j = 0; j < nlv; ++j) lv[j] = 0xffffu;
           }
           l_vl[i] = dv_label(sv0, k, lv, nlv);
-#endif
         } else if (CTR && w < e0) {  // capability string: added ones first, then dropped ones
           const uint32_t k = w - ek;
           if (k >= nk) continue;
           if (k < nka) {
             const uint32_t cc = lit(COL_CAP, S_CAPADD, k);
             // single-chunk pass: the capability's mutation bit itself (P2 reads no class table)
-            c_add[k] = (uint16_t)((KW_P1_HOIST && t.nchunk == 1 && h0.caps) ? sv0.capmb(cc) : cc);
+            c_add[k] = (uint16_t)cc;
             l_vadd[k] = (h0.caps && h0.caps_strict) ? sv0.row(T_NACAP, cc) : 0ull;
           } else {
             const uint32_t dc = lit(COL_CAP, S_CAPDROP, k - nka);
-            c_drop[k - nka] = (uint16_t)((KW_P1_HOIST && t.nchunk == 1 && h0.caps) ? sv0.capmb(dc) : dc);
+            c_drop[k - nka] = (uint16_t)dc;
           }
         } else if (CTR && w < e1) {  // container (its added capabilities' sets stay in l_vadd: P2 ORs them)
           const uint32_t i = w - e0;
@@ -904,7 +767,7 @@ __global__ void __launch_bounds__(kSlotThreads, (tile_min_waves<LDST, F>()))
           if (classify && (fl & KW_CTR_HAS_IMAGE)) {
             uint32_t b, e;
             str(S_IMG, i, &b, &e);
-            classify_image<true, LDST && KW_IMG_LDSADDR, NFA>(C, il, lds + t.o_sb[S_IMG], b, e, [&](uint32_t j, uint32_t c) { ic[j] = (uint16_t)c; },
+            classify_image<true, LDST, NFA>(C, il, lds + t.o_sb[S_IMG], b, e, [&](uint32_t j, uint32_t c) { ic[j] = (uint16_t)c; },
                                  t.debug, NFA ? a.nfa_img + (uint64_t)(cb + i) * nim : nullptr);
           } else {
             for (uint32_t j = 0; j < nim; ++j) ic[j] = 0;
@@ -929,9 +792,7 @@ __global__ void __launch_bounds__(kSlotThreads, (tile_min_waves<LDST, F>()))
     lds_barrier();
     if (timing) sg_add(SG_P1_WAIT, clock64() - p1_end);
     mark(1);
-#if !KW_PF_EARLY
     prefetch_next();
-#endif
 
     for (uint32_t ck = 0; ck < t.nchunk; ++ck) {
       const SlotView sv = chunk_view(ck);
@@ -1042,13 +903,8 @@ __global__ void __launch_bounds__(kSlotThreads, (tile_min_waves<LDST, F>()))
             }
             if (CTR && SH.caps && !(t.debug & 8192u)) {  // mutation: required drops missing, default adds neither added nor dropped
               uint64_t addm = 0, dropm = 0;
-              if (KW_P1_HOIST && t.nchunk == 1) {  // P1 stored the mutation bits
-                for (uint32_t k = ka; k < ka1; ++k) addm |= bit_of(c_add[k]);
-                for (uint32_t k = l_cdrop[i] - kdb, k1 = l_cdrop[i + 1] - kdb; k < k1; ++k) dropm |= bit_of(c_drop[k]);
-              } else {
-                for (uint32_t k = ka; k < ka1; ++k) addm |= bit_of(sv.capmb(c_add[k]));
-                for (uint32_t k = l_cdrop[i] - kdb, k1 = l_cdrop[i + 1] - kdb; k < k1; ++k) dropm |= bit_of(sv.capmb(c_drop[k]));
-              }
+              for (uint32_t k = ka; k < ka1; ++k) addm |= bit_of(sv.capmb(c_add[k]));
+              for (uint32_t k = l_cdrop[i] - kdb, k1 = l_cdrop[i + 1] - kdb; k < k1; ++k) dropm |= bit_of(sv.capmb(c_drop[k]));
               const uint64_t mut = caps_mutation(sv, addm, dropm);
               if (mut) atomicOr((unsigned long long*)&l_mut[q], (unsigned long long)mut);
             }
@@ -1063,7 +919,7 @@ __global__ void __launch_bounds__(kSlotThreads, (tile_min_waves<LDST, F>()))
             for (uint32_t j = l0; j < i; ++j) pre |= l_vl[j];
             const uint64_t nv = v & ~pre;
             if (!nv || (t.debug & 16384u)) continue;
-            const uint64_t den = sv.row(T_DENY, KW_LK_PACK && t.lk_pack ? c_lk[i] & 0xffu : c_lk[i]);
+            const uint64_t den = sv.row(T_DENY, c_lk[i]);
             const uint32_t li = i - l0;
             ViolSink vs{l_vw + q * t.vw_stride, nullptr};
             vs.put(nv & den, KW_R_LABEL_DENIED, li);
@@ -1082,31 +938,10 @@ __global__ void __launch_bounds__(kSlotThreads, (tile_min_waves<LDST, F>()))
             }
             if (LBL && SH.lbl && SH.mand_union && !(t.debug & 1024u)) {
               uint64_t present = 0, lrej = 0;
-              if (KW_LK_PACK && t.lk_pack) {  // the keys' mandatory bits stored by P1, four labels a round
-                const uint32_t l0 = l_loff[i] - lb, l1 = l_loff[i + 1] - lb;
-                for (uint32_t l = l0; l < l1; l += 4u) {
-                  uint32_t kk[4];
-                  uint64_t vv[4];
-#pragma unroll
-                  for (int u = 0; u < 4; ++u) {
-                    const uint32_t x = l + (uint32_t)u < l1 ? l + (uint32_t)u : l0;
-                    kk[u] = c_lk[x];
-                    vv[u] = l_vl[x];
-                  }
-#pragma unroll
-                  for (int u = 0; u < 4; ++u)
-                    if (l + (uint32_t)u < l1) {
-                      present |= bit_of(kk[u] >> 8);
-                      lrej |= vv[u];
-                    }
-                }
-              } else {
-                for (uint32_t l = l_loff[i] - lb, l1 = l_loff[i + 1] - lb; l < l1; ++l) {
-                  present |= bit_of(sv.lkmb(c_lk[l]));
-                  lrej |= l_vl[l];
-                }
+              for (uint32_t l = l_loff[i] - lb, l1 = l_loff[i + 1] - lb; l < l1; ++l) {
+                present |= bit_of(sv.lkmb(c_lk[l]));
+                lrej |= l_vl[l];
               }
-#if KW_MAND_BATCH
               // slots missing a mandatory key: rows of the missing local bits, four loads per round
               uint64_t miss = SH.mand_union & ~present, nw = 0;
               const uint64_t* mt = sv.mand();
@@ -1138,15 +973,6 @@ __global__ void __launch_bounds__(kSlotThreads, (tile_min_waves<LDST, F>()))
                 for (int u = 0; u < 4; ++u)
                   if (ss[u] < 64u) vs.vw[ss[u]] = vword(KW_R_LABEL_MANDATORY, first_missing_packed(sv, ss[u], pk[u], present));
               }
-#else
-              uint64_t nw = tab_or(sv.mand(), SH.mand_union & ~present) & ~lrej;
-              rej |= nw;
-              while (nw) {  // the first missing mandatory key of each such slot, settings order
-                const uint32_t s = kw_ctz64(nw);
-                nw &= nw - 1;
-                vs.put(1ull << s, KW_R_LABEL_MANDATORY, first_missing(sv, s, present));
-              }
-#endif
             }
             if (rej) atomicOr((unsigned long long*)&l_rej[i], (unsigned long long)rej);
           }
@@ -1158,9 +984,6 @@ __global__ void __launch_bounds__(kSlotThreads, (tile_min_waves<LDST, F>()))
       lds_barrier();
       if (timing) sg_add(SG_P2_WAIT, clock64() - p2_end);
       mark(3);
-#if KW_LATE_ATOMIC
-      if (dyn && tid == 0 && ck == 0) l_nx[cur] = nxt2;  // read after this tile's last barrier
-#endif
 
       // ---- P3: verdict words. All-pairs: items = (request, 4 columns), 16 lanes per 256-B row,
       //      column records from LDS (group / constant columns from the record's global copy).
@@ -1220,12 +1043,8 @@ __global__ void __launch_bounds__(kSlotThreads, (tile_min_waves<LDST, F>()))
               wv.z = pw(c4.ks.z, c4.ok.z, c4.mu.z, c4.rj.z, 4 * g + 2);
               wv.w = pw(c4.ks.w, c4.ok.w, c4.mu.w, c4.rj.w, 4 * g + 3);
             }
-#if KW_NT_STORE
             const u32x4 nv4 = {wv.x, wv.y, wv.z, wv.w};
             __builtin_nontemporal_store(nv4, (u32x4*)dst);  // streamed once
-#else
-            *(uint4*)dst = wv;
-#endif
           };
           if ((G & (G - 1u)) == 0 && G <= kSlotThreads) {
             // G a power of two dividing the workgroup: each thread keeps one column group for every
@@ -1234,7 +1053,6 @@ __global__ void __launch_bounds__(kSlotThreads, (tile_min_waves<LDST, F>()))
             const Cols4 c4 = load4(g);
             uint32_t* dst = out + (r0 + (tid >> lg)) * npol + CA.col0 + 4 * g;
             const uint64_t dstep = (uint64_t)step * npol;
-#if KW_P3_BITS
             // (not in image-only instantiations: two more VGPRs there cross C2's 6-wave boundary, +8 %)
             if (!GRP && (LBL || CTR)) {
               // branch-free words from 32-bit halves: per column, the slot's rejected / mutated bits
@@ -1272,14 +1090,9 @@ __global__ void __launch_bounds__(kSlotThreads, (tile_min_waves<LDST, F>()))
                 }
                 u32x4 wv = {wk[0], wk[1], wk[2], wk[3]};
                 if (byp) wv = u32x4{kBypassWord, kBypassWord, kBypassWord, kBypassWord};
-#if KW_NT_STORE
                 __builtin_nontemporal_store(wv, (u32x4*)dst);  // streamed once
-#else
-                *(u32x4*)dst = wv;
-#endif
               }
             } else
-#endif
             if (!GRP) {
               // branch-free words: the thread's four columns are loop-invariant; every row reads its
               // four violation words whether or not the slot rejected, then selects
@@ -1300,11 +1113,7 @@ __global__ void __launch_bounds__(kSlotThreads, (tile_min_waves<LDST, F>()))
                 u32x4 wv = {one(pl0, cs0, a0, c4.ok.x, c4.mu.x, c4.rj.x), one(pl1, cs1, a1, c4.ok.y, c4.mu.y, c4.rj.y),
                             one(pl2, cs2, a2, c4.ok.z, c4.mu.z, c4.rj.z), one(pl3, cs3, a3, c4.ok.w, c4.mu.w, c4.rj.w)};
                 if (byp) wv = u32x4{kBypassWord, kBypassWord, kBypassWord, kBypassWord};
-#if KW_NT_STORE
                 __builtin_nontemporal_store(wv, (u32x4*)dst);  // streamed once
-#else
-                *(u32x4*)dst = wv;
-#endif
               }
             } else {
               for (uint32_t rr = tid >> lg; rr < nr; rr += step, dst += dstep) emit(rr, g, c4, dst);

@@ -106,8 +106,6 @@ struct TileArgs {
   uint32_t prefetch;                   // warm L2 with the next tile (small tiles at >= 3 workgroups per CU)
   uint32_t feat;                       // kFeat* families of the launch (selects the kernel instantiation)
   uint32_t ctr_ranges;                 // many containers per request: P2 ORs predecessor ranges four a round
-  uint32_t lk_pack;                    // single-chunk launch, < 256 label-key classes: P1 stores the key's
-                                       // mandatory local bit in the high byte of its class (P2 reads no table)
   uint32_t o_sa;                       // u32[NSTR]: the tile's staged byte start per string column
   uint32_t o_vw, vw_stride;            // violation words [rows][vw_stride] (aliases the staged strings)
   uint32_t o_so[NSTR], o_sb[NSTR], sb_cap[NSTR];  // staged string offsets / bytes (0 = not staged)
