@@ -20,7 +20,7 @@ HOST_SRCS := json yaml automaton expr env flatten service slotplan metrics capi
 HOST_OBJS := $(addprefix $(OBJ)/,$(addsuffix .o,$(HOST_SRCS)))
 HEADERS := $(wildcard $(SRC)/*.hpp) include/kwgpu.h
 
-all: $(PKG)/libkwgpu.so $(PKG)/libkwsynth.so $(PKG)/kwhost $(PKG)/kwload oracle/build/libkworacle.so scripts/lds_calib scripts/fmt_bench
+all: $(PKG)/libkwgpu.so $(PKG)/libkwsynth.so $(PKG)/kwhost $(PKG)/kwload oracle/build/libkworacle.so scripts/lds_calib scripts/lds_occ scripts/fmt_bench
 
 # kwhost's host stages (flatten, response JSON) timed without a GPU
 scripts/fmt_bench: scripts/fmt_bench.cpp include/kwgpu.h $(PKG)/libkwgpu.so $(PKG)/libkwsynth.so
@@ -28,6 +28,10 @@ scripts/fmt_bench: scripts/fmt_bench.cpp include/kwgpu.h $(PKG)/libkwgpu.so $(PK
 
 # LDS counter calibration micro-kernels (scripts/lds_calib.sh runs them under rocprofv3 --pmc)
 scripts/lds_calib: scripts/lds_calib.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -o $@ $<
+
+# LDS residency probe: workgroups a CU holds per dynamic LDS size (profiles/r05_lds_residency.txt)
+scripts/lds_occ: scripts/lds_occ.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -o $@ $<
 
 $(OBJ)/%.o: $(SRC)/%.cpp $(HEADERS)

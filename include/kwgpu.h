@@ -254,9 +254,19 @@ int kw_debug_host_walk(const kw_env *env, const kw_batch *b, const int32_t *poli
 
 /* Diagnostic (tests): plan an all-pairs pass over the batch's host columns without launching it.
  * out[0..8): LDS bytes per workgroup, launches, slot-plan chunks, classifiers staged in LDS (1) or
- * read from global memory (0), requests per tile, container / capability / label capacities. */
+ * read from global memory (0), requests per tile, container / capability / label capacities (of the
+ * first region). cap >= 16 adds out[8..15): regions (1, or 2 for a light / heavy split batch), the
+ * light region's rows, the first region's grid, the heavy region's LDS bytes, requests per tile,
+ * container capacity and grid. */
 int kw_debug_plan(const kw_env *env, kw_batch *b, const int32_t *policies, uint32_t npol, int origin, uint32_t *out,
                   int cap);
+
+/* Diagnostic (tests): the device-row order kw_batch_to_device gives this batch — the light / heavy
+ * split (rows with more than 5 containers after the others when they are 1-50 % of
+ * a batch of >= 2^18 rows and hold >= 30 % of its containers; KW_SPLIT=0 / 1 never / always) — as a
+ * new host batch *out in that order. *split: the light region's rows (0: not split, *out in batch
+ * order); perm[d] (cap >= rows) the batch row at device row d. */
+int kw_debug_reorder(const kw_batch *b, uint64_t *perm, size_t cap, uint64_t *split, kw_batch **out);
 
 /* ---------------------------------------------------------------------------------------------
  * The hot path: EvaluationEnvironment::validate + service::evaluate constraints, batched.

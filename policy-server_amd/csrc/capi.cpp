@@ -255,6 +255,13 @@ void parallel_copy_segs(const std::vector<CopySeg>& segs) {
 
 // Requests per tile of the tile kernel forced by KW_SLOT_ROWS (8..255, A/B knob), 0 = chosen per
 // batch (plan_pass: kSlotRows, or taller tiles where they keep enough workgroups per CU).
+// Tile height of a split batch's heavy region (KW_HEAVY_ROWS, A/B knob; 0: planned like any batch).
+uint32_t heavy_rows() {
+  const char* e = getenv("KW_HEAVY_ROWS");
+  const int v = e ? atoi(e) : 0;
+  return (v >= 8 && v <= 255) ? (uint32_t)v : 0u;
+}
+
 uint32_t slot_rows_forced() {
   const char* e = getenv("KW_SLOT_ROWS");  // read per pass (tests switch it between passes)
   const int v = e ? atoi(e) : 0;
@@ -274,6 +281,22 @@ bool l2_prefetch() {
 struct TileStats {
   uint32_t ctr = 0, lbl = 0, kadd = 0, kdrop = 0;
   uint32_t bytes[NSTR] = {};
+};
+
+// A split batch's entity maps (upload_batch, permute_batch): the source entity of each destination
+// entity, per level — what the upload gathers the string bytes by (gather_column).
+struct RowOrder {
+  const std::vector<uint64_t>* perm = nullptr;  // rows (DeviceBatch::perm)
+  std::vector<uint32_t> cmap, lmap, amap, dmap;  // containers, labels, added / dropped capabilities
+  uint64_t src(int m, uint64_t e) const {
+    switch (m) {
+      case S_NS: return (*perm)[e];
+      case S_CAPADD: return amap[e];
+      case S_CAPDROP: return dmap[e];
+      case S_LK: case S_LV: return lmap[e];
+      default: return cmap[e];
+    }
+  }
 };
 
 // Device copy of a batch: one allocation for the input columns, lazily sized verdict / plan /
@@ -300,6 +323,17 @@ struct DeviceBatch {
   uint32_t* verdicts = nullptr;
   size_t verdict_cap = 0;
   size_t last_verdicts = 0;
+  uint32_t last_row_words = 0;  // verdict words per row of the last pass (npol; rows mode 1)
+  // light / heavy split (upload_batch, split_rows): the device copy holds the batch's rows in
+  // another order — the light rows, then the heavy ones — and every device buffer indexed by row
+  // (verdicts, side data, the rows-mode column map) follows that order; kw_batch_verdicts and
+  // load_side_data scatter them back. perm[d]: the batch row at device row d; split: the light
+  // region's rows (0: not split); dev_b: the reordered batch the planner reads (its offsets only:
+  // the string bytes are dropped after the upload).
+  std::vector<uint64_t> perm;
+  uint64_t split = 0;
+  std::unique_ptr<Batch> dev_b;
+  std::unique_ptr<RowOrder> order;  // (until the upload's staging is filled)
   uint32_t loaded = 0;        // string columns (bits of Str) whose bytes are resident (kw_validate_host uploads only its pass's)
   uint32_t* sched = nullptr;  // tile counters (zeroed once; each launch leaves them zero)
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
@@ -322,6 +356,7 @@ struct DeviceBatch {
   std::vector<uint32_t> h_ovf;
   uint32_t n_overflow = 0;
   uint64_t ndesc = 0;
+  uint64_t reg_desc[2] = {0, 0}, reg_ndesc[2] = {0, 0};  // each region's descriptors within desc
   uint64_t desc_key = 0;
   bool desc_valid = false;   // D.desc holds the whole batch's descriptors for desc_key
   uint32_t needs_stride = 1;  // tile needs sampled every needs_stride-th tile (set by kw_validate_host)
@@ -359,7 +394,8 @@ struct DeviceBatch {
   // tile capacities of this batch (plan_pass), per tile height tried
   struct RowsPlan {
     uint32_t rows = 0;
-    uint32_t stride = 1;             // needs of every stride-th tile (kw_validate_host samples)
+    uint64_t lo = 0, hi = 0;         // the region's rows
+    uint32_t stride = 1;            // needs of every stride-th tile (kw_validate_host samples)
     std::vector<TileStats> need, q;  // per-tile needs and their quantiles
     uint64_t cap_key = 0;
     int cap_choice = -1;   // quantile index chosen for cap_key
@@ -486,10 +522,10 @@ constexpr uint32_t kTileLdsBudget = 160 * 1024;  // tile-kernel LDS per workgrou
 constexpr uint32_t kMaxTileEntities = 60000;    // per-request indices in a tile stay below ARG's 65535
 constexpr double kTileQuantiles[] = {1.0, 0.99995, 0.9999, 0.9995, 0.999, 0.998};  // capacity candidates
 
-// What each tile of `rows` requests stages: entity counts and the 16-B aligned byte span of each
-// string column.
-std::vector<TileStats> tile_needs(const Batch& B, uint32_t rows, uint32_t stride = 1) {
-  const uint64_t ntiles_all = (B.n + rows - 1) / rows;
+// What each tile of `rows` requests of rows [lo, hi) stages: entity counts and the 16-B aligned byte
+// span of each string column.
+std::vector<TileStats> tile_needs(const Batch& B, uint32_t rows, uint32_t stride, uint64_t lo, uint64_t hi) {
+  const uint64_t ntiles_all = (hi - lo + rows - 1) / rows;
   const uint64_t ntiles = (ntiles_all + stride - 1) / stride;  // sampled tiles: every stride-th
   std::vector<TileStats> v(ntiles);
   // tiles in ranges of 256 on the host workers (each tile's reads are cache misses: 1M requests
@@ -498,7 +534,7 @@ std::vector<TileStats> tile_needs(const Batch& B, uint32_t rows, uint32_t stride
   HostWorkers::get().run((size_t)((ntiles + kRange - 1) / kRange), [&](size_t q) {
   for (uint64_t j = q * kRange, t1 = std::min<uint64_t>(ntiles, (q + 1) * kRange); j < t1; ++j) {
     const uint64_t t = j * stride;
-    const uint64_t r0 = t * rows, r1 = std::min<uint64_t>(B.n, (t + 1) * rows);
+    const uint64_t r0 = lo + t * rows, r1 = std::min<uint64_t>(hi, lo + (t + 1) * rows);
     TileStats& st = v[j];
     st.ctr = B.ctr_off[r1] - B.ctr_off[r0];
     st.lbl = B.lbl_off[r1] - B.lbl_off[r0];
@@ -585,9 +621,18 @@ struct PassPlan {
   std::vector<TileArgs> tiles;                          // one per launch (record pointers filled at upload)
   std::vector<uint8_t> slot_blob;                       // the chunks' records, concatenated
   std::vector<uint32_t> slot_at;                        // offset of each chunk's record in slot_blob
-  TileArgs geom;
+  TileArgs geom;  // the first region's geometry (the fields every region shares)
   EvalArgs args;
   uint32_t grid = 0;
+  // tile geometry per region of the device rows: one, or the light and heavy regions of a split
+  // batch (DeviceBatch::split), each with its own capacities, LDS layout and grid; `tiles` holds
+  // region k's launches at [k * launches.size(), (k + 1) * launches.size())
+  struct Region {
+    uint64_t lo = 0, hi = 0;
+    TileArgs geom;
+    uint32_t grid = 0;
+  };
+  std::vector<Region> regions;
   uint32_t nwide = 0;
   std::vector<int32_t> wide_policy;
   std::vector<uint32_t> rowcol;  // rows mode
@@ -698,13 +743,16 @@ void plan_wide_groups(const Env& E, const std::vector<int32_t>& list, const std:
   }
 }
 
+// The rows the device holds, in device order: the reordered copy of a split batch, else the batch.
+const Batch& dev_rows(const kw_batch* kb) { return kb->dev && kb->dev->dev_b ? *kb->dev->dev_b : kb->b; }
+
 // Plan one pass: slot-plan chunks of the policy list, the launches they take, the tile geometry
 // and LDS layout, the kernel arguments.
 int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npol, const int32_t* row_policy,
               int origin, PassPlan* plan) {
   const Env& E = env->e;
   DeviceBatch& D = *kb->dev;
-  const Batch& B = kb->b;
+  const Batch& B = dev_rows(kb);
   const DevHeader* H = (const DevHeader*)E.blob.data();
   plan->env_blob = E.blob.data();
   plan->rows_mode = row_policy != nullptr;
@@ -728,8 +776,8 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
     for (uint32_t c = 0; c < plan->chunks.size(); ++c)
       for (uint32_t j = 0; j < plan->chunks[c].ncols; ++j) at[plan->chunks[c].col0 + j] = (c << 16) | j;
     plan_wide_groups(E, list, &at, origin, plan);
-    plan->rowcol.resize(B.n);
-    for (uint64_t r = 0; r < B.n; ++r) plan->rowcol[r] = at[col_of[row_policy[r]]];
+    plan->rowcol.resize(B.n);  // (in device-row order)
+    for (uint64_t r = 0; r < B.n; ++r) plan->rowcol[r] = at[col_of[row_policy[D.split ? D.perm[r] : r]]];
   }
   plan->nwide = 0;
   plan->wide_policy.clear();
@@ -895,25 +943,28 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
     }
     return T.lds_bytes;
   };
-  auto per_cu = [](uint32_t b) { return std::min<uint32_t>(2048 / kSlotThreads, (160 * 1024) / std::max<uint32_t>(b, 1)); };
+  auto per_cu = [](uint32_t b) { return std::min<uint32_t>(2048 / kSlotThreads, lds_workgroups_per_cu(b)); };
   // Capacities at a tile height: the highest occupancy (workgroups per CU, LDS-bound) whose layout
   // splits at most 2 % of the tiles (a tile beyond the capacities runs as halves, upload_tile_descs),
   // over per-dimension quantiles of the tile needs; at a given occupancy the largest capacities
   // (fewest split tiles). Chosen once per batch, tile height and layout signature.
   const uint64_t key = ((uint64_t)area << 40) ^ ((uint64_t)nslots << 20) ^ ((uint64_t)nim << 12) ^ ((uint64_t)nlv << 8) ^ need;
+  uint64_t rlo = 0, rhi = B.n;  // the region being planned
   auto plan_rows = [&](uint32_t r) -> DeviceBatch::RowsPlan& {
     DeviceBatch::RowsPlan* R = nullptr;
     for (auto& x : D.rows_plans)
-      if (x.rows == r) R = &x;
+      if (x.rows == r && x.lo == rlo && x.hi == rhi) R = &x;
     if (!R) {
       D.rows_plans.emplace_back();
       R = &D.rows_plans.back();
       R->rows = r;
+      R->lo = rlo;
+      R->hi = rhi;
       R->stride = 0;
     }
     if (R->stride == 0 || R->stride > D.needs_stride) {  // (a sampled plan is refined when a pass wants every tile)
       R->stride = std::max<uint32_t>(1, D.needs_stride);
-      R->need = tile_needs(B, r, R->stride);
+      R->need = tile_needs(B, r, R->stride, rlo, rhi);
       R->q = tile_quantiles(R->need, kTileQuantiles, sizeof(kTileQuantiles) / sizeof(kTileQuantiles[0]));
       R->cap_choice = -1;
     }
@@ -957,7 +1008,14 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
   // tile sends one wave through the segment twice, and its phase waits for that wave (r03: half of
   // C2 / C3's 128-row tiles had more than 256 images). Taller tiles amortise the per-tile latency
   // (staging, barriers) where the per-request LDS is small: C2 -12 %, C3 -25 % at 128 rows (r02);
-  // the C4-C6 layouts need 64 rows for 4 workgroups per CU (r02 sweeps).
+  // the C4-C6 layouts need 64 rows for 4 workgroups per CU (r02 sweeps). Per region: a split
+  // batch's light region takes the capacities (and occupancy) of its own tiles.
+  std::vector<std::pair<uint64_t, uint64_t>> bounds{{0, B.n}};
+  if (D.split && D.split < B.n) bounds = {{0, D.split}, {D.split, B.n}};
+  plan->regions.clear();
+  for (const auto& [lo, hi] : bounds) {
+  rlo = lo;
+  rhi = hi;
   const DeviceBatch::RowsPlan* pick = nullptr;
   const double round_split = getenv("KW_ROUND_SPLIT") ? atof(getenv("KW_ROUND_SPLIT")) : 0.02;  // A/B knob
   auto two_rounds = [&](const DeviceBatch::RowsPlan& R) {  // share of tiles with a segment beyond one round
@@ -973,6 +1031,21 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
   };
   if (const uint32_t f = slot_rows_forced()) {
     pick = &plan_rows(f);
+  } else if (lo > 0) {
+    // the heavy region of a split batch: the tallest tile height whose capacities reach the
+    // kernel's register-bound occupancy (<= 128 VGPRs: 4 workgroups of 256 threads per CU), else
+    // the one with the most workgroups per CU. r05 C5 sweep (profiles/r05_split_ab.txt): at equal
+    // occupancy taller tiles win (heavy > 5: 12 rows 6.31 ms, 10 rows 6.85), and a layout one
+    // workgroup per CU short loses 10-15 % whatever its height.
+    if (const uint32_t h = heavy_rows()) {
+      pick = &plan_rows(h);
+    } else {
+      for (uint32_t r : {64u, 48u, 40u, 32u, 28u, 24u, 20u, 16u, 14u, 12u, 10u, 8u}) {
+        const DeviceBatch::RowsPlan& R = plan_rows(r);
+        if (!pick || R.cap_cu > pick->cap_cu) pick = &R;
+        if (R.cap_cu >= 4) break;
+      }
+    }
   } else {
     const DeviceBatch::RowsPlan& base = plan_rows(kSlotRows);
     pick = &base;
@@ -980,9 +1053,9 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
     for (uint32_t r : {128u, 120u, 112u, 104u, 96u}) {
       const uint64_t est = fixed + (uint64_t)per64 * r / kSlotRows;
       if (getenv("KW_TILE_DEBUG") && (atoi(getenv("KW_TILE_DEBUG")) & 256))
-        fprintf(stderr, "[kw tile] rows=%u estimated lds=%llu (64-row layout %u, fixed %u) batch rows %llu\n", r,
-                (unsigned long long)est, base.cap_lds, fixed, (unsigned long long)B.n);
-      if (per_cu((uint32_t)std::min<uint64_t>(est, 1u << 30)) < 4 || B.n < (uint64_t)r * 4 * 256 * 4) continue;
+        fprintf(stderr, "[kw tile] rows=%u estimated lds=%llu (64-row layout %u, fixed %u) region rows %llu\n", r,
+                (unsigned long long)est, base.cap_lds, fixed, (unsigned long long)(rhi - rlo));
+      if (per_cu((uint32_t)std::min<uint64_t>(est, 1u << 30)) < 4 || rhi - rlo < (uint64_t)r * 4 * 256 * 4) continue;
       const DeviceBatch::RowsPlan& R = plan_rows(r);
       const double tr = two_rounds(R);
       if (getenv("KW_TILE_DEBUG") && (atoi(getenv("KW_TILE_DEBUG")) & 256))
@@ -1008,8 +1081,19 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
   // predecessor ranges four loads a round where tiles hold many containers per request (C5 -6 %;
   // C4, two per request, keeps the plain loops: r02 s80)
   T.ctr_ranges = T.cmax > 4u * T.rows ? 1u : 0u;
+  PassPlan::Region g;
+  g.lo = lo;
+  g.hi = hi;
+  g.geom = T;
+  const uint64_t nt = (hi - lo + T.rows - 1) / T.rows;
+  g.grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nt, 256ull * per_cu(T.lds_bytes)));
+  plan->regions.push_back(g);
+  }
   bool any_grp = false;
   for (const SlotChunk& c : plan->chunks) any_grp = any_grp || c.groups;
+  // the fields every region shares
+  for (PassPlan::Region& rg : plan->regions) {
+  T = rg.geom;
   T.feat = ((need & (1u << S_IMG)) ? kFeatImg : 0u) | (any_lbl ? kFeatLbl : 0u) | (any_ctr_fam ? kFeatCtr : 0u) |
            (any_grp ? kFeatGrp : 0u);
   // NFA elements among the classifiers the pass reads: the one instantiation that reads their classes
@@ -1082,8 +1166,11 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
             T.o_vadd - T.o_lv, T.o_vl - T.o_vadd, T.o_vc - T.o_vl, T.o_vtr - T.o_vc, T.o_own_c - T.o_vtr, T.o_rej - T.o_own_c,
             T.o_sa - T.o_rej, T.o_vw, so, sb, T.rows * T.vw_stride * 4, T.lds_bytes);
   }
+  rg.geom = T;
+  }
+  T = plan->regions[0].geom;
 
-  // ---- per-launch TileArgs (record pointers filled in at upload, run_pass)
+  // ---- per-launch TileArgs (record pointers filled in at upload, run_pass), region by region
   plan->slot_blob.clear();
   plan->slot_at.clear();
   for (const SlotChunk& c : plan->chunks) {
@@ -1091,8 +1178,9 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
     plan->slot_blob.insert(plan->slot_blob.end(), c.rec.begin(), c.rec.end());
   }
   plan->tiles.clear();
+  for (const PassPlan::Region& rg : plan->regions)
   for (const auto& [c0, c1] : plan->launches) {
-    TileArgs t = T;
+    TileArgs t = rg.geom;
     t.nchunk = c1 - c0;
     uint32_t at = 16 + table_bytes;
     for (uint32_t k = 0; k < t.nchunk; ++k) {
@@ -1140,18 +1228,17 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
     if (need & (1u << m)) eb += (double)D.str[m].nbytes + 4.0 * (double)D.str[m].n;
   plan->evaluate_bytes = eb;
 
-  const uint64_t ntiles = (B.n + T.rows - 1) / T.rows;
-  plan->grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ntiles, 256ull * per_cu(T.lds_bytes)));
+  plan->grid = plan->regions[0].grid;
   return KW_OK;
 }
 
 // Tile descriptors (kernels.hpp TileDesc) and the overflow list of one plan geometry, built from the
 // host copy of the batch and uploaded once; reused while the geometry stays the same.
-// The descriptors of tiles [t0, t1) of geometry T, in row order, and the requests that exceed the
+// The descriptors of tiles [t0, t1) of geometry T over rows [lo, hi), in row order, and the requests that exceed the
 // capacities alone (overflow); a run that does not fit is halved until its parts do. Tiles in ranges
 // of `range` on the host workers. KW_E_ARG when an overflow request index exceeds u32.
-int build_descs(const Batch& B, const TileArgs& T, uint64_t t0, uint64_t t1, uint64_t range, std::vector<TileDesc>* desc,
-                std::vector<uint32_t>* ovf) {
+int build_descs(const Batch& B, const TileArgs& T, uint64_t lo, uint64_t hi, uint64_t t0, uint64_t t1, uint64_t range,
+                std::vector<TileDesc>* desc, std::vector<uint32_t>* ovf) {
   // descriptor of requests [r0, r1); false when it exceeds the capacities
   auto make = [&](uint64_t r0, uint64_t r1, TileDesc* dp) {
     TileDesc& d = *dp;
@@ -1189,7 +1276,7 @@ int build_descs(const Batch& B, const TileArgs& T, uint64_t t0, uint64_t t1, uin
     std::vector<TileDesc>& dv = qdesc[q];
     dv.reserve((size_t)range + range / 64);
     for (uint64_t tile = t0 + q * range, te = std::min<uint64_t>(t1, t0 + (q + 1) * range); tile < te; ++tile) {
-      todo.assign(1, {tile * T.rows, std::min<uint64_t>(B.n, (tile + 1) * T.rows)});
+      todo.assign(1, {lo + tile * T.rows, std::min<uint64_t>(hi, lo + (tile + 1) * T.rows)});
       while (!todo.empty()) {
         const auto [r0, r1] = todo.back();
         todo.pop_back();
@@ -1215,25 +1302,37 @@ int build_descs(const Batch& B, const TileArgs& T, uint64_t t0, uint64_t t1, uin
   return KW_OK;
 }
 
-int upload_tile_descs(const Batch& B, DeviceBatch* D, const TileArgs& T, hipStream_t s) {
+int upload_tile_descs(const Batch& B, DeviceBatch* D, const PassPlan& plan, hipStream_t s) {
   uint64_t key = 1469598103934665603ull;
   auto mix = [&](uint64_t v) { key = (key ^ v) * 1099511628211ull; };
-  mix(T.rows);
-  mix(T.cmax);
-  mix(T.kmax);
-  mix(T.lmax);
-  for (int m = 0; m < (int)NSTR; ++m) {
-    mix(T.o_sb[m] != 0);
-    mix(T.sb_cap[m]);
+  for (const PassPlan::Region& rg : plan.regions) {
+    const TileArgs& T = rg.geom;
+    mix(rg.lo);
+    mix(rg.hi);
+    mix(T.rows);
+    mix(T.cmax);
+    mix(T.kmax);
+    mix(T.lmax);
+    for (int m = 0; m < (int)NSTR; ++m) {
+      mix(T.o_sb[m] != 0);
+      mix(T.sb_cap[m]);
+    }
   }
   if (D->desc && D->desc_valid && key == D->desc_key) return KW_OK;
   static const bool dbg = getenv("KW_BULK_DEBUG") && atoi(getenv("KW_BULK_DEBUG")) != 0;  // diagnostics
   const auto t0 = std::chrono::steady_clock::now();
-  const uint64_t ntiles = (B.n + T.rows - 1) / T.rows;
   std::vector<TileDesc> desc;
-  desc.reserve(ntiles + ntiles / 64 + 1);
   std::vector<uint32_t> ovf{0};
-  if (int rc = build_descs(B, T, 0, ntiles, 4096, &desc, &ovf)) return rc;
+  if (plan.regions.size() > 2) return KW_E_ARG;
+  uint64_t at[2] = {0, 0}, nd[2] = {0, 0};
+  for (size_t k = 0; k < plan.regions.size(); ++k) {  // region k's descriptors after region k-1's; one overflow list
+    const PassPlan::Region& rg = plan.regions[k];
+    const uint64_t ntiles = (rg.hi - rg.lo + rg.geom.rows - 1) / rg.geom.rows;
+    at[k] = desc.size();
+    desc.reserve(desc.size() + ntiles + ntiles / 64 + 1);
+    if (int rc = build_descs(B, rg.geom, rg.lo, rg.hi, 0, ntiles, 4096, &desc, &ovf)) return rc;
+    nd[k] = desc.size() - at[k];
+  }
   ovf[0] = (uint32_t)(ovf.size() - 1);
   const auto t1 = std::chrono::steady_clock::now();
   HIPCHK(hipStreamSynchronize(s));  // a running pass may still read the previous descriptors
@@ -1244,6 +1343,10 @@ int upload_tile_descs(const Batch& B, DeviceBatch* D, const TileArgs& T, hipStre
   if (!D->h_desc.empty())
     HIPCHK(hipMemcpyAsync(D->desc, D->h_desc.data(), D->h_desc.size() * sizeof(TileDesc), hipMemcpyHostToDevice, s));
   D->ndesc = D->h_desc.size();
+  for (int k = 0; k < 2; ++k) {
+    D->reg_desc[k] = at[k];
+    D->reg_ndesc[k] = nd[k];
+  }
   HIPCHK(hipMemcpyAsync(D->overflow, D->h_ovf.data(), D->h_ovf.size() * sizeof(uint32_t), hipMemcpyHostToDevice, s));
   D->n_overflow = D->h_ovf[0];
   D->desc_key = key;
@@ -1323,7 +1426,7 @@ int ensure_nfa(kw_batch* kb, PassPlan& plan, EvalArgs* A) {
 // side-data buffers; *out_args: the launch arguments.
 int prepare_pass(kw_batch* kb, PassPlan& plan, hipStream_t s, EvalArgs* out_args, bool descs = true) {
   DeviceBatch& D = *kb->dev;
-  const Batch& B = kb->b;
+  const Batch& B = dev_rows(kb);
   if (D.cur && D.cur != s) HIPCHK(hipStreamSynchronize(D.cur));  // order against the previous pass's stream
   D.cur = s;
   // plan upload: records, per-launch TileArgs (with their record pointers), rows-mode column map
@@ -1331,7 +1434,7 @@ int prepare_pass(kw_batch* kb, PassPlan& plan, hipStream_t s, EvalArgs* out_args
   if (int rc = ensure(&D.d_tiles, &D.d_tiles_cap, plan.tiles.size())) return rc;
   for (size_t l = 0; l < plan.tiles.size(); ++l)
     for (uint32_t k = 0; k < plan.tiles[l].nchunk; ++k)
-      plan.tiles[l].chunk[k].rec = D.d_slots + plan.slot_at[plan.launches[l].first + k];
+      plan.tiles[l].chunk[k].rec = D.d_slots + plan.slot_at[plan.launches[l % plan.launches.size()].first + k];
   if (D.h_slots != plan.slot_blob || D.h_tiles.size() != plan.tiles.size() ||
       (!plan.tiles.empty() && std::memcmp(D.h_tiles.data(), plan.tiles.data(), plan.tiles.size() * sizeof(TileArgs)) != 0)) {
     HIPCHK(hipStreamSynchronize(s));  // a running pass may still read the previous plan
@@ -1351,11 +1454,12 @@ int prepare_pass(kw_batch* kb, PassPlan& plan, hipStream_t s, EvalArgs* out_args
     A.rowcol = D.rowcol;
   }
   if (descs) {
-    if (int rc = upload_tile_descs(B, &D, plan.geom, s)) return rc;
+    if (int rc = upload_tile_descs(B, &D, plan, s)) return rc;
   } else {  // the caller builds and uploads descriptors per row chunk (kw_validate_host)
     HIPCHK(hipStreamSynchronize(s));  // a running pass may still read the previous descriptors
     D.desc_valid = false;
     D.ndesc = 0;
+    D.reg_ndesc[0] = D.reg_ndesc[1] = 0;
     D.n_overflow = 0;
   }
   A.ndesc = D.ndesc;
@@ -1401,6 +1505,7 @@ int prepare_pass(kw_batch* kb, PassPlan& plan, hipStream_t s, EvalArgs* out_args
   D.last_nwide = plan.nwide;
   D.last_wide_policy = plan.wide_policy;
   D.last_rows_mode = plan.rows_mode;
+  D.last_row_words = plan.args.npol;
   D.last_wide_cap = A.wide_cap;
   *out_args = A;
   return KW_OK;
@@ -1413,29 +1518,38 @@ int run_pass(kw_batch* kb, PassPlan& plan, bool timed, hipStream_t s) {
   // diagnostics: per-phase clocks of the tile kernel (KW_TILE_DEBUG & 512), printed per launch
   const bool phases = (plan.geom.debug & 512u) != 0;
   void* d_phase = nullptr;
-  const size_t phase_bytes = (size_t)plan.grid * kPhaseWords * sizeof(uint64_t);
+  uint32_t gmax = 0;
+  for (const PassPlan::Region& rg : plan.regions) gmax = std::max(gmax, rg.grid);
+  const size_t phase_bytes = (size_t)gmax * kPhaseWords * sizeof(uint64_t);
   if (phases) {
     HIPCHK(hipMalloc(&d_phase, phase_bytes));
     A.phase = (uint64_t*)d_phase;
   }
   if (timed) HIPCHK(hipEventRecord(D.ev[0], s));
   if (plan.geom.feat & kFeatNfa) HIPCHK(launch_nfa_classify(A, D.d_tiles, plan.nfa, plan.nfa_threads, s));
+  // region by region (a split batch: the light rows' launches, then the heavy rows'), each over its
+  // own descriptors; the overflow kernels after the last region, over the one overflow list
+  const size_t nl = plan.launches.size();
   for (size_t l = 0; l < plan.tiles.size(); ++l) {
+    const size_t k = l / nl;
     if (phases) HIPCHK(hipMemsetAsync(d_phase, 0, phase_bytes, s));
-    HIPCHK(launch_evaluate_tiles(A, plan.tiles[l], D.d_tiles + l, D.desc, plan.grid, s));
+    const uint32_t grid = plan.regions[k].grid;
+    EvalArgs Ak = A;
+    Ak.ndesc = D.reg_ndesc[k];
+    HIPCHK(launch_evaluate_tiles(Ak, plan.tiles[l], D.d_tiles + l, D.desc + D.reg_desc[k], grid, s));
     if (phases) {
-      std::vector<uint64_t> ph((size_t)plan.grid * kPhaseWords);
-      HIPCHK(hipMemcpyAsync(ph.data(), d_phase, phase_bytes, hipMemcpyDeviceToHost, s));
+      std::vector<uint64_t> ph((size_t)grid * kPhaseWords);
+      HIPCHK(hipMemcpyAsync(ph.data(), d_phase, ph.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
       double sum[kPhaseWords] = {0};
-      for (uint32_t g = 0; g < plan.grid; ++g)
+      for (uint32_t g = 0; g < grid; ++g)
         for (uint32_t k = 0; k < kPhaseWords; ++k) sum[k] += (double)ph[(size_t)g * kPhaseWords + k];
       const double tiles = std::max(1.0, sum[5]);
       fprintf(stderr,
               "[kw phase] launch %zu grid %u tiles %.0f: cycles/tile P0 %.0f P1 %.0f D %.0f P2 %.0f P3+next %.0f "
               "(sum %.0f); per workgroup: %.0f cycles, %.2f tiles, table staging %.0f\n",
-              l, plan.grid, tiles, sum[0] / tiles, sum[1] / tiles, sum[2] / tiles, sum[3] / tiles, sum[4] / tiles,
-              (sum[0] + sum[1] + sum[2] + sum[3] + sum[4]) / tiles, sum[6] / plan.grid, tiles / plan.grid, sum[7] / plan.grid);
+              l, grid, tiles, sum[0] / tiles, sum[1] / tiles, sum[2] / tiles, sum[3] / tiles, sum[4] / tiles,
+              (sum[0] + sum[1] + sum[2] + sum[3] + sum[4]) / tiles, sum[6] / grid, tiles / grid, sum[7] / grid);
       // per wave and tile: P1 / P2 segment cycles, each phase's busy time and its barrier wait
       const double wt = tiles * (double)(kSlotThreads / 64u);
       const double* g = sum + 8;
@@ -1445,8 +1559,16 @@ int run_pass(kw_batch* kb, PassPlan& plan, bool timed, hipStream_t s) {
               g[SG_P0_WAIT] / wt, g[SG_P1_BUSY] / wt, g[SG_P1_WAIT] / wt, g[SG_P1_LABEL] / wt, g[SG_P1_CAPSTR] / wt,
               g[SG_P1_CTR] / wt, g[SG_P1_IMAGE] / wt, g[SG_P1_REQ] / wt, g[SG_P2_BUSY] / wt, g[SG_P2_WAIT] / wt,
               g[SG_P2_CTR] / wt, g[SG_P2_LABEL] / wt, g[SG_P2_REQ] / wt, g[SG_P3_BUSY] / wt, g[SG_P3_WAIT] / wt);
+      // workgroup start times: a grid the CUs do not hold at once starts in waves
+      std::vector<uint64_t> st(grid);
+      for (uint32_t q = 0; q < grid; ++q) st[q] = ph[(size_t)q * kPhaseWords + 8 + SG_START];
+      std::sort(st.begin(), st.end());
+      uint32_t late = 0;
+      for (uint64_t x : st) late += x > st[0] + 2000;  // > 20 us after the first
+      fprintf(stderr, "[kw start] launch %zu: %u of %u workgroups started > 20 us after the first (spread %.1f us)\n", l, late,
+              grid, (double)(st.back() - st[0]) / 100.0);
     }
-    if (D.n_overflow) HIPCHK(launch_overflow(A, D.d_tiles + l, D.overflow, D.n_overflow, s));
+    if (D.n_overflow && k + 1 == plan.regions.size()) HIPCHK(launch_overflow(A, D.d_tiles + l, D.overflow, D.n_overflow, s));
   }
   if (timed) HIPCHK(hipEventRecord(D.ev[2], s));
   if (phases) HIPCHK(hipFree(d_phase));
@@ -2003,11 +2125,128 @@ struct Piece {
   size_t at;     // offset in the device image and in the pinned staging
   PieceKind kind;
   int m;         // string column (PK_STR_*), else -1
+  bool gather;   // string bytes of a reordered batch (gather_column), src null
 };
 
 // Allocates the batch's device image (one pooled allocation, 256-B aligned sub-arrays) and its
 // pinned staging block, and points the DeviceBatch views at it; nothing is copied.
-int layout_batch(kw_batch* kb, int device, hipStream_t stream, std::vector<Piece>* pieces) {
+// ---- light / heavy split at upload. A batch whose container counts
+// are heavy-tailed (C5: Zipf over 1..64 — 14.7 % of the requests hold 63 % of the containers) sizes
+// every tile's capacities, and so the occupancy, by the heavy requests scattered through it. The
+// device copy instead holds the light requests (<= kHeavyCtr containers) first and the heavy ones
+// after them, in batch order within each region; the planner gives each region its own tile
+// geometry (plan_pass), and verdicts and side data are scattered back to batch rows on the host.
+constexpr uint32_t kHeavyCtr = 5;
+constexpr uint64_t kSplitMinRows = 1ull << 18;
+
+// The light region's row count and the device-row order (perm[d] = batch row), or 0 when the batch
+// stays in order: the heavy rows must be between 1 % and 50 % of the rows and hold at least 30 % of
+// the containers, in a batch of at least kSplitMinRows rows. KW_SPLIT=0 never splits, KW_SPLIT=1
+// splits whenever both regions are non-empty (tests).
+uint64_t split_rows(const Batch& B, std::vector<uint64_t>* perm) {
+  const char* env = getenv("KW_SPLIT");
+  const int mode = env ? atoi(env) : -1;
+  if (mode == 0 || B.n == 0) return 0;
+  const char* hc = getenv("KW_HEAVY_CTR");  // A/B knob: the container count above which a request is heavy
+  const uint32_t thr = hc && atoi(hc) > 0 ? (uint32_t)atoi(hc) : kHeavyCtr;
+  auto heavy = [&](uint64_t r) { return B.ctr_off[r + 1] - B.ctr_off[r] > thr; };
+  uint64_t nh = 0, ch = 0;
+  for (uint64_t r = 0; r < B.n; ++r)
+    if (heavy(r)) ++nh, ch += B.ctr_off[r + 1] - B.ctr_off[r];
+  if (nh == 0 || nh == B.n) return 0;
+  if (mode != 1 && (B.n < kSplitMinRows || nh * 100 < B.n || nh * 2 > B.n || ch * 10 < 3ull * B.containers())) return 0;
+  perm->resize(B.n);
+  uint64_t l = 0, h = B.n - nh;
+  for (uint64_t r = 0; r < B.n; ++r) (*perm)[heavy(r) ? h++ : l++] = r;
+  return B.n - nh;
+}
+
+// Batch rows in `perm` order as a new batch (P's row d = B's row perm[d]). with_bytes false: the
+// device string columns get their offsets only — the upload gathers their bytes straight into its
+// staging (gather_column) — and the host-only string columns stay empty. *order: the entity maps.
+constexpr uint64_t kGatherTask = 1 << 16;
+size_t gather_tasks(uint64_t m) { return (size_t)((m + kGatherTask - 1) / kGatherTask); }
+
+void permute_batch(const Batch& B, const std::vector<uint64_t>& perm, Batch* P, bool with_bytes, RowOrder* order) {
+  const uint64_t n = B.n;
+  RowOrder& o = *order;
+  o.perm = &perm;
+  // an entity level: the destination offsets per parent and the source entity of each destination one
+  auto level = [&](const std::vector<uint32_t>& off, uint64_t np, auto parent, std::vector<uint32_t>* doff,
+                   std::vector<uint32_t>* emap) {
+    doff->resize(np + 1);
+    (*doff)[0] = 0;
+    for (uint64_t d = 0; d < np; ++d) {
+      const uint64_t p = parent(d);
+      (*doff)[d + 1] = (*doff)[d] + (off[p + 1] - off[p]);
+    }
+    emap->resize((*doff)[np]);
+    HostWorkers::get().run(gather_tasks(np), [&](size_t q) {
+      for (uint64_t d = q * kGatherTask, e = std::min<uint64_t>(np, (q + 1) * kGatherTask); d < e; ++d) {
+        const uint32_t s0 = off[parent(d)];
+        for (uint32_t k = 0, c = (*doff)[d + 1] - (*doff)[d]; k < c; ++k) (*emap)[(*doff)[d] + k] = s0 + k;
+      }
+    });
+  };
+  auto gather_str = [&](const StrCol& src, uint64_t ne, auto map, StrCol* dst) {
+    dst->off.resize(ne + 1);
+    dst->off[0] = 0;
+    for (uint64_t e = 0; e < ne; ++e) {
+      const uint64_t s = map(e);
+      dst->off[e + 1] = dst->off[e] + (src.off[s + 1] - src.off[s]);
+    }
+    if (!with_bytes) return;
+    dst->bytes.assign(dst->off[ne], 0);
+    HostWorkers::get().run(gather_tasks(ne), [&](size_t q) {
+      for (uint64_t e = q * kGatherTask, f = std::min<uint64_t>(ne, (q + 1) * kGatherTask); e < f; ++e) {
+        const uint64_t s = map(e);
+        memcpy(dst->bytes.data() + dst->off[e], src.bytes.data() + src.off[s], src.off[s + 1] - src.off[s]);
+      }
+    });
+  };
+  P->n = n;
+  auto row = [&](uint64_t d) { return perm[d]; };
+  P->req_flags.resize(n);
+  for (uint64_t d = 0; d < n; ++d) P->req_flags[d] = B.req_flags[perm[d]];
+  gather_str(B.ns, n, row, &P->ns);
+  if (with_bytes)
+    for (auto [s, t] : {std::pair<const StrCol*, StrCol*>(&B.uid, &P->uid), std::pair<const StrCol*, StrCol*>(&B.op, &P->op),
+                        std::pair<const StrCol*, StrCol*>(&B.kind, &P->kind), std::pair<const StrCol*, StrCol*>(&B.rkind, &P->rkind)})
+      gather_str(*s, n, row, t);
+  level(B.ctr_off, n, row, &P->ctr_off, &o.cmap);
+  level(B.lbl_off, n, row, &P->lbl_off, &o.lmap);
+  const uint64_t nc = o.cmap.size(), nl = o.lmap.size();
+  auto ctr = [&](uint64_t e) { return (uint64_t)o.cmap[e]; };
+  auto lbl = [&](uint64_t e) { return (uint64_t)o.lmap[e]; };
+  P->ctr_flags.resize(nc);
+  for (uint64_t e = 0; e < nc; ++e) P->ctr_flags[e] = B.ctr_flags[o.cmap[e]];
+  gather_str(B.ctr_image, nc, ctr, &P->ctr_image);
+  gather_str(B.ctr_aa, nc, ctr, &P->ctr_aa);
+  if (with_bytes) gather_str(B.ctr_name, nc, ctr, &P->ctr_name);
+  level(B.capadd_off, nc, ctr, &P->capadd_off, &o.amap);
+  level(B.capdrop_off, nc, ctr, &P->capdrop_off, &o.dmap);
+  gather_str(B.cap_add, o.amap.size(), [&](uint64_t e) { return (uint64_t)o.amap[e]; }, &P->cap_add);
+  gather_str(B.cap_drop, o.dmap.size(), [&](uint64_t e) { return (uint64_t)o.dmap[e]; }, &P->cap_drop);
+  gather_str(B.lbl_key, nl, lbl, &P->lbl_key);
+  gather_str(B.lbl_val, nl, lbl, &P->lbl_val);
+  if (with_bytes) P->finalize();
+}
+
+// String column m of the reordered batch P into `dst` (a piece of `bytes` bytes of the upload
+// staging): every string from B by the entity maps, then the zero tail.
+void gather_column(const Batch& B, const Batch& P, const RowOrder& o, int m, uint8_t* dst, size_t bytes) {
+  const StrCol &s = host_str(B, m), &d = host_str(P, m);
+  const uint64_t ne = d.n();
+  HostWorkers::get().run(gather_tasks(ne), [&](size_t q) {
+    for (uint64_t e = q * kGatherTask, f = std::min<uint64_t>(ne, (q + 1) * kGatherTask); e < f; ++e) {
+      const uint64_t x = o.src(m, e);
+      memcpy(dst + d.off[e], s.bytes.data() + s.off[x], s.off[x + 1] - s.off[x]);
+    }
+  });
+  if (bytes > d.off[ne]) memset(dst + d.off[ne], 0, bytes - d.off[ne]);
+}
+
+int layout_batch(kw_batch* kb, int device, hipStream_t stream, std::vector<Piece>* pieces, bool may_split = false) {
   if (!kb || device < 0) return KW_E_ARG;
   HIPCHK(hipSetDevice(device));
   if (kb->dev) kb->dev.reset();  // re-upload: the previous device copy returns to the pools
@@ -2019,13 +2258,23 @@ int layout_batch(kw_batch* kb, int device, hipStream_t stream, std::vector<Piece
   } else {
     HIPCHK(stream_pool().get(device, &D->stream));
   }
-  Batch& B = kb->b;
-  B.finalize();
+  kb->b.finalize();
+  if (may_split) {
+    D->split = split_rows(kb->b, &D->perm);
+    if (D->split) {
+      D->dev_b = std::make_unique<Batch>();
+      D->order = std::make_unique<RowOrder>();
+      permute_batch(kb->b, D->perm, D->dev_b.get(), /*with_bytes=*/false, D->order.get());
+    } else {
+      D->perm.clear();
+    }
+  }
+  const Batch& B = D->dev_b ? *D->dev_b : kb->b;
   pieces->clear();
   size_t total = 0;
   auto add = [&](const void* src, size_t bytes, PieceKind k, int m) {
     size_t at = total;
-    pieces->push_back({src, bytes, at, k, m});
+    pieces->push_back({src, bytes, at, k, m, false});
     total += (bytes + 255) & ~(size_t)255;
     return at;
   };
@@ -2039,7 +2288,12 @@ int layout_batch(kw_batch* kb, int device, hipStream_t stream, std::vector<Piece
   for (int m = 0; m < (int)NSTR; ++m) {
     const StrCol& c = host_str(B, m);
     c_off[m] = add(c.off.data(), c.off.size() * 4, PK_STR_OFF, m);
-    c_bytes[m] = add(c.bytes.data(), c.bytes.size(), PK_STR_BYTES, m);
+    if (D->order) {  // reordered: gathered into the staging at upload (>= 16 B zero tail, StrCol::pad)
+      c_bytes[m] = add(nullptr, ((size_t)c.off.back() + 31) & ~(size_t)15, PK_STR_BYTES, m);
+      pieces->back().gather = true;
+    } else {
+      c_bytes[m] = add(c.bytes.data(), c.bytes.size(), PK_STR_BYTES, m);
+    }
   }
   total = std::max<size_t>(total, 256);
   void* dcols = nullptr;
@@ -2069,11 +2323,17 @@ int layout_batch(kw_batch* kb, int device, hipStream_t stream, std::vector<Piece
 
 int upload_batch(kw_batch* kb, int device, hipStream_t stream, bool sync) {
   std::vector<Piece> pieces;
-  if (int rc = layout_batch(kb, device, stream, &pieces)) return rc;
+  if (int rc = layout_batch(kb, device, stream, &pieces, /*may_split=*/true)) return rc;
   DeviceBatch& D = *kb->dev;
   uint8_t* st = (uint8_t*)D.staging;
-  for (auto& p : pieces)
-    if (p.bytes) parallel_copy(st + p.at, p.src, p.bytes);
+  for (auto& p : pieces) {
+    if (!p.bytes) continue;
+    if (p.gather)
+      gather_column(kb->b, *D.dev_b, *D.order, p.m, st + p.at, p.bytes);
+    else
+      parallel_copy(st + p.at, p.src, p.bytes);
+  }
+  D.order.reset();  // (the planner reads the reordered batch's offsets only)
   HIPCHK(hipMemcpyAsync(D.cols, st, D.cols_bytes, hipMemcpyHostToDevice, D.stream));
   if (sync) HIPCHK(hipStreamSynchronize(D.stream));
   D.loaded = ~0u;
@@ -2129,11 +2389,25 @@ int load_side_data(kw_batch* b, hipStream_t s) {
       HIPCHK(hipMemcpyAsync(W.groups.data(), D.wide_groups, W.groups.size() * 8, hipMemcpyDeviceToHost, s));
   }
   HIPCHK(hipStreamSynchronize(s));
+  if (D.split) {  // device-row order (light / heavy split) -> batch rows
+    auto unperm = [&](std::vector<uint64_t>* v, uint32_t stride) {
+      if (v->empty() || !stride) return;
+      std::vector<uint64_t> t(v->size());
+      for (uint64_t d = 0; d < b->b.n; ++d)
+        std::copy_n(v->data() + d * stride, stride, t.data() + D.perm[d] * stride);
+      v->swap(t);
+    };
+    unperm(&W.big, W.big_stride);
+    unperm(&W.groups, W.nwide);
+  }
   nrec = std::min(nrec, D.last_wide_cap);
   if (nrec) {
     std::vector<WideRec> rec(nrec);
     HIPCHK(hipMemcpy(rec.data(), D.wide_rec, nrec * sizeof(WideRec), hipMemcpyDeviceToHost));
-    for (const WideRec& r : rec) W.recs.push_back({(uint64_t)r.row_lo | ((uint64_t)r.row_hi << 32), (int32_t)r.policy, r.value});
+    for (const WideRec& r : rec) {
+      const uint64_t d = (uint64_t)r.row_lo | ((uint64_t)r.row_hi << 32);
+      W.recs.push_back({D.split ? D.perm[d] : d, (int32_t)r.policy, r.value});
+    }
     std::sort(W.recs.begin(), W.recs.end(), [](const WideData::Rec& x, const WideData::Rec& y) {
       return x.row < y.row || (x.row == y.row && x.policy < y.policy);
     });
@@ -2326,7 +2600,7 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
     const auto td = clk::now();
     cd.clear();
     co.assign(1, 0u);
-    if (code(build_descs(B, G, tb[k], tb[k + 1], 128, &cd, &co))) break;
+    if (code(build_descs(B, G, 0, B.n, tb[k], tb[k + 1], 128, &cd, &co))) break;
     co[0] = (uint32_t)(co.size() - 1);
     if (cd.size() > dcap) {  // more split tiles than the halves hold: wait for every launch, regrow
       if (fail(hipStreamSynchronize(s_in)) || fail(hipStreamSynchronize(sc))) break;
@@ -2496,7 +2770,27 @@ int kw_batch_verdicts(kw_batch* b, uint32_t* host_out, size_t count) {
   hipStream_t s = D.cur ? D.cur : D.stream;
   const size_t vbytes = count * sizeof(uint32_t);
   constexpr size_t kBounce = (size_t)64 << 20;
-  if (vbytes > ((size_t)16 << 20)) {
+  if (D.split && count) {
+    // rows in device order (light / heavy split): whole device rows through a pinned bounce block,
+    // each scattered to its batch row's words below `count`
+    const uint64_t rw = std::max<uint32_t>(D.last_row_words, 1), nrows = D.last_verdicts / rw;
+    const uint64_t per = std::max<uint64_t>(1, kBounce / (rw * 4));
+    void* bounce = nullptr;
+    HIPCHK(host_pool().alloc(D.device, kBounce, &bounce));
+    for (uint64_t d0 = 0; d0 < nrows; d0 += per) {
+      const uint64_t d1 = std::min(nrows, d0 + per);
+      HIPCHK(hipMemcpyAsync(bounce, D.verdicts + d0 * rw, (d1 - d0) * rw * 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      const uint32_t* src = (const uint32_t*)bounce;
+      HostWorkers::get().run((size_t)((d1 - d0 + 4095) / 4096), [&](size_t q) {
+        for (uint64_t d = d0 + q * 4096, e = std::min(d1, d0 + (q + 1) * 4096); d < e; ++d) {
+          const uint64_t w0 = D.perm[d] * rw;
+          if (w0 < count) memcpy(host_out + w0, src + (d - d0) * rw, std::min<uint64_t>(rw, count - w0) * 4);
+        }
+      });
+    }
+    host_pool().release(D.device, bounce, kBounce);
+  } else if (vbytes > ((size_t)16 << 20)) {
     // large read-backs through a pinned bounce block (full-rate DMA), fanned out to the caller's
     // (pageable) buffer by several threads
     void* bounce = nullptr;
@@ -2517,11 +2811,22 @@ int kw_batch_verdicts(kw_batch* b, uint32_t* host_out, size_t count) {
 int kw_debug_plan(const kw_env* env, kw_batch* kb, const int32_t* policies, uint32_t npol, int origin, uint32_t* out,
                   int cap) {
   if (!env || !kb || !out || cap < 8 || (!policies && npol)) return KW_E_ARG;
-  // plan against a host view of the batch (no device memory, nothing launched)
+  // plan against a host view of the batch (no device memory, nothing launched), in the device-row
+  // order kw_batch_to_device would give it
   std::unique_ptr<DeviceBatch> saved = std::move(kb->dev);
-  Batch& B = kb->b;
-  B.finalize();
+  kb->b.finalize();
+  std::vector<uint64_t> perm;
+  const uint64_t split = split_rows(kb->b, &perm);
+  std::unique_ptr<Batch> P;
+  if (split) {
+    P = std::make_unique<Batch>();
+    RowOrder o;
+    permute_batch(kb->b, perm, P.get(), /*with_bytes=*/false, &o);
+  }
+  const Batch& B = P ? *P : kb->b;
   auto D = std::make_unique<DeviceBatch>();
+  D->split = split;
+  D->perm = std::move(perm);
   static uint32_t dummy;
   D->req_flags = B.req_flags.data();
   D->ctr_off = B.ctr_off.data();
@@ -2531,9 +2836,10 @@ int kw_debug_plan(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
   D->capdrop_off = B.capdrop_off.data();
   for (int m = 0; m < (int)NSTR; ++m) {
     const StrCol& c = host_str(B, m);
-    D->str[m] = {c.off.data(), c.bytes.data(), c.n(), c.off.back()};
+    D->str[m] = {c.off.data(), c.bytes.empty() ? (const uint8_t*)&dummy : c.bytes.data(), c.n(), c.off.back()};
   }
   D->verdicts = &dummy;
+  D->dev_b = std::move(P);
   kb->dev = std::move(D);
   PassPlan plan;
   int rc = plan_pass(env, kb, policies, npol, nullptr, origin, &plan);
@@ -2541,9 +2847,33 @@ int kw_debug_plan(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
   const uint32_t vals[8] = {T.lds_bytes, (uint32_t)plan.launches.size(), (uint32_t)plan.chunks.size(), T.lds_tables,
                             T.rows, T.cmax, T.kmax, T.lmax};
   for (int i = 0; i < 8; ++i) out[i] = rc == KW_OK ? vals[i] : 0u;
+  if (cap >= 16) {  // regions: count, light rows, the first region's grid, the heavy region's LDS / rows / cmax / grid
+    const bool two = rc == KW_OK && plan.regions.size() == 2;
+    const TileArgs* H = two ? &plan.regions[1].geom : nullptr;
+    const uint32_t more[8] = {rc == KW_OK ? (uint32_t)plan.regions.size() : 0u, (uint32_t)split,
+                              rc == KW_OK ? plan.regions[0].grid : 0u, H ? H->lds_bytes : 0u, H ? H->rows : 0u,
+                              H ? H->cmax : 0u, two ? plan.regions[1].grid : 0u, 0u};
+    for (int i = 0; i < 8; ++i) out[8 + i] = more[i];
+  }
   kb->dev->verdicts = nullptr;  // host memory: not the DeviceBatch's to free
   kb->dev = std::move(saved);
   return rc;
+}
+
+int kw_debug_reorder(const kw_batch* kb, uint64_t* perm, size_t cap, uint64_t* split, kw_batch** out) {
+  if (!kb || !split || !out || (!perm && kb->b.n) || cap < kb->b.n) return KW_E_ARG;
+  std::vector<uint64_t> p;
+  *split = split_rows(kb->b, &p);
+  if (!*split) {
+    p.resize(kb->b.n);
+    for (uint64_t r = 0; r < kb->b.n; ++r) p[r] = r;
+  }
+  auto nb = std::make_unique<kw_batch>();
+  RowOrder o;
+  permute_batch(kb->b, p, &nb->b, /*with_bytes=*/true, &o);
+  std::copy(p.begin(), p.end(), perm);
+  *out = nb.release();
+  return KW_OK;
 }
 
 int kw_batch_group_causes(const kw_batch* b, uint64_t row, int32_t policy, uint32_t verdict, uint64_t* words,

@@ -496,6 +496,7 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
   auto sg_add = [&](uint32_t k, uint64_t d) {
     if (timing && lane == 0) atomicAdd((unsigned long long*)&a.phase[(uint64_t)blockIdx.x * kPhaseWords + 8u + k], (unsigned long long)d);
   };
+  if (timing && tid == 0) a.phase[(uint64_t)blockIdx.x * kPhaseWords + 8u + SG_START] = __builtin_amdgcn_s_memrealtime();
   uint64_t sg_t = 0;
   int sg_k = -1;
   auto seg = [&](int k) {
@@ -1552,6 +1553,8 @@ hipError_t launch_evaluate_tiles(const EvalArgs& a, const TileArgs& t, const Til
       c_ncu = ncu;
       c_occ = occ;
     }
+    // (the API's LDS bound is floor(160 KiB / bytes); the CU allocates 1280-byte granules)
+    c_occ = std::min<int>(c_occ, (int)lds_workgroups_per_cu(t.lds_bytes));
     if (c_occ > 0 && c_ncu > 0) grid = std::max<uint32_t>(1u, std::min<uint32_t>(grid, (uint32_t)(c_occ * c_ncu)));
     if (t.debug & 256u)
       fprintf(stderr, "[kw tile] launch grid=%u occupancy=%d wg/cu x %d CUs lds=%u\n", grid, c_occ, c_ncu, t.lds_bytes);

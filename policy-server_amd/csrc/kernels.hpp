@@ -54,7 +54,9 @@ struct EvalArgs {
 // loop iteration), each phase's busy time and its barrier wait.
 enum Seg : uint32_t {
   SG_P1_LABEL = 0, SG_P1_CAPSTR, SG_P1_CTR, SG_P1_IMAGE, SG_P1_REQ, SG_P2_CTR, SG_P2_LABEL, SG_P2_REQ,
-  SG_P1_BUSY, SG_P1_WAIT, SG_P2_BUSY, SG_P2_WAIT, SG_P0_WAIT, SG_P3_BUSY, SG_P3_WAIT, kSegWords = 16
+  SG_P1_BUSY, SG_P1_WAIT, SG_P2_BUSY, SG_P2_WAIT, SG_P0_WAIT, SG_P3_BUSY, SG_P3_WAIT,
+  SG_START,  // the workgroup's start (s_memrealtime, 100 MHz): residency of the grid
+  kSegWords = 16
 };
 constexpr uint32_t kPhaseWords = 8 + kSegWords;
 
@@ -65,6 +67,16 @@ constexpr uint32_t kSlotRows = 64;
 #define KW_THREADS 256
 #endif
 constexpr uint32_t kSlotThreads = KW_THREADS;
+// Workgroups of `bytes` dynamic LDS one gfx950 CU holds at once (256 threads, LDS-bound): the CU's
+// 160 KiB are allocated in 1280-byte granules, 128 of them — measured (scripts/lds_occ.hip,
+// profiles/r05_lds_residency.txt): 53760 B holds 3, 53768 B holds 2, 32000 B 5, 32004 B 4. The HIP
+// occupancy API's floor(160 KiB / bytes) overstates it between granule boundaries (r05: a C5 heavy
+// layout of 53664 B planned at 3 ran at 2, a third of its grid waiting for the first two-thirds).
+constexpr uint32_t kLdsGranule = 1280, kLdsGranules = 128;
+constexpr uint32_t lds_workgroups_per_cu(uint32_t bytes) {
+  const uint32_t g = (bytes + kLdsGranule - 1) / kLdsGranule;
+  return g ? kLdsGranules / g : kLdsGranules;
+}
 // Families a tile-kernel instantiation carries (TileArgs::feat).
 constexpr uint32_t kFeatImg = 1, kFeatLbl = 2, kFeatCtr = 4, kFeatGrp = 8, kFeatAll = 15;
 // A pass whose classifiers hold NFA elements runs the one instantiation that reads their classes

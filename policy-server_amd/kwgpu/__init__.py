@@ -397,10 +397,22 @@ class Batch:
     def debug_plan(self, env, policies, origin=VALIDATE):
         """Diagnostic (kw_debug_plan): the tile kernel's plan for an all-pairs pass, on the host."""
         arr = (C.c_int32 * len(policies))(*[env._idx(p) for p in policies])
-        out = (C.c_uint32 * 8)()
-        raise_for(self._L.kw_debug_plan(env._h, self._h, arr, len(policies), origin, out, 8), "kw_debug_plan failed")
-        keys = ("lds_bytes", "launches", "chunks", "lds_tables", "rows", "cmax", "kmax", "lmax")
-        return dict(zip(keys, out[:8]))
+        out = (C.c_uint32 * 16)()
+        raise_for(self._L.kw_debug_plan(env._h, self._h, arr, len(policies), origin, out, 16), "kw_debug_plan failed")
+        keys = ("lds_bytes", "launches", "chunks", "lds_tables", "rows", "cmax", "kmax", "lmax", "regions", "split",
+                "grid", "heavy_lds_bytes", "heavy_rows", "heavy_cmax", "heavy_grid")
+        return dict(zip(keys, out[:15]))
+
+    def debug_reorder(self):
+        """Diagnostic (kw_debug_reorder): the device-row order kw_batch_to_device gives this batch,
+        as (batch in that order, perm, light-region rows); perm[d] is the batch row at device row d."""
+        import numpy as np
+        perm = np.zeros(max(self.n, 1), dtype=np.uint64)
+        split, h = C.c_uint64(), C.c_void_p()
+        rc = self._L.kw_debug_reorder(self._h, perm.ctypes.data_as(C.POINTER(C.c_uint64)), len(perm), C.byref(split),
+                                      C.byref(h))
+        raise_for(rc, "kw_debug_reorder failed")
+        return Batch(h.value), perm[:self.n], split.value
 
     def wide_arg(self, row, policy):
         """Full argument of a verdict word whose ARG is KW_ARG_WIDE (kw_batch_wide_arg), or None."""

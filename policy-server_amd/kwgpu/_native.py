@@ -85,7 +85,7 @@ EXPORTS = [
     "kw_env_get_policy_allowed_to_mutate",
     "kw_env_should_always_accept_requests_made_inside_of_namespace",
     "kw_env_policy_initialization_error", "kw_env_validate_settings", "kw_pattern_match", "kw_pattern_match_many", "kw_env_pattern_count",
-    "kw_env_pattern", "kw_env_classify", "kw_batch_wide_arg", "kw_batch_group_causes", "kw_debug_plan",
+    "kw_env_pattern", "kw_env_classify", "kw_batch_wide_arg", "kw_batch_group_causes", "kw_debug_plan", "kw_debug_reorder",
     "kw_batch_from_json", "kw_batch_from_soa", "kw_batch_view", "kw_batch_to_device", "kw_batch_to_device_async",
     "kw_stream_create", "kw_stream_destroy", "kw_validate_host", "kw_batch_pin_host", "kw_host_alloc", "kw_host_free",
     "kw_batch_destroy", "kw_debug_host_walk", "kw_validate_batch", "kw_validate_rows", "kw_batch_verdicts",
@@ -132,6 +132,7 @@ def lib():
         "kw_batch_wide_arg": (ip, [vp, u64, i32, C.POINTER(u64)]),
         "kw_batch_group_causes": (ip, [vp, u64, i32, C.c_uint32, C.POINTER(u64), C.c_size_t, C.POINTER(C.c_size_t)]),
         "kw_debug_plan": (ip, [vp, vp, C.POINTER(i32), u32, ip, C.POINTER(u32), ip]),
+        "kw_debug_reorder": (ip, [vp, C.POINTER(u64), sz, C.POINTER(u64), C.POINTER(vp)]),
         "kw_batch_from_json": (ip, [C.POINTER(cp), C.POINTER(sz), sz, ip, C.POINTER(vp), C.POINTER(C.c_int64), cp, sz]),
         "kw_batch_from_soa": (ip, [C.POINTER(KwSoa), C.POINTER(vp)]),
         "kw_batch_view": (ip, [vp, C.POINTER(KwSoa)]),
