@@ -38,18 +38,24 @@ namespace kw {
 
 // Caching allocators for device memory and pinned host staging: a micro-batch front evaluates
 // thousands of small batches per second, and hipMalloc / hipHostMalloc per batch would dominate.
-// Blocks are kept per (device, power-of-two size class) up to kMaxCached bytes per pool.
+// Blocks are kept per (device, size class) up to max_cached() bytes per pool.
 struct BlockPool {
   bool host;
   std::mutex m;
   std::map<std::pair<int, size_t>, std::vector<void*>> free;
   size_t cached = 0;
-  static constexpr size_t kMaxCached = (size_t)4 << 30;
+  // cached bytes: device 32 GiB (of 288), pinned host 16 GiB — the bulk path's per-call blocks
+  // (bounce, ring, descriptors) and a re-uploaded batch's image come back from the cache
+  size_t max_cached() const { return host ? (size_t)16 << 30 : (size_t)32 << 30; }
   explicit BlockPool(bool h) : host(h) {}
+  // size classes: 4 KiB, then eight steps per power of two (<= 12.5 % slack: C5's 3.6 GB image
+  // took a 4 GiB block before)
   static size_t cls(size_t n) {
-    size_t c = 4096;
-    while (c < n) c <<= 1;
-    return c;
+    if (n <= 4096) return 4096;
+    size_t p = 4096;
+    while (p * 2 < n) p <<= 1;  // p < n <= 2p
+    const size_t step = p / 8;
+    return (n + step - 1) / step * step;
   }
   hipError_t alloc(int dev, size_t n, void** p) {
     const size_t c = cls(n);
@@ -69,7 +75,7 @@ struct BlockPool {
     if (!p) return;
     const size_t c = cls(n);
     std::lock_guard<std::mutex> g(m);
-    if (cached + c > kMaxCached) {
+    if (cached + c > max_cached()) {
       (void)(host ? hipHostFree(p) : hipFree(p));
       return;
     }
@@ -2246,7 +2252,8 @@ void gather_column(const Batch& B, const Batch& P, const RowOrder& o, int m, uin
   if (bytes > d.off[ne]) memset(dst + d.off[ne], 0, bytes - d.off[ne]);
 }
 
-int layout_batch(kw_batch* kb, int device, hipStream_t stream, std::vector<Piece>* pieces, bool may_split = false) {
+int layout_batch(kw_batch* kb, int device, hipStream_t stream, std::vector<Piece>* pieces, bool may_split = false,
+                 bool staging = true) {
   if (!kb || device < 0) return KW_E_ARG;
   HIPCHK(hipSetDevice(device));
   if (kb->dev) kb->dev.reset();  // re-upload: the previous device copy returns to the pools
@@ -2300,8 +2307,10 @@ int layout_batch(kw_batch* kb, int device, hipStream_t stream, std::vector<Piece
   HIPCHK(dev_pool().alloc(device, total, &dcols));
   D->cols = (uint8_t*)dcols;
   D->cols_bytes = total;
-  HIPCHK(host_pool().alloc(device, total, &D->staging));
-  D->staging_bytes = total;
+  if (staging) {
+    HIPCHK(host_pool().alloc(device, total, &D->staging));
+    D->staging_bytes = total;
+  }
   D->cur = D->stream;
   D->req_flags = D->cols + o_rf;
   D->ctr_off = (const uint32_t*)(D->cols + o_co);
@@ -2437,7 +2446,7 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
   double t_layout = 0, t_plan = 0, t_prep = 0, t_desc = 0, t_fill = 0, t_enq = 0, t_out = 0, t_first = -1;
   auto since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
   std::vector<Piece> pieces;
-  if (int rc = layout_batch(kb, device, nullptr, &pieces)) return rc;
+  if (int rc = layout_batch(kb, device, nullptr, &pieces, /*may_split=*/false, /*staging=*/false)) return rc;
   t_layout = since(t_start);
   DeviceBatch& D = *kb->dev;
   const Batch& B = kb->b;
@@ -2465,12 +2474,19 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
                pa.type == hipMemoryTypeHost;
       (void)hipGetLastError();
     }
-  uint8_t* st = (uint8_t*)D.staging;
   hipStream_t sc = D.stream;
   EvalArgs A;
   // (NFA elements: their pre-pass reads whole columns, so such passes are not chunked)
   const bool chunked = plan.tiles.size() == 1 && plan.wide.groups.empty() && plan.nwide == 0 && !plan.rows_mode &&
                        !(plan.geom.debug & 512u) && !(plan.geom.feat & kFeatNfa) && B.n > 0;
+  // the staging image of the whole batch only where it is used: the unchunked path and per-range
+  // copies (packed chunks go through their own ring; pinning C5's 3.6 GB image cost 360 ms a call)
+  static const bool pack_knob = !(getenv("KW_BULK_PACK") && atoi(getenv("KW_BULK_PACK")) == 0);
+  if ((!chunked || !pack_knob) && !D.staging) {
+    HIPCHK(host_pool().alloc(device, D.cols_bytes, &D.staging));
+    D.staging_bytes = D.cols_bytes;
+  }
+  uint8_t* st = (uint8_t*)D.staging;
   if (!chunked) {  // one upload, the full pass, one read-back
     std::vector<CopySeg> segs;
     for (size_t i = 0; i < pieces.size(); ++i)
@@ -2498,14 +2514,26 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
   const uint64_t per = chunk_rows ? chunk_rows : def_chunk;
   // chunk k: tiles [tb[k], tb[k+1]). The read-back stream is the longest (4 B x npol per request
   // out vs the request's columns in), so the first chunks are small (1/16 of `per`, doubling) to
-  // start it early; then `per` rows a chunk, at most 256 chunks.
+  // start it early; then `per` rows a chunk.
   static const bool ramp = !(getenv("KW_BULK_RAMP") && atoi(getenv("KW_BULK_RAMP")) == 0);  // A/B knob
-  const uint64_t tper = std::max<uint64_t>(1, per / G.rows);
+  // The last chunks shrink the same way (r05): the final chunk's read-back overlaps nothing, so a
+  // full-size last chunk left ~1 ms of C4's read-back exposed. At most ~240 chunks (per grows).
+  const uint64_t tper = std::max<uint64_t>({1, per / G.rows, (ntiles + 239) / 240});
   std::vector<uint64_t> tb{0};
-  for (uint64_t step = ramp ? std::max<uint64_t>(1, tper / 16) : tper; tb.back() < ntiles;) {
-    const uint64_t left = ntiles - tb.back();
-    tb.push_back(tb.back() + (tb.size() >= 256 ? left : std::min(step, left)));
-    step = std::min(tper, step * 2);
+  {
+    std::vector<uint64_t> head, tail;  // chunk sizes in tiles, from the front and from the back
+    uint64_t left = ntiles, sh = ramp ? std::max<uint64_t>(1, tper / 16) : tper, st_ = sh;
+    while (left) {
+      head.push_back(std::min(sh, left));
+      left -= head.back();
+      sh = std::min(tper, sh * 2);
+      if (!left || !ramp) continue;
+      tail.push_back(std::min(st_, left));
+      left -= tail.back();
+      st_ = std::min(tper, st_ * 2);
+    }
+    for (uint64_t h : head) tb.push_back(tb.back() + h);
+    for (auto it = tail.rbegin(); it != tail.rend(); ++it) tb.push_back(tb.back() + *it);
   }
   const uint64_t K = tb.size() - 1;
   auto row_of = [&](uint64_t t) { return std::min<uint64_t>(B.n, t * G.rows); };
@@ -2521,7 +2549,7 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
   static const int depth_knob = getenv("KW_BULK_DEPTH") ? std::max(0, atoi(getenv("KW_BULK_DEPTH"))) : -1;
   const bool any_dma = std::count(dma.begin(), dma.end(), 1) > 0;
   const uint64_t depth = depth_knob >= 0 ? (uint64_t)depth_knob : (any_dma ? 2 : 3);
-  // (the largest chunk, not `per`: past 256 chunks the last one takes every remaining tile)
+  // (the largest chunk: `per` grows past ~240 chunks)
   uint64_t max_rows = 0;
   for (uint64_t k = 0; k < K; ++k) max_rows = std::max(max_rows, row_of(tb[k + 1]) - row_of(tb[k]));
   const size_t bounce_bytes = (size_t)max_rows * npol * 4;
@@ -2553,6 +2581,27 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
     return !code(ensure(&D.desc, &D.desc_cap, (size_t)(2 * dcap)));
   };
   if (rc == KW_OK) (void)alloc_descs();
+  // staged columns: each chunk's ranges packed into one pinned slot, one H2D into the device slot,
+  // then the scatter kernel puts them in place (one copy per chunk, not one per column). kRing
+  // slots: packing chunk k waits for chunk k - kRing's upload. KW_BULK_PACK=0: a copy per column
+  // range (A/B knob, profiles/r05_bulk_copies.txt).
+  constexpr uint64_t kRing = 4;
+  const bool packed = pack_knob && std::count(dma.begin(), dma.end(), 0) > 0;
+  size_t slot_bytes = 0;
+  void *hpack = nullptr, *dland = nullptr;
+  if (packed && rc == KW_OK) {
+    for (uint64_t k = 0; k < K; ++k) {
+      size_t b = 0;
+      for (size_t i = 0; i < pieces.size(); ++i) {
+        if (!wanted(pieces[i]) || dma[i]) continue;
+        size_t lo, hi;
+        piece_range(B, pieces[i], row_of(tb[k]), row_of(tb[k + 1]), k + 1 == K, &lo, &hi);
+        if (hi > lo) b += (hi - lo) + 32;
+      }
+      slot_bytes = std::max(slot_bytes, (b + 255) & ~(size_t)255);
+    }
+    if (!fail(host_pool().alloc(device, kRing * slot_bytes, &hpack))) (void)fail(dev_pool().alloc(device, kRing * slot_bytes, &dland));
+  }
   StreamPool& SP = stream_pool();
   if (rc == KW_OK && !fail(SP.get(device, &s_in)) && !fail(SP.get(device, &s_out)))
     for (auto& e : ev)
@@ -2574,27 +2623,46 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
     // the chunk's columns first: their H2D starts at once, and the descriptor build below then
     // reads offsets the fill has just brought into the host caches
     std::vector<CopySeg> segs, dsegs;  // (staged, direct)
+    const size_t slot = (size_t)(k % kRing) * slot_bytes;
+    ScatterArgs sa;
+    sa.dst = D.cols;
+    sa.src = (const uint8_t*)dland + slot;
+    sa.nseg = 0;
+    size_t pk = 0;  // packed bytes of the chunk (each range at its device offset's residue mod 16)
     for (size_t i = 0; i < pieces.size(); ++i) {
       const Piece& p = pieces[i];
       if (!wanted(p)) continue;
       size_t lo, hi;
       piece_range(B, p, r0, r1, k + 1 == K, &lo, &hi);
       if (hi <= lo) continue;
-      if (dma[i])
+      if (dma[i]) {
         dsegs.push_back({D.cols + p.at + lo, (const uint8_t*)p.src + lo, hi - lo});
-      else
+      } else if (packed) {
+        const size_t at = ((pk + 15) & ~(size_t)15) + ((p.at + lo) & 15);
+        segs.push_back({(uint8_t*)hpack + slot + at, (const uint8_t*)p.src + lo, hi - lo});
+        sa.seg[sa.nseg++] = {p.at + lo, at, hi - lo};
+        pk = at + (hi - lo);
+      } else {
         segs.push_back({st + p.at + lo, (const uint8_t*)p.src + lo, hi - lo});
+      }
     }
+    if (packed && k >= kRing && fail(hipEventSynchronize(ev[3 * (k - kRing)]))) break;  // its slot's upload is done
     const auto t0 = clk::now();
     parallel_copy_segs(segs);
     t_fill += since(t0);
     const auto t1 = clk::now();
     for (const CopySeg& c : dsegs)
       if (fail(hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyHostToDevice, s_in))) break;
-    for (const CopySeg& c : segs)
-      if (rc != KW_OK ||
-          fail(hipMemcpyAsync(D.cols + ((uint8_t*)c.dst - st), c.dst, c.bytes, hipMemcpyHostToDevice, s_in)))
+    if (packed) {
+      if (pk && (fail(hipMemcpyAsync((uint8_t*)dland + slot, (uint8_t*)hpack + slot, pk, hipMemcpyHostToDevice, s_in)) ||
+                 fail(launch_scatter(sa, s_in))))
         break;
+    } else {
+      for (const CopySeg& c : segs)
+        if (rc != KW_OK ||
+            fail(hipMemcpyAsync(D.cols + ((uint8_t*)c.dst - st), c.dst, c.bytes, hipMemcpyHostToDevice, s_in)))
+          break;
+    }
     if (rc != KW_OK) break;
     t_enq += since(t1);
     const auto td = clk::now();
@@ -2662,6 +2730,8 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
   SP.put(device, s_out);
   for (auto& b : bounce) host_pool().release(device, b, bounce_bytes);
   if (hdesc) host_pool().release(device, hdesc, hdesc_bytes);
+  if (hpack) host_pool().release(device, hpack, kRing * slot_bytes);
+  if (dland) dev_pool().release(device, dland, kRing * slot_bytes);
   D.last_wide_cap = A.wide_cap;
   D.cur = sc;
   if (rc != KW_OK) {

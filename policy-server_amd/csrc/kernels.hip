@@ -1565,6 +1565,31 @@ hipError_t launch_evaluate_tiles(const EvalArgs& a, const TileArgs& t, const Til
   return hipGetLastError();
 }
 
+__global__ void __launch_bounds__(256) scatter_kernel(ScatterArgs a) {
+  const uint64_t tid = (uint64_t)blockIdx.x * 256u + threadIdx.x, nt = (uint64_t)gridDim.x * 256u;
+  for (uint32_t k = 0; k < a.nseg; ++k) {
+    const ScatterSeg g = a.seg[k];
+    uint8_t* d = a.dst + g.dst_off;
+    const uint8_t* s = a.src + g.src_off;
+    const uint64_t head = std::min<uint64_t>(g.bytes, (16u - ((uintptr_t)d & 15u)) & 15u);
+    const uint64_t words = (g.bytes - head) / 16u, tail = g.bytes - head - words * 16u;
+    if (tid < head) d[tid] = s[tid];
+    const u32x4* sw = (const u32x4*)(s + head);
+    u32x4* dw = (u32x4*)(d + head);
+    for (uint64_t i = tid; i < words; i += nt) __builtin_nontemporal_store(__builtin_nontemporal_load(sw + i), dw + i);
+    if (tid < tail) d[head + words * 16u + tid] = s[head + words * 16u + tid];
+  }
+}
+
+hipError_t launch_scatter(const ScatterArgs& a, hipStream_t s) {
+  uint64_t bytes = 0;
+  for (uint32_t k = 0; k < a.nseg; ++k) bytes += a.seg[k].bytes;
+  if (!bytes) return hipSuccess;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(1024, std::max<uint64_t>(1, bytes / (256u * 64u)));
+  hipLaunchKernelGGL(scatter_kernel, dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_overflow(const EvalArgs& a, const TileArgs* d_t, const uint32_t* d_overflow, uint32_t n_overflow,
                            hipStream_t s) {
   if (n_overflow == 0 || a.nrows == 0) return hipSuccess;

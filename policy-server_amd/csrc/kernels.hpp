@@ -231,6 +231,22 @@ struct NfaPass {
   uint64_t nlabels, nctrs;
   uint32_t do_lv, do_img;
 };
+// Bulk path (kw_validate_host): a chunk's column ranges arrive in one H2D copy, packed, and this
+// kernel moves each range to its place in the batch's device image (one copy per chunk instead of
+// one per column: a pinned H2D copy costs ~9.6 us on its own, profiles/r05_bulk_copies.txt).
+// src_off == dst_off (mod 16), so the body moves 16-byte words.
+constexpr uint32_t kMaxScatterSegs = 24;
+struct ScatterSeg {
+  uint64_t dst_off, src_off, bytes;
+};
+struct ScatterArgs {
+  uint8_t* dst;
+  const uint8_t* src;
+  uint32_t nseg;
+  ScatterSeg seg[kMaxScatterSegs];
+};
+hipError_t launch_scatter(const ScatterArgs& a, hipStream_t s);
+
 hipError_t launch_nfa_classify(const EvalArgs& a, const TileArgs* d_t, const NfaPass& np, uint32_t threads, hipStream_t s);
 // threads of the NFA pass's grid for `items` entities within a scratch budget
 uint32_t nfa_threads(uint64_t items, uint64_t words_per_thread);
