@@ -30,8 +30,16 @@
 
 using namespace kw;
 
+extern char** environ;  // (POSIX; kw_knob_hash)
+
 struct kw_env {
   Env e;
+  // identity of this environment for plan caches (an address can be reused by a later one)
+  uint64_t uid = next_uid();
+  static uint64_t next_uid() {
+    static std::atomic<uint64_t> n{1};
+    return n++;
+  }
 };
 
 namespace kw {
@@ -261,6 +269,21 @@ void parallel_copy_segs(const std::vector<CopySeg>& segs) {
 
 // Requests per tile of the tile kernel forced by KW_SLOT_ROWS (8..255, A/B knob), 0 = chosen per
 // batch (plan_pass: kSlotRows, or taller tiles where they keep enough workgroups per CU).
+// Tile schedule of a launch of `ntiles` tiles over `grid` workgroups: the dynamic one (per-XCD
+// counters, kernels.hip) only where a workgroup runs more than 16 tiles, so that drift between
+// workgroups has room to build up; below that the strided schedule is as balanced and skips the
+// counter traffic: every fetch is an atomic on one L2 line per XCD, serialised — r05 same-box A/B
+// (profiles/r05_sched_ab.txt): strided C4 -2.4 %, C2 -6 %, C1 -40 %, a 64k-request shard -47 %; the
+// dynamic one C5 -7 % (its heavy region), C6 -2 %, C3 -2 %. KW_SCHED=static / dynamic forces one.
+// Tables read from global memory (C6) make tile costs vary with the caches: there the dynamic
+// schedule pays from 4 tiles a workgroup (C6 at 15: -2 %).
+bool sched_dynamic(uint64_t ntiles, uint32_t grid, bool lds_tables) {
+  const char* e = getenv("KW_SCHED");
+  if (e && std::string(e) == "static") return false;
+  if (e && std::string(e) == "dynamic") return true;
+  return ntiles > (lds_tables ? 16ull : 4ull) * std::max<uint32_t>(grid, 1);
+}
+
 // Tile height of a split batch's heavy region (KW_HEAVY_ROWS, A/B knob; 0: planned like any batch).
 uint32_t heavy_rows() {
   const char* e = getenv("KW_HEAVY_ROWS");
@@ -339,6 +362,13 @@ struct DeviceBatch {
   std::vector<uint64_t> perm;
   uint64_t split = 0;
   std::unique_ptr<Batch> dev_b;
+  // the last all-pairs pass's plan (capi.cpp validate_cached; a PassPlan): reused while the
+  // environment, the policy list, the origin and every KW_* setting stay the same — planning a
+  // 64-policy pass is ~60-300 us of host time, the whole GPU time of a small shard
+  std::shared_ptr<void> plan_cache;
+  uint64_t plan_env = 0, plan_knobs = 0;
+  std::vector<int32_t> plan_pols;
+  int plan_origin = -1;
   std::unique_ptr<RowOrder> order;  // (until the upload's staging is filled)
   uint32_t loaded = 0;        // string columns (bits of Str) whose bytes are resident (kw_validate_host uploads only its pass's)
   uint32_t* sched = nullptr;  // tile counters (zeroed once; each launch leaves them zero)
@@ -637,6 +667,7 @@ struct PassPlan {
     uint64_t lo = 0, hi = 0;
     TileArgs geom;
     uint32_t grid = 0;
+    bool dyn = true;  // the dynamic tile schedule (sched_dynamic), else the strided one
   };
   std::vector<Region> regions;
   uint32_t nwide = 0;
@@ -1093,6 +1124,7 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
   g.geom = T;
   const uint64_t nt = (hi - lo + T.rows - 1) / T.rows;
   g.grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nt, 256ull * per_cu(T.lds_bytes)));
+  g.dyn = sched_dynamic(nt, g.grid, ldst);
   plan->regions.push_back(g);
   }
   bool any_grp = false;
@@ -1474,15 +1506,15 @@ int prepare_pass(kw_batch* kb, PassPlan& plan, hipStream_t s, EvalArgs* out_args
   // instead of keeping an earlier pass's words
   if (const char* pz = getenv("KW_POISON_VERDICTS"); pz && atoi(pz) != 0)
     HIPCHK(hipMemsetAsync(D.verdicts, 0xA5, D.last_verdicts * sizeof(uint32_t), s));
-  // dynamic tile schedule (per-XCD counters); KW_SCHED=static selects the strided schedule (A/B)
-  static const bool dyn = !(getenv("KW_SCHED") && std::string(getenv("KW_SCHED")) == "static");
-  if (dyn && !D.sched) {
+  // the dynamic tile schedule's per-XCD counters (used by the regions whose plan says so,
+  // sched_dynamic; run_pass hands them to those launches only)
+  if (!D.sched) {
     void* p = nullptr;
     HIPCHK(dev_pool().alloc(D.device, 512 * sizeof(uint32_t), &p));
     D.sched = (uint32_t*)p;
     HIPCHK(hipMemsetAsync(D.sched, 0, 512 * sizeof(uint32_t), s));
   }
-  A.sched = dyn ? D.sched : nullptr;
+  A.sched = D.sched;
   // side data: dense group causes, the overflow path's class arrays and wide-argument list
   if (plan.nwide) {
     if (int rc = ensure(&D.wide_groups, &D.wide_groups_cap, (size_t)(B.n * plan.nwide))) return rc;
@@ -1542,6 +1574,7 @@ int run_pass(kw_batch* kb, PassPlan& plan, bool timed, hipStream_t s) {
     const uint32_t grid = plan.regions[k].grid;
     EvalArgs Ak = A;
     Ak.ndesc = D.reg_ndesc[k];
+    if (!plan.regions[k].dyn) Ak.sched = nullptr;  // the strided schedule
     HIPCHK(launch_evaluate_tiles(Ak, plan.tiles[l], D.d_tiles + l, D.desc + D.reg_desc[k], grid, s));
     if (phases) {
       std::vector<uint64_t> ph((size_t)grid * kPhaseWords);
@@ -1647,6 +1680,15 @@ int run_validate(const kw_env* env, kw_batch* kb, PassPlan& plan, int origin, bo
   return KW_OK;
 }
 
+// A hash of every KW_* environment variable (tests and A/B knobs switch them between passes).
+uint64_t kw_knob_hash() {
+  uint64_t h = 1469598103934665603ull;
+  for (char** e = environ; e && *e; ++e)
+    if ((*e)[0] == 'K' && (*e)[1] == 'W' && (*e)[2] == '_')
+      for (const char* c = *e; *c; ++c) h = (h ^ (uint8_t)*c) * 1099511628211ull;
+  return h;
+}
+
 int validate_common(const kw_env* env, kw_batch* kb, const int32_t* policies, uint32_t npol, const int32_t* row_policy,
                     int origin, PassPlan* plan) {
   if (!env || !kb) return KW_E_ARG;
@@ -1674,6 +1716,45 @@ int validate_common(const kw_env* env, kw_batch* kb, const int32_t* policies, ui
   kb->b.wide.clear();
   if (int rc = plan_pass(env, kb, policies, npol, row_policy, origin, plan)) return rc;
   return (plan->geom.need & ~D.loaded) ? KW_E_ARG : KW_OK;  // a column the upload left out (kw_validate_host)
+}
+
+// validate_common for an all-pairs pass through the batch's plan cache (DeviceBatch::plan_cache):
+// a repeated pass (same environment, policy list, origin and KW_* settings) skips planning; the
+// checks and the verdict buffer are redone every time.
+int validate_cached(const kw_env* env, kw_batch* kb, const int32_t* policies, uint32_t npol, int origin, PassPlan** out) {
+  DeviceBatch* D = kb && kb->dev ? kb->dev.get() : nullptr;
+  const uint64_t knobs = kw_knob_hash();
+  if (env && D && D->plan_cache && D->plan_env == env->uid && D->plan_origin == origin && D->plan_knobs == knobs &&
+      D->plan_pols.size() == npol && policies && std::equal(policies, policies + npol, D->plan_pols.begin())) {
+    PassPlan* plan = (PassPlan*)D->plan_cache.get();
+    const Env& E = env->e;
+    if (E.device < 0 || !E.d_blob) return KW_E_DEVICE;
+    if (D->device != E.device) return KW_E_ARG;
+    HIPCHK(hipSetDevice(D->device));
+    const uint64_t npairs = kb->b.n * (uint64_t)npol;
+    uint32_t* before = D->verdicts;
+    if (int rc = ensure(&D->verdicts, &D->verdict_cap, npairs)) return rc;
+    if (D->verdicts != before) {  // (reallocated by another pass's larger need: re-plan)
+      D->plan_cache.reset();
+      return validate_cached(env, kb, policies, npol, origin, out);
+    }
+    D->last_verdicts = npairs;
+    kb->b.wide.clear();
+    if (plan->geom.need & ~D->loaded) return KW_E_ARG;
+    *out = plan;
+    return KW_OK;
+  }
+  auto plan = std::make_shared<PassPlan>();
+  if (D) D->plan_cache.reset();
+  if (int rc = validate_common(env, kb, policies, npol, nullptr, origin, plan.get())) return rc;
+  D = kb->dev.get();
+  D->plan_cache = plan;
+  D->plan_env = env->uid;
+  D->plan_origin = origin;
+  D->plan_knobs = knobs;
+  D->plan_pols.assign(policies, policies + npol);
+  *out = plan.get();
+  return KW_OK;
 }
 
 }  // namespace
@@ -2687,6 +2768,7 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
     if (fail(hipEventRecord(ev[3 * k], s_in)) || fail(hipStreamWaitEvent(sc, ev[3 * k], 0))) break;
     EvalArgs Ak = A;
     Ak.ndesc = cd.size();
+    if (!sched_dynamic(cd.size(), plan.grid, plan.geom.lds_tables != 0)) Ak.sched = nullptr;
     if (!cd.empty() && fail(launch_evaluate_tiles(Ak, plan.tiles[0], D.d_tiles, dd, plan.grid, sc))) break;
     if (co[0]) {  // rare: synchronous set-up, then the overflow kernels on the chunk's requests
       if (fail(hipStreamSynchronize(sc))) break;
@@ -2820,9 +2902,9 @@ int kw_batch_pin_host(kw_batch* kb, int device) {
 }
 
 int kw_validate_batch(const kw_env* env, kw_batch* b, const int32_t* policies, uint32_t npol, int origin, void* stream) {
-  PassPlan plan;
-  if (int rc = validate_common(env, b, policies, npol, nullptr, origin, &plan)) return rc;
-  return run_validate(env, b, plan, origin, false, stream ? (hipStream_t)stream : b->dev->stream);
+  PassPlan* plan = nullptr;
+  if (int rc = validate_cached(env, b, policies, npol, origin, &plan)) return rc;
+  return run_validate(env, b, *plan, origin, false, stream ? (hipStream_t)stream : b->dev->stream);
 }
 
 int kw_validate_rows(const kw_env* env, kw_batch* b, const int32_t* row_policy, int origin, void* stream) {

@@ -600,15 +600,16 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
                                        (__attribute__((address_space(3))) void*)(l_desc + s), 4, 0, 0);
   };
   auto sfield = [](const uint32_t& f) -> uint32_t { return __builtin_amdgcn_readfirstlane(f); };
+  // Dynamic: a workgroup's first two tiles are static (the XCD's range in workgroup order), so a
+  // launch does not open with every workgroup's counter fetches queued on one L2 line; the counter
+  // hands out the range from its third tile-set on (value v = tile dbase + v). r05: the opening
+  // fetches cost a 1M C4 pass 2.4 % and a 64k-request shard 57 % (profiles/r05_sched_ab.txt).
+  const uint32_t wpx = (gridDim.x - xcd + nx - 1u) / nx;  // workgroups b < gridDim.x with b % nx == xcd
+  const uint64_t dbase = t_lo + 2ull * wpx;
   uint64_t tile = blockIdx.x, next = tile + gridDim.x;
   if (dyn) {
-    if (tid == 0) {
-      l_nx[0] = atomicAdd(cnt, 1u);
-      l_nx[1] = atomicAdd(cnt, 1u);
-    }
-    __syncthreads();
-    tile = t_lo + l_nx[0];
-    next = t_lo + l_nx[1];  // (l_nx is rewritten only after the staging barrier of the first tile)
+    tile = t_lo + blockIdx.x / nx;
+    next = tile + wpx;
   }
   if (tile < t_hi) fetch_desc(tile, 0);
   __syncthreads();
@@ -624,7 +625,7 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
       if (dyn && tid == 0) l_nx[cur] = nxt2;
       __syncthreads();  // also waits for the next descriptor
       tile = next;
-      next = dyn ? t_lo + l_nx[cur] : next + gridDim.x;
+      next = dyn ? dbase + l_nx[cur] : next + gridDim.x;
       continue;
     }
     const uint64_t r0 = ((uint64_t)KW_DF(d.r0hi) << 32) | KW_DF(d.r0lo);
@@ -1143,7 +1144,7 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
     if (timing) sg_add(SG_P3_WAIT, clock64() - p3_end);
     mark(4);
     tile = next;
-    next = dyn ? t_lo + l_nx[cur] : next + gridDim.x;
+    next = dyn ? dbase + l_nx[cur] : next + gridDim.x;
   }
   if (timing && tid == 0) {  // one lane's vector stores
     ph[6] = clock64() - t_begin;
@@ -1151,9 +1152,8 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
   }
   if (dyn && tid == 0) {  // the XCD's last workgroup (every other one has taken its last tile) resets
     uint32_t* done = a.sched + 256u + xcd * 32u;
-    const uint32_t nwg = (gridDim.x - xcd + nx - 1u) / nx;  // workgroups b < gridDim.x with b % nx == xcd
     __threadfence();  // this workgroup's last counter fetch is ordered before its done count
-    if (atomicAdd(done, 1u) == nwg - 1u) {
+    if (atomicAdd(done, 1u) == wpx - 1u) {
       atomicExch(cnt, 0u);
       atomicExch(done, 0u);
     }

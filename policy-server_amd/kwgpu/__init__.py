@@ -242,6 +242,19 @@ class EvaluationEnvironment:
     def _idx(self, policy):
         return policy if isinstance(policy, int) else self.lookup(policy)
 
+    def _array(self, policies):
+        """The policy list as the C ABI's int32 index array, memoised per list: building it costs a
+        lookup per policy (~100 us for 64 on the host), more than a small shard's whole pass."""
+        key = tuple(policies)
+        memo = self.__dict__.setdefault("_arrays", {})
+        arr = memo.get(key)
+        if arr is None:
+            arr = (C.c_int32 * len(policies))(*[self._idx(p) for p in policies])
+            if len(memo) > 256:
+                memo.clear()
+            memo[key] = arr
+        return arr
+
     # --- service::evaluate for one request (service.rs:30-152)
     def evaluate(self, policy_id, document, origin=VALIDATE, raw=False):
         """Returns the AdmissionResponse dict; raises the EvaluationError the handler maps to HTTP."""
@@ -344,7 +357,7 @@ class Batch:
     def validate(self, env, policies, origin=VALIDATE, stream=None):
         """All pairs rows x policies on the GPU; returns nothing (verdicts stay in HBM). stream: a
         hipStream_t (int) of the batch's device to run on, None = the batch's own stream."""
-        arr = (C.c_int32 * len(policies))(*[env._idx(p) for p in policies])
+        arr = env._array(policies)
         rc = self._L.kw_validate_batch(env._h, self._h, arr, len(policies), origin,
                                        C.c_void_p(stream) if stream else None)
         raise_for(rc, "kw_validate_batch failed")
@@ -396,7 +409,7 @@ class Batch:
 
     def debug_plan(self, env, policies, origin=VALIDATE):
         """Diagnostic (kw_debug_plan): the tile kernel's plan for an all-pairs pass, on the host."""
-        arr = (C.c_int32 * len(policies))(*[env._idx(p) for p in policies])
+        arr = env._array(policies)
         out = (C.c_uint32 * 16)()
         raise_for(self._L.kw_debug_plan(env._h, self._h, arr, len(policies), origin, out, 16), "kw_debug_plan failed")
         keys = ("lds_bytes", "launches", "chunks", "lds_tables", "rows", "cmax", "kmax", "lmax", "regions", "split",
@@ -436,7 +449,7 @@ class Batch:
         """Diagnostic (tests only): the device kernel's slot compiler + entity walks run on the host
         (kw_debug_host_walk). Never part of the validate path."""
         import numpy as np
-        arr = (C.c_int32 * len(policies))(*[env._idx(p) for p in policies])
+        arr = env._array(policies)
         out = np.zeros(self.n * len(policies), dtype=np.uint32)
         rc = self._L.kw_debug_host_walk(env._h, self._h, arr, len(policies), origin,
                                         out.ctypes.data_as(C.POINTER(C.c_uint32)))
@@ -444,7 +457,7 @@ class Batch:
         return out
 
     def timed(self, env, policies, origin=VALIDATE, warmup=3, reps=10):
-        arr = (C.c_int32 * len(policies))(*[env._idx(p) for p in policies])
+        arr = env._array(policies)
         t = KwTiming()
         rc = self._L.kw_validate_timed(env._h, self._h, arr, len(policies), origin, warmup, reps, C.byref(t))
         raise_for(rc, "kw_validate_timed failed")
