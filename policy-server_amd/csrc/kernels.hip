@@ -577,8 +577,9 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
   const uint32_t need = t.need;
 
   const uint32_t npol = a.npol;
-  // Tile schedule. Static: tiles strided by the grid. Dynamic (a.sched): workgroup b runs on XCD
-  // b % 8 and takes the tiles of that XCD's contiguous range one at a time from the XCD's own
+  // Tile schedule (capi.cpp sched_dynamic picks one per launch). Workgroup b runs on XCD b % 8 and
+  // serves that XCD's contiguous range of tiles. Static: the range strided by the XCD's
+  // workgroups. Dynamic (a.sched): the tiles one at a time from the XCD's own
   // counter (a 128-B line each, so no counter is shared between XCDs); the atomic for the next tile
   // is issued when the current tile starts and its result is read only at the tile's end, so its
   // latency hides behind the tile. The XCD's last workgroup to finish zeroes the counter again.
@@ -589,7 +590,9 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
   const bool dyn = a.sched != nullptr;
   const uint32_t nx = min(8u, gridDim.x);
   const uint32_t xcd = blockIdx.x % nx;
-  const uint64_t t_lo = dyn ? a.ndesc * xcd / nx : 0ull, t_hi = dyn ? a.ndesc * (xcd + 1) / nx : a.ndesc;
+  // both schedules serve the XCD's contiguous range (adjacent tiles share the cache lines at their
+  // boundaries, so they stay in one L2)
+  const uint64_t t_lo = a.ndesc * xcd / nx, t_hi = a.ndesc * (xcd + 1) / nx;
   uint32_t* cnt = dyn ? a.sched + xcd * 32u : nullptr;
   uint32_t* l_nx = (uint32_t*)(lds + t.o_nx);  // the tile after next, double-buffered
   TileDesc* l_desc = (TileDesc*)(lds + t.o_desc);
@@ -606,11 +609,7 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
   // fetches cost a 1M C4 pass 2.4 % and a 64k-request shard 57 % (profiles/r05_sched_ab.txt).
   const uint32_t wpx = (gridDim.x - xcd + nx - 1u) / nx;  // workgroups b < gridDim.x with b % nx == xcd
   const uint64_t dbase = t_lo + 2ull * wpx;
-  uint64_t tile = blockIdx.x, next = tile + gridDim.x;
-  if (dyn) {
-    tile = t_lo + blockIdx.x / nx;
-    next = tile + wpx;
-  }
+  uint64_t tile = t_lo + blockIdx.x / nx, next = tile + wpx;
   if (tile < t_hi) fetch_desc(tile, 0);
   __syncthreads();
   mark(4);
@@ -625,7 +624,7 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
       if (dyn && tid == 0) l_nx[cur] = nxt2;
       __syncthreads();  // also waits for the next descriptor
       tile = next;
-      next = dyn ? dbase + l_nx[cur] : next + gridDim.x;
+      next = dyn ? dbase + l_nx[cur] : next + wpx;
       continue;
     }
     const uint64_t r0 = ((uint64_t)KW_DF(d.r0hi) << 32) | KW_DF(d.r0lo);
@@ -1144,7 +1143,7 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
     if (timing) sg_add(SG_P3_WAIT, clock64() - p3_end);
     mark(4);
     tile = next;
-    next = dyn ? dbase + l_nx[cur] : next + gridDim.x;
+    next = dyn ? dbase + l_nx[cur] : next + wpx;
   }
   if (timing && tid == 0) {  // one lane's vector stores
     ph[6] = clock64() - t_begin;
