@@ -255,9 +255,9 @@ int kw_debug_host_walk(const kw_env *env, const kw_batch *b, const int32_t *poli
 /* Diagnostic (tests): plan an all-pairs pass over the batch's host columns without launching it.
  * out[0..8): LDS bytes per workgroup, launches, slot-plan chunks, classifiers staged in LDS (1) or
  * read from global memory (0), requests per tile, container / capability / label capacities (of the
- * first region). cap >= 16 adds out[8..15): regions (1, or 2 for a light / heavy split batch), the
+ * first region). cap >= 16 adds out[8..16): regions (1, or 2 for a light / heavy split batch), the
  * light region's rows, the first region's grid, the heavy region's LDS bytes, requests per tile,
- * container capacity and grid. */
+ * container capacity and grid, and a bit per region launched as the container wave-scan kernel. */
 int kw_debug_plan(const kw_env *env, kw_batch *b, const int32_t *policies, uint32_t npol, int origin, uint32_t *out,
                   int cap);
 

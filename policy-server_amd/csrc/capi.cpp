@@ -1139,6 +1139,8 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
                        ((H->col[COL_REG].flags | H->col[COL_TAG].flags | H->col[COL_IMG].flags) & 1u);
   const bool nfa_lv = (need & (1u << S_LV)) && (H->col[COL_LV].flags & 1u);
   if (nfa_img || nfa_lv) T.feat = kFeatAll | kFeatNfa;
+  // many containers per request (C5's heavy region): the wave-scan instantiation (kernels.hpp kFeatRng)
+  if (T.ctr_ranges && ldst && T.feat == (kFeatLbl | kFeatCtr)) T.feat |= kFeatRng;
   T.il = il;
   T.nlv = nlv;
   T.need = need;
@@ -2999,12 +3001,14 @@ int kw_debug_plan(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
   const uint32_t vals[8] = {T.lds_bytes, (uint32_t)plan.launches.size(), (uint32_t)plan.chunks.size(), T.lds_tables,
                             T.rows, T.cmax, T.kmax, T.lmax};
   for (int i = 0; i < 8; ++i) out[i] = rc == KW_OK ? vals[i] : 0u;
-  if (cap >= 16) {  // regions: count, light rows, the first region's grid, the heavy region's LDS / rows / cmax / grid
+  if (cap >= 16) {  // regions: count, light rows, the first region's grid, the heavy region's LDS / rows / cmax / grid, scan regions
     const bool two = rc == KW_OK && plan.regions.size() == 2;
     const TileArgs* H = two ? &plan.regions[1].geom : nullptr;
-    const uint32_t more[8] = {rc == KW_OK ? (uint32_t)plan.regions.size() : 0u, (uint32_t)split,
+    uint32_t more[8] = {rc == KW_OK ? (uint32_t)plan.regions.size() : 0u, (uint32_t)split,
                               rc == KW_OK ? plan.regions[0].grid : 0u, H ? H->lds_bytes : 0u, H ? H->rows : 0u,
                               H ? H->cmax : 0u, two ? plan.regions[1].grid : 0u, 0u};
+    if (rc == KW_OK)  // regions launched as the wave-scan instantiation (kFeatRng), one bit each
+      for (size_t k = 0; k < plan.regions.size() && k < 32; ++k) more[7] |= (plan.regions[k].geom.feat & kFeatRng) ? 1u << k : 0u;
     for (int i = 0; i < 8; ++i) out[8 + i] = more[i];
   }
   kb->dev->verdicts = nullptr;  // host memory: not the DeviceBatch's to free

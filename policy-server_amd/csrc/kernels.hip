@@ -401,6 +401,40 @@ __device__ inline uint64_t or_range(const uint64_t* a, uint32_t lo, uint32_t hi)
   return r;
 }
 
+// A 64-bit value from another lane by DPP (CTRL: row_shr:n 0x110+n, row_bcast:15 0x142, row_bcast:31
+// 0x143, wave_shr:1 0x138; rows outside ROWS and lanes with no source read 0). The move must run
+// on every lane (a disabled source lane reads as no source), so the volatile asm keeps the
+// compiler from folding the caller's select into the move's EXEC mask.
+template <int CTRL, int ROWS>
+__device__ inline uint64_t dpp64(uint64_t v) {
+  uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, ROWS, 0xf, false);
+  uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, ROWS, 0xf, false);
+  asm volatile("" : "+v"(lo), "+v"(hi));
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Segmented exclusive OR-scan over the wave's 64 lanes (all active): lane l, item i = base + l, gets
+// the OR of x over the lanes l' < l whose item is >= first (the first item of l's segment). Row
+// shifts within 16 lanes, then the row broadcasts of lanes 15 / 31 (GFX9 DPP), then one wave shift.
+__device__ inline uint64_t seg_or_scan_excl(uint64_t x, uint32_t lane, uint32_t i, uint32_t first) {
+  const uint32_t r = lane & 15u;
+  uint64_t y;
+  y = dpp64<0x111, 0xf>(x);
+  x |= (first + 1u <= i) ? y : 0ull;
+  y = dpp64<0x112, 0xf>(x);
+  x |= (first + 2u <= i) ? y : 0ull;
+  y = dpp64<0x114, 0xf>(x);
+  x |= (first + 4u <= i) ? y : 0ull;
+  y = dpp64<0x118, 0xf>(x);
+  x |= (first + 8u <= i) ? y : 0ull;
+  y = dpp64<0x142, 0xa>(x);  // rows 1, 3: lane 16 row - 1
+  x |= (first + r + 1u <= i) ? y : 0ull;
+  y = dpp64<0x143, 0xc>(x);  // rows 2, 3: lane 31
+  x |= (lane >= 32u && first + lane - 31u <= i) ? y : 0ull;
+  y = dpp64<0x138, 0xf>(x);
+  return (first + 1u <= i) ? y : 0ull;
+}
+
 // ------------------------------------------------------------------------------------------
 // The tile kernel
 // ------------------------------------------------------------------------------------------
@@ -472,6 +506,7 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
   // container families (pod-privileged, psp-capabilities, psp-apparmor), group columns
   constexpr bool IMG = (F & kFeatImg) != 0, LBL = (F & kFeatLbl) != 0, CTR = (F & kFeatCtr) != 0, GRP = (F & kFeatGrp) != 0;
   constexpr bool NFA = (F & kFeatNfa) != 0;  // classifiers with NFA elements (their classes precomputed in HBM)
+  constexpr bool RNG = (F & kFeatRng) != 0;  // many containers per request: predecessor sets by wave scan
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
@@ -849,15 +884,39 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
           seg(w < f0 ? SG_P2_CTR : w < f1 ? SG_P2_LABEL : SG_P2_REQ);
           if (w < f0) {  // container
             const uint32_t i = w;
+            const bool capv = CTR && SH.caps != 0;
+            uint32_t q, c0, ka0, ka, ka1;
+            uint64_t pre = 0, own;
+            if constexpr (RNG) {
+              // many containers per request: a container's set X = its own families', its image's and
+              // its added capabilities'; the predecessors' union is a segmented exclusive OR-scan of X
+              // over the wave's lanes (a segment = one request's containers), plus, for a request
+              // that began before this wave's first container, the OR of that part from LDS.
+              const bool act = i < n1;
+              q = act ? own_c[i] : 0u;
+              c0 = act ? l_coff[q] - cb : i;
+              ka = act ? l_cadd[i] - kab : 0u;
+              ka1 = act ? l_cadd[i + 1] - kab : 0u;
+              own = act ? vset(i) : 0ull;
+              if (capv) own |= or_range(l_vadd, ka, ka1);
+              // lane 0 adds the part of its request before this wave (c0 < i): the scan hands it on
+              uint64_t carry = 0;
+              if (lane == 0u && c0 < i) {
+                carry = (CTR ? or_range(l_vc, c0, i) : 0ull) | (trs ? or_range(l_vtr, c0, i) : 0ull);
+                if (capv) carry |= or_range(l_vadd, l_cadd[c0] - kab, ka);
+              }
+              pre = seg_or_scan_excl(own | carry, lane, i, c0) | carry;
+              if (t.debug & 4096u) pre = 0;  // (ablation bit 4096: no predecessor ORs, in every form)
+              if (!act || !(l_rf[q] & KW_REQ_HAS_PODSPEC)) continue;
+            } else {
             if (i >= n1) continue;
-            const uint32_t q = own_c[i];
+            q = own_c[i];
             if (!(l_rf[q] & KW_REQ_HAS_PODSPEC)) continue;
-            const uint32_t c0 = l_coff[q] - cb;
+            c0 = l_coff[q] - cb;
             // predecessors' sets: their own families' and images', and their added capabilities'
             // (a contiguous range of l_vadd); the same for this container
-            const bool capv = CTR && SH.caps != 0;
-            const uint32_t ka0 = l_cadd[c0] - kab, ka = l_cadd[i] - kab, ka1 = l_cadd[i + 1] - kab;
-            uint64_t pre = 0, own = vset(i);
+            ka0 = l_cadd[c0] - kab, ka = l_cadd[i] - kab, ka1 = l_cadd[i + 1] - kab;
+            own = vset(i);
             if (t.ctr_ranges) {  // many containers per request: the ranges four loads a round
               if (!(t.debug & 4096u)) {  // (ablation bit 4096: no predecessor ORs, in both forms)
                 pre = (CTR ? or_range(l_vc, c0, i) : 0ull) | (trs ? or_range(l_vtr, c0, i) : 0ull);
@@ -872,6 +931,7 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
               }
               if (capv)
                 for (uint32_t k = ka; k < ka1; ++k) own |= l_vadd[k];
+            }
             }
             const uint64_t nv = own & ~pre;
             const uint32_t ci = i - c0;
@@ -1499,15 +1559,17 @@ const void* tile_fn(bool ldst, bool timing, uint32_t feat) {
   if (feat & kFeatNfa)  // the one instantiation with NFA elements: every family (timing runs it too)
     return ldst ? (const void*)evaluate_tiles_kernel<true, false, kFeatAll | kFeatNfa>
                 : (const void*)evaluate_tiles_kernel<false, false, kFeatAll | kFeatNfa>;
+  if ((feat & kFeatRng) && ldst && !timing && (feat & kFeatAll) == (kFeatLbl | kFeatCtr))
+    return (const void*)evaluate_tiles_kernel<true, false, kFeatLbl | kFeatCtr | kFeatRng>;
   if (timing) {  // diagnostics: the C2 / C3 / C4 family sets with LDS tables (same registers as the product), else every family
-    if (ldst && feat == kFeatImg) return (const void*)evaluate_tiles_kernel<true, true, kFeatImg>;
-    if (ldst && feat == (kFeatImg | kFeatGrp)) return (const void*)evaluate_tiles_kernel<true, true, kFeatImg | kFeatGrp>;
-    if (ldst && feat == (kFeatLbl | kFeatCtr)) return (const void*)evaluate_tiles_kernel<true, true, kFeatLbl | kFeatCtr>;
+    if (ldst && (feat & kFeatAll) == kFeatImg) return (const void*)evaluate_tiles_kernel<true, true, kFeatImg>;
+    if (ldst && (feat & kFeatAll) == (kFeatImg | kFeatGrp)) return (const void*)evaluate_tiles_kernel<true, true, kFeatImg | kFeatGrp>;
+    if (ldst && (feat & kFeatAll) == (kFeatLbl | kFeatCtr)) return (const void*)evaluate_tiles_kernel<true, true, kFeatLbl | kFeatCtr>;
     return ldst ? (const void*)evaluate_tiles_kernel<true, true, kFeatAll> : (const void*)evaluate_tiles_kernel<false, true, kFeatAll>;
   }
   return ldst ? l[feat & kFeatAll] : g[feat & kFeatAll];
 }
-uint32_t tile_feat(const TileArgs& t) { return t.feat & (kFeatAll | kFeatNfa); }
+uint32_t tile_feat(const TileArgs& t) { return t.feat & (kFeatAll | kFeatNfa | kFeatRng); }
 
 hipError_t ensure_attrs() {
   int dev = 0;
@@ -1517,8 +1579,8 @@ hipError_t ensure_attrs() {
   std::call_once(g_attr_once[dev], [dev] {
     // allow > 64 KB of dynamic LDS per workgroup (gfx950: 160 KB per CU)
     hipError_t e = hipSuccess;
-    for (int k = 0; k < 68; ++k) {  // (LDS tables, timing, families; then the two NFA instantiations)
-      const uint32_t feat = k < 64 ? (uint32_t)(k >> 2) & kFeatAll : (kFeatAll | kFeatNfa);
+    for (int k = 0; k < 70; ++k) {  // (LDS tables, timing, families; the two NFA instantiations; the scan one at k = 69)
+      const uint32_t feat = k < 64 ? (uint32_t)(k >> 2) & kFeatAll : k < 68 ? (kFeatAll | kFeatNfa) : (kFeatLbl | kFeatCtr | kFeatRng);
       const hipError_t ek =
           hipFuncSetAttribute(tile_fn(k & 1, (k & 2) != 0, feat), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e == hipSuccess) e = ek;

@@ -82,6 +82,10 @@ constexpr uint32_t kFeatImg = 1, kFeatLbl = 2, kFeatCtr = 4, kFeatGrp = 8, kFeat
 // A pass whose classifiers hold NFA elements runs the one instantiation that reads their classes
 // (kFeatAll | kFeatNfa): no other instantiation carries that code.
 constexpr uint32_t kFeatNfa = 16;
+// Tiles with many containers per request (TileArgs::ctr_ranges) in the label / container family set
+// with LDS tables (C5's heavy region): P2 takes a container's predecessor sets from a segmented
+// wave OR-scan. Its own instantiation, so the others (C4's) keep their code and registers.
+constexpr uint32_t kFeatRng = 32;
 #ifndef KW_PREFETCH  // tile kernel: the code of the next-tile L2 prefetch (run only when the plan asks:
 #define KW_PREFETCH 1   // capi.cpp l2_prefetch, off by default; r02 s60: running it cost C4 0.3442 vs 0.3294 ms)
 #endif

@@ -413,8 +413,8 @@ class Batch:
         out = (C.c_uint32 * 16)()
         raise_for(self._L.kw_debug_plan(env._h, self._h, arr, len(policies), origin, out, 16), "kw_debug_plan failed")
         keys = ("lds_bytes", "launches", "chunks", "lds_tables", "rows", "cmax", "kmax", "lmax", "regions", "split",
-                "grid", "heavy_lds_bytes", "heavy_rows", "heavy_cmax", "heavy_grid")
-        return dict(zip(keys, out[:15]))
+                "grid", "heavy_lds_bytes", "heavy_rows", "heavy_cmax", "heavy_grid", "scan_regions")
+        return dict(zip(keys, out[:16]))
 
     def debug_reorder(self):
         """Diagnostic (kw_debug_reorder): the device-row order kw_batch_to_device gives this batch,

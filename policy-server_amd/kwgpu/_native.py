@@ -105,6 +105,14 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
+    # One HIP runtime per process. The torch wheel bundles its own libamdhip64 (soname
+    # libamdhip64.so.7, needed by torch as "libamdhip64.so"): loaded first, it also serves this
+    # library's libamdhip64.so.7; loaded after /opt/rocm's, it is a second runtime that then finds
+    # no GPU ("No HIP GPUs are available" on the caller's first torch stream). So torch goes first.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     vp, sz, i32, u32, u64 = C.c_void_p, C.c_size_t, C.c_int32, C.c_uint32, C.c_uint64
     cp, ip = C.c_char_p, C.c_int
