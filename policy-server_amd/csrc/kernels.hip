@@ -763,15 +763,23 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
           const uint32_t k = lit(COL_LK, S_LK, i);
           c_lk[i] = (uint16_t)k;
           uint16_t* lv = c_lv + i * nlv;
+          // chunk 0's failed-constraint slots folded in as the walk yields each value class; the
+          // classes themselves are stored only for a pass whose later chunks rederive l_vl (D)
+          const bool keep = t.nchunk > 1u;
+          uint64_t vf = 0;
+          auto out = [&](uint32_t j, uint32_t c) {
+            if (keep) lv[j] = (uint16_t)c;
+            if (h0.lbl && c != 0xffffu) vf |= sv0.row(T_FAIL, c);
+          };
           if (k && classify && t.o_sb[S_LV] && !(t.debug & 2048u)) {
             uint32_t b, e;
             str(S_LV, i, &b, &e);
-            classify_value<NFA>(C, LDST && t.kv_lds, k, nlv, lds + t.o_sb[S_LV], b, e, [&](uint32_t j, uint32_t c) { lv[j] = (uint16_t)c; },
+            classify_value<NFA>(C, LDST && t.kv_lds, k, nlv, lds + t.o_sb[S_LV], b, e, out,
                                 NFA ? a.nfa_lv + (uint64_t)(lb + i) * nlv : nullptr);
-          } else {
+          } else if (keep) {
             for (uint32_t j = 0; j < nlv; ++j) lv[j] = 0xffffu;
           }
-          l_vl[i] = dv_label(sv0, k, lv, nlv);
+          l_vl[i] = (h0.lbl && k) ? sv0.row(T_DENY, k) | vf : 0ull;  // (dv_label's sets)
         } else if (CTR && w < e0) {  // capability string: added ones first, then dropped ones
           const uint32_t k = w - ek;
           if (k >= nk) continue;
