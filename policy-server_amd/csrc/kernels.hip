@@ -267,6 +267,85 @@ __device__ inline void classify_image(const Classifiers& C, const ImgLayout& il,
 template <int AS>
 using as_ptr = const __attribute__((address_space(AS))) uint8_t*;
 
+// A label-value chain record (two 16-B loads: a struct copy cannot bind an address-space-qualified
+// reference).
+template <int AS>
+__device__ inline KvDfa kv_record(as_ptr<AS> R, uint32_t rel) {
+  typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+  typedef const __attribute__((address_space(AS))) v4* v4p;
+  KvDfa d;
+  const v4 lo = ((v4p)(R + rel))[0], hi = ((v4p)(R + rel))[1];
+  __builtin_memcpy(&d, &lo, 16);
+  __builtin_memcpy((uint8_t*)&d + 16, &hi, 16);
+  return d;
+}
+
+// One DFA of a chain over bytes [b, e) from d.start: the final state. 8-byte windows: the window's
+// dwords, then its 8 byte classes, load as two batches; only the transitions form a dependent chain
+// (bytes past the string read the zero tail, unused); the walk ends at a window starting in the dead
+// state or an absorbing one.
+template <int AS>
+__device__ inline uint32_t kv_walk(as_ptr<AS> R, const KvDfa& d, const uint8_t* __restrict__ bytes, uint32_t b, uint32_t e) {
+  typedef const __attribute__((address_space(AS))) uint16_t* u16p;
+  uint32_t st = d.start;
+  for (uint32_t p = b; p < e && dfa_live(st, d.abs_lo); p += 8u) {
+    const uint32_t* q = (const uint32_t*)(bytes + (p & ~3u));
+    const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], sh = p & 3u;
+    const uint32_t x0 = align_bytes(q1, q0, sh), x1 = align_bytes(q2, q1, sh);
+    uint32_t c[8];
+    const uint32_t lim = min(8u, e - p);
+    if constexpr (AS == 3) {
+      // LDS region: branch-free (every class load and step of the window runs; `fin` keeps the
+      // state after the lane's last byte; a step no lane of the wave needs ends the window). The
+      // global-table form below keeps its masked steps: extra lanes' gathers cost L2 bandwidth.
+      // Classes come out as LDS byte addresses of their column in the transition table (tb +
+      // class << t16), so a step is one 24-bit multiply-add and the load (trans_at).
+      const uint32_t t16 = d.t16, tb = (uint32_t)(uintptr_t)(R + d.trans_off), ncs = (uint32_t)d.ncls << t16;
+      const uint32_t bm = 128u + (uint32_t)d.wide * 127u;  // narrow maps: entry 128 is the class of bytes >= 128 (wide: 0 / 1)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t by = ((i < 4 ? x0 : x1) >> (8 * (i & 3))) & 0xffu;
+        c[i] = tb + ((uint32_t)R[d.cls_off + min(by, bm)] << t16);
+      }
+      uint32_t fin = st;
+      if (t16) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          if (i > 0 && !__any((uint32_t)i < lim)) break;
+          st = *(u16p)(uintptr_t)trans_at(st, ncs, c[i]);
+          fin = (uint32_t)i < lim ? st : fin;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          if (i > 0 && !__any((uint32_t)i < lim)) break;
+          st = *(as_ptr<AS>)(uintptr_t)trans_at(st, ncs, c[i]);
+          fin = (uint32_t)i < lim ? st : fin;
+        }
+      }
+      st = fin;
+      continue;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t by = ((i < 4 ? x0 : x1) >> (8 * (i & 3))) & 0xffu;
+      c[i] = R[d.cls_off + min(by, 128u + (uint32_t)d.wide * 127u)];
+    }
+    const as_ptr<AS> tr = R + d.trans_off;
+    if (d.t16) {
+      const uint32_t nc2 = (uint32_t)d.ncls << 1;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if ((uint32_t)i < lim) st = *(u16p)(tr + trans_at(st, nc2, c[i] << 1));
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if ((uint32_t)i < lim) st = tr[trans_at(st, d.ncls, c[i])];
+    }
+  }
+  return st;
+}
+
 template <int AS, bool NFA, class Out>
 __device__ inline uint32_t classify_value_as(as_ptr<AS> R, uint32_t nlk, uint32_t k, const uint8_t* __restrict__ bytes,
                                              uint32_t b, uint32_t e, Out out, const uint16_t* __restrict__ nfa_row) {
@@ -275,79 +354,14 @@ __device__ inline uint32_t classify_value_as(as_ptr<AS> R, uint32_t nlk, uint32_
   uint32_t j = 0;
   const uint32_t kbase = ((u32p)R)[nlk + k];
   for (uint32_t rel = ((u32p)R)[k]; rel;) {
-    KvDfa d;  // two 16-B loads (a struct copy cannot bind an address-space-qualified reference)
-    {
-      typedef uint32_t v4 __attribute__((ext_vector_type(4)));
-      typedef const __attribute__((address_space(AS))) v4* v4p;
-      const v4 lo = ((v4p)(R + rel))[0], hi = ((v4p)(R + rel))[1];
-      __builtin_memcpy(&d, &lo, 16);
-      __builtin_memcpy((uint8_t*)&d + 16, &hi, 16);
-    }
+    const KvDfa d = kv_record<AS>(R, rel);
     if (NFA && d.nfa) {  // an NFA element: its class from the pass's nfa_classify_kernel
       out(j, (uint32_t)nfa_row[j]);
       ++j;
       rel = d.next;
       continue;
     }
-    uint32_t st = d.start;
-    // 8-byte windows: the window's dwords, then its 8 byte classes, load as two batches; only the
-    // transitions form a dependent chain (bytes past the string read the zero tail, unused); the
-    // walk ends at a window starting in the dead state or an absorbing one
-    for (uint32_t p = b; p < e && dfa_live(st, d.abs_lo); p += 8u) {
-      const uint32_t* q = (const uint32_t*)(bytes + (p & ~3u));
-      const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], sh = p & 3u;
-      const uint32_t x0 = align_bytes(q1, q0, sh), x1 = align_bytes(q2, q1, sh);
-      uint32_t c[8];
-      const uint32_t lim = min(8u, e - p);
-      if constexpr (AS == 3) {
-        // LDS region: branch-free (every class load and step of the window runs; `fin` keeps the
-        // state after the lane's last byte; a step no lane of the wave needs ends the window). The
-        // global-table form below keeps its masked steps: extra lanes' gathers cost L2 bandwidth.
-        // Classes come out as LDS byte addresses of their column in the transition table (tb +
-        // class << t16), so a step is one 24-bit multiply-add and the load (trans_at).
-        const uint32_t t16 = d.t16, tb = (uint32_t)(uintptr_t)(R + d.trans_off), ncs = (uint32_t)d.ncls << t16;
-        const uint32_t bm = 128u + (uint32_t)d.wide * 127u;  // narrow maps: entry 128 is the class of bytes >= 128 (wide: 0 / 1)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const uint32_t by = ((i < 4 ? x0 : x1) >> (8 * (i & 3))) & 0xffu;
-          c[i] = tb + ((uint32_t)R[d.cls_off + min(by, bm)] << t16);
-        }
-        uint32_t fin = st;
-        if (t16) {
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            if (i > 0 && !__any((uint32_t)i < lim)) break;
-            st = *(u16p)(uintptr_t)trans_at(st, ncs, c[i]);
-            fin = (uint32_t)i < lim ? st : fin;
-          }
-        } else {
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            if (i > 0 && !__any((uint32_t)i < lim)) break;
-            st = *(as_ptr<AS>)(uintptr_t)trans_at(st, ncs, c[i]);
-            fin = (uint32_t)i < lim ? st : fin;
-          }
-        }
-        st = fin;
-        continue;
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const uint32_t by = ((i < 4 ? x0 : x1) >> (8 * (i & 3))) & 0xffu;
-        c[i] = R[d.cls_off + min(by, 128u + (uint32_t)d.wide * 127u)];
-      }
-      const as_ptr<AS> tr = R + d.trans_off;
-      if (d.t16) {
-        const uint32_t nc2 = (uint32_t)d.ncls << 1;
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          if ((uint32_t)i < lim) st = *(u16p)(tr + trans_at(st, nc2, c[i] << 1));
-      } else {
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          if ((uint32_t)i < lim) st = tr[trans_at(st, d.ncls, c[i])];
-      }
-    }
+    const uint32_t st = kv_walk<AS>(R, d, bytes, b, e);
     out(j++, kbase + d.cbase + ((u16p)(R + d.acc_off))[st]);
     rel = d.next;
   }
@@ -754,11 +768,92 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
       const uint32_t n1 = (IMG && (need & (1u << S_IMG))) ? nc : 0u;
       const uint32_t n0 = nr;
       const uint32_t ek = rup64(n3), e0 = ek + rup64(nk), e1 = e0 + rup64(n2), e2 = e1 + rup64(n1), e3 = e2 + rup64(n0);
+      // helper lanes for second label-value DFAs (below): LDS tables, chains of at most two DFAs, and
+      // one chunk (its class array, unused then, holds the 4 waves' 128-B mailboxes)
+      const bool label_pairs = LDST && C.kv && t.kv_lds && nlv == 2u && t.nchunk == 1u && t.lmax >= 128u && classify &&
+                               t.o_sb[S_LV] && !(t.debug & 2048u);
       const uint64_t p1_t0 = timing ? clock64() : 0;
       for (uint32_t w = tid; w < e3; w += kSlotThreads) {
         seg(w < ek ? SG_P1_LABEL : w < e0 ? SG_P1_CAPSTR : w < e1 ? SG_P1_CTR : w < e2 ? SG_P1_IMAGE : SG_P1_REQ);
         if (LBL && w < ek) {  // label
           const uint32_t i = w;
+          if (!NFA && LDST && label_pairs) {
+            // Two-DFA chains, single-chunk pass: a wave walks one DFA per lane, not two. A label whose
+            // key's chain has a second DFA hands that walk to a lane with nothing to walk (a key
+            // without value constraints, or past the tile's labels): the n-th such label to the
+            // n-th idle lane, matched through a per-wave mailbox in the (here unused) class array;
+            // the task and its class cross lanes by ds_bpermute. Labels left without a helper walk
+            // their second DFA themselves.
+            const bool act = i < n3;
+            uint32_t k = 0;
+            if (act) {
+              k = lit(COL_LK, S_LK, i);
+              c_lk[i] = (uint16_t)k;
+            }
+            const as_ptr<3> R = (as_ptr<3>)C.kv;
+            typedef const __attribute__((address_space(3))) uint32_t* u32l;
+            typedef const __attribute__((address_space(3))) uint16_t* u16l;
+            uint32_t b = 0, e = 0, rel1 = 0, rel2 = 0, kbase = 0;
+            if (k) {
+              str(S_LV, i, &b, &e);
+              rel1 = ((u32l)R)[k];
+              kbase = ((u32l)R)[C.nlk + k];
+            }
+            if (rel1) rel2 = kv_record<3>(R, rel1).next;
+            const uint64_t needm = __ballot(rel2 != 0u), idlem = __ballot(rel1 == 0u);
+            uint32_t wrel = rel1, wb = b, we = e, wkb = kbase, helper = 64u;
+            if (needm) {
+              uint8_t* mb = (uint8_t*)c_lv + wave * 128u;
+              const uint32_t rn = __builtin_amdgcn_mbcnt_hi((uint32_t)(needm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)needm, 0u));
+              const uint32_t ri = __builtin_amdgcn_mbcnt_hi((uint32_t)(idlem >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idlem, 0u));
+              const uint32_t nidle = (uint32_t)__popcll(idlem), nneed = (uint32_t)__popcll(needm);
+              if (rel1 == 0u) mb[ri] = (uint8_t)lane;
+              if (rel2) mb[64u + rn] = (uint8_t)lane;
+              // (a wave's LDS operations complete in order: the reads below see these writes; the
+              // empty asm keeps the compiler from moving a read above another lane's write)
+              asm volatile("" ::: "memory");
+              helper = (rel2 && rn < nidle) ? mb[rn] : 64u;
+              const uint32_t served = (rel1 == 0u && ri < nneed) ? mb[64u + ri] : lane;
+              const int sa = (int)(served * 4u);
+              const uint32_t t_rel = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)rel2);
+              const uint32_t t_b = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)b);
+              const uint32_t t_e = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)e);
+              const uint32_t t_kb = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)kbase);
+              if (served != lane) {
+                wrel = t_rel;
+                wb = t_b;
+                we = t_e;
+                wkb = t_kb;
+              }
+            }
+            // walk 0: the lane's first DFA (or its served lane's second); walk 1: second DFAs no
+            // idle lane took
+            uint32_t res[2] = {0xffffu, 0xffffu};
+#pragma nounroll
+            for (uint32_t it = 0; it < 2u; ++it) {
+              const bool self2 = rel2 && helper == 64u;
+              if (it == 1u && !__any(self2)) break;
+              const uint32_t r = it == 0u ? wrel : (self2 ? rel2 : 0u);
+              if (r) {
+                const KvDfa d = kv_record<3>(R, r);
+                const uint32_t st = kv_walk<3>(R, d, lds + t.o_sb[S_LV], it == 0u ? wb : b, it == 0u ? we : e);
+                res[it] = (it == 0u ? wkb : kbase) + d.cbase + ((u16l)(R + d.acc_off))[st];
+              }
+            }
+            const uint32_t hc = needm ? (uint32_t)__builtin_amdgcn_ds_bpermute((int)((helper < 64u ? helper : lane) * 4u), (int)res[0]) : 0u;
+            if (act) {
+              const uint32_t c1 = rel1 ? res[0] : 0xffffu;
+              const uint32_t c2 = rel2 ? (helper < 64u ? hc : res[1]) : 0xffffu;
+              uint64_t v = 0;
+              if (h0.lbl && k) {
+                v = sv0.row(T_DENY, k);
+                if (c1 != 0xffffu) v |= sv0.row(T_FAIL, c1);
+                if (c2 != 0xffffu) v |= sv0.row(T_FAIL, c2);
+              }
+              l_vl[i] = v;
+            }
+            continue;
+          }
           if (i >= n3) continue;
           const uint32_t k = lit(COL_LK, S_LK, i);
           c_lk[i] = (uint16_t)k;
