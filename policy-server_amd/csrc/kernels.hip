@@ -711,9 +711,11 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
     // the next tile's staged ranges into L2 (covered by this tile's classification, walk and stores),
     // from its descriptor in LDS
     auto prefetch_next = [&]() {
-      // (instantiated for LDS-staged tables only: in the global-table instantiations the code made
-      // C6 2 % slower, while its presence in the others cut their SGPR spills, r04)
-      if (KW_PREFETCH && LDST && t.prefetch && next < t_hi) {
+      // (compiled only into the LDS-table image instantiations: its presence, never run, changes
+      // their register allocation — C2 -3.3 %, C3 -1.7 % against builds without it — while r05's
+      // label / container instantiations are 1.1-1.3 % faster without it and the global-table
+      // ones 2 % (r04); profiles/r05_prefetch_code_ab.txt)
+      if (KW_PREFETCH && LDST && IMG && t.prefetch && next < t_hi) {
         const TileDesc& dn = l_desc[cur ^ 1u];
         if (sfield(dn.fits)) {
           const uint64_t q0 = ((uint64_t)sfield(dn.r0hi) << 32) | sfield(dn.r0lo);
