@@ -652,6 +652,18 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
                                        (__attribute__((address_space(3))) void*)(l_desc + s), 4, 0, 0);
   };
   auto sfield = [](const uint32_t& f) -> uint32_t { return __builtin_amdgcn_readfirstlane(f); };
+  // P1 / P2 item blocks (64 items, one wave each, costliest segments first). DYNB (the instantiations
+  // without image code: C4, C5): a wave's first block is its own, each further one comes from the
+  // phase's LDS counter (l_nx[2] / l_nx[3]), so a wave that drew cheap blocks takes more instead of
+  // waiting at the barrier for one that drew costly ones (C5 -8 %, C4 flat). The image
+  // instantiations keep blocks strided by the waves (C2 +1.6 %, C3 +3.6 % with the counters;
+  // profiles/r05_dyn_blocks_ab.txt).
+  constexpr bool DYNB = !IMG;
+  auto next_block = [&](uint32_t k) -> uint32_t {
+    uint32_t v = 0;
+    if (lane == 0u) v = atomicAdd(&l_nx[2u + k], 1u);
+    return (kSlotThreads >> 6) + __builtin_amdgcn_readfirstlane(v);
+  };
   // Dynamic: a workgroup's first two tiles are static (the XCD's range in workgroup order), so a
   // launch does not open with every workgroup's counter fetches queued on one L2 line; the counter
   // hands out the range from its third tile-set on (value v = tile dbase + v). r05: the opening
@@ -700,6 +712,7 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
       glds_x4((const u32x4*)(t.s_bytes[m] + KW_DF(d.sa[m])), (u32x4*)(lds + t.o_sb[m]), KW_DF(d.nv[m]), tid);
     }
     for (uint32_t i = tid; i < nr; i += kSlotThreads) l_rej[i] = l_mut[i] = 0;
+    if (DYNB && tid == 0) l_nx[2] = l_nx[3] = 0;  // P1 / P2 block counters (below)
     if (tid < NSTR) l_sa[tid] = d.sa[tid];
 #undef KW_DF
     const uint64_t p0_end = timing ? clock64() : 0;
@@ -775,7 +788,7 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
       const bool label_pairs = LDST && C.kv && t.kv_lds && nlv == 2u && t.nchunk == 1u && t.lmax >= 128u && classify &&
                                t.o_sb[S_LV] && !(t.debug & 2048u);
       const uint64_t p1_t0 = timing ? clock64() : 0;
-      for (uint32_t w = tid; w < e3; w += kSlotThreads) {
+      for (uint32_t w = tid; w < e3; w = DYNB ? next_block(0u) * 64u + lane : w + kSlotThreads) {
         seg(w < ek ? SG_P1_LABEL : w < e0 ? SG_P1_CAPSTR : w < e1 ? SG_P1_CTR : w < e2 ? SG_P1_IMAGE : SG_P1_REQ);
         if (LBL && w < ek) {  // label
           const uint32_t i = w;
@@ -983,10 +996,12 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
         const uint32_t n1 = ctr_fam ? nc : 0u, n2 = (LBL && SH.lbl) ? nl : 0u;
         // a container's violation set: its own families' (V_c) and its image's (V_tr)
         auto vset = [&](uint32_t j) -> uint64_t { return (CTR ? l_vc[j] : 0ull) | (trs ? l_vtr[j] : 0ull); };
-        const uint32_t f0 = rup64(n1), f1 = f0 + rup64(n2), f2 = f1 + rup64(nr);
+        // item order: containers, labels, requests; DYNB: containers, requests, labels (the costly
+        // request block drawn before the label blocks, most of whose items end at once)
+        const uint32_t f0 = rup64(n1), f1 = f0 + rup64(DYNB ? nr : n2), f2 = f1 + rup64(DYNB ? n2 : nr);
         const uint64_t p2_t0 = timing ? clock64() : 0;
-        for (uint32_t w = tid; w < f2; w += kSlotThreads) {
-          seg(w < f0 ? SG_P2_CTR : w < f1 ? SG_P2_LABEL : SG_P2_REQ);
+        for (uint32_t w = tid; w < f2; w = DYNB ? next_block(1u) * 64u + lane : w + kSlotThreads) {
+          seg(w < f0 ? SG_P2_CTR : (w < f1) == DYNB ? SG_P2_REQ : SG_P2_LABEL);
           if (w < f0) {  // container
             const uint32_t i = w;
             const bool capv = CTR && SH.caps != 0;
@@ -1074,8 +1089,8 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
               const uint64_t mut = caps_mutation(sv, addm, dropm);
               if (mut) atomicOr((unsigned long long*)&l_mut[q], (unsigned long long)mut);
             }
-          } else if (LBL && w < f1) {  // label
-            const uint32_t i = w - f0;
+          } else if (LBL && (DYNB ? w >= f1 : w < f1)) {  // label
+            const uint32_t i = w - (DYNB ? f1 : f0);
             if (i >= n2) continue;
             const uint64_t v = l_vl[i];
             if (!v) continue;
@@ -1091,8 +1106,8 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
             vs.put(nv & den, KW_R_LABEL_DENIED, li);
             vs.put(nv & ~den, KW_R_LABEL_CONSTRAINT, li);
             atomicOr((unsigned long long*)&l_rej[q], (unsigned long long)nv);
-          } else if (w >= f1) {  // request: namespace, mandatory labels
-            const uint32_t i = w - f1;
+          } else if (DYNB ? w < f1 : w >= f1) {  // request: namespace, mandatory labels
+            const uint32_t i = w - (DYNB ? f0 : f1);
             if (i >= nr) continue;
             const uint32_t rf = l_rf[i];
             ViolSink vs{l_vw + i * t.vw_stride, nullptr};
@@ -1299,6 +1314,7 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
       }
       if (timing) sg_add(SG_P3_BUSY, clock64() - p3_t0);
       if (ck + 1 < t.nchunk) {
+        if (DYNB && tid == 0) l_nx[3] = 0;  // the next chunk's P2 block counter
         lds_barrier();  // the next chunk rewrites the violation sets and words
         mark(4);
       }
