@@ -948,7 +948,7 @@ int plan_pass(const kw_env* env, kw_batch* kb, const int32_t* pols, uint32_t npo
       T.o_mut = take(rows * 8);
       T.o_byp = take(rows);
       T.o_sa = take(NSTR * 4);
-      T.o_nx = take(8);
+      T.o_nx = take(16);  // (kernels.hpp TileArgs::o_nx)
       T.o_desc = take(2 * sizeof(TileDesc));
       T.o_pf = l2_prefetch() ? take(4 * kPfLanes) : 0u;
       // union: the staged strings (P0-P1) and the violation words (P2-P3)

@@ -116,7 +116,7 @@ struct TileArgs {
   uint32_t o_vadd, o_vl, o_vc, o_vtr;  // u64 violation sets: per added capability, per label, per container (2)
   uint32_t o_own_c, o_own_l;           // u8 tile-local request of each staged container / label
   uint32_t o_rej, o_mut, o_byp;        // per-request results: rejected / mutated slots, bypass flag
-  uint32_t o_nx;                       // u32[2]: the tile after next (dynamic schedule), double-buffered
+  uint32_t o_nx;                       // u32[4]: the tile after next (dynamic schedule), double-buffered; P1 / P2 block counters
   uint32_t o_desc;                     // TileDesc[2]: this tile's and the next tile's descriptor
   uint32_t o_pf;                       // 4 x kPfLanes B: LDS-DMA landing of the L2 prefetch (never read)
   uint32_t prefetch;                   // warm L2 with the next tile (small tiles at >= 3 workgroups per CU)
