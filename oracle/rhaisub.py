@@ -13,8 +13,14 @@ Values: None is (), bool, int (i64), str, list (array). Supported: let / const, 
 do-while / do-until, for over arrays and ranges (with a counter), break [value], continue, return,
 fn definitions (top level, overloaded by arity, no access to the caller's variables), array
 literals, indexing, `in` / `!in`, `??`, `a..b` / `a..=b` / range(a, b) as for-iterables and `in`
-operands, and the built-ins len, is_empty, contains, to_string, type_of, starts_with, ends_with,
-push. Everything else rhai has is refused by name ("unsupported by this engine: ..."). The engine
+operands, string `-`, and the functions of rhai's standard packages (Engine::new(), DESIGN.md
+§2.1) over these values: len is_empty contains to_string type_of starts_with ends_with push, abs
+sign is_zero is_odd is_even max min to_hex to_octal to_binary parse_int, to_upper to_lower
+make_upper make_lower trim sub_string crop index_of replace split split_rev bytes, append insert
+pop shift remove reverse sort clear truncate chop get set extract drain retain splice dedup pad.
+The packages' other names (_STD_REFUSED) and the constructs the engine leaves out are refused by
+name at load ("unsupported by this engine: ..."); an overload whose result type the engine lacks
+(a string's pop / get: characters; a string's pad) is refused by name when it runs. The engine
 limits of kwdev.hpp (16384 bytes built, 100000 loop iterations + calls, 64 nested calls, arrays 16
 deep in a comparison) are applied exactly as the product applies them.
 """
@@ -323,6 +329,8 @@ class _Parser:
                                             or self.at_op(",")):
                     val = self.expr(0)
                 return (w, val)
+        if any(self.at_id(w) for w in ("if", "switch", "while", "loop", "do", "for")) or self.at_op("{"):
+            return self.primary()  # a statement of its own: nothing continues it (rhai's parse_stmt)
         e = self.expr(0)
         for a in _ASSIGN:
             if self.at_op(a):
@@ -399,9 +407,9 @@ class _Parser:
                     self.err(UNSUP + f"property access (.{m})")
                 self.p += 1
                 args = [e] + self.arglist()
-                if m == "push" and e[0] == "index":
-                    self.err(UNSUP + "mutating an element in place (x[i].push(..))")
-                if m == "push" and e[0] == "var" and self.is_const(e[1]):
+                if m in _ALWAYS_MUT and e[0] == "index":
+                    self.err(UNSUP + f"mutating an element in place (x[i].{m}(..))")
+                if m in _ALWAYS_MUT and e[0] == "var" and self.is_const(e[1]):
                     self.err(f"Syntax error: cannot assign to the constant '{e[1]}'")
                 e = ("call", m, args, True)
             elif self.at_op("["):
@@ -653,8 +661,40 @@ def _stray_range(n, fns, members):
     return any(_stray_range(c, fns, members) for c, _ in _children(n))
 
 
+# rhai 1.21's standard packages (Engine::new()) over the engine's values: (name, arity) of every
+# function implemented here, those rhai gives a `&mut` first parameter (a method call on a variable
+# changes it), and the rest of the packages' names, refused by name at load
 _BUILTINS = {("len", 1), ("is_empty", 1), ("contains", 2), ("to_string", 1), ("type_of", 1), ("starts_with", 2),
-             ("ends_with", 2), ("push", 2)}
+             ("ends_with", 2), ("push", 2),
+             ("abs", 1), ("sign", 1), ("is_zero", 1), ("is_odd", 1), ("is_even", 1), ("max", 2), ("min", 2),
+             ("to_hex", 1), ("to_octal", 1), ("to_binary", 1), ("parse_int", 1), ("parse_int", 2),
+             ("to_upper", 1), ("to_lower", 1), ("make_upper", 1), ("make_lower", 1), ("trim", 1), ("sub_string", 2),
+             ("sub_string", 3), ("crop", 2), ("crop", 3), ("index_of", 2), ("index_of", 3), ("replace", 3),
+             ("split", 1), ("split", 2), ("split", 3), ("split_rev", 2), ("split_rev", 3), ("bytes", 1),
+             ("append", 2), ("insert", 3), ("pop", 1), ("shift", 1), ("remove", 2), ("reverse", 1), ("sort", 1),
+             ("clear", 1), ("truncate", 2), ("chop", 2), ("get", 2), ("set", 3), ("extract", 2), ("extract", 3),
+             ("drain", 3), ("retain", 3), ("splice", 4), ("dedup", 1), ("pad", 3)}
+_MUT = {("push", 2), ("make_upper", 1), ("make_lower", 1), ("trim", 1), ("crop", 2), ("crop", 3), ("replace", 3),
+        ("split", 2), ("append", 2), ("insert", 3), ("pop", 1), ("shift", 1), ("remove", 2), ("reverse", 1),
+        ("sort", 1), ("clear", 1), ("truncate", 2), ("chop", 2), ("set", 3), ("drain", 3), ("retain", 3),
+        ("splice", 4), ("dedup", 1), ("pad", 3)}
+_ALWAYS_MUT = {n for n, _ in _MUT} - {"split"}  # (split changes arrays only)
+_STD_REFUSED = {
+    "tag", "set_tag", "take", "sleep", "name", "is_anonymous", "to_debug",
+    "print", "debug", "eval", "Fn", "call", "curry", "is_def_var", "is_def_fn", "is_shared",
+    "get_bit", "set_bit", "get_bits", "set_bits", "bits",
+    "to_int", "to_float", "parse_float", "sqrt", "exp", "ln", "log", "floor", "ceiling", "round", "int", "fraction",
+    "is_nan", "is_finite", "is_infinite", "sin", "cos", "tan", "sinh", "cosh", "tanh", "asin", "acos", "atan",
+    "asinh", "acosh", "atanh", "hypot", "to_degrees", "to_radians", "PI", "E",
+    "chars", "to_chars",
+    "map", "filter", "reduce", "reduce_rev", "some", "all", "find", "find_map", "for_each", "zip", "sort_desc",
+    "blob", "to_blob", "as_string", "write_ascii", "write_utf8", "write_le", "write_be", "parse_le_int",
+    "parse_be_int", "parse_le_float", "parse_be_float",
+    "keys", "values", "mixin", "fill_with", "to_json",
+    "timestamp", "elapsed"}
+# White_Space (PropList.txt): Rust's char::is_whitespace, for trim / split() / parse_int
+_WS = "".join(map(chr, [9, 10, 11, 12, 13, 0x20, 0x85, 0xA0, 0x1680] + list(range(0x2000, 0x200B)) +
+                  [0x2028, 0x2029, 0x202F, 0x205F, 0x3000]))
 
 
 def _resolves(n, fns, members):
@@ -675,7 +715,22 @@ def parse(s, members):
         _walk_ranges(body, False)
     if _stray_range(root, ps.fns, members) or any(_stray_range(b, ps.fns, members) for _, b in ps.fns.values()):
         raise ExprError(UNSUP + "range values outside `for` and `in`")
+    for body in [root] + [b for _, b in ps.fns.values()]:
+        name = _refused(body, ps.fns, members)
+        if name:
+            raise ExprError(UNSUP + name)
     return Program(root, ps.fns)
+
+
+def _refused(n, fns, members):
+    """The first call of a standard-package function outside the engine (_STD_REFUSED), or None."""
+    if n[0] == "call" and n[1] in _STD_REFUSED and not _resolves(n, fns, members):
+        return n[1]
+    for c, _ in _children(n):
+        r = _refused(c, fns, members)
+        if r:
+            return r
+    return None
 
 
 # ----------------------------------------------------------------------------- evaluation
@@ -693,6 +748,103 @@ def type_name(v):
 
 def _kind(v):
     return type_name(v)
+
+
+def _offset_len(n, start, ln):
+    """rhai's calc_offset_len: (start, len) within n elements; a negative start counts from the end."""
+    if start < 0:
+        st = max(0, n + start)
+    elif start >= n:
+        return n, 0
+    else:
+        st = start
+    return st, 0 if ln <= 0 else min(ln, n - st)
+
+
+def _elem_index(n, i):
+    """The element position of get / set / remove, or None out of range."""
+    at = n + i if i < 0 else i
+    return at if 0 <= at < n else None
+
+
+def _sub_chars(s, start, ln):
+    if not s or ln <= 0:
+        return ""
+    n = len(s)
+    if start < 0:
+        off = max(0, n + start)
+    elif start >= n:
+        return ""
+    else:
+        off = start
+    return s[off:off + ln]
+
+
+def _split_ws(s):
+    out, cur = [], None
+    for ch in s:
+        if ch in _WS:
+            if cur is not None:
+                out.append(cur)
+            cur = None
+        else:
+            cur = (cur or "") + ch
+    if cur is not None:
+        out.append(cur)
+    return out
+
+
+def _rsplit_pieces(s, d, rev, lim):
+    """Rust's str::split / rsplit (and splitn / rsplitn with lim > 0). An empty pattern matches at
+    every character boundary, both ends included."""
+    if d:
+        if rev:
+            parts = s.rsplit(d, lim - 1) if lim else s.rsplit(d)
+            return parts[::-1]
+        return s.split(d, lim - 1) if lim else s.split(d)
+    cuts = list(range(len(s) + 1))  # match positions (characters)
+    out = []
+    if not rev:
+        prev = 0
+        for c in cuts:
+            if lim and len(out) + 1 == lim:
+                break
+            out.append(s[prev:c])
+            prev = c
+        out.append(s[prev:])
+    else:
+        prev = len(s)
+        for c in reversed(cuts):
+            if lim and len(out) + 1 == lim:
+                break
+            out.append(s[c:prev])
+            prev = c
+        out.append(s[:prev])
+    return out
+
+
+def _parse_int(text, radix):
+    """i64::from_str_radix(text.trim(), radix) with its ParseIntError texts, as rhai words them."""
+    t = text.strip(_WS)
+
+    def err(e):
+        raise ExprError(f"Error parsing integer number '{text}': {e}")
+    if not t:
+        err("cannot parse integer from empty string")
+    neg = t[0] == "-"
+    if t[0] in "+-":
+        t = t[1:]
+        if not t:
+            err("invalid digit found in string")
+    v = 0
+    for ch in t:
+        d = int(ch, 36) if ch.isascii() and ch.isalnum() else 99
+        if d >= radix:
+            err("invalid digit found in string")
+        v = v * radix + d
+        if (-v if neg else v) < I64_MIN or (-v if neg else v) > I64_MAX:
+            err("number too small to fit in target type" if neg else "number too large to fit in target type")
+    return -v if neg else v
 
 
 def _utf8len(s):
@@ -785,11 +937,24 @@ class Run:
         return at
 
     def builtin(self, name, args):
+        """A built-in over its arguments: its result; for a `&mut` function (_MUT) the pair
+        (receiver as changed, result). Charges as expr.cpp's interpreter states: a new string its
+        UTF-8 bytes, a new or copied array 16 B a cell; slices are free."""
         a = args
+        mut = (name, len(a)) in _MUT
+        kinds = [type_name(v) for v in a]
+
+        def out(recv, res):
+            return (recv, res) if mut else res
+
+        def refuse(why):
+            raise ExprError(UNSUP + f"{name} (" + ", ".join(kinds) + ")" + why)
+
+        def isa(k, t):
+            return len(a) > k and kinds[k] == t
+
         if name in ("len", "is_empty"):
-            if isinstance(a[0], list):
-                n = len(a[0])
-            elif isinstance(a[0], str):
+            if isinstance(a[0], (list, str)):
                 n = len(a[0])
             else:
                 self.nf(name, *a)
@@ -806,18 +971,246 @@ class Run:
             if not isinstance(a[0], list):
                 self.nf(name, *a)
             self.charge(16 * (len(a[0]) + 1))
-            return a[0] + [a[1]]
-        if name == "contains":
-            hay, x = a
+            return out(a[0] + [a[1]], None)
+        if name in ("contains", "index_of"):
+            if len(a) == 3 and not isa(2, "i64"):
+                self.nf(name, *a)
+            hay, x = a[0], a[1]
+            idx = name == "index_of"
             if isinstance(hay, list):
-                return any(self.equal(e, x) for e in hay)
+                start = _offset_len(len(hay), a[2], 0)[0] if len(a) == 3 else 0
+                for k in range(start, len(hay)):
+                    if self.equal(hay[k], x):
+                        return k if idx else True
+                return -1 if idx else False
             if isinstance(hay, str) and isinstance(x, str):
-                return x in hay
+                if not idx:
+                    return x in hay
+                if not hay:
+                    return -1
+                start = 0
+                if len(a) == 3:
+                    st, n = a[2], len(hay)
+                    if st < 0:
+                        start = max(0, n + st)
+                    elif st >= n and st != 0:
+                        return -1
+                    else:
+                        start = st
+                return hay.find(x, start)
             self.nf(name, *a)
         if name in ("starts_with", "ends_with"):
             if not (isinstance(a[0], str) and isinstance(a[1], str)):
                 self.nf(name, *a)
             return a[0].startswith(a[1]) if name == "starts_with" else a[0].endswith(a[1])
+        # ---- integers
+        if name in ("abs", "sign", "is_zero", "is_odd", "is_even", "to_hex", "to_octal", "to_binary"):
+            if not isa(0, "i64"):
+                self.nf(name, *a)
+            x = a[0]
+            if name == "abs":
+                if x == I64_MIN:
+                    raise ExprError(f"Negation overflow: -{x}")
+                return abs(x)
+            if name == "sign":
+                return (x > 0) - (x < 0)
+            if name in ("is_zero", "is_odd", "is_even"):
+                return {"is_zero": x == 0, "is_odd": x % 2 == 1, "is_even": x % 2 == 0}[name]
+            t = format(x & U64_MAX, {"to_hex": "x", "to_octal": "o", "to_binary": "b"}[name])
+            self.charge(len(t))
+            return t
+        if name in ("max", "min"):
+            if not (isa(0, "i64") and isa(1, "i64")):
+                self.nf(name, *a)
+            return max(a[0], a[1]) if name == "max" else min(a[0], a[1])
+        if name == "parse_int":
+            if not isa(0, "string") or (len(a) == 2 and not isa(1, "i64")):
+                self.nf(name, *a)
+            radix = a[1] if len(a) == 2 else 10
+            if not 2 <= radix <= 36:
+                raise ExprError(f"Invalid radix: '{radix}'")
+            return _parse_int(a[0], radix)
+        # ---- strings
+        if name in ("to_upper", "to_lower", "make_upper", "make_lower"):
+            if not isa(0, "string"):
+                self.nf(name, *a)
+            r = a[0].upper() if name.endswith("upper") else a[0].lower()
+            self.charge(_utf8len(r))
+            return r if name.startswith("to_") else (r, None)
+        if name == "trim":
+            if not isa(0, "string"):
+                self.nf(name, *a)
+            return a[0].strip(_WS), None
+        if name in ("sub_string", "crop"):
+            if not (isa(0, "string") and isa(1, "i64")) or (len(a) == 3 and not isa(2, "i64")):
+                self.nf(name, *a)
+            r = _sub_chars(a[0], a[1], a[2] if len(a) == 3 else _utf8len(a[0]))
+            return r if name == "sub_string" else (r, None)
+        if name == "replace":
+            if not all(isinstance(v, str) for v in a):
+                self.nf(name, *a)
+            if not a[0]:
+                return a[0], None
+            r = a[2].join(_rsplit_pieces(a[0], a[1], False, 0))
+            self.charge(_utf8len(r))
+            return r, None
+        if name in ("split", "split_rev"):
+            if name == "split" and len(a) == 2 and isinstance(a[0], list) and isa(1, "i64"):
+                st = _offset_len(len(a[0]), a[1], I64_MAX)[0]
+                return a[0][:st], a[0][st:]
+            if not isa(0, "string"):
+                self.nf(name, *a)
+            s = a[0]
+            if len(a) == 1:
+                parts = [p for p in _split_ws(s) if p]
+            elif name == "split" and len(a) == 2 and isa(1, "i64"):
+                i, n = a[1], len(s)
+                at = (0 if -i > n else n + i) if i <= 0 else min(i, n)
+                parts = [s[:at], s[at:]]
+            else:
+                if not isa(1, "string") or (len(a) == 3 and not isa(2, "i64")):
+                    self.nf(name, *a)
+                lim = (1 if a[2] < 1 else a[2]) if len(a) == 3 else 0
+                parts = _rsplit_pieces(s, a[1], name == "split_rev", lim)
+            self.charge(16 * len(parts))
+            return out(s, parts)
+        if name == "bytes":
+            if not isa(0, "string"):
+                self.nf(name, *a)
+            return _utf8len(a[0])
+        # ---- arrays, and the string forms of append / remove / clear / truncate
+        if name == "append":
+            if isinstance(a[0], list) and isinstance(a[1], list):
+                self.charge(16 * (len(a[0]) + len(a[1])))
+                return a[0] + a[1], None
+            if isinstance(a[0], str):
+                t = self.text(a[1])
+                self.charge(_utf8len(a[0]) + _utf8len(t))
+                return a[0] + t, None
+            self.nf(name, *a)
+        if name == "insert":
+            if not (isinstance(a[0], list) and isa(1, "i64")):
+                self.nf(name, *a)
+            self.charge(16 * (len(a[0]) + 1))
+            at = _offset_len(len(a[0]), a[1], 0)[0]
+            return a[0][:at] + [a[2]] + a[0][at:], None
+        if name in ("pop", "shift"):
+            if isinstance(a[0], str):
+                refuse(": it returns a character")
+            if not isinstance(a[0], list):
+                self.nf(name, *a)
+            v = a[0]
+            if not v:
+                return v, None
+            return (v[:-1], v[-1]) if name == "pop" else (v[1:], v[0])
+        if name == "remove":
+            if isinstance(a[0], str) and isinstance(a[1], str):
+                if not a[0] or not a[1]:
+                    return a[0], None
+                r = "".join(_rsplit_pieces(a[0], a[1], False, 0))
+                self.charge(_utf8len(r))
+                return r, None
+            if not (isinstance(a[0], list) and isa(1, "i64")):
+                self.nf(name, *a)
+            at = _elem_index(len(a[0]), a[1])
+            if at is None:
+                return a[0], None
+            self.charge(16 * (len(a[0]) - 1))
+            return a[0][:at] + a[0][at + 1:], a[0][at]
+        if name == "reverse":
+            if not isinstance(a[0], list):
+                self.nf(name, *a)
+            self.charge(16 * len(a[0]))
+            return a[0][::-1], None
+        if name == "sort":
+            if not isinstance(a[0], list):
+                self.nf(name, *a)
+            v = a[0]
+            if len(v) <= 1:
+                return v, None
+            ts = {type_name(e) for e in v}
+            if len(ts) > 1:
+                raise ExprError("Function not found: sort() cannot be called with elements of different types")
+            if ts <= {"array", "()"}:
+                return v, None
+            self.charge(16 * len(v))
+            return sorted(v), None  # (bool: False < True; str: code point order = Rust's byte order)
+        if name == "clear":
+            if isinstance(a[0], list):
+                return [], None
+            if isinstance(a[0], str):
+                return "", None
+            self.nf(name, *a)
+        if name in ("truncate", "chop"):
+            if not isa(1, "i64"):
+                self.nf(name, *a)
+            n = a[1]
+            if isinstance(a[0], str) and name == "truncate":
+                return ("" if n <= 0 else a[0][:n]), None
+            if not isinstance(a[0], list):
+                self.nf(name, *a)
+            v = a[0]
+            if n <= 0:
+                return [], None
+            if n >= len(v):
+                return v, None
+            return (v[:n] if name == "truncate" else v[len(v) - n:]), None
+        if name in ("get", "set"):
+            if isinstance(a[0], str) and isa(1, "i64"):
+                refuse(": characters")
+            if not (isinstance(a[0], list) and isa(1, "i64")):
+                self.nf(name, *a)
+            at = _elem_index(len(a[0]), a[1])
+            if name == "get":
+                return None if at is None else a[0][at]
+            if at is None:
+                return a[0], None
+            self.charge(16 * len(a[0]))
+            return a[0][:at] + [a[2]] + a[0][at + 1:], None
+        if name in ("extract", "drain", "retain"):
+            if not (isinstance(a[0], list) and isa(1, "i64")) or (len(a) == 3 and not isa(2, "i64")):
+                self.nf(name, *a)
+            v = a[0]
+            ln = a[2] if len(a) == 3 else I64_MAX
+            st, n = (0, 0) if not v or ln <= 0 else _offset_len(len(v), a[1], ln)
+            mid, rest = v[st:st + n], v[:st] + v[st + n:]
+            if name == "extract":
+                return mid if n else []
+            if n == 0:
+                return v, []
+            self.charge(16 * len(rest))
+            return (rest, mid) if name == "drain" else (mid, rest)
+        if name == "splice":
+            if not (isinstance(a[0], list) and isa(1, "i64") and isa(2, "i64") and isinstance(a[3], list)):
+                self.nf(name, *a)
+            v = a[0]
+            st, n = _offset_len(len(v), a[1], a[2]) if v else (0, 0)
+            self.charge(16 * (len(v) - n + len(a[3])))
+            return v[:st] + a[3] + v[st + n:], None
+        if name == "dedup":
+            if not isinstance(a[0], list):
+                self.nf(name, *a)
+            v = a[0]
+            if len(v) <= 1:
+                return v, None
+            r = [v[0]]
+            for e in v[1:]:
+                if not self.equal(e, r[-1]):
+                    r.append(e)
+            self.charge(16 * len(r))
+            return r, None
+        if name == "pad":
+            if isinstance(a[0], str) and isa(1, "i64"):
+                refuse(": padding strings")
+            if not (isinstance(a[0], list) and isa(1, "i64")):
+                self.nf(name, *a)
+            n = a[1]
+            if n <= 0 or n <= len(a[0]):
+                return a[0], None
+            if n > MAX_ALLOC:
+                raise ExprError(f"engine limit: more than {MAX_ALLOC} bytes of strings and arrays built")
+            self.charge(16 * n)
+            return a[0] + [a[2]] * (n - len(a[0])), None
         raise AssertionError(name)
 
     def arith(self, op, a, b, assign=False):
@@ -844,6 +1237,12 @@ class Run:
             joined = self.text(a) + self.text(b)
             self.charge(_utf8len(joined))
             return joined
+        if op == "-" and isinstance(a, str) and isinstance(b, str):  # every occurrence of b removed
+            if not a or not b:
+                return a
+            r = a.replace(b, "")
+            self.charge(_utf8len(r))
+            return r
         if not (_is_int(a) and _is_int(b)):
             self.nf(op, a, b)
         text = f"{a} {op} {b}"
@@ -917,11 +1316,12 @@ class Run:
             return bool(self.ok[s])
         if (name, len(args)) in _BUILTINS:
             v = self.builtin(name, args)
-            if name == "push" and method:
-                if argn[0][0] == "var":
-                    self.put(argn[0][1], v)
-                return None
-            return v
+            if (name, len(args)) not in _MUT:
+                return v
+            recv, res = v
+            if method and argn[0][0] == "var":  # rhai's `&mut` receiver: the variable changes
+                self.put(argn[0][1], recv)
+            return res
         self.nf(name, *args)
 
     def ev(self, n):

@@ -30,7 +30,6 @@
 
 using namespace kw;
 
-extern char** environ;  // (POSIX; kw_knob_hash)
 
 struct kw_env {
   Env e;
@@ -1682,12 +1681,20 @@ int run_validate(const kw_env* env, kw_batch* kb, PassPlan& plan, int origin, bo
   return KW_OK;
 }
 
-// A hash of every KW_* environment variable (tests and A/B knobs switch them between passes).
+// The plan cache's key for the diagnostic / A-B settings (tests switch them between passes): the
+// values of exactly the KW_* variables that planning reads (plan_pass and the planners it calls),
+// looked up by name — no walk over `environ`, which a concurrent setenv could free under it.
 uint64_t kw_knob_hash() {
+  static const char* const kPlanKnobs[] = {"KW_TILE_DEBUG", "KW_TILE_SPLIT", "KW_ROUND_SPLIT", "KW_L2_PREFETCH",
+                                           "KW_KV_GLOBAL", "KW_TILE_QUANTILE", "KW_SPLIT", "KW_SLOT_ROWS",
+                                           "KW_SCHED", "KW_HEAVY_ROWS", "KW_HEAVY_CTR", "KW_GLOBAL_TABLES",
+                                           "KW_NO_MPACK", "KW_POISON_VERDICTS", "KW_GROUP_FORM"};
   uint64_t h = 1469598103934665603ull;
-  for (char** e = environ; e && *e; ++e)
-    if ((*e)[0] == 'K' && (*e)[1] == 'W' && (*e)[2] == '_')
-      for (const char* c = *e; *c; ++c) h = (h ^ (uint8_t)*c) * 1099511628211ull;
+  for (const char* k : kPlanKnobs) {
+    const char* v = getenv(k);
+    h = (h ^ (v ? 0x100u : 0x200u)) * 1099511628211ull;
+    for (const char* c = v; c && *c; ++c) h = (h ^ (uint8_t)*c) * 1099511628211ull;
+  }
   return h;
 }
 
@@ -2669,7 +2676,10 @@ int validate_host(const kw_env* env, kw_batch* kb, const int32_t* policies, uint
   // slots: packing chunk k waits for chunk k - kRing's upload. KW_BULK_PACK=0: a copy per column
   // range (A/B knob, profiles/r05_bulk_copies.txt).
   constexpr uint64_t kRing = 4;
-  const bool packed = pack_knob && std::count(dma.begin(), dma.end(), 0) > 0;
+  // (the scatter kernel's argument holds kMaxScatterSegs ranges: a layout with more staged pieces
+  // than that — none today, 6 row pieces + 2 per string column — copies each range on its own)
+  const bool packed = pack_knob && std::count(dma.begin(), dma.end(), 0) > 0 &&
+                      (size_t)std::count(dma.begin(), dma.end(), 0) <= kMaxScatterSegs;
   size_t slot_bytes = 0;
   void *hpack = nullptr, *dland = nullptr;
   if (packed && rc == KW_OK) {

@@ -12,6 +12,7 @@
 #include <set>
 
 #include "kwdev.hpp"
+#include "unicode_data.hpp"
 
 namespace kw {
 
@@ -303,6 +304,89 @@ struct Lexer {
   }
 };
 
+// Built-in functions: rhai 1.21's standard packages (Engine::new()) over the
+// engine's values, one SFn id per (name, arity). `mut`: rhai gives the function a `&mut` first
+// parameter, so a method-style call on a variable changes the variable (a function-style call works
+// on a copy). Argument types are dispatched when the call runs, as rhai dispatches its overloads.
+struct BuiltinDef {
+  const char* name;
+  uint8_t nargs, fid;
+  bool mut;
+};
+const BuiltinDef kBuiltins[] = {
+    {"len", 1, F_LEN, false}, {"is_empty", 1, F_IS_EMPTY, false}, {"contains", 2, F_CONTAINS, false},
+    {"to_string", 1, F_TO_STRING, false}, {"type_of", 1, F_TYPE_OF, false}, {"starts_with", 2, F_STARTS_WITH, false},
+    {"ends_with", 2, F_ENDS_WITH, false}, {"push", 2, F_PUSH, true},
+    {"abs", 1, F_ABS, false}, {"sign", 1, F_SIGN, false}, {"is_zero", 1, F_IS_ZERO, false},
+    {"is_odd", 1, F_IS_ODD, false}, {"is_even", 1, F_IS_EVEN, false}, {"max", 2, F_MAX, false},
+    {"min", 2, F_MIN, false}, {"to_hex", 1, F_TO_HEX, false}, {"to_octal", 1, F_TO_OCTAL, false},
+    {"to_binary", 1, F_TO_BINARY, false}, {"parse_int", 1, F_PARSE_INT, false}, {"parse_int", 2, F_PARSE_INT_R, false},
+    {"to_upper", 1, F_TO_UPPER, false}, {"to_lower", 1, F_TO_LOWER, false}, {"make_upper", 1, F_MAKE_UPPER, true},
+    {"make_lower", 1, F_MAKE_LOWER, true}, {"trim", 1, F_TRIM, true}, {"sub_string", 2, F_SUB_STRING, false},
+    {"sub_string", 3, F_SUB_STRING_N, false}, {"crop", 2, F_CROP, true}, {"crop", 3, F_CROP_N, true},
+    {"index_of", 2, F_INDEX_OF, false}, {"index_of", 3, F_INDEX_OF_FROM, false}, {"replace", 3, F_REPLACE, true},
+    {"split", 1, F_SPLIT_WS, false}, {"split", 2, F_SPLIT, true}, {"split", 3, F_SPLIT_N, false},
+    {"split_rev", 2, F_SPLIT_REV, false}, {"split_rev", 3, F_SPLIT_REV_N, false}, {"bytes", 1, F_BYTES, false},
+    {"append", 2, F_APPEND, true}, {"insert", 3, F_INSERT, true}, {"pop", 1, F_POP, true}, {"shift", 1, F_SHIFT, true},
+    {"remove", 2, F_REMOVE, true}, {"reverse", 1, F_REVERSE, true}, {"sort", 1, F_SORT, true},
+    {"clear", 1, F_CLEAR, true}, {"truncate", 2, F_TRUNCATE, true}, {"chop", 2, F_CHOP, true},
+    {"get", 2, F_GET, false}, {"set", 3, F_SET, true}, {"extract", 2, F_EXTRACT, false},
+    {"extract", 3, F_EXTRACT_N, false}, {"drain", 3, F_DRAIN, true}, {"retain", 3, F_RETAIN, true},
+    {"splice", 4, F_SPLICE, true}, {"dedup", 1, F_DEDUP, true}, {"pad", 3, F_PAD, true},
+};
+
+int builtin_id(const std::string& name, size_t nargs) {
+  for (const BuiltinDef& b : kBuiltins)
+    if (name == b.name && nargs == b.nargs) return b.fid;
+  return -1;
+}
+bool builtin_mut(int fid) {
+  for (const BuiltinDef& b : kBuiltins)
+    if (b.fid == fid) return b.mut;
+  return false;
+}
+// a method that always changes its receiver (split changes arrays only): never on a constant or on
+// an element in place
+bool always_mutates(const std::string& m) {
+  for (const BuiltinDef& b : kBuiltins)
+    if (m == b.name && b.mut && b.fid != F_SPLIT) return true;
+  return false;
+}
+
+// The rest of rhai 1.21's standard packages (Engine::new(): CorePackage, BitFieldPackage,
+// BasicMathPackage, BasicArrayPackage, BasicBlobPackage, BasicMapPackage, BasicTimePackage,
+// MoreStringPackage; the language keywords are refused by the parser). A call of one of these names
+// that no script function or member takes is refused by name at load, as the engine's other
+// omissions are, never answered with rhai's own "Function not found".
+const char* const kStdRefused[] = {
+    // core and function pointers (LanguageCorePackage, BasicFnPackage)
+    "tag", "set_tag", "take", "sleep", "name", "is_anonymous", "to_debug",
+    // keyword functions in method style (as functions the parser refuses them by their own words)
+    "print", "debug", "eval", "Fn", "call", "curry", "is_def_var", "is_def_fn", "is_shared",
+    // bit fields
+    "get_bit", "set_bit", "get_bits", "set_bits", "bits",
+    // floating point and conversions
+    "to_int", "to_float", "parse_float", "sqrt", "exp", "ln", "log", "floor", "ceiling", "round", "int", "fraction",
+    "is_nan", "is_finite", "is_infinite", "sin", "cos", "tan", "sinh", "cosh", "tanh", "asin", "acos", "atan",
+    "asinh", "acosh", "atanh", "hypot", "to_degrees", "to_radians", "PI", "E",
+    // characters
+    "chars", "to_chars",
+    // arrays through function pointers
+    "map", "filter", "reduce", "reduce_rev", "some", "all", "find", "find_map", "for_each", "zip", "sort_desc",
+    // blobs
+    "blob", "to_blob", "as_string", "write_ascii", "write_utf8", "write_le", "write_be", "parse_le_int",
+    "parse_be_int", "parse_le_float", "parse_be_float",
+    // object maps
+    "keys", "values", "mixin", "fill_with", "to_json",
+    // time
+    "timestamp", "elapsed",
+};
+bool std_refused(const std::string& name) {
+  for (const char* r : kStdRefused)
+    if (name == r) return true;
+  return false;
+}
+
 bool is_kw(const std::string& s) {
   static const std::set<std::string> kw = {"let",   "const", "if",     "else",  "true", "false", "switch", "while",
                                            "loop",  "do",    "until",  "for",   "in",   "break", "continue",
@@ -495,6 +579,10 @@ struct Parser {
       }
       return n;
     }
+    // an if / switch / loop / block at the start of a statement is a statement of its own: no
+    // operator, index or method call continues it (rhai's parse_stmt; `for .. { } [1]` is two)
+    if (ident("if") || ident("switch") || ident("while") || ident("loop") || ident("do") || ident("for") || punct("{"))
+      return primary();
     P e = expr();
     if (!e) return nullptr;
     static const char* aops[] = {"=", "+=", "-=", "*=", "/=", "%=", "|=", "&=", "^="};
@@ -614,9 +702,9 @@ struct Parser {
         c->flag = true;
         c->kids.push_back(std::move(e));
         if (!args(&c->kids)) return nullptr;
-        if (m == "push" && c->kids[0]->k == Node::Index)
-          return unsupported("mutating an element in place (x[i].push(..))");
-        if (m == "push" && c->kids[0]->k == Node::Var && is_const_var(c->kids[0]->name))
+        if (always_mutates(m) && c->kids[0]->k == Node::Index)
+          return unsupported("mutating an element in place (x[i]." + m + "(..))");
+        if (always_mutates(m) && c->kids[0]->k == Node::Var && is_const_var(c->kids[0]->name))
           return fail("Syntax error: cannot assign to the constant '" + c->kids[0]->name + "'");
         e = std::move(c);
       } else if (punct("[")) {
@@ -927,15 +1015,6 @@ bool check_ranges(const Node* n, bool allowed, std::string* err) {
   return true;
 }
 
-int builtin_id(const std::string& name, size_t nargs) {
-  static const std::map<std::string, std::pair<int, size_t>> b = {
-      {"len", {F_LEN, 1}},          {"is_empty", {F_IS_EMPTY, 1}},       {"contains", {F_CONTAINS, 2}},
-      {"to_string", {F_TO_STRING, 1}}, {"type_of", {F_TYPE_OF, 1}},     {"starts_with", {F_STARTS_WITH, 2}},
-      {"ends_with", {F_ENDS_WITH, 2}}, {"push", {F_PUSH, 2}}};
-  auto it = b.find(name);
-  return it != b.end() && it->second.second == nargs ? it->second.first : -1;
-}
-
 // call resolution, as rhai's: a script function of that name and arity, else a member policy
 // (a native function of no arguments), else a built-in; anything else is "Function not found"
 // when called (after its arguments ran)
@@ -958,6 +1037,19 @@ void resolve(Node* n, const ExprAst& ast, const std::vector<std::string>& member
   }
 }
 
+// a call of a standard-package function the engine does not implement (kStdRefused): its name
+const Node* refused_call(const Node* n) {
+  if (n->k == Node::Call && n->fn < 0 && n->slot < 0 && n->builtin < 0 && std_refused(n->name)) return n;
+  for (const P& k : n->kids)
+    if (const Node* r = refused_call(k.get())) return r;
+  for (const SwitchCase& c : n->cases) {
+    if (c.guard)
+      if (const Node* r = refused_call(c.guard.get())) return r;
+    if (const Node* r = refused_call(c.body.get())) return r;
+  }
+  return nullptr;
+}
+
 // range(a, b) outside a `for` would be a range value: not supported (check_ranges)
 bool stray_range_call(const Node* n) {
   if (n->k == Node::Call && n->name == "range" && n->fn < 0 && n->slot < 0 && n->builtin < 0) return true;
@@ -966,6 +1058,211 @@ bool stray_range_call(const Node* n) {
   for (const SwitchCase& c : n->cases)
     if ((c.guard && stray_range_call(c.guard.get())) || stray_range_call(c.body.get())) return true;
   return false;
+}
+
+// ------------------------------------------------------------------------------------------
+// Strings as Rust's str methods see them (rhai's string functions are Rust's): code points of
+// valid UTF-8 (every string here is), White_Space, and the full case mappings with Σ's
+// Final_Sigma context (unicode_data.hpp, Unicode 13.0)
+// ------------------------------------------------------------------------------------------
+std::vector<uint32_t> cps_of(const std::string& s) {
+  std::vector<uint32_t> out;
+  for (size_t k = 0; k < s.size();) {
+    const unsigned char c = (unsigned char)s[k];
+    const size_t n = c < 0x80 ? 1 : c < 0xE0 ? 2 : c < 0xF0 ? 3 : 4;
+    uint32_t v = n == 1 ? c : n == 2 ? (c & 0x1Fu) : n == 3 ? (c & 0x0Fu) : (c & 0x07u);
+    for (size_t j = 1; j < n && k + j < s.size(); ++j) v = (v << 6) | ((unsigned char)s[k + j] & 0x3Fu);
+    out.push_back(v);
+    k += n;
+  }
+  return out;
+}
+std::string utf8_of(const std::vector<uint32_t>& v, size_t lo = 0, size_t hi = SIZE_MAX) {
+  std::string o;
+  for (size_t k = lo; k < v.size() && k < hi; ++k) put_utf8(v[k], &o);
+  return o;
+}
+bool uni_ws(uint32_t c) {
+  return (c >= 9 && c <= 13) || c == ' ' || c == 0x85 || c == 0xA0 || c == 0x1680 || (c >= 0x2000 && c <= 0x200A) ||
+         c == 0x2028 || c == 0x2029 || c == 0x202F || c == 0x205F || c == 0x3000;
+}
+bool uni_in(const UniRange* r, uint32_t n, uint32_t c) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t m = (lo + hi) / 2;
+    if (r[m].hi < c) lo = m + 1;
+    else hi = m;
+  }
+  return lo < n && r[lo].lo <= c;
+}
+const UniCaseMap* uni_map(const UniCaseMap* t, uint32_t n, uint32_t c) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t m = (lo + hi) / 2;
+    if (t[m].cp < c) lo = m + 1;
+    else hi = m;
+  }
+  return lo < n && t[lo].cp == c ? &t[lo] : nullptr;
+}
+bool uni_ignorable(uint32_t c) { return uni_in(kUniCaseIgnorable, kUniCaseIgnorableN, c); }
+bool uni_cased(uint32_t c) { return uni_in(kUniCased, kUniCasedN, c); }  // (and not Case_Ignorable)
+// str::to_lowercase / str::to_uppercase
+std::string str_case(const std::string& s, bool upper) {
+  const std::vector<uint32_t> v = cps_of(s);
+  std::vector<uint32_t> o;
+  for (size_t k = 0; k < v.size(); ++k) {
+    const uint32_t c = v[k];
+    if (!upper && c == 0x3A3) {  // Σ: ς at the end of a word (Unicode 3.13 Final_Sigma)
+      size_t j = k;
+      while (j > 0 && uni_ignorable(v[j - 1])) --j;
+      bool fin = j > 0 && uni_cased(v[j - 1]);
+      if (fin) {
+        j = k + 1;
+        while (j < v.size() && uni_ignorable(v[j])) ++j;
+        fin = !(j < v.size() && uni_cased(v[j]));
+      }
+      o.push_back(fin ? 0x3C2 : 0x3C3);
+      continue;
+    }
+    const UniCaseMap* m = upper ? uni_map(kUniUpper, kUniUpperN, c) : uni_map(kUniLower, kUniLowerN, c);
+    if (!m) o.push_back(c);
+    else
+      for (uint32_t j = 0; j < m->n; ++j) o.push_back(m->m[j]);
+  }
+  return utf8_of(o);
+}
+// rhai's calc_offset_len (start counts from the end when negative, clamped; len clamped)
+void offset_len(size_t n, int64_t start, int64_t len, size_t* st, size_t* ln) {
+  size_t s0;
+  if (start < 0) {
+    const uint64_t a = (uint64_t)0 - (uint64_t)start;
+    s0 = a >= n ? 0 : n - (size_t)a;
+  } else if ((uint64_t)start >= n) {
+    *st = n;
+    *ln = 0;
+    return;
+  } else {
+    s0 = (size_t)start;
+  }
+  *st = s0;
+  *ln = len <= 0 ? 0 : (uint64_t)len > n - s0 ? n - s0 : (size_t)len;
+}
+// an element position for get / set / remove: negative from the end; out of range: none
+bool elem_index(size_t n, int64_t i, size_t* at) {
+  if (i < 0) {
+    const uint64_t a = (uint64_t)0 - (uint64_t)i;
+    if (a > n) return false;
+    *at = n - (size_t)a;
+    return true;
+  }
+  if ((uint64_t)i >= n) return false;
+  *at = (size_t)i;
+  return true;
+}
+// the characters [from, from + len) of a string by rhai's sub_string rules
+std::string sub_chars(const std::string& s, int64_t start, int64_t len) {
+  const std::vector<uint32_t> v = cps_of(s);
+  if (v.empty() || len <= 0) return "";
+  size_t off;
+  if (start < 0) {
+    const uint64_t a = (uint64_t)0 - (uint64_t)start;
+    off = a > v.size() ? 0 : v.size() - (size_t)a;
+  } else if ((uint64_t)start >= v.size()) {
+    return "";
+  } else {
+    off = (size_t)start;
+  }
+  const size_t take = (uint64_t)len > v.size() - off ? v.size() - off : (size_t)len;
+  return utf8_of(v, off, off + take);
+}
+// Rust's str::split / rsplit / splitn / rsplitn over a string pattern (an empty pattern matches at
+// every character boundary, both ends included); n = 0: no limit
+std::vector<std::string> str_split(const std::string& s, const std::string& d, bool rev, size_t n) {
+  std::vector<size_t> at;  // match starts (byte offsets), left to right
+  if (d.empty()) {
+    for (size_t k = 0; k <= s.size(); ++k)
+      if (k == s.size() || ((unsigned char)s[k] & 0xC0u) != 0x80u) at.push_back(k);
+  } else if (!rev) {
+    for (size_t k = s.find(d); k != std::string::npos; k = s.find(d, k + d.size())) at.push_back(k);
+  } else {  // right to left, non-overlapping
+    std::vector<size_t> r;
+    for (size_t e = s.size(); e >= d.size();) {
+      const size_t k = s.rfind(d, e - d.size());
+      if (k == std::string::npos) break;
+      r.push_back(k);
+      if (k < d.size()) break;
+      e = k;
+    }
+    at.assign(r.rbegin(), r.rend());
+  }
+  std::vector<std::string> out;
+  if (!rev) {
+    size_t from = 0;
+    for (size_t k : at) {
+      if (n && out.size() + 1 == n) break;
+      out.push_back(s.substr(from, k - from));
+      from = k + d.size();
+    }
+    out.push_back(s.substr(from));
+  } else {
+    size_t to = s.size();
+    for (size_t j = at.size(); j-- > 0;) {
+      if (n && out.size() + 1 == n) break;
+      const size_t k = at[j];
+      out.push_back(s.substr(k + d.size(), to - k - d.size()));
+      to = k;
+    }
+    out.push_back(s.substr(0, to));
+  }
+  return out;
+}
+// i64::from_str_radix(s.trim(), radix) and its ParseIntError texts
+bool parse_i64(const std::string& text, int64_t radix, int64_t* out, std::string* err) {
+  std::vector<uint32_t> v = cps_of(text);
+  size_t a = 0, b = v.size();
+  while (a < b && uni_ws(v[a])) ++a;
+  while (b > a && uni_ws(v[b - 1])) --b;
+  if (a == b) {
+    *err = "cannot parse integer from empty string";
+    return false;
+  }
+  bool neg = false;
+  if (v[a] == '+' || v[a] == '-') {
+    neg = v[a] == '-';
+    ++a;
+    if (a == b) {
+      *err = "invalid digit found in string";
+      return false;
+    }
+  }
+  long long r = 0;
+  for (size_t k = a; k < b; ++k) {
+    const uint32_t c = v[k];
+    int64_t d = c >= '0' && c <= '9' ? c - '0' : c >= 'a' && c <= 'z' ? c - 'a' + 10 : c >= 'A' && c <= 'Z' ? c - 'A' + 10 : 99;
+    if (d >= radix) {
+      *err = "invalid digit found in string";
+      return false;
+    }
+    if (__builtin_mul_overflow(r, (long long)radix, &r) ||
+        (neg ? __builtin_sub_overflow(r, (long long)d, &r) : __builtin_add_overflow(r, (long long)d, &r))) {
+      *err = neg ? "number too small to fit in target type" : "number too large to fit in target type";
+      return false;
+    }
+  }
+  *out = r;
+  return true;
+}
+std::string radix_text(int64_t v, unsigned bits) {  // Rust's {:x} / {:o} / {:b} of an i64 (two's complement)
+  uint64_t u = (uint64_t)v;
+  const char* dig = "0123456789abcdef";
+  std::string o;
+  const unsigned mask = (1u << bits) - 1u;
+  do {
+    o.push_back(dig[u & mask]);
+    u >>= bits;
+  } while (u);
+  std::reverse(o.begin(), o.end());
+  return o;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1068,9 +1365,25 @@ struct Interp {
     return fail(std::string("Indexer unavailable: ") + tname(v.t));
   }
 
+  // A built-in over its arguments a (a[0] by value: the function changes it in place when rhai's
+  // takes `&mut`, and the caller stores it back for a method-style call on a variable). Charges
+  // against kMaxScriptAlloc (slots.hpp charges the same): a new string its bytes, a new or copied
+  // array 16 B a cell; slices (sub_string, trim, split pieces, extract, pop, ...) are free.
   Flow builtin(int fid, const std::string& name, std::vector<Val>& a, Val* out) {
     std::vector<const Val*> ap;
     for (const Val& v : a) ap.push_back(&v);
+    auto refuse = [&](const char* why) {
+      std::string s = std::string(kUnsupported) + name + " (";
+      for (size_t k = 0; k < a.size(); ++k) s += (k ? ", " : "") + std::string(tname(a[k].t));
+      return fail(s + ")" + why);
+    };
+    auto is = [&](size_t k, VT t) { return a.size() > k && a[k].t == t; };
+    auto new_str = [&](std::string s) -> Flow {
+      if (!charge(s.size())) return fail(limit_alloc());
+      *out = vstr(std::move(s));
+      return OK;
+    };
+    *out = Val{};
     switch (fid) {
       case F_LEN:
       case F_IS_EMPTY: {
@@ -1089,33 +1402,59 @@ struct Interp {
         }
         std::string s;
         if (!text(a[0], &s)) return fail(std::string(kUnsupported) + "converting an array to a string");
-        if (!charge(s.size())) return fail(limit_alloc());
-        *out = vstr(s);
-        return OK;
+        return new_str(s);
       }
       case F_PUSH: {
         if (a[0].t != VT::Arr) return nf(name, ap);
         if (!charge(16ull * (a[0].a.size() + 1))) return fail(limit_alloc());
-        *out = a[0];
-        out->a.push_back(a[1]);
+        a[0].a.push_back(a[1]);
         return OK;
       }
-      case F_CONTAINS: {
+      case F_CONTAINS:
+      case F_INDEX_OF:
+      case F_INDEX_OF_FROM: {
         const Val &c = a[0], &x = a[1];
+        if (fid == F_INDEX_OF_FROM && !is(2, VT::Int)) return nf(name, ap);
         if (c.t == VT::Arr) {
-          for (const Val& e : c.a) {
-            const int r = eq(e, x, 0);
+          size_t from = 0, ln;
+          if (fid == F_INDEX_OF_FROM) offset_len(c.a.size(), a[2].i, 0, &from, &ln);
+          for (size_t k = from; k < c.a.size(); ++k) {
+            const int r = eq(c.a[k], x, 0);
             if (r < 0) return fail(limit_depth());
             if (r) {
-              *out = vbool(true);
+              *out = fid == F_CONTAINS ? vbool(true) : vint((int64_t)k);
               return OK;
             }
           }
-          *out = vbool(false);
+          *out = fid == F_CONTAINS ? vbool(false) : vint(-1);
           return OK;
         }
         if (c.t == VT::Str && x.t == VT::Str) {
-          *out = vbool(c.s.find(x.s) != std::string::npos);
+          if (fid == F_CONTAINS) {
+            *out = vbool(c.s.find(x.s) != std::string::npos);
+            return OK;
+          }
+          // index_of: the character position of the first match at or after `start` characters
+          int64_t r = -1;
+          if (!c.s.empty()) {
+            const std::vector<uint32_t> v = cps_of(c.s);
+            size_t from = 0;
+            bool none = false;
+            if (fid == F_INDEX_OF_FROM) {
+              const int64_t st = a[2].i;
+              if (st < 0) {
+                const uint64_t m = (uint64_t)0 - (uint64_t)st;
+                from = m > v.size() ? 0 : utf8_of(v, 0, v.size() - (size_t)m).size();
+              } else if ((uint64_t)st >= v.size()) {
+                none = st != 0;
+              } else {
+                from = utf8_of(v, 0, (size_t)st).size();
+              }
+            }
+            const size_t k = none ? std::string::npos : c.s.find(x.s, from);
+            if (k != std::string::npos) r = (int64_t)chars(c.s.substr(0, k));
+          }
+          *out = vint(r);
           return OK;
         }
         return nf(name, ap);
@@ -1127,6 +1466,318 @@ struct Interp {
         const bool r = n.size() <= h.size() && (fid == F_STARTS_WITH ? h.compare(0, n.size(), n) == 0
                                                                       : h.compare(h.size() - n.size(), n.size(), n) == 0);
         *out = vbool(r);
+        return OK;
+      }
+      // ---- integers (ArithmeticPackage, LogicPackage, BasicMathPackage)
+      case F_ABS:
+      case F_SIGN:
+      case F_IS_ZERO:
+      case F_IS_ODD:
+      case F_IS_EVEN:
+      case F_TO_HEX:
+      case F_TO_OCTAL:
+      case F_TO_BINARY: {
+        if (a[0].t != VT::Int) return nf(name, ap);
+        const int64_t x = a[0].i;
+        switch (fid) {
+          case F_ABS:
+            if (x == INT64_MIN) return fail("Negation overflow: -" + std::to_string(x));
+            *out = vint(x < 0 ? -x : x);
+            return OK;
+          case F_SIGN: *out = vint(x < 0 ? -1 : x > 0 ? 1 : 0); return OK;
+          case F_IS_ZERO: *out = vbool(x == 0); return OK;
+          case F_IS_ODD: *out = vbool((x & 1) != 0); return OK;
+          case F_IS_EVEN: *out = vbool((x & 1) == 0); return OK;
+          default: return new_str(radix_text(x, fid == F_TO_HEX ? 4 : fid == F_TO_OCTAL ? 3 : 1));
+        }
+      }
+      case F_MAX:
+      case F_MIN:
+        if (a[0].t != VT::Int || a[1].t != VT::Int) return nf(name, ap);
+        *out = vint(fid == F_MAX ? std::max(a[0].i, a[1].i) : std::min(a[0].i, a[1].i));
+        return OK;
+      case F_PARSE_INT:
+      case F_PARSE_INT_R: {
+        if (a[0].t != VT::Str || (fid == F_PARSE_INT_R && a[1].t != VT::Int)) return nf(name, ap);
+        const int64_t radix = fid == F_PARSE_INT_R ? a[1].i : 10;
+        if (radix < 2 || radix > 36) return fail("Invalid radix: '" + std::to_string(radix) + "'");
+        int64_t v;
+        std::string e;
+        if (!parse_i64(a[0].s, radix, &v, &e)) return fail("Error parsing integer number '" + a[0].s + "': " + e);
+        *out = vint(v);
+        return OK;
+      }
+      // ---- strings (BasicStringPackage, MoreStringPackage)
+      case F_TO_UPPER:
+      case F_TO_LOWER:
+      case F_MAKE_UPPER:
+      case F_MAKE_LOWER: {
+        if (a[0].t != VT::Str) return nf(name, ap);
+        const std::string r = str_case(a[0].s, fid == F_TO_UPPER || fid == F_MAKE_UPPER);
+        if (!charge(r.size())) return fail(limit_alloc());
+        if (fid == F_TO_UPPER || fid == F_TO_LOWER) *out = vstr(r);
+        else a[0].s = r;
+        return OK;
+      }
+      case F_TRIM: {
+        if (a[0].t != VT::Str) return nf(name, ap);
+        const std::vector<uint32_t> v = cps_of(a[0].s);
+        size_t lo = 0, hi = v.size();
+        while (lo < hi && uni_ws(v[lo])) ++lo;
+        while (hi > lo && uni_ws(v[hi - 1])) --hi;
+        a[0].s = utf8_of(v, lo, hi);
+        return OK;
+      }
+      case F_SUB_STRING:
+      case F_SUB_STRING_N:
+      case F_CROP:
+      case F_CROP_N: {
+        const bool n3 = fid == F_SUB_STRING_N || fid == F_CROP_N;
+        if (a[0].t != VT::Str || a[1].t != VT::Int || (n3 && a[2].t != VT::Int)) return nf(name, ap);
+        const int64_t len = n3 ? a[2].i : (int64_t)a[0].s.size();
+        std::string r = sub_chars(a[0].s, a[1].i, len);
+        if (fid == F_SUB_STRING || fid == F_SUB_STRING_N) *out = vstr(std::move(r));
+        else a[0].s = std::move(r);
+        return OK;
+      }
+      case F_REPLACE: {
+        if (a[0].t != VT::Str || a[1].t != VT::Str || a[2].t != VT::Str) return nf(name, ap);
+        if (a[0].s.empty()) return OK;
+        const std::vector<std::string> parts = str_split(a[0].s, a[1].s, false, 0);
+        std::string r;
+        for (size_t k = 0; k < parts.size(); ++k) r += (k ? a[2].s : "") + parts[k];
+        if (!charge(r.size())) return fail(limit_alloc());
+        a[0].s = std::move(r);
+        return OK;
+      }
+      case F_SPLIT_WS:
+      case F_SPLIT:
+      case F_SPLIT_N:
+      case F_SPLIT_REV:
+      case F_SPLIT_REV_N: {
+        if (fid == F_SPLIT && a[0].t == VT::Arr && a[1].t == VT::Int) {  // array: cut off the tail from index
+          size_t st, ln;
+          offset_len(a[0].a.size(), a[1].i, INT64_MAX, &st, &ln);
+          out->t = VT::Arr;
+          out->a.assign(a[0].a.begin() + (std::ptrdiff_t)st, a[0].a.end());
+          a[0].a.resize(st);
+          return OK;
+        }
+        if (a[0].t != VT::Str) return nf(name, ap);
+        std::vector<std::string> parts;
+        if (fid == F_SPLIT_WS) {
+          const std::vector<uint32_t> v = cps_of(a[0].s);
+          for (size_t k = 0; k < v.size();) {
+            while (k < v.size() && uni_ws(v[k])) ++k;
+            const size_t b = k;
+            while (k < v.size() && !uni_ws(v[k])) ++k;
+            if (k > b) parts.push_back(utf8_of(v, b, k));
+          }
+        } else if (fid == F_SPLIT && a[1].t == VT::Int) {  // at a character position
+          const std::vector<uint32_t> v = cps_of(a[0].s);
+          const int64_t i = a[1].i;
+          size_t at;
+          if (i <= 0) {
+            const uint64_t m = (uint64_t)0 - (uint64_t)i;
+            at = m > v.size() ? 0 : v.size() - (size_t)m;
+          } else {
+            at = (uint64_t)i > v.size() ? v.size() : (size_t)i;
+          }
+          parts = {utf8_of(v, 0, at), utf8_of(v, at)};
+        } else {
+          if (a[1].t != VT::Str) return nf(name, ap);
+          const bool lim = fid == F_SPLIT_N || fid == F_SPLIT_REV_N;
+          if (lim && a[2].t != VT::Int) return nf(name, ap);
+          size_t n = 0;
+          if (lim) n = a[2].i < 1 ? 1 : (size_t)std::min<int64_t>(a[2].i, INT64_MAX);
+          parts = str_split(a[0].s, a[1].s, fid == F_SPLIT_REV || fid == F_SPLIT_REV_N, n);
+        }
+        if (!charge(16ull * parts.size())) return fail(limit_alloc());
+        out->t = VT::Arr;
+        for (std::string& p : parts) out->a.push_back(vstr(std::move(p)));
+        return OK;
+      }
+      case F_BYTES:
+        if (a[0].t != VT::Str) return nf(name, ap);
+        *out = vint((int64_t)a[0].s.size());
+        return OK;
+      // ---- arrays (BasicArrayPackage), and the string forms of append / remove / clear / truncate
+      case F_APPEND:
+        if (a[0].t == VT::Arr && a[1].t == VT::Arr) {
+          if (!charge(16ull * (a[0].a.size() + a[1].a.size()))) return fail(limit_alloc());
+          a[0].a.insert(a[0].a.end(), a[1].a.begin(), a[1].a.end());
+          return OK;
+        }
+        if (a[0].t == VT::Str) {
+          std::string t;
+          if (!text(a[1], &t)) return fail(std::string(kUnsupported) + "converting an array to a string");
+          if (!charge(a[0].s.size() + t.size())) return fail(limit_alloc());
+          a[0].s += t;
+          return OK;
+        }
+        return nf(name, ap);
+      case F_INSERT: {
+        if (a[0].t != VT::Arr || a[1].t != VT::Int) return nf(name, ap);
+        if (!charge(16ull * (a[0].a.size() + 1))) return fail(limit_alloc());
+        size_t st, ln;
+        offset_len(a[0].a.size(), a[1].i, 0, &st, &ln);
+        a[0].a.insert(a[0].a.begin() + (std::ptrdiff_t)st, a[2]);
+        return OK;
+      }
+      case F_POP:
+      case F_SHIFT:
+        if (a[0].t == VT::Str) return refuse(": it returns a character");
+        if (a[0].t != VT::Arr) return nf(name, ap);
+        if (!a[0].a.empty()) {
+          if (fid == F_POP) {
+            *out = std::move(a[0].a.back());
+            a[0].a.pop_back();
+          } else {
+            *out = std::move(a[0].a.front());
+            a[0].a.erase(a[0].a.begin());
+          }
+        }
+        return OK;
+      case F_REMOVE: {
+        if (a[0].t == VT::Str && a[1].t == VT::Str) {  // every occurrence of the substring
+          if (a[1].s.empty() || a[0].s.empty()) return OK;
+          std::string r;
+          for (const std::string& p : str_split(a[0].s, a[1].s, false, 0)) r += p;
+          if (!charge(r.size())) return fail(limit_alloc());
+          a[0].s = std::move(r);
+          return OK;
+        }
+        if (a[0].t != VT::Arr || a[1].t != VT::Int) return nf(name, ap);
+        size_t at;
+        if (!elem_index(a[0].a.size(), a[1].i, &at)) return OK;
+        if (!charge(16ull * (a[0].a.size() - 1))) return fail(limit_alloc());
+        *out = std::move(a[0].a[at]);
+        a[0].a.erase(a[0].a.begin() + (std::ptrdiff_t)at);
+        return OK;
+      }
+      case F_REVERSE:
+        if (a[0].t != VT::Arr) return nf(name, ap);
+        if (!charge(16ull * a[0].a.size())) return fail(limit_alloc());
+        std::reverse(a[0].a.begin(), a[0].a.end());
+        return OK;
+      case F_SORT: {
+        if (a[0].t != VT::Arr) return nf(name, ap);
+        std::vector<Val>& v = a[0].a;
+        if (v.size() <= 1) return OK;
+        for (const Val& e : v)
+          if (e.t != v[0].t) return fail("Function not found: sort() cannot be called with elements of different types");
+        if (v[0].t == VT::Arr || v[0].t == VT::Unit) return OK;
+        if (!charge(16ull * v.size())) return fail(limit_alloc());
+        std::stable_sort(v.begin(), v.end(), [](const Val& x, const Val& y) {
+          if (x.t == VT::Int) return x.i < y.i;
+          if (x.t == VT::Bool) return !x.b && y.b;
+          return x.s < y.s;  // (byte order: Rust's str ordering)
+        });
+        return OK;
+      }
+      case F_CLEAR:
+        if (a[0].t == VT::Arr) a[0].a.clear();
+        else if (a[0].t == VT::Str) a[0].s.clear();
+        else return nf(name, ap);
+        return OK;
+      case F_TRUNCATE:
+      case F_CHOP: {
+        if (a[1].t != VT::Int) return nf(name, ap);
+        const int64_t n = a[1].i;
+        if (a[0].t == VT::Str && fid == F_TRUNCATE) {
+          const std::vector<uint32_t> v = cps_of(a[0].s);
+          if (n <= 0) a[0].s.clear();
+          else if ((uint64_t)n < v.size()) a[0].s = utf8_of(v, 0, (size_t)n);
+          return OK;
+        }
+        if (a[0].t != VT::Arr) return nf(name, ap);
+        std::vector<Val>& v = a[0].a;
+        if (n <= 0) v.clear();
+        else if ((uint64_t)n < v.size()) {
+          if (fid == F_TRUNCATE) v.resize((size_t)n);
+          else v.erase(v.begin(), v.end() - (std::ptrdiff_t)n);
+        }
+        return OK;
+      }
+      case F_GET:
+      case F_SET: {
+        if (a[0].t == VT::Str && a[1].t == VT::Int) return refuse(": characters");
+        if (a[0].t != VT::Arr || a[1].t != VT::Int) return nf(name, ap);
+        size_t at;
+        if (!elem_index(a[0].a.size(), a[1].i, &at)) return OK;
+        if (fid == F_GET) {
+          *out = a[0].a[at];
+          return OK;
+        }
+        if (!charge(16ull * a[0].a.size())) return fail(limit_alloc());
+        a[0].a[at] = a[2];
+        return OK;
+      }
+      case F_EXTRACT:
+      case F_EXTRACT_N:
+      case F_DRAIN:
+      case F_RETAIN: {
+        const bool n3 = fid != F_EXTRACT;
+        if (a[0].t != VT::Arr || a[1].t != VT::Int || (n3 && a[2].t != VT::Int)) return nf(name, ap);
+        std::vector<Val>& v = a[0].a;
+        out->t = VT::Arr;
+        const int64_t len = n3 ? a[2].i : INT64_MAX;
+        if (v.empty() || len <= 0) return OK;
+        size_t st, ln;
+        offset_len(v.size(), a[1].i, len, &st, &ln);
+        if (ln == 0) return OK;
+        const auto b = v.begin() + (std::ptrdiff_t)st, e = b + (std::ptrdiff_t)ln;
+        if (fid == F_EXTRACT || fid == F_EXTRACT_N) {
+          out->a.assign(b, e);
+        } else if (fid == F_DRAIN) {  // the range out; the rest is a copy
+          if (!charge(16ull * (v.size() - ln))) return fail(limit_alloc());
+          out->a.assign(b, e);
+          v.erase(b, e);
+        } else {  // retain the range; what is cut off is a copy
+          if (!charge(16ull * (v.size() - ln))) return fail(limit_alloc());
+          out->a.assign(v.begin(), b);
+          out->a.insert(out->a.end(), e, v.end());
+          std::vector<Val> keep(b, e);
+          v = std::move(keep);
+        }
+        return OK;
+      }
+      case F_SPLICE: {
+        if (a[0].t != VT::Arr || a[1].t != VT::Int || a[2].t != VT::Int || a[3].t != VT::Arr) return nf(name, ap);
+        std::vector<Val>& v = a[0].a;
+        size_t st = 0, ln = 0;
+        if (!v.empty()) offset_len(v.size(), a[1].i, a[2].i, &st, &ln);
+        if (!charge(16ull * (v.size() - ln + a[3].a.size()))) return fail(limit_alloc());
+        if (v.empty()) {
+          v = a[3].a;
+        } else {
+          v.erase(v.begin() + (std::ptrdiff_t)st, v.begin() + (std::ptrdiff_t)(st + ln));
+          v.insert(v.begin() + (std::ptrdiff_t)st, a[3].a.begin(), a[3].a.end());
+        }
+        return OK;
+      }
+      case F_DEDUP: {
+        if (a[0].t != VT::Arr) return nf(name, ap);
+        std::vector<Val>& v = a[0].a;
+        if (v.size() <= 1) return OK;
+        std::vector<Val> r;
+        r.push_back(v[0]);
+        for (size_t k = 1; k < v.size(); ++k) {
+          const int e = eq(v[k], r.back(), 0);
+          if (e < 0) return fail(limit_depth());
+          if (!e) r.push_back(v[k]);
+        }
+        if (!charge(16ull * r.size())) return fail(limit_alloc());
+        v = std::move(r);
+        return OK;
+      }
+      case F_PAD: {
+        if (a[0].t == VT::Str && a[1].t == VT::Int) return refuse(": padding strings");
+        if (a[0].t != VT::Arr || a[1].t != VT::Int) return nf(name, ap);
+        const int64_t n = a[1].i;
+        if (n <= 0 || (uint64_t)n <= a[0].a.size()) return OK;
+        if ((uint64_t)n > kMaxScriptAlloc || !charge(16ull * (uint64_t)n)) return fail(limit_alloc());
+        a[0].a.resize((size_t)n, a[2]);
         return OK;
       }
     }
@@ -1167,13 +1818,12 @@ struct Interp {
     }
     if (n->builtin >= 0) {
       if (Flow f = builtin(n->builtin, n->name, a, out)) return f;
-      if (n->builtin == F_PUSH && n->flag) {  // method style on a variable: push into it
-        if (n->kids[0]->k == Node::Var) {
-          Val* v = lookup(n->kids[0]->name);
-          if (!v) return fail("Variable not found: " + n->kids[0]->name);
-          *v = std::move(*out);
-        }
-        *out = Val{};
+      // a method-style call on a variable changes it (rhai's `&mut` first parameter; a constant
+      // never reaches here for a function that always changes it, the parser refuses that)
+      if (n->flag && builtin_mut(n->builtin) && n->kids[0]->k == Node::Var) {
+        Val* v = lookup(n->kids[0]->name);
+        if (!v) return fail("Variable not found: " + n->kids[0]->name);
+        *v = std::move(a[0]);
       }
       return OK;
     }
@@ -1232,6 +1882,17 @@ struct Interp {
     }
     if (op == "+" && (a.t == VT::Str || b.t == VT::Str))
       return fail(std::string(kUnsupported) + "converting an array to a string");
+    if (op == "-" && a.t == VT::Str && b.t == VT::Str) {  // every occurrence of b removed
+      if (a.s.empty() || b.s.empty()) {
+        *out = a;
+        return OK;
+      }
+      std::string r;
+      for (const std::string& p : str_split(a.s, b.s, false, 0)) r += p;
+      if (!charge(r.size())) return fail(limit_alloc());
+      *out = vstr(std::move(r));
+      return OK;
+    }
     if (a.t != VT::Int || b.t != VT::Int) return nf(shown, {&a, &b});
     const std::string ex = std::to_string(a.i) + " " + op + " " + std::to_string(b.i);
     long long r = 0;
@@ -1777,7 +2438,7 @@ struct ScriptEmitter {
     u8(S_BIN);
     u8(b);
     pop();
-    if (b == SB_ADD || b == SB_ADDA) allocates = true;
+    if (b == SB_ADD || b == SB_ADDA || b == SB_SUB) allocates = true;
   }
   static uint8_t bin_code(const std::string& op, bool assign) {
     static const char* ops[] = {"|", "^", "&", "==", "!=", "<", "<=", ">", ">=", "+", "-", "*", "/", "%"};
@@ -1785,6 +2446,16 @@ struct ScriptEmitter {
     for (uint8_t k = 0; k < 14; ++k)
       if (op == ops[k]) return k;
     return 0;
+  }
+  bool uses_chars = false;  // a function that reads character properties (the char table)
+  void note_fn(int fid) {
+    if (fid == F_TYPE_OF) uses_type_of = true;
+    if (fid == F_TO_UPPER || fid == F_TO_LOWER || fid == F_MAKE_UPPER || fid == F_MAKE_LOWER || fid == F_TRIM ||
+        fid == F_SPLIT_WS || fid == F_PARSE_INT || fid == F_PARSE_INT_R)
+      uses_chars = true;
+    static const int pure[] = {F_LEN, F_IS_EMPTY, F_CONTAINS, F_TYPE_OF, F_STARTS_WITH, F_ENDS_WITH, F_ABS, F_SIGN,
+                               F_IS_ZERO, F_IS_ODD, F_IS_EVEN, F_MAX, F_MIN, F_PARSE_INT, F_PARSE_INT_R, F_BYTES};
+    if (std::find(std::begin(pure), std::end(pure), fid) == std::end(pure)) allocates = true;
   }
   void fail_op() {  // a value the run never gets past
     u8(S_FAIL);
@@ -1829,25 +2500,24 @@ struct ScriptEmitter {
           return;
         }
         if (n->builtin >= 0) {
+          const int fid = n->builtin;
+          const bool mut = builtin_mut(fid);
           u8(S_FN);
-          u8((uint8_t)n->builtin);
+          u8((uint8_t)fid);
+          u8((uint8_t)(na | (mut ? 0x80 : 0)));
           pop(na);
-          push();
-          if (n->builtin == F_TO_STRING || n->builtin == F_PUSH) allocates = true;
-          if (n->builtin == F_TYPE_OF) uses_type_of = true;
-          if (n->builtin == F_PUSH && n->flag) {  // method style: into the variable, the value is ()
+          push(mut ? 2 : 1);
+          note_fn(fid);
+          if (mut) {  // [receiver as changed, result]: into the variable for a method call on one
             uint32_t s;
-            if (n->kids[0]->k == Node::Var) {
-              if (lookup(n->kids[0]->name, &s)) store(s);
-              else {
-                u8(S_FAIL);
-                pop();
-              }
+            if (n->flag && n->kids[0]->k == Node::Var && lookup(n->kids[0]->name, &s)) {
+              u8(S_XSTORE);
+              u16(s);
             } else {
-              u8(S_POP);
-              pop();
+              u8(S_DROPKEEP);
+              u16(1);
             }
-            lit(Val{});
+            pop();
           }
           return;
         }
@@ -1896,6 +2566,7 @@ struct ScriptEmitter {
           emit(h);
           u8(S_FN);
           u8(F_IN);
+          u8(2);
           pop();
         }
         if (n->flag) u8(S_NOT);
@@ -2241,6 +2912,53 @@ bool emit_script(const ExprAst& ast, std::vector<uint8_t>* out, uint32_t* depth,
     *err = "policy group expression exceeds the engine's limits";
     return false;
   }
+  // the char table: every non-ASCII code point a run can hold (the literals', closed under the case
+  // mappings; ς for Σ's final form), with its White_Space / Cased / Case_Ignorable bits and mappings
+  uint32_t ctab = 0, nchar = 0;
+  if (e.uses_chars) {
+    std::set<uint32_t> cs;
+    std::function<void(const Node*)> walk = [&](const Node* n) {
+      auto add = [&](const Val& v) {
+        if (v.t == VT::Str)
+          for (uint32_t c : cps_of(v.s))
+            if (c >= 0x80) cs.insert(c);
+      };
+      add(n->lit);
+      for (const P& k : n->kids) walk(k.get());
+      for (const SwitchCase& c : n->cases) {
+        for (const Val& v : c.vals) add(v);
+        if (c.guard) walk(c.guard.get());
+        walk(c.body.get());
+      }
+    };
+    walk(ast.root.get());
+    for (const FnDef& f : ast.fns) walk(f.body.get());
+    std::vector<uint32_t> work(cs.begin(), cs.end());
+    if (cs.count(0x3A3)) work.push_back(0x3C2);
+    while (!work.empty()) {
+      const uint32_t c = work.back();
+      work.pop_back();
+      cs.insert(c);
+      for (const UniCaseMap* m : {uni_map(kUniLower, kUniLowerN, c), uni_map(kUniUpper, kUniUpperN, c)})
+        if (m)
+          for (uint32_t j = 0; j < m->n; ++j)
+            if (m->m[j] >= 0x80 && !cs.count(m->m[j])) work.push_back(m->m[j]);
+    }
+    while (e.pool.size() % 4) e.pool.push_back(0);
+    ctab = (uint32_t)e.pool.size();
+    for (uint32_t c : cs) {
+      const UniCaseMap* lo = uni_map(kUniLower, kUniLowerN, c);
+      const UniCaseMap* up = uni_map(kUniUpper, kUniUpperN, c);
+      const uint32_t nlo = lo ? lo->n : 1u, nup = up ? up->n : 1u;
+      uint32_t w[8] = {c,
+                       (uni_ws(c) ? kChWs : 0u) | (uni_cased(c) ? kChCased : 0u) | (uni_ignorable(c) ? kChIgnorable : 0u) |
+                           (nlo << 8) | (nup << 10),
+                       lo ? lo->m[0] : c, lo ? lo->m[1] : 0u, lo ? lo->m[2] : 0u,
+                       up ? up->m[0] : c, up ? up->m[1] : 0u, up ? up->m[2] : 0u};
+      e.pool.insert(e.pool.end(), (const uint8_t*)w, (const uint8_t*)w + kChEntry);
+      ++nchar;
+    }
+  }
   uint32_t tnames = 0;
   if (e.uses_type_of) {
     tnames = (uint32_t)e.pool.size();
@@ -2252,7 +2970,8 @@ bool emit_script(const ExprAst& ast, std::vector<uint8_t>* out, uint32_t* depth,
   for (size_t pc = 0; pc < e.code.size();) {
     const uint8_t op = e.code[pc++];
     switch (op) {
-      case S_BOOL: case S_BIN: case S_FN: case S_INRANGE: pc += 1; break;
+      case S_BOOL: case S_BIN: case S_INRANGE: pc += 1; break;
+      case S_FN: case S_XSTORE: pc += 2; break;
       case S_INT: pc += 8; break;
       case S_STR: {
         uint32_t off = 0;
@@ -2277,8 +2996,8 @@ bool emit_script(const ExprAst& ast, std::vector<uint8_t>* out, uint32_t* depth,
                          code_len,
                          has_fns ? kMaxCallDepth : 0u,
                          tnames + kScriptHeader + code_len,
-                         0,
-                         0};
+                         nchar ? ctab + kScriptHeader + code_len : 0u,
+                         nchar};
   out->insert(out->end(), (const uint8_t*)h, (const uint8_t*)h + kScriptHeader);
   out->insert(out->end(), e.code.begin(), e.code.end());
   out->insert(out->end(), e.pool.begin(), e.pool.end());
@@ -2337,6 +3056,12 @@ GroupProgram compile_group_expression(const std::string& expr, const std::vector
     for (const FnDef& f : ast->fns) stray = stray || stray_range_call(f.body.get());
     if (stray) {
       g.error = std::string(kUnsupported) + "range values outside `for` and `in`";
+      return g;
+    }
+    const Node* r = refused_call(ast->root.get());
+    for (const FnDef& f : ast->fns) r = r ? r : refused_call(f.body.get());
+    if (r) {
+      g.error = std::string(kUnsupported) + r->name;
       return g;
     }
   }

@@ -784,7 +784,10 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
       const uint32_t n0 = nr;
       const uint32_t ek = rup64(n3), e0 = ek + rup64(nk), e1 = e0 + rup64(n2), e2 = e1 + rup64(n1), e3 = e2 + rup64(n0);
       // helper lanes for second label-value DFAs (below): LDS tables, chains of at most two DFAs, and
-      // one chunk (its class array, unused then, holds the 4 waves' 128-B mailboxes)
+      // one chunk (its class array, unused then, holds the 4 waves' 128-B mailboxes: lmax * nlv * 2
+      // bytes with nlv == 2, so lmax >= 128 holds them only while a workgroup is 4 waves)
+      static_assert(kSlotThreads == 256u && (kSlotThreads / 64u) * 128u == 128u * 2u * 2u,
+                    "the label-pair mailboxes assume 4 waves and a class array of >= 128 labels x 2 x u16");
       const bool label_pairs = LDST && C.kv && t.kv_lds && nlv == 2u && t.nchunk == 1u && t.lmax >= 128u && classify &&
                                t.o_sb[S_LV] && !(t.debug & 2048u);
       const uint64_t p1_t0 = timing ? clock64() : 0;
@@ -1637,7 +1640,11 @@ __global__ void __launch_bounds__(kWideThreads) wide_groups_kernel(WideGroupPass
     };
     auto cause = [&](uint32_t s) { cz[s >> 6] |= 1ull << (s & 63u); };
     // a group of at most 15 members carries its causes in ARG, as column_word's forms do
-    auto rej = [&]() { return g.nmem <= 15 ? (g.rejb & 0xffffu) | ((uint32_t)cz[0] << 16) : g.rejb; };
+    // (a group without members has no cause words: cz then points past its own range)
+    auto rej = [&]() {
+      const uint32_t c0 = g.cause_words ? (uint32_t)cz[0] : 0u;
+      return g.nmem <= 15 ? (g.rejb & 0xffffu) | (c0 << 16) : g.rejb;
+    };
     if (g.kind == 1) {  // script bytecode: true, false or an evaluation error
       const int v = run_script_prog(w.progs + g.prog_off, stack, ok, cause);
       *dst = v == 1 ? g.okw : v == 0 ? rej() : g.errw;

@@ -108,7 +108,9 @@ struct TileArgs {
   uint32_t cmax, kmax, lmax;      // container / capability / label capacity of a staged tile
   uint32_t o_rf, o_coff, o_loff, o_cflags, o_cadd, o_cdrop;  // staged headers (LDS byte offsets)
   // per-entity classes (u16): namespace [rows], AppArmor [cmax], image [cmax][il.n()], added /
-  // dropped capabilities [kmax], label keys [lmax], label values [lmax][nlv]
+  // dropped capabilities [kmax], label keys [lmax], label values [lmax][nlv]. In a single-chunk
+  // pass whose value classes fold into the walk, o_lv's region doubles as the label-pair helper
+  // lanes' per-wave 128-B mailboxes (kernels.hip label_pairs: needs lmax * nlv * 2 >= 4 x 128)
   uint32_t o_ns, o_aa, o_img, o_capadd, o_capdrop, o_lk, o_lv;
   ImgLayout il;
   uint32_t nlv;

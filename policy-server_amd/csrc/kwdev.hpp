@@ -14,7 +14,7 @@
 namespace kw {
 
 constexpr uint32_t kBlobMagic = 0x4b574733;  // "KWG3"
-constexpr uint32_t kBlobVersion = 7;
+constexpr uint32_t kBlobVersion = 8;  // 8: S_FN u8 fid u8 nargs|mut, the script char table (r06)
 
 // request columns that carry strings classified by a DFA or a literal table
 enum Col : uint32_t {
@@ -60,8 +60,12 @@ enum GOp : uint8_t { G_CONST0 = 0, G_CONST1 = 1, G_CALL = 2, G_NOT = 3, G_JT = 4
 // Script bytecode (groups beyond the bool-only subset that no truth table covers; expr.cpp emits
 // it, slots.hpp run_script_prog runs it). Header (32 B): u32 depth (value stack bound), nvars
 // (variable slots of every frame a run can hold), arena (bytes of strings and arrays a run may
-// build), code_len, nframes (script-function frames: 0 or kMaxCallDepth), 3 reserved; then the
-// code, then the string pool. Values are 16 B: word 0 = type (0 unit, 1 bool, 2 i64, 3 string,
+// build), code_len, nframes (script-function frames: 0 or kMaxCallDepth), type_of names offset,
+// char table offset and entry count; then the code, then the string pool, then the char table.
+// The char table (r06) holds, for every non-ASCII code point a run can ever hold (those of the
+// script's string literals, closed under the case mappings), 32-B entries sorted by code point:
+// u32 cp, u32 flags (bit 0 White_Space, bit 1 Cased and not Case_Ignorable, bit 2 Case_Ignorable,
+// bits 8-9 / 10-11 the lengths of the lower / upper mappings), u32 lower[3], u32 upper[3]. Values are 16 B: word 0 = type (0 unit, 1 bool, 2 i64, 3 string,
 // 4 array) | 256 when the bytes are in the arena | length << 32 (string bytes, array elements);
 // word 1 = the bool / i64 value, or the byte offset of the string (program-relative, or
 // arena-relative with 256) or of the array's 16-B cells (arena-relative). Values are immutable:
@@ -82,7 +86,12 @@ enum GOp : uint8_t { G_CONST0 = 0, G_CONST1 = 1, G_CALL = 2, G_NOT = 3, G_JT = 4
 //   S_INDEX                                   pop index, pop array: push the element (rhai's
 //                                             negative indices count from the end)
 //   S_SETIDX u16 slot                         pop value, pop index: slot's array with that element set
-//   S_FN u8 fid                               built-in function (SFn) over its arguments
+//   S_FN u8 fid u8 nargs | mut << 7           built-in function (SFn) over its nargs arguments: pushes
+//                                             its result, or for a function rhai gives a `&mut`
+//                                             first parameter (mut) the receiver as changed and
+//                                             then the result (S_XSTORE / S_DROPKEEP 1 follow)
+//   S_XSTORE u16 slot                         store the value under the top into a variable slot
+//                                             and drop it, keeping the top
 //   S_COAL u32                                ??: top not (): jump keeping it, else pop
 //   S_INRANGE u8 incl                         pop hi, lo, x: x in lo..hi (all i64, else an error)
 //   S_RCASE i64 lo i64 hi u8 incl             pop x: push x is an i64 in the range (switch cases)
@@ -98,13 +107,31 @@ enum GOp : uint8_t { G_CONST0 = 0, G_CONST1 = 1, G_CALL = 2, G_NOT = 3, G_JT = 4
 //   S_DROP u16 n / S_DROPKEEP u16 n           drop n values / n values under the top (break, continue)
 enum SOp : uint8_t { S_UNIT = 0, S_BOOL, S_INT, S_STR, S_LOAD, S_STORE, S_CALL, S_FAIL, S_NOT, S_NEG, S_POS, S_BIN,
                      S_AND, S_OR, S_CHKB, S_IF, S_JMP, S_POP, S_END, S_ARR, S_INDEX, S_SETIDX, S_FN, S_COAL,
-                     S_INRANGE, S_RCASE, S_TICK, S_FORR, S_FORA, S_RANGECHK, S_CALLF, S_RET, S_DROP, S_DROPKEEP };
+                     S_INRANGE, S_RCASE, S_TICK, S_FORR, S_FORA, S_RANGECHK, S_CALLF, S_RET, S_DROP, S_DROPKEEP,
+                     S_XSTORE };
 // | ^ & == != < <= > >= + - * / %, then the compound assignments that differ from their operator:
 // `+=` (an array pushes / appends; otherwise `+`) and the `x op= y` forms whose errors name `op=`
 enum SBin : uint8_t { SB_OR = 0, SB_XOR, SB_AND, SB_EQ, SB_NE, SB_LT, SB_LE, SB_GT, SB_GE, SB_ADD, SB_SUB, SB_MUL, SB_DIV,
                       SB_MOD, SB_ADDA };
-// Built-in functions (method or function-call style; `x in y` is contains(y, x))
-enum SFn : uint8_t { F_LEN = 0, F_IS_EMPTY, F_CONTAINS, F_TO_STRING, F_TYPE_OF, F_STARTS_WITH, F_ENDS_WITH, F_PUSH, F_IN };
+// Built-in functions (method or function-call style; `x in y` is contains(y, x)). r06: rhai's
+// standard packages over the engine's values (i64, string, array), one id per
+// (name, arity); the argument types are dispatched at run time as rhai's overloads are.
+enum SFn : uint8_t {
+  F_LEN = 0, F_IS_EMPTY, F_CONTAINS, F_TO_STRING, F_TYPE_OF, F_STARTS_WITH, F_ENDS_WITH, F_PUSH, F_IN,
+  // integers
+  F_ABS, F_SIGN, F_IS_ZERO, F_IS_ODD, F_IS_EVEN, F_MAX, F_MIN, F_TO_HEX, F_TO_OCTAL, F_TO_BINARY, F_PARSE_INT,
+  F_PARSE_INT_R,
+  // strings
+  F_TO_UPPER, F_TO_LOWER, F_MAKE_UPPER, F_MAKE_LOWER, F_TRIM, F_SUB_STRING, F_SUB_STRING_N, F_CROP, F_CROP_N,
+  F_INDEX_OF, F_INDEX_OF_FROM, F_REPLACE, F_SPLIT_WS, F_SPLIT, F_SPLIT_N, F_SPLIT_REV, F_SPLIT_REV_N, F_BYTES,
+  // arrays (and the string forms of append / remove / clear / truncate)
+  F_APPEND, F_INSERT, F_POP, F_SHIFT, F_REMOVE, F_REVERSE, F_SORT, F_CLEAR, F_TRUNCATE, F_CHOP, F_GET, F_SET,
+  F_EXTRACT, F_EXTRACT_N, F_DRAIN, F_RETAIN, F_SPLICE, F_DEDUP, F_PAD,
+  F_COUNT
+};
+// char table flags (script programs, above)
+constexpr uint32_t kChWs = 1u, kChCased = 2u, kChIgnorable = 4u;
+constexpr uint32_t kChEntry = 32;
 // Engine limits of one run of a group expression (host interpreter, device bytecode and the oracle
 // apply them identically; each is named in the run's error message)
 constexpr uint32_t kMaxScriptAlloc = 16384;   // bytes of strings and array cells a run may build
@@ -120,9 +147,6 @@ constexpr int kMaxLocalBits = 64;     // per chunk: distinct mandatory label key
 #define KW_HD __host__ __device__
 #else
 #define KW_HD
-#endif
-#ifndef KW_MIX_LSHL  // device literal hash: h * 5 as v_lshl_add_u32 (lit_mix); r03 A/B: C3 -0.5 %,
-#define KW_MIX_LSHL 0   // C4 +0.9 / +1.4 % (the asm's hazard padding and VGPR constraint): off
 #endif
 
 // Compact DFA of the per-key label-value region (offsets region-relative). A label value is only
@@ -192,15 +216,7 @@ inline KW_HD uint32_t lit_init(uint32_t seed, uint32_t len) { return seed ^ (len
 inline KW_HD uint32_t lit_mix(uint32_t h, uint32_t w) {
   h ^= w;
   h = (h << 13) | (h >> 19);
-#if defined(__HIP_DEVICE_COMPILE__) && KW_MIX_LSHL
-  // h * 5 as one full-rate shift-add: left to itself the compiler folds the multiply and the add
-  // into v_mad_u64_u32, a quarter-rate op on the literal probe's dependent chain
-  uint32_t r;
-  asm("v_lshl_add_u32 %0, %1, 2, %1" : "=v"(r) : "v"(h));
-  return r + 0xE6546B64u;
-#else
-  return h * 5u + 0xE6546B64u;
-#endif
+  return h * 5u + 0xE6546B64u;  // (an inline-asm v_lshl_add_u32 form lost at C4 in r03: DESIGN.md §10)
 }
 inline KW_HD uint32_t lit_final(uint32_t h) {
   h ^= h >> 16;

@@ -591,6 +591,186 @@ KW_HD inline int run_script_prog(const uint8_t* prog, uint64_t* scratch, Ok ok, 
     }
     return true;
   };
+  // ---- helpers of the standard-package functions (r06; expr.cpp's interpreter states each rule)
+  const uint32_t ctab = h[6], nch = h[7];  // the char table (kwdev.hpp): non-ASCII code points
+  auto rd32p = [&](uint32_t off) {         // a u32 of the program (little-endian, any alignment)
+    return (uint32_t)prog[off] | ((uint32_t)prog[off + 1] << 8) | ((uint32_t)prog[off + 2] << 16) |
+           ((uint32_t)prog[off + 3] << 24);
+  };
+  auto ch_entry = [&](uint32_t c) -> int64_t {  // program offset of c's entry, or -1
+    uint32_t lo = 0, hi = nch;
+    while (lo < hi) {
+      const uint32_t m = (lo + hi) / 2;
+      if (rd32p(ctab + m * kChEntry) < c) lo = m + 1;
+      else hi = m;
+    }
+    return lo < nch && rd32p(ctab + lo * kChEntry) == c ? (int64_t)(ctab + lo * kChEntry) : -1;
+  };
+  auto ch_flags = [&](uint32_t c) -> uint32_t {
+    if (c < 0x80u) {
+      const bool letter = (c | 0x20u) >= 'a' && (c | 0x20u) <= 'z';
+      return ((c >= 9u && c <= 13u) || c == ' ' ? kChWs : 0u) | (letter ? kChCased : 0u) |
+             (c == '\'' || c == '.' || c == ':' || c == '^' || c == '`' ? kChIgnorable : 0u);
+    }
+    const int64_t e = ch_entry(c);
+    return e < 0 ? 0u : rd32p((uint32_t)e + 4u);
+  };
+  auto ch_map = [&](uint32_t c, bool up, uint32_t* m) -> uint32_t {  // full case mapping of c
+    if (c < 0x80u) {
+      m[0] = up && c >= 'a' && c <= 'z' ? c - 32u : !up && c >= 'A' && c <= 'Z' ? c + 32u : c;
+      return 1;
+    }
+    const int64_t e = ch_entry(c);
+    if (e < 0) {
+      m[0] = c;
+      return 1;
+    }
+    const uint32_t n = (rd32p((uint32_t)e + 4u) >> (up ? 10 : 8)) & 3u;
+    for (uint32_t j = 0; j < n; ++j) m[j] = rd32p((uint32_t)e + (up ? 20u : 8u) + 4u * j);
+    return n;
+  };
+  auto utf8_next = [](const uint8_t* p, uint32_t n, uint32_t k, uint32_t* c) -> uint32_t {
+    const uint32_t b = p[k];
+    const uint32_t len = b < 0x80u ? 1u : b < 0xE0u ? 2u : b < 0xF0u ? 3u : 4u;
+    uint32_t v = len == 1 ? b : len == 2 ? (b & 0x1Fu) : len == 3 ? (b & 0x0Fu) : (b & 0x07u);
+    for (uint32_t j = 1; j < len && k + j < n; ++j) v = (v << 6) | (p[k + j] & 0x3Fu);
+    *c = v;
+    return k + len;
+  };
+  auto put_utf8_at = [](uint32_t c, uint8_t* d) -> uint32_t {  // bytes of c (written when d)
+    const uint32_t n = c < 0x80u ? 1u : c < 0x800u ? 2u : c < 0x10000u ? 3u : 4u;
+    if (d) {
+      if (n == 1) d[0] = (uint8_t)c;
+      else {
+        d[0] = (uint8_t)((n == 2 ? 0xC0u : n == 3 ? 0xE0u : 0xF0u) | (c >> (6 * (n - 1))));
+        for (uint32_t j = 1; j < n; ++j) d[j] = (uint8_t)(0x80u | ((c >> (6 * (n - 1 - j))) & 0x3Fu));
+      }
+    }
+    return n;
+  };
+  auto nchars = [](const uint8_t* p, uint32_t n) -> uint32_t {
+    uint32_t c = 0;
+    for (uint32_t k = 0; k < n; ++k) c += (p[k] & 0xC0u) != 0x80u;
+    return c;
+  };
+  auto char_byte = [](const uint8_t* p, uint32_t n, uint32_t ch) -> uint32_t {  // byte offset of char ch
+    uint32_t c = 0;
+    for (uint32_t k = 0; k < n; ++k)
+      if ((p[k] & 0xC0u) != 0x80u && c++ == ch) return k;
+    return n;
+  };
+  // Σ at bytes [k, k1): preceded by a cased letter and not followed by one (Case_Ignorable skipped)
+  auto final_sigma = [&](const uint8_t* p, uint32_t n, uint32_t k, uint32_t k1) -> bool {
+    bool fin = false;
+    for (uint32_t j = k; j > 0;) {
+      uint32_t b = j - 1;
+      while (b > 0 && (p[b] & 0xC0u) == 0x80u) --b;
+      uint32_t c;
+      utf8_next(p, n, b, &c);
+      const uint32_t f = ch_flags(c);
+      if (!(f & kChIgnorable)) {
+        fin = (f & kChCased) != 0;
+        break;
+      }
+      j = b;
+    }
+    if (!fin) return false;
+    for (uint32_t j = k1; j < n;) {
+      uint32_t c;
+      const uint32_t j1 = utf8_next(p, n, j, &c);
+      const uint32_t f = ch_flags(c);
+      if (!(f & kChIgnorable)) return (f & kChCased) == 0;
+      j = j1;
+    }
+    return true;
+  };
+  auto trim_ws = [&](const uint8_t* p, uint32_t* b, uint32_t* e) {  // White_Space off both ends
+    while (*b < *e) {
+      uint32_t c;
+      const uint32_t k1 = utf8_next(p, *e, *b, &c);
+      if (!(ch_flags(c) & kChWs)) break;
+      *b = k1;
+    }
+    while (*e > *b) {
+      uint32_t s = *e - 1;
+      while (s > *b && (p[s] & 0xC0u) == 0x80u) --s;
+      uint32_t c;
+      utf8_next(p, *e, s, &c);
+      if (!(ch_flags(c) & kChWs)) break;
+      *e = s;
+    }
+  };
+  // the first match of f at or after byte `from` (an empty f matches at every character boundary)
+  auto next_match = [](const uint8_t* p, uint32_t n, const uint8_t* f, uint32_t fn, uint32_t from) -> int64_t {
+    for (uint32_t k = from; k + fn <= n; ++k) {
+      if (fn == 0) {
+        if (k == n || (p[k] & 0xC0u) != 0x80u) return k;
+        continue;
+      }
+      bool m = true;
+      for (uint32_t j = 0; m && j < fn; ++j) m = p[k + j] == f[j];
+      if (m) return k;
+    }
+    return -1;
+  };
+  // the last match of f ending at or before byte `end`
+  auto prev_match = [](const uint8_t* p, uint32_t n, const uint8_t* f, uint32_t fn, uint32_t end) -> int64_t {
+    if (end < fn) return -1;
+    for (uint32_t k = end - fn + 1; k-- > 0;) {
+      if (fn == 0) {
+        if (k == n || (p[k] & 0xC0u) != 0x80u) return k;
+        continue;
+      }
+      bool m = true;
+      for (uint32_t j = 0; m && j < fn; ++j) m = p[k + j] == f[j];
+      if (m) return k;
+    }
+    return -1;
+  };
+  auto find_bytes = [&](const uint8_t* p, uint32_t n, const uint8_t* f, uint32_t fn, uint32_t from) -> int64_t {
+    return fn == 0 ? (from <= n ? (int64_t)from : -1) : next_match(p, n, f, fn, from);
+  };
+  auto str_slice = [](uint64_t w0, uint32_t b, uint32_t e) -> uint64_t {  // word 0 of bytes [b, e)
+    return (w0 & 0xffffffffull) | ((uint64_t)(e - b) << 32);
+  };
+  auto arr_word = [](uint32_t n) -> uint64_t { return sv::ARR | sv::ARENA | ((uint64_t)n << 32); };
+  // rhai's calc_offset_len and the element position of get / set / remove
+  auto offset_len = [](uint32_t n, int64_t start, int64_t len, uint32_t* s0, uint32_t* ln) {
+    uint32_t s;
+    if (start < 0) {
+      const uint64_t a = (uint64_t)0 - (uint64_t)start;
+      s = a >= n ? 0u : n - (uint32_t)a;
+    } else if ((uint64_t)start >= n) {
+      *s0 = n;
+      *ln = 0;
+      return;
+    } else {
+      s = (uint32_t)start;
+    }
+    *s0 = s;
+    *ln = len <= 0 ? 0u : (uint64_t)len > n - s ? n - s : (uint32_t)len;
+  };
+  auto elem_index = [](uint32_t n, int64_t i, uint32_t* at) -> bool {
+    if (i < 0) {
+      const uint64_t a = (uint64_t)0 - (uint64_t)i;
+      if (a > n) return false;
+      *at = n - (uint32_t)a;
+      return true;
+    }
+    if ((uint64_t)i >= n) return false;
+    *at = (uint32_t)i;
+    return true;
+  };
+  auto vless = [&](uint64_t x0, uint64_t x1, uint64_t y0, uint64_t y1) -> bool {  // (one element type)
+    const uint32_t t = (uint32_t)(x0 & 0xffu);
+    if (t == sv::INT) return (int64_t)x1 < (int64_t)y1;
+    if (t == sv::BOOL) return !x1 && y1;
+    const uint32_t la = len_of(x0), lb = len_of(y0);
+    const uint8_t *pa = bytes_of(x0, x1), *pb = bytes_of(y0, y1);
+    uint32_t k = 0;
+    while (k < la && k < lb && pa[k] == pb[k]) ++k;
+    return k < la && k < lb ? pa[k] < pb[k] : la < lb;
+  };
   for (uint32_t pc = 0; pc < code_len;) {
     const uint32_t op = code[pc++];
     switch (op) {
@@ -818,96 +998,687 @@ KW_HD inline int run_script_prog(const uint8_t* prog, uint64_t* scratch, Ok ok, 
         ++sp;
         break;
       }
+      case S_XSTORE: {  // [.., changed receiver, result]: the receiver into a variable, keep the result
+        const uint32_t v = fp + rd16(pc);
+        pc += 2;
+        vars[2 * v] = st[2 * (sp - 2)];
+        vars[2 * v + 1] = st[2 * (sp - 2) + 1];
+        st[2 * (sp - 2)] = st[2 * (sp - 1)];
+        st[2 * (sp - 2) + 1] = st[2 * (sp - 1) + 1];
+        --sp;
+        break;
+      }
       case S_FN: {
-        const uint32_t fid = code[pc++];
-        if (fid == F_LEN || fid == F_IS_EMPTY || fid == F_TO_STRING || fid == F_TYPE_OF) {
-          const uint32_t i = sp - 1, t = type(i);
-          const uint64_t w0 = st[2 * i], w1 = st[2 * i + 1];
-          if (fid == F_TYPE_OF) {
-            const uint32_t o = t == sv::UNIT ? 0u : t == sv::BOOL ? 2u : t == sv::INT ? 6u : t == sv::STR ? 9u : 15u;
-            const uint32_t n = t == sv::UNIT ? 2u : t == sv::BOOL ? 4u : t == sv::INT ? 3u : t == sv::STR ? 6u : 5u;
-            st[2 * i] = sv::STR | ((uint64_t)n << 32);
-            st[2 * i + 1] = tnames + o;
-          } else if (fid == F_TO_STRING) {
-            if (t == sv::STR) break;
-            uint8_t tmp[24];
-            const uint8_t* p;
-            uint32_t n;
-            if (!text_of(w0, w1, tmp, &p, &n)) return 2;
-            if (!charge(n)) return 2;
-            uint8_t* d = new_str(n);
-            if (!d && n) return 2;
-            for (uint32_t k = 0; k < n; ++k) d[k] = p[k];
-            st[2 * i] = sv::STR | sv::ARENA | ((uint64_t)n << 32);
-            st[2 * i + 1] = d ? (uint64_t)(d - arena) : 0u;
-          } else {
-            uint64_t n;
-            if (t == sv::ARR) {
-              n = len_of(w0);
-            } else if (t == sv::STR) {  // characters: UTF-8 lead bytes
-              const uint8_t* p = bytes_of(w0, w1);
-              n = 0;
-              for (uint32_t k = 0; k < len_of(w0); ++k) n += (p[k] & 0xC0u) != 0x80u;
+        const uint32_t fid = code[pc], na = code[pc + 1] & 0x7fu, mut = code[pc + 1] >> 7;
+        pc += 2;
+        const uint32_t A = sp - na;  // the arguments are st[A .. sp)
+        // the result r (and for a `&mut` function the receiver as changed, rv) replace the arguments
+        uint64_t r0 = sv::UNIT, r1 = 0, rv0 = st[2 * A], rv1 = st[2 * A + 1];
+        const uint32_t t0 = type(A), t1 = na > 1 ? type(A + 1) : 0u, t2 = na > 2 ? type(A + 2) : 0u;
+        const uint64_t a0 = st[2 * A], v0 = st[2 * A + 1];
+        const int64_t i1 = na > 1 ? (int64_t)st[2 * (A + 1) + 1] : 0, i2 = na > 2 ? (int64_t)st[2 * (A + 2) + 1] : 0;
+        const uint32_t n0 = len_of(a0);
+        auto res_int = [&](int64_t x) {
+          r0 = sv::INT;
+          r1 = (uint64_t)x;
+        };
+        auto res_bool = [&](bool x) {
+          r0 = sv::BOOL;
+          r1 = x ? 1u : 0u;
+        };
+        switch (fid) {
+          case F_LEN:
+          case F_IS_EMPTY:
+          case F_TYPE_OF:
+          case F_TO_STRING: {
+            if (fid == F_TYPE_OF) {
+              const uint32_t o = t0 == sv::UNIT ? 0u : t0 == sv::BOOL ? 2u : t0 == sv::INT ? 6u : t0 == sv::STR ? 9u : 15u;
+              const uint32_t n = t0 == sv::UNIT ? 2u : t0 == sv::BOOL ? 4u : t0 == sv::INT ? 3u : t0 == sv::STR ? 6u : 5u;
+              r0 = sv::STR | ((uint64_t)n << 32);
+              r1 = tnames + o;
+            } else if (fid == F_TO_STRING) {
+              if (t0 == sv::STR) {
+                r0 = a0;
+                r1 = v0;
+                break;
+              }
+              uint8_t tmp[24];
+              const uint8_t* p;
+              uint32_t n;
+              if (!text_of(a0, v0, tmp, &p, &n)) return 2;
+              if (!charge(n)) return 2;
+              uint8_t* d = new_str(n);
+              if (!d && n) return 2;
+              for (uint32_t k = 0; k < n; ++k) d[k] = p[k];
+              r0 = sv::STR | sv::ARENA | ((uint64_t)n << 32);
+              r1 = d ? (uint64_t)(d - arena) : 0u;
+            } else {
+              uint64_t n;
+              if (t0 == sv::ARR) n = n0;
+              else if (t0 == sv::STR) n = nchars(bytes_of(a0, v0), n0);
+              else return 2;
+              if (fid == F_LEN) res_int((int64_t)n);
+              else res_bool(n == 0);
+            }
+            break;
+          }
+          case F_PUSH: {
+            if (t0 != sv::ARR) return 2;
+            if (!charge(16u * (n0 + 1))) return 2;
+            uint64_t* c = new_cells(n0 + 1);
+            if (!c) return 2;
+            const uint64_t* o = cells_of(v0);
+            for (uint32_t k = 0; k < 2 * n0; ++k) c[k] = o[k];
+            c[2 * n0] = st[2 * (A + 1)];
+            c[2 * n0 + 1] = st[2 * (A + 1) + 1];
+            rv0 = arr_word(n0 + 1);
+            rv1 = (uint64_t)((uint8_t*)c - arena);
+            break;
+          }
+          case F_CONTAINS:
+          case F_IN:
+          case F_INDEX_OF:
+          case F_INDEX_OF_FROM: {
+            // F_IN is contains(b, a): the haystack is the second argument
+            const uint32_t ic = fid == F_IN ? A + 1 : A, ix = fid == F_IN ? A : A + 1;
+            const uint32_t tc = type(ic), tx = type(ix);
+            const uint64_t c0 = st[2 * ic], c1 = st[2 * ic + 1], x0 = st[2 * ix], x1 = st[2 * ix + 1];
+            const bool idx = fid == F_INDEX_OF || fid == F_INDEX_OF_FROM;
+            if (fid == F_INDEX_OF_FROM && t2 != sv::INT) return 2;
+            int64_t found = -1;
+            if (tc == sv::ARR) {
+              const uint32_t n = len_of(c0);
+              uint32_t from = 0, ln;
+              if (fid == F_INDEX_OF_FROM) offset_len(n, i2, 0, &from, &ln);
+              const uint64_t* c = cells_of(c1);
+              for (uint32_t k = from; k < n && found < 0; ++k) {
+                const int e = veq(c[2 * k], c[2 * k + 1], x0, x1);
+                if (e < 0) return 2;
+                if (e) found = k;
+              }
+            } else if (tc == sv::STR && tx == sv::STR) {
+              const uint8_t *hs = bytes_of(c0, c1), *nd = bytes_of(x0, x1);
+              const uint32_t hn = len_of(c0), nn = len_of(x0);
+              if (!idx) {
+                found = find_bytes(hs, hn, nd, nn, 0) < 0 ? -1 : 0;
+              } else if (hn) {
+                uint32_t from = 0;
+                bool none = false;
+                if (fid == F_INDEX_OF_FROM) {
+                  const uint32_t nc = nchars(hs, hn);
+                  if (i2 < 0) {
+                    const uint64_t m = (uint64_t)0 - (uint64_t)i2;
+                    from = m > nc ? 0u : char_byte(hs, hn, nc - (uint32_t)m);
+                  } else if ((uint64_t)i2 >= nc) {
+                    none = i2 != 0;
+                  } else {
+                    from = char_byte(hs, hn, (uint32_t)i2);
+                  }
+                }
+                const int64_t k = none ? -1 : find_bytes(hs, hn, nd, nn, from);
+                found = k < 0 ? -1 : (int64_t)nchars(hs, (uint32_t)k);
+              }
             } else {
               return 2;
             }
-            if (fid == F_LEN) set(i, sv::INT, n);
-            else set(i, sv::BOOL, n == 0 ? 1u : 0u);
+            if (idx) res_int(found);
+            else res_bool(found >= 0);
+            break;
           }
-          break;
-        }
-        // two arguments: (a, b) on the stack; F_IN is contains(b, a)
-        uint32_t ic = sp - 2, ix = sp - 1;
-        if (fid == F_IN) {
-          ic = sp - 1;
-          ix = sp - 2;
-        }
-        const uint32_t tc = type(ic), tx = type(ix);
-        const uint64_t c0 = st[2 * ic], c1 = st[2 * ic + 1], x0 = st[2 * ix], x1 = st[2 * ix + 1];
-        uint64_t r = 0;
-        if (fid == F_PUSH) {
-          if (tc != sv::ARR) return 2;
-          const uint32_t n = len_of(c0);
-          if (!charge(16u * (n + 1))) return 2;
-          uint64_t* c = new_cells(n + 1);
-          if (!c) return 2;
-          const uint64_t* o = cells_of(c1);
-          for (uint32_t k = 0; k < 2 * n; ++k) c[k] = o[k];
-          c[2 * n] = x0;
-          c[2 * n + 1] = x1;
-          st[2 * (sp - 2)] = sv::ARR | sv::ARENA | ((uint64_t)(n + 1) << 32);
-          st[2 * (sp - 2) + 1] = (uint64_t)((uint8_t*)c - arena);
-          --sp;
-          break;
-        }
-        if (fid == F_CONTAINS || fid == F_IN) {
-          if (tc == sv::ARR) {
-            const uint64_t* c = cells_of(c1);
-            for (uint32_t k = 0; k < len_of(c0) && !r; ++k) {
-              const int e = veq(c[2 * k], c[2 * k + 1], x0, x1);
+          case F_STARTS_WITH:
+          case F_ENDS_WITH: {
+            if (t0 != sv::STR || t1 != sv::STR) return 2;
+            const uint32_t hn = n0, nn = len_of(st[2 * (A + 1)]);
+            const uint8_t *hs = bytes_of(a0, v0) + (fid == F_ENDS_WITH && nn <= hn ? hn - nn : 0u),
+                          *nd = bytes_of(st[2 * (A + 1)], st[2 * (A + 1) + 1]);
+            bool m = nn <= hn;
+            for (uint32_t j = 0; m && j < nn; ++j) m = hs[j] == nd[j];
+            res_bool(m);
+            break;
+          }
+          // ---- integers
+          case F_ABS:
+          case F_SIGN:
+          case F_IS_ZERO:
+          case F_IS_ODD:
+          case F_IS_EVEN: {
+            if (t0 != sv::INT) return 2;
+            const int64_t x = (int64_t)v0;
+            if (fid == F_ABS) {
+              if (x == INT64_MIN) return 2;
+              res_int(x < 0 ? -x : x);
+            } else if (fid == F_SIGN) {
+              res_int(x < 0 ? -1 : x > 0 ? 1 : 0);
+            } else {
+              res_bool(fid == F_IS_ZERO ? x == 0 : fid == F_IS_ODD ? (x & 1) != 0 : (x & 1) == 0);
+            }
+            break;
+          }
+          case F_MAX:
+          case F_MIN: {
+            if (t0 != sv::INT || t1 != sv::INT) return 2;
+            const int64_t x = (int64_t)v0;
+            res_int(fid == F_MAX ? (x >= i1 ? x : i1) : (x <= i1 ? x : i1));
+            break;
+          }
+          case F_TO_HEX:
+          case F_TO_OCTAL:
+          case F_TO_BINARY: {
+            if (t0 != sv::INT) return 2;
+            const uint32_t bits = fid == F_TO_HEX ? 4u : fid == F_TO_OCTAL ? 3u : 1u;
+            uint8_t tmp[64];
+            uint32_t n = 0;
+            uint64_t u = v0;
+            do {
+              tmp[n++] = (uint8_t)"0123456789abcdef"[u & ((1u << bits) - 1u)];
+              u >>= bits;
+            } while (u);
+            if (!charge(n)) return 2;
+            uint8_t* d = new_str(n);
+            if (!d) return 2;
+            for (uint32_t k = 0; k < n; ++k) d[k] = tmp[n - 1 - k];
+            r0 = sv::STR | sv::ARENA | ((uint64_t)n << 32);
+            r1 = (uint64_t)(d - arena);
+            break;
+          }
+          case F_PARSE_INT:
+          case F_PARSE_INT_R: {
+            if (t0 != sv::STR || (fid == F_PARSE_INT_R && t1 != sv::INT)) return 2;
+            const int64_t radix = fid == F_PARSE_INT_R ? i1 : 10;
+            if (radix < 2 || radix > 36) return 2;
+            const uint8_t* p = bytes_of(a0, v0);
+            uint32_t b = 0, e = n0;
+            trim_ws(p, &b, &e);
+            if (b == e) return 2;
+            bool neg = false;
+            if (p[b] == '+' || p[b] == '-') {
+              neg = p[b] == '-';
+              if (++b == e) return 2;
+            }
+            long long acc = 0;
+            for (uint32_t k = b; k < e; ++k) {
+              const uint32_t c = p[k];
+              const int64_t d = c >= '0' && c <= '9' ? (int64_t)c - '0' : c >= 'a' && c <= 'z' ? (int64_t)c - 'a' + 10
+                                : c >= 'A' && c <= 'Z' ? (int64_t)c - 'A' + 10 : 99;
+              if (d >= radix) return 2;
+              if (__builtin_mul_overflow(acc, (long long)radix, &acc)) return 2;
+              if (neg ? __builtin_sub_overflow(acc, (long long)d, &acc) : __builtin_add_overflow(acc, (long long)d, &acc))
+                return 2;
+            }
+            res_int(acc);
+            break;
+          }
+          // ---- strings
+          case F_TO_UPPER:
+          case F_TO_LOWER:
+          case F_MAKE_UPPER:
+          case F_MAKE_LOWER: {
+            if (t0 != sv::STR) return 2;
+            const bool up = fid == F_TO_UPPER || fid == F_MAKE_UPPER;
+            const uint8_t* p = bytes_of(a0, v0);
+            uint32_t n = 0;
+            for (int pass = 0; pass < 2; ++pass) {
+              uint8_t* d = nullptr;
+              if (pass == 1) {
+                if (!charge(n)) return 2;
+                d = new_str(n);
+                if (!d && n) return 2;
+                r0 = sv::STR | sv::ARENA | ((uint64_t)n << 32);
+                r1 = d ? (uint64_t)(d - arena) : 0u;
+              }
+              uint32_t w = 0;
+              for (uint32_t k = 0; k < n0;) {
+                uint32_t c;
+                const uint32_t k1 = utf8_next(p, n0, k, &c);
+                uint32_t m[3], nm;
+                if (!up && c == 0x3A3u) {  // Σ: ς at the end of a word (Final_Sigma)
+                  m[0] = final_sigma(p, n0, k, k1) ? 0x3C2u : 0x3C3u;
+                  nm = 1;
+                } else {
+                  nm = ch_map(c, up, m);
+                }
+                for (uint32_t j = 0; j < nm; ++j) w += put_utf8_at(m[j], d ? d + w : nullptr);
+                k = k1;
+              }
+              n = w;
+            }
+            if (fid == F_MAKE_UPPER || fid == F_MAKE_LOWER) {
+              rv0 = r0;
+              rv1 = r1;
+              r0 = sv::UNIT;
+              r1 = 0;
+            }
+            break;
+          }
+          case F_TRIM: {
+            if (t0 != sv::STR) return 2;
+            uint32_t b = 0, e = n0;
+            trim_ws(bytes_of(a0, v0), &b, &e);
+            rv0 = str_slice(a0, b, e);
+            rv1 = v0 + b;
+            break;
+          }
+          case F_SUB_STRING:
+          case F_SUB_STRING_N:
+          case F_CROP:
+          case F_CROP_N: {
+            const bool n3 = fid == F_SUB_STRING_N || fid == F_CROP_N;
+            if (t0 != sv::STR || t1 != sv::INT || (n3 && t2 != sv::INT)) return 2;
+            const uint8_t* p = bytes_of(a0, v0);
+            const int64_t len = n3 ? i2 : (int64_t)n0;
+            const uint32_t nc = nchars(p, n0);
+            uint32_t b = 0, e = 0;
+            if (nc && len > 0) {
+              uint32_t off = 0;
+              bool empty = false;
+              if (i1 < 0) {
+                const uint64_t m = (uint64_t)0 - (uint64_t)i1;
+                off = m > nc ? 0u : nc - (uint32_t)m;
+              } else if ((uint64_t)i1 >= nc) {
+                empty = true;
+              } else {
+                off = (uint32_t)i1;
+              }
+              if (!empty) {
+                const uint32_t take = (uint64_t)len > nc - off ? nc - off : (uint32_t)len;
+                b = char_byte(p, n0, off);
+                e = char_byte(p, n0, off + take);
+              }
+            }
+            const uint64_t s0 = str_slice(a0, b, e), s1 = v0 + b;
+            if (fid == F_SUB_STRING || fid == F_SUB_STRING_N) {
+              r0 = s0;
+              r1 = s1;
+            } else {
+              rv0 = s0;
+              rv1 = s1;
+            }
+            break;
+          }
+          case F_REPLACE:
+          case F_REMOVE: {
+            if (fid == F_REMOVE && t0 == sv::ARR) {
+              if (t1 != sv::INT) return 2;
+              uint32_t at;
+              if (!elem_index(n0, i1, &at)) break;
+              if (!charge(16u * (n0 - 1))) return 2;
+              uint64_t* c = n0 > 1 ? new_cells(n0 - 1) : nullptr;
+              if (n0 > 1 && !c) return 2;
+              const uint64_t* o = cells_of(v0);
+              r0 = o[2 * at];
+              r1 = o[2 * at + 1];
+              for (uint32_t k = 0, j = 0; k < n0; ++k) {
+                if (k == at) continue;
+                c[2 * j] = o[2 * k];
+                c[2 * j + 1] = o[2 * k + 1];
+                ++j;
+              }
+              rv0 = arr_word(n0 - 1);
+              rv1 = c ? (uint64_t)((uint8_t*)c - arena) : 0u;
+              break;
+            }
+            // replace(s, find, sub) / remove(s, sub) = replace(s, sub, "")
+            if (t0 != sv::STR || t1 != sv::STR || (fid == F_REPLACE && t2 != sv::STR)) return 2;
+            const uint32_t fn = len_of(st[2 * (A + 1)]);
+            if (n0 == 0 || (fid == F_REMOVE && fn == 0)) break;
+            const uint8_t *p = bytes_of(a0, v0), *f = bytes_of(st[2 * (A + 1)], st[2 * (A + 1) + 1]);
+            const uint8_t* sub = fid == F_REPLACE ? bytes_of(st[2 * (A + 2)], st[2 * (A + 2) + 1]) : nullptr;
+            const uint32_t sn = fid == F_REPLACE ? len_of(st[2 * (A + 2)]) : 0u;
+            uint32_t nm = 0;
+            for (int64_t k = next_match(p, n0, f, fn, 0); k >= 0; k = next_match(p, n0, f, fn, (uint32_t)k + (fn ? fn : 1u)))
+              ++nm;
+            const uint32_t n = n0 - nm * fn + nm * sn;
+            if (!charge(n)) return 2;
+            uint8_t* d = new_str(n);
+            if (!d && n) return 2;
+            uint32_t w = 0, from = 0;
+            for (int64_t k = next_match(p, n0, f, fn, 0); k >= 0; k = next_match(p, n0, f, fn, (uint32_t)k + (fn ? fn : 1u))) {
+              for (uint32_t j = from; j < (uint32_t)k; ++j) d[w++] = p[j];
+              for (uint32_t j = 0; j < sn; ++j) d[w++] = sub[j];
+              from = (uint32_t)k + fn;
+            }
+            for (uint32_t j = from; j < n0; ++j) d[w++] = p[j];
+            rv0 = sv::STR | sv::ARENA | ((uint64_t)n << 32);
+            rv1 = d ? (uint64_t)(d - arena) : 0u;
+            break;
+          }
+          case F_SPLIT_WS:
+          case F_SPLIT:
+          case F_SPLIT_N:
+          case F_SPLIT_REV:
+          case F_SPLIT_REV_N: {
+            if (fid == F_SPLIT && t0 == sv::ARR && t1 == sv::INT) {  // the array's tail from the index
+              uint32_t s0, ln;
+              offset_len(n0, i1, INT64_MAX, &s0, &ln);
+              r0 = arr_word(n0 - s0);
+              r1 = v0 + 16ull * s0;
+              rv0 = arr_word(s0);
+              break;
+            }
+            if (t0 != sv::STR) return 2;
+            const uint8_t* p = bytes_of(a0, v0);
+            if (fid == F_SPLIT && t1 == sv::INT) {  // at a character position
+              const uint32_t nc = nchars(p, n0);
+              uint32_t at;
+              if (i1 <= 0) {
+                const uint64_t m = (uint64_t)0 - (uint64_t)i1;
+                at = m > nc ? 0u : nc - (uint32_t)m;
+              } else {
+                at = (uint64_t)i1 > nc ? nc : (uint32_t)i1;
+              }
+              const uint32_t bb = char_byte(p, n0, at);
+              if (!charge(32u)) return 2;
+              uint64_t* c = new_cells(2);
+              if (!c) return 2;
+              c[0] = str_slice(a0, 0, bb);
+              c[1] = v0;
+              c[2] = str_slice(a0, bb, n0);
+              c[3] = v0 + bb;
+              r0 = arr_word(2);
+              r1 = (uint64_t)((uint8_t*)c - arena);
+              break;
+            }
+            const bool rev = fid == F_SPLIT_REV || fid == F_SPLIT_REV_N, lim = fid == F_SPLIT_N || fid == F_SPLIT_REV_N;
+            if (fid != F_SPLIT_WS && t1 != sv::STR) return 2;
+            if (lim && t2 != sv::INT) return 2;
+            const uint64_t maxp = lim ? (i2 < 1 ? 1ull : (uint64_t)i2) : ~0ull;
+            const uint8_t* f = fid == F_SPLIT_WS ? nullptr : bytes_of(st[2 * (A + 1)], st[2 * (A + 1) + 1]);
+            const uint32_t fn = fid == F_SPLIT_WS ? 0u : len_of(st[2 * (A + 1)]);
+            uint64_t* c = nullptr;
+            uint32_t np = 0;
+            for (int pass = 0; pass < 2; ++pass) {
+              if (pass == 1) {
+                if (!charge(16u * np)) return 2;
+                c = np ? new_cells(np) : nullptr;
+                if (np && !c) return 2;
+              }
+              uint32_t w = 0;
+              auto piece = [&](uint32_t b, uint32_t e) {
+                if (c) {
+                  c[2 * w] = str_slice(a0, b, e);
+                  c[2 * w + 1] = v0 + b;
+                }
+                ++w;
+              };
+              if (fid == F_SPLIT_WS) {  // split_whitespace: the non-empty runs between White_Space
+                for (uint32_t k = 0; k < n0;) {
+                  uint32_t cp, k1 = utf8_next(p, n0, k, &cp);
+                  if (ch_flags(cp) & kChWs) {
+                    k = k1;
+                    continue;
+                  }
+                  const uint32_t b = k;
+                  while (k < n0) {
+                    k1 = utf8_next(p, n0, k, &cp);
+                    if (ch_flags(cp) & kChWs) break;
+                    k = k1;
+                  }
+                  piece(b, k);
+                }
+              } else if (!rev) {
+                uint32_t from = 0;
+                for (int64_t k = next_match(p, n0, f, fn, 0); k >= 0;
+                     k = next_match(p, n0, f, fn, (uint32_t)k + (fn ? fn : 1u))) {
+                  if (w + 1 == maxp) break;
+                  piece(from, (uint32_t)k);
+                  from = (uint32_t)k + fn;
+                }
+                piece(from, n0);
+              } else {
+                uint32_t to = n0;
+                for (int64_t k = prev_match(p, n0, f, fn, n0); k >= 0;
+                     k = fn ? prev_match(p, n0, f, fn, (uint32_t)k) : (k == 0 ? -1 : prev_match(p, n0, f, fn, (uint32_t)k - 1))) {
+                  if (w + 1 == maxp) break;
+                  piece((uint32_t)k + fn, to);
+                  to = (uint32_t)k;
+                }
+                piece(0, to);
+              }
+              np = w;
+            }
+            r0 = arr_word(np);
+            r1 = c ? (uint64_t)((uint8_t*)c - arena) : 0u;
+            break;
+          }
+          case F_BYTES:
+            if (t0 != sv::STR) return 2;
+            res_int(n0);
+            break;
+          // ---- arrays, and the string forms of append / clear / truncate
+          case F_APPEND: {
+            if (t0 == sv::ARR && t1 == sv::ARR) {
+              const uint32_t nb = len_of(st[2 * (A + 1)]);
+              if (!charge(16u * (n0 + nb))) return 2;
+              uint64_t* c = n0 + nb ? new_cells(n0 + nb) : nullptr;
+              if (n0 + nb && !c) return 2;
+              const uint64_t *pa = cells_of(v0), *pb = cells_of(st[2 * (A + 1) + 1]);
+              for (uint32_t k = 0; k < 2 * n0; ++k) c[k] = pa[k];
+              for (uint32_t k = 0; k < 2 * nb; ++k) c[2 * n0 + k] = pb[k];
+              rv0 = arr_word(n0 + nb);
+              rv1 = c ? (uint64_t)((uint8_t*)c - arena) : 0u;
+              break;
+            }
+            if (t0 != sv::STR) return 2;
+            uint8_t tmp[24];
+            const uint8_t* pb;
+            uint32_t lb;
+            if (!text_of(st[2 * (A + 1)], st[2 * (A + 1) + 1], tmp, &pb, &lb)) return 2;
+            if (!charge(n0 + lb)) return 2;
+            uint8_t* d = new_str(n0 + lb);
+            if (!d && n0 + lb) return 2;
+            const uint8_t* pa = bytes_of(a0, v0);
+            for (uint32_t k = 0; k < n0; ++k) d[k] = pa[k];
+            for (uint32_t k = 0; k < lb; ++k) d[n0 + k] = pb[k];
+            rv0 = sv::STR | sv::ARENA | ((uint64_t)(n0 + lb) << 32);
+            rv1 = d ? (uint64_t)(d - arena) : 0u;
+            break;
+          }
+          case F_INSERT:
+          case F_SET:
+          case F_REVERSE:
+          case F_SPLICE:
+          case F_PAD: {
+            // an array rebuilt into new cells: n cells from the old ones by the function's rule
+            if (t0 != sv::ARR) return 2;
+            if ((fid == F_INSERT || fid == F_SET || fid == F_PAD) && t1 != sv::INT) return 2;
+            if (fid == F_SPLICE && (t1 != sv::INT || t2 != sv::INT || type(A + 3) != sv::ARR)) return 2;
+            uint32_t at = 0, ln = 0, n = n0;
+            if (fid == F_INSERT) {
+              offset_len(n0, i1, 0, &at, &ln);
+              n = n0 + 1;
+            } else if (fid == F_SET) {
+              if (!elem_index(n0, i1, &at)) break;
+            } else if (fid == F_SPLICE) {
+              if (n0) offset_len(n0, i1, i2, &at, &ln);
+              n = n0 - ln + len_of(st[2 * (A + 3)]);
+            } else if (fid == F_PAD) {
+              if (i1 <= 0 || (uint64_t)i1 <= n0) break;
+              if ((uint64_t)i1 > kMaxScriptAlloc) return 2;
+              n = (uint32_t)i1;
+            }
+            if (!charge(16u * n)) return 2;
+            uint64_t* c = n ? new_cells(n) : nullptr;
+            if (n && !c) return 2;
+            const uint64_t* o = cells_of(v0);
+            auto put = [&](uint32_t k, const uint64_t* src) {
+              c[2 * k] = src[0];
+              c[2 * k + 1] = src[1];
+            };
+            if (fid == F_INSERT) {
+              for (uint32_t k = 0, j = 0; k < n; ++k) put(k, k == at ? &st[2 * (A + 2)] : &o[2 * j++]);
+            } else if (fid == F_SET) {
+              for (uint32_t k = 0; k < n; ++k) put(k, k == at ? &st[2 * (A + 2)] : &o[2 * k]);
+            } else if (fid == F_REVERSE) {
+              for (uint32_t k = 0; k < n; ++k) put(k, &o[2 * (n - 1 - k)]);
+            } else if (fid == F_SPLICE) {
+              const uint32_t m = len_of(st[2 * (A + 3)]);
+              const uint64_t* rp = cells_of(st[2 * (A + 3) + 1]);
+              uint32_t w = 0;
+              for (uint32_t k = 0; k < at; ++k) put(w++, &o[2 * k]);
+              for (uint32_t k = 0; k < m; ++k) put(w++, &rp[2 * k]);
+              for (uint32_t k = at + ln; k < n0; ++k) put(w++, &o[2 * k]);
+            } else {  // pad
+              for (uint32_t k = 0; k < n; ++k) put(k, k < n0 ? &o[2 * k] : &st[2 * (A + 2)]);
+            }
+            rv0 = arr_word(n);
+            rv1 = c ? (uint64_t)((uint8_t*)c - arena) : 0u;
+            break;
+          }
+          case F_POP:
+          case F_SHIFT:
+            if (t0 != sv::ARR) return 2;  // (a string's pop returns a character: refused by name)
+            if (n0) {
+              const uint64_t* o = cells_of(v0);
+              const uint32_t k = fid == F_POP ? n0 - 1 : 0u;
+              r0 = o[2 * k];
+              r1 = o[2 * k + 1];
+              rv0 = arr_word(n0 - 1);
+              rv1 = fid == F_POP ? v0 : v0 + 16u;
+            }
+            break;
+          case F_SORT:
+          case F_DEDUP: {
+            if (t0 != sv::ARR) return 2;
+            if (n0 <= 1) break;
+            const uint64_t* o = cells_of(v0);
+            if (fid == F_SORT) {
+              const uint32_t te = (uint32_t)(o[0] & 0xffu);
+              for (uint32_t k = 1; k < n0; ++k)
+                if ((uint32_t)(o[2 * k] & 0xffu) != te) return 2;
+              if (te == sv::ARR || te == sv::UNIT) break;
+              if (!charge(16u * n0)) return 2;
+              uint64_t* c = new_cells(n0);
+              if (!c) return 2;
+              for (uint32_t k = 0; k < 2 * n0; ++k) c[k] = o[k];
+              for (uint32_t k = 1; k < n0; ++k) {  // insertion sort: stable, as Rust's sort_by
+                const uint64_t x0 = c[2 * k], x1 = c[2 * k + 1];
+                uint32_t j = k;
+                while (j > 0 && vless(x0, x1, c[2 * (j - 1)], c[2 * (j - 1) + 1])) {
+                  c[2 * j] = c[2 * (j - 1)];
+                  c[2 * j + 1] = c[2 * (j - 1) + 1];
+                  --j;
+                }
+                c[2 * j] = x0;
+                c[2 * j + 1] = x1;
+              }
+              rv0 = arr_word(n0);
+              rv1 = (uint64_t)((uint8_t*)c - arena);
+              break;
+            }
+            // dedup: drop each element equal to the last one kept
+            uint32_t n = 1, last = 0;
+            for (uint32_t k = 1; k < n0; ++k) {
+              const int e = veq(o[2 * k], o[2 * k + 1], o[2 * last], o[2 * last + 1]);
               if (e < 0) return 2;
-              r = (uint64_t)e;
+              if (!e) {
+                ++n;
+                last = k;
+              }
             }
-          } else if (tc == sv::STR && tx == sv::STR) {
-            const uint8_t *hs = bytes_of(c0, c1), *nd = bytes_of(x0, x1);
-            const uint32_t hn = len_of(c0), nn = len_of(x0);
-            for (uint32_t k = 0; k + nn <= hn && !r; ++k) {
-              bool m = true;
-              for (uint32_t j = 0; m && j < nn; ++j) m = hs[k + j] == nd[j];
-              r = m;
+            if (!charge(16u * n)) return 2;
+            uint64_t* c = new_cells(n);
+            if (!c) return 2;
+            c[0] = o[0];
+            c[1] = o[1];
+            last = 0;
+            for (uint32_t k = 1, w = 1; k < n0; ++k) {
+              if (veq(o[2 * k], o[2 * k + 1], o[2 * last], o[2 * last + 1])) continue;
+              c[2 * w] = o[2 * k];
+              c[2 * w + 1] = o[2 * k + 1];
+              ++w;
+              last = k;
             }
-          } else {
-            return 2;
+            rv0 = arr_word(n);
+            rv1 = (uint64_t)((uint8_t*)c - arena);
+            break;
           }
-        } else {  // F_STARTS_WITH / F_ENDS_WITH
-          if (tc != sv::STR || tx != sv::STR) return 2;
-          const uint32_t hn = len_of(c0), nn = len_of(x0);
-          const uint8_t *hs = bytes_of(c0, c1) + (fid == F_ENDS_WITH && nn <= hn ? hn - nn : 0u), *nd = bytes_of(x0, x1);
-          r = nn <= hn;
-          for (uint32_t j = 0; r && j < nn; ++j) r = hs[j] == nd[j];
+          case F_CLEAR:
+            if (t0 == sv::ARR) rv0 = arr_word(0);
+            else if (t0 == sv::STR) rv0 = str_slice(a0, 0, 0);
+            else return 2;
+            break;
+          case F_TRUNCATE:
+          case F_CHOP: {
+            if (t1 != sv::INT) return 2;
+            if (t0 == sv::STR && fid == F_TRUNCATE) {
+              const uint8_t* p = bytes_of(a0, v0);
+              if (i1 <= 0) rv0 = str_slice(a0, 0, 0);
+              else if ((uint64_t)i1 < nchars(p, n0)) rv0 = str_slice(a0, 0, char_byte(p, n0, (uint32_t)i1));
+              break;
+            }
+            if (t0 != sv::ARR) return 2;
+            if (i1 <= 0) {
+              rv0 = arr_word(0);
+            } else if ((uint64_t)i1 < n0) {
+              rv0 = arr_word((uint32_t)i1);
+              if (fid == F_CHOP) rv1 = v0 + 16ull * (n0 - (uint32_t)i1);
+            }
+            break;
+          }
+          case F_GET: {
+            if (t0 != sv::ARR || t1 != sv::INT) return 2;
+            uint32_t at;
+            if (elem_index(n0, i1, &at)) {
+              r0 = cells_of(v0)[2 * at];
+              r1 = cells_of(v0)[2 * at + 1];
+            }
+            break;
+          }
+          case F_EXTRACT:
+          case F_EXTRACT_N:
+          case F_DRAIN:
+          case F_RETAIN: {
+            const bool n3 = fid != F_EXTRACT;
+            if (t0 != sv::ARR || t1 != sv::INT || (n3 && t2 != sv::INT)) return 2;
+            const int64_t len = n3 ? i2 : INT64_MAX;
+            r0 = arr_word(0);
+            r1 = 0;
+            uint32_t s0 = 0, ln = 0;
+            if (n0 && len > 0) offset_len(n0, i1, len, &s0, &ln);
+            if (ln == 0) break;
+            const uint64_t slice0 = arr_word(ln), slice1 = v0 + 16ull * s0;
+            if (fid == F_EXTRACT || fid == F_EXTRACT_N) {
+              r0 = slice0;
+              r1 = slice1;
+              break;
+            }
+            // drain: the range is the result, the rest a copy; retain: the other way round
+            const uint32_t n = n0 - ln;
+            if (!charge(16u * n)) return 2;
+            uint64_t* c = n ? new_cells(n) : nullptr;
+            if (n && !c) return 2;
+            const uint64_t* o = cells_of(v0);
+            for (uint32_t k = 0, w = 0; k < n0; ++k) {
+              if (k >= s0 && k < s0 + ln) continue;
+              c[2 * w] = o[2 * k];
+              c[2 * w + 1] = o[2 * k + 1];
+              ++w;
+            }
+            const uint64_t rest0 = arr_word(n), rest1 = c ? (uint64_t)((uint8_t*)c - arena) : 0u;
+            if (fid == F_DRAIN) {
+              r0 = slice0;
+              r1 = slice1;
+              rv0 = rest0;
+              rv1 = rest1;
+            } else {
+              r0 = rest0;
+              r1 = rest1;
+              rv0 = slice0;
+              rv1 = slice1;
+            }
+            break;
+          }
+          default: return 2;
         }
-        set(sp - 2, sv::BOOL, r);
-        --sp;
+        sp = A;
+        if (mut) {
+          st[2 * sp] = rv0;
+          st[2 * sp + 1] = rv1;
+          ++sp;
+        }
+        st[2 * sp] = r0;
+        st[2 * sp + 1] = r1;
+        ++sp;
         break;
       }
       case S_BIN: {
@@ -988,6 +1759,26 @@ KW_HD inline int run_script_prog(const uint8_t* prog, uint64_t* scratch, Ok ok, 
           for (uint32_t k = 0; k < la; ++k) d[k] = pa[k];
           for (uint32_t k = 0; k < lb; ++k) d[la + k] = pb[k];
           st[2 * ia] = sv::STR | sv::ARENA | ((uint64_t)(la + lb) << 32);
+          st[2 * ia + 1] = d ? (uint64_t)(d - arena) : 0u;
+          break;
+        }
+        if (b_op == SB_SUB && ta == sv::STR && tb == sv::STR) {  // every occurrence of b removed
+          const uint32_t la = len_of(a0), lb = len_of(b0);
+          if (la == 0 || lb == 0) break;
+          const uint8_t *pa = bytes_of(a0, va), *pb = bytes_of(b0, vb);
+          uint32_t nm = 0;
+          for (int64_t k = next_match(pa, la, pb, lb, 0); k >= 0; k = next_match(pa, la, pb, lb, (uint32_t)k + lb)) ++nm;
+          const uint32_t n = la - nm * lb;
+          if (!charge(n)) return 2;
+          uint8_t* d = new_str(n);
+          if (!d && n) return 2;
+          uint32_t w = 0, from = 0;
+          for (int64_t k = next_match(pa, la, pb, lb, 0); k >= 0; k = next_match(pa, la, pb, lb, (uint32_t)k + lb)) {
+            for (uint32_t j = from; j < (uint32_t)k; ++j) d[w++] = pa[j];
+            from = (uint32_t)k + lb;
+          }
+          for (uint32_t j = from; j < la; ++j) d[w++] = pa[j];
+          st[2 * ia] = sv::STR | sv::ARENA | ((uint64_t)n << 32);
           st[2 * ia + 1] = d ? (uint64_t)(d - arena) : 0u;
           break;
         }

@@ -117,10 +117,64 @@ def _script(rng, names):
     `in`, switch, `??`, to_string, compound assignment, for and while loops, script functions), now
     and then with an operation that fails at evaluation for some member results (a bool + an int
     behind a branch, an index out of bounds)."""
-    bools, ints = [], []
+    bools, ints, strs, arrs = [], [], [], []
     fns = []
+    # r06: rhai's standard-package functions (DESIGN.md §2.1), drawn about a fifth of the time
+    lits = ['""', '"a"', '"ab,c"', '" x y "', '"\u03a3\u0391\u03a3"', '"\u00e9t\u00e9"', '"\u00df"', '"AbC"', '"1,2,,3"',
+            '"-42"', '"ff"', '"\u00a0z\u3000"']
+
+    def t(d):
+        r = rng.random()
+        if d <= 0 or r < 0.3:
+            return rng.choice(lits + strs)
+        if r < 0.4:
+            return f"({t(d - 1)} + {t(d - 1)})"
+        if r < 0.5:
+            return f"{t(d - 1)}.{rng.choice(['to_upper', 'to_lower'])}()"
+        if r < 0.6:
+            return f"{t(d - 1)}.sub_string({i(d - 1)}{', ' + i(d - 1) if rng.random() < 0.6 else ''})"
+        if r < 0.68:
+            return f"({t(d - 1)} - {t(d - 1)})"
+        if r < 0.75:
+            return f"({i(d - 1)}).{rng.choice(['to_hex', 'to_octal', 'to_binary', 'to_string'])}()"
+        if r < 0.82:
+            return f"{b(d - 1)}.to_string()"
+        if r < 0.9:
+            return f"({a(d - 1)}).get({i(d - 1)}) ?? {t(d - 1)}"  # (non-strings fail at comparison only)
+        return f"(if {b(d - 1)} {{ {t(d - 1)} }} else {{ {t(d - 1)} }})"
+
+    def a(d):
+        r = rng.random()
+        if d <= 0 or r < 0.3:
+            return rng.choice([f"[{rng.randint(-2, 3)}, {rng.randint(-2, 3)}, {rng.randint(-2, 3)}]", "[]"] + arrs)
+        if r < 0.45:
+            m = rng.choice(['split(",")', "split()", 'split_rev(",")', "split(1)"])
+            return f"{t(d - 1)}.{m}"
+        if r < 0.55:
+            return f"[{b(d - 1)}, {b(d - 1)}, {b(d - 1)}]"
+        if r < 0.65:
+            return f"{a(d - 1)}.extract({i(d - 1)}{', ' + i(d - 1) if rng.random() < 0.5 else ''})"
+        if r < 0.75:
+            return f"({a(d - 1)} + {a(d - 1)})"
+        if r < 0.85:
+            return f"{t(d - 1)}.split({t(0)}, {i(d - 1)})"
+        return f"[{i(d - 1)}, {t(d - 1)}]"
 
     def b(d):
+        r = rng.random()
+        if d > 0 and r < 0.18:
+            q = rng.random()
+            if q < 0.25:
+                return f"({t(d - 1)} {rng.choice(['==', '!=', '<', '>='])} {t(d - 1)})"
+            if q < 0.4:
+                return f"{t(d - 1)}.{rng.choice(['contains', 'starts_with', 'ends_with'])}({t(d - 1)})"
+            if q < 0.55:
+                return f"({a(d - 1)} {rng.choice(['==', '!='])} {a(d - 1)})"
+            if q < 0.7:
+                return f"({i(d - 1)}).{rng.choice(['is_odd', 'is_even', 'is_zero'])}()"
+            if q < 0.85:
+                return f"{a(d - 1)}.contains({rng.choice([i(d - 1), b(d - 1), t(d - 1)])})"
+            return f"({a(d - 1)}.get({i(d - 1)}) ?? {b(d - 1)})"
         r = rng.random()
         if d <= 0 or r < 0.2:
             pool = [f"{rng.choice(names)}()"] * 3 + bools
@@ -160,6 +214,22 @@ def _script(rng, names):
 
     def i(d):
         r = rng.random()
+        if d > 0 and r < 0.2:
+            q = rng.random()
+            if q < 0.2:
+                return f"{rng.choice(['abs', 'sign'])}({i(d - 1)})"
+            if q < 0.35:
+                return f"{rng.choice(['max', 'min'])}({i(d - 1)}, {i(d - 1)})"
+            if q < 0.5:
+                return f"{t(d - 1)}.{rng.choice(['len()', 'bytes()'])}"
+            if q < 0.65:
+                return f"{t(d - 1)}.index_of({t(d - 1)}{', ' + i(d - 1) if rng.random() < 0.4 else ''})"
+            if q < 0.75:
+                return f"parse_int({t(d - 1)}{', 16' if rng.random() < 0.3 else ''})"  # mostly an error
+            if q < 0.9:
+                return f"{a(d - 1)}.len()"
+            return f"{a(d - 1)}.index_of({i(d - 1)})"
+        r = rng.random()
         if d <= 0 or r < 0.3:
             return rng.choice([str(rng.randint(-3, 9))] + ints)
         if r < 0.55:
@@ -191,6 +261,21 @@ def _script(rng, names):
         elif r < 0.85:
             stmts.append(f"let n{k} = 0; while n{k} < {rng.randint(0, 4)} {{ n{k} += 1; }}")
             ints.append(f"n{k}")
+        elif r < 0.9:  # a variable changed through the standard packages' `&mut` functions
+            if rng.random() < 0.5:
+                op = rng.choice(["make_upper()", "make_lower()", "trim()", f"crop({i(1)})", f"crop({i(1)}, {i(1)})",
+                                 f'replace({t(0)}, {t(0)})', f"truncate({i(1)})", f"append({rng.choice([i(0), t(0), b(0)])})",
+                                 f"remove({t(0)})", "clear()"])
+                stmts.append(f"let s{k} = {t(1)}; s{k}.{op};")
+                strs.append(f"s{k}")
+            else:
+                op = rng.choice(["pop()", "shift()", "reverse()", "sort()", "dedup()", f"insert({i(1)}, {i(0)})",
+                                 f"remove({i(1)})", f"truncate({i(1)})", f"chop({i(1)})", f"set({i(1)}, {b(0)})",
+                                 f"append({a(1)})", f"pad({rng.randint(-1, 5)}, {i(0)})", f"drain({i(1)}, {i(1)})",
+                                 f"retain({i(1)}, {i(1)})", f"splice({i(1)}, {i(1)}, {a(1)})", f"split({i(1)})",
+                                 f"push({i(0)})"])
+                stmts.append(f"let a{k} = {a(1)}; a{k}.{op};")
+                arrs.append(f"a{k}")
         elif ints:
             stmts.append(f"{rng.choice(ints)} {rng.choice(['+=', '-=', '*='])} {i(1)};")
     return " ".join(stmts + [b(3)])

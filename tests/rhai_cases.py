@@ -34,7 +34,9 @@ VALID = [
     ("let a1 = [[1, 2], [3]]; a1[1] == [3] && [[1, 2], [3]].contains([1, 2]) && a()", [("a", True)]),
     ("[] == [] && [1] != [1, 2] && [1] != [\"1\"] && [()] == [()] && a()", [("a", True)]),
     ("[1, 2] + [3] == [1, 2, 3] && [].is_empty() && ![0].is_empty() && a()", [("a", True)]),
-    ("push([1], 2) == [1, 2] && a()", [("a", True)]),
+    # r06: push's receiver is rhai's `&mut` parameter and its result is (); function-call style
+    # works on a copy (r05's table wrongly had push([1], 2) == [1, 2])
+    ("push([1], 2) == () && a()", [("a", True)]),
     ("let v = [1]; push(v, 2); v == [1] && a()", [("a", True)]),  # function-call style: a copy
     ("a() in [true, b()]", [("a", True), ("ab", True), ("", True), ("b", ("causes", {"a"}))]),
     ('"b" !in ["a"] && a()', [("a", True)]),
@@ -96,6 +98,97 @@ VALID = [
     # numbers, strings, comments
     ("0x10 + 0o10 + 0b10 == 26 && 1_000 == 1000 && a()", [("a", True)]),
     ('"\\x41\\u00e9" == "Aé" && a() /* block /* nested */ comment */', [("a", True)]),
+    # r06: rhai's standard packages (Engine::new()) — integers
+    ("abs(-3) == 3 && (-3).abs() == 3 && abs(0) == 0 && a()", [("a", True)]),
+    ("sign(-7) == -1 && sign(0) == 0 && (9).sign() == 1 && a()", [("a", True)]),
+    ("is_zero(0) && !is_zero(5) && (-3).is_odd() && (4).is_even() && !(0).is_odd() && a()", [("a", True)]),
+    ("max(3, 8) == 8 && min(3, 8) == 3 && max(-1, -1) == -1 && (2).min(-5) == -5 && a()", [("a", True)]),
+    ('(255).to_hex() == "ff" && (8).to_octal() == "10" && (5).to_binary() == "101" && '
+     '(-1).to_hex() == "ffffffffffffffff" && (0).to_binary() == "0" && a()', [("a", True)]),
+    ('parse_int("42") == 42 && parse_int(" -17\t") == -17 && parse_int("+8") == 8 && parse_int("ff", 16) == 255 '
+     '&& parse_int("-Z", 36) == -35 && parse_int("-9223372036854775808") == -9223372036854775807 - 1 && a()',
+     [("a", True)]),
+    ('if a() { true } else { parse_int("4x") == 4 }',
+     [("a", True), ("", ("error", "Error parsing integer number '4x': invalid digit found in string"))]),
+    ('if a() { true } else { parse_int(" ") == 0 }',
+     [("", ("error", "Error parsing integer number ' ': cannot parse integer from empty string"))]),
+    ('if a() { true } else { parse_int("9223372036854775808") == 0 }',
+     [("", ("error", "number too large to fit in target type"))]),
+    ('if a() { true } else { parse_int("-", 10) == 0 }', [("", ("error", "invalid digit found in string"))]),
+    ('if a() { true } else { parse_int("1", 40) == 1 }', [("", ("error", "Invalid radix: '40'"))]),
+    ("if a() { true } else { abs(-9223372036854775807 - 1) == 0 }", [("", ("error", "Negation overflow"))]),
+    ('if a() { true } else { abs("x") == 1 }', [("", ("error", "Function not found: abs (string)"))]),
+    # strings
+    ('"AbC".to_upper() == "ABC" && "AbC".to_lower() == "abc" && to_upper("\u00df") == "SS" && '
+     '"\u0130".to_lower() == "i\u0307" && "\u00e9".to_upper() == "\u00c9" && a()', [("a", True)]),
+    # Σ lowers to ς at the end of a word (Final_Sigma), else to σ; ' between letters is case-ignorable
+    ('"\u039f\u0394\u039f\u03a3 \u03a3\u0391".to_lower() == "\u03bf\u03b4\u03bf\u03c2 \u03c3\u03b1" && '
+     '"\u03a3".to_lower() == "\u03c3" && "A\u03a3\'".to_lower() == "a\u03c2\'" && '
+     '"A\u03a3\'B".to_lower() == "a\u03c3\'b" && a()', [("a", True)]),
+    ('let s = "Hello"; s.make_upper(); let t = "Hi"; make_lower(t); s == "HELLO" && t == "Hi" && a()',
+     [("a", True)]),
+    ('let s = "  x y \t"; s.trim(); let u = "\u00a0z\u3000"; u.trim(); s == "x y" && u == "z" && a()',
+     [("a", True)]),
+    ('let r = " x ".trim(); r == () && a()', [("a", True)]),  # trim changes its receiver, returns ()
+    ('"hello".sub_string(1, 3) == "ell" && "hello".sub_string(-3, 2) == "ll" && "hello".sub_string(3) == "lo" && '
+     '"h\u00e9llo".sub_string(1, 1) == "\u00e9" && "abc".sub_string(5, 1) == "" && "abc".sub_string(0, -1) == "" '
+     '&& "abc".sub_string(-9, 2) == "ab" && sub_string("abc", 1) == "bc" && a()', [("a", True)]),
+    ('let s = "hello"; s.crop(1, 3); let t = "hello"; t.crop(-2); let u = "abc"; u.crop(7); '
+     's == "ell" && t == "lo" && u == "" && a()', [("a", True)]),
+    ('"abcb".index_of("b") == 1 && "abcb".index_of("b", 2) == 3 && "abc".index_of("z") == -1 && '
+     '"h\u00e9llo".index_of("l") == 2 && "abc".index_of("c", -1) == 2 && "abc".index_of("a", 5) == -1 && '
+     '"".index_of("") == -1 && "ab".index_of("") == 0 && "ab".index_of("", 1) == 1 && a()', [("a", True)]),
+    ('let s = "a-b-c"; s.replace("-", "+"); let t = "abc"; t.replace("", "."); let u = "aaa"; u.replace("aa", "b"); '
+     's == "a+b+c" && t == ".a.b.c." && u == "ba" && a()', [("a", True)]),
+    ('"a,b,,c".split(",") == ["a", "b", "", "c"] && " a b  c ".split() == ["a", "b", "c"] && '
+     '"abc".split(1) == ["a", "bc"] && "abc".split(-1) == ["ab", "c"] && "abc".split(0) == ["abc", ""] && '
+     '"a,b,c".split(",", 2) == ["a", "b,c"] && "a,b,c".split(",", 0) == ["a,b,c"] && '
+     '"a,b,c".split_rev(",") == ["c", "b", "a"] && "a,b,c".split_rev(",", 2) == ["c", "a,b"] && '
+     '"ab".split("") == ["", "a", "b", ""] && "aaa".split_rev("aa") == ["", "a"] && a()', [("a", True)]),
+    ('"h\u00e9llo".bytes() == 6 && "h\u00e9llo".len() == 5 && a()', [("a", True)]),
+    ('let s = "ab"; s.append(1); s.append(true); s.append(()); let t = "banana"; t.remove("an"); '
+     'let u = "xyz"; u.truncate(2); let v = "q"; v.clear(); s == "ab1true" && t == "ba" && u == "xy" && v == "" && a()',
+     [("a", True)]),
+    ('"banana" - "an" == "ba" && "abc" - "" == "abc" && a()', [("a", True)]),
+    ('let s = "aXbX"; s -= "X"; s == "ab" && a()', [("a", True)]),
+    ('if a() { true } else { "abc".pop() == () }',
+     [("", ("error", "unsupported by this engine: pop (string): it returns a character"))]),
+    ('if a() { true } else { "abc".get(0) == () }', [("", ("error", "unsupported by this engine: get (string, i64)"))]),
+    # arrays
+    ("let v = [1, 2, 3]; let x = v.pop(); let y = v.shift(); x == 3 && y == 1 && v == [2] && [].pop() == () && a()",
+     [("a", True)]),
+    ("let v = [1, 3]; v.insert(1, 2); v.insert(-1, 9); v.insert(10, 4); v.insert(-10, 0); v == [0, 1, 2, 9, 3, 4] "
+     "&& a()", [("a", True)]),
+    ("let v = [1, 2, 3]; let r = v.remove(1); let z = v.remove(5); let w = v.remove(-1); let q = v.remove(-5); "
+     "r == 2 && z == () && w == 3 && q == () && v == [1] && a()", [("a", True)]),
+    ('let v = [3, 1, 2]; v.sort(); let w = ["b", "a", "B", "\u00e9"]; w.sort(); let b = [true, false]; b.sort(); '
+     'let r = [1, 2, 3]; r.reverse(); let n = [[2], [1]]; n.sort(); '
+     'v == [1, 2, 3] && w == ["B", "a", "b", "\u00e9"] && b == [false, true] && r == [3, 2, 1] && n == [[2], [1]] '
+     '&& a()', [("a", True)]),
+    ('if a() { true } else { let v = [1, "x"]; v.sort(); true }',
+     [("", ("error", "sort() cannot be called with elements of different types"))]),
+    ("let v = [1]; v.append([2, 3]); let w = [1, 2, 3, 4]; w.truncate(2); let x = [1, 2, 3, 4]; x.chop(1); "
+     "let y = [1]; y.clear(); let z = [1, 2]; z.truncate(0); v == [1, 2, 3] && w == [1, 2] && x == [4] && y == [] "
+     "&& z == [] && a()", [("a", True)]),
+    ("let v = [1, 2, 3]; v.set(0, 9); v.set(7, 0); v.set(-1, 8); v.get(-1) == 8 && v.get(5) == () && "
+     "v.get(-4) == () && v == [9, 2, 8] && a()", [("a", True)]),
+    ("let v = [1, 2, 3, 4, 5]; let e = v.extract(1, 2); let t = v.extract(3); let d = v.drain(1, 2); "
+     "e == [2, 3] && t == [4, 5] && d == [2, 3] && v == [1, 4, 5] && v.extract(0, 0) == [] && a()", [("a", True)]),
+    ("let v = [1, 2, 3, 4, 5]; let r = v.retain(1, 3); let w = [1, 2]; let q = w.retain(0, 0); "
+     "r == [1, 5] && v == [2, 3, 4] && q == [] && w == [1, 2] && a()", [("a", True)]),
+    ('let v = [1, 2, 3]; v.splice(1, 1, ["x", "y"]); let w = []; w.splice(0, 3, [7]); let z = [1]; '
+     'z.splice(5, 1, [2]); v == [1, "x", "y", 3] && w == [7] && z == [1, 2] && a()', [("a", True)]),
+    ("let v = [1, 1, 2, 2, 1]; v.dedup(); let p = [1]; p.pad(3, 0); let s = [1, 2, 3, 4]; let t = s.split(1); "
+     "v == [1, 2, 1] && p == [1, 0, 0] && s == [1] && t == [2, 3, 4] && [5, 6, 5].index_of(5, 1) == 2 && "
+     "[5].index_of(7) == -1 && a()", [("a", True)]),
+    ("let v = [1, 2]; pop(v); reverse(v); v == [1, 2] && a()", [("a", True)]),  # function style: copies
+    ("let oks = [a(), b(), c()]; oks.dedup(); oks.len() == 1",
+     [("abc", True), ("", True), ("ab", ("causes", {"c"})), ("a", ("causes", {"b", "c"}))]),
+    ("let v = [a(), b()]; v.sort(); v[1]", [("a", True), ("b", True), ("", ("causes", {"a", "b"}))]),
+    ('let n = 0; for p in "x,y,z".split(",") { if p == "y" && b() { n += 1; } } n == 1 && a()',
+     [("ab", True), ("a", ("causes", {"b"}))]),
+    ("if a() { true } else { [].pad(5000, 1) == [] }",
+     [("", ("error", "engine limit: more than 16384 bytes of strings and arrays built"))]),
     # evaluation errors on some paths (500 for those requests)
     ("if a() { true } else { [1][5] == 1 }",
      [("a", True), ("", ("error", "Array index 5 out of bounds: only 1 element in array"))]),
@@ -150,6 +243,15 @@ INVALID = [
     ("if true { fn f() { 1 } } a()", "Syntax error: functions can only be defined at global level"),
     ("fn f(x) { x } fn f(y) { y } a()", "Syntax error: function 'f' with 1 parameters is defined more than once"),
     ("let x = 1; x.push(2); a()", "Function not found: push (i64, i64)"),
+    # r06: the standard packages' functions outside the engine are refused by name at load
+    ("sqrt(4) == 2 && a()", "unsupported by this engine: sqrt"),
+    ("let f = 1; [1].filter(f) == [] && a()", "unsupported by this engine: filter"),
+    ("timestamp() == () || a()", "unsupported by this engine: timestamp"),
+    ('"ab".chars() == [] && a()', "unsupported by this engine: chars"),
+    ("(5).get_bit(1) && a()", "unsupported by this engine: get_bit"),
+    ("const V = [1]; V.pop(); a()", "Syntax error: cannot assign to the constant 'V'"),
+    ("let v = [[1]]; v[0].sort(); a()", "unsupported by this engine: mutating an element in place (x[i].sort(..))"),
+    ('parse_int("z") == 0 && a()', "Error parsing integer number 'z': invalid digit found in string"),
     ("nope(1, 2) || a()", "Function not found: nope (i64, i64)"),
     ("let s = 0; for i in 0..200000 { s += 1; } a()", "engine limit: more than 100000 loop iterations"),
     ("99999999999999999999 > 1", "Syntax error: integer literal too large"),

@@ -32,7 +32,8 @@ VALID = [
     '"abc" < "abd" && (reg() | latest())',
     "ns() == 1 || priv()",             # mixed types compare unequal (rhai built-in)
     "ns() != 1 && priv() ^ reg()",
-    "{ let y = 3; y * 2 } > 5 && latest()",
+    "({ let y = 3; y * 2 }) > 5 && latest()",    # a block as an operand (a statement expression)
+    "for x in [1] { } [ns()].contains(true)",     # two statements: a loop, then an array
     "let z = 5; let z = z + 1; z == 6 && reg()",
     "if priv() { true } else { ns() + 1 == 2 }",  # an evaluation error on one path only
     "if reg() { 1 } else { true }",               # not a bool on one path
@@ -49,6 +50,7 @@ INVALID = [
     "x || ns()",
     "9223372036854775807 + 1 == 0 || ns()",
     "1 / 0 == 1",
+    "{ let y = 3; y * 2 } > 5 && latest()",  # a block statement ends at its brace (rhai's parse_stmt)
 ]
 
 
