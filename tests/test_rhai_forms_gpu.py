@@ -10,7 +10,7 @@ import kwgpu as K
 import oracle as O
 from helpers import diff_verdicts
 from rhai_cases import VALID
-from test_rhai_forms import VECTORS, check_expected, groups_doc, review
+from test_rhai_forms import MEMBERS, VECTORS, check_expected, groups_doc, review
 
 pytestmark = pytest.mark.gpu
 
@@ -51,3 +51,29 @@ def test_forms_on_device_match_oracle(monkeypatch, form):
             r = VECTORS.index(acc)
             resp = b.format_response(env, r, j, int(v[r, j]), [int(v[r, m]) for m in members], doc=docs[r])
             check_expected(resp, exp, (form, expr, acc))
+
+
+@pytest.mark.parametrize("form", ["table", "script"])
+def test_groups_without_members_on_device(monkeypatch, form):
+    """a group with no members (evaluation_environment.rs:793-799, "2 > 1" with an empty
+    policies map) next to wide script groups; its verdict and the script groups' causes must equal
+    the oracle's (the combine kernel reads a group's cause words only when it has some)."""
+    monkeypatch.setenv("KW_POISON_VERDICTS", "1")
+    if form == "script":
+        monkeypatch.setenv("KW_GROUP_FORM", "script")
+    else:
+        monkeypatch.delenv("KW_GROUP_FORM", raising=False)
+    doc = {"empty_true": {"policies": {}, "expression": "2 > 1", "message": "m"},
+           "empty_false": {"policies": {}, "expression": "let v = [1]; v.pop(); v.len() > 0", "message": "m"},
+           "scripted": {"policies": MEMBERS, "expression": 'let s = "a"; s.make_upper(); s == "A" && a() && b()',
+                        "message": "m"}}
+    env = K.EvaluationEnvironment(doc, continue_on_errors=True, device=0)
+    oe = O.OracleEnv(doc, continue_on_errors=True)
+    ids = env.policy_ids()
+    docs = [review(VECTORS[k % len(VECTORS)], f"uid-{k}") for k in range(256)]
+    b = K.Batch.from_json(docs).to_device(0)
+    for origin in (K.VALIDATE, K.AUDIT):
+        b.validate(env, ids, origin)
+        got = b.verdicts()
+        want = oe.eval(b.view(), ids, origin)
+        assert np.array_equal(got, want), diff_verdicts(got, want, len(ids), ids)
