@@ -6,7 +6,8 @@
  * safe-labels family (constrained_labels; upstream policy absent),
  * in the dialect DESIGN.md §2 fixes: Rust syntax, matching over Unicode scalar values, Rust's
  * Unicode `\d \w \s`, word boundaries and simple case folding (ASCII ones under `(?-u)`; tables:
- * oracle/unicode_data.h), `\p{..}` / back-references / look-around / the R flag refused.
+ * oracle/unicode_data.h), `\p{..}` General_Category classes (r06; other properties refused),
+ * back-references / look-around / the R flag refused.
  *
  * Independent of the product's automaton compiler (policy-server_amd/csrc/automaton.cpp, a byte-level
  * DFA built by subset construction): this file parses the pattern itself into a tree over code
@@ -172,6 +173,105 @@ static void uni_class(char which, cset *out) {
     for (size_t k = 0; k < n; ++k) cs_push(out, t[2 * k], t[2 * k + 1]);
   }
   cs_canon(out);
+}
+
+/* \p{..} (r06): a General_Category value, matched loosely as regex-syntax's symbolic_name_normalize
+   (ASCII letters lowercased; ' ', '_', '-' and non-ASCII bytes dropped; a leading "is" dropped, but
+   "isc" stays), bare or after gc= / general_category=; Any, ASCII, Assigned; White_Space. 1 = a set
+   in *out, 0 = not supported */
+static void gc_norm(const char *s, size_t n, char *out) {
+  size_t at = 0, k = 0;
+  int is = n >= 2 && (s[0] | 0x20) == 'i' && (s[1] | 0x20) == 's';
+  if (is) k = 2;
+  for (; k < n; ++k) {
+    unsigned char b = (unsigned char)s[k];
+    if (b == ' ' || b == '_' || b == '-' || b >= 0x80) continue;
+    out[at++] = (char)(b >= 'A' && b <= 'Z' ? b + 32 : b);
+  }
+  out[at] = 0;
+  if (is && !strcmp(out, "c")) strcpy(out, "isc");
+}
+static int gc_value_set(const char *v, cset *out) {
+  static const char *const names[][2] = {
+      {"lu", "Lu"}, {"uppercaseletter", "Lu"}, {"ll", "Ll"}, {"lowercaseletter", "Ll"}, {"lt", "Lt"},
+      {"titlecaseletter", "Lt"}, {"lc", "LC"}, {"casedletter", "LC"}, {"l&", "LC"}, {"lm", "Lm"},
+      {"modifierletter", "Lm"}, {"lo", "Lo"}, {"otherletter", "Lo"}, {"l", "L"}, {"letter", "L"},
+      {"mn", "Mn"}, {"nonspacingmark", "Mn"}, {"mc", "Mc"}, {"spacingmark", "Mc"}, {"me", "Me"},
+      {"enclosingmark", "Me"}, {"m", "M"}, {"mark", "M"}, {"combiningmark", "M"}, {"nd", "Nd"},
+      {"decimalnumber", "Nd"}, {"digit", "Nd"}, {"nl", "Nl"}, {"letternumber", "Nl"}, {"no", "No"},
+      {"othernumber", "No"}, {"n", "N"}, {"number", "N"}, {"pc", "Pc"}, {"connectorpunctuation", "Pc"},
+      {"pd", "Pd"}, {"dashpunctuation", "Pd"}, {"ps", "Ps"}, {"openpunctuation", "Ps"}, {"pe", "Pe"},
+      {"closepunctuation", "Pe"}, {"pi", "Pi"}, {"initialpunctuation", "Pi"}, {"pf", "Pf"},
+      {"finalpunctuation", "Pf"}, {"po", "Po"}, {"otherpunctuation", "Po"}, {"p", "P"}, {"punctuation", "P"},
+      {"punct", "P"}, {"sm", "Sm"}, {"mathsymbol", "Sm"}, {"sc", "Sc"}, {"currencysymbol", "Sc"},
+      {"sk", "Sk"}, {"modifiersymbol", "Sk"}, {"so", "So"}, {"othersymbol", "So"}, {"s", "S"},
+      {"symbol", "S"}, {"zs", "Zs"}, {"spaceseparator", "Zs"}, {"zl", "Zl"}, {"lineseparator", "Zl"},
+      {"zp", "Zp"}, {"paragraphseparator", "Zp"}, {"z", "Z"}, {"separator", "Z"}, {"cc", "Cc"},
+      {"control", "Cc"}, {"cntrl", "Cc"}, {"cf", "Cf"}, {"format", "Cf"}, {"cs", "Cs"}, {"surrogate", "Cs"},
+      {"co", "Co"}, {"privateuse", "Co"}, {"cn", "Cn"}, {"unassigned", "Cn"}, {"c", "C"}, {"other", "C"},
+      {"any", "Any"}, {"ascii", "ASCII"}, {"assigned", "Assigned"}};
+  const char *g = NULL;
+  for (size_t k = 0; k < sizeof(names) / sizeof(names[0]); ++k)
+    if (!strcmp(v, names[k][0])) g = names[k][1];
+  if (!g) return 0;
+  memset(out, 0, sizeof(*out));
+  if (!strcmp(g, "Any")) {
+    cs_push(out, 0, 0x10FFFF);
+  } else if (!strcmp(g, "ASCII")) {
+    cs_push(out, 0, 0x7F);
+  } else {
+    /* the runs of every category the value covers; the unassigned code points are the gaps */
+    cset assigned = {0};
+    for (size_t k = 0; k < ORC_UNI_GC_N; ++k) {
+      const char *c = ORC_GC_NAMES[orc_uni_gc[3 * k + 2]];
+      int take;
+      if (!strcmp(g, "LC")) take = !strcmp(c, "Lu") || !strcmp(c, "Ll") || !strcmp(c, "Lt");
+      else if (g[1] == 0) take = c[0] == g[0];
+      else take = !strcmp(c, g);
+      cs_push(&assigned, orc_uni_gc[3 * k], orc_uni_gc[3 * k + 1]);
+      if (take && strcmp(g, "Assigned")) cs_push(out, orc_uni_gc[3 * k], orc_uni_gc[3 * k + 1]);
+    }
+    cs_canon(&assigned);
+    if (!strcmp(g, "Assigned")) {
+      cs_add_all(out, &assigned);
+    } else if (!strcmp(g, "Cn") || !strcmp(g, "C")) {
+      cset gaps = cs_complement(&assigned); /* (surrogates excluded by the complement) */
+      cs_add_all(out, &gaps);
+      cs_free(&gaps);
+    }
+    cs_free(&assigned);
+  }
+  /* scalar values only: intersect with the complement of the empty set */
+  cs_canon(out);
+  cset none = {0}, all = cs_complement(&none);
+  cset v2 = cs_and(out, &all);
+  cs_free(&all);
+  cs_free(out);
+  *out = v2;
+  return 1;
+}
+static int unicode_property(const char *body, size_t n, cset *out, int *negate) {
+  char prop[128], val[128];
+  const char *eq = memchr(body, '=', n);
+  if (!eq) eq = memchr(body, ':', n);
+  if (n >= sizeof(val)) return 0;
+  if (eq) {
+    size_t pn = (size_t)(eq - body);
+    if (pn && body[pn - 1] == '!') {
+      *negate = !*negate;
+      --pn;
+    }
+    gc_norm(body, pn, prop);
+    if (strcmp(prop, "gc") && strcmp(prop, "generalcategory")) return 0;
+    gc_norm(eq + 1, n - (size_t)(eq + 1 - body), val);
+  } else {
+    gc_norm(body, n, val);
+    if (!strcmp(val, "whitespace") || !strcmp(val, "wspace") || !strcmp(val, "space")) {
+      uni_class('s', out);
+      return 1;
+    }
+  }
+  return gc_value_set(val, out);
 }
 
 /* the ASCII classes ([:name:], \d \w \s) */
@@ -384,12 +484,40 @@ static int parse_escape(rparse *P, int in_class, cset *out, int64_t *single, int
   default: have = 0; break;
   }
   if (!have) {
-    if (c == 'p' || c == 'P') return bad(P, "Unicode classes unsupported"), 0;
+    if (c == 'p' || c == 'P') {
+      if (!P->fl.u) return bad(P, "Unicode class with Unicode mode off"), 0;
+      const char *body = P->p + P->at;
+      size_t n;
+      if (peek(P) == '{') {
+        const char *e = memchr(body, '}', P->n - P->at);
+        if (!e) return bad(P, "unclosed Unicode class"), 0;
+        ++body;
+        n = (size_t)(e - body);
+        P->at += n + 2;
+      } else {
+        if (at_end(P)) return bad(P, "incomplete Unicode class"), 0;
+        int64_t l = next_char(P);
+        if (l < 0 || l >= 0x80) return bad(P, "bad Unicode class name"), 0;
+        n = 1;
+      }
+      int negate = c == 'P';
+      if (!unicode_property(body, n, out, &negate)) return bad(P, "Unicode property outside this dialect"), 0;
+      if (P->fl.i) cs_casefold(out); /* regex-syntax folds a Unicode class before negating it */
+      if (negate) {
+        cset neg = cs_complement(out);
+        cs_free(out);
+        *out = neg;
+      }
+      return 1;
+    }
     if (!in_class) {
       int k = -1;
       if (c == 'A') k = A_TEXT_START;
       else if (c == 'z') k = A_TEXT_END;
-      else if (c == 'B') k = A_NOT_WORD;
+      else if (c == 'B') {
+        if (!P->fl.u) return bad(P, "ASCII \\B can match inside a code point"), 0; /* regex-syntax InvalidUtf8 */
+        k = A_NOT_WORD;
+      }
       else if (c == '<') k = A_WORD_START;
       else if (c == '>') k = A_WORD_END;
       else if (c == 'b') {

@@ -370,6 +370,111 @@ CSet cs_uni_space() {
 }
 constexpr uint32_t kAssertUni = 1u << 16;  // an assertion over the kinds of code points
 
+// \p{..} / \P{..} (r06): the General_Category values of regex-syntax, by their short
+// and long names and aliases, matched loosely (UAX44-LM3 as regex-syntax's symbolic_name_normalize:
+// ASCII case, ' ', '_' and '-' ignored, an "is" prefix dropped), bare or as gc= / general_category=
+// (':' and '!=' too); plus Any, ASCII, Assigned and the White_Space property. Script and the other
+// properties are refused by name: this image's Unicode data has no Script property.
+std::string uni_name_normalize(const std::string& x) {
+  size_t start = 0;
+  const bool is = x.size() >= 2 && (x[0] == 'i' || x[0] == 'I') && (x[1] == 's' || x[1] == 'S');
+  if (is) start = 2;
+  std::string o;
+  for (size_t k = start; k < x.size(); ++k) {
+    const unsigned char b = (unsigned char)x[k];
+    if (b == ' ' || b == '_' || b == '-' || b >= 0x80) continue;
+    o.push_back((char)(b >= 'A' && b <= 'Z' ? b + 32 : b));
+  }
+  if (is && o == "c") o = "isc";  // (regex-syntax: ISO_Comment's 'isc', not Other)
+  return o;
+}
+// the set of a General_Category value (normalized name), false when it is none
+bool uni_gencat(const std::string& v, CSet* out) {
+  static const std::map<std::string, std::string> alias = {
+      {"lu", "Lu"}, {"uppercaseletter", "Lu"}, {"ll", "Ll"}, {"lowercaseletter", "Ll"}, {"lt", "Lt"},
+      {"titlecaseletter", "Lt"}, {"lc", "LC"}, {"casedletter", "LC"}, {"l&", "LC"}, {"lm", "Lm"},
+      {"modifierletter", "Lm"}, {"lo", "Lo"}, {"otherletter", "Lo"}, {"l", "L"}, {"letter", "L"},
+      {"mn", "Mn"}, {"nonspacingmark", "Mn"}, {"mc", "Mc"}, {"spacingmark", "Mc"}, {"me", "Me"},
+      {"enclosingmark", "Me"}, {"m", "M"}, {"mark", "M"}, {"combiningmark", "M"}, {"nd", "Nd"},
+      {"decimalnumber", "Nd"}, {"digit", "Nd"}, {"nl", "Nl"}, {"letternumber", "Nl"}, {"no", "No"},
+      {"othernumber", "No"}, {"n", "N"}, {"number", "N"}, {"pc", "Pc"}, {"connectorpunctuation", "Pc"},
+      {"pd", "Pd"}, {"dashpunctuation", "Pd"}, {"ps", "Ps"}, {"openpunctuation", "Ps"}, {"pe", "Pe"},
+      {"closepunctuation", "Pe"}, {"pi", "Pi"}, {"initialpunctuation", "Pi"}, {"pf", "Pf"},
+      {"finalpunctuation", "Pf"}, {"po", "Po"}, {"otherpunctuation", "Po"}, {"p", "P"}, {"punctuation", "P"},
+      {"punct", "P"}, {"sm", "Sm"}, {"mathsymbol", "Sm"}, {"sc", "Sc"}, {"currencysymbol", "Sc"}, {"sk", "Sk"},
+      {"modifiersymbol", "Sk"}, {"so", "So"}, {"othersymbol", "So"}, {"s", "S"}, {"symbol", "S"},
+      {"zs", "Zs"}, {"spaceseparator", "Zs"}, {"zl", "Zl"}, {"lineseparator", "Zl"}, {"zp", "Zp"},
+      {"paragraphseparator", "Zp"}, {"z", "Z"}, {"separator", "Z"}, {"cc", "Cc"}, {"control", "Cc"},
+      {"cntrl", "Cc"}, {"cf", "Cf"}, {"format", "Cf"}, {"cs", "Cs"}, {"surrogate", "Cs"}, {"co", "Co"},
+      {"privateuse", "Co"}, {"cn", "Cn"}, {"unassigned", "Cn"}, {"c", "C"}, {"other", "C"},
+      {"any", "Any"}, {"ascii", "ASCII"}, {"assigned", "Assigned"}};
+  auto it = alias.find(v);
+  if (it == alias.end()) return false;
+  const std::string& g = it->second;
+  if (g == "Any") {
+    *out = {{0, 0x10FFFF}};
+  } else if (g == "ASCII") {
+    *out = {{0, 0x7F}};
+  } else {
+    // a value names the categories whose two-letter names it prefixes (L: Lu Ll Lt Lm Lo; LC: Lu Ll
+    // Lt); Cn and Assigned are the code points outside / inside the runs
+    auto member = [&](const char* name) {
+      if (g == "LC") return !strcmp(name, "Lu") || !strcmp(name, "Ll") || !strcmp(name, "Lt");
+      if (g.size() == 1) return name[0] == g[0];
+      return g == name;
+    };
+    CSet assigned, hit;
+    for (uint32_t k = 0; k < kUniGcN; ++k) {
+      assigned.push_back({kUniGc[k].lo, kUniGc[k].hi});
+      if (g != "Assigned" && member(kUniGcNames[kUniGc[k].gc])) hit.push_back({kUniGc[k].lo, kUniGc[k].hi});
+    }
+    assigned = cs_union(assigned, {});
+    if (g == "Assigned") hit = assigned;
+    else if (g == "Cn" || g == "C") hit = cs_union(hit, cs_neg(assigned));
+    else hit = cs_union(hit, {});
+    *out = hit;
+  }
+  CSet noncs;  // (surrogates are no scalar values: never matched)
+  for (const CRange& r : *out) {
+    if (r.hi < 0xD800 || r.lo > 0xDFFF) noncs.push_back(r);
+    else {
+      if (r.lo < 0xD800) noncs.push_back({r.lo, 0xD7FF});
+      if (r.hi > 0xDFFF) noncs.push_back({0xE000, r.hi});
+    }
+  }
+  *out = noncs;
+  return true;
+}
+bool uni_property(const std::string& body, CSet* out, bool* negate, std::string* err) {
+  size_t eq = body.find('=');
+  const size_t colon = body.find(':');
+  if (eq == std::string::npos) eq = colon;
+  std::string value = body;
+  if (eq != std::string::npos) {
+    std::string prop = body.substr(0, eq);
+    if (!prop.empty() && prop.back() == '!') {  // name!=value
+      prop.pop_back();
+      *negate = !*negate;
+    }
+    value = body.substr(eq + 1);
+    const std::string np = uni_name_normalize(prop);
+    if (np != "gc" && np != "generalcategory") {
+      *err = std::string("unsupported by this engine: the Unicode property \\p{") + body + "}" +
+             (np == "sc" || np == "script" || np == "scx" || np == "scriptextensions" ? " (scripts)" : "");
+      return false;
+    }
+  }
+  const std::string nv = uni_name_normalize(value);
+  if (eq == std::string::npos && (nv == "whitespace" || nv == "wspace" || nv == "space")) {
+    *out = cs_uni_space();
+    return true;
+  }
+  if (uni_gencat(nv, out)) return true;
+  *err = std::string("unsupported by this engine: the Unicode property \\p{") + body +
+         "} (only General_Category values and White_Space)";
+  return false;
+}
+
 // ASCII classes: [:name:] and the \d \w \s escapes
 bool ascii_class(const std::string& name, CSet* s) {
   static const std::map<std::string, CSet> k = {
@@ -645,16 +750,48 @@ struct RParser {
         return 1;
       }
       case 'p':
-      case 'P':
-        err = "Unicode property classes (\\p, \\P) are not supported";
-        return 0;
+      case 'P': {
+        if (!f.u) {
+          err = "Unicode classes are not allowed with Unicode mode off";
+          return 0;
+        }
+        std::string body;
+        if (!eof() && p[i] == '{') {
+          const size_t e = p.find('}', i);
+          if (e == std::string::npos) {
+            err = "unclosed Unicode class";
+            return 0;
+          }
+          body = p.substr(i + 1, e - i - 1);
+          i = e + 1;
+        } else {
+          const int64_t n = eof() ? -1 : getc_();
+          if (n < 0) {
+            err = "incomplete Unicode class";
+            return 0;
+          }
+          body = std::string(1, n < 0x80 ? (char)n : '?');  // (a one-letter name is ASCII)
+        }
+        bool negate = c == 'P';
+        if (!uni_property(body, cs, &negate, &err)) return 0;
+        // regex-syntax folds a Unicode class under (?i) before negating it
+        if (f.i) cs_fold(cs, true);
+        if (negate) *cs = cs_neg(*cs);
+        return 1;
+      }
       default: break;
     }
     if (!in_class) {
       switch (c) {
         case 'A': *mask = kind_mask([](uint32_t p_, uint32_t) { return p_ == BK_EDGE; }); return uni_word(c), 2;
         case 'z': *mask = kind_mask([](uint32_t, uint32_t n) { return n == BK_EDGE; }); return uni_word(c), 2;
-        case 'B': *mask = kind_mask([](uint32_t p_, uint32_t n) { return kw_word(p_) == kw_word(n); }); return uni_word(c), 2;
+        case 'B':
+          if (!f.u) {  // (regex-syntax: an ASCII \B can match inside a code point, InvalidUtf8)
+            err = "pattern can match invalid UTF-8 (Unicode mode is off)";
+            return 0;
+          }
+          *mask = kind_mask([](uint32_t p_, uint32_t n) { return kw_word(p_) == kw_word(n); });
+          return uni_word(c), 2;
         case '<': *mask = kind_mask([](uint32_t p_, uint32_t n) { return !kw_word(p_) && kw_word(n); }); return uni_word(c), 2;
         case '>': *mask = kind_mask([](uint32_t p_, uint32_t n) { return kw_word(p_) && !kw_word(n); }); return uni_word(c), 2;
         case 'b': {
@@ -1404,6 +1541,12 @@ bool compile_dfa(const std::vector<Pattern>& pats, Dfa* out, std::string* err, u
     for (unsigned c = 0; c < 256; ++c)
       if (byte_kind(c) == BK_WORD) s.set(c);
     refine.push_back(s);
+    // (?-u) word assertions could hold inside a UTF-8 sequence (lead and continuation bytes are
+    // both non-word), where Rust never reports an empty match: a position whose next byte is a
+    // continuation byte passes no assertion (NL / edge anchors never hold there anyway)
+    BSet cont;
+    for (unsigned c = 0x80; c < 0xC0; ++c) cont.set(c);
+    refine.push_back(cont);
   }
   std::array<uint16_t, 256> cl{};
   uint32_t ncl = 1;
@@ -1423,7 +1566,11 @@ bool compile_dfa(const std::vector<Pattern>& pats, Dfa* out, std::string* err, u
   std::vector<unsigned> rep(ncl);
   for (int b = 255; b >= 0; --b) rep[cl[(unsigned)b]] = (unsigned)b;
   std::vector<uint32_t> kind_of(ncl);
-  for (uint32_t c = 0; c < ncl; ++c) kind_of[c] = canon(byte_kind(rep[c]));
+  std::vector<int> next_of(ncl);  // the kind a class shows as the next byte (-1: no assertion holds)
+  for (uint32_t c = 0; c < ncl; ++c) {
+    kind_of[c] = canon(byte_kind(rep[c]));
+    next_of[c] = need_word && rep[c] >= 0x80 && rep[c] < 0xC0 ? -1 : (int)kind_of[c];
+  }
   // per NFA set: membership per class
   std::vector<std::vector<uint8_t>> set_has(nfa.sets.size(), std::vector<uint8_t>(ncl));
   for (size_t s = 0; s < nfa.sets.size(); ++s)
@@ -1480,7 +1627,7 @@ bool compile_dfa(const std::vector<Pattern>& pats, Dfa* out, std::string* err, u
     for (uint32_t c = 0; c < ncl; ++c) {
       const uint32_t k = kind_of[c];
       std::vector<uint32_t> cur = dstates[d];
-      closure(nfa, &cur, (int)dprev[d], (int)k, &mark, ++stamp);
+      closure(nfa, &cur, (int)dprev[d], next_of[c], &mark, ++stamp);
       std::vector<uint32_t> nx;
       ++stamp;
       for (uint32_t x : cur)

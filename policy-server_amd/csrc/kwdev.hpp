@@ -324,11 +324,11 @@ inline KW_HD bool nfa_run(const uint8_t* rec, const uint8_t* s, uint32_t n, uint
     const uint32_t q = i >= n ? NK_EDGE : nfa_uni_kind(nfa_cp_at(s, i, n), uword, R.uni_n);
     return 1u << (p * 4u + q);
   };
-  // the closure of `node` at a position between byte kinds (p, q) into list L; ubit: the
-  // position's code-point kinds as a mask bit (assertions flagged kNfaUni test that one)
-  auto add = [&](uint32_t node, uint32_t p, uint32_t q, uint32_t ubit, uint32_t* L, uint32_t* cnt) {
+  // the closure of `node` at a position into list L; bit: the position's byte kinds (p, q) as a mask
+  // bit, ubit: its code-point kinds (assertions flagged kNfaUni test that one); both 0 inside a
+  // UTF-8 sequence, where Rust never reports an empty match
+  auto add = [&](uint32_t node, uint32_t bit, uint32_t ubit, uint32_t* L, uint32_t* cnt) {
     const uint32_t g = *gen;
-    const uint32_t bit = 1u << (p * 4u + q);
     uint32_t sp = 0;
     stack[sp++] = node;
     while (sp) {
@@ -346,20 +346,21 @@ inline KW_HD bool nfa_run(const uint8_t* rec, const uint8_t* s, uint32_t n, uint
     }
   };
   ++*gen;
-  add(R.start, NK_EDGE, n ? nfa_kind(s[0]) : NK_EDGE, uni_bit(0), cur, &ncur);
+  add(R.start, 1u << (NK_EDGE * 4u + (n ? nfa_kind(s[0]) : NK_EDGE)), uni_bit(0), cur, &ncur);
   for (uint32_t i = 0; i < n; ++i) {
     if (hit && R.search) return true;
     hit = false;
     const uint32_t c = s[i], p = nfa_kind(c), q = i + 1 < n ? nfa_kind(s[i + 1]) : NK_EDGE;
     ++*gen;
     nnxt = 0;
-    const uint32_t ub = uni_bit(i + 1);
+    const bool inside = i + 1 < n && (s[i + 1] & 0xC0u) == 0x80u;
+    const uint32_t ub = inside ? 0u : uni_bit(i + 1), bb = inside ? 0u : 1u << (p * 4u + q);
     for (uint32_t t = 0; t < ncur; ++t) {
       const uint32_t x = cur[t];
       for (uint32_t e = first[x], e1 = first[x + 1]; e < e1; ++e) {
         if ((edge[2 * e] & 0xffu) != NE_BYTE) continue;
         const uint32_t set = edge[2 * e] >> 8;
-        if ((sets[set * 8u + (c >> 5)] >> (c & 31u)) & 1u) add(edge[2 * e + 1], p, q, ub, nxt, &nnxt);
+        if ((sets[set * 8u + (c >> 5)] >> (c & 31u)) & 1u) add(edge[2 * e + 1], bb, ub, nxt, &nnxt);
       }
     }
     uint32_t* t = cur;

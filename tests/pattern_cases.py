@@ -3,7 +3,8 @@
 classes with set operations, verbose mode) and patterns whose DFA exceeds the state budget (the
 label regex `a[a-z]{14}b`, the image glob `*a?????????????????`, a registry and a tag glob of the
 same shape), which must evaluate as NFA elements instead of failing the environment, plus refused
-constructs (\\p{L}, look-around) that are init errors on both sides."""
+constructs (a Script property \\p{Greek}, look-around) that are init errors on both sides, and
+(r06) \\p{..} General_Category classes and the no-assertion-inside-a-code-point rule."""
 import json
 
 MOD = "registry://ghcr.io/kubewarden/policies/"
@@ -29,6 +30,11 @@ UNICODE_REGEXES = {
     "kelvin": "(?i)^k$",
     "uniword": "é\\b",                            # a Unicode word boundary: an NFA element
     "asciiword": "^(?-u:\\w)+$",
+    # r06: General_Category classes and \B between the bytes of one code point
+    "gcletter": "^\\p{Lu}[\\p{Ll}\\p{Nd}]*$",
+    "gcmixed": "^[\\p{L}--\\p{Lu}]+\\P{L}?$",
+    "gcsymbol": "\\p{Sc}|\\p{gc=So}",
+    "notboundary": "a\\Bb|\\B",
 }
 
 
@@ -42,7 +48,7 @@ def policies():
         "labels-blowup": {"module": MOD + "safe-labels:v0.1.14",
                           "settings": {"constrained_labels": {"app": "a[a-z]{14}b"}}},
         "labels-refused": {"module": MOD + "safe-labels:v0.1.14",
-                           "settings": {"constrained_labels": {"app": "\\p{L}+"}}},
+                           "settings": {"constrained_labels": {"app": "\\p{Greek}+"}}},
         "labels-lookaround": {"module": MOD + "safe-labels:v0.1.14",
                               "settings": {"constrained_labels": {"tier": "(?<=a)b"}}},
         "images-blowup": {"module": MOD + "trusted-repos-policy:v0.1.12",
@@ -79,6 +85,10 @@ VALUES = {
     "kelvin": ["\u212a", "K", "k", "x"],
     "uniword": ["é x", "éa", "é", "aé-"],
     "asciiword": ["é", "ab"],
+    "gcletter": ["Abc1", "Éé٣", "abc", "A", "AB", "Aǅ"],
+    "gcmixed": ["abc", "ǅa1", "aB", "é€", "ab12"],
+    "gcsymbol": ["€", "©", "$", "x", "a+b"],
+    "notboundary": ["a\u2003b", "\u2003", "ab", "é", "a b"],
 }
 
 IMAGES = ["nginx", "ghcr.io/kubewarden/policy-server:v1.2.3", "quay.io/aaaaaaaaaaaaaaaaaaaaaaaaa:latest",

@@ -16,6 +16,8 @@ ALPHA characters Python puts in it:
   [...] with &&, --, ~~, nesting  the ALPHA characters of the set (each item's members asked of
                                  Python's engine), (?!) when empty
   \\d \\w \\s \\D \\W \\S           \\d \\w \\s \\D \\W \\S (Unicode)
+  \\p{gc} \\P{gc} \\pX             the ALPHA characters of those categories (unicodedata), folded under
+                                 (?i) before a \\P negates them
   [:name:]                       its ASCII members (Rust's ASCII classes stay ASCII)
   ^ $ \\A \\z  (?m)^ (?m)$        \\A \\Z \\A \\Z (?<![^\\n]) (?![^\\n])
   \\b \\< \\> \\b{start-half} \\b{end-half}   \\b \\b(?=\\w) \\b(?<=\\w) (?<!\\w) (?!\\w) (Unicode \\w)
@@ -41,6 +43,23 @@ NAMED = {"alnum": [(48, 57), (65, 90), (97, 122)], "alpha": [(65, 90), (97, 122)
          "lower": [(97, 122)], "upper": [(65, 90)], "space": [(9, 13), (32, 32)], "word": [(48, 57), (65, 90),
          (95, 95), (97, 122)], "xdigit": [(48, 57), (65, 70), (97, 102)],
          "punct": [(33, 47), (58, 64), (91, 96), (123, 126)], "blank": [(9, 9), (32, 32)], "ascii": [(0, 127)]}
+
+
+# \p{..} General_Category values (r06): (Rust spelling, categories) — short and long names, aliases,
+# loose spellings (case, ' ', '_', '-', an "is" prefix) and gc= forms; Python has no \p, so the
+# rendering is the set of ALPHA characters whose unicodedata.category is one of the categories
+GC_VALUES = [("L", "Lu Ll Lt Lm Lo"), ("Letter", "Lu Ll Lt Lm Lo"), ("Lu", "Lu"), ("Uppercase_Letter", "Lu"),
+             ("lowercase letter", "Ll"), ("Ll", "Ll"), ("Lt", "Lt"), ("LC", "Lu Ll Lt"), ("Cased-Letter", "Lu Ll Lt"),
+             ("Lo", "Lo"), ("isLm", "Lm"), ("N", "Nd Nl No"), ("Nd", "Nd"), ("digit", "Nd"), ("Nl", "Nl"),
+             ("No", "No"), ("P", "Pc Pd Ps Pe Pi Pf Po"), ("punct", "Pc Pd Ps Pe Pi Pf Po"), ("Pc", "Pc"),
+             ("Pd", "Pd"), ("Po", "Po"), ("S", "Sm Sc Sk So"), ("So", "So"), ("Z", "Zs Zl Zp"), ("Zs", "Zs"),
+             ("space_separator", "Zs"), ("C", "Cc Cf Cs Co Cn"), ("Cc", "Cc"), ("M", "Mn Mc Me"),
+             ("gc=Lu", "Lu"), ("General_Category=Nd", "Nd"), ("gc:L", "Lu Ll Lt Lm Lo")]
+
+
+def gc_members(cats):
+    import unicodedata
+    return frozenset(c for c in ALPHA if unicodedata.category(c) in cats.split())
 
 
 def py_members(py_item):
@@ -130,6 +149,8 @@ class Gen:
         if r < 0.7:
             e = self.r.choice("dDwWsS")
             return "\\" + e, py_members("\\" + e)
+        if r < 0.76:  # \p{..} / \P{..} / \pX: regex-syntax folds before it negates
+            return self.gc_class(f)
         if r < 0.82:
             nm = self.r.choice(sorted(NAMED))
             s = fold(named(nm)) if f.i else named(nm)
@@ -140,6 +161,20 @@ class Gen:
             return self.cls(f, depth + 1)
         ch = self.r.choice(ALPHA)
         return self.cls_char_rust(ch, f), frozenset([ch])
+
+    def gc_class(self, f):
+        name, cats = self.r.choice(GC_VALUES)
+        s = gc_members(cats)
+        if f.i:
+            s = fold(s)
+        negate = self.r.random() < 0.3
+        if len(name) == 1 and self.r.random() < 0.5:
+            txt = ("\\P" if negate else "\\p") + name
+        else:
+            txt = ("\\P{" if negate else "\\p{") + name + "}"
+        if f.x and " " in txt:
+            txt = txt.replace(" ", "_")
+        return txt, neg(s) if negate else s
 
     def cls(self, f, depth=0):
         """(rust text '[...]', set)"""
@@ -186,9 +221,12 @@ class Gen:
         if r < 0.6:
             t, s = self.cls(f)
             return t, py_class(s)
-        if r < 0.68:
+        if r < 0.64:
             e = self.r.choice("dDwWsS")
             return "\\" + e, "\\" + e
+        if r < 0.68:
+            t, s = self.gc_class(f)
+            return t, py_class(s)
         if r < 0.8:
             k = self.r.choice(["^", "$", "\\A", "\\z", "\\b", "\\B", "\\<", "\\>", "\\b{start}", "\\b{end}",
                                "\\b{start-half}", "\\b{end-half}"])

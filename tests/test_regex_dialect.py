@@ -8,7 +8,8 @@ matching over code points), three ways:
 * Python's `re` WITHOUT re.ASCII (its own Unicode tables and folding) on a rendering of the same
   tree (tests/regex_gen.py), for random patterns over the characters where Rust and Python agree;
   and a hand table of the constructs VERDICT r03 / r04 named (`(?:)`, `(?i)`, `\\b`, `\\A`/`\\z`,
-  Unicode classes and folding, `(?-u)`, `\\p` refused) with Rust's answers written down.
+  Unicode classes and folding, `(?-u)`, `\\p{..}` General_Category classes, Script and other
+  properties refused) with Rust's answers written down.
 
 All three must agree on every (pattern, subject). -1 = the pattern is refused (an init error)."""
 import re
@@ -50,8 +51,33 @@ TABLE = [
     (r"é", "é", 1), (r"(?i)\x41", "a", 1), (r"a{2}{3}", "aaaaaa", 1), (r"a{,3}", "a", -1), (r"a{3,1}", "a", -1),
     (r"a{1001}", "a" * 1001, 1), (r"\-\ \#\&\~", "- #&~", 1), (r"a*?b", "aab", 1), (r"(|a)b", "b", 1), (r"()", "", 1),
     (r"", "", 1), (r"a|", "x", 1),
+    # \p{..} General_Category classes (r06): Rust's regex answers, by hand
+    (r"\p{L}", "a", 1), (r"\pL", "a", 1), (r"\pL", "1", 0), (r"^\p{Lu}+$", "ÀB", 1), (r"^\p{Lu}+$", "Ab", 0),
+    (r"(?i)^\p{Lu}+$", "Ab", 1), (r"(?i)^\P{Lu}$", "a", 0), (r"^\P{Lu}$", "a", 1), (r"^\P{L}$", "é", 0),
+    (r"^\p{Ll}$", "ß", 1), (r"^\p{Lt}$", "ǅ", 1), (r"^\p{LC}$", "ǅ", 1), (r"^\p{Lo}$", "中", 1),
+    (r"^\p{Lm}$", "ʰ", 1), (r"^\p{Nd}$", "٣", 1), (r"^\p{Nl}$", "ⅻ", 1), (r"^\p{No}$", "²", 1),
+    (r"^\p{N}+$", "1²ⅻ", 1), (r"^\p{Mn}$", "\u0301", 1), (r"^\p{M}$", "a", 0), (r"^\p{Pc}$", "_", 1),
+    (r"^\p{Pd}$", "-", 1), (r"^\p{Ps}\p{Pe}$", "()", 1), (r"^\p{Pi}\p{Pf}$", "«»", 1), (r"^\p{Po}$", "!", 1),
+    (r"^\p{Sm}$", "+", 1), (r"^\p{Sc}$", "€", 1), (r"^\p{Sk}$", "^", 1), (r"^\p{So}$", "©", 1),
+    (r"^\p{Zs}$", "\u00a0", 1), (r"^\p{Zl}$", "\u2028", 1), (r"^\p{Zp}$", "\u2029", 1), (r"^\p{Cc}$", "\x1f", 1),
+    (r"^\p{Cf}$", "\u200d", 1), (r"^\p{Co}$", "\ue000", 1), (r"^\p{Cn}$", "\U000e0080", 1), (r"^\p{Cs}$", "a", 0),
+    (r"^\p{C}$", "\x00", 1), (r"^\p{Z}$", " ", 1), (r"^\p{S}$", "a", 0), (r"^\p{P}$", "a", 0),
+    (r"^\p{Uppercase_Letter}$", "A", 1), (r"^\p{uppercaseletter}$", "A", 1), (r"^\p{ Upper-Case_letter }$", "A", 1),
+    (r"^\p{isLu}$", "A", 1), (r"^\p{gc=Lu}$", "A", 1), (r"^\p{General_Category:Lu}$", "A", 1),
+    (r"^\p{gc!=Lu}$", "A", 0), (r"^\P{gc!=Lu}$", "A", 1), (r"^\p{digit}$", "٣", 1), (r"^\p{punct}$", "!", 1),
+    (r"^\p{cntrl}$", "\x7f", 1), (r"^\p{Combining_Mark}$", "\u0301", 1), (r"^\p{Any}$", "\U0010FFFD", 1),
+    (r"^\p{ASCII}$", "é", 0), (r"^\p{Assigned}$", "\U000e0080", 0), (r"^\p{White_Space}$", "\u3000", 1),
+    (r"^[\p{L}\d]+$", "a1é", 1), (r"^[\p{L}&&\p{Ll}]$", "A", 0), (r"^[\p{L}--\p{Lu}]$", "a", 1),
+    (r"^[^\p{L}]$", "1", 1), (r"^[\P{L}]$", "1", 1), (r"\pN\pL", "1a", 1),
+    # no assertion holds inside a UTF-8 sequence (r06: the product's \B matched between the bytes of
+    # U+2003; Rust never reports an empty match that splits a code point)
+    (r"\B", "a\u2003b", 0), (r"\B", "é", 0), (r"\B", "\u2003", 1), (r"a\b{end-half}", "a\u00a0", 1),
+    (r"\b{start-half}b", "\u2003b", 1), (r"(?-u)\b{start-half}\b{end-half}", "\u2003", 1),
+    (r"(?-u)\B", "ab", -1), (r"(?-u:\B)a", "a", -1),
     # refused by both (as by Rust's parser, or by this dialect: DESIGN.md §2)
-    (r"\p{L}", "a", -1), (r"\pL", "a", -1), (r"\P{Greek}", "a", -1), (r"(?-u).", "a", -1), (r"(?-u)[^a]", "b", -1),
+    (r"\P{Greek}", "a", -1), (r"\p{Greek}", "a", -1), (r"\p{sc=Latin}", "a", -1), (r"\p{Alphabetic}", "a", -1),
+    (r"\p{IsC}", "\x01", -1), (r"\p{L", "a", -1), (r"(?-u)\pL", "a", -1), (r"\p", "a", -1),
+    (r"(?-u).", "a", -1), (r"(?-u)[^a]", "b", -1),
     (r"(?-u)\W", "b", -1), (r"(?-u)\xFF", "b", -1), (r"(?-u)a\w", "ab", 1), (r"(?-u)é", "é", 1),
     (r"a\Z", "a", -1), (r"(?R)a", "a", -1), (r"\1", "a", -1), (r"(a)\1", "aa", -1), (r"(?=a)", "a", -1),
     (r"(?<=a)b", "ab", -1), (r"(?!a)", "b", -1), (r"(a", "a", -1), (r"a)", "a", -1), (r"\y", "y", -1),
