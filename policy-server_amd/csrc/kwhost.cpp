@@ -29,9 +29,15 @@
 //                                             (src/metrics.rs; the reference exports them over OTLP)
 //   unknown route                        404  (empty)
 //
-// Usage: kwhost --policies policies.yml [--addr 127.0.0.1] [--port 3000] [--device 0]
+// Usage: kwhost --policies policies.yml [--addr 127.0.0.1] [--port 3000] [--device 0 | --devices 0,1,..]
 //   [--max-batch 512] [--max-wait-us 200] [--workers 4] [--max-body-bytes 2097152]
 //   [--always-accept-admission-reviews-on-namespace NS] [--continue-on-errors] [--no-device]
+// --devices (r06) shards the serving front over several GPUs: the environment is compiled once, on
+// the first device, and its blob deserialized onto every other one (the same path as the batch
+// shards' RCCL broadcast, kw_env_serialize / kw_env_deserialize: each copy re-derives its host
+// records and byte-compares the tables); pipeline worker k runs on devices[k % n] with that device's
+// environment, so the batcher's idle-worker hand-off balances the devices. A device may be listed
+// twice (two environments, one GPU: the multi-device path on a one-GPU box).
 // --policies is the reference's policies.yml (read with the native YAML reader, config.rs:449-453;
 // a file whose first character is '{' is read as JSON). --no-device serves the HTTP layer without
 // device tables: every evaluation then fails with 500 (used by the CPU test suite for routing and
@@ -67,12 +73,15 @@ struct Opts {
   int port = 3000, device = 0, max_batch = 512, max_wait_us = 200, workers = 4;
   size_t max_body = 2u << 20;  // axum DefaultBodyLimit (2 MiB)
   bool continue_on_errors = false, no_device = false;
+  std::vector<int> devices;  // --devices (default: {device})
   int stats_ms = 0;  // --stats-ms N: a JSON line of cumulative stage times on stderr every N ms
 };
 
 // Where a worker's time goes (--stats-ms): cumulative nanoseconds per stage over all batches.
 struct StageStats {
+  static constexpr size_t kMaxDev = 16;
   std::atomic<uint64_t> batches{0}, rows{0}, wait_ns{0}, flatten_ns{0}, gpu_ns{0}, format_ns{0}, handoff_ns{0};
+  std::atomic<uint64_t> device_batches[kMaxDev] = {};  // batches per entry of --devices
 };
 static uint64_t ns_since(std::chrono::steady_clock::time_point t) {
   return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t).count();
@@ -150,7 +159,7 @@ Reply evaluation_error(int code, const std::string& msg) {  // handle_evaluation
 
 class Server {
  public:
-  Server(const Opts& o, kw_env* env) : o_(o), env_(env) {}
+  Server(const Opts& o, std::vector<kw_env*> envs) : o_(o), envs_(std::move(envs)) {}
   size_t max_body() const { return o_.max_body; }
 
   void submit(Job* j) {
@@ -189,10 +198,13 @@ class Server {
     }
   }
 
-  // A pipeline worker: its own stream; one batch at a time.
-  void worker() {
+  // A pipeline worker: its own device (o_.devices[k % n]) and stream; one batch at a time.
+  void worker(int k) {
+    const size_t d = (size_t)k % o_.devices.size();
+    const int device = o_.devices[d];
+    kw_env* env = envs_[d];
     void* stream = nullptr;
-    if (!o_.no_device && kw_stream_create(o_.device, &stream) != KW_OK) stream = nullptr;
+    if (!o_.no_device && kw_stream_create(device, &stream) != KW_OK) stream = nullptr;
     for (;;) {
       std::vector<Job*> jobs;
       {
@@ -207,12 +219,13 @@ class Server {
         stats_.wait_ns += w;  // arrival -> a worker holds the batch (summed over requests)
         stats_.batches += 1;
         stats_.rows += jobs.size();
+        stats_.device_batches[d % StageStats::kMaxDev] += 1;
       }
       // partition first: a job belongs to its connection thread again once it is answered
       std::vector<Job*> part[3];
       for (Job* j : jobs) part[j->route].push_back(j);
       for (Route r : {R_VALIDATE, R_AUDIT, R_RAW})
-        if (!part[r].empty()) run(r, part[r], stream);
+        if (!part[r].empty()) run(r, part[r], env, device, stream);
       {
         std::lock_guard<std::mutex> g(wm_);
         ++idle_;
@@ -223,14 +236,14 @@ class Server {
 
   void start() {
     idle_ = std::max(1, o_.workers);
-    for (int k = 0; k < std::max(1, o_.workers); ++k) std::thread(&Server::worker, this).detach();
+    for (int k = 0; k < std::max(1, o_.workers); ++k) std::thread(&Server::worker, this, k).detach();
     std::thread(&Server::batcher, this).detach();
   }
 
  private:
   // One kw_validate_rows pass over the jobs of one route. A group's members run as extra rows of
   // the same document (their verdicts give the causes of a rejected group).
-  void run(Route route, std::vector<Job*> jobs, void* stream) {
+  void run(Route route, std::vector<Job*> jobs, kw_env* env_, int device, void* stream) {
     const int kind = route == R_RAW ? KW_DOC_RAW_REVIEW : KW_DOC_ADMISSION_REVIEW;
     const int origin = route == R_AUDIT ? KW_ORIGIN_AUDIT : KW_ORIGIN_VALIDATE;
     // 1. the extractor: bodies that are not a request of this route's type are answered first
@@ -302,7 +315,7 @@ class Server {
     stats_.flatten_ns += ns_since(t_flat);
     const auto t_gpu = std::chrono::steady_clock::now();
     if (rc == KW_OK && o_.no_device) rc = KW_E_DEVICE;
-    if (rc == KW_OK) rc = stream ? kw_batch_to_device_async(b, o_.device, stream) : kw_batch_to_device(b, o_.device);
+    if (rc == KW_OK) rc = stream ? kw_batch_to_device_async(b, device, stream) : kw_batch_to_device(b, device);
     if (rc == KW_OK) rc = kw_validate_rows(env_, b, row_policy.data(), origin, stream);
     std::vector<uint32_t> v(row_policy.size());
     if (rc == KW_OK) rc = kw_batch_verdicts(b, v.data(), v.size());
@@ -323,7 +336,7 @@ class Server {
         mv.push_back(v[r.first]);
         mlat.push_back((uint64_t)std::chrono::duration_cast<std::chrono::milliseconds>(now - r.job->t0).count());
       }
-      kw_metrics_record(metrics_, env_, b, mrow.data(), mpol.data(), mv.data(), mlat.data(), mrow.size(), origin);
+      kw_metrics_record(metrics_, envs_[0], b, mrow.data(), mpol.data(), mv.data(), mlat.data(), mrow.size(), origin);
     }
     // 4. service epilogue + response envelope (AdmissionReviewResponse / RawReviewResponse)
     stats_.gpu_ns += ns_since(t_gpu);
@@ -367,18 +380,22 @@ class Server {
     for (;;) {
       std::this_thread::sleep_for(std::chrono::milliseconds(o_.stats_ms));
       const uint64_t rows = stats_.rows, batches = stats_.batches;
+      std::string per_dev;
+      for (size_t d = 0; d < o_.devices.size() && d < StageStats::kMaxDev; ++d)
+        per_dev += (d ? ", " : "") + std::to_string((unsigned long long)stats_.device_batches[d]);
       fprintf(stderr,
               "{\"kwhost_stats\": {\"batches\": %llu, \"rows\": %llu, \"mean_batch\": %.1f, \"wait_s_per_request\": %.3g, "
-              "\"worker_s\": {\"flatten\": %.4f, \"gpu_upload_validate_readback\": %.4f, \"format\": %.4f, \"handoff\": %.4f}}}\n",
+              "\"worker_s\": {\"flatten\": %.4f, \"gpu_upload_validate_readback\": %.4f, \"format\": %.4f, \"handoff\": %.4f}, "
+              "\"device_batches\": [%s]}}\n",
               (unsigned long long)batches, (unsigned long long)rows, batches ? (double)rows / batches : 0.0,
               rows ? stats_.wait_ns / 1e9 / rows : 0.0, stats_.flatten_ns / 1e9, stats_.gpu_ns / 1e9, stats_.format_ns / 1e9,
-              stats_.handoff_ns / 1e9);
+              stats_.handoff_ns / 1e9, per_dev.c_str());
       fflush(stderr);
     }
   }
  private:
   const Opts& o_;
-  kw_env* env_;
+  std::vector<kw_env*> envs_;  // per entry of o_.devices (same policies, same indices)
  public:
   kw_metrics* metrics_ = nullptr;  // GET /metrics (owned by main)
  private:
@@ -598,7 +615,7 @@ void serve(Server* srv, int fd) {
 
 int usage() {
   fprintf(stderr,
-          "usage: kwhost --policies policies.yml [--addr A] [--port P] [--device D] [--max-batch N]\n"
+          "usage: kwhost --policies policies.yml [--addr A] [--port P] [--device D | --devices D0,D1,..] [--max-batch N]\n"
           "              [--max-wait-us T] [--workers W] [--max-body-bytes B] [--stats-ms N]\n"
           "              [--always-accept-admission-reviews-on-namespace NS] [--continue-on-errors] [--no-device]\n");
   return 2;
@@ -616,6 +633,14 @@ int main(int argc, char** argv) {
     else if (a == "--addr" && (v = val())) o.addr = v;
     else if (a == "--port" && (v = val())) o.port = atoi(v);
     else if (a == "--device" && (v = val())) o.device = atoi(v);
+    else if (a == "--devices" && (v = val())) {
+      o.devices.clear();
+      for (const char* c = v; *c;) {
+        o.devices.push_back(atoi(c));
+        while (*c && *c != ',') ++c;
+        if (*c == ',') ++c;
+      }
+    }
     else if (a == "--max-batch" && (v = val())) o.max_batch = std::max(1, atoi(v));
     else if (a == "--max-wait-us" && (v = val())) o.max_wait_us = std::max(0, atoi(v));
     else if (a == "--workers" && (v = val())) o.workers = std::max(1, atoi(v));
@@ -627,6 +652,9 @@ int main(int argc, char** argv) {
     else return usage();
   }
   if (o.policies.empty()) return usage();
+  if (o.devices.empty()) o.devices.push_back(o.device);
+  if (o.devices.size() > StageStats::kMaxDev) return usage();
+  o.device = o.devices[0];
   std::ifstream f(o.policies, std::ios::binary);
   if (!f) {
     fprintf(stderr, "kwhost: cannot read %s\n", o.policies.c_str());
@@ -647,6 +675,27 @@ int main(int argc, char** argv) {
     fprintf(stderr, "kwhost: %s (code %d)\n", err, rc);
     return 1;
   }
+  // the other devices' environments: the first one's blob, deserialized there
+  std::vector<kw_env*> envs = {env};
+  if (o.devices.size() > 1 && !o.no_device) {
+    size_t need = 0;
+    kw_env_serialize(env, nullptr, 0, &need);
+    std::vector<char> blob(need);
+    if (int rc = kw_env_serialize(env, blob.data(), blob.size(), &need)) {
+      fprintf(stderr, "kwhost: cannot serialize the environment (code %d)\n", rc);
+      return 1;
+    }
+    for (size_t d = 1; d < o.devices.size(); ++d) {
+      kw_env* e = nullptr;
+      if (int rc = kw_env_deserialize(blob.data(), blob.size(), o.devices[d], &e, err, sizeof(err))) {
+        fprintf(stderr, "kwhost: device %d: %s (code %d)\n", o.devices[d], err, rc);
+        return 1;
+      }
+      envs.push_back(e);
+    }
+  } else {
+    while (envs.size() < o.devices.size()) envs.push_back(env);
+  }
   const int ls = socket(AF_INET, SOCK_STREAM, 0);
   int one = 1;
   setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
@@ -660,11 +709,12 @@ int main(int argc, char** argv) {
     return 1;
   }
   signal(SIGPIPE, SIG_IGN);
-  Server srv(o, env);
+  Server srv(o, envs);
   srv.metrics_ = kw_metrics_create();
   srv.start();
   if (o.stats_ms > 0) std::thread(&Server::stats_loop, &srv).detach();
-  fprintf(stderr, "kwhost: %d policies, listening on %s:%d\n", kw_env_policy_count(env), o.addr.c_str(), o.port);
+  fprintf(stderr, "kwhost: %d policies on %zu device pipeline(s), listening on %s:%d\n", kw_env_policy_count(env),
+          o.devices.size(), o.addr.c_str(), o.port);
   for (;;) {
     const int fd = accept(ls, nullptr, nullptr);
     if (fd < 0) continue;

@@ -28,8 +28,12 @@ def _expect(oe, soa, origin, r, j, raw, doc):
     return 200, {"kind": "AdmissionReview", "apiVersion": "admission.k8s.io/v1", "response": resp}
 
 
-@pytest.mark.parametrize("name,scfg", [("parity", 0), ("c4_64", 4)])
-def test_concurrent_routes_match_oracle(name, scfg):
+@pytest.mark.parametrize("name,scfg,pipes", [("parity", 0, 1), ("c4_64", 4, 1), ("c4_64", 4, 2)],
+                         ids=["parity", "c4_64", "c4_64-two-pipelines"])
+def test_concurrent_routes_match_oracle(name, scfg, pipes):
+    """pipes = 2 (r06): `--devices 0,0` — the serving front sharded over two device
+    pipelines, the second environment deserialized from the first one's blob (kw_env_serialize /
+    kw_env_deserialize, as for the RCCL broadcast), both serving batches."""
     doc = config(name)
     oe = O.OracleEnv(doc, continue_on_errors=True, always_accept_namespace=NS)
     ids = [p["id"] for p in oe.pol]
@@ -45,7 +49,8 @@ def test_concurrent_routes_match_oracle(name, scfg):
         calls.append(("validate", r, j, _expect(oe, soa, K.VALIDATE, r, j, False, docs[r])))
         calls.append(("audit", r, j, _expect(oe, soa, K.AUDIT, r, j, False, docs[r])))
         calls.append(("validate_raw", r, j, _expect(oe, raw_soa, K.VALIDATE, r, j, True, docs[r])))
-    with Host(name, extra=["--device", "0", "--max-wait-us", "300"]) as h:
+    dev = ["--device", "0"] if pipes == 1 else ["--devices", ",".join(["0"] * pipes), "--stats-ms", "100"]
+    with Host(name, extra=dev + ["--max-wait-us", "300"]) as h:
         def one(c):
             route, r, j, want = c
             # member ids ("group/member") travel percent-encoded, as axum's Path extractor decodes them
@@ -54,6 +59,12 @@ def test_concurrent_routes_match_oracle(name, scfg):
         with ThreadPoolExecutor(max_workers=24) as ex:
             results = list(ex.map(one, calls))
         st, _, metrics = h.request("GET", "/metrics")
+        if pipes > 1:
+            import time
+            time.sleep(0.3)  # one more stats line after the last batch
+            stats = [json.loads(line)["kwhost_stats"] for line in h.stderr().splitlines() if "kwhost_stats" in line]
+            per_dev = stats[-1]["device_batches"]
+            assert len(per_dev) == pipes and all(b > 0 for b in per_dev), per_dev
     assert st == 200
     # every evaluated call (200) is one kubewarden_policy_evaluations_total data point (service.rs:40-150)
     total = sum(int(line.rsplit(" ", 1)[1]) for line in metrics.decode().splitlines()
