@@ -12,3 +12,9 @@ for r in ${ROWS_LIST:-125000 250000}; do
     done
   done
 done
+# phase clocks of one pass at 125k and 1M (the timing instantiation: table staging per workgroup,
+# cycles per tile, workgroup start spread)
+for r in 125000 1000000; do
+  KW_TILE_DEBUG=512 timeout -k 10 200 python bench.py --rows $r --steps 2 --warmup 1 --no-cpu-baseline --no-host-modes > /dev/null 2> gpurun_out/ph_$r.err || exit $?
+  echo "[phases] rows=$r"; grep -E "^\[kw (phase|start|seg)\]" gpurun_out/ph_$r.err | tail -n 3
+done
