@@ -482,6 +482,9 @@ __device__ inline void glds_x4(const u32x4* src, u32x4* dst, uint32_t n, uint32_
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + i),
                                      (__attribute__((address_space(3))) void*)(dst + (i - lane)), 16, 0, 0);
 }
+#ifndef KW_DESC_EARLY
+#define KW_DESC_EARLY 1
+#endif
 __device__ inline void copy_x4(const uint8_t* src, uint8_t* dst, uint32_t bytes, uint32_t tid) {
   const auto* s = gp((const u32x4*)src);
   u32x4* d = (u32x4*)dst;
@@ -557,6 +560,58 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
     }
   };
 
+  const uint32_t npol = a.npol;
+  // Tile schedule (capi.cpp sched_dynamic picks one per launch). Workgroup b runs on XCD b % 8 and
+  // serves that XCD's contiguous range of tiles. Static: the range strided by the XCD's
+  // workgroups. Dynamic (a.sched): the tiles one at a time from the XCD's own
+  // counter (a 128-B line each, so no counter is shared between XCDs); the atomic for the next tile
+  // is issued when the current tile starts and its result is read only at the tile's end, so its
+  // latency hides behind the tile. The XCD's last workgroup to finish zeroes the counter again.
+  // The schedule runs two tiles ahead: while a tile is evaluated, the index of the next one is
+  // already known, so its descriptor is copied into LDS under this tile's staging (the next tile's
+  // P0 and its L2 prefetch read it there, with no dependent global load), and the counter fetch
+  // issued now names the tile after next.
+  const bool dyn = a.sched != nullptr;
+  const uint32_t nx = min(8u, gridDim.x);
+  const uint32_t xcd = blockIdx.x % nx;
+  // both schedules serve the XCD's contiguous range (adjacent tiles share the cache lines at their
+  // boundaries, so they stay in one L2)
+  const uint64_t t_lo = a.ndesc * xcd / nx, t_hi = a.ndesc * (xcd + 1) / nx;
+  uint32_t* cnt = dyn ? a.sched + xcd * 32u : nullptr;
+  uint32_t* l_nx = (uint32_t*)(lds + t.o_nx);  // the tile after next, double-buffered
+  TileDesc* l_desc = (TileDesc*)(lds + t.o_desc);
+  // descriptor `i` into LDS slot `s`: 32 lanes of wave 0, one dword each (LDS-DMA, counted by vmcnt)
+  auto fetch_desc = [&](uint64_t i, uint32_t s) {
+    if (tid < 32u)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)((const uint32_t*)(desc + i) + tid),
+                                       (__attribute__((address_space(3))) void*)(l_desc + s), 4, 0, 0);
+  };
+  auto sfield = [](const uint32_t& f) -> uint32_t { return __builtin_amdgcn_readfirstlane(f); };
+  // P1 / P2 item blocks (64 items, one wave each, costliest segments first). DYNB (the instantiations
+  // without image code: C4, C5): a wave's first block is its own, each further one comes from the
+  // phase's LDS counter (l_nx[2] / l_nx[3]), so a wave that drew cheap blocks takes more instead of
+  // waiting at the barrier for one that drew costly ones (C5 -8 %, C4 flat). The image
+  // instantiations keep blocks strided by the waves (C2 +1.6 %, C3 +3.6 % with the counters;
+  // profiles/r05_dyn_blocks_ab.txt).
+  constexpr bool DYNB = !IMG;
+  auto next_block = [&](uint32_t k) -> uint32_t {
+    uint32_t v = 0;
+    if (lane == 0u) v = atomicAdd(&l_nx[2u + k], 1u);
+    return (kSlotThreads >> 6) + __builtin_amdgcn_readfirstlane(v);
+  };
+  // Dynamic: a workgroup's first two tiles are static (the XCD's range in workgroup order), so a
+  // launch does not open with every workgroup's counter fetches queued on one L2 line; the counter
+  // hands out the range from its third tile-set on (value v = tile dbase + v). r05: the opening
+  // fetches cost a 1M C4 pass 2.4 % and a 64k-request shard 57 % (profiles/r05_sched_ab.txt).
+  const uint32_t wpx = (gridDim.x - xcd + nx - 1u) / nx;  // workgroups b < gridDim.x with b % nx == xcd
+  const uint64_t dbase = t_lo + 2ull * wpx;
+  uint64_t tile = t_lo + blockIdx.x / nx, next = tile + wpx;
+  // the first tile's descriptor goes out with the table staging below (r06: one memory round trip
+  // fewer before the first tile, which a small shard's ~2 tiles a workgroup feel; KW_DESC_EARLY=0
+  // restores the separate fetch and barrier for A/B)
+#if KW_DESC_EARLY
+  if (tile < t_hi) fetch_desc(tile, 0);
+#endif
   // ---- once per workgroup: the column classifiers and the chunks' staged record prefixes
   if (LDST) {
     for (uint32_t s = 0; s < t.nstage; ++s) copy_x4(a.blob + t.stage_blob[s], lds + t.stage_lds[s], t.stage_bytes[s], tid);
@@ -625,54 +680,10 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
   const uint32_t nim = il.n(), nlv = t.nlv;
   const uint32_t need = t.need;
 
-  const uint32_t npol = a.npol;
-  // Tile schedule (capi.cpp sched_dynamic picks one per launch). Workgroup b runs on XCD b % 8 and
-  // serves that XCD's contiguous range of tiles. Static: the range strided by the XCD's
-  // workgroups. Dynamic (a.sched): the tiles one at a time from the XCD's own
-  // counter (a 128-B line each, so no counter is shared between XCDs); the atomic for the next tile
-  // is issued when the current tile starts and its result is read only at the tile's end, so its
-  // latency hides behind the tile. The XCD's last workgroup to finish zeroes the counter again.
-  // The schedule runs two tiles ahead: while a tile is evaluated, the index of the next one is
-  // already known, so its descriptor is copied into LDS under this tile's staging (the next tile's
-  // P0 and its L2 prefetch read it there, with no dependent global load), and the counter fetch
-  // issued now names the tile after next.
-  const bool dyn = a.sched != nullptr;
-  const uint32_t nx = min(8u, gridDim.x);
-  const uint32_t xcd = blockIdx.x % nx;
-  // both schedules serve the XCD's contiguous range (adjacent tiles share the cache lines at their
-  // boundaries, so they stay in one L2)
-  const uint64_t t_lo = a.ndesc * xcd / nx, t_hi = a.ndesc * (xcd + 1) / nx;
-  uint32_t* cnt = dyn ? a.sched + xcd * 32u : nullptr;
-  uint32_t* l_nx = (uint32_t*)(lds + t.o_nx);  // the tile after next, double-buffered
-  TileDesc* l_desc = (TileDesc*)(lds + t.o_desc);
-  // descriptor `i` into LDS slot `s`: 32 lanes of wave 0, one dword each (LDS-DMA, counted by vmcnt)
-  auto fetch_desc = [&](uint64_t i, uint32_t s) {
-    if (tid < 32u)
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)((const uint32_t*)(desc + i) + tid),
-                                       (__attribute__((address_space(3))) void*)(l_desc + s), 4, 0, 0);
-  };
-  auto sfield = [](const uint32_t& f) -> uint32_t { return __builtin_amdgcn_readfirstlane(f); };
-  // P1 / P2 item blocks (64 items, one wave each, costliest segments first). DYNB (the instantiations
-  // without image code: C4, C5): a wave's first block is its own, each further one comes from the
-  // phase's LDS counter (l_nx[2] / l_nx[3]), so a wave that drew cheap blocks takes more instead of
-  // waiting at the barrier for one that drew costly ones (C5 -8 %, C4 flat). The image
-  // instantiations keep blocks strided by the waves (C2 +1.6 %, C3 +3.6 % with the counters;
-  // profiles/r05_dyn_blocks_ab.txt).
-  constexpr bool DYNB = !IMG;
-  auto next_block = [&](uint32_t k) -> uint32_t {
-    uint32_t v = 0;
-    if (lane == 0u) v = atomicAdd(&l_nx[2u + k], 1u);
-    return (kSlotThreads >> 6) + __builtin_amdgcn_readfirstlane(v);
-  };
-  // Dynamic: a workgroup's first two tiles are static (the XCD's range in workgroup order), so a
-  // launch does not open with every workgroup's counter fetches queued on one L2 line; the counter
-  // hands out the range from its third tile-set on (value v = tile dbase + v). r05: the opening
-  // fetches cost a 1M C4 pass 2.4 % and a 64k-request shard 57 % (profiles/r05_sched_ab.txt).
-  const uint32_t wpx = (gridDim.x - xcd + nx - 1u) / nx;  // workgroups b < gridDim.x with b % nx == xcd
-  const uint64_t dbase = t_lo + 2ull * wpx;
-  uint64_t tile = t_lo + blockIdx.x / nx, next = tile + wpx;
+#if !KW_DESC_EARLY
   if (tile < t_hi) fetch_desc(tile, 0);
   __syncthreads();
+#endif
   mark(4);
   for (uint32_t it = 0; tile < t_hi; ++it) {
     const uint32_t cur = it & 1u;
