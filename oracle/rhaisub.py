@@ -403,8 +403,11 @@ class _Parser:
                 if k != "id":
                     self.err(f"Syntax error: expecting a method name after '.', found {self.near()}")
                 self.p += 1
-                if not self.at_op("("):
-                    self.err(UNSUP + f"property access (.{m})")
+                if not self.at_op("("):  # property getters of the packages: len, is_empty, bytes
+                    if m not in ("len", "is_empty", "bytes"):
+                        self.err(UNSUP + f"property access (.{m})")
+                    e = ("call", m, [e], True)
+                    continue
                 self.p += 1
                 args = [e] + self.arglist()
                 if m in _ALWAYS_MUT and e[0] == "index":

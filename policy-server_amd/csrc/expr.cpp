@@ -694,13 +694,19 @@ struct Parser {
         if (peek().t != Tk::Ident) return fail("Syntax error: expecting a method name after '.', found " + near());
         const std::string m = peek().s;
         ++i;
-        if (!punct("(")) return unsupported("property access (." + m + ")");
-        ++i;
         auto c = std::make_unique<Node>();
         c->k = Node::Call;
         c->name = m;
         c->flag = true;
         c->kids.push_back(std::move(e));
+        if (!punct("(")) {
+          // the packages' property getters (len, is_empty: strings and arrays; bytes: strings) read
+          // as the method call; any other property needs object maps or custom types
+          if (m != "len" && m != "is_empty" && m != "bytes") return unsupported("property access (." + m + ")");
+          e = std::move(c);
+          continue;
+        }
+        ++i;
         if (!args(&c->kids)) return nullptr;
         if (always_mutates(m) && c->kids[0]->k == Node::Index)
           return unsupported("mutating an element in place (x[i]." + m + "(..))");

@@ -146,6 +146,8 @@ VALID = [
      '"a,b,c".split_rev(",") == ["c", "b", "a"] && "a,b,c".split_rev(",", 2) == ["c", "a,b"] && '
      '"ab".split("") == ["", "a", "b", ""] && "aaa".split_rev("aa") == ["", "a"] && a()', [("a", True)]),
     ('"h\u00e9llo".bytes() == 6 && "h\u00e9llo".len() == 5 && a()', [("a", True)]),
+    ('"ab".len == 2 && [1, 2, 3].len == 3 && "".is_empty && ![1].is_empty && "\u00e9".bytes == 2 && a()',
+     [("a", True)]),  # the packages' property getters
     ('let s = "ab"; s.append(1); s.append(true); s.append(()); let t = "banana"; t.remove("an"); '
      'let u = "xyz"; u.truncate(2); let v = "q"; v.clear(); s == "ab1true" && t == "ba" && u == "xy" && v == "" && a()',
      [("a", True)]),
@@ -230,7 +232,7 @@ INVALID = [
     ("let r = 1..3; a()", "unsupported by this engine: range values outside `for` and `in`"),
     ("let r = range(1, 3); a()", "unsupported by this engine: range values outside `for` and `in`"),
     ("for i in range(0, 9, 2) {} a()", "unsupported by this engine: range() with a step"),
-    ("\"ab\".len && a()", "unsupported by this engine: property access (.len)"),
+    ("\"ab\".size == 2 && a()", "unsupported by this engine: property access (.size)"),
     ("throw \"x\"; a()", "unsupported by this engine: throw"),
     ("print(1); a()", "unsupported by this engine: print"),
     ("a() && [1, 2].to_string() == \"[1, 2]\"", "unsupported by this engine: converting an array to a string"),
