@@ -77,3 +77,36 @@ def test_groups_without_members_on_device(monkeypatch, form):
         got = b.verdicts()
         want = oe.eval(b.view(), ids, origin)
         assert np.array_equal(got, want), diff_verdicts(got, want, len(ids), ids)
+
+
+# KW_SCRIPT_SEEDS widens the sweep for a deep run (r06: profiles/r06_script_fuzz_deep.log)
+@pytest.mark.parametrize("seed", range(int(__import__("os").environ.get("KW_SCRIPT_SEEDS", "3"))))
+def test_random_scripts_on_device(monkeypatch, seed):
+    """tests/fuzz.py's script generator (r06: with the standard-package functions and `&mut` method
+    calls) in the typed-bytecode form run by wide_groups_kernel: 60 random groups per seed, every
+    member vector, verdict words and formatted responses against the oracle's interpreter."""
+    import random
+
+    from fuzz import _script
+    monkeypatch.setenv("KW_POISON_VERDICTS", "1")
+    monkeypatch.setenv("KW_GROUP_FORM", "script")
+    rng = random.Random(8000 + seed)
+    rows = [(_script(rng, ["a", "b", "c"]), []) for _ in range(60)]
+    doc = groups_doc(rows)
+    env = K.EvaluationEnvironment(doc, continue_on_errors=True, device=0)
+    oe = O.OracleEnv(doc, continue_on_errors=True)
+    ids = env.policy_ids()
+    docs = [review(VECTORS[k % len(VECTORS)], f"uid-{k}") for k in range(len(VECTORS) * 16)]
+    b = K.Batch.from_json(docs).to_device(0)
+    for origin in (K.VALIDATE, K.AUDIT):
+        b.validate(env, ids, origin)
+        got = b.verdicts()
+        want = oe.eval(b.view(), ids, origin)
+        assert np.array_equal(got, want), diff_verdicts(got, want, len(ids), ids)
+    v = got.reshape(len(docs), len(ids))
+    for k in range(len(rows)):
+        j = ids.index(f"g{k}")
+        members = env.group_members(j)
+        for r in range(len(VECTORS)):
+            resp = b.format_response(env, r, j, int(v[r, j]), [int(v[r, m]) for m in members], doc=docs[r])
+            assert resp == oe.response_doc(b.view(), r, j, K.AUDIT, doc=docs[r]), (rows[k][0], VECTORS[r])
