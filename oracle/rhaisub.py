@@ -62,9 +62,9 @@ _REFUSED = {"import": "modules (import)", "export": "modules (export)", "as": "m
             "curry": "function pointers", "eval": "eval", "print": "print", "debug": "debug",
             "is_def_var": "is_def_var", "is_def_fn": "is_def_fn", "is_shared": "shared values", "static": "static",
             "exit": "exit"}
-_BAD_OPS = [("#{", "object maps"), ("**", "the ** operator"), ("<<", "bit shifts"), (">>", "bit shifts"),
+_BAD_OPS = [("#{", "object maps"),
             ("::", "modules and namespaces"), ("?.", "the ?. operator"), ("?[", "the ?[ operator")]
-_OPS = ["..=", "=>", "??", "..", "||", "&&", "==", "!=", "<=", ">=", "+=", "-=", "*=", "/=", "%=", "|=", "&=", "^="] + \
+_OPS = ["..=", "**=", "<<=", ">>=", "=>", "??", "..", "**", "<<", ">>", "||", "&&", "==", "!=", "<=", ">=", "+=", "-=", "*=", "/=", "%=", "|=", "&=", "^="] + \
     list("<>+-*/%!|&^(){}[];=,.")
 _IDENT = re.compile(r"[A-Za-z_][A-Za-z0-9_]*")
 _NUMBODY = re.compile(r"[A-Za-z0-9_]*")
@@ -184,10 +184,11 @@ def tokenize(s):
 
 # ----------------------------------------------------------------------------- parser
 # binding powers (rhai 1.x): || | ^ 30, && & 60, == != 90, in !in 110, < <= > >= 130, ?? 135,
-# .. ..= 140, + - 150, * / % 180
+# .. ..= 140, + - 150, * / % 180, ** 190 (right-associative), << >> 210
 _BP = {"||": 30, "|": 30, "^": 30, "&&": 60, "&": 60, "==": 90, "!=": 90, "!in": 110, "<": 130, "<=": 130, ">": 130,
-       ">=": 130, "??": 135, "..": 140, "..=": 140, "+": 150, "-": 150, "*": 180, "/": 180, "%": 180}
-_ASSIGN = ["=", "+=", "-=", "*=", "/=", "%=", "|=", "&=", "^="]
+       ">=": 130, "??": 135, "..": 140, "..=": 140, "+": 150, "-": 150, "*": 180, "/": 180, "%": 180, "**": 190,
+       "<<": 210, ">>": 210}
+_ASSIGN = ["=", "+=", "-=", "*=", "/=", "%=", "|=", "&=", "^=", "**=", "<<=", ">>="]
 _BLOCKLIKE = {"if", "switch", "while", "loop", "for", "block"}
 
 
@@ -336,7 +337,7 @@ class _Parser:
             if self.at_op(a):
                 self.p += 1
                 rhs = self.expr(0)
-                op = "" if a == "=" else a[0]
+                op = "" if a == "=" else a[:-1]
                 if e[0] == "var":
                     node, name = ("assign", e[1], op, rhs), e[1]
                 elif e[0] == "index" and e[1][0] == "var":
@@ -366,7 +367,7 @@ class _Parser:
                 return left
             op = self.peek()[1]
             self.p += 1
-            right = self.expr(bp + 1)
+            right = self.expr(bp if op == "**" else bp + 1)
             if op in ("in", "!in"):
                 left = ("in", op == "!in", left, right)
             elif op == "??":
@@ -751,6 +752,35 @@ def type_name(v):
 
 def _kind(v):
     return type_name(v)
+
+
+def _int_pow_shift(op, x, y):
+    """rhai's checked ** << >> on i64 (ArithmeticPackage power / shift_left / shift_right): a negative
+    shift shifts the other way; 64 or more bits is an error, as is an exponent outside [0, u32::MAX]
+    or a power that overflows i64; >> is arithmetic."""
+    if op == "**":
+        if y > 0xFFFFFFFF:
+            raise ExprError(f"Integer raised to too large an index: {x} ** {y}")
+        if y < 0:
+            raise ExprError(f"Integer raised to a negative index: {x} ** {y}")
+        r = x ** y if abs(x) < 2 or y < 64 else None  # (|x| >= 2 overflows i64 within 63 steps)
+        if r is None or not I64_MIN <= r <= I64_MAX:
+            raise ExprError(f"Exponential overflow: {x} ** {y}")
+        return r
+    left = op == "<<"
+    name = "Left-shift" if left else "Right-shift"
+    if y > 0xFFFFFFFF:
+        raise ExprError(f"{name} by too many bits: {x} {op} {y}")
+    if y < 0:
+        if y == I64_MIN:
+            raise ExprError(f"{name} by too many bits: {x} {op} {y}")
+        return _int_pow_shift(">>" if left else "<<", x, -y)
+    if y >= 64:
+        raise ExprError(f"{name} by too many bits: {x} {op} {y}")
+    if left:
+        r = (x << y) & U64_MAX
+        return r - (1 << 64) if r > I64_MAX else r
+    return x >> y
 
 
 def _offset_len(n, start, ln):
@@ -1249,6 +1279,8 @@ class Run:
         if not (_is_int(a) and _is_int(b)):
             self.nf(op, a, b)
         text = f"{a} {op} {b}"
+        if op in ("**", "<<", ">>"):
+            return _int_pow_shift(op, a, b)
         if op in ("/", "%"):
             if b == 0:
                 raise ExprError(f"Division by zero: {text}")

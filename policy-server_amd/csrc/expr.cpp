@@ -271,12 +271,11 @@ struct Lexer {
           toks.push_back(t);
           continue;
         }
-        static const char* bad[][2] = {{"#{", "object maps"}, {"**", "the ** operator"}, {"<<", "bit shifts"},
-                                       {">>", "bit shifts"},  {"::", "modules and namespaces"},
+        static const char* bad[][2] = {{"#{", "object maps"}, {"::", "modules and namespaces"},
                                        {"?.", "the ?. operator"}, {"?[", "the ?[ operator"}};
         for (auto& b : bad)
           if (s.compare(k, std::char_traits<char>::length(b[0]), b[0]) == 0) return unsupported(b[1]);
-        static const char* ops[] = {"..=", "=>", "??", "..", "||", "&&", "==", "!=", "<=", ">=", "+=", "-=", "*=", "/=",
+        static const char* ops[] = {"..=", "**=", "<<=", ">>=", "=>", "??", "..", "**", "<<", ">>", "||", "&&", "==", "!=", "<=", ">=", "+=", "-=", "*=", "/=",
                                     "%=",  "|=", "&=", "^=", "<",  ">",  "+",  "-",  "*",  "/",  "%",  "!",  "|",  "&",
                                     "^",   "(",  ")",  "{",  "}",  "[",  "]",  ";",  "=",  ",",  "."};
         bool ok = false;
@@ -585,14 +584,14 @@ struct Parser {
       return primary();
     P e = expr();
     if (!e) return nullptr;
-    static const char* aops[] = {"=", "+=", "-=", "*=", "/=", "%=", "|=", "&=", "^="};
+    static const char* aops[] = {"=", "+=", "-=", "*=", "/=", "%=", "|=", "&=", "^=", "**=", "<<=", ">>="};
     for (const char* ao : aops) {
       if (!punct(ao)) continue;
       ++i;
       P rhs = expr();
       if (!rhs) return nullptr;
       auto a = std::make_unique<Node>();
-      a->op = std::string(ao) == "=" ? "" : std::string(ao).substr(0, 1);
+      a->op = std::string(ao) == "=" ? "" : std::string(ao).substr(0, std::char_traits<char>::length(ao) - 1);
       if (e->k == Node::Var) {
         a->k = Node::Assign;
         a->name = e->name;
@@ -614,7 +613,8 @@ struct Parser {
   }
 
   // precedence climbing (rhai 1.x): || | ^ (30), && & (60), == != (90), in !in (110),
-  // < <= > >= (130), ?? (135), .. ..= (140), + - (150), * / % (180)
+  // < <= > >= (130), ?? (135), .. ..= (140), + - (150), * / % (180), ** (190, right-associative),
+  // << >> (210)
   static int prec(const Token& t) {
     if (t.t == Tk::Ident) return t.s == "in" ? 110 : -1;
     if (t.t != Tk::Punct) return -1;
@@ -628,6 +628,8 @@ struct Parser {
     if (o == ".." || o == "..=") return 140;
     if (o == "+" || o == "-") return 150;
     if (o == "*" || o == "/" || o == "%") return 180;
+    if (o == "**") return 190;
+    if (o == "<<" || o == ">>") return 210;
     return -1;
   }
   P expr(int min_prec = 0) {
@@ -637,7 +639,7 @@ struct Parser {
       if (p < 0 || p < min_prec) break;
       const std::string o = peek().s;
       ++i;
-      P r = expr(p + 1);
+      P r = expr(o == "**" ? p : p + 1);
       if (!r) return nullptr;
       auto n = std::make_unique<Node>();
       if (o == "in" || o == "!in") {
@@ -1137,6 +1139,34 @@ std::string str_case(const std::string& s, bool upper) {
   }
   return utf8_of(o);
 }
+// rhai's checked ** << >> on i64: a negative shift shifts the other way; 64 or more bits, an exponent
+// outside [0, u32::MAX] or a power past i64 is an error; >> is arithmetic (slots.hpp int_pow_shift
+// is the device form)
+bool int_pow_shift(const std::string& op, int64_t x, int64_t y, int64_t* r, std::string* err) {
+  const std::string ex = std::to_string(x) + " " + op + " " + std::to_string(y);
+  if (op == "**") {
+    if (y > (int64_t)0xFFFFFFFFll) return *err = "Integer raised to too large an index: " + ex, false;
+    if (y < 0) return *err = "Integer raised to a negative index: " + ex, false;
+    long long v = 1;
+    for (int64_t k = 0; k < y; ++k) {
+      if (__builtin_mul_overflow(v, (long long)x, &v)) return *err = "Exponential overflow: " + ex, false;
+      if (v == 0 || ((v == 1 || v == -1) && (x == 1 || x == -1))) {  // 0, 1, -1: the rest is a parity
+        if (v != 0 && x == -1) v = (y % 2 == 0) ? 1 : -1;
+        break;
+      }
+    }
+    *r = v;
+    return true;
+  }
+  const bool left = op == "<<";
+  const std::string name = left ? "Left-shift" : "Right-shift";
+  if (y > (int64_t)0xFFFFFFFFll || y == INT64_MIN) return *err = name + " by too many bits: " + ex, false;
+  if (y < 0) return int_pow_shift(left ? ">>" : "<<", x, -y, r, err);
+  if (y >= 64) return *err = name + " by too many bits: " + ex, false;
+  *r = left ? (int64_t)((uint64_t)x << y) : (x >> y);
+  return true;
+}
+
 // rhai's calc_offset_len (start counts from the end when negative, clamped; len clamped)
 void offset_len(size_t n, int64_t start, int64_t len, size_t* st, size_t* ln) {
   size_t s0;
@@ -1901,6 +1931,13 @@ struct Interp {
     }
     if (a.t != VT::Int || b.t != VT::Int) return nf(shown, {&a, &b});
     const std::string ex = std::to_string(a.i) + " " + op + " " + std::to_string(b.i);
+    if (op == "**" || op == "<<" || op == ">>") {  // rhai's checked power / shifts (ArithmeticPackage)
+      int64_t r;
+      std::string e;
+      if (!int_pow_shift(op, a.i, b.i, &r, &e)) return fail(e);
+      *out = vint(r);
+      return OK;
+    }
     long long r = 0;
     if (op == "+") {
       if (__builtin_add_overflow(a.i, b.i, &r)) return fail("Addition overflow: " + ex);
@@ -2451,6 +2488,9 @@ struct ScriptEmitter {
     if (assign && op == "+") return SB_ADDA;
     for (uint8_t k = 0; k < 14; ++k)
       if (op == ops[k]) return k;
+    if (op == "**") return SB_POW;
+    if (op == "<<") return SB_SHL;
+    if (op == ">>") return SB_SHR;
     return 0;
   }
   bool uses_chars = false;  // a function that reads character properties (the char table)

@@ -112,7 +112,7 @@ enum SOp : uint8_t { S_UNIT = 0, S_BOOL, S_INT, S_STR, S_LOAD, S_STORE, S_CALL, 
 // | ^ & == != < <= > >= + - * / %, then the compound assignments that differ from their operator:
 // `+=` (an array pushes / appends; otherwise `+`) and the `x op= y` forms whose errors name `op=`
 enum SBin : uint8_t { SB_OR = 0, SB_XOR, SB_AND, SB_EQ, SB_NE, SB_LT, SB_LE, SB_GT, SB_GE, SB_ADD, SB_SUB, SB_MUL, SB_DIV,
-                      SB_MOD, SB_ADDA };
+                      SB_MOD, SB_ADDA, SB_POW, SB_SHL, SB_SHR };  // (r06: ** << >>)
 // Built-in functions (method or function-call style; `x in y` is contains(y, x)). r06: rhai's
 // standard packages over the engine's values (i64, string, array), one id per
 // (name, arity); the argument types are dispatched at run time as rhai's overloads are.

@@ -1785,6 +1785,32 @@ KW_HD inline int run_script_prog(const uint8_t* prog, uint64_t* scratch, Ok ok, 
         if (ta != sv::INT || tb != sv::INT) return 2;
         const int64_t a = (int64_t)va, b = (int64_t)vb;
         long long r = 0;
+        if (b_op == SB_POW || b_op == SB_SHL || b_op == SB_SHR) {  // rhai's checked ** << >> (expr.cpp)
+          int64_t y = b;
+          uint32_t o = b_op;
+          if (o != SB_POW && y < 0) {  // a negative shift shifts the other way
+            if (y == INT64_MIN) return 2;
+            y = -y;
+            o = o == SB_SHL ? SB_SHR : SB_SHL;
+          }
+          if (o == SB_POW) {
+            if (y < 0 || y > (int64_t)0xFFFFFFFFll) return 2;
+            long long v = 1;
+            for (int64_t k = 0; k < y; ++k) {
+              if (__builtin_mul_overflow(v, (long long)a, &v)) return 2;
+              if (v == 0 || ((v == 1 || v == -1) && (a == 1 || a == -1))) {
+                if (v != 0 && a == -1) v = (y % 2 == 0) ? 1 : -1;
+                break;
+              }
+            }
+            r = v;
+          } else {
+            if (y >= 64) return 2;
+            r = o == SB_SHL ? (long long)((uint64_t)a << y) : (long long)(a >> y);
+          }
+          set(ia, sv::INT, (uint64_t)r);
+          break;
+        }
         if (b_op == SB_ADD || b_op == SB_ADDA) {
           if (__builtin_add_overflow(a, b, &r)) return 2;
         } else if (b_op == SB_SUB) {

@@ -219,6 +219,8 @@ def _script(rng, names):
             if q < 0.2:
                 return f"{rng.choice(['abs', 'sign'])}({i(d - 1)})"
             if q < 0.35:
+                if rng.random() < 0.4:  # ** << >> (now and then out of range: an error on that path)
+                    return f"({i(d - 1)} {rng.choice(['**', '<<', '>>'])} {rng.choice(['0', '1', '2', '3', '-1', '63', '64'])})"
                 return f"{rng.choice(['max', 'min'])}({i(d - 1)}, {i(d - 1)})"
             if q < 0.5:
                 return f"{t(d - 1)}.{rng.choice(['len()', 'bytes()'])}"

@@ -118,6 +118,17 @@ VALID = [
     ('if a() { true } else { parse_int("1", 40) == 1 }', [("", ("error", "Invalid radix: '40'"))]),
     ("if a() { true } else { abs(-9223372036854775807 - 1) == 0 }", [("", ("error", "Negation overflow"))]),
     ('if a() { true } else { abs("x") == 1 }', [("", ("error", "Function not found: abs (string)"))]),
+    # r06: ** (right-associative, binds tighter than *), << >> (tighter still), their compound forms
+    ("2 ** 3 == 8 && 2 ** 3 ** 2 == 512 && -2 ** 2 == 4 && 2 * 3 ** 2 == 18 && 0 ** 0 == 1 && (-1) ** 7 == -1 && a()",
+     [("a", True)]),
+    ("1 << 2 == 4 && -8 >> 1 == -4 && 1 << 63 == -9223372036854775807 - 1 && 5 << -1 == 2 && -8 >> -2 == -32 && "
+     "1 << 2 + 1 == 5 && 2 ** 1 << 2 == 16 && a()", [("a", True)]),  # (<< binds tighter than + and **)
+    ("let x = 3; x **= 2; x <<= 1; x >>= 2; x == 4 && a()", [("a", True)]),
+    ("if a() { true } else { 2 ** 63 == 0 }", [("", ("error", "Exponential overflow: 2 ** 63"))]),
+    ("if a() { true } else { 2 ** -1 == 0 }", [("", ("error", "Integer raised to a negative index: 2 ** -1"))]),
+    ("if a() { true } else { 1 << 64 == 0 }", [("", ("error", "Left-shift by too many bits: 1 << 64"))]),
+    ("if a() { true } else { 1 >> -70 == 0 }", [("", ("error", "Left-shift by too many bits: 1 << 70"))]),
+    ('if a() { true } else { "x" << 1 == 0 }', [("", ("error", "Function not found: << (string, i64)"))]),
     # strings
     ('"AbC".to_upper() == "ABC" && "AbC".to_lower() == "abc" && to_upper("\u00df") == "SS" && '
      '"\u0130".to_lower() == "i\u0307" && "\u00e9".to_upper() == "\u00c9" && a()', [("a", True)]),
@@ -226,8 +237,6 @@ INVALID = [
     ("let m = #{x: 1}; a()", "unsupported by this engine: object maps"),
     ("'c' == 'c' && a()", "unsupported by this engine: character literals"),
     ("`x${1}` == \"x1\" && a()", "unsupported by this engine: back-tick strings"),
-    ("2 ** 3 == 8 && a()", "unsupported by this engine: the ** operator"),
-    ("1 << 2 == 4 && a()", "unsupported by this engine: bit shifts"),
     ("let f = |x| x + 1; a()", "unsupported by this engine: closures"),
     ("let r = 1..3; a()", "unsupported by this engine: range values outside `for` and `in`"),
     ("let r = range(1, 3); a()", "unsupported by this engine: range values outside `for` and `in`"),
