@@ -324,9 +324,6 @@ __device__ inline uint32_t kv_walk(as_ptr<AS> R, const KvDfa& d, const uint8_t* 
         }
       }
       st = fin;
-#if KW_ABL_ONEWIN  // (diagnostic variant: value walks stop after their first window; wrong classes)
-      break;
-#endif
       continue;
     }
 #pragma unroll
@@ -487,9 +484,6 @@ __device__ inline void glds_x4(const u32x4* src, u32x4* dst, uint32_t n, uint32_
 }
 #ifndef KW_DESC_EARLY
 #define KW_DESC_EARLY 1
-#endif
-#ifndef KW_ABL_ONEWIN
-#define KW_ABL_ONEWIN 0
 #endif
 __device__ inline void copy_x4(const uint8_t* src, uint8_t* dst, uint32_t bytes, uint32_t tid) {
   const auto* s = gp((const u32x4*)src);
