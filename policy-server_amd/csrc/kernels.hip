@@ -609,9 +609,10 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
   // the first tile's descriptor goes out with the table staging below (r06: one memory round trip
   // fewer before the first tile, which a small shard's ~2 tiles a workgroup feel; KW_DESC_EARLY=0
   // restores the separate fetch and barrier for A/B)
-#if KW_DESC_EARLY
-  if (tile < t_hi) fetch_desc(tile, 0);
-#endif
+  // (LDS-table instantiations only: the global-table one, C6, stages no tables and runs 1.2 % slower
+  // with the early fetch, profiles/r06_c6_desc_early_ab.txt)
+  constexpr bool desc_early = KW_DESC_EARLY && LDST;
+  if (desc_early && tile < t_hi) fetch_desc(tile, 0);
   // ---- once per workgroup: the column classifiers and the chunks' staged record prefixes
   if (LDST) {
     for (uint32_t s = 0; s < t.nstage; ++s) copy_x4(a.blob + t.stage_blob[s], lds + t.stage_lds[s], t.stage_bytes[s], tid);
@@ -680,10 +681,10 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
   const uint32_t nim = il.n(), nlv = t.nlv;
   const uint32_t need = t.need;
 
-#if !KW_DESC_EARLY
-  if (tile < t_hi) fetch_desc(tile, 0);
-  __syncthreads();
-#endif
+  if (!desc_early) {
+    if (tile < t_hi) fetch_desc(tile, 0);
+    __syncthreads();
+  }
   mark(4);
   for (uint32_t it = 0; tile < t_hi; ++it) {
     const uint32_t cur = it & 1u;
