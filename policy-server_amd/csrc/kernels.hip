@@ -482,8 +482,22 @@ __device__ inline void glds_x4(const u32x4* src, u32x4* dst, uint32_t n, uint32_
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + i),
                                      (__attribute__((address_space(3))) void*)(dst + (i - lane)), 16, 0, 0);
 }
+// The same copies issued by one wave alone (lane l of the wave lands at dst + i for element i).
+__device__ inline void wglds_dwords(const uint32_t* src, uint32_t* dst, uint32_t n, uint32_t lane) {
+  for (uint32_t i = lane; i < n; i += 64u)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + i),
+                                     (__attribute__((address_space(3))) void*)(dst + (i - lane)), 4, 0, 0);
+}
+__device__ inline void wglds_x4(const u32x4* src, u32x4* dst, uint32_t n, uint32_t lane) {
+  for (uint32_t i = lane; i < n; i += 64u)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + i),
+                                     (__attribute__((address_space(3))) void*)(dst + (i - lane)), 16, 0, 0);
+}
 #ifndef KW_DESC_EARLY
 #define KW_DESC_EARLY 1
+#endif
+#ifndef KW_P0_SPREAD  // P0 copy jobs spread over the waves (below)
+#define KW_P0_SPREAD 1
 #endif
 __device__ inline void copy_x4(const uint8_t* src, uint8_t* dst, uint32_t bytes, uint32_t tid) {
   const auto* s = gp((const u32x4*)src);
@@ -709,19 +723,49 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
     // ---- P0: stage request headers, container offsets and the tile's strings. Every copy is an
     //      LDS-DMA (global_load_lds: no VGPR round trip), so all of a tile's loads are in flight
     //      together and the barrier waits for one memory latency, not one per array.
-    glds_dwords((const uint32_t*)(a.req_flags + r0), (uint32_t*)l_rf, (nr + 3u) >> 2, tid);
-    glds_dwords(a.ctr_off + r0, l_coff, nr + 1, tid);
-    glds_dwords(a.lbl_off + r0, l_loff, nr + 1, tid);
-    glds_dwords((const uint32_t*)a.ctr_flags + (cb >> 2), (uint32_t*)l_cflags, ((ce + 3u) >> 2) - (cb >> 2), tid);
-    glds_dwords(a.capadd_off + cb, l_cadd, nc + 1, tid);
-    glds_dwords(a.capdrop_off + cb, l_cdrop, nc + 1, tid);
+    // Label / container instantiations (several staged string columns): each copy job runs on one
+    // wave (job j on wave j % 4). A job's setup is a chain of dependent round trips (the column's
+    // addresses are scalar loads from TileArgs, its span descriptor fields LDS reads, each waited
+    // for before the copy can issue); spread over the waves, each wave waits for a quarter of them,
+    // and the copies take a few more trips of a cheap loop. r06 (profiles/r06_p0_spread_ab.txt):
+    // C4 -3.2 %, C6 -0.7 %; the image-only ones (C2 / C3: one string column) +0.5-1 %, so they
+    // keep the workgroup-wide copies.
+    constexpr bool p0_spread = KW_P0_SPREAD && (LBL || CTR);
+    if constexpr (p0_spread) {
+      auto job = [&](uint32_t j) { return wave == (j & 3u); };
+      if (job(0)) wglds_dwords((const uint32_t*)(a.req_flags + r0), (uint32_t*)l_rf, (nr + 3u) >> 2, lane);
+      if (job(1)) wglds_dwords(a.ctr_off + r0, l_coff, nr + 1, lane);
+      if (job(2)) wglds_dwords(a.lbl_off + r0, l_loff, nr + 1, lane);
+      if (job(3)) wglds_dwords((const uint32_t*)a.ctr_flags + (cb >> 2), (uint32_t*)l_cflags, ((ce + 3u) >> 2) - (cb >> 2), lane);
+      if (job(4)) wglds_dwords(a.capadd_off + cb, l_cadd, nc + 1, lane);
+      if (job(5)) wglds_dwords(a.capdrop_off + cb, l_cdrop, nc + 1, lane);
 #pragma unroll
-    for (int m = 0; m < (int)NSTR; ++m) {
-      if (!t.o_sb[m]) continue;
-      const uint32_t g0 = str_g0(m, (uint32_t)r0, cb, kab, kdb, lb);
-      const uint32_t n = str_n(m, nr, nc, kae - kab, kde - kdb, nl);
-      glds_dwords(t.s_off[m] + g0, (uint32_t*)(lds + t.o_so[m]), n + 1, tid);  // absolute: rebased by l_sa
-      glds_x4((const u32x4*)(t.s_bytes[m] + KW_DF(d.sa[m])), (u32x4*)(lds + t.o_sb[m]), KW_DF(d.nv[m]), tid);
+      for (int m = 0; m < (int)NSTR; ++m) {
+        const uint32_t jo = 6u + 2u * (uint32_t)m, jb = jo + 1u;
+        if (!(job(jo) || job(jb)) || !t.o_sb[m]) continue;
+        if (job(jo)) {
+          const uint32_t g0 = str_g0(m, (uint32_t)r0, cb, kab, kdb, lb);
+          const uint32_t n = str_n(m, nr, nc, kae - kab, kde - kdb, nl);
+          wglds_dwords(t.s_off[m] + g0, (uint32_t*)(lds + t.o_so[m]), n + 1, lane);  // absolute: rebased by l_sa
+        } else {
+          wglds_x4((const u32x4*)(t.s_bytes[m] + KW_DF(d.sa[m])), (u32x4*)(lds + t.o_sb[m]), KW_DF(d.nv[m]), lane);
+        }
+      }
+    } else {
+      glds_dwords((const uint32_t*)(a.req_flags + r0), (uint32_t*)l_rf, (nr + 3u) >> 2, tid);
+      glds_dwords(a.ctr_off + r0, l_coff, nr + 1, tid);
+      glds_dwords(a.lbl_off + r0, l_loff, nr + 1, tid);
+      glds_dwords((const uint32_t*)a.ctr_flags + (cb >> 2), (uint32_t*)l_cflags, ((ce + 3u) >> 2) - (cb >> 2), tid);
+      glds_dwords(a.capadd_off + cb, l_cadd, nc + 1, tid);
+      glds_dwords(a.capdrop_off + cb, l_cdrop, nc + 1, tid);
+#pragma unroll
+      for (int m = 0; m < (int)NSTR; ++m) {
+        if (!t.o_sb[m]) continue;
+        const uint32_t g0 = str_g0(m, (uint32_t)r0, cb, kab, kdb, lb);
+        const uint32_t n = str_n(m, nr, nc, kae - kab, kde - kdb, nl);
+        glds_dwords(t.s_off[m] + g0, (uint32_t*)(lds + t.o_so[m]), n + 1, tid);  // absolute: rebased by l_sa
+        glds_x4((const u32x4*)(t.s_bytes[m] + KW_DF(d.sa[m])), (u32x4*)(lds + t.o_sb[m]), KW_DF(d.nv[m]), tid);
+    }
     }
     for (uint32_t i = tid; i < nr; i += kSlotThreads) l_rej[i] = l_mut[i] = 0;
     if (DYNB && tid == 0) l_nx[2] = l_nx[3] = 0;  // P1 / P2 block counters (below)
