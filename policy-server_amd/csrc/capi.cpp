@@ -1595,10 +1595,12 @@ int run_pass(kw_batch* kb, PassPlan& plan, bool timed, hipStream_t s) {
       const double* g = sum + 8;
       fprintf(stderr,
               "[kw seg] per wave-tile: P0 wait %.0f | P1 busy %.0f wait %.0f (label %.0f capstr %.0f ctr %.0f image %.0f req %.0f) "
-              "| P2 busy %.0f wait %.0f (ctr %.0f label %.0f req %.0f) | P3 busy %.0f wait %.0f\n",
+              "| P2 busy %.0f wait %.0f (ctr %.0f label %.0f req %.0f) | P3 busy %.0f wait %.0f | P0 issue: top %.0f "
+              "request arrays %.0f strings %.0f\n",
               g[SG_P0_WAIT] / wt, g[SG_P1_BUSY] / wt, g[SG_P1_WAIT] / wt, g[SG_P1_LABEL] / wt, g[SG_P1_CAPSTR] / wt,
               g[SG_P1_CTR] / wt, g[SG_P1_IMAGE] / wt, g[SG_P1_REQ] / wt, g[SG_P2_BUSY] / wt, g[SG_P2_WAIT] / wt,
-              g[SG_P2_CTR] / wt, g[SG_P2_LABEL] / wt, g[SG_P2_REQ] / wt, g[SG_P3_BUSY] / wt, g[SG_P3_WAIT] / wt);
+              g[SG_P2_CTR] / wt, g[SG_P2_LABEL] / wt, g[SG_P2_REQ] / wt, g[SG_P3_BUSY] / wt, g[SG_P3_WAIT] / wt,
+              g[SG_P0_TOP] / wt, g[SG_P0_REQ] / wt, g[SG_P0_STR] / wt);
       // workgroup start times: a grid the CUs do not hold at once starts in waves. The real-time
       // counter is compared only within an XCD (workgroup b runs on XCD b % 8): the XCDs' counters
       // are not synchronised with each other.

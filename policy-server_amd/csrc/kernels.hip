@@ -701,6 +701,7 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
   }
   mark(4);
   for (uint32_t it = 0; tile < t_hi; ++it) {
+    const uint64_t p0_t0 = timing ? clock64() : 0;
     const uint32_t cur = it & 1u;
     uint32_t nxt2 = 0;
     if (dyn && tid == 0) nxt2 = atomicAdd(cnt, 1u);  // the tile after next (read after the staging barrier)
@@ -719,6 +720,11 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
     const uint32_t cb = KW_DF(d.cb), ce = KW_DF(d.ce), lb = KW_DF(d.lb), le = KW_DF(d.le);
     const uint32_t kab = KW_DF(d.kab), kae = KW_DF(d.kae), kdb = KW_DF(d.kdb), kde = KW_DF(d.kde);
     const uint32_t nc = ce - cb, nl = le - lb;
+    uint64_t p0_t1 = 0, p0_t2 = 0;
+    if (timing) {
+      p0_t1 = clock64();
+      sg_add(SG_P0_TOP, p0_t1 - p0_t0);
+    }
 
     // ---- P0: stage request headers, container offsets and the tile's strings. Every copy is an
     //      LDS-DMA (global_load_lds: no VGPR round trip), so all of a tile's loads are in flight
@@ -739,6 +745,10 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
       if (job(3)) wglds_dwords((const uint32_t*)a.ctr_flags + (cb >> 2), (uint32_t*)l_cflags, ((ce + 3u) >> 2) - (cb >> 2), lane);
       if (job(4)) wglds_dwords(a.capadd_off + cb, l_cadd, nc + 1, lane);
       if (job(5)) wglds_dwords(a.capdrop_off + cb, l_cdrop, nc + 1, lane);
+      if (timing) {
+        p0_t2 = clock64();
+        sg_add(SG_P0_REQ, p0_t2 - p0_t1);
+      }
 #pragma unroll
       for (int m = 0; m < (int)NSTR; ++m) {
         const uint32_t jo = 6u + 2u * (uint32_t)m, jb = jo + 1u;
@@ -758,6 +768,10 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
       glds_dwords((const uint32_t*)a.ctr_flags + (cb >> 2), (uint32_t*)l_cflags, ((ce + 3u) >> 2) - (cb >> 2), tid);
       glds_dwords(a.capadd_off + cb, l_cadd, nc + 1, tid);
       glds_dwords(a.capdrop_off + cb, l_cdrop, nc + 1, tid);
+      if (timing) {
+        p0_t2 = clock64();
+        sg_add(SG_P0_REQ, p0_t2 - p0_t1);
+      }
 #pragma unroll
       for (int m = 0; m < (int)NSTR; ++m) {
         if (!t.o_sb[m]) continue;
@@ -767,6 +781,7 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
         glds_x4((const u32x4*)(t.s_bytes[m] + KW_DF(d.sa[m])), (u32x4*)(lds + t.o_sb[m]), KW_DF(d.nv[m]), tid);
     }
     }
+    if (timing) sg_add(SG_P0_STR, clock64() - p0_t2);
     for (uint32_t i = tid; i < nr; i += kSlotThreads) l_rej[i] = l_mut[i] = 0;
     if (DYNB && tid == 0) l_nx[2] = l_nx[3] = 0;  // P1 / P2 block counters (below)
     if (tid < NSTR) l_sa[tid] = d.sa[tid];

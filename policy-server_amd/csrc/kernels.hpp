@@ -56,7 +56,8 @@ enum Seg : uint32_t {
   SG_P1_LABEL = 0, SG_P1_CAPSTR, SG_P1_CTR, SG_P1_IMAGE, SG_P1_REQ, SG_P2_CTR, SG_P2_LABEL, SG_P2_REQ,
   SG_P1_BUSY, SG_P1_WAIT, SG_P2_BUSY, SG_P2_WAIT, SG_P0_WAIT, SG_P3_BUSY, SG_P3_WAIT,
   SG_START,  // the workgroup's start (s_memrealtime, 100 MHz): residency of the grid
-  kSegWords = 16
+  SG_P0_TOP, SG_P0_REQ, SG_P0_STR,  // P0 issue: tile loop top to the descriptor fields, request-array copies, string copies
+  kSegWords = 19
 };
 constexpr uint32_t kPhaseWords = 8 + kSegWords;
 
