@@ -19,7 +19,8 @@ WAIT=${WAIT:-200}
 PORT=$((20000 + RANDOM % 20000))
 OUT=gpurun_out/${TAG}_serve.jsonl
 : > "$OUT"; : > gpurun_out/${TAG}_serve_stats.jsonl
-policy-server_amd/kwhost --policies "$YML" --port $PORT --device 0 --continue-on-errors \
+DEVARG="--device 0"; [ -n "${DEVICES:-}" ] && DEVARG="--devices $DEVICES"  # DEVICES=0,0: two pipelines on one GPU
+policy-server_amd/kwhost --policies "$YML" --port $PORT $DEVARG --continue-on-errors \
   --always-accept-admission-reviews-on-namespace kubewarden --workers $WORKERS --max-batch $MAXB --max-wait-us $WAIT --stats-ms 1000 \
   2> gpurun_out/${TAG}_kwhost.err &
 KW=$!
