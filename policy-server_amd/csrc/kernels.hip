@@ -496,9 +496,6 @@ __device__ inline void wglds_x4(const u32x4* src, u32x4* dst, uint32_t n, uint32
 #ifndef KW_DESC_EARLY
 #define KW_DESC_EARLY 1
 #endif
-#ifndef KW_LABEL_STEAL  // a fifth label block's labels taken by idle lanes of the first four (P1)
-#define KW_LABEL_STEAL 1
-#endif
 #ifndef KW_P0_SPREAD  // P0 copy jobs spread over the waves (below)
 #define KW_P0_SPREAD 1
 #endif
@@ -696,11 +693,6 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
   uint8_t* own_l = region(t.o_own_l);
   const ImgLayout il = t.il;
   const uint32_t nim = il.n(), nlv = t.nlv;
-  // remainder-label absorption (P1 below): the label-pair pass shape, and tiles that can hold a fifth
-  // label block (more than 256 labels: the class array then has room for the counts at byte 512)
-  const bool steal_ok = KW_LABEL_STEAL && LBL && LDST && !NFA && C.kv && t.kv_lds && nlv == 2u && t.nchunk == 1u &&
-                        t.lmax > 256u && t.lmax <= 320u && !(t.debug & (1u | 2048u));
-  uint8_t* c_lv_u8 = (uint8_t*)c_lv;
   const uint32_t need = t.need;
 
   if (!desc_early) {
@@ -792,7 +784,6 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
     if (timing) sg_add(SG_P0_STR, clock64() - p0_t2);
     for (uint32_t i = tid; i < nr; i += kSlotThreads) l_rej[i] = l_mut[i] = 0;
     if (DYNB && tid == 0) l_nx[2] = l_nx[3] = 0;  // P1 / P2 block counters (below)
-    if (steal_ok && tid < 4u) c_lv_u8[512u + tid] = 0;  // remainder labels absorbed per first block (P1)
     if (tid < NSTR) l_sa[tid] = d.sa[tid];
 #undef KW_DF
     const uint64_t p0_end = timing ? clock64() : 0;
@@ -882,15 +873,7 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
             // n-th idle lane, matched through a per-wave mailbox in the (here unused) class array;
             // the task and its class cross lanes by ds_bpermute. Labels left without a helper walk
             // their second DFA themselves.
-            // A tile of 257-320 labels has a fifth label block (remainder labels 256 + r). The first
-            // four blocks' lanes whose own key has no value constraint take them (remainder r to the
-            // n-th such lane of first block r % 4, n = r / 4): one more key probe there instead of a
-            // whole fifth block on one wave. Each first block publishes how many it took; the fifth
-            // block skips those. (Read before the count is written, a label is classified twice,
-            // with the same outputs.)
-            const uint32_t nrem = (steal_ok && ek == 320u && n3 > 256u) ? n3 - 256u : 0u;
-            bool act = i < n3;
-            if (nrem && i >= 256u && act && ((i - 256u) >> 2) < (uint32_t)c_lv_u8[512u + ((i - 256u) & 3u)]) act = false;
+            const bool act = i < n3;
             uint32_t k = 0;
             if (act) {
               k = lit(COL_LK, S_LK, i);
@@ -904,25 +887,6 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
               str(S_LV, i, &b, &e);
               rel1 = ((u32l)R)[k];
               kbase = ((u32l)R)[C.nlk + k];
-            }
-            uint32_t li = i, kw = k;  // the label this lane's walks classify (its own or a remainder one) and its key
-            if (nrem && i < 256u) {
-              const uint32_t blk = i >> 6;
-              const uint64_t freem = __ballot(rel1 == 0u);
-              const uint32_t fi = __builtin_amdgcn_mbcnt_hi((uint32_t)(freem >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)freem, 0u));
-              const uint32_t mine = nrem > blk ? (nrem - blk + 3u) >> 2 : 0u;
-              const uint32_t take = min(mine, (uint32_t)__popcll(freem));
-              if (lane == 0u) c_lv_u8[512u + blk] = (uint8_t)take;
-              if (rel1 == 0u && fi < take) {
-                li = 256u + blk + 4u * fi;
-                kw = lit(COL_LK, S_LK, li);
-                c_lk[li] = (uint16_t)kw;
-                if (kw) {
-                  str(S_LV, li, &b, &e);
-                  rel1 = ((u32l)R)[kw];
-                  kbase = ((u32l)R)[C.nlk + kw];
-                }
-              }
             }
             if (rel1) rel2 = kv_record<3>(R, rel1).next;
             const uint64_t needm = __ballot(rel2 != 0u), idlem = __ballot(rel1 == 0u);
@@ -966,18 +930,16 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
               }
             }
             const uint32_t hc = needm ? (uint32_t)__builtin_amdgcn_ds_bpermute((int)((helper < 64u ? helper : lane) * 4u), (int)res[0]) : 0u;
-            if (act || li != i) {
+            if (act) {
               const uint32_t c1 = rel1 ? res[0] : 0xffffu;
               const uint32_t c2 = rel2 ? (helper < 64u ? hc : res[1]) : 0xffffu;
               uint64_t v = 0;
-              if (h0.lbl && kw) {
-                v = sv0.row(T_DENY, kw);
+              if (h0.lbl && k) {
+                v = sv0.row(T_DENY, k);
                 if (c1 != 0xffffu) v |= sv0.row(T_FAIL, c1);
                 if (c2 != 0xffffu) v |= sv0.row(T_FAIL, c2);
               }
-              l_vl[li] = v;
-              // a lane that took a remainder label: its own key has no value constraint
-              if (li != i) l_vl[i] = (h0.lbl && k) ? sv0.row(T_DENY, k) : 0ull;
+              l_vl[i] = v;
             }
             continue;
           }
