@@ -302,6 +302,29 @@ def host_modes(env, ids, syn, device, args, alg_bytes=None):
             hb.close()
         return best
 
+    # two HBM-resident passes in flight (serving-like: kwhost's pipeline workers run theirs on separate
+    # streams). Two device copies of the batch, each on its own stream, steps alternating between
+    # them: the second pass's workgroups take the CUs the first one's last tile round leaves idle.
+    # Reported beside `value` (one pass at a time), not as it.
+    if device >= 0:
+        ba, bb = syn.batch().to_device(device), syn.batch().to_device(device)
+        try:
+            for _ in range(2):
+                ba.validate(env, ids)
+                bb.validate(env, ids)
+            torch.cuda.synchronize()
+            k = max(10, args.steps)
+            t = time.perf_counter()
+            for i in range(k):
+                (ba if i % 2 == 0 else bb).validate(env, ids)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t
+            out["two_in_flight"] = {"value": syn.n * k / dt, "unit": "requests/s", "steps": k, "ms_per_step": dt * 1e3 / k,
+                                    "what": "HBM-resident passes over two device copies of the batch, each on its own "
+                                            "stream, alternating: two passes in flight"}
+        finally:
+            ba.close()
+            bb.close()
     # the PCIe ceiling of the bulk path: its input columns in and its verdict words out, each at the
     # measured pinned copy rate of that direction (the two directions overlap)
     out_bytes = syn.n * npol * 4
