@@ -496,6 +496,9 @@ __device__ inline void wglds_x4(const u32x4* src, u32x4* dst, uint32_t n, uint32
 #ifndef KW_DESC_EARLY
 #define KW_DESC_EARLY 1
 #endif
+#ifndef KW_TABLE_DMA  // the workgroup's table staging by LDS-DMA (below)
+#define KW_TABLE_DMA 1
+#endif
 #ifndef KW_P0_SPREAD  // P0 copy jobs spread over the waves (below)
 #define KW_P0_SPREAD 1
 #endif
@@ -629,9 +632,18 @@ __global__ void __launch_bounds__(kSlotThreads, 1)
   if (desc_early && tile < t_hi) fetch_desc(tile, 0);
   // ---- once per workgroup: the column classifiers and the chunks' staged record prefixes
   if (LDST) {
+#if KW_TABLE_DMA
+    // LDS-DMA: every 16-B piece of the tables in flight at once, one memory latency before the barrier
+    // (a copy through VGPRs waits a latency per loop trip: ~3 trips of 256 x 16 B for C4's 12 KB)
+    for (uint32_t s = 0; s < t.nstage; ++s)
+      glds_x4((const u32x4*)(a.blob + t.stage_blob[s]), (u32x4*)(lds + t.stage_lds[s]), t.stage_bytes[s] / 16u, tid);
+    for (uint32_t c = 0; c < t.nchunk; ++c)
+      glds_x4((const u32x4*)t.chunk[c].rec, (u32x4*)(lds + t.chunk[c].o_lds), ((const SlotHdr*)t.chunk[c].rec)->staged / 16u, tid);
+#else
     for (uint32_t s = 0; s < t.nstage; ++s) copy_x4(a.blob + t.stage_blob[s], lds + t.stage_lds[s], t.stage_bytes[s], tid);
     for (uint32_t c = 0; c < t.nchunk; ++c)
       copy_x4(t.chunk[c].rec, lds + t.chunk[c].o_lds, ((const SlotHdr*)t.chunk[c].rec)->staged, tid);
+#endif
   }
   __syncthreads();
   mark(7);
