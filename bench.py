@@ -424,17 +424,26 @@ def traffic(args, rows):
     None when the file is absent, was measured on another workload or shard size, or on another build
     of the library (its sha256 differs from the running one's): a kernel change must not keep printing
     an old measurement."""
-    path = os.path.join(ROOT, "profiles", "traffic.json")  # written by scripts/pmc.sh (copied from the GPU box)
-    try:
-        with open(path) as f:
-            t = json.load(f)
-    except (OSError, ValueError):
-        return None, "no profiles/traffic.json"
+    # profiles/traffic.json holds the metric's config (C4); profiles/traffic_<config>.json the others
+    # (written by scripts/pmc.sh, copied from the GPU box)
+    t, name = None, None
+    for name in ("traffic.json", f"traffic_{args.config}.json"):
+        try:
+            with open(os.path.join(ROOT, "profiles", name)) as f:
+                t = json.load(f)
+        except (OSError, ValueError):
+            t = None
+            continue
+        if t.get("config") == args.config:
+            break
+    if t is None:
+        return None, f"no profiles/traffic.json or traffic_{args.config}.json"
     if t.get("config") != args.config or t.get("rows") != rows:
-        return None, f"profiles/traffic.json is for {t.get('config')} x {t.get('rows')} rows, not this workload"
+        return None, f"profiles/{name} is for {t.get('config')} x {t.get('rows')} rows, not this workload"
     if t.get("lib_sha256") != library_sha256():
-        return None, "profiles/traffic.json was measured on another build of libkwgpu.so (sha256 differs)"
-    return t.get("bytes_per_launch"), f"{t.get('source')}; round {t.get('round')}; lib sha256 {t.get('lib_sha256')[:16]}"
+        return None, f"profiles/{name} was measured on another build of libkwgpu.so (sha256 differs)"
+    return t.get("bytes_per_launch"), (f"profiles/{name}: {t.get('source')}; round {t.get('round')}; "
+                                       f"lib sha256 {t.get('lib_sha256')[:16]}")
 
 
 def cpu_threads():
